@@ -1,0 +1,214 @@
+/*
+ * accord_deps.h — C-ABI of the MI355X batched dependency-resolution engine.
+ *
+ * This is the drop-in boundary for Accord's PreAccept-deps -> Deps.merge -> execution-order
+ * hot path.  Every entry point is plain C (pointers + sizes, integer status codes, no
+ * exceptions, no torch/HIP types) so a Java host can bind it through Panama FFM
+ * (java.lang.foreign) and rebuild Accord objects through the reference's raw-CSR constructors.
+ * See INTEGRATION.md for the Java-side binding.
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * accord-core/src/main/java/accord/):
+ *
+ *   ad_preaccept_deps / ad_fetch_deps
+ *       SafeCommandStore.mapReduceActive            local/SafeCommandStore.java:292
+ *       InMemorySafeStore.mapReduceActive           impl/InMemoryCommandStore.java:864-871
+ *       CommandsForKey.mapReduceActive              local/cfk/CommandsForKey.java:925-983
+ *       PreAccept.calculatePartialDeps              messages/PreAccept.java:245-267
+ *       Deps.AbstractBuilder.add / build            primitives/Deps.java:80-135
+ *       RelationMultiMap.AbstractBuilder.build      utils/RelationMultiMap.java:201-260
+ *     output layout == KeyDeps.SerializerSupport.create(Keys, TxnId[], int[])  primitives/KeyDeps.java:69-72
+ *                       RangeDeps.SerializerSupport.create(Range[], TxnId[], int[]) primitives/RangeDeps.java:100-103
+ *   ad_merge_deps
+ *       Deps.merge(List, Function)                  primitives/Deps.java:281-286
+ *       KeyDeps.merge / RelationMultiMap.LinearMerger  primitives/KeyDeps.java:115-135, utils/RelationMultiMap.java:284-406
+ *       RelationMultiMap.linearUnion                utils/RelationMultiMap.java:562-816
+ *   ad_exec_levels
+ *       Commands.initialiseWaitingOn/updateWaitingOn/maybeExecute  local/Commands.java:617-775
+ *       CommandsForKey.notifyManaged                local/cfk/CommandsForKey.java:1208-1289
+ *
+ * Threading: one handle per CommandStore-shard / GPU; a handle owns one HIP stream and its
+ * device arena.  Calls on different handles may run concurrently; calls on one handle must
+ * be serialised by the caller (InMemoryCommandStore.SingleThread, impl/InMemoryCommandStore.java:1144).
+ *
+ * Ownership: the caller owns every host buffer passed in; the library never retains a caller
+ * pointer after a call returns.  Output sizes come from a two-call protocol (sizes, then a
+ * fetch into caller-allocated buffers), mirroring ArrayBuffers' complete/discard discipline
+ * (utils/ArrayBuffers.java:32-50).
+ */
+#ifndef ACCORD_DEPS_H
+#define ACCORD_DEPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* Status codes (Invariants.illegalArgument / illegalState map onto the negative values).      */
+/* ------------------------------------------------------------------------------------------ */
+typedef enum ad_status {
+    AD_OK = 0,
+    AD_ERR_ARGUMENT = -1,      /* IllegalArgumentException (e.g. duplicate key within a txn)  */
+    AD_ERR_STATE = -2,         /* IllegalStateException (call order, missing batch)           */
+    AD_ERR_UNSORTED = -3,      /* batch TxnIds not strictly ascending (CFK byId order)        */
+    AD_ERR_UNSUPPORTED = -4,   /* timestamp/key widths beyond the packed encoding             */
+    AD_ERR_DEVICE = -5,        /* HIP runtime error                                           */
+    AD_ERR_NOMEM = -6
+} ad_status;
+
+/* Txn.Kind ordinals (primitives/Txn.java:53-113); TxnId flags = kind << 1 | domain (TxnId.java:132-165). */
+enum { AD_KIND_READ = 0, AD_KIND_WRITE = 1, AD_KIND_EPHEMERAL_READ = 2, AD_KIND_SYNC_POINT = 3,
+       AD_KIND_EXCLUSIVE_SYNC_POINT = 4, AD_KIND_LOCAL_ONLY = 5 };
+enum { AD_DOMAIN_KEY = 0, AD_DOMAIN_RANGE = 1 };
+
+/* CommandsForKey.InternalStatus ordinals (local/cfk/CommandsForKey.java:493-502). */
+enum { AD_ST_TRANSITIVELY_KNOWN = 0, AD_ST_HISTORICAL = 1, AD_ST_PREACCEPTED = 2, AD_ST_ACCEPTED = 3,
+       AD_ST_COMMITTED = 4, AD_ST_STABLE = 5, AD_ST_APPLIED = 6, AD_ST_INVALID = 7 };
+
+/* Deps classes, in Deps' own index order (primitives/Deps.java:143-155; DepsTest index order). */
+enum { AD_CLASS_KEY = 0, AD_CLASS_DIRECT_KEY = 1, AD_CLASS_RANGE = 2, AD_NUM_CLASSES = 3 };
+
+/* ------------------------------------------------------------------------------------------ */
+/* Batch input (host SoA).  One batch = the transactions one CommandStore shard resolves.      */
+/*                                                                                             */
+/* Timestamps are passed as Accord's raw bits: msb = epoch<<15 | hlc>>>48, lsb = hlc<<16|flags, */
+/* node = Node.Id.id (Timestamp.java:77-96).  Ordering is Timestamp.compareTo                  */
+/* (Timestamp.java:208-217): msb unsigned, lsb>>>16, lsb & 0x1E, node signed.                  */
+/*                                                                                             */
+/* TxnIds must be strictly ascending: the batch is CommandsForKey.byId order, which is also    */
+/* the arrival order of the status model below.                                               */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct ad_batch {
+    size_t n;                       /* transactions                                           */
+    const uint64_t* txn_msb;        /* [n] TxnId                                              */
+    const uint64_t* txn_lsb;        /* [n]                                                    */
+    const int32_t*  txn_node;       /* [n]                                                    */
+    const uint64_t* exec_msb;       /* [n] final (committed) executeAt                        */
+    const uint64_t* exec_lsb;       /* [n]                                                    */
+    const int32_t*  exec_node;      /* [n]                                                    */
+    const uint8_t*  status;         /* [n] InternalStatus a txn has once outside the in-flight window */
+    const uint32_t* key_off;        /* [n+1] key footprint CSR                                */
+    const uint64_t* keys;           /* [key_off[n]] order-preserving key encoding (Key.compareTo) */
+    const uint32_t* range_off;      /* [n+1] range footprint CSR (NULL when no range txns)    */
+    const uint64_t* range_start;    /* [range_off[n]] Range.EndInclusive (start, end]         */
+    const uint64_t* range_end;      /* [range_off[n]]                                         */
+} ad_batch;
+
+/* Status model for one batch query: when txn i (rank order) is PreAccepted, every
+ * txn j < i with j >= i - window is still in flight (PREACCEPTED_OR_ACCEPTED_INVALIDATE); every
+ * j < i - window has its given final status.  window = 0 is the plain snapshot query.
+ * A replica view r in [0, replicas) additionally has not yet witnessed each in-flight j with
+ * probability drop_p, decided by ad_drop_hash(seed, r, i, j) (the same function the oracle uses). */
+typedef struct ad_config {
+    uint32_t window;                /* W (BASELINE: 32)                                        */
+    uint32_t replicas;              /* R replica views to build (1..8)                          */
+    float    drop_p;                /* per in-flight dependency drop probability per view       */
+    uint32_t pad_;
+    uint64_t seed;                  /* drop hash seed                                          */
+} ad_config;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Batched PartialDeps output.  For class c of view v, per txn i:                               */
+/*   keys      [key_off[i]   .. key_off[i+1])    sorted unique keys (u64) that carry deps       */
+/*   txn ranks [txn_off[i]   .. txn_off[i]+txn_cnt[i])  sorted unique dependency ranks (into   */
+/*                                                the batch; rank -> TxnId is the batch row)   */
+/*   k2t       [k2t_off[i]   .. k2t_off[i+1])    exactly KeyDeps.keysToTxnIds for this txn:    */
+/*             nKeys end-offsets (first offset base = nKeys) followed by txn indices           */
+/*             (KeyDeps.java:153-172).  For RangeDeps the "keys" are ranges (start,end pairs). */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct ad_csr_sizes {
+    size_t n;                       /* txns                                                     */
+    size_t keys;                    /* total key (or range) entries over all txns              */
+    size_t k2t;                     /* total keysToTxnIds ints                                  */
+    size_t txn_cap;                 /* total txn-rank capacity (sum of per-txn entry counts)    */
+    size_t txns;                    /* total unique dependency txns (sum of txn_cnt)            */
+} ad_csr_sizes;
+
+typedef struct ad_csr_out {         /* caller-allocated, sized by ad_csr_sizes                  */
+    uint32_t* key_off;              /* [n+1]                                                    */
+    uint64_t* keys;                 /* [keys]  (RangeDeps: [2*keys] start,end interleaved)      */
+    uint32_t* k2t_off;              /* [n+1]                                                    */
+    int32_t*  k2t;                  /* [k2t]                                                    */
+    uint32_t* txn_off;              /* [n+1]  compacted: txn_off[i+1]-txn_off[i] == txn_cnt[i]  */
+    uint32_t* txns;                 /* [txns] dependency ranks                                  */
+} ad_csr_out;
+
+typedef struct ad_handle ad_handle;
+
+/* Drop decision shared by the device path and the oracle (splitmix64 finaliser). */
+static inline uint64_t ad_mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline uint32_t ad_drop_hash(uint64_t seed, uint32_t view, uint32_t i, uint32_t j) {
+    return (uint32_t)(ad_mix64(seed ^ ad_mix64(((uint64_t)view << 56) ^ ((uint64_t)i << 28) ^ (uint64_t)j)) >> 32);
+}
+static inline uint32_t ad_drop_threshold(float p) {
+    if (p <= 0.0f) return 0u;
+    if (p >= 1.0f) return 0xFFFFFFFFu;
+    return (uint32_t)((double)p * 4294967296.0);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Lifecycle                                                                                   */
+/* ------------------------------------------------------------------------------------------ */
+int  ad_open(int device, const ad_config* cfg, ad_handle** out);
+void ad_close(ad_handle* h);
+const char* ad_last_error(const ad_handle* h);
+int  ad_device_count(void);
+
+/* Copy one batch host->device (the only PCIe transfer of the inputs).  Replaces the previous batch. */
+int  ad_load_batch(ad_handle* h, const ad_batch* batch);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Stage 1 — PreAccept deps for every txn of the loaded batch under cfg->replicas views.       */
+/* Runs on the device; sizes[v * AD_NUM_CLASSES + c] receives the CSR sizes of view v class c. */
+/* ------------------------------------------------------------------------------------------ */
+int  ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes /* [replicas*AD_NUM_CLASSES] */);
+int  ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out);
+
+/* Stage 2 — Deps.merge of the R replica replies produced by stage 1 (device-resident). */
+int  ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
+int  ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out);
+
+/* Stage 2' — Deps.merge of caller-supplied replies (host CSR, same batch).  parts[r*AD_NUM_CLASSES+c]. */
+typedef struct ad_csr_in {
+    const uint32_t* key_off; const uint64_t* keys; const uint32_t* k2t_off; const int32_t* k2t;
+    const uint32_t* txn_off; const uint32_t* txns;
+} ad_csr_in;
+int  ad_merge_host(ad_handle* h, const ad_csr_in* parts, uint32_t r, ad_csr_sizes* sizes);
+
+/* Stage 3 — execution order over the merged deps: level_out[i] = Kahn wavefront index of txn i,
+ * order_out = txn ranks sorted by (level, executeAt).  Either pointer may be NULL. */
+int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint32_t* iterations_out);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Device-resident pipeline (benchmark / service loop): stage 1 + 2 + 3 with no host copies of */
+/* outputs.  Kernel timing: HIP events on the handle's stream.                                 */
+/* ------------------------------------------------------------------------------------------ */
+int  ad_run_pipeline(ad_handle* h);
+typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline, event-timed */
+    float prepare, sort, deps, merge, levels, total;
+    uint64_t deps_entries;          /* emitted (key,txn) entries over all views/classes      */
+    uint64_t merged_entries;        /* entries of the merged Deps                             */
+    uint64_t level_edges;           /* key-chain entries visited per level sweep              */
+    uint32_t level_iterations;
+    uint32_t pad_;
+} ad_stage_times;
+int  ad_last_times(ad_handle* h, ad_stage_times* out);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Multi-GPU: per-shard fragments are combined with an all-gather (RCCL over xGMI, driven by   */
+/* the host runtime) followed by this local union of the gathered fragments.                  */
+/* ------------------------------------------------------------------------------------------ */
+int  ad_shard_bounds(const uint64_t* keys, size_t nkeys, uint32_t shards, uint64_t* bounds_out /* [shards+1] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACCORD_DEPS_H */

@@ -1,0 +1,746 @@
+/*
+ * oracle.cpp — CPU restatement of Accord's PreAccept-deps / Deps.merge / execution-order path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker the HIP path is compared against and the
+ * "port" CPU baseline that bench.py times; nothing in the product library links, loads or calls
+ * it.  It restates the reference algorithms literally (object-free, but loop-for-loop), citing the
+ * Java it follows (paths relative to accord-core/src/main/java/accord/):
+ *
+ *   Timestamp.compareTo ............................ primitives/Timestamp.java:208-217
+ *   Txn.Kind.witnesses .............................. primitives/Txn.java:221-245
+ *   CommandsForKey.manages / managesExecution ....... local/cfk/CommandsForKey.java:185-199
+ *   CommandsForKey.mapReduceActive .................. local/cfk/CommandsForKey.java:925-983
+ *   CommandsForKey(...) committedByExecuteAt ........ local/cfk/CommandsForKey.java:642-681
+ *   InMemorySafeStore.mapReduceActive ............... impl/InMemoryCommandStore.java:864-871, 272-307
+ *   mapReduceRangesInternal ......................... impl/InMemoryCommandStore.java:884-1017
+ *   PreAccept.calculatePartialDeps .................. messages/PreAccept.java:245-267
+ *   Deps.AbstractBuilder.add ........................ primitives/Deps.java:80-106
+ *   RelationMultiMap.AbstractBuilder ................ utils/RelationMultiMap.java:88-271
+ *   RelationMultiMap.linearUnion .................... utils/RelationMultiMap.java:562-816
+ *   RelationMultiMap.LinearMerger / KeyDeps.merge ... utils/RelationMultiMap.java:284-406, primitives/KeyDeps.java:115-135
+ *   Pruning (steady-state CFK trimming, baseline) ... local/cfk/Pruning.java:164-233
+ *   Execution order (WaitingOn / notifyManaged) ..... local/Commands.java:617-821,
+ *                                                      local/cfk/CommandsForKey.java:1208-1330,
+ *                                                      local/cfk/Updating.java:715-800 (Unmanaged)
+ *
+ * Parity pins: see tests/test_oracle_*.py (restated KeyDepsTest / SortedArraysTest properties,
+ * PreAcceptTest known answers, CommandsForKeyTest.Canon execution invariant) — the reference itself
+ * is Java and cannot be compiled or run in this image (no JVM), see DESIGN.md §Oracle.
+ */
+#include "../include/accord_deps.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Ts { uint64_t msb, lsb; int32_t node; };
+
+static inline int cmpu(uint64_t a, uint64_t b) { return a < b ? -1 : a > b ? 1 : 0; }
+
+// Timestamp.compareTo — primitives/Timestamp.java:208-217
+static inline int ts_cmp(const Ts& a, const Ts& b) {
+    int c = cmpu(a.msb, b.msb);                                   // Long.compareUnsigned(msb)
+    if (c == 0) c = cmpu(a.lsb >> 16, b.lsb >> 16);               // Long.compare(lowHlc) (non-negative)
+    if (c == 0) c = cmpu(a.lsb & 0x1E, b.lsb & 0x1E);             // IDENTITY_FLAGS
+    if (c == 0) c = a.node < b.node ? -1 : a.node > b.node ? 1 : 0; // Id.compareTo (signed int)
+    return c;
+}
+
+static inline int kind_of(const Ts& t) { return (int)((t.lsb >> 1) & 7); }   // TxnId.java:157-160
+static inline int domain_of(const Ts& t) { return (int)(t.lsb & 1); }        // TxnId.java:162-165
+
+// Txn.Kind.witnesses — primitives/Txn.java:221-245 (+ Kinds.test :140-152)
+static inline bool witnesses(int q, int d) {
+    switch (q) {
+        case AD_KIND_EPHEMERAL_READ:
+        case AD_KIND_READ: return d == AD_KIND_WRITE;                                      // Ws
+        case AD_KIND_WRITE:
+        case AD_KIND_SYNC_POINT: return d == AD_KIND_READ || d == AD_KIND_WRITE;          // RsOrWs
+        case AD_KIND_EXCLUSIVE_SYNC_POINT:                                                 // AnyGloballyVisible
+            return d == AD_KIND_READ || d == AD_KIND_WRITE || d == AD_KIND_SYNC_POINT || d == AD_KIND_EXCLUSIVE_SYNC_POINT;
+        default: return false;
+    }
+}
+static inline bool globally_visible(int k) {   // Txn.Kind.isGloballyVisible :187-201
+    return k == AD_KIND_READ || k == AD_KIND_WRITE || k == AD_KIND_SYNC_POINT || k == AD_KIND_EXCLUSIVE_SYNC_POINT;
+}
+// CommandsForKey.manages :185-188
+static inline bool manages(const Ts& t) { return domain_of(t) == AD_DOMAIN_KEY && globally_visible(kind_of(t)); }
+// CommandsForKey.managesExecution :196-199 (Write.witnesses(kind) && key)
+static inline bool manages_execution(const Ts& t) {
+    return domain_of(t) == AD_DOMAIN_KEY && witnesses(AD_KIND_WRITE, kind_of(t));
+}
+// Txn.Kind.awaitsOnlyDeps :211-214
+static inline bool awaits_only_deps(int k) { return k == AD_KIND_EXCLUSIVE_SYNC_POINT || k == AD_KIND_EPHEMERAL_READ; }
+
+// InternalStatus.isCommitted-and-visible-in-committedByExecuteAt (CommandsForKey.java:659,667)
+static inline bool in_committed_by_execute_at(int st) {
+    return st >= AD_ST_COMMITTED && st != AD_ST_INVALID;
+}
+
+struct RangeK { uint64_t s, e; };   // Range.EndInclusive (start, end]
+static inline int range_cmp(const RangeK& a, const RangeK& b) {  // Range.compare — Range.java:310-317
+    int c = cmpu(a.s, b.s);
+    if (c == 0) c = cmpu(a.e, b.e);
+    return c;
+}
+static inline bool range_contains(const RangeK& r, uint64_t k) { return r.s < k && k <= r.e; }   // EndInclusive.compareTo :48-55
+static inline bool ranges_intersect(const RangeK& a, const RangeK& b) {                           // compareIntersecting :296-305
+    return !(a.s >= b.e) && !(a.e <= b.s);
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Canonical relation map (one per txn per class): KeyDeps / RangeDeps raw layout.                 */
+/* ---------------------------------------------------------------------------------------------- */
+template <class K>
+struct Csr {
+    std::vector<K> keys;          // sorted unique
+    std::vector<uint32_t> vals;   // sorted unique txn ranks
+    std::vector<int32_t> k2t;     // keys.size() end offsets, then value indices
+    bool empty() const { return k2t.size() == keys.size(); }
+};
+
+template <class K> struct KeyOps;
+template <> struct KeyOps<uint64_t> {
+    static int cmp(uint64_t a, uint64_t b) { return cmpu(a, b); }
+};
+template <> struct KeyOps<RangeK> {
+    static int cmp(const RangeK& a, const RangeK& b) { return range_cmp(a, b); }
+};
+
+// RelationMultiMap.AbstractBuilder — utils/RelationMultiMap.java:88-271 (restated on value ranks,
+// which order exactly as TxnId.compareTo because the batch is TxnId-sorted).
+template <class K>
+struct Builder {
+    std::vector<K> keys;
+    std::vector<int> keyLimits;
+    std::vector<uint32_t> kv;     // keysToValues
+    int keyOffset = 0;
+    bool hasOrderedKeys = true, hasOrderedValues = true;
+
+    int totalCount() const { return (int)kv.size(); }
+
+    void nextKey(const K& key) {                                           // :125-145
+        if (!keys.empty() && KeyOps<K>::cmp(keys.back(), key) >= 0) hasOrderedKeys = false;
+        finishKey();
+        keys.push_back(key);
+        keyLimits.push_back(0);
+        hasOrderedValues = true;
+    }
+    void finishKey() {                                                     // :147-173
+        if (totalCount() == keyOffset && !keys.empty()) { keys.pop_back(); keyLimits.pop_back(); return; }
+        if (keys.empty()) return;
+        if (!hasOrderedValues) {
+            std::sort(kv.begin() + keyOffset, kv.end());
+            kv.erase(std::unique(kv.begin() + keyOffset, kv.end()), kv.end());
+        }
+        keyLimits.back() = totalCount();
+        keyOffset = totalCount();
+    }
+    void add(const K& key, uint32_t v) {                                   // :175-180
+        if (keys.empty() || KeyOps<K>::cmp(keys.back(), key) != 0) nextKey(key);
+        add(v);
+    }
+    void add(uint32_t v) {                                                 // :185-199
+        if (hasOrderedValues && totalCount() > keyOffset && kv.back() >= v) hasOrderedValues = false;
+        kv.push_back(v);
+    }
+    Csr<K> build() {                                                       // :201-260
+        Csr<K> out;
+        if (totalCount() == 0) return out;                                 // none()
+        finishKey();
+        std::vector<uint32_t> uniq(kv);
+        std::sort(uniq.begin(), uniq.end());
+        uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+        const int keyCount = (int)keys.size();
+        std::vector<int> order(keyCount);
+        for (int i = 0; i < keyCount; ++i) order[i] = i;
+        if (!hasOrderedKeys) {
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return KeyOps<K>::cmp(keys[a], keys[b]) < 0; });
+            for (int i = 1; i < keyCount; ++i)
+                if (KeyOps<K>::cmp(keys[order[i - 1]], keys[order[i]]) == 0)
+                    throw std::invalid_argument("Key has been visited more than once");   // :234-239
+        }
+        out.keys.resize(keyCount);
+        out.k2t.assign(keyCount + totalCount(), 0);
+        int offset = keyCount;
+        for (int ki = 0; ki < keyCount; ++ki) {
+            int k = order[ki];
+            out.keys[ki] = keys[k];
+            int from = k == 0 ? 0 : keyLimits[k - 1];
+            int to = keyLimits[k];
+            // foldlIntersection(values, keysToValues[from..to)) -> index of each value (:252-255)
+            size_t li = 0;
+            for (int ri = from; ri < to; ++ri) {
+                while (uniq[li] < kv[ri]) ++li;
+                out.k2t[offset++] = (int32_t)li;
+            }
+            out.k2t[ki] = offset;
+        }
+        out.k2t.resize(offset);
+        out.vals = std::move(uniq);
+        return out;
+    }
+};
+
+// RelationMultiMap.linearUnion — utils/RelationMultiMap.java:562-816 (general branch; the two
+// pass-through branches :583-730 return an input that equals the union, so the result is identical).
+template <class K>
+static Csr<K> linear_union(const Csr<K>& L, const Csr<K>& R) {
+    if (L.empty()) return R;                               // KeyDeps.with :252-253
+    if (R.empty()) return L;
+    Csr<K> out;
+    // SortedArrays.linearUnion on keys and values (SortedArrays.java:198-333)
+    {
+        size_t i = 0, j = 0;
+        while (i < L.keys.size() || j < R.keys.size()) {
+            int c = i == L.keys.size() ? 1 : j == R.keys.size() ? -1 : KeyOps<K>::cmp(L.keys[i], R.keys[j]);
+            if (c <= 0) { out.keys.push_back(L.keys[i]); ++i; if (c == 0) ++j; }
+            else { out.keys.push_back(R.keys[j]); ++j; }
+        }
+        std::set_union(L.vals.begin(), L.vals.end(), R.vals.begin(), R.vals.end(), std::back_inserter(out.vals));
+    }
+    // remapToSuperset (SortedArrays.java:1249-1275)
+    auto remap = [&](const std::vector<uint32_t>& v) {
+        std::vector<int32_t> m(v.size());
+        size_t o = 0;
+        for (size_t x = 0; x < v.size(); ++x) { while (out.vals[o] < v[x]) ++o; m[x] = (int32_t)o; }
+        return m;
+    };
+    std::vector<int32_t> remapL = remap(L.vals), remapR = remap(R.vals);
+    const int nk = (int)out.keys.size();
+    out.k2t.assign(nk, 0);
+    int lk = 0, rk = 0, ok = 0;
+    int l = (int)L.keys.size(), r = (int)R.keys.size();
+    const int lkn = (int)L.keys.size(), rkn = (int)R.keys.size();
+    while (lk < lkn && rk < rkn) {                                      // :736-783
+        int ck = KeyOps<K>::cmp(L.keys[lk], R.keys[rk]);
+        if (ck < 0) {
+            while (l < L.k2t[lk]) out.k2t.push_back(remapL[L.k2t[l++]]);
+            out.k2t[ok++] = (int32_t)out.k2t.size(); lk++;
+        } else if (ck > 0) {
+            while (r < R.k2t[rk]) out.k2t.push_back(remapR[R.k2t[r++]]);
+            out.k2t[ok++] = (int32_t)out.k2t.size(); rk++;
+        } else {
+            while (l < L.k2t[lk] && r < R.k2t[rk]) {
+                int nl = remapL[L.k2t[l]], nr = remapR[R.k2t[r]];
+                if (nl <= nr) { out.k2t.push_back(nl); l += 1; r += nl == nr ? 1 : 0; }
+                else { out.k2t.push_back(nr); ++r; }
+            }
+            while (l < L.k2t[lk]) out.k2t.push_back(remapL[L.k2t[l++]]);
+            while (r < R.k2t[rk]) out.k2t.push_back(remapR[R.k2t[r++]]);
+            out.k2t[ok++] = (int32_t)out.k2t.size(); rk++; lk++;
+        }
+    }
+    while (lk < lkn) { while (l < L.k2t[lk]) out.k2t.push_back(remapL[L.k2t[l++]]); out.k2t[ok++] = (int32_t)out.k2t.size(); lk++; }
+    while (rk < rkn) { while (r < R.k2t[rk]) out.k2t.push_back(remapR[R.k2t[r++]]); out.k2t[ok++] = (int32_t)out.k2t.size(); rk++; }
+    return out;
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* The batch                                                                                       */
+/* ---------------------------------------------------------------------------------------------- */
+struct Batch {
+    size_t n = 0;
+    std::vector<Ts> tx, ex;
+    std::vector<uint8_t> st;
+    std::vector<uint32_t> key_off, range_off;
+    std::vector<uint64_t> keys;
+    std::vector<RangeK> ranges;
+
+    explicit Batch(const ad_batch* b) {
+        n = b->n;
+        tx.resize(n); ex.resize(n); st.assign(b->status, b->status + n);
+        for (size_t i = 0; i < n; ++i) {
+            tx[i] = Ts{b->txn_msb[i], b->txn_lsb[i], b->txn_node[i]};
+            ex[i] = Ts{b->exec_msb[i], b->exec_lsb[i], b->exec_node[i]};
+        }
+        key_off.assign(b->key_off, b->key_off + n + 1);
+        keys.assign(b->keys, b->keys + key_off[n]);
+        range_off.assign(n + 1, 0);
+        if (b->range_off) {
+            range_off.assign(b->range_off, b->range_off + n + 1);
+            ranges.resize(range_off[n]);
+            for (size_t q = 0; q < ranges.size(); ++q) ranges[q] = RangeK{b->range_start[q], b->range_end[q]};
+        }
+        for (size_t i = 1; i < n; ++i)
+            if (ts_cmp(tx[i - 1], tx[i]) >= 0) throw std::invalid_argument("batch TxnIds must be strictly ascending");
+    }
+};
+
+struct TxnDeps { Csr<uint64_t> key, direct; Csr<RangeK> range; };
+
+struct Config {
+    uint32_t window = 32, replicas = 1; uint64_t seed = 0; uint32_t drop_thresh = 0;
+};
+
+/* CommandsForKey for one key: byId = ranks of managed txns touching the key, ascending. */
+struct Cfk {
+    uint64_t key;
+    std::vector<uint32_t> byId;
+    // baseline pruning state (Pruning.java:164-233): a prefix of byId that can never again be
+    // emitted (committed, executeAt below the running maxCommittedWriteBefore) is dropped.
+    size_t prunedBefore = 0;
+    bool hasPrunedMaxWrite = false;
+    Ts prunedMaxWrite{0, 0, 0};
+};
+
+struct Oracle {
+    const Batch& B;
+    Config cfg;
+    bool prune;
+    std::vector<Cfk> cfks;              // sorted by key
+    std::vector<uint32_t> rangeTxns;    // ranks of range-domain txns (rangeCommands registry)
+
+    Oracle(const Batch& b, const Config& c, bool prune_) : B(b), cfg(c), prune(prune_) {
+        std::map<uint64_t, std::vector<uint32_t>> m;
+        for (uint32_t i = 0; i < B.n; ++i) {
+            if (domain_of(B.tx[i]) == AD_DOMAIN_RANGE) { rangeTxns.push_back(i); continue; }
+            if (!manages(B.tx[i])) continue;   // EphemeralRead etc: never registered in CFK
+            for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) m[B.keys[p]].push_back(i);
+        }
+        for (auto& e : m) { Cfk c2; c2.key = e.first; c2.byId = std::move(e.second); cfks.push_back(std::move(c2)); }
+    }
+
+    bool in_window(uint32_t i, uint32_t j) const { return cfg.window > 0 && (uint64_t)j + cfg.window >= i; }
+    // status of j as seen when i is PreAccepted (SURVEY §8d status model)
+    int seen_status(uint32_t i, uint32_t j) const { return in_window(i, j) ? (int)AD_ST_PREACCEPTED : (int)B.st[j]; }
+    bool dropped(uint32_t view, uint32_t i, uint32_t j) const {
+        return in_window(i, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, i, j) < cfg.drop_thresh;
+    }
+
+    // CommandsForKey.mapReduceActive(startedBefore = TxnId_i, testKind = kind_i.witnesses()) — CommandsForKey.java:925-983
+    template <class F>
+    void map_reduce_active(Cfk& cfk, uint32_t i, uint32_t view, F&& emit) {
+        const Ts& bound = B.tx[i];
+        const int qkind = kind_of(bound);
+        // int end = insertPos(startedBefore)  (:929, :1373-1378); byId is rank-ordered
+        size_t end = std::lower_bound(cfk.byId.begin(), cfk.byId.end(), i) - cfk.byId.begin();
+        // maxCommittedWriteBefore (:930-943): the greatest executeAt of a committed Write in
+        // committedByExecuteAt with executeAt < startedBefore.  committedByExecuteAt holds the byId
+        // entries (all have TxnId < bound here) whose status >= COMMITTED and != INVALID.
+        bool hasM = cfk.hasPrunedMaxWrite;
+        Ts M = cfk.prunedMaxWrite;
+        for (size_t x = cfk.prunedBefore; x < end; ++x) {
+            uint32_t j = cfk.byId[x];
+            if (!in_committed_by_execute_at(seen_status(i, j))) continue;
+            if (kind_of(B.tx[j]) != AD_KIND_WRITE) continue;
+            if (ts_cmp(B.ex[j], bound) >= 0) continue;
+            if (!hasM || ts_cmp(B.ex[j], M) > 0) { M = B.ex[j]; hasM = true; }
+        }
+        for (size_t x = cfk.prunedBefore; x < end; ++x) {                       // :945-965
+            uint32_t j = cfk.byId[x];
+            const Ts& txn = B.tx[j];
+            if (!witnesses(qkind, kind_of(txn))) continue;
+            switch (seen_status(i, j)) {
+                case AD_ST_COMMITTED: case AD_ST_STABLE: case AD_ST_APPLIED:
+                    if (!hasM || ts_cmp(B.ex[j], M) >= 0 || !witnesses(AD_KIND_WRITE, kind_of(txn))) break;
+                    continue;                                                    // elided (falls into :959-961)
+                case AD_ST_TRANSITIVELY_KNOWN: case AD_ST_INVALID:
+                    continue;
+                default: break;
+            }
+            if (dropped(view, i, j)) continue;
+            emit(cfk.key, j);
+        }
+        // prunedBefore future-dependency branch (:967-980) never fires: queries arrive in TxnId
+        // order, so startedBefore > prunedBefore always.
+        if (prune && hasM) {
+            // Pruning.maybePrune restated for the steady state: later queries have a larger bound and
+            // a larger-or-equal M, so committed entries (seen committed by every later query) with
+            // executeAt < M, before any non-prunable entry, are never emitted again.
+            size_t x = cfk.prunedBefore;
+            while (x < end) {
+                uint32_t j = cfk.byId[x];
+                if (in_window(i + 1, j)) break;                 // still in flight for the next query
+                int st = B.st[j];
+                bool committed = in_committed_by_execute_at(st);
+                bool skip = st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID;
+                if (!skip && !(committed && ts_cmp(B.ex[j], M) < 0 && witnesses(AD_KIND_WRITE, kind_of(B.tx[j])))) break;
+                if (committed && kind_of(B.tx[j]) == AD_KIND_WRITE && ts_cmp(B.ex[j], bound) < 0) {
+                    if (!cfk.hasPrunedMaxWrite || ts_cmp(B.ex[j], cfk.prunedMaxWrite) > 0) { cfk.prunedMaxWrite = B.ex[j]; cfk.hasPrunedMaxWrite = true; }
+                }
+                ++x;
+            }
+            cfk.prunedBefore = x;
+        }
+    }
+
+    Cfk* find_cfk(uint64_t key) {
+        auto it = std::lower_bound(cfks.begin(), cfks.end(), key, [](const Cfk& c, uint64_t k) { return c.key < k; });
+        return it != cfks.end() && it->key == key ? &*it : nullptr;
+    }
+
+    // PreAccept.calculatePartialDeps (PreAccept.java:245-267) via InMemorySafeStore.mapReduceActive
+    TxnDeps preaccept(uint32_t i, uint32_t view) {
+        Builder<uint64_t> kb, db;
+        Builder<RangeK> rb;
+        const Ts& me = B.tx[i];
+        const int qkind = kind_of(me);
+        // Deps.AbstractBuilder.add — Deps.java:80-106
+        auto emit_key = [&](uint64_t key, uint32_t j) {
+            if (manages_execution(B.tx[j])) kb.add(key, j); else db.add(key, j);
+        };
+        // mapReduceForKey — InMemoryCommandStore.java:272-307
+        if (domain_of(me) == AD_DOMAIN_KEY) {
+            std::vector<uint64_t> ks(B.keys.begin() + B.key_off[i], B.keys.begin() + B.key_off[i + 1]);
+            std::sort(ks.begin(), ks.end());                     // Keys are sorted
+            for (uint64_t k : ks) { Cfk* c = find_cfk(k); if (c) map_reduce_active(*c, i, view, emit_key); }
+        } else {
+            for (uint32_t q = B.range_off[i]; q < B.range_off[i + 1]; ++q) {
+                const RangeK& r = B.ranges[q];
+                // commandsForKey.subMap(start, false, end, true)
+                auto it = std::upper_bound(cfks.begin(), cfks.end(), r.s, [](uint64_t k, const Cfk& c) { return k < c.key; });
+                for (; it != cfks.end() && it->key <= r.e; ++it) map_reduce_active(*it, i, view, emit_key);
+            }
+        }
+        // mapReduceRangesInternal(STARTED_BEFORE, ANY_DEPS, ANY_STATUS) — InMemoryCommandStore.java:884-1017
+        std::vector<std::pair<RangeK, std::vector<uint32_t>>> collect;   // TreeMap<Range, List> by Range::compare
+        for (uint32_t j : rangeTxns) {
+            if (j >= i) break;                                       // txnId.compareTo(testTimestamp) >= 0 -> return
+            if (seen_status(i, j) == AD_ST_INVALID) continue;        // saveStatus >= Erased
+            if (!witnesses(qkind, kind_of(B.tx[j]))) continue;
+            if (dropped(view, i, j)) continue;
+            for (uint32_t q = B.range_off[j]; q < B.range_off[j + 1]; ++q) {
+                const RangeK& r = B.ranges[q];
+                bool hit = false;
+                if (domain_of(me) == AD_DOMAIN_KEY) {
+                    for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1] && !hit; ++p) hit = range_contains(r, B.keys[p]);
+                } else {
+                    for (uint32_t p = B.range_off[i]; p < B.range_off[i + 1] && !hit; ++p) hit = ranges_intersect(r, B.ranges[p]);
+                }
+                if (!hit) continue;
+                auto it = std::lower_bound(collect.begin(), collect.end(), r, [](const std::pair<RangeK, std::vector<uint32_t>>& e, const RangeK& x) { return range_cmp(e.first, x) < 0; });
+                if (it == collect.end() || range_cmp(it->first, r) != 0) it = collect.insert(it, {r, {}});
+                if (it->second.empty() || it->second.back() != j) it->second.push_back(j);
+            }
+        }
+        for (auto& e : collect) for (uint32_t j : e.second) rb.add(e.first, j);
+        TxnDeps d;
+        d.key = kb.build(); d.direct = db.build(); d.range = rb.build();
+        return d;
+    }
+};
+
+/* Flattened batched CSR (ad_csr_out layout, compacted txn lists). */
+struct Flat {
+    std::vector<uint32_t> key_off{0}, k2t_off{0}, txn_off{0}, txns;
+    std::vector<uint64_t> keys;
+    std::vector<int32_t> k2t;
+    void push(const Csr<uint64_t>& c) {
+        keys.insert(keys.end(), c.keys.begin(), c.keys.end());
+        key_off.push_back((uint32_t)(key_off.back() + c.keys.size()));
+        k2t.insert(k2t.end(), c.k2t.begin(), c.k2t.end());
+        k2t_off.push_back((uint32_t)k2t.size());
+        txns.insert(txns.end(), c.vals.begin(), c.vals.end());
+        txn_off.push_back((uint32_t)txns.size());
+    }
+    void push(const Csr<RangeK>& c) {
+        for (auto& r : c.keys) { keys.push_back(r.s); keys.push_back(r.e); }
+        key_off.push_back((uint32_t)(key_off.back() + c.keys.size()));
+        k2t.insert(k2t.end(), c.k2t.begin(), c.k2t.end());
+        k2t_off.push_back((uint32_t)k2t.size());
+        txns.insert(txns.end(), c.vals.begin(), c.vals.end());
+        txn_off.push_back((uint32_t)txns.size());
+    }
+};
+
+}  // namespace
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Execution levels                                                                                 */
+/* ---------------------------------------------------------------------------------------------- */
+namespace {
+
+// Execution order over the committed batch.  Every edge D -> T increases executeAt, so processing in
+// executeAt order is a topological order and level[T] = 1 + max level over predecessors (0 if none):
+//  * managed T (key Read/Write): per key, every earlier-executeAt managed txn T witnesses
+//    (CommandsForKey.notifyManaged :1208-1289 with unappliedCounters :1291-1330: a Write waits for
+//    all earlier Reads+Writes, a Read for earlier Writes; CommandsForKeyTest.Canon.readyToExecute :169-174),
+//  * every T: direct-key and range deps with executeAt < T's (Commands.updateWaitingOn :740-755),
+//  * unmanaged T (range domain): per key of its keyDeps, every managed txn with executeAt <= the
+//    greatest executeAt among its deps on that key below its own (Updating.updateUnmanaged :740-757
+//    -> Unmanaged APPLY "wait for it and all earlier txn to Apply", CommandsForKey.java:437-445).
+static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDeps>& merged, std::vector<uint32_t>& order) {
+    const uint32_t n = (uint32_t)B.n;
+    for (uint32_t i = 0; i < n; ++i) {
+        int k = kind_of(B.tx[i]);
+        if (awaits_only_deps(k) || k == AD_KIND_SYNC_POINT || k == AD_KIND_LOCAL_ONLY)
+            throw std::invalid_argument("exec levels: sync points / ephemeral reads not supported in batch execution order");
+    }
+    std::vector<uint32_t> byExec(n);
+    for (uint32_t i = 0; i < n; ++i) byExec[i] = i;
+    std::sort(byExec.begin(), byExec.end(), [&](uint32_t a, uint32_t b) { return ts_cmp(B.ex[a], B.ex[b]) < 0; });
+    std::vector<int64_t> level(n, -1);
+    struct Chain { std::vector<Ts> exec; std::vector<int64_t> pmAll; int64_t maxAll = -1, maxW = -1; };
+    std::map<uint64_t, Chain> chains;
+    for (uint32_t t : byExec) {
+        int64_t lv = -1;
+        const Ts& me = B.tx[t];
+        const Ts& myExec = B.ex[t];
+        const TxnDeps& d = merged[t];
+        auto dep_pred = [&](uint32_t dep) {
+            if (ts_cmp(B.ex[dep], myExec) < 0) lv = std::max(lv, level[dep]);
+        };
+        for (uint32_t v : d.direct.vals) dep_pred(v);
+        for (uint32_t v : d.range.vals) dep_pred(v);
+        if (manages_execution(me)) {
+            bool w = kind_of(me) == AD_KIND_WRITE;
+            for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
+                auto it = chains.find(B.keys[p]);
+                if (it == chains.end()) continue;
+                lv = std::max(lv, w ? it->second.maxAll : it->second.maxW);
+            }
+        } else {
+            // unmanaged: per key of keyDeps, bound = max executeAt of its deps there below its own
+            const Csr<uint64_t>& kd = d.key;
+            for (size_t ki = 0; ki < kd.keys.size(); ++ki) {
+                int from = ki == 0 ? (int)kd.keys.size() : kd.k2t[ki - 1];
+                bool has = false; Ts bnd{0, 0, 0};
+                for (int x = from; x < kd.k2t[ki]; ++x) {
+                    uint32_t dep = kd.vals[kd.k2t[x]];
+                    if (ts_cmp(B.ex[dep], myExec) < 0 && (!has || ts_cmp(B.ex[dep], bnd) > 0)) { bnd = B.ex[dep]; has = true; }
+                }
+                if (!has) continue;
+                auto it = chains.find(kd.keys[ki]);
+                if (it == chains.end()) continue;
+                Chain& c = it->second;
+                size_t pos = std::upper_bound(c.exec.begin(), c.exec.end(), bnd, [](const Ts& a, const Ts& b) { return ts_cmp(a, b) < 0; }) - c.exec.begin();
+                if (pos > 0) lv = std::max(lv, c.pmAll[pos - 1]);
+            }
+        }
+        level[t] = lv + 1;
+        if (manages_execution(me)) {
+            bool w = kind_of(me) == AD_KIND_WRITE;
+            for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
+                Chain& c = chains[B.keys[p]];
+                c.maxAll = std::max(c.maxAll, level[t]);
+                if (w) c.maxW = std::max(c.maxW, level[t]);
+                c.exec.push_back(myExec);
+                c.pmAll.push_back(c.maxAll);
+            }
+        }
+    }
+    std::vector<uint32_t> out(n);
+    for (uint32_t i = 0; i < n; ++i) out[i] = (uint32_t)level[i];
+    order = byExec;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return out[a] < out[b]; });
+    return out;
+}
+
+}  // namespace
+
+/* ---------------------------------------------------------------------------------------------- */
+/* C API for tests / bench (ctypes)                                                                 */
+/* ---------------------------------------------------------------------------------------------- */
+struct oracle_result {
+    uint32_t replicas = 0;
+    std::vector<Flat> deps;      // [view * 3 + class]
+    std::vector<Flat> merged;    // [class]
+    std::vector<uint32_t> level, order;
+    double t_deps = 0, t_merge = 0, t_levels = 0;
+    uint64_t deps_entries = 0, merged_entries = 0;
+    std::string error;
+};
+
+extern "C" {
+
+/* flags: bit0 = pruning (baseline mode), bit1 = merge, bit2 = levels; threads: key-range shards
+ * for the deps stage (InMemoryCommandStore.SingleThread per shard + PreAccept.reduce). */
+oracle_result* oracle_run(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads) {
+    oracle_result* res = new oracle_result();
+    try {
+        Batch B(b);
+        Config cfg;
+        cfg.window = c->window; cfg.replicas = c->replicas ? c->replicas : 1; cfg.seed = c->seed;
+        cfg.drop_thresh = ad_drop_threshold(c->drop_p);
+        res->replicas = cfg.replicas;
+        const uint32_t R = cfg.replicas;
+        const uint32_t n = (uint32_t)B.n;
+        std::vector<std::vector<TxnDeps>> all(R, std::vector<TxnDeps>(n));
+        auto t0 = std::chrono::steady_clock::now();
+        if (threads <= 1) {
+            for (uint32_t v = 0; v < R; ++v) {
+                Oracle o(B, cfg, flags & 1);
+                for (uint32_t i = 0; i < n; ++i) all[v][i] = o.preaccept(i, v);
+            }
+        } else {
+            // Shard the key space into `threads` contiguous ranges of the batch's distinct keys
+            // (ShardDistributor.EvenSplit, local/ShardDistributor.java:32-80), one single-threaded
+            // store per shard; each store answers the part of every query that falls in its range;
+            // PreAccept.reduce (PreAccept.java:141-156) then combines per txn with Deps.with.
+            // Range txns / range deps are kept on shard 0 only (single-store semantics).
+            std::vector<uint64_t> uk(B.keys);
+            std::sort(uk.begin(), uk.end()); uk.erase(std::unique(uk.begin(), uk.end()), uk.end());
+            std::vector<uint64_t> bounds;  // shard s owns keys < bounds[s]
+            for (uint32_t s = 1; s < threads; ++s) bounds.push_back(uk.empty() ? 0 : uk[std::min(uk.size() - 1, uk.size() * s / threads)]);
+            bounds.push_back(UINT64_MAX);
+            if (B.range_off[n] > 0) throw std::invalid_argument("threaded oracle: range txns unsupported");
+            std::vector<std::vector<std::vector<TxnDeps>>> part(threads, std::vector<std::vector<TxnDeps>>(R, std::vector<TxnDeps>(n)));
+            std::vector<std::thread> pool;
+            for (uint32_t s = 0; s < threads; ++s) {
+                pool.emplace_back([&, s]() {
+                    uint64_t lo = s == 0 ? 0 : bounds[s - 1], hi = bounds[s];
+                    // a batch view containing only this shard's keys
+                    ad_batch sb = *b;
+                    std::vector<uint32_t> off(n + 1, 0); std::vector<uint64_t> ks;
+                    for (uint32_t i = 0; i < n; ++i) {
+                        for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p)
+                            if (B.keys[p] >= lo && (B.keys[p] < hi || (hi == UINT64_MAX))) ks.push_back(B.keys[p]);
+                        off[i + 1] = (uint32_t)ks.size();
+                    }
+                    sb.key_off = off.data(); sb.keys = ks.data();
+                    Batch SB(&sb);
+                    for (uint32_t v = 0; v < R; ++v) {
+                        Oracle o(SB, cfg, flags & 1);
+                        for (uint32_t i = 0; i < n; ++i) part[s][v][i] = o.preaccept(i, v);
+                    }
+                });
+            }
+            for (auto& th : pool) th.join();
+            for (uint32_t v = 0; v < R; ++v)
+                for (uint32_t i = 0; i < n; ++i) {
+                    TxnDeps acc = part[0][v][i];
+                    for (uint32_t s = 1; s < threads; ++s) {
+                        acc.key = linear_union(acc.key, part[s][v][i].key);
+                        acc.direct = linear_union(acc.direct, part[s][v][i].direct);
+                    }
+                    all[v][i] = std::move(acc);
+                }
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        res->t_deps = std::chrono::duration<double>(t1 - t0).count();
+        res->deps.resize(R * AD_NUM_CLASSES);
+        for (uint32_t v = 0; v < R; ++v)
+            for (uint32_t i = 0; i < n; ++i) {
+                res->deps[v * 3 + 0].push(all[v][i].key);
+                res->deps[v * 3 + 1].push(all[v][i].direct);
+                res->deps[v * 3 + 2].push(all[v][i].range);
+                res->deps_entries += all[v][i].key.k2t.size() - all[v][i].key.keys.size()
+                                   + all[v][i].direct.k2t.size() - all[v][i].direct.keys.size()
+                                   + all[v][i].range.k2t.size() - all[v][i].range.keys.size();
+            }
+        std::vector<TxnDeps> merged;
+        if (flags & 6) {
+            auto t2 = std::chrono::steady_clock::now();
+            // Deps.merge(list) = per class LinearMerger over the replies in order (Deps.java:281-286)
+            merged.resize(n);
+            for (uint32_t i = 0; i < n; ++i) {
+                TxnDeps acc;
+                for (uint32_t v = 0; v < R; ++v) {
+                    acc.key = linear_union(acc.key, all[v][i].key);
+                    acc.direct = linear_union(acc.direct, all[v][i].direct);
+                    acc.range = linear_union(acc.range, all[v][i].range);
+                }
+                merged[i] = std::move(acc);
+            }
+            auto t3 = std::chrono::steady_clock::now();
+            res->t_merge = std::chrono::duration<double>(t3 - t2).count();
+            res->merged.resize(AD_NUM_CLASSES);
+            for (uint32_t i = 0; i < n; ++i) {
+                res->merged[0].push(merged[i].key);
+                res->merged[1].push(merged[i].direct);
+                res->merged[2].push(merged[i].range);
+                res->merged_entries += merged[i].key.k2t.size() - merged[i].key.keys.size()
+                                     + merged[i].direct.k2t.size() - merged[i].direct.keys.size()
+                                     + merged[i].range.k2t.size() - merged[i].range.keys.size();
+            }
+        }
+        if (flags & 4) {
+            auto t4 = std::chrono::steady_clock::now();
+            res->level = exec_levels(B, merged, res->order);
+            auto t5 = std::chrono::steady_clock::now();
+            res->t_levels = std::chrono::duration<double>(t5 - t4).count();
+        }
+    } catch (const std::exception& e) {
+        res->error = e.what();
+    }
+    return res;
+}
+
+const char* oracle_error(const oracle_result* r) { return r->error.empty() ? nullptr : r->error.c_str(); }
+
+static const Flat* pick(const oracle_result* r, int stage, uint32_t view, uint32_t cls) {
+    if (cls >= AD_NUM_CLASSES) return nullptr;
+    if (stage == 0) { if (view >= r->replicas || r->deps.empty()) return nullptr; return &r->deps[view * 3 + cls]; }
+    if (r->merged.empty()) return nullptr;
+    return &r->merged[cls];
+}
+
+int oracle_sizes(const oracle_result* r, int stage, uint32_t view, uint32_t cls, ad_csr_sizes* out) {
+    const Flat* f = pick(r, stage, view, cls);
+    if (!f) return AD_ERR_ARGUMENT;
+    out->n = f->key_off.size() - 1;
+    out->keys = f->key_off.back();
+    out->k2t = f->k2t.size();
+    out->txn_cap = f->txns.size();
+    out->txns = f->txns.size();
+    return AD_OK;
+}
+
+int oracle_fetch(const oracle_result* r, int stage, uint32_t view, uint32_t cls, ad_csr_out* out) {
+    const Flat* f = pick(r, stage, view, cls);
+    if (!f) return AD_ERR_ARGUMENT;
+    std::memcpy(out->key_off, f->key_off.data(), f->key_off.size() * 4);
+    std::memcpy(out->keys, f->keys.data(), f->keys.size() * 8);
+    std::memcpy(out->k2t_off, f->k2t_off.data(), f->k2t_off.size() * 4);
+    std::memcpy(out->k2t, f->k2t.data(), f->k2t.size() * 4);
+    std::memcpy(out->txn_off, f->txn_off.data(), f->txn_off.size() * 4);
+    std::memcpy(out->txns, f->txns.data(), f->txns.size() * 4);
+    return AD_OK;
+}
+
+int oracle_levels(const oracle_result* r, uint32_t* level, uint32_t* order) {
+    if (r->level.empty()) return AD_ERR_STATE;
+    if (level) std::memcpy(level, r->level.data(), r->level.size() * 4);
+    if (order) std::memcpy(order, r->order.data(), r->order.size() * 4);
+    return AD_OK;
+}
+
+void oracle_stats(const oracle_result* r, double* times3, uint64_t* entries2) {
+    times3[0] = r->t_deps; times3[1] = r->t_merge; times3[2] = r->t_levels;
+    entries2[0] = r->deps_entries; entries2[1] = r->merged_entries;
+}
+
+void oracle_free(oracle_result* r) { delete r; }
+
+/* --- primitive entry points for the restated KeyDepsTest / SortedArraysTest properties --------- */
+
+/* RelationMultiMap.AbstractBuilder over (key, value) pairs in the given add order. Returns the
+ * canonical CSR in caller buffers sized n_keys+n_pairs (k2t), n_pairs (keys), n_pairs (vals). */
+int oracle_build(const uint64_t* keys, const uint32_t* vals, size_t n, uint64_t* out_keys, size_t* n_keys,
+                 uint32_t* out_vals, size_t* n_vals, int32_t* out_k2t, size_t* n_k2t) {
+    try {
+        Builder<uint64_t> bld;
+        for (size_t x = 0; x < n; ++x) bld.add(keys[x], vals[x]);
+        Csr<uint64_t> c = bld.build();
+        std::copy(c.keys.begin(), c.keys.end(), out_keys); *n_keys = c.keys.size();
+        std::copy(c.vals.begin(), c.vals.end(), out_vals); *n_vals = c.vals.size();
+        std::copy(c.k2t.begin(), c.k2t.end(), out_k2t); *n_k2t = c.k2t.size();
+        return AD_OK;
+    } catch (const std::invalid_argument&) { return AD_ERR_ARGUMENT; }
+}
+
+/* RelationMultiMap.linearUnion of two canonical CSRs. */
+int oracle_union(const uint64_t* lk, size_t nlk, const uint32_t* lv, size_t nlv, const int32_t* lm, size_t nlm,
+                 const uint64_t* rk, size_t nrk, const uint32_t* rv, size_t nrv, const int32_t* rm, size_t nrm,
+                 uint64_t* ok, size_t* nok, uint32_t* ov, size_t* nov, int32_t* om, size_t* nom) {
+    Csr<uint64_t> L, R;
+    L.keys.assign(lk, lk + nlk); L.vals.assign(lv, lv + nlv); L.k2t.assign(lm, lm + nlm);
+    R.keys.assign(rk, rk + nrk); R.vals.assign(rv, rv + nrv); R.k2t.assign(rm, rm + nrm);
+    Csr<uint64_t> o = linear_union(L, R);
+    std::copy(o.keys.begin(), o.keys.end(), ok); *nok = o.keys.size();
+    std::copy(o.vals.begin(), o.vals.end(), ov); *nov = o.vals.size();
+    std::copy(o.k2t.begin(), o.k2t.end(), om); *nom = o.k2t.size();
+    return AD_OK;
+}
+
+}  // extern "C"
