@@ -1,0 +1,155 @@
+"""Python binding of libaccord_deps.so (the gfx950 deps engine) over its C-ABI.
+
+This is a thin ctypes layer mirroring the reference operations a host drives on this path:
+
+* ``preaccept_deps()``  — PreAccept.calculatePartialDeps for every txn of the batch, per replica view
+  (messages/PreAccept.java:245-267)
+* ``merge()``           — Deps.merge of the replica replies (primitives/Deps.java:281-286)
+* ``exec_levels()``     — execution order (local/Commands.java:617-821, CommandsForKey.notifyManaged)
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible the constructor raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libaccord_deps.so")
+_LIB = None
+
+
+class AccordDepsError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__("%s (rc=%d)" % (msg, rc))
+        self.rc = rc
+
+
+class IllegalArgumentException(AccordDepsError):
+    pass
+
+
+class IllegalStateException(AccordDepsError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libaccord_deps.so not built (run `make -C cassandra-accord_amd` / __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.ad_open.argtypes = [C.c_int, C.POINTER(abi.AdConfig), C.POINTER(vp)]
+        L.ad_close.argtypes = [vp]
+        L.ad_close.restype = None
+        L.ad_last_error.argtypes = [vp]
+        L.ad_last_error.restype = C.c_char_p
+        L.ad_device_count.restype = C.c_int
+        L.ad_load_batch.argtypes = [vp, C.POINTER(abi.AdBatch)]
+        L.ad_preaccept_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
+        L.ad_fetch_deps.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut)]
+        L.ad_merge_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
+        L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
+        L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ad_run_pipeline.argtypes = [vp]
+        L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
+        L.ad_shard_bounds.argtypes = [C.POINTER(C.c_uint64), C.c_size_t, C.c_uint32, C.POINTER(C.c_uint64)]
+        _LIB = L
+    return _LIB
+
+
+EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
+            "ad_fetch_deps", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
+            "ad_run_pipeline", "ad_last_times", "ad_shard_bounds")
+
+
+class DepsEngine:
+    """One CommandStore shard on one GPU (an ad_handle)."""
+
+    def __init__(self, device=0, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1):
+        self.cfg = abi.make_config(window, replicas, drop_p, seed)
+        self.replicas = replicas
+        h = C.c_void_p()
+        rc = lib().ad_open(device, C.byref(self.cfg), C.byref(h))
+        if rc != abi.AD_OK:
+            raise AccordDepsError(rc, "ad_open(device=%d) failed" % device)
+        self.h = h
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ad_close(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc == abi.AD_OK:
+            return
+        msg = "%s: %s" % (what, lib().ad_last_error(self.h).decode())
+        if rc == abi.AD_ERR_ARGUMENT:
+            raise IllegalArgumentException(rc, msg)
+        if rc == abi.AD_ERR_STATE:
+            raise IllegalStateException(rc, msg)
+        raise AccordDepsError(rc, msg)
+
+    def load(self, batch):
+        self._batch = abi.make_batch(batch)
+        self.n = batch["n"]
+        self._check(lib().ad_load_batch(self.h, C.byref(self._batch)), "ad_load_batch")
+
+    def preaccept_deps(self):
+        sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
+        self._check(lib().ad_preaccept_deps(self.h, sizes), "ad_preaccept_deps")
+        self._dep_sizes = sizes
+        return sizes
+
+    def fetch_deps(self, view, cls):
+        s = self._dep_sizes[view * abi.NUM_CLASSES + cls]
+        out = abi.Csr.alloc(s, is_range=(cls == abi.CLASS_RANGE))
+        o = out.as_out()
+        self._check(lib().ad_fetch_deps(self.h, view, cls, C.byref(o)), "ad_fetch_deps")
+        return out
+
+    def merge(self):
+        sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
+        self._check(lib().ad_merge_deps(self.h, sizes), "ad_merge_deps")
+        self._merge_sizes = sizes
+        return sizes
+
+    def fetch_merged(self, cls):
+        s = self._merge_sizes[cls]
+        out = abi.Csr.alloc(s, is_range=(cls == abi.CLASS_RANGE))
+        o = out.as_out()
+        self._check(lib().ad_fetch_merged(self.h, cls, C.byref(o)), "ad_fetch_merged")
+        return out
+
+    def exec_levels(self, want_order=True):
+        lv = np.zeros(max(self.n, 1), np.uint32)
+        order = np.zeros(max(self.n, 1), np.uint32) if want_order else None
+        it = C.c_uint32()
+        self._check(lib().ad_exec_levels(self.h, lv.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         order.ctypes.data_as(C.POINTER(C.c_uint32)) if want_order else None,
+                                         C.byref(it)), "ad_exec_levels")
+        return lv[:self.n], (order[:self.n] if want_order else None), it.value
+
+    def run_pipeline(self):
+        self._check(lib().ad_run_pipeline(self.h), "ad_run_pipeline")
+
+    def last_times(self):
+        t = abi.AdStageTimes()
+        self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
+        return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_ if f != "pad_"}
+
+
+def device_count():
+    return lib().ad_device_count()

@@ -1,0 +1,109 @@
+// common.h — device-side encodings and helpers shared by the gfx950 kernels.
+//
+// Timestamps are compared through a packed 64-bit order key ("ts64") built per batch:
+//   ts64 = (msb - msb_min) << (HB+4+NB) | (lowHlc - hlc_min) << (4+NB) | ((lsb>>1)&0xF) << NB | (node - node_min)
+// which orders exactly as Timestamp.compareTo (Timestamp.java:208-217: msb unsigned, lsb>>>16,
+// lsb & 0x1E, node signed) whenever MB+HB+4+NB <= 64 (checked per batch; AD_ERR_UNSUPPORTED otherwise).
+// Equality of ts64 is Timestamp.equals (IDENTITY_LSB = hlc bits | 0x1E, Timestamp.java:41,244-249).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/accord_deps.h"
+
+namespace ad {
+
+constexpr int WAVE = 64;
+constexpr uint64_t TS_NONE = 0xFFFFFFFFFFFFFFFFull;   // "no timestamp" sentinel (never a packed value: widths < 64)
+
+// Per-txn metadata byte: bits 0-2 kind, bit 3 domain, bits 4-6 final InternalStatus.
+__host__ __device__ inline uint32_t meta_kind(uint32_t m) { return m & 7u; }
+__host__ __device__ inline uint32_t meta_domain(uint32_t m) { return (m >> 3) & 1u; }
+__host__ __device__ inline uint32_t meta_status(uint32_t m) { return (m >> 4) & 7u; }
+
+// Txn.Kind.witnesses (primitives/Txn.java:221-245, Kinds.test :140-152)
+//   Read/EphemeralRead -> Ws; Write/SyncPoint -> RsOrWs; ExclusiveSyncPoint -> AnyGloballyVisible.
+__host__ __device__ inline bool witnesses(uint32_t q, uint32_t d) {
+    switch (q) {
+        case AD_KIND_READ:
+        case AD_KIND_EPHEMERAL_READ: return d == AD_KIND_WRITE;
+        case AD_KIND_WRITE:
+        case AD_KIND_SYNC_POINT: return d == AD_KIND_READ || d == AD_KIND_WRITE;
+        case AD_KIND_EXCLUSIVE_SYNC_POINT:
+            return d == AD_KIND_READ || d == AD_KIND_WRITE || d == AD_KIND_SYNC_POINT || d == AD_KIND_EXCLUSIVE_SYNC_POINT;
+        default: return false;
+    }
+}
+// CommandsForKey.manages (key domain, globally visible) — CommandsForKey.java:185-188
+__host__ __device__ inline bool manages(uint32_t m) {
+    uint32_t k = meta_kind(m);
+    return meta_domain(m) == AD_DOMAIN_KEY && (k == AD_KIND_READ || k == AD_KIND_WRITE || k == AD_KIND_SYNC_POINT ||
+                                               k == AD_KIND_EXCLUSIVE_SYNC_POINT);
+}
+// CommandsForKey.managesExecution (key Read/Write) — CommandsForKey.java:196-199
+__host__ __device__ inline bool manages_execution(uint32_t m) {
+    uint32_t k = meta_kind(m);
+    return meta_domain(m) == AD_DOMAIN_KEY && (k == AD_KIND_READ || k == AD_KIND_WRITE);
+}
+// Entry categories for an out-of-window CFK entry (CommandsForKey.mapReduceActive :951-962)
+enum : uint32_t { CAT_SKIP = 0, CAT_ALWAYS = 1, CAT_ELIDABLE = 2 };
+__host__ __device__ inline uint32_t category(uint32_t m) {
+    uint32_t st = meta_status(m);
+    if (!manages(m)) return CAT_SKIP;                      // not in CommandsForKey.byId at all
+    if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID) return CAT_SKIP;
+    bool committed = st == AD_ST_COMMITTED || st == AD_ST_STABLE || st == AD_ST_APPLIED;
+    if (committed && witnesses(AD_KIND_WRITE, meta_kind(m))) return CAT_ELIDABLE;
+    return CAT_ALWAYS;                                     // undecided, or committed sync point
+}
+
+struct TsPack {            // per-batch packing parameters (device + host)
+    uint64_t msb_min, hlc_min;
+    int64_t node_min;
+    uint32_t sh_msb, sh_hlc, sh_flags;   // shifts
+    uint32_t total_bits;                 // width of the packed key
+};
+
+__host__ __device__ inline uint64_t ts_pack(const TsPack& p, uint64_t msb, uint64_t lsb, int32_t node) {
+    return ((msb - p.msb_min) << p.sh_msb) | (((lsb >> 16) - p.hlc_min) << p.sh_hlc) |
+           (((lsb >> 1) & 0xFull) << p.sh_flags) | (uint64_t)((int64_t)node - p.node_min);
+}
+
+// Device twin of ad_drop_hash (include/accord_deps.h) — must stay bit-identical (tests check it).
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline uint32_t drop_hash(uint64_t seed, uint32_t view, uint32_t i, uint32_t j) {
+    return (uint32_t)(mix64(seed ^ mix64(((uint64_t)view << 56) ^ ((uint64_t)i << 28) ^ (uint64_t)j)) >> 32);
+}
+
+__device__ inline uint32_t lane_id() { return __lane_id(); }
+
+template <class T>
+__device__ inline T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { T u = __shfl_xor(v, o); v = u > v ? u : v; }
+    return v;
+}
+template <class T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One batched per-txn CSR on the device (one Deps class of one replica view, or merged):
+//   key_off[n+1], keys[nkeys], k2t_off[n+1], k2t[nk2t] (exact KeyDeps.keysToTxnIds per txn),
+//   ent_off[n+1] txn-rank capacity offsets (= entry counts), tcnt[n] unique TxnIds, txns[ncap].
+struct DevCsr {
+    uint32_t *key_off = nullptr, *k2t_off = nullptr, *ent_off = nullptr, *tcnt = nullptr, *txns = nullptr;
+    uint64_t* keys = nullptr;
+    int32_t* k2t = nullptr;
+    size_t nkeys = 0, nk2t = 0, ncap = 0;
+};
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace ad

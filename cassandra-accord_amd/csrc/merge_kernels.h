@@ -1,0 +1,147 @@
+// merge_kernels.h — Deps.merge of R replica replies, per txn (gfx950).
+//
+// Replaces KeyDeps.merge / RelationMultiMap.LinearMerger (primitives/KeyDeps.java:115-135,
+// utils/RelationMultiMap.java:284-406), which folds the replies pairwise with linearUnion
+// (RelationMultiMap.java:562-816).  Because every reply is canonical (sorted unique keys, sorted
+// unique TxnIds, sorted per-key index lists), the fold equals the canonical CSR of the union of the
+// (key, TxnId) relations, which this kernel builds in one R-way merge-path pass per txn:
+//   1. TxnIds: R-way merge of the replies' sorted TxnId lists (SortedArrays.linearUnion :198-333)
+//   2. keys:   R-way merge of the sorted key lists; for each merged key, R-way merge of the replies'
+//              per-key lists mapped to TxnIds, then to indices in (1) (remapToSuperset :1249-1275)
+// Two launches: count (key / entry / TxnId totals per txn), then write into scanned offsets.
+#pragma once
+#include "deps_kernels.h"
+
+namespace ad {
+
+struct MergeArgs {
+    size_t n;
+    int nv;
+    const uint32_t* key_off[MAXV];
+    const uint64_t* keys[MAXV];
+    const uint32_t* k2t_off[MAXV];
+    const int32_t* k2t[MAXV];
+    const uint32_t* ent_off[MAXV];
+    const uint32_t* txns[MAXV];
+    const uint32_t* tcnt[MAXV];
+    uint32_t *mk, *me, *mu;      // count pass outputs
+    const uint32_t* o_key_off;
+    uint64_t* o_keys;
+    const uint32_t* o_k2t_off;
+    int32_t* o_k2t;
+    const uint32_t* o_ent_off;
+    uint32_t* o_txns;
+    uint32_t* o_tcnt;
+};
+
+template <int NV, bool WRITE>
+__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    constexpr uint32_t INF = 0xFFFFFFFFu;
+    // ---- 1. union of TxnId rank lists
+    uint32_t cur[NV], end[NV], head[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        cur[v] = a.ent_off[v][t];
+        end[v] = cur[v] + a.tcnt[v][t];
+        head[v] = cur[v] < end[v] ? a.txns[v][cur[v]] : INF;
+    }
+    uint32_t* out = WRITE ? a.o_txns + a.o_ent_off[t] : nullptr;
+    uint32_t mu = 0;
+    while (true) {
+        uint32_t mn = INF;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) mn = head[v] < mn ? head[v] : mn;
+        if (mn == INF) break;
+        if (WRITE) out[mu] = mn;
+        ++mu;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (head[v] == mn) { ++cur[v]; head[v] = cur[v] < end[v] ? a.txns[v][cur[v]] : INF; }
+    }
+    // ---- 2. union of keys; per merged key union of the per-key TxnId lists
+    uint32_t kc[NV], ke[NV], mb[NV], tb[NV], nkv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        kc[v] = a.key_off[v][t];
+        ke[v] = a.key_off[v][t + 1];
+        nkv[v] = ke[v] - kc[v];
+        mb[v] = a.k2t_off[v][t];
+        tb[v] = a.ent_off[v][t];
+    }
+    const uint32_t okb = WRITE ? a.o_key_off[t] : 0;
+    const uint32_t onk = WRITE ? a.o_key_off[t + 1] - okb : 0;
+    const uint32_t omb = WRITE ? a.o_k2t_off[t] : 0;
+    uint32_t mk = 0, me = 0;
+    uint32_t ep = omb + onk;         // next entry slot (write pass)
+    while (true) {
+        bool any = false;
+        uint64_t kmin = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (kc[v] < ke[v]) {
+                uint64_t k = a.keys[v][kc[v]];
+                if (!any || k < kmin) { kmin = k; any = true; }
+            }
+        }
+        if (!any) break;
+        // per-view list bounds for this key
+        uint32_t lc[NV], le[NV], lh[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            lc[v] = 0; le[v] = 0; lh[v] = INF;
+            if (kc[v] < ke[v] && a.keys[v][kc[v]] == kmin) {
+                const uint32_t ki = kc[v] - a.key_off[v][t];
+                lc[v] = mb[v] + (ki == 0 ? nkv[v] : (uint32_t)a.k2t[v][mb[v] + ki - 1]);
+                le[v] = mb[v] + (uint32_t)a.k2t[v][mb[v] + ki];
+                lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF;
+                ++kc[v];
+            }
+        }
+        uint32_t x = 0;   // position in the merged TxnId list (monotone)
+        while (true) {
+            uint32_t mn = INF;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) mn = lh[v] < mn ? lh[v] : mn;
+            if (mn == INF) break;
+            if (WRITE) {
+                while (out[x] < mn) ++x;
+                a.o_k2t[ep++] = (int32_t)x;
+            }
+            ++me;
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (lh[v] == mn) { ++lc[v]; lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF; }
+        }
+        if (WRITE) {
+            a.o_keys[okb + mk] = kmin;
+            a.o_k2t[omb + mk] = (int32_t)(ep - omb);
+        }
+        ++mk;
+    }
+    if (WRITE) a.o_tcnt[t] = mu;
+    else { a.mk[t] = mk; a.me[t] = me; a.mu[t] = mu; }
+}
+
+template <int NV>
+inline void merge_launch_nv(const MergeArgs& a, bool write, hipStream_t st) {
+    const int g = ceil_div((long)a.n, 256);
+    if (write) k_merge<NV, true><<<g, 256, 0, st>>>(a);
+    else k_merge<NV, false><<<g, 256, 0, st>>>(a);
+}
+
+inline void merge_launch(const MergeArgs& a, int nv, bool write, hipStream_t st) {
+    switch (nv) {
+        case 1: merge_launch_nv<1>(a, write, st); break;
+        case 2: merge_launch_nv<2>(a, write, st); break;
+        case 3: merge_launch_nv<3>(a, write, st); break;
+        case 4: merge_launch_nv<4>(a, write, st); break;
+        case 5: merge_launch_nv<5>(a, write, st); break;
+        case 6: merge_launch_nv<6>(a, write, st); break;
+        case 7: merge_launch_nv<7>(a, write, st); break;
+        default: merge_launch_nv<8>(a, write, st); break;
+    }
+}
+
+}  // namespace ad

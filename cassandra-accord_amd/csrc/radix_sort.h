@@ -1,0 +1,137 @@
+// radix_sort.h — LDS-staged stable LSD radix sort of (u32 key, u32 value) pairs for gfx950.
+//
+// One pass per 8-bit digit.  A tile is 256 threads x 16 items = 4096 pairs; each of the 4 waves owns
+// 1024 consecutive pairs and walks them in 16 rounds of 64 lanes, so (round, lane) order == input
+// order and the pass is stable.  Per round, lanes holding equal digits are found with 8 wave ballots
+// (64-bit masks: the CDNA wavefront is 64 lanes), the in-round rank is popcount(mask & lanes-below),
+// and per-wave digit counters live in LDS.  Pass structure:
+//   k_radix_hist    : per-tile digit histogram (LDS, per-wave privatised) -> hist[digit][tile]
+//   device_scan     : exclusive sum over hist (digit-major) -> global digit offsets per tile
+//   k_radix_scatter : recompute ranks, scatter keys/values to their final slots
+// Replaces the per-key Arrays.sort in RelationMultiMap.AbstractBuilder.finishKey/build
+// (utils/RelationMultiMap.java:158-169, 208-216, 230-243) by one batch-wide stable key sort.
+#pragma once
+#include "scan.h"
+
+namespace ad {
+
+constexpr int RS_BLOCK = 256;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_BLOCK * RS_ITEMS;
+constexpr int RS_WAVES = RS_BLOCK / WAVE;
+constexpr int RS_ROUNDS = RS_TILE / RS_WAVES / WAVE;   // 16
+
+__global__ __launch_bounds__(RS_BLOCK) void k_radix_hist(const uint32_t* __restrict__ keys, size_t n, int shift,
+                                                         int ntiles, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[RS_WAVES][256];
+    const int w = threadIdx.x / WAVE;
+    for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_BLOCK) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        size_t i = base + (size_t)k * RS_BLOCK + threadIdx.x;   // coalesced
+        if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 0xFF], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < 256; d += RS_BLOCK) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int x = 0; x < RS_WAVES; ++x) s += h[x][d];
+        hist[(size_t)d * ntiles + blockIdx.x] = s;
+    }
+}
+
+__device__ inline uint64_t match_digit(uint32_t d, bool valid) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        bool bit = (d >> b) & 1u;
+        uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                            size_t n, int shift, int ntiles,
+                                                            const uint32_t* __restrict__ offs) {
+    __shared__ uint32_t cnt[RS_WAVES][256];
+    const int w = threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE;
+    for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_BLOCK) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const size_t wbase = (size_t)blockIdx.x * RS_TILE + (size_t)w * (RS_ROUNDS * WAVE);
+    uint32_t k[RS_ROUNDS], v[RS_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        size_t i = wbase + (size_t)r * WAVE + lane;
+        k[r] = i < n ? kin[i] : 0u;
+        v[r] = i < n ? vin[i] : 0u;
+    }
+    const uint64_t below = (1ull << lane) - 1ull;
+    // pass A: per-wave digit counts
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        size_t i = wbase + (size_t)r * WAVE + lane;
+        bool valid = i < n;
+        uint32_t d = (k[r] >> shift) & 0xFF;
+        uint64_t m = match_digit(d, valid);
+        if (valid && (m & below) == 0) cnt[w][d] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    // per digit: global tile offset + counts of earlier waves
+    for (int d = threadIdx.x; d < 256; d += RS_BLOCK) {
+        uint32_t run = offs[(size_t)d * ntiles + blockIdx.x];
+#pragma unroll
+        for (int x = 0; x < RS_WAVES; ++x) {
+            uint32_t c = cnt[x][d];
+            cnt[x][d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    // pass B: scatter
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        size_t i = wbase + (size_t)r * WAVE + lane;
+        bool valid = i < n;
+        uint32_t d = (k[r] >> shift) & 0xFF;
+        uint64_t m = match_digit(d, valid);
+        uint32_t pos = cnt[w][d] + (uint32_t)__popcll(m & below);
+        if (valid) { kout[pos] = k[r]; vout[pos] = v[r]; }
+        if (valid && (m & below) == 0) cnt[w][d] += (uint32_t)__popcll(m);
+    }
+}
+
+struct RadixScratch {
+    uint32_t* hist;     // [256 * ntiles + 1]
+    uint32_t* offs;     // [256 * ntiles + 1]
+    uint32_t* agg;      // scan aggregates
+};
+
+inline size_t radix_hist_len(size_t n) { return (size_t)256 * ceil_div((long)n, RS_TILE) + 1; }
+
+// Sorts (k0, v0) by the low `bits` bits of the key using (k1, v1) as ping-pong buffers.
+// Returns true if the result ended in (k1, v1).
+inline bool radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, size_t n, int bits,
+                             const RadixScratch& s, hipStream_t st) {
+    if (n == 0 || bits <= 0) return false;
+    const int ntiles = ceil_div((long)n, RS_TILE);
+    const size_t hl = (size_t)256 * ntiles;
+    bool flip = false;
+    for (int shift = 0; shift < bits; shift += 8) {
+        const uint32_t* ki = flip ? k1 : k0;
+        const uint32_t* vi = flip ? v1 : v0;
+        uint32_t* ko = flip ? k0 : k1;
+        uint32_t* vo = flip ? v0 : v1;
+        k_radix_hist<<<ntiles, RS_BLOCK, 0, st>>>(ki, n, shift, ntiles, s.hist);
+        device_scan(SumOp<uint32_t>{s.hist, s.offs, hl}, hl, s.agg, st);
+        k_radix_scatter<<<ntiles, RS_BLOCK, 0, st>>>(ki, vi, ko, vo, n, shift, ntiles, s.offs);
+        flip = !flip;
+    }
+    return flip;
+}
+
+}  // namespace ad

@@ -1,0 +1,113 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Compared per txn: PreAccept PartialDeps of every replica view (keyDeps + directKeyDeps in the exact
+KeyDeps.SerializerSupport layout), the merged Deps, and execution levels + order.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from accord_amd import abi, workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_csr(name, got, want):
+    if got.equal(want):
+        return
+    i = got.first_difference(want)
+    raise AssertionError("%s differs at txn %s:\n gpu=%s\n cpu=%s" % (name, i, got.txn(i) if i is not None and i < got.n else None,
+                                                                      want.txn(i) if i is not None and i < want.n else None))
+
+
+def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, levels=True):
+    cfg = abi.make_config(window, replicas, drop_p, seed)
+    flags = O.FLAG_MERGE | (O.FLAG_LEVELS if levels else 0)
+    ref = O.OracleResult(batch, cfg, flags)
+    eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
+    eng.load(batch)
+    eng.preaccept_deps()
+    for v in range(replicas):
+        for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY, abi.CLASS_RANGE):
+            _assert_csr("deps view %d %s" % (v, abi.CLASS_NAMES[c]), eng.fetch_deps(v, c), ref.deps(v, c))
+    eng.merge()
+    for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY, abi.CLASS_RANGE):
+        _assert_csr("merged %s" % abi.CLASS_NAMES[c], eng.fetch_merged(c), ref.merged(c))
+    if levels:
+        lv, order, iters = eng.exec_levels()
+        rlv, rorder = ref.levels()
+        assert np.array_equal(lv, rlv), "levels differ at %s" % np.nonzero(lv != rlv)[0][:10]
+        assert np.array_equal(order, rorder), "order differs"
+    return ref
+
+
+@pytest.mark.parametrize("name,n", [("C2", 20000), ("C3", 20000), ("C2", 200000)])
+def test_configs_small(engine_factory, name, n):
+    check(engine_factory, workload.config(name, n=n))
+
+
+def test_c3_more_views_no_drop(engine_factory):
+    b = workload.config("C3", n=30000, seed=77)
+    check(engine_factory, b, replicas=1, drop_p=0.0)
+    check(engine_factory, b, replicas=5, drop_p=0.3, seed=5)
+
+
+def test_snapshot_window_zero(engine_factory):
+    check(engine_factory, workload.config("C3", n=5000, seed=3), window=0)
+
+
+def test_hot_single_key_and_big_bumps(engine_factory):
+    # every txn on one of 3 keys; slow path bumps far beyond the window's hlc span exercise the exact
+    # maxCommittedWriteBefore fallback (executeAt of an applied write >= the query's TxnId)
+    b = workload.generate(4000, keys_per_txn=2, keyspace=3, slow_frac=0.5, bump_max=600, seed=11)
+    check(engine_factory, b, window=4)
+
+
+def test_mixed_kinds_and_statuses(engine_factory):
+    rng = np.random.default_rng(9)
+    n = 6000
+    kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT,
+                        abi.KIND_EXCLUSIVE_SYNC_POINT], size=n, p=[0.35, 0.35, 0.1, 0.1, 0.1])
+    status = rng.choice([abi.ST_APPLIED, abi.ST_STABLE, abi.ST_COMMITTED, abi.ST_PREACCEPTED, abi.ST_ACCEPTED,
+                         abi.ST_INVALID, abi.ST_TRANSITIVELY_KNOWN, abi.ST_HISTORICAL], size=n,
+                        p=[0.5, 0.1, 0.1, 0.05, 0.05, 0.1, 0.05, 0.05]).astype(np.uint8)
+    b = workload.generate(n, keys_per_txn=3, keyspace=200, kinds=kinds, status=status, seed=12)
+    check(engine_factory, b, window=8, levels=False)
+
+
+def test_ragged_keys(engine_factory):
+    # 1..16 keys per txn
+    rng = np.random.default_rng(4)
+    base = workload.generate(3000, keys_per_txn=1, keyspace=500, seed=4)
+    cnt = rng.integers(1, 17, size=3000)
+    keys, off = [], [0]
+    for c in cnt:
+        keys.append(rng.choice(500, size=c, replace=False).astype(np.uint64))
+        off.append(off[-1] + c)
+    base["keys"] = np.concatenate(keys)
+    base["key_off"] = np.array(off, np.uint32)
+    check(engine_factory, base, window=16)
+
+
+def test_edge_sizes(engine_factory):
+    for n in (1, 2, 63, 64, 65, 4095, 4096, 4097):
+        check(engine_factory, workload.generate(n, keyspace=50, seed=n))
+
+
+def test_empty_batch(engine_factory):
+    b = workload.generate(0)
+    eng = engine_factory()
+    eng.load(b)
+    sizes = eng.preaccept_deps()
+    assert all(s.keys == 0 for s in sizes)
+
+
+def test_unsorted_batch_rejected(engine_factory):
+    from accord_amd import engine
+
+    b = workload.generate(100, seed=1)
+    b["txn_lsb"] = b["txn_lsb"][::-1].copy()
+    eng = engine_factory()
+    eng.load(b)
+    with pytest.raises(engine.AccordDepsError):
+        eng.preaccept_deps()
