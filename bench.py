@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py — txn deps + execution order resolved per second on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one device-resident 1M-txn batch (BASELINE.json configs[1],
+C2: 1M txns x 4 keys, uniform over a 10M keyspace):
+  PreAccept deps for every txn under R=3 replica views (CommandsForKey.mapReduceActive + Deps.Builder),
+  Deps.merge of the 3 replies, and execution levels/order over the merged graph — ad_run_pipeline().
+
+Multi-GPU: one process per GPU (torch.distributed.run).  Each rank is one CommandStore owning a
+disjoint key range (keys offset by rank * keyspace) with its own 1M-txn batch, so the per-GPU work
+is fixed as N grows ("weak").  Ranks share no data on this config (C5's cross-shard exchange is a
+separate path), so the only inter-rank traffic is the timing barrier/max over a gloo group.
+
+Timing: W untimed warmup steps; then barrier + device sync, K timed steps, device sync + barrier,
+max over ranks.  The HIP work runs on the engine's own stream and every ad_run_pipeline() ends with
+an event synchronisation on it, so "device sync" is that stream's completion (this process never
+creates a torch HIP context).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+
+import numpy as np  # noqa: E402
+
+from accord_amd import abi, engine, workload  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+WINDOW, REPLICAS, DROP_P = 32, 3, 0.1
+KEYSPACE = 10_000_000
+
+
+def alg_bytes(kernel, n, P, R, st):
+    """Algorithmic HBM bytes of ONE launch of `kernel` (DESIGN.md §Roofline lists the per-unit figures).
+
+    n txns, P (txn,key) pairs, R replica views; st = ad_last_times() counts of the step."""
+    D = st["deps_entries"]           # emitted dependency entries over all views/classes
+    M = st["merged_entries"]
+    per = {
+        "k_minmax": n * 44 + P * 8,
+        "k_pack": n * 62 + P * 20,
+        "k_radix_hist": P * 4,
+        "k_radix_scatter": P * 16,
+        "k_gather_entries": P * 34,
+        "scan_elide": P * 37,
+        "k_deps_walk<count>": P * (37 + 8 * R),
+        "k_deps_walk<fill>": P * (37 + 16 * R) + 4 * D,
+        "k_txn_counts": n * 8 + P * (4 + 8 * R) + n * 16 * R,
+        "k_txn_union": 8 * D + 4 * D,
+        # per class launch: read the R replies (offsets 16 B/txn + entries 4 B + txn ranks 4 B), write merged
+        "k_merge<count>": (n * 16 * R + 8 * D / 2 + n * 12),
+        "k_merge<write>": (n * 16 * R + 8 * D / 2 + n * 16 + 8 * M / 2),
+        "scan_chain": P * 13 + n * 4,
+    }
+    return per.get(kernel)
+
+
+def pipeline_alg_bytes(n, P, R, st):
+    """SURVEY §8(d) B_alg for one batch (B_in + B_sort + B_scan + B_out + B_merge + B_level)."""
+    D, M = st["deps_entries"], st["merged_entries"]
+    key_bits = 24
+    b_in = n * 40 + P * 12
+    b_sort = -(-key_bits // 8) * 2 * P * 8
+    b_scan = P * (8 + 24)
+    b_out = n * 4 * 3 * R + D * 8
+    b_merge = (n * 12 * R + D * 8) + (n * 12 + M * 8)
+    b_level = P * 8 + P * 8 + n * 4 * 2
+    return b_in + b_sort + b_scan + b_out + b_merge + b_level
+
+
+def cpu_baseline(sample_n):
+    """The oracle (oracle/, the CPU restatement of the reference algorithms) on a bounded sample of the
+    same workload, 1 thread, this host.  Test infrastructure: timed here as the reported baseline only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    b = workload.config("C2", n=sample_n)
+    cfg = abi.make_config(WINDOW, REPLICAS, DROP_P, workload.SEEDS["C2"])
+    r = O.OracleResult(b, cfg, O.FLAG_PRUNE | O.FLAG_MERGE | O.FLAG_LEVELS, threads=1)
+    s = r.stats()
+    t = s["t_deps"] + s["t_merge"] + s["t_levels"]
+    return {"value": sample_n / t, "unit": "txn/s", "cores": 1, "kind": "port",
+            "sample": "C2 generator, first %d txns (seed 0xACC0D1), PreAccept deps x%d views + Deps.merge + "
+                      "exec levels, %.1f s (deps %.1f, merge %.1f, levels %.1f)"
+                      % (sample_n, REPLICAS, t, s["t_deps"], s["t_merge"], s["t_levels"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1 << 20, help="txns per GPU batch (C2: 1M)")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 18, help="txns in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--breakdown", action="store_true", help="print the per-kernel breakdown to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dist = tdist
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if not dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # this rank's CommandStore: a disjoint key range, its own seeded batch
+    batch = workload.generate(args.n, 4, KEYSPACE, "uniform", seed=workload.SEEDS["C2"] + rank)
+    batch["keys"] = batch["keys"] + np.uint64(rank * KEYSPACE)
+    n, P = batch["n"], int(batch["key_off"][-1])
+
+    eng = engine.DepsEngine(device=local, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C2"])
+    eng.load(batch)                                   # host -> HBM once; the timed region starts resident
+    ids = engine.kernel_ids()
+
+    for _ in range(max(args.warmup, 1)):
+        eng.run_pipeline()
+    # untimed breakdown pass: every kernel traced -> the dominant kernel
+    eng.set_trace((1 << len(ids)) - 1)
+    eng.reset_kernel_stats()
+    eng.run_pipeline()
+    brk = eng.kernel_stats()
+    st = eng.last_times()
+    dom = max((k for k in brk if alg_bytes(k, n, P, REPLICAS, st) is not None), key=lambda k: brk[k][1])
+    if args.breakdown and rank == 0:
+        tot = sum(v[1] for v in brk.values())
+        for k, (c, ms) in sorted(brk.items(), key=lambda kv: -kv[1][1]):
+            print("  %-22s %5d launches %9.3f ms  %5.1f%%" % (k, c, ms, 100 * ms / tot), file=sys.stderr)
+        print("  stages: %s" % {k: round(v, 3) if isinstance(v, float) else v for k, v in st.items()}, file=sys.stderr)
+
+    # timed region: only the dominant kernel is event-timed (on the engine's stream)
+    eng.set_trace(1 << ids[dom])
+    eng.reset_kernel_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run_pipeline()                             # ends with an event sync on the engine stream
+    t1 = time.perf_counter()
+    barrier()
+    dt = max_over_ranks(t1 - t0)
+    kst = eng.kernel_stats()[dom]
+    st = eng.last_times()
+    eng.set_trace(0)
+
+    avg_ms = kst[1] / kst[0]
+    ab = alg_bytes(dom, n, P, REPLICAS, st)
+    achieved = ab / (avg_ms * 1e-3) / 1e9
+    ms_per_step = dt * 1e3 / args.steps
+    value = world * n * args.steps / dt
+    pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st) / (dt / args.steps) / 1e9
+
+    out = {
+        "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
+        "value": value, "unit": "txn/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C2 generator, BASELINE configs[1])",
+        "config": {"workload": "C2: %d txns x 4 keys uniform over 10M keys per GPU; PreAccept deps under R=%d "
+                               "replica views (in-flight window W=%d, drop p=%.1f) + Deps.merge + exec levels/order"
+                               % (n, REPLICAS, WINDOW, DROP_P),
+                   "txns_per_gpu": n, "keys_per_txn": 4, "keyspace": KEYSPACE, "replicas": REPLICAS,
+                   "window": WINDOW, "parallelism": "key-range shard per GPU (%d)" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": ab,
+                     "avg_launch_ms": avg_ms, "launches": kst[0]},
+        "pipeline": {"alg_bytes": pipeline_alg_bytes(n, P, REPLICAS, st), "alg_GBps": pipe_gbs,
+                     "frac": pipe_gbs / HBM_PEAK_GBS,
+                     "stage_ms": {k: st[k] for k in ("prepare", "sort", "deps", "merge", "levels", "total")},
+                     "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
+                     "level_iterations": st["level_iterations"]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+        out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    eng.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

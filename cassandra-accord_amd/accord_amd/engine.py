@@ -56,6 +56,12 @@ def lib():
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ad_run_pipeline.argtypes = [vp]
         L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
+        L.ad_set_trace.argtypes = [vp, C.c_uint64]
+        L.ad_kernel_count.restype = C.c_int
+        L.ad_kernel_name.argtypes = [C.c_int]
+        L.ad_kernel_name.restype = C.c_char_p
+        L.ad_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        L.ad_reset_kernel_stats.argtypes = [vp]
         L.ad_shard_bounds.argtypes = [C.POINTER(C.c_uint64), C.c_size_t, C.c_uint32, C.POINTER(C.c_uint64)]
         _LIB = L
     return _LIB
@@ -63,7 +69,8 @@ def lib():
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
             "ad_fetch_deps", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
-            "ad_run_pipeline", "ad_last_times", "ad_shard_bounds")
+            "ad_run_pipeline", "ad_last_times", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats",
+            "ad_reset_kernel_stats", "ad_shard_bounds")
 
 
 class DepsEngine:
@@ -149,6 +156,31 @@ class DepsEngine:
         t = abi.AdStageTimes()
         self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
         return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_ if f != "pad_"}
+
+    def set_trace(self, mask):
+        """Enable HIP-event timing of the kernels whose id bit is set (see kernel_ids())."""
+        self._check(lib().ad_set_trace(self.h, mask), "ad_set_trace")
+
+    def reset_kernel_stats(self):
+        self._check(lib().ad_reset_kernel_stats(self.h), "ad_reset_kernel_stats")
+
+    def kernel_stats(self):
+        """{kernel name: (launches, total ms)} for every traced kernel with at least one launch."""
+        out = {}
+        for k in range(lib().ad_kernel_count()):
+            name, calls, ms = C.c_char_p(), C.c_uint64(), C.c_double()
+            self._check(lib().ad_kernel_stats(self.h, k, C.byref(name), C.byref(calls), C.byref(ms)), "ad_kernel_stats")
+            if calls.value:
+                out[name.value.decode()] = (calls.value, ms.value)
+        return out
+
+
+def kernel_ids():
+    """{kernel name: id} of the traceable kernels."""
+    out = {}
+    for k in range(lib().ad_kernel_count()):
+        out[lib().ad_kernel_name(k).decode()] = k
+    return out
 
 
 def device_count():

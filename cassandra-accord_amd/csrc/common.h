@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "../../include/accord_deps.h"
+#include "trace.h"
 
 namespace ad {
 

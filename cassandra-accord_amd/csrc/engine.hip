@@ -73,6 +73,7 @@ struct ad_handle {
     // timing
     hipEvent_t ev[8]{};
     ad_stage_times times{};
+    Tracer tracer;
     uint64_t deps_entries = 0, merged_entries = 0;
 };
 
@@ -156,7 +157,7 @@ int stage_prepare(ad_handle* h) {
     hipStream_t st = h->st;
     k_params_init<<<1, 1, 0, st>>>(h->prm);
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(n, P) + 255) / 256));
-    k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_off, h->prm);
+    { KScope ks(K_MINMAX); k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_off, h->prm); }
     HIPCHK(h, hipMemcpyAsync(&h->hprm, h->prm, sizeof(Params), hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     const Params& p = h->hprm;
@@ -174,6 +175,7 @@ int stage_prepare(ad_handle* h) {
     h->pack.total_bits = NB + 4 + HB + MB;
     h->key_bits = P ? bits_of(p.key_max - p.key_min) : 0;
     if (h->key_bits > 32) return set_err(h, AD_ERR_UNSUPPORTED, "key spread exceeds 32 bits");
+    KScope ks(K_PACK);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, h->tx_ts, h->ex1, h->meta, h->pair_txn,
                                                     h->ka, h->va, h->prm);
@@ -201,6 +203,7 @@ int stage_sort(ad_handle* h) {
 template <int NV>
 void launch_walk(const WalkArgs& a, bool fill, hipStream_t st) {
     const int g = ceil_div((long)a.P, 256);
+    KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT);
     if (fill) k_deps_walk<NV, true><<<g, 256, 0, st>>>(a);
     else k_deps_walk<NV, false><<<g, 256, 0, st>>>(a);
 }
@@ -224,9 +227,10 @@ int stage_deps(ad_handle* h) {
     h->deps.resize(nvc);
     for (int vc = 0; vc < nvc; ++vc) CK(alloc_csr(h, S_CSR0 + 10 * vc, h->deps[vc], n));
     if (P > 0) {
-        k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->pair_txn, h->meta, h->ex1, h->e_txn, h->e_meta,
-                                                                   h->e_exec1, h->spos);
+        { KScope ks(K_GATHER); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->pair_txn, h->meta, h->ex1, h->e_txn, h->e_meta,
+                                                                   h->e_exec1, h->spos); }
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c};
+        KScope ks(K_SCAN_ELIDE);
         device_scan(eop, P, (ElideOp::S*)h->scratch, st);
     }
     WalkArgs wa{};
@@ -238,8 +242,9 @@ int stage_deps(ad_handle* h) {
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.spos = h->spos; ta.cnt = h->cnt;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
-    if (n > 0) k_txn_counts<<<ceil_div((long)n, 256), 256, 0, st>>>(ta);
+    if (n > 0) { KScope ks(K_TXN_COUNTS); k_txn_counts<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
     for (int vc = 0; vc < nvc; ++vc) {
+        KScope ks(K_SCAN_OFFSETS);
         Csr& c = h->deps[vc];
         scan_offsets(h, h->nk + (size_t)vc * n, c.key_off, n);
         scan_offsets(h, h->ne + (size_t)vc * n, c.ent_off, n);
@@ -266,7 +271,7 @@ int stage_deps(ad_handle* h) {
         ta.out_key_off[vc] = c.key_off; ta.out_k2t_off[vc] = c.k2t_off; ta.out_keys[vc] = c.keys; ta.out_k2t[vc] = c.k2t;
         wa.k2t[vc] = c.k2t;
     }
-    if (n > 0) k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta);
+    if (n > 0) { KScope ks(K_TXN_LAYOUT); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
     if (P > 0) walk(wa, nv, true, st);
     UnionArgs ua{};
     ua.n = n; ua.nvc = nvc;
@@ -275,7 +280,7 @@ int stage_deps(ad_handle* h) {
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    if (n > 0) k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua);
+    if (n > 0) { KScope ks(K_TXN_UNION); k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua); }
     h->have_deps = true;
     return AD_OK;
 }
@@ -301,10 +306,13 @@ int stage_merge(ad_handle* h) {
         }
         ma.mk = h->nk; ma.me = h->ne; ma.mu = h->nk + n;   // scratch counters (n each)
         if (n > 0) merge_launch(ma, nv, false, st);
-        scan_offsets(h, ma.mk, m.key_off, n);
-        scan_offsets(h, ma.mu, m.ent_off, n);
-        if (n) device_scan(Sum2Op<uint32_t>{ma.mk, ma.me, m.k2t_off, n}, n, (uint32_t*)h->scratch, st);
-        else hipMemsetAsync(m.k2t_off, 0, 4, st);
+        {
+            KScope ks(K_SCAN_OFFSETS);
+            scan_offsets(h, ma.mk, m.key_off, n);
+            scan_offsets(h, ma.mu, m.ent_off, n);
+            if (n) device_scan(Sum2Op<uint32_t>{ma.mk, ma.me, m.k2t_off, n}, n, (uint32_t*)h->scratch, st);
+            else hipMemsetAsync(m.k2t_off, 0, 4, st);
+        }
         uint32_t tot[3];
         HIPCHK(h, hipMemcpyAsync(&tot[0], m.key_off + n, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipMemcpyAsync(&tot[1], m.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
@@ -404,6 +412,7 @@ int ad_open(int device, const ad_config* cfg, ad_handle** out) {
         return AD_ERR_DEVICE;
     }
     for (auto& e : h->ev) hipEventCreate(&e);
+    h->tracer.st = h->st;
     *out = h;
     return AD_OK;
 }
@@ -477,6 +486,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
 
 int ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes) {
     if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
     hipSetDevice(h->device);
     CK(stage_prepare(h));
@@ -509,6 +519,7 @@ int ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out) {
 
 int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
     if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
     hipSetDevice(h->device);
     CK(stage_merge(h));
     if (sizes) {
@@ -534,6 +545,7 @@ int ad_merge_host(ad_handle* h, const ad_csr_in*, uint32_t, ad_csr_sizes*) {
 
 int ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint32_t* iterations_out) {
     if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
     hipSetDevice(h->device);
     CK(stage_levels(h, order_out != nullptr));
     hipStream_t st = h->st;
@@ -546,6 +558,7 @@ int ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint3
 
 int ad_run_pipeline(ad_handle* h) {
     if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
@@ -572,12 +585,43 @@ int ad_run_pipeline(ad_handle* h) {
     h->times.merged_entries = h->merged_entries;
     h->times.level_iterations = h->level_iters;
     h->times.level_edges = h->P;
+    h->tracer.resolve();
     return AD_OK;
 }
 
 int ad_last_times(ad_handle* h, ad_stage_times* out) {
     if (!h || !out) return AD_ERR_ARGUMENT;
     *out = h->times;
+    return AD_OK;
+}
+
+int ad_kernel_count(void) { return K_COUNT; }
+
+const char* ad_kernel_name(int kid) { return kernel_name(kid); }
+
+int ad_set_trace(ad_handle* h, uint64_t mask) {
+    if (!h) return AD_ERR_ARGUMENT;
+    h->tracer.mask = mask;
+    return AD_OK;
+}
+
+int ad_kernel_stats(ad_handle* h, int kid, const char** name, uint64_t* calls, double* total_ms) {
+    if (!h || kid < 0 || kid >= K_COUNT) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->tracer.resolve();
+    if (name) *name = kernel_name(kid);
+    if (calls) *calls = h->tracer.calls[kid];
+    if (total_ms) *total_ms = h->tracer.total_ms[kid];
+    return AD_OK;
+}
+
+int ad_reset_kernel_stats(ad_handle* h) {
+    if (!h) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->tracer.resolve();
+    h->tracer.reset_counts();
     return AD_OK;
 }
 

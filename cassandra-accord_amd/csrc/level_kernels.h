@@ -227,12 +227,15 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
     *iters = 0;
     if (P > 0) {
-        k_chain_copy<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
-        k_chain_order<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
+        {
+            KScope ks(K_CHAIN_PREP);
+            k_chain_copy<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
+            k_chain_order<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
+        }
         ChainOp op{ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.flags};
         for (int it = 0; it < (1 << 22); ++it) {
             hipMemsetAsync(ls.flags, 0, 4, st);
-            device_scan(op, P, (ChainOp::S*)ls.agg, st);
+            { KScope ks(K_SCAN_CHAIN); device_scan(op, P, (ChainOp::S*)ls.agg, st); }
             uint32_t changed = 0;
             if (hipMemcpyAsync(&changed, ls.flags, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {

@@ -127,6 +127,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 template <int NV>
 inline void merge_launch_nv(const MergeArgs& a, bool write, hipStream_t st) {
     const int g = ceil_div((long)a.n, 256);
+    KScope ks(write ? K_MERGE_WRITE : K_MERGE_COUNT);
     if (write) k_merge<NV, true><<<g, 256, 0, st>>>(a);
     else k_merge<NV, false><<<g, 256, 0, st>>>(a);
 }

@@ -202,6 +202,16 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
+/* Per-kernel HIP-event timing (trace mode).  mask bit k enables kernel id k (0 <= k < ad_kernel_count()); the
+ * events are recorded on the handle's stream around each launch of that kernel.  ad_kernel_stats
+ * synchronises the stream and returns the kernel's name, launches and summed milliseconds since the
+ * last ad_reset_kernel_stats. */
+int  ad_set_trace(ad_handle* h, uint64_t mask);
+int  ad_kernel_count(void);
+const char* ad_kernel_name(int kid);
+int  ad_kernel_stats(ad_handle* h, int kid, const char** name, uint64_t* calls, double* total_ms);
+int  ad_reset_kernel_stats(ad_handle* h);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU: per-shard fragments are combined with an all-gather (RCCL over xGMI, driven by   */
 /* the host runtime) followed by this local union of the gathered fragments.                  */
