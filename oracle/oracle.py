@@ -40,6 +40,10 @@ def lib():
         L.oracle_build.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_size_t,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]
+        u64p, u32p, i32p, szp = C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)
+        L.oracle_union.argtypes = [u64p, C.c_size_t, u32p, C.c_size_t, i32p, C.c_size_t,
+                                   u64p, C.c_size_t, u32p, C.c_size_t, i32p, C.c_size_t,
+                                   u64p, szp, u32p, szp, i32p, szp]
         _LIB = L
     return _LIB
 
@@ -113,3 +117,27 @@ def build_relation(keys, vals):
     if rc != abi.AD_OK:
         raise ValueError("builder rejected input (rc=%d)" % rc)
     return ok[:nk.value].copy(), ov[:nv.value].copy(), om[:nm.value].copy()
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def union_relation(left, right):
+    """RelationMultiMap.linearUnion of two canonical (keys, vals, k2t) relations -> (keys, vals, k2t)."""
+    lk, lv, lm = (np.ascontiguousarray(left[0], np.uint64), np.ascontiguousarray(left[1], np.uint32),
+                  np.ascontiguousarray(left[2], np.int32))
+    rk, rv, rm = (np.ascontiguousarray(right[0], np.uint64), np.ascontiguousarray(right[1], np.uint32),
+                  np.ascontiguousarray(right[2], np.int32))
+    cap = len(lk) + len(rk) + 1
+    ok = np.zeros(cap, np.uint64)
+    ov = np.zeros(len(lv) + len(rv) + 1, np.uint32)
+    om = np.zeros(len(lm) + len(rm) + 1, np.int32)
+    nk, nv, nm = C.c_size_t(), C.c_size_t(), C.c_size_t()
+    lib().oracle_union(_p(lk, C.c_uint64), len(lk), _p(lv, C.c_uint32), len(lv), _p(lm, C.c_int32), len(lm),
+                       _p(rk, C.c_uint64), len(rk), _p(rv, C.c_uint32), len(rv), _p(rm, C.c_int32), len(rm),
+                       _p(ok, C.c_uint64), C.byref(nk), _p(ov, C.c_uint32), C.byref(nv), _p(om, C.c_int32), C.byref(nm))
+    return ok[:nk.value].copy(), ov[:nv.value].copy(), om[:nm.value].copy()
+
+
+EMPTY_RELATION = (np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int32))

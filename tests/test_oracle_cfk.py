@@ -1,0 +1,185 @@
+"""Known-answer tests of the oracle's PreAccept deps (CommandsForKey.mapReduceActive + range scan +
+Deps.Builder routing) on hand-built batches, and the CommandsForKeyTest.Canon execution-order
+invariant on its execution levels.
+
+Each expected answer is derived by hand from the reference code cited in the test; the PreAcceptTest
+known answers (test/messages/PreAcceptTest.java:85-290) are the first two cases.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from accord_amd import abi, workload
+from batchkit import T, deps_of, make_batch
+
+R, W, EPH, SP, ESP = abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT
+KEY, DIRECT, RANGE = abi.CLASS_KEY, abi.CLASS_DIRECT_KEY, abi.CLASS_RANGE
+
+
+def run(txns, window=32, levels=False):
+    b = make_batch(txns)
+    cfg = abi.make_config(window, 1, 0.0, 1)
+    flags = O.FLAG_MERGE | (O.FLAG_LEVELS if levels else 0)
+    return O.OracleResult(b, cfg, flags), b
+
+
+def d(res, cls, i):
+    return deps_of(res.deps(0, cls), i)
+
+
+def test_initial_command_no_deps():
+    # PreAcceptTest.initialCommandTest: first write on a key -> KeyDeps.NONE, RangeDeps.NONE, KeyDeps.NONE
+    res, _ = run([T(100, W, [10])])
+    for c in (KEY, DIRECT, RANGE):
+        assert d(res, c, 0) == {}
+
+
+def test_later_txn_not_a_dependency():
+    # PreAcceptTest.multiKeyTimestampUpdate: txnId2 (hlc 50) < txn1 (hlc 110) -> no deps for txnId2
+    # (CommandsForKey.mapReduceActive only visits byId[0, insertPos(startedBefore)), :929)
+    res, _ = run([T(110, W, [10], node=2), T(50, W, [10, 11], node=3)])
+    assert d(res, KEY, 0) == {}            # rank 0 = hlc 50
+    assert d(res, KEY, 1) == {10: [0]}     # rank 1 = hlc 110 sees the earlier txn on key 10
+
+
+def test_witness_matrix_in_flight():
+    # Txn.Kind.witnesses (Txn.java:221-245): Read -> Writes; Write -> Reads+Writes
+    res, _ = run([T(1, R, [7]), T(2, R, [7]), T(3, W, [7]), T(4, R, [7]), T(5, W, [7])])
+    assert d(res, KEY, 1) == {}                       # R2 does not witness R1
+    assert d(res, KEY, 2) == {7: [0, 1]}              # W3 witnesses R1, R2
+    assert d(res, KEY, 3) == {7: [2]}                 # R4 witnesses only W3
+    assert d(res, KEY, 4) == {7: [0, 1, 2, 3]}        # W5 witnesses all
+
+
+def test_transitive_elision():
+    # CommandsForKey.mapReduceActive :930-962 with every earlier txn APPLIED (window 0 = final statuses):
+    # maxCommittedWriteBefore = executeAt of the last committed Write before the bound; committed R/W txns
+    # executing strictly before it are elided; the write itself (executeAt == M) is kept.
+    res, _ = run([T(1, W, [5]), T(2, W, [5]), T(3, R, [5]), T(4, W, [5])], window=0)
+    assert d(res, KEY, 1) == {5: [0]}
+    assert d(res, KEY, 2) == {5: [1]}                 # W1 elided (executeAt < executeAt(W2))
+    assert d(res, KEY, 3) == {5: [1, 2]}              # W1 elided; R3 executes after W2 -> kept
+
+
+def test_slow_path_executeat_beyond_bound_not_used_for_elision():
+    # W1's executeAt was bumped past T3's TxnId: it is not "before" T3, so maxCommittedWriteBefore = W2
+    # (binary search over committedByExecuteAt for executeAt < startedBefore, :930-943); W1 executes
+    # after W2 so it is kept.
+    res, _ = run([T(1, W, [5], exec_hlc=10), T(2, W, [5]), T(3, W, [5])], window=0)
+    assert d(res, KEY, 2) == {5: [0, 1]}
+    res, _ = run([T(1, W, [5]), T(2, W, [5], exec_hlc=10), T(3, W, [5])], window=0)
+    assert d(res, KEY, 2) == {5: [0, 1]}              # no committed write before the bound -> nothing elided
+
+
+def test_statuses_skipped():
+    # TRANSITIVELY_KNOWN and INVALID_OR_TRUNCATED are never emitted (:959-961); undecided always are
+    res, _ = run([T(1, W, [5], status=abi.ST_INVALID), T(2, W, [5], status=abi.ST_TRANSITIVELY_KNOWN),
+                  T(3, W, [5], status=abi.ST_PREACCEPTED), T(4, W, [5], status=abi.ST_ACCEPTED), T(5, W, [5])], window=0)
+    assert d(res, KEY, 4) == {5: [2, 3]}
+
+
+def test_sync_points_routed_to_direct_key_deps():
+    # Deps.AbstractBuilder.add (Deps.java:80-106): a key-domain dep that CommandsForKey does not manage
+    # execution of (SyncPoint / ExclusiveSyncPoint) goes to directKeyDeps; ExclusiveSyncPoint witnesses
+    # every globally visible kind (Txn.java:221-245); a Write does not witness a SyncPoint.
+    res, _ = run([T(1, SP, [9]), T(2, W, [9]), T(3, ESP, [9])])
+    assert d(res, KEY, 1) == {} and d(res, DIRECT, 1) == {}
+    assert d(res, KEY, 2) == {9: [1]}
+    assert d(res, DIRECT, 2) == {9: [0]}
+
+
+def test_ephemeral_read_is_not_registered():
+    # CommandsForKey.manages (:185-188): EphemeralRead is not globally visible -> never in byId, so
+    # nothing takes a dependency on it; it itself witnesses Writes.
+    res, _ = run([T(1, W, [4]), T(2, EPH, [4]), T(3, W, [4])])
+    assert d(res, KEY, 1) == {4: [0]}
+    assert d(res, KEY, 2) == {4: [0]}
+
+
+def test_range_deps_end_inclusive():
+    # mapReduceRangesInternal (InMemoryCommandStore.java:884-1017): a range txn R is a dep of a key txn
+    # whose key lies in R's (start, end] (Range.EndInclusive, Range.java:48-55); the entry carries R's
+    # own range.
+    res, _ = run([T(1, W, ranges=[(5, 15)]), T(2, W, [5]), T(3, W, [15]), T(4, R, [16])])
+    assert d(res, RANGE, 1) == {}                      # key 5 is not in (5, 15]
+    assert d(res, RANGE, 2) == {(5, 15): [0]}          # key 15 is
+    assert d(res, KEY, 2) == {}
+    assert d(res, RANGE, 3) == {}
+
+
+def test_range_query_visits_cfk_keys_in_range():
+    # InMemorySafeStore.mapReduceActive for a Range: every CommandsForKey key in (start, end] is queried
+    # (commandsForKey.subMap(start, false, end, true)); range txns intersecting the range are deps too.
+    res, _ = run([T(1, W, [3]), T(2, W, [8]), T(3, W, [20]), T(4, W, ranges=[(0, 4)]), T(5, W, ranges=[(2, 8)])])
+    assert d(res, KEY, 4) == {3: [0], 8: [1]}
+    assert d(res, RANGE, 4) == {(0, 4): [3]}
+    res, _ = run([T(1, W, ranges=[(0, 10)]), T(2, R, ranges=[(10, 12)]), T(3, R, ranges=[(9, 11)])])
+    assert d(res, RANGE, 1) == {}                      # (0,10] and (10,12] do not intersect
+    assert d(res, RANGE, 2) == {(0, 10): [0]}
+
+
+def test_merge_is_union_of_views():
+    # Deps.merge of replica replies == per-class union (RelationMultiMap.LinearMerger)
+    b = workload.config("C3", n=3000, seed=5)
+    cfg = abi.make_config(16, 4, 0.4, 9)
+    res = O.OracleResult(b, cfg, O.FLAG_MERGE)
+    for c in (KEY, DIRECT):
+        views = [res.deps(v, c) for v in range(4)]
+        m = res.merged(c)
+        for i in range(0, 3000, 37):
+            want = {}
+            for vcsr in views:
+                for k, ts in deps_of(vcsr, i).items():
+                    want.setdefault(k, set()).update(ts)
+            assert deps_of(m, i) == {k: sorted(v) for k, v in want.items()}
+
+
+# ------------------------------------------------------------------------------------------------
+# CommandsForKeyTest.Canon invariant (test/local/cfk/CommandsForKeyTest.java:175-222): when T becomes
+# ready to execute, every command T witnesses that executes earlier on a shared key has Applied; and
+# every dependency with an earlier executeAt has Applied (Commands.updateWaitingOn :740-755).  With
+# level = Kahn wavefront index this is: level[D] < level[T] for each such D, and level[T] is minimal.
+# ------------------------------------------------------------------------------------------------
+def _exec_key(b, i):
+    return (int(b["exec_msb"][i]), int(b["exec_lsb"][i]) >> 16, int(b["exec_lsb"][i]) & 0x1E, int(b["exec_node"][i]))
+
+
+def canon_check(b, res):
+    lv, order = res.levels()
+    n = b["n"]
+    kind = (b["txn_lsb"] >> np.uint64(1)) & np.uint64(7)
+    ex = [_exec_key(b, i) for i in range(n)]
+    keys_of = [set(int(k) for k in b["keys"][b["key_off"][i]:b["key_off"][i + 1]]) for i in range(n)]
+    by_key = {}
+    for i in range(n):
+        for k in keys_of[i]:
+            by_key.setdefault(k, []).append(i)
+    direct, rng = res.merged(DIRECT), res.merged(RANGE)
+    for t in range(n):
+        preds = set()
+        for k in keys_of[t]:
+            for dd in by_key[k]:
+                if ex[dd] < ex[t] and (kind[t] == W or kind[dd] == W):
+                    preds.add(dd)
+        for csr in (direct, rng):
+            for deps in deps_of(csr, t).values():
+                preds.update(x for x in deps if ex[x] < ex[t])
+        want = 1 + max((int(lv[p]) for p in preds), default=-1)
+        assert int(lv[t]) == want, "txn %d level %d, Canon-minimal %d" % (t, lv[t], want)
+    # order = txns sorted by (level, executeAt)
+    assert list(order) == sorted(range(n), key=lambda i: (int(lv[i]), ex[i]))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_levels_canon_invariant(seed):
+    b = workload.generate(1500, keys_per_txn=2, keyspace=60, slow_frac=0.3, bump_max=40, seed=seed)
+    res = O.OracleResult(b, abi.make_config(8, 3, 0.2, seed), O.FLAG_MERGE | O.FLAG_LEVELS)
+    canon_check(b, res)
+
+
+def test_levels_read_batches_released_together():
+    # Reads between two writes share a level (CommandsForKey unappliedCounters, :1291-1330)
+    res, b = run([T(1, W, [1]), T(2, R, [1]), T(3, R, [1]), T(4, R, [1]), T(5, W, [1]), T(6, R, [1])], levels=True)
+    lv, order = res.levels()
+    assert list(lv) == [0, 1, 1, 1, 2, 3]
+    canon_check(b, res)
