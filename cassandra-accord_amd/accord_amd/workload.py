@@ -7,7 +7,7 @@ A batch is a dict of numpy arrays in the ad_batch layout (include/accord_deps.h)
   (Timestamp.java:81-89).  Arrival order == TxnId order (the batch is CommandsForKey.byId order).
 * executeAt: == TxnId on the fast path; with probability ``slow_frac`` bumped by 1..``bump_max``
   hlc and witnessed by a replica node id (101..103) so that every executeAt is a distinct Timestamp.
-* Keys: ``keys_per_txn`` distinct keys per key txn, uniform or Zipf(s) over ``keyspace`` (Zipf ranks are
+* Keys: ``keys_per_txn`` distinct keys per key txn, ascending (Keys is a sorted set), uniform or Zipf(s) over ``keyspace`` (Zipf ranks are
   scattered over the key space by an affine bijection so hot keys do not cluster in one shard).
 * Kinds: key txns Write with probability ``write_frac`` else Read (BurnTest.java:161-164); range
   txns (``range_frac``) carry 1-2 disjoint ranges of width U[1, range_width_max] (BurnTest.randomRange
@@ -109,6 +109,7 @@ def generate(n, keys_per_txn=4, keyspace=10_000_000, dist="uniform", zipf_s=0.99
     else:
         raise ValueError(dist)
     kk = _distinct_rows(rng, draw, nkey_txn, keys_per_txn) if nkey_txn else np.zeros((0, keys_per_txn), np.uint64)
+    kk = np.sort(kk, axis=1)                   # Keys are a sorted set (primitives/Keys.java)
     cnt = np.where(is_range, 0, keys_per_txn).astype(np.int64)
     key_off = np.zeros(n + 1, np.uint32)
     key_off[1:] = np.cumsum(cnt)

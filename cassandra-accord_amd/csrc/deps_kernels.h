@@ -1,38 +1,47 @@
-// deps_kernels.h — PreAccept conflict-dependency kernels (gfx950).
+// deps_kernels.h — PreAccept conflict-dependency kernels for key footprints (gfx950).
 //
-// Data flow for one batch (all device resident, P = key pairs, sorted order = (key, TxnId rank)):
-//   k_minmax / k_pack   TxnId / executeAt -> packed ts64, per-txn meta byte, pair owner, sort input
+// Data flow for one batch (all device resident, P = (txn,key) pairs, sorted order = (key, TxnId rank)):
+//   k_minmax / k_pack   batch statistics, TxnId/executeAt -> packed ts64, per-txn meta byte, pair owner,
+//                       footprint validation (keys ascending per txn, ranges sorted and disjoint)
 //   radix sort          (key - key_min, pair) pairs, stable => each key segment is CFK.byId order
 //   k_gather_entries    sorted entry SoA: txn rank, meta, executeAt+1, inverse permutation
-//   ElideOp scan        per entry: segment start, prefix max executeAt of committed writes (for
-//                       maxCommittedWriteBefore), prefix max executeAt of elidable entries, last
+//   ElideOp scan        per entry: segment start, distinct-key index, prefix max executeAt of committed
+//                       writes (maxCommittedWriteBefore), prefix max executeAt of elidable entries, last
 //                       "always emitted" entry — CommandsForKey.mapReduceActive's state
-//                       (CommandsForKey.java:925-983) as segmented scans
-//   k_deps_walk<count>  per (txn,key) pair and replica view: emitted-dependency counts
-//   k_txn_counts / scans / k_txn_layout   per txn: keys that carry deps, KeyDeps header, slots
-//   k_deps_walk<fill>   writes dependency ranks straight into each txn's keysToTxnIds
-//   k_txn_union         per txn: sorted unique TxnIds + remap entries to indices
-//                       (RelationMultiMap.AbstractBuilder.build, RelationMultiMap.java:201-260)
+//                       (CommandsForKey.java:925-983) as one segmented scan
+//   walk<count|fill>    per query item (txn i, key segment, insert position) and replica view: the
+//                       dependencies mapReduceActive emits (CommandsForKey.java:945-965)
+//   small txns (key txns with <= KMAX keys): one thread per txn builds the per-txn KeyDeps layout and
+//   the TxnId union in registers (k_txn_counts / k_txn_layout / k_txn_union)
+//   large txns (range-domain txns querying every CFK key inside their ranges, and key txns with more
+//   than KMAX keys) go through "virtual items" (vitem_kernels in engine.hip) and union_kernels.h.
 #pragma once
 #include "scan.h"
 
 namespace ad {
 
 constexpr int MAXV = 8;       // replica views
-constexpr int KMAX = 16;      // keys per key-domain txn handled by the per-txn kernels
+constexpr int KMAX = 16;      // keys per key-domain txn handled by the per-txn register kernels
 constexpr int NVC_MAX = MAXV * 2;
+constexpr uint32_t META_LARGE = 0x80u;   // meta bit 7: txn takes the large (virtual item) path
 
-struct Params {                // device-side batch statistics (filled by k_minmax)
+struct Params {                // device-side batch statistics (filled by k_minmax / k_pack)
     unsigned long long msb_min, msb_max, hlc_min, hlc_max;
     unsigned long long key_min, key_max;
-    unsigned int node_min_b, node_max_b;   // node + 2^31
-    unsigned int max_keys, err;            // err bits below
+    unsigned long long rs_min, re_max, rw_max;   // range starts min, ends max, max width (end - start)
+    unsigned int node_min_b, node_max_b;         // node + 2^31
+    unsigned int max_keys, err;                  // err bits below
+    unsigned int n_large, n_keys_u;              // large txns; distinct keys (after sort)
+    unsigned long long n_vitems;                 // virtual items
 };
-enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_RANGE = 8 };
+enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
+                  ERR_RANGEBITS = 32, ERR_CAP = 64 };
 
 __global__ void k_params_init(Params* p) {
     p->msb_min = ~0ull; p->msb_max = 0; p->hlc_min = ~0ull; p->hlc_max = 0;
-    p->key_min = ~0ull; p->key_max = 0; p->node_min_b = ~0u; p->node_max_b = 0; p->max_keys = 0; p->err = 0;
+    p->key_min = ~0ull; p->key_max = 0; p->rs_min = ~0ull; p->re_max = 0; p->rw_max = 0;
+    p->node_min_b = ~0u; p->node_max_b = 0; p->max_keys = 0; p->err = 0;
+    p->n_large = 0; p->n_keys_u = 0; p->n_vitems = 0;
 }
 
 __device__ inline unsigned long long wmin64(unsigned long long v) {
@@ -46,63 +55,116 @@ __device__ inline unsigned long long wmax64(unsigned long long v) {
     return v;
 }
 
+// Batch statistics: per-thread accumulation, wave shuffles, one LDS combine per block, one atomic per
+// block and field (per-wave atomics on one address serialise: the first version spent 0.44 ms here).
 __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __restrict__ tm, const uint64_t* __restrict__ tl,
                                                 const int32_t* __restrict__ tn, const uint64_t* __restrict__ em,
                                                 const uint64_t* __restrict__ el, const int32_t* __restrict__ en,
                                                 const uint32_t* __restrict__ key_off, const uint64_t* __restrict__ keys,
-                                                size_t P, const uint32_t* __restrict__ range_off, Params* out) {
-    unsigned long long mmin = ~0ull, mmax = 0, hmin = ~0ull, hmax = 0, kmin = ~0ull, kmax = 0, nmin = ~0ull, nmax = 0, kc = 0;
-    unsigned rng = 0;
+                                                size_t P, const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
+                                                size_t Q, Params* out) {
+    constexpr int NF = 13;
+    // fields: 0 msb_min 1 msb_max 2 hlc_min 3 hlc_max 4 node_min 5 node_max 6 key_min 7 key_max 8 max_keys
+    //         9 rs_min 10 re_max 11 rw_max ; *_min are stored complemented so every field is a max
+    //         12 large txns (a sum)
+    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         unsigned long long a = tm[i], b = em[i], ha = tl[i] >> 16, hb = el[i] >> 16;
         unsigned long long na = (unsigned)tn[i] ^ 0x80000000u, nb = (unsigned)en[i] ^ 0x80000000u;
-        mmin = min(mmin, min(a, b)); mmax = max(mmax, max(a, b));
-        hmin = min(hmin, min(ha, hb)); hmax = max(hmax, max(ha, hb));
-        nmin = min(nmin, min(na, nb)); nmax = max(nmax, max(na, nb));
-        kc = max(kc, (unsigned long long)(key_off[i + 1] - key_off[i]));
-        if (range_off && range_off[i + 1] != range_off[i]) rng = 1;
+        f[0] = max(f[0], ~min(a, b)); f[1] = max(f[1], max(a, b));
+        f[2] = max(f[2], ~min(ha, hb)); f[3] = max(f[3], max(ha, hb));
+        f[4] = max(f[4], ~min(na, nb)); f[5] = max(f[5], max(na, nb));
+        const unsigned kc = key_off[i + 1] - key_off[i];
+        f[8] = max(f[8], (unsigned long long)kc);
+        f[12] += ((tl[i] & 1) == AD_DOMAIN_RANGE || kc > (unsigned)KMAX) ? 1ull : 0ull;
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
         unsigned long long k = keys[i];
-        kmin = min(kmin, k); kmax = max(kmax, k);
+        f[6] = max(f[6], ~k); f[7] = max(f[7], k);
     }
-    mmin = wmin64(mmin); mmax = wmax64(mmax); hmin = wmin64(hmin); hmax = wmax64(hmax);
-    nmin = wmin64(nmin); nmax = wmax64(nmax); kmin = wmin64(kmin); kmax = wmax64(kmax); kc = wmax64(kc);
-    bool anyr = __any(rng);
-    if (__lane_id() == 0) {
-        atomicMin(&out->msb_min, mmin); atomicMax(&out->msb_max, mmax);
-        atomicMin(&out->hlc_min, hmin); atomicMax(&out->hlc_max, hmax);
-        atomicMin(&out->key_min, kmin); atomicMax(&out->key_max, kmax);
-        atomicMin(&out->node_min_b, (unsigned)nmin); atomicMax(&out->node_max_b, (unsigned)nmax);
-        atomicMax(&out->max_keys, (unsigned)kc);
-        if (anyr) atomicOr(&out->err, ERR_RANGE);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < Q; i += stride) {
+        unsigned long long s = rs[i], e = re[i];
+        f[9] = max(f[9], ~s); f[10] = max(f[10], e); f[11] = max(f[11], e > s ? e - s : 0ull);
+    }
+    __shared__ unsigned long long red[4][NF];
+    const int w = threadIdx.x / WAVE;
+#pragma unroll
+    for (int k = 0; k < NF - 1; ++k) {
+        unsigned long long v = wmax64(f[k]);
+        if (__lane_id() == 0) red[w][k] = v;
+    }
+    {
+        unsigned long long v = f[NF - 1];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (__lane_id() == 0) red[w][NF - 1] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NF) {
+        const int k = threadIdx.x;
+        unsigned long long v = k == NF - 1 ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
+                                           : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
+        switch (k) {
+            case 0: atomicMin(&out->msb_min, ~v); break;
+            case 1: atomicMax(&out->msb_max, v); break;
+            case 2: atomicMin(&out->hlc_min, ~v); break;
+            case 3: atomicMax(&out->hlc_max, v); break;
+            case 4: atomicMin(&out->node_min_b, (unsigned)~v); break;
+            case 5: atomicMax(&out->node_max_b, (unsigned)v); break;
+            case 6: atomicMin(&out->key_min, ~v); break;
+            case 7: atomicMax(&out->key_max, v); break;
+            case 8: atomicMax(&out->max_keys, (unsigned)v); break;
+            case 9: atomicMin(&out->rs_min, ~v); break;
+            case 10: atomicMax(&out->re_max, v); break;
+            case 11: atomicMax(&out->rw_max, v); break;
+            case 12: if (v) atomicAdd(&out->n_large, (unsigned)v); break;
+        }
     }
 }
 
-// Packs timestamps, builds per-txn meta and the sort input.  One thread per txn.
+// Packs timestamps, builds per-txn meta, the sort input and validates footprints.  One thread per txn.
 __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_min,
                                               const uint64_t* __restrict__ tm, const uint64_t* __restrict__ tl,
                                               const int32_t* __restrict__ tn, const uint64_t* __restrict__ em,
                                               const uint64_t* __restrict__ el, const int32_t* __restrict__ en,
                                               const uint8_t* __restrict__ status, const uint32_t* __restrict__ key_off,
-                                              const uint64_t* __restrict__ keys, uint64_t* __restrict__ tx_ts,
-                                              uint64_t* __restrict__ ex1, uint8_t* __restrict__ meta,
-                                              uint32_t* __restrict__ pair_txn, uint32_t* __restrict__ skey,
-                                              uint32_t* __restrict__ sval, Params* prm) {
+                                              const uint64_t* __restrict__ keys, const uint32_t* __restrict__ range_off,
+                                              const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
+                                              uint64_t* __restrict__ tx_ts, uint64_t* __restrict__ ex1,
+                                              uint8_t* __restrict__ meta, uint32_t* __restrict__ pair_txn,
+                                              uint32_t* __restrict__ skey, uint32_t* __restrict__ sval, Params* prm) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t lsb = tl[i];
     uint64_t t = ts_pack(pk, tm[i], lsb, tn[i]);
     tx_ts[i] = t;
     ex1[i] = ts_pack(pk, em[i], el[i], en[i]) + 1;
-    meta[i] = (uint8_t)(((lsb >> 1) & 7) | ((lsb & 1) << 3) | ((uint32_t)(status[i] & 7) << 4));
-    if (i > 0 && ts_pack(pk, tm[i - 1], tl[i - 1], tn[i - 1]) >= t) atomicOr(&prm->err, ERR_UNSORTED);
-    for (uint32_t p = key_off[i]; p < key_off[i + 1]; ++p) {
+    const uint32_t kb = key_off[i], ke = key_off[i + 1];
+    const uint32_t rb = range_off ? range_off[i] : 0u, rend = range_off ? range_off[i + 1] : 0u;
+    const uint32_t domain = (uint32_t)(lsb & 1);
+    unsigned err = 0;
+    if (domain == AD_DOMAIN_RANGE && ke != kb) err |= ERR_KEYORDER;        // a range txn's footprint is its ranges
+    if (domain == AD_DOMAIN_KEY && rend != rb) err |= ERR_RANGEORDER;
+    const bool large = domain == AD_DOMAIN_RANGE || (ke - kb) > (uint32_t)KMAX;
+    meta[i] = (uint8_t)(((lsb >> 1) & 7) | ((lsb & 1) << 3) | ((uint32_t)(status[i] & 7) << 4) | (large ? META_LARGE : 0u));
+    if (i > 0 && ts_pack(pk, tm[i - 1], tl[i - 1], tn[i - 1]) >= t) err |= ERR_UNSORTED;
+    uint64_t prev = 0;
+    for (uint32_t p = kb; p < ke; ++p) {
+        const uint64_t k = keys[p];
+        if (p > kb && k <= prev) err |= ERR_KEYORDER;                      // Keys: sorted unique
+        prev = k;
         pair_txn[p] = (uint32_t)i;
-        skey[p] = (uint32_t)(keys[p] - key_min);
+        skey[p] = (uint32_t)(k - key_min);
         sval[p] = p;
     }
+    uint64_t pe = 0;
+    for (uint32_t q = rb; q < rend; ++q) {                                 // Ranges: sorted, disjoint, start < end
+        const uint64_t s = rs[q], e = re[q];
+        if (s >= e || (q > rb && s < pe)) err |= ERR_RANGEORDER;
+        pe = e;
+    }
+    if (err) atomicOr(&prm->err, err);
 }
 
 // Sorted entry SoA + inverse permutation.
@@ -127,7 +189,7 @@ struct ElideOp {
         uint32_t head;
         int32_t ss;          // segment start (max of head indices)
         int32_t ud;          // last CAT_ALWAYS entry index
-        uint32_t pad;
+        uint32_t hc;         // heads so far (distinct-key index + 1)
         uint64_t pw;         // prefix max executeAt+1 of committed writes (0 = none)
         uint64_t pc;         // prefix max executeAt+1 of elidable entries (0 = none)
     };
@@ -138,6 +200,12 @@ struct ElideOp {
     int32_t* ud_prev;
     uint64_t* pm_w;
     uint64_t* pm_c;
+    uint32_t* uidx;          // distinct-key index of each entry
+    uint64_t* ukey;          // [U] distinct keys (raw u64)
+    uint32_t* useg;          // [U+1] segment starts
+    uint64_t key_min;
+    size_t n;
+    Params* prm;
 
     __device__ S load(size_t i) const {
         S s;
@@ -146,7 +214,7 @@ struct ElideOp {
         uint32_t m = e_meta[i];
         uint32_t cat = category(m);
         s.ud = cat == CAT_ALWAYS ? (int32_t)i : -1;
-        s.pad = 0;
+        s.hc = s.head;
         uint64_t e = e_exec1[i];
         s.pc = cat == CAT_ELIDABLE ? e : 0;
         s.pw = (cat == CAT_ELIDABLE && meta_kind(m) == AD_KIND_WRITE) ? e : 0;
@@ -158,16 +226,26 @@ struct ElideOp {
         r.head = a.head | b.head;
         r.ss = max(a.ss, b.ss);
         r.ud = max(a.ud, b.ud);
-        r.pad = 0;
+        r.hc = a.hc + b.hc;
         r.pw = b.head ? b.pw : (a.pw > b.pw ? a.pw : b.pw);
         r.pc = b.head ? b.pc : (a.pc > b.pc ? a.pc : b.pc);
         return r;
     }
-    __device__ void store(size_t i, const S&, const S& inc, const S&) const {
+    __device__ void store(size_t i, const S&, const S& inc, const S& el) const {
         seg_start[i] = inc.ss;
         ud_prev[i] = inc.ud;
         pm_w[i] = inc.pw;
         pm_c[i] = inc.pc;
+        const uint32_t u = inc.hc - 1;
+        uidx[i] = u;
+        if (el.head) {
+            ukey[u] = (uint64_t)skey[i] + key_min;
+            useg[u] = (uint32_t)i;
+        }
+        if (i + 1 == n) {
+            useg[inc.hc] = (uint32_t)n;
+            prm->n_keys_u = inc.hc;
+        }
     }
 };
 
@@ -180,13 +258,21 @@ struct WalkArgs {
     const uint64_t* pm_w;
     const uint64_t* pm_c;
     const uint64_t* tx_ts;
+    const uint8_t* meta;      // per txn
     size_t P;
     uint32_t window;
     uint32_t thresh;
     uint64_t seed;
-    uint32_t* cnt;            // [vc * P + s], vc = view * 2 + class
-    const uint32_t* dst;      // [vc * P + s] absolute k2t slot of the first entry (fill)
+    uint32_t* cnt;            // real pairs: [vc * P + s], vc = view * 2 + class
+    const uint32_t* dst;      // real pairs: [vc * P + s] absolute k2t slot of the first entry (fill)
     int32_t* k2t[NVC_MAX];    // per-vc keysToTxnIds (fill)
+    // virtual items (large txns): item x queries key segment [vi_seg0[x], ...) before position vi_pos[x]
+    size_t V;
+    const uint32_t* vi_txn;
+    const uint32_t* vi_pos;
+    const uint32_t* vi_seg0;
+    uint32_t* vcnt;           // [x * nvc + vc]
+    const uint32_t* vdst;     // [x * nvc + vc]
 };
 
 // Next emitted "elidable" (committed Read/Write) entry at or before q, or seg0-1.
@@ -199,6 +285,63 @@ __device__ inline int next_elidable(const WalkArgs& a, int q, int seg0, uint64_t
     return seg0 - 1;
 }
 
+// CommandsForKey.mapReduceActive(startedBefore = TxnId_i) for one key segment, over the entries
+// [seg0, s) (all with TxnId < i), every replica view at once.  emit(v, direct, j) in descending order.
+template <int NV, class Emit>
+__device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, int s, int seg0, Emit&& emit) {
+    const uint32_t lo = a.window == 0 ? i : (i > a.window ? i - a.window : 0u);
+    // 1. in-flight window: txns j in [i - W, i) are PREACCEPTED from i's viewpoint; replica view v has
+    //    not witnessed j with probability drop_p (ad_drop_hash).
+    int q = s - 1;
+    for (; q >= seg0; --q) {
+        const uint32_t j = a.e_txn[q];
+        if (j < lo) break;
+        const uint32_t mj = a.e_meta[q];
+        if (!manages(mj) || !witnesses(qk, meta_kind(mj))) continue;
+        const bool direct = !manages_execution(mj);
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh)) emit(v, direct, j);
+    }
+    // 2. the committed prefix [seg0, p]: mapReduceActive with transitive-dependency elision.
+    const int p = q;
+    if (p < seg0) return;
+    uint64_t M1 = a.pm_w[p];
+    const uint64_t b1 = a.tx_ts[i] + 1;
+    if (M1 >= b1) {   // a bumped executeAt beyond the bound: exact maxCommittedWriteBefore
+        M1 = 0;
+        for (int x = p; x >= seg0; --x) {
+            uint32_t m = a.e_meta[x];
+            uint64_t e = a.e_exec1[x];
+            if (category(m) == CAT_ELIDABLE && meta_kind(m) == AD_KIND_WRITE && e < b1 && e > M1) M1 = e;
+        }
+    }
+    int qe = next_elidable(a, p, seg0, M1, qk);
+    int qa = a.ud_prev[p];
+    if (qa < seg0) qa = -1;
+    while (qe >= seg0 || qa >= 0) {
+        if (qa > qe) {
+            const uint32_t mj = a.e_meta[qa];
+            if (witnesses(qk, meta_kind(mj))) {
+                const uint32_t j = a.e_txn[qa];
+                const bool direct = !manages_execution(mj);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) emit(v, direct, j);
+            }
+            const int nx = qa - 1;
+            qa = nx >= seg0 ? a.ud_prev[nx] : -1;
+            if (qa < seg0) qa = -1;
+        } else {
+            const uint32_t j = a.e_txn[qe];
+            const bool direct = !manages_execution(a.e_meta[qe]);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) emit(v, direct, j);
+            qe = next_elidable(a, qe - 1, seg0, M1, qk);
+        }
+    }
+}
+
+// Real pairs of small key txns, one thread per sorted entry (neighbouring threads walk one segment).
 template <int NV, bool FILL>
 __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -224,61 +367,9 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
             if (direct) c1[v]++; else c0[v]++;
         }
     };
-    const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT;
-    if (query) {
-        const int seg0 = a.seg_start[s];
-        const uint32_t lo = a.window == 0 ? i : (i > a.window ? i - a.window : 0u);
-        // 1. in-flight window: txns j in [i - W, i) are PREACCEPTED from i's viewpoint; replica
-        //    view v has not witnessed j with probability drop_p (ad_drop_hash).
-        int q = (int)s - 1;
-        for (; q >= seg0; --q) {
-            const uint32_t j = a.e_txn[q];
-            if (j < lo) break;
-            const uint32_t mj = a.e_meta[q];
-            if (!manages(mj) || !witnesses(qk, meta_kind(mj))) continue;
-            const bool direct = !manages_execution(mj);
-#pragma unroll
-            for (int v = 0; v < NV; ++v)
-                if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh)) emit(v, direct, j);
-        }
-        // 2. the committed prefix [seg0, p]: mapReduceActive with transitive-dependency elision.
-        const int p = q;
-        if (p >= seg0) {
-            uint64_t M1 = a.pm_w[p];
-            const uint64_t b1 = a.tx_ts[i] + 1;
-            if (M1 >= b1) {   // a bumped executeAt beyond the bound: exact maxCommittedWriteBefore
-                M1 = 0;
-                for (int x = p; x >= seg0; --x) {
-                    uint32_t m = a.e_meta[x];
-                    uint64_t e = a.e_exec1[x];
-                    if (category(m) == CAT_ELIDABLE && meta_kind(m) == AD_KIND_WRITE && e < b1 && e > M1) M1 = e;
-                }
-            }
-            int qe = next_elidable(a, p, seg0, M1, qk);
-            int qa = a.ud_prev[p];
-            if (qa < seg0) qa = -1;
-            while (qe >= seg0 || qa >= 0) {
-                if (qa > qe) {
-                    const uint32_t mj = a.e_meta[qa];
-                    if (witnesses(qk, meta_kind(mj))) {
-                        const uint32_t j = a.e_txn[qa];
-                        const bool direct = !manages_execution(mj);
-#pragma unroll
-                        for (int v = 0; v < NV; ++v) emit(v, direct, j);
-                    }
-                    const int nx = qa - 1;
-                    qa = nx >= seg0 ? a.ud_prev[nx] : -1;
-                    if (qa < seg0) qa = -1;
-                } else {
-                    const uint32_t j = a.e_txn[qe];
-                    const bool direct = !manages_execution(a.e_meta[qe]);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) emit(v, direct, j);
-                    qe = next_elidable(a, qe - 1, seg0, M1, qk);
-                }
-            }
-        }
-    }
+    // small key-domain query txns only (large ones are virtual items)
+    const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE);
+    if (query) walk_query<NV>(a, i, qk, (int)s, a.seg_start[s], emit);
     if (!FILL) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -288,11 +379,36 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     }
 }
 
+// Virtual items (large txns), one thread per item; counts/slots AoS [x * 2NV + vc].
+template <int NV, bool FILL>
+__global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= a.V) return;
+    const uint32_t i = a.vi_txn[x];
+    const uint32_t mi = a.meta[i];
+    const uint32_t qk = meta_kind(mi);
+    uint32_t c[2 * NV];
+#pragma unroll
+    for (int vc = 0; vc < 2 * NV; ++vc)
+        c[vc] = FILL ? a.vdst[x * (2 * NV) + vc] + a.vcnt[x * (2 * NV) + vc] - 1 : 0u;
+    auto emit = [&](int v, bool direct, uint32_t j) {
+        const int vc = 2 * v + (direct ? 1 : 0);
+        if (FILL) a.k2t[vc][c[vc]--] = (int32_t)j;
+        else c[vc]++;
+    };
+    if (qk <= AD_KIND_EXCLUSIVE_SYNC_POINT) walk_query<NV>(a, i, qk, (int)a.vi_pos[x], (int)a.vi_seg0[x], emit);
+    if (!FILL) {
+#pragma unroll
+        for (int vc = 0; vc < 2 * NV; ++vc) a.vcnt[x * (2 * NV) + vc] = c[vc];
+    }
+}
+
 struct TxnArgs {
     size_t n, P;
     int nvc;
     const uint32_t* key_off;
     const uint64_t* keys;
+    const uint8_t* meta;
     const uint32_t* spos;
     const uint32_t* cnt;          // [vc * P + s]
     uint32_t* nk;                 // [vc * n + t]
@@ -303,13 +419,31 @@ struct TxnArgs {
     int32_t* out_k2t[NVC_MAX];
     uint32_t* dst;                // [vc * P + s]
     Params* prm;
+    // large txns (virtual items, in (txn, key) order): items [voff[t], voff[t+1])
+    const uint32_t* voff;
+    const uint32_t* vcnt;         // [x * nvc + vc]
+    uint32_t* vdst;               // [x * nvc + vc]
+    const uint64_t* vi_key;
 };
 
 __global__ __launch_bounds__(256) void k_txn_counts(TxnArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
+    if (a.meta[t] & META_LARGE) {
+        const uint32_t b = a.voff[t], e = a.voff[t + 1];
+        for (int vc = 0; vc < a.nvc; ++vc) {
+            uint32_t nk = 0, ne = 0;
+            for (uint32_t x = b; x < e; ++x) {
+                uint32_t c = a.vcnt[(size_t)x * a.nvc + vc];
+                nk += c > 0;
+                ne += c;
+            }
+            a.nk[(size_t)vc * a.n + t] = nk;
+            a.ne[(size_t)vc * a.n + t] = ne;
+        }
+        return;
+    }
     const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
-    if (e - b > KMAX) { atomicOr(&a.prm->err, ERR_KEYS); return; }
     for (int vc = 0; vc < a.nvc; ++vc) {
         uint32_t nk = 0, ne = 0;
         for (uint32_t p = b; p < e; ++p) {
@@ -322,53 +456,29 @@ __global__ __launch_bounds__(256) void k_txn_counts(TxnArgs a) {
     }
 }
 
-// Per txn: keys in ascending order, KeyDeps header offsets, per-pair first-entry slot.
+// Per txn: keys in ascending order (Keys are sorted), KeyDeps header offsets, per-item first-entry slot.
 __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
-    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
-    const int K = (int)(e - b);
-    if (K > KMAX || K == 0) return;
-    uint64_t ks[KMAX];
-    uint32_t ss[KMAX];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        if (k < K) { ks[k] = a.keys[b + k]; ss[k] = a.spos[b + k]; }
-    }
-    // insertion sort by key (Keys are a sorted set: KeyDeps keys ascending)
-#pragma unroll
-    for (int k = 1; k < KMAX; ++k) {
-        if (k < K) {
-#pragma unroll
-            for (int x = k; x > 0; --x) {
-                if (ks[x - 1] > ks[x]) {
-                    uint64_t tk = ks[x - 1]; ks[x - 1] = ks[x]; ks[x] = tk;
-                    uint32_t ts = ss[x - 1]; ss[x - 1] = ss[x]; ss[x] = ts;
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 1; k < KMAX; ++k)
-        if (k < K && ks[k] == ks[k - 1]) atomicOr(&a.prm->err, ERR_DUPKEY);
+    const bool large = a.meta[t] & META_LARGE;
+    const uint32_t b = large ? a.voff[t] : a.key_off[t], e = large ? a.voff[t + 1] : a.key_off[t + 1];
     for (int vc = 0; vc < a.nvc; ++vc) {
         const uint32_t kb = a.out_key_off[vc][t];
         const uint32_t nk = a.out_key_off[vc][t + 1] - kb;
         if (nk == 0) continue;
         const uint32_t mb = a.out_k2t_off[vc][t];
         uint32_t run = nk, kk = 0;
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            if (k < K) {
-                const uint32_t c = a.cnt[(size_t)vc * a.P + ss[k]];
-                if (c > 0) {
-                    a.out_keys[vc][kb + kk] = ks[k];
-                    a.dst[(size_t)vc * a.P + ss[k]] = mb + run;
-                    run += c;
-                    a.out_k2t[vc][mb + kk] = (int32_t)run;
-                    ++kk;
-                }
-            }
+        for (uint32_t x = b; x < e; ++x) {
+            uint32_t c;
+            if (large) c = a.vcnt[(size_t)x * a.nvc + vc];
+            else c = a.cnt[(size_t)vc * a.P + a.spos[x]];
+            if (c == 0) continue;
+            a.out_keys[vc][kb + kk] = large ? a.vi_key[x] : a.keys[x];
+            if (large) a.vdst[(size_t)x * a.nvc + vc] = mb + run;
+            else a.dst[(size_t)vc * a.P + a.spos[x]] = mb + run;
+            run += c;
+            a.out_k2t[vc][mb + kk] = (int32_t)run;
+            ++kk;
         }
     }
 }
@@ -416,6 +526,7 @@ __device__ inline uint32_t union_lists(int32_t* __restrict__ k2t, const uint32_t
 struct UnionArgs {
     size_t n;
     int nvc;
+    const uint8_t* meta;
     const uint32_t* key_off[NVC_MAX];
     const uint32_t* k2t_off[NVC_MAX];
     const uint32_t* ent_off[NVC_MAX];
@@ -424,9 +535,11 @@ struct UnionArgs {
     uint32_t* tcnt[NVC_MAX];
 };
 
+// Small txns: register K-way merge of the per-key lists (large txns: k_union_lds).
 __global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
+    if (a.meta[t] & META_LARGE) return;
     for (int vc = 0; vc < a.nvc; ++vc) {
         const uint32_t nk = a.key_off[vc][t + 1] - a.key_off[vc][t];
         if (nk == 0) { a.tcnt[vc][t] = 0; continue; }

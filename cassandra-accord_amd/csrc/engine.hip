@@ -2,11 +2,12 @@
 //
 // One ad_handle = one CommandStore shard on one GPU: a HIP stream, a device arena and the loaded
 // batch.  Stages:
-//   prepare   batch statistics, timestamp packing (ts64), pair owners       (deps_kernels.h)
-//   sort      stable LSD radix sort of (key, pair)                          (radix_sort.h)
-//   deps      CFK elision scans, per-pair walk (count/fill), per-txn layout and TxnId union
-//   merge     Deps.merge of the R replica views per txn                     (merge_kernels.h)
-//   levels    execution levels over key chains + deps                       (level_kernels.h)
+//   prepare   batch statistics, timestamp packing (ts64), pair owners, footprint checks   (deps_kernels.h)
+//   sort      stable LSD radix sort of (key, pair); range entries by (start, end, owner)  (radix_sort.h)
+//   deps      CFK elision scan, per-pair / per-virtual-item walks (count, fill), per-txn KeyDeps
+//             layout, TxnId unions; RangeDeps interval join                               (deps/union/range)
+//   merge     Deps.merge of the R replica views per txn, all three classes                (merge_kernels.h)
+//   levels    execution levels over key chains + deps                                     (level_kernels.h)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -15,7 +16,6 @@
 #include <string>
 #include <vector>
 
-#include "deps_kernels.h"
 #include "level_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
@@ -51,20 +51,33 @@ struct ad_handle {
     Params* prm = nullptr;
     Params hprm{};
     TsPack pack{};
-    int key_bits = 0;
+    int key_bits = 0, range_bits = 0;
+    uint64_t rbase = 0, wmax = 0;
+    uint32_t n_large = 0;
     uint64_t *tx_ts = nullptr, *ex1 = nullptr;
     uint8_t* meta = nullptr;
     uint32_t *pair_txn = nullptr, *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;
     uint32_t *skey = nullptr, *sval = nullptr;           // sorted (alias ka/kb)
-    uint32_t *e_txn = nullptr, *spos = nullptr;
+    uint32_t *e_txn = nullptr, *spos = nullptr, *uidx = nullptr, *useg = nullptr;
+    uint64_t* ukey = nullptr;
     uint8_t* e_meta = nullptr;
     uint64_t *e_exec1 = nullptr, *pm_w = nullptr, *pm_c = nullptr;
     int32_t *seg_start = nullptr, *ud_prev = nullptr;
     uint32_t *cnt = nullptr, *dst = nullptr, *nk = nullptr, *ne = nullptr;
+    // virtual items (large txns)
+    size_t V = 0;
+    uint32_t *vn = nullptr, *voff = nullptr, *vi_txn = nullptr, *vi_pos = nullptr, *vi_seg0 = nullptr;
+    uint32_t *vcnt = nullptr, *vdst = nullptr;
+    uint64_t* vi_key = nullptr;
+    // range entries sorted by (start, end, owner)
+    uint32_t *rowner = nullptr, *rk0 = nullptr, *rv0 = nullptr, *rk1 = nullptr, *rv1 = nullptr, *eown = nullptr;
+    uint64_t *es = nullptr, *ee = nullptr;
+    uint32_t *rnk = nullptr, *rne = nullptr;
     void* scratch = nullptr;
     size_t scratch_cap = 0;
     std::vector<Csr> deps;           // [view * 2 + class]  (key, direct)
-    Csr merged[2];
+    Csr rdeps[MAXV];                 // RangeDeps per view
+    Csr merged[3];
     bool have_deps = false, have_merged = false, have_levels = false;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
@@ -100,9 +113,13 @@ int dalloc(ad_handle* h, size_t slot, T** out, size_t count) {
     DBuf& b = h->bufs[slot];
     size_t bytes = std::max<size_t>(count * sizeof(T), 256);
     if (b.cap < bytes) {
-        if (b.p) { HIPCHK(h, hipStreamSynchronize(h->st)); HIPCHK(h, hipFree(b.p)); }
+        if (b.p) { HIPCHK(h, hipStreamSynchronize(h->st)); HIPCHK(h, hipFree(b.p)); b.p = nullptr; b.cap = 0; }
         size_t nb = std::max(bytes, b.cap + b.cap / 4);
-        HIPCHK(h, hipMalloc(&b.p, nb));
+        if (hipMalloc(&b.p, nb) != hipSuccess) {
+            b.p = nullptr;
+            (void)hipGetLastError();
+            return set_err(h, AD_ERR_NOMEM, "device allocation of " + std::to_string(nb) + " bytes failed");
+        }
         b.cap = nb;
     }
     *out = (T*)b.p;
@@ -113,9 +130,13 @@ enum Slot : size_t {
     S_TM, S_TL, S_TN, S_EM, S_EL, S_EN, S_ST, S_KOFF, S_KEYS, S_ROFF, S_RS, S_RE,
     S_PRM, S_TXTS, S_EX1, S_META, S_PTXN, S_KA, S_VA, S_KB, S_VB, S_ETXN, S_SPOS, S_EMETA, S_EEXEC,
     S_PMW, S_PMC, S_SEG, S_UD, S_CNT, S_DST, S_NK, S_NE, S_SCRATCH,
-    S_LVL, S_ORDER, S_LEVEL0,
+    S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
+    S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE,
     S_CSR0 = 100
 };
+// CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
+// merged [NVC_MAX + MAXV, +3)
+constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV;
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
 
@@ -129,17 +150,19 @@ int ensure_scratch(ad_handle* h, size_t bytes) {
     return AD_OK;
 }
 
-int alloc_csr(ad_handle* h, size_t slot_base, Csr& c, size_t n) {
-    CK(dalloc(h, slot_base + 0, &c.key_off, n + 1));
-    CK(dalloc(h, slot_base + 1, &c.k2t_off, n + 1));
-    CK(dalloc(h, slot_base + 2, &c.ent_off, n + 1));
-    CK(dalloc(h, slot_base + 3, &c.tcnt, n));
+int alloc_csr(ad_handle* h, size_t block, Csr& c, size_t n) {
+    const size_t base = S_CSR0 + 10 * block;
+    CK(dalloc(h, base + 0, &c.key_off, n + 1));
+    CK(dalloc(h, base + 1, &c.k2t_off, n + 1));
+    CK(dalloc(h, base + 2, &c.ent_off, n + 1));
+    CK(dalloc(h, base + 3, &c.tcnt, n));
     return AD_OK;
 }
-int alloc_csr_data(ad_handle* h, size_t slot_base, Csr& c) {
-    CK(dalloc(h, slot_base + 4, &c.keys, c.nkeys));
-    CK(dalloc(h, slot_base + 5, &c.k2t, c.nk2t));
-    CK(dalloc(h, slot_base + 6, &c.txns, c.ncap));
+int alloc_csr_data(ad_handle* h, size_t block, Csr& c, int kw) {
+    const size_t base = S_CSR0 + 10 * block;
+    CK(dalloc(h, base + 4, &c.keys, c.nkeys * kw));
+    CK(dalloc(h, base + 5, &c.k2t, c.nk2t));
+    CK(dalloc(h, base + 6, &c.txns, c.ncap));
     return AD_OK;
 }
 
@@ -149,20 +172,42 @@ void scan_offsets(ad_handle* h, const T* in, T* out, size_t n) {
     device_scan(SumOp<T>{in, out, n}, n, (T*)h->scratch, h->st);
 }
 
+// key_off / ent_off / k2t_off of one batched CSR from per-txn (keys, entries) counts
+void csr_offsets(ad_handle* h, Csr& c, const uint32_t* nk, const uint32_t* ne) {
+    const size_t n = h->n;
+    KScope ks(K_SCAN_OFFSETS);
+    scan_offsets(h, nk, c.key_off, n);
+    scan_offsets(h, ne, c.ent_off, n);
+    if (n) device_scan(Sum2Op<uint32_t>{nk, ne, c.k2t_off, n}, n, (uint32_t*)h->scratch, h->st);
+    else hipMemsetAsync(c.k2t_off, 0, 4, h->st);
+}
+
+int read_params(ad_handle* h) {
+    HIPCHK(h, hipMemcpyAsync(&h->hprm, h->prm, sizeof(Params), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
+int check_params(ad_handle* h) {
+    const unsigned e = h->hprm.err;
+    if (e & ERR_UNSORTED) return set_err(h, AD_ERR_UNSORTED, "batch TxnIds are not strictly ascending");
+    if (e & ERR_KEYORDER) return set_err(h, AD_ERR_ARGUMENT, "a txn's keys must be strictly ascending (Keys), and range txns carry no keys");
+    if (e & ERR_RANGEORDER) return set_err(h, AD_ERR_ARGUMENT, "a txn's ranges must be sorted, disjoint, start < end (Ranges), and key txns carry no ranges");
+    if (e & ERR_CAP) return set_err(h, AD_ERR_UNSUPPORTED, "more than 8192 dependency entries in one txn's CSR (LDS union capacity)");
+    return AD_OK;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // prepare + sort
 // ---------------------------------------------------------------------------------------------------
 int stage_prepare(ad_handle* h) {
-    const size_t n = h->n, P = h->P;
+    const size_t n = h->n, P = h->P, Q = h->Q;
     hipStream_t st = h->st;
     k_params_init<<<1, 1, 0, st>>>(h->prm);
-    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(n, P) + 255) / 256));
-    { KScope ks(K_MINMAX); k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_off, h->prm); }
-    HIPCHK(h, hipMemcpyAsync(&h->hprm, h->prm, sizeof(Params), hipMemcpyDeviceToHost, st));
-    HIPCHK(h, hipStreamSynchronize(st));
+    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
+    { KScope ks(K_MINMAX); k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_s, h->range_e, Q, h->prm); }
+    CK(read_params(h));
     const Params& p = h->hprm;
-    if (p.err & ERR_RANGE) return set_err(h, AD_ERR_UNSUPPORTED, "range-domain transactions are not supported by this build's device path");
-    if (p.max_keys > (unsigned)KMAX) return set_err(h, AD_ERR_UNSUPPORTED, "more than 16 keys in one transaction");
     if (n == 0) return AD_OK;
     int MB = bits_of(p.msb_max - p.msb_min), HB = bits_of(p.hlc_max - p.hlc_min), NB = bits_of((uint64_t)(p.node_max_b - p.node_min_b));
     if (MB + HB + 4 + NB > 63) return set_err(h, AD_ERR_UNSUPPORTED, "timestamp spread exceeds the 63-bit packed order key");
@@ -175,25 +220,46 @@ int stage_prepare(ad_handle* h) {
     h->pack.total_bits = NB + 4 + HB + MB;
     h->key_bits = P ? bits_of(p.key_max - p.key_min) : 0;
     if (h->key_bits > 32) return set_err(h, AD_ERR_UNSUPPORTED, "key spread exceeds 32 bits");
+    h->n_large = p.n_large;
+    h->rbase = Q ? p.rs_min : 0;
+    h->wmax = Q ? p.rw_max : 0;
+    h->range_bits = Q ? bits_of(p.re_max - p.rs_min) : 0;
+    if (h->range_bits > 32) return set_err(h, AD_ERR_UNSUPPORTED, "range spread exceeds 32 bits");
     KScope ks(K_PACK);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
-                                                    h->status, h->key_off, h->keys, h->tx_ts, h->ex1, h->meta, h->pair_txn,
-                                                    h->ka, h->va, h->prm);
+                                                    h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
+                                                    h->range_e, h->tx_ts, h->ex1, h->meta, h->pair_txn, h->ka, h->va, h->prm);
     return AD_OK;
 }
 
-int stage_sort(ad_handle* h) {
-    const size_t P = h->P;
-    if (P == 0) return AD_OK;
+RadixScratch radix_scratch(ad_handle* h, size_t n) {
     RadixScratch rs;
-    const size_t hl = radix_hist_len(P);
+    const size_t hl = radix_hist_len(n);
     uint8_t* base = (uint8_t*)h->scratch;
     rs.hist = (uint32_t*)base;
     rs.offs = rs.hist + hl + 64;
     rs.agg = rs.offs + hl + 64;
-    bool flip = radix_sort_pairs(h->ka, h->va, h->kb, h->vb, P, h->key_bits, rs, h->st);
-    h->skey = flip ? h->kb : h->ka;
-    h->sval = flip ? h->vb : h->va;
+    return rs;
+}
+
+int stage_sort(ad_handle* h) {
+    const size_t n = h->n, P = h->P, Q = h->Q;
+    hipStream_t st = h->st;
+    if (P > 0) {
+        bool flip = radix_sort_pairs(h->ka, h->va, h->kb, h->vb, P, h->key_bits, radix_scratch(h, P), st);
+        h->skey = flip ? h->kb : h->ka;
+        h->sval = flip ? h->vb : h->va;
+    }
+    if (Q > 0) {
+        // (start, end, owner): stable by end, then stable by start, over the owner-ordered input
+        k_range_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->meta, h->range_off, h->range_s, h->range_e, h->rbase,
+                                                              h->rowner, h->rk0, h->rv0);
+        uint32_t *k = h->rk0, *v = h->rv0, *ko = h->rk1, *vo = h->rv1;
+        if (radix_sort_pairs(k, v, ko, vo, Q, h->range_bits, radix_scratch(h, Q), st)) { std::swap(k, ko); std::swap(v, vo); }
+        k_range_startkey<<<ceil_div((long)Q, 256), 256, 0, st>>>(Q, h->range_s, v, h->rbase, k);
+        if (radix_sort_pairs(k, v, ko, vo, Q, h->range_bits, radix_scratch(h, Q), st)) { std::swap(k, ko); std::swap(v, vo); }
+        k_range_gather<<<ceil_div((long)Q, 256), 256, 0, st>>>(Q, v, h->range_s, h->range_e, h->rowner, h->es, h->ee, h->eown);
+    }
     return AD_OK;
 }
 
@@ -202,85 +268,160 @@ int stage_sort(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 template <int NV>
 void launch_walk(const WalkArgs& a, bool fill, hipStream_t st) {
-    const int g = ceil_div((long)a.P, 256);
-    KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT);
-    if (fill) k_deps_walk<NV, true><<<g, 256, 0, st>>>(a);
-    else k_deps_walk<NV, false><<<g, 256, 0, st>>>(a);
-}
-void walk(const WalkArgs& a, int nv, bool fill, hipStream_t st) {
-    switch (nv) {
-        case 1: launch_walk<1>(a, fill, st); break;
-        case 2: launch_walk<2>(a, fill, st); break;
-        case 3: launch_walk<3>(a, fill, st); break;
-        case 4: launch_walk<4>(a, fill, st); break;
-        case 5: launch_walk<5>(a, fill, st); break;
-        case 6: launch_walk<6>(a, fill, st); break;
-        case 7: launch_walk<7>(a, fill, st); break;
-        default: launch_walk<8>(a, fill, st); break;
+    if (a.P > 0) {
+        const int g = ceil_div((long)a.P, 256);
+        KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT);
+        if (fill) k_deps_walk<NV, true><<<g, 256, 0, st>>>(a);
+        else k_deps_walk<NV, false><<<g, 256, 0, st>>>(a);
+    }
+    if (a.V > 0) {
+        const int g = ceil_div((long)a.V, 256);
+        KScope ks(K_VITEMS);
+        if (fill) k_vitem_walk<NV, true><<<g, 256, 0, st>>>(a);
+        else k_vitem_walk<NV, false><<<g, 256, 0, st>>>(a);
     }
 }
+template <int NV>
+void launch_range(const RangeArgs& a, bool fill, hipStream_t st) {
+    const int g = ceil_div((long)a.n * WAVE, 256);
+    KScope ks(K_RANGE);
+    if (fill) k_range_deps<NV, true><<<g, 256, 0, st>>>(a);
+    else k_range_deps<NV, false><<<g, 256, 0, st>>>(a);
+}
+#define NV_DISPATCH(nv, F, ...)                      \
+    switch (nv) {                                    \
+        case 1: F<1>(__VA_ARGS__); break;            \
+        case 2: F<2>(__VA_ARGS__); break;            \
+        case 3: F<3>(__VA_ARGS__); break;            \
+        case 4: F<4>(__VA_ARGS__); break;            \
+        case 5: F<5>(__VA_ARGS__); break;            \
+        case 6: F<6>(__VA_ARGS__); break;            \
+        case 7: F<7>(__VA_ARGS__); break;            \
+        default: F<8>(__VA_ARGS__); break;           \
+    }
 
 int stage_deps(ad_handle* h) {
-    const size_t n = h->n, P = h->P;
+    const size_t n = h->n, P = h->P, Q = h->Q;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     hipStream_t st = h->st;
     h->deps.resize(nvc);
-    for (int vc = 0; vc < nvc; ++vc) CK(alloc_csr(h, S_CSR0 + 10 * vc, h->deps[vc], n));
+    for (int vc = 0; vc < nvc; ++vc) CK(alloc_csr(h, vc, h->deps[vc], n));
+    for (int v = 0; v < nv; ++v) CK(alloc_csr(h, CSR_RANGE0 + v, h->rdeps[v], n));
     if (P > 0) {
         { KScope ks(K_GATHER); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->pair_txn, h->meta, h->ex1, h->e_txn, h->e_meta,
-                                                                   h->e_exec1, h->spos); }
-        ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c};
+                                                                                          h->e_exec1, h->spos); }
+        ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
+                    h->uidx, h->ukey, h->useg, h->hprm.key_min, P, h->prm};
         KScope ks(K_SCAN_ELIDE);
         device_scan(eop, P, (ElideOp::S*)h->scratch, st);
     }
+    // ---- virtual items of large txns
+    h->V = 0;
+    VItemArgs va{};
+    va.n = n; va.meta = h->meta; va.key_off = h->key_off; va.keys = h->keys; va.range_off = h->range_off;
+    va.rs = h->range_s; va.re = h->range_e; va.spos = h->spos; va.seg_start = h->seg_start; va.e_txn = h->e_txn;
+    va.ukey = h->ukey; va.useg = h->useg; va.prm = h->prm; va.vn = h->vn; va.voff = h->voff;
+    if (h->n_large > 0) {
+        KScope ks(K_VITEMS);
+        k_vitems<false><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
+        scan_offsets(h, h->vn, h->voff, n);
+        uint32_t V = 0;
+        HIPCHK(h, hipMemcpyAsync(&V, h->voff + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        h->V = V;
+        CK(dalloc(h, S_VTXN, &h->vi_txn, V)); CK(dalloc(h, S_VPOS, &h->vi_pos, V)); CK(dalloc(h, S_VSEG, &h->vi_seg0, V));
+        CK(dalloc(h, S_VKEY, &h->vi_key, V));
+        CK(dalloc(h, S_VCNT, &h->vcnt, (size_t)V * nvc)); CK(dalloc(h, S_VDST, &h->vdst, (size_t)V * nvc));
+        va.vi_txn = h->vi_txn; va.vi_pos = h->vi_pos; va.vi_seg0 = h->vi_seg0; va.vi_key = h->vi_key;
+        if (V > 0) k_vitems<true><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
+    }
+    // ---- walk (count)
     WalkArgs wa{};
     wa.e_txn = h->e_txn; wa.e_meta = h->e_meta; wa.e_exec1 = h->e_exec1; wa.seg_start = h->seg_start;
-    wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.P = P;
+    wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
     wa.cnt = h->cnt; wa.dst = h->dst;
-    if (P > 0) walk(wa, nv, false, st);
+    wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
+    NV_DISPATCH(nv, launch_walk, wa, false, st);
     TxnArgs ta{};
-    ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.spos = h->spos; ta.cnt = h->cnt;
+    ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.spos = h->spos; ta.cnt = h->cnt;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
+    ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
     if (n > 0) { KScope ks(K_TXN_COUNTS); k_txn_counts<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
-    for (int vc = 0; vc < nvc; ++vc) {
-        KScope ks(K_SCAN_OFFSETS);
-        Csr& c = h->deps[vc];
-        scan_offsets(h, h->nk + (size_t)vc * n, c.key_off, n);
-        scan_offsets(h, h->ne + (size_t)vc * n, c.ent_off, n);
-        if (n) device_scan(Sum2Op<uint32_t>{h->nk + (size_t)vc * n, h->ne + (size_t)vc * n, c.k2t_off, n}, n, (uint32_t*)h->scratch, st);
-        else hipMemsetAsync(c.k2t_off, 0, 4, st);
+    for (int vc = 0; vc < nvc; ++vc) csr_offsets(h, h->deps[vc], h->nk + (size_t)vc * n, h->ne + (size_t)vc * n);
+    // ---- RangeDeps (count)
+    RangeArgs ra{};
+    ra.n = n; ra.Q = Q; ra.key_off = h->key_off; ra.keys = h->keys; ra.range_off = h->range_off; ra.rs = h->range_s;
+    ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.wmax = h->wmax;
+    ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
+    if (Q > 0 && n > 0) {
+        NV_DISPATCH(nv, launch_range, ra, false, st);
+        for (int v = 0; v < nv; ++v) csr_offsets(h, h->rdeps[v], h->rnk + (size_t)v * n, h->rne + (size_t)v * n);
     }
-    // sizes -> host (one sync), allocate outputs
-    std::vector<uint32_t> tot(3 * nvc);
-    for (int vc = 0; vc < nvc; ++vc) {
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * vc + 0], h->deps[vc].key_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * vc + 1], h->deps[vc].k2t_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * vc + 2], h->deps[vc].ent_off + n, 4, hipMemcpyDeviceToHost, st));
+    // ---- sizes -> host (one sync), allocate outputs
+    const int ncsr = nvc + nv;
+    std::vector<uint32_t> tot(3 * ncsr, 0);
+    auto csr_at = [&](int c) -> Csr& { return c < nvc ? h->deps[c] : h->rdeps[c - nvc]; };
+    for (int c = 0; c < ncsr; ++c) {
+        if (c >= nvc && Q == 0) continue;
+        Csr& x = csr_at(c);
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * c + 0], x.key_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * c + 1], x.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * c + 2], x.ent_off + n, 4, hipMemcpyDeviceToHost, st));
     }
-    HIPCHK(h, hipMemcpyAsync(&h->hprm, h->prm, sizeof(Params), hipMemcpyDeviceToHost, st));
-    HIPCHK(h, hipStreamSynchronize(st));
-    if (h->hprm.err & ERR_UNSORTED) return set_err(h, AD_ERR_UNSORTED, "batch TxnIds are not strictly ascending");
-    if (h->hprm.err & ERR_KEYS) return set_err(h, AD_ERR_UNSUPPORTED, "more than 16 keys in one transaction");
+    CK(read_params(h));
+    CK(check_params(h));
     h->deps_entries = 0;
-    for (int vc = 0; vc < nvc; ++vc) {
-        Csr& c = h->deps[vc];
-        c.nkeys = tot[3 * vc]; c.nk2t = tot[3 * vc + 1]; c.ncap = tot[3 * vc + 2];
-        h->deps_entries += c.ncap;
-        CK(alloc_csr_data(h, S_CSR0 + 10 * vc, c));
-        ta.out_key_off[vc] = c.key_off; ta.out_k2t_off[vc] = c.k2t_off; ta.out_keys[vc] = c.keys; ta.out_k2t[vc] = c.k2t;
-        wa.k2t[vc] = c.k2t;
+    for (int c = 0; c < ncsr; ++c) {
+        Csr& x = csr_at(c);
+        x.nkeys = tot[3 * c]; x.nk2t = tot[3 * c + 1]; x.ncap = tot[3 * c + 2];
+        h->deps_entries += x.ncap;
+        if (c < nvc) {
+            CK(alloc_csr_data(h, c, x, 1));
+            ta.out_key_off[c] = x.key_off; ta.out_k2t_off[c] = x.k2t_off; ta.out_keys[c] = x.keys; ta.out_k2t[c] = x.k2t;
+            wa.k2t[c] = x.k2t;
+        } else {
+            CK(alloc_csr_data(h, CSR_RANGE0 + (c - nvc), x, 2));
+            const int v = c - nvc;
+            ra.key_off_v[v] = x.key_off; ra.k2t_off_v[v] = x.k2t_off; ra.keys_v[v] = x.keys; ra.k2t_v[v] = x.k2t;
+        }
     }
+    // ---- fill
     if (n > 0) { KScope ks(K_TXN_LAYOUT); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
-    if (P > 0) walk(wa, nv, true, st);
+    NV_DISPATCH(nv, launch_walk, wa, true, st);
+    if (Q > 0 && n > 0) NV_DISPATCH(nv, launch_range, ra, true, st);
     UnionArgs ua{};
-    ua.n = n; ua.nvc = nvc;
+    ua.n = n; ua.nvc = nvc; ua.meta = h->meta;
     for (int vc = 0; vc < nvc; ++vc) {
         Csr& c = h->deps[vc];
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
     if (n > 0) { KScope ks(K_TXN_UNION); k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua); }
+    // large txns' key CSRs and every RangeDeps CSR: LDS sort union
+    if (n > 0 && (h->n_large > 0 || Q > 0)) {
+        KScope ks(K_UNION_LDS);
+        LdsUnionArgs la{};
+        la.n = n; la.meta = h->meta; la.prm = h->prm;
+        if (h->n_large > 0) {
+            la.ncsr = nvc; la.only_large = 1;
+            for (int vc = 0; vc < nvc; ++vc) {
+                Csr& c = h->deps[vc];
+                la.key_off[vc] = c.key_off; la.k2t_off[vc] = c.k2t_off; la.ent_off[vc] = c.ent_off; la.k2t[vc] = c.k2t;
+                la.txns[vc] = c.txns; la.tcnt[vc] = c.tcnt;
+            }
+            k_union_lds<<<dim3((unsigned)n, (unsigned)nvc), UB, 0, st>>>(la);
+        }
+        if (Q > 0) {
+            la.ncsr = nv; la.only_large = 0;
+            for (int v = 0; v < nv; ++v) {
+                Csr& c = h->rdeps[v];
+                la.key_off[v] = c.key_off; la.k2t_off[v] = c.k2t_off; la.ent_off[v] = c.ent_off; la.k2t[v] = c.k2t;
+                la.txns[v] = c.txns; la.tcnt[v] = c.tcnt;
+            }
+            k_union_lds<<<dim3((unsigned)n, (unsigned)nv), UB, 0, st>>>(la);
+        }
+    }
     h->have_deps = true;
     return AD_OK;
 }
@@ -294,18 +435,20 @@ int stage_merge(ad_handle* h) {
     const int nv = (int)h->cfg.replicas;
     hipStream_t st = h->st;
     h->merged_entries = 0;
-    for (int cls = 0; cls < 2; ++cls) {
+    for (int cls = 0; cls < 3; ++cls) {
         Csr& m = h->merged[cls];
-        CK(alloc_csr(h, S_CSR0 + 10 * (NVC_MAX + cls), m, n));
+        CK(alloc_csr(h, CSR_MERGED0 + cls, m, n));
+        if (cls == AD_CLASS_RANGE && h->Q == 0) { m.nkeys = m.nk2t = m.ncap = 0; continue; }
+        const int kw = cls == AD_CLASS_RANGE ? 2 : 1;
         MergeArgs ma{};
         ma.n = n; ma.nv = nv;
         for (int v = 0; v < nv; ++v) {
-            const Csr& c = h->deps[2 * v + cls];
+            const Csr& c = cls == AD_CLASS_RANGE ? h->rdeps[v] : h->deps[2 * v + cls];
             ma.key_off[v] = c.key_off; ma.keys[v] = c.keys; ma.k2t_off[v] = c.k2t_off; ma.k2t[v] = c.k2t;
             ma.ent_off[v] = c.ent_off; ma.txns[v] = c.txns; ma.tcnt[v] = c.tcnt;
         }
         ma.mk = h->nk; ma.me = h->ne; ma.mu = h->nk + n;   // scratch counters (n each)
-        if (n > 0) merge_launch(ma, nv, false, st);
+        if (n > 0) merge_launch(ma, nv, false, kw, st);
         {
             KScope ks(K_SCAN_OFFSETS);
             scan_offsets(h, ma.mk, m.key_off, n);
@@ -317,13 +460,14 @@ int stage_merge(ad_handle* h) {
         HIPCHK(h, hipMemcpyAsync(&tot[0], m.key_off + n, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipMemcpyAsync(&tot[1], m.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipMemcpyAsync(&tot[2], m.ent_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipStreamSynchronize(st));
+        CK(read_params(h));
+        CK(check_params(h));
         m.nkeys = tot[0]; m.nk2t = tot[1]; m.ncap = tot[2];
         h->merged_entries += m.nk2t - m.nkeys;
-        CK(alloc_csr_data(h, S_CSR0 + 10 * (NVC_MAX + cls), m));
+        CK(alloc_csr_data(h, CSR_MERGED0 + cls, m, kw));
         ma.o_key_off = m.key_off; ma.o_keys = m.keys; ma.o_k2t_off = m.k2t_off; ma.o_k2t = m.k2t;
         ma.o_ent_off = m.ent_off; ma.o_txns = m.txns; ma.o_tcnt = m.tcnt;
-        if (n > 0) merge_launch(ma, nv, true, st);
+        if (n > 0) merge_launch(ma, nv, true, kw, st);
     }
     h->have_merged = true;
     return AD_OK;
@@ -338,7 +482,9 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.n = h->n; li.P = h->P; li.skey = h->skey; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
     li.seg_start = h->seg_start; li.meta = h->meta; li.ex1 = h->ex1; li.lvl = h->lvl; li.order = h->order;
     li.scratch = h->scratch; li.scratch_cap = h->scratch_cap;
-    li.merged_direct = &h->merged[1];
+    li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
+    li.merged_range = &h->merged[AD_CLASS_RANGE];
+    li.n_large = h->n_large;
     li.exec_bits = h->pack.total_bits;
     int iters = 0;
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
@@ -348,12 +494,12 @@ int stage_levels(ad_handle* h, bool want_order) {
     return AD_OK;
 }
 
-int fetch_csr(ad_handle* h, const Csr& c, ad_csr_out* out) {
+int fetch_csr(ad_handle* h, const Csr& c, int kw, ad_csr_out* out) {
     const size_t n = h->n;
     hipStream_t st = h->st;
     std::vector<uint32_t> ent(n + 1), cnt(n);
     HIPCHK(h, hipMemcpyAsync(out->key_off, c.key_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
-    if (c.nkeys) HIPCHK(h, hipMemcpyAsync(out->keys, c.keys, c.nkeys * 8, hipMemcpyDeviceToHost, st));
+    if (c.nkeys) HIPCHK(h, hipMemcpyAsync(out->keys, c.keys, c.nkeys * 8 * kw, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipMemcpyAsync(out->k2t_off, c.k2t_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
     if (c.nk2t) HIPCHK(h, hipMemcpyAsync(out->k2t, c.k2t, c.nk2t * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipMemcpyAsync(ent.data(), c.ent_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
@@ -375,7 +521,7 @@ int fetch_csr(ad_handle* h, const Csr& c, ad_csr_out* out) {
 int csr_sizes(ad_handle* h, const Csr& c, ad_csr_sizes* s) {
     s->n = h->n; s->keys = c.nkeys; s->k2t = c.nk2t; s->txn_cap = c.ncap;
     std::vector<uint32_t> cnt(h->n);
-    if (h->n) {
+    if (h->n && c.ncap) {
         HIPCHK(h, hipMemcpyAsync(cnt.data(), c.tcnt, h->n * 4, hipMemcpyDeviceToHost, h->st));
         HIPCHK(h, hipStreamSynchronize(h->st));
     }
@@ -437,11 +583,14 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     if (n >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
     const size_t P = n ? b->key_off[n] : 0;
     const size_t Q = (n && b->range_off) ? b->range_off[n] : 0;
+    if (P >= (1ull << 31) || Q >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
     h->n = n; h->P = P; h->Q = Q;
+    h->loaded = false;
     h->have_deps = h->have_merged = h->have_levels = false;
     CK(dalloc(h, S_TM, &h->tm, n)); CK(dalloc(h, S_TL, &h->tl, n)); CK(dalloc(h, S_TN, &h->tn, n));
     CK(dalloc(h, S_EM, &h->em, n)); CK(dalloc(h, S_EL, &h->el, n)); CK(dalloc(h, S_EN, &h->en, n));
     CK(dalloc(h, S_ST, &h->status, n)); CK(dalloc(h, S_KOFF, &h->key_off, n + 1)); CK(dalloc(h, S_KEYS, &h->keys, P));
+    CK(dalloc(h, S_ROFF, &h->range_off, n + 1)); CK(dalloc(h, S_RS, &h->range_s, Q)); CK(dalloc(h, S_RE, &h->range_e, Q));
     hipStream_t st = h->st;
     if (n) {
         HIPCHK(h, hipMemcpyAsync(h->tm, b->txn_msb, n * 8, hipMemcpyHostToDevice, st));
@@ -456,15 +605,15 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     } else {
         HIPCHK(h, hipMemsetAsync(h->key_off, 0, 4, st));
     }
-    h->range_off = nullptr;
     if (Q) {
-        CK(dalloc(h, S_ROFF, &h->range_off, n + 1)); CK(dalloc(h, S_RS, &h->range_s, Q)); CK(dalloc(h, S_RE, &h->range_e, Q));
         HIPCHK(h, hipMemcpyAsync(h->range_off, b->range_off, (n + 1) * 4, hipMemcpyHostToDevice, st));
         HIPCHK(h, hipMemcpyAsync(h->range_s, b->range_start, Q * 8, hipMemcpyHostToDevice, st));
         HIPCHK(h, hipMemcpyAsync(h->range_e, b->range_end, Q * 8, hipMemcpyHostToDevice, st));
+    } else {
+        HIPCHK(h, hipMemsetAsync(h->range_off, 0, (n + 1) * 4, st));
     }
     // working buffers
-    const int nvc = 2 * (int)h->cfg.replicas;
+    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     CK(dalloc(h, S_PRM, &h->prm, 1));
     CK(dalloc(h, S_TXTS, &h->tx_ts, n)); CK(dalloc(h, S_EX1, &h->ex1, n)); CK(dalloc(h, S_META, &h->meta, n));
     CK(dalloc(h, S_PTXN, &h->pair_txn, P));
@@ -472,11 +621,18 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     CK(dalloc(h, S_ETXN, &h->e_txn, P)); CK(dalloc(h, S_SPOS, &h->spos, P)); CK(dalloc(h, S_EMETA, &h->e_meta, P));
     CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
     CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
+    CK(dalloc(h, S_UIDX, &h->uidx, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
     CK(dalloc(h, S_CNT, &h->cnt, (size_t)nvc * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
     CK(dalloc(h, S_NK, &h->nk, (size_t)nvc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nvc * n + n));
+    CK(dalloc(h, S_VN, &h->vn, n)); CK(dalloc(h, S_VOFF, &h->voff, n + 1));
     CK(dalloc(h, S_LVL, &h->lvl, n + 1)); CK(dalloc(h, S_ORDER, &h->order, n + 1));
-    size_t sc = std::max<size_t>(1 << 20, 3 * (radix_hist_len(std::max(P, n)) + 128) * 4 + 64 * 1024);
-    sc = std::max(sc, device_scan_scratch<ElideOp>(std::max(P, n)) + 4096);
+    CK(dalloc(h, S_ROWN, &h->rowner, Q)); CK(dalloc(h, S_RK0, &h->rk0, Q)); CK(dalloc(h, S_RV0, &h->rv0, Q));
+    CK(dalloc(h, S_RK1, &h->rk1, Q)); CK(dalloc(h, S_RV1, &h->rv1, Q));
+    CK(dalloc(h, S_ES, &h->es, Q)); CK(dalloc(h, S_EE, &h->ee, Q)); CK(dalloc(h, S_EOWN, &h->eown, Q));
+    CK(dalloc(h, S_RNK, &h->rnk, (size_t)nv * n)); CK(dalloc(h, S_RNE, &h->rne, (size_t)nv * n));
+    const size_t big = std::max(std::max(P, n), Q);
+    size_t sc = std::max<size_t>(1 << 20, 3 * (radix_hist_len(big) + 128) * 4 + 64 * 1024);
+    sc = std::max(sc, device_scan_scratch<ElideOp>(big) + 4096);
     sc = std::max(sc, level_scratch_bytes(n, P));
     CK(ensure_scratch(h, sc));
     HIPCHK(h, hipStreamSynchronize(st));
@@ -492,12 +648,15 @@ int ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes) {
     CK(stage_prepare(h));
     CK(stage_sort(h));
     CK(stage_deps(h));
+    CK(read_params(h));
+    CK(check_params(h));
     if (sizes) {
         const int nv = (int)h->cfg.replicas;
         for (int v = 0; v < nv; ++v) {
             CK(csr_sizes(h, h->deps[2 * v], &sizes[v * AD_NUM_CLASSES + 0]));
             CK(csr_sizes(h, h->deps[2 * v + 1], &sizes[v * AD_NUM_CLASSES + 1]));
-            sizes[v * AD_NUM_CLASSES + 2] = ad_csr_sizes{h->n, 0, 0, 0, 0};
+            if (h->Q) CK(csr_sizes(h, h->rdeps[v], &sizes[v * AD_NUM_CLASSES + 2]));
+            else sizes[v * AD_NUM_CLASSES + 2] = ad_csr_sizes{h->n, 0, 0, 0, 0};
         }
     }
     return AD_OK;
@@ -513,8 +672,8 @@ int ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
     if (view >= h->cfg.replicas || cls >= AD_NUM_CLASSES) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    if (cls == AD_CLASS_RANGE) return fetch_empty(h, out);
-    return fetch_csr(h, h->deps[2 * view + cls], out);
+    if (cls == AD_CLASS_RANGE) return h->Q ? fetch_csr(h, h->rdeps[view], 2, out) : fetch_empty(h, out);
+    return fetch_csr(h, h->deps[2 * view + cls], 1, out);
 }
 
 int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
@@ -525,7 +684,8 @@ int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
     if (sizes) {
         CK(csr_sizes(h, h->merged[0], &sizes[0]));
         CK(csr_sizes(h, h->merged[1], &sizes[1]));
-        sizes[2] = ad_csr_sizes{h->n, 0, 0, 0, 0};
+        if (h->Q) CK(csr_sizes(h, h->merged[2], &sizes[2]));
+        else sizes[2] = ad_csr_sizes{h->n, 0, 0, 0, 0};
     }
     return AD_OK;
 }
@@ -535,8 +695,8 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     if (cls >= AD_NUM_CLASSES) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    if (cls == AD_CLASS_RANGE) return fetch_empty(h, out);
-    return fetch_csr(h, h->merged[cls], out);
+    if (cls == AD_CLASS_RANGE) return h->Q ? fetch_csr(h, h->merged[2], 2, out) : fetch_empty(h, out);
+    return fetch_csr(h, h->merged[cls], 1, out);
 }
 
 int ad_merge_host(ad_handle* h, const ad_csr_in*, uint32_t, ad_csr_sizes*) {

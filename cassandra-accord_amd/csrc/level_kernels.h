@@ -186,6 +186,8 @@ struct LevelInputs {
     void* scratch;
     size_t scratch_cap;
     const DevCsr* merged_direct;
+    const DevCsr* merged_range;
+    uint32_t n_large;
     uint32_t exec_bits;
 };
 
@@ -199,8 +201,8 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         cap = bytes;
         return true;
     };
-    if (in.merged_direct && in.merged_direct->nkeys > 0) {
-        err = "exec levels: direct-key (sync point) dependencies are not supported by this build's device path";
+    if ((in.merged_direct && in.merged_direct->nkeys > 0) || (in.merged_range && in.merged_range->nkeys > 0) || in.n_large > 0) {
+        err = "exec levels: direct-key / range dependencies and range txns are not supported by this build's device path";
         return AD_ERR_UNSUPPORTED;
     }
     if (ls.capP < P || !ls.c_txn) {

@@ -10,7 +10,7 @@
 //              per-key lists mapped to TxnIds, then to indices in (1) (remapToSuperset :1249-1275)
 // Two launches: count (key / entry / TxnId totals per txn), then write into scanned offsets.
 #pragma once
-#include "deps_kernels.h"
+#include "range_kernels.h"
 
 namespace ad {
 
@@ -34,7 +34,21 @@ struct MergeArgs {
     uint32_t* o_tcnt;
 };
 
-template <int NV, bool WRITE>
+// KW = u64 words per key: 1 for KeyDeps keys, 2 for RangeDeps (start, end) compared as Range::compare.
+template <int KW>
+struct MKey {
+    uint64_t a, b;
+    __device__ static MKey load(const uint64_t* k, size_t x) {
+        MKey r;
+        r.a = k[KW * x];
+        r.b = KW == 2 ? k[KW * x + 1] : 0ull;
+        return r;
+    }
+    __device__ bool operator<(const MKey& o) const { return a < o.a || (a == o.a && b < o.b); }
+    __device__ bool operator==(const MKey& o) const { return a == o.a && b == o.b; }
+};
+
+template <int NV, bool WRITE, int KW>
 __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
@@ -77,11 +91,11 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     uint32_t ep = omb + onk;         // next entry slot (write pass)
     while (true) {
         bool any = false;
-        uint64_t kmin = 0;
+        MKey<KW> kmin{0ull, 0ull};
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if (kc[v] < ke[v]) {
-                uint64_t k = a.keys[v][kc[v]];
+                MKey<KW> k = MKey<KW>::load(a.keys[v], kc[v]);
                 if (!any || k < kmin) { kmin = k; any = true; }
             }
         }
@@ -91,7 +105,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             lc[v] = 0; le[v] = 0; lh[v] = INF;
-            if (kc[v] < ke[v] && a.keys[v][kc[v]] == kmin) {
+            if (kc[v] < ke[v] && MKey<KW>::load(a.keys[v], kc[v]) == kmin) {
                 const uint32_t ki = kc[v] - a.key_off[v][t];
                 lc[v] = mb[v] + (ki == 0 ? nkv[v] : (uint32_t)a.k2t[v][mb[v] + ki - 1]);
                 le[v] = mb[v] + (uint32_t)a.k2t[v][mb[v] + ki];
@@ -115,7 +129,8 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
                 if (lh[v] == mn) { ++lc[v]; lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF; }
         }
         if (WRITE) {
-            a.o_keys[okb + mk] = kmin;
+            a.o_keys[KW * (size_t)(okb + mk)] = kmin.a;
+            if (KW == 2) a.o_keys[KW * (size_t)(okb + mk) + 1] = kmin.b;
             a.o_k2t[omb + mk] = (int32_t)(ep - omb);
         }
         ++mk;
@@ -125,23 +140,28 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 }
 
 template <int NV>
-inline void merge_launch_nv(const MergeArgs& a, bool write, hipStream_t st) {
+inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t st) {
     const int g = ceil_div((long)a.n, 256);
     KScope ks(write ? K_MERGE_WRITE : K_MERGE_COUNT);
-    if (write) k_merge<NV, true><<<g, 256, 0, st>>>(a);
-    else k_merge<NV, false><<<g, 256, 0, st>>>(a);
+    if (kw == 2) {
+        if (write) k_merge<NV, true, 2><<<g, 256, 0, st>>>(a);
+        else k_merge<NV, false, 2><<<g, 256, 0, st>>>(a);
+    } else {
+        if (write) k_merge<NV, true, 1><<<g, 256, 0, st>>>(a);
+        else k_merge<NV, false, 1><<<g, 256, 0, st>>>(a);
+    }
 }
 
-inline void merge_launch(const MergeArgs& a, int nv, bool write, hipStream_t st) {
+inline void merge_launch(const MergeArgs& a, int nv, bool write, int kw, hipStream_t st) {
     switch (nv) {
-        case 1: merge_launch_nv<1>(a, write, st); break;
-        case 2: merge_launch_nv<2>(a, write, st); break;
-        case 3: merge_launch_nv<3>(a, write, st); break;
-        case 4: merge_launch_nv<4>(a, write, st); break;
-        case 5: merge_launch_nv<5>(a, write, st); break;
-        case 6: merge_launch_nv<6>(a, write, st); break;
-        case 7: merge_launch_nv<7>(a, write, st); break;
-        default: merge_launch_nv<8>(a, write, st); break;
+        case 1: merge_launch_nv<1>(a, write, kw, st); break;
+        case 2: merge_launch_nv<2>(a, write, kw, st); break;
+        case 3: merge_launch_nv<3>(a, write, kw, st); break;
+        case 4: merge_launch_nv<4>(a, write, kw, st); break;
+        case 5: merge_launch_nv<5>(a, write, kw, st); break;
+        case 6: merge_launch_nv<6>(a, write, kw, st); break;
+        case 7: merge_launch_nv<7>(a, write, kw, st); break;
+        default: merge_launch_nv<8>(a, write, kw, st); break;
     }
 }
 

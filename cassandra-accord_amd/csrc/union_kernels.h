@@ -1,0 +1,221 @@
+// union_kernels.h — virtual query items of large txns, and the per-txn TxnId union in LDS (gfx950).
+//
+// Large txns are range-domain txns (InMemorySafeStore.mapReduceActive visits every CommandsForKey key
+// inside each range: commandsForKey.subMap(start, false, end, true), impl/InMemoryCommandStore.java:272-307)
+// and key txns with more than KMAX keys.  Each (txn, distinct key) they query is a "virtual item":
+// (txn i, key, segment start, insert position of TxnId i in the key's (key, TxnId)-sorted segment).
+// Items of one txn are contiguous and in key order, so the KeyDeps layout is an in-order pass.
+//
+// k_union_lds is RelationMultiMap.AbstractBuilder.build's global value sort + index mapping
+// (utils/RelationMultiMap.java:208-257) for one txn's CSR: a bitonic sort of the txn's dependency
+// ranks in LDS, a compaction to the sorted unique TxnId list, and a binary-search remap of each
+// keysToTxnIds entry to its index.  Used for large txns' key CSRs and every RangeDeps CSR.
+#pragma once
+#include "deps_kernels.h"
+
+namespace ad {
+
+__device__ inline uint32_t lb_u64(const uint64_t* a, uint32_t lo, uint32_t hi, uint64_t v) {   // first a[x] >= v
+    while (lo < hi) {
+        uint32_t m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+__device__ inline uint32_t ub_u64(const uint64_t* a, uint32_t lo, uint32_t hi, uint64_t v) {   // first a[x] > v
+    while (lo < hi) {
+        uint32_t m = (lo + hi) >> 1;
+        if (a[m] <= v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+__device__ inline uint32_t ub_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {   // first a[x] > v
+    while (lo < hi) {
+        uint32_t m = (lo + hi) >> 1;
+        if (a[m] <= v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+struct VItemArgs {
+    size_t n;
+    const uint8_t* meta;
+    const uint32_t* key_off;
+    const uint64_t* keys;
+    const uint32_t* range_off;
+    const uint64_t* rs;
+    const uint64_t* re;
+    const uint32_t* spos;
+    const int32_t* seg_start;
+    const uint32_t* e_txn;
+    const uint64_t* ukey;        // [U] distinct keys
+    const uint32_t* useg;        // [U+1]
+    const Params* prm;           // n_keys_u
+    uint32_t* vn;                // [n] items per txn (count pass)
+    const uint32_t* voff;        // [n+1] (fill pass)
+    uint32_t* vi_txn;
+    uint32_t* vi_pos;
+    uint32_t* vi_seg0;
+    uint64_t* vi_key;
+};
+
+// CFK keys inside (s, e]  (EndInclusive: start excluded, end included)
+__device__ inline void keys_in_range(const VItemArgs& a, uint32_t U, uint64_t s, uint64_t e, uint32_t& lo, uint32_t& hi) {
+    lo = ub_u64(a.ukey, 0, U, s);
+    hi = ub_u64(a.ukey, lo, U, e);
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint32_t m = a.meta[t];
+    if (!(m & META_LARGE)) {
+        if (!FILL) a.vn[t] = 0;
+        return;
+    }
+    const uint32_t U = a.prm->n_keys_u;
+    if (meta_domain(m) == AD_DOMAIN_KEY) {
+        const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
+        if (!FILL) { a.vn[t] = e - b; return; }
+        uint32_t x = a.voff[t];
+        for (uint32_t p = b; p < e; ++p, ++x) {
+            const uint32_t s = a.spos[p];
+            a.vi_txn[x] = (uint32_t)t;
+            a.vi_pos[x] = s;                       // the pair itself: walk [seg0, s)
+            a.vi_seg0[x] = (uint32_t)a.seg_start[s];
+            a.vi_key[x] = a.keys[p];
+        }
+        return;
+    }
+    const uint32_t rb = a.range_off[t], rend = a.range_off[t + 1];
+    uint32_t c = 0;
+    uint32_t x = FILL ? a.voff[t] : 0u;
+    for (uint32_t q = rb; q < rend; ++q) {
+        uint32_t lo, hi;
+        keys_in_range(a, U, a.rs[q], a.re[q], lo, hi);
+        if (!FILL) { c += hi - lo; continue; }
+        for (uint32_t u = lo; u < hi; ++u, ++x) {
+            const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+            a.vi_txn[x] = (uint32_t)t;
+            a.vi_pos[x] = ub_u32(a.e_txn, s0, s1, (uint32_t)t);   // insertPos(TxnId t): first entry with txn > t
+            a.vi_seg0[x] = s0;
+            a.vi_key[x] = a.ukey[u];
+        }
+    }
+    if (!FILL) a.vn[t] = c;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Block-level helpers (256 threads)
+// ---------------------------------------------------------------------------------------------------
+constexpr int UB = 256;
+
+// exclusive scan of one u32 per thread; returns the exclusive prefix, *total = block sum
+__device__ inline uint32_t block_scan_u32(uint32_t v, uint32_t* lds_w /* [UB/WAVE] */, uint32_t* total) {
+    const int lane = __lane_id(), w = threadIdx.x / WAVE;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == WAVE - 1) lds_w[w] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < UB / WAVE; ++k) {
+        uint32_t s = lds_w[k];
+        if (k < w) base += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+template <int CAP>
+__device__ inline void bitonic_sort_lds(uint32_t* buf, uint32_t n2) {
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t x = threadIdx.x; x < n2; x += UB) {
+                const uint32_t y = x ^ j;
+                if (y > x) {
+                    const uint32_t a = buf[x], b = buf[y];
+                    const bool up = (x & k) == 0;
+                    if ((a > b) == up) { buf[x] = b; buf[y] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+constexpr int UNION_CAP = 8192;   // dependency entries of one txn's CSR sorted in LDS (32 KiB)
+
+struct LdsUnionArgs {
+    size_t n;
+    int ncsr;
+    int only_large;
+    const uint8_t* meta;
+    const uint32_t* key_off[NVC_MAX];
+    const uint32_t* k2t_off[NVC_MAX];
+    const uint32_t* ent_off[NVC_MAX];
+    int32_t* k2t[NVC_MAX];
+    uint32_t* txns[NVC_MAX];
+    uint32_t* tcnt[NVC_MAX];
+    Params* prm;
+};
+
+// grid (n, ncsr): one workgroup per (txn, CSR)
+__global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
+    const size_t t = blockIdx.x;
+    const int c = blockIdx.y;
+    if (t >= a.n) return;
+    if (a.only_large && !(a.meta[t] & META_LARGE)) return;
+    __shared__ uint32_t buf[UNION_CAP];
+    __shared__ uint32_t wsum[UB / WAVE];
+    const uint32_t nk = a.key_off[c][t + 1] - a.key_off[c][t];
+    if (nk == 0) {
+        if (threadIdx.x == 0) a.tcnt[c][t] = 0;
+        return;
+    }
+    const uint32_t mb = a.k2t_off[c][t];
+    const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
+    int32_t* body = a.k2t[c] + mb + nk;
+    if (ne > (uint32_t)UNION_CAP) {
+        if (threadIdx.x == 0) { atomicOr(&a.prm->err, ERR_CAP); a.tcnt[c][t] = 0; }
+        return;
+    }
+    uint32_t n2 = 1;
+    while (n2 < ne) n2 <<= 1;
+    for (uint32_t x = threadIdx.x; x < n2; x += UB) buf[x] = x < ne ? (uint32_t)body[x] : 0xFFFFFFFFu;
+    __syncthreads();
+    bitonic_sort_lds<UNION_CAP>(buf, n2);
+    // unique compaction: each thread owns a contiguous chunk
+    const uint32_t per = (ne + UB - 1) / UB;
+    const uint32_t b0 = min(ne, threadIdx.x * per), b1 = min(ne, b0 + per);
+    uint32_t cnt = 0;
+    for (uint32_t x = b0; x < b1; ++x) cnt += (x == 0 || buf[x] != buf[x - 1]) ? 1u : 0u;
+    uint32_t total;
+    uint32_t o = block_scan_u32(cnt, wsum, &total);
+    uint32_t* out = a.txns[c] + a.ent_off[c][t];
+    for (uint32_t x = b0; x < b1; ++x)
+        if (x == 0 || buf[x] != buf[x - 1]) out[o++] = buf[x];
+    __syncthreads();
+    // unique list back into LDS, then remap every entry to its index
+    for (uint32_t x = threadIdx.x; x < total; x += UB) buf[x] = out[x];
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < ne; x += UB) {
+        const uint32_t v = (uint32_t)body[x];
+        uint32_t lo = 0, hi = total;
+        while (lo < hi) {
+            uint32_t m = (lo + hi) >> 1;
+            if (buf[m] < v) lo = m + 1; else hi = m;
+        }
+        body[x] = (int32_t)lo;
+    }
+    if (threadIdx.x == 0) a.tcnt[c][t] = total;
+}
+
+}  // namespace ad

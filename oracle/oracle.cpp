@@ -273,6 +273,18 @@ struct Batch {
         }
         for (size_t i = 1; i < n; ++i)
             if (ts_cmp(tx[i - 1], tx[i]) >= 0) throw std::invalid_argument("batch TxnIds must be strictly ascending");
+        // Keys / Ranges are sorted sets (primitives/Keys.java, AbstractRanges): the ABI requires them so
+        for (size_t i = 0; i < n; ++i) {
+            for (uint32_t p = key_off[i] + 1; p < key_off[i + 1]; ++p)
+                if (keys[p - 1] >= keys[p]) throw std::invalid_argument("a txn's keys must be strictly ascending");
+            for (uint32_t q = range_off[i]; q < range_off[i + 1]; ++q)
+                if (ranges[q].s >= ranges[q].e || (q > range_off[i] && ranges[q].s < ranges[q - 1].e))
+                    throw std::invalid_argument("a txn's ranges must be sorted, disjoint, start < end");
+            if (domain_of(tx[i]) == AD_DOMAIN_RANGE && key_off[i + 1] != key_off[i])
+                throw std::invalid_argument("range txns carry no keys");
+            if (domain_of(tx[i]) == AD_DOMAIN_KEY && range_off[i + 1] != range_off[i])
+                throw std::invalid_argument("key txns carry no ranges");
+        }
     }
 };
 

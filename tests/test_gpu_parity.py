@@ -82,7 +82,7 @@ def test_ragged_keys(engine_factory):
     cnt = rng.integers(1, 17, size=3000)
     keys, off = [], [0]
     for c in cnt:
-        keys.append(rng.choice(500, size=c, replace=False).astype(np.uint64))
+        keys.append(np.sort(rng.choice(500, size=c, replace=False)).astype(np.uint64))
         off.append(off[-1] + c)
     base["keys"] = np.concatenate(keys)
     base["key_off"] = np.array(off, np.uint32)
@@ -110,4 +110,47 @@ def test_unsorted_batch_rejected(engine_factory):
     eng = engine_factory()
     eng.load(b)
     with pytest.raises(engine.AccordDepsError):
+        eng.preaccept_deps()
+
+
+@pytest.mark.parametrize("seed,width", [(21, 400), (22, 40), (23, 3000)])
+def test_range_txns_mixed(engine_factory, seed, width):
+    # RangeDeps interval join + range-domain queries over CFK keys (virtual items)
+    b = workload.generate(3000, 3, 20000, "uniform", range_frac=0.15, range_width_max=width, seed=seed)
+    check(engine_factory, b, window=16, levels=False)
+
+
+def test_range_txns_writes_and_sync_points(engine_factory):
+    rng = np.random.default_rng(31)
+    n = 2500
+    kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT], size=n,
+                       p=[0.4, 0.4, 0.1, 0.1])
+    status = rng.choice([abi.ST_APPLIED, abi.ST_INVALID, abi.ST_COMMITTED], size=n, p=[0.8, 0.1, 0.1]).astype(np.uint8)
+    b = workload.generate(n, 2, 3000, "uniform", range_frac=0.3, range_width_max=200, kinds=kinds, status=status, seed=31)
+    check(engine_factory, b, window=8, levels=False, replicas=4, drop_p=0.25)
+
+
+def test_many_keys_large_path(engine_factory):
+    # key txns with more than KMAX (16) keys take the virtual-item path
+    rng = np.random.default_rng(8)
+    base = workload.generate(1500, keys_per_txn=1, keyspace=400, seed=8)
+    cnt = rng.integers(1, 41, size=1500)
+    keys, off = [], [0]
+    for c in cnt:
+        keys.append(np.sort(rng.choice(400, size=c, replace=False)).astype(np.uint64))
+        off.append(off[-1] + c)
+    base["keys"] = np.concatenate(keys)
+    base["key_off"] = np.array(off, np.uint32)
+    check(engine_factory, base, window=12)
+
+
+def test_unsorted_keys_rejected(engine_factory):
+    from accord_amd import engine
+
+    b = workload.generate(50, keys_per_txn=3, seed=2)
+    b["keys"] = b["keys"].copy()
+    b["keys"][0], b["keys"][1] = b["keys"][1], b["keys"][0]
+    eng = engine_factory()
+    eng.load(b)
+    with pytest.raises(engine.IllegalArgumentException):
         eng.preaccept_deps()
