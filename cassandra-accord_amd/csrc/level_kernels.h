@@ -1,23 +1,32 @@
 // level_kernels.h — execution levels (Kahn wavefront index) over the resolved dependency graph.
 //
 // Semantics (the reference's dynamic release order, local/Commands.java:617-821 and
-// local/cfk/CommandsForKey.java:1208-1330): on every key, a Write waits for all earlier-executeAt
-// Reads and Writes, a Read for earlier-executeAt Writes; every edge raises executeAt, so
-//   level[T] = 1 + max level over T's predecessors (0 if none)
-// is a topological wavefront numbering, and `order` = txns sorted by (level, executeAt).
+// local/cfk/CommandsForKey.java:1208-1330), level[T] = 1 + max level over T's predecessors (0 if none):
+//   (a) managed T (key Read/Write), on every key of T: a Write waits for all earlier-executeAt Reads and
+//       Writes, a Read for earlier-executeAt Writes (notifyManaged, unappliedCounters :1291-1330);
+//   (b) every T: its merged direct-key and range deps with an earlier executeAt
+//       (Commands.updateWaitingOn :740-755);
+//   (c) unmanaged T (range txns), per key of its merged KeyDeps: every managed txn on that key with
+//       executeAt <= the greatest executeAt among T's deps there below T's own (Updating.updateUnmanaged
+//       :740-757 -> Unmanaged APPLY: "wait for it and all earlier txn to Apply", CommandsForKey.java:437-445).
+// Every edge raises executeAt, so the levels are a topological wavefront numbering and `order` = txns
+// sorted by (level, executeAt).
 //
 // Device algorithm (no per-level launches — C3 chains are ~10^5 deep):
-//   1. chain order: the (key, TxnId)-sorted entries are re-sorted by executeAt inside each key
-//      segment (in-place fix-up; nearly sorted because only slow-path txns move).
-//   2. along one key chain the recurrence is a max-plus affine map on the state (y = max level so far,
-//      w = max Write level so far):  Read: y' = max(y, w+1, a), w' = w;  Write: y' = w' = max(y+1, a)
-//      where a = the txn's current level from its other keys.  Maps compose associatively, so one
-//      segmented scan (scan.h) resolves an entire chain at once, whatever its depth.
-//   3. a txn's level is the max over its keys (atomicMax); 2-3 repeat until no level changes.  The
-//      iteration count is the number of chain-to-chain hops on the critical path (C2: ~5).
-//   4. order: LSD radix sorts by executeAt (64-bit, two 32-bit halves) then stably by level.
+//   1. chain order: the (key, TxnId)-sorted entries are re-sorted by executeAt inside each key segment
+//      (in-place fix-up; nearly sorted because only slow-path txns move).
+//   2. along one key chain (a) is a max-plus affine map on the state (y = max level so far, w = max
+//      Write level so far):  Read: y' = max(y, w+1, a), w' = w;  Write: y' = w' = max(y+1, a), where a is
+//      the txn's current level from its other constraints.  Maps compose associatively, so one segmented
+//      scan (scan.h) resolves an entire chain at once, whatever its depth; it also materialises the
+//      inclusive prefix max pm_all used by (c).
+//   3. (b) and (c) are relaxations over the merged CSRs (atomicMax on the level array).
+//   4. 2-3 repeat until no level changes; the iteration count is the number of chain-to-chain hops on
+//      the critical path (C2: ~9).
+//   5. order: LSD radix sorts by executeAt (64-bit, two 32-bit halves) then stably by level.
 #pragma once
 #include "radix_sort.h"
+#include "union_kernels.h"
 
 namespace ad {
 
@@ -37,6 +46,7 @@ struct ChainOp {
     const int32_t* seg_start;     // key segments (same in (key,TxnId) and (key,executeAt) order)
     uint32_t* L;
     uint32_t* changed;
+    int32_t* pm_all;              // inclusive prefix max level along the chain (nullable)
 
     __device__ S identity() const { return S{0, NEG, NEG, 0, NEG, NEG, 0, 0u}; }
     __device__ S load(size_t i) const {
@@ -76,14 +86,18 @@ struct ChainOp {
         return h;
     }
     __device__ void store(size_t i, const S& ex, const S&, const S& el) const {
-        if (!(el.flags & 2u)) return;
         int py, pw;
         if (el.flags & 1u) { py = -1; pw = -1; }
         else {
             py = mp_max(mp_max(mp_add(ex.m00, -1), mp_add(ex.m01, -1)), ex.c0);
             pw = mp_max(mp_max(mp_add(ex.m10, -1), mp_add(ex.m11, -1)), ex.c1);
         }
+        if (!(el.flags & 2u)) {
+            if (pm_all) pm_all[i] = py;
+            return;
+        }
         const int x = (el.flags & 4u) ? mp_max(py + 1, el.a) : mp_max(pw + 1, el.a);
+        if (pm_all) pm_all[i] = mp_max(py, x);
         if (x > el.a) {
             uint32_t old = atomicMax(&L[c_txn[i]], (uint32_t)x);
             if (old < (uint32_t)x) *changed = 1u;
@@ -130,6 +144,109 @@ __global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __
     }
 }
 
+// Rejects kinds the batch execution order does not model (sync points, ephemeral reads, local-only).
+__global__ __launch_bounds__(256) void k_level_kinds(size_t n, const uint8_t* __restrict__ meta, uint32_t* __restrict__ flag) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (t < n) {
+        const uint32_t k = meta_kind(meta[t]);
+        bad = !(k == AD_KIND_READ || k == AD_KIND_WRITE);
+    }
+    if (__ballot(bad) && __lane_id() == 0) atomicOr(flag, 1u);
+}
+
+struct EdgeArgs {
+    size_t n;
+    const uint8_t* meta;
+    const uint64_t* ex1;
+    uint32_t* L;
+    uint32_t* changed;
+    // (b) merged direct / range deps: unique dependency lists
+    const uint32_t* ent_off[2];
+    const uint32_t* tcnt[2];
+    const uint32_t* txns[2];
+    // (c) unmanaged txns, merged KeyDeps
+    const uint32_t* mk_key_off;
+    const uint64_t* mk_keys;
+    const uint32_t* mk_k2t_off;
+    const int32_t* mk_k2t;
+    const uint32_t* mk_ent_off;
+    const uint32_t* mk_txns;
+    int32_t* cons_pos;           // [merged key slot] chain position or -1
+    const int32_t* pm_all;
+    const uint64_t* ukey;
+    const uint32_t* useg;
+    uint32_t U;
+    const uint64_t* c_exec1;
+};
+
+// (c) preparation: for unmanaged T and each key of its merged KeyDeps, the last chain position (in
+// executeAt order) whose executeAt <= bnd = max executeAt of T's deps on that key below T's own.
+__global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint32_t kb = a.mk_key_off[t], ke = a.mk_key_off[t + 1];
+    const bool unmanaged = !manages_execution(a.meta[t]);
+    const uint32_t nk = ke - kb;
+    const uint32_t mb = a.mk_k2t_off[t];
+    const uint32_t tb = a.mk_ent_off[t];
+    const uint64_t my = a.ex1[t];
+    for (uint32_t ki = 0; ki < nk; ++ki) {
+        int32_t pos = -1;
+        if (unmanaged) {
+            const uint32_t from = mb + (ki == 0 ? nk : (uint32_t)a.mk_k2t[mb + ki - 1]);
+            const uint32_t to = mb + (uint32_t)a.mk_k2t[mb + ki];
+            uint64_t bnd = 0;
+            for (uint32_t x = from; x < to; ++x) {
+                const uint64_t e = a.ex1[a.mk_txns[tb + (uint32_t)a.mk_k2t[x]]];
+                if (e < my && e > bnd) bnd = e;
+            }
+            if (bnd != 0) {
+                const uint64_t key = a.mk_keys[kb + ki];
+                const uint32_t u = lb_u64(a.ukey, 0, a.U, key);
+                if (u < a.U && a.ukey[u] == key) {
+                    const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+                    const uint32_t p = ub_u64(a.c_exec1, s0, s1, bnd);     // first executeAt+1 > bnd
+                    pos = p > s0 ? (int32_t)(p - 1) : -1;
+                }
+            }
+        }
+        a.cons_pos[kb + ki] = pos;
+    }
+}
+
+// (b) + (c) relaxation, one thread per txn.
+__global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int do_c) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint64_t my = a.ex1[t];
+    int best = -1;
+    if (do_b) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (!a.txns[c]) continue;
+            const uint32_t b = a.ent_off[c][t], e = b + a.tcnt[c][t];
+            for (uint32_t x = b; x < e; ++x) {
+                const uint32_t d = a.txns[c][x];
+                if (a.ex1[d] < my) best = max(best, (int)a.L[d]);
+            }
+        }
+    }
+    if (do_c && !manages_execution(a.meta[t])) {
+        for (uint32_t x = a.mk_key_off[t]; x < a.mk_key_off[t + 1]; ++x) {
+            const int32_t p = a.cons_pos[x];
+            if (p >= 0) best = max(best, a.pm_all[p]);
+        }
+    }
+    if (best >= 0) {
+        const uint32_t v = (uint32_t)(best + 1);
+        if (v > a.L[t]) {
+            const uint32_t old = atomicMax(&a.L[t], v);
+            if (old < v) *a.changed = 1u;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_exec_split(size_t n, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ idx,
                                                     uint32_t* __restrict__ key, int hi) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -142,21 +259,31 @@ __global__ __launch_bounds__(256) void k_iota(size_t n, uint32_t* __restrict__ v
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
 }
+// gather + block-reduced max (one atomic per block)
 __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx,
                                                     uint32_t* __restrict__ dst, uint32_t* __restrict__ maxv) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t v = 0;
     if (i < n) { v = src[idx[i]]; dst[i] = v; }
     v = wave_max(v);
-    if (maxv && __lane_id() == 0) atomicMax(maxv, v);
+    __shared__ uint32_t red[256 / WAVE];
+    if (__lane_id() == 0) red[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0 && maxv) {
+        uint32_t m = red[0];
+        for (int k = 1; k < 256 / WAVE; ++k) m = m > red[k] ? m : red[k];
+        atomicMax(maxv, m);
+    }
 }
 
 struct LevelState {
-    size_t capP = 0, capN = 0;
+    size_t capP = 0, capN = 0, capK = 0;
     uint32_t* c_txn = nullptr;
     uint8_t* c_meta = nullptr;
     uint64_t* c_exec1 = nullptr;
-    uint32_t* flags = nullptr;          // [0] changed, [1] max level
+    int32_t* pm_all = nullptr;
+    int32_t* cons_pos = nullptr;
+    uint32_t* flags = nullptr;          // [0] changed, [1] max level, [2] unsupported kinds
     void* agg = nullptr;
     size_t agg_cap = 0;
     uint32_t *sk0 = nullptr, *sv0 = nullptr, *sk1 = nullptr, *sv1 = nullptr;
@@ -165,7 +292,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -185,8 +312,12 @@ struct LevelInputs {
     uint32_t* order;
     void* scratch;
     size_t scratch_cap;
+    const DevCsr* merged_key;
     const DevCsr* merged_direct;
     const DevCsr* merged_range;
+    const uint64_t* ukey;
+    const uint32_t* useg;
+    uint32_t U;
     uint32_t n_large;
     uint32_t exec_bits;
 };
@@ -194,50 +325,81 @@ struct LevelInputs {
 inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hipStream_t st, int* iters,
                       std::string& err) {
     const size_t n = in.n, P = in.P;
-    auto grow = [&](void** p, size_t bytes, size_t& cap) -> bool {
-        if (cap >= bytes && *p) return true;
+    auto grow = [&](void** p, size_t bytes) -> bool {
         if (*p) { hipStreamSynchronize(st); hipFree(*p); *p = nullptr; }
-        if (hipMalloc(p, bytes) != hipSuccess) return false;
-        cap = bytes;
+        if (hipMalloc(p, bytes) != hipSuccess) { *p = nullptr; return false; }
         return true;
     };
-    if ((in.merged_direct && in.merged_direct->nkeys > 0) || (in.merged_range && in.merged_range->nkeys > 0) || in.n_large > 0) {
-        err = "exec levels: direct-key / range dependencies and range txns are not supported by this build's device path";
-        return AD_ERR_UNSUPPORTED;
-    }
+    const size_t nkm = in.merged_key ? in.merged_key->nkeys : 0;
     if (ls.capP < P || !ls.c_txn) {
         size_t c = std::max<size_t>(P, 1);
-        size_t dummy;
-        dummy = 0; if (!grow((void**)&ls.c_txn, c * 4, dummy)) goto oom;
-        dummy = 0; if (!grow((void**)&ls.c_meta, c, dummy)) goto oom;
-        dummy = 0; if (!grow((void**)&ls.c_exec1, c * 8, dummy)) goto oom;
+        if (!grow((void**)&ls.c_txn, c * 4) || !grow((void**)&ls.c_meta, c) || !grow((void**)&ls.c_exec1, c * 8) ||
+            !grow((void**)&ls.pm_all, c * 4))
+            goto oom;
         ls.capP = c;
     }
     if (ls.capN < n || !ls.sk0) {
         size_t c = std::max<size_t>(n, 1);
-        size_t dummy;
-        dummy = 0; if (!grow((void**)&ls.sk0, c * 4, dummy)) goto oom;
-        dummy = 0; if (!grow((void**)&ls.sv0, c * 4, dummy)) goto oom;
-        dummy = 0; if (!grow((void**)&ls.sk1, c * 4, dummy)) goto oom;
-        dummy = 0; if (!grow((void**)&ls.sv1, c * 4, dummy)) goto oom;
+        if (!grow((void**)&ls.sk0, c * 4) || !grow((void**)&ls.sv0, c * 4) || !grow((void**)&ls.sk1, c * 4) ||
+            !grow((void**)&ls.sv1, c * 4))
+            goto oom;
         ls.capN = c;
     }
-    if (!ls.flags) { size_t d = 0; if (!grow((void**)&ls.flags, 256, d)) goto oom; }
-    if (!grow(&ls.agg, device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)) + 256, ls.agg_cap)) goto oom;
-    if (!grow((void**)&ls.rs, (3 * (radix_hist_len(std::max<size_t>(n, 1)) + 128) + 64 * 1024) * 4, ls.rs_cap)) goto oom;
+    if (ls.capK < nkm || !ls.cons_pos) {
+        size_t c = std::max<size_t>(nkm, 1);
+        if (!grow((void**)&ls.cons_pos, c * 4)) goto oom;
+        ls.capK = c;
+    }
+    if (!ls.flags && !grow((void**)&ls.flags, 256)) goto oom;
+    {
+        const size_t need = device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)) + 256;
+        if (ls.agg_cap < need) { if (!grow(&ls.agg, need)) goto oom; ls.agg_cap = need; }
+        const size_t rneed = (3 * (radix_hist_len(std::max<size_t>(n, 1)) + 128) + 64 * 1024) * 4;
+        if (ls.rs_cap < rneed) { if (!grow((void**)&ls.rs, rneed)) goto oom; ls.rs_cap = rneed; }
+    }
 
+    hipMemsetAsync(ls.flags, 0, 16, st);
+    if (n > 0) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 2);
+    {
+        uint32_t bad = 0;
+        hipMemcpyAsync(&bad, ls.flags + 2, 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
+        if (bad) {
+            err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+            return AD_ERR_UNSUPPORTED;
+        }
+    }
     hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
     *iters = 0;
-    if (P > 0) {
-        {
+    {
+        const bool has_b = (in.merged_direct && in.merged_direct->ncap > 0) || (in.merged_range && in.merged_range->ncap > 0);
+        const bool has_c = in.n_large > 0 && nkm > 0 && P > 0;
+        EdgeArgs ea{};
+        ea.n = n; ea.meta = in.meta; ea.ex1 = in.ex1; ea.L = in.lvl; ea.changed = ls.flags;
+        const DevCsr* bc[2] = {in.merged_direct, in.merged_range};
+        for (int c = 0; c < 2; ++c) {
+            if (bc[c] && bc[c]->ncap > 0) { ea.ent_off[c] = bc[c]->ent_off; ea.tcnt[c] = bc[c]->tcnt; ea.txns[c] = bc[c]->txns; }
+        }
+        if (in.merged_key) {
+            ea.mk_key_off = in.merged_key->key_off; ea.mk_keys = in.merged_key->keys; ea.mk_k2t_off = in.merged_key->k2t_off;
+            ea.mk_k2t = in.merged_key->k2t; ea.mk_ent_off = in.merged_key->ent_off; ea.mk_txns = in.merged_key->txns;
+        }
+        ea.cons_pos = ls.cons_pos; ea.pm_all = ls.pm_all; ea.ukey = in.ukey; ea.useg = in.useg; ea.U = in.U;
+        ea.c_exec1 = ls.c_exec1;
+        if (P > 0) {
             KScope ks(K_CHAIN_PREP);
             k_chain_copy<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
             k_chain_order<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
+            if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);
         }
-        ChainOp op{ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.flags};
+        ChainOp op{ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.flags, has_c ? ls.pm_all : nullptr};
         for (int it = 0; it < (1 << 22); ++it) {
             hipMemsetAsync(ls.flags, 0, 4, st);
-            { KScope ks(K_SCAN_CHAIN); device_scan(op, P, (ChainOp::S*)ls.agg, st); }
+            if (P > 0) { KScope ks(K_SCAN_CHAIN); device_scan(op, P, (ChainOp::S*)ls.agg, st); }
+            if ((has_b || has_c) && n > 0) {
+                KScope ks(K_LEVEL_EDGES);
+                k_level_edges<<<ceil_div((long)n, 256), 256, 0, st>>>(ea, has_b ? 1 : 0, has_c ? 1 : 0);
+            }
             uint32_t changed = 0;
             if (hipMemcpyAsync(&changed, ls.flags, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {
@@ -249,6 +411,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         }
     }
     if (want_order && n > 0) {
+        KScope ks(K_ORDER);
         RadixScratch rs;
         const size_t hl = radix_hist_len(n);
         rs.hist = ls.rs;

@@ -117,7 +117,7 @@ def test_unsorted_batch_rejected(engine_factory):
 def test_range_txns_mixed(engine_factory, seed, width):
     # RangeDeps interval join + range-domain queries over CFK keys (virtual items)
     b = workload.generate(3000, 3, 20000, "uniform", range_frac=0.15, range_width_max=width, seed=seed)
-    check(engine_factory, b, window=16, levels=False)
+    check(engine_factory, b, window=16)
 
 
 def test_range_txns_writes_and_sync_points(engine_factory):
@@ -154,3 +154,23 @@ def test_unsorted_keys_rejected(engine_factory):
     eng.load(b)
     with pytest.raises(engine.IllegalArgumentException):
         eng.preaccept_deps()
+
+
+def test_levels_reject_sync_points(engine_factory):
+    from accord_amd import engine
+
+    kinds = np.array([abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_READ] * 10)
+    b = workload.generate(30, 2, 50, kinds=kinds, seed=3)
+    eng = engine_factory()
+    eng.load(b)
+    eng.preaccept_deps()
+    eng.merge()
+    with pytest.raises(engine.AccordDepsError):
+        eng.exec_levels()
+
+
+def test_c4_scaled(engine_factory):
+    # BASELINE configs[3] shape (10% range txns, widths U[1, 2^13]) scaled to 40k txns over a 400k keyspace
+    b = workload.generate(40000, 4, 400_000, "uniform", range_frac=0.1, range_width_max=1 << 13,
+                          seed=workload.SEEDS["C4"])
+    check(engine_factory, b)

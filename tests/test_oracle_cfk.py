@@ -154,13 +154,22 @@ def canon_check(b, res):
     for i in range(n):
         for k in keys_of[i]:
             by_key.setdefault(k, []).append(i)
-    direct, rng = res.merged(DIRECT), res.merged(RANGE)
+    direct, rng, keyd = res.merged(DIRECT), res.merged(RANGE), res.merged(KEY)
+    is_range = (b["txn_lsb"] & np.uint64(1)).astype(bool)
     for t in range(n):
         preds = set()
         for k in keys_of[t]:
             for dd in by_key[k]:
                 if ex[dd] < ex[t] and (kind[t] == W or kind[dd] == W):
                     preds.add(dd)
+        if is_range[t]:
+            # unmanaged (Updating.updateUnmanaged): per key of its KeyDeps, every managed txn executing at or
+            # before the latest of its deps there that executes before it
+            for k, deps in deps_of(keyd, t).items():
+                below = [ex[x] for x in deps if ex[x] < ex[t]]
+                if below:
+                    bnd = max(below)
+                    preds.update(dd for dd in by_key.get(k, []) if ex[dd] <= bnd)
         for csr in (direct, rng):
             for deps in deps_of(csr, t).values():
                 preds.update(x for x in deps if ex[x] < ex[t])
@@ -182,4 +191,12 @@ def test_levels_read_batches_released_together():
     res, b = run([T(1, W, [1]), T(2, R, [1]), T(3, R, [1]), T(4, R, [1]), T(5, W, [1]), T(6, R, [1])], levels=True)
     lv, order = res.levels()
     assert list(lv) == [0, 1, 1, 1, 2, 3]
+    canon_check(b, res)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_levels_canon_invariant_with_range_txns(seed):
+    b = workload.generate(1200, keys_per_txn=2, keyspace=400, range_frac=0.2, range_width_max=60, slow_frac=0.3,
+                          bump_max=40, seed=seed)
+    res = O.OracleResult(b, abi.make_config(8, 3, 0.2, seed), O.FLAG_MERGE | O.FLAG_LEVELS)
     canon_check(b, res)
