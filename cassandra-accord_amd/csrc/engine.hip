@@ -479,9 +479,9 @@ int stage_merge(ad_handle* h) {
 int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_exec_levels before ad_merge_deps");
     LevelInputs li{};
-    li.n = h->n; li.P = h->P; li.skey = h->skey; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.meta = h->meta; li.ex1 = h->ex1; li.lvl = h->lvl; li.order = h->order;
-    li.scratch = h->scratch; li.scratch_cap = h->scratch_cap;
+    li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
+    li.seg_start = h->seg_start; li.spos = h->spos; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.lvl = h->lvl; li.order = h->order;
     li.merged_key = &h->merged[AD_CLASS_KEY];
     li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
     li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;

@@ -34,6 +34,39 @@ constexpr int NEG = -(1 << 29);
 __device__ inline int mp_add(int x, int y) { return (x <= NEG || y <= NEG) ? NEG : x + y; }
 __device__ inline int mp_max(int x, int y) { return x > y ? x : y; }
 
+// Re-queue the other chain segments of txn t after its level rose to x (worklist fixpoint).
+struct PushCtx {
+    const uint32_t* key_off;     // [n+1] txn -> pair range
+    const int32_t* pair_seg;     // [P] head position of each pair's chain segment
+    const uint32_t* seg_len;     // [P] valid at head positions
+    uint32_t* stamp;             // [P] at heads: the iteration the segment is (re)queued for
+    uint32_t* long_dirty;        // long segments must be rescanned next iteration
+    uint32_t iter1;              // current iteration + 1
+};
+constexpr uint32_t SHORT_SEG = 64;   // chains up to this length: one thread walks them
+
+// Returns true if some short segment was newly queued for the next iteration (the caller reports it
+// once per wave, so the "work left" flag sees one store per wave, not one per push).
+__device__ inline bool raise_level(uint32_t* L, uint32_t t, uint32_t x, int32_t own_seg, const PushCtx& c) {
+    const uint32_t old = atomicMax(&L[t], x);
+    if (old >= x) return false;
+    bool queued = false;
+    for (uint32_t p = c.key_off[t]; p < c.key_off[t + 1]; ++p) {
+        const int32_t h = c.pair_seg[p];
+        if (h == own_seg) continue;
+        const uint32_t len = c.seg_len[h];
+        if (len < 2) continue;
+        if (len > SHORT_SEG) {
+            if (*(volatile uint32_t*)c.long_dirty == 0u) *c.long_dirty = 1u;
+            continue;
+        }
+        if (atomicMax(&c.stamp[h], c.iter1) < c.iter1) queued = true;
+    }
+    return queued;
+}
+
+// Long chains: the (a) recurrence as a segmented max-plus scan over the concatenated long segments
+// (positions through `idx`), whatever their depth.
 struct ChainOp {
     struct S {
         int m00, m01, m10, m11;   // max-plus matrix
@@ -41,17 +74,20 @@ struct ChainOp {
         int a;                    // element only: the txn's level estimate
         uint32_t flags;           // element only: bit0 head, bit1 participates, bit2 write
     };
+    const uint32_t* idx;          // scan index -> chain position
     const uint32_t* c_txn;
     const uint8_t* c_meta;
     const int32_t* seg_start;     // key segments (same in (key,TxnId) and (key,executeAt) order)
     uint32_t* L;
-    uint32_t* changed;
-    int32_t* pm_all;              // inclusive prefix max level along the chain (nullable)
+    int32_t* pm_all;              // inclusive prefix max level along the chain
+    PushCtx push;
+    uint32_t* work_left;          // some short segment is queued for the next iteration
 
     __device__ S identity() const { return S{0, NEG, NEG, 0, NEG, NEG, 0, 0u}; }
     __device__ S load(size_t i) const {
-        const uint32_t m = c_meta[i];
-        const bool head = seg_start[i] == (int32_t)i;
+        const uint32_t pos = idx[i];
+        const uint32_t m = c_meta[pos];
+        const bool head = seg_start[pos] == (int32_t)pos;
         const bool part = manages_execution(m);
         const bool wr = meta_kind(m) == AD_KIND_WRITE;
         S s = identity();
@@ -60,7 +96,7 @@ struct ChainOp {
             if (head) { s.m00 = s.m01 = s.m10 = s.m11 = NEG; s.c0 = -1; s.c1 = -1; }
             return s;
         }
-        const int a = (int)L[c_txn[i]];
+        const int a = (int)L[c_txn[pos]];
         s.a = a;
         if (head) {                          // constant map: f(init = (-1,-1))
             s.m00 = s.m01 = s.m10 = s.m11 = NEG;
@@ -86,6 +122,7 @@ struct ChainOp {
         return h;
     }
     __device__ void store(size_t i, const S& ex, const S&, const S& el) const {
+        const uint32_t pos = idx[i];
         int py, pw;
         if (el.flags & 1u) { py = -1; pw = -1; }
         else {
@@ -93,17 +130,89 @@ struct ChainOp {
             pw = mp_max(mp_max(mp_add(ex.m10, -1), mp_add(ex.m11, -1)), ex.c1);
         }
         if (!(el.flags & 2u)) {
-            if (pm_all) pm_all[i] = py;
+            pm_all[pos] = py;
             return;
         }
         const int x = (el.flags & 4u) ? mp_max(py + 1, el.a) : mp_max(pw + 1, el.a);
-        if (pm_all) pm_all[i] = mp_max(py, x);
-        if (x > el.a) {
-            uint32_t old = atomicMax(&L[c_txn[i]], (uint32_t)x);
-            if (old < (uint32_t)x) *changed = 1u;
-        }
+        pm_all[pos] = mp_max(py, x);
+        if (x > el.a && raise_level(L, c_txn[pos], (uint32_t)x, seg_start[pos], push))
+            if (*(volatile uint32_t*)work_left == 0u) *work_left = 1u;
     }
 };
+
+// Short chains: one thread per short multi-entry segment; segments not queued for this iteration
+// (stamp != it) exit at once.  Walks the chain in executeAt order with the same recurrence.
+__global__ __launch_bounds__(256) void k_seg_short(const uint32_t* __restrict__ heads, uint32_t count, uint32_t it,
+                                                   const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
+                                                   uint32_t* L, int32_t* __restrict__ pm_all, PushCtx push,
+                                                   uint32_t* __restrict__ work_left) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool queued = false;
+    if (i < count) {
+        const uint32_t h = heads[i];
+        if (push.stamp[h] == it) {
+            const uint32_t len = push.seg_len[h];
+            int y = -1, w = -1;
+            for (uint32_t p = h; p < h + len; ++p) {
+                const uint32_t m = c_meta[p];
+                if (manages_execution(m)) {
+                    const uint32_t t = c_txn[p];
+                    const int a = (int)L[t];
+                    const bool wr = meta_kind(m) == AD_KIND_WRITE;
+                    const int x = wr ? mp_max(y + 1, a) : mp_max(w + 1, a);
+                    if (x > a) queued |= raise_level(L, t, (uint32_t)x, (int32_t)h, push);
+                    y = mp_max(y, x);
+                    if (wr) w = mp_max(w, x);
+                }
+                pm_all[p] = y;
+            }
+        }
+    }
+    if (__ballot(queued) && __lane_id() == 0) atomicOr(work_left, 1u);
+}
+
+// Segment table: length and stamp at each head; per position: is it the head of a short multi-entry
+// segment (-> heads list), is it inside a long segment (-> long positions list).
+__global__ __launch_bounds__(256) void k_seg_table(size_t P, const int32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_len,
+                                                   uint32_t* __restrict__ stamp) {
+    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P) return;
+    const int32_t h = seg_start[s];
+    if (s + 1 == P || seg_start[s + 1] != h) {
+        seg_len[h] = (uint32_t)(s + 1 - (size_t)h);
+        stamp[h] = 0u;
+    }
+}
+struct SegListOp {                 // two compactions in one scan: short multi heads, long positions
+    struct S { uint32_t a, b; };
+    const int32_t* seg_start;
+    const uint32_t* seg_len;
+    uint32_t* heads;
+    uint32_t* long_pos;
+    uint32_t* totals;              // [0] heads, [1] long positions
+    size_t n;
+    __device__ S load(size_t i) const {
+        const int32_t h = seg_start[i];
+        const uint32_t len = seg_len[h];
+        S s;
+        s.a = (h == (int32_t)i && len >= 2 && len <= SHORT_SEG) ? 1u : 0u;
+        s.b = len > SHORT_SEG ? 1u : 0u;
+        return s;
+    }
+    __device__ S identity() const { return S{0u, 0u}; }
+    __device__ S combine(const S& x, const S& y) const { return S{x.a + y.a, x.b + y.b}; }
+    __device__ void store(size_t i, const S& ex, const S& inc, const S& el) const {
+        if (el.a) heads[ex.a] = (uint32_t)i;
+        if (el.b) long_pos[ex.b] = (uint32_t)i;
+        if (i + 1 == n) { totals[0] = inc.a; totals[1] = inc.b; }
+    }
+};
+// txn pair -> head position of its segment
+__global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ spos, const int32_t* __restrict__ seg_start,
+                                                  int32_t* __restrict__ pair_seg) {
+    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P) pair_seg[p] = seg_start[spos[p]];
+}
 
 __global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                                     const uint64_t* __restrict__ e_exec1, uint32_t* __restrict__ c_txn,
@@ -160,7 +269,6 @@ struct EdgeArgs {
     const uint8_t* meta;
     const uint64_t* ex1;
     uint32_t* L;
-    uint32_t* changed;
     // (b) merged direct / range deps: unique dependency lists
     const uint32_t* ent_off[2];
     const uint32_t* tcnt[2];
@@ -178,6 +286,11 @@ struct EdgeArgs {
     const uint32_t* useg;
     uint32_t U;
     const uint64_t* c_exec1;
+    const uint32_t* c_txn;
+    const int32_t* seg_start;
+    PushCtx push;
+    uint32_t* changed;           // any edge raised a level this iteration
+    uint32_t* work_left;
 };
 
 // (c) preparation: for unmanaged T and each key of its merged KeyDeps, the last chain position (in
@@ -218,33 +331,41 @@ __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
 // (b) + (c) relaxation, one thread per txn.
 __global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int do_c) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    const uint64_t my = a.ex1[t];
-    int best = -1;
-    if (do_b) {
+    bool raised = false, queued = false;
+    if (t < a.n) {
+        const uint64_t my = a.ex1[t];
+        int best = -1;
+        if (do_b) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if (!a.txns[c]) continue;
-            const uint32_t b = a.ent_off[c][t], e = b + a.tcnt[c][t];
-            for (uint32_t x = b; x < e; ++x) {
-                const uint32_t d = a.txns[c][x];
-                if (a.ex1[d] < my) best = max(best, (int)a.L[d]);
+            for (int c = 0; c < 2; ++c) {
+                if (!a.txns[c]) continue;
+                const uint32_t b = a.ent_off[c][t], e = b + a.tcnt[c][t];
+                for (uint32_t x = b; x < e; ++x) {
+                    const uint32_t d = a.txns[c][x];
+                    if (a.ex1[d] < my) best = max(best, (int)a.L[d]);
+                }
+            }
+        }
+        if (do_c && !manages_execution(a.meta[t])) {
+            for (uint32_t x = a.mk_key_off[t]; x < a.mk_key_off[t + 1]; ++x) {
+                const int32_t p = a.cons_pos[x];
+                if (p < 0) continue;
+                // singleton chains are never walked: their prefix max is the entry's own level
+                const bool single = a.push.seg_len[a.seg_start[p]] < 2;
+                best = max(best, single ? (int)a.L[a.c_txn[p]] : a.pm_all[p]);
+            }
+        }
+        if (best >= 0) {
+            const uint32_t v = (uint32_t)(best + 1);
+            if (v > a.L[t]) {
+                const uint32_t old = a.L[t];
+                queued = raise_level(a.L, (uint32_t)t, v, -1, a.push);
+                raised = old < v;
             }
         }
     }
-    if (do_c && !manages_execution(a.meta[t])) {
-        for (uint32_t x = a.mk_key_off[t]; x < a.mk_key_off[t + 1]; ++x) {
-            const int32_t p = a.cons_pos[x];
-            if (p >= 0) best = max(best, a.pm_all[p]);
-        }
-    }
-    if (best >= 0) {
-        const uint32_t v = (uint32_t)(best + 1);
-        if (v > a.L[t]) {
-            const uint32_t old = atomicMax(&a.L[t], v);
-            if (old < v) *a.changed = 1u;
-        }
-    }
+    if (__ballot(raised) && __lane_id() == 0) atomicOr(a.changed, 1u);
+    if (__ballot(queued) && __lane_id() == 0) atomicOr(a.work_left, 1u);
 }
 
 __global__ __launch_bounds__(256) void k_exec_split(size_t n, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ idx,
@@ -282,8 +403,11 @@ struct LevelState {
     uint8_t* c_meta = nullptr;
     uint64_t* c_exec1 = nullptr;
     int32_t* pm_all = nullptr;
+    int32_t* pair_seg = nullptr;
+    uint32_t *seg_len = nullptr, *stamp = nullptr, *heads = nullptr, *long_pos = nullptr;
     int32_t* cons_pos = nullptr;
-    uint32_t* flags = nullptr;          // [0] changed, [1] max level, [2] unsupported kinds
+    uint32_t* flags = nullptr;          // [0] heads, [1] long entries, [2] long dirty (next), [3] edge changed,
+                                        // [4] max level, [5] unsupported kinds, [6] work left (next)
     void* agg = nullptr;
     size_t agg_cap = 0;
     uint32_t *sk0 = nullptr, *sv0 = nullptr, *sk1 = nullptr, *sv1 = nullptr;
@@ -292,7 +416,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -301,17 +425,16 @@ inline size_t level_scratch_bytes(size_t, size_t) { return 0; }
 
 struct LevelInputs {
     size_t n, P;
-    const uint32_t* skey;
     const uint32_t* e_txn;
     const uint8_t* e_meta;
     const uint64_t* e_exec1;
     const int32_t* seg_start;
+    const uint32_t* spos;
+    const uint32_t* key_off;
     const uint8_t* meta;
     const uint64_t* ex1;
     uint32_t* lvl;
     uint32_t* order;
-    void* scratch;
-    size_t scratch_cap;
     const DevCsr* merged_key;
     const DevCsr* merged_direct;
     const DevCsr* merged_range;
@@ -334,7 +457,8 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     if (ls.capP < P || !ls.c_txn) {
         size_t c = std::max<size_t>(P, 1);
         if (!grow((void**)&ls.c_txn, c * 4) || !grow((void**)&ls.c_meta, c) || !grow((void**)&ls.c_exec1, c * 8) ||
-            !grow((void**)&ls.pm_all, c * 4))
+            !grow((void**)&ls.pm_all, c * 4) || !grow((void**)&ls.pair_seg, c * 4) || !grow((void**)&ls.seg_len, c * 4) ||
+            !grow((void**)&ls.stamp, c * 4) || !grow((void**)&ls.heads, c * 4) || !grow((void**)&ls.long_pos, c * 4))
             goto oom;
         ls.capP = c;
     }
@@ -352,30 +476,27 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     }
     if (!ls.flags && !grow((void**)&ls.flags, 256)) goto oom;
     {
-        const size_t need = device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)) + 256;
+        const size_t need = std::max(device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)),
+                                     device_scan_scratch<SegListOp>(std::max<size_t>(P, 1))) + 256;
         if (ls.agg_cap < need) { if (!grow(&ls.agg, need)) goto oom; ls.agg_cap = need; }
         const size_t rneed = (3 * (radix_hist_len(std::max<size_t>(n, 1)) + 128) + 64 * 1024) * 4;
         if (ls.rs_cap < rneed) { if (!grow((void**)&ls.rs, rneed)) goto oom; ls.rs_cap = rneed; }
     }
 
-    hipMemsetAsync(ls.flags, 0, 16, st);
-    if (n > 0) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 2);
-    {
-        uint32_t bad = 0;
-        hipMemcpyAsync(&bad, ls.flags + 2, 4, hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
-        if (bad) {
-            err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
-            return AD_ERR_UNSUPPORTED;
-        }
-    }
+    hipMemsetAsync(ls.flags, 0, 64, st);
+    if (n > 0) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
     hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
     *iters = 0;
     {
+        // ---- chain order, segment table, pair -> segment, long-segment positions, (c) constraints
+        const int gP = ceil_div((long)std::max<size_t>(P, 1), 256);
         const bool has_b = (in.merged_direct && in.merged_direct->ncap > 0) || (in.merged_range && in.merged_range->ncap > 0);
         const bool has_c = in.n_large > 0 && nkm > 0 && P > 0;
+        PushCtx push{};
+        push.key_off = in.key_off; push.pair_seg = ls.pair_seg; push.seg_len = ls.seg_len; push.stamp = ls.stamp;
+        push.long_dirty = ls.flags + 2;
         EdgeArgs ea{};
-        ea.n = n; ea.meta = in.meta; ea.ex1 = in.ex1; ea.L = in.lvl; ea.changed = ls.flags;
+        ea.n = n; ea.meta = in.meta; ea.ex1 = in.ex1; ea.L = in.lvl; ea.changed = ls.flags + 3; ea.work_left = ls.flags + 6;
         const DevCsr* bc[2] = {in.merged_direct, in.merged_range};
         for (int c = 0; c < 2; ++c) {
             if (bc[c] && bc[c]->ncap > 0) { ea.ent_off[c] = bc[c]->ent_off; ea.tcnt[c] = bc[c]->tcnt; ea.txns[c] = bc[c]->txns; }
@@ -385,29 +506,51 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             ea.mk_k2t = in.merged_key->k2t; ea.mk_ent_off = in.merged_key->ent_off; ea.mk_txns = in.merged_key->txns;
         }
         ea.cons_pos = ls.cons_pos; ea.pm_all = ls.pm_all; ea.ukey = in.ukey; ea.useg = in.useg; ea.U = in.U;
-        ea.c_exec1 = ls.c_exec1;
+        ea.c_exec1 = ls.c_exec1; ea.c_txn = ls.c_txn; ea.seg_start = in.seg_start;
+        uint32_t host[8] = {0};
         if (P > 0) {
             KScope ks(K_CHAIN_PREP);
-            k_chain_copy<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
-            k_chain_order<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
+            k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
+            k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
+            k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp);
+            k_pair_seg<<<gP, 256, 0, st>>>(P, in.spos, in.seg_start, ls.pair_seg);
+            device_scan(SegListOp{in.seg_start, ls.seg_len, ls.heads, ls.long_pos, ls.flags, P}, P, (SegListOp::S*)ls.agg, st);
             if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);
         }
-        ChainOp op{ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.flags, has_c ? ls.pm_all : nullptr};
-        for (int it = 0; it < (1 << 22); ++it) {
-            hipMemsetAsync(ls.flags, 0, 4, st);
-            if (P > 0) { KScope ks(K_SCAN_CHAIN); device_scan(op, P, (ChainOp::S*)ls.agg, st); }
+        hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
+        if (host[5]) {
+            err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+            return AD_ERR_UNSUPPORTED;
+        }
+        const uint32_t nheads = host[0], nlong = host[1];
+        bool short_work = nheads > 0, long_dirty = nlong > 0;
+        ChainOp op{ls.long_pos, ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.pm_all, push, ls.flags + 6};
+        for (int it = 0; it < (1 << 24); ++it) {
+            if (!short_work && !long_dirty && !(has_b || has_c)) break;
+            push.iter1 = (uint32_t)it + 1;
+            op.push = push;
+            ea.push = push;
+            hipMemsetAsync(ls.flags + 2, 0, 20, st);       // long dirty, edge changed, max level, kinds, work left
+            if (short_work) {
+                KScope ks(K_SCAN_CHAIN);
+                k_seg_short<<<ceil_div((long)nheads, 256), 256, 0, st>>>(ls.heads, nheads, (uint32_t)it, ls.c_txn, ls.c_meta, in.lvl,
+                                                                          ls.pm_all, push, ls.flags + 6);
+            }
+            if (long_dirty) { KScope ks(K_SCAN_CHAIN); device_scan(op, nlong, (ChainOp::S*)ls.agg, st); }
             if ((has_b || has_c) && n > 0) {
                 KScope ks(K_LEVEL_EDGES);
                 k_level_edges<<<ceil_div((long)n, 256), 256, 0, st>>>(ea, has_b ? 1 : 0, has_c ? 1 : 0);
             }
-            uint32_t changed = 0;
-            if (hipMemcpyAsync(&changed, ls.flags, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            if (hipMemcpyAsync(host + 2, ls.flags + 2, 20, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {
                 err = "exec levels: device error";
                 return AD_ERR_DEVICE;
             }
             *iters = it + 1;
-            if (!changed) break;
+            long_dirty = host[2] != 0;
+            short_work = host[6] != 0;
+            if (!short_work && !long_dirty && host[3] == 0) break;
         }
     }
     if (want_order && n > 0) {
@@ -429,10 +572,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             if (radix_sort_pairs(k, v, ko, vo, n, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
         }
         // then stably by level
-        hipMemsetAsync(ls.flags + 1, 0, 4, st);
-        k_gather_u32<<<g, 256, 0, st>>>(n, in.lvl, v, k, ls.flags + 1);
+        hipMemsetAsync(ls.flags + 4, 0, 4, st);
+        k_gather_u32<<<g, 256, 0, st>>>(n, in.lvl, v, k, ls.flags + 4);
         uint32_t maxl = 0;
-        hipMemcpyAsync(&maxl, ls.flags + 1, 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&maxl, ls.flags + 4, 4, hipMemcpyDeviceToHost, st);
         hipStreamSynchronize(st);
         int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
         if (radix_sort_pairs(k, v, ko, vo, n, lb, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
