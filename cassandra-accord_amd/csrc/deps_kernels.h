@@ -263,8 +263,9 @@ struct WalkArgs {
     uint32_t window;
     uint32_t thresh;
     uint64_t seed;
-    uint32_t* cnt;            // real pairs: [vc * P + s], vc = view * 2 + class
-    const uint32_t* dst;      // real pairs: [vc * P + s] absolute k2t slot of the first entry (fill)
+    const uint32_t* sval;     // sorted position -> pair index p
+    uint32_t* cnt;            // real pairs, AoS by pair: [p * 2NV + vc], vc = view * 2 + class
+    const uint32_t* dst;      // real pairs, AoS by pair: absolute k2t slot of the first entry (fill)
     int32_t* k2t[NVC_MAX];    // per-vc keysToTxnIds (fill)
     // virtual items (large txns): item x queries key segment [vi_seg0[x], ...) before position vi_pos[x]
     size_t V;
@@ -349,12 +350,14 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
     const uint32_t qk = meta_kind(mi);
+    // the pair's counts / slots live AoS by pair index (the per-txn kernels read them contiguously)
+    const size_t pb = (size_t)a.sval[s] * (2 * NV);
     uint32_t c0[NV], c1[NV];   // count mode: counts; fill mode: next write slot (descending)
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         if (FILL) {
-            c0[v] = a.dst[(size_t)(2 * v) * a.P + s] + a.cnt[(size_t)(2 * v) * a.P + s] - 1;
-            c1[v] = a.dst[(size_t)(2 * v + 1) * a.P + s] + a.cnt[(size_t)(2 * v + 1) * a.P + s] - 1;
+            c0[v] = a.dst[pb + 2 * v] + a.cnt[pb + 2 * v] - 1;
+            c1[v] = a.dst[pb + 2 * v + 1] + a.cnt[pb + 2 * v + 1] - 1;
         } else {
             c0[v] = 0; c1[v] = 0;
         }
@@ -373,8 +376,8 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     if (!FILL) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-            a.cnt[(size_t)(2 * v) * a.P + s] = c0[v];
-            a.cnt[(size_t)(2 * v + 1) * a.P + s] = c1[v];
+            a.cnt[pb + 2 * v] = c0[v];
+            a.cnt[pb + 2 * v + 1] = c1[v];
         }
     }
 }
@@ -410,14 +413,14 @@ struct TxnArgs {
     const uint64_t* keys;
     const uint8_t* meta;
     const uint32_t* spos;
-    const uint32_t* cnt;          // [vc * P + s]
+    const uint32_t* cnt;          // AoS by pair [p * nvc + vc]
     uint32_t* nk;                 // [vc * n + t]
     uint32_t* ne;                 // [vc * n + t]
     const uint32_t* out_key_off[NVC_MAX];
     const uint32_t* out_k2t_off[NVC_MAX];
     uint64_t* out_keys[NVC_MAX];
     int32_t* out_k2t[NVC_MAX];
-    uint32_t* dst;                // [vc * P + s]
+    uint32_t* dst;                // AoS by pair [p * nvc + vc]
     Params* prm;
     // large txns (virtual items, in (txn, key) order): items [voff[t], voff[t+1])
     const uint32_t* voff;
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(256) void k_txn_counts(TxnArgs a) {
     for (int vc = 0; vc < a.nvc; ++vc) {
         uint32_t nk = 0, ne = 0;
         for (uint32_t p = b; p < e; ++p) {
-            uint32_t c = a.cnt[(size_t)vc * a.P + a.spos[p]];
+            uint32_t c = a.cnt[(size_t)p * a.nvc + vc];
             nk += c > 0;
             ne += c;
         }
@@ -471,17 +474,75 @@ __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
         for (uint32_t x = b; x < e; ++x) {
             uint32_t c;
             if (large) c = a.vcnt[(size_t)x * a.nvc + vc];
-            else c = a.cnt[(size_t)vc * a.P + a.spos[x]];
+            else c = a.cnt[(size_t)x * a.nvc + vc];
             if (c == 0) continue;
             a.out_keys[vc][kb + kk] = large ? a.vi_key[x] : a.keys[x];
             if (large) a.vdst[(size_t)x * a.nvc + vc] = mb + run;
-            else a.dst[(size_t)vc * a.P + a.spos[x]] = mb + run;
+            else a.dst[(size_t)x * a.nvc + vc] = mb + run;
             run += c;
             a.out_k2t[vc][mb + kk] = (int32_t)run;
             ++kk;
         }
     }
 }
+
+// Per-txn (keys, entries) of every (view, class) key CSR, counted from the pairs' AoS counts inside the
+// scan's load, and the exclusive offsets key_off / ent_off / k2t_off of all of them in one scan (replaces
+// 2NV separate count reductions and 3 * 2NV scans).
+template <int NVC>
+struct OffsetsOp {
+    struct S { uint32_t k[NVC], e[NVC]; };
+    size_t n;
+    const uint8_t* meta;
+    const uint32_t* key_off;
+    const uint32_t* cnt;          // AoS by pair
+    const uint32_t* voff;
+    const uint32_t* vcnt;         // AoS by virtual item
+    uint32_t* o_key_off[NVC];
+    uint32_t* o_ent_off[NVC];
+    uint32_t* o_k2t_off[NVC];
+
+    __device__ S identity() const {
+        S s;
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) { s.k[c] = 0; s.e[c] = 0; }
+        return s;
+    }
+    __device__ S load(size_t t) const {
+        S s = identity();
+        const bool large = meta[t] & META_LARGE;
+        const uint32_t b = large ? voff[t] : key_off[t], e = large ? voff[t + 1] : key_off[t + 1];
+        const uint32_t* src = large ? vcnt : cnt;
+        for (uint32_t x = b; x < e; ++x) {
+#pragma unroll
+            for (int c = 0; c < NVC; ++c) {
+                const uint32_t v = src[(size_t)x * NVC + c];
+                s.k[c] += v > 0 ? 1u : 0u;
+                s.e[c] += v;
+            }
+        }
+        return s;
+    }
+    __device__ S combine(const S& x, const S& y) const {
+        S r;
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) { r.k[c] = x.k[c] + y.k[c]; r.e[c] = x.e[c] + y.e[c]; }
+        return r;
+    }
+    __device__ void store(size_t t, const S& ex, const S& inc, const S&) const {
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) {
+            o_key_off[c][t] = ex.k[c];
+            o_ent_off[c][t] = ex.e[c];
+            o_k2t_off[c][t] = ex.k[c] + ex.e[c];
+            if (t + 1 == n) {
+                o_key_off[c][n] = inc.k[c];
+                o_ent_off[c][n] = inc.e[c];
+                o_k2t_off[c][n] = inc.k[c] + inc.e[c];
+            }
+        }
+    }
+};
 
 // Union of up to KMAX sorted lists living in k2t[lo[k] .. hi[k]) -> out (unique, ascending); then
 // every entry is rewritten as its index in out.  Returns |out|.

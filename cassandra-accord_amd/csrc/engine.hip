@@ -300,6 +300,17 @@ void launch_range(const RangeArgs& a, bool fill, hipStream_t st) {
         default: F<8>(__VA_ARGS__); break;           \
     }
 
+template <int NV>
+void launch_offsets(ad_handle* h, const TxnArgs& ta) {
+    OffsetsOp<2 * NV> op;
+    op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt; op.voff = h->voff; op.vcnt = h->vcnt;
+    for (int c = 0; c < 2 * NV; ++c) {
+        op.o_key_off[c] = h->deps[c].key_off; op.o_ent_off[c] = h->deps[c].ent_off; op.o_k2t_off[c] = h->deps[c].k2t_off;
+    }
+    device_scan(op, h->n, (typename OffsetsOp<2 * NV>::S*)h->scratch, h->st);
+    (void)ta;
+}
+
 int stage_deps(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
@@ -340,15 +351,19 @@ int stage_deps(ad_handle* h) {
     wa.e_txn = h->e_txn; wa.e_meta = h->e_meta; wa.e_exec1 = h->e_exec1; wa.seg_start = h->seg_start;
     wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
-    wa.cnt = h->cnt; wa.dst = h->dst;
+    wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
     NV_DISPATCH(nv, launch_walk, wa, false, st);
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.spos = h->spos; ta.cnt = h->cnt;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
-    if (n > 0) { KScope ks(K_TXN_COUNTS); k_txn_counts<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
-    for (int vc = 0; vc < nvc; ++vc) csr_offsets(h, h->deps[vc], h->nk + (size_t)vc * n, h->ne + (size_t)vc * n);
+    if (n > 0) {
+        KScope ks(K_SCAN_OFFSETS);
+        NV_DISPATCH(nv, launch_offsets, h, ta);
+    } else {
+        for (int vc = 0; vc < nvc; ++vc) csr_offsets(h, h->deps[vc], h->nk, h->ne);
+    }
     // ---- RangeDeps (count)
     RangeArgs ra{};
     ra.n = n; ra.Q = Q; ra.key_off = h->key_off; ra.keys = h->keys; ra.range_off = h->range_off; ra.rs = h->range_s;

@@ -15,33 +15,53 @@
 
 namespace ad {
 
+// 64-lane shuffle of an arbitrary 4-byte-multiple state
+template <class S>
+__device__ inline S shfl_up_state(const S& v, int delta) {
+    static_assert(sizeof(S) % 4 == 0, "scan state must be a multiple of 4 bytes");
+    constexpr int W = sizeof(S) / 4;
+    S r;
+    const int* src = reinterpret_cast<const int*>(&v);
+    int* dst = reinterpret_cast<int*>(&r);
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = __shfl_up(src[k], delta);
+    return r;
+}
+
+// Block-wide exclusive scan: 64-lane shuffle scan per wave (no LDS round trips), then one LDS slot per
+// wave for the wave totals.  Returns the thread's exclusive prefix; *total = block aggregate.
 template <class Op, int BLOCK>
 __device__ inline typename Op::S block_exclusive_scan(const Op& op, typename Op::S v, typename Op::S* lds,
                                                       typename Op::S* total) {
     using S = typename Op::S;
-    const int t = threadIdx.x;
-    lds[t] = v;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over the BLOCK thread aggregates
-    for (int off = 1; off < BLOCK; off <<= 1) {
-        S x = lds[t];
-        S y = t >= off ? op.combine(lds[t - off], x) : x;
-        __syncthreads();
-        lds[t] = y;
-        __syncthreads();
+    constexpr int NW = BLOCK / WAVE;
+    const int lane = __lane_id();
+    const int w = threadIdx.x / WAVE;
+    S x = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        S y = shfl_up_state(x, o);
+        if (lane >= o) x = op.combine(y, x);
     }
-    S incl = lds[t];
-    S excl = t == 0 ? op.identity() : lds[t - 1];
-    if (total) *total = lds[BLOCK - 1];
+    S ex_w = shfl_up_state(x, 1);
+    if (lane == 0) ex_w = op.identity();
+    if (lane == WAVE - 1) lds[w] = x;
     __syncthreads();
-    (void)incl;
-    return excl;
+    S pre = op.identity();
+    for (int k = 0; k < w; ++k) pre = op.combine(pre, lds[k]);
+    if (total) {
+        S tot = pre;
+        for (int k = w; k < NW; ++k) tot = op.combine(tot, lds[k]);
+        *total = tot;
+    }
+    __syncthreads();
+    return op.combine(pre, ex_w);
 }
 
 template <class Op, int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename Op::S* agg) {
     using S = typename Op::S;
-    __shared__ S lds[BLOCK];
+    __shared__ S lds[BLOCK / WAVE];
     const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
     S acc = op.identity();
 #pragma unroll
@@ -56,7 +76,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename
 template <class Op, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, typename Op::S* agg) {
     using S = typename Op::S;
-    __shared__ S lds[BLOCK];
+    __shared__ S lds[BLOCK / WAVE];
     S carry = op.identity();
     for (int c0 = 0; c0 < nblk; c0 += BLOCK) {
         int i = c0 + threadIdx.x;
@@ -72,7 +92,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, type
 template <class Op, int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_scan_apply(Op op, size_t n, const typename Op::S* agg) {
     using S = typename Op::S;
-    __shared__ S lds[BLOCK];
+    __shared__ S lds[BLOCK / WAVE];
     const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
     S el[ITEMS];
     S acc = op.identity();
