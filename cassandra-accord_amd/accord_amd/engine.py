@@ -53,6 +53,7 @@ def lib():
         L.ad_fetch_deps.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut)]
         L.ad_merge_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
+        L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ad_run_pipeline.argtypes = [vp]
         L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
@@ -130,6 +131,22 @@ class DepsEngine:
     def merge(self):
         sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
         self._check(lib().ad_merge_deps(self.h, sizes), "ad_merge_deps")
+        self._merge_sizes = sizes
+        return sizes
+
+    def merge_host(self, replies):
+        """Deps.merge of caller-supplied replies over the loaded batch: replies[r][cls] is an abi.Csr (the
+        same per-txn canonical layout ad_fetch_deps returns).  Fetch the result with fetch_merged()."""
+        r = len(replies)
+        arr = (abi.AdCsrIn * (r * abi.NUM_CLASSES))()
+        keep = []
+        for v, rep in enumerate(replies):
+            for c in range(abi.NUM_CLASSES):
+                csr = rep[c]
+                keep.append(csr)
+                arr[v * abi.NUM_CLASSES + c] = csr.as_in()
+        sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
+        self._check(lib().ad_merge_host(self.h, arr, r, sizes), "ad_merge_host")
         self._merge_sizes = sizes
         return sizes
 

@@ -78,7 +78,8 @@ struct ad_handle {
     std::vector<Csr> deps;           // [view * 2 + class]  (key, direct)
     Csr rdeps[MAXV];                 // RangeDeps per view
     Csr merged[3];
-    bool have_deps = false, have_merged = false, have_levels = false;
+    Csr hparts[3][MAXV];             // ad_merge_host uploads
+    bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -131,12 +132,12 @@ enum Slot : size_t {
     S_PRM, S_TXTS, S_EX1, S_META, S_PTXN, S_KA, S_VA, S_KB, S_VB, S_ETXN, S_SPOS, S_EMETA, S_EEXEC,
     S_PMW, S_PMC, S_SEG, S_UD, S_CNT, S_DST, S_NK, S_NE, S_SCRATCH,
     S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
-    S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE,
+    S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
 // merged [NVC_MAX + MAXV, +3)
-constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV;
+constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV, CSR_HOST0 = CSR_MERGED0 + 3;
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
 
@@ -444,48 +445,118 @@ int stage_deps(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 // merge
 // ---------------------------------------------------------------------------------------------------
-int stage_merge(ad_handle* h) {
-    if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps before ad_preaccept_deps");
+// Deps.merge of `np` parts per class into h->merged (all classes counted, scanned and sized together:
+// one host sync).  parts[cls][v] are batched per-txn CSRs over the loaded batch.
+int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_range) {
     const size_t n = h->n;
-    const int nv = (int)h->cfg.replicas;
     hipStream_t st = h->st;
     h->merged_entries = 0;
+    uint32_t *mk, *me, *mu;
+    CK(dalloc(h, S_MSCR, &mk, 9 * n + 3));
+    me = mk + 3 * n;
+    mu = me + 3 * n;
+    MergeArgs ma[3]{};
+    MergeOffsetsOp op{};
+    op.n = n; op.mk = mk; op.me = me; op.mu = mu;
     for (int cls = 0; cls < 3; ++cls) {
         Csr& m = h->merged[cls];
         CK(alloc_csr(h, CSR_MERGED0 + cls, m, n));
-        if (cls == AD_CLASS_RANGE && h->Q == 0) { m.nkeys = m.nk2t = m.ncap = 0; continue; }
+        const bool live = !(cls == AD_CLASS_RANGE && !has_range);
+        op.live[cls] = live ? 1 : 0;
+        op.key_off[cls] = m.key_off; op.ent_off[cls] = m.ent_off; op.k2t_off[cls] = m.k2t_off;
+        if (!live) {
+            m.nkeys = m.nk2t = m.ncap = 0;
+            HIPCHK(h, hipMemsetAsync(m.key_off, 0, (n + 1) * 4, st));
+            HIPCHK(h, hipMemsetAsync(m.ent_off, 0, (n + 1) * 4, st));
+            HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, (n + 1) * 4, st));
+            continue;
+        }
+        MergeArgs& a = ma[cls];
+        a.n = n; a.nv = np;
+        for (int v = 0; v < np; ++v) {
+            const Csr& c = *parts[cls][v];
+            a.key_off[v] = c.key_off; a.keys[v] = c.keys; a.k2t_off[v] = c.k2t_off; a.k2t[v] = c.k2t;
+            a.ent_off[v] = c.ent_off; a.txns[v] = c.txns; a.tcnt[v] = c.tcnt;
+        }
+        a.mk = mk + cls * n; a.me = me + cls * n; a.mu = mu + cls * n;
+        if (n > 0) merge_launch(a, np, false, cls == AD_CLASS_RANGE ? 2 : 1, st);
+    }
+    if (n > 0) {
+        KScope ks(K_SCAN_OFFSETS);
+        device_scan(op, n, (MergeOffsetsOp::S*)h->scratch, st);
+    }
+    uint32_t tot[9] = {0};
+    for (int cls = 0; cls < 3; ++cls) {
+        if (!op.live[cls] || n == 0) continue;
+        Csr& m = h->merged[cls];
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * cls + 0], m.key_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * cls + 1], m.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * cls + 2], m.ent_off + n, 4, hipMemcpyDeviceToHost, st));
+    }
+    CK(read_params(h));
+    CK(check_params(h));
+    for (int cls = 0; cls < 3; ++cls) {
+        if (!op.live[cls]) continue;
+        Csr& m = h->merged[cls];
         const int kw = cls == AD_CLASS_RANGE ? 2 : 1;
-        MergeArgs ma{};
-        ma.n = n; ma.nv = nv;
-        for (int v = 0; v < nv; ++v) {
-            const Csr& c = cls == AD_CLASS_RANGE ? h->rdeps[v] : h->deps[2 * v + cls];
-            ma.key_off[v] = c.key_off; ma.keys[v] = c.keys; ma.k2t_off[v] = c.k2t_off; ma.k2t[v] = c.k2t;
-            ma.ent_off[v] = c.ent_off; ma.txns[v] = c.txns; ma.tcnt[v] = c.tcnt;
-        }
-        ma.mk = h->nk; ma.me = h->ne; ma.mu = h->nk + n;   // scratch counters (n each)
-        if (n > 0) merge_launch(ma, nv, false, kw, st);
-        {
-            KScope ks(K_SCAN_OFFSETS);
-            scan_offsets(h, ma.mk, m.key_off, n);
-            scan_offsets(h, ma.mu, m.ent_off, n);
-            if (n) device_scan(Sum2Op<uint32_t>{ma.mk, ma.me, m.k2t_off, n}, n, (uint32_t*)h->scratch, st);
-            else hipMemsetAsync(m.k2t_off, 0, 4, st);
-        }
-        uint32_t tot[3];
-        HIPCHK(h, hipMemcpyAsync(&tot[0], m.key_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[1], m.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[2], m.ent_off + n, 4, hipMemcpyDeviceToHost, st));
-        CK(read_params(h));
-        CK(check_params(h));
-        m.nkeys = tot[0]; m.nk2t = tot[1]; m.ncap = tot[2];
+        m.nkeys = tot[3 * cls]; m.nk2t = tot[3 * cls + 1]; m.ncap = tot[3 * cls + 2];
         h->merged_entries += m.nk2t - m.nkeys;
         CK(alloc_csr_data(h, CSR_MERGED0 + cls, m, kw));
-        ma.o_key_off = m.key_off; ma.o_keys = m.keys; ma.o_k2t_off = m.k2t_off; ma.o_k2t = m.k2t;
-        ma.o_ent_off = m.ent_off; ma.o_txns = m.txns; ma.o_tcnt = m.tcnt;
-        if (n > 0) merge_launch(ma, nv, true, kw, st);
+        MergeArgs& a = ma[cls];
+        a.o_key_off = m.key_off; a.o_keys = m.keys; a.o_k2t_off = m.k2t_off; a.o_k2t = m.k2t;
+        a.o_ent_off = m.ent_off; a.o_txns = m.txns; a.o_tcnt = m.tcnt;
+        if (n > 0) merge_launch(a, np, true, kw, st);
     }
     h->have_merged = true;
     return AD_OK;
+}
+
+int stage_merge(ad_handle* h) {
+    if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps before ad_preaccept_deps");
+    const int nv = (int)h->cfg.replicas;
+    const Csr* parts[3][MAXV] = {};
+    for (int v = 0; v < nv; ++v) {
+        parts[0][v] = &h->deps[2 * v];
+        parts[1][v] = &h->deps[2 * v + 1];
+        parts[2][v] = &h->rdeps[v];
+    }
+    return merge_parts(h, parts, nv, h->Q > 0);
+}
+
+// Validates one caller-supplied canonical CSR over n txns (host side: a malformed reply must never reach a
+// kernel as an out-of-range index).  Returns the three lengths via *keys/*k2t/*txns.
+bool valid_part(const ad_csr_in& c, size_t n, int kw, size_t* nkeys, size_t* nk2t, size_t* ntx, std::string& why) {
+    if (!c.key_off || !c.k2t_off || !c.txn_off) { why = "null offsets"; return false; }
+    if (c.key_off[0] != 0 || c.k2t_off[0] != 0 || c.txn_off[0] != 0) { why = "offsets must start at 0"; return false; }
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t k0 = c.key_off[i], k1 = c.key_off[i + 1], m0 = c.k2t_off[i], m1 = c.k2t_off[i + 1];
+        const uint32_t t0 = c.txn_off[i], t1 = c.txn_off[i + 1];
+        if (k1 < k0 || m1 < m0 || t1 < t0) { why = "offsets not monotone at txn " + std::to_string(i); return false; }
+        const uint32_t nk = k1 - k0, len = m1 - m0, nt = t1 - t0;
+        if ((nk == 0) != (len == 0) || (nk == 0) != (nt == 0) || len < nk) { why = "inconsistent CSR at txn " + std::to_string(i); return false; }
+        // keys strictly ascending (Range::compare for ranges)
+        for (uint32_t k = k0 + 1; k < k1; ++k) {
+            const uint64_t* a = c.keys + (size_t)kw * (k - 1);
+            const uint64_t* b = c.keys + (size_t)kw * k;
+            const bool lt = kw == 1 ? a[0] < b[0] : (a[0] < b[0] || (a[0] == b[0] && a[1] < b[1]));
+            if (!lt) { why = "keys not strictly ascending at txn " + std::to_string(i); return false; }
+        }
+        for (uint32_t x = t0; x < t1; ++x)
+            if (c.txns[x] >= n || (x > t0 && c.txns[x] <= c.txns[x - 1])) { why = "TxnIds not sorted unique ranks at txn " + std::to_string(i); return false; }
+        uint32_t prev = nk;
+        for (uint32_t k = 0; k < nk; ++k) {
+            const uint32_t end = (uint32_t)c.k2t[m0 + k];
+            if (end < prev || end > len || (end == prev)) { why = "keysToTxnIds header invalid at txn " + std::to_string(i); return false; }
+            for (uint32_t x = prev; x < end; ++x) {
+                const int32_t ix = c.k2t[m0 + x];
+                if (ix < 0 || (uint32_t)ix >= nt || (x > prev && ix <= c.k2t[m0 + x - 1])) { why = "keysToTxnIds index invalid at txn " + std::to_string(i); return false; }
+            }
+            prev = end;
+        }
+        if (prev != len) { why = "keysToTxnIds length mismatch at txn " + std::to_string(i); return false; }
+    }
+    *nkeys = c.key_off[n]; *nk2t = c.k2t_off[n]; *ntx = c.txn_off[n];
+    return true;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -493,6 +564,7 @@ int stage_merge(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_exec_levels before ad_merge_deps");
+    if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_exec_levels needs ad_preaccept_deps on this batch (its key chains)");
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
     li.seg_start = h->seg_start; li.spos = h->spos; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
@@ -698,6 +770,7 @@ int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
     g_tracer = &h->tracer;
     hipSetDevice(h->device);
     CK(stage_merge(h));
+    h->merged_has_range = h->Q > 0;
     if (sizes) {
         CK(csr_sizes(h, h->merged[0], &sizes[0]));
         CK(csr_sizes(h, h->merged[1], &sizes[1]));
@@ -712,12 +785,53 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     if (cls >= AD_NUM_CLASSES) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    if (cls == AD_CLASS_RANGE) return h->Q ? fetch_csr(h, h->merged[2], 2, out) : fetch_empty(h, out);
+    if (cls == AD_CLASS_RANGE) return h->merged_has_range ? fetch_csr(h, h->merged[2], 2, out) : fetch_empty(h, out);
     return fetch_csr(h, h->merged[cls], 1, out);
 }
 
-int ad_merge_host(ad_handle* h, const ad_csr_in*, uint32_t, ad_csr_sizes*) {
-    return h ? set_err(h, AD_ERR_UNSUPPORTED, "ad_merge_host: not in this build") : AD_ERR_ARGUMENT;
+int ad_merge_host(ad_handle* h, const ad_csr_in* parts, uint32_t r, ad_csr_sizes* sizes) {
+    if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
+    if (!parts || r < 1 || r > (uint32_t)MAXV) return set_err(h, AD_ERR_ARGUMENT, "ad_merge_host: 1..8 replies");
+    hipSetDevice(h->device);
+    const size_t n = h->n;
+    hipStream_t st = h->st;
+    bool has_range = false;
+    const Csr* ptr[3][MAXV] = {};
+    for (uint32_t v = 0; v < r; ++v) {
+        for (int cls = 0; cls < 3; ++cls) {
+            const ad_csr_in& in = parts[v * AD_NUM_CLASSES + cls];
+            const int kw = cls == AD_CLASS_RANGE ? 2 : 1;
+            size_t nk = 0, nm = 0, nt = 0;
+            std::string why;
+            if (!valid_part(in, n, kw, &nk, &nm, &nt, why))
+                return set_err(h, AD_ERR_ARGUMENT, "ad_merge_host: reply " + std::to_string(v) + " class " + std::to_string(cls) + ": " + why);
+            if (cls == AD_CLASS_RANGE && nk > 0) has_range = true;
+            Csr& c = h->hparts[cls][v];
+            const size_t block = CSR_HOST0 + cls * MAXV + v;
+            CK(alloc_csr(h, block, c, n));
+            c.nkeys = nk; c.nk2t = nm; c.ncap = nt;
+            CK(alloc_csr_data(h, block, c, kw));
+            HIPCHK(h, hipMemcpyAsync(c.key_off, in.key_off, (n + 1) * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(h, hipMemcpyAsync(c.k2t_off, in.k2t_off, (n + 1) * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(h, hipMemcpyAsync(c.ent_off, in.txn_off, (n + 1) * 4, hipMemcpyHostToDevice, st));
+            if (nk) HIPCHK(h, hipMemcpyAsync(c.keys, in.keys, nk * 8 * kw, hipMemcpyHostToDevice, st));
+            if (nm) HIPCHK(h, hipMemcpyAsync(c.k2t, in.k2t, nm * 4, hipMemcpyHostToDevice, st));
+            if (nt) HIPCHK(h, hipMemcpyAsync(c.txns, in.txns, nt * 4, hipMemcpyHostToDevice, st));
+            if (n) k_tcnt_from_off<<<ceil_div((long)n, 256), 256, 0, st>>>(n, c.ent_off, c.tcnt);
+            ptr[cls][v] = &c;
+        }
+    }
+    CK(merge_parts(h, ptr, (int)r, has_range));
+    h->merged_has_range = has_range;
+    if (sizes) {
+        CK(csr_sizes(h, h->merged[0], &sizes[0]));
+        CK(csr_sizes(h, h->merged[1], &sizes[1]));
+        if (has_range) CK(csr_sizes(h, h->merged[2], &sizes[2]));
+        else sizes[2] = ad_csr_sizes{h->n, 0, 0, 0, 0};
+    }
+    return AD_OK;
 }
 
 int ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint32_t* iterations_out) {
@@ -747,6 +861,7 @@ int ad_run_pipeline(ad_handle* h) {
     CK(stage_deps(h));
     HIPCHK(h, hipEventRecord(h->ev[3], st));
     CK(stage_merge(h));
+    h->merged_has_range = h->Q > 0;
     HIPCHK(h, hipEventRecord(h->ev[4], st));
     CK(stage_levels(h, true));
     HIPCHK(h, hipEventRecord(h->ev[5], st));

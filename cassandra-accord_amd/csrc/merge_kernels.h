@@ -139,6 +139,54 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     else { a.mk[t] = mk; a.me[t] = me; a.mu[t] = mu; }
 }
 
+// Offsets of the three merged classes from the count pass, in one scan: state (keys, entries, TxnIds) x 3.
+struct MergeOffsetsOp {
+    struct S { uint32_t k[3], e[3], u[3]; };
+    size_t n;
+    const uint32_t* mk;           // [cls * n + t]
+    const uint32_t* me;
+    const uint32_t* mu;
+    int live[3];
+    uint32_t* key_off[3];
+    uint32_t* ent_off[3];
+    uint32_t* k2t_off[3];
+    __device__ S identity() const {
+        S s;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { s.k[c] = 0; s.e[c] = 0; s.u[c] = 0; }
+        return s;
+    }
+    __device__ S load(size_t t) const {
+        S s = identity();
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            if (live[c]) { s.k[c] = mk[c * n + t]; s.e[c] = me[c * n + t]; s.u[c] = mu[c * n + t]; }
+        return s;
+    }
+    __device__ S combine(const S& x, const S& y) const {
+        S r;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { r.k[c] = x.k[c] + y.k[c]; r.e[c] = x.e[c] + y.e[c]; r.u[c] = x.u[c] + y.u[c]; }
+        return r;
+    }
+    __device__ void store(size_t t, const S& ex, const S& inc, const S&) const {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (!live[c]) continue;
+            key_off[c][t] = ex.k[c];
+            ent_off[c][t] = ex.u[c];
+            k2t_off[c][t] = ex.k[c] + ex.e[c];
+            if (t + 1 == n) { key_off[c][n] = inc.k[c]; ent_off[c][n] = inc.u[c]; k2t_off[c][n] = inc.k[c] + inc.e[c]; }
+        }
+    }
+};
+
+// Uploaded replies (ad_merge_host): per-txn unique-TxnId counts from the compacted txn_off.
+__global__ __launch_bounds__(256) void k_tcnt_from_off(size_t n, const uint32_t* __restrict__ off, uint32_t* __restrict__ tcnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) tcnt[t] = off[t + 1] - off[t];
+}
+
 template <int NV>
 inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t st) {
     const int g = ceil_div((long)a.n, 256);

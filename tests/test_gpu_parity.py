@@ -174,3 +174,48 @@ def test_c4_scaled(engine_factory):
     b = workload.generate(40000, 4, 400_000, "uniform", range_frac=0.1, range_width_max=1 << 13,
                           seed=workload.SEEDS["C4"])
     check(engine_factory, b)
+
+
+def test_merge_host_equals_oracle_merge(engine_factory):
+    # Deps.merge of replies supplied by the host (the coordinator's network replies): feed the oracle's
+    # per-view replies in, compare with the oracle's LinearMerger result
+    for b, cfg in ((workload.config("C3", n=8000, seed=41), (16, 4, 0.3, 41)),
+                   (workload.generate(3000, 3, 20000, "uniform", range_frac=0.15, range_width_max=400, seed=42), (16, 3, 0.2, 42))):
+        w, r, p, s = cfg
+        ref = O.OracleResult(b, abi.make_config(w, r, p, s), O.FLAG_MERGE)
+        eng = engine_factory(window=w, replicas=r, drop_p=p, seed=s)
+        eng.load(b)
+        replies = [[ref.deps(v, c) for c in range(abi.NUM_CLASSES)] for v in range(r)]
+        eng.merge_host(replies)
+        for c in range(abi.NUM_CLASSES):
+            _assert_csr("merge_host %s" % abi.CLASS_NAMES[c], eng.fetch_merged(c), ref.merged(c))
+        # merge of one reply is that reply; of two in reverse order, the per-txn union (testMergedProperty)
+        eng.merge_host([replies[r - 1]])
+        for c in range(abi.NUM_CLASSES):
+            _assert_csr("merge_host single %s" % abi.CLASS_NAMES[c], eng.fetch_merged(c), replies[r - 1][c])
+        eng.merge_host([replies[2], replies[0]])
+        from batchkit import deps_of
+        for c in range(abi.NUM_CLASSES):
+            got = eng.fetch_merged(c)
+            for i in range(0, b["n"], 97):
+                want = {}
+                for rep in (replies[0], replies[2]):
+                    for k, ts in deps_of(rep[c], i).items():
+                        want.setdefault(k, set()).update(ts)
+                assert deps_of(got, i) == {k: sorted(v) for k, v in want.items()}
+
+
+def test_merge_host_rejects_malformed(engine_factory):
+    from accord_amd import engine
+
+    b = workload.config("C2", n=2000)
+    ref = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE)
+    eng = engine_factory(replicas=1)
+    eng.load(b)
+    rep = [ref.deps(0, c) for c in range(abi.NUM_CLASSES)]
+    bad = abi.Csr(rep[0].key_off.copy(), rep[0].keys.copy(), rep[0].k2t_off.copy(), rep[0].k2t.copy(),
+                  rep[0].txn_off.copy(), rep[0].txns.copy())
+    i = int(np.nonzero(np.diff(bad.txn_off) > 0)[0][0])
+    bad.k2t[bad.k2t_off[i] + (bad.key_off[i + 1] - bad.key_off[i])] = 10 ** 6      # index out of range
+    with pytest.raises(engine.IllegalArgumentException):
+        eng.merge_host([[bad, rep[1], rep[2]]])
