@@ -1,0 +1,275 @@
+"""Key-range sharding of a batch across CommandStores / GPUs (BASELINE C5).
+
+Mirrors Accord's per-range CommandStore sharding (local/CommandStores.java:576-593,
+local/ShardDistributor.java:32-80) and PreAccept.reduce across stores (messages/PreAccept.java:141-156):
+
+* ``even_bounds`` / ``slice_for_shard`` — host-side partitioning: store s owns keys in [bounds[s], bounds[s+1]);
+  its local batch is every txn touching that range with its keys sliced to it, in global TxnId order; ``gid``
+  maps local rows to global ranks and ``home`` marks txns whose first key lies in the range.
+* ``ShardStore`` — one store on one GPU (an ad_handle in sharded mode), driving the C-ABI protocol.
+* transports — how stores exchange blobs and level arrays: ``RcclTransport`` (ncclAllGather /
+  ncclAllReduce on device buffers over xGMI, inside libaccord_deps; torch.distributed/gloo only carries the
+  128-byte unique id and two scalars), ``GlooTransport`` (host staging over a gloo group; used for tests
+  and as the explicit host path), ``LocalTransport`` (several stores in one process, for tests).
+* ``run_store`` — the per-store protocol: preaccept, export, exchange, merge, distributed levels, order.
+
+Every computation runs on the GPU through the C-ABI; the transports only move bytes.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi, engine
+
+
+def even_bounds(key_lo, key_hi, shards):
+    """ShardDistributor.EvenSplit over [key_lo, key_hi): shards + 1 boundaries (last = 2^64-1)."""
+    span = key_hi - key_lo
+    b = [key_lo + (span * s) // shards for s in range(shards)]
+    return np.array(b + [np.iinfo(np.uint64).max], np.uint64)
+
+
+def slice_for_shard(batch, lo, hi):
+    """(local batch, gid, home) of the store owning keys in [lo, hi)."""
+    if batch.get("range_off") is not None and int(batch["range_off"][-1]) > 0:
+        raise ValueError("sharded mode: range txns are not supported")
+    n = batch["n"]
+    ko = batch["key_off"].astype(np.int64)
+    keys = batch["keys"]
+    inr = (keys >= np.uint64(lo)) & (keys < np.uint64(hi))
+    owner = np.repeat(np.arange(n, dtype=np.int64), np.diff(ko))
+    cnt = np.bincount(owner[inr], minlength=n)
+    touch = cnt > 0
+    gid = np.nonzero(touch)[0].astype(np.uint32)
+    first = np.full(n, np.iinfo(np.uint64).max, np.uint64)
+    nz = ko[1:] > ko[:-1]
+    first[nz] = keys[ko[:-1][nz]]
+    home = ((first >= np.uint64(lo)) & (first < np.uint64(hi)))[gid].astype(np.uint8)
+    local = {"n": int(len(gid))}
+    for f in ("txn_msb", "txn_lsb", "txn_node", "exec_msb", "exec_lsb", "exec_node", "status"):
+        local[f] = np.ascontiguousarray(batch[f][gid])
+    lk = np.zeros(len(gid) + 1, np.uint32)
+    lk[1:] = np.cumsum(cnt[gid])
+    local["key_off"] = lk
+    local["keys"] = np.ascontiguousarray(keys[inr])
+    local["range_off"] = local["range_start"] = local["range_end"] = None
+    return local, gid, home
+
+
+def _u32p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+class ShardStore:
+    """One CommandStore of a key-range-sharded batch on one GPU."""
+
+    def __init__(self, device, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1):
+        self.eng = engine.DepsEngine(device=device, window=window, replicas=replicas, drop_p=drop_p, seed=seed)
+        self.replicas = replicas
+        self.L = engine.lib()
+        L = self.L
+        vp = C.c_void_p
+        L.ad_shard_setup.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint8), C.c_size_t]
+        L.ad_shard_export.argtypes = [vp, C.POINTER(C.c_size_t)]
+        L.ad_shard_blob_to_host.argtypes = [vp, C.c_void_p]
+        L.ad_shard_import_host.argtypes = [vp, C.c_void_p, C.c_uint32, C.c_size_t]
+        L.ad_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+        L.ad_comm_init.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
+        L.ad_shard_allgather.argtypes = [vp, C.c_size_t]
+        L.ad_shard_merge.argtypes = [vp, C.POINTER(abi.AdCsrSizes), C.POINTER(C.c_size_t)]
+        L.ad_shard_fetch.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut), C.POINTER(C.c_uint32)]
+        L.ad_shard_levels_round.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32)]
+        L.ad_shard_levels_get.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.ad_shard_levels_set.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.ad_shard_levels_allreduce.argtypes = [vp]
+        L.ad_shard_order.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+
+    def close(self):
+        self.eng.close()
+
+    def _check(self, rc, what):
+        self.eng._check(rc, what)
+
+    # ---- protocol steps
+    def load(self, local_batch, gid, home, n_global):
+        self.eng.load(local_batch)
+        self.gid = np.ascontiguousarray(gid, np.uint32)
+        self.home = np.ascontiguousarray(home, np.uint8)
+        self.n_global = n_global
+        self._check(self.L.ad_shard_setup(self.eng.h, _u32p(self.gid), self.home.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                          n_global), "ad_shard_setup")
+
+    def preaccept(self):
+        self._check(self.L.ad_preaccept_deps(self.eng.h, None), "ad_preaccept_deps")
+
+    def export(self):
+        b = C.c_size_t()
+        self._check(self.L.ad_shard_export(self.eng.h, C.byref(b)), "ad_shard_export")
+        self.blob_bytes = b.value
+        return b.value
+
+    def blob(self):
+        out = np.zeros(self.blob_bytes, np.uint8)
+        self._check(self.L.ad_shard_blob_to_host(self.eng.h, out.ctypes.data), "ad_shard_blob_to_host")
+        return out
+
+    def import_host(self, recv, world, stride):
+        recv = np.ascontiguousarray(recv, np.uint8)
+        self._check(self.L.ad_shard_import_host(self.eng.h, recv.ctypes.data, world, stride), "ad_shard_import_host")
+
+    def comm_init(self, world, rank, uid):
+        u = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._check(self.L.ad_comm_init(self.eng.h, world, rank, u), "ad_comm_init")
+
+    def allgather(self, stride):
+        self._check(self.L.ad_shard_allgather(self.eng.h, stride), "ad_shard_allgather")
+
+    def merge(self):
+        sizes = (abi.AdCsrSizes * ((self.replicas + 1) * abi.NUM_CLASSES))()
+        nh = C.c_size_t()
+        self._check(self.L.ad_shard_merge(self.eng.h, sizes, C.byref(nh)), "ad_shard_merge")
+        self._sizes = sizes
+        self.n_home = nh.value
+        return nh.value
+
+    def fetch(self, view, cls):
+        """Home txns' CSR of `view` (view == replicas: merged) and their global ranks."""
+        s = self._sizes[view * abi.NUM_CLASSES + cls]
+        out = abi.Csr.alloc(s, is_range=(cls == abi.CLASS_RANGE))
+        hg = np.zeros(max(self.n_home, 1), np.uint32)
+        o = out.as_out()
+        self._check(self.L.ad_shard_fetch(self.eng.h, view, cls, C.byref(o), _u32p(hg)), "ad_shard_fetch")
+        return out, hg[:self.n_home]
+
+    def levels_round(self, first):
+        ch = C.c_uint32()
+        self._check(self.L.ad_shard_levels_round(self.eng.h, 1 if first else 0, C.byref(ch)), "ad_shard_levels_round")
+        return bool(ch.value)
+
+    def levels_get(self):
+        g = np.zeros(max(self.n_global, 1), np.uint32)
+        self._check(self.L.ad_shard_levels_get(self.eng.h, _u32p(g)), "ad_shard_levels_get")
+        return g[:self.n_global]
+
+    def levels_set(self, g):
+        g = np.ascontiguousarray(g, np.uint32)
+        self._check(self.L.ad_shard_levels_set(self.eng.h, _u32p(g)), "ad_shard_levels_set")
+
+    def levels_allreduce(self):
+        self._check(self.L.ad_shard_levels_allreduce(self.eng.h), "ad_shard_levels_allreduce")
+
+    def order(self):
+        lv = np.zeros(max(self.n_home, 1), np.uint32)
+        od = np.zeros(max(self.n_home, 1), np.uint32)
+        self._check(self.L.ad_shard_order(self.eng.h, _u32p(lv), _u32p(od)), "ad_shard_order")
+        return lv[:self.n_home], od[:self.n_home]
+
+
+def unique_id():
+    buf = (C.c_uint8 * 128)()
+    rc = engine.lib().ad_comm_unique_id(buf)
+    if rc != abi.AD_OK:
+        raise engine.AccordDepsError(rc, "ad_comm_unique_id failed")
+    return bytes(buf)
+
+
+# ------------------------------------------------------------------------------------------------
+# transports
+# ------------------------------------------------------------------------------------------------
+class GlooTransport:
+    """Host staging over a torch.distributed (gloo) process group."""
+
+    name = "host(gloo)"
+
+    def __init__(self, dist):
+        self.dist = dist
+        import torch
+        self.torch = torch
+
+    def max_u64(self, x):
+        t = self.torch.tensor([x], dtype=self.torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return int(t.item())
+
+    def any(self, flag):
+        return self.max_u64(1 if flag else 0) > 0
+
+    def exchange_blobs(self, store):
+        n = store.export()
+        stride = (self.max_u64(n) + 7) // 8 * 8
+        mine = np.zeros(stride, np.uint8)
+        mine[:n] = store.blob()
+        world = self.dist.get_world_size()
+        parts = [self.torch.zeros(stride, dtype=self.torch.uint8) for _ in range(world)]
+        self.dist.all_gather(parts, self.torch.from_numpy(mine))
+        store.import_host(np.concatenate([p.numpy() for p in parts]), world, stride)
+
+    def allreduce_levels(self, store):
+        g = self.torch.from_numpy(store.levels_get().astype(np.int64))
+        self.dist.all_reduce(g, op=self.dist.ReduceOp.MAX)
+        store.levels_set(g.numpy().astype(np.uint32))
+
+
+class RcclTransport(GlooTransport):
+    """Blobs and level arrays move over RCCL (ncclAllGather / ncclAllReduce on device buffers, xGMI);
+    the gloo group only carries the unique id and the stride / convergence scalars."""
+
+    name = "rccl"
+
+    def __init__(self, dist, store, rank, world):
+        super().__init__(dist)
+        obj = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        store.comm_init(world, rank, obj[0])
+
+    def exchange_blobs(self, store):
+        n = store.export()
+        stride = (self.max_u64(n) + 7) // 8 * 8
+        store.allgather(stride)
+
+    def allreduce_levels(self, store):
+        store.levels_allreduce()
+
+
+def run_store(store, transport, max_rounds=1 << 16):
+    """The per-store protocol after load(): returns the number of distributed level rounds."""
+    store.preaccept()
+    transport.exchange_blobs(store)
+    store.merge()
+    changed = store.levels_round(True)
+    rounds = 1
+    while True:
+        transport.allreduce_levels(store)
+        if not transport.any(changed) or rounds >= max_rounds:
+            break
+        changed = store.levels_round(False)
+        rounds += 1
+    return rounds
+
+
+class LocalTransport:
+    """Several stores in one process (tests): the same protocol with in-process exchange."""
+
+    @staticmethod
+    def run(stores):
+        for s in stores:
+            s.preaccept()
+        sizes = [s.export() for s in stores]
+        stride = (max(sizes) + 7) // 8 * 8
+        recv = np.zeros(stride * len(stores), np.uint8)
+        for k, s in enumerate(stores):
+            recv[k * stride:k * stride + sizes[k]] = s.blob()
+        for s in stores:
+            s.import_host(recv, len(stores), stride)
+            s.merge()
+        changed = [s.levels_round(True) for s in stores]
+        rounds = 1
+        while True:
+            g = np.maximum.reduce([s.levels_get() for s in stores])
+            for s in stores:
+                s.levels_set(g)
+            if not any(changed):
+                break
+            changed = [s.levels_round(False) for s in stores]
+            rounds += 1
+        return rounds

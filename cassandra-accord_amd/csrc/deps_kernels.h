@@ -259,6 +259,7 @@ struct WalkArgs {
     const uint64_t* pm_c;
     const uint64_t* tx_ts;
     const uint8_t* meta;      // per txn
+    const uint32_t* gid;      // sharded batches: local row -> global arrival rank (nullable = identity)
     size_t P;
     uint32_t window;
     uint32_t thresh;
@@ -290,19 +291,22 @@ __device__ inline int next_elidable(const WalkArgs& a, int q, int seg0, uint64_t
 // [seg0, s) (all with TxnId < i), every replica view at once.  emit(v, direct, j) in descending order.
 template <int NV, class Emit>
 __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, int s, int seg0, Emit&& emit) {
-    const uint32_t lo = a.window == 0 ? i : (i > a.window ? i - a.window : 0u);
+    // window and drop decisions use global arrival ranks (shard-invariant); emitted ids stay local rows
+    const uint32_t gi = a.gid ? a.gid[i] : i;
+    const uint32_t lo = a.window == 0 ? gi : (gi > a.window ? gi - a.window : 0u);
     // 1. in-flight window: txns j in [i - W, i) are PREACCEPTED from i's viewpoint; replica view v has
     //    not witnessed j with probability drop_p (ad_drop_hash).
     int q = s - 1;
     for (; q >= seg0; --q) {
         const uint32_t j = a.e_txn[q];
-        if (j < lo) break;
+        const uint32_t gj = a.gid ? a.gid[j] : j;
+        if (gj < lo) break;
         const uint32_t mj = a.e_meta[q];
         if (!manages(mj) || !witnesses(qk, meta_kind(mj))) continue;
         const bool direct = !manages_execution(mj);
 #pragma unroll
         for (int v = 0; v < NV; ++v)
-            if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh)) emit(v, direct, j);
+            if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh)) emit(v, direct, j);
     }
     // 2. the committed prefix [seg0, p]: mapReduceActive with transitive-dependency elision.
     const int p = q;

@@ -11,14 +11,18 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "level_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
+#include "shard_kernels.h"
 
 using namespace ad;
 
@@ -79,6 +83,25 @@ struct ad_handle {
     Csr rdeps[MAXV];                 // RangeDeps per view
     Csr merged[3];
     Csr hparts[3][MAXV];             // ad_merge_host uploads
+    // key-range sharding (shard_kernels.h)
+    bool sharded = false;
+    size_t n_global = 0;
+    uint32_t* gid = nullptr;         // local row -> global arrival rank
+    uint8_t* home = nullptr;         // local row is homed here (first key in this store's range)
+    uint8_t* send = nullptr;
+    size_t send_bytes = 0;
+    uint8_t* recv = nullptr;
+    uint32_t world = 0;
+    size_t stride = 0;
+    size_t H = 0;                    // home txns
+    uint32_t *home_rows = nullptr, *home_gid = nullptr, *G = nullptr;
+    int32_t* src_rows = nullptr;     // [source * H + h]
+    std::vector<Csr> src_csr;        // [source * nvc + vc] views into recv
+    std::vector<uint32_t*> src_gid;
+    std::vector<uint32_t> src_n;
+    std::vector<Csr> sdeps;          // home-indexed per (view, class)
+    Csr smerged[3];
+    ncclComm_t comm = nullptr;
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
@@ -133,11 +156,13 @@ enum Slot : size_t {
     S_PMW, S_PMC, S_SEG, S_UD, S_CNT, S_DST, S_NK, S_NE, S_SCRATCH,
     S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
+    S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
 // merged [NVC_MAX + MAXV, +3)
 constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV, CSR_HOST0 = CSR_MERGED0 + 3;
+constexpr size_t CSR_SHARD0 = CSR_HOST0 + 3 * MAXV, CSR_SMERGED0 = CSR_SHARD0 + NVC_MAX;
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
 
@@ -352,6 +377,7 @@ int stage_deps(ad_handle* h) {
     wa.e_txn = h->e_txn; wa.e_meta = h->e_meta; wa.e_exec1 = h->e_exec1; wa.seg_start = h->seg_start;
     wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
+    wa.gid = h->sharded ? h->gid : nullptr;
     wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
     NV_DISPATCH(nv, launch_walk, wa, false, st);
@@ -439,74 +465,114 @@ int stage_deps(ad_handle* h) {
         }
     }
     h->have_deps = true;
+    h->ls.chains_ready = false;
     return AD_OK;
 }
 
 // ---------------------------------------------------------------------------------------------------
 // merge
 // ---------------------------------------------------------------------------------------------------
-// Deps.merge of `np` parts per class into h->merged (all classes counted, scanned and sized together:
-// one host sync).  parts[cls][v] are batched per-txn CSRs over the loaded batch.
-int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_range) {
-    const size_t n = h->n;
-    hipStream_t st = h->st;
-    h->merged_entries = 0;
-    uint32_t *mk, *me, *mu;
-    CK(dalloc(h, S_MSCR, &mk, 9 * n + 3));
-    me = mk + 3 * n;
-    mu = me + 3 * n;
-    MergeArgs ma[3]{};
-    MergeOffsetsOp op{};
+template <int K>
+void launch_multi_offsets(ad_handle* h, size_t n, const uint32_t* mk, const uint32_t* me, const uint32_t* mu, Csr* const* out) {
+    MultiOffsetsOp<K> op{};
     op.n = n; op.mk = mk; op.me = me; op.mu = mu;
-    for (int cls = 0; cls < 3; ++cls) {
-        Csr& m = h->merged[cls];
-        CK(alloc_csr(h, CSR_MERGED0 + cls, m, n));
-        const bool live = !(cls == AD_CLASS_RANGE && !has_range);
-        op.live[cls] = live ? 1 : 0;
-        op.key_off[cls] = m.key_off; op.ent_off[cls] = m.ent_off; op.k2t_off[cls] = m.k2t_off;
-        if (!live) {
-            m.nkeys = m.nk2t = m.ncap = 0;
-            HIPCHK(h, hipMemsetAsync(m.key_off, 0, (n + 1) * 4, st));
-            HIPCHK(h, hipMemsetAsync(m.ent_off, 0, (n + 1) * 4, st));
-            HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, (n + 1) * 4, st));
-            continue;
-        }
-        MergeArgs& a = ma[cls];
+    for (int c = 0; c < K; ++c) { op.key_off[c] = out[c]->key_off; op.ent_off[c] = out[c]->ent_off; op.k2t_off[c] = out[c]->k2t_off; }
+    device_scan(op, n, (typename MultiOffsetsOp<K>::S*)h->scratch, h->st);
+}
+
+// K unions computed together (count, one fused offsets scan, ONE host sync, allocation, write):
+// out[k] = Deps.merge over in[k][0..np) per output txn; rows[k][v] (nullable) maps output txn -> input row.
+int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* out_block, const int* kw,
+                const Csr* const (*in)[MAXV], const int32_t* const (*rows)[MAXV], int np, uint64_t* entries) {
+    hipStream_t st = h->st;
+    uint32_t *mk, *me, *mu;
+    CK(dalloc(h, S_MSCR, &mk, 3 * (size_t)K * n + 3));
+    me = mk + (size_t)K * n;
+    mu = me + (size_t)K * n;
+    std::vector<MergeArgs> ma(K);
+    for (int k = 0; k < K; ++k) {
+        CK(alloc_csr(h, out_block[k], *out[k], n));
+        MergeArgs& a = ma[k];
+        a = MergeArgs{};
         a.n = n; a.nv = np;
         for (int v = 0; v < np; ++v) {
-            const Csr& c = *parts[cls][v];
+            const Csr& c = *in[k][v];
             a.key_off[v] = c.key_off; a.keys[v] = c.keys; a.k2t_off[v] = c.k2t_off; a.k2t[v] = c.k2t;
             a.ent_off[v] = c.ent_off; a.txns[v] = c.txns; a.tcnt[v] = c.tcnt;
+            a.row[v] = rows ? rows[k][v] : nullptr;
         }
-        a.mk = mk + cls * n; a.me = me + cls * n; a.mu = mu + cls * n;
-        if (n > 0) merge_launch(a, np, false, cls == AD_CLASS_RANGE ? 2 : 1, st);
+        a.mk = mk + (size_t)k * n; a.me = me + (size_t)k * n; a.mu = mu + (size_t)k * n;
+        if (n > 0) merge_launch(a, np, false, kw[k], st);
     }
     if (n > 0) {
         KScope ks(K_SCAN_OFFSETS);
-        device_scan(op, n, (MergeOffsetsOp::S*)h->scratch, st);
+        switch (K) {
+            case 1: launch_multi_offsets<1>(h, n, mk, me, mu, out); break;
+            case 2: launch_multi_offsets<2>(h, n, mk, me, mu, out); break;
+            case 3: launch_multi_offsets<3>(h, n, mk, me, mu, out); break;
+            case 4: launch_multi_offsets<4>(h, n, mk, me, mu, out); break;
+            case 6: launch_multi_offsets<6>(h, n, mk, me, mu, out); break;
+            case 8: launch_multi_offsets<8>(h, n, mk, me, mu, out); break;
+            case 10: launch_multi_offsets<10>(h, n, mk, me, mu, out); break;
+            case 12: launch_multi_offsets<12>(h, n, mk, me, mu, out); break;
+            case 14: launch_multi_offsets<14>(h, n, mk, me, mu, out); break;
+            case 16: launch_multi_offsets<16>(h, n, mk, me, mu, out); break;
+            default: return set_err(h, AD_ERR_UNSUPPORTED, "merge_multi: unsupported output count");
+        }
+    } else {
+        for (int k = 0; k < K; ++k) {
+            HIPCHK(h, hipMemsetAsync(out[k]->key_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(out[k]->ent_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(out[k]->k2t_off, 0, 4, st));
+        }
     }
-    uint32_t tot[9] = {0};
-    for (int cls = 0; cls < 3; ++cls) {
-        if (!op.live[cls] || n == 0) continue;
-        Csr& m = h->merged[cls];
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * cls + 0], m.key_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * cls + 1], m.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * cls + 2], m.ent_off + n, 4, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> tot(3 * K, 0);
+    for (int k = 0; k < K; ++k) {
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * k + 0], out[k]->key_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * k + 1], out[k]->k2t_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[3 * k + 2], out[k]->ent_off + n, 4, hipMemcpyDeviceToHost, st));
     }
     CK(read_params(h));
     CK(check_params(h));
-    for (int cls = 0; cls < 3; ++cls) {
-        if (!op.live[cls]) continue;
-        Csr& m = h->merged[cls];
-        const int kw = cls == AD_CLASS_RANGE ? 2 : 1;
-        m.nkeys = tot[3 * cls]; m.nk2t = tot[3 * cls + 1]; m.ncap = tot[3 * cls + 2];
-        h->merged_entries += m.nk2t - m.nkeys;
-        CK(alloc_csr_data(h, CSR_MERGED0 + cls, m, kw));
-        MergeArgs& a = ma[cls];
+    for (int k = 0; k < K; ++k) {
+        Csr& m = *out[k];
+        m.nkeys = tot[3 * k]; m.nk2t = tot[3 * k + 1]; m.ncap = tot[3 * k + 2];
+        if (entries) *entries += m.nk2t - m.nkeys;
+        CK(alloc_csr_data(h, out_block[k], m, kw[k]));
+        MergeArgs& a = ma[k];
         a.o_key_off = m.key_off; a.o_keys = m.keys; a.o_k2t_off = m.k2t_off; a.o_k2t = m.k2t;
         a.o_ent_off = m.ent_off; a.o_txns = m.txns; a.o_tcnt = m.tcnt;
-        if (n > 0) merge_launch(a, np, true, kw, st);
+        if (n > 0) merge_launch(a, np, true, kw[k], st);
     }
+    return AD_OK;
+}
+
+// Deps.merge of `np` parts per class into h->merged.  parts[cls][v] are batched per-txn CSRs over the loaded batch.
+int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_range) {
+    const size_t n = h->n;
+    h->merged_entries = 0;
+    Csr* out[3];
+    size_t blocks[3];
+    int kw[3];
+    const Csr* in[3][MAXV] = {};
+    int K = 0;
+    for (int cls = 0; cls < 3; ++cls) {
+        if (cls == AD_CLASS_RANGE && !has_range) {
+            Csr& m = h->merged[cls];
+            CK(alloc_csr(h, CSR_MERGED0 + cls, m, n));
+            m.nkeys = m.nk2t = m.ncap = 0;
+            HIPCHK(h, hipMemsetAsync(m.key_off, 0, (n + 1) * 4, h->st));
+            HIPCHK(h, hipMemsetAsync(m.ent_off, 0, (n + 1) * 4, h->st));
+            HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, (n + 1) * 4, h->st));
+            continue;
+        }
+        out[K] = &h->merged[cls];
+        blocks[K] = CSR_MERGED0 + cls;
+        kw[K] = cls == AD_CLASS_RANGE ? 2 : 1;
+        for (int v = 0; v < np; ++v) in[K][v] = parts[cls][v];
+        ++K;
+    }
+    CK(merge_multi(h, n, K, out, blocks, kw, in, nullptr, np, &h->merged_entries));
     h->have_merged = true;
     return AD_OK;
 }
@@ -655,6 +721,7 @@ int ad_open(int device, const ad_config* cfg, ad_handle** out) {
 void ad_close(ad_handle* h) {
     if (!h) return;
     hipSetDevice(h->device);
+    if (h->comm) ncclCommDestroy(h->comm);
     if (h->st) hipStreamSynchronize(h->st);
     for (auto& b : h->bufs) if (b.p) hipFree(b.p);
     for (auto& e : h->ev) if (e) hipEventDestroy(e);
@@ -914,6 +981,338 @@ int ad_reset_kernel_stats(ad_handle* h) {
     HIPCHK(h, hipStreamSynchronize(h->st));
     h->tracer.resolve();
     h->tracer.reset_counts();
+    return AD_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Key-range sharding across GPUs (shard_kernels.h)
+// ---------------------------------------------------------------------------------------------------
+static size_t align8(size_t x) { return (x + 7) & ~(size_t)7; }
+
+int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home, size_t n_global) {
+    if (!h || (!gid && h->n) || (!home && h->n)) return AD_ERR_ARGUMENT;
+    if (!h->loaded) return set_err(h, AD_ERR_STATE, "ad_shard_setup: load the store's batch first");
+    if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "sharded mode: range txns are not supported in this build");
+    hipSetDevice(h->device);
+    const size_t n = h->n;
+    for (size_t i = 0; i < n; ++i)
+        if (gid[i] >= n_global || (i > 0 && gid[i] <= gid[i - 1])) return set_err(h, AD_ERR_ARGUMENT, "gid must be ascending global ranks < n_global");
+    CK(dalloc(h, S_GID, &h->gid, n)); CK(dalloc(h, S_HOME, &h->home, n));
+    if (n) {
+        HIPCHK(h, hipMemcpyAsync(h->gid, gid, n * 4, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->home, home, n, hipMemcpyHostToDevice, h->st));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->sharded = true;
+    h->n_global = n_global;
+    h->have_deps = h->have_merged = h->have_levels = false;
+    return AD_OK;
+}
+
+// Pack this store's deps (every view, key + direct class), TxnIds rewritten to global ranks, into one blob.
+int ad_shard_export(ad_handle* h, size_t* bytes) {
+    if (!h || !bytes) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_export: ad_shard_setup + ad_preaccept_deps first");
+    hipSetDevice(h->device);
+    const size_t n = h->n;
+    const int nvc = 2 * (int)h->cfg.replicas;
+    hipStream_t st = h->st;
+    for (int vc = 0; vc < nvc; ++vc) {
+        Csr& c = h->deps[vc];
+        if (n) k_txns_to_global<<<ceil_div((long)n, 256), 256, 0, st>>>(n, c.ent_off, c.tcnt, c.txns, h->gid);
+    }
+    // layout: header u64[3 + 3 nvc] | gid | per vc: key_off k2t_off ent_off tcnt keys k2t txns  (8-byte aligned)
+    const size_t hdr_words = 3 + 3 * (size_t)nvc;
+    size_t off = align8(hdr_words * 8);
+    std::vector<Segment> segs;
+    segs.push_back(Segment{h->gid, (void*)off, n * 4}); off = align8(off + n * 4);
+    for (int vc = 0; vc < nvc; ++vc) {
+        Csr& c = h->deps[vc];
+        segs.push_back(Segment{c.key_off, (void*)off, (n + 1) * 4}); off = align8(off + (n + 1) * 4);
+        segs.push_back(Segment{c.k2t_off, (void*)off, (n + 1) * 4}); off = align8(off + (n + 1) * 4);
+        segs.push_back(Segment{c.ent_off, (void*)off, (n + 1) * 4}); off = align8(off + (n + 1) * 4);
+        segs.push_back(Segment{c.tcnt, (void*)off, n * 4}); off = align8(off + n * 4);
+        segs.push_back(Segment{c.keys, (void*)off, c.nkeys * 8}); off = align8(off + c.nkeys * 8);
+        segs.push_back(Segment{c.k2t, (void*)off, c.nk2t * 4}); off = align8(off + c.nk2t * 4);
+        segs.push_back(Segment{c.txns, (void*)off, c.ncap * 4}); off = align8(off + c.ncap * 4);
+    }
+    const size_t total = off;
+    CK(dalloc(h, S_SEND, &h->send, total));
+    std::vector<uint64_t> hdr(hdr_words);
+    hdr[0] = 0xAD5EC0DEull; hdr[1] = n; hdr[2] = (uint64_t)nvc;
+    for (int vc = 0; vc < nvc; ++vc) {
+        hdr[3 + 3 * vc] = h->deps[vc].nkeys; hdr[4 + 3 * vc] = h->deps[vc].nk2t; hdr[5 + 3 * vc] = h->deps[vc].ncap;
+    }
+    HIPCHK(h, hipMemcpyAsync(h->send, hdr.data(), hdr_words * 8, hipMemcpyHostToDevice, st));
+    for (size_t b = 0; b < segs.size(); b += MAX_SEGS) {
+        SegTable tab{};
+        tab.count = (int)std::min<size_t>(MAX_SEGS, segs.size() - b);
+        for (int k = 0; k < tab.count; ++k) {
+            tab.s[k] = segs[b + k];
+            tab.s[k].dst = h->send + (size_t)segs[b + k].dst;
+            if (tab.s[k].bytes == 0) tab.s[k].src = tab.s[k].dst;
+        }
+        k_copy_segments<<<dim3(64, tab.count), 256, 0, st>>>(tab);
+    }
+    HIPCHK(h, hipStreamSynchronize(st));   // host header buffer lifetime
+    h->send_bytes = total;
+    *bytes = total;
+    return AD_OK;
+}
+
+int ad_shard_blob_to_host(ad_handle* h, void* dst) {
+    if (!h || !dst || !h->send) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipMemcpyAsync(dst, h->send, h->send_bytes, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
+static int parse_recv(ad_handle* h) {
+    const int nvc = 2 * (int)h->cfg.replicas;
+    const size_t hdr_words = 3 + 3 * (size_t)nvc;
+    std::vector<uint64_t> hdr(hdr_words * h->world);
+    for (uint32_t s = 0; s < h->world; ++s)
+        HIPCHK(h, hipMemcpyAsync(hdr.data() + s * hdr_words, h->recv + s * h->stride, hdr_words * 8, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->src_csr.assign((size_t)h->world * nvc, Csr{});
+    h->src_gid.assign(h->world, nullptr);
+    h->src_n.assign(h->world, 0);
+    for (uint32_t s = 0; s < h->world; ++s) {
+        const uint64_t* hd = hdr.data() + s * hdr_words;
+        if (hd[0] != 0xAD5EC0DEull || hd[2] != (uint64_t)nvc) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": bad header (replicas must match)");
+        const size_t ns = hd[1];
+        uint8_t* base = h->recv + s * h->stride;
+        size_t off = align8(hdr_words * 8);
+        h->src_gid[s] = (uint32_t*)(base + off); off = align8(off + ns * 4);
+        h->src_n[s] = (uint32_t)ns;
+        for (int vc = 0; vc < nvc; ++vc) {
+            Csr& c = h->src_csr[(size_t)s * nvc + vc];
+            c.nkeys = hd[3 + 3 * vc]; c.nk2t = hd[4 + 3 * vc]; c.ncap = hd[5 + 3 * vc];
+            c.key_off = (uint32_t*)(base + off); off = align8(off + (ns + 1) * 4);
+            c.k2t_off = (uint32_t*)(base + off); off = align8(off + (ns + 1) * 4);
+            c.ent_off = (uint32_t*)(base + off); off = align8(off + (ns + 1) * 4);
+            c.tcnt = (uint32_t*)(base + off); off = align8(off + ns * 4);
+            c.keys = (uint64_t*)(base + off); off = align8(off + c.nkeys * 8);
+            c.k2t = (int32_t*)(base + off); off = align8(off + c.nk2t * 4);
+            c.txns = (uint32_t*)(base + off); off = align8(off + c.ncap * 4);
+        }
+        if (off > h->stride) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + " exceeds the stride");
+    }
+    return AD_OK;
+}
+
+int ad_shard_import_host(ad_handle* h, const void* src, uint32_t world, size_t stride) {
+    if (!h || !src || world == 0 || world > 64) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    CK(dalloc(h, S_RECV, &h->recv, (size_t)world * stride));
+    HIPCHK(h, hipMemcpyAsync(h->recv, src, (size_t)world * stride, hipMemcpyHostToDevice, h->st));
+    h->world = world; h->stride = stride;
+    return parse_recv(h);
+}
+
+int ad_comm_unique_id(uint8_t* out /* [128] */) {
+    if (!out) return AD_ERR_ARGUMENT;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return AD_ERR_DEVICE;
+    std::memcpy(out, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+    return AD_OK;
+}
+
+int ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id_bytes) {
+    if (!h || !id_bytes || rank >= world) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    ncclUniqueId id;
+    std::memcpy(&id, id_bytes, sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&h->comm, (int)world, id, (int)rank);
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    h->world = world;
+    return AD_OK;
+}
+
+// RCCL all-gather of the packed blobs over xGMI (every rank passes the same stride >= max blob bytes).
+int ad_shard_allgather(ad_handle* h, size_t stride) {
+    if (!h || !h->comm || !h->send) return set_err(h, AD_ERR_STATE, "ad_shard_allgather: ad_comm_init + ad_shard_export first");
+    if (stride < h->send_bytes) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    CK(dalloc(h, S_SEND, &h->send, stride));   // grows in place only if needed (keeps contents: slot already >= bytes)
+    CK(dalloc(h, S_RECV, &h->recv, (size_t)h->world * stride));
+    h->stride = stride;
+    ncclResult_t r = ncclAllGather(h->send, h->recv, stride, ncclUint8, h->comm, h->st);
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    return parse_recv(h);
+}
+
+// Home txns: merge every store's fragment per view (k_merge over sources with row indirection), then
+// Deps.merge across the replica views.  sizes[view * 3 + cls] (view == replicas: merged).
+int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
+    if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (h->src_csr.empty()) return set_err(h, AD_ERR_STATE, "ad_shard_merge: exchange the blobs first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const size_t n = h->n;
+    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
+    if (h->world > (uint32_t)MAXV) return set_err(h, AD_ERR_UNSUPPORTED, "more than 8 shards");
+    // home rows + global ids
+    CK(dalloc(h, S_HROWS, &h->home_rows, n + 1));
+    uint32_t* tot = nullptr;
+    CK(dalloc(h, S_NK, &tot, 16));
+    if (n) device_scan(CompactFlagOp{h->home, h->home_rows, tot, n}, n, (uint32_t*)h->scratch, st);
+    else HIPCHK(h, hipMemsetAsync(tot, 0, 4, st));
+    uint32_t Hh = 0;
+    HIPCHK(h, hipMemcpyAsync(&Hh, tot, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    const size_t H = Hh;
+    h->H = H;
+    CK(dalloc(h, S_HGID, &h->home_gid, H));
+    CK(dalloc(h, S_SROWS, &h->src_rows, H * h->world));
+    if (H) {
+        k_home_gid<<<ceil_div((long)H, 256), 256, 0, st>>>(H, h->home_rows, h->gid, h->home_gid);
+        for (uint32_t s = 0; s < h->world; ++s)
+            k_source_rows<<<ceil_div((long)H, 256), 256, 0, st>>>(H, h->home_gid, h->src_gid[s], h->src_n[s], h->src_rows + s * H);
+    }
+    // per (view, class): union over sources
+    h->sdeps.resize(nvc);
+    std::vector<Csr*> out(nvc);
+    std::vector<size_t> blocks(nvc);
+    std::vector<int> kw(nvc, 1);
+    std::vector<std::array<const Csr*, MAXV>> in(nvc);
+    std::vector<std::array<const int32_t*, MAXV>> rows(nvc);
+    for (int vc = 0; vc < nvc; ++vc) {
+        out[vc] = &h->sdeps[vc];
+        blocks[vc] = CSR_SHARD0 + vc;
+        for (uint32_t s = 0; s < h->world; ++s) {
+            in[vc][s] = &h->src_csr[(size_t)s * nvc + vc];
+            rows[vc][s] = h->src_rows + s * H;
+        }
+    }
+    CK(merge_multi(h, H, nvc, out.data(), blocks.data(), kw.data(),
+                   reinterpret_cast<const Csr* const (*)[MAXV]>(in.data()),
+                   reinterpret_cast<const int32_t* const (*)[MAXV]>(rows.data()), (int)h->world, nullptr));
+    // Deps.merge across views (key, direct); RangeDeps are empty in sharded mode
+    Csr* mout[2] = {&h->smerged[0], &h->smerged[1]};
+    size_t mblocks[2] = {CSR_SMERGED0, CSR_SMERGED0 + 1};
+    int mkw[2] = {1, 1};
+    const Csr* min_[2][MAXV] = {};
+    for (int v = 0; v < nv; ++v) { min_[0][v] = &h->sdeps[2 * v]; min_[1][v] = &h->sdeps[2 * v + 1]; }
+    uint64_t ent = 0;
+    CK(merge_multi(h, H, 2, mout, mblocks, mkw, min_, nullptr, nv, &ent));
+    h->merged_entries = ent;
+    if (n_home) *n_home = H;
+    if (sizes) {
+        for (int v = 0; v <= nv; ++v) {
+            for (int c = 0; c < 2; ++c) {
+                const Csr& x = v < nv ? h->sdeps[2 * v + c] : h->smerged[c];
+                std::vector<uint32_t> cnt(H);
+                if (H && x.ncap) {
+                    HIPCHK(h, hipMemcpyAsync(cnt.data(), x.tcnt, H * 4, hipMemcpyDeviceToHost, st));
+                    HIPCHK(h, hipStreamSynchronize(st));
+                }
+                size_t t = 0;
+                for (uint32_t q : cnt) t += q;
+                sizes[v * 3 + c] = ad_csr_sizes{H, x.nkeys, x.nk2t, x.ncap, t};
+            }
+            sizes[v * 3 + 2] = ad_csr_sizes{H, 0, 0, 0, 0};
+        }
+    }
+    return AD_OK;
+}
+
+int ad_shard_fetch(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out, uint32_t* home_gid) {
+    if (!h || !out || cls >= AD_NUM_CLASSES || view > h->cfg.replicas) return AD_ERR_ARGUMENT;
+    if (h->sdeps.empty()) return set_err(h, AD_ERR_STATE, "ad_shard_fetch: ad_shard_merge first");
+    hipSetDevice(h->device);
+    const size_t n_saved = h->n;
+    h->n = h->H;                          // fetch_csr / fetch_empty work over the home txns
+    int rc;
+    if (cls == AD_CLASS_RANGE) rc = fetch_empty(h, out);
+    else rc = fetch_csr(h, view < h->cfg.replicas ? h->sdeps[2 * view + cls] : h->smerged[cls], 1, out);
+    h->n = n_saved;
+    if (rc == AD_OK && home_gid && h->H) {
+        HIPCHK(h, hipMemcpyAsync(home_gid, h->home_gid, h->H * 4, hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipStreamSynchronize(h->st));
+    }
+    return rc;
+}
+
+// One round of the distributed level fixpoint: local chains from the replicated global levels, then
+// this store's levels back into the global array.  *changed: this store raised some global level.
+int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
+    if (!h || !changed) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_levels_round: sharded deps first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const size_t n = h->n;
+    CK(dalloc(h, S_G, &h->G, h->n_global + 1));
+    uint32_t* flag = nullptr;
+    CK(dalloc(h, S_NE, &flag, 16));
+    if (first) HIPCHK(h, hipMemsetAsync(h->G, 0, (h->n_global + 1) * 4, st));
+    else if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
+    LevelInputs li{};
+    li.n = n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
+    li.seg_start = h->seg_start; li.spos = h->spos; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.lvl = h->lvl; li.order = h->order;
+    li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;
+    li.n_large = 0;
+    li.exec_bits = h->pack.total_bits;
+    li.keep_levels = first ? 0 : 1;
+    int iters = 0;
+    CK(run_levels(h->ls, li, false, st, &iters, h->err));
+    if (first) h->ls.chains_ready = true;
+    HIPCHK(h, hipMemsetAsync(flag, 0, 4, st));
+    if (n) k_levels_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl, flag);
+    HIPCHK(h, hipMemcpyAsync(changed, flag, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    h->level_iters += (uint32_t)iters;
+    return AD_OK;
+}
+
+int ad_shard_levels_get(ad_handle* h, uint32_t* G) {
+    if (!h || !G || !h->G) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipMemcpyAsync(G, h->G, h->n_global * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
+int ad_shard_levels_set(ad_handle* h, const uint32_t* G) {
+    if (!h || !G || !h->G) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipMemcpyAsync(h->G, G, h->n_global * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
+// RCCL all-reduce(max) of the replicated global level array.
+int ad_shard_levels_allreduce(ad_handle* h) {
+    if (!h || !h->comm || !h->G) return set_err(h, AD_ERR_STATE, "ad_shard_levels_allreduce: ad_comm_init + a round first");
+    hipSetDevice(h->device);
+    ncclResult_t r = ncclAllReduce(h->G, h->G, h->n_global, ncclUint32, ncclMax, h->comm, h->st);
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return AD_OK;
+}
+
+// Home txns' levels and execution order (by (level, executeAt)), as global ranks; on the device.
+int ad_shard_order(ad_handle* h, uint32_t* level_out, uint32_t* order_out) {
+    if (!h || !h->G || h->sdeps.empty()) return set_err(h, AD_ERR_STATE, "ad_shard_order: levels rounds + ad_shard_merge first");
+    hipSetDevice(h->device);
+    g_tracer = &h->tracer;
+    hipStream_t st = h->st;
+    const size_t H = h->H, n = h->n;
+    if (H == 0) return AD_OK;
+    if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
+    uint32_t *ord, *tmp;
+    CK(dalloc(h, S_ORDER, &ord, std::max(n, H) + 1));
+    CK(dalloc(h, S_MSCR, &tmp, 2 * H + 2));
+    order_rows(h->ls, H, h->home_rows, h->ex1, h->lvl, h->pack.total_bits, ord, st);
+    k_home_gid<<<ceil_div((long)H, 256), 256, 0, st>>>(H, ord, h->home_gid, tmp);           // order -> global ids
+    k_home_gid<<<ceil_div((long)H, 256), 256, 0, st>>>(H, h->home_rows, h->lvl, tmp + H);  // home levels
+    if (order_out) HIPCHK(h, hipMemcpyAsync(order_out, tmp, H * 4, hipMemcpyDeviceToHost, st));
+    if (level_out) HIPCHK(h, hipMemcpyAsync(level_out, tmp + H, H * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
     return AD_OK;
 }
 

@@ -207,6 +207,11 @@ struct SegListOp {                 // two compactions in one scan: short multi h
         if (i + 1 == n) { totals[0] = inc.a; totals[1] = inc.b; }
     }
 };
+__global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict__ heads, uint32_t count, uint32_t* __restrict__ stamp) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) stamp[heads[i]] = 0u;
+}
+
 // txn pair -> head position of its segment
 __global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ spos, const int32_t* __restrict__ seg_start,
                                                   int32_t* __restrict__ pair_seg) {
@@ -413,6 +418,8 @@ struct LevelState {
     uint32_t *sk0 = nullptr, *sv0 = nullptr, *sk1 = nullptr, *sv1 = nullptr;
     uint32_t* rs = nullptr;              // radix scratch
     size_t rs_cap = 0;
+    bool chains_ready = false;           // chain order / segment table valid for the current batch
+    uint32_t nheads = 0, nlong = 0;
 };
 
 inline void free_level_state(LevelState& s) {
@@ -443,7 +450,67 @@ struct LevelInputs {
     uint32_t U;
     uint32_t n_large;
     uint32_t exec_bits;
+    int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
 };
+
+// Execution order over m txns (rows[k], or k when rows is null): LSD radix sort by executeAt (two 32-bit
+// halves) then stably by level; order_out[k'] = k of the k'-th txn.  ls.sk*/sv*/rs must hold m entries.
+__global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint32_t* __restrict__ lvl, const uint32_t* __restrict__ rows,
+                                                           const uint32_t* __restrict__ perm, uint32_t* __restrict__ dst,
+                                                           uint32_t* __restrict__ maxv) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t v = 0;
+    if (i < m) {
+        const uint32_t k = perm[i];
+        v = lvl[rows ? rows[k] : k];
+        dst[i] = v;
+    }
+    v = wave_max(v);
+    __shared__ uint32_t red[256 / WAVE];
+    if (__lane_id() == 0) red[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t mx = red[0];
+        for (int k = 1; k < 256 / WAVE; ++k) mx = mx > red[k] ? mx : red[k];
+        atomicMax(maxv, mx);
+    }
+}
+__global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
+                                                         const uint32_t* __restrict__ perm, uint32_t* __restrict__ key, int hi) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t k = perm ? perm[i] : (uint32_t)i;
+    const uint64_t e = ex1[rows ? rows[k] : k] - 1;
+    key[i] = hi ? (uint32_t)(e >> 32) : (uint32_t)e;
+}
+
+inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
+                       uint32_t exec_bits, uint32_t* order_out, hipStream_t st) {
+    KScope ks(K_ORDER);
+    RadixScratch rs;
+    const size_t hl = radix_hist_len(m);
+    rs.hist = ls.rs;
+    rs.offs = rs.hist + hl + 64;
+    rs.agg = rs.offs + hl + 64;
+    const int g = ceil_div((long)m, 256);
+    const int eb = (int)exec_bits;
+    k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, nullptr, ls.sk0, 0);
+    k_iota<<<g, 256, 0, st>>>(m, ls.sv0);
+    uint32_t *k = ls.sk0, *v = ls.sv0, *ko = ls.sk1, *vo = ls.sv1;
+    if (radix_sort_pairs(k, v, ko, vo, m, eb < 32 ? eb : 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
+    if (eb > 32) {
+        k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, v, k, 1);
+        if (radix_sort_pairs(k, v, ko, vo, m, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
+    }
+    hipMemsetAsync(ls.flags + 4, 0, 4, st);
+    k_gather_level_rows<<<g, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
+    uint32_t maxl = 0;
+    hipMemcpyAsync(&maxl, ls.flags + 4, 4, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    const int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
+    if (radix_sort_pairs(k, v, ko, vo, m, lb, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
+    hipMemcpyAsync(order_out, v, m * 4, hipMemcpyDeviceToDevice, st);
+}
 
 inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hipStream_t st, int* iters,
                       std::string& err) {
@@ -485,7 +552,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
 
     hipMemsetAsync(ls.flags, 0, 64, st);
     if (n > 0) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
-    hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
+    if (!in.keep_levels) hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
     *iters = 0;
     {
         // ---- chain order, segment table, pair -> segment, long-segment positions, (c) constraints
@@ -508,7 +575,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         ea.cons_pos = ls.cons_pos; ea.pm_all = ls.pm_all; ea.ukey = in.ukey; ea.useg = in.useg; ea.U = in.U;
         ea.c_exec1 = ls.c_exec1; ea.c_txn = ls.c_txn; ea.seg_start = in.seg_start;
         uint32_t host[8] = {0};
-        if (P > 0) {
+        const bool reuse = in.keep_levels && ls.chains_ready;
+        if (P > 0 && reuse) {
+            k_stamp_reset<<<ceil_div((long)std::max<uint32_t>(ls.nheads, 1), 256), 256, 0, st>>>(ls.heads, ls.nheads, ls.stamp);
+        } else if (P > 0) {
             KScope ks(K_CHAIN_PREP);
             k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
             k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
@@ -523,7 +593,8 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
             return AD_ERR_UNSUPPORTED;
         }
-        const uint32_t nheads = host[0], nlong = host[1];
+        if (!reuse) { ls.nheads = host[0]; ls.nlong = host[1]; ls.chains_ready = true; }
+        const uint32_t nheads = ls.nheads, nlong = ls.nlong;
         bool short_work = nheads > 0, long_dirty = nlong > 0;
         ChainOp op{ls.long_pos, ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.pm_all, push, ls.flags + 6};
         for (int it = 0; it < (1 << 24); ++it) {
@@ -553,34 +624,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             if (!short_work && !long_dirty && host[3] == 0) break;
         }
     }
-    if (want_order && n > 0) {
-        KScope ks(K_ORDER);
-        RadixScratch rs;
-        const size_t hl = radix_hist_len(n);
-        rs.hist = ls.rs;
-        rs.offs = rs.hist + hl + 64;
-        rs.agg = rs.offs + hl + 64;
-        const int g = ceil_div((long)n, 256);
-        const int eb = (int)in.exec_bits;
-        // executeAt order: low 32 bits then high bits (stable LSD)
-        k_exec_split<<<g, 256, 0, st>>>(n, in.ex1, nullptr, ls.sk0, 0);
-        k_iota<<<g, 256, 0, st>>>(n, ls.sv0);
-        uint32_t *k = ls.sk0, *v = ls.sv0, *ko = ls.sk1, *vo = ls.sv1;
-        if (radix_sort_pairs(k, v, ko, vo, n, eb < 32 ? eb : 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
-        if (eb > 32) {
-            k_exec_split<<<g, 256, 0, st>>>(n, in.ex1, v, k, 1);
-            if (radix_sort_pairs(k, v, ko, vo, n, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
-        }
-        // then stably by level
-        hipMemsetAsync(ls.flags + 4, 0, 4, st);
-        k_gather_u32<<<g, 256, 0, st>>>(n, in.lvl, v, k, ls.flags + 4);
-        uint32_t maxl = 0;
-        hipMemcpyAsync(&maxl, ls.flags + 4, 4, hipMemcpyDeviceToHost, st);
-        hipStreamSynchronize(st);
-        int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
-        if (radix_sort_pairs(k, v, ko, vo, n, lb, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
-        hipMemcpyAsync(in.order, v, n * 4, hipMemcpyDeviceToDevice, st);
-    }
+    if (want_order && n > 0) order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
     return AD_OK;
 oom:
     err = "exec levels: out of device memory";

@@ -24,6 +24,7 @@ struct MergeArgs {
     const uint32_t* ent_off[MAXV];
     const uint32_t* txns[MAXV];
     const uint32_t* tcnt[MAXV];
+    const int32_t* row[MAXV];    // optional per-part row indirection (nullptr = identity)
     uint32_t *mk, *me, *mu;      // count pass outputs
     const uint32_t* o_key_off;
     uint64_t* o_keys;
@@ -54,11 +55,15 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     if (t >= a.n) return;
     constexpr uint32_t INF = 0xFFFFFFFFu;
     // ---- 1. union of TxnId rank lists
+    // input row of output txn t in each part (shard merge: a global txn's row in each source, -1 = absent)
+    int64_t rv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) rv[v] = a.row[v] ? (int64_t)a.row[v][t] : (int64_t)t;
     uint32_t cur[NV], end[NV], head[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        cur[v] = a.ent_off[v][t];
-        end[v] = cur[v] + a.tcnt[v][t];
+        cur[v] = rv[v] >= 0 ? a.ent_off[v][rv[v]] : 0u;
+        end[v] = rv[v] >= 0 ? cur[v] + a.tcnt[v][rv[v]] : 0u;
         head[v] = cur[v] < end[v] ? a.txns[v][cur[v]] : INF;
     }
     uint32_t* out = WRITE ? a.o_txns + a.o_ent_off[t] : nullptr;
@@ -78,11 +83,12 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     uint32_t kc[NV], ke[NV], mb[NV], tb[NV], nkv[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        kc[v] = a.key_off[v][t];
-        ke[v] = a.key_off[v][t + 1];
+        const bool has = rv[v] >= 0;
+        kc[v] = has ? a.key_off[v][rv[v]] : 0u;
+        ke[v] = has ? a.key_off[v][rv[v] + 1] : 0u;
         nkv[v] = ke[v] - kc[v];
-        mb[v] = a.k2t_off[v][t];
-        tb[v] = a.ent_off[v][t];
+        mb[v] = has ? a.k2t_off[v][rv[v]] : 0u;
+        tb[v] = has ? a.ent_off[v][rv[v]] : 0u;
     }
     const uint32_t okb = WRITE ? a.o_key_off[t] : 0;
     const uint32_t onk = WRITE ? a.o_key_off[t + 1] - okb : 0;
@@ -106,7 +112,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
         for (int v = 0; v < NV; ++v) {
             lc[v] = 0; le[v] = 0; lh[v] = INF;
             if (kc[v] < ke[v] && MKey<KW>::load(a.keys[v], kc[v]) == kmin) {
-                const uint32_t ki = kc[v] - a.key_off[v][t];
+                const uint32_t ki = kc[v] - a.key_off[v][rv[v]];
                 lc[v] = mb[v] + (ki == 0 ? nkv[v] : (uint32_t)a.k2t[v][mb[v] + ki - 1]);
                 le[v] = mb[v] + (uint32_t)a.k2t[v][mb[v] + ki];
                 lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF;
@@ -139,40 +145,38 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     else { a.mk[t] = mk; a.me[t] = me; a.mu[t] = mu; }
 }
 
-// Offsets of the three merged classes from the count pass, in one scan: state (keys, entries, TxnIds) x 3.
-struct MergeOffsetsOp {
-    struct S { uint32_t k[3], e[3], u[3]; };
+// Offsets of K merged outputs from the count pass, in one scan: state (keys, entries, TxnIds) x K.
+template <int K>
+struct MultiOffsetsOp {
+    struct S { uint32_t k[K], e[K], u[K]; };
     size_t n;
-    const uint32_t* mk;           // [cls * n + t]
+    const uint32_t* mk;           // [k * n + t]
     const uint32_t* me;
     const uint32_t* mu;
-    int live[3];
-    uint32_t* key_off[3];
-    uint32_t* ent_off[3];
-    uint32_t* k2t_off[3];
+    uint32_t* key_off[K];
+    uint32_t* ent_off[K];
+    uint32_t* k2t_off[K];
     __device__ S identity() const {
         S s;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { s.k[c] = 0; s.e[c] = 0; s.u[c] = 0; }
+        for (int c = 0; c < K; ++c) { s.k[c] = 0; s.e[c] = 0; s.u[c] = 0; }
         return s;
     }
     __device__ S load(size_t t) const {
-        S s = identity();
+        S s;
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            if (live[c]) { s.k[c] = mk[c * n + t]; s.e[c] = me[c * n + t]; s.u[c] = mu[c * n + t]; }
+        for (int c = 0; c < K; ++c) { s.k[c] = mk[c * n + t]; s.e[c] = me[c * n + t]; s.u[c] = mu[c * n + t]; }
         return s;
     }
     __device__ S combine(const S& x, const S& y) const {
         S r;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { r.k[c] = x.k[c] + y.k[c]; r.e[c] = x.e[c] + y.e[c]; r.u[c] = x.u[c] + y.u[c]; }
+        for (int c = 0; c < K; ++c) { r.k[c] = x.k[c] + y.k[c]; r.e[c] = x.e[c] + y.e[c]; r.u[c] = x.u[c] + y.u[c]; }
         return r;
     }
     __device__ void store(size_t t, const S& ex, const S& inc, const S&) const {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            if (!live[c]) continue;
+        for (int c = 0; c < K; ++c) {
             key_off[c][t] = ex.k[c];
             ent_off[c][t] = ex.u[c];
             k2t_off[c][t] = ex.k[c] + ex.e[c];
