@@ -1,20 +1,23 @@
 #!/usr/bin/env python3
 """bench.py — txn deps + execution order resolved per second on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path over one device-resident 1M-txn batch (BASELINE.json configs[1],
-C2: 1M txns x 4 keys, uniform over a 10M keyspace):
+One step = one pass of the hot path over one device-resident batch:
   PreAccept deps for every txn under R=3 replica views (CommandsForKey.mapReduceActive + Deps.Builder),
-  Deps.merge of the 3 replies, and execution levels/order over the merged graph — ad_run_pipeline().
+  Deps.merge of the 3 replies, and execution levels/order over the merged graph.
 
-Multi-GPU: one process per GPU (torch.distributed.run).  Each rank is one CommandStore owning a
-disjoint key range (keys offset by rank * keyspace) with its own 1M-txn batch, so the per-GPU work
-is fixed as N grows ("weak").  Ranks share no data on this config (C5's cross-shard exchange is a
-separate path), so the only inter-rank traffic is the timing barrier/max over a gloo group.
+N = 1 (BASELINE.json configs[1], C2): one 1M-txn batch (4 keys/txn, uniform over 10M keys) on one GPU,
+  ad_run_pipeline().
+N > 1 (configs[4], C5 shape, weak scaling): a global batch of N x 1M txns over N x 10M keys, key-range
+  sharded across the N GPUs (one process and CommandStore per GPU, ShardDistributor.EvenSplit).  Most txns
+  span several stores, so each step is the full cross-shard protocol (accord_amd.sharding.run_store):
+  local deps on the store's slice, export, all-gather of the per-store fragments over RCCL/xGMI, merge of
+  the fragments of the store's home txns (PreAccept.reduce) and across replica views (Deps.merge), and the
+  distributed level fixpoint (rounds of local chain relaxation + RCCL all-reduce(max)), then the order.
 
 Timing: W untimed warmup steps; then barrier + device sync, K timed steps, device sync + barrier,
-max over ranks.  The HIP work runs on the engine's own stream and every ad_run_pipeline() ends with
-an event synchronisation on it, so "device sync" is that stream's completion (this process never
-creates a torch HIP context).
+max over ranks.  The HIP work runs on the engine's own stream; every step ends synchronised on it, so
+"device sync" is that stream's completion (this process never creates a torch HIP context; torch.distributed
+carries only the RCCL unique id and scalars over gloo).
 """
 import argparse
 import json
@@ -88,14 +91,114 @@ def cpu_baseline(sample_n):
                       % (sample_n, REPLICAS, t, s["t_deps"], s["t_merge"], s["t_levels"])}
 
 
+def trace_roofline(eng, run_step, n, P, steps):
+    """Untimed all-kernels breakdown -> dominant kernel; then `steps` timed steps with only that kernel
+    event-timed on the engine stream.  Returns (wall seconds, roofline dict, breakdown, last times)."""
+    ids = engine.kernel_ids()
+    eng.set_trace((1 << len(ids)) - 1)
+    eng.reset_kernel_stats()
+    run_step()
+    brk = eng.kernel_stats()
+    st = eng.last_times()
+    dom = max((k for k in brk if alg_bytes(k, n, P, REPLICAS, st) is not None), key=lambda k: brk[k][1])
+    return dom, brk, st
+
+
+def roofline_of(eng, dom, n, P, st):
+    kst = eng.kernel_stats()[dom]
+    avg_ms = kst[1] / kst[0]
+    ab = alg_bytes(dom, n, P, REPLICAS, st)
+    achieved = ab / (avg_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": ab,
+            "avg_launch_ms": avg_ms, "launches": kst[0]}
+
+
+def print_breakdown(brk, st):
+    tot = sum(v[1] for v in brk.values())
+    for k, (c, ms) in sorted(brk.items(), key=lambda kv: -kv[1][1]):
+        print("  %-22s %5d launches %9.3f ms  %5.1f%%" % (k, c, ms, 100 * ms / tot), file=sys.stderr)
+    print("  stages: %s" % {k: round(v, 3) if isinstance(v, float) else v for k, v in st.items()}, file=sys.stderr)
+
+
+def main_sharded(args, rank, world, local, dist):
+    """N > 1: the C5 cross-shard protocol (see module docstring)."""
+    from accord_amd import sharding
+    n_total = args.n * world
+    batch = workload.generate(n_total, 4, KEYSPACE * world, "uniform", seed=workload.SEEDS["C5"])
+    bounds = sharding.even_bounds(0, KEYSPACE * world, world)
+    lb, gid, home = sharding.slice_for_shard(batch, bounds[rank], bounds[rank + 1])
+    del batch
+    device = local % max(1, engine.device_count())
+    store = sharding.ShardStore(device, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C5"])
+    store.load(lb, gid, home, n_total)
+    tr = None
+    if args.transport == "rccl":
+        try:
+            tr = sharding.RcclTransport(dist, store, rank, world)
+        except engine.AccordDepsError as e:     # e.g. ranks sharing one GPU: RCCL refuses duplicate devices
+            print("rank %d: RCCL unavailable (%s); using the host transport" % (rank, e), file=sys.stderr)
+        ok = tr is not None
+        t = __import__("torch").tensor([1 if ok else 0], dtype=__import__("torch").int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if not t.item():
+            tr = None
+    if tr is None:
+        tr = sharding.GlooTransport(dist)
+
+    def step():
+        r = sharding.run_store(store, tr)
+        store.order()
+        return r
+
+    rounds = 0
+    for _ in range(max(args.warmup, 1)):
+        rounds = step()
+    n_loc, P_loc = lb["n"], int(lb["key_off"][-1])
+    dom, brk, st = trace_roofline(store.eng, step, n_loc, P_loc, args.steps)
+    if args.breakdown and rank == 0:
+        print_breakdown(brk, st)
+    store.eng.set_trace(1 << engine.kernel_ids()[dom])
+    store.eng.reset_kernel_stats()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rounds = step()
+    t1 = time.perf_counter()
+    dist.barrier()
+    t = __import__("torch").tensor([t1 - t0], dtype=__import__("torch").float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    roof = roofline_of(store.eng, dom, n_loc, P_loc, store.eng.last_times())
+    store.eng.set_trace(0)
+    out = {
+        "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
+        "value": n_total * args.steps / dt, "unit": "txn/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C5 generator, BASELINE configs[4] shape)",
+        "config": {"workload": "C5: %d txns x 4 keys uniform over %dM keys, key-range sharded over %d GPUs "
+                               "(cross-shard deps all-gathered, distributed level rounds); R=%d views, W=%d, drop %.1f"
+                               % (n_total, 10 * world, world, REPLICAS, WINDOW, DROP_P),
+                   "txns_total": n_total, "txns_per_gpu": args.n, "local_txns_rank0": n_loc, "local_pairs_rank0": P_loc,
+                   "keys_per_txn": 4, "keyspace": KEYSPACE * world, "replicas": REPLICAS, "window": WINDOW,
+                   "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds},
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    store.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1 << 20, help="txns per GPU batch (C2: 1M)")
+    ap.add_argument("--txns-per-gpu", dest="n", type=int, default=1 << 20, help="txns per GPU batch (C2: 1M)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 18, help="txns in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel breakdown to stderr")
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl", help="N>1 exchange: RCCL over xGMI or host/gloo")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,10 +206,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as tdist
         tdist.init_process_group("gloo")
-        dist = tdist
+        try:
+            main_sharded(args, rank, world, local, tdist)
+        finally:
+            tdist.destroy_process_group()
+        return
 
     def barrier():
         if dist:

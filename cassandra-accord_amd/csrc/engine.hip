@@ -466,6 +466,8 @@ int stage_deps(ad_handle* h) {
     }
     h->have_deps = true;
     h->ls.chains_ready = false;
+    h->times.deps_entries = h->deps_entries;
+    h->times.level_edges = h->P;
     return AD_OK;
 }
 
@@ -1136,7 +1138,13 @@ int ad_shard_allgather(ad_handle* h, size_t stride) {
     if (!h || !h->comm || !h->send) return set_err(h, AD_ERR_STATE, "ad_shard_allgather: ad_comm_init + ad_shard_export first");
     if (stride < h->send_bytes) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    CK(dalloc(h, S_SEND, &h->send, stride));   // grows in place only if needed (keeps contents: slot already >= bytes)
+    if (h->bufs[S_SEND].cap < stride) {        // the collective reads `stride` bytes: grow, keeping the packed blob
+        uint8_t* tmp = nullptr;
+        CK(dalloc(h, S_RECV, &tmp, h->send_bytes));
+        HIPCHK(h, hipMemcpyAsync(tmp, h->send, h->send_bytes, hipMemcpyDeviceToDevice, h->st));
+        CK(dalloc(h, S_SEND, &h->send, stride));
+        HIPCHK(h, hipMemcpyAsync(h->send, tmp, h->send_bytes, hipMemcpyDeviceToDevice, h->st));
+    }
     CK(dalloc(h, S_RECV, &h->recv, (size_t)h->world * stride));
     h->stride = stride;
     ncclResult_t r = ncclAllGather(h->send, h->recv, stride, ncclUint8, h->comm, h->st);
@@ -1200,6 +1208,7 @@ int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
     uint64_t ent = 0;
     CK(merge_multi(h, H, 2, mout, mblocks, mkw, min_, nullptr, nv, &ent));
     h->merged_entries = ent;
+    h->times.merged_entries = ent;
     if (n_home) *n_home = H;
     if (sizes) {
         for (int v = 0; v <= nv; ++v) {
