@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __rest
                                                 const uint64_t* __restrict__ el, const int32_t* __restrict__ en,
                                                 const uint32_t* __restrict__ key_off, const uint64_t* __restrict__ keys,
                                                 size_t P, const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
-                                                size_t Q, Params* out) {
+                                                size_t Q, unsigned long long* __restrict__ partial) {
     constexpr int NF = 13;
     // fields: 0 msb_min 1 msb_max 2 hlc_min 3 hlc_max 4 node_min 5 node_max 6 key_min 7 key_max 8 max_keys
     //         9 rs_min 10 re_max 11 rw_max ; *_min are stored complemented so every field is a max
@@ -99,6 +99,35 @@ __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __rest
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if (__lane_id() == 0) red[w][NF - 1] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NF) {
+        const int k = threadIdx.x;
+        unsigned long long v = k == NF - 1 ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
+                                           : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
+        partial[(size_t)blockIdx.x * NF + k] = v;
+    }
+}
+
+// second level of k_minmax: one block folds the per-block partials into Params (no contended atomics)
+__global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out) {
+    constexpr int NF = 13;
+    __shared__ unsigned long long red[4][NF];
+    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+        for (int k = 0; k < NF; ++k) {
+            const unsigned long long v = partial[(size_t)b * NF + k];
+            f[k] = k == NF - 1 ? f[k] + v : max(f[k], v);
+        }
+    const int w = threadIdx.x / WAVE;
+    for (int k = 0; k < NF; ++k) {
+        unsigned long long v = f[k];
+        if (k == NF - 1) {
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        } else {
+            v = wmax64(v);
+        }
+        if (__lane_id() == 0) red[w][k] = v;
     }
     __syncthreads();
     if (threadIdx.x < NF) {
@@ -237,7 +266,6 @@ struct ElideOp {
         pm_w[i] = inc.pw;
         pm_c[i] = inc.pc;
         const uint32_t u = inc.hc - 1;
-        uidx[i] = u;
         if (el.head) {
             ukey[u] = (uint64_t)skey[i] + key_min;
             useg[u] = (uint32_t)i;

@@ -231,7 +231,12 @@ int stage_prepare(ad_handle* h) {
     hipStream_t st = h->st;
     k_params_init<<<1, 1, 0, st>>>(h->prm);
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
-    { KScope ks(K_MINMAX); k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_s, h->range_e, Q, h->prm); }
+    {
+        KScope ks(K_MINMAX);
+        unsigned long long* partial = (unsigned long long*)h->scratch;
+        k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_s, h->range_e, Q, partial);
+        k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm);
+    }
     CK(read_params(h));
     const Params& p = h->hprm;
     if (n == 0) return AD_OK;

@@ -47,9 +47,11 @@ constexpr uint32_t SHORT_SEG = 64;   // chains up to this length: one thread wal
 
 // Returns true if some short segment was newly queued for the next iteration (the caller reports it
 // once per wave, so the "work left" flag sees one store per wave, not one per push).
+// Fire-and-forget atomics: the caller already saw L[t] < x, so it re-queues t's other segments without
+// waiting for the atomics' round trips (a concurrent higher raise only makes the re-queue redundant; the
+// fixpoint still terminates because a segment whose inputs did not rise raises nothing).
 __device__ inline bool raise_level(uint32_t* L, uint32_t t, uint32_t x, int32_t own_seg, const PushCtx& c) {
-    const uint32_t old = atomicMax(&L[t], x);
-    if (old >= x) return false;
+    atomicMax(&L[t], x);
     bool queued = false;
     for (uint32_t p = c.key_off[t]; p < c.key_off[t + 1]; ++p) {
         const int32_t h = c.pair_seg[p];
@@ -60,7 +62,8 @@ __device__ inline bool raise_level(uint32_t* L, uint32_t t, uint32_t x, int32_t 
             if (*(volatile uint32_t*)c.long_dirty == 0u) *c.long_dirty = 1u;
             continue;
         }
-        if (atomicMax(&c.stamp[h], c.iter1) < c.iter1) queued = true;
+        atomicMax(&c.stamp[h], c.iter1);
+        queued = true;
     }
     return queued;
 }
@@ -82,9 +85,11 @@ struct ChainOp {
     int32_t* pm_all;              // inclusive prefix max level along the chain
     PushCtx push;
     uint32_t* work_left;          // some short segment is queued for the next iteration
+    const uint32_t* enable;       // previous iteration dirtied a long chain (nullptr: always run)
 
     __device__ S identity() const { return S{0, NEG, NEG, 0, NEG, NEG, 0, 0u}; }
     __device__ S load(size_t i) const {
+        if (enable && !*enable) return identity();
         const uint32_t pos = idx[i];
         const uint32_t m = c_meta[pos];
         const bool head = seg_start[pos] == (int32_t)pos;
@@ -122,6 +127,7 @@ struct ChainOp {
         return h;
     }
     __device__ void store(size_t i, const S& ex, const S&, const S& el) const {
+        if (enable && !*enable) return;
         const uint32_t pos = idx[i];
         int py, pw;
         if (el.flags & 1u) { py = -1; pw = -1; }
@@ -334,7 +340,8 @@ __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
 }
 
 // (b) + (c) relaxation, one thread per txn.
-__global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int do_c) {
+__global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int do_c, const uint32_t* prev) {
+    if (prev && !(prev[0] | prev[1] | prev[2])) return;     // nothing changed in the previous iteration
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool raised = false, queued = false;
     if (t < a.n) {
@@ -418,12 +425,13 @@ struct LevelState {
     uint32_t *sk0 = nullptr, *sv0 = nullptr, *sk1 = nullptr, *sv1 = nullptr;
     uint32_t* rs = nullptr;              // radix scratch
     size_t rs_cap = 0;
+    uint32_t* iflags = nullptr;          // per iteration of a launch batch: [long dirty, edge changed, work left, -]
     bool chains_ready = false;           // chain order / segment table valid for the current batch
     uint32_t nheads = 0, nlong = 0;
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -542,6 +550,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         ls.capK = c;
     }
     if (!ls.flags && !grow((void**)&ls.flags, 256)) goto oom;
+    if (!ls.iflags && !grow((void**)&ls.iflags, 4 * 64 * 4)) goto oom;
     {
         const size_t need = std::max(device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)),
                                      device_scan_scratch<SegListOp>(std::max<size_t>(P, 1))) + 256;
@@ -597,31 +606,55 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         const uint32_t nheads = ls.nheads, nlong = ls.nlong;
         bool short_work = nheads > 0, long_dirty = nlong > 0;
         ChainOp op{ls.long_pos, ls.c_txn, ls.c_meta, in.seg_start, in.lvl, ls.pm_all, push, ls.flags + 6};
-        for (int it = 0; it < (1 << 24); ++it) {
-            if (!short_work && !long_dirty && !(has_b || has_c)) break;
-            push.iter1 = (uint32_t)it + 1;
-            op.push = push;
-            ea.push = push;
-            hipMemsetAsync(ls.flags + 2, 0, 20, st);       // long dirty, edge changed, max level, kinds, work left
-            if (short_work) {
-                KScope ks(K_SCAN_CHAIN);
-                k_seg_short<<<ceil_div((long)nheads, 256), 256, 0, st>>>(ls.heads, nheads, (uint32_t)it, ls.c_txn, ls.c_meta, in.lvl,
-                                                                          ls.pm_all, push, ls.flags + 6);
+        // Iterations run in launch batches of up to ITB with no host sync inside a batch: every kernel of
+        // iteration k reads iteration k-1's flags on the device and exits at once when nothing changed.
+        constexpr int ITB = 8;
+        int it = 0;
+        bool any_work = short_work || long_dirty || has_b || has_c;
+        while (any_work && it < (1 << 24)) {
+            hipMemsetAsync(ls.iflags, 0, ITB * 4 * 4, st);
+            for (int k = 0; k < ITB; ++k) {
+                uint32_t* fl = ls.iflags + 4 * k;
+                const uint32_t* prev = k == 0 ? nullptr : ls.iflags + 4 * (k - 1);
+                push.iter1 = (uint32_t)(it + k) + 1;
+                push.long_dirty = fl + 0;
+                ea.push = push;
+                ea.changed = fl + 1;
+                ea.work_left = fl + 2;
+                if (short_work || k > 0) {
+                    KScope ks(K_SCAN_CHAIN);
+                    k_seg_short<<<ceil_div((long)std::max<uint32_t>(nheads, 1), 256), 256, 0, st>>>(
+                        ls.heads, nheads, (uint32_t)(it + k), ls.c_txn, ls.c_meta, in.lvl, ls.pm_all, push, fl + 2);
+                }
+                if (nlong > 0 && (long_dirty || k > 0)) {
+                    ChainOp opk = op;
+                    opk.push = push;
+                    opk.work_left = fl + 2;
+                    opk.enable = k == 0 ? nullptr : prev;   // prev[0] = long chains dirtied last iteration
+                    KScope ks(K_SCAN_CHAIN);
+                    device_scan(opk, nlong, (ChainOp::S*)ls.agg, st);
+                }
+                if ((has_b || has_c) && n > 0) {
+                    KScope ks(K_LEVEL_EDGES);
+                    k_level_edges<<<ceil_div((long)n, 256), 256, 0, st>>>(ea, has_b ? 1 : 0, has_c ? 1 : 0, prev);
+                }
             }
-            if (long_dirty) { KScope ks(K_SCAN_CHAIN); device_scan(op, nlong, (ChainOp::S*)ls.agg, st); }
-            if ((has_b || has_c) && n > 0) {
-                KScope ks(K_LEVEL_EDGES);
-                k_level_edges<<<ceil_div((long)n, 256), 256, 0, st>>>(ea, has_b ? 1 : 0, has_c ? 1 : 0);
-            }
-            if (hipMemcpyAsync(host + 2, ls.flags + 2, 20, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            uint32_t fh[ITB * 4];
+            if (hipMemcpyAsync(fh, ls.iflags, sizeof(fh), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {
                 err = "exec levels: device error";
                 return AD_ERR_DEVICE;
             }
-            *iters = it + 1;
-            long_dirty = host[2] != 0;
-            short_work = host[6] != 0;
-            if (!short_work && !long_dirty && host[3] == 0) break;
+            any_work = false;
+            for (int k = 0; k < ITB; ++k) {
+                const uint32_t* f = fh + 4 * k;
+                *iters = it + k + 1;
+                if (!(f[0] | f[1] | f[2])) { any_work = false; break; }
+                any_work = true;
+                long_dirty = f[0] != 0;
+                short_work = f[2] != 0;
+            }
+            it += ITB;
         }
     }
     if (want_order && n > 0) order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);

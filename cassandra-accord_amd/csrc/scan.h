@@ -58,18 +58,52 @@ __device__ inline typename Op::S block_exclusive_scan(const Op& op, typename Op:
     return op.combine(pre, ex_w);
 }
 
+// Wave-striped tiles: wave w of a block owns 64 * ITEMS consecutive elements; in round k lane l holds
+// element wbase + 64k + l, so every load/store instruction of a wave touches 64 consecutive elements
+// (coalesced).  Order is preserved: each round is an ordered 64-lane shuffle scan, rounds are folded in
+// order, waves in wave order (the ops are associative, not commutative).
+template <class Op>
+__device__ inline typename Op::S wave_incl_scan(const Op& op, typename Op::S x) {
+    const int lane = __lane_id();
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        typename Op::S y = shfl_up_state(x, o);
+        if (lane >= o) x = op.combine(y, x);
+    }
+    return x;
+}
+template <class S>
+__device__ inline S shfl_state(const S& v, int src) {
+    constexpr int W = sizeof(S) / 4;
+    S r;
+    const int* a = reinterpret_cast<const int*>(&v);
+    int* d = reinterpret_cast<int*>(&r);
+#pragma unroll
+    for (int k = 0; k < W; ++k) d[k] = __shfl(a[k], src);
+    return r;
+}
+
 template <class Op, int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename Op::S* agg) {
     using S = typename Op::S;
-    __shared__ S lds[BLOCK / WAVE];
-    const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
+    constexpr int NW = BLOCK / WAVE;
+    __shared__ S lds[NW];
+    const int lane = __lane_id(), w = threadIdx.x / WAVE;
+    const size_t wbase = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)w * WAVE * ITEMS;
     S acc = op.identity();
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k)
-        if (base + k < n) acc = op.combine(acc, op.load(base + k));
-    S total;
-    block_exclusive_scan<Op, BLOCK>(op, acc, lds, &total);
-    if (threadIdx.x == 0) agg[blockIdx.x] = total;
+    for (int k = 0; k < ITEMS; ++k) {
+        const size_t i = wbase + (size_t)k * WAVE + lane;
+        S x = wave_incl_scan(op, i < n ? op.load(i) : op.identity());
+        acc = op.combine(acc, shfl_state(x, WAVE - 1));
+    }
+    if (lane == 0) lds[w] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        S t = lds[0];
+        for (int k = 1; k < NW; ++k) t = op.combine(t, lds[k]);
+        agg[blockIdx.x] = t;
+    }
 }
 
 // Exclusive scan of nblk aggregates in place by one workgroup (chunks of BLOCK with a carry).
@@ -92,28 +126,35 @@ __global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, type
 template <class Op, int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_scan_apply(Op op, size_t n, const typename Op::S* agg) {
     using S = typename Op::S;
-    __shared__ S lds[BLOCK / WAVE];
-    const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
-    S el[ITEMS];
+    constexpr int NW = BLOCK / WAVE;
+    __shared__ S lds[NW];
+    const int lane = __lane_id(), w = threadIdx.x / WAVE;
+    const size_t wbase = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)w * WAVE * ITEMS;
+    S el[ITEMS], x[ITEMS];
     S acc = op.identity();
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        el[k] = base + k < n ? op.load(base + k) : op.identity();
-        acc = op.combine(acc, el[k]);
+        const size_t i = wbase + (size_t)k * WAVE + lane;
+        el[k] = i < n ? op.load(i) : op.identity();
+        x[k] = wave_incl_scan(op, el[k]);
+        acc = op.combine(acc, shfl_state(x[k], WAVE - 1));
     }
-    S ex = block_exclusive_scan<Op, BLOCK>(op, acc, lds, nullptr);
-    S run = op.combine(agg[blockIdx.x], ex);
+    if (lane == 0) lds[w] = acc;
+    __syncthreads();
+    S carry = agg[blockIdx.x];
+    for (int k = 0; k < w; ++k) carry = op.combine(carry, lds[k]);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        if (base + k < n) {
-            S inc = op.combine(run, el[k]);
-            op.store(base + k, run, inc, el[k]);
-            run = inc;
-        }
+        const size_t i = wbase + (size_t)k * WAVE + lane;
+        S prev = shfl_up_state(x[k], 1);
+        const S ex = lane == 0 ? carry : op.combine(carry, prev);
+        const S inc = op.combine(carry, x[k]);
+        if (i < n) op.store(i, ex, inc, el[k]);
+        carry = op.combine(carry, shfl_state(x[k], WAVE - 1));
     }
 }
 
-template <class Op, int BLOCK = 256, int ITEMS = 8>
+template <class Op, int BLOCK = 256, int ITEMS = 4>
 inline void device_scan(const Op& op, size_t n, typename Op::S* agg_scratch, hipStream_t st) {
     if (n == 0) return;
     const int nblk = ceil_div((long)n, (long)BLOCK * ITEMS);
@@ -121,7 +162,7 @@ inline void device_scan(const Op& op, size_t n, typename Op::S* agg_scratch, hip
     k_scan_aggregates<Op, 1024><<<1, 1024, 0, st>>>(op, nblk, agg_scratch);
     k_scan_apply<Op, BLOCK, ITEMS><<<nblk, BLOCK, 0, st>>>(op, n, agg_scratch);
 }
-template <class Op, int BLOCK = 256, int ITEMS = 8>
+template <class Op, int BLOCK = 256, int ITEMS = 4>
 inline size_t device_scan_scratch(size_t n) {
     return (size_t)ceil_div((long)n, (long)BLOCK * ITEMS) * sizeof(typename Op::S) + 64;
 }
