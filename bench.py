@@ -37,27 +37,24 @@ WINDOW, REPLICAS, DROP_P = 32, 3, 0.1
 KEYSPACE = 10_000_000
 
 
-def alg_bytes(kernel, n, P, R, st):
-    """Algorithmic HBM bytes of ONE launch of `kernel` (DESIGN.md §Roofline lists the per-unit figures).
-
-    n txns, P (txn,key) pairs, R replica views; st = ad_last_times() counts of the step."""
+def alg_bytes(kernel, calls, units, n, P, R, st):
+    """Algorithmic HBM bytes moved by all traced launches of `kernel` (DESIGN.md §3 lists the per-unit
+    figures): the minimum bytes the kernel must read + write for the elements it processed.  `units` is
+    the sum of elements over the launches (pairs, txns or sort items, recorded per launch by the engine's
+    tracer); n txns, P (txn,key) pairs, R replica views; st = ad_last_times() counts of the step.
+    Kernels whose work is data dependent in a way the tracer does not count (the level worklist walk,
+    composite scans) return None and are not roofline candidates."""
     D = st["deps_entries"]           # emitted dependency entries over all views/classes
-    M = st["merged_entries"]
     per = {
-        "k_minmax": n * 44 + P * 8,
-        "k_pack": n * 62 + P * 20,
-        "k_radix_hist": P * 4,
-        "k_radix_scatter": P * 16,
-        "k_gather_entries": P * 34,
-        "scan_elide": P * 37,
-        "k_deps_walk<count>": P * (37 + 8 * R),
-        "k_deps_walk<fill>": P * (37 + 16 * R) + 4 * D,
-        "k_txn_counts": n * 8 + P * (4 + 8 * R) + n * 16 * R,
-        "k_txn_union": 8 * D + 4 * D,
-        # per class launch: read the R replies (offsets 16 B/txn + entries 4 B + txn ranks 4 B), write merged
-        "k_merge<count>": (n * 16 * R + 8 * D / 2 + n * 12),
-        "k_merge<write>": (n * 16 * R + 8 * D / 2 + n * 16 + 8 * M / 2),
-        "scan_chain": P * 13 + n * 4,
+        "k_minmax": calls * (n * 44 + P * 8),                    # TxnId/executeAt SoA + key_off; keys
+        "k_pack": calls * (n * 62 + P * 20),                     # read 45 B/txn, write 17 B/txn; 8+12 B/pair
+        "k_radix_hist": units * 4,                               # read the key
+        "k_radix_scatter": units * 16,                           # read key+value, write key+value
+        "k_gather_entries": units * 34,                          # sval, pair_txn, meta, ex1 -> e_txn, e_meta, e_exec1, spos
+        "scan_elide": units * 37,                                # skey, e_meta, e_exec1 -> seg, ud, pm_w, pm_c
+        "k_deps_walk<count>": units * (33 + 8 * R),              # entry state + tx_ts; write 2R counts
+        "k_deps_walk<fill>": units * (33 + 16 * R) + 4 * D,      # + read counts/slots, write the entries
+        "k_txn_layout": units * (8 + 16 * R),                    # key + 2R counts in, 2R slots out
     }
     return per.get(kernel)
 
@@ -91,33 +88,35 @@ def cpu_baseline(sample_n):
                       % (sample_n, REPLICAS, t, s["t_deps"], s["t_merge"], s["t_levels"])}
 
 
-def trace_roofline(eng, run_step, n, P, steps):
-    """Untimed all-kernels breakdown -> dominant kernel; then `steps` timed steps with only that kernel
-    event-timed on the engine stream.  Returns (wall seconds, roofline dict, breakdown, last times)."""
+def trace_roofline(eng, run_step, n, P):
+    """Untimed all-kernels breakdown pass -> the dominant kernel among those with an algorithmic byte
+    model.  Returns (dominant kernel, breakdown, last times)."""
     ids = engine.kernel_ids()
     eng.set_trace((1 << len(ids)) - 1)
     eng.reset_kernel_stats()
     run_step()
     brk = eng.kernel_stats()
     st = eng.last_times()
-    dom = max((k for k in brk if alg_bytes(k, n, P, REPLICAS, st) is not None), key=lambda k: brk[k][1])
+    cands = [k for k in brk if alg_bytes(k, brk[k][0], brk[k][2], n, P, REPLICAS, st) is not None]
+    dom = max(cands, key=lambda k: brk[k][1])
     return dom, brk, st
 
 
 def roofline_of(eng, dom, n, P, st):
-    kst = eng.kernel_stats()[dom]
-    avg_ms = kst[1] / kst[0]
-    ab = alg_bytes(dom, n, P, REPLICAS, st)
-    achieved = ab / (avg_ms * 1e-3) / 1e9
+    """achieved = the dominant kernel's algorithmic bytes over its launches in the timed region / its summed
+    HIP-event time (events on the engine stream, bracketing only this kernel)."""
+    calls, ms, units = eng.kernel_stats()[dom]
+    ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st)
+    achieved = ab / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": ab,
-            "avg_launch_ms": avg_ms, "launches": kst[0]}
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": ab / calls,
+            "avg_launch_ms": ms / calls, "launches": calls}
 
 
 def print_breakdown(brk, st):
     tot = sum(v[1] for v in brk.values())
-    for k, (c, ms) in sorted(brk.items(), key=lambda kv: -kv[1][1]):
-        print("  %-22s %5d launches %9.3f ms  %5.1f%%" % (k, c, ms, 100 * ms / tot), file=sys.stderr)
+    for k, (c, ms, u) in sorted(brk.items(), key=lambda kv: -kv[1][1]):
+        print("  %-22s %5d launches %9.3f ms  %5.1f%%  %12d units" % (k, c, ms, 100 * ms / tot, u), file=sys.stderr)
     print("  stages: %s" % {k: round(v, 3) if isinstance(v, float) else v for k, v in st.items()}, file=sys.stderr)
 
 
@@ -155,7 +154,7 @@ def main_sharded(args, rank, world, local, dist):
     for _ in range(max(args.warmup, 1)):
         rounds = step()
     n_loc, P_loc = lb["n"], int(lb["key_off"][-1])
-    dom, brk, st = trace_roofline(store.eng, step, n_loc, P_loc, args.steps)
+    dom, brk, st = trace_roofline(store.eng, step, n_loc, P_loc)
     if args.breakdown and rank == 0:
         print_breakdown(brk, st)
     store.eng.set_trace(1 << engine.kernel_ids()[dom])
@@ -204,7 +203,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
     if world > 1:
         import torch.distributed as tdist
         tdist.init_process_group("gloo")
@@ -214,76 +212,43 @@ def main():
             tdist.destroy_process_group()
         return
 
-    def barrier():
-        if dist:
-            dist.barrier()
-
-    def max_over_ranks(x):
-        if not dist:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    # this rank's CommandStore: a disjoint key range, its own seeded batch
-    batch = workload.generate(args.n, 4, KEYSPACE, "uniform", seed=workload.SEEDS["C2"] + rank)
-    batch["keys"] = batch["keys"] + np.uint64(rank * KEYSPACE)
+    batch = workload.config("C2", n=args.n)
     n, P = batch["n"], int(batch["key_off"][-1])
-
     eng = engine.DepsEngine(device=local, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C2"])
     eng.load(batch)                                   # host -> HBM once; the timed region starts resident
-    ids = engine.kernel_ids()
 
     for _ in range(max(args.warmup, 1)):
         eng.run_pipeline()
-    # untimed breakdown pass: every kernel traced -> the dominant kernel
-    eng.set_trace((1 << len(ids)) - 1)
-    eng.reset_kernel_stats()
-    eng.run_pipeline()
-    brk = eng.kernel_stats()
-    st = eng.last_times()
-    dom = max((k for k in brk if alg_bytes(k, n, P, REPLICAS, st) is not None), key=lambda k: brk[k][1])
-    if args.breakdown and rank == 0:
-        tot = sum(v[1] for v in brk.values())
-        for k, (c, ms) in sorted(brk.items(), key=lambda kv: -kv[1][1]):
-            print("  %-22s %5d launches %9.3f ms  %5.1f%%" % (k, c, ms, 100 * ms / tot), file=sys.stderr)
-        print("  stages: %s" % {k: round(v, 3) if isinstance(v, float) else v for k, v in st.items()}, file=sys.stderr)
+    dom, brk, st = trace_roofline(eng, eng.run_pipeline, n, P)
+    if args.breakdown:
+        print_breakdown(brk, st)
 
     # timed region: only the dominant kernel is event-timed (on the engine's stream)
-    eng.set_trace(1 << ids[dom])
+    eng.set_trace(1 << engine.kernel_ids()[dom])
     eng.reset_kernel_stats()
-    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.run_pipeline()                             # ends with an event sync on the engine stream
     t1 = time.perf_counter()
-    barrier()
-    dt = max_over_ranks(t1 - t0)
-    kst = eng.kernel_stats()[dom]
+    dt = t1 - t0
     st = eng.last_times()
+    roof = roofline_of(eng, dom, n, P, st)
     eng.set_trace(0)
-
-    avg_ms = kst[1] / kst[0]
-    ab = alg_bytes(dom, n, P, REPLICAS, st)
-    achieved = ab / (avg_ms * 1e-3) / 1e9
     ms_per_step = dt * 1e3 / args.steps
-    value = world * n * args.steps / dt
+    value = n * args.steps / dt
     pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st) / (dt / args.steps) / 1e9
 
     out = {
         "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
-        "value": value, "unit": "txn/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": value, "unit": "txn/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C2 generator, BASELINE configs[1])",
-        "config": {"workload": "C2: %d txns x 4 keys uniform over 10M keys per GPU; PreAccept deps under R=%d "
+        "config": {"workload": "C2: %d txns x 4 keys uniform over 10M keys; PreAccept deps under R=%d "
                                "replica views (in-flight window W=%d, drop p=%.1f) + Deps.merge + exec levels/order"
                                % (n, REPLICAS, WINDOW, DROP_P),
                    "txns_per_gpu": n, "keys_per_txn": 4, "keyspace": KEYSPACE, "replicas": REPLICAS,
-                   "window": WINDOW, "parallelism": "key-range shard per GPU (%d)" % world},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": ab,
-                     "avg_launch_ms": avg_ms, "launches": kst[0]},
+                   "window": WINDOW, "parallelism": "single CommandStore on 1 GPU"},
+        "roofline": roof,
         "pipeline": {"alg_bytes": pipeline_alg_bytes(n, P, REPLICAS, st), "alg_GBps": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS,
                      "stage_ms": {k: st[k] for k in ("prepare", "sort", "deps", "merge", "levels", "total")},
@@ -295,10 +260,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     eng.close()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -63,6 +63,7 @@ def lib():
         L.ad_kernel_name.restype = C.c_char_p
         L.ad_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
         L.ad_reset_kernel_stats.argtypes = [vp]
+        L.ad_kernel_units.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64)]
         L.ad_shard_bounds.argtypes = [C.POINTER(C.c_uint64), C.c_size_t, C.c_uint32, C.POINTER(C.c_uint64)]
         _LIB = L
     return _LIB
@@ -70,7 +71,7 @@ def lib():
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
             "ad_fetch_deps", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
-            "ad_run_pipeline", "ad_last_times", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats",
+            "ad_run_pipeline", "ad_last_times", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_blob_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_allgather", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
@@ -185,13 +186,14 @@ class DepsEngine:
         self._check(lib().ad_reset_kernel_stats(self.h), "ad_reset_kernel_stats")
 
     def kernel_stats(self):
-        """{kernel name: (launches, total ms)} for every traced kernel with at least one launch."""
+        """{kernel name: (launches, total ms, elements processed)} for every traced kernel with a launch."""
         out = {}
         for k in range(lib().ad_kernel_count()):
-            name, calls, ms = C.c_char_p(), C.c_uint64(), C.c_double()
+            name, calls, ms, units = C.c_char_p(), C.c_uint64(), C.c_double(), C.c_uint64()
             self._check(lib().ad_kernel_stats(self.h, k, C.byref(name), C.byref(calls), C.byref(ms)), "ad_kernel_stats")
+            self._check(lib().ad_kernel_units(self.h, k, C.byref(units)), "ad_kernel_units")
             if calls.value:
-                out[name.value.decode()] = (calls.value, ms.value)
+                out[name.value.decode()] = (calls.value, ms.value, units.value)
         return out
 
 

@@ -232,7 +232,7 @@ int stage_prepare(ad_handle* h) {
     k_params_init<<<1, 1, 0, st>>>(h->prm);
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
-        KScope ks(K_MINMAX);
+        KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
         k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_s, h->range_e, Q, partial);
         k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm);
@@ -256,7 +256,7 @@ int stage_prepare(ad_handle* h) {
     h->wmax = Q ? p.rw_max : 0;
     h->range_bits = Q ? bits_of(p.re_max - p.rs_min) : 0;
     if (h->range_bits > 32) return set_err(h, AD_ERR_UNSUPPORTED, "range spread exceeds 32 bits");
-    KScope ks(K_PACK);
+    KScope ks(K_PACK, n);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
                                                     h->range_e, h->tx_ts, h->ex1, h->meta, h->pair_txn, h->ka, h->va, h->prm);
@@ -301,7 +301,7 @@ template <int NV>
 void launch_walk(const WalkArgs& a, bool fill, hipStream_t st) {
     if (a.P > 0) {
         const int g = ceil_div((long)a.P, 256);
-        KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT);
+        KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT, a.P);
         if (fill) k_deps_walk<NV, true><<<g, 256, 0, st>>>(a);
         else k_deps_walk<NV, false><<<g, 256, 0, st>>>(a);
     }
@@ -350,11 +350,11 @@ int stage_deps(ad_handle* h) {
     for (int vc = 0; vc < nvc; ++vc) CK(alloc_csr(h, vc, h->deps[vc], n));
     for (int v = 0; v < nv; ++v) CK(alloc_csr(h, CSR_RANGE0 + v, h->rdeps[v], n));
     if (P > 0) {
-        { KScope ks(K_GATHER); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->pair_txn, h->meta, h->ex1, h->e_txn, h->e_meta,
+        { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->pair_txn, h->meta, h->ex1, h->e_txn, h->e_meta,
                                                                                           h->e_exec1, h->spos); }
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
                     h->uidx, h->ukey, h->useg, h->hprm.key_min, P, h->prm};
-        KScope ks(K_SCAN_ELIDE);
+        KScope ks(K_SCAN_ELIDE, P);
         device_scan(eop, P, (ElideOp::S*)h->scratch, st);
     }
     // ---- virtual items of large txns
@@ -391,7 +391,7 @@ int stage_deps(ad_handle* h) {
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
     if (n > 0) {
-        KScope ks(K_SCAN_OFFSETS);
+        KScope ks(K_SCAN_OFFSETS, n);
         NV_DISPATCH(nv, launch_offsets, h, ta);
     } else {
         for (int vc = 0; vc < nvc; ++vc) csr_offsets(h, h->deps[vc], h->nk, h->ne);
@@ -434,7 +434,7 @@ int stage_deps(ad_handle* h) {
         }
     }
     // ---- fill
-    if (n > 0) { KScope ks(K_TXN_LAYOUT); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
+    if (n > 0) { KScope ks(K_TXN_LAYOUT, P); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
     NV_DISPATCH(nv, launch_walk, wa, true, st);
     if (Q > 0 && n > 0) NV_DISPATCH(nv, launch_range, ra, true, st);
     UnionArgs ua{};
@@ -444,7 +444,7 @@ int stage_deps(ad_handle* h) {
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    if (n > 0) { KScope ks(K_TXN_UNION); k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua); }
+    if (n > 0) { KScope ks(K_TXN_UNION, n); k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua); }
     // large txns' key CSRs and every RangeDeps CSR: LDS sort union
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
         KScope ks(K_UNION_LDS);
@@ -979,6 +979,15 @@ int ad_kernel_stats(ad_handle* h, int kid, const char** name, uint64_t* calls, d
     if (name) *name = kernel_name(kid);
     if (calls) *calls = h->tracer.calls[kid];
     if (total_ms) *total_ms = h->tracer.total_ms[kid];
+    return AD_OK;
+}
+
+int ad_kernel_units(ad_handle* h, int kid, uint64_t* units) {
+    if (!h || !units || kid < 0 || kid >= K_COUNT) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->tracer.resolve();
+    *units = h->tracer.units[kid];
     return AD_OK;
 }
 

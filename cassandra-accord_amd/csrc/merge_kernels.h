@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_tcnt_from_off(size_t n, const uint32_t*
 template <int NV>
 inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t st) {
     const int g = ceil_div((long)a.n, 256);
-    KScope ks(write ? K_MERGE_WRITE : K_MERGE_COUNT);
+    KScope ks(write ? K_MERGE_WRITE : K_MERGE_COUNT, a.n);
     if (kw == 2) {
         if (write) k_merge<NV, true, 2><<<g, 256, 0, st>>>(a);
         else k_merge<NV, false, 2><<<g, 256, 0, st>>>(a);

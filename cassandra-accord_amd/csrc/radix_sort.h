@@ -126,9 +126,9 @@ inline bool radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t*
         const uint32_t* vi = flip ? v1 : v0;
         uint32_t* ko = flip ? k0 : k1;
         uint32_t* vo = flip ? v0 : v1;
-        { KScope ks(K_RADIX_HIST); k_radix_hist<<<ntiles, RS_BLOCK, 0, st>>>(ki, n, shift, ntiles, s.hist); }
-        { KScope ks(K_SCAN_RADIX); device_scan(SumOp<uint32_t>{s.hist, s.offs, hl}, hl, s.agg, st); }
-        { KScope ks(K_RADIX_SCATTER); k_radix_scatter<<<ntiles, RS_BLOCK, 0, st>>>(ki, vi, ko, vo, n, shift, ntiles, s.offs); }
+        { KScope ks(K_RADIX_HIST, n); k_radix_hist<<<ntiles, RS_BLOCK, 0, st>>>(ki, n, shift, ntiles, s.hist); }
+        { KScope ks(K_SCAN_RADIX, hl); device_scan(SumOp<uint32_t>{s.hist, s.offs, hl}, hl, s.agg, st); }
+        { KScope ks(K_RADIX_SCATTER, n); k_radix_scatter<<<ntiles, RS_BLOCK, 0, st>>>(ki, vi, ko, vo, n, shift, ntiles, s.offs); }
         flip = !flip;
     }
     return flip;

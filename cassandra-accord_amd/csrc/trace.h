@@ -30,12 +30,13 @@ inline const char* kernel_name(int k) {
 struct Tracer {
     hipStream_t st = nullptr;
     uint64_t mask = 0;
-    struct Rec { int kid; hipEvent_t a, b; };
+    struct Rec { int kid; hipEvent_t a, b; uint64_t units; };
     std::vector<hipEvent_t> pool;
     size_t used = 0;
     std::vector<Rec> recs;
     double total_ms[K_COUNT] = {};
     uint64_t calls[K_COUNT] = {};
+    uint64_t units[K_COUNT] = {};      // elements processed (the kernel's algorithmic unit), summed
 
     hipEvent_t get() {
         if (used == pool.size()) {
@@ -46,7 +47,7 @@ struct Tracer {
         return pool[used++];
     }
     void reset_counts() {
-        for (int k = 0; k < K_COUNT; ++k) { total_ms[k] = 0; calls[k] = 0; }
+        for (int k = 0; k < K_COUNT; ++k) { total_ms[k] = 0; calls[k] = 0; units[k] = 0; }
     }
     // After the stream has been synchronised: fold the recorded pairs into the totals.
     void resolve() {
@@ -55,6 +56,7 @@ struct Tracer {
             if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
                 total_ms[r.kid] += ms;
                 calls[r.kid] += 1;
+                units[r.kid] += r.units;
             }
         }
         recs.clear();
@@ -71,12 +73,12 @@ struct KScope {
     Tracer* t;
     int kid;
     hipEvent_t b = nullptr;
-    explicit KScope(int k) : t(g_tracer), kid(k) {
+    explicit KScope(int k, uint64_t units = 0) : t(g_tracer), kid(k) {
         if (t && (t->mask >> k & 1ull)) {
             hipEvent_t a = t->get();
             b = t->get();
             hipEventRecord(a, t->st);
-            t->recs.push_back(Tracer::Rec{k, a, b});
+            t->recs.push_back(Tracer::Rec{k, a, b, units});
         } else {
             t = nullptr;
         }

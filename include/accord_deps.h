@@ -211,6 +211,8 @@ int  ad_kernel_count(void);
 const char* ad_kernel_name(int kid);
 int  ad_kernel_stats(ad_handle* h, int kid, const char** name, uint64_t* calls, double* total_ms);
 int  ad_reset_kernel_stats(ad_handle* h);
+/* elements the traced launches of kernel kid processed (its algorithmic unit: pairs, txns, sort items) */
+int  ad_kernel_units(ad_handle* h, int kid, uint64_t* units);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU key-range sharding (one handle = one CommandStore = one GPU).                     */
