@@ -54,11 +54,9 @@ __device__ inline bool raise_level(uint32_t* L, uint32_t t, uint32_t x, int32_t 
     atomicMax(&L[t], x);
     bool queued = false;
     for (uint32_t p = c.key_off[t]; p < c.key_off[t + 1]; ++p) {
-        const int32_t h = c.pair_seg[p];
-        if (h == own_seg) continue;
-        const uint32_t len = c.seg_len[h];
-        if (len < 2) continue;
-        if (len > SHORT_SEG) {
+        const int32_t h = c.pair_seg[p];          // push target: short chain head, -1 singleton, -2 long chain
+        if (h == own_seg || h == -1) continue;
+        if (h == -2) {
             if (*(volatile uint32_t*)c.long_dirty == 0u) *c.long_dirty = 1u;
             continue;
         }
@@ -218,11 +216,15 @@ __global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict_
     if (i < count) stamp[heads[i]] = 0u;
 }
 
-// txn pair -> head position of its segment
+// txn pair -> push target: head position of its chain if that chain is short and has 2+ entries,
+// -1 for a single-entry chain (nothing to re-walk), -2 for a long chain (rescanned by the segmented scan)
 __global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ spos, const int32_t* __restrict__ seg_start,
-                                                  int32_t* __restrict__ pair_seg) {
+                                                  const uint32_t* __restrict__ seg_len, int32_t* __restrict__ pair_seg) {
     const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < P) pair_seg[p] = seg_start[spos[p]];
+    if (p >= P) return;
+    const int32_t h = seg_start[spos[p]];
+    const uint32_t len = seg_len[h];
+    pair_seg[p] = len < 2 ? -1 : (len > SHORT_SEG ? -2 : h);
 }
 
 __global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
@@ -423,6 +425,7 @@ struct LevelState {
     void* agg = nullptr;
     size_t agg_cap = 0;
     uint32_t *sk0 = nullptr, *sv0 = nullptr, *sk1 = nullptr, *sv1 = nullptr;
+    uint64_t* key64 = nullptr;           // executeAt keys of the order fast path
     uint32_t* rs = nullptr;              // radix scratch
     size_t rs_cap = 0;
     uint32_t* iflags = nullptr;          // per iteration of a launch batch: [long dirty, edge changed, work left, -]
@@ -431,7 +434,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -492,29 +495,86 @@ __global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_
     key[i] = hi ? (uint32_t)(e >> 32) : (uint32_t)e;
 }
 
+// Near-sorted fast path for the executeAt order: executeAt == TxnId on the fast path and a slow-path
+// bump moves a txn only a few ranks, so the rank order is executeAt order up to bounded displacement.
+// Two rounds of LDS block sorts (windows of BS_N, the second shifted by BS_N/2) sort any sequence whose
+// displacement is below BS_N/2; a check kernel verifies global order (else: full LSD radix fallback).
+constexpr int BS_N = 1024, BS_T = 256;
+__global__ __launch_bounds__(256) void k_exec_init(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
+                                                   uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    key[i] = ex1[rows ? rows[i] : i];
+    idx[i] = (uint32_t)i;
+}
+__global__ __launch_bounds__(BS_T) void k_block_sort64(size_t m, size_t off, uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
+    __shared__ uint64_t sk[BS_N];
+    __shared__ uint32_t si[BS_N];
+    const size_t base = off + (size_t)blockIdx.x * BS_N;
+    if (base >= m) return;
+    const uint32_t cnt = (uint32_t)((m - base) < (size_t)BS_N ? (m - base) : (size_t)BS_N);
+    for (uint32_t x = threadIdx.x; x < BS_N; x += BS_T) {
+        sk[x] = x < cnt ? key[base + x] : ~0ull;
+        si[x] = x < cnt ? idx[base + x] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= (uint32_t)BS_N; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t x = threadIdx.x; x < (uint32_t)BS_N; x += BS_T) {
+                const uint32_t y = x ^ j;
+                if (y > x) {
+                    const uint64_t a = sk[x], b = sk[y];
+                    const uint32_t ia = si[x], ib = si[y];
+                    const bool gt = a > b || (a == b && ia > ib);      // (executeAt, rank): stable
+                    if (gt == ((x & k) == 0)) { sk[x] = b; sk[y] = a; si[x] = ib; si[y] = ia; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t x = threadIdx.x; x < cnt; x += BS_T) { key[base + x] = sk[x]; idx[base + x] = si[x]; }
+}
+// flags[0] |= unsorted; flags[1] = max level (of the txns in idx order)
+__global__ __launch_bounds__(256) void k_check_exec_order(size_t m, const uint64_t* __restrict__ key, uint32_t* __restrict__ flags) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool bad = i + 1 < m && key[i] > key[i + 1];
+    if (__ballot(bad) && __lane_id() == 0) atomicOr(flags, 1u);
+}
+
 inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
                        uint32_t exec_bits, uint32_t* order_out, hipStream_t st) {
-    KScope ks(K_ORDER);
+    KScope ks(K_ORDER, m);
     RadixScratch rs;
     const size_t hl = radix_hist_len(m);
     rs.hist = ls.rs;
     rs.offs = rs.hist + hl + 64;
     rs.agg = rs.offs + hl + 64;
     const int g = ceil_div((long)m, 256);
-    const int eb = (int)exec_bits;
-    k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, nullptr, ls.sk0, 0);
-    k_iota<<<g, 256, 0, st>>>(m, ls.sv0);
     uint32_t *k = ls.sk0, *v = ls.sv0, *ko = ls.sk1, *vo = ls.sv1;
-    if (radix_sort_pairs(k, v, ko, vo, m, eb < 32 ? eb : 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
-    if (eb > 32) {
-        k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, v, k, 1);
-        if (radix_sort_pairs(k, v, ko, vo, m, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
-    }
-    hipMemsetAsync(ls.flags + 4, 0, 4, st);
+    // fast path: bounded-displacement block sorts + verification (one host sync: sortedness + max level)
+    k_exec_init<<<g, 256, 0, st>>>(m, ex1, rows, ls.key64, v);
+    k_block_sort64<<<ceil_div((long)m, BS_N), BS_T, 0, st>>>(m, 0, ls.key64, v);
+    if (m > (size_t)BS_N / 2)
+        k_block_sort64<<<ceil_div((long)(m - BS_N / 2), BS_N), BS_T, 0, st>>>(m, BS_N / 2, ls.key64, v);
+    hipMemsetAsync(ls.flags + 4, 0, 8, st);
+    k_check_exec_order<<<g, 256, 0, st>>>(m, ls.key64, ls.flags + 5);
     k_gather_level_rows<<<g, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
-    uint32_t maxl = 0;
-    hipMemcpyAsync(&maxl, ls.flags + 4, 4, hipMemcpyDeviceToHost, st);
+    uint32_t fl[2] = {0, 0};
+    hipMemcpyAsync(fl, ls.flags + 4, 8, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
+    if (fl[1]) {
+        // general executeAt distribution: LSD radix sort by executeAt (two 32-bit halves)
+        const int eb = (int)exec_bits;
+        k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, nullptr, k, 0);
+        k_iota<<<g, 256, 0, st>>>(m, v);
+        if (radix_sort_pairs(k, v, ko, vo, m, eb < 32 ? eb : 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
+        if (eb > 32) {
+            k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, v, k, 1);
+            if (radix_sort_pairs(k, v, ko, vo, m, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
+        }
+        k_gather_level_rows<<<g, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
+    }
+    const uint32_t maxl = fl[0];
     const int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
     if (radix_sort_pairs(k, v, ko, vo, m, lb, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
     hipMemcpyAsync(order_out, v, m * 4, hipMemcpyDeviceToDevice, st);
@@ -540,7 +600,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     if (ls.capN < n || !ls.sk0) {
         size_t c = std::max<size_t>(n, 1);
         if (!grow((void**)&ls.sk0, c * 4) || !grow((void**)&ls.sv0, c * 4) || !grow((void**)&ls.sk1, c * 4) ||
-            !grow((void**)&ls.sv1, c * 4))
+            !grow((void**)&ls.sv1, c * 4) || !grow((void**)&ls.key64, c * 8))
             goto oom;
         ls.capN = c;
     }
@@ -592,7 +652,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
             k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
             k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp);
-            k_pair_seg<<<gP, 256, 0, st>>>(P, in.spos, in.seg_start, ls.pair_seg);
+            k_pair_seg<<<gP, 256, 0, st>>>(P, in.spos, in.seg_start, ls.seg_len, ls.pair_seg);
             device_scan(SegListOp{in.seg_start, ls.seg_len, ls.heads, ls.long_pos, ls.flags, P}, P, (SegListOp::S*)ls.agg, st);
             if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);
         }

@@ -53,16 +53,24 @@ __device__ inline uint64_t match_digit(uint32_t d, bool valid) {
     return m;
 }
 
+// LDS-staged scatter: every item's position inside the tile sorted by digit is computed from the
+// per-wave ballot ranks, the tile's (key, value) pairs are written to LDS in that order, and then read
+// back sequentially: consecutive threads write consecutive global slots of one digit's run, so the global
+// stores are coalesced bursts instead of 4-byte scatters (measured: 3.6x write amplification before).
 __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             size_t n, int shift, int ntiles,
                                                             const uint32_t* __restrict__ offs) {
     __shared__ uint32_t cnt[RS_WAVES][256];
+    __shared__ uint32_t gbase[256];          // global slot of the tile's first item of digit d, minus its tile slot
+    __shared__ uint32_t wsum[RS_WAVES];
+    __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
     const int w = threadIdx.x / WAVE;
     const int lane = threadIdx.x % WAVE;
     for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_BLOCK) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    const size_t wbase = (size_t)blockIdx.x * RS_TILE + (size_t)w * (RS_ROUNDS * WAVE);
+    const size_t tbase = (size_t)blockIdx.x * RS_TILE;
+    const size_t wbase = tbase + (size_t)w * (RS_ROUNDS * WAVE);
     uint32_t k[RS_ROUNDS], v[RS_ROUNDS];
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
@@ -81,9 +89,24 @@ __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __re
         if (valid && (m & below) == 0) cnt[w][d] += (uint32_t)__popcll(m);
     }
     __syncthreads();
-    // per digit: global tile offset + counts of earlier waves
-    for (int d = threadIdx.x; d < 256; d += RS_BLOCK) {
-        uint32_t run = offs[(size_t)d * ntiles + blockIdx.x];
+    // tile slot bases: exclusive scan over digits of the tile's digit totals (thread d owns digit d)
+    {
+        const int d = threadIdx.x;      // RS_BLOCK == 256
+        uint32_t tot = 0;
+#pragma unroll
+        for (int x = 0; x < RS_WAVES; ++x) tot += cnt[x][d];
+        uint32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == WAVE - 1) wsum[w] = incl;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int x = 0; x < w; ++x) pre += wsum[x];
+        uint32_t run = pre + incl - tot;          // tile slot of digit d's first item
+        gbase[d] = offs[(size_t)d * ntiles + blockIdx.x] - run;
 #pragma unroll
         for (int x = 0; x < RS_WAVES; ++x) {
             uint32_t c = cnt[x][d];
@@ -92,7 +115,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __re
         }
     }
     __syncthreads();
-    // pass B: scatter
+    // pass B: stage in LDS in tile-sorted order
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
         size_t i = wbase + (size_t)r * WAVE + lane;
@@ -100,8 +123,17 @@ __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __re
         uint32_t d = (k[r] >> shift) & 0xFF;
         uint64_t m = match_digit(d, valid);
         uint32_t pos = cnt[w][d] + (uint32_t)__popcll(m & below);
-        if (valid) { kout[pos] = k[r]; vout[pos] = v[r]; }
+        if (valid) { sk[pos] = k[r]; sv[pos] = v[r]; }
         if (valid && (m & below) == 0) cnt[w][d] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    // pass C: sequential read-out, coalesced runs per digit
+    const uint32_t tn = (uint32_t)((n - tbase) < (size_t)RS_TILE ? (n - tbase) : (size_t)RS_TILE);
+    for (uint32_t x = threadIdx.x; x < tn; x += RS_BLOCK) {
+        const uint32_t key = sk[x];
+        const uint32_t pos = gbase[(key >> shift) & 0xFF] + x;
+        kout[pos] = key;
+        vout[pos] = sv[x];
     }
 }
 
