@@ -108,9 +108,42 @@ def roofline_of(eng, dom, n, P, st):
     calls, ms, units = eng.kernel_stats()[dom]
     ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st)
     achieved = ab / (ms * 1e-3) / 1e9
+    traffic, src = pmc_traffic(dom)
     return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": ab / calls,
-            "avg_launch_ms": ms / calls, "launches": calls}
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+            "alg_bytes_per_launch": ab / calls, "avg_launch_ms": ms / calls, "launches": calls}
+
+
+ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol (profiles/*_pmc.json keys)
+    "k_deps_walk<fill>": "ad::k_deps_walk<3, true>", "k_deps_walk<count>": "ad::k_deps_walk<3, false>",
+    "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
+    "k_gather_entries": "ad::k_gather_entries", "k_txn_layout": "ad::k_txn_layout",
+    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack",
+}
+
+
+def pmc_traffic(kernel):
+    """HBM-side bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
+    written by profiles/collect.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3 passes of this bench).
+    The largest-grid dispatch of the kernel is the batch-sized one.  FETCH_SIZE is reported as counted
+    (Infinity-Cache hits included; 4-byte accesses, so the guide's 2x wide-stream correction does not
+    apply — the file carries a 4-byte streaming calibration measured on k_radix_hist).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    want = ROCPROF_NAME.get(kernel)
+    if not files or not want:
+        return None, None
+    with open(files[-1]) as f:
+        doc = json.load(f)
+    best = None
+    for k, e in doc.get("kernels", {}).items():
+        name, grid = k.rsplit(" grid=", 1)
+        if name == want and "FETCH_SIZE_KB_mean" in e and "WRITE_SIZE_KB_mean" in e:
+            if best is None or int(grid) > best[0]:
+                best = (int(grid), (e["FETCH_SIZE_KB_mean"] + e["WRITE_SIZE_KB_mean"]) * 1024.0)
+    if best is None:
+        return None, None
+    return best[1], os.path.relpath(files[-1], ROOT)
 
 
 def print_breakdown(brk, st):

@@ -294,7 +294,7 @@ struct WalkArgs {
     uint64_t seed;
     const uint32_t* sval;     // sorted position -> pair index p
     uint32_t* cnt;            // real pairs, AoS by pair: [p * 2NV + vc], vc = view * 2 + class
-    const uint32_t* dst;      // real pairs, AoS by pair: absolute k2t slot of the first entry (fill)
+    const uint32_t* dst;      // real pairs, AoS by pair: absolute k2t slot of the last entry (fill)
     int32_t* k2t[NVC_MAX];    // per-vc keysToTxnIds (fill)
     // virtual items (large txns): item x queries key segment [vi_seg0[x], ...) before position vi_pos[x]
     size_t V;
@@ -388,8 +388,8 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         if (FILL) {
-            c0[v] = a.dst[pb + 2 * v] + a.cnt[pb + 2 * v] - 1;
-            c1[v] = a.dst[pb + 2 * v + 1] + a.cnt[pb + 2 * v + 1] - 1;
+            c0[v] = a.dst[pb + 2 * v];          // last slot of the pair's run (filled descending)
+            c1[v] = a.dst[pb + 2 * v + 1];
         } else {
             c0[v] = 0; c1[v] = 0;
         }
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
     uint32_t c[2 * NV];
 #pragma unroll
     for (int vc = 0; vc < 2 * NV; ++vc)
-        c[vc] = FILL ? a.vdst[x * (2 * NV) + vc] + a.vcnt[x * (2 * NV) + vc] - 1 : 0u;
+        c[vc] = FILL ? a.vdst[x * (2 * NV) + vc] : 0u;
     auto emit = [&](int v, bool direct, uint32_t j) {
         const int vc = 2 * v + (direct ? 1 : 0);
         if (FILL) a.k2t[vc][c[vc]--] = (int32_t)j;
@@ -509,8 +509,9 @@ __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
             else c = a.cnt[(size_t)x * a.nvc + vc];
             if (c == 0) continue;
             a.out_keys[vc][kb + kk] = large ? a.vi_key[x] : a.keys[x];
-            if (large) a.vdst[(size_t)x * a.nvc + vc] = mb + run;
-            else a.dst[(size_t)x * a.nvc + vc] = mb + run;
+            // the fill walk emits descending from the run's last slot
+            if (large) a.vdst[(size_t)x * a.nvc + vc] = mb + run + c - 1;
+            else a.dst[(size_t)x * a.nvc + vc] = mb + run + c - 1;
             run += c;
             a.out_k2t[vc][mb + kk] = (int32_t)run;
             ++kk;

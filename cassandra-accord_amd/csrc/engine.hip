@@ -54,6 +54,7 @@ struct ad_handle {
     // derived
     Params* prm = nullptr;
     Params hprm{};
+    uint32_t* totd = nullptr;          // device: gathered CSR totals (read_totals_params)
     TsPack pack{};
     int key_bits = 0, range_bits = 0;
     uint64_t rbase = 0, wmax = 0;
@@ -156,7 +157,7 @@ enum Slot : size_t {
     S_PMW, S_PMC, S_SEG, S_UD, S_CNT, S_DST, S_NK, S_NE, S_SCRATCH,
     S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
-    S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS,
+    S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -212,6 +213,22 @@ int read_params(ad_handle* h) {
     HIPCHK(h, hipMemcpyAsync(&h->hprm, h->prm, sizeof(Params), hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return AD_OK;
+}
+
+// The [n] totals of several device offset arrays -> host with one gather launch and one copy (instead of
+// one 4-byte copy each), then the batch Params, under one stream sync.
+constexpr int MAX_TOTALS = 96;
+struct TotTable { const uint32_t* src[MAX_TOTALS]; int count; };
+__global__ void k_collect_totals(TotTable t, uint32_t* out) {
+    const int i = threadIdx.x;
+    if (i < t.count) out[i] = *t.src[i];
+}
+int read_totals_params(ad_handle* h, const TotTable& t, uint32_t* host) {
+    if (t.count > 0) {
+        k_collect_totals<<<1, MAX_TOTALS, 0, h->st>>>(t, h->totd);
+        HIPCHK(h, hipMemcpyAsync(host, h->totd, (size_t)t.count * 4, hipMemcpyDeviceToHost, h->st));
+    }
+    return read_params(h);
 }
 
 int check_params(ad_handle* h) {
@@ -409,14 +426,13 @@ int stage_deps(ad_handle* h) {
     const int ncsr = nvc + nv;
     std::vector<uint32_t> tot(3 * ncsr, 0);
     auto csr_at = [&](int c) -> Csr& { return c < nvc ? h->deps[c] : h->rdeps[c - nvc]; };
-    for (int c = 0; c < ncsr; ++c) {
-        if (c >= nvc && Q == 0) continue;
+    TotTable tt{};
+    for (int c = 0; c < (Q > 0 ? ncsr : nvc); ++c) {
         Csr& x = csr_at(c);
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * c + 0], x.key_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * c + 1], x.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * c + 2], x.ent_off + n, 4, hipMemcpyDeviceToHost, st));
+        tt.src[3 * c + 0] = x.key_off + n; tt.src[3 * c + 1] = x.k2t_off + n; tt.src[3 * c + 2] = x.ent_off + n;
+        tt.count = 3 * c + 3;
     }
-    CK(read_params(h));
+    CK(read_totals_params(h, tt, tot.data()));
     CK(check_params(h));
     h->deps_entries = 0;
     for (int c = 0; c < ncsr; ++c) {
@@ -534,12 +550,12 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
         }
     }
     std::vector<uint32_t> tot(3 * K, 0);
+    TotTable tt{};
     for (int k = 0; k < K; ++k) {
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * k + 0], out[k]->key_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * k + 1], out[k]->k2t_off + n, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(&tot[3 * k + 2], out[k]->ent_off + n, 4, hipMemcpyDeviceToHost, st));
+        tt.src[3 * k + 0] = out[k]->key_off + n; tt.src[3 * k + 1] = out[k]->k2t_off + n; tt.src[3 * k + 2] = out[k]->ent_off + n;
     }
-    CK(read_params(h));
+    tt.count = 3 * K;
+    CK(read_totals_params(h, tt, tot.data()));
     CK(check_params(h));
     for (int k = 0; k < K; ++k) {
         Csr& m = *out[k];
@@ -640,7 +656,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_exec_levels needs ad_preaccept_deps on this batch (its key chains)");
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.spos = h->spos; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.spos = h->spos; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.merged_key = &h->merged[AD_CLASS_KEY];
     li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
@@ -777,7 +793,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     }
     // working buffers
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
-    CK(dalloc(h, S_PRM, &h->prm, 1));
+    CK(dalloc(h, S_PRM, &h->prm, 1)); CK(dalloc(h, S_TOT, &h->totd, MAX_TOTALS));
     CK(dalloc(h, S_TXTS, &h->tx_ts, n)); CK(dalloc(h, S_EX1, &h->ex1, n)); CK(dalloc(h, S_META, &h->meta, n));
     CK(dalloc(h, S_PTXN, &h->pair_txn, P));
     CK(dalloc(h, S_KA, &h->ka, P)); CK(dalloc(h, S_VA, &h->va, P)); CK(dalloc(h, S_KB, &h->kb, P)); CK(dalloc(h, S_VB, &h->vb, P));
@@ -1276,7 +1292,7 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     else if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
     LevelInputs li{};
     li.n = n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.spos = h->spos; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.spos = h->spos; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;
     li.n_large = 0;

@@ -217,14 +217,16 @@ __global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict_
 }
 
 // txn pair -> push target: head position of its chain if that chain is short and has 2+ entries,
-// -1 for a single-entry chain (nothing to re-walk), -2 for a long chain (rescanned by the segmented scan)
-__global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ spos, const int32_t* __restrict__ seg_start,
+// -1 for a single-entry chain (nothing to re-walk), -2 for a long chain (rescanned by the segmented scan).
+// One thread per sorted entry: segment start and length are read (nearly) coalesced and the target is
+// scattered to the pair (one random 4-byte store instead of two dependent random loads per pair).
+__global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ sval, const int32_t* __restrict__ seg_start,
                                                   const uint32_t* __restrict__ seg_len, int32_t* __restrict__ pair_seg) {
-    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    const int32_t h = seg_start[spos[p]];
+    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P) return;
+    const int32_t h = seg_start[s];
     const uint32_t len = seg_len[h];
-    pair_seg[p] = len < 2 ? -1 : (len > SHORT_SEG ? -2 : h);
+    pair_seg[sval[s]] = len < 2 ? -1 : (len > SHORT_SEG ? -2 : h);
 }
 
 __global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
@@ -448,6 +450,7 @@ struct LevelInputs {
     const uint64_t* e_exec1;
     const int32_t* seg_start;
     const uint32_t* spos;
+    const uint32_t* sval;                // sorted position -> pair
     const uint32_t* key_off;
     const uint8_t* meta;
     const uint64_t* ex1;
@@ -466,24 +469,32 @@ struct LevelInputs {
 
 // Execution order over m txns (rows[k], or k when rows is null): LSD radix sort by executeAt (two 32-bit
 // halves) then stably by level; order_out[k'] = k of the k'-th txn.  ls.sk*/sv*/rs must hold m entries.
+// level of each txn in `perm` order (dst) + max level; with `key`, also checks that key[] is ascending
+// (flags[1] |= 1 if not).  Grid-stride over a bounded grid: one atomic per block (a per-block atomic on
+// one address from ~4K blocks serialised into ~40 us).
+constexpr int ORDER_GRID = 1024;
 __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint32_t* __restrict__ lvl, const uint32_t* __restrict__ rows,
                                                            const uint32_t* __restrict__ perm, uint32_t* __restrict__ dst,
-                                                           uint32_t* __restrict__ maxv) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                           const uint64_t* __restrict__ key, uint32_t* __restrict__ flags) {
     uint32_t v = 0;
-    if (i < m) {
+    bool bad = false;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t k = perm[i];
-        v = lvl[rows ? rows[k] : k];
-        dst[i] = v;
+        const uint32_t x = lvl[rows ? rows[k] : k];
+        dst[i] = x;
+        v = x > v ? x : v;
+        if (key && i + 1 < m && key[i] > key[i + 1]) bad = true;
     }
     v = wave_max(v);
-    __shared__ uint32_t red[256 / WAVE];
-    if (__lane_id() == 0) red[threadIdx.x / WAVE] = v;
+    const bool wbad = __ballot(bad) != 0;
+    __shared__ uint32_t red[256 / WAVE], rb[256 / WAVE];
+    if (__lane_id() == 0) { red[threadIdx.x / WAVE] = v; rb[threadIdx.x / WAVE] = wbad ? 1u : 0u; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t mx = red[0];
-        for (int k = 1; k < 256 / WAVE; ++k) mx = mx > red[k] ? mx : red[k];
-        atomicMax(maxv, mx);
+        uint32_t mx = red[0], b = rb[0];
+        for (int k = 1; k < 256 / WAVE; ++k) { mx = mx > red[k] ? mx : red[k]; b |= rb[k]; }
+        atomicMax(&flags[0], mx);
+        if (b) atomicOr(&flags[1], 1u);
     }
 }
 __global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
@@ -534,13 +545,6 @@ __global__ __launch_bounds__(BS_T) void k_block_sort64(size_t m, size_t off, uin
     }
     for (uint32_t x = threadIdx.x; x < cnt; x += BS_T) { key[base + x] = sk[x]; idx[base + x] = si[x]; }
 }
-// flags[0] |= unsorted; flags[1] = max level (of the txns in idx order)
-__global__ __launch_bounds__(256) void k_check_exec_order(size_t m, const uint64_t* __restrict__ key, uint32_t* __restrict__ flags) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool bad = i + 1 < m && key[i] > key[i + 1];
-    if (__ballot(bad) && __lane_id() == 0) atomicOr(flags, 1u);
-}
-
 inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
                        uint32_t exec_bits, uint32_t* order_out, hipStream_t st) {
     KScope ks(K_ORDER, m);
@@ -557,8 +561,8 @@ inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     if (m > (size_t)BS_N / 2)
         k_block_sort64<<<ceil_div((long)(m - BS_N / 2), BS_N), BS_T, 0, st>>>(m, BS_N / 2, ls.key64, v);
     hipMemsetAsync(ls.flags + 4, 0, 8, st);
-    k_check_exec_order<<<g, 256, 0, st>>>(m, ls.key64, ls.flags + 5);
-    k_gather_level_rows<<<g, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
+    const int gg = std::min(g, ORDER_GRID);
+    k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, ls.key64, ls.flags + 4);
     uint32_t fl[2] = {0, 0};
     hipMemcpyAsync(fl, ls.flags + 4, 8, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
@@ -572,7 +576,7 @@ inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
             k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, v, k, 1);
             if (radix_sort_pairs(k, v, ko, vo, m, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
         }
-        k_gather_level_rows<<<g, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
+        k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, nullptr, ls.flags + 4);
     }
     const uint32_t maxl = fl[0];
     const int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
@@ -652,7 +656,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
             k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
             k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp);
-            k_pair_seg<<<gP, 256, 0, st>>>(P, in.spos, in.seg_start, ls.seg_len, ls.pair_seg);
+            k_pair_seg<<<gP, 256, 0, st>>>(P, in.sval, in.seg_start, ls.seg_len, ls.pair_seg);
             device_scan(SegListOp{in.seg_start, ls.seg_len, ls.heads, ls.long_pos, ls.flags, P}, P, (SegListOp::S*)ls.agg, st);
             if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);
         }

@@ -1,0 +1,27 @@
+#!/bin/bash
+# profiles/collect.sh TAG — the round's measurement recipe, run on the GPU box from the repo root:
+#   /usr/local/graft/bin/gpurun --timeout 900 -- 'bash profiles/collect.sh r01_v2'
+# 1. the default bench line (C2, with the CPU baseline leg) + its per-kernel HIP-event breakdown;
+# 2. rocprofv3 --kernel-trace --stats of a short bench run (kernel durations to cross-check `roofline`);
+# 3. two separate PMC passes (FETCH_SIZE, WRITE_SIZE — they do not fit one pass on gfx950);
+# then, back in the build container (gpurun merges gpurun_out/ back):
+#   python3 profiles/summarize.py gpurun_out/TAG TAG      -> profiles/TAG_*
+# Every GPU step has its own time limit and the steps are chained (set -e): a failure ends the script.
+set -eo pipefail
+TAG=${1:?tag}
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 420 python3 -u "$ROOT/bench.py" --breakdown > "$OUT/bench.json" 2> "$OUT/bench.err"
+echo "bench done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --cpu-sample 0 > "$OUT/stats.json" 2> "$OUT/stats.err"
+echo "stats done"
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 > "$OUT/fetch.log" 2>&1
+echo "fetch done"
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 > "$OUT/write.log" 2>&1
+echo "write done"
