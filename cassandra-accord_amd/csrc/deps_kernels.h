@@ -4,7 +4,7 @@
 //   k_minmax / k_pack   batch statistics, TxnId/executeAt -> packed ts64, per-txn meta byte, pair owner,
 //                       footprint validation (keys ascending per txn, ranges sorted and disjoint)
 //   radix sort          (key - key_min, pair) pairs, stable => each key segment is CFK.byId order
-//   k_gather_entries    sorted entry SoA: txn rank, meta, executeAt+1, inverse permutation
+//   k_gather_entries    sorted entry SoA: txn rank, meta, executeAt+1 (one 16-byte record per entry)
 //   ElideOp scan        per entry: segment start, distinct-key index, prefix max executeAt of committed
 //                       writes (maxCommittedWriteBefore), prefix max executeAt of elidable entries, last
 //                       "always emitted" entry — CommandsForKey.mapReduceActive's state
@@ -24,6 +24,12 @@ constexpr int MAXV = 8;       // replica views
 constexpr int KMAX = 16;      // keys per key-domain txn handled by the per-txn register kernels
 constexpr int NVC_MAX = MAXV * 2;
 constexpr uint32_t META_LARGE = 0x80u;   // meta bit 7: txn takes the large (virtual item) path
+
+struct alignas(16) PairRec {  // per (txn, key) pair, in pair order: what the sorted entries gather
+    uint64_t ex1;             // the txn's executeAt + 1 (packed)
+    uint32_t txn;             // batch rank
+    uint32_t meta;            // meta byte
+};
 
 struct Params {                // device-side batch statistics (filled by k_minmax / k_pack)
     unsigned long long msb_min, msb_max, hlc_min, hlc_max;
@@ -161,14 +167,15 @@ __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_
                                               const uint64_t* __restrict__ keys, const uint32_t* __restrict__ range_off,
                                               const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
                                               uint64_t* __restrict__ tx_ts, uint64_t* __restrict__ ex1,
-                                              uint8_t* __restrict__ meta, uint32_t* __restrict__ pair_txn,
+                                              uint8_t* __restrict__ meta, PairRec* __restrict__ prec,
                                               uint32_t* __restrict__ skey, uint32_t* __restrict__ sval, Params* prm) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t lsb = tl[i];
     uint64_t t = ts_pack(pk, tm[i], lsb, tn[i]);
     tx_ts[i] = t;
-    ex1[i] = ts_pack(pk, em[i], el[i], en[i]) + 1;
+    const uint64_t e1 = ts_pack(pk, em[i], el[i], en[i]) + 1;
+    ex1[i] = e1;
     const uint32_t kb = key_off[i], ke = key_off[i + 1];
     const uint32_t rb = range_off ? range_off[i] : 0u, rend = range_off ? range_off[i + 1] : 0u;
     const uint32_t domain = (uint32_t)(lsb & 1);
@@ -176,14 +183,16 @@ __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_
     if (domain == AD_DOMAIN_RANGE && ke != kb) err |= ERR_KEYORDER;        // a range txn's footprint is its ranges
     if (domain == AD_DOMAIN_KEY && rend != rb) err |= ERR_RANGEORDER;
     const bool large = domain == AD_DOMAIN_RANGE || (ke - kb) > (uint32_t)KMAX;
-    meta[i] = (uint8_t)(((lsb >> 1) & 7) | ((lsb & 1) << 3) | ((uint32_t)(status[i] & 7) << 4) | (large ? META_LARGE : 0u));
+    const uint8_t mi = (uint8_t)(((lsb >> 1) & 7) | ((lsb & 1) << 3) | ((uint32_t)(status[i] & 7) << 4) | (large ? META_LARGE : 0u));
+    meta[i] = mi;
+    const uint64_t x1 = e1;
     if (i > 0 && ts_pack(pk, tm[i - 1], tl[i - 1], tn[i - 1]) >= t) err |= ERR_UNSORTED;
     uint64_t prev = 0;
     for (uint32_t p = kb; p < ke; ++p) {
         const uint64_t k = keys[p];
         if (p > kb && k <= prev) err |= ERR_KEYORDER;                      // Keys: sorted unique
         prev = k;
-        pair_txn[p] = (uint32_t)i;
+        prec[p] = PairRec{x1, (uint32_t)i, (uint32_t)mi};
         skey[p] = (uint32_t)(k - key_min);
         sval[p] = p;
     }
@@ -196,20 +205,18 @@ __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_
     if (err) atomicOr(&prm->err, err);
 }
 
-// Sorted entry SoA + inverse permutation.
+// Sorted entry SoA: one random 16-byte record read per entry (the pair's txn, meta and executeAt were
+// packed per pair by k_pack in pair order, i.e. coalesced), instead of three dependent random loads.
 __global__ __launch_bounds__(256) void k_gather_entries(size_t P, const uint32_t* __restrict__ sval,
-                                                        const uint32_t* __restrict__ pair_txn,
-                                                        const uint8_t* __restrict__ meta, const uint64_t* __restrict__ ex1,
+                                                        const PairRec* __restrict__ prec,
                                                         uint32_t* __restrict__ e_txn, uint8_t* __restrict__ e_meta,
-                                                        uint64_t* __restrict__ e_exec1, uint32_t* __restrict__ spos) {
+                                                        uint64_t* __restrict__ e_exec1) {
     size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P) return;
-    uint32_t p = sval[s];
-    uint32_t t = pair_txn[p];
-    e_txn[s] = t;
-    e_meta[s] = meta[t];
-    e_exec1[s] = ex1[t];
-    spos[p] = (uint32_t)s;
+    const PairRec r = prec[sval[s]];
+    e_txn[s] = r.txn;
+    e_meta[s] = (uint8_t)r.meta;
+    e_exec1[s] = r.ex1;
 }
 
 // Segmented prefix state of CommandsForKey.mapReduceActive over the (key, TxnId)-sorted entries.
@@ -444,7 +451,6 @@ struct TxnArgs {
     const uint32_t* key_off;
     const uint64_t* keys;
     const uint8_t* meta;
-    const uint32_t* spos;
     const uint32_t* cnt;          // AoS by pair [p * nvc + vc]
     uint32_t* nk;                 // [vc * n + t]
     uint32_t* ne;                 // [vc * n + t]

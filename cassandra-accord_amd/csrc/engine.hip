@@ -61,9 +61,10 @@ struct ad_handle {
     uint32_t n_large = 0;
     uint64_t *tx_ts = nullptr, *ex1 = nullptr;
     uint8_t* meta = nullptr;
-    uint32_t *pair_txn = nullptr, *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;
+    PairRec* prec = nullptr;
+    uint32_t *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;
     uint32_t *skey = nullptr, *sval = nullptr;           // sorted (alias ka/kb)
-    uint32_t *e_txn = nullptr, *spos = nullptr, *uidx = nullptr, *useg = nullptr;
+    uint32_t *e_txn = nullptr, *uidx = nullptr, *useg = nullptr;
     uint64_t* ukey = nullptr;
     uint8_t* e_meta = nullptr;
     uint64_t *e_exec1 = nullptr, *pm_w = nullptr, *pm_c = nullptr;
@@ -276,7 +277,7 @@ int stage_prepare(ad_handle* h) {
     KScope ks(K_PACK, n);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
-                                                    h->range_e, h->tx_ts, h->ex1, h->meta, h->pair_txn, h->ka, h->va, h->prm);
+                                                    h->range_e, h->tx_ts, h->ex1, h->meta, h->prec, h->ka, h->va, h->prm);
     return AD_OK;
 }
 
@@ -367,8 +368,7 @@ int stage_deps(ad_handle* h) {
     for (int vc = 0; vc < nvc; ++vc) CK(alloc_csr(h, vc, h->deps[vc], n));
     for (int v = 0; v < nv; ++v) CK(alloc_csr(h, CSR_RANGE0 + v, h->rdeps[v], n));
     if (P > 0) {
-        { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->pair_txn, h->meta, h->ex1, h->e_txn, h->e_meta,
-                                                                                          h->e_exec1, h->spos); }
+        { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->e_txn, h->e_meta, h->e_exec1); }
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
                     h->uidx, h->ukey, h->useg, h->hprm.key_min, P, h->prm};
         KScope ks(K_SCAN_ELIDE, P);
@@ -378,7 +378,7 @@ int stage_deps(ad_handle* h) {
     h->V = 0;
     VItemArgs va{};
     va.n = n; va.meta = h->meta; va.key_off = h->key_off; va.keys = h->keys; va.range_off = h->range_off;
-    va.rs = h->range_s; va.re = h->range_e; va.spos = h->spos; va.seg_start = h->seg_start; va.e_txn = h->e_txn;
+    va.rs = h->range_s; va.re = h->range_e; va.e_txn = h->e_txn;
     va.ukey = h->ukey; va.useg = h->useg; va.prm = h->prm; va.vn = h->vn; va.voff = h->voff;
     if (h->n_large > 0) {
         KScope ks(K_VITEMS);
@@ -404,7 +404,7 @@ int stage_deps(ad_handle* h) {
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
     NV_DISPATCH(nv, launch_walk, wa, false, st);
     TxnArgs ta{};
-    ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.spos = h->spos; ta.cnt = h->cnt;
+    ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt = h->cnt;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
     if (n > 0) {
@@ -656,7 +656,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_exec_levels needs ad_preaccept_deps on this batch (its key chains)");
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.spos = h->spos; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.merged_key = &h->merged[AD_CLASS_KEY];
     li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
@@ -795,9 +795,9 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     CK(dalloc(h, S_PRM, &h->prm, 1)); CK(dalloc(h, S_TOT, &h->totd, MAX_TOTALS));
     CK(dalloc(h, S_TXTS, &h->tx_ts, n)); CK(dalloc(h, S_EX1, &h->ex1, n)); CK(dalloc(h, S_META, &h->meta, n));
-    CK(dalloc(h, S_PTXN, &h->pair_txn, P));
+    CK(dalloc(h, S_PTXN, &h->prec, P));
     CK(dalloc(h, S_KA, &h->ka, P)); CK(dalloc(h, S_VA, &h->va, P)); CK(dalloc(h, S_KB, &h->kb, P)); CK(dalloc(h, S_VB, &h->vb, P));
-    CK(dalloc(h, S_ETXN, &h->e_txn, P)); CK(dalloc(h, S_SPOS, &h->spos, P)); CK(dalloc(h, S_EMETA, &h->e_meta, P));
+    CK(dalloc(h, S_ETXN, &h->e_txn, P)); CK(dalloc(h, S_EMETA, &h->e_meta, P));
     CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
     CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
     CK(dalloc(h, S_UIDX, &h->uidx, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
@@ -1292,7 +1292,7 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     else if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
     LevelInputs li{};
     li.n = n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.spos = h->spos; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;
     li.n_large = 0;

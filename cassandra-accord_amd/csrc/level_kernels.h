@@ -217,32 +217,47 @@ __global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict_
 }
 
 // txn pair -> push target: head position of its chain if that chain is short and has 2+ entries,
-// -1 for a single-entry chain (nothing to re-walk), -2 for a long chain (rescanned by the segmented scan).
-// One thread per sorted entry: segment start and length are read (nearly) coalesced and the target is
-// scattered to the pair (one random 4-byte store instead of two dependent random loads per pair).
-__global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ sval, const int32_t* __restrict__ seg_start,
-                                                  const uint32_t* __restrict__ seg_len, int32_t* __restrict__ pair_seg) {
-    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P) return;
-    const int32_t h = seg_start[s];
+// -1 for nothing to re-walk, -2 for a long chain (rescanned by the segmented scan).  One thread per chain
+// position (executeAt order); the target is scattered to the pair (c_pair).
+// Without (c) constraints a raise of T only matters to the entries of the chain that wait for T: a Write
+// has dependants iff it is not the chain's last entry, a Read iff a Write follows it.  A pair with no
+// dependants gets -1, so raising T does not re-walk that chain.  With (c), every position's prefix max
+// (pm_all) is read by unmanaged txns, so every chain containing T is re-walked.
+__global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ c_pair, const uint8_t* __restrict__ c_meta,
+                                                  const int32_t* __restrict__ seg_start, const uint32_t* __restrict__ seg_len,
+                                                  int32_t* __restrict__ pair_seg, int prune) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    const int32_t h = seg_start[q];
     const uint32_t len = seg_len[h];
-    pair_seg[sval[s]] = len < 2 ? -1 : (len > SHORT_SEG ? -2 : h);
+    int32_t tgt = len < 2 ? -1 : (len > SHORT_SEG ? -2 : h);
+    if (prune && tgt >= 0) {
+        const size_t end = (size_t)h + len;
+        bool dep = false;
+        if (meta_kind(c_meta[q]) == AD_KIND_WRITE) dep = q + 1 < end;
+        else
+            for (size_t x = q + 1; x < end && !dep; ++x) dep = meta_kind(c_meta[x]) == AD_KIND_WRITE;
+        if (!dep) tgt = -1;
+    }
+    pair_seg[c_pair[q]] = tgt;
 }
 
 __global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
-                                                    const uint64_t* __restrict__ e_exec1, uint32_t* __restrict__ c_txn,
-                                                    uint8_t* __restrict__ c_meta, uint64_t* __restrict__ c_exec1) {
+                                                    const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                                    uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                                    uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P) return;
     c_txn[s] = e_txn[s];
     c_meta[s] = e_meta[s];
     c_exec1[s] = e_exec1[s];
+    c_pair[s] = sval[s];
 }
 
 // Per-segment fix-up: entries of one key ordered by executeAt (insertion sort; one thread per segment).
 __global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __restrict__ seg_start,
                                                      uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
-                                                     uint64_t* __restrict__ c_exec1) {
+                                                     uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P || seg_start[s] != (int32_t)s) return;
     size_t e = s + 1;
@@ -259,12 +274,13 @@ __global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __
         uint64_t kx = c_exec1[x];
         uint32_t tx = c_txn[x];
         uint8_t mx = c_meta[x];
+        uint32_t px = c_pair[x];
         size_t y = x;
         while (y > s && c_exec1[y - 1] > kx) {
-            c_exec1[y] = c_exec1[y - 1]; c_txn[y] = c_txn[y - 1]; c_meta[y] = c_meta[y - 1];
+            c_exec1[y] = c_exec1[y - 1]; c_txn[y] = c_txn[y - 1]; c_meta[y] = c_meta[y - 1]; c_pair[y] = c_pair[y - 1];
             --y;
         }
-        c_exec1[y] = kx; c_txn[y] = tx; c_meta[y] = mx;
+        c_exec1[y] = kx; c_txn[y] = tx; c_meta[y] = mx; c_pair[y] = px;
     }
 }
 
@@ -419,6 +435,7 @@ struct LevelState {
     uint8_t* c_meta = nullptr;
     uint64_t* c_exec1 = nullptr;
     int32_t* pm_all = nullptr;
+    uint32_t* c_pair = nullptr;         // chain position -> pair
     int32_t* pair_seg = nullptr;
     uint32_t *seg_len = nullptr, *stamp = nullptr, *heads = nullptr, *long_pos = nullptr;
     int32_t* cons_pos = nullptr;
@@ -436,7 +453,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -449,7 +466,6 @@ struct LevelInputs {
     const uint8_t* e_meta;
     const uint64_t* e_exec1;
     const int32_t* seg_start;
-    const uint32_t* spos;
     const uint32_t* sval;                // sorted position -> pair
     const uint32_t* key_off;
     const uint8_t* meta;
@@ -596,7 +612,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     if (ls.capP < P || !ls.c_txn) {
         size_t c = std::max<size_t>(P, 1);
         if (!grow((void**)&ls.c_txn, c * 4) || !grow((void**)&ls.c_meta, c) || !grow((void**)&ls.c_exec1, c * 8) ||
-            !grow((void**)&ls.pm_all, c * 4) || !grow((void**)&ls.pair_seg, c * 4) || !grow((void**)&ls.seg_len, c * 4) ||
+            !grow((void**)&ls.pm_all, c * 4) || !grow((void**)&ls.c_pair, c * 4) || !grow((void**)&ls.pair_seg, c * 4) || !grow((void**)&ls.seg_len, c * 4) ||
             !grow((void**)&ls.stamp, c * 4) || !grow((void**)&ls.heads, c * 4) || !grow((void**)&ls.long_pos, c * 4))
             goto oom;
         ls.capP = c;
@@ -653,10 +669,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             k_stamp_reset<<<ceil_div((long)std::max<uint32_t>(ls.nheads, 1), 256), 256, 0, st>>>(ls.heads, ls.nheads, ls.stamp);
         } else if (P > 0) {
             KScope ks(K_CHAIN_PREP);
-            k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, ls.c_txn, ls.c_meta, ls.c_exec1);
-            k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1);
+            k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+            k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
             k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp);
-            k_pair_seg<<<gP, 256, 0, st>>>(P, in.sval, in.seg_start, ls.seg_len, ls.pair_seg);
+            k_pair_seg<<<gP, 256, 0, st>>>(P, ls.c_pair, ls.c_meta, in.seg_start, ls.seg_len, ls.pair_seg, has_c ? 0 : 1);
             device_scan(SegListOp{in.seg_start, ls.seg_len, ls.heads, ls.long_pos, ls.flags, P}, P, (SegListOp::S*)ls.agg, st);
             if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);
         }

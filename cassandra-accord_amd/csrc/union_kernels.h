@@ -45,8 +45,6 @@ struct VItemArgs {
     const uint32_t* range_off;
     const uint64_t* rs;
     const uint64_t* re;
-    const uint32_t* spos;
-    const int32_t* seg_start;
     const uint32_t* e_txn;
     const uint64_t* ukey;        // [U] distinct keys
     const uint32_t* useg;        // [U+1]
@@ -80,11 +78,15 @@ __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
         if (!FILL) { a.vn[t] = e - b; return; }
         uint32_t x = a.voff[t];
         for (uint32_t p = b; p < e; ++p, ++x) {
-            const uint32_t s = a.spos[p];
+            // the pair's own sorted entry: its key's segment, then TxnId t inside it (byId order)
+            const uint64_t k = a.keys[p];
+            const uint32_t u = lb_u64(a.ukey, 0, U, k);
+            const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+            const uint32_t s = ub_u32(a.e_txn, s0, s1, (uint32_t)t) - 1;
             a.vi_txn[x] = (uint32_t)t;
             a.vi_pos[x] = s;                       // the pair itself: walk [seg0, s)
-            a.vi_seg0[x] = (uint32_t)a.seg_start[s];
-            a.vi_key[x] = a.keys[p];
+            a.vi_seg0[x] = s0;
+            a.vi_key[x] = k;
         }
         return;
     }
