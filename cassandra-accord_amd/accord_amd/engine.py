@@ -58,6 +58,7 @@ def lib():
         L.ad_run_pipeline.argtypes = [vp]
         L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
         L.ad_set_trace.argtypes = [vp, C.c_uint64]
+        L.ad_set_level_mode.argtypes = [vp, C.c_int]
         L.ad_kernel_count.restype = C.c_int
         L.ad_kernel_name.argtypes = [C.c_int]
         L.ad_kernel_name.restype = C.c_char_p
@@ -71,7 +72,7 @@ def lib():
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
             "ad_fetch_deps", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
-            "ad_run_pipeline", "ad_last_times", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
+            "ad_run_pipeline", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_blob_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_allgather", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
@@ -177,6 +178,10 @@ class DepsEngine:
         t = abi.AdStageTimes()
         self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
         return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_ if f != "pad_"}
+
+    def set_level_mode(self, fixpoint):
+        """False (default): Kahn wavefront where it applies, else the chain fixpoint; True: always the fixpoint."""
+        self._check(lib().ad_set_level_mode(self.h, 1 if fixpoint else 0), "ad_set_level_mode")
 
     def set_trace(self, mask):
         """Enable HIP-event timing of the kernels whose id bit is set (see kernel_ids())."""

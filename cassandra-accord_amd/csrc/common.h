@@ -107,4 +107,11 @@ struct DevCsr {
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Raise a 0/1 "something happened" flag from one lane of every wave that saw the event.  Thousands of
+// waves doing atomicOr on one address serialise at the memory side (measured: 150+ us in one launch), so
+// a lane first reads the flag and only stores if it is still clear; every writer stores the same value.
+__device__ inline void wave_set_flag(bool event, uint32_t* flag) {
+    if (__ballot(event) && __lane_id() == 0 && *(volatile uint32_t*)flag == 0u) *(volatile uint32_t*)flag = 1u;
+}
+
 }  // namespace ad

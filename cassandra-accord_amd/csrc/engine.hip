@@ -55,6 +55,7 @@ struct ad_handle {
     Params* prm = nullptr;
     Params hprm{};
     uint32_t* totd = nullptr;          // device: gathered CSR totals (read_totals_params)
+    int level_mode = AD_LEVELS_AUTO;
     TsPack pack{};
     int key_bits = 0, range_bits = 0;
     uint64_t rbase = 0, wmax = 0;
@@ -664,6 +665,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.merged_range = &h->merged[AD_CLASS_RANGE];
     li.n_large = h->n_large;
     li.exec_bits = h->pack.total_bits;
+    li.kahn_ok = h->level_mode == AD_LEVELS_AUTO ? 1 : 0;
     int iters = 0;
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
     if (rc != AD_OK) return rc;
@@ -980,6 +982,12 @@ int ad_last_times(ad_handle* h, ad_stage_times* out) {
 int ad_kernel_count(void) { return K_COUNT; }
 
 const char* ad_kernel_name(int kid) { return kernel_name(kid); }
+
+int ad_set_level_mode(ad_handle* h, int mode) {
+    if (!h || (mode != AD_LEVELS_AUTO && mode != AD_LEVELS_FIXPOINT)) return AD_ERR_ARGUMENT;
+    h->level_mode = mode;
+    return AD_OK;
+}
 
 int ad_set_trace(ad_handle* h, uint64_t mask) {
     if (!h) return AD_ERR_ARGUMENT;

@@ -172,20 +172,25 @@ __global__ __launch_bounds__(256) void k_seg_short(const uint32_t* __restrict__ 
             }
         }
     }
-    if (__ballot(queued) && __lane_id() == 0) atomicOr(work_left, 1u);
+    wave_set_flag(queued, work_left);
 }
 
 // Segment table: length and stamp at each head; per position: is it the head of a short multi-entry
 // segment (-> heads list), is it inside a long segment (-> long positions list).
 __global__ __launch_bounds__(256) void k_seg_table(size_t P, const int32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_len,
-                                                   uint32_t* __restrict__ stamp) {
+                                                   uint32_t* __restrict__ stamp, uint32_t* __restrict__ any_long) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P) return;
-    const int32_t h = seg_start[s];
-    if (s + 1 == P || seg_start[s + 1] != h) {
-        seg_len[h] = (uint32_t)(s + 1 - (size_t)h);
-        stamp[h] = 0u;
+    bool lng = false;
+    if (s < P) {
+        const int32_t h = seg_start[s];
+        if (s + 1 == P || seg_start[s + 1] != h) {
+            const uint32_t len = (uint32_t)(s + 1 - (size_t)h);
+            seg_len[h] = len;
+            stamp[h] = 0u;
+            lng = len > SHORT_SEG;
+        }
     }
+    wave_set_flag(lng, any_long);
 }
 struct SegListOp {                 // two compactions in one scan: short multi heads, long positions
     struct S { uint32_t a, b; };
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(256) void k_level_kinds(size_t n, const uint8_t* __
         const uint32_t k = meta_kind(meta[t]);
         bad = !(k == AD_KIND_READ || k == AD_KIND_WRITE);
     }
-    if (__ballot(bad) && __lane_id() == 0) atomicOr(flag, 1u);
+    wave_set_flag(bad, flag);
 }
 
 struct EdgeArgs {
@@ -396,8 +401,8 @@ __global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int d
             }
         }
     }
-    if (__ballot(raised) && __lane_id() == 0) atomicOr(a.changed, 1u);
-    if (__ballot(queued) && __lane_id() == 0) atomicOr(a.work_left, 1u);
+    wave_set_flag(raised, a.changed);
+    wave_set_flag(queued, a.work_left);
 }
 
 __global__ __launch_bounds__(256) void k_exec_split(size_t n, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ idx,
@@ -429,6 +434,74 @@ __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Kahn wavefront for shallow key-chain graphs (no chain longer than SHORT_SEG, no (b)/(c) constraints):
+// every txn is visited once, when its last predecessor is released, instead of re-walking chains until
+// a fixpoint.  Per chain position the (a) rule reduces to a transitive reduction:
+//   Read R   waits for the last Write before it (1 edge, if any);
+//   Write W  waits for the Reads since the last Write before it, or for that Write if none; with no
+//            earlier Write, for every earlier entry (all Reads).
+// so each position's successors are one contiguous run of its chain: after a Write, the Reads that follow
+// it (or the next Write if a Write follows directly); after a Read, the next Write.  Same chain order and
+// rule as the fixpoint walk, so the levels are identical.
+// ---------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_kahn_prep(size_t P, const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
+                                                   const uint32_t* __restrict__ c_pair, const int32_t* __restrict__ seg_start,
+                                                   const uint32_t* __restrict__ seg_len, uint32_t* __restrict__ indeg,
+                                                   uint2* __restrict__ succ) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    const size_t h = (size_t)seg_start[q];
+    const size_t end = h + seg_len[h];
+    uint2 sc = make_uint2(0u, 0u);
+    if (end - h >= 2) {
+        const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
+        uint32_t reads = 0;
+        bool pw = false;
+        for (size_t x = q; x > h;) {
+            --x;
+            if (meta_kind(c_meta[x]) == AD_KIND_WRITE) { pw = true; break; }
+            ++reads;
+        }
+        const uint32_t pc = wr ? (reads > 0 ? reads : (pw ? 1u : 0u)) : (pw ? 1u : 0u);
+        if (pc) atomicAdd(&indeg[c_txn[q]], pc);
+        if (q + 1 < end) {
+            if (wr && meta_kind(c_meta[q + 1]) == AD_KIND_WRITE) {
+                sc = make_uint2((uint32_t)(q + 1), 1u);
+            } else {
+                size_t x = q + 1;
+                while (x < end && meta_kind(c_meta[x]) != AD_KIND_WRITE) ++x;
+                if (wr) sc = make_uint2((uint32_t)(q + 1), (uint32_t)(x - (q + 1)));   // the Reads after W
+                else if (x < end) sc = make_uint2((uint32_t)x, 1u);                     // the next Write
+            }
+        }
+    }
+    succ[c_pair[q]] = sc;
+}
+
+// One wavefront: the txns released at level `lvl` (level 0: indeg == 0 in the snapshot; later levels:
+// L == lvl, which only a release sets) release their successors; the last release of S sets L[S] = lvl+1.
+// prev: the previous wavefront's "released something" flag (nullptr: run); *work: this one released some.
+__global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
+                                                   uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
+                                                   const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
+                                                   const uint32_t* __restrict__ c_txn, const uint32_t* prev,
+                                                   uint32_t* __restrict__ work) {
+    if (prev && *prev == 0u) return;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool released = false;
+    if (t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl)) {
+        for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) {
+            const uint2 sc = succ[p];
+            for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) {
+                const uint32_t s = c_txn[x];
+                if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
+            }
+        }
+    }
+    wave_set_flag(released, work);
+}
+
 struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
     uint32_t* c_txn = nullptr;
@@ -439,6 +512,8 @@ struct LevelState {
     int32_t* pair_seg = nullptr;
     uint32_t *seg_len = nullptr, *stamp = nullptr, *heads = nullptr, *long_pos = nullptr;
     int32_t* cons_pos = nullptr;
+    uint32_t *indeg = nullptr, *rem = nullptr;   // Kahn path: [n] predecessor counts (snapshot, remaining)
+    uint2* succ = nullptr;                       // Kahn path: [P] successor run of each pair
     uint32_t* flags = nullptr;          // [0] heads, [1] long entries, [2] long dirty (next), [3] edge changed,
                                         // [4] max level, [5] unsupported kinds, [6] work left (next)
     void* agg = nullptr;
@@ -453,7 +528,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -481,6 +556,7 @@ struct LevelInputs {
     uint32_t n_large;
     uint32_t exec_bits;
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
+    int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
 };
 
 // Execution order over m txns (rows[k], or k when rows is null): LSD radix sort by executeAt (two 32-bit
@@ -612,7 +688,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     if (ls.capP < P || !ls.c_txn) {
         size_t c = std::max<size_t>(P, 1);
         if (!grow((void**)&ls.c_txn, c * 4) || !grow((void**)&ls.c_meta, c) || !grow((void**)&ls.c_exec1, c * 8) ||
-            !grow((void**)&ls.pm_all, c * 4) || !grow((void**)&ls.c_pair, c * 4) || !grow((void**)&ls.pair_seg, c * 4) || !grow((void**)&ls.seg_len, c * 4) ||
+            !grow((void**)&ls.pm_all, c * 4) || !grow((void**)&ls.c_pair, c * 4) || !grow((void**)&ls.succ, c * 8) || !grow((void**)&ls.pair_seg, c * 4) || !grow((void**)&ls.seg_len, c * 4) ||
             !grow((void**)&ls.stamp, c * 4) || !grow((void**)&ls.heads, c * 4) || !grow((void**)&ls.long_pos, c * 4))
             goto oom;
         ls.capP = c;
@@ -620,7 +696,8 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     if (ls.capN < n || !ls.sk0) {
         size_t c = std::max<size_t>(n, 1);
         if (!grow((void**)&ls.sk0, c * 4) || !grow((void**)&ls.sv0, c * 4) || !grow((void**)&ls.sk1, c * 4) ||
-            !grow((void**)&ls.sv1, c * 4) || !grow((void**)&ls.key64, c * 8))
+            !grow((void**)&ls.sv1, c * 4) || !grow((void**)&ls.key64, c * 8) ||
+            !grow((void**)&ls.indeg, c * 4) || !grow((void**)&ls.rem, c * 4))
             goto oom;
         ls.capN = c;
     }
@@ -671,7 +748,57 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             KScope ks(K_CHAIN_PREP);
             k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
             k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-            k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp);
+            k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp, ls.flags + 7);
+        }
+        bool kahn = false;
+        if (!reuse) {
+            // one sync: unsupported kinds, and whether the Kahn wavefront applies (no long chain, no (b)/(c))
+            hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
+            if (host[5]) {
+                err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                return AD_ERR_UNSUPPORTED;
+            }
+            kahn = in.kahn_ok && !in.keep_levels && !has_b && !has_c && host[7] == 0 && P > 0;
+        }
+        if (kahn) {
+            ls.chains_ready = false;
+            int lv = 0;
+            {
+                KScope ks(K_KAHN);
+                hipMemsetAsync(ls.indeg, 0, n * 4, st);
+                k_kahn_prep<<<gP, 256, 0, st>>>(P, ls.c_txn, ls.c_meta, ls.c_pair, in.seg_start, ls.seg_len, ls.indeg, ls.succ);
+                hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
+                // wavefronts per launch batch, no host sync inside a batch (a wavefront after the last
+                // one exits at once); the first batch covers typical uniform-key depths (C2: 10)
+                constexpr int KB_MAX = 16;
+                const int gn = ceil_div((long)n, 256);
+                bool more = true;
+                while (more && lv < (1 << 24)) {
+                    const int KB = lv == 0 ? KB_MAX : 8;
+                    hipMemsetAsync(ls.iflags, 0, KB * 4, st);
+                    for (int k = 0; k < KB; ++k)
+                        k_kahn_step<<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ, ls.c_txn,
+                                                        k == 0 ? nullptr : ls.iflags + (k - 1), ls.iflags + k);
+                    uint32_t fh[KB_MAX];
+                    if (hipMemcpyAsync(fh, ls.iflags, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess) {
+                        err = "exec levels: device error";
+                        return AD_ERR_DEVICE;
+                    }
+                    int k = 0;
+                    while (k < KB && fh[k]) ++k;
+                    if (k == KB) { lv += KB; continue; }     // every wavefront released more: next batch
+                    lv += k + 1;
+                    more = false;
+                }
+            }
+            *iters = lv;
+            if (want_order && n > 0) order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
+            return AD_OK;
+        }
+        if (P > 0 && !reuse) {
+            KScope ks(K_CHAIN_PREP);
             k_pair_seg<<<gP, 256, 0, st>>>(P, ls.c_pair, ls.c_meta, in.seg_start, ls.seg_len, ls.pair_seg, has_c ? 0 : 1);
             device_scan(SegListOp{in.seg_start, ls.seg_len, ls.heads, ls.long_pos, ls.flags, P}, P, (SegListOp::S*)ls.agg, st);
             if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);

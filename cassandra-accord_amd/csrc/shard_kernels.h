@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_levels_scatter(size_t n, const uint32_t
         const uint32_t g = gid[i], l = L[i];
         if (l > G[g]) { G[g] = l; up = true; }
     }
-    if (__ballot(up) && __lane_id() == 0) atomicOr(changed, 1u);
+    wave_set_flag(up, changed);
 }
 
 }  // namespace ad

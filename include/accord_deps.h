@@ -202,6 +202,14 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
+/* Execution-level algorithm (both give identical levels; the choice only affects speed):
+ * AD_LEVELS_AUTO (default) uses the Kahn wavefront (each txn visited once, when released) for batches whose
+ * key chains are all short and that carry no direct/range deps and no range txns, and the chain fixpoint
+ * otherwise; AD_LEVELS_FIXPOINT always uses the fixpoint (tests cross-check the two). */
+#define AD_LEVELS_AUTO 0
+#define AD_LEVELS_FIXPOINT 1
+int  ad_set_level_mode(ad_handle* h, int mode);
+
 /* Per-kernel HIP-event timing (trace mode).  mask bit k enables kernel id k (0 <= k < ad_kernel_count()); the
  * events are recorded on the handle's stream around each launch of that kernel.  ad_kernel_stats
  * synchronises the stream and returns the kernel's name, launches and summed milliseconds since the

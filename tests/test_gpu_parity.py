@@ -20,11 +20,13 @@ def _assert_csr(name, got, want):
                                                                       want.txn(i) if i is not None and i < want.n else None))
 
 
-def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, levels=True):
+def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, levels=True, fixpoint=False):
     cfg = abi.make_config(window, replicas, drop_p, seed)
     flags = O.FLAG_MERGE | (O.FLAG_LEVELS if levels else 0)
     ref = O.OracleResult(batch, cfg, flags)
     eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
+    if fixpoint:
+        eng.set_level_mode(True)
     eng.load(batch)
     eng.preaccept_deps()
     for v in range(replicas):
@@ -44,6 +46,15 @@ def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D
 @pytest.mark.parametrize("name,n", [("C2", 20000), ("C3", 20000), ("C2", 200000)])
 def test_configs_small(engine_factory, name, n):
     check(engine_factory, workload.config(name, n=n))
+
+
+@pytest.mark.parametrize("fixpoint", [False, True])
+@pytest.mark.parametrize("keyspace,n", [(10_000_000, 200000), (40000, 20000), (4000, 6000), (300, 2000)])
+def test_levels_kahn_and_fixpoint(engine_factory, keyspace, n, fixpoint):
+    # short key chains and no range txns: AUTO takes the Kahn wavefront, FIXPOINT the chain fixpoint; both
+    # must give the oracle's levels and order (the denser keyspaces give deeper graphs, up to long chains)
+    b = workload.generate(n, keys_per_txn=4, keyspace=keyspace, seed=keyspace % 97 + n)
+    check(engine_factory, b, fixpoint=fixpoint)
 
 
 def test_c3_more_views_no_drop(engine_factory):
