@@ -561,21 +561,65 @@ struct LevelInputs {
 
 // Execution order over m txns (rows[k], or k when rows is null): LSD radix sort by executeAt (two 32-bit
 // halves) then stably by level; order_out[k'] = k of the k'-th txn.  ls.sk*/sv*/rs must hold m entries.
-// level of each txn in `perm` order (dst) + max level; with `key`, also checks that key[] is ascending
-// (flags[1] |= 1 if not).  Grid-stride over a bounded grid: one atomic per block (a per-block atomic on
-// one address from ~4K blocks serialised into ~40 us).
-constexpr int ORDER_GRID = 1024;
-__global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint32_t* __restrict__ lvl, const uint32_t* __restrict__ rows,
-                                                           const uint32_t* __restrict__ perm, uint32_t* __restrict__ dst,
-                                                           const uint64_t* __restrict__ key, uint32_t* __restrict__ flags) {
+__global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
+                                                         const uint32_t* __restrict__ perm, uint32_t* __restrict__ key, int hi) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t k = perm ? perm[i] : (uint32_t)i;
+    const uint64_t e = ex1[rows ? rows[k] : k] - 1;
+    key[i] = hi ? (uint32_t)(e >> 32) : (uint32_t)e;
+}
+
+// Near-sorted fast path for the executeAt order: executeAt == TxnId on the fast path and a slow-path bump
+// moves a txn only a few ranks, so every inversion of the TxnId order is between ranks less than WR_D
+// apart.  Then each txn's rank in (executeAt, row) order is its row index corrected by the inversions
+// inside a +-WR_D window:  rank_i = i + #{j in (i, i+D] : e_j < e_i} - #{j in [i-D, i) : e_j > e_i}
+// (one LDS tile of 1024 rows plus halos per block, 128 compares per row), and the row is scattered to
+// its rank together with its executeAt and level.  A check pass verifies that every slot was written
+// (no collision, via a sentinel) and that the keys ascend; otherwise the full LSD radix sort runs.
+constexpr int WR_N = 1024, WR_D = 64, WR_T = 256;
+constexpr uint32_t WR_EMPTY = 0xFFFFFFFFu;
+__global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
+                                                      const uint32_t* __restrict__ lvl, uint64_t* __restrict__ okey,
+                                                      uint32_t* __restrict__ oidx, uint32_t* __restrict__ olvl,
+                                                      uint32_t* __restrict__ bad) {
+    __shared__ uint64_t sk[WR_N + 2 * WR_D];
+    const long base = (long)blockIdx.x * WR_N;
+    for (int x = threadIdx.x; x < WR_N + 2 * WR_D; x += WR_T) {
+        const long g = base + x - WR_D;
+        // out-of-range neighbours: 0 before the batch (never greater), ~0 after it (never smaller)
+        sk[x] = g < 0 ? 0ull : (g >= (long)m ? ~0ull : ex1[rows ? rows[g] : (size_t)g]);
+    }
+    __syncthreads();
+    bool oob = false;
+    for (int e = threadIdx.x; e < WR_N; e += WR_T) {
+        const long i = base + e;
+        if (i >= (long)m) break;
+        const uint64_t key = sk[e + WR_D];
+        int r = 0;
+#pragma unroll 16
+        for (int k = 1; k <= WR_D; ++k) {
+            r += sk[e + WR_D + k] < key ? 1 : 0;
+            r -= sk[e + WR_D - k] > key ? 1 : 0;
+        }
+        const long rank = i + r;
+        if (rank < 0 || rank >= (long)m) { oob = true; continue; }
+        okey[rank] = key;
+        oidx[rank] = (uint32_t)i;
+        olvl[rank] = lvl[rows ? rows[i] : (size_t)i];
+    }
+    wave_set_flag(oob, bad);
+}
+// flags[0] = max level, flags[1] |= 1 unless okey ascends and every slot is filled
+__global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ oidx,
+                                                    const uint32_t* __restrict__ olvl, uint32_t* __restrict__ flags) {
     uint32_t v = 0;
     bool bad = false;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t k = perm[i];
-        const uint32_t x = lvl[rows ? rows[k] : k];
-        dst[i] = x;
+        if (oidx[i] == WR_EMPTY) { bad = true; continue; }
+        const uint32_t x = olvl[i];
         v = x > v ? x : v;
-        if (key && i + 1 < m && key[i] > key[i + 1]) bad = true;
+        if (i + 1 < m && okey[i] > okey[i + 1]) bad = true;
     }
     v = wave_max(v);
     const bool wbad = __ballot(bad) != 0;
@@ -589,54 +633,30 @@ __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint3
         if (b) atomicOr(&flags[1], 1u);
     }
 }
-__global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
-                                                         const uint32_t* __restrict__ perm, uint32_t* __restrict__ key, int hi) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t k = perm ? perm[i] : (uint32_t)i;
-    const uint64_t e = ex1[rows ? rows[k] : k] - 1;
-    key[i] = hi ? (uint32_t)(e >> 32) : (uint32_t)e;
+// level of each txn in `perm` order (dst) + max level (fallback path).  Grid-stride over a bounded grid:
+// one atomic per block.
+constexpr int ORDER_GRID = 1024;
+__global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint32_t* __restrict__ lvl, const uint32_t* __restrict__ rows,
+                                                           const uint32_t* __restrict__ perm, uint32_t* __restrict__ dst,
+                                                           uint32_t* __restrict__ flags) {
+    uint32_t v = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t k = perm[i];
+        const uint32_t x = lvl[rows ? rows[k] : k];
+        dst[i] = x;
+        v = x > v ? x : v;
+    }
+    v = wave_max(v);
+    __shared__ uint32_t red[256 / WAVE];
+    if (__lane_id() == 0) red[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t mx = red[0];
+        for (int k = 1; k < 256 / WAVE; ++k) mx = mx > red[k] ? mx : red[k];
+        atomicMax(&flags[0], mx);
+    }
 }
 
-// Near-sorted fast path for the executeAt order: executeAt == TxnId on the fast path and a slow-path
-// bump moves a txn only a few ranks, so the rank order is executeAt order up to bounded displacement.
-// Two rounds of LDS block sorts (windows of BS_N, the second shifted by BS_N/2) sort any sequence whose
-// displacement is below BS_N/2; a check kernel verifies global order (else: full LSD radix fallback).
-constexpr int BS_N = 1024, BS_T = 256;
-__global__ __launch_bounds__(256) void k_exec_init(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
-                                                   uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    key[i] = ex1[rows ? rows[i] : i];
-    idx[i] = (uint32_t)i;
-}
-__global__ __launch_bounds__(BS_T) void k_block_sort64(size_t m, size_t off, uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
-    __shared__ uint64_t sk[BS_N];
-    __shared__ uint32_t si[BS_N];
-    const size_t base = off + (size_t)blockIdx.x * BS_N;
-    if (base >= m) return;
-    const uint32_t cnt = (uint32_t)((m - base) < (size_t)BS_N ? (m - base) : (size_t)BS_N);
-    for (uint32_t x = threadIdx.x; x < BS_N; x += BS_T) {
-        sk[x] = x < cnt ? key[base + x] : ~0ull;
-        si[x] = x < cnt ? idx[base + x] : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    for (uint32_t k = 2; k <= (uint32_t)BS_N; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t x = threadIdx.x; x < (uint32_t)BS_N; x += BS_T) {
-                const uint32_t y = x ^ j;
-                if (y > x) {
-                    const uint64_t a = sk[x], b = sk[y];
-                    const uint32_t ia = si[x], ib = si[y];
-                    const bool gt = a > b || (a == b && ia > ib);      // (executeAt, rank): stable
-                    if (gt == ((x & k) == 0)) { sk[x] = b; sk[y] = a; si[x] = ib; si[y] = ia; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (uint32_t x = threadIdx.x; x < cnt; x += BS_T) { key[base + x] = sk[x]; idx[base + x] = si[x]; }
-}
 inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
                        uint32_t exec_bits, uint32_t* order_out, hipStream_t st) {
     KScope ks(K_ORDER, m);
@@ -647,14 +667,12 @@ inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     rs.agg = rs.offs + hl + 64;
     const int g = ceil_div((long)m, 256);
     uint32_t *k = ls.sk0, *v = ls.sv0, *ko = ls.sk1, *vo = ls.sv1;
-    // fast path: bounded-displacement block sorts + verification (one host sync: sortedness + max level)
-    k_exec_init<<<g, 256, 0, st>>>(m, ex1, rows, ls.key64, v);
-    k_block_sort64<<<ceil_div((long)m, BS_N), BS_T, 0, st>>>(m, 0, ls.key64, v);
-    if (m > (size_t)BS_N / 2)
-        k_block_sort64<<<ceil_div((long)(m - BS_N / 2), BS_N), BS_T, 0, st>>>(m, BS_N / 2, ls.key64, v);
-    hipMemsetAsync(ls.flags + 4, 0, 8, st);
+    // fast path: windowed inversion ranks + verification (one host sync: sortedness + max level)
     const int gg = std::min(g, ORDER_GRID);
-    k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, ls.key64, ls.flags + 4);
+    hipMemsetAsync(ls.flags + 4, 0, 8, st);
+    hipMemsetAsync(v, 0xFF, m * 4, st);                       // WR_EMPTY: detects rank collisions
+    k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, ls.flags + 5);
+    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, ls.flags + 4);
     uint32_t fl[2] = {0, 0};
     hipMemcpyAsync(fl, ls.flags + 4, 8, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
@@ -668,10 +686,14 @@ inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
             k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, v, k, 1);
             if (radix_sort_pairs(k, v, ko, vo, m, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
         }
-        k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, nullptr, ls.flags + 4);
+        k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
     }
     const uint32_t maxl = fl[0];
     const int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
+    if (lb > 0 && lb <= 8) {         // one stable pass by level, written straight into order_out
+        radix_sort_pairs(k, v, ko, order_out, m, lb, rs, st);
+        return;
+    }
     if (radix_sort_pairs(k, v, ko, vo, m, lb, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
     hipMemcpyAsync(order_out, v, m * 4, hipMemcpyDeviceToDevice, st);
 }
