@@ -386,6 +386,10 @@ template <int NV, bool FILL>
 __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.P) return;
+    // a key segment's first entry has nothing before it: no deps, and its counts stay at the zeros the
+    // caller cleared (so only pairs with earlier entries touch their random AoS slots)
+    const int seg0 = a.seg_start[s];
+    if (seg0 == (int)s) return;
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
     const uint32_t qk = meta_kind(mi);
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     };
     // small key-domain query txns only (large ones are virtual items)
     const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE);
-    if (query) walk_query<NV>(a, i, qk, (int)s, a.seg_start[s], emit);
+    if (query) walk_query<NV>(a, i, qk, (int)s, seg0, emit);
     if (!FILL) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {

@@ -403,6 +403,7 @@ int stage_deps(ad_handle* h) {
     wa.gid = h->sharded ? h->gid : nullptr;
     wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
+    if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt, 0, (size_t)nvc * P * 4, st));   // segment heads keep zero counts
     NV_DISPATCH(nv, launch_walk, wa, false, st);
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt = h->cnt;

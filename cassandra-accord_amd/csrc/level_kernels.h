@@ -453,8 +453,9 @@ __global__ __launch_bounds__(256) void k_kahn_prep(size_t P, const uint32_t* __r
     if (q >= P) return;
     const size_t h = (size_t)seg_start[q];
     const size_t end = h + seg_len[h];
+    if (end - h < 2) return;                 // single-entry chain: no edges (succ was cleared)
     uint2 sc = make_uint2(0u, 0u);
-    if (end - h >= 2) {
+    {
         const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
         uint32_t reads = 0;
         bool pw = false;
@@ -789,6 +790,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             {
                 KScope ks(K_KAHN);
                 hipMemsetAsync(ls.indeg, 0, n * 4, st);
+                hipMemsetAsync(ls.succ, 0, P * 8, st);
                 k_kahn_prep<<<gP, 256, 0, st>>>(P, ls.c_txn, ls.c_meta, ls.c_pair, in.seg_start, ls.seg_len, ls.indeg, ls.succ);
                 hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
                 // wavefronts per launch batch, no host sync inside a batch (a wavefront after the last
