@@ -15,17 +15,52 @@
 
 namespace ad {
 
-// 64-lane shuffle of an arbitrary 4-byte-multiple state
-template <class S>
-__device__ inline S shfl_up_state(const S& v, int delta) {
+// Cross-lane moves of an arbitrary 4-byte-multiple state, dword by dword, through DPP (VALU-rate lane
+// moves; ds_bpermute-based __shfl costs an LDS-crossbar round trip per dword, which made the 32-40 B
+// scan states of the elision and chain scans shuffle-bound).  Lanes whose DPP source is outside the
+// pattern (or whose row is masked off) receive `old`.
+template <int CTRL, int ROW_MASK, class S>
+__device__ inline S dpp_state(const S& v, const S& old) {
     static_assert(sizeof(S) % 4 == 0, "scan state must be a multiple of 4 bytes");
     constexpr int W = sizeof(S) / 4;
     S r;
-    const int* src = reinterpret_cast<const int*>(&v);
-    int* dst = reinterpret_cast<int*>(&r);
+    const int* a = reinterpret_cast<const int*>(&v);
+    const int* o = reinterpret_cast<const int*>(&old);
+    int* d = reinterpret_cast<int*>(&r);
 #pragma unroll
-    for (int k = 0; k < W; ++k) dst[k] = __shfl_up(src[k], delta);
+    for (int k = 0; k < W; ++k) d[k] = __builtin_amdgcn_update_dpp(o[k], a[k], CTRL, ROW_MASK, 0xf, false);
     return r;
+}
+template <class S>
+__device__ inline S readlane_state(const S& v, int lane) {
+    constexpr int W = sizeof(S) / 4;
+    S r;
+    const int* a = reinterpret_cast<const int*>(&v);
+    int* d = reinterpret_cast<int*>(&r);
+#pragma unroll
+    for (int k = 0; k < W; ++k) d[k] = __builtin_amdgcn_readlane(a[k], lane);
+    return r;
+}
+// DPP controls (GFX9 family, wave64): row_shr:n = 0x110+n, row_bcast:15 = 0x142, row_bcast:31 = 0x143,
+// wave_shr:1 = 0x138
+// Inclusive ordered scan of one state per lane across the 64-lane wave: 4 row_shr steps inside each
+// 16-lane row, then row 0/2's last lane into rows 1/3 and lane 31 into rows 2/3.
+template <class Op>
+__device__ inline typename Op::S wave_incl_scan(const Op& op, typename Op::S x) {
+    using S = typename Op::S;
+    const S id = op.identity();
+    x = op.combine(dpp_state<0x111, 0xf>(x, id), x);
+    x = op.combine(dpp_state<0x112, 0xf>(x, id), x);
+    x = op.combine(dpp_state<0x114, 0xf>(x, id), x);
+    x = op.combine(dpp_state<0x118, 0xf>(x, id), x);
+    x = op.combine(dpp_state<0x142, 0xa>(x, id), x);
+    x = op.combine(dpp_state<0x143, 0xc>(x, id), x);
+    return x;
+}
+// the previous lane's value (lane 0: identity)
+template <class Op>
+__device__ inline typename Op::S wave_shift_up1(const Op& op, const typename Op::S& x) {
+    return dpp_state<0x138, 0xf>(x, op.identity());
 }
 
 // Block-wide exclusive scan: 64-lane shuffle scan per wave (no LDS round trips), then one LDS slot per
@@ -37,14 +72,8 @@ __device__ inline typename Op::S block_exclusive_scan(const Op& op, typename Op:
     constexpr int NW = BLOCK / WAVE;
     const int lane = __lane_id();
     const int w = threadIdx.x / WAVE;
-    S x = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        S y = shfl_up_state(x, o);
-        if (lane >= o) x = op.combine(y, x);
-    }
-    S ex_w = shfl_up_state(x, 1);
-    if (lane == 0) ex_w = op.identity();
+    const S x = wave_incl_scan(op, v);
+    S ex_w = wave_shift_up1(op, x);
     if (lane == WAVE - 1) lds[w] = x;
     __syncthreads();
     S pre = op.identity();
@@ -60,29 +89,8 @@ __device__ inline typename Op::S block_exclusive_scan(const Op& op, typename Op:
 
 // Wave-striped tiles: wave w of a block owns 64 * ITEMS consecutive elements; in round k lane l holds
 // element wbase + 64k + l, so every load/store instruction of a wave touches 64 consecutive elements
-// (coalesced).  Order is preserved: each round is an ordered 64-lane shuffle scan, rounds are folded in
-// order, waves in wave order (the ops are associative, not commutative).
-template <class Op>
-__device__ inline typename Op::S wave_incl_scan(const Op& op, typename Op::S x) {
-    const int lane = __lane_id();
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        typename Op::S y = shfl_up_state(x, o);
-        if (lane >= o) x = op.combine(y, x);
-    }
-    return x;
-}
-template <class S>
-__device__ inline S shfl_state(const S& v, int src) {
-    constexpr int W = sizeof(S) / 4;
-    S r;
-    const int* a = reinterpret_cast<const int*>(&v);
-    int* d = reinterpret_cast<int*>(&r);
-#pragma unroll
-    for (int k = 0; k < W; ++k) d[k] = __shfl(a[k], src);
-    return r;
-}
-
+// (coalesced).  Order is preserved: each round is an ordered 64-lane scan, rounds are folded in order,
+// waves in wave order (the ops are associative, not commutative).
 template <class Op, int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename Op::S* agg) {
     using S = typename Op::S;
@@ -95,7 +103,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename
     for (int k = 0; k < ITEMS; ++k) {
         const size_t i = wbase + (size_t)k * WAVE + lane;
         S x = wave_incl_scan(op, i < n ? op.load(i) : op.identity());
-        acc = op.combine(acc, shfl_state(x, WAVE - 1));
+        acc = op.combine(acc, readlane_state(x, WAVE - 1));
     }
     if (lane == 0) lds[w] = acc;
     __syncthreads();
@@ -137,7 +145,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_apply(Op op, size_t n, const typ
         const size_t i = wbase + (size_t)k * WAVE + lane;
         el[k] = i < n ? op.load(i) : op.identity();
         x[k] = wave_incl_scan(op, el[k]);
-        acc = op.combine(acc, shfl_state(x[k], WAVE - 1));
+        acc = op.combine(acc, readlane_state(x[k], WAVE - 1));
     }
     if (lane == 0) lds[w] = acc;
     __syncthreads();
@@ -146,11 +154,10 @@ __global__ __launch_bounds__(BLOCK) void k_scan_apply(Op op, size_t n, const typ
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
         const size_t i = wbase + (size_t)k * WAVE + lane;
-        S prev = shfl_up_state(x[k], 1);
-        const S ex = lane == 0 ? carry : op.combine(carry, prev);
+        const S ex = op.combine(carry, wave_shift_up1(op, x[k]));
         const S inc = op.combine(carry, x[k]);
         if (i < n) op.store(i, ex, inc, el[k]);
-        carry = op.combine(carry, shfl_state(x[k], WAVE - 1));
+        carry = op.combine(carry, readlane_state(x[k], WAVE - 1));
     }
 }
 
