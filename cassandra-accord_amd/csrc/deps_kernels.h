@@ -544,6 +544,18 @@ struct OffsetsOp {
     uint32_t* o_key_off[NVC];
     uint32_t* o_ent_off[NVC];
     uint32_t* o_k2t_off[NVC];
+    // fused per-txn layout (k_txn_layout's work) into output buffers allocated by an earlier batch:
+    // written only where the txn's rows fit the current capacities, else *overflow is raised and the
+    // caller runs k_txn_layout after sizing the buffers (layout == 0: offsets only)
+    int layout;
+    const uint64_t* keys;
+    const uint64_t* vi_key;
+    uint64_t* out_keys[NVC];
+    int32_t* out_k2t[NVC];
+    uint32_t cap_keys[NVC], cap_k2t[NVC];
+    uint32_t* dst;                // AoS by pair: last k2t slot of the pair's run
+    uint32_t* vdst;
+    uint32_t* overflow;
 
     __device__ S identity() const {
         S s;
@@ -572,7 +584,7 @@ struct OffsetsOp {
         for (int c = 0; c < NVC; ++c) { r.k[c] = x.k[c] + y.k[c]; r.e[c] = x.e[c] + y.e[c]; }
         return r;
     }
-    __device__ void store(size_t t, const S& ex, const S& inc, const S&) const {
+    __device__ void store(size_t t, const S& ex, const S& inc, const S& el) const {
 #pragma unroll
         for (int c = 0; c < NVC; ++c) {
             o_key_off[c][t] = ex.k[c];
@@ -582,6 +594,30 @@ struct OffsetsOp {
                 o_key_off[c][n] = inc.k[c];
                 o_ent_off[c][n] = inc.e[c];
                 o_k2t_off[c][n] = inc.k[c] + inc.e[c];
+            }
+        }
+        if (!layout) return;
+        const bool large = meta[t] & META_LARGE;
+        const uint32_t b = large ? voff[t] : key_off[t], e = large ? voff[t + 1] : key_off[t + 1];
+        const uint32_t* src = large ? vcnt : cnt;
+        uint32_t* d = large ? vdst : dst;
+        for (int c = 0; c < NVC; ++c) {
+            const uint32_t nk = el.k[c];
+            if (nk == 0) continue;
+            const uint32_t kb = ex.k[c], mb = ex.k[c] + ex.e[c];
+            if (kb + nk > cap_keys[c] || mb + nk + el.e[c] > cap_k2t[c]) {
+                if (*(volatile uint32_t*)overflow == 0u) *(volatile uint32_t*)overflow = 1u;
+                continue;
+            }
+            uint32_t run = nk, kk = 0;
+            for (uint32_t x = b; x < e; ++x) {
+                const uint32_t cc = src[(size_t)x * NVC + c];
+                if (cc == 0) continue;
+                out_keys[c][kb + kk] = large ? vi_key[x] : keys[x];
+                d[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
+                run += cc;
+                out_k2t[c][mb + kk] = (int32_t)run;
+                ++kk;
             }
         }
     }

@@ -350,12 +350,28 @@ void launch_range(const RangeArgs& a, bool fill, hipStream_t st) {
         default: F<8>(__VA_ARGS__); break;           \
     }
 
+// Capacity (elements) of CSR block `block`'s data buffers as currently allocated (0 if none).
+size_t csr_cap(ad_handle* h, size_t block, int which, size_t elem) {
+    const size_t slot = S_CSR0 + 10 * block + which;
+    return slot < h->bufs.size() ? h->bufs[slot].cap / elem : 0;
+}
+
+// Offsets of every key-class CSR in one scan; with buffers left by an earlier batch, also the per-txn
+// layout (fused; *overflow reports rows that did not fit, then k_txn_layout runs after sizing).
 template <int NV>
-void launch_offsets(ad_handle* h, const TxnArgs& ta) {
-    OffsetsOp<2 * NV> op;
+void launch_offsets(ad_handle* h, const TxnArgs& ta, uint32_t* overflow) {
+    OffsetsOp<2 * NV> op{};
     op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt; op.voff = h->voff; op.vcnt = h->vcnt;
+    op.layout = 1;
+    op.keys = h->keys; op.vi_key = h->vi_key; op.dst = h->dst; op.vdst = h->vdst; op.overflow = overflow;
     for (int c = 0; c < 2 * NV; ++c) {
         op.o_key_off[c] = h->deps[c].key_off; op.o_ent_off[c] = h->deps[c].ent_off; op.o_k2t_off[c] = h->deps[c].k2t_off;
+        const size_t base = S_CSR0 + 10 * (size_t)c;
+        const size_t ck = csr_cap(h, c, 4, 8), cm = csr_cap(h, c, 5, 4);
+        op.out_keys[c] = ck ? (uint64_t*)h->bufs[base + 4].p : nullptr;
+        op.out_k2t[c] = cm ? (int32_t*)h->bufs[base + 5].p : nullptr;
+        op.cap_keys[c] = (uint32_t)std::min<size_t>(ck, 0xFFFFFFFFu);
+        op.cap_k2t[c] = (uint32_t)std::min<size_t>(cm, 0xFFFFFFFFu);
     }
     device_scan(op, h->n, (typename OffsetsOp<2 * NV>::S*)h->scratch, h->st);
     (void)ta;
@@ -409,9 +425,11 @@ int stage_deps(ad_handle* h) {
     ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt = h->cnt;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
+    uint32_t* overflow = h->totd + MAX_TOTALS - 1;       // fused-layout overflow flag (read with the totals)
     if (n > 0) {
+        HIPCHK(h, hipMemsetAsync(overflow, 0, 4, st));
         KScope ks(K_SCAN_OFFSETS, n);
-        NV_DISPATCH(nv, launch_offsets, h, ta);
+        NV_DISPATCH(nv, launch_offsets, h, ta, overflow);
     } else {
         for (int vc = 0; vc < nvc; ++vc) csr_offsets(h, h->deps[vc], h->nk, h->ne);
     }
@@ -434,7 +452,12 @@ int stage_deps(ad_handle* h) {
         tt.src[3 * c + 0] = x.key_off + n; tt.src[3 * c + 1] = x.k2t_off + n; tt.src[3 * c + 2] = x.ent_off + n;
         tt.count = 3 * c + 3;
     }
-    CK(read_totals_params(h, tt, tot.data()));
+    const int ncol = tt.count;
+    tt.src[tt.count++] = overflow;
+    std::vector<uint32_t> got(tt.count, 0);
+    CK(read_totals_params(h, tt, got.data()));
+    std::copy(got.begin(), got.begin() + ncol, tot.begin());
+    const bool fused_layout = n > 0 && got[ncol] == 0;
     CK(check_params(h));
     h->deps_entries = 0;
     for (int c = 0; c < ncsr; ++c) {
@@ -452,7 +475,7 @@ int stage_deps(ad_handle* h) {
         }
     }
     // ---- fill
-    if (n > 0) { KScope ks(K_TXN_LAYOUT, P); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
+    if (n > 0 && !fused_layout) { KScope ks(K_TXN_LAYOUT, P); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
     NV_DISPATCH(nv, launch_walk, wa, true, st);
     if (Q > 0 && n > 0) NV_DISPATCH(nv, launch_range, ra, true, st);
     UnionArgs ua{};

@@ -20,11 +20,12 @@ def _assert_csr(name, got, want):
                                                                       want.txn(i) if i is not None and i < want.n else None))
 
 
-def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, levels=True, fixpoint=False):
+def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, levels=True, fixpoint=False, eng=None):
     cfg = abi.make_config(window, replicas, drop_p, seed)
     flags = O.FLAG_MERGE | (O.FLAG_LEVELS if levels else 0)
     ref = O.OracleResult(batch, cfg, flags)
-    eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
+    if eng is None:
+        eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
     if fixpoint:
         eng.set_level_mode(True)
     eng.load(batch)
@@ -55,6 +56,18 @@ def test_levels_kahn_and_fixpoint(engine_factory, keyspace, n, fixpoint):
     # must give the oracle's levels and order (the denser keyspaces give deeper graphs, up to long chains)
     b = workload.generate(n, keys_per_txn=4, keyspace=keyspace, seed=keyspace % 97 + n)
     check(engine_factory, b, fixpoint=fixpoint)
+
+
+def test_repeated_batches_one_engine(engine_factory):
+    # a handle reuses its device buffers across batches: the deps offsets scan then also lays out the
+    # per-txn CSR rows in place (fused), falling back to the separate layout kernel when a batch outgrows
+    # the buffers; every batch must still match the oracle
+    eng = engine_factory()
+    batches = [workload.config("C2", n=20000), workload.config("C3", n=20000, seed=5),
+               workload.config("C2", n=60000, seed=6), workload.config("C2", n=20000),
+               workload.generate(3000, keys_per_txn=1, keyspace=40, seed=8)]
+    for b in batches:
+        check(engine_factory, b, eng=eng)
 
 
 def test_c3_more_views_no_drop(engine_factory):
