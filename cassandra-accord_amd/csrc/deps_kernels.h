@@ -236,7 +236,7 @@ struct ElideOp {
     int32_t* ud_prev;
     uint64_t* pm_w;
     uint64_t* pm_c;
-    uint32_t* uidx;          // distinct-key index of each entry
+    uint32_t* nh;            // non-head entries (entries with an earlier entry of their key), in order
     uint64_t* ukey;          // [U] distinct keys (raw u64)
     uint32_t* useg;          // [U+1] segment starts
     uint64_t key_min;
@@ -276,6 +276,8 @@ struct ElideOp {
         if (el.head) {
             ukey[u] = (uint64_t)skey[i] + key_min;
             useg[u] = (uint32_t)i;
+        } else {
+            nh[i - inc.hc] = (uint32_t)i;     // (i + 1 - hc) non-heads so far, this one included
         }
         if (i + 1 == n) {
             useg[inc.hc] = (uint32_t)n;
@@ -296,6 +298,8 @@ struct WalkArgs {
     const uint8_t* meta;      // per txn
     const uint32_t* gid;      // sharded batches: local row -> global arrival rank (nullable = identity)
     size_t P;
+    const uint32_t* nh;       // non-head entries (ElideOp), P - n_keys_u of them: the only ones with deps
+    const Params* prm;
     uint32_t window;
     uint32_t thresh;
     uint64_t seed;
@@ -382,14 +386,15 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, in
 }
 
 // Real pairs of small key txns, one thread per sorted entry (neighbouring threads walk one segment).
+// One thread per non-head entry (a key segment's first entry has nothing before it: no deps, and its
+// counts stay at the zeros the caller cleared).  The list is dense, so the active threads fill whole
+// waves (a grid over all P entries left ~5 of 6 lanes idle in every wave of this latency-bound walk).
 template <int NV, bool FILL>
 __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
-    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.P) return;
-    // a key segment's first entry has nothing before it: no deps, and its counts stay at the zeros the
-    // caller cleared (so only pairs with earlier entries touch their random AoS slots)
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= a.P - a.prm->n_keys_u) return;
+    const size_t s = a.nh[x];
     const int seg0 = a.seg_start[s];
-    if (seg0 == (int)s) return;
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
     const uint32_t qk = meta_kind(mi);
@@ -663,6 +668,21 @@ __device__ inline uint32_t union_lists(int32_t* __restrict__ k2t, const uint32_t
     return u;
 }
 
+template <int KM>
+__device__ inline uint32_t union_small(int32_t* __restrict__ k2t, uint32_t mb, uint32_t nk, uint32_t* __restrict__ out) {
+    uint32_t lo[KM], hi[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        if (k < (int)nk) {
+            lo[k] = mb + (k == 0 ? nk : (uint32_t)k2t[mb + k - 1]);
+            hi[k] = mb + (uint32_t)k2t[mb + k];
+        } else {
+            lo[k] = hi[k] = 0;
+        }
+    }
+    return union_lists<KM>(k2t, lo, hi, (int)nk, out);
+}
+
 struct UnionArgs {
     size_t n;
     int nvc;
@@ -685,15 +705,17 @@ __global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
         if (nk == 0) { a.tcnt[vc][t] = 0; continue; }
         const uint32_t mb = a.k2t_off[vc][t];
         int32_t* k2t = a.k2t[vc];
-        uint32_t lo[KMAX], hi[KMAX];
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            if (k < (int)nk) {
-                lo[k] = mb + (k == 0 ? nk : (uint32_t)k2t[mb + k - 1]);
-                hi[k] = mb + (uint32_t)k2t[mb + k];
-            }
+        uint32_t* out = a.txns[vc] + a.ent_off[vc][t];
+        if (nk == 1) {                 // one key: its list is already sorted and unique
+            const uint32_t b = mb + 1, e = mb + (uint32_t)k2t[mb];
+            for (uint32_t q = b; q < e; ++q) { out[q - b] = (uint32_t)k2t[q]; k2t[q] = (int32_t)(q - b); }
+            a.tcnt[vc][t] = e - b;
+            continue;
         }
-        a.tcnt[vc][t] = union_lists<KMAX>(k2t, lo, hi, (int)nk, a.txns[vc] + a.ent_off[vc][t]);
+        // register K-way merge sized to the key count (C2/C3 txns: 4 keys)
+        if (nk <= 4) a.tcnt[vc][t] = union_small<4>(k2t, mb, nk, out);
+        else if (nk <= 8) a.tcnt[vc][t] = union_small<8>(k2t, mb, nk, out);
+        else a.tcnt[vc][t] = union_small<KMAX>(k2t, mb, nk, out);
     }
 }
 

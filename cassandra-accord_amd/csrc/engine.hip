@@ -56,6 +56,8 @@ struct ad_handle {
     Params hprm{};
     uint32_t* totd = nullptr;          // device: gathered CSR totals (read_totals_params)
     int level_mode = AD_LEVELS_AUTO;
+    size_t mrange_zero_n = ~(size_t)0;   // merged RangeDeps offsets known zero for this n / buffer
+    const uint32_t* mrange_zero_p = nullptr;
     TsPack pack{};
     int key_bits = 0, range_bits = 0;
     uint64_t rbase = 0, wmax = 0;
@@ -65,7 +67,7 @@ struct ad_handle {
     PairRec* prec = nullptr;
     uint32_t *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;
     uint32_t *skey = nullptr, *sval = nullptr;           // sorted (alias ka/kb)
-    uint32_t *e_txn = nullptr, *uidx = nullptr, *useg = nullptr;
+    uint32_t *e_txn = nullptr, *nh = nullptr, *useg = nullptr;   // nh: non-head entries
     uint64_t* ukey = nullptr;
     uint8_t* e_meta = nullptr;
     uint64_t *e_exec1 = nullptr, *pm_w = nullptr, *pm_c = nullptr;
@@ -387,7 +389,7 @@ int stage_deps(ad_handle* h) {
     if (P > 0) {
         { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->e_txn, h->e_meta, h->e_exec1); }
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
-                    h->uidx, h->ukey, h->useg, h->hprm.key_min, P, h->prm};
+                    h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm};
         KScope ks(K_SCAN_ELIDE, P);
         device_scan(eop, P, (ElideOp::S*)h->scratch, st);
     }
@@ -417,6 +419,7 @@ int stage_deps(ad_handle* h) {
     wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
     wa.gid = h->sharded ? h->gid : nullptr;
+    wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
     if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt, 0, (size_t)nvc * P * 4, st));   // segment heads keep zero counts
@@ -609,11 +612,17 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
             Csr& m = h->merged[cls];
             CK(alloc_csr(h, CSR_MERGED0 + cls, m, n));
             m.nkeys = m.nk2t = m.ncap = 0;
-            HIPCHK(h, hipMemsetAsync(m.key_off, 0, (n + 1) * 4, h->st));
-            HIPCHK(h, hipMemsetAsync(m.ent_off, 0, (n + 1) * 4, h->st));
-            HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, (n + 1) * 4, h->st));
+            // an empty merged RangeDeps: zero offsets, kept from the previous batch when still valid
+            if (h->mrange_zero_n != n || h->mrange_zero_p != m.key_off) {
+                HIPCHK(h, hipMemsetAsync(m.key_off, 0, (n + 1) * 4, h->st));
+                HIPCHK(h, hipMemsetAsync(m.ent_off, 0, (n + 1) * 4, h->st));
+                HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, (n + 1) * 4, h->st));
+                h->mrange_zero_n = n;
+                h->mrange_zero_p = m.key_off;
+            }
             continue;
         }
+        if (cls == AD_CLASS_RANGE) h->mrange_zero_p = nullptr;     // about to be written
         out[K] = &h->merged[cls];
         blocks[K] = CSR_MERGED0 + cls;
         kw[K] = cls == AD_CLASS_RANGE ? 2 : 1;
@@ -681,7 +690,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_exec_levels needs ad_preaccept_deps on this batch (its key chains)");
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.sval = h->sval; li.nh = h->nh; li.prm = h->prm; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.merged_key = &h->merged[AD_CLASS_KEY];
     li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
@@ -826,7 +835,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     CK(dalloc(h, S_ETXN, &h->e_txn, P)); CK(dalloc(h, S_EMETA, &h->e_meta, P));
     CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
     CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
-    CK(dalloc(h, S_UIDX, &h->uidx, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
+    CK(dalloc(h, S_UIDX, &h->nh, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
     CK(dalloc(h, S_CNT, &h->cnt, (size_t)nvc * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
     CK(dalloc(h, S_NK, &h->nk, (size_t)nvc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nvc * n + n));
     CK(dalloc(h, S_VN, &h->vn, n)); CK(dalloc(h, S_VOFF, &h->voff, n + 1));
@@ -1324,7 +1333,7 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     else if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
     LevelInputs li{};
     li.n = n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.sval = h->sval; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.sval = h->sval; li.nh = h->nh; li.prm = h->prm; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;
     li.n_large = 0;

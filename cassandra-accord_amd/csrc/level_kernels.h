@@ -443,52 +443,147 @@ __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __
 //            earlier Write, for every earlier entry (all Reads).
 // so each position's successors are one contiguous run of its chain: after a Write, the Reads that follow
 // it (or the next Write if a Write follows directly); after a Read, the next Write.  Same chain order and
-// rule as the fixpoint walk, so the levels are identical.
+// rule as the fixpoint walk, so the levels are identical.  k_chain_build derives both per segment.
 // ---------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_kahn_prep(size_t P, const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
-                                                   const uint32_t* __restrict__ c_pair, const int32_t* __restrict__ seg_start,
-                                                   const uint32_t* __restrict__ seg_len, uint32_t* __restrict__ indeg,
-                                                   uint2* __restrict__ succ) {
-    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= P) return;
-    const size_t h = (size_t)seg_start[q];
-    const size_t end = h + seg_len[h];
-    if (end - h < 2) return;                 // single-entry chain: no edges (succ was cleared)
-    uint2 sc = make_uint2(0u, 0u);
-    {
-        const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
-        uint32_t reads = 0;
-        bool pw = false;
-        for (size_t x = q; x > h;) {
-            --x;
-            if (meta_kind(c_meta[x]) == AD_KIND_WRITE) { pw = true; break; }
-            ++reads;
-        }
-        const uint32_t pc = wr ? (reads > 0 ? reads : (pw ? 1u : 0u)) : (pw ? 1u : 0u);
-        if (pc) atomicAdd(&indeg[c_txn[q]], pc);
-        if (q + 1 < end) {
-            if (wr && meta_kind(c_meta[q + 1]) == AD_KIND_WRITE) {
-                sc = make_uint2((uint32_t)(q + 1), 1u);
-            } else {
-                size_t x = q + 1;
-                while (x < end && meta_kind(c_meta[x]) != AD_KIND_WRITE) ++x;
-                if (wr) sc = make_uint2((uint32_t)(q + 1), (uint32_t)(x - (q + 1)));   // the Reads after W
-                else if (x < end) sc = make_uint2((uint32_t)x, 1u);                     // the next Write
+// Register version of the chain build for segments of at most CB_REG entries (C2: all multi-entry
+// segments): odd-even transposition sort on (executeAt, arrival) in registers, both passes unrolled, and
+// only c_txn (what the wavefronts read) is written back.
+constexpr int CB_REG = 8;
+__device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                        const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                        uint32_t* __restrict__ c_txn, uint32_t* __restrict__ indeg, uint2* __restrict__ succ) {
+    uint64_t k[CB_REG];
+    uint32_t t[CB_REG], pr[CB_REG], wr[CB_REG], ord[CB_REG];
+#pragma unroll
+    for (int i = 0; i < CB_REG; ++i) {
+        const bool v = i < len;
+        k[i] = v ? e_exec1[s + i] : ~0ull;
+        t[i] = v ? e_txn[s + i] : 0u;
+        pr[i] = v ? sval[s + i] : 0u;
+        wr[i] = v ? (meta_kind(e_meta[s + i]) == AD_KIND_WRITE ? 1u : 0u) : 0u;
+        ord[i] = (uint32_t)i;
+    }
+#pragma unroll
+    for (int r = 0; r < CB_REG; ++r) {
+#pragma unroll
+        for (int i = r & 1; i + 1 < CB_REG; i += 2) {
+            const bool sw = k[i] > k[i + 1] || (k[i] == k[i + 1] && ord[i] > ord[i + 1]);
+            if (sw) {
+                uint64_t a = k[i]; k[i] = k[i + 1]; k[i + 1] = a;
+                uint32_t b = t[i]; t[i] = t[i + 1]; t[i + 1] = b;
+                b = pr[i]; pr[i] = pr[i + 1]; pr[i + 1] = b;
+                b = wr[i]; wr[i] = wr[i + 1]; wr[i + 1] = b;
+                b = ord[i]; ord[i] = ord[i + 1]; ord[i + 1] = b;
             }
         }
     }
-    succ[c_pair[q]] = sc;
+    bool seen_w = false;
+    uint32_t reads = 0;
+#pragma unroll
+    for (int q = 0; q < CB_REG; ++q) {
+        if (q < len) {
+            c_txn[s + q] = t[q];
+            const uint32_t pc = wr[q] ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
+            if (pc) atomicAdd(&indeg[t[q]], pc);
+            if (wr[q]) { seen_w = true; reads = 0; } else ++reads;
+        }
+    }
+    int next_w = len;
+#pragma unroll
+    for (int q = CB_REG - 1; q >= 0; --q) {
+        if (q < len) {
+            uint2 sc = make_uint2(0u, 0u);
+            if (wr[q]) {
+                if (q + 1 < len) sc = next_w == q + 1 ? make_uint2((uint32_t)(s + q + 1), 1u)
+                                                      : make_uint2((uint32_t)(s + q + 1), (uint32_t)(next_w - (q + 1)));
+                next_w = q;
+            } else if (next_w < len) {
+                sc = make_uint2((uint32_t)(s + next_w), 1u);
+            }
+            succ[pr[q]] = sc;
+        }
+    }
+}
+
+// Kahn path chain build, one thread per multi-entry key segment (fuses k_chain_copy, k_chain_order,
+// k_seg_table and k_kahn_prep): the segment is copied into executeAt order (stable insertion: entries
+// arrive in TxnId order and only slow-path ones move), then a forward pass counts each position's reduced
+// predecessors (indeg) and a backward pass gives its successor run (succ[pair]).  Single-entry segments
+// have no edges and are skipped; a segment longer than SHORT_SEG raises *any_long and the caller falls
+// back to the fixpoint (whose chain preparation handles long chains).
+// One thread per non-head entry (ElideOp's dense list); the second entry of each segment builds it.
+__global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
+                                                     const int32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                                     const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                                     uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                                     uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
+                                                     uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
+                                                     uint32_t* __restrict__ any_long) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool lng = false;
+    const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
+    const size_t s = s2 - 1;
+    if (s2 > 0 && seg_start[s2] == (int32_t)s) {
+        size_t end = s + 2;
+        while (end < P && seg_start[end] == (int32_t)s && end - s <= SHORT_SEG) ++end;
+        if (end - s > SHORT_SEG) {
+            lng = true;
+        } else if (end - s <= CB_REG) {
+            chain_build_regs(s, (int)(end - s), e_txn, e_meta, e_exec1, sval, c_txn, indeg, succ);
+        } else {
+            for (size_t x = s; x < end; ++x) {
+                const uint64_t kx = e_exec1[x];
+                const uint32_t tx = e_txn[x], px = sval[x];
+                const uint8_t mx = e_meta[x];
+                size_t y = x;
+                while (y > s && c_exec1[y - 1] > kx) {
+                    c_exec1[y] = c_exec1[y - 1]; c_txn[y] = c_txn[y - 1]; c_meta[y] = c_meta[y - 1]; c_pair[y] = c_pair[y - 1];
+                    --y;
+                }
+                c_exec1[y] = kx; c_txn[y] = tx; c_meta[y] = mx; c_pair[y] = px;
+            }
+            // predecessors: a Read waits for the last Write before it; a Write for the Reads since the last
+            // Write, else for that Write (k_kahn_prep states the reduction)
+            bool seen_w = false;
+            uint32_t reads = 0;
+            for (size_t q = s; q < end; ++q) {
+                const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
+                const uint32_t pc = wr ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
+                if (pc) atomicAdd(&indeg[c_txn[q]], pc);
+                if (wr) { seen_w = true; reads = 0; } else ++reads;
+            }
+            // successors: after a Write the Reads that follow it (or the next Write if one follows
+            // directly); after a Read the next Write
+            size_t next_w = end;
+            for (size_t q = end; q-- > s;) {
+                const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
+                uint2 sc = make_uint2(0u, 0u);
+                if (wr) {
+                    if (q + 1 < end) sc = next_w == q + 1 ? make_uint2((uint32_t)(q + 1), 1u)
+                                                          : make_uint2((uint32_t)(q + 1), (uint32_t)(next_w - (q + 1)));
+                    next_w = q;
+                } else if (next_w < end) {
+                    sc = make_uint2((uint32_t)next_w, 1u);
+                }
+                succ[c_pair[q]] = sc;
+            }
+        }
+    }
+    wave_set_flag(lng, any_long);
 }
 
 // One wavefront: the txns released at level `lvl` (level 0: indeg == 0 in the snapshot; later levels:
 // L == lvl, which only a release sets) release their successors; the last release of S sets L[S] = lvl+1.
 // prev: the previous wavefront's "released something" flag (nullptr: run); *work: this one released some.
+// gate: the previous wavefront's "released something" flag (run if set), or for the first wavefront of a
+// batch (gate_is_abort) the chain build's long-chain flag (run if clear).
 __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
                                                    uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
                                                    const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
-                                                   const uint32_t* __restrict__ c_txn, const uint32_t* prev,
+                                                   const uint32_t* __restrict__ c_txn, const uint32_t* gate, int gate_is_abort,
                                                    uint32_t* __restrict__ work) {
-    if (prev && *prev == 0u) return;
+    if (gate_is_abort ? *gate != 0u : *gate == 0u) return;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool released = false;
     if (t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl)) {
@@ -543,6 +638,8 @@ struct LevelInputs {
     const uint64_t* e_exec1;
     const int32_t* seg_start;
     const uint32_t* sval;                // sorted position -> pair
+    const uint32_t* nh;                  // non-head entries (ElideOp), P - prm->n_keys_u of them
+    const Params* prm;
     const uint32_t* key_off;
     const uint8_t* meta;
     const uint64_t* ex1;
@@ -764,34 +861,19 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         ea.cons_pos = ls.cons_pos; ea.pm_all = ls.pm_all; ea.ukey = in.ukey; ea.useg = in.useg; ea.U = in.U;
         ea.c_exec1 = ls.c_exec1; ea.c_txn = ls.c_txn; ea.seg_start = in.seg_start;
         uint32_t host[8] = {0};
-        const bool reuse = in.keep_levels && ls.chains_ready;
-        if (P > 0 && reuse) {
-            k_stamp_reset<<<ceil_div((long)std::max<uint32_t>(ls.nheads, 1), 256), 256, 0, st>>>(ls.heads, ls.nheads, ls.stamp);
-        } else if (P > 0) {
-            KScope ks(K_CHAIN_PREP);
-            k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-            k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-            k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp, ls.flags + 7);
-        }
-        bool kahn = false;
-        if (!reuse) {
-            // one sync: unsupported kinds, and whether the Kahn wavefront applies (no long chain, no (b)/(c))
-            hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st);
-            if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
-            if (host[5]) {
-                err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
-                return AD_ERR_UNSUPPORTED;
-            }
-            kahn = in.kahn_ok && !in.keep_levels && !has_b && !has_c && host[7] == 0 && P > 0;
-        }
-        if (kahn) {
+        // ---- Kahn wavefront (short-chain key batches): chain build + wavefronts with no decision sync;
+        // the first batch's readback also carries the kinds / long-chain flags, and a long chain found by
+        // the build sends the batch to the fixpoint below
+        if (in.kahn_ok && !in.keep_levels && !has_b && !has_c && P > 0) {
             ls.chains_ready = false;
             int lv = 0;
+            bool fallback = false;
             {
                 KScope ks(K_KAHN);
                 hipMemsetAsync(ls.indeg, 0, n * 4, st);
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
-                k_kahn_prep<<<gP, 256, 0, st>>>(P, ls.c_txn, ls.c_meta, ls.c_pair, in.seg_start, ls.seg_len, ls.indeg, ls.succ);
+                k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
+                                                  ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7);
                 hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
                 // wavefronts per launch batch, no host sync inside a batch (a wavefront after the last
                 // one exits at once); the first batch covers typical uniform-key depths (C2: 10)
@@ -803,12 +885,20 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     hipMemsetAsync(ls.iflags, 0, KB * 4, st);
                     for (int k = 0; k < KB; ++k)
                         k_kahn_step<<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ, ls.c_txn,
-                                                        k == 0 ? nullptr : ls.iflags + (k - 1), ls.iflags + k);
+                                                        k == 0 ? ls.flags + 7 : ls.iflags + (k - 1), k == 0, ls.iflags + k);
                     uint32_t fh[KB_MAX];
                     if (hipMemcpyAsync(fh, ls.iflags, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        (lv == 0 && hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess) ||
                         hipStreamSynchronize(st) != hipSuccess) {
                         err = "exec levels: device error";
                         return AD_ERR_DEVICE;
+                    }
+                    if (lv == 0) {
+                        if (host[5]) {
+                            err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                            return AD_ERR_UNSUPPORTED;
+                        }
+                        if (host[7]) { fallback = true; break; }
                     }
                     int k = 0;
                     while (k < KB && fh[k]) ++k;
@@ -817,9 +907,22 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     more = false;
                 }
             }
-            *iters = lv;
-            if (want_order && n > 0) order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
-            return AD_OK;
+            if (!fallback) {
+                *iters = lv;
+                if (want_order && n > 0) order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
+                return AD_OK;
+            }
+            hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
+        }
+        // ---- chain fixpoint
+        const bool reuse = in.keep_levels && ls.chains_ready;
+        if (P > 0 && reuse) {
+            k_stamp_reset<<<ceil_div((long)std::max<uint32_t>(ls.nheads, 1), 256), 256, 0, st>>>(ls.heads, ls.nheads, ls.stamp);
+        } else if (P > 0) {
+            KScope ks(K_CHAIN_PREP);
+            k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+            k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+            k_seg_table<<<gP, 256, 0, st>>>(P, in.seg_start, ls.seg_len, ls.stamp, ls.flags + 7);
         }
         if (P > 0 && !reuse) {
             KScope ks(K_CHAIN_PREP);
