@@ -56,6 +56,7 @@ def lib():
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ad_run_pipeline.argtypes = [vp]
+        L.ad_fetch_levels.argtypes = [vp, vp, vp]
         L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
         L.ad_set_trace.argtypes = [vp, C.c_uint64]
         L.ad_set_level_mode.argtypes = [vp, C.c_int]
@@ -72,7 +73,7 @@ def lib():
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
             "ad_fetch_deps", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
-            "ad_run_pipeline", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
+            "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_blob_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_allgather", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
@@ -173,6 +174,13 @@ class DepsEngine:
 
     def run_pipeline(self):
         self._check(lib().ad_run_pipeline(self.h), "ad_run_pipeline")
+
+    def fetch_levels(self):
+        """(levels, order) left on the device by the last run_pipeline / exec_levels."""
+        lv = np.zeros(max(self.n, 1), np.uint32)
+        order = np.zeros(max(self.n, 1), np.uint32)
+        self._check(lib().ad_fetch_levels(self.h, lv.ctypes.data, order.ctypes.data), "ad_fetch_levels")
+        return lv[:self.n], order[:self.n]
 
     def last_times(self):
         t = abi.AdStageTimes()

@@ -56,6 +56,8 @@ struct ad_handle {
     Params hprm{};
     uint32_t* totd = nullptr;          // device: gathered CSR totals (read_totals_params)
     int level_mode = AD_LEVELS_AUTO;
+    bool order_pending = false;          // optimistic order issued; order_bad valid after a stream sync
+    uint32_t order_bad = 0;
     size_t mrange_zero_n = ~(size_t)0;   // merged RangeDeps offsets known zero for this n / buffer
     const uint32_t* mrange_zero_p = nullptr;
     TsPack pack{};
@@ -699,6 +701,10 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.n_large = h->n_large;
     li.exec_bits = h->pack.total_bits;
     li.kahn_ok = h->level_mode == AD_LEVELS_AUTO ? 1 : 0;
+    h->order_pending = false;
+    h->order_bad = 0;
+    li.order_verify = &h->order_bad;
+    li.order_pending = &h->order_pending;
     int iters = 0;
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
     if (rc != AD_OK) return rc;
@@ -959,16 +965,39 @@ int ad_merge_host(ad_handle* h, const ad_csr_in* parts, uint32_t r, ad_csr_sizes
     return AD_OK;
 }
 
+// After a stream sync: if the optimistic execution order failed its verification, redo it on the
+// general path (radix sort by executeAt) and wait for it.
+int finish_order(ad_handle* h) {
+    if (!h->order_pending) return AD_OK;
+    h->order_pending = false;
+    if (!h->order_bad) return AD_OK;
+    order_rows(h->ls, h->n, nullptr, h->ex1, h->lvl, h->pack.total_bits, h->order, h->st);
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
 int ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint32_t* iterations_out) {
     if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     hipSetDevice(h->device);
     CK(stage_levels(h, order_out != nullptr));
     hipStream_t st = h->st;
+    HIPCHK(h, hipStreamSynchronize(st));
+    CK(finish_order(h));
     if (level_out && h->n) HIPCHK(h, hipMemcpyAsync(level_out, h->lvl, h->n * 4, hipMemcpyDeviceToHost, st));
     if (order_out && h->n) HIPCHK(h, hipMemcpyAsync(order_out, h->order, h->n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     if (iterations_out) *iterations_out = h->level_iters;
+    return AD_OK;
+}
+
+int ad_fetch_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out) {
+    if (!h) return AD_ERR_ARGUMENT;
+    if (!h->have_levels) return set_err(h, AD_ERR_STATE, "no levels computed for this batch");
+    hipSetDevice(h->device);
+    if (level_out && h->n) HIPCHK(h, hipMemcpyAsync(level_out, h->lvl, h->n * 4, hipMemcpyDeviceToHost, h->st));
+    if (order_out && h->n) HIPCHK(h, hipMemcpyAsync(order_out, h->order, h->n * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
     return AD_OK;
 }
 
@@ -991,6 +1020,12 @@ int ad_run_pipeline(ad_handle* h) {
     CK(stage_levels(h, true));
     HIPCHK(h, hipEventRecord(h->ev[5], st));
     HIPCHK(h, hipEventSynchronize(h->ev[5]));
+    if (h->order_pending && h->order_bad) {      // optimistic order failed its check: general path, timed in
+        CK(finish_order(h));
+        HIPCHK(h, hipEventRecord(h->ev[5], st));
+        HIPCHK(h, hipEventSynchronize(h->ev[5]));
+    }
+    h->order_pending = false;
     float ms;
     hipEventElapsedTime(&ms, h->ev[0], h->ev[1]); h->times.prepare = ms;
     hipEventElapsedTime(&ms, h->ev[1], h->ev[2]); h->times.sort = ms;

@@ -655,6 +655,8 @@ struct LevelInputs {
     uint32_t exec_bits;
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
+    uint32_t* order_verify;              // optimistic order: host word receiving the fast-path failure flag
+    bool* order_pending;                 // set when the caller must check *order_verify after its sync
 };
 
 // Execution order over m txns (rows[k], or k when rows is null): LSD radix sort by executeAt (two 32-bit
@@ -755,8 +757,12 @@ __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint3
     }
 }
 
-inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
-                       uint32_t exec_bits, uint32_t* order_out, hipStream_t st) {
+// Returns true when the order was produced optimistically (known_maxl >= 0: the level count is known,
+// so no host sync is needed here): the fast path's verification flag is then copied to *verify_host and
+// the caller, after its own stream sync, reruns order_rows with known_maxl = -1 if it is set.
+inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
+                       uint32_t exec_bits, uint32_t* order_out, hipStream_t st, int known_maxl = -1,
+                       uint32_t* verify_host = nullptr) {
     KScope ks(K_ORDER, m);
     RadixScratch rs;
     const size_t hl = radix_hist_len(m);
@@ -765,15 +771,22 @@ inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     rs.agg = rs.offs + hl + 64;
     const int g = ceil_div((long)m, 256);
     uint32_t *k = ls.sk0, *v = ls.sv0, *ko = ls.sk1, *vo = ls.sv1;
-    // fast path: windowed inversion ranks + verification (one host sync: sortedness + max level)
+    uint32_t* of = ls.flags + 8;                              // [0] max level, [1] fast path failed
     const int gg = std::min(g, ORDER_GRID);
-    hipMemsetAsync(ls.flags + 4, 0, 8, st);
-    hipMemsetAsync(v, 0xFF, m * 4, st);                       // WR_EMPTY: detects rank collisions
-    k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, ls.flags + 5);
-    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, ls.flags + 4);
+    const bool optimistic = known_maxl >= 0 && verify_host != nullptr;
     uint32_t fl[2] = {0, 0};
-    hipMemcpyAsync(fl, ls.flags + 4, 8, hipMemcpyDeviceToHost, st);
-    hipStreamSynchronize(st);
+    // fast path: windowed inversion ranks + verification
+    hipMemsetAsync(of, 0, 8, st);
+    hipMemsetAsync(v, 0xFF, m * 4, st);                       // WR_EMPTY: detects rank collisions
+    k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1);
+    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, of);
+    if (optimistic) {
+        hipMemcpyAsync(verify_host, of + 1, 4, hipMemcpyDeviceToHost, st);
+        fl[0] = (uint32_t)known_maxl;
+    } else {
+        hipMemcpyAsync(fl, of, 8, hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+    }
     if (fl[1]) {
         // general executeAt distribution: LSD radix sort by executeAt (two 32-bit halves)
         const int eb = (int)exec_bits;
@@ -784,16 +797,17 @@ inline void order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
             k_exec_split_rows<<<g, 256, 0, st>>>(m, ex1, rows, v, k, 1);
             if (radix_sort_pairs(k, v, ko, vo, m, eb - 32, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
         }
-        k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, ls.flags + 4);
+        k_gather_level_rows<<<gg, 256, 0, st>>>(m, lvl, rows, v, k, of);
     }
     const uint32_t maxl = fl[0];
     const int lb = maxl == 0 ? 0 : 32 - __builtin_clz(maxl);
     if (lb > 0 && lb <= 8) {         // one stable pass by level, written straight into order_out
         radix_sort_pairs(k, v, ko, order_out, m, lb, rs, st);
-        return;
+        return optimistic;
     }
     if (radix_sort_pairs(k, v, ko, vo, m, lb, rs, st)) { std::swap(k, ko); std::swap(v, vo); }
     hipMemcpyAsync(order_out, v, m * 4, hipMemcpyDeviceToDevice, st);
+    return optimistic;
 }
 
 inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hipStream_t st, int* iters,
@@ -909,7 +923,12 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             }
             if (!fallback) {
                 *iters = lv;
-                if (want_order && n > 0) order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
+                // the wavefront count gives the level range: the order needs no host sync of its own
+                if (want_order && n > 0 && in.order_verify)
+                    *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, lv - 1,
+                                                   in.order_verify);
+                else if (want_order && n > 0)
+                    order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
                 return AD_OK;
             }
             hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);

@@ -192,6 +192,9 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
 /* outputs.  Kernel timing: HIP events on the handle's stream.                                 */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_run_pipeline(ad_handle* h);
+/* Levels and execution order left on the device by the last ad_run_pipeline / ad_exec_levels (no
+ * recomputation).  Either pointer may be NULL.  AD_ERR_STATE if none were computed for this batch. */
+int  ad_fetch_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out);
 typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline, event-timed */
     float prepare, sort, deps, merge, levels, total;
     uint64_t deps_entries;          /* emitted (key,txn) entries over all views/classes      */
