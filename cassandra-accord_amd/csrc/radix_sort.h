@@ -79,13 +79,16 @@ __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __re
         v[r] = i < n ? vin[i] : 0u;
     }
     const uint64_t below = (1ull << lane) - 1ull;
-    // pass A: per-wave digit counts
+    // pass A: per-wave digit counts; each item keeps its offset among the wave's items of its digit
+    // (items of earlier rounds + lower lanes of this round), so the staging pass needs no second match
+    uint32_t off[RS_ROUNDS];
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
         size_t i = wbase + (size_t)r * WAVE + lane;
         bool valid = i < n;
         uint32_t d = (k[r] >> shift) & 0xFF;
         uint64_t m = match_digit(d, valid);
+        off[r] = cnt[w][d] + (uint32_t)__popcll(m & below);      // read before the group leader's update
         if (valid && (m & below) == 0) cnt[w][d] += (uint32_t)__popcll(m);
     }
     __syncthreads();
@@ -119,12 +122,11 @@ __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __re
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
         size_t i = wbase + (size_t)r * WAVE + lane;
-        bool valid = i < n;
-        uint32_t d = (k[r] >> shift) & 0xFF;
-        uint64_t m = match_digit(d, valid);
-        uint32_t pos = cnt[w][d] + (uint32_t)__popcll(m & below);
-        if (valid) { sk[pos] = k[r]; sv[pos] = v[r]; }
-        if (valid && (m & below) == 0) cnt[w][d] += (uint32_t)__popcll(m);
+        if (i < n) {
+            const uint32_t pos = cnt[w][(k[r] >> shift) & 0xFF] + off[r];
+            sk[pos] = k[r];
+            sv[pos] = v[r];
+        }
     }
     __syncthreads();
     // pass C: sequential read-out, coalesced runs per digit
