@@ -45,6 +45,7 @@ def alg_bytes(kernel, calls, units, n, P, R, st):
     Kernels whose work is data dependent in a way the tracer does not count (the level worklist walk,
     composite scans) return None and are not roofline candidates."""
     D = st["deps_entries"]           # emitted dependency entries over all views/classes
+    W = st["walk_items"]             # entries the deps walks visit
     per = {
         "k_minmax": calls * (n * 44 + P * 8),                    # TxnId/executeAt SoA + key_off; keys
         "k_pack": calls * (n * 62 + P * 20),                     # read 45 B/txn, write 17 B/txn; 8+12 B/pair
@@ -52,9 +53,13 @@ def alg_bytes(kernel, calls, units, n, P, R, st):
         "k_radix_scatter": units * 16,                           # read key+value, write key+value
         "k_gather_entries": units * 34,                          # sval, pair_txn, meta, ex1 -> e_txn, e_meta, e_exec1, spos
         "scan_elide": units * 37,                                # skey, e_meta, e_exec1 -> seg, ud, pm_w, pm_c
-        "k_deps_walk<count>": units * (33 + 8 * R),              # entry state + tx_ts; write 2R counts
-        "k_deps_walk<fill>": units * (33 + 16 * R) + 4 * D,      # + read counts/slots, write the entries
+        # the walks visit only entries with an earlier entry of their key (ad_stage_times.walk_items):
+        # list index, entry state, own txn's TxnId, predecessor entry, prefix state; 2R counts out
+        "k_deps_walk<count>": calls * W * (46 + 8 * R),
+        "k_deps_walk<fill>": calls * (W * (46 + 8 * R) + 4 * D),  # 2R end slots in, the entries out
         "k_txn_layout": units * (8 + 16 * R),                    # key + 2R counts in, 2R slots out
+        # per txn: 3 offsets x 2R CSRs, the per-key lists in, unique TxnIds + remapped lists out
+        "k_txn_union": calls * (n * (12 * 2 * R + 4 * 2 * R) + 12 * D),
     }
     return per.get(kernel)
 

@@ -185,7 +185,7 @@ class DepsEngine:
     def last_times(self):
         t = abi.AdStageTimes()
         self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
-        return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_ if f != "pad_"}
+        return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_}
 
     def set_level_mode(self, fixpoint):
         """False (default): Kahn wavefront where it applies, else the chain fixpoint; True: always the fixpoint."""

@@ -519,6 +519,7 @@ int stage_deps(ad_handle* h) {
     h->ls.chains_ready = false;
     h->times.deps_entries = h->deps_entries;
     h->times.level_edges = h->P;
+    h->times.walk_items = (uint32_t)(h->P - (h->P ? h->hprm.n_keys_u : 0));
     return AD_OK;
 }
 
@@ -1037,6 +1038,7 @@ int ad_run_pipeline(ad_handle* h) {
     h->times.merged_entries = h->merged_entries;
     h->times.level_iterations = h->level_iters;
     h->times.level_edges = h->P;
+    h->times.walk_items = (uint32_t)(h->P - (h->P ? h->hprm.n_keys_u : 0));
     h->tracer.resolve();
     return AD_OK;
 }

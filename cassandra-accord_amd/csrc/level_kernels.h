@@ -578,20 +578,42 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
 // prev: the previous wavefront's "released something" flag (nullptr: run); *work: this one released some.
 // gate: the previous wavefront's "released something" flag (run if set), or for the first wavefront of a
 // batch (gate_is_abort) the chain build's long-chain flag (run if clear).
+// Grid-stride over a bounded grid (an empty wavefront costs one small launch).  For txns with up to 4
+// keys the first successor of every pair is released with all loads and atomics issued together (the
+// returning atomics are the latency of this kernel); longer runs and wider txns go serially.
+constexpr int KAHN_GRID = 2048;
+__device__ inline void kahn_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
+    if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
+}
 __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
                                                    uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
                                                    const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
                                                    const uint32_t* __restrict__ c_txn, const uint32_t* gate, int gate_is_abort,
                                                    uint32_t* __restrict__ work) {
     if (gate_is_abort ? *gate != 0u : *gate == 0u) return;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool released = false;
-    if (t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl)) {
-        for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) {
-            const uint2 sc = succ[p];
-            for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) {
-                const uint32_t s = c_txn[x];
-                if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x) {
+        if (!(lvl == 0 ? indeg0[t] == 0u : L[t] == lvl)) continue;
+        const uint32_t b = key_off[t], e = key_off[t + 1];
+        if (e - b <= 4) {
+            uint2 sc[4];
+            uint32_t sx[4], rr[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sc[j] = b + j < e ? succ[b + j] : make_uint2(0u, 0u);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sx[j] = sc[j].y ? c_txn[sc[j].x] : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rr[j] = sc[j].y ? atomicSub(&rem[sx[j]], 1u) : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (sc[j].y && rr[j] == 1u) { L[sx[j]] = lvl + 1; released = true; }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+        } else {
+            for (uint32_t p = b; p < e; ++p) {
+                const uint2 sc = succ[p];
+                for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
             }
         }
     }
@@ -892,7 +914,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 // wavefronts per launch batch, no host sync inside a batch (a wavefront after the last
                 // one exits at once); the first batch covers typical uniform-key depths (C2: 10)
                 constexpr int KB_MAX = 16;
-                const int gn = ceil_div((long)n, 256);
+                const int gn = std::min(ceil_div((long)n, 256), KAHN_GRID);
                 bool more = true;
                 while (more && lv < (1 << 24)) {
                     const int KB = lv == 0 ? KB_MAX : 8;

@@ -59,11 +59,21 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     int64_t rv[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) rv[v] = a.row[v] ? (int64_t)a.row[v][t] : (int64_t)t;
+    // a txn without deps in every reply (no TxnIds => no keys in a canonical CSR) merges to nothing:
+    // settle it from the TxnId counts alone (C2: about half the txns)
+    uint32_t tc[NV], any_tc = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) { tc[v] = rv[v] >= 0 ? a.tcnt[v][rv[v]] : 0u; any_tc |= tc[v]; }
+    if (any_tc == 0) {
+        if (WRITE) a.o_tcnt[t] = 0;
+        else { a.mk[t] = 0; a.me[t] = 0; a.mu[t] = 0; }
+        return;
+    }
     uint32_t cur[NV], end[NV], head[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         cur[v] = rv[v] >= 0 ? a.ent_off[v][rv[v]] : 0u;
-        end[v] = rv[v] >= 0 ? cur[v] + a.tcnt[v][rv[v]] : 0u;
+        end[v] = cur[v] + tc[v];
         head[v] = cur[v] < end[v] ? a.txns[v][cur[v]] : INF;
     }
     uint32_t* out = WRITE ? a.o_txns + a.o_ent_off[t] : nullptr;

@@ -201,7 +201,8 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
     uint64_t merged_entries;        /* entries of the merged Deps                             */
     uint64_t level_edges;           /* key-chain entries visited per level sweep              */
     uint32_t level_iterations;
-    uint32_t pad_;
+    uint32_t walk_items;            /* (txn,key) entries with an earlier entry of their key: the */
+                                    /* ones the deps walks visit (P - distinct keys)             */
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
