@@ -123,7 +123,7 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol (profiles
     "k_deps_walk<fill>": "ad::k_deps_walk<3, true>", "k_deps_walk<count>": "ad::k_deps_walk<3, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
     "k_gather_entries": "ad::k_gather_entries", "k_txn_layout": "ad::k_txn_layout",
-    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack",
+    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union",
 }
 
 
@@ -131,8 +131,9 @@ def pmc_traffic(kernel):
     """HBM-side bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
     written by profiles/collect.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3 passes of this bench).
     The largest-grid dispatch of the kernel is the batch-sized one.  FETCH_SIZE is reported as counted
-    (Infinity-Cache hits included; 4-byte accesses, so the guide's 2x wide-stream correction does not
-    apply — the file carries a 4-byte streaming calibration measured on k_radix_hist).  None if absent."""
+    (Infinity-Cache hits included).  FETCH_SIZE is divided by the file's streaming-read calibration (bytes
+    counted per algorithmic byte of k_radix_hist's coalesced 4-byte key reads: 0.50 on gfx950, the guide's
+    "1/2 of wide streams" also holds at 4 B/lane); random accesses are not calibrated.  None if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     want = ROCPROF_NAME.get(kernel)
@@ -140,12 +141,14 @@ def pmc_traffic(kernel):
         return None, None
     with open(files[-1]) as f:
         doc = json.load(f)
+    cal = (doc.get("calibration_4B_stream_read") or {}).get("fetch_per_alg_byte") or 1.0
     best = None
     for k, e in doc.get("kernels", {}).items():
         name, grid = k.rsplit(" grid=", 1)
         if name == want and "FETCH_SIZE_KB_mean" in e and "WRITE_SIZE_KB_mean" in e:
             if best is None or int(grid) > best[0]:
-                best = (int(grid), (e["FETCH_SIZE_KB_mean"] + e["WRITE_SIZE_KB_mean"]) * 1024.0)
+                # FETCH_SIZE corrected by the measured streaming-read calibration (gfx950 counts 1/2)
+                best = (int(grid), (e["FETCH_SIZE_KB_mean"] / cal + e["WRITE_SIZE_KB_mean"]) * 1024.0)
     if best is None:
         return None, None
     return best[1], os.path.relpath(files[-1], ROOT)
