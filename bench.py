@@ -168,10 +168,11 @@ def main_sharded(args, rank, world, local, dist):
     batch = workload.generate(n_total, 4, KEYSPACE * world, "uniform", seed=workload.SEEDS["C5"])
     bounds = sharding.even_bounds(0, KEYSPACE * world, world)
     lb, gid, home = sharding.slice_for_shard(batch, bounds[rank], bounds[rank + 1])
+    hs = sharding.home_stores(batch, bounds)[gid]
     del batch
     device = local % max(1, engine.device_count())
     store = sharding.ShardStore(device, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C5"])
-    store.load(lb, gid, home, n_total)
+    store.load(lb, gid, hs, n_total, rank, world)
     tr = None
     if args.transport == "rccl":
         try:
@@ -186,9 +187,14 @@ def main_sharded(args, rank, world, local, dist):
     if tr is None:
         tr = sharding.GlooTransport(dist)
 
-    def step():
-        r = sharding.run_store(store, tr)
+    phases = {}
+
+    def step(timings=None):
+        r = sharding.run_store(store, tr, timings=timings)
+        t0 = time.perf_counter()
         store.order()
+        if timings is not None:
+            timings["order"] = timings.get("order", 0.0) + time.perf_counter() - t0
         return r
 
     rounds = 0
@@ -203,7 +209,7 @@ def main_sharded(args, rank, world, local, dist):
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        rounds = step()
+        rounds = step(phases)
     t1 = time.perf_counter()
     dist.barrier()
     t = __import__("torch").tensor([t1 - t0], dtype=__import__("torch").float64)
@@ -217,11 +223,12 @@ def main_sharded(args, rank, world, local, dist):
         "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C5 generator, BASELINE configs[4] shape)",
         "config": {"workload": "C5: %d txns x 4 keys uniform over %dM keys, key-range sharded over %d GPUs "
-                               "(cross-shard deps all-gathered, distributed level rounds); R=%d views, W=%d, drop %.1f"
+                               "(cross-shard deps all-to-all to the home store, distributed level rounds); R=%d views, W=%d, drop %.1f"
                                % (n_total, 10 * world, world, REPLICAS, WINDOW, DROP_P),
                    "txns_total": n_total, "txns_per_gpu": args.n, "local_txns_rank0": n_loc, "local_pairs_rank0": P_loc,
                    "keys_per_txn": 4, "keyspace": KEYSPACE * world, "replicas": REPLICAS, "window": WINDOW,
-                   "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds},
+                   "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds,
+                   "phase_ms_rank0": {k: round(v * 1e3 / args.steps, 3) for k, v in phases.items()}},
         "roofline": roof,
         "cpu_baseline": None,
     }
@@ -246,7 +253,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("gloo")
+        # gloo prints connection notices on the C-level stdout; keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            tdist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         try:
             main_sharded(args, rank, world, local, tdist)
         finally:

@@ -3,14 +3,17 @@
 Mirrors Accord's per-range CommandStore sharding (local/CommandStores.java:576-593,
 local/ShardDistributor.java:32-80) and PreAccept.reduce across stores (messages/PreAccept.java:141-156):
 
-* ``even_bounds`` / ``slice_for_shard`` — host-side partitioning: store s owns keys in [bounds[s], bounds[s+1]);
-  its local batch is every txn touching that range with its keys sliced to it, in global TxnId order; ``gid``
-  maps local rows to global ranks and ``home`` marks txns whose first key lies in the range.
+* ``even_bounds`` / ``slice_for_shard`` / ``home_stores`` — host-side partitioning: store s owns keys in
+  [bounds[s], bounds[s+1]); its local batch is every txn touching that range with its keys sliced to it, in
+  global TxnId order; ``gid`` maps local rows to global ranks; a txn's home store is the store of its first
+  key (the store that merges its deps).
 * ``ShardStore`` — one store on one GPU (an ad_handle in sharded mode), driving the C-ABI protocol.
-* transports — how stores exchange blobs and level arrays: ``RcclTransport`` (ncclAllGather /
-  ncclAllReduce on device buffers over xGMI, inside libaccord_deps; torch.distributed/gloo only carries the
-  128-byte unique id and two scalars), ``GlooTransport`` (host staging over a gloo group; used for tests
-  and as the explicit host path), ``LocalTransport`` (several stores in one process, for tests).
+* transports — how stores exchange blobs and level arrays: ``RcclTransport`` (grouped ncclSend/ncclRecv
+  all-to-all and ncclAllReduce on device buffers over xGMI, inside libaccord_deps; torch.distributed/gloo
+  only carries the unique id, the per-destination byte counts and one scalar per level round),
+  ``GlooTransport`` (host staging over a gloo group; used for tests and as the explicit host path),
+  ``LocalTransport`` (several stores in one process, for tests).  Each store sends every other store only
+  the deps rows of the txns homed there, and only rows that have deps.
 * ``run_store`` — the per-store protocol: preaccept, export, exchange, merge, distributed levels, order.
 
 Every computation runs on the GPU through the C-ABI; the transports only move bytes.
@@ -56,6 +59,18 @@ def slice_for_shard(batch, lo, hi):
     return local, gid, home
 
 
+def home_stores(batch, bounds):
+    """Per global txn: the store owning its first key (its home; merges its deps)."""
+    ko = batch["key_off"].astype(np.int64)
+    keys = batch["keys"]
+    n = batch["n"]
+    first = np.zeros(n, np.uint64)
+    nz = ko[1:] > ko[:-1]
+    first[nz] = keys[ko[:-1][nz]]
+    hs = np.searchsorted(np.asarray(bounds, np.uint64), first, side="right") - 1
+    return np.clip(hs, 0, len(bounds) - 2).astype(np.uint8)
+
+
 def _u32p(a):
     return a.ctypes.data_as(C.POINTER(C.c_uint32))
 
@@ -69,13 +84,14 @@ class ShardStore:
         self.L = engine.lib()
         L = self.L
         vp = C.c_void_p
-        L.ad_shard_setup.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint8), C.c_size_t]
-        L.ad_shard_export.argtypes = [vp, C.POINTER(C.c_size_t)]
-        L.ad_shard_blob_to_host.argtypes = [vp, C.c_void_p]
-        L.ad_shard_import_host.argtypes = [vp, C.c_void_p, C.c_uint32, C.c_size_t]
+        u64p = C.POINTER(C.c_uint64)
+        L.ad_shard_setup.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32, C.c_size_t]
+        L.ad_shard_export.argtypes = [vp, u64p]
+        L.ad_shard_send_to_host.argtypes = [vp, C.c_void_p]
+        L.ad_shard_import_host.argtypes = [vp, C.c_void_p, C.c_uint32, u64p]
         L.ad_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ad_comm_init.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
-        L.ad_shard_allgather.argtypes = [vp, C.c_size_t]
+        L.ad_shard_alltoall.argtypes = [vp, u64p]
         L.ad_shard_merge.argtypes = [vp, C.POINTER(abi.AdCsrSizes), C.POINTER(C.c_size_t)]
         L.ad_shard_fetch.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut), C.POINTER(C.c_uint32)]
         L.ad_shard_levels_round.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32)]
@@ -91,38 +107,49 @@ class ShardStore:
         self.eng._check(rc, what)
 
     # ---- protocol steps
-    def load(self, local_batch, gid, home, n_global):
+    def load(self, local_batch, gid, home_store, n_global, rank, world):
+        """home_store: per local row, the store of the txn's first key (home_stores(global)[gid])."""
         self.eng.load(local_batch)
         self.gid = np.ascontiguousarray(gid, np.uint32)
-        self.home = np.ascontiguousarray(home, np.uint8)
+        self.home_store = np.ascontiguousarray(home_store, np.uint8)
         self.n_global = n_global
-        self._check(self.L.ad_shard_setup(self.eng.h, _u32p(self.gid), self.home.ctypes.data_as(C.POINTER(C.c_uint8)),
-                                          n_global), "ad_shard_setup")
+        self.rank, self.world = rank, world
+        self._check(self.L.ad_shard_setup(self.eng.h, _u32p(self.gid), self.home_store.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                          rank, world, n_global), "ad_shard_setup")
 
     def preaccept(self):
         self._check(self.L.ad_preaccept_deps(self.eng.h, None), "ad_preaccept_deps")
 
     def export(self):
-        b = C.c_size_t()
-        self._check(self.L.ad_shard_export(self.eng.h, C.byref(b)), "ad_shard_export")
-        self.blob_bytes = b.value
-        return b.value
+        """Per-destination blobs on the device; returns their byte sizes (np.uint64[world])."""
+        b = np.zeros(self.world, np.uint64)
+        self._check(self.L.ad_shard_export(self.eng.h, b.ctypes.data_as(C.POINTER(C.c_uint64))), "ad_shard_export")
+        self.send_sizes = b
+        return b
 
-    def blob(self):
-        out = np.zeros(self.blob_bytes, np.uint8)
-        self._check(self.L.ad_shard_blob_to_host(self.eng.h, out.ctypes.data), "ad_shard_blob_to_host")
-        return out
+    def send_buffer(self):
+        """The blobs, concatenated in destination order (host copy)."""
+        out = np.zeros(max(int(self.send_sizes.sum()), 1), np.uint8)
+        self._check(self.L.ad_shard_send_to_host(self.eng.h, out.ctypes.data), "ad_shard_send_to_host")
+        return out[:int(self.send_sizes.sum())]
 
-    def import_host(self, recv, world, stride):
+    def import_host(self, recv, sizes):
+        """Blobs received from every store (source order), sizes[s] bytes each."""
         recv = np.ascontiguousarray(recv, np.uint8)
-        self._check(self.L.ad_shard_import_host(self.eng.h, recv.ctypes.data, world, stride), "ad_shard_import_host")
+        if recv.size == 0:
+            recv = np.zeros(1, np.uint8)
+        sizes = np.ascontiguousarray(sizes, np.uint64)
+        self._check(self.L.ad_shard_import_host(self.eng.h, recv.ctypes.data, self.world,
+                                                sizes.ctypes.data_as(C.POINTER(C.c_uint64))), "ad_shard_import_host")
+
+    def alltoall(self, recv_sizes):
+        rs = np.ascontiguousarray(recv_sizes, np.uint64)
+        self._check(self.L.ad_shard_alltoall(self.eng.h, rs.ctypes.data_as(C.POINTER(C.c_uint64))), "ad_shard_alltoall")
 
     def comm_init(self, world, rank, uid):
         u = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
         self._check(self.L.ad_comm_init(self.eng.h, world, rank, u), "ad_comm_init")
 
-    def allgather(self, stride):
-        self._check(self.L.ad_shard_allgather(self.eng.h, stride), "ad_shard_allgather")
 
     def merge(self):
         sizes = (abi.AdCsrSizes * ((self.replicas + 1) * abi.NUM_CLASSES))()
@@ -194,15 +221,20 @@ class GlooTransport:
     def any(self, flag):
         return self.max_u64(1 if flag else 0) > 0
 
+    def recv_sizes(self, send_sizes):
+        """All-to-all of the per-destination byte counts: what every peer sends this store."""
+        out = self.torch.zeros(len(send_sizes), dtype=self.torch.int64)
+        self.dist.all_to_all_single(out, self.torch.from_numpy(np.asarray(send_sizes, np.int64)))
+        return out.numpy().astype(np.uint64)
+
     def exchange_blobs(self, store):
-        n = store.export()
-        stride = (self.max_u64(n) + 7) // 8 * 8
-        mine = np.zeros(stride, np.uint8)
-        mine[:n] = store.blob()
-        world = self.dist.get_world_size()
-        parts = [self.torch.zeros(stride, dtype=self.torch.uint8) for _ in range(world)]
-        self.dist.all_gather(parts, self.torch.from_numpy(mine))
-        store.import_host(np.concatenate([p.numpy() for p in parts]), world, stride)
+        sizes = store.export()
+        rsz = self.recv_sizes(sizes)
+        send = self.torch.from_numpy(store.send_buffer().copy())
+        recv = self.torch.zeros(int(rsz.sum()), dtype=self.torch.uint8)
+        self.dist.all_to_all_single(recv, send, output_split_sizes=[int(x) for x in rsz],
+                                    input_split_sizes=[int(x) for x in sizes])
+        store.import_host(recv.numpy(), rsz)
 
     def allreduce_levels(self, store):
         g = self.torch.from_numpy(store.levels_get().astype(np.int64))
@@ -211,8 +243,9 @@ class GlooTransport:
 
 
 class RcclTransport(GlooTransport):
-    """Blobs and level arrays move over RCCL (ncclAllGather / ncclAllReduce on device buffers, xGMI);
-    the gloo group only carries the unique id and the stride / convergence scalars."""
+    """Blobs and level arrays move over RCCL (grouped ncclSend/ncclRecv all-to-all, ncclAllReduce, on
+    device buffers over xGMI); the gloo group carries the unique id, the byte counts and one scalar per
+    level round."""
 
     name = "rccl"
 
@@ -223,26 +256,44 @@ class RcclTransport(GlooTransport):
         store.comm_init(world, rank, obj[0])
 
     def exchange_blobs(self, store):
-        n = store.export()
-        stride = (self.max_u64(n) + 7) // 8 * 8
-        store.allgather(stride)
+        sizes = store.export()
+        store.alltoall(self.recv_sizes(sizes))
 
     def allreduce_levels(self, store):
         store.levels_allreduce()
 
 
-def run_store(store, transport, max_rounds=1 << 16):
-    """The per-store protocol after load(): returns the number of distributed level rounds."""
+def run_store(store, transport, max_rounds=1 << 16, timings=None):
+    """The per-store protocol after load(): returns the number of distributed level rounds.
+    timings (dict, optional) accumulates wall seconds per phase (each phase ends synchronised)."""
+    import time
+    clock = time.perf_counter
+    t = [clock()]
+
+    def lap(name):
+        now = clock()
+        if timings is not None:
+            timings[name] = timings.get(name, 0.0) + now - t[0]
+        t[0] = now
+
     store.preaccept()
+    lap("deps")
     transport.exchange_blobs(store)
+    lap("exchange")
     store.merge()
+    lap("merge")
     changed = store.levels_round(True)
+    lap("levels_local")
     rounds = 1
     while True:
         transport.allreduce_levels(store)
+        lap("levels_exchange")
         if not transport.any(changed) or rounds >= max_rounds:
+            lap("levels_exchange")
             break
+        lap("levels_exchange")
         changed = store.levels_round(False)
+        lap("levels_local")
         rounds += 1
     return rounds
 
@@ -255,12 +306,12 @@ class LocalTransport:
         for s in stores:
             s.preaccept()
         sizes = [s.export() for s in stores]
-        stride = (max(sizes) + 7) // 8 * 8
-        recv = np.zeros(stride * len(stores), np.uint8)
-        for k, s in enumerate(stores):
-            recv[k * stride:k * stride + sizes[k]] = s.blob()
-        for s in stores:
-            s.import_host(recv, len(stores), stride)
+        bufs = [s.send_buffer() for s in stores]
+        offs = [np.concatenate([[0], np.cumsum(z)]).astype(np.int64) for z in sizes]
+        for d, s in enumerate(stores):
+            parts = [bufs[k][offs[k][d]:offs[k][d + 1]] for k in range(len(stores))]
+            s.import_host(np.concatenate(parts) if parts else np.zeros(0, np.uint8),
+                          np.array([sizes[k][d] for k in range(len(stores))], np.uint64))
             s.merge()
         changed = [s.levels_round(True) for s in stores]
         rounds = 1

@@ -95,11 +95,14 @@ struct ad_handle {
     size_t n_global = 0;
     uint32_t* gid = nullptr;         // local row -> global arrival rank
     uint8_t* home = nullptr;         // local row is homed here (first key in this store's range)
-    uint8_t* send = nullptr;
+    uint8_t* hstore = nullptr;       // local row -> its home store (destination of its fragment)
+    uint32_t self = 0;               // this store's rank
+    uint8_t* send = nullptr;         // per-destination blobs, concatenated in destination order
     size_t send_bytes = 0;
-    uint8_t* recv = nullptr;
+    std::vector<uint64_t> send_sizes;
+    std::vector<uint64_t> send_hdr;  // host copy of the blob headers (outlives the async upload)
+    uint8_t* recv = nullptr;         // per-source blobs (this store's home txns), concatenated
     uint32_t world = 0;
-    size_t stride = 0;
     size_t H = 0;                    // home txns
     uint32_t *home_rows = nullptr, *home_gid = nullptr, *G = nullptr;
     int32_t* src_rows = nullptr;     // [source * H + h]
@@ -163,7 +166,8 @@ enum Slot : size_t {
     S_PMW, S_PMC, S_SEG, S_UD, S_CNT, S_DST, S_NK, S_NE, S_SCRATCH,
     S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
-    S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT,
+    S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT, S_HSTORE, S_XRANK, S_XLIST, S_XOFF,
+    S_XBND, S_XSEC,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -1099,127 +1103,216 @@ int ad_reset_kernel_stats(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 static size_t align8(size_t x) { return (x + 7) & ~(size_t)7; }
 
-int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home, size_t n_global) {
-    if (!h || (!gid && h->n) || (!home && h->n)) return AD_ERR_ARGUMENT;
+int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home_store, uint32_t self, uint32_t world, size_t n_global) {
+    if (!h || (!gid && h->n) || (!home_store && h->n) || world == 0 || world > (uint32_t)MAX_STORES || self >= world)
+        return AD_ERR_ARGUMENT;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "ad_shard_setup: load the store's batch first");
     if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "sharded mode: range txns are not supported in this build");
     hipSetDevice(h->device);
     const size_t n = h->n;
-    for (size_t i = 0; i < n; ++i)
+    for (size_t i = 0; i < n; ++i) {
         if (gid[i] >= n_global || (i > 0 && gid[i] <= gid[i - 1])) return set_err(h, AD_ERR_ARGUMENT, "gid must be ascending global ranks < n_global");
-    CK(dalloc(h, S_GID, &h->gid, n)); CK(dalloc(h, S_HOME, &h->home, n));
+        if (home_store[i] >= world) return set_err(h, AD_ERR_ARGUMENT, "home store out of range");
+    }
+    std::vector<uint8_t> home(n);
+    for (size_t i = 0; i < n; ++i) home[i] = home_store[i] == self ? 1 : 0;
+    CK(dalloc(h, S_GID, &h->gid, n)); CK(dalloc(h, S_HOME, &h->home, n)); CK(dalloc(h, S_HSTORE, &h->hstore, n));
     if (n) {
         HIPCHK(h, hipMemcpyAsync(h->gid, gid, n * 4, hipMemcpyHostToDevice, h->st));
-        HIPCHK(h, hipMemcpyAsync(h->home, home, n, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->home, home.data(), n, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->hstore, home_store, n, hipMemcpyHostToDevice, h->st));
     }
     HIPCHK(h, hipStreamSynchronize(h->st));
     h->sharded = true;
     h->n_global = n_global;
+    h->self = self;
+    h->world = world;
     h->have_deps = h->have_merged = h->have_levels = false;
     return AD_OK;
 }
 
-// Pack this store's deps (every view, key + direct class), TxnIds rewritten to global ranks, into one blob.
-int ad_shard_export(ad_handle* h, size_t* bytes) {
+// Blob of one destination: header u64[3 + 3 nvc] = {magic, rows, nvc, per vc (keys, k2t, txns)}, then
+// gid[rows], then per vc key_off[rows+1] k2t_off[rows+1] ent_off[rows+1] tcnt[rows] keys k2t txns (8-aligned).
+static size_t blob_layout(size_t rows, int nvc, const uint32_t* cnt /* [nvc*3] */, uint64_t* sec /* [SEC_PER_DEST] or null */) {
+    size_t off = align8((3 + 3 * (size_t)nvc) * 8);
+    if (sec) sec[0] = off;
+    off = align8(off + rows * 4);
+    for (int c = 0; c < nvc; ++c) {
+        const size_t nk = cnt[3 * c], nm = cnt[3 * c + 1], nt = cnt[3 * c + 2];
+        const size_t sz[7] = {(rows + 1) * 4, (rows + 1) * 4, (rows + 1) * 4, rows * 4, nk * 8, nm * 4, nt * 4};
+        for (int k = 0; k < 7; ++k) {
+            if (sec) sec[1 + 7 * c + k] = off;
+            off = align8(off + sz[k]);
+        }
+    }
+    return off;
+}
+
+}  // extern "C"
+
+template <int NVC>
+void launch_export_offsets(ad_handle* h, size_t K, const uint32_t* list, const ExportOffs& o) {
+    ExportOffsetsOp<NVC> op{};
+    op.list = list; op.n = K;
+    for (int c = 0; c < NVC; ++c) {
+        const Csr& x = h->deps[c];
+        op.key_off[c] = x.key_off; op.k2t_off[c] = x.k2t_off; op.tcnt[c] = x.tcnt;
+        op.ok[c] = o.ok[c]; op.om[c] = o.om[c]; op.ot[c] = o.ot[c];
+    }
+    device_scan(op, K, (typename ExportOffsetsOp<NVC>::S*)h->scratch, h->st);
+}
+
+template <int NV>
+void launch_export_offsets_nv(ad_handle* h, size_t K, const uint32_t* list, const ExportOffs& o) {
+    launch_export_offsets<2 * NV>(h, K, list, o);
+}
+
+extern "C" {
+
+// Pack this store's deps rows (every view, key + direct class) per destination store: the local txns
+// homed at destination d that have deps here, TxnIds as global ranks.  bytes[d] = blob size for d.
+int ad_shard_export(ad_handle* h, uint64_t* bytes /* [world] */) {
     if (!h || !bytes) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_export: ad_shard_setup + ad_preaccept_deps first");
     hipSetDevice(h->device);
     const size_t n = h->n;
     const int nvc = 2 * (int)h->cfg.replicas;
+    const uint32_t W = h->world;
     hipStream_t st = h->st;
-    for (int vc = 0; vc < nvc; ++vc) {
-        Csr& c = h->deps[vc];
-        if (n) k_txns_to_global<<<ceil_div((long)n, 256), 256, 0, st>>>(n, c.ent_off, c.tcnt, c.txns, h->gid);
+    // 1. rows with deps, partitioned by destination
+    uint32_t *rank = nullptr, *list = nullptr, *xtot = h->totd;              // totals: totd[0..MAX_STORES)
+    CK(dalloc(h, S_XRANK, &rank, n)); CK(dalloc(h, S_XLIST, &list, n));
+    std::vector<uint32_t> tot(MAX_STORES, 0);
+    if (n) {
+        DestOp op{};
+        op.dest = h->hstore; op.nvc = nvc; op.rank = rank; op.totals = xtot; op.n = n;
+        for (int c = 0; c < nvc; ++c) op.tcnt[c] = h->deps[c].tcnt;
+        device_scan(op, n, (DestOp::S*)h->scratch, st);
+        k_export_list<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->hstore, rank, xtot, list);
+        HIPCHK(h, hipMemcpyAsync(tot.data(), xtot, MAX_STORES * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
     }
-    // layout: header u64[3 + 3 nvc] | gid | per vc: key_off k2t_off ent_off tcnt keys k2t txns  (8-byte aligned)
+    size_t K = 0;
+    for (uint32_t d = 0; d < W; ++d) K += tot[d];
+    // 2. offsets over the export list, read at every destination boundary
+    uint32_t* xoff = nullptr;
+    CK(dalloc(h, S_XOFF, &xoff, (size_t)3 * nvc * (K + 1)));
+    ExportOffs o{};
+    for (int c = 0; c < nvc; ++c) {
+        o.ok[c] = xoff + (size_t)(3 * c + 0) * (K + 1);
+        o.om[c] = xoff + (size_t)(3 * c + 1) * (K + 1);
+        o.ot[c] = xoff + (size_t)(3 * c + 2) * (K + 1);
+    }
+    uint32_t* bnd = nullptr;
+    CK(dalloc(h, S_XBND, &bnd, (size_t)(MAX_STORES + 1) * NVC_MAX * 3));
+    std::vector<uint32_t> hb((size_t)(W + 1) * nvc * 3, 0);
+    if (K) {
+        NV_DISPATCH((int)h->cfg.replicas, launch_export_offsets_nv, h, K, list, o);
+        k_export_bounds<<<1, 256, 0, st>>>((int)W, nvc, xtot, o, bnd);
+        HIPCHK(h, hipMemcpyAsync(hb.data(), bnd, hb.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    // 3. per-destination layout, headers, fill
+    std::vector<uint64_t> sec((size_t)MAX_STORES * SEC_PER_DEST, 0);
+    h->send_sizes.assign(W, 0);
     const size_t hdr_words = 3 + 3 * (size_t)nvc;
-    size_t off = align8(hdr_words * 8);
-    std::vector<Segment> segs;
-    segs.push_back(Segment{h->gid, (void*)off, n * 4}); off = align8(off + n * 4);
-    for (int vc = 0; vc < nvc; ++vc) {
-        Csr& c = h->deps[vc];
-        segs.push_back(Segment{c.key_off, (void*)off, (n + 1) * 4}); off = align8(off + (n + 1) * 4);
-        segs.push_back(Segment{c.k2t_off, (void*)off, (n + 1) * 4}); off = align8(off + (n + 1) * 4);
-        segs.push_back(Segment{c.ent_off, (void*)off, (n + 1) * 4}); off = align8(off + (n + 1) * 4);
-        segs.push_back(Segment{c.tcnt, (void*)off, n * 4}); off = align8(off + n * 4);
-        segs.push_back(Segment{c.keys, (void*)off, c.nkeys * 8}); off = align8(off + c.nkeys * 8);
-        segs.push_back(Segment{c.k2t, (void*)off, c.nk2t * 4}); off = align8(off + c.nk2t * 4);
-        segs.push_back(Segment{c.txns, (void*)off, c.ncap * 4}); off = align8(off + c.ncap * 4);
+    h->send_hdr.assign((size_t)W * hdr_words, 0);
+    size_t total = 0;
+    std::vector<size_t> base(W, 0);
+    for (uint32_t d = 0; d < W; ++d) {
+        std::vector<uint32_t> cnt((size_t)3 * nvc, 0);
+        for (int c = 0; c < nvc; ++c)
+            for (int k = 0; k < 3; ++k) cnt[3 * c + k] = hb[((size_t)(d + 1) * nvc + c) * 3 + k] - hb[((size_t)d * nvc + c) * 3 + k];
+        const size_t sz = blob_layout(tot[d], nvc, cnt.data(), sec.data() + (size_t)d * SEC_PER_DEST);
+        for (int k = 0; k < SEC_PER_DEST; ++k) sec[(size_t)d * SEC_PER_DEST + k] += total;
+        uint64_t* hd = h->send_hdr.data() + (size_t)d * hdr_words;
+        hd[0] = 0xAD5EC0DFull; hd[1] = tot[d]; hd[2] = (uint64_t)nvc;
+        for (int c = 0; c < 3 * nvc; ++c) hd[3 + c] = cnt[c];
+        base[d] = total;
+        h->send_sizes[d] = sz;
+        bytes[d] = sz;
+        total += sz;
     }
-    const size_t total = off;
-    CK(dalloc(h, S_SEND, &h->send, total));
-    std::vector<uint64_t> hdr(hdr_words);
-    hdr[0] = 0xAD5EC0DEull; hdr[1] = n; hdr[2] = (uint64_t)nvc;
-    for (int vc = 0; vc < nvc; ++vc) {
-        hdr[3 + 3 * vc] = h->deps[vc].nkeys; hdr[4 + 3 * vc] = h->deps[vc].nk2t; hdr[5 + 3 * vc] = h->deps[vc].ncap;
-    }
-    HIPCHK(h, hipMemcpyAsync(h->send, hdr.data(), hdr_words * 8, hipMemcpyHostToDevice, st));
-    for (size_t b = 0; b < segs.size(); b += MAX_SEGS) {
-        SegTable tab{};
-        tab.count = (int)std::min<size_t>(MAX_SEGS, segs.size() - b);
-        for (int k = 0; k < tab.count; ++k) {
-            tab.s[k] = segs[b + k];
-            tab.s[k].dst = h->send + (size_t)segs[b + k].dst;
-            if (tab.s[k].bytes == 0) tab.s[k].src = tab.s[k].dst;
+    CK(dalloc(h, S_SEND, &h->send, std::max<size_t>(total, 8)));
+    uint64_t* dsec = nullptr;
+    CK(dalloc(h, S_XSEC, &dsec, sec.size()));
+    HIPCHK(h, hipMemsetAsync(h->send, 0, total, st));
+    HIPCHK(h, hipMemcpyAsync(dsec, sec.data(), sec.size() * 8, hipMemcpyHostToDevice, st));
+    for (uint32_t d = 0; d < W; ++d)
+        HIPCHK(h, hipMemcpyAsync(h->send + base[d], h->send_hdr.data() + (size_t)d * hdr_words, hdr_words * 8, hipMemcpyHostToDevice, st));
+    if (K) {
+        ExportFillArgs fa{};
+        fa.K = K; fa.nvc = nvc; fa.list = list; fa.dest = h->hstore; fa.totals = xtot; fa.gid = h->gid; fa.bnd = bnd;
+        fa.sec = dsec; fa.send = h->send; fa.o = o;
+        for (int c = 0; c < nvc; ++c) {
+            const Csr& x = h->deps[c];
+            fa.key_off[c] = x.key_off; fa.keys[c] = x.keys; fa.k2t_off[c] = x.k2t_off; fa.k2t[c] = x.k2t;
+            fa.ent_off[c] = x.ent_off; fa.tcnt[c] = x.tcnt; fa.txns[c] = x.txns;
         }
-        k_copy_segments<<<dim3(64, tab.count), 256, 0, st>>>(tab);
+        k_export_fill<<<ceil_div((long)K, 256), 256, 0, st>>>(fa);
     }
-    HIPCHK(h, hipStreamSynchronize(st));   // host header buffer lifetime
+    HIPCHK(h, hipStreamSynchronize(st));   // host header / section buffers
     h->send_bytes = total;
-    *bytes = total;
     return AD_OK;
 }
 
-int ad_shard_blob_to_host(ad_handle* h, void* dst) {
+int ad_shard_send_to_host(ad_handle* h, void* dst) {
     if (!h || !dst || !h->send) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    HIPCHK(h, hipMemcpyAsync(dst, h->send, h->send_bytes, hipMemcpyDeviceToHost, h->st));
+    if (h->send_bytes) HIPCHK(h, hipMemcpyAsync(dst, h->send, h->send_bytes, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return AD_OK;
 }
 
-static int parse_recv(ad_handle* h) {
+// Views into the received per-source blobs (concatenated in source order, sizes[s] bytes each).
+static int parse_recv(ad_handle* h, const uint64_t* sizes) {
     const int nvc = 2 * (int)h->cfg.replicas;
     const size_t hdr_words = 3 + 3 * (size_t)nvc;
-    std::vector<uint64_t> hdr(hdr_words * h->world);
-    for (uint32_t s = 0; s < h->world; ++s)
-        HIPCHK(h, hipMemcpyAsync(hdr.data() + s * hdr_words, h->recv + s * h->stride, hdr_words * 8, hipMemcpyDeviceToHost, h->st));
+    const uint32_t W = h->world;
+    std::vector<size_t> off(W, 0);
+    for (uint32_t s = 1; s < W; ++s) off[s] = off[s - 1] + sizes[s - 1];
+    std::vector<uint64_t> hdr(hdr_words * W, 0);
+    for (uint32_t s = 0; s < W; ++s) {
+        if (sizes[s] < hdr_words * 8) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": truncated");
+        HIPCHK(h, hipMemcpyAsync(hdr.data() + s * hdr_words, h->recv + off[s], hdr_words * 8, hipMemcpyDeviceToHost, h->st));
+    }
     HIPCHK(h, hipStreamSynchronize(h->st));
-    h->src_csr.assign((size_t)h->world * nvc, Csr{});
-    h->src_gid.assign(h->world, nullptr);
-    h->src_n.assign(h->world, 0);
-    for (uint32_t s = 0; s < h->world; ++s) {
+    h->src_csr.assign((size_t)W * nvc, Csr{});
+    h->src_gid.assign(W, nullptr);
+    h->src_n.assign(W, 0);
+    for (uint32_t s = 0; s < W; ++s) {
         const uint64_t* hd = hdr.data() + s * hdr_words;
-        if (hd[0] != 0xAD5EC0DEull || hd[2] != (uint64_t)nvc) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": bad header (replicas must match)");
-        const size_t ns = hd[1];
-        uint8_t* base = h->recv + s * h->stride;
-        size_t off = align8(hdr_words * 8);
-        h->src_gid[s] = (uint32_t*)(base + off); off = align8(off + ns * 4);
-        h->src_n[s] = (uint32_t)ns;
-        for (int vc = 0; vc < nvc; ++vc) {
-            Csr& c = h->src_csr[(size_t)s * nvc + vc];
-            c.nkeys = hd[3 + 3 * vc]; c.nk2t = hd[4 + 3 * vc]; c.ncap = hd[5 + 3 * vc];
-            c.key_off = (uint32_t*)(base + off); off = align8(off + (ns + 1) * 4);
-            c.k2t_off = (uint32_t*)(base + off); off = align8(off + (ns + 1) * 4);
-            c.ent_off = (uint32_t*)(base + off); off = align8(off + (ns + 1) * 4);
-            c.tcnt = (uint32_t*)(base + off); off = align8(off + ns * 4);
-            c.keys = (uint64_t*)(base + off); off = align8(off + c.nkeys * 8);
-            c.k2t = (int32_t*)(base + off); off = align8(off + c.nk2t * 4);
-            c.txns = (uint32_t*)(base + off); off = align8(off + c.ncap * 4);
+        if (hd[0] != 0xAD5EC0DFull || hd[2] != (uint64_t)nvc)
+            return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": bad header (replicas must match)");
+        const size_t rows = hd[1];
+        std::vector<uint32_t> cnt((size_t)3 * nvc);
+        for (int c = 0; c < 3 * nvc; ++c) cnt[c] = (uint32_t)hd[3 + c];
+        std::vector<uint64_t> sec(SEC_PER_DEST, 0);
+        if (blob_layout(rows, nvc, cnt.data(), sec.data()) > sizes[s])
+            return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + " exceeds its size");
+        uint8_t* b = h->recv + off[s];
+        h->src_gid[s] = (uint32_t*)(b + sec[0]);
+        h->src_n[s] = (uint32_t)rows;
+        for (int c = 0; c < nvc; ++c) {
+            Csr& x = h->src_csr[(size_t)s * nvc + c];
+            x.nkeys = cnt[3 * c]; x.nk2t = cnt[3 * c + 1]; x.ncap = cnt[3 * c + 2];
+            x.key_off = (uint32_t*)(b + sec[1 + 7 * c]); x.k2t_off = (uint32_t*)(b + sec[2 + 7 * c]);
+            x.ent_off = (uint32_t*)(b + sec[3 + 7 * c]); x.tcnt = (uint32_t*)(b + sec[4 + 7 * c]);
+            x.keys = (uint64_t*)(b + sec[5 + 7 * c]); x.k2t = (int32_t*)(b + sec[6 + 7 * c]); x.txns = (uint32_t*)(b + sec[7 + 7 * c]);
         }
-        if (off > h->stride) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + " exceeds the stride");
     }
     return AD_OK;
 }
 
-int ad_shard_import_host(ad_handle* h, const void* src, uint32_t world, size_t stride) {
-    if (!h || !src || world == 0 || world > 64) return AD_ERR_ARGUMENT;
+int ad_shard_import_host(ad_handle* h, const void* src, uint32_t world, const uint64_t* sizes /* [world] */) {
+    if (!h || !src || !sizes || world != h->world) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    CK(dalloc(h, S_RECV, &h->recv, (size_t)world * stride));
-    HIPCHK(h, hipMemcpyAsync(h->recv, src, (size_t)world * stride, hipMemcpyHostToDevice, h->st));
-    h->world = world; h->stride = stride;
-    return parse_recv(h);
+    size_t total = 0;
+    for (uint32_t s = 0; s < world; ++s) total += sizes[s];
+    CK(dalloc(h, S_RECV, &h->recv, std::max<size_t>(total, 8)));
+    if (total) HIPCHK(h, hipMemcpyAsync(h->recv, src, total, hipMemcpyHostToDevice, h->st));
+    return parse_recv(h, sizes);
 }
 
 int ad_comm_unique_id(uint8_t* out /* [128] */) {
@@ -1237,27 +1330,30 @@ int ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id_
     std::memcpy(&id, id_bytes, sizeof(id));
     ncclResult_t r = ncclCommInitRank(&h->comm, (int)world, id, (int)rank);
     if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    h->world = world;
     return AD_OK;
 }
 
-// RCCL all-gather of the packed blobs over xGMI (every rank passes the same stride >= max blob bytes).
-int ad_shard_allgather(ad_handle* h, size_t stride) {
-    if (!h || !h->comm || !h->send) return set_err(h, AD_ERR_STATE, "ad_shard_allgather: ad_comm_init + ad_shard_export first");
-    if (stride < h->send_bytes) return AD_ERR_ARGUMENT;
+// RCCL all-to-all of the per-destination blobs over xGMI (grouped point-to-point send/recv; the recv
+// sizes come from the peers' export sizes, exchanged by the caller).
+int ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world] */) {
+    if (!h || !recv_sizes) return AD_ERR_ARGUMENT;
+    if (!h->comm || !h->send) return set_err(h, AD_ERR_STATE, "ad_shard_alltoall: ad_comm_init + ad_shard_export first");
     hipSetDevice(h->device);
-    if (h->bufs[S_SEND].cap < stride) {        // the collective reads `stride` bytes: grow, keeping the packed blob
-        uint8_t* tmp = nullptr;
-        CK(dalloc(h, S_RECV, &tmp, h->send_bytes));
-        HIPCHK(h, hipMemcpyAsync(tmp, h->send, h->send_bytes, hipMemcpyDeviceToDevice, h->st));
-        CK(dalloc(h, S_SEND, &h->send, stride));
-        HIPCHK(h, hipMemcpyAsync(h->send, tmp, h->send_bytes, hipMemcpyDeviceToDevice, h->st));
+    const uint32_t W = h->world;
+    size_t total = 0;
+    for (uint32_t s = 0; s < W; ++s) total += recv_sizes[s];
+    CK(dalloc(h, S_RECV, &h->recv, std::max<size_t>(total, 8)));
+    size_t so = 0, ro = 0;
+    if (ncclGroupStart() != ncclSuccess) return set_err(h, AD_ERR_DEVICE, "ncclGroupStart");
+    for (uint32_t p = 0; p < W; ++p) {
+        if (h->send_sizes[p]) ncclSend(h->send + so, h->send_sizes[p], ncclUint8, (int)p, h->comm, h->st);
+        if (recv_sizes[p]) ncclRecv(h->recv + ro, recv_sizes[p], ncclUint8, (int)p, h->comm, h->st);
+        so += h->send_sizes[p];
+        ro += recv_sizes[p];
     }
-    CK(dalloc(h, S_RECV, &h->recv, (size_t)h->world * stride));
-    h->stride = stride;
-    ncclResult_t r = ncclAllGather(h->send, h->recv, stride, ncclUint8, h->comm, h->st);
-    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-    return parse_recv(h);
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclSend/Recv: ") + ncclGetErrorString(r));
+    return parse_recv(h, recv_sizes);
 }
 
 // Home txns: merge every store's fragment per view (k_merge over sources with row indirection), then
@@ -1271,6 +1367,7 @@ int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
     const size_t n = h->n;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     if (h->world > (uint32_t)MAXV) return set_err(h, AD_ERR_UNSUPPORTED, "more than 8 shards");
+    if (h->src_csr.size() != (size_t)h->world * nvc) return set_err(h, AD_ERR_STATE, "ad_shard_merge: exchange the blobs first");
     // home rows + global ids
     CK(dalloc(h, S_HROWS, &h->home_rows, n + 1));
     uint32_t* tot = nullptr;
@@ -1319,17 +1416,11 @@ int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
     h->times.merged_entries = ent;
     if (n_home) *n_home = H;
     if (sizes) {
+        // merge outputs carry exact unique-TxnId offsets (MultiOffsetsOp), so ncap is the TxnId total
         for (int v = 0; v <= nv; ++v) {
             for (int c = 0; c < 2; ++c) {
                 const Csr& x = v < nv ? h->sdeps[2 * v + c] : h->smerged[c];
-                std::vector<uint32_t> cnt(H);
-                if (H && x.ncap) {
-                    HIPCHK(h, hipMemcpyAsync(cnt.data(), x.tcnt, H * 4, hipMemcpyDeviceToHost, st));
-                    HIPCHK(h, hipStreamSynchronize(st));
-                }
-                size_t t = 0;
-                for (uint32_t q : cnt) t += q;
-                sizes[v * 3 + c] = ad_csr_sizes{H, x.nkeys, x.nk2t, x.ncap, t};
+                sizes[v * 3 + c] = ad_csr_sizes{H, x.nkeys, x.nk2t, x.ncap, x.ncap};
             }
             sizes[v * 3 + 2] = ad_csr_sizes{H, 0, 0, 0, 0};
         }

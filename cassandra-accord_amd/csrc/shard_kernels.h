@@ -5,42 +5,19 @@
 // the PreAccept deps that its keys produce (its local batch: the txns, with their keys sliced to the range,
 // in global TxnId order; row -> global arrival rank through `gid`).  PreAccept.reduce across stores
 // (messages/PreAccept.java:141-156: Deps.with of the per-store PartialDeps) becomes:
-//   export    each store packs its per-(view, class) CSRs, TxnIds rewritten to global ranks, into one blob;
-//   exchange  all-gather of the blobs (RCCL over xGMI, or host staging over gloo);
-//   merge     each store's home txns (first key in its range) merge the fragments of every store, per view
-//             (k_merge with per-source row indirection), then Deps.merge across the replica views.
+//   export    each store packs, per destination store, the per-(view, class) CSR rows of the local txns
+//             homed there (home = the store of the txn's first key) that have any deps, TxnIds rewritten
+//             to global ranks: one blob per destination, concatenated in destination order;
+//   exchange  all-to-all of the blobs (RCCL grouped send/recv over xGMI, or host staging over gloo):
+//             every store receives only the fragments of its own home txns;
+//   merge     each store's home txns merge the fragments of every store, per view (k_merge with
+//             per-source row indirection), then Deps.merge across the replica views.
 // Execution levels: each store runs the chain fixpoint over its own keys on a replicated global level
 // array; stores exchange it with an all-reduce(max) until no store raises a level.
 #pragma once
 #include "level_kernels.h"
 
 namespace ad {
-
-// txns lists of a capacity-form CSR: local row -> global rank (valid entries only; the capacity slack
-// past tcnt is never read)
-__global__ __launch_bounds__(256) void k_txns_to_global(size_t n, const uint32_t* __restrict__ ent_off, const uint32_t* __restrict__ tcnt,
-                                                        uint32_t* __restrict__ txns, const uint32_t* __restrict__ gid) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint32_t b = ent_off[t], e = b + tcnt[t];
-    for (uint32_t x = b; x < e; ++x) txns[x] = gid[txns[x]];
-}
-
-struct Segment { const void* src; void* dst; uint64_t bytes; };
-constexpr int MAX_SEGS = 160;
-struct SegTable { Segment s[MAX_SEGS]; int count; };
-
-// batched device memcpy: blockIdx.y = segment, blocks stride over its 16-byte words
-__global__ __launch_bounds__(256) void k_copy_segments(SegTable tab) {
-    const int k = blockIdx.y;
-    if (k >= tab.count) return;
-    const Segment sg = tab.s[k];
-    const uint64_t words = sg.bytes / 4;
-    const uint32_t* src = (const uint32_t*)sg.src;
-    uint32_t* dst = (uint32_t*)sg.dst;
-    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < words; x += (uint64_t)gridDim.x * blockDim.x)
-        dst[x] = src[x];
-}
 
 struct CompactFlagOp {            // rows with flag -> out[] (exclusive-scan scatter)
     using S = uint32_t;
@@ -56,6 +33,150 @@ struct CompactFlagOp {            // rows with flag -> out[] (exclusive-scan sca
         if (i + 1 == n) *total = inc;
     }
 };
+
+// ---- export: rows with deps, partitioned by destination store ----------------------------------------
+constexpr int MAX_STORES = 8;
+struct DestOp {                       // per row: rank among the kept rows of its destination
+    struct S { uint32_t c[MAX_STORES]; };
+    const uint8_t* dest;
+    const uint32_t* tcnt[NVC_MAX];    // per (view, class): per-row unique TxnId counts
+    int nvc;
+    uint32_t* rank;                   // [n] rank within destination, or ~0u (no deps: not exported)
+    uint32_t* totals;                 // [MAX_STORES]
+    size_t n;
+    __device__ S identity() const { S s; for (int k = 0; k < MAX_STORES; ++k) s.c[k] = 0; return s; }
+    __device__ bool keep(size_t r) const {
+        uint32_t any = 0;
+        for (int vc = 0; vc < nvc; ++vc) any |= tcnt[vc][r];
+        return any != 0;
+    }
+    __device__ S load(size_t r) const {
+        S s = identity();
+        if (keep(r)) s.c[dest[r]] = 1;
+        return s;
+    }
+    __device__ S combine(const S& a, const S& b) const { S s; for (int k = 0; k < MAX_STORES; ++k) s.c[k] = a.c[k] + b.c[k]; return s; }
+    __device__ void store(size_t r, const S& ex, const S& inc, const S& el) const {
+        const uint32_t d = dest[r];
+        rank[r] = el.c[d] ? ex.c[d] : ~0u;
+        if (r + 1 == n) for (int k = 0; k < MAX_STORES; ++k) totals[k] = inc.c[k];
+    }
+};
+// list[base[d] + rank] = r  (base = exclusive prefix of the destination totals, computed in-kernel)
+__global__ __launch_bounds__(256) void k_export_list(size_t n, const uint8_t* __restrict__ dest, const uint32_t* __restrict__ rank,
+                                                     const uint32_t* __restrict__ totals, uint32_t* __restrict__ list) {
+    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n || rank[r] == ~0u) return;
+    uint32_t base = 0;
+    for (uint32_t d = 0; d < dest[r]; ++d) base += totals[d];
+    list[base + rank[r]] = (uint32_t)r;
+}
+// global (over the export list) offsets of keys / keysToTxnIds / TxnIds per (view, class)
+template <int NVC>
+struct ExportOffsetsOp {
+    struct S { uint32_t k[NVC], m[NVC], t[NVC]; };
+    static constexpr int nvc = NVC;
+    const uint32_t* list;
+    const uint32_t* key_off[NVC];     // source CSRs (capacity form)
+    const uint32_t* k2t_off[NVC];
+    const uint32_t* tcnt[NVC];
+    uint32_t* ok[NVC];                // [K+1] each
+    uint32_t* om[NVC];
+    uint32_t* ot[NVC];
+    size_t n;                         // K
+    __device__ S identity() const { S s; for (int c = 0; c < NVC; ++c) { s.k[c] = s.m[c] = s.t[c] = 0; } return s; }
+    __device__ S load(size_t j) const {
+        S s = identity();
+        const uint32_t r = list[j];
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) {
+            s.k[c] = key_off[c][r + 1] - key_off[c][r];
+            s.m[c] = k2t_off[c][r + 1] - k2t_off[c][r];
+            s.t[c] = tcnt[c][r];
+        }
+        return s;
+    }
+    __device__ S combine(const S& a, const S& b) const {
+        S s;
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) { s.k[c] = a.k[c] + b.k[c]; s.m[c] = a.m[c] + b.m[c]; s.t[c] = a.t[c] + b.t[c]; }
+        return s;
+    }
+    __device__ void store(size_t j, const S& ex, const S& inc, const S&) const {
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) {
+            ok[c][j] = ex.k[c]; om[c][j] = ex.m[c]; ot[c][j] = ex.t[c];
+            if (j + 1 == n) { ok[c][n] = inc.k[c]; om[c][n] = inc.m[c]; ot[c][n] = inc.t[c]; }
+        }
+    }
+};
+// the global offsets at every destination boundary: out[(d * nvc + c) * 3 + {0,1,2}], d = 0..world
+struct ExportOffs { uint32_t* ok[NVC_MAX]; uint32_t* om[NVC_MAX]; uint32_t* ot[NVC_MAX]; };
+__global__ void k_export_bounds(int world, int nvc, const uint32_t* __restrict__ totals, ExportOffs o, uint32_t* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i >= (world + 1) * nvc) return;
+    const int d = i / nvc, c = i % nvc;
+    uint32_t base = 0;
+    for (int x = 0; x < d; ++x) base += totals[x];
+    out[i * 3 + 0] = o.ok[c][base];
+    out[i * 3 + 1] = o.om[c][base];
+    out[i * 3 + 2] = o.ot[c][base];
+}
+// Destination blob sections (byte offsets from the send buffer base), per destination:
+// [0] gid, then per vc: [1+7c] key_off [2+7c] k2t_off [3+7c] ent_off [4+7c] tcnt [5+7c] keys [6+7c] k2t [7+7c] txns
+constexpr int SEC_PER_DEST = 1 + 7 * NVC_MAX;
+struct ExportFillArgs {
+    size_t K;
+    int nvc;
+    const uint32_t* list;
+    const uint8_t* dest;
+    const uint32_t* totals;           // rows per destination
+    const uint32_t* gid;
+    const uint32_t* bnd;              // k_export_bounds output
+    const uint64_t* sec;              // [MAX_STORES * SEC_PER_DEST]
+    uint8_t* send;
+    const uint32_t* key_off[NVC_MAX];
+    const uint64_t* keys[NVC_MAX];
+    const uint32_t* k2t_off[NVC_MAX];
+    const int32_t* k2t[NVC_MAX];
+    const uint32_t* ent_off[NVC_MAX];
+    const uint32_t* tcnt[NVC_MAX];
+    const uint32_t* txns[NVC_MAX];
+    ExportOffs o;
+};
+// one thread per exported row: its gid, rebased offsets, and its keys / keysToTxnIds / TxnIds (as global
+// ranks) copied into its destination's blob; the destination's last row writes the closing offsets
+__global__ __launch_bounds__(256) void k_export_fill(ExportFillArgs a) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.K) return;
+    const uint32_t r = a.list[j];
+    const uint32_t d = a.dest[r];
+    uint32_t base = 0;
+    for (uint32_t x = 0; x < d; ++x) base += a.totals[x];
+    const uint32_t i = (uint32_t)j - base;
+    const bool last = i + 1 == a.totals[d];
+    const uint64_t* sec = a.sec + (size_t)d * SEC_PER_DEST;
+    reinterpret_cast<uint32_t*>(a.send + sec[0])[i] = a.gid[r];
+    for (int c = 0; c < a.nvc; ++c) {
+        const uint32_t* b0 = a.bnd + ((size_t)d * a.nvc + c) * 3;         // this destination's first row
+        const uint32_t kb = a.o.ok[c][j] - b0[0], mb = a.o.om[c][j] - b0[1], tb = a.o.ot[c][j] - b0[2];
+        uint32_t* key_off = reinterpret_cast<uint32_t*>(a.send + sec[1 + 7 * c]);
+        uint32_t* k2t_off = reinterpret_cast<uint32_t*>(a.send + sec[2 + 7 * c]);
+        uint32_t* ent_off = reinterpret_cast<uint32_t*>(a.send + sec[3 + 7 * c]);
+        uint32_t* tcnt = reinterpret_cast<uint32_t*>(a.send + sec[4 + 7 * c]);
+        uint64_t* keys = reinterpret_cast<uint64_t*>(a.send + sec[5 + 7 * c]);
+        int32_t* k2t = reinterpret_cast<int32_t*>(a.send + sec[6 + 7 * c]);
+        uint32_t* txns = reinterpret_cast<uint32_t*>(a.send + sec[7 + 7 * c]);
+        const uint32_t sk = a.key_off[c][r], nk = a.key_off[c][r + 1] - sk;
+        const uint32_t sm = a.k2t_off[c][r], nm = a.k2t_off[c][r + 1] - sm;
+        const uint32_t st = a.ent_off[c][r], nt = a.tcnt[c][r];
+        key_off[i] = kb; k2t_off[i] = mb; ent_off[i] = tb; tcnt[i] = nt;
+        if (last) { key_off[i + 1] = kb + nk; k2t_off[i + 1] = mb + nm; ent_off[i + 1] = tb + nt; }
+        for (uint32_t x = 0; x < nk; ++x) keys[kb + x] = a.keys[c][sk + x];
+        for (uint32_t x = 0; x < nm; ++x) k2t[mb + x] = a.k2t[c][sm + x];
+        for (uint32_t x = 0; x < nt; ++x) txns[tb + x] = a.gid[a.txns[c][st + x]];
+    }
+}
 
 // home txns: global ids
 __global__ __launch_bounds__(256) void k_home_gid(size_t H, const uint32_t* __restrict__ rows, const uint32_t* __restrict__ gid,

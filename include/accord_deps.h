@@ -233,23 +233,29 @@ int  ad_kernel_units(ad_handle* h, int kid, uint64_t* units);
 /* PreAccept.reduce (messages/PreAccept.java:141-156, Deps.with of the per-store PartialDeps). */
 /* Protocol per store:                                                                         */
 /*   ad_load_batch(local batch: txns touching the store's key range, keys sliced to it)        */
-/*   ad_shard_setup(local row -> global rank, home flags)   then ad_preaccept_deps              */
-/*   ad_shard_export -> exchange (ad_comm_init + ad_shard_allgather over RCCL/xGMI, or          */
-/*   ad_shard_blob_to_host / ad_shard_import_host over a host transport) -> ad_shard_merge      */
+/*   ad_shard_setup(local row -> global rank, local row -> home store)   then ad_preaccept_deps */
+/*   ad_shard_export: per destination store, the deps rows of the local txns homed there (rows  */
+/*   without deps are not sent), TxnIds as global ranks -> bytes[d]                             */
+/*   exchange: all-to-all (the peers' byte counts give recv_sizes): ad_comm_init +              */
+/*   ad_shard_alltoall over RCCL/xGMI, or ad_shard_send_to_host / ad_shard_import_host over a   */
+/*   host transport -> ad_shard_merge                                                          */
 /*   levels: ad_shard_levels_round, all-reduce(max) of the global level array                  */
 /*   (ad_shard_levels_allreduce over RCCL, or _get/_set), repeat until no store raised a level; */
 /*   ad_shard_order.                                                                           */
 /* Home txn = its first key lies in this store's range; results are per home txn, TxnIds as    */
-/* global ranks.  Range txns are not supported in sharded mode (AD_ERR_UNSUPPORTED).           */
+/* global ranks.  Range txns are not supported in sharded mode (AD_ERR_UNSUPPORTED).  At most 8 */
+/* stores.                                                                                     */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_shard_bounds(const uint64_t* keys, size_t nkeys, uint32_t shards, uint64_t* bounds_out /* [shards+1] */);
-int  ad_shard_setup(ad_handle* h, const uint32_t* gid /* [n] ascending */, const uint8_t* home /* [n] */, size_t n_global);
-int  ad_shard_export(ad_handle* h, size_t* bytes);
-int  ad_shard_blob_to_host(ad_handle* h, void* dst);
-int  ad_shard_import_host(ad_handle* h, const void* src /* [world * stride] */, uint32_t world, size_t stride);
+int  ad_shard_setup(ad_handle* h, const uint32_t* gid /* [n] ascending */, const uint8_t* home_store /* [n] */,
+                    uint32_t self, uint32_t world, size_t n_global);
+int  ad_shard_export(ad_handle* h, uint64_t* bytes /* [world]: blob size per destination */);
+int  ad_shard_send_to_host(ad_handle* h, void* dst /* [sum bytes]: blobs in destination order */);
+int  ad_shard_import_host(ad_handle* h, const void* src /* blobs in source order */, uint32_t world,
+                          const uint64_t* sizes /* [world] */);
 int  ad_comm_unique_id(uint8_t* out /* [128] */);
 int  ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id /* [128] */);
-int  ad_shard_allgather(ad_handle* h, size_t stride /* max blob bytes over ranks */);
+int  ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world]: peers' bytes[this store] */);
 int  ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes /* [(replicas+1)*3]; view == replicas: merged */, size_t* n_home);
 int  ad_shard_fetch(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out, uint32_t* home_gid /* [n_home] or NULL */);
 int  ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed);

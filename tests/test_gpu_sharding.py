@@ -32,13 +32,15 @@ def test_sharded_equals_unsharded(engine_factory, name, shards):
     b = workload.config(name, n=30000)
     views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
     bounds = sharding.even_bounds(0, 10_000_000, shards)
+    hs = sharding.home_stores(b, bounds)
     stores = []
     try:
         for k in range(shards):
             local, gid, home = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+            assert np.array_equal(home, (hs[gid] == k).astype(np.uint8))
             st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
             stores.append(st)
-            st.load(local, gid, home, b["n"])
+            st.load(local, gid, hs[gid], b["n"], k, shards)
         rounds = sharding.LocalTransport.run(stores)
         assert rounds >= 1
         seen = np.zeros(b["n"], bool)
