@@ -161,6 +161,22 @@ def print_breakdown(brk, st):
     print("  stages: %s" % {k: round(v, 3) if isinstance(v, float) else v for k, v in st.items()}, file=sys.stderr)
 
 
+class stdout_to_stderr:
+    """Native libraries (gloo, RCCL) print banners on the C-level stdout; the bench's stdout carries only
+    its one JSON line, so their output is sent to stderr while they initialise."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def main_sharded(args, rank, world, local, dist):
     """N > 1: the C5 cross-shard protocol (see module docstring)."""
     from accord_amd import sharding
@@ -176,7 +192,8 @@ def main_sharded(args, rank, world, local, dist):
     tr = None
     if args.transport == "rccl":
         try:
-            tr = sharding.RcclTransport(dist, store, rank, world)
+            with stdout_to_stderr():      # RCCL's version banner
+                tr = sharding.RcclTransport(dist, store, rank, world)
         except engine.AccordDepsError as e:     # e.g. ranks sharing one GPU: RCCL refuses duplicate devices
             print("rank %d: RCCL unavailable (%s); using the host transport" % (rank, e), file=sys.stderr)
         ok = tr is not None
@@ -253,16 +270,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as tdist
-        # gloo prints connection notices on the C-level stdout; keep stdout for the one JSON line
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
+        with stdout_to_stderr():          # gloo's connection notices
             tdist.init_process_group("gloo")
-        finally:
-            sys.stdout.flush()
-            os.dup2(saved, 1)
-            os.close(saved)
         try:
             main_sharded(args, rank, world, local, tdist)
         finally:

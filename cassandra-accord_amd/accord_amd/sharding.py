@@ -97,7 +97,7 @@ class ShardStore:
         L.ad_shard_levels_round.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32)]
         L.ad_shard_levels_get.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.ad_shard_levels_set.argtypes = [vp, C.POINTER(C.c_uint32)]
-        L.ad_shard_levels_allreduce.argtypes = [vp]
+        L.ad_shard_levels_allreduce.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.ad_shard_order.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
 
     def close(self):
@@ -183,7 +183,10 @@ class ShardStore:
         self._check(self.L.ad_shard_levels_set(self.eng.h, _u32p(g)), "ad_shard_levels_set")
 
     def levels_allreduce(self):
-        self._check(self.L.ad_shard_levels_allreduce(self.eng.h), "ad_shard_levels_allreduce")
+        """RCCL all-reduce(max) of the level array; returns whether any store raised a level this round."""
+        ch = C.c_uint32()
+        self._check(self.L.ad_shard_levels_allreduce(self.eng.h, C.byref(ch)), "ad_shard_levels_allreduce")
+        return bool(ch.value)
 
     def order(self):
         lv = np.zeros(max(self.n_home, 1), np.uint32)
@@ -236,10 +239,12 @@ class GlooTransport:
                                     input_split_sizes=[int(x) for x in sizes])
         store.import_host(recv.numpy(), rsz)
 
-    def allreduce_levels(self, store):
-        g = self.torch.from_numpy(store.levels_get().astype(np.int64))
+    def allreduce_levels(self, store, changed):
+        """All-reduce(max) of the level array; returns whether any store raised a level this round."""
+        g = self.torch.from_numpy(store.levels_get().astype(np.int32))
         self.dist.all_reduce(g, op=self.dist.ReduceOp.MAX)
         store.levels_set(g.numpy().astype(np.uint32))
+        return self.any(changed)
 
 
 class RcclTransport(GlooTransport):
@@ -259,8 +264,8 @@ class RcclTransport(GlooTransport):
         sizes = store.export()
         store.alltoall(self.recv_sizes(sizes))
 
-    def allreduce_levels(self, store):
-        store.levels_allreduce()
+    def allreduce_levels(self, store, changed):
+        return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
 
 def run_store(store, transport, max_rounds=1 << 16, timings=None):
@@ -286,12 +291,10 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None):
     lap("levels_local")
     rounds = 1
     while True:
-        transport.allreduce_levels(store)
+        any_changed = transport.allreduce_levels(store, changed)
         lap("levels_exchange")
-        if not transport.any(changed) or rounds >= max_rounds:
-            lap("levels_exchange")
+        if not any_changed or rounds >= max_rounds:
             break
-        lap("levels_exchange")
         changed = store.levels_round(False)
         lap("levels_local")
         rounds += 1

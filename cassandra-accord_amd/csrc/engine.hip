@@ -1472,6 +1472,8 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     if (first) h->ls.chains_ready = true;
     HIPCHK(h, hipMemsetAsync(flag, 0, 4, st));
     if (n) k_levels_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl, flag);
+    // the flag also rides in G[n_global], so the RCCL all-reduce(max) returns "any store changed"
+    HIPCHK(h, hipMemcpyAsync(h->G + h->n_global, flag, 4, hipMemcpyDeviceToDevice, st));
     HIPCHK(h, hipMemcpyAsync(changed, flag, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     h->level_iters += (uint32_t)iters;
@@ -1494,12 +1496,17 @@ int ad_shard_levels_set(ad_handle* h, const uint32_t* G) {
     return AD_OK;
 }
 
-// RCCL all-reduce(max) of the replicated global level array.
-int ad_shard_levels_allreduce(ad_handle* h) {
+// RCCL all-reduce(max) of the replicated global level array and, in its last element, of the stores'
+// "raised a level this round" flags (*any_changed, if given: no separate host collective per round).
+int ad_shard_levels_allreduce(ad_handle* h, uint32_t* any_changed) {
     if (!h || !h->comm || !h->G) return set_err(h, AD_ERR_STATE, "ad_shard_levels_allreduce: ad_comm_init + a round first");
     hipSetDevice(h->device);
-    ncclResult_t r = ncclAllReduce(h->G, h->G, h->n_global, ncclUint32, ncclMax, h->comm, h->st);
+    ncclResult_t r = ncclAllReduce(h->G, h->G, h->n_global + 1, ncclUint32, ncclMax, h->comm, h->st);
     if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    if (any_changed) {
+        HIPCHK(h, hipMemcpyAsync(any_changed, h->G + h->n_global, 4, hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipStreamSynchronize(h->st));
+    }
     return AD_OK;
 }
 

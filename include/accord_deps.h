@@ -261,7 +261,7 @@ int  ad_shard_fetch(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out, 
 int  ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed);
 int  ad_shard_levels_get(ad_handle* h, uint32_t* G /* [n_global] */);
 int  ad_shard_levels_set(ad_handle* h, const uint32_t* G);
-int  ad_shard_levels_allreduce(ad_handle* h);
+int  ad_shard_levels_allreduce(ad_handle* h, uint32_t* any_changed /* out: max of the stores' round flags, or NULL */);
 int  ad_shard_order(ad_handle* h, uint32_t* level_out /* [n_home] */, uint32_t* order_out /* [n_home] global ranks */);
 
 #ifdef __cplusplus
