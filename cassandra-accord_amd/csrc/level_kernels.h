@@ -500,7 +500,7 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
             } else if (next_w < len) {
                 sc = make_uint2((uint32_t)(s + next_w), 1u);
             }
-            succ[pr[q]] = sc;
+            if (sc.y) succ[pr[q]] = sc;        // succ was cleared: empty runs need no store
         }
     }
 }
