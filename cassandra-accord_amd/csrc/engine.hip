@@ -167,7 +167,7 @@ enum Slot : size_t {
     S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
     S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT, S_HSTORE, S_XRANK, S_XLIST, S_XOFF,
-    S_XBND, S_XSEC,
+    S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -385,6 +385,66 @@ void launch_offsets(ad_handle* h, const TxnArgs& ta, uint32_t* overflow) {
     (void)ta;
 }
 
+__global__ void k_ovf_sizes(uint32_t count, const uint2* items, const uint32_t* const* key_off, const uint32_t* const* k2t_off,
+                            uint32_t* ne) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t t = items[i].x, c = items[i].y;
+    ne[i] = k2t_off[c][t + 1] - k2t_off[c][t] - (key_off[c][t + 1] - key_off[c][t]);
+}
+
+// CSRs that overflowed the LDS union: one sync to learn how many; each gets a 1024-thread workgroup with
+// 128 KiB of LDS, or a slice of global memory above UNION_CAP_BIG entries.  The CSR blocks are the key
+// classes (large txns) and, when the batch has ranges, the RangeDeps views (item.y >= 2R: range view).
+int union_overflow(ad_handle* h, LdsUnionArgs la, uint32_t* ovf_count, uint2* ovf, bool has_range) {
+    hipStream_t st = h->st;
+    uint32_t count = 0;
+    HIPCHK(h, hipMemcpyAsync(&count, ovf_count, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (count == 0) return AD_OK;
+    count = std::min<uint32_t>(count, 1u << 20);
+    (void)has_range;
+    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
+    // tables of all CSRs the first pass may have queued: key classes [0, nvc), range views [nvc, nvc+nv)
+    LdsUnionArgs b = la;
+    std::vector<const uint32_t*> ko(nvc + nv), mo(nvc + nv);
+    for (int c = 0; c < nvc + nv; ++c) {
+        const Csr& x = c < nvc ? h->deps[c] : h->rdeps[c - nvc];
+        ko[c] = x.key_off; mo[c] = x.k2t_off;
+        b.key_off[c] = x.key_off; b.k2t_off[c] = x.k2t_off; b.ent_off[c] = x.ent_off; b.k2t[c] = x.k2t;
+        b.txns[c] = x.txns; b.tcnt[c] = x.tcnt;
+    }
+    const uint32_t** dko = nullptr;
+    uint32_t* ne = nullptr;
+    CK(dalloc(h, S_OVFT, (uint64_t**)&dko, 2 * (nvc + nv)));
+    CK(dalloc(h, S_OVFN, &ne, count));
+    HIPCHK(h, hipMemcpyAsync(dko, ko.data(), (nvc + nv) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(dko + nvc + nv, mo.data(), (nvc + nv) * 8, hipMemcpyHostToDevice, st));
+    k_ovf_sizes<<<ceil_div((long)count, 256), 256, 0, st>>>(count, ovf, dko, dko + nvc + nv, ne);
+    std::vector<uint32_t> hne(count);
+    HIPCHK(h, hipMemcpyAsync(hne.data(), ne, count * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    std::vector<uint64_t> goff(count, 0);
+    uint64_t gtot = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        if (hne[i] > (uint32_t)UNION_CAP_BIG) {
+            uint64_t n2 = 1;
+            while (n2 < hne[i]) n2 <<= 1;
+            goff[i] = gtot;
+            gtot += n2;
+        }
+    }
+    uint32_t* gbuf = nullptr;
+    uint64_t* dgoff = nullptr;
+    CK(dalloc(h, S_OVFG, &gbuf, std::max<uint64_t>(gtot, 1)));
+    CK(dalloc(h, S_OVFO, &dgoff, count));
+    HIPCHK(h, hipMemcpyAsync(dgoff, goff.data(), count * 8, hipMemcpyHostToDevice, st));
+    b.items = ovf; b.gbuf = gbuf; b.gbuf_off = dgoff;
+    k_union_big<<<count, UB_BIG, 0, st>>>(b, count);
+    HIPCHK(h, hipStreamSynchronize(st));    // host tables
+    return AD_OK;
+}
+
 int stage_deps(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
@@ -495,13 +555,20 @@ int stage_deps(ad_handle* h) {
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
     if (n > 0) { KScope ks(K_TXN_UNION, n); k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua); }
-    // large txns' key CSRs and every RangeDeps CSR: LDS sort union
+    // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
         KScope ks(K_UNION_LDS);
         LdsUnionArgs la{};
         la.n = n; la.meta = h->meta; la.prm = h->prm;
+        constexpr uint32_t OVF_CAP = 1u << 20;
+        uint32_t* ovf_count = nullptr;
+        uint2* ovf = nullptr;
+        CK(dalloc(h, S_OVF, &ovf_count, 64));
+        CK(dalloc(h, S_OVFL, &ovf, OVF_CAP));
+        HIPCHK(h, hipMemsetAsync(ovf_count, 0, 4, st));
+        la.ovf_count = ovf_count; la.ovf = ovf; la.ovf_cap = OVF_CAP;
         if (h->n_large > 0) {
-            la.ncsr = nvc; la.only_large = 1;
+            la.ncsr = nvc; la.csr_base = 0; la.only_large = 1;
             for (int vc = 0; vc < nvc; ++vc) {
                 Csr& c = h->deps[vc];
                 la.key_off[vc] = c.key_off; la.k2t_off[vc] = c.k2t_off; la.ent_off[vc] = c.ent_off; la.k2t[vc] = c.k2t;
@@ -510,14 +577,15 @@ int stage_deps(ad_handle* h) {
             k_union_lds<<<dim3((unsigned)n, (unsigned)nvc), UB, 0, st>>>(la);
         }
         if (Q > 0) {
-            la.ncsr = nv; la.only_large = 0;
+            la.ncsr = nv; la.csr_base = nvc; la.only_large = 0;
             for (int v = 0; v < nv; ++v) {
                 Csr& c = h->rdeps[v];
-                la.key_off[v] = c.key_off; la.k2t_off[v] = c.k2t_off; la.ent_off[v] = c.ent_off; la.k2t[v] = c.k2t;
-                la.txns[v] = c.txns; la.tcnt[v] = c.tcnt;
+                la.key_off[nvc + v] = c.key_off; la.k2t_off[nvc + v] = c.k2t_off; la.ent_off[nvc + v] = c.ent_off;
+                la.k2t[nvc + v] = c.k2t; la.txns[nvc + v] = c.txns; la.tcnt[nvc + v] = c.tcnt;
             }
             k_union_lds<<<dim3((unsigned)n, (unsigned)nv), UB, 0, st>>>(la);
         }
+        CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
     }
     h->have_deps = true;
     h->ls.chains_ready = false;

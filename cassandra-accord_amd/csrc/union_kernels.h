@@ -113,8 +113,9 @@ __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
 // ---------------------------------------------------------------------------------------------------
 constexpr int UB = 256;
 
-// exclusive scan of one u32 per thread; returns the exclusive prefix, *total = block sum
-__device__ inline uint32_t block_scan_u32(uint32_t v, uint32_t* lds_w /* [UB/WAVE] */, uint32_t* total) {
+// exclusive scan of one u32 per thread over an NT-thread block; returns the exclusive prefix, *total = sum
+template <int NT = UB>
+__device__ inline uint32_t block_scan_u32(uint32_t v, uint32_t* lds_w /* [NT/WAVE] */, uint32_t* total) {
     const int lane = __lane_id(), w = threadIdx.x / WAVE;
     uint32_t x = v;
 #pragma unroll
@@ -126,7 +127,7 @@ __device__ inline uint32_t block_scan_u32(uint32_t v, uint32_t* lds_w /* [UB/WAV
     __syncthreads();
     uint32_t base = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < UB / WAVE; ++k) {
+    for (int k = 0; k < NT / WAVE; ++k) {
         uint32_t s = lds_w[k];
         if (k < w) base += s;
         tot += s;
@@ -136,11 +137,13 @@ __device__ inline uint32_t block_scan_u32(uint32_t v, uint32_t* lds_w /* [UB/WAV
     return base + x - v;
 }
 
-template <int CAP>
-__device__ inline void bitonic_sort_lds(uint32_t* buf, uint32_t n2) {
+// bitonic sort of n2 (a power of two) u32 in buf — LDS, or global memory owned by this block (same CU:
+// the barrier orders the block's global accesses as it does its LDS ones)
+template <int NT>
+__device__ inline void bitonic_sort_block(uint32_t* buf, uint32_t n2) {
     for (uint32_t k = 2; k <= n2; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t x = threadIdx.x; x < n2; x += UB) {
+            for (uint32_t x = threadIdx.x; x < n2; x += NT) {
                 const uint32_t y = x ^ j;
                 if (y > x) {
                     const uint32_t a = buf[x], b = buf[y];
@@ -153,26 +156,72 @@ __device__ inline void bitonic_sort_lds(uint32_t* buf, uint32_t n2) {
     }
 }
 
-constexpr int UNION_CAP = 8192;   // dependency entries of one txn's CSR sorted in LDS (32 KiB)
+constexpr int UNION_CAP = 8192;        // dependency entries of one txn's CSR sorted in LDS (32 KiB)
+constexpr int UNION_CAP_BIG = 32768;   // overflow pass: 1024 threads, 128 KiB of LDS (gfx950: 160 KiB per CU)
+constexpr int UB_BIG = 1024;
 
+constexpr int UNION_CSRS = NVC_MAX + MAXV;   // key classes of every view, then RangeDeps of every view
 struct LdsUnionArgs {
     size_t n;
     int ncsr;
+    int csr_base;                      // this launch's CSRs are [csr_base, csr_base + ncsr) of the tables
     int only_large;
     const uint8_t* meta;
-    const uint32_t* key_off[NVC_MAX];
-    const uint32_t* k2t_off[NVC_MAX];
-    const uint32_t* ent_off[NVC_MAX];
-    int32_t* k2t[NVC_MAX];
-    uint32_t* txns[NVC_MAX];
-    uint32_t* tcnt[NVC_MAX];
+    const uint32_t* key_off[UNION_CSRS];
+    const uint32_t* k2t_off[UNION_CSRS];
+    const uint32_t* ent_off[UNION_CSRS];
+    int32_t* k2t[UNION_CSRS];
+    uint32_t* txns[UNION_CSRS];
+    uint32_t* tcnt[UNION_CSRS];
     Params* prm;
+    // overflow: (txn, csr) pairs with more than UNION_CAP entries, for the big pass
+    uint32_t* ovf_count;
+    uint2* ovf;                        // {txn, csr}
+    uint32_t ovf_cap;
+    // big pass
+    const uint2* items;                // overflow items
+    uint32_t* gbuf;                    // global sort space for items above UNION_CAP_BIG
+    const uint64_t* gbuf_off;          // [item] offset into gbuf (u32 elements)
 };
 
-// grid (n, ncsr): one workgroup per (txn, CSR)
+// Union of one (txn, CSR): sort the txn's per-key TxnId ranks in buf (n2 >= ne), unique them into the
+// CSR's TxnId table, then remap every entry to its index (RelationMultiMap.java:201-260).
+template <int NT>
+__device__ inline void union_body(uint32_t* buf, uint32_t* wsum, int32_t* body, uint32_t ne, uint32_t* out, uint32_t* tcnt) {
+    uint32_t n2 = 1;
+    while (n2 < ne) n2 <<= 1;
+    for (uint32_t x = threadIdx.x; x < n2; x += NT) buf[x] = x < ne ? (uint32_t)body[x] : 0xFFFFFFFFu;
+    __syncthreads();
+    bitonic_sort_block<NT>(buf, n2);
+    // unique compaction: each thread owns a contiguous chunk
+    const uint32_t per = (ne + NT - 1) / NT;
+    const uint32_t b0 = min(ne, threadIdx.x * per), b1 = min(ne, b0 + per);
+    uint32_t cnt = 0;
+    for (uint32_t x = b0; x < b1; ++x) cnt += (x == 0 || buf[x] != buf[x - 1]) ? 1u : 0u;
+    uint32_t total;
+    uint32_t o = block_scan_u32<NT>(cnt, wsum, &total);
+    for (uint32_t x = b0; x < b1; ++x)
+        if (x == 0 || buf[x] != buf[x - 1]) out[o++] = buf[x];
+    __syncthreads();
+    // unique list back into buf, then remap every entry to its index
+    for (uint32_t x = threadIdx.x; x < total; x += NT) buf[x] = out[x];
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < ne; x += NT) {
+        const uint32_t v = (uint32_t)body[x];
+        uint32_t lo = 0, hi = total;
+        while (lo < hi) {
+            uint32_t m = (lo + hi) >> 1;
+            if (buf[m] < v) lo = m + 1; else hi = m;
+        }
+        body[x] = (int32_t)lo;
+    }
+    if (threadIdx.x == 0) *tcnt = total;
+}
+
+// grid (n, ncsr): one workgroup per (txn, CSR); CSRs above UNION_CAP entries are queued for k_union_big
 __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
     const size_t t = blockIdx.x;
-    const int c = blockIdx.y;
+    const int c = a.csr_base + (int)blockIdx.y;
     if (t >= a.n) return;
     if (a.only_large && !(a.meta[t] & META_LARGE)) return;
     __shared__ uint32_t buf[UNION_CAP];
@@ -184,40 +233,31 @@ __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
     }
     const uint32_t mb = a.k2t_off[c][t];
     const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
-    int32_t* body = a.k2t[c] + mb + nk;
     if (ne > (uint32_t)UNION_CAP) {
-        if (threadIdx.x == 0) { atomicOr(&a.prm->err, ERR_CAP); a.tcnt[c][t] = 0; }
+        if (threadIdx.x == 0) {
+            const uint32_t k = atomicAdd(a.ovf_count, 1u);
+            if (k < a.ovf_cap) a.ovf[k] = make_uint2((uint32_t)t, (uint32_t)c);
+            else atomicOr(&a.prm->err, ERR_CAP);
+            a.tcnt[c][t] = 0;
+        }
         return;
     }
-    uint32_t n2 = 1;
-    while (n2 < ne) n2 <<= 1;
-    for (uint32_t x = threadIdx.x; x < n2; x += UB) buf[x] = x < ne ? (uint32_t)body[x] : 0xFFFFFFFFu;
-    __syncthreads();
-    bitonic_sort_lds<UNION_CAP>(buf, n2);
-    // unique compaction: each thread owns a contiguous chunk
-    const uint32_t per = (ne + UB - 1) / UB;
-    const uint32_t b0 = min(ne, threadIdx.x * per), b1 = min(ne, b0 + per);
-    uint32_t cnt = 0;
-    for (uint32_t x = b0; x < b1; ++x) cnt += (x == 0 || buf[x] != buf[x - 1]) ? 1u : 0u;
-    uint32_t total;
-    uint32_t o = block_scan_u32(cnt, wsum, &total);
-    uint32_t* out = a.txns[c] + a.ent_off[c][t];
-    for (uint32_t x = b0; x < b1; ++x)
-        if (x == 0 || buf[x] != buf[x - 1]) out[o++] = buf[x];
-    __syncthreads();
-    // unique list back into LDS, then remap every entry to its index
-    for (uint32_t x = threadIdx.x; x < total; x += UB) buf[x] = out[x];
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < ne; x += UB) {
-        const uint32_t v = (uint32_t)body[x];
-        uint32_t lo = 0, hi = total;
-        while (lo < hi) {
-            uint32_t m = (lo + hi) >> 1;
-            if (buf[m] < v) lo = m + 1; else hi = m;
-        }
-        body[x] = (int32_t)lo;
-    }
-    if (threadIdx.x == 0) a.tcnt[c][t] = total;
+    union_body<UB>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
+}
+
+// overflow pass, one 1024-thread workgroup per queued (txn, CSR): LDS up to UNION_CAP_BIG entries, beyond
+// that a bitonic sort in this item's slice of global memory
+__global__ __launch_bounds__(UB_BIG) void k_union_big(LdsUnionArgs a, uint32_t count) {
+    const uint32_t it = blockIdx.x;
+    if (it >= count) return;
+    __shared__ uint32_t buf[UNION_CAP_BIG];
+    __shared__ uint32_t wsum[UB_BIG / WAVE];
+    const uint32_t t = a.items[it].x, c = a.items[it].y;
+    const uint32_t nk = a.key_off[c][t + 1] - a.key_off[c][t];
+    const uint32_t mb = a.k2t_off[c][t];
+    const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
+    uint32_t* space = ne > (uint32_t)UNION_CAP_BIG ? a.gbuf + a.gbuf_off[it] : buf;
+    union_body<UB_BIG>(space, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
 }
 
 }  // namespace ad

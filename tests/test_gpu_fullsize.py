@@ -1,0 +1,215 @@
+"""GPU parity at BASELINE.json's full sizes (C2 and C3: 1,048,576 txns; C4's key + range mix at 1,048,576 txns,
+a quarter of its full size — see the test), where the oracle cannot run the whole batch within a test.  Two kinds of evidence:
+
+* exact prefix parity — a txn's PreAccept deps depend only on txns with a smaller TxnId (the query bound is
+  its own TxnId; window and drops use ranks), so the oracle on the first K txns must reproduce the GPU's
+  first K rows of every view and of the merged Deps bit for bit;
+* size-independent properties of the whole batch, vectorised in numpy: canonical CSR form (sorted unique keys
+  and TxnIds, per-key lists sorted, unique and covering the TxnId table), the PreAccept bound (deps rank
+  below the txn), key membership (every dependency holds the key), merged == union of the views (Deps.merge),
+  the execution levels as the solution of their defining equations on every key chain (C2/C3), the order
+  sorted by (level, executeAt), and determinism of the device pipeline.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from accord_amd import abi, workload
+
+pytestmark = pytest.mark.gpu
+
+W, R, DROP = 32, 3, 0.1
+CLASSES = (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)
+
+
+def prefix(csr, k):
+    w = 2 if csr.is_range else 1
+    return abi.Csr(csr.key_off[:k + 1], csr.keys[:w * csr.key_off[k]], csr.k2t_off[:k + 1], csr.k2t[:csr.k2t_off[k]],
+                   csr.txn_off[:k + 1], csr.txns[:csr.txn_off[k]], csr.is_range)
+
+
+def owner(off):
+    return np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off.astype(np.int64)))
+
+
+def triples(csr):
+    """(txn, key index into csr.keys, dependency rank) of every entry, and the per-txn canonical checks."""
+    n = csr.n
+    ko, mo, to = (x.astype(np.int64) for x in (csr.key_off, csr.k2t_off, csr.txn_off))
+    nk, tc = np.diff(ko), np.diff(to)
+    # keys (ranges: by (start, end)) and TxnIds strictly ascending inside each txn
+    if csr.is_range:
+        r2 = csr.keys.reshape(-1, 2)
+        asc = (r2[1:, 0] > r2[:-1, 0]) | ((r2[1:, 0] == r2[:-1, 0]) & (r2[1:, 1] > r2[:-1, 1]))
+        checks = ((asc, ko),)
+    else:
+        checks = ((csr.keys[1:] > csr.keys[:-1], ko),)
+    checks += ((csr.txns[1:] > csr.txns[:-1], to),)
+    for asc, off in checks:
+        if len(asc):
+            same = owner(off)[1:] == owner(off)[:-1]
+            assert asc[same].all(), "not strictly ascending inside a txn"
+    # keysToTxnIds: nk cumulative end offsets (base nk), then per-key index lists
+    k2t = csr.k2t.astype(np.int64)
+    t_of = owner(mo)
+    rel = np.arange(len(k2t), dtype=np.int64) - mo[t_of]
+    is_hdr = rel < nk[t_of]
+    hdr_t = t_of[is_hdr]
+    ends = k2t[is_hdr]
+    starts = np.where(rel[is_hdr] == 0, nk[hdr_t], np.r_[0, ends[:-1]])
+    assert (ends > starts).all(), "empty or non-monotone per-key list"
+    last = np.zeros(n, np.int64)
+    last[hdr_t] = ends
+    assert np.array_equal(last[nk > 0], (mo[1:] - mo[:-1])[nk > 0]), "header does not close the txn's k2t"
+    # entry -> (txn, key ordinal)
+    ent_t = t_of[~is_hdr]
+    ent_rel = rel[~is_hdr]
+    key_base = np.repeat(ko[:-1], nk)                    # header row -> its key's global index
+    hdr_key = key_base + (rel[is_hdr])
+    # which header row covers each entry: searchsorted over (txn, end) pairs
+    hdr_keyidx = np.searchsorted(hdr_t * (1 << 32) + ends, ent_t * (1 << 32) + ent_rel, side="right")
+    ent_key = hdr_key[hdr_keyidx]
+    idx = k2t[~is_hdr]
+    assert (idx >= 0).all() and (idx < tc[ent_t]).all(), "index outside the TxnId table"
+    # per-key lists strictly ascending
+    same = (ent_t[1:] == ent_t[:-1]) & (ent_key[1:] == ent_key[:-1])
+    assert (np.diff(idx)[same] > 0).all(), "per-key list not strictly ascending"
+    dep = csr.txns[to[ent_t] + idx].astype(np.int64)
+    # every TxnId of the table is referenced (the table is the union of the per-key lists)
+    used = np.zeros(len(csr.txns), bool)
+    used[to[ent_t] + idx] = True
+    assert used.all(), "TxnId table holds an unreferenced id"
+    return ent_t, csr.keys[ent_key] if not csr.is_range else ent_key, dep
+
+
+def check_view(csr, batch):
+    t, key, dep = triples(csr)
+    assert (dep < t).all(), "PreAccept bound: a dependency must have a smaller TxnId"
+    # key membership: (key, dep) is a (key, txn) pair of the batch
+    ko = batch["key_off"].astype(np.int64)
+    pair = batch["keys"].astype(np.uint64) * np.uint64(1 << 24) + owner(ko).astype(np.uint64)
+    want = key.astype(np.uint64) * np.uint64(1 << 24) + dep.astype(np.uint64)
+    assert np.isin(want, pair).all(), "a dependency does not hold the key"
+    return t, key, dep
+
+
+def enc(t, key, dep):
+    return np.unique((t.astype(np.uint64) << np.uint64(42)) ^ (key.astype(np.uint64) << np.uint64(21)) ^ dep.astype(np.uint64))
+
+
+def ts_key(msb, lsb, node):
+    """Timestamp.compareTo order (Timestamp.java:209-217): msb unsigned, hlc = lsb >> 16, the identity flags
+    lsb & 0x1E (IDENTITY_FLAGS), then node — most significant first."""
+    lsb = lsb.astype(np.uint64)
+    return (msb.astype(np.uint64), lsb >> np.uint64(16), lsb & np.uint64(0x1E), node.astype(np.int64))
+
+
+def level_equations(batch, lv):
+    """Every txn's level equals 1 + max over its key chains of the (a) rule (0 without predecessors)."""
+    ko = batch["key_off"].astype(np.int64)
+    t = owner(ko)
+    keys = batch["keys"].astype(np.int64)
+    exe = ts_key(batch["exec_msb"], batch["exec_lsb"], batch["exec_node"])
+    # chain order: key, then executeAt (Timestamp.compareTo)
+    order = np.lexsort(tuple(x[t] for x in reversed(exe)) + (keys,))
+    t, keys = t[order], keys[order]
+    wr = ((batch["txn_lsb"].astype(np.int64) >> 1) & 7)[t] == abi.KIND_WRITE
+    L = lv.astype(np.int64)[t]
+    seg = np.r_[0, np.cumsum(keys[1:] != keys[:-1])]
+    big = np.int64(1 << 40)
+    # exclusive segmented prefix max of all levels and of write levels (-1 = none)
+    def excl_cummax(v):
+        x = seg * big + v
+        inc = np.maximum.accumulate(x)
+        ex = np.r_[np.int64(-1), inc[:-1]]
+        ex = np.where(np.r_[True, seg[1:] != seg[:-1]], -1, ex - seg * big)
+        return ex
+    pm_all = excl_cummax(L)
+    pm_w = excl_cummax(np.where(wr, L, -1))
+    need = np.where(wr, pm_all, pm_w) + 1                 # 0 when no predecessor
+    req = np.zeros(batch["n"], np.int64)
+    np.maximum.at(req, t, need)
+    assert np.array_equal(req, lv.astype(np.int64)), "levels are not the solution of the chain equations"
+
+
+def run_full(engine_factory, batch):
+    eng = engine_factory(window=W, replicas=R, drop_p=DROP, seed=0xACC0D1)
+    eng.load(batch)
+    eng.preaccept_deps()
+    views = [[eng.fetch_deps(v, c) for c in CLASSES] for v in range(R)]
+    eng.merge()
+    merged = [eng.fetch_merged(c) for c in CLASSES]
+    lv, order, _ = eng.exec_levels()
+    return eng, views, merged, lv, order
+
+
+def check_prefix(batch, views, merged, k):
+    ref = O.OracleResult(workload.slice_batch(batch, 0, k), abi.make_config(W, R, DROP, 0xACC0D1), O.FLAG_MERGE)
+    for v in range(R):
+        for ci, c in enumerate(CLASSES):
+            assert prefix(views[v][ci], k).equal(ref.deps(v, c)), "view %d class %d prefix differs" % (v, c)
+    for ci, c in enumerate(CLASSES):
+        assert prefix(merged[ci], k).equal(ref.merged(c)), "merged class %d prefix differs" % c
+
+
+def check_order(batch, lv, order):
+    n = batch["n"]
+    assert np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32)), "order is not a permutation"
+    key = (lv[order].astype(np.uint64),) + ts_key(batch["exec_msb"][order], batch["exec_lsb"][order], batch["exec_node"][order])
+    d = np.lexsort((np.arange(n),) + tuple(reversed(key)))
+    assert np.array_equal(d, np.arange(n)), "order is not sorted by (level, executeAt)"
+
+
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_full_size_key_batches(engine_factory, name):
+    batch = workload.config(name)
+    assert batch["n"] == 1 << 20
+    eng, views, merged, lv, order = run_full(engine_factory, batch)
+    check_prefix(batch, views, merged, 60000 if name == "C2" else 20000)
+    for ci in range(len(CLASSES)):
+        parts = [check_view(views[v][ci], batch) for v in range(R)]
+        mt = check_view(merged[ci], batch)
+        union = enc(*[np.concatenate([p[i] for p in parts]) for i in range(3)])
+        assert np.array_equal(enc(*mt), union), "merged Deps != union of the replica views"
+    level_equations(batch, lv)
+    check_order(batch, lv, order)
+    # the device pipeline (Kahn or fixpoint, optimistic order) reproduces the staged calls
+    eng.run_pipeline()
+    plv, porder = eng.fetch_levels()
+    assert np.array_equal(plv, lv) and np.array_equal(porder, order)
+
+
+def test_c4_mixed_ranges_quarter_size(engine_factory):
+    # C4's mix at 1,048,576 txns.  At its full 4,194,304 txns the RangeDeps alone are ~10^9 entries per
+    # replica view (every key txn depends on the ~80 earlier ranges covering each of its keys), ~150 GB of
+    # device CSRs for 3 views + merge in this per-txn layout: beyond one GPU without chunking the queries
+    # (DESIGN.md §7); the quarter-size batch keeps the same density per key (4x fewer ranges cover a key).
+    batch = workload.config("C4", n=1 << 20)
+    eng = engine_factory(window=W, replicas=R, drop_p=DROP, seed=0xACC0D1)
+    eng.load(batch)
+    eng.preaccept_deps()
+    views = [[eng.fetch_deps(v, c) for c in CLASSES] for v in range(R)]
+    rviews = [eng.fetch_deps(v, abi.CLASS_RANGE) for v in range(R)]
+    eng.merge()
+    merged = [eng.fetch_merged(c) for c in CLASSES]
+    rmerged = eng.fetch_merged(abi.CLASS_RANGE)
+    lv, order, _ = eng.exec_levels()
+    k = 8000
+    ref = O.OracleResult(workload.slice_batch(batch, 0, k), abi.make_config(W, R, DROP, 0xACC0D1), O.FLAG_MERGE)
+    for v in range(R):
+        for ci, c in enumerate(CLASSES):
+            assert prefix(views[v][ci], k).equal(ref.deps(v, c)), "view %d class %d prefix differs" % (v, c)
+        assert prefix(rviews[v], k).equal(ref.deps(v, abi.CLASS_RANGE)), "RangeDeps view %d prefix differs" % v
+    for ci, c in enumerate(CLASSES):
+        assert prefix(merged[ci], k).equal(ref.merged(c))
+    assert prefix(rmerged, k).equal(ref.merged(abi.CLASS_RANGE))
+    for ci in range(len(CLASSES)):
+        for v in range(R):
+            t, _, dep = triples(views[v][ci])
+            assert (dep < t).all()
+        triples(merged[ci])
+    for v in range(R):
+        t, _, dep = triples(rviews[v])
+        assert (dep < t).all()
+    triples(rmerged)
+    check_order(batch, lv, order)

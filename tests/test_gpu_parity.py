@@ -170,6 +170,33 @@ def test_range_txns_mixed(engine_factory, seed, width):
     check(engine_factory, b, window=16)
 
 
+def wide_range_batch(keyspace):
+    """keyspace single-key Writes over keyspace keys, then 3 range Reads over the whole key space: each range
+    txn's KeyDeps hold about one TxnId per key (more than one LDS union pass holds)."""
+    b = workload.generate(keyspace, 1, keyspace, "uniform", seed=keyspace)
+    n = b["n"]
+    is_range = np.zeros(n, bool)
+    is_range[-3:] = True
+    kind = np.where(is_range, abi.KIND_READ, abi.KIND_WRITE).astype(np.uint64)
+    flags = (kind << np.uint64(1)) | is_range.astype(np.uint64)
+    b["txn_lsb"] = (b["txn_lsb"].astype(np.uint64) & ~np.uint64(0xF)) | flags
+    b["exec_lsb"] = (b["exec_lsb"].astype(np.uint64) & ~np.uint64(0xF)) | flags
+    ko = b["key_off"].astype(np.int64)
+    b["keys"] = np.ascontiguousarray(b["keys"][np.repeat(~is_range, np.diff(ko))])
+    b["key_off"] = np.concatenate([[0], np.cumsum(np.where(is_range, 0, np.diff(ko)))]).astype(np.uint32)
+    ro = np.concatenate([[0], np.cumsum(is_range.astype(np.int64))]).astype(np.uint32)
+    b["range_off"] = ro
+    b["range_start"] = np.zeros(int(ro[-1]), np.uint64)
+    b["range_end"] = np.full(int(ro[-1]), keyspace + 1, np.uint64)
+    return b
+
+
+@pytest.mark.parametrize("keyspace", [24000, 70000])
+def test_union_overflow_wide_ranges(engine_factory, keyspace):
+    # 24k keys: the 1024-thread 128 KiB LDS overflow pass; 70k keys: its global-memory sort
+    check(engine_factory, wide_range_batch(keyspace), window=4, levels=False)
+
+
 def test_range_txns_writes_and_sync_points(engine_factory):
     rng = np.random.default_rng(31)
     n = 2500
