@@ -200,3 +200,27 @@ def test_levels_canon_invariant_with_range_txns(seed):
                           bump_max=40, seed=seed)
     res = O.OracleResult(b, abi.make_config(8, 3, 0.2, seed), O.FLAG_MERGE | O.FLAG_LEVELS)
     canon_check(b, res)
+
+
+def test_threaded_oracle_equals_single_store():
+    # the CPU baseline's T-thread mode (one single-threaded store per key range, PreAccept.reduce by
+    # linearUnion) must give the single-store answer: KeyDeps are shard-invariant
+    import oracle as O
+    from accord_amd import abi, workload
+    b = workload.config("C2", n=6000)
+    b["keys"] = b["keys"] % np.uint64(5000)
+    ko = b["key_off"]
+    for t in range(b["n"]):
+        row = np.unique(b["keys"][ko[t]:ko[t + 1]])
+        if len(row) != ko[t + 1] - ko[t]:
+            row = np.arange(ko[t + 1] - ko[t], dtype=np.uint64) + np.uint64(5000 + 4 * t)
+        b["keys"][ko[t]:ko[t + 1]] = np.sort(row)
+    cfg = abi.make_config(32, 3, 0.1, 7)
+    one = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS, threads=1)
+    four = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS, threads=4)
+    for v in range(3):
+        for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
+            assert one.deps(v, c).equal(four.deps(v, c))
+    for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
+        assert one.merged(c).equal(four.merged(c))
+    assert all(np.array_equal(x, y) for x, y in zip(one.levels(), four.levels()))
