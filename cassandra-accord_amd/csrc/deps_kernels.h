@@ -696,16 +696,29 @@ struct UnionArgs {
 };
 
 // Small txns: register K-way merge of the per-key lists (large txns: k_union_lds).
+template <int NVC>
 __global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     if (a.meta[t] & META_LARGE) return;
-    for (int vc = 0; vc < a.nvc; ++vc) {
-        const uint32_t nk = a.key_off[vc][t + 1] - a.key_off[vc][t];
+    // every CSR's key range up front: the loads issue together instead of behind each CSR's stores
+    uint32_t kb[NVC], ke[NVC];
+#pragma unroll
+    for (int vc = 0; vc < NVC; ++vc) { kb[vc] = a.key_off[vc][t]; ke[vc] = a.key_off[vc][t + 1]; }
+    uint32_t mbv[NVC], obv[NVC];
+#pragma unroll
+    for (int vc = 0; vc < NVC; ++vc) {
+        const bool any = ke[vc] != kb[vc];
+        mbv[vc] = any ? a.k2t_off[vc][t] : 0u;
+        obv[vc] = any ? a.ent_off[vc][t] : 0u;
+    }
+#pragma unroll
+    for (int vc = 0; vc < NVC; ++vc) {
+        const uint32_t nk = ke[vc] - kb[vc];
         if (nk == 0) { a.tcnt[vc][t] = 0; continue; }
-        const uint32_t mb = a.k2t_off[vc][t];
+        const uint32_t mb = mbv[vc];
         int32_t* k2t = a.k2t[vc];
-        uint32_t* out = a.txns[vc] + a.ent_off[vc][t];
+        uint32_t* out = a.txns[vc] + obv[vc];
         if (nk == 1) {                 // one key: its list is already sorted and unique
             const uint32_t b = mb + 1, e = mb + (uint32_t)k2t[mb];
             for (uint32_t q = b; q < e; ++q) { out[q - b] = (uint32_t)k2t[q]; k2t[q] = (int32_t)(q - b); }

@@ -445,6 +445,11 @@ int union_overflow(ad_handle* h, LdsUnionArgs la, uint32_t* ovf_count, uint2* ov
     return AD_OK;
 }
 
+template <int NV>
+void launch_union(const UnionArgs& ua, hipStream_t st) {
+    k_txn_union<2 * NV><<<ceil_div((long)ua.n, 256), 256, 0, st>>>(ua);
+}
+
 int stage_deps(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
@@ -554,7 +559,7 @@ int stage_deps(ad_handle* h) {
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    if (n > 0) { KScope ks(K_TXN_UNION, n); k_txn_union<<<ceil_div((long)n, 256), 256, 0, st>>>(ua); }
+    if (n > 0) { KScope ks(K_TXN_UNION, n); NV_DISPATCH(nv, launch_union, ua, st); }
     // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
         KScope ks(K_UNION_LDS);
