@@ -160,6 +160,16 @@ int dalloc(ad_handle* h, size_t slot, T** out, size_t count) {
     return AD_OK;
 }
 
+// Releases slot `slot` (its next dalloc allocates afresh).
+int drelease(ad_handle* h, size_t slot) {
+    if (slot < h->bufs.size() && h->bufs[slot].p) {
+        HIPCHK(h, hipStreamSynchronize(h->st));
+        HIPCHK(h, hipFree(h->bufs[slot].p));
+        h->bufs[slot] = DBuf{};
+    }
+    return AD_OK;
+}
+
 enum Slot : size_t {
     S_TM, S_TL, S_TN, S_EM, S_EL, S_EN, S_ST, S_KOFF, S_KEYS, S_ROFF, S_RS, S_RE,
     S_PRM, S_TXTS, S_EX1, S_META, S_PTXN, S_KA, S_VA, S_KB, S_VB, S_ETXN, S_SPOS, S_EMETA, S_EEXEC,
@@ -591,6 +601,14 @@ int stage_deps(ad_handle* h) {
             k_union_lds<<<dim3((unsigned)n, (unsigned)nv), UB, 0, st>>>(la);
         }
         CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
+    }
+    // Virtual-item work arrays are dead once the CSRs are filled.  Range-domain txns query every CFK key
+    // of their ranges, so for wide-range batches (C4: ~10^9 items x 2R counts and slots) they are the
+    // largest allocation of the handle: give them back before the merge allocates its outputs.
+    if ((size_t)h->V * nvc * 8 > ((size_t)1 << 30)) {
+        for (size_t sl : {S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST}) CK(drelease(h, sl));
+        h->vi_txn = h->vi_pos = h->vi_seg0 = h->vcnt = h->vdst = nullptr;
+        h->vi_key = nullptr;
     }
     h->have_deps = true;
     h->ls.chains_ready = false;

@@ -451,7 +451,8 @@ __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __
 constexpr int CB_REG = 8;
 __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                         const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
-                                        uint32_t* __restrict__ c_txn, uint32_t* __restrict__ indeg, uint2* __restrict__ succ) {
+                                        uint32_t* __restrict__ c_txn, uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
+                                        uint8_t* __restrict__ c_meta, uint64_t* __restrict__ c_exec1) {
     uint64_t k[CB_REG];
     uint32_t t[CB_REG], pr[CB_REG], wr[CB_REG], ord[CB_REG];
 #pragma unroll
@@ -460,7 +461,7 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
         k[i] = v ? e_exec1[s + i] : ~0ull;
         t[i] = v ? e_txn[s + i] : 0u;
         pr[i] = v ? sval[s + i] : 0u;
-        wr[i] = v ? (meta_kind(e_meta[s + i]) == AD_KIND_WRITE ? 1u : 0u) : 0u;
+        wr[i] = v ? (uint32_t)e_meta[s + i] : 0u;        // meta byte (kind tested below)
         ord[i] = (uint32_t)i;
     }
 #pragma unroll
@@ -477,6 +478,13 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
             }
         }
     }
+    if (c_exec1) {                        // (c) constraints search the executeAt-ordered chain
+#pragma unroll
+        for (int q = 0; q < CB_REG; ++q)
+            if (q < len) { c_exec1[s + q] = k[q]; c_meta[s + q] = (uint8_t)wr[q]; }
+    }
+#pragma unroll
+    for (int q = 0; q < CB_REG; ++q) wr[q] = meta_kind((uint8_t)wr[q]) == AD_KIND_WRITE ? 1u : 0u;
     bool seen_w = false;
     uint32_t reads = 0;
 #pragma unroll
@@ -519,7 +527,7 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
                                                      uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
                                                      uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
                                                      uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
-                                                     uint32_t* __restrict__ any_long) {
+                                                     uint32_t* __restrict__ any_long, int full) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool lng = false;
     const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
@@ -530,7 +538,8 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
         if (end - s > SHORT_SEG) {
             lng = true;
         } else if (end - s <= CB_REG) {
-            chain_build_regs(s, (int)(end - s), e_txn, e_meta, e_exec1, sval, c_txn, indeg, succ);
+            chain_build_regs(s, (int)(end - s), e_txn, e_meta, e_exec1, sval, c_txn, indeg, succ, full ? c_meta : nullptr,
+                             full ? c_exec1 : nullptr);
         } else {
             for (size_t x = s; x < end; ++x) {
                 const uint64_t kx = e_exec1[x];
@@ -585,39 +594,119 @@ constexpr int KAHN_GRID = 2048;
 __device__ inline void kahn_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
     if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
 }
+// Extra successors (mixed key + range batches): xs[xoff[t] .. xoff[t+1]) are the txns waiting on t through a
+// (b) dependency edge or a (c) chain-prefix constraint (k_xedges).  A txn with at most XLIGHT of them releases
+// them itself; heavier ones (a range txn can have thousands of dependants) are released by the whole wave,
+// 64 lanes per edge run.
+constexpr uint64_t XLIGHT = 8;
 __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
                                                    uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
                                                    const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
                                                    const uint32_t* __restrict__ c_txn, const uint32_t* gate, int gate_is_abort,
-                                                   uint32_t* __restrict__ work) {
+                                                   uint32_t* __restrict__ work, const uint64_t* __restrict__ xoff,
+                                                   const uint32_t* __restrict__ xs) {
     if (gate_is_abort ? *gate != 0u : *gate == 0u) return;
     bool released = false;
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x) {
-        if (!(lvl == 0 ? indeg0[t] == 0u : L[t] == lvl)) continue;
-        const uint32_t b = key_off[t], e = key_off[t + 1];
-        if (e - b <= 4) {
-            uint2 sc[4];
-            uint32_t sx[4], rr[4];
+    // block-aligned stride: every lane of a wave runs the same iterations (the heavy-run ballot below)
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
+        const size_t t = base + threadIdx.x;
+        const bool mine = t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
+        if (mine) {
+            const uint32_t b = key_off[t], e = key_off[t + 1];
+            if (e - b <= 4) {
+                uint2 sc[4];
+                uint32_t sx[4], rr[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) sc[j] = b + j < e ? succ[b + j] : make_uint2(0u, 0u);
+                for (int j = 0; j < 4; ++j) sc[j] = b + j < e ? succ[b + j] : make_uint2(0u, 0u);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) sx[j] = sc[j].y ? c_txn[sc[j].x] : 0u;
+                for (int j = 0; j < 4; ++j) sx[j] = sc[j].y ? c_txn[sc[j].x] : 0u;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) rr[j] = sc[j].y ? atomicSub(&rem[sx[j]], 1u) : 0u;
+                for (int j = 0; j < 4; ++j) rr[j] = sc[j].y ? atomicSub(&rem[sx[j]], 1u) : 0u;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (sc[j].y && rr[j] == 1u) { L[sx[j]] = lvl + 1; released = true; }
+                for (int j = 0; j < 4; ++j)
+                    if (sc[j].y && rr[j] == 1u) { L[sx[j]] = lvl + 1; released = true; }
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
-        } else {
-            for (uint32_t p = b; p < e; ++p) {
-                const uint2 sc = succ[p];
-                for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+                for (int j = 0; j < 4; ++j)
+                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+            } else {
+                for (uint32_t p = b; p < e; ++p) {
+                    const uint2 sc = succ[p];
+                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+                }
+            }
+        }
+        if (xoff) {
+            uint64_t xb = 0, xe = 0;
+            if (mine) { xb = xoff[t]; xe = xoff[t + 1]; }
+            const bool heavy = xe - xb > XLIGHT;
+            if (mine && !heavy)
+                for (uint64_t j = xb; j < xe; ++j) kahn_release(xs[j], lvl, rem, L, released);
+            uint64_t hm = __ballot(heavy);
+            while (hm) {
+                const int l = __ffsll((unsigned long long)hm) - 1;
+                hm &= hm - 1;
+                const uint64_t b0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(xb >> 32), l) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)xb, l);
+                const uint64_t e0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(xe >> 32), l) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)xe, l);
+                for (uint64_t j = b0 + __lane_id(); j < e0; j += WAVE) kahn_release(xs[j], lvl, rem, L, released);
             }
         }
     }
     wave_set_flag(released, work);
+}
+
+// (b) and (c) as explicit Kahn edges, one thread per txn T (count pass: per-source out-degrees and T's
+// in-degree; fill pass: T appended to each source's successor run):
+//   (b) every merged direct-key / range dependency D of T with executeAt(D) < executeAt(T);
+//   (c) unmanaged T, per key of its merged KeyDeps with a constraint position p (k_unmanaged_prep): every
+//       managed entry of that key's chain at positions <= p.  The chain rule already orders the prefix, so
+//       its maximum level sits on the last Write at or before p or on a Read after it: the edges come from
+//       the Reads in (last Write, p] and that Write (all entries down to the segment head if none).
+struct XEdgeArgs {
+    EdgeArgs e;
+    const uint8_t* c_meta;
+    int do_b, do_c;
+    uint32_t* indeg;
+    unsigned long long* outcnt;          // count pass: [n] per-source out-degree
+    unsigned long long* cur;             // fill pass: [n] per-source write cursor (starts at xoff)
+    uint32_t* xs;
+};
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.e.n) return;
+    const EdgeArgs& e = a.e;
+    uint32_t local = 0;
+    auto emit = [&](uint32_t src) {
+        if (FILL) a.xs[atomicAdd(&a.cur[src], 1ull)] = (uint32_t)t;
+        else atomicAdd(&a.outcnt[src], 1ull);
+        ++local;
+    };
+    if (a.do_b) {
+        const uint64_t my = e.ex1[t];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (!e.txns[c]) continue;
+            const uint32_t b = e.ent_off[c][t], end = b + e.tcnt[c][t];
+            for (uint32_t x = b; x < end; ++x) {
+                const uint32_t d = e.txns[c][x];
+                if (e.ex1[d] < my) emit(d);
+            }
+        }
+    }
+    if (a.do_c && !manages_execution(e.meta[t])) {
+        for (uint32_t x = e.mk_key_off[t]; x < e.mk_key_off[t + 1]; ++x) {
+            const int32_t p = e.cons_pos[x];
+            if (p < 0) continue;
+            const int32_t s0 = e.seg_start[p];
+            for (int32_t q = p;; --q) {
+                emit(e.c_txn[q]);
+                if (meta_kind(a.c_meta[q]) == AD_KIND_WRITE || q == s0) break;
+            }
+        }
+    }
+    if (!FILL && local) atomicAdd(&a.indeg[t], local);
 }
 
 struct LevelState {
@@ -643,10 +732,14 @@ struct LevelState {
     uint32_t* iflags = nullptr;          // per iteration of a launch batch: [long dirty, edge changed, work left, -]
     bool chains_ready = false;           // chain order / segment table valid for the current batch
     uint32_t nheads = 0, nlong = 0;
+    // Kahn path with (b)/(c) edges: per-source out-degree, successor offsets, write cursor, successors
+    unsigned long long *xcnt = nullptr, *xoff = nullptr, *xcur = nullptr;
+    uint32_t* xs = nullptr;
+    size_t capX = 0, xs_cap = 0;
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -865,8 +958,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     if (!ls.flags && !grow((void**)&ls.flags, 256)) goto oom;
     if (!ls.iflags && !grow((void**)&ls.iflags, 4 * 64 * 4)) goto oom;
     {
-        const size_t need = std::max(device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)),
-                                     device_scan_scratch<SegListOp>(std::max<size_t>(P, 1))) + 256;
+        const size_t need = std::max(std::max(device_scan_scratch<ChainOp>(std::max<size_t>(P, 1)),
+                                              device_scan_scratch<SegListOp>(std::max<size_t>(P, 1))),
+                                     device_scan_scratch<SumOp<unsigned long long>>(std::max<size_t>(n, 1))) + 256;
         if (ls.agg_cap < need) { if (!grow(&ls.agg, need)) goto oom; ls.agg_cap = need; }
         const size_t rneed = (3 * (radix_hist_len(std::max<size_t>(n, 1)) + 128) + 64 * 1024) * 4;
         if (ls.rs_cap < rneed) { if (!grow((void**)&ls.rs, rneed)) goto oom; ls.rs_cap = rneed; }
@@ -900,28 +994,71 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // ---- Kahn wavefront (short-chain key batches): chain build + wavefronts with no decision sync;
         // the first batch's readback also carries the kinds / long-chain flags, and a long chain found by
         // the build sends the batch to the fixpoint below
-        if (in.kahn_ok && !in.keep_levels && !has_b && !has_c && P > 0) {
+        if (in.kahn_ok && !in.keep_levels && P > 0) {
             ls.chains_ready = false;
             int lv = 0;
             bool fallback = false;
+            const bool xedges = has_b || has_c;
             {
                 KScope ks(K_KAHN);
                 hipMemsetAsync(ls.indeg, 0, n * 4, st);
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
+                // (c) searches every chain in executeAt order, singletons included
+                if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
                 k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
-                                                  ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7);
-                hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
+                                                  ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0);
+                if (xedges) {
+                    // (b)/(c) successor runs: count, offsets (one sync: total + long-chain / kinds flags), fill
+                    if (ls.capX < n + 1 || !ls.xcnt) {
+                        const size_t c = n + 1;
+                        if (!grow((void**)&ls.xcnt, c * 8) || !grow((void**)&ls.xoff, c * 8) || !grow((void**)&ls.xcur, c * 8)) goto oom;
+                        ls.capX = c;
+                    }
+                    const int gn1 = ceil_div((long)n, 256);
+                    if (has_c) k_unmanaged_prep<<<gn1, 256, 0, st>>>(ea);
+                    XEdgeArgs xa{};
+                    xa.e = ea; xa.c_meta = ls.c_meta; xa.do_b = has_b ? 1 : 0; xa.do_c = has_c ? 1 : 0;
+                    xa.indeg = ls.indeg; xa.outcnt = ls.xcnt; xa.cur = ls.xcur;
+                    hipMemsetAsync(ls.xcnt, 0, n * 8, st);
+                    k_xedges<false><<<gn1, 256, 0, st>>>(xa);
+                    device_scan(SumOp<unsigned long long>{ls.xcnt, ls.xoff, n}, n, (unsigned long long*)ls.agg, st);
+                    unsigned long long etot = 0;
+                    if (hipMemcpyAsync(&etot, ls.xoff + n, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess) {
+                        err = "exec levels: device error";
+                        return AD_ERR_DEVICE;
+                    }
+                    if (host[5]) {
+                        err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                        return AD_ERR_UNSUPPORTED;
+                    }
+                    if (host[7]) fallback = true;         // a long chain: the fixpoint below
+                    else {
+                        if (ls.xs_cap < etot || !ls.xs) {
+                            const size_t c = std::max<size_t>(etot + etot / 8, 1);
+                            if (!grow((void**)&ls.xs, c * 4)) goto oom;
+                            ls.xs_cap = c;
+                        }
+                        hipMemcpyAsync(ls.xcur, ls.xoff, n * 8, hipMemcpyDeviceToDevice, st);
+                        xa.xs = ls.xs;
+                        k_xedges<true><<<gn1, 256, 0, st>>>(xa);
+                    }
+                }
+                if (!fallback) hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
                 // wavefronts per launch batch, no host sync inside a batch (a wavefront after the last
-                // one exits at once); the first batch covers typical uniform-key depths (C2: 10)
-                constexpr int KB_MAX = 16;
+                // one exits at once); the first batch covers typical uniform-key depths (C2: 10), later
+                // batches double while every wavefront keeps releasing (mixed batches: thousands of levels)
+                constexpr int KB_MAX = 64;
                 const int gn = std::min(ceil_div((long)n, 256), KAHN_GRID);
-                bool more = true;
+                bool more = !fallback;
+                int KB = 16;
                 while (more && lv < (1 << 24)) {
-                    const int KB = lv == 0 ? KB_MAX : 8;
                     hipMemsetAsync(ls.iflags, 0, KB * 4, st);
                     for (int k = 0; k < KB; ++k)
                         k_kahn_step<<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ, ls.c_txn,
-                                                        k == 0 ? ls.flags + 7 : ls.iflags + (k - 1), k == 0, ls.iflags + k);
+                                                        k == 0 ? ls.flags + 7 : ls.iflags + (k - 1), k == 0, ls.iflags + k,
+                                                        xedges ? (const uint64_t*)ls.xoff : nullptr, xedges ? ls.xs : nullptr);
                     uint32_t fh[KB_MAX];
                     if (hipMemcpyAsync(fh, ls.iflags, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         (lv == 0 && hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess) ||
@@ -938,7 +1075,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     }
                     int k = 0;
                     while (k < KB && fh[k]) ++k;
-                    if (k == KB) { lv += KB; continue; }     // every wavefront released more: next batch
+                    if (k == KB) { lv += KB; KB = std::min(KB_MAX, 2 * KB); continue; }   // all released more: next batch
                     lv += k + 1;
                     more = false;
                 }
