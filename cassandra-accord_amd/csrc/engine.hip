@@ -113,6 +113,8 @@ struct ad_handle {
     Csr smerged[3];
     ncclComm_t comm = nullptr;
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
+    int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
+    bool evicting = false;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -140,23 +142,36 @@ int set_err(ad_handle* h, int code, const std::string& msg) {
     return code;
 }
 
-// Grow-only device allocation slot `slot` of at least `bytes`.
+enum Stage { STAGE_NONE = 0, STAGE_DEPS, STAGE_MERGE };
+void release_dead(ad_handle* h);
+
+// Grow-only device allocation slot `slot` of at least `bytes`.  When HBM is exhausted, the buffers the
+// running stage makes dead (release_dead) are given back once and the allocation retried.
 template <class T>
 int dalloc(ad_handle* h, size_t slot, T** out, size_t count) {
     if (h->bufs.size() <= slot) h->bufs.resize(slot + 1);
-    DBuf& b = h->bufs[slot];
     size_t bytes = std::max<size_t>(count * sizeof(T), 256);
-    if (b.cap < bytes) {
+    if (h->bufs[slot].cap < bytes) {
+        DBuf& b = h->bufs[slot];
         if (b.p) { HIPCHK(h, hipStreamSynchronize(h->st)); HIPCHK(h, hipFree(b.p)); b.p = nullptr; b.cap = 0; }
         size_t nb = std::max(bytes, b.cap + b.cap / 4);
-        if (hipMalloc(&b.p, nb) != hipSuccess) {
-            b.p = nullptr;
+        void* p = nullptr;
+        if (hipMalloc(&p, nb) != hipSuccess) {
             (void)hipGetLastError();
-            return set_err(h, AD_ERR_NOMEM, "device allocation of " + std::to_string(nb) + " bytes failed");
+            if (h->stage != STAGE_NONE && !h->evicting) {
+                h->evicting = true;
+                release_dead(h);
+                h->evicting = false;
+                if (hipMalloc(&p, nb) != hipSuccess) { (void)hipGetLastError(); p = nullptr; }
+            } else {
+                p = nullptr;
+            }
+            if (!p) return set_err(h, AD_ERR_NOMEM, "device allocation of " + std::to_string(nb) + " bytes failed");
         }
-        b.cap = nb;
+        h->bufs[slot].p = p;
+        h->bufs[slot].cap = nb;
     }
-    *out = (T*)b.p;
+    *out = (T*)h->bufs[slot].p;
     return AD_OK;
 }
 
@@ -177,7 +192,7 @@ enum Slot : size_t {
     S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
     S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT, S_HSTORE, S_XRANK, S_XLIST, S_XOFF,
-    S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO,
+    S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -186,6 +201,27 @@ constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV, CSR_HOST0 =
 constexpr size_t CSR_SHARD0 = CSR_HOST0 + 3 * MAXV, CSR_SMERGED0 = CSR_SHARD0 + NVC_MAX;
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
+
+// Buffers no later step of the running stage reads: while the deps of a new batch are built, the previous
+// batch's merged Deps, uploaded replies, merge scratch and level state; while merging, the level state.
+// (Full-size mixed batches hold ~10^9 dependency entries per replica view; this is what lets consecutive
+// batches reuse one handle inside 288 GB.)
+void release_dead(ad_handle* h) {
+    (void)hipStreamSynchronize(h->st);
+    auto rel = [&](size_t slot) {
+        if (slot < h->bufs.size() && h->bufs[slot].p) { (void)hipFree(h->bufs[slot].p); h->bufs[slot] = DBuf{}; }
+    };
+    if (h->stage == STAGE_DEPS) {
+        for (size_t blk = CSR_MERGED0; blk < CSR_HOST0 + 3 * MAXV; ++blk)
+            for (size_t k = 0; k < 10; ++k) rel(S_CSR0 + 10 * blk + k);
+        rel(S_MSCR); rel(S_MHL);
+        h->have_merged = h->have_levels = false;
+        h->mrange_zero_p = nullptr;
+        h->mrange_zero_n = ~(size_t)0;
+    }
+    free_level_state(h->ls);
+    h->have_levels = false;
+}
 
 inline int bits_of(uint64_t x) { return x == 0 ? 0 : 64 - __builtin_clzll(x); }
 
@@ -460,7 +496,14 @@ void launch_union(const UnionArgs& ua, hipStream_t st) {
     k_txn_union<2 * NV><<<ceil_div((long)ua.n, 256), 256, 0, st>>>(ua);
 }
 
+struct StageScope {
+    ad_handle* h;
+    StageScope(ad_handle* x, int st) : h(x) { h->stage = st; }
+    ~StageScope() { h->stage = STAGE_NONE; }
+};
+
 int stage_deps(ad_handle* h) {
+    StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     hipStream_t st = h->st;
@@ -638,6 +681,10 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
     CK(dalloc(h, S_MSCR, &mk, 3 * (size_t)K * n + 3));
     me = mk + (size_t)K * n;
     mu = me + (size_t)K * n;
+    uint32_t* hl;                                   // heavy-txn lists [K * n] + counters [K]
+    CK(dalloc(h, S_MHL, &hl, (size_t)K * n + 64));
+    uint32_t* hc = hl + (size_t)K * n;
+    if (n > 0) HIPCHK(h, hipMemsetAsync(hc, 0, (size_t)K * 4, st));
     std::vector<MergeArgs> ma(K);
     for (int k = 0; k < K; ++k) {
         CK(alloc_csr(h, out_block[k], *out[k], n));
@@ -651,6 +698,7 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
             a.row[v] = rows ? rows[k][v] : nullptr;
         }
         a.mk = mk + (size_t)k * n; a.me = me + (size_t)k * n; a.mu = mu + (size_t)k * n;
+        a.hlist = hl + (size_t)k * n; a.hcount = hc + k;
         if (n > 0) merge_launch(a, np, false, kw[k], st);
     }
     if (n > 0) {
@@ -733,6 +781,7 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
 }
 
 int stage_merge(ad_handle* h) {
+    StageScope sc(h, STAGE_MERGE);
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps before ad_preaccept_deps");
     const int nv = (int)h->cfg.replicas;
     const Csr* parts[3][MAXV] = {};

@@ -33,7 +33,14 @@ struct MergeArgs {
     const uint32_t* o_ent_off;
     uint32_t* o_txns;
     uint32_t* o_tcnt;
+    // heavy txns (long lists: range txns' KeyDeps, key txns' RangeDeps) go to k_merge_heavy
+    uint32_t* hcount;            // [1] appended by the count pass
+    uint32_t* hlist;             // [n]
 };
+
+// A txn whose replies hold more than MERGE_HEAVY TxnIds + keys in total is merged by one workgroup
+// (k_merge_heavy) instead of one thread: its serial merge would be thousands of dependent loads long.
+constexpr uint32_t MERGE_HEAVY = 256;
 
 // KW = u64 words per key: 1 for KeyDeps keys, 2 for RangeDeps (start, end) compared as Range::compare.
 template <int KW>
@@ -68,6 +75,23 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
         if (WRITE) a.o_tcnt[t] = 0;
         else { a.mk[t] = 0; a.me[t] = 0; a.mu[t] = 0; }
         return;
+    }
+    if (a.hlist) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) w += tc[v] + (rv[v] >= 0 ? a.key_off[v][rv[v] + 1] - a.key_off[v][rv[v]] : 0u);
+        const bool hv = w > MERGE_HEAVY;
+        if (!WRITE) {
+            const uint64_t m = __ballot(hv);
+            if (hv) {                     // wave-aggregated append
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                uint32_t base = 0;
+                if ((int)__lane_id() == leader) base = atomicAdd(a.hcount, (uint32_t)__popcll(m));
+                base = __builtin_amdgcn_readlane(base, leader);
+                a.hlist[base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull))] = (uint32_t)t;
+            }
+        }
+        if (hv) return;
     }
     uint32_t cur[NV], end[NV], head[NV];
 #pragma unroll
@@ -155,6 +179,218 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     else { a.mk[t] = mk; a.me[t] = me; a.mu[t] = mu; }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Heavy txns: one 256-thread workgroup per txn (grid-stride over the heavy list).  The txn's TxnId lists
+// are cut into chunks at every MCH-th TxnId of the reply holding the most, its key lists likewise by keys;
+// each chunk is a value interval, so the R-way merge of one chunk (the same loops as k_merge) is
+// independent of the others.  Thread j takes a contiguous run of chunks; a block scan of the per-thread
+// totals gives each thread its output offsets.  Write pass: TxnIds first (a barrier), then keys and
+// per-key lists, whose TxnIds are remapped by binary search in the txn's merged TxnId list.
+constexpr int MCH = 32, MH_T = 256, MH_GRID = 1024;
+
+__device__ inline uint32_t lb_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {   // first a[x] >= v
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (a[m] < v) lo = m + 1; else hi = m; }
+    return lo;
+}
+template <int KW>
+__device__ inline uint32_t lb_key(const uint64_t* k, uint32_t lo, uint32_t hi, const MKey<KW>& v) {
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (MKey<KW>::load(k, m) < v) lo = m + 1; else hi = m; }
+    return lo;
+}
+// exclusive block scan of three counters (MH_T threads); returns the block totals in tot[]
+__device__ inline void block_scan3(uint32_t x[3], uint32_t tot[3]) {
+    __shared__ uint32_t sh[3][MH_T / WAVE];
+    const int lane = (int)__lane_id(), w = (int)threadIdx.x / WAVE;
+    uint32_t inc[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        uint32_t v = x[c];
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+            const uint32_t y = __shfl_up(v, d);
+            if (lane >= d) v += y;
+        }
+        inc[c] = v;
+        if (lane == WAVE - 1) sh[c][w] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        uint32_t before = 0, all = 0;
+        for (int k = 0; k < MH_T / WAVE; ++k) { if (k < w) before += sh[c][k]; all += sh[c][k]; }
+        x[c] = before + inc[c] - x[c];
+        tot[c] = all;
+    }
+    __syncthreads();
+}
+
+template <int NV, bool WRITE, int KW>
+__global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
+    constexpr uint32_t INF = 0xFFFFFFFFu;
+    const uint32_t H = *a.hcount;
+    for (uint32_t hi = blockIdx.x; hi < H; hi += gridDim.x) {
+        const uint32_t t = a.hlist[hi];
+        int64_t rv[NV];
+        uint32_t tb[NV], tc[NV], kb[NV], nk[NV], mb[NV];
+        int pv = 0, pk = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            rv[v] = a.row[v] ? (int64_t)a.row[v][t] : (int64_t)t;
+            const bool has = rv[v] >= 0;
+            tc[v] = has ? a.tcnt[v][rv[v]] : 0u;
+            tb[v] = has ? a.ent_off[v][rv[v]] : 0u;
+            kb[v] = has ? a.key_off[v][rv[v]] : 0u;
+            nk[v] = has ? a.key_off[v][rv[v] + 1] - kb[v] : 0u;
+            mb[v] = has ? a.k2t_off[v][rv[v]] : 0u;
+            if (tc[v] > tc[pv]) pv = v;
+            if (nk[v] > nk[pk]) pk = v;
+        }
+        const uint32_t nT = (tc[pv] + MCH - 1) / MCH, nK = (nk[pk] + MCH - 1) / MCH;
+        const uint32_t nch = nT > nK ? nT : nK;
+        const uint32_t cpt = (nch + MH_T - 1) / MH_T;
+        const uint32_t c0 = threadIdx.x * cpt, c1 = min(nch, c0 + cpt);
+        // chunk c of the TxnIds: [T_pv[c*MCH], T_pv[(c+1)*MCH]) in every reply
+        auto t_bounds = [&](uint32_t c, uint32_t* cur, uint32_t* end) {
+            const uint32_t lo = c == 0 ? 0u : a.txns[pv][tb[pv] + c * MCH];
+            const uint32_t hiv = (c + 1) * MCH < tc[pv] ? a.txns[pv][tb[pv] + (c + 1) * MCH] : INF;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const uint32_t b = tb[v], e = tb[v] + tc[v];
+                cur[v] = c == 0 ? b : lb_u32(a.txns[v], b, e, lo);
+                end[v] = hiv == INF ? e : lb_u32(a.txns[v], cur[v], e, hiv);
+            }
+        };
+        auto k_bounds = [&](uint32_t c, uint32_t* kc, uint32_t* ke) {
+            const bool first = c == 0, last = (c + 1) * MCH >= nk[pk];
+            const MKey<KW> lo = first ? MKey<KW>{0ull, 0ull} : MKey<KW>::load(a.keys[pk], kb[pk] + c * MCH);
+            const MKey<KW> hv = last ? MKey<KW>{0ull, 0ull} : MKey<KW>::load(a.keys[pk], kb[pk] + (c + 1) * MCH);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const uint32_t b = kb[v], e = kb[v] + nk[v];
+                kc[v] = first ? b : lb_key<KW>(a.keys[v], b, e, lo);
+                ke[v] = last ? e : lb_key<KW>(a.keys[v], kc[v], e, hv);
+            }
+        };
+        // TxnId union of one chunk (count, or write at out[pos..])
+        auto t_union = [&](uint32_t c, uint32_t* out) -> uint32_t {
+            if (c >= nT) return 0u;
+            uint32_t cur[NV], end[NV], head[NV];
+            t_bounds(c, cur, end);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) head[v] = cur[v] < end[v] ? a.txns[v][cur[v]] : INF;
+            uint32_t m = 0;
+            while (true) {
+                uint32_t mn = INF;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) mn = head[v] < mn ? head[v] : mn;
+                if (mn == INF) break;
+                if (out) out[m] = mn;
+                ++m;
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    if (head[v] == mn) { ++cur[v]; head[v] = cur[v] < end[v] ? a.txns[v][cur[v]] : INF; }
+            }
+            return m;
+        };
+        // key union of one chunk: (keys, entries); write: keys at okey, header slots from kpos, entries from
+        // ep (absolute k2t positions), TxnIds remapped into U[0, mu)
+        auto k_union = [&](uint32_t c, bool wr, uint32_t kpos, uint32_t ep, const uint32_t* U, uint32_t mu,
+                           uint32_t okb, uint32_t omb, uint32_t onk, uint32_t* n_e) -> uint32_t {
+            *n_e = 0;
+            if (c >= nK) return 0u;
+            uint32_t kc[NV], ke[NV];
+            k_bounds(c, kc, ke);
+            uint32_t mk = 0, me = 0;
+            while (true) {
+                bool any = false;
+                MKey<KW> kmin{0ull, 0ull};
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    if (kc[v] < ke[v]) {
+                        MKey<KW> k = MKey<KW>::load(a.keys[v], kc[v]);
+                        if (!any || k < kmin) { kmin = k; any = true; }
+                    }
+                }
+                if (!any) break;
+                uint32_t lc[NV], le[NV], lh[NV];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    lc[v] = 0; le[v] = 0; lh[v] = INF;
+                    if (kc[v] < ke[v] && MKey<KW>::load(a.keys[v], kc[v]) == kmin) {
+                        const uint32_t ki = kc[v] - kb[v];
+                        lc[v] = mb[v] + (ki == 0 ? nk[v] : (uint32_t)a.k2t[v][mb[v] + ki - 1]);
+                        le[v] = mb[v] + (uint32_t)a.k2t[v][mb[v] + ki];
+                        lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF;
+                        ++kc[v];
+                    }
+                }
+                uint32_t x = 0;
+                while (true) {
+                    uint32_t mn = INF;
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) mn = lh[v] < mn ? lh[v] : mn;
+                    if (mn == INF) break;
+                    if (wr) {
+                        x = lb_u32(U, x, mu, mn);
+                        a.o_k2t[ep++] = (int32_t)x;
+                    }
+                    ++me;
+#pragma unroll
+                    for (int v = 0; v < NV; ++v)
+                        if (lh[v] == mn) { ++lc[v]; lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF; }
+                }
+                if (wr) {
+                    a.o_keys[KW * (size_t)(okb + kpos + mk)] = kmin.a;
+                    if (KW == 2) a.o_keys[KW * (size_t)(okb + kpos + mk) + 1] = kmin.b;
+                    a.o_k2t[omb + kpos + mk] = (int32_t)(ep - omb);
+                }
+                ++mk;
+            }
+            (void)onk;
+            *n_e = me;
+            return mk;
+        };
+        uint32_t x[3] = {0, 0, 0}, tot[3];
+        if (!WRITE) {
+            for (uint32_t c = c0; c < c1; ++c) {
+                x[2] += t_union(c, nullptr);
+                uint32_t ne;
+                x[0] += k_union(c, false, 0, 0, nullptr, 0, 0, 0, 0, &ne);
+                x[1] += ne;
+            }
+            block_scan3(x, tot);
+            if (threadIdx.x == 0) { a.mk[t] = tot[0]; a.me[t] = tot[1]; a.mu[t] = tot[2]; }
+        } else {
+            uint32_t* U = a.o_txns + a.o_ent_off[t];
+            for (uint32_t c = c0; c < c1; ++c) x[2] += t_union(c, nullptr);
+            block_scan3(x, tot);
+            uint32_t pos = x[2];
+            for (uint32_t c = c0; c < c1; ++c) pos += t_union(c, U + pos);
+            const uint32_t mu = tot[2];
+            __threadfence_block();
+            __syncthreads();
+            // keys: per-thread (keys, entries) totals, then the writes
+            x[0] = x[1] = x[2] = 0;
+            for (uint32_t c = c0; c < c1; ++c) {
+                uint32_t ne;
+                x[0] += k_union(c, false, 0, 0, nullptr, 0, 0, 0, 0, &ne);
+                x[1] += ne;
+            }
+            block_scan3(x, tot);
+            const uint32_t okb = a.o_key_off[t], omb = a.o_k2t_off[t];
+            const uint32_t onk = a.o_key_off[t + 1] - okb;
+            uint32_t kpos = x[0], ep = omb + onk + x[1];
+            for (uint32_t c = c0; c < c1; ++c) {
+                uint32_t ne;
+                kpos += k_union(c, true, kpos, ep, U, mu, okb, omb, onk, &ne);
+                ep += ne;
+            }
+            if (threadIdx.x == 0) a.o_tcnt[t] = mu;
+        }
+        __syncthreads();
+    }
+}
+
 // Offsets of K merged outputs from the count pass, in one scan: state (keys, entries, TxnIds) x K.
 template <int K>
 struct MultiOffsetsOp {
@@ -204,6 +440,7 @@ __global__ __launch_bounds__(256) void k_tcnt_from_off(size_t n, const uint32_t*
 template <int NV>
 inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t st) {
     const int g = ceil_div((long)a.n, 256);
+    {
     KScope ks(write ? K_MERGE_WRITE : K_MERGE_COUNT, a.n);
     if (kw == 2) {
         if (write) k_merge<NV, true, 2><<<g, 256, 0, st>>>(a);
@@ -211,6 +448,17 @@ inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t 
     } else {
         if (write) k_merge<NV, true, 1><<<g, 256, 0, st>>>(a);
         else k_merge<NV, false, 1><<<g, 256, 0, st>>>(a);
+    }
+    }
+    if (!a.hlist) return;
+    const int gh = std::min<int>(g, MH_GRID);
+    KScope kh(write ? K_MERGE_HEAVY_WRITE : K_MERGE_HEAVY_COUNT);
+    if (kw == 2) {
+        if (write) k_merge_heavy<NV, true, 2><<<gh, MH_T, 0, st>>>(a);
+        else k_merge_heavy<NV, false, 2><<<gh, MH_T, 0, st>>>(a);
+    } else {
+        if (write) k_merge_heavy<NV, true, 1><<<gh, MH_T, 0, st>>>(a);
+        else k_merge_heavy<NV, false, 1><<<gh, MH_T, 0, st>>>(a);
     }
 }
 
