@@ -53,6 +53,8 @@ def lib():
         L.ad_fetch_deps.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut)]
         L.ad_merge_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
+        L.ad_fetch_rows.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, C.POINTER(abi.AdCsrSizes),
+                                    C.POINTER(abi.AdCsrOut)]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ad_run_pipeline.argtypes = [vp]
@@ -72,7 +74,7 @@ def lib():
 
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
-            "ad_fetch_deps", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_alltoall", "ad_shard_merge",
@@ -132,6 +134,16 @@ class DepsEngine:
         out = abi.Csr.alloc(s, is_range=(cls == abi.CLASS_RANGE))
         o = out.as_out()
         self._check(lib().ad_fetch_deps(self.h, view, cls, C.byref(o)), "ad_fetch_deps")
+        return out
+
+    def fetch_rows(self, view, cls, lo, hi):
+        """Rows [lo, hi) of replica view `view` (view == replicas: the merged Deps) for class `cls`, as an
+        abi.Csr over hi - lo txns (paged fetch: full-size batches hold ~10^9 entries per view)."""
+        s = abi.AdCsrSizes()
+        self._check(lib().ad_fetch_rows(self.h, view, cls, lo, hi, C.byref(s), None), "ad_fetch_rows")
+        out = abi.Csr.alloc(s, is_range=(cls == abi.CLASS_RANGE))
+        o = out.as_out()
+        self._check(lib().ad_fetch_rows(self.h, view, cls, lo, hi, C.byref(s), C.byref(o)), "ad_fetch_rows")
         return out
 
     def merge(self):

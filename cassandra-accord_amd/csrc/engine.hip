@@ -895,6 +895,36 @@ int csr_sizes(ad_handle* h, const Csr& c, ad_csr_sizes* s) {
     return AD_OK;
 }
 
+// Rows [lo, hi) of one CSR, offsets rebased to 0 (sizes always; the arrays when out != nullptr).
+int fetch_rows(ad_handle* h, const Csr& c, int kw, size_t lo, size_t hi, ad_csr_sizes* s, ad_csr_out* out) {
+    hipStream_t st = h->st;
+    const size_t m = hi - lo;
+    std::vector<uint32_t> ko(m + 1), mo(m + 1), eo(m + 1), cnt(m);
+    HIPCHK(h, hipMemcpyAsync(ko.data(), c.key_off + lo, (m + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(mo.data(), c.k2t_off + lo, (m + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(eo.data(), c.ent_off + lo, (m + 1) * 4, hipMemcpyDeviceToHost, st));
+    if (m) HIPCHK(h, hipMemcpyAsync(cnt.data(), c.tcnt + lo, m * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    size_t tot = 0;
+    for (uint32_t x : cnt) tot += x;
+    s->n = m; s->keys = ko[m] - ko[0]; s->k2t = mo[m] - mo[0]; s->txn_cap = eo[m] - eo[0]; s->txns = tot;
+    if (!out) return AD_OK;
+    for (size_t i = 0; i <= m; ++i) { out->key_off[i] = ko[i] - ko[0]; out->k2t_off[i] = mo[i] - mo[0]; }
+    if (s->keys) HIPCHK(h, hipMemcpyAsync(out->keys, c.keys + (size_t)kw * ko[0], s->keys * 8 * kw, hipMemcpyDeviceToHost, st));
+    if (s->k2t) HIPCHK(h, hipMemcpyAsync(out->k2t, c.k2t + mo[0], s->k2t * 4, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> tx(s->txn_cap);
+    if (s->txn_cap) HIPCHK(h, hipMemcpyAsync(tx.data(), c.txns + eo[0], s->txn_cap * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    uint32_t o = 0;
+    out->txn_off[0] = 0;
+    for (size_t i = 0; i < m; ++i) {
+        std::memcpy(out->txns + o, tx.data() + (eo[i] - eo[0]), cnt[i] * 4);
+        o += cnt[i];
+        out->txn_off[i + 1] = o;
+    }
+    return AD_OK;
+}
+
 }  // namespace
 
 // =====================================================================================================
@@ -1063,6 +1093,27 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
     hipSetDevice(h->device);
     if (cls == AD_CLASS_RANGE) return h->merged_has_range ? fetch_csr(h, h->merged[2], 2, out) : fetch_empty(h, out);
     return fetch_csr(h, h->merged[cls], 1, out);
+}
+
+int ad_fetch_rows(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t hi, ad_csr_sizes* sizes, ad_csr_out* out) {
+    if (!h || !sizes) return AD_ERR_ARGUMENT;
+    if (cls >= AD_NUM_CLASSES || view > h->cfg.replicas) return set_err(h, AD_ERR_ARGUMENT, "view/class out of range");
+    if (lo > hi || hi > h->n) return set_err(h, AD_ERR_ARGUMENT, "row range outside the batch");
+    hipSetDevice(h->device);
+    const Csr* c;
+    if (view == h->cfg.replicas) {
+        if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_fetch_rows of the merged Deps before ad_merge_deps");
+        c = &h->merged[cls];
+    } else {
+        if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_fetch_rows before ad_preaccept_deps");
+        c = cls == AD_CLASS_RANGE ? &h->rdeps[view] : &h->deps[2 * view + cls];
+    }
+    if (c->ncap == 0 && c->nkeys == 0) {          // empty class: offsets are zero
+        sizes->n = hi - lo; sizes->keys = sizes->k2t = sizes->txn_cap = sizes->txns = 0;
+        if (out) for (size_t i = 0; i <= hi - lo; ++i) out->key_off[i] = out->k2t_off[i] = out->txn_off[i] = 0;
+        return AD_OK;
+    }
+    return fetch_rows(h, *c, cls == AD_CLASS_RANGE ? 2 : 1, lo, hi, sizes, out);
 }
 
 int ad_merge_host(ad_handle* h, const ad_csr_in* parts, uint32_t r, ad_csr_sizes* sizes) {

@@ -176,6 +176,12 @@ int  ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out);
 int  ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
 int  ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out);
 
+/* Paged fetch: rows [lo, hi) of replica view `view`'s CSR of class `cls` (view == replicas: the merged
+ * Deps), offsets rebased to 0.  Two calls: out == NULL fills *sizes (n = hi - lo), then the caller
+ * allocates and passes out.  Lets a host stream a full-size batch's Deps (C4: ~10^9 entries per view)
+ * txn window by txn window, as the replies of KeyDeps/RangeDeps.SerializerSupport.create are consumed. */
+int  ad_fetch_rows(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t hi, ad_csr_sizes* sizes, ad_csr_out* out);
+
 /* Stage 2' — Deps.merge of caller-supplied replies (host CSR, same batch).  parts[r*AD_NUM_CLASSES+c]. */
 typedef struct ad_csr_in {
     const uint32_t* key_off; const uint64_t* keys; const uint32_t* k2t_off; const int32_t* k2t;

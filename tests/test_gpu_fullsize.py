@@ -132,6 +132,71 @@ def level_equations(batch, lv):
     assert np.array_equal(req, lv.astype(np.int64)), "levels are not the solution of the chain equations"
 
 
+def chain_req(batch, lv):
+    """(a) per txn: 1 + max level of its chain predecessors on every key (0 if none); plus the chains
+    (key, executeAt rank)-sorted with their inclusive prefix max level, for the (c) check."""
+    ko = batch["key_off"].astype(np.int64)
+    t = owner(ko)
+    keys = batch["keys"].astype(np.int64)
+    exe = ts_key(batch["exec_msb"], batch["exec_lsb"], batch["exec_node"])
+    erank = np.empty(batch["n"], np.int64)
+    erank[np.lexsort(tuple(reversed(exe)))] = np.arange(batch["n"])
+    order = np.lexsort((erank[t], keys))
+    t, keys = t[order], keys[order]
+    wr = ((batch["txn_lsb"].astype(np.int64) >> 1) & 7)[t] == abi.KIND_WRITE
+    L = lv.astype(np.int64)[t]
+    seg = np.r_[0, np.cumsum(keys[1:] != keys[:-1])]
+    big = np.int64(1 << 40)
+    inc_all = np.maximum.accumulate(seg * big + L) - seg * big
+
+    def excl_cummax(v):
+        inc = np.maximum.accumulate(seg * big + v)
+        ex = np.r_[np.int64(-1), inc[:-1]]
+        return np.where(np.r_[True, seg[1:] != seg[:-1]], -1, ex - seg * big)
+    need = np.where(wr, excl_cummax(L), excl_cummax(np.where(wr, L, -1))) + 1
+    req = np.zeros(batch["n"], np.int64)
+    np.maximum.at(req, t, need)
+    return req, (keys, erank[t], inc_all), erank
+
+
+def level_exact_window(batch, lv, lo, mkey, mdirect, mrange):
+    """Rows [lo, lo + m) (merged CSRs fetched by ad_fetch_rows): every level equals 1 + the max over
+    (a) its key chains, (b) merged direct/range deps with an earlier executeAt, (c) for unmanaged (range)
+    txns, per key of its merged KeyDeps, the chain prefix up to the greatest executeAt among its deps there
+    below its own (Updating.updateUnmanaged); 0 with no predecessor."""
+    req, (ckey, crank, cpm), erank = chain_req(batch, lv)
+    m = mkey.n
+    rows = np.arange(lo, lo + m, dtype=np.int64)
+    want = req[rows].copy()
+    L = lv.astype(np.int64)
+    for csr in (mdirect, mrange):
+        to = csr.txn_off.astype(np.int64)
+        t = owner(to)
+        d = csr.txns.astype(np.int64)
+        ok = erank[d] < erank[lo + t]
+        need = np.full(m, 0, np.int64)
+        np.maximum.at(need, t[ok], L[d[ok]] + 1)
+        want = np.maximum(want, need)
+    t, key, dep = triples(mkey)
+    unmanaged = (batch["txn_lsb"].astype(np.int64) & 1)[lo + t] == 1
+    e = erank[dep]
+    sel = unmanaged & (e < erank[lo + t])
+    t, key, e = t[sel], key[sel].astype(np.int64), e[sel]
+    if len(t):
+        tk = np.unique(np.stack([t, key]), axis=1)
+        grp = np.searchsorted(tk[0] * (1 << 40) + tk[1], t * (1 << 40) + key)
+        bnd = np.full(tk.shape[1], -1, np.int64)
+        np.maximum.at(bnd, grp, e)
+        # last chain entry of the key with executeAt rank <= bnd
+        comp = ckey * (1 << 24) + crank
+        pos = np.searchsorted(comp, tk[1] * (1 << 24) + bnd, side="right") - 1
+        hit = (pos >= 0) & (ckey[np.maximum(pos, 0)] == tk[1])
+        need = np.full(m, 0, np.int64)
+        np.maximum.at(need, tk[0][hit], cpm[pos[hit]] + 1)
+        want = np.maximum(want, need)
+    assert np.array_equal(want, L[rows]), "levels in rows [%d, %d) are not the solution of their constraints" % (lo, lo + m)
+
+
 def run_full(engine_factory, batch):
     eng = engine_factory(window=W, replicas=R, drop_p=DROP, seed=0xACC0D1)
     eng.load(batch)
@@ -180,10 +245,7 @@ def test_full_size_key_batches(engine_factory, name):
 
 
 def test_c4_mixed_ranges_quarter_size(engine_factory):
-    # C4's mix at 1,048,576 txns.  At its full 4,194,304 txns the RangeDeps alone are ~10^9 entries per
-    # replica view (every key txn depends on the ~80 earlier ranges covering each of its keys), ~150 GB of
-    # device CSRs for 3 views + merge in this per-txn layout: beyond one GPU without chunking the queries
-    # (DESIGN.md §7); the quarter-size batch keeps the same density per key (4x fewer ranges cover a key).
+    # C4's mix at 1,048,576 txns with whole-CSR fetches (the full 4,194,304 txns: the test below).
     batch = workload.config("C4", n=1 << 20)
     eng = engine_factory(window=W, replicas=R, drop_p=DROP, seed=0xACC0D1)
     eng.load(batch)
@@ -212,4 +274,56 @@ def test_c4_mixed_ranges_quarter_size(engine_factory):
         t, _, dep = triples(rviews[v])
         assert (dep < t).all()
     triples(rmerged)
+    check_order(batch, lv, order)
+
+
+def exact_triples(csr, lo):
+    """Sorted unique (txn, key or range, dependency) rows of a fetched window, checked for canonical form
+    and the PreAccept bound (dependency rank below the txn's)."""
+    t, key, dep = triples(csr)
+    assert (dep < lo + t).all(), "PreAccept bound: a dependency must have a smaller TxnId"
+    rec = np.zeros(len(t), dtype=[("td", np.uint64), ("s", np.uint64), ("e", np.uint64)])
+    rec["td"] = (t.astype(np.uint64) << np.uint64(32)) | dep.astype(np.uint64)
+    if csr.is_range:
+        r2 = csr.keys.reshape(-1, 2)
+        rec["s"], rec["e"] = r2[key, 0], r2[key, 1]
+    else:
+        rec["s"] = key
+    out = np.unique(rec)
+    assert len(out) == len(rec), "duplicate (key, TxnId) entry"
+    return out
+
+
+def test_c4_full_size(engine_factory):
+    """BASELINE configs[3] at its full size: 4,194,304 mixed key + range txns on one GPU.  The Deps hold
+    ~0.8*10^9 KeyDeps and ~10^9 RangeDeps entries per replica view (each key Write depends on the earlier
+    range Reads covering its keys; each range Read on the last Writes of the ~3000 keys it spans), so the
+    CSRs are read back by txn window (ad_fetch_rows): exact prefix parity against the oracle, then three
+    windows across the batch checked for canonical form, the PreAccept bound, merged == union of the views,
+    and levels exactly solving their (a)/(b)/(c) constraints; the order over the whole batch."""
+    batch = workload.config("C4")
+    n = batch["n"]
+    assert n == 1 << 22
+    eng = engine_factory(window=W, replicas=R, drop_p=DROP, seed=0xACC0D1)
+    eng.load(batch)
+    sizes = eng.preaccept_deps()
+    assert sizes[abi.CLASS_RANGE].keys > 5 * 10 ** 8, "C4 RangeDeps far smaller than modelled"
+    eng.merge()
+    lv, order, _ = eng.exec_levels()
+    all_cls = (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY, abi.CLASS_RANGE)
+    k = 4000
+    ref = O.OracleResult(workload.slice_batch(batch, 0, k), abi.make_config(W, R, DROP, 0xACC0D1), O.FLAG_MERGE)
+    for c in all_cls:
+        for v in range(R):
+            assert eng.fetch_rows(v, c, 0, k).equal(ref.deps(v, c)), "view %d class %d prefix differs" % (v, c)
+        assert eng.fetch_rows(R, c, 0, k).equal(ref.merged(c)), "merged class %d prefix differs" % c
+    for lo in (n // 4, n // 2 + 12345, n - 3000):
+        hi = min(n, lo + 3000)
+        merged = {}
+        for c in all_cls:
+            parts = [exact_triples(eng.fetch_rows(v, c, lo, hi), lo) for v in range(R)]
+            merged[c] = eng.fetch_rows(R, c, lo, hi)
+            union = np.unique(np.concatenate(parts))
+            assert np.array_equal(exact_triples(merged[c], lo), union), "merged != union of the views in [%d, %d)" % (lo, hi)
+        level_exact_window(batch, lv, lo, merged[abi.CLASS_KEY], merged[abi.CLASS_DIRECT_KEY], merged[abi.CLASS_RANGE])
     check_order(batch, lv, order)
