@@ -64,12 +64,12 @@ def alg_bytes(kernel, calls, units, n, P, R, st):
     return per.get(kernel)
 
 
-def pipeline_alg_bytes(n, P, R, st):
+def pipeline_alg_bytes(n, P, R, st, Q=0):
     """SURVEY §8(d) B_alg for one batch (B_in + B_sort + B_scan + B_out + B_merge + B_level)."""
     D, M = st["deps_entries"], st["merged_entries"]
     key_bits = 24
-    b_in = n * 40 + P * 12
-    b_sort = -(-key_bits // 8) * 2 * P * 8
+    b_in = n * 40 + P * 12 + Q * 20
+    b_sort = -(-key_bits // 8) * 2 * P * 8 + 2 * 3 * 2 * Q * 12     # ranges: by end then start, 24-bit each
     b_scan = P * (8 + 24)
     b_out = n * 4 * 3 * R + D * 8
     b_merge = (n * 12 * R + D * 8) + (n * 12 + M * 8)
@@ -77,7 +77,7 @@ def pipeline_alg_bytes(n, P, R, st):
     return b_in + b_sort + b_scan + b_out + b_merge + b_level
 
 
-def cpu_baseline(sample_n):
+def cpu_baseline(sample_n, cfg="C2"):
     """The oracle (oracle/, the CPU restatement of the reference algorithms) on a bounded sample of the
     same workload on this host, with 1 thread and with T threads (T in {1, nproc}; the deps
     stage runs one single-threaded store per key-range shard as InMemoryCommandStore.SingleThread,
@@ -85,11 +85,14 @@ def cpu_baseline(sample_n):
     share is 16 cores.  Test infrastructure: timed here as the reported baseline only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    b = workload.config("C2", n=sample_n)
-    cfg = abi.make_config(WINDOW, REPLICAS, DROP_P, workload.SEEDS["C2"])
+    b = workload.config(cfg, n=sample_n)
+    name = cfg
+    cfg = abi.make_config(WINDOW, REPLICAS, DROP_P, workload.SEEDS[name])
     flags = O.FLAG_PRUNE | O.FLAG_MERGE | O.FLAG_LEVELS
     runs = {}
-    for threads in sorted({1, max(1, min(16, os.cpu_count() or 1))}):
+    # the threaded restatement shards key txns only (range txns span stores: single-threaded oracle)
+    tset = {1} if b.get("range_off") is not None else {1, max(1, min(16, os.cpu_count() or 1))}
+    for threads in sorted(tset):
         s = O.OracleResult(b, cfg, flags, threads=threads).stats()
         runs[threads] = (s["t_deps"] + s["t_merge"] + s["t_levels"], s)
     T = max(runs)
@@ -97,9 +100,9 @@ def cpu_baseline(sample_n):
     t1 = runs[1][0]
     return {"value": sample_n / t, "unit": "txn/s", "cores": T, "kind": "port",
             "single_thread_value": sample_n / t1,
-            "sample": "C2 generator, first %d txns (seed 0xACC0D1), PreAccept deps x%d views + Deps.merge + "
+            "sample": "%s generator, first %d txns (seed %#x), PreAccept deps x%d views + Deps.merge + "
                       "exec levels; %d threads %.1f s (deps %.1f, merge %.1f, levels %.1f); 1 thread %.1f s"
-                      % (sample_n, REPLICAS, T, t, s["t_deps"], s["t_merge"], s["t_levels"], t1)}
+                      % (name, sample_n, workload.SEEDS[name], REPLICAS, T, t, s["t_deps"], s["t_merge"], s["t_levels"], t1)}
 
 
 def trace_roofline(eng, run_step, n, P):
@@ -268,8 +271,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--txns-per-gpu", dest="n", type=int, default=1 << 20, help="txns per GPU batch (C2: 1M)")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 18, help="txns in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--txns-per-gpu", dest="n", type=int, default=None,
+                    help="txns per GPU batch (default: the config's size, C2/C3 1M, C4 4M; N>1: 1M per GPU)")
+    ap.add_argument("--config", choices=("C2", "C3", "C4"), default="C2",
+                    help="N=1 workload: C2 (BASELINE configs[1], the metric's config; default), C3 (Zipf hot keys) "
+                         "or C4 (mixed key + range txns, 4M); the JSON line names it in config.workload")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="txns in the CPU-baseline sample (default 262144; C4: 16384; 0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel breakdown to stderr")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl", help="N>1 exchange: RCCL over xGMI or host/gloo")
     args = ap.parse_args()
@@ -278,6 +286,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        args.n = args.n or (1 << 20)
         import torch.distributed as tdist
         with stdout_to_stderr():          # gloo's connection notices
             tdist.init_process_group("gloo")
@@ -287,9 +296,11 @@ def main():
             tdist.destroy_process_group()
         return
 
-    batch = workload.config("C2", n=args.n)
+    cfgname = args.config
+    batch = workload.config(cfgname, n=args.n)
     n, P = batch["n"], int(batch["key_off"][-1])
-    eng = engine.DepsEngine(device=local, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C2"])
+    Q = int(batch["range_off"][-1]) if batch.get("range_off") is not None else 0
+    eng = engine.DepsEngine(device=local, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS[cfgname])
     eng.load(batch)                                   # host -> HBM once; the timed region starts resident
 
     for _ in range(max(args.warmup, 1)):
@@ -311,28 +322,32 @@ def main():
     eng.set_trace(0)
     ms_per_step = dt * 1e3 / args.steps
     value = n * args.steps / dt
-    pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st) / (dt / args.steps) / 1e9
+    pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st, Q) / (dt / args.steps) / 1e9
 
     out = {
         "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
         "value": value, "unit": "txn/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C2 generator, BASELINE configs[1])",
-        "config": {"workload": "C2: %d txns x 4 keys uniform over 10M keys; PreAccept deps under R=%d "
+        "dtype": "u32/u64 (integer)",
+        "data": "synthetic (seeded %s generator, BASELINE configs[%d])" % (cfgname, {"C2": 1, "C3": 2, "C4": 3}[cfgname]),
+        "config": {"workload": "%s: %d txns x 4 keys %s over 10M keys%s; PreAccept deps under R=%d "
                                "replica views (in-flight window W=%d, drop p=%.1f) + Deps.merge + exec levels/order"
-                               % (n, REPLICAS, WINDOW, DROP_P),
+                               % (cfgname, n, "Zipf(0.99)" if cfgname == "C3" else "uniform",
+                                  "; 10%% range txns, %d ranges of width U[1, 8192]" % Q if Q else "",
+                                  REPLICAS, WINDOW, DROP_P),
                    "txns_per_gpu": n, "keys_per_txn": 4, "keyspace": KEYSPACE, "replicas": REPLICAS,
                    "window": WINDOW, "parallelism": "single CommandStore on 1 GPU"},
         "roofline": roof,
-        "pipeline": {"alg_bytes": pipeline_alg_bytes(n, P, REPLICAS, st), "alg_GBps": pipe_gbs,
+        "pipeline": {"alg_bytes": pipeline_alg_bytes(n, P, REPLICAS, st, Q), "alg_GBps": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS,
                      "stage_ms": {k: st[k] for k in ("prepare", "sort", "deps", "merge", "levels", "total")},
                      "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
                      "level_iterations": st["level_iterations"]},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+    sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 18)
+    if rank == 0 and world == 1 and sample > 0:
+        out["cpu_baseline"] = cpu_baseline(sample, cfgname)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     eng.close()
     print(json.dumps(out), flush=True)

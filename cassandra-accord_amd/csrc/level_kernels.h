@@ -594,6 +594,121 @@ constexpr int KAHN_GRID = 2048;
 __device__ inline void kahn_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
     if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
 }
+// ---------------------------------------------------------------------------------------------------
+// Kahn chain build for batches with long chains (C3's Zipf hot keys: ~10^5 entries on one key), all
+// positions in parallel instead of one thread per segment:
+//   1. k_chain_rank: executeAt order inside each key segment by windowed inversion ranks (entries arrive in
+//      TxnId order; only slow-path bumps move, a few positions): rank = i + #{later j in the segment and
+//      the +-CR_D window with a smaller executeAt} - #{earlier j with a larger one}, scattered with the
+//      entry; k_chain_check verifies every slot was filled and executeAt ascends per segment (else the
+//      serial k_chain_order runs).
+//   2. two segmented scans: last Write before each position, next Write after it (or the segment end);
+//   3. k_chain_links: the transitive reduction of the (a) rule from those two positions: in-degree per
+//      txn and the successor run per pair, the same edges k_chain_build derives serially.
+constexpr int CR_N = 1024, CR_D = 64, CR_T = 256;
+__global__ __launch_bounds__(CR_T) void k_chain_rank(size_t P, const int32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                                     const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                                     uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                                     uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair) {
+    __shared__ uint64_t sk[CR_N + 2 * CR_D];
+    __shared__ int32_t ss[CR_N + 2 * CR_D];
+    const long base = (long)blockIdx.x * CR_N;
+    for (int x = threadIdx.x; x < CR_N + 2 * CR_D; x += CR_T) {
+        const long g = base + x - CR_D;
+        const bool in = g >= 0 && g < (long)P;
+        sk[x] = in ? e_exec1[g] : 0ull;
+        ss[x] = in ? seg_start[g] : -2;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < CR_N; e += CR_T) {
+        const long i = base + e;
+        if (i >= (long)P) break;
+        const uint64_t key = sk[e + CR_D];
+        const int32_t sg = ss[e + CR_D];
+        int r = 0;
+#pragma unroll 16
+        for (int k = 1; k <= CR_D; ++k) {
+            r += (ss[e + CR_D + k] == sg && sk[e + CR_D + k] < key) ? 1 : 0;
+            r -= (ss[e + CR_D - k] == sg && sk[e + CR_D - k] > key) ? 1 : 0;
+        }
+        const long q = i + r;
+        if (q < 0 || q >= (long)P) continue;          // the check pass sees the hole
+        c_txn[q] = e_txn[i];
+        c_meta[q] = e_meta[i];
+        c_exec1[q] = key;
+        c_pair[q] = sval[i];
+    }
+}
+__global__ __launch_bounds__(256) void k_chain_check(size_t P, const int32_t* __restrict__ seg_start,
+                                                     const uint64_t* __restrict__ c_exec1, const uint32_t* __restrict__ c_pair,
+                                                     uint32_t* __restrict__ bad) {
+    bool b = false;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < P; q += (size_t)gridDim.x * blockDim.x) {
+        if (c_pair[q] == 0xFFFFFFFFu) b = true;
+        else if (q + 1 < P && seg_start[q + 1] == seg_start[q] && c_exec1[q] > c_exec1[q + 1]) b = true;
+    }
+    wave_set_flag(b, bad);
+}
+// MIN = false: exclusive prefix max of Write positions per segment (-1: none) = last Write before q.
+// MIN = true (scanned from the end): exclusive suffix min of Write positions per segment, the segment end
+// when none = next Write after q.
+template <bool MIN>
+struct WriteLinkOp {
+    struct S { int32_t f, v; };
+    size_t P;
+    const int32_t* seg_start;
+    const uint8_t* c_meta;
+    int32_t* out;
+    __device__ size_t pos(size_t i) const { return MIN ? P - 1 - i : i; }
+    __device__ S identity() const { return S{0, MIN ? 0x7FFFFFFF : -1}; }
+    __device__ S load(size_t i) const {
+        const size_t q = pos(i);
+        const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
+        S s;
+        if (MIN) {
+            const bool last = q + 1 == P || seg_start[q + 1] != seg_start[q];
+            s.f = last ? 1 : 0;
+            s.v = wr ? (int32_t)q : (last ? (int32_t)(q + 1) : 0x7FFFFFFF);
+        } else {
+            s.f = seg_start[q] == (int32_t)q ? 1 : 0;
+            s.v = wr ? (int32_t)q : -1;
+        }
+        return s;
+    }
+    __device__ S combine(const S& x, const S& y) const {
+        if (y.f) return y;
+        return S{x.f, MIN ? (x.v < y.v ? x.v : y.v) : (x.v > y.v ? x.v : y.v)};
+    }
+    __device__ void store(size_t i, const S& ex, const S&, const S& el) const {
+        const size_t q = pos(i);
+        out[q] = el.f ? (MIN ? (int32_t)(q + 1) : -1) : ex.v;
+    }
+};
+__global__ __launch_bounds__(256) void k_chain_links(size_t P, const int32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
+                                                     const uint32_t* __restrict__ c_pair, const int32_t* __restrict__ last_w,
+                                                     const int32_t* __restrict__ next_w, uint32_t* __restrict__ indeg,
+                                                     uint2* __restrict__ succ) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    const int32_t s0 = seg_start[q];
+    const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
+    const int32_t lw = last_w[q], nw = next_w[q];
+    const bool last = q + 1 == P || seg_start[q + 1] != s0;
+    uint32_t pc;
+    if (wr) pc = lw >= 0 ? ((int32_t)q - lw - 1 > 0 ? (uint32_t)((int32_t)q - lw - 1) : 1u) : (uint32_t)((int32_t)q - s0);
+    else pc = lw >= 0 ? 1u : 0u;
+    if (pc) atomicAdd(&indeg[c_txn[q]], pc);
+    uint2 sc = make_uint2(0u, 0u);
+    if (wr) {
+        if (!last) sc = nw == (int32_t)q + 1 ? make_uint2((uint32_t)q + 1, 1u) : make_uint2((uint32_t)q + 1, (uint32_t)(nw - ((int32_t)q + 1)));
+    } else if (nw < (int32_t)P && seg_start[nw] == s0) {
+        sc = make_uint2((uint32_t)nw, 1u);
+    }
+    if (sc.y) succ[c_pair[q]] = sc;
+}
+
 // Extra successors (mixed key + range batches): xs[xoff[t] .. xoff[t+1]) are the txns waiting on t through a
 // (b) dependency edge or a (c) chain-prefix constraint (k_xedges).  A txn with at most XLIGHT of them releases
 // them itself; heavier ones (a range txn can have thousands of dependants) are released by the whole wave,
@@ -654,6 +769,96 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
         }
     }
     wave_set_flag(released, work);
+}
+
+// Deep graphs (C3: the hot key's ~10^5 Writes make ~10^5 levels, a handful of txns each): one launch per
+// wavefront costs more than the wavefront.  k_kahn_small runs consecutive wavefronts inside ONE workgroup:
+// the frontier is an explicit list (LDS counter, global slots), released successors are appended to the
+// next list, a workgroup barrier separates levels.  It stops when a frontier exceeds KS_MAX (the
+// grid-wide k_kahn_step takes over from that level: its L == lvl test needs no list) or is empty.
+// k_frontier_collect builds the list of the txns at level lvl for the switch.
+constexpr int KS_T = 1024;
+constexpr uint32_t KS_MAX = 4096;
+__global__ __launch_bounds__(256) void k_frontier_collect(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
+                                                          const uint32_t* __restrict__ L, uint32_t* __restrict__ F,
+                                                          uint32_t* __restrict__ count) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
+    const uint64_t m = __ballot(in);
+    if (!in) return;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+    if (pos < KS_MAX) F[pos] = (uint32_t)t;
+}
+// state[0] = frontier size in (level lvl0, list in F0); out: [0] = the size of the frontier left (0 = done,
+// all levels final), [1] = its level (the grid-wide steps resume there through L == lvl).
+__global__ __launch_bounds__(KS_T) void k_kahn_small(uint32_t lvl0, uint32_t* __restrict__ state, uint32_t* __restrict__ F0,
+                                                      uint32_t* __restrict__ F1, uint32_t* __restrict__ rem,
+                                                      uint32_t* __restrict__ L, const uint32_t* __restrict__ key_off,
+                                                      const uint2* __restrict__ succ, const uint32_t* __restrict__ c_txn) {
+    __shared__ uint32_t nf;
+    __shared__ uint32_t fa[KS_MAX], fb[KS_MAX];      // frontier lists live in LDS
+    uint32_t count = state[0], lvl = lvl0;
+    for (uint32_t i = threadIdx.x; i < count && i < KS_MAX; i += KS_T) fa[i] = F0[i];
+    uint32_t* cur = fa;
+    uint32_t* nxt = fb;
+    int which = 0;
+    auto release = [&](uint32_t sx, uint32_t r) {
+        if (r == 1u) {
+            L[sx] = lvl + 1;
+            const uint32_t pos = atomicAdd(&nf, 1u);
+            if (pos < KS_MAX) nxt[pos] = sx;
+        }
+    };
+    while (count > 0 && count <= KS_MAX) {
+        if (threadIdx.x == 0) nf = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < count; i += KS_T) {
+            const uint32_t t = cur[i];
+            const uint32_t b = key_off[t], e = key_off[t + 1];
+            if (e - b <= 4) {
+                // every key's first successor: loads and atomics issued together (one dependent chain)
+                uint2 sc[4];
+                uint32_t sx[4], rr[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sc[j] = b + j < e ? succ[b + j] : make_uint2(0u, 0u);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sx[j] = sc[j].y ? c_txn[sc[j].x] : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) rr[j] = sc[j].y ? atomicSub(&rem[sx[j]], 1u) : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) if (sc[j].y) release(sx[j], rr[j]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) {
+                        const uint32_t y = c_txn[x];
+                        release(y, atomicSub(&rem[y], 1u));
+                    }
+            } else {
+                for (uint32_t p = b; p < e; ++p) {
+                    const uint2 sc = succ[p];
+                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) {
+                        const uint32_t y = c_txn[x];
+                        release(y, atomicSub(&rem[y], 1u));
+                    }
+                }
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        const uint32_t c = nf;
+        __syncthreads();
+        if (c == 0) { count = 0; break; }
+        ++lvl;
+        count = c;
+        uint32_t* tmp = cur; cur = nxt; nxt = tmp;
+        which ^= 1;
+        if (count > KS_MAX) break;       // too wide for one workgroup: the grid-wide steps continue at lvl
+    }
+    if (threadIdx.x == 0) { state[0] = count; state[1] = lvl; state[2] = (uint32_t)which; }
 }
 
 // (b) and (c) as explicit Kahn edges, one thread per txn T (count pass: per-source out-degrees and T's
@@ -735,11 +940,12 @@ struct LevelState {
     // Kahn path with (b)/(c) edges: per-source out-degree, successor offsets, write cursor, successors
     unsigned long long *xcnt = nullptr, *xoff = nullptr, *xcur = nullptr;
     uint32_t* xs = nullptr;
+    uint32_t* kfront = nullptr;          // k_kahn_small: two frontier lists of KS_MAX + state[4]
     size_t capX = 0, xs_cap = 0;
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront};
     for (void* p : ps) if (p) hipFree(p);
     s = LevelState{};
 }
@@ -1007,6 +1213,33 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
                 k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
                                                   ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0);
+                // long chains found by the build (flags[7]): rebuild every chain with the parallel kernels
+                bool long_done = false;
+                auto long_build = [&]() -> bool {
+                    hipMemsetAsync(ls.indeg, 0, n * 4, st);
+                    hipMemsetAsync(ls.succ, 0, P * 8, st);
+                    hipMemsetAsync(ls.c_pair, 0xFF, P * 4, st);
+                    hipMemsetAsync(ls.flags + 12, 0, 4, st);
+                    k_chain_rank<<<ceil_div((long)P, CR_N), CR_T, 0, st>>>(P, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval,
+                                                                           ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+                    k_chain_check<<<std::min(gP, 2048), 256, 0, st>>>(P, in.seg_start, ls.c_exec1, ls.c_pair, ls.flags + 12);
+                    uint32_t bad = 0;
+                    if (hipMemcpyAsync(&bad, ls.flags + 12, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess)
+                        return false;
+                    if (bad) {       // a far slow-path bump: the serial per-segment insertion order
+                        k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+                        k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+                    }
+                    int32_t* last_w = ls.pm_all;
+                    int32_t* next_w = ls.pair_seg;
+                    device_scan(WriteLinkOp<false>{P, in.seg_start, ls.c_meta, last_w}, P, (WriteLinkOp<false>::S*)ls.agg, st);
+                    device_scan(WriteLinkOp<true>{P, in.seg_start, ls.c_meta, next_w}, P, (WriteLinkOp<true>::S*)ls.agg, st);
+                    k_chain_links<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_pair, last_w, next_w, ls.indeg, ls.succ);
+                    hipMemsetAsync(ls.flags + 7, 0, 4, st);
+                    long_done = true;
+                    return true;
+                };
                 if (xedges) {
                     // (b)/(c) successor runs: count, offsets (one sync: total + long-chain / kinds flags), fill
                     if (ls.capX < n + 1 || !ls.xcnt) {
@@ -1015,6 +1248,16 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                         ls.capX = c;
                     }
                     const int gn1 = ceil_div((long)n, 256);
+                    // long chains first: (c) searches the executeAt-ordered chains, and the rebuild resets indeg
+                    if (hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+                        err = "exec levels: device error";
+                        return AD_ERR_DEVICE;
+                    }
+                    if (host[5]) {
+                        err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                        return AD_ERR_UNSUPPORTED;
+                    }
+                    if (host[7] && !long_build()) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
                     if (has_c) k_unmanaged_prep<<<gn1, 256, 0, st>>>(ea);
                     XEdgeArgs xa{};
                     xa.e = ea; xa.c_meta = ls.c_meta; xa.do_b = has_b ? 1 : 0; xa.do_c = has_c ? 1 : 0;
@@ -1024,17 +1267,11 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     device_scan(SumOp<unsigned long long>{ls.xcnt, ls.xoff, n}, n, (unsigned long long*)ls.agg, st);
                     unsigned long long etot = 0;
                     if (hipMemcpyAsync(&etot, ls.xoff + n, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         hipStreamSynchronize(st) != hipSuccess) {
                         err = "exec levels: device error";
                         return AD_ERR_DEVICE;
                     }
-                    if (host[5]) {
-                        err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
-                        return AD_ERR_UNSUPPORTED;
-                    }
-                    if (host[7]) fallback = true;         // a long chain: the fixpoint below
-                    else {
+                    {
                         if (ls.xs_cap < etot || !ls.xs) {
                             const size_t c = std::max<size_t>(etot + etot / 8, 1);
                             if (!grow((void**)&ls.xs, c * 4)) goto oom;
@@ -1071,11 +1308,38 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                             err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
                             return AD_ERR_UNSUPPORTED;
                         }
-                        if (host[7]) { fallback = true; break; }
+                        if (host[7] && !long_done) {      // the batch's wavefronts were gated off: rebuild, restart
+                            if (!long_build()) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
+                            hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
+                            host[7] = 0;
+                            KB = 16;
+                            continue;
+                        }
                     }
                     int k = 0;
                     while (k < KB && fh[k]) ++k;
-                    if (k == KB) { lv += KB; KB = std::min(KB_MAX, 2 * KB); continue; }   // all released more: next batch
+                    if (k == KB) {                   // all released more: next batch
+                        lv += KB;
+                        KB = std::min(KB_MAX, 2 * KB);
+                        if (!xedges) {
+                            // a deep graph: narrow wavefronts run inside one workgroup until one is wide again
+                            if (!ls.kfront && !grow((void**)&ls.kfront, (2 * KS_MAX + 4) * 4)) goto oom;
+                            uint32_t* kst = ls.kfront + 2 * KS_MAX;
+                            hipMemsetAsync(kst, 0, 16, st);
+                            k_frontier_collect<<<ceil_div((long)n, 256), 256, 0, st>>>(n, (uint32_t)lv, ls.indeg, in.lvl, ls.kfront, kst);
+                            k_kahn_small<<<1, KS_T, 0, st>>>((uint32_t)lv, kst, ls.kfront, ls.kfront + KS_MAX, ls.rem, in.lvl,
+                                                              in.key_off, ls.succ, ls.c_txn);
+                            uint32_t ks[3] = {0, 0, 0};
+                            if (hipMemcpyAsync(ks, kst, 12, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+                                err = "exec levels: device error";
+                                return AD_ERR_DEVICE;
+                            }
+                            if (ks[0] == 0) { lv = (int)ks[1] + 1; more = false; break; }
+                            if ((int)ks[1] != lv) KB = 16;     // resumed at a new wide level
+                            lv = (int)ks[1];
+                        }
+                        continue;
+                    }
                     lv += k + 1;
                     more = false;
                 }
