@@ -511,6 +511,7 @@ __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     const bool large = a.meta[t] & META_LARGE;
+    if (large) return;            // k_large_layout
     const uint32_t b = large ? a.voff[t] : a.key_off[t], e = large ? a.voff[t + 1] : a.key_off[t + 1];
     for (int vc = 0; vc < a.nvc; ++vc) {
         const uint32_t kb = a.out_key_off[vc][t];
@@ -530,6 +531,72 @@ __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
             run += c;
             a.out_k2t[vc][mb + kk] = (int32_t)run;
             ++kk;
+        }
+    }
+}
+
+// Large txns (virtual items: range-domain txns, >16-key txns), one wave per txn: per-CSR key and entry
+// totals (k_large_sums, read by OffsetsOp's load) and the layout (k_large_layout, after the CSRs are
+// allocated): the items with deps become the txn's keys in item order, the k2t header gets the running
+// entry end, and each item its last k2t slot (the fill walk emits descending).  A C4 range txn has
+// ~3*10^3 items: one lane per item instead of one thread walking them all.
+__device__ inline uint32_t wave_incl_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d);
+        if ((int)__lane_id() >= d) v += y;
+    }
+    return v;
+}
+template <int NVC>
+__global__ __launch_bounds__(256) void k_large_sums(TxnArgs a) {
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (t >= a.n || !(a.meta[t] & META_LARGE)) return;
+    const uint32_t b = a.voff[t], e = a.voff[t + 1];
+    uint32_t k[NVC], en[NVC];
+#pragma unroll
+    for (int c = 0; c < NVC; ++c) { k[c] = 0; en[c] = 0; }
+    for (uint32_t x = b + __lane_id(); x < e; x += WAVE) {
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) {
+            const uint32_t v = a.vcnt[(size_t)x * NVC + c];
+            k[c] += v > 0 ? 1u : 0u;
+            en[c] += v;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NVC; ++c) {
+        const uint32_t ks = wave_incl_sum(k[c]), es = wave_incl_sum(en[c]);
+        if (__lane_id() == WAVE - 1) { a.nk[(size_t)c * a.n + t] = ks; a.ne[(size_t)c * a.n + t] = es; }
+    }
+}
+template <int NVC>
+__global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (t >= a.n || !(a.meta[t] & META_LARGE)) return;
+    const uint32_t b = a.voff[t], e = a.voff[t + 1];
+    const uint64_t below = (1ull << __lane_id()) - 1ull;
+#pragma unroll 1
+    for (int c = 0; c < NVC; ++c) {
+        const uint32_t kb = a.out_key_off[c][t];
+        const uint32_t nk = a.out_key_off[c][t + 1] - kb;
+        if (nk == 0) continue;
+        const uint32_t mb = a.out_k2t_off[c][t];
+        uint32_t run = nk, kk = 0;
+        for (uint32_t x0 = b; x0 < e; x0 += WAVE) {
+            const uint32_t x = x0 + __lane_id();
+            const uint32_t v = x < e ? a.vcnt[(size_t)x * NVC + c] : 0u;
+            const uint32_t incl = wave_incl_sum(v);
+            const uint64_t nz = __ballot(v > 0);
+            if (v > 0) {
+                const uint32_t r = kk + (uint32_t)__popcll(nz & below);
+                const uint32_t before = run + incl - v;
+                a.out_keys[c][kb + r] = a.vi_key[x];
+                a.vdst[(size_t)x * NVC + c] = mb + before + v - 1;
+                a.out_k2t[c][mb + r] = (int32_t)(before + v);
+            }
+            run += __builtin_amdgcn_readlane(incl, WAVE - 1);
+            kk += (uint32_t)__popcll(nz);
         }
     }
 }
@@ -561,6 +628,8 @@ struct OffsetsOp {
     uint32_t* dst;                // AoS by pair: last k2t slot of the pair's run
     uint32_t* vdst;
     uint32_t* overflow;
+    const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
+    const uint32_t* lsum_e;
 
     __device__ S identity() const {
         S s;
@@ -571,8 +640,13 @@ struct OffsetsOp {
     __device__ S load(size_t t) const {
         S s = identity();
         const bool large = meta[t] & META_LARGE;
-        const uint32_t b = large ? voff[t] : key_off[t], e = large ? voff[t + 1] : key_off[t + 1];
-        const uint32_t* src = large ? vcnt : cnt;
+        if (large) {              // summed by k_large_sums (one wave per txn: range txns have ~10^3 items)
+#pragma unroll
+            for (int c = 0; c < NVC; ++c) { s.k[c] = lsum_k[(size_t)c * n + t]; s.e[c] = lsum_e[(size_t)c * n + t]; }
+            return s;
+        }
+        const uint32_t b = key_off[t], e = key_off[t + 1];
+        const uint32_t* src = cnt;
         for (uint32_t x = b; x < e; ++x) {
 #pragma unroll
             for (int c = 0; c < NVC; ++c) {
@@ -603,6 +677,7 @@ struct OffsetsOp {
         }
         if (!layout) return;
         const bool large = meta[t] & META_LARGE;
+        if (large) return;        // k_large_layout
         const uint32_t b = large ? voff[t] : key_off[t], e = large ? voff[t + 1] : key_off[t + 1];
         const uint32_t* src = large ? vcnt : cnt;
         uint32_t* d = large ? vdst : dst;

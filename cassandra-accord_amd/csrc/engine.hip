@@ -418,6 +418,7 @@ void launch_offsets(ad_handle* h, const TxnArgs& ta, uint32_t* overflow) {
     op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt; op.voff = h->voff; op.vcnt = h->vcnt;
     op.layout = 1;
     op.keys = h->keys; op.vi_key = h->vi_key; op.dst = h->dst; op.vdst = h->vdst; op.overflow = overflow;
+    op.lsum_k = h->nk; op.lsum_e = h->ne;
     for (int c = 0; c < 2 * NV; ++c) {
         op.o_key_off[c] = h->deps[c].key_off; op.o_ent_off[c] = h->deps[c].ent_off; op.o_k2t_off[c] = h->deps[c].k2t_off;
         const size_t base = S_CSR0 + 10 * (size_t)c;
@@ -492,6 +493,15 @@ int union_overflow(ad_handle* h, LdsUnionArgs la, uint32_t* ovf_count, uint2* ov
 }
 
 template <int NV>
+void launch_large_sums(const TxnArgs& ta, hipStream_t st) {
+    k_large_sums<2 * NV><<<ceil_div((long)ta.n * WAVE, 256), 256, 0, st>>>(ta);
+}
+template <int NV>
+void launch_large_layout(const TxnArgs& ta, hipStream_t st) {
+    k_large_layout<2 * NV><<<ceil_div((long)ta.n * WAVE, 256), 256, 0, st>>>(ta);
+}
+
+template <int NV>
 void launch_union(const UnionArgs& ua, hipStream_t st) {
     k_txn_union<2 * NV><<<ceil_div((long)ua.n, 256), 256, 0, st>>>(ua);
 }
@@ -553,6 +563,10 @@ int stage_deps(ad_handle* h) {
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
     uint32_t* overflow = h->totd + MAX_TOTALS - 1;       // fused-layout overflow flag (read with the totals)
+    if (n > 0 && h->V > 0) {
+        KScope ks(K_VITEMS);
+        NV_DISPATCH(nv, launch_large_sums, ta, st);
+    }
     if (n > 0) {
         HIPCHK(h, hipMemsetAsync(overflow, 0, 4, st));
         KScope ks(K_SCAN_OFFSETS, n);
@@ -603,6 +617,7 @@ int stage_deps(ad_handle* h) {
     }
     // ---- fill
     if (n > 0 && !fused_layout) { KScope ks(K_TXN_LAYOUT, P); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
+    if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); NV_DISPATCH(nv, launch_large_layout, ta, st); }
     NV_DISPATCH(nv, launch_walk, wa, true, st);
     if (Q > 0 && n > 0) NV_DISPATCH(nv, launch_range, ra, true, st);
     UnionArgs ua{};

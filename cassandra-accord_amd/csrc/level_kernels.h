@@ -331,8 +331,9 @@ struct EdgeArgs {
 
 // (c) preparation: for unmanaged T and each key of its merged KeyDeps, the last chain position (in
 // executeAt order) whose executeAt <= bnd = max executeAt of T's deps on that key below T's own.
+// One wave per txn, one lane per key of its merged KeyDeps (a C4 range txn has ~3*10^3 of them).
 __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n) return;
     const uint32_t kb = a.mk_key_off[t], ke = a.mk_key_off[t + 1];
     const bool unmanaged = !manages_execution(a.meta[t]);
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
     const uint32_t mb = a.mk_k2t_off[t];
     const uint32_t tb = a.mk_ent_off[t];
     const uint64_t my = a.ex1[t];
-    for (uint32_t ki = 0; ki < nk; ++ki) {
+    for (uint32_t ki = __lane_id(); ki < nk; ki += WAVE) {
         int32_t pos = -1;
         if (unmanaged) {
             const uint32_t from = mb + (ki == 0 ? nk : (uint32_t)a.mk_k2t[mb + ki - 1]);
@@ -1258,7 +1259,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                         return AD_ERR_UNSUPPORTED;
                     }
                     if (host[7] && !long_build()) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
-                    if (has_c) k_unmanaged_prep<<<gn1, 256, 0, st>>>(ea);
+                    if (has_c) k_unmanaged_prep<<<ceil_div((long)n * WAVE, 256), 256, 0, st>>>(ea);
                     XEdgeArgs xa{};
                     xa.e = ea; xa.c_meta = ls.c_meta; xa.do_b = has_b ? 1 : 0; xa.do_c = has_c ? 1 : 0;
                     xa.indeg = ls.indeg; xa.outcnt = ls.xcnt; xa.cur = ls.xcur;
@@ -1370,7 +1371,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             KScope ks(K_CHAIN_PREP);
             k_pair_seg<<<gP, 256, 0, st>>>(P, ls.c_pair, ls.c_meta, in.seg_start, ls.seg_len, ls.pair_seg, has_c ? 0 : 1);
             device_scan(SegListOp{in.seg_start, ls.seg_len, ls.heads, ls.long_pos, ls.flags, P}, P, (SegListOp::S*)ls.agg, st);
-            if (has_c) k_unmanaged_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(ea);
+            if (has_c) k_unmanaged_prep<<<ceil_div((long)n * WAVE, 256), 256, 0, st>>>(ea);
         }
         hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }

@@ -180,13 +180,13 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Heavy txns: one 256-thread workgroup per txn (grid-stride over the heavy list).  The txn's TxnId lists
+// Heavy txns: one 64-lane workgroup (a wave) per txn (grid-stride over the heavy list).  The txn's TxnId lists
 // are cut into chunks at every MCH-th TxnId of the reply holding the most, its key lists likewise by keys;
 // each chunk is a value interval, so the R-way merge of one chunk (the same loops as k_merge) is
 // independent of the others.  Thread j takes a contiguous run of chunks; a block scan of the per-thread
 // totals gives each thread its output offsets.  Write pass: TxnIds first (a barrier), then keys and
 // per-key lists, whose TxnIds are remapped by binary search in the txn's merged TxnId list.
-constexpr int MCH = 32, MH_T = 256, MH_GRID = 1024;
+constexpr int MCH = 32, MH_T = 64, MH_GRID = 8192;
 
 __device__ inline uint32_t lb_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {   // first a[x] >= v
     while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (a[m] < v) lo = m + 1; else hi = m; }
