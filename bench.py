@@ -135,7 +135,7 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol (profiles
     "k_deps_walk<fill>": "ad::k_deps_walk<3, true>", "k_deps_walk<count>": "ad::k_deps_walk<3, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
     "k_gather_entries": "ad::k_gather_entries", "k_txn_layout": "ad::k_txn_layout",
-    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union",
+    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<6>",
 }
 
 

@@ -604,6 +604,10 @@ __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
 // Per-txn (keys, entries) of every (view, class) key CSR, counted from the pairs' AoS counts inside the
 // scan's load, and the exclusive offsets key_off / ent_off / k2t_off of all of them in one scan (replaces
 // 2NV separate count reductions and 3 * 2NV scans).
+// Deps.merge sends txns whose replies total more than this many TxnIds + keys to k_merge_heavy
+// (merge_kernels.h: MERGE_HEAVY); the offsets scan flags batches that may have any, so batches without
+// (C2) skip the heavy launches.  Entries bound TxnIds from above, so the hint is conservative.
+constexpr uint32_t MERGE_HEAVY_HINT = 256;
 template <int NVC>
 struct OffsetsOp {
     struct S { uint32_t k[NVC], e[NVC]; };
@@ -630,6 +634,7 @@ struct OffsetsOp {
     uint32_t* overflow;
     const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
     const uint32_t* lsum_e;
+    uint32_t* heavy;              // set when some txn's CSRs total more than MERGE_HEAVY keys + entries
 
     __device__ S identity() const {
         S s;
@@ -664,6 +669,10 @@ struct OffsetsOp {
         return r;
     }
     __device__ void store(size_t t, const S& ex, const S& inc, const S& el) const {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) w += el.k[c] + el.e[c];
+        if (w > MERGE_HEAVY_HINT && *(volatile uint32_t*)heavy == 0u) *(volatile uint32_t*)heavy = 1u;
 #pragma unroll
         for (int c = 0; c < NVC; ++c) {
             o_key_off[c][t] = ex.k[c];

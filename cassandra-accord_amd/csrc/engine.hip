@@ -115,6 +115,7 @@ struct ad_handle {
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
+    bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -418,7 +419,7 @@ void launch_offsets(ad_handle* h, const TxnArgs& ta, uint32_t* overflow) {
     op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt; op.voff = h->voff; op.vcnt = h->vcnt;
     op.layout = 1;
     op.keys = h->keys; op.vi_key = h->vi_key; op.dst = h->dst; op.vdst = h->vdst; op.overflow = overflow;
-    op.lsum_k = h->nk; op.lsum_e = h->ne;
+    op.lsum_k = h->nk; op.lsum_e = h->ne; op.heavy = overflow - 1;
     for (int c = 0; c < 2 * NV; ++c) {
         op.o_key_off[c] = h->deps[c].key_off; op.o_ent_off[c] = h->deps[c].ent_off; op.o_k2t_off[c] = h->deps[c].k2t_off;
         const size_t base = S_CSR0 + 10 * (size_t)c;
@@ -568,7 +569,7 @@ int stage_deps(ad_handle* h) {
         NV_DISPATCH(nv, launch_large_sums, ta, st);
     }
     if (n > 0) {
-        HIPCHK(h, hipMemsetAsync(overflow, 0, 4, st));
+        HIPCHK(h, hipMemsetAsync(overflow - 1, 0, 8, st));     // [heavy-merge hint, layout overflow]
         KScope ks(K_SCAN_OFFSETS, n);
         NV_DISPATCH(nv, launch_offsets, h, ta, overflow);
     } else {
@@ -595,10 +596,12 @@ int stage_deps(ad_handle* h) {
     }
     const int ncol = tt.count;
     tt.src[tt.count++] = overflow;
+    tt.src[tt.count++] = overflow - 1;
     std::vector<uint32_t> got(tt.count, 0);
     CK(read_totals_params(h, tt, got.data()));
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
     const bool fused_layout = n > 0 && got[ncol] == 0;
+    h->merge_heavy = n == 0 || got[ncol + 1] != 0 || h->n_large > 0 || Q > 0;
     CK(check_params(h));
     h->deps_entries = 0;
     for (int c = 0; c < ncsr; ++c) {
@@ -713,7 +716,7 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
             a.row[v] = rows ? rows[k][v] : nullptr;
         }
         a.mk = mk + (size_t)k * n; a.me = me + (size_t)k * n; a.mu = mu + (size_t)k * n;
-        a.hlist = hl + (size_t)k * n; a.hcount = hc + k;
+        if (h->merge_heavy) { a.hlist = hl + (size_t)k * n; a.hcount = hc + k; }
         if (n > 0) merge_launch(a, np, false, kw[k], st);
     }
     if (n > 0) {
@@ -1132,6 +1135,7 @@ int ad_fetch_rows(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t h
 }
 
 int ad_merge_host(ad_handle* h, const ad_csr_in* parts, uint32_t r, ad_csr_sizes* sizes) {
+    if (h) h->merge_heavy = true;      // caller-supplied replies: any shape
     if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
@@ -1565,6 +1569,7 @@ int ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world] */) {
 // Home txns: merge every store's fragment per view (k_merge over sources with row indirection), then
 // Deps.merge across the replica views.  sizes[view * 3 + cls] (view == replicas: merged).
 int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
+    if (h) h->merge_heavy = true;      // fragments from every store: any shape
     if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (h->src_csr.empty()) return set_err(h, AD_ERR_STATE, "ad_shard_merge: exchange the blobs first");

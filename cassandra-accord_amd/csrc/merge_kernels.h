@@ -40,7 +40,7 @@ struct MergeArgs {
 
 // A txn whose replies hold more than MERGE_HEAVY TxnIds + keys in total is merged by one workgroup
 // (k_merge_heavy) instead of one thread: its serial merge would be thousands of dependent loads long.
-constexpr uint32_t MERGE_HEAVY = 256;
+constexpr uint32_t MERGE_HEAVY = MERGE_HEAVY_HINT;
 
 // KW = u64 words per key: 1 for KeyDeps keys, 2 for RangeDeps (start, end) compared as Range::compare.
 template <int KW>
