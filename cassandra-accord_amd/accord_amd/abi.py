@@ -14,6 +14,7 @@ AD_ERR_UNSORTED = -3
 AD_ERR_UNSUPPORTED = -4
 AD_ERR_DEVICE = -5
 AD_ERR_NOMEM = -6
+AD_RANK_NONE = 0xFFFFFFFF   # ad_max_conflicts: Timestamp.NONE
 
 # Txn.Kind ordinals (primitives/Txn.java:53-113)
 KIND_READ, KIND_WRITE, KIND_EPHEMERAL_READ, KIND_SYNC_POINT, KIND_EXCLUSIVE_SYNC_POINT, KIND_LOCAL_ONLY = range(6)

@@ -6,6 +6,7 @@ This is a thin ctypes layer mirroring the reference operations a host drives on 
   (messages/PreAccept.java:245-267)
 * ``merge()``           — Deps.merge of the replica replies (primitives/Deps.java:281-286)
 * ``exec_levels()``     — execution order (local/Commands.java:617-821, CommandsForKey.notifyManaged)
+* ``max_conflicts()``   — CommandStore.preaccept's witnessedAt proposal per view (local/CommandStore.java:322-347)
 
 There is no CPU fallback: if the HIP library is missing or no GPU is visible the constructor raises.
 """
@@ -58,6 +59,7 @@ def lib():
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ad_run_pipeline.argtypes = [vp]
+        L.ad_max_conflicts.argtypes = [vp, vp, vp]
         L.ad_fetch_levels.argtypes = [vp, vp, vp]
         L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
         L.ad_set_trace.argtypes = [vp, C.c_uint64]
@@ -74,7 +76,7 @@ def lib():
 
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_alltoall", "ad_shard_merge",
@@ -183,6 +185,17 @@ class DepsEngine:
                                          order.ctypes.data_as(C.POINTER(C.c_uint32)) if want_order else None,
                                          C.byref(it)), "ad_exec_levels")
         return lv[:self.n], (order[:self.n] if want_order else None), it.value
+
+    def max_conflicts(self):
+        """CommandStore.preaccept per replica view (local/CommandStore.java:322-347), after preaccept_deps():
+        (max_rank [R, n] uint32 — rank of the txn whose executeAt is maxConflicts.get(keys), AD_RANK_NONE for
+        Timestamp.NONE; fast [R, n] uint8 — 1 when the replica answers witnessedAt = TxnId).  A slow-path
+        replica answers time.uniqueNow(that executeAt), which the host clock supplies."""
+        R, n = self.replicas, self.n
+        rank = np.zeros((R, max(n, 1)), np.uint32)
+        fast = np.zeros((R, max(n, 1)), np.uint8)
+        self._check(lib().ad_max_conflicts(self.h, rank.ctypes.data, fast.ctypes.data), "ad_max_conflicts")
+        return rank[:, :n], fast[:, :n]
 
     def run_pipeline(self):
         self._check(lib().ad_run_pipeline(self.h), "ad_run_pipeline")

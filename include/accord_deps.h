@@ -193,6 +193,19 @@ int  ad_merge_host(ad_handle* h, const ad_csr_in* parts, uint32_t r, ad_csr_size
  * order_out = txn ranks sorted by (level, executeAt).  Either pointer may be NULL. */
 int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint32_t* iterations_out);
 
+/* Stage 1b — the replica's witnessedAt proposal per view, after ad_preaccept_deps on the same batch:
+ *   CommandStore.preaccept            local/CommandStore.java:322-347   (maxConflicts.get(keys), fast-path test :342-344)
+ *   MaxConflicts.get / update         local/MaxConflicts.java:46-59
+ *   CommandStore.updateMaxConflicts   local/CommandStore.java:282-291, SafeCommandStore.java:210-222 (globally visible kinds)
+ * max_rank[v*n + i] = the batch rank of the txn whose executeAt is maxConflicts.get(keys of i) in view v — the greatest
+ * executeAt (Timestamp.compareTo; ties to the larger rank) over the txns j < i sharing a key with i that the view has
+ * stored (CommandsForKey entries not TRANSITIVELY_KNOWN/INVALID; in-flight j unless the view dropped it) — or
+ * AD_RANK_NONE (Timestamp.NONE).  fast[v*n + i] = 1 when TxnId_i >= that timestamp (or NONE): the replica answers
+ * witnessedAt = TxnId (fast path), else time.uniqueNow(maxConflict), which the host clock supplies.
+ * Key-domain batches (AD_ERR_UNSUPPORTED when the batch has range txns).  Either pointer may be NULL. */
+#define AD_RANK_NONE 0xFFFFFFFFu
+int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8_t* fast /* [replicas*n] */);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Device-resident pipeline (benchmark / service loop): stage 1 + 2 + 3 with no host copies of */
 /* outputs.  Kernel timing: HIP events on the handle's stream.                                 */

@@ -440,6 +440,29 @@ struct Oracle {
         d.key = kb.build(); d.direct = db.build(); d.range = rb.build();
         return d;
     }
+
+    // CommandStore.preaccept's maxConflicts.get(keys) (local/CommandStore.java:342) as replica view `view`
+    // holds it when txn i arrives: MaxConflicts.update (local/MaxConflicts.java:56-59) has folded in the
+    // executeAt of every globally visible txn the store holds on each key (CommandStore.updateMaxConflicts
+    // :282-291, SafeCommandStore.updateMaxConflicts :210-222) — the CFK byId entries j < i that are not
+    // TRANSITIVELY_KNOWN/INVALID, in-flight ones unless the view dropped them.  Returns the rank of the
+    // greatest executeAt (Timestamp::max, ties to the larger rank) or UINT32_MAX for Timestamp.NONE.
+    uint32_t max_conflict(uint32_t i, uint32_t view) {
+        uint32_t best = UINT32_MAX;
+        for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
+            Cfk* c = find_cfk(B.keys[p]);
+            if (!c) continue;
+            for (uint32_t j : c->byId) {
+                if (j >= i) break;
+                int st = seen_status(i, j);
+                if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID) continue;
+                if (dropped(view, i, j)) continue;
+                int cmp = best == UINT32_MAX ? 1 : ts_cmp(B.ex[j], B.ex[best]);
+                if (cmp > 0 || (cmp == 0 && j > best)) best = j;
+            }
+        }
+        return best;
+    }
 };
 
 /* Flattened batched CSR (ad_csr_out layout, compacted txn lists). */
@@ -679,6 +702,30 @@ oracle_result* oracle_run(const ad_batch* b, const ad_config* c, uint32_t flags,
 }
 
 const char* oracle_error(const oracle_result* r) { return r->error.empty() ? nullptr : r->error.c_str(); }
+
+/* witnessedAt proposal per view (CommandStore.preaccept, local/CommandStore.java:322-347): max_rank[v*n+i] =
+ * Oracle::max_conflict, fast[v*n+i] = TxnId_i >= that executeAt (or none) — the fast-path test :343.
+ * Key-domain batches only (returns -4 = AD_ERR_UNSUPPORTED with range txns), -1 on invalid input. */
+int oracle_max_conflicts(const ad_batch* b, const ad_config* c, uint32_t* max_rank, uint8_t* fast) {
+    try {
+        Batch B(b);
+        if (B.range_off[B.n] > 0) return AD_ERR_UNSUPPORTED;
+        Config cfg;
+        cfg.window = c->window; cfg.replicas = c->replicas ? c->replicas : 1; cfg.seed = c->seed;
+        cfg.drop_thresh = ad_drop_threshold(c->drop_p);
+        Oracle o(B, cfg, false);
+        const uint32_t n = (uint32_t)B.n;
+        for (uint32_t v = 0; v < cfg.replicas; ++v)
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t m = o.max_conflict(i, v);
+                max_rank[(size_t)v * n + i] = m;
+                fast[(size_t)v * n + i] = (m == UINT32_MAX || ts_cmp(B.tx[i], B.ex[m]) >= 0) ? 1 : 0;
+            }
+        return AD_OK;
+    } catch (const std::exception&) {
+        return AD_ERR_ARGUMENT;
+    }
+}
 
 static const Flat* pick(const oracle_result* r, int stage, uint32_t view, uint32_t cls) {
     if (cls >= AD_NUM_CLASSES) return nullptr;

@@ -37,6 +37,8 @@ def lib():
         L.oracle_levels.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
         L.oracle_free.argtypes = [C.c_void_p]
+        L.oracle_max_conflicts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.POINTER(C.c_uint32),
+                                           C.POINTER(C.c_uint8)]
         L.oracle_build.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_size_t,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]
@@ -99,6 +101,19 @@ class OracleResult:
         e = (C.c_uint64 * 2)()
         lib().oracle_stats(self.h, t, e)
         return {"t_deps": t[0], "t_merge": t[1], "t_levels": t[2], "deps_entries": e[0], "merged_entries": e[1]}
+
+
+def max_conflicts(batch, cfg):
+    """CommandStore.preaccept's maxConflicts.get(keys) per view (oracle.cpp Oracle::max_conflict) ->
+    (max_rank [R, n] uint32, AD_RANK_NONE = 0xFFFFFFFF; fast [R, n] uint8: TxnId >= that executeAt)."""
+    b = abi.make_batch(batch)
+    n, R = batch["n"], cfg.replicas
+    rank = np.zeros((R, max(n, 1)), np.uint32)
+    fast = np.zeros((R, max(n, 1)), np.uint8)
+    rc = lib().oracle_max_conflicts(C.byref(b), C.byref(cfg), _p(rank, C.c_uint32), _p(fast, C.c_uint8))
+    if rc != abi.AD_OK:
+        raise ValueError("oracle_max_conflicts rc=%d" % rc)
+    return rank[:, :n].copy(), fast[:, :n].copy()
 
 
 def build_relation(keys, vals):

@@ -1,0 +1,115 @@
+"""GPU parity of ad_max_conflicts (CommandStore.preaccept's witnessedAt proposal, local/CommandStore.java:322-347)
+against the oracle (oracle.cpp Oracle::max_conflict), bit-exact: per view and txn the rank holding
+maxConflicts.get(keys) and the fast-path flag.  Full sizes: a txn's answer depends only on txns with a smaller
+TxnId, so the oracle on a prefix must equal the GPU's first rows of the full batch.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from accord_amd import abi, engine, workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _slice(b, m):
+    """The first m txns of a key batch (TxnId order = arrival order)."""
+    ko = b["key_off"][:m + 1]
+    out = {"n": m, "key_off": ko.copy(), "keys": b["keys"][:int(ko[-1])].copy(),
+           "range_off": None, "range_start": None, "range_end": None}
+    for f in ("txn_msb", "txn_lsb", "txn_node", "exec_msb", "exec_lsb", "exec_node", "status"):
+        out[f] = b[f][:m].copy()
+    return out
+
+
+def check(engine_factory, b, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, prefix=None, eng=None):
+    cfg = abi.make_config(window, replicas, drop_p, seed)
+    if eng is None:
+        eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
+    eng.load(b)
+    eng.preaccept_deps()
+    rank, fast = eng.max_conflicts()
+    m = b["n"] if prefix is None else min(prefix, b["n"])
+    want_rank, want_fast = O.max_conflicts(_slice(b, m) if m < b["n"] else b, cfg)
+    bad = np.nonzero((rank[:, :m] != want_rank).any(axis=0))[0]
+    assert len(bad) == 0, "max_rank differs at txns %s: gpu %s cpu %s" % (bad[:8], rank[:, bad[:4]], want_rank[:, bad[:4]])
+    assert np.array_equal(fast[:, :m], want_fast)
+    return eng, rank, fast
+
+
+@pytest.mark.parametrize("name,n", [("C2", 20000), ("C3", 20000), ("C2", 200000)])
+def test_configs(engine_factory, name, n):
+    _, rank, fast = check(engine_factory, workload.config(name, n=n))
+    assert (rank != abi.AD_RANK_NONE).any()
+    if name == "C3":
+        assert fast.min() == 0          # Zipf hot keys: slow-path bumps above later TxnIds (594 rows at 20k)
+
+
+@pytest.mark.parametrize("window,replicas,drop_p", [(0, 1, 0.0), (32, 1, 0.0), (32, 5, 0.3), (200, 8, 0.5)])
+def test_window_views_drops(engine_factory, window, replicas, drop_p):
+    b = workload.generate(30000, keys_per_txn=4, keyspace=20000, slow_frac=0.3, bump_max=200, seed=window + replicas)
+    check(engine_factory, b, window=window, replicas=replicas, drop_p=drop_p)
+
+
+def test_kinds_statuses_and_wide_txns(engine_factory):
+    rng = np.random.default_rng(5)
+    n = 20000
+    kinds = rng.integers(0, 5, size=n)                  # Read, Write, EphemeralRead, SyncPoint, ExclusiveSyncPoint
+    status = rng.integers(0, 8, size=n).astype(np.uint8)  # every InternalStatus
+    b = workload.generate(n, keys_per_txn=20, keyspace=30000, kinds=kinds, status=status, slow_frac=0.4,
+                          bump_max=100, seed=6)             # 20 keys > KMAX: the large-txn pairs as well
+    check(engine_factory, b)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 4097])
+def test_edge_sizes(engine_factory, n):
+    check(engine_factory, workload.generate(n, keys_per_txn=2, keyspace=5, seed=n))
+
+
+def test_after_merge_and_levels(engine_factory):
+    # the sorted entries the kernels read survive Deps.merge and the level stage
+    b = workload.config("C3", n=20000, seed=11)
+    eng = engine_factory()
+    eng.load(b)
+    eng.preaccept_deps()
+    r0, f0 = eng.max_conflicts()
+    r0, f0 = r0.copy(), f0.copy()
+    eng.merge()
+    eng.exec_levels()
+    r1, f1 = eng.max_conflicts()
+    assert np.array_equal(r0, r1) and np.array_equal(f0, f1)
+
+
+def test_rejects_range_batches_and_call_order(engine_factory):
+    eng = engine_factory()
+    b = workload.generate(2000, range_frac=0.1, seed=3)
+    eng.load(b)
+    with pytest.raises(engine.IllegalStateException):
+        eng.max_conflicts()                            # before ad_preaccept_deps
+    eng.preaccept_deps()
+    with pytest.raises(engine.AccordDepsError) as e:
+        eng.max_conflicts()
+    assert e.value.rc == abi.AD_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_full_size_prefix(engine_factory, name):
+    b = workload.config(name)                          # 1,048,576 txns
+    _, rank, fast = check(engine_factory, b, prefix=60000)
+    # whole batch: the named txn precedes the query; fast == TxnId >= its executeAt
+    n = b["n"]
+    has = rank != abi.AD_RANK_NONE
+    for v in range(rank.shape[0]):
+        i = np.nonzero(has[v])[0]
+        j = rank[v, i].astype(np.int64)
+        assert (j < i).all()
+        # Timestamp.compareTo (Timestamp.java:208-217): msb unsigned, lowHlc, identity flags, node signed
+        fa = (b["txn_msb"][i], b["txn_lsb"][i] >> 16, b["txn_lsb"][i] & 0x1E, b["txn_node"][i])
+        fb = (b["exec_msb"][j], b["exec_lsb"][j] >> 16, b["exec_lsb"][j] & 0x1E, b["exec_node"][j])
+        gt, eq = np.zeros(len(i), bool), np.ones(len(i), bool)
+        for x, y in zip(fa, fb):
+            gt |= eq & (x > y)
+            eq &= x == y
+        assert np.array_equal(fast[v, i].astype(bool), gt | eq)
+        assert fast[v, ~has[v]].all()
+    assert n == 1 << 20
