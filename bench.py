@@ -37,13 +37,16 @@ WINDOW, REPLICAS, DROP_P = 32, 3, 0.1
 KEYSPACE = 10_000_000
 
 
-def alg_bytes(kernel, calls, units, n, P, R, st):
+def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
     """Algorithmic HBM bytes moved by all traced launches of `kernel` (DESIGN.md §3 lists the per-unit
     figures): the minimum bytes the kernel must read + write for the elements it processed.  `units` is
     the sum of elements over the launches (pairs, txns or sort items, recorded per launch by the engine's
     tracer); n txns, P (txn,key) pairs, R replica views; st = ad_last_times() counts of the step.
     Kernels whose work is data dependent in a way the tracer does not count (the level worklist walk,
-    composite scans) return None and are not roofline candidates."""
+    composite scans) return None and are not roofline candidates.  With large txns in the batch (range txns,
+    C4) the run's entry count D also holds the entries the virtual-item walks and the LDS unions produce,
+    which k_txn_union / k_deps_walk<fill> never touch: their D-based models would overcount, so they are not
+    candidates there."""
     D = st["deps_entries"]           # emitted dependency entries over all views/classes
     W = st["walk_items"]             # entries the deps walks visit
     per = {
@@ -61,7 +64,16 @@ def alg_bytes(kernel, calls, units, n, P, R, st):
         # per txn: 3 offsets x 2R CSRs, the per-key lists in, unique TxnIds + remapped lists out
         "k_txn_union": calls * (n * (12 * 2 * R + 4 * 2 * R) + 12 * D),
     }
+    if large and kernel in ("k_txn_union", "k_deps_walk<fill>"):
+        return None
     return per.get(kernel)
+
+
+def max_conflicts_alg_bytes(n, P, R):
+    """ad_max_conflicts: scan 17 B/pair read + 12 B/pair write; per-entry walk 24 B/pair read
+    (seg_start, e_txn, sval, prefix value) + 12R B/pair write; per-txn fold 12R B/pair read + 12 B/txn read
+    (key_off, tx_ts) + 5R B/txn write.  In-window entry reads are not counted (a lower bound)."""
+    return P * (29 + 24 + 24 * R) + n * (12 + 5 * R)
 
 
 def pipeline_alg_bytes(n, P, R, st, Q=0):
@@ -105,7 +117,7 @@ def cpu_baseline(sample_n, cfg="C2"):
                       % (name, sample_n, workload.SEEDS[name], REPLICAS, T, t, s["t_deps"], s["t_merge"], s["t_levels"], t1)}
 
 
-def trace_roofline(eng, run_step, n, P):
+def trace_roofline(eng, run_step, n, P, large=False):
     """Untimed all-kernels breakdown pass -> the dominant kernel among those with an algorithmic byte
     model.  Returns (dominant kernel, breakdown, last times)."""
     ids = engine.kernel_ids()
@@ -114,18 +126,19 @@ def trace_roofline(eng, run_step, n, P):
     run_step()
     brk = eng.kernel_stats()
     st = eng.last_times()
-    cands = [k for k in brk if alg_bytes(k, brk[k][0], brk[k][2], n, P, REPLICAS, st) is not None]
+    cands = [k for k in brk if alg_bytes(k, brk[k][0], brk[k][2], n, P, REPLICAS, st, large) is not None]
     dom = max(cands, key=lambda k: brk[k][1])
     return dom, brk, st
 
 
-def roofline_of(eng, dom, n, P, st):
+def roofline_of(eng, dom, n, P, st, large=False, pmc=True):
     """achieved = the dominant kernel's algorithmic bytes over its launches in the timed region / its summed
     HIP-event time (events on the engine stream, bracketing only this kernel)."""
     calls, ms, units = eng.kernel_stats()[dom]
-    ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st)
+    ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st, large)
     achieved = ab / (ms * 1e-3) / 1e9
-    traffic, src = pmc_traffic(dom)
+    # the committed PMC passes (profiles/collect.sh) run the default C2 bench: other configs report no traffic
+    traffic, src = pmc_traffic(dom) if pmc else (None, None)
     return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "alg_bytes_per_launch": ab / calls, "avg_launch_ms": ms / calls, "launches": calls}
@@ -244,7 +257,7 @@ def main_sharded(args, rank, world, local, dist):
     t = __import__("torch").tensor([t1 - t0], dtype=__import__("torch").float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    roof = roofline_of(store.eng, dom, n_loc, P_loc, store.eng.last_times())
+    roof = roofline_of(store.eng, dom, n_loc, P_loc, store.eng.last_times(), pmc=False)
     store.eng.set_trace(0)
     out = {
         "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
@@ -305,7 +318,7 @@ def main():
 
     for _ in range(max(args.warmup, 1)):
         eng.run_pipeline()
-    dom, brk, st = trace_roofline(eng, eng.run_pipeline, n, P)
+    dom, brk, st = trace_roofline(eng, eng.run_pipeline, n, P, large=Q > 0)
     if args.breakdown:
         print_breakdown(brk, st)
 
@@ -318,7 +331,20 @@ def main():
     t1 = time.perf_counter()
     dt = t1 - t0
     st = eng.last_times()
-    roof = roofline_of(eng, dom, n, P, st)
+    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc=cfgname == "C2")
+    mc = None
+    if Q == 0:
+        # side measurement, outside the timed region: the witnessedAt proposal (ad_max_conflicts) on the same
+        # resident batch, its device work (scan + walk + fold) event-timed on the engine stream
+        eng.set_trace(1 << engine.kernel_ids()["max_conflicts"])
+        eng.reset_kernel_stats()
+        for _ in range(3):
+            eng.max_conflicts()
+        calls, ms, _units = eng.kernel_stats()["max_conflicts"]
+        ab = max_conflicts_alg_bytes(n, P, REPLICAS)
+        gbs = ab / (ms / calls) / 1e6
+        mc = {"bound": "hbm", "avg_ms": ms / calls, "launches": calls, "alg_bytes": ab, "achieved_GBps": gbs,
+              "frac": gbs / HBM_PEAK_GBS}
     eng.set_trace(0)
     ms_per_step = dt * 1e3 / args.steps
     value = n * args.steps / dt
@@ -343,6 +369,7 @@ def main():
                      "stage_ms": {k: st[k] for k in ("prepare", "sort", "deps", "merge", "levels", "total")},
                      "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
                      "level_iterations": st["level_iterations"]},
+        "max_conflicts": mc,
         "cpu_baseline": None,
     }
     sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 18)

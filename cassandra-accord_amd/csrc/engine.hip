@@ -1113,16 +1113,20 @@ int ad_max_conflicts(ad_handle* h, uint32_t* max_rank, uint8_t* fast) {
     CK(dalloc(h, S_MCE, &pe, std::max<size_t>(P * nv, 1))); CK(dalloc(h, S_MCR, &pr, std::max<size_t>(P * nv, 1)));
     CK(dalloc(h, S_MCRANK, &rank, n * nv)); CK(dalloc(h, S_MCFAST, &fst, n * nv));
     a.pm_e = pm_e; a.pm_r = pm_r; a.pe = pe; a.pr = pr; a.max_rank = rank; a.fast = fst;
-    if (P > 0) {
-        CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<MaxConflictOp>(P))));
-        MaxConflictOp op{h->seg_start, h->e_meta, h->e_exec1, h->e_txn, pm_e, pm_r};
-        device_scan(op, P, (MaxConflictOp::S*)h->scratch, st);
+    if (P > 0) CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<MaxConflictOp>(P))));
+    {
+        KScope ks(K_MAX_CONFLICTS, P);      // scan + per-entry walk + per-txn fold
+        if (P > 0) {
+            MaxConflictOp op{h->seg_start, h->e_meta, h->e_exec1, h->e_txn, pm_e, pm_r};
+            device_scan(op, P, (MaxConflictOp::S*)h->scratch, st);
+        }
+        NV_DISPATCH(nv, launch_mc, a, st);
     }
-    NV_DISPATCH(nv, launch_mc, a, st);
     HIPCHK(h, hipGetLastError());
     if (max_rank) HIPCHK(h, hipMemcpyAsync(max_rank, rank, n * nv * 4, hipMemcpyDeviceToHost, st));
     if (fast) HIPCHK(h, hipMemcpyAsync(fast, fst, n * nv, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
+    h->tracer.resolve();
     return AD_OK;
 }
 
