@@ -71,6 +71,36 @@ def home_stores(batch, bounds):
     return np.clip(hs, 0, len(bounds) - 2).astype(np.uint8)
 
 
+def reduce_witnessed(batch, parts):
+    """PreAccept.reduce of the stores' witnessedAt proposals (messages/PreAccept.java:141-156: witnessedAt =
+    Timestamp.mergeMax, Timestamp.java:273-279) for the global batch: parts = [(gid, max_rank, fast)] per
+    store (ShardStore.max_conflicts).  Per view and global txn: the rank of the greatest executeAt over the
+    stores (Timestamp.compareTo, ties to the larger rank, as each store breaks them) and the fast-path flag
+    (every store answered TxnId).  A host-side fold of n x R integers, like the coordinator's fold over
+    replica replies; the per-store work runs on the GPU."""
+    n = batch["n"]
+    R = parts[0][1].shape[0] if parts else 1
+    j = np.arange(n, dtype=np.int64)
+    # strict total order of (executeAt, rank): msb unsigned, lowHlc, identity flags, node signed, then rank
+    order = np.lexsort((j, batch["exec_node"].astype(np.int64), batch["exec_lsb"] & np.uint64(0x1E),
+                        batch["exec_lsb"] >> np.uint64(16), batch["exec_msb"]))
+    pos = np.empty(n, np.int64)
+    pos[order] = j
+    best = np.full((R, n), -1, np.int64)
+    fast = np.ones((R, n), np.uint8)
+    for gid, rank, f in parts:
+        gid = np.asarray(gid, np.int64)
+        has = rank != abi.AD_RANK_NONE
+        p = np.where(has, pos[np.where(has, rank, 0).astype(np.int64)], -1)
+        for v in range(R):
+            best[v, gid] = np.maximum(best[v, gid], p[v])
+            fast[v, gid] &= f[v]
+    out = np.full((R, n), abi.AD_RANK_NONE, np.uint32)
+    has = best >= 0
+    out[has] = order[best[has]].astype(np.uint32)
+    return out, fast
+
+
 def _u32p(a):
     return a.ctypes.data_as(C.POINTER(C.c_uint32))
 
@@ -119,6 +149,11 @@ class ShardStore:
 
     def preaccept(self):
         self._check(self.L.ad_preaccept_deps(self.eng.h, None), "ad_preaccept_deps")
+
+    def max_conflicts(self):
+        """This store's witnessedAt proposal per view for its local rows (ad_max_conflicts after the deps
+        stage): (max_rank [R, n_local] as global ranks, fast [R, n_local])."""
+        return self.eng.max_conflicts()
 
     def export(self):
         """Per-destination blobs on the device; returns their byte sizes (np.uint64[world])."""

@@ -18,10 +18,8 @@
 
 namespace ad {
 
-struct McVal {
-    uint64_t e;      // executeAt + 1 (packed ts64), 0 = Timestamp.NONE
-    uint32_t r;      // batch rank of the txn holding it (ties: the larger rank)
-};
+// (executeAt+1, rank) pairs: executeAt+1 = packed ts64 + 1 (0 = Timestamp.NONE), rank = batch row of the txn
+// holding it; ordered lexicographically, so equal executeAts go to the larger rank
 __device__ inline bool mc_less(uint64_t ae, uint32_t ar, uint64_t be, uint32_t br) {
     return ae < be || (ae == be && ar < br);
 }
@@ -134,7 +132,8 @@ __global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
     const uint64_t t1 = a.tx_ts[t] + 1;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        a.max_rank[(size_t)v * a.n + t] = be[v] ? br[v] : AD_RANK_NONE;
+        // sharded stores answer in global arrival ranks (ascending with local rows: the tie rule is kept)
+        a.max_rank[(size_t)v * a.n + t] = be[v] ? (a.gid ? a.gid[br[v]] : br[v]) : AD_RANK_NONE;
         a.fast[(size_t)v * a.n + t] = (be[v] == 0 || t1 >= be[v]) ? 1 : 0;   // TxnId.compareTo(max) >= 0
     }
 }

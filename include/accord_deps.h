@@ -202,7 +202,9 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
  * stored (CommandsForKey entries not TRANSITIVELY_KNOWN/INVALID; in-flight j unless the view dropped it) — or
  * AD_RANK_NONE (Timestamp.NONE).  fast[v*n + i] = 1 when TxnId_i >= that timestamp (or NONE): the replica answers
  * witnessedAt = TxnId (fast path), else time.uniqueNow(maxConflict), which the host clock supplies.
- * Key-domain batches (AD_ERR_UNSUPPORTED when the batch has range txns).  Either pointer may be NULL. */
+ * Key-domain batches (AD_ERR_UNSUPPORTED when the batch has range txns).  Either pointer may be NULL.
+ * Sharded stores (ad_shard_setup): rows are local, max_rank holds global arrival ranks; PreAccept.reduce's
+ * mergeMax across stores (messages/PreAccept.java:141-156) is then a per-txn max over the stores' answers. */
 #define AD_RANK_NONE 0xFFFFFFFFu
 int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8_t* fast /* [replicas*n] */);
 

@@ -63,3 +63,34 @@ def test_sharded_equals_unsharded(engine_factory, name, shards):
     finally:
         for st in stores:
             st.close()
+
+
+@pytest.mark.parametrize("name,shards", [("C2", 2), ("C3", 3), ("C3", 4)])
+def test_sharded_witnessed_at(engine_factory, name, shards):
+    # per-store witnessedAt proposals (ad_max_conflicts on each store's sliced batch, global ranks) folded by
+    # PreAccept.reduce's mergeMax equal the unsharded store's: MaxConflicts is a max over the txn's keys
+    w, r, p, s = 32, 3, 0.1, 0xACC0D1
+    b = workload.config(name, n=30000)
+    eng = engine_factory(window=w, replicas=r, drop_p=p, seed=s)
+    eng.load(b)
+    eng.preaccept_deps()
+    want_rank, want_fast = eng.max_conflicts()
+    bounds = sharding.even_bounds(0, 10_000_000, shards)
+    hs = sharding.home_stores(b, bounds)
+    stores, parts = [], []
+    try:
+        for k in range(shards):
+            local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+            st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
+            stores.append(st)
+            st.load(local, gid, hs[gid], b["n"], k, shards)
+            st.preaccept()
+            rank, fast = st.max_conflicts()
+            parts.append((gid, rank.copy(), fast.copy()))
+        got_rank, got_fast = sharding.reduce_witnessed(b, parts)
+        assert np.array_equal(got_rank, want_rank) and np.array_equal(got_fast, want_fast)
+        if name == "C3":
+            assert want_fast.min() == 0
+    finally:
+        for st in stores:
+            st.close()

@@ -135,3 +135,24 @@ def test_oracle_equals_independent_model():
         mr, mf = _model(b, cfg)
         assert np.array_equal(rank, mr) and np.array_equal(fast, mf)
         assert fast.min() == 0 and (rank != NONE).any()     # both outcomes exercised
+
+
+def test_reduce_witnessed_across_stores():
+    # PreAccept.reduce (messages/PreAccept.java:141-156) of per-store answers: with the snapshot model (W = 0, no
+    # drops) each store's answer depends only on its own keys, so the oracle per key-range slice, folded by
+    # sharding.reduce_witnessed, must equal the oracle on the whole batch
+    from accord_amd import sharding
+    b = workload.generate(3000, keys_per_txn=4, keyspace=400, seed=8, slow_frac=0.4, bump_max=300)
+    cfg = abi.make_config(0, 2, 0.0, 1)
+    want_rank, want_fast = O.max_conflicts(b, cfg)
+    for shards in (2, 3, 5):
+        bounds = sharding.even_bounds(0, 400, shards)
+        parts = []
+        for k in range(shards):
+            local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+            rank, fast = O.max_conflicts(local, cfg)
+            g = np.where(rank != NONE, gid[np.where(rank != NONE, rank, 0)], NONE).astype(np.uint32)
+            parts.append((gid, g, fast))
+        got_rank, got_fast = sharding.reduce_witnessed(b, parts)
+        assert np.array_equal(got_rank, want_rank) and np.array_equal(got_fast, want_fast)
+    assert want_fast.min() == 0
