@@ -70,10 +70,11 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
 
 
 def max_conflicts_alg_bytes(n, P, R):
-    """ad_max_conflicts: scan 17 B/pair read + 12 B/pair write; per-entry walk 24 B/pair read
-    (seg_start, e_txn, sval, prefix value) + 12R B/pair write; per-txn fold 12R B/pair read + 12 B/txn read
-    (key_off, tx_ts) + 5R B/txn write.  In-window entry reads are not counted (a lower bound)."""
-    return P * (29 + 24 + 24 * R) + n * (12 + 5 * R)
+    """ad_max_conflicts: scan 21 B/pair read (seg_start, meta, executeAt, txn, sval) + 16 B/pair
+    write (prefix value, inverse permutation); per-txn walk 24 B/pair read (inverse, seg_start, the entry below,
+    prefix value) + 12 B/txn read (key_off, TxnId) + 5R B/txn write.  In-window entry reads beyond the first are
+    not counted (a lower bound)."""
+    return P * (37 + 24) + n * (12 + 5 * R)
 
 
 def pipeline_alg_bytes(n, P, R, st, Q=0):

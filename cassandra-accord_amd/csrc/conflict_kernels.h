@@ -9,10 +9,11 @@
 // (category != CAT_SKIP) plus in-flight ones the view did not drop — the same entry set the deps walk
 // visits (deps_kernels.h walk_query), without the witness/elision filters.
 //
-//   MaxConflictOp scan   segmented inclusive prefix max of (executeAt+1, rank) over recorded entries
-//   k_mc_entries<NV>     one thread per sorted entry: the in-flight window walk per view, then the prefix
-//                        max of the entry just below the window; result AoS by pair [p * NV + v]
-//   k_mc_txns<NV>        one thread per txn: max over its pairs per view, fast-path test
+//   MaxConflictOp scan   segmented inclusive prefix max of (executeAt+1, rank) over recorded entries; its
+//                        store also inverts the sort permutation (pair -> sorted position)
+//   k_mc_txns<NV>        one thread per txn: per pair, the in-flight window walk per view from the pair's
+//                        sorted position, then the prefix max of the entry just below the window; max over
+//                        the txn's pairs per view, fast-path test (no per-pair intermediate in HBM)
 #pragma once
 #include "deps_kernels.h"
 
@@ -34,8 +35,10 @@ struct MaxConflictOp {
     const uint8_t* e_meta;
     const uint64_t* e_exec1;
     const uint32_t* e_txn;
+    const uint32_t* sval;      // sorted position -> pair index
     uint64_t* pm_e;
     uint32_t* pm_r;
+    uint32_t* inv;             // pair index -> sorted position
 
     __device__ S load(size_t i) const {
         const uint32_t m = e_meta[i];
@@ -51,6 +54,7 @@ struct MaxConflictOp {
     __device__ void store(size_t i, const S&, const S& inc, const S&) const {
         pm_e[i] = inc.e;
         pm_r[i] = inc.r;
+        inv[sval[i]] = (uint32_t)i;
     }
 };
 
@@ -60,14 +64,12 @@ struct McArgs {
     const uint8_t* e_meta;
     const uint64_t* e_exec1;
     const int32_t* seg_start;
-    const uint32_t* sval;      // sorted position -> pair index
+    const uint32_t* inv;       // pair index -> sorted position
     const uint32_t* gid;       // sharded batches: local row -> global arrival rank (nullable)
     const uint64_t* pm_e;
     const uint32_t* pm_r;
     uint32_t window, thresh;
     uint64_t seed;
-    uint64_t* pe;              // [p * NV + v]
-    uint32_t* pr;
     const uint32_t* key_off;
     const uint64_t* tx_ts;
     uint32_t* max_rank;        // [v * n + t]
@@ -75,58 +77,39 @@ struct McArgs {
 };
 
 template <int NV>
-__global__ __launch_bounds__(256) void k_mc_entries(McArgs a) {
-    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.P) return;
-    const int seg0 = a.seg_start[s];
-    const uint32_t i = a.e_txn[s];
-    const uint32_t gi = a.gid ? a.gid[i] : i;
+__global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint32_t gi = a.gid ? a.gid[t] : (uint32_t)t;
     const uint32_t lo = a.window == 0 ? gi : (gi > a.window ? gi - a.window : 0u);
     uint64_t be[NV];
     uint32_t br[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) { be[v] = 0; br[v] = 0; }
-    // in-flight window [i - W, i): recorded as PreAccepted by every view that did not drop it
-    int q = (int)s - 1;
-    for (; q >= seg0; --q) {
-        const uint32_t j = a.e_txn[q];
-        const uint32_t gj = a.gid ? a.gid[j] : j;
-        if (gj < lo) break;
-        if (!manages(a.e_meta[q])) continue;
-        const uint64_t e = a.e_exec1[q];
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-            if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh) && mc_less(be[v], br[v], e, j)) {
-                be[v] = e; br[v] = j;
-            }
-    }
-    // recorded prefix [seg0, q]: one segmented-scan value, identical for every view
-    if (q >= seg0) {
-        const uint64_t e = a.pm_e[q];
-        const uint32_t r = a.pm_r[q];
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-            if (mc_less(be[v], br[v], e, r)) { be[v] = e; br[v] = r; }
-    }
-    const size_t pb = (size_t)a.sval[s] * NV;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) { a.pe[pb + v] = be[v]; a.pr[pb + v] = br[v]; }
-}
-
-template <int NV>
-__global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    uint64_t be[NV];
-    uint32_t br[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) { be[v] = 0; br[v] = 0; }
     for (uint32_t p = a.key_off[t]; p < a.key_off[t + 1]; ++p) {
+        const int s = (int)a.inv[p];
+        const int seg0 = a.seg_start[s];
+        // in-flight window [i - W, i): recorded as PreAccepted by every view that did not drop it
+        int q = s - 1;
+        for (; q >= seg0; --q) {
+            const uint32_t j = a.e_txn[q];
+            const uint32_t gj = a.gid ? a.gid[j] : j;
+            if (gj < lo) break;
+            if (!manages(a.e_meta[q])) continue;
+            const uint64_t e = a.e_exec1[q];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const uint64_t e = a.pe[(size_t)p * NV + v];
-            const uint32_t r = a.pr[(size_t)p * NV + v];
-            if (mc_less(be[v], br[v], e, r)) { be[v] = e; br[v] = r; }
+            for (int v = 0; v < NV; ++v)
+                if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh) && mc_less(be[v], br[v], e, j)) {
+                    be[v] = e; br[v] = j;
+                }
+        }
+        // recorded prefix [seg0, q]: one segmented-scan value, identical for every view
+        if (q >= seg0) {
+            const uint64_t e = a.pm_e[q];
+            const uint32_t r = a.pm_r[q];
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (mc_less(be[v], br[v], e, r)) { be[v] = e; br[v] = r; }
         }
     }
     const uint64_t t1 = a.tx_ts[t] + 1;

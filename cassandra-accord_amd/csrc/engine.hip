@@ -195,7 +195,7 @@ enum Slot : size_t {
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
     S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT, S_HSTORE, S_XRANK, S_XLIST, S_XOFF,
     S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
-    S_MCPE, S_MCPR, S_MCE, S_MCR, S_MCRANK, S_MCFAST,
+    S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -511,7 +511,6 @@ void launch_union(const UnionArgs& ua, hipStream_t st) {
 
 template <int NV>
 void launch_mc(const McArgs& a, hipStream_t st) {
-    if (a.P > 0) k_mc_entries<NV><<<ceil_div((long)a.P, 256), 256, 0, st>>>(a);
     k_mc_txns<NV><<<ceil_div((long)a.n, 256), 256, 0, st>>>(a);
 }
 
@@ -1102,22 +1101,22 @@ int ad_max_conflicts(ad_handle* h, uint32_t* max_rank, uint8_t* fast) {
     hipStream_t st = h->st;
     McArgs a{};
     a.n = n; a.P = P;
-    a.e_txn = h->e_txn; a.e_meta = h->e_meta; a.e_exec1 = h->e_exec1; a.seg_start = h->seg_start; a.sval = h->sval;
+    a.e_txn = h->e_txn; a.e_meta = h->e_meta; a.e_exec1 = h->e_exec1; a.seg_start = h->seg_start;
     a.gid = h->sharded ? h->gid : nullptr;
     a.window = h->cfg.window; a.thresh = ad_drop_threshold(h->cfg.drop_p); a.seed = h->cfg.seed;
     a.key_off = h->key_off; a.tx_ts = h->tx_ts;
-    uint64_t *pm_e = nullptr, *pe = nullptr;
-    uint32_t *pm_r = nullptr, *pr = nullptr, *rank = nullptr;
+    uint64_t* pm_e = nullptr;
+    uint32_t *pm_r = nullptr, *inv = nullptr, *rank = nullptr;
     uint8_t* fst = nullptr;
     CK(dalloc(h, S_MCPE, &pm_e, std::max<size_t>(P, 1))); CK(dalloc(h, S_MCPR, &pm_r, std::max<size_t>(P, 1)));
-    CK(dalloc(h, S_MCE, &pe, std::max<size_t>(P * nv, 1))); CK(dalloc(h, S_MCR, &pr, std::max<size_t>(P * nv, 1)));
+    CK(dalloc(h, S_MCINV, &inv, std::max<size_t>(P, 1)));
     CK(dalloc(h, S_MCRANK, &rank, n * nv)); CK(dalloc(h, S_MCFAST, &fst, n * nv));
-    a.pm_e = pm_e; a.pm_r = pm_r; a.pe = pe; a.pr = pr; a.max_rank = rank; a.fast = fst;
+    a.pm_e = pm_e; a.pm_r = pm_r; a.inv = inv; a.max_rank = rank; a.fast = fst;
     if (P > 0) CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<MaxConflictOp>(P))));
     {
-        KScope ks(K_MAX_CONFLICTS, P);      // scan + per-entry walk + per-txn fold
+        KScope ks(K_MAX_CONFLICTS, P);      // scan (+ inverse permutation) + per-txn walk and fold
         if (P > 0) {
-            MaxConflictOp op{h->seg_start, h->e_meta, h->e_exec1, h->e_txn, pm_e, pm_r};
+            MaxConflictOp op{h->seg_start, h->e_meta, h->e_exec1, h->e_txn, h->sval, pm_e, pm_r, inv};
             device_scan(op, P, (MaxConflictOp::S*)h->scratch, st);
         }
         NV_DISPATCH(nv, launch_mc, a, st);
