@@ -220,13 +220,8 @@ def main_sharded(args, rank, world, local, dist):
         try:
             with stdout_to_stderr():      # RCCL's version banner
                 tr = sharding.RcclTransport(dist, store, rank, world)
-        except engine.AccordDepsError as e:     # e.g. ranks sharing one GPU: RCCL refuses duplicate devices
+        except sharding.RcclUnavailable as e:   # decided on every rank together (e.g. ranks sharing one GPU)
             print("rank %d: RCCL unavailable (%s); using the host transport" % (rank, e), file=sys.stderr)
-        ok = tr is not None
-        t = __import__("torch").tensor([1 if ok else 0], dtype=__import__("torch").int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        if not t.item():
-            tr = None
     if tr is None:
         tr = sharding.GlooTransport(dist)
 

@@ -90,6 +90,7 @@ class DepsEngine:
     def __init__(self, device=0, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1):
         self.cfg = abi.make_config(window, replicas, drop_p, seed)
         self.replicas = replicas
+        self.device = device
         h = C.c_void_p()
         rc = lib().ad_open(device, C.byref(self.cfg), C.byref(h))
         if rc != abi.AD_OK:

@@ -74,31 +74,41 @@ def home_stores(batch, bounds):
 def reduce_witnessed(batch, parts):
     """PreAccept.reduce of the stores' witnessedAt proposals (messages/PreAccept.java:141-156: witnessedAt =
     Timestamp.mergeMax, Timestamp.java:273-279) for the global batch: parts = [(gid, max_rank, fast)] per
-    store (ShardStore.max_conflicts).  Per view and global txn: the rank of the greatest executeAt over the
-    stores (Timestamp.compareTo, ties to the larger rank, as each store breaks them) and the fast-path flag
-    (every store answered TxnId).  A host-side fold of n x R integers, like the coordinator's fold over
-    replica replies; the per-store work runs on the GPU."""
+    store (ShardStore.max_conflicts).  Per view and global txn:
+      rank   the txn whose executeAt wins mergeMax over the stores' answers: Timestamp.compareToWithoutEpoch
+             (Timestamp.java:219-227: highHlc, lowHlc, identity flags, node), ties to the larger rank;
+      fast   every store answered TxnId (fast path);
+      epoch  mergeMax's withEpochAtLeast: the greatest epoch among the stores' answers (0 for Timestamp.NONE).
+    In a single-epoch batch the winner's executeAt is exactly the merged witnessedAt; across epochs the merged
+    value is the winner's (hlc, flags, node) at `epoch`.  A host-side fold of n x R integers, like the
+    coordinator's fold over replica replies; the per-store work runs on the GPU."""
     n = batch["n"]
     R = parts[0][1].shape[0] if parts else 1
     j = np.arange(n, dtype=np.int64)
-    # strict total order of (executeAt, rank): msb unsigned, lowHlc, identity flags, node signed, then rank
-    order = np.lexsort((j, batch["exec_node"].astype(np.int64), batch["exec_lsb"] & np.uint64(0x1E),
-                        batch["exec_lsb"] >> np.uint64(16), batch["exec_msb"]))
+    msb, lsb = batch["exec_msb"], batch["exec_lsb"]
+    # strict total order of (executeAt without epoch, rank): highHlc, lowHlc, identity flags, node signed, rank
+    order = np.lexsort((j, batch["exec_node"].astype(np.int64), lsb & np.uint64(0x1E),
+                        lsb >> np.uint64(16), msb & np.uint64(0x7FFF)))
     pos = np.empty(n, np.int64)
     pos[order] = j
+    epoch_of = (msb >> np.uint64(15)).astype(np.int64)
     best = np.full((R, n), -1, np.int64)
+    ep = np.zeros((R, n), np.int64)
     fast = np.ones((R, n), np.uint8)
     for gid, rank, f in parts:
         gid = np.asarray(gid, np.int64)
         has = rank != abi.AD_RANK_NONE
-        p = np.where(has, pos[np.where(has, rank, 0).astype(np.int64)], -1)
+        safe = np.where(has, rank, 0).astype(np.int64)
+        p = np.where(has, pos[safe], -1)
+        e = np.where(has, epoch_of[safe], 0)
         for v in range(R):
             best[v, gid] = np.maximum(best[v, gid], p[v])
+            ep[v, gid] = np.maximum(ep[v, gid], e[v])
             fast[v, gid] &= f[v]
     out = np.full((R, n), abi.AD_RANK_NONE, np.uint32)
     has = best >= 0
     out[has] = order[best[has]].astype(np.uint32)
-    return out, fast
+    return out, fast, ep.astype(np.uint64)
 
 
 def _u32p(a):
@@ -282,18 +292,52 @@ class GlooTransport:
         return self.any(changed)
 
 
+class RcclUnavailable(RuntimeError):
+    """RCCL cannot be used by this group (decided identically on every rank, before any collective RCCL call)."""
+
+
 class RcclTransport(GlooTransport):
     """Blobs and level arrays move over RCCL (grouped ncclSend/ncclRecv all-to-all, ncclAllReduce, on
     device buffers over xGMI); the gloo group carries the unique id, the byte counts and one scalar per
-    level round."""
+    level round.
+
+    ncclCommInitRank is collective: a rank that fails before or inside it would leave its peers blocked in it.
+    So the ranks first agree over gloo that RCCL is usable — every rank on a distinct (host, device) (RCCL
+    refuses two ranks on one GPU) and rank 0 produced a unique id — and raise RcclUnavailable together
+    otherwise; after the init an all-reduce(min) of the outcome makes a failure on any rank everyone's."""
 
     name = "rccl"
 
     def __init__(self, dist, store, rank, world):
         super().__init__(dist)
-        obj = [unique_id() if rank == 0 else None]
+        import socket
+        me = (socket.gethostname(), int(store.eng.device))
+        everyone = [None] * world
+        dist.all_gather_object(everyone, me)
+        if len(set(everyone)) != world:
+            raise RcclUnavailable("ranks share a GPU: %s" % (everyone,))
+        uid = None
+        if rank == 0:
+            try:
+                uid = unique_id()
+            except engine.AccordDepsError:
+                uid = None
+        obj = [uid]
         dist.broadcast_object_list(obj, src=0)
-        store.comm_init(world, rank, obj[0])
+        if obj[0] is None:
+            raise RcclUnavailable("ncclGetUniqueId failed on rank 0")
+        err = None
+        try:
+            store.comm_init(world, rank, obj[0])
+        except engine.AccordDepsError as e:
+            err = e
+        if not self.all_ok(err is None):
+            raise RcclUnavailable("ncclCommInitRank failed on some rank%s" % (": %s" % err if err else ""))
+
+    def all_ok(self, ok):
+        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return bool(t.item())
 
     def exchange_blobs(self, store):
         sizes = store.export()
@@ -303,8 +347,14 @@ class RcclTransport(GlooTransport):
         return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
 
+class LevelsNotConverged(RuntimeError):
+    """The distributed level rounds hit their cap while some store still raised a level: the levels are not
+    final and must not be reported (every store raises it in the same round: the flag is all-reduced)."""
+
+
 def run_store(store, transport, max_rounds=1 << 16, timings=None):
-    """The per-store protocol after load(): returns the number of distributed level rounds.
+    """The per-store protocol after load(): returns the number of distributed level rounds.  Raises
+    LevelsNotConverged if the rounds reach max_rounds while levels are still changing.
     timings (dict, optional) accumulates wall seconds per phase (each phase ends synchronised)."""
     import time
     clock = time.perf_counter
@@ -328,8 +378,10 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None):
     while True:
         any_changed = transport.allreduce_levels(store, changed)
         lap("levels_exchange")
-        if not any_changed or rounds >= max_rounds:
+        if not any_changed:
             break
+        if rounds >= max_rounds:
+            raise LevelsNotConverged("distributed execution levels still changing after %d rounds" % rounds)
         changed = store.levels_round(False)
         lap("levels_local")
         rounds += 1
@@ -340,7 +392,7 @@ class LocalTransport:
     """Several stores in one process (tests): the same protocol with in-process exchange."""
 
     @staticmethod
-    def run(stores):
+    def run(stores, max_rounds=1 << 16):
         for s in stores:
             s.preaccept()
         sizes = [s.export() for s in stores]
@@ -359,6 +411,8 @@ class LocalTransport:
                 s.levels_set(g)
             if not any(changed):
                 break
+            if rounds >= max_rounds:
+                raise LevelsNotConverged("distributed execution levels still changing after %d rounds" % rounds)
             changed = [s.levels_round(False) for s in stores]
             rounds += 1
         return rounds

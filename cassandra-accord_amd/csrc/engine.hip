@@ -1585,10 +1585,14 @@ int ad_comm_unique_id(uint8_t* out /* [128] */) {
 int ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id_bytes) {
     if (!h || !id_bytes || rank >= world) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
+    if (h->comm) return set_err(h, AD_ERR_STATE, "ad_comm_init: the handle already has a communicator");
+    if (h->sharded && world != h->world) return set_err(h, AD_ERR_ARGUMENT, "ad_comm_init: world differs from ad_shard_setup's");
     ncclUniqueId id;
     std::memcpy(&id, id_bytes, sizeof(id));
-    ncclResult_t r = ncclCommInitRank(&h->comm, (int)world, id, (int)rank);
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclCommInitRank(&comm, (int)world, id, (int)rank);
     if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    h->comm = comm;
     return AD_OK;
 }
 
@@ -1602,16 +1606,27 @@ int ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world] */) {
     size_t total = 0;
     for (uint32_t s = 0; s < W; ++s) total += recv_sizes[s];
     CK(dalloc(h, S_RECV, &h->recv, std::max<size_t>(total, 8)));
+    if (h->send_sizes.size() != W) return set_err(h, AD_ERR_STATE, "ad_shard_alltoall: export for this world first");
     size_t so = 0, ro = 0;
     if (ncclGroupStart() != ncclSuccess) return set_err(h, AD_ERR_DEVICE, "ncclGroupStart");
-    for (uint32_t p = 0; p < W; ++p) {
-        if (h->send_sizes[p]) ncclSend(h->send + so, h->send_sizes[p], ncclUint8, (int)p, h->comm, h->st);
-        if (recv_sizes[p]) ncclRecv(h->recv + ro, recv_sizes[p], ncclUint8, (int)p, h->comm, h->st);
+    // every send/recv is checked; on an argument error the group is still closed before returning
+    ncclResult_t first = ncclSuccess;
+    std::string what;
+    for (uint32_t p = 0; p < W && first == ncclSuccess; ++p) {
+        if (h->send_sizes[p]) {
+            ncclResult_t r = ncclSend(h->send + so, h->send_sizes[p], ncclUint8, (int)p, h->comm, h->st);
+            if (r != ncclSuccess) { first = r; what = "ncclSend to " + std::to_string(p); }
+        }
+        if (first == ncclSuccess && recv_sizes[p]) {
+            ncclResult_t r = ncclRecv(h->recv + ro, recv_sizes[p], ncclUint8, (int)p, h->comm, h->st);
+            if (r != ncclSuccess) { first = r; what = "ncclRecv from " + std::to_string(p); }
+        }
         so += h->send_sizes[p];
         ro += recv_sizes[p];
     }
     ncclResult_t r = ncclGroupEnd();
-    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclSend/Recv: ") + ncclGetErrorString(r));
+    if (first != ncclSuccess) return set_err(h, AD_ERR_DEVICE, what + ": " + ncclGetErrorString(first));
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclGroupEnd (send/recv): ") + ncclGetErrorString(r));
     return parse_recv(h, recv_sizes);
 }
 

@@ -202,6 +202,11 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
  * stored (CommandsForKey entries not TRANSITIVELY_KNOWN/INVALID; in-flight j unless the view dropped it) — or
  * AD_RANK_NONE (Timestamp.NONE).  fast[v*n + i] = 1 when TxnId_i >= that timestamp (or NONE): the replica answers
  * witnessedAt = TxnId (fast path), else time.uniqueNow(maxConflict), which the host clock supplies.
+ * Model assumption (stated, not pinned by the reference): an in-flight j the view holds contributes its batch
+ * executeAt — the value MaxConflicts holds once j commits.  In the reference a PreAccepted j contributes the
+ * view's own earlier witnessedAt proposal for j (<= its final executeAt for slow-path txns) until it commits,
+ * so for views holding slow-path j in flight max_rank / fast may be higher / lower than a live replica's.
+ * The oracle (oracle.cpp Oracle::max_conflict) makes the same assumption.
  * Key-domain batches (AD_ERR_UNSUPPORTED when the batch has range txns).  Either pointer may be NULL.
  * Sharded stores (ad_shard_setup): rows are local, max_rank holds global arrival ranks; PreAccept.reduce's
  * mergeMax across stores (messages/PreAccept.java:141-156) is then a per-txn max over the stores' answers. */

@@ -5,7 +5,7 @@ arrival ranks."""
 import numpy as np
 import pytest
 
-from accord_amd import abi, sharding, workload
+from accord_amd import abi, blob, sharding, workload
 
 pytestmark = pytest.mark.gpu
 
@@ -87,10 +87,154 @@ def test_sharded_witnessed_at(engine_factory, name, shards):
             st.preaccept()
             rank, fast = st.max_conflicts()
             parts.append((gid, rank.copy(), fast.copy()))
-        got_rank, got_fast = sharding.reduce_witnessed(b, parts)
+        got_rank, got_fast, _ = sharding.reduce_witnessed(b, parts)
         assert np.array_equal(got_rank, want_rank) and np.array_equal(got_fast, want_fast)
         if name == "C3":
             assert want_fast.min() == 0
+    finally:
+        for st in stores:
+            st.close()
+
+
+def _make_stores(b, shards, w, r, p, s, keyspace):
+    bounds = sharding.even_bounds(0, keyspace, shards)
+    hs = sharding.home_stores(b, bounds)
+    stores = []
+    for k in range(shards):
+        local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+        st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
+        stores.append(st)
+        st.load(local, gid, hs[gid], b["n"], k, shards)
+    return stores, bounds, hs
+
+
+def _check_against_unsharded(stores, views, merged, lv, order, r, n_global):
+    """Every store's home txns (vectorised row selection): per-view and merged deps, levels, and its order
+    equal to the global order restricted to its home txns."""
+    pos = np.empty(len(order), np.int64)
+    pos[order] = np.arange(len(order))
+    seen = np.zeros(n_global, bool)
+    for st in stores:
+        for v in range(r + 1):
+            for ci, c in enumerate((abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)):
+                got, hg = st.fetch(v, c)
+                want = merged[ci] if v == r else views[v][ci]
+                assert blob._rows_of(want, hg).equal(got), "store view %d class %d differs" % (v, c)
+        hl, ho = st.order()
+        _, hg = st.fetch(r, abi.CLASS_KEY)
+        assert np.array_equal(hl, lv[hg]), "levels differ"
+        assert np.all(np.diff(pos[ho]) > 0), "store order is not the global order restricted to its home txns"
+        assert not seen[hg].any()
+        seen[hg] = True
+    return seen
+
+
+def test_blob_codec_matches_engine_bytes(engine_factory):
+    # accord_amd.blob.export over a store's own local CSRs (local ranks) must reproduce the bytes ad_shard_export
+    # wrote for every destination (the codec the CPU gloo test pushes is the engine's format)
+    w, r, p, s = 32, 3, 0.1, 0xACC0D1
+    b = workload.config("C2", n=20000)
+    stores, bounds, hs = _make_stores(b, 3, w, r, p, s, 10_000_000)
+    try:
+        for k, st in enumerate(stores):
+            st.eng.preaccept_deps()
+            csrs = [st.eng.fetch_deps(v, c) for v in range(r) for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)]
+            sizes = st.export()
+            dev = st.send_buffer()
+            host, hsz = blob.export(st.gid, st.home_store, csrs, 3)
+            assert np.array_equal(sizes, hsz)
+            assert np.array_equal(dev, host), "store %d: blob bytes differ from the host codec" % k
+    finally:
+        for st in stores:
+            st.close()
+
+
+def test_host_fragments_import(engine_factory):
+    # fragments resolved elsewhere and packed by the host codec: ad_shard_import_host + ad_shard_merge on every
+    # store must equal the unsharded engine (the engine merges what the wire format carries, whoever produced it)
+    w, r, p, s = 32, 2, 0.1, 0xACC0D1
+    b = workload.config("C2", n=20000)
+    views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
+    shards = 3
+    stores, bounds, hs = _make_stores(b, shards, w, r, p, s, 10_000_000)
+    try:
+        bufs, sizes = [], []
+        for st in stores:
+            st.eng.preaccept_deps()
+            csrs = [st.eng.fetch_deps(v, c) for v in range(r) for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)]
+            bb, sz = blob.export(st.gid, st.home_store, csrs, shards)
+            bufs.append(bb)
+            sizes.append(sz)
+        offs = [np.concatenate([[0], np.cumsum(z)]).astype(np.int64) for z in sizes]
+        for d, st in enumerate(stores):
+            parts = [bufs[k][offs[k][d]:offs[k][d + 1]] for k in range(shards)]
+            st.import_host(np.concatenate(parts), np.array([sizes[k][d] for k in range(shards)], np.uint64))
+            st.merge()
+            for v in range(r + 1):
+                for ci, c in enumerate((abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)):
+                    got, hg = st.fetch(v, c)
+                    want = merged[ci] if v == r else views[v][ci]
+                    assert blob._rows_of(want, hg).equal(got)
+    finally:
+        for st in stores:
+            st.close()
+
+
+def test_rccl_world1_run_store(engine_factory, tmp_path):
+    # the RCCL transport end to end on the one GPU: a world = 1 communicator (ad_comm_init), the grouped
+    # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and ncclAllReduce level rounds
+    # (ad_shard_levels_allreduce), driven by the same run_store the N>1 bench uses; equal to the unsharded engine
+    import torch.distributed as dist
+    w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
+    b = workload.generate(200_000, 4, 10_000_000, "uniform", seed=s)
+    views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
+    dist.init_process_group("gloo", init_method="file://%s" % (tmp_path / "rdv"), rank=0, world_size=1)
+    stores = []
+    try:
+        stores, _, _ = _make_stores(b, 1, w, r, p, s, 10_000_000)
+        tr = sharding.RcclTransport(dist, stores[0], 0, 1)
+        assert tr.name == "rccl"
+        rounds = sharding.run_store(stores[0], tr)
+        assert rounds >= 1
+        seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
+        assert seen[np.diff(b["key_off"]) > 0].all()
+        # a second communicator on the same handle is refused (no leak of the first)
+        import accord_amd.engine as E
+        with pytest.raises(E.AccordDepsError):
+            stores[0].comm_init(1, 0, sharding.unique_id())
+    finally:
+        for st in stores:
+            st.close()
+        dist.destroy_process_group()
+
+
+def test_levels_round_cap_raises(engine_factory):
+    # run_store / LocalTransport must not report levels that are still changing when the round cap is hit
+    w, r, p, s = 32, 2, 0.1, 0xACC0D1
+    b = workload.config("C3", n=20000)
+    stores, _, _ = _make_stores(b, 3, w, r, p, s, 10_000_000)
+    try:
+        with pytest.raises(sharding.LevelsNotConverged):
+            sharding.LocalTransport.run(stores, max_rounds=1)
+    finally:
+        for st in stores:
+            st.close()
+
+
+def test_c5_four_stores_1m_each(engine_factory):
+    # C5's generator at 1,048,576 txns per store over S = 4 key-range stores (4,194,304 txns, 40M keys): the full
+    # cross-store protocol (local deps, export, exchange, home merge, distributed level rounds, order) equals the
+    # unsharded engine on the whole batch, bit for bit, for every home txn of every store
+    w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
+    shards, per = 4, 1 << 20
+    b = workload.generate(shards * per, 4, 10_000_000 * shards, "uniform", seed=s)
+    views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
+    stores, _, _ = _make_stores(b, shards, w, r, p, s, 10_000_000 * shards)
+    try:
+        rounds = sharding.LocalTransport.run(stores)
+        assert rounds >= 1
+        seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
+        assert seen[np.diff(b["key_off"]) > 0].all(), "every txn has exactly one home store"
     finally:
         for st in stores:
             st.close()

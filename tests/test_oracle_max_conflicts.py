@@ -153,6 +153,6 @@ def test_reduce_witnessed_across_stores():
             rank, fast = O.max_conflicts(local, cfg)
             g = np.where(rank != NONE, gid[np.where(rank != NONE, rank, 0)], NONE).astype(np.uint32)
             parts.append((gid, g, fast))
-        got_rank, got_fast = sharding.reduce_witnessed(b, parts)
+        got_rank, got_fast, _ = sharding.reduce_witnessed(b, parts)
         assert np.array_equal(got_rank, want_rank) and np.array_equal(got_fast, want_fast)
     assert want_fast.min() == 0

@@ -2,10 +2,13 @@
 
 Each rank slices the batch to its key range (accord_amd.sharding.slice_for_shard), resolves its local batch
 with the oracle (the test-only stand-in for the GPU engine; W = 0 and no drops so local ranks and global
-ranks give the same answers), rewrites TxnIds to global ranks, exchanges fragments over gloo
-(all_gather_object — the GlooTransport path) and merges, for its home txns, every store's fragment
-(PreAccept.reduce = Deps.with, messages/PreAccept.java:141-156).  The result must equal the unsharded oracle.
-The transport's scalar collectives (max / any) are exercised on the same group.
+ranks give the same answers), packs its fragments in the engine's own blob format (accord_amd.blob.export:
+per destination store, the rows homed there with any deps, TxnIds as global ranks — byte-identical to
+ad_shard_export, pinned by tests/test_gpu_sharding.py) and moves them with the product transport's
+GlooTransport.exchange_blobs (all_to_all_single of the per-destination byte counts, then of the blobs).  Each
+store decodes what it received and merges, for its home txns, every store's fragment (PreAccept.reduce =
+Deps.with, messages/PreAccept.java:141-156).  The result must equal the unsharded oracle.  The transport's
+scalar collectives (max / any) are exercised on the same group.
 """
 import os
 import socket
@@ -37,7 +40,7 @@ def _worker(rank, world, port, n):
     sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    from accord_amd import abi, sharding, workload
+    from accord_amd import abi, blob, sharding, workload
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -59,30 +62,29 @@ def _worker(rank, world, port, n):
         bounds = sharding.even_bounds(0, 20000, world)
         local, gid, home = sharding.slice_for_shard(b, bounds[rank], bounds[rank + 1])
         res = O.OracleResult(local, cfg, O.FLAG_MERGE)
-        frag = {}
-        for v in range(2):
-            for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
-                csr = res.deps(v, c)
-                for i in range(local["n"]):
-                    ks, txns, k2t = _relation(csr, i)
-                    frag[(v, c, int(gid[i]))] = (ks, gid[txns] if len(txns) else txns, k2t)
-        allfrag = [None] * world
-        dist.all_gather_object(allfrag, frag)
-
-        ref = O.OracleResult(b, cfg, O.FLAG_MERGE)
+        vcs = [(v, c) for v in range(2) for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)]
+        hs = sharding.home_stores(b, bounds)
+        store = blob.HostFragmentStore(gid, hs[gid], [res.deps(v, c) for v, c in vcs], world)
+        tr.exchange_blobs(store)                       # the product path: byte counts, then the blobs
+        assert store.received is not None and len(store.received) == world
         homes = gid[home.astype(bool)]
         assert len(homes) > 0
-        for v in range(2):
-            for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
-                want = ref.deps(v, c)
-                for g in homes:
-                    acc = O.EMPTY_RELATION
-                    for f in allfrag:
-                        if (v, c, int(g)) in f:
-                            acc = O.union_relation(acc, f[(v, c, int(g))])
-                    wk, wt, wm = want.txn(int(g))
-                    assert np.array_equal(acc[0], wk) and np.array_equal(acc[1], wt) and np.array_equal(acc[2], wm), \
-                        "rank %d view %d class %d txn %d" % (rank, v, c, g)
+        for src_gid, _ in store.received:              # every received row is homed here
+            assert np.isin(src_gid, homes).all()
+
+        ref = O.OracleResult(b, cfg, O.FLAG_MERGE)
+        rowpos = [{int(g): i for i, g in enumerate(src_gid)} for src_gid, _ in store.received]
+        for k, (v, c) in enumerate(vcs):
+            want = ref.deps(v, c)
+            for g in homes:
+                acc = O.EMPTY_RELATION
+                for s, (_, csrs) in enumerate(store.received):
+                    r = rowpos[s].get(int(g))
+                    if r is not None:
+                        acc = O.union_relation(acc, _relation(csrs[k], r))
+                wk, wt, wm = want.txn(int(g))
+                assert np.array_equal(acc[0], wk) and np.array_equal(acc[1], wt) and np.array_equal(acc[2], wm), \
+                    "rank %d view %d class %d txn %d" % (rank, v, c, g)
         # every txn is homed exactly once across the stores
         counts = torch.zeros(n, dtype=torch.int64)
         counts[torch.from_numpy(homes.astype(np.int64))] = 1
