@@ -65,7 +65,8 @@ class AdStageTimes(C.Structure):
     _fields_ = [("prepare", C.c_float), ("sort", C.c_float), ("deps", C.c_float), ("merge", C.c_float),
                 ("levels", C.c_float), ("total", C.c_float),
                 ("deps_entries", C.c_uint64), ("merged_entries", C.c_uint64), ("level_edges", C.c_uint64),
-                ("level_iterations", C.c_uint32), ("walk_items", C.c_uint32)]
+                ("level_iterations", C.c_uint32), ("walk_items", C.c_uint32),
+                ("level_blocks", C.c_uint32), ("level_rounds", C.c_uint32)]
 
 
 def ptr(a, ctype):

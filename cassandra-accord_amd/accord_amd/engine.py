@@ -213,9 +213,14 @@ class DepsEngine:
         self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
         return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_}
 
-    def set_level_mode(self, fixpoint):
-        """False (default): Kahn wavefront where it applies, else the chain fixpoint; True: always the fixpoint."""
-        self._check(lib().ad_set_level_mode(self.h, 1 if fixpoint else 0), "ad_set_level_mode")
+    LEVELS_AUTO, LEVELS_FIXPOINT, LEVELS_BLOCKS = 0, 1, 2
+
+    def set_level_mode(self, mode):
+        """LEVELS_AUTO (default; False): Kahn wavefront for short key chains, executeAt blocks for deep key-only
+        batches, Kahn with explicit edges for mixed batches; LEVELS_FIXPOINT (True): always the chain fixpoint;
+        LEVELS_BLOCKS: executeAt blocks for every key-only batch."""
+        mode = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
+        self._check(lib().ad_set_level_mode(self.h, mode), "ad_set_level_mode")
 
     def set_trace(self, mask):
         """Enable HIP-event timing of the kernels whose id bit is set (see kernel_ids())."""

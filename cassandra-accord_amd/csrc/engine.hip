@@ -870,7 +870,10 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.merged_range = &h->merged[AD_CLASS_RANGE];
     li.n_large = h->n_large;
     li.exec_bits = h->pack.total_bits;
-    li.kahn_ok = h->level_mode == AD_LEVELS_AUTO ? 1 : 0;
+    li.kahn_ok = h->level_mode != AD_LEVELS_FIXPOINT ? 1 : 0;
+    li.force_blocks = h->level_mode == AD_LEVELS_BLOCKS ? 1 : 0;
+    h->ls.bl_rounds = 0;
+    h->ls.bl_used = false;
     h->order_pending = false;
     h->order_bad = 0;
     li.order_verify = &h->order_bad;
@@ -879,6 +882,8 @@ int stage_levels(ad_handle* h, bool want_order) {
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
     if (rc != AD_OK) return rc;
     h->level_iters = (uint32_t)iters;
+    h->times.level_rounds = h->ls.bl_rounds;
+    h->times.level_blocks = h->ls.bl_used ? h->ls.bl.nblocks : 0;
     h->have_levels = true;
     return AD_OK;
 }
@@ -1317,7 +1322,7 @@ int ad_kernel_count(void) { return K_COUNT; }
 const char* ad_kernel_name(int kid) { return kernel_name(kid); }
 
 int ad_set_level_mode(ad_handle* h, int mode) {
-    if (!h || (mode != AD_LEVELS_AUTO && mode != AD_LEVELS_FIXPOINT)) return AD_ERR_ARGUMENT;
+    if (!h || (mode != AD_LEVELS_AUTO && mode != AD_LEVELS_FIXPOINT && mode != AD_LEVELS_BLOCKS)) return AD_ERR_ARGUMENT;
     h->level_mode = mode;
     return AD_OK;
 }

@@ -27,6 +27,7 @@
 #pragma once
 #include "radix_sort.h"
 #include "union_kernels.h"
+#include "block_levels.h"
 
 namespace ad {
 
@@ -943,11 +944,15 @@ struct LevelState {
     uint32_t* xs = nullptr;
     uint32_t* kfront = nullptr;          // k_kahn_small: two frontier lists of KS_MAX + state[4]
     size_t capX = 0, xs_cap = 0;
+    BlockBufs bl;                        // deep key-chain batches: executeAt blocks (block_levels.h)
+    uint32_t bl_rounds = 0;              // block scan rounds of the last block-path run
+    bool bl_used = false;                // the last run_levels took the block path
 };
 
 inline void free_level_state(LevelState& s) {
     void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront};
     for (void* p : ps) if (p) hipFree(p);
+    free_block_bufs(s.bl);
     s = LevelState{};
 }
 
@@ -977,6 +982,7 @@ struct LevelInputs {
     uint32_t exec_bits;
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
+    int force_blocks;                    // pure key-chain batches: executeAt blocks even for short chains (tests)
     uint32_t* order_verify;              // optimistic order: host word receiving the fast-path failure flag
     bool* order_pending;                 // set when the caller must check *order_verify after its sync
 };
@@ -1132,6 +1138,115 @@ inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     return optimistic;
 }
 
+// Levels of a pure key-chain batch (no direct / range deps, no range txns) by executeAt blocks.  Leaves the
+// levels in in.lvl; *depth = greatest level + 1; *rounds_out = scan rounds over all blocks.
+inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in, hipStream_t st, int* depth,
+                            uint32_t* rounds_out, std::string& err) {
+    const size_t n = in.n, P = in.P;
+    auto grow = [&](void** p, size_t bytes) -> bool {
+        if (*p) { hipStreamSynchronize(st); hipFree(*p); *p = nullptr; }
+        return hipMalloc(p, bytes) == hipSuccess;
+    };
+    const uint32_t bcap = BL_CAP - 16;         // n_large == 0: at most 16 keys per txn
+    const size_t B = P / bcap + 2;             // upper bound on blocks (the entry prefix counts key-less txns too)
+    const size_t Bmax = (P + n) / bcap + 2;
+    if (bb.capP < P || !bb.rec) {
+        const size_t c = std::max<size_t>(P, 1);
+        if (!grow((void**)&bb.rec, c * 8) || !grow((void**)&bb.bk, c * 4) || !grow((void**)&bb.bv, c * 4) ||
+            !grow((void**)&bb.bk2, c * 4) || !grow((void**)&bb.bv2, c * 4) || !grow((void**)&bb.carry, c * 8))
+            goto oom;
+        bb.capP = c;
+    }
+    if (bb.capN < n + 1 || !bb.epre) {
+        const size_t c = n + 1;
+        if (!grow((void**)&bb.epre, c * 4) || !grow((void**)&bb.erank, c * 4)) goto oom;
+        bb.capN = c;
+    }
+    if (bb.capB < Bmax + 1 || !bb.tb) {
+        const size_t c = Bmax + 1;
+        if (!grow((void**)&bb.tb, c * 4) || !grow((void**)&bb.boff, c * 4)) goto oom;
+        bb.capB = c;
+    }
+    if (!bb.stats && !grow((void**)&bb.stats, 64)) goto oom;
+    {
+        const size_t rneed = (3 * (radix_hist_len(std::max<size_t>(P, 1)) + 128) + 64 * 1024) * 4;
+        if (bb.rs_cap < rneed) { if (!grow((void**)&bb.rs, rneed)) goto oom; bb.rs_cap = rneed; }
+        const size_t sneed = device_scan_scratch<BlCntOp>(n) + 256;
+        if (ls.agg_cap < sneed) { if (!grow(&ls.agg, sneed)) goto oom; ls.agg_cap = sneed; }
+    }
+    (void)B;
+    {
+        const int gP = ceil_div((long)P, 256), gn = ceil_div((long)n, 256);
+        // 1. chain order (key, executeAt): windowed inversion ranks, else the serial per-key insertion
+        hipMemsetAsync(ls.c_pair, 0xFF, P * 4, st);
+        hipMemsetAsync(bb.stats, 0, 64, st);
+        k_chain_rank<<<ceil_div((long)P, CR_N), CR_T, 0, st>>>(P, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval,
+                                                               ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+        k_chain_check<<<std::min(gP, 2048), 256, 0, st>>>(P, in.seg_start, ls.c_exec1, ls.c_pair, bb.stats + 2);
+        // 2. executeAt order of the txns (levels all zero: order_rows sorts by executeAt only)
+        hipMemsetAsync(in.lvl, 0, n * 4, st);
+        order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);    // syncs: reads its own flags
+        uint32_t bad = 0;
+        if (hipMemcpyAsync(&bad, bb.stats + 2, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+            err = "exec levels: device error";
+            return AD_ERR_DEVICE;
+        }
+        if (bad) {
+            k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+            k_chain_order<<<gP, 256, 0, st>>>(P, in.seg_start, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+        }
+        // 3. blocks: entry prefix in executeAt order, block of every chain position, stable sort by block
+        k_bl_erank<<<gn, 256, 0, st>>>(n, in.order, bb.erank);
+        device_scan(BlCntOp{in.order, in.key_off, bb.epre, n}, n, (uint32_t*)ls.agg, st);
+        uint32_t etot = 0;
+        if (hipMemcpyAsync(&etot, bb.epre + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+            err = "exec levels: device error";
+            return AD_ERR_DEVICE;
+        }
+        const uint32_t nb = etot / bcap + 1;
+        bb.nblocks = nb;
+        k_bl_chain_block<<<gP, 256, 0, st>>>(P, ls.c_txn, bb.erank, bb.epre, bcap, bb.bk, bb.bv);
+        RadixScratch rs;
+        const size_t hl = radix_hist_len(P);
+        rs.hist = bb.rs;
+        rs.offs = rs.hist + hl + 64;
+        rs.agg = rs.offs + hl + 64;
+        uint32_t *sk = bb.bk, *sv = bb.bv;
+        const int bits = 32 - __builtin_clz(std::max<uint32_t>(nb, 1));
+        if (radix_sort_pairs(bb.bk, bb.bv, bb.bk2, bb.bv2, P, bits, rs, st)) { sk = bb.bk2; sv = bb.bv2; }
+        k_bl_bounds<<<ceil_div((long)nb + 1, 256), 256, 0, st>>>(nb, n, P, bb.epre, bcap, sk, bb.tb, bb.boff);
+        uint32_t* inv = sk == bb.bk ? bb.bk2 : bb.bk;         // the sort's free ping-pong buffer
+        k_bl_inverse<<<gP, 256, 0, st>>>(P, sv, inv);
+        k_bl_records<<<gP, 256, 0, st>>>(P, sk, sv, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.epre, bcap, bb.tb,
+                                         bb.boff, bb.rec, bb.stats + 3);
+        // 4. the walk
+        hipMemsetAsync(bb.carry, 0xFF, P * 8, st);
+        k_level_blocks<<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.carry, in.order, in.lvl, bb.stats);
+        uint32_t s4[4] = {0, 0, 0, 0};
+        if (hipMemcpyAsync(s4, bb.stats, 16, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+            err = "exec levels: device error";
+            return AD_ERR_DEVICE;
+        }
+        if (s4[3]) {
+            err = "exec levels: block layout invariant violated (txn index beyond the block)";
+            return AD_ERR_STATE;
+        }
+        *depth = (int)s4[0];
+        if (rounds_out) *rounds_out = s4[1];
+        if (getenv("AD_DEBUG_LEVELS")) {
+            uint32_t s6[6];
+            hipMemcpy(s6, bb.stats, 24, hipMemcpyDeviceToHost);
+            const double tr = (double)((uint64_t)s6[3] << 32 | s6[2]), tt = (double)((uint64_t)s6[5] << 32 | s6[4]);
+            fprintf(stderr, "block levels: %u blocks, %u rounds, depth %u; clock64 rounds %.0f (%.1f%%) of %.0f\n", nb, s6[1],
+                    s6[0], tr, 100.0 * tr / (tt > 0 ? tt : 1), tt);
+        }
+    }
+    return AD_OK;
+oom:
+    err = "exec levels: out of device memory";
+    return AD_ERR_NOMEM;
+}
+
 inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hipStream_t st, int* iters,
                       std::string& err) {
     const size_t n = in.n, P = in.P;
@@ -1198,6 +1313,35 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         ea.cons_pos = ls.cons_pos; ea.pm_all = ls.pm_all; ea.ukey = in.ukey; ea.useg = in.useg; ea.U = in.U;
         ea.c_exec1 = ls.c_exec1; ea.c_txn = ls.c_txn; ea.seg_start = in.seg_start;
         uint32_t host[8] = {0};
+        // ---- executeAt blocks (block_levels.h): pure key-chain batches whose chains are long (found by the
+        // Kahn chain build below), or always when forced
+        const bool pure = !has_b && !has_c && in.n_large == 0;
+        auto block_path = [&]() -> int {
+            int depth = 0;
+            uint32_t rounds = 0;
+            const int rc = run_block_levels(ls, ls.bl, in, st, &depth, &rounds, err);
+            if (rc != AD_OK) return rc;
+            ls.bl_rounds = rounds;
+            ls.bl_used = true;
+            ls.chains_ready = false;
+            *iters = depth;
+            if (want_order && n > 0 && in.order_verify)
+                *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, depth - 1, in.order_verify);
+            else if (want_order && n > 0)
+                order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
+            return AD_OK;
+        };
+        if (in.force_blocks && pure && !in.keep_levels && P > 0) {
+            if (hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+                err = "exec levels: device error";
+                return AD_ERR_DEVICE;
+            }
+            if (host[5]) {
+                err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                return AD_ERR_UNSUPPORTED;
+            }
+            return block_path();
+        }
         // ---- Kahn wavefront (short-chain key batches): chain build + wavefronts with no decision sync;
         // the first batch's readback also carries the kinds / long-chain flags, and a long chain found by
         // the build sends the batch to the fixpoint below
@@ -1310,6 +1454,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                             return AD_ERR_UNSUPPORTED;
                         }
                         if (host[7] && !long_done) {      // the batch's wavefronts were gated off: rebuild, restart
+                            if (pure) return block_path();   // deep key chains: executeAt blocks, not wavefronts
                             if (!long_build()) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
                             hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
                             host[7] = 0;

@@ -229,15 +229,21 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
     uint32_t level_iterations;
     uint32_t walk_items;            /* (txn,key) entries with an earlier entry of their key: the */
                                     /* ones the deps walks visit (P - distinct keys)             */
+    uint32_t level_blocks;          /* executeAt blocks walked by the block level path (0: Kahn)  */
+    uint32_t level_rounds;          /* block-scan rounds over those blocks                        */
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
-/* Execution-level algorithm (both give identical levels; the choice only affects speed):
- * AD_LEVELS_AUTO (default) uses the Kahn wavefront (each txn visited once, when released) for batches whose
- * key chains are all short and that carry no direct/range deps and no range txns, and the chain fixpoint
- * otherwise; AD_LEVELS_FIXPOINT always uses the fixpoint (tests cross-check the two). */
+/* Execution-level algorithm (all give identical levels; the choice only affects speed):
+ * AD_LEVELS_AUTO (default): batches with only key Read/Write txns (no direct/range deps, no range txns) use the
+ * Kahn wavefront (each txn visited once, when released) while every key chain is short, and executeAt blocks
+ * (block_levels.h: one LDS max-plus scan fixpoint per block, walked in executeAt order) when some chain is
+ * long (deep graphs: Zipf hot keys); mixed batches use the Kahn wavefront with explicit (b)/(c) edges.
+ * AD_LEVELS_FIXPOINT always uses the chain fixpoint; AD_LEVELS_BLOCKS uses the executeAt blocks for every
+ * key-only batch (tests cross-check the algorithms). */
 #define AD_LEVELS_AUTO 0
 #define AD_LEVELS_FIXPOINT 1
+#define AD_LEVELS_BLOCKS 2
 int  ad_set_level_mode(ad_handle* h, int mode);
 
 /* Per-kernel HIP-event timing (trace mode).  mask bit k enables kernel id k (0 <= k < ad_kernel_count()); the
