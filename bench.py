@@ -39,21 +39,22 @@ KEYSPACE = 10_000_000
 
 def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
     """Algorithmic HBM bytes moved by all traced launches of `kernel` (DESIGN.md §3 lists the per-unit
-    figures): the minimum bytes the kernel must read + write for the elements it processed.  `units` is
-    the sum of elements over the launches (pairs, txns or sort items, recorded per launch by the engine's
-    tracer); n txns, P (txn,key) pairs, R replica views; st = ad_last_times() counts of the step.
-    Kernels whose work is data dependent in a way the tracer does not count (the level worklist walk,
-    composite scans) return None and are not roofline candidates.  With large txns in the batch (range txns,
-    C4) the run's entry count D also holds the entries the virtual-item walks and the LDS unions produce,
-    which k_txn_union / k_deps_walk<fill> never touch: their D-based models would overcount, so they are not
-    candidates there."""
+    figures): the minimum bytes the kernel must read + write for the elements it processed.  `units` is the
+    sum of elements over the launches (pairs, txns, sort items or output rows, recorded per launch by the
+    engine's tracer); n txns, P (txn,key) pairs, R replica views; st = ad_last_times() counts of the step.
+    Every kernel the C2 / C3 pipelines trace has a model, so the roofline kernel is the one with the most
+    time.  With large txns (range txns, C4) the run's entry count D also holds the entries of the
+    virtual-item walks and the LDS unions, so the D-based models of k_txn_union / k_deps_walk<fill> /
+    k_merge would overcount: those return None there (not candidates)."""
     D = st["deps_entries"]           # emitted dependency entries over all views/classes
+    M = st["merged_entries"]         # entries of the merged Deps
     W = st["walk_items"]             # entries the deps walks visit
     per = {
         "k_minmax": calls * (n * 44 + P * 8),                    # TxnId/executeAt SoA + key_off; keys
         "k_pack": calls * (n * 62 + P * 20),                     # read 45 B/txn, write 17 B/txn; 8+12 B/pair
         "k_radix_hist": units * 4,                               # read the key
         "k_radix_scatter": units * 16,                           # read key+value, write key+value
+        "scan_radix": units * 12,                                # digit histogram: read twice (reduce, apply), write once
         "k_gather_entries": units * 34,                          # sval, pair_txn, meta, ex1 -> e_txn, e_meta, e_exec1, spos
         "scan_elide": units * 37,                                # skey, e_meta, e_exec1 -> seg, ud, pm_w, pm_c
         # the walks visit only entries with an earlier entry of their key (ad_stage_times.walk_items):
@@ -61,10 +62,27 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
         "k_deps_walk<count>": calls * W * (46 + 8 * R),
         "k_deps_walk<fill>": calls * (W * (46 + 8 * R) + 4 * D),  # 2R end slots in, the entries out
         "k_txn_layout": units * (8 + 16 * R),                    # key + 2R counts in, 2R slots out
+        # OffsetsOp: per pair the key + 2R counts in and 2R slots out; per txn 3 offsets x 2R CSRs out
+        "scan_offsets": calls * (P * (8 + 16 * R)) + units * 24 * R,
+        "csr_offsets": units * 24,                               # 3 exclusive scans of one count array
+        "merge_offsets": units * 24,                             # per (txn, output): 3 counts in, 3 offsets out
         # per txn: 3 offsets x 2R CSRs, the per-key lists in, unique TxnIds + remapped lists out
         "k_txn_union": calls * (n * (12 * 2 * R + 4 * 2 * R) + 12 * D),
+        # R-way merge: every reply's per-txn offsets (16 B) and TxnIds + keysToTxnIds (8 B/entry) in; the
+        # write pass also writes the merged rows (16 B/txn + 8 B/entry)
+        "k_merge<count>": units * 16 * R + 8 * D,
+        "k_merge<write>": units * (16 * R + 16) + 8 * D + 8 * M,
+        # Kahn region per pair: the entry read by the chain build (17 B), its executeAt-ordered txn + successor
+        # run written (12 B), the release (successor run, txn, remaining-count RMW, level: 24 B); per txn the
+        # in-degree, remaining count and level (16 B)
+        "kahn_levels": units * (17 + 12 + 24) + calls * n * 16,
+        # executeAt blocks per pair: chain order (17 B in, 17 B out), block sort (2 x 16 B), record (16 B in,
+        # 8 B out), the walk's record read (8 B); per txn executeAt rank, block prefix, order and level (20 B)
+        "block_levels": units * (34 + 32 + 24 + 8) + calls * n * 20,
+        # window rank (12 B in, 16 B out), check (16 B), one level radix pass (4 + 16 B), order out (4 B)
+        "order_sort": units * 68,
     }
-    if large and kernel in ("k_txn_union", "k_deps_walk<fill>"):
+    if large and kernel in ("k_txn_union", "k_deps_walk<fill>", "k_merge<count>", "k_merge<write>"):
         return None
     return per.get(kernel)
 
@@ -90,32 +108,80 @@ def pipeline_alg_bytes(n, P, R, st, Q=0):
     return b_in + b_sort + b_scan + b_out + b_merge + b_level
 
 
-def cpu_baseline(sample_n, cfg="C2"):
-    """The oracle (oracle/, the CPU restatement of the reference algorithms) on a bounded sample of the
-    same workload on this host, with 1 thread and with T threads (T in {1, nproc}; the deps
-    stage runs one single-threaded store per key-range shard as InMemoryCommandStore.SingleThread,
-    combined by PreAccept.reduce; merge and levels stay serial).  T = min(16, cpu_count): a GPU box's
-    share is 16 cores.  Test infrastructure: timed here as the reported baseline only."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sample_n, cfg="C2", reps=5):
+    """The oracle (oracle/, the CPU restatement of the reference algorithms) on a bounded sample of the same
+    workload on this host, SURVEY §8d / BASELINE.md §2: one warm-up, then the median of `reps` runs, with 1
+    thread and with T threads (T in {1, nproc}, capped at the box's 16-core share; the deps stage runs one
+    single-threaded store per key-range shard as InMemoryCommandStore.SingleThread, combined by
+    PreAccept.reduce; merge and levels stay serial).  The sample is the first `sample_n` txns of the step's own
+    generator (seeded identically): per-txn work is uniform along a C2/C3 batch, so the rate extrapolates to
+    the full batch.  Test infrastructure: timed here as the reported baseline only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     b = workload.config(cfg, n=sample_n)
     name = cfg
     cfg = abi.make_config(WINDOW, REPLICAS, DROP_P, workload.SEEDS[name])
     flags = O.FLAG_PRUNE | O.FLAG_MERGE | O.FLAG_LEVELS
-    runs = {}
+    nproc = os.cpu_count() or 1
     # the threaded restatement shards key txns only (range txns span stores: single-threaded oracle)
-    tset = {1} if b.get("range_off") is not None else {1, max(1, min(16, os.cpu_count() or 1))}
+    tset = {1} if b.get("range_off") is not None else {1, max(1, min(16, nproc))}
+    runs = {}
     for threads in sorted(tset):
-        s = O.OracleResult(b, cfg, flags, threads=threads).stats()
-        runs[threads] = (s["t_deps"] + s["t_merge"] + s["t_levels"], s)
+        O.OracleResult(b, cfg, flags, threads=threads).stats()          # warm-up
+        ts = []
+        for _ in range(reps):
+            s = O.OracleResult(b, cfg, flags, threads=threads).stats()
+            ts.append((s["t_deps"] + s["t_merge"] + s["t_levels"], s))
+        ts.sort(key=lambda x: x[0])
+        runs[threads] = ts[len(ts) // 2]
     T = max(runs)
     t, s = runs[T]
     t1 = runs[1][0]
     return {"value": sample_n / t, "unit": "txn/s", "cores": T, "kind": "port",
-            "single_thread_value": sample_n / t1,
-            "sample": "%s generator, first %d txns (seed %#x), PreAccept deps x%d views + Deps.merge + "
-                      "exec levels; %d threads %.1f s (deps %.1f, merge %.1f, levels %.1f); 1 thread %.1f s"
-                      % (name, sample_n, workload.SEEDS[name], REPLICAS, T, t, s["t_deps"], s["t_merge"], s["t_levels"], t1)}
+            "single_thread_value": sample_n / t1, "nproc": nproc, "cpu_model": cpu_model(), "median_of": reps,
+            "warmup": 1,
+            "sample": "%s generator, first %d txns of the same seeded batch (seed %#x; the rate extrapolates to the "
+                      "full batch), PreAccept deps x%d views + Deps.merge + exec levels, oracle with CFK pruning "
+                      "(restatement, not the Java reference: byId is built up front and levels are one sweep); "
+                      "median of %d after 1 warm-up: %d threads %.2f s (deps %.2f, merge %.2f, levels %.2f), "
+                      "1 thread %.2f s"
+                      % (name, sample_n, workload.SEEDS[name], REPLICAS, reps, T, t, s["t_deps"], s["t_merge"],
+                         s["t_levels"], t1)}
+
+
+def end_to_end(eng, batch, steps):
+    """The C-ABI round trip a host pays per batch (GPU wall time including host<->device copies):
+    ad_load_batch (H2D of the SoA batch), ad_run_pipeline, then the merged Deps of every class paged back
+    (ad_fetch_rows over the whole batch) and the levels + order (ad_fetch_levels).  Reported next to the
+    device-resident rate; not the headline value."""
+    n = batch["n"]
+    h2d = sum(np.asarray(batch[f]).nbytes for f in abi.BATCH_FIELDS if batch.get(f) is not None)
+    d2h = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.load(batch)
+        eng.run_pipeline()
+        d2h = 0
+        for c in range(abi.NUM_CLASSES):
+            csr = eng.fetch_rows(REPLICAS, c, 0, n)
+            d2h += sum(getattr(csr, f).nbytes for f in ("key_off", "keys", "k2t_off", "k2t", "txn_off", "txns"))
+        lv, order = eng.fetch_levels()
+        d2h += lv.nbytes + order.nbytes
+    dt = (time.perf_counter() - t0) / steps
+    return {"ms_per_step": dt * 1e3, "value": n / dt, "unit": "txn/s", "h2d_bytes": h2d, "d2h_bytes": d2h,
+            "steps": steps,
+            "what": "ad_load_batch + ad_run_pipeline + ad_fetch_rows(merged Deps, 3 classes) + ad_fetch_levels"}
 
 
 def trace_roofline(eng, run_step, n, P, large=False):
@@ -129,6 +195,9 @@ def trace_roofline(eng, run_step, n, P, large=False):
     st = eng.last_times()
     cands = [k for k in brk if alg_bytes(k, brk[k][0], brk[k][2], n, P, REPLICAS, st, large) is not None]
     dom = max(cands, key=lambda k: brk[k][1])
+    top = max(brk, key=lambda k: brk[k][1])
+    if top != dom:
+        print("note: the top traced kernel %s has no byte model in this config; roofline on %s" % (top, dom), file=sys.stderr)
     return dom, brk, st
 
 
@@ -145,21 +214,30 @@ def roofline_of(eng, dom, n, P, st, large=False, pmc=True):
             "alg_bytes_per_launch": ab / calls, "avg_launch_ms": ms / calls, "launches": calls}
 
 
-ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol (profiles/*_pmc.json keys)
+ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profiles/*_pmc.json keys)
     "k_deps_walk<fill>": "ad::k_deps_walk<3, true>", "k_deps_walk<count>": "ad::k_deps_walk<3, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
     "k_gather_entries": "ad::k_gather_entries", "k_txn_layout": "ad::k_txn_layout",
     "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<6>",
+    "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
+    # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
+    # are shared fill/copy kernels and are not attributed)
+    "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_step", "ad::k_chain_rank", "ad::k_chain_check",
+                    "ad::k_chain_links", "ad::k_frontier_collect", "ad::k_kahn_small"),
+    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<6>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<6>, 1024>",
+                     "ad::k_scan_apply<ad::OffsetsOp<6>, 256, 4>"),
+    "order_sort": ("ad::k_window_rank", "ad::k_rank_check"),
 }
 
 
 def pmc_traffic(kernel):
-    """HBM-side bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
-    written by profiles/collect.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3 passes of this bench).
-    The largest-grid dispatch of the kernel is the batch-sized one.  FETCH_SIZE is reported as counted
-    (Infinity-Cache hits included).  FETCH_SIZE is divided by the file's streaming-read calibration (bytes
-    counted per algorithmic byte of k_radix_hist's coalesced 4-byte key reads: 0.50 on gfx950, the guide's
-    "1/2 of wide streams" also holds at 4 B/lane); random accesses are not calibrated.  None if absent."""
+    """HBM-side bytes per launch (per pipeline step for a composite region) of `kernel` from the newest committed
+    PMC summary (profiles/*_pmc.json, written by profiles/collect.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3
+    passes of this bench).  For a single kernel the largest-grid dispatch is the batch-sized one; a composite
+    region sums its member kernels' (mean x dispatches) and divides by the dispatches of k_pack (once per
+    pipeline step).  FETCH_SIZE is divided by the file's streaming-read calibration (bytes counted per
+    algorithmic byte of k_radix_hist's coalesced 4-byte key reads: 0.50 on gfx950, the guide's "1/2 of wide
+    streams" also holds at 4 B/lane); random accesses are not calibrated.  None if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     want = ROCPROF_NAME.get(kernel)
@@ -168,16 +246,29 @@ def pmc_traffic(kernel):
     with open(files[-1]) as f:
         doc = json.load(f)
     cal = (doc.get("calibration_4B_stream_read") or {}).get("fetch_per_alg_byte") or 1.0
-    best = None
-    for k, e in doc.get("kernels", {}).items():
-        name, grid = k.rsplit(" grid=", 1)
-        if name == want and "FETCH_SIZE_KB_mean" in e and "WRITE_SIZE_KB_mean" in e:
-            if best is None or int(grid) > best[0]:
-                # FETCH_SIZE corrected by the measured streaming-read calibration (gfx950 counts 1/2)
-                best = (int(grid), (e["FETCH_SIZE_KB_mean"] / cal + e["WRITE_SIZE_KB_mean"]) * 1024.0)
-    if best is None:
+    ks = doc.get("kernels", {})
+
+    def entries(name):
+        for k, e in ks.items():
+            nm, grid = k.rsplit(" grid=", 1)
+            if nm == name and "FETCH_SIZE_KB_mean" in e and "WRITE_SIZE_KB_mean" in e:
+                yield int(grid), e
+
+    def bytes_of(e):
+        return (e["FETCH_SIZE_KB_mean"] / cal + e["WRITE_SIZE_KB_mean"]) * 1024.0
+
+    if isinstance(want, str):
+        best = max(entries(want), key=lambda ge: ge[0], default=None)
+        return (None, None) if best is None else (bytes_of(best[1]), os.path.relpath(files[-1], ROOT))
+    steps = sum(e["dispatches"] for _, e in entries("ad::k_pack"))
+    if not steps:
         return None, None
-    return best[1], os.path.relpath(files[-1], ROOT)
+    tot, seen = 0.0, False
+    for name in want:
+        for _, e in entries(name):
+            tot += bytes_of(e) * e["dispatches"]
+            seen = True
+    return (tot / steps, os.path.relpath(files[-1], ROOT)) if seen else (None, None)
 
 
 def print_breakdown(brk, st):
@@ -288,6 +379,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="txns in the CPU-baseline sample (default 262144; C4: 16384; 0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel breakdown to stderr")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false",
+                    help="skip the end-to-end (H2D + pipeline + D2H through the C-ABI) side measurement")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl", help="N>1 exchange: RCCL over xGMI or host/gloo")
     args = ap.parse_args()
 
@@ -342,6 +435,7 @@ def main():
         mc = {"bound": "hbm", "avg_ms": ms / calls, "launches": calls, "alg_bytes": ab, "achieved_GBps": gbs,
               "frac": gbs / HBM_PEAK_GBS}
     eng.set_trace(0)
+    e2e = end_to_end(eng, batch, max(1, min(args.steps, 3))) if args.e2e and Q == 0 else None
     ms_per_step = dt * 1e3 / args.steps
     value = n * args.steps / dt
     pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st, Q) / (dt / args.steps) / 1e9
@@ -366,9 +460,10 @@ def main():
                      "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
                      "level_iterations": st["level_iterations"]},
         "max_conflicts": mc,
+        "end_to_end": e2e,
         "cpu_baseline": None,
     }
-    sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 18)
+    sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 17)
     if rank == 0 and world == 1 and sample > 0:
         out["cpu_baseline"] = cpu_baseline(sample, cfgname)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -71,11 +71,15 @@ def lib():
         L.ad_reset_kernel_stats.argtypes = [vp]
         L.ad_kernel_units.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64)]
         L.ad_shard_bounds.argtypes = [C.POINTER(C.c_uint64), C.c_size_t, C.c_uint32, C.POINTER(C.c_uint64)]
+        L.ad_max_conflicts_carry.argtypes = [vp, C.c_size_t, vp, vp, vp, vp]
+        L.ad_max_conflicts_ts.argtypes = [vp, vp, vp, vp, vp]
+        L.ad_max_conflicts_export.argtypes = [vp, C.POINTER(C.c_size_t), vp, vp, vp, vp]
         _LIB = L
     return _LIB
 
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
+            "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export",
             "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
@@ -197,6 +201,39 @@ class DepsEngine:
         fast = np.zeros((R, max(n, 1)), np.uint8)
         self._check(lib().ad_max_conflicts(self.h, rank.ctypes.data, fast.ctypes.data), "ad_max_conflicts")
         return rank[:, :n], fast[:, :n]
+
+    def max_conflicts_carry(self, table):
+        """The store's MaxConflicts map from earlier batches: (keys u64 ascending, msb, lsb, node) arrays."""
+        k, m, l, nd = (np.ascontiguousarray(table[0], np.uint64), np.ascontiguousarray(table[1], np.uint64),
+                       np.ascontiguousarray(table[2], np.uint64), np.ascontiguousarray(table[3], np.int32))
+        self._carry = (k, m, l, nd)
+        self._check(lib().ad_max_conflicts_carry(self.h, len(k), k.ctypes.data, m.ctypes.data, l.ctypes.data,
+                                                 nd.ctypes.data), "ad_max_conflicts_carry")
+
+    def max_conflicts_ts(self):
+        """maxConflicts.get(keys) per view and txn over the carry and the batch as raw timestamps:
+        (msb [R, n], lsb [R, n], node [R, n], fast [R, n]); Timestamp.NONE = (0, 0, 0)."""
+        R, n = self.replicas, self.n
+        msb = np.zeros((R, max(n, 1)), np.uint64)
+        lsb = np.zeros((R, max(n, 1)), np.uint64)
+        node = np.zeros((R, max(n, 1)), np.int32)
+        fast = np.zeros((R, max(n, 1)), np.uint8)
+        self._check(lib().ad_max_conflicts_ts(self.h, msb.ctypes.data, lsb.ctypes.data, node.ctypes.data, fast.ctypes.data),
+                    "ad_max_conflicts_ts")
+        return msb[:, :n], lsb[:, :n], node[:, :n], fast[:, :n]
+
+    def max_conflicts_export(self):
+        """The MaxConflicts table after this batch: (keys, msb, lsb, node)."""
+        m = C.c_size_t()
+        self._check(lib().ad_max_conflicts_export(self.h, C.byref(m), None, None, None, None), "ad_max_conflicts_export")
+        k = np.zeros(max(m.value, 1), np.uint64)
+        ms = np.zeros(max(m.value, 1), np.uint64)
+        ls = np.zeros(max(m.value, 1), np.uint64)
+        nd = np.zeros(max(m.value, 1), np.int32)
+        self._check(lib().ad_max_conflicts_export(self.h, C.byref(m), k.ctypes.data, ms.ctypes.data, ls.ctypes.data,
+                                                  nd.ctypes.data), "ad_max_conflicts_export")
+        c = m.value
+        return k[:c], ms[:c], ls[:c], nd[:c]
 
     def run_pipeline(self):
         self._check(lib().ad_run_pipeline(self.h), "ad_run_pipeline")

@@ -74,6 +74,7 @@ struct McArgs {
     const uint64_t* tx_ts;
     uint32_t* max_rank;        // [v * n + t]
     uint8_t* fast;             // [v * n + t]
+    uint32_t* local_rank;      // [v * n + t] the batch row holding the max (AD_RANK_NONE), or nullptr
 };
 
 template <int NV>
@@ -117,8 +118,118 @@ __global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
     for (int v = 0; v < NV; ++v) {
         // sharded stores answer in global arrival ranks (ascending with local rows: the tie rule is kept)
         a.max_rank[(size_t)v * a.n + t] = be[v] ? (a.gid ? a.gid[br[v]] : br[v]) : AD_RANK_NONE;
+        if (a.local_rank) a.local_rank[(size_t)v * a.n + t] = be[v] ? br[v] : AD_RANK_NONE;
         a.fast[(size_t)v * a.n + t] = (be[v] == 0 || t1 >= be[v]) ? 1 : 0;   // TxnId.compareTo(max) >= 0
     }
+}
+
+// ---- MaxConflicts carried across batches (the store's state from its earlier batches) ----------------------
+// A store's MaxConflicts map outlives a batch.  The host passes it in as a sorted table (key -> greatest
+// executeAt recorded), the witnessedAt inputs then fold it in as timestamps, and the table after the batch is
+// exported for the next one.  Timestamps are raw (msb, lsb, node) here: a carried value need not fit the
+// batch's packed ts64 range.
+struct Ts3 { uint64_t msb, lsb; int32_t node; };
+__device__ inline int ts3_cmp(const Ts3& a, const Ts3& b) {          // Timestamp.compareTo (:208-217)
+    if (a.msb != b.msb) return a.msb < b.msb ? -1 : 1;
+    const uint64_t ah = a.lsb >> 16, bh = b.lsb >> 16;
+    if (ah != bh) return ah < bh ? -1 : 1;
+    const uint32_t af = (uint32_t)(a.lsb & 0x1E), bf = (uint32_t)(b.lsb & 0x1E);
+    if (af != bf) return af < bf ? -1 : 1;
+    return a.node < b.node ? -1 : (a.node > b.node ? 1 : 0);
+}
+struct McCarryArgs {
+    size_t n;
+    int nv;
+    const uint32_t* key_off;
+    const uint64_t* keys;
+    const uint64_t *tm, *tl, *em, *el;       // batch TxnId / executeAt
+    const int32_t *tn, *en;
+    const uint32_t* local_rank;              // [v * n + t]
+    size_t m;                                 // carry table
+    const uint64_t *ck, *cm, *cl;
+    const int32_t* cn;
+    uint64_t *om, *ol;                       // [v * n + t] maxConflicts.get(keys) as a timestamp (NONE = 0, 0, 0)
+    int32_t* on;
+    uint8_t* fast;                           // [v * n + t]
+};
+__global__ __launch_bounds__(256) void k_mc_carry(McCarryArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    Ts3 cb{0, 0, 0};
+    bool has = false;
+    for (uint32_t p = a.key_off[t]; p < a.key_off[t + 1] && a.m; ++p) {
+        const uint64_t k = a.keys[p];
+        size_t lo = 0, hi = a.m;
+        while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (a.ck[mid] < k) lo = mid + 1; else hi = mid; }
+        if (lo < a.m && a.ck[lo] == k) {
+            const Ts3 c{a.cm[lo], a.cl[lo], a.cn[lo]};
+            if (!has || ts3_cmp(c, cb) > 0) { cb = c; has = true; }
+        }
+    }
+    const Ts3 me{a.tm[t], a.tl[t], a.tn[t]};
+    for (int v = 0; v < a.nv; ++v) {
+        const size_t o = (size_t)v * a.n + t;
+        const uint32_t r = a.local_rank[o];
+        Ts3 best = cb;
+        bool any = has;
+        if (r != AD_RANK_NONE) {
+            const Ts3 b{a.em[r], a.el[r], a.en[r]};
+            if (!any || ts3_cmp(b, best) > 0) { best = b; any = true; }
+        }
+        a.om[o] = any ? best.msb : 0ull;
+        a.ol[o] = any ? best.lsb : 0ull;
+        a.on[o] = any ? best.node : 0;
+        a.fast[o] = (!any || ts3_cmp(me, best) >= 0) ? 1 : 0;               // TxnId.compareTo(max) >= 0
+    }
+}
+// Export: the union of the carry table and the batch's per-key maxima (the recorded-entry prefix max at each
+// key segment's end), merged by key ranks into slots with gaps (a key in both lands on one slot), then
+// compacted.  slot[i] of a batch key = i + #carry keys below it; of a carry key = j + #batch keys below it.
+__global__ __launch_bounds__(256) void k_mc_export_slots(uint32_t U, const uint64_t* __restrict__ ukey, const uint32_t* __restrict__ useg,
+                                                         const uint64_t* __restrict__ pm_e, const uint32_t* __restrict__ pm_r,
+                                                         const uint64_t* __restrict__ em, const uint64_t* __restrict__ el,
+                                                         const int32_t* __restrict__ en, size_t m, const uint64_t* __restrict__ ck,
+                                                         const uint64_t* __restrict__ cm, const uint64_t* __restrict__ cl,
+                                                         const int32_t* __restrict__ cn, uint64_t* __restrict__ sk,
+                                                         uint64_t* __restrict__ sm, uint64_t* __restrict__ sl,
+                                                         int32_t* __restrict__ sn, uint8_t* __restrict__ used) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < U) {
+        const uint64_t k = ukey[i];
+        size_t lo = 0, hi = m;
+        while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (ck[mid] < k) lo = mid + 1; else hi = mid; }
+        const size_t slot = i + lo;
+        const uint32_t last = useg[i + 1] - 1;                       // the segment's last entry: prefix max of all
+        Ts3 b{0, 0, 0};
+        bool any = pm_e[last] != 0;
+        if (any) { const uint32_t r = pm_r[last]; b = Ts3{em[r], el[r], en[r]}; }
+        if (lo < m && ck[lo] == k) {
+            const Ts3 c{cm[lo], cl[lo], cn[lo]};
+            if (!any || ts3_cmp(c, b) > 0) { b = c; any = true; }
+        }
+        sk[slot] = k; sm[slot] = b.msb; sl[slot] = b.lsb; sn[slot] = b.node;
+        used[slot] = any ? 1 : 0;                                     // a key with nothing recorded stays out
+    } else if (i < U + m) {
+        const size_t j = i - U;
+        const uint64_t k = ck[j];
+        size_t lo = 0, hi = U;
+        while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (ukey[mid] < k) lo = mid + 1; else hi = mid; }
+        if (lo < U && ukey[lo] == k) return;                          // written by the batch key's thread
+        const size_t slot = j + lo;
+        sk[slot] = k; sm[slot] = cm[j]; sl[slot] = cl[j]; sn[slot] = cn[j];
+        used[slot] = 1;
+    }
+}
+// CompactFlagOp gives out[k] = the k-th used slot: gather them in slot (= key) order
+__global__ __launch_bounds__(256) void k_mc_export_gather(uint32_t count, const uint32_t* __restrict__ slot,
+                                                          const uint64_t* __restrict__ sk, const uint64_t* __restrict__ sm,
+                                                          const uint64_t* __restrict__ sl, const int32_t* __restrict__ sn,
+                                                          uint64_t* __restrict__ ok, uint64_t* __restrict__ om,
+                                                          uint64_t* __restrict__ ol, int32_t* __restrict__ on) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count) return;
+    const uint32_t i = slot[k];
+    ok[k] = sk[i]; om[k] = sm[i]; ol[k] = sl[i]; on[k] = sn[i];
 }
 
 }  // namespace ad

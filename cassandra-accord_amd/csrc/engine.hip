@@ -113,6 +113,11 @@ struct ad_handle {
     std::vector<Csr> sdeps;          // home-indexed per (view, class)
     Csr smerged[3];
     ncclComm_t comm = nullptr;
+    // MaxConflicts carried from earlier batches (ad_max_conflicts_carry): sorted keys + timestamps on the device
+    size_t mc_m = 0;
+    uint64_t *mc_ck = nullptr, *mc_cm = nullptr, *mc_cl = nullptr;
+    int32_t* mc_cn = nullptr;
+    bool mc_ready = false;           // the MaxConflicts scan of the current batch is on the device (export)
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
@@ -195,7 +200,8 @@ enum Slot : size_t {
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
     S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT, S_HSTORE, S_XRANK, S_XLIST, S_XOFF,
     S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
-    S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST,
+    S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST, S_MCLOCAL, S_MCCK, S_MCCM, S_MCCL, S_MCCN,
+    S_MCOM, S_MCOL, S_MCON, S_MCOF, S_MCSK, S_MCSM, S_MCSL, S_MCSN, S_MCSU, S_MCSP,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -261,7 +267,7 @@ void scan_offsets(ad_handle* h, const T* in, T* out, size_t n) {
 // key_off / ent_off / k2t_off of one batched CSR from per-txn (keys, entries) counts
 void csr_offsets(ad_handle* h, Csr& c, const uint32_t* nk, const uint32_t* ne) {
     const size_t n = h->n;
-    KScope ks(K_SCAN_OFFSETS);
+    KScope ks(K_CSR_OFFSETS, n);
     scan_offsets(h, nk, c.key_off, n);
     scan_offsets(h, ne, c.ent_off, n);
     if (n) device_scan(Sum2Op<uint32_t>{nk, ne, c.k2t_off, n}, n, (uint32_t*)h->scratch, h->st);
@@ -727,7 +733,7 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
         if (n > 0) merge_launch(a, np, false, kw[k], st);
     }
     if (n > 0) {
-        KScope ks(K_SCAN_OFFSETS);
+        KScope ks(K_MERGE_OFFSETS, n * (size_t)K);
         switch (K) {
             case 1: launch_multi_offsets<1>(h, n, mk, me, mu, out); break;
             case 2: launch_multi_offsets<2>(h, n, mk, me, mu, out); break;
@@ -1012,6 +1018,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     h->n = n; h->P = P; h->Q = Q;
     h->loaded = false;
     h->have_deps = h->have_merged = h->have_levels = false;
+    h->mc_ready = false;
     CK(dalloc(h, S_TM, &h->tm, n)); CK(dalloc(h, S_TL, &h->tl, n)); CK(dalloc(h, S_TN, &h->tn, n));
     CK(dalloc(h, S_EM, &h->em, n)); CK(dalloc(h, S_EL, &h->el, n)); CK(dalloc(h, S_EN, &h->en, n));
     CK(dalloc(h, S_ST, &h->status, n)); CK(dalloc(h, S_KOFF, &h->key_off, n + 1)); CK(dalloc(h, S_KEYS, &h->keys, P));
@@ -1093,16 +1100,14 @@ static int fetch_empty(ad_handle* h, ad_csr_out* out) {
 }
 
 // CommandStore.preaccept's maxConflicts.get(keys) per view (conflict_kernels.h), over the sorted entries the
-// deps stage left on the device.
-int ad_max_conflicts(ad_handle* h, uint32_t* max_rank, uint8_t* fast) {
-    if (!h) return AD_ERR_ARGUMENT;
+// deps stage left on the device: leaves max_rank / fast (and the batch-local rank) in their slots.
+static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_out, uint32_t** local_out) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
     if (h->Q > 0) return set_err(h, AD_ERR_UNSUPPORTED, "max conflicts: range txns are not supported");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     const size_t n = h->n, P = h->P;
     const int nv = (int)h->cfg.replicas;
-    if (n == 0) return AD_OK;
     hipStream_t st = h->st;
     McArgs a{};
     a.n = n; a.P = P;
@@ -1111,14 +1116,15 @@ int ad_max_conflicts(ad_handle* h, uint32_t* max_rank, uint8_t* fast) {
     a.window = h->cfg.window; a.thresh = ad_drop_threshold(h->cfg.drop_p); a.seed = h->cfg.seed;
     a.key_off = h->key_off; a.tx_ts = h->tx_ts;
     uint64_t* pm_e = nullptr;
-    uint32_t *pm_r = nullptr, *inv = nullptr, *rank = nullptr;
+    uint32_t *pm_r = nullptr, *inv = nullptr, *rank = nullptr, *local = nullptr;
     uint8_t* fst = nullptr;
     CK(dalloc(h, S_MCPE, &pm_e, std::max<size_t>(P, 1))); CK(dalloc(h, S_MCPR, &pm_r, std::max<size_t>(P, 1)));
     CK(dalloc(h, S_MCINV, &inv, std::max<size_t>(P, 1)));
-    CK(dalloc(h, S_MCRANK, &rank, n * nv)); CK(dalloc(h, S_MCFAST, &fst, n * nv));
-    a.pm_e = pm_e; a.pm_r = pm_r; a.inv = inv; a.max_rank = rank; a.fast = fst;
+    CK(dalloc(h, S_MCRANK, &rank, std::max<size_t>(n * nv, 1))); CK(dalloc(h, S_MCFAST, &fst, std::max<size_t>(n * nv, 1)));
+    if (local_out) CK(dalloc(h, S_MCLOCAL, &local, std::max<size_t>(n * nv, 1)));
+    a.pm_e = pm_e; a.pm_r = pm_r; a.inv = inv; a.max_rank = rank; a.fast = fst; a.local_rank = local;
     if (P > 0) CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<MaxConflictOp>(P))));
-    {
+    if (n > 0) {
         KScope ks(K_MAX_CONFLICTS, P);      // scan (+ inverse permutation) + per-txn walk and fold
         if (P > 0) {
             MaxConflictOp op{h->seg_start, h->e_meta, h->e_exec1, h->e_txn, h->sval, pm_e, pm_r, inv};
@@ -1127,10 +1133,115 @@ int ad_max_conflicts(ad_handle* h, uint32_t* max_rank, uint8_t* fast) {
         NV_DISPATCH(nv, launch_mc, a, st);
     }
     HIPCHK(h, hipGetLastError());
-    if (max_rank) HIPCHK(h, hipMemcpyAsync(max_rank, rank, n * nv * 4, hipMemcpyDeviceToHost, st));
-    if (fast) HIPCHK(h, hipMemcpyAsync(fast, fst, n * nv, hipMemcpyDeviceToHost, st));
+    h->mc_ready = true;
+    *rank_out = rank; *fast_out = fst;
+    if (local_out) *local_out = local;
+    return AD_OK;
+}
+
+int ad_max_conflicts(ad_handle* h, uint32_t* max_rank, uint8_t* fast) {
+    if (!h) return AD_ERR_ARGUMENT;
+    uint32_t* rank = nullptr;
+    uint8_t* fst = nullptr;
+    CK(run_max_conflicts(h, &rank, &fst, nullptr));
+    const size_t n = h->n, nv = h->cfg.replicas;
+    hipStream_t st = h->st;
+    if (max_rank && n) HIPCHK(h, hipMemcpyAsync(max_rank, rank, n * nv * 4, hipMemcpyDeviceToHost, st));
+    if (fast && n) HIPCHK(h, hipMemcpyAsync(fast, fst, n * nv, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     h->tracer.resolve();
+    return AD_OK;
+}
+
+int ad_max_conflicts_carry(ad_handle* h, size_t m, const uint64_t* keys, const uint64_t* msb, const uint64_t* lsb,
+                           const int32_t* node) {
+    if (!h || (m && (!keys || !msb || !lsb || !node))) return AD_ERR_ARGUMENT;
+    for (size_t i = 1; i < m; ++i)
+        if (keys[i] <= keys[i - 1]) return set_err(h, AD_ERR_ARGUMENT, "carried MaxConflicts keys must be strictly ascending");
+    hipSetDevice(h->device);
+    CK(dalloc(h, S_MCCK, &h->mc_ck, std::max<size_t>(m, 1))); CK(dalloc(h, S_MCCM, &h->mc_cm, std::max<size_t>(m, 1)));
+    CK(dalloc(h, S_MCCL, &h->mc_cl, std::max<size_t>(m, 1))); CK(dalloc(h, S_MCCN, &h->mc_cn, std::max<size_t>(m, 1)));
+    if (m) {
+        HIPCHK(h, hipMemcpyAsync(h->mc_ck, keys, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mc_cm, msb, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mc_cl, lsb, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mc_cn, node, m * 4, hipMemcpyHostToDevice, h->st));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->mc_m = m;
+    return AD_OK;
+}
+
+int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast) {
+    if (!h) return AD_ERR_ARGUMENT;
+    uint32_t *rank = nullptr, *local = nullptr;
+    uint8_t* fst = nullptr;
+    CK(run_max_conflicts(h, &rank, &fst, &local));
+    const size_t n = h->n, nv = h->cfg.replicas;
+    hipStream_t st = h->st;
+    uint64_t *om = nullptr, *ol = nullptr;
+    int32_t* on = nullptr;
+    uint8_t* of = nullptr;
+    CK(dalloc(h, S_MCOM, &om, std::max<size_t>(n * nv, 1))); CK(dalloc(h, S_MCOL, &ol, std::max<size_t>(n * nv, 1)));
+    CK(dalloc(h, S_MCON, &on, std::max<size_t>(n * nv, 1))); CK(dalloc(h, S_MCOF, &of, std::max<size_t>(n * nv, 1)));
+    if (n) {
+        McCarryArgs c{};
+        c.n = n; c.nv = (int)nv; c.key_off = h->key_off; c.keys = h->keys;
+        c.tm = h->tm; c.tl = h->tl; c.tn = h->tn; c.em = h->em; c.el = h->el; c.en = h->en;
+        c.local_rank = local; c.m = h->mc_m; c.ck = h->mc_ck; c.cm = h->mc_cm; c.cl = h->mc_cl; c.cn = h->mc_cn;
+        c.om = om; c.ol = ol; c.on = on; c.fast = of;
+        KScope ks(K_MAX_CONFLICTS);
+        k_mc_carry<<<ceil_div((long)n, 256), 256, 0, st>>>(c);
+        HIPCHK(h, hipGetLastError());
+        if (msb) HIPCHK(h, hipMemcpyAsync(msb, om, n * nv * 8, hipMemcpyDeviceToHost, st));
+        if (lsb) HIPCHK(h, hipMemcpyAsync(lsb, ol, n * nv * 8, hipMemcpyDeviceToHost, st));
+        if (node) HIPCHK(h, hipMemcpyAsync(node, on, n * nv * 4, hipMemcpyDeviceToHost, st));
+        if (fast) HIPCHK(h, hipMemcpyAsync(fast, of, n * nv, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    h->tracer.resolve();
+    return AD_OK;
+}
+
+int ad_max_conflicts_export(ad_handle* h, size_t* m_out, uint64_t* keys, uint64_t* msb, uint64_t* lsb, int32_t* node) {
+    if (!h || !m_out) return AD_ERR_ARGUMENT;
+    if (!h->mc_ready) return set_err(h, AD_ERR_STATE, "ad_max_conflicts_export: run ad_max_conflicts(_ts) on this batch first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const uint32_t U = h->P ? h->hprm.n_keys_u : 0;
+    const size_t S = (size_t)U + h->mc_m;
+    uint64_t *sk, *sm, *sl, *ok_, *om_, *ol_;
+    int32_t *sn, *on_;
+    uint8_t* su;
+    uint32_t *sp, *tot;
+    CK(dalloc(h, S_MCSK, &sk, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCSM, &sm, std::max<size_t>(S, 1)));
+    CK(dalloc(h, S_MCSL, &sl, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCSN, &sn, std::max<size_t>(S, 1)));
+    CK(dalloc(h, S_MCSU, &su, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCSP, &sp, std::max<size_t>(S, 1) + 16));
+    CK(dalloc(h, S_MCOM, &ok_, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCOL, &om_, std::max<size_t>(S, 1)));
+    CK(dalloc(h, S_MCON, &on_, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCOF, &ol_, std::max<size_t>(S, 1)));
+    tot = sp + std::max<size_t>(S, 1);
+    uint32_t count = 0;
+    if (S) {
+        HIPCHK(h, hipMemsetAsync(su, 0, S, st));
+        k_mc_export_slots<<<ceil_div((long)S, 256), 256, 0, st>>>(U, h->ukey, h->useg, (const uint64_t*)h->bufs[S_MCPE].p,
+                                                                   (const uint32_t*)h->bufs[S_MCPR].p, h->em, h->el, h->en,
+                                                                   h->mc_m, h->mc_ck, h->mc_cm, h->mc_cl, h->mc_cn, sk, sm, sl, sn, su);
+        CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<CompactFlagOp>(S))));
+        device_scan(CompactFlagOp{su, sp, tot, S}, S, (uint32_t*)h->scratch, st);
+        HIPCHK(h, hipMemcpyAsync(&count, tot, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    *m_out = count;
+    if (!keys) return AD_OK;
+    if (count) {
+        // CompactFlagOp wrote out[rank] = slot: gather the used slots in order
+        k_mc_export_gather<<<ceil_div((long)count, 256), 256, 0, st>>>(count, sp, sk, sm, sl, sn, ok_, om_, ol_, on_);
+        HIPCHK(h, hipMemcpyAsync(keys, ok_, count * 8, hipMemcpyDeviceToHost, st));
+        if (msb) HIPCHK(h, hipMemcpyAsync(msb, om_, count * 8, hipMemcpyDeviceToHost, st));
+        if (lsb) HIPCHK(h, hipMemcpyAsync(lsb, ol_, count * 8, hipMemcpyDeviceToHost, st));
+        if (node) HIPCHK(h, hipMemcpyAsync(node, on_, count * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
     return AD_OK;
 }
 

@@ -1319,7 +1319,11 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         auto block_path = [&]() -> int {
             int depth = 0;
             uint32_t rounds = 0;
-            const int rc = run_block_levels(ls, ls.bl, in, st, &depth, &rounds, err);
+            int rc;
+            {
+                KScope ks(K_BLOCK_LEVELS, P);
+                rc = run_block_levels(ls, ls.bl, in, st, &depth, &rounds, err);
+            }
             if (rc != AD_OK) return rc;
             ls.bl_rounds = rounds;
             ls.bl_used = true;
@@ -1350,8 +1354,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             int lv = 0;
             bool fallback = false;
             const bool xedges = has_b || has_c;
+            bool go_blocks = false;             // deep key chains found: leave the Kahn region for the block path
             {
-                KScope ks(K_KAHN);
+                KScope ks(K_KAHN, P);
                 hipMemsetAsync(ls.indeg, 0, n * 4, st);
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
                 // (c) searches every chain in executeAt order, singletons included
@@ -1454,7 +1459,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                             return AD_ERR_UNSUPPORTED;
                         }
                         if (host[7] && !long_done) {      // the batch's wavefronts were gated off: rebuild, restart
-                            if (pure) return block_path();   // deep key chains: executeAt blocks, not wavefronts
+                            if (pure) { go_blocks = true; break; }   // deep key chains: executeAt blocks, not wavefronts
                             if (!long_build()) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
                             hipMemcpyAsync(ls.rem, ls.indeg, n * 4, hipMemcpyDeviceToDevice, st);
                             host[7] = 0;
@@ -1490,6 +1495,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     more = false;
                 }
             }
+            if (go_blocks) return block_path();
             if (!fallback) {
                 *iters = lv;
                 // the wavefront count gives the level range: the order needs no host sync of its own

@@ -213,6 +213,23 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
 #define AD_RANK_NONE 0xFFFFFFFFu
 int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8_t* fast /* [replicas*n] */);
 
+/* Stage 1b across batches — the store's MaxConflicts map outlives a batch (local/MaxConflicts.java:32-96,
+ * CommandStore.updateMaxConflicts :282-291).  The host carries it between batches as a table sorted by key:
+ *   ad_max_conflicts_carry   the table from earlier batches (keys strictly ascending; m = 0 clears it); it applies
+ *                            to every later ad_max_conflicts_ts on this handle and to the export
+ *   ad_max_conflicts_ts      per view v and txn i: maxConflicts.get(keys of i) over the carried table AND the batch
+ *                            (as ad_max_conflicts), as a raw Timestamp (msb, lsb, node; Timestamp.NONE = 0, 0, 0),
+ *                            and fast = TxnId >= it (CommandStore.java:343).  Arrays [replicas*n]; NULL skips one
+ *   ad_max_conflicts_export  the table after this batch: the carry merged with every key's greatest recorded
+ *                            executeAt in the batch (final statuses; TRANSITIVELY_KNOWN / INVALID unrecorded).
+ *                            Two calls: keys == NULL returns *m only.  Needs ad_max_conflicts(_ts) on the batch.
+ * A txn that PreAccepts in a later batch than a larger-TxnId txn (arrival order != TxnId order,
+ * PreAcceptTest.multiKeyTimestampUpdate) sees it through the carry. */
+int  ad_max_conflicts_carry(ad_handle* h, size_t m, const uint64_t* keys, const uint64_t* msb, const uint64_t* lsb,
+                            const int32_t* node);
+int  ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast);
+int  ad_max_conflicts_export(ad_handle* h, size_t* m, uint64_t* keys, uint64_t* msb, uint64_t* lsb, int32_t* node);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Device-resident pipeline (benchmark / service loop): stage 1 + 2 + 3 with no host copies of */
 /* outputs.  Kernel timing: HIP events on the handle's stream.                                 */

@@ -727,6 +727,77 @@ int oracle_max_conflicts(const ad_batch* b, const ad_config* c, uint32_t* max_ra
     }
 }
 
+/* MaxConflicts carried across batches (ad_max_conflicts_carry / _ts / _export): the carry table is the store's
+ * MaxConflicts map from earlier batches (local/MaxConflicts.java:32-96); maxConflicts.get(keys) of a batch txn
+ * is the greatest of the carried values on its keys and the batch answer above (Timestamp::max). */
+static bool carry_lookup(size_t m, const uint64_t* ck, const uint64_t* cm, const uint64_t* cl, const int32_t* cn,
+                         uint64_t k, Ts* out) {
+    const uint64_t* it = std::lower_bound(ck, ck + m, k);
+    if (it == ck + m || *it != k) return false;
+    const size_t x = (size_t)(it - ck);
+    *out = Ts{cm[x], cl[x], cn[x]};
+    return true;
+}
+
+int oracle_max_conflicts_ts(const ad_batch* b, const ad_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
+                            const uint64_t* cl, const int32_t* cn, uint64_t* om, uint64_t* ol, int32_t* on, uint8_t* fast) {
+    try {
+        Batch B(b);
+        if (B.range_off[B.n] > 0) return AD_ERR_UNSUPPORTED;
+        Config cfg;
+        cfg.window = c->window; cfg.replicas = c->replicas ? c->replicas : 1; cfg.seed = c->seed;
+        cfg.drop_thresh = ad_drop_threshold(c->drop_p);
+        Oracle o(B, cfg, false);
+        const uint32_t n = (uint32_t)B.n;
+        for (uint32_t i = 0; i < n; ++i) {
+            bool has = false;
+            Ts cb{0, 0, 0};
+            for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
+                Ts t;
+                if (carry_lookup(m, ck, cm, cl, cn, B.keys[p], &t) && (!has || ts_cmp(t, cb) > 0)) { cb = t; has = true; }
+            }
+            for (uint32_t v = 0; v < cfg.replicas; ++v) {
+                const uint32_t r = o.max_conflict(i, v);
+                Ts best = cb;
+                bool any = has;
+                if (r != UINT32_MAX && (!any || ts_cmp(B.ex[r], best) > 0)) { best = B.ex[r]; any = true; }
+                const size_t x = (size_t)v * n + i;
+                om[x] = any ? best.msb : 0; ol[x] = any ? best.lsb : 0; on[x] = any ? best.node : 0;
+                fast[x] = (!any || ts_cmp(B.tx[i], best) >= 0) ? 1 : 0;
+            }
+        }
+        return AD_OK;
+    } catch (const std::exception&) {
+        return AD_ERR_ARGUMENT;
+    }
+}
+
+/* The MaxConflicts table after the batch: carry merged with, per key, the greatest executeAt of the batch txns
+ * the store recorded there (globally visible, not TRANSITIVELY_KNOWN / INVALID).  out == NULL: size only. */
+int oracle_max_conflicts_export(const ad_batch* b, size_t m, const uint64_t* ck, const uint64_t* cm, const uint64_t* cl,
+                                const int32_t* cn, size_t* count, uint64_t* ok, uint64_t* om, uint64_t* ol, int32_t* on) {
+    try {
+        Batch B(b);
+        std::map<uint64_t, Ts> t;
+        for (size_t x = 0; x < m; ++x) t[ck[x]] = Ts{cm[x], cl[x], cn[x]};
+        for (uint32_t i = 0; i < (uint32_t)B.n; ++i) {
+            if (!manages(B.tx[i]) || B.st[i] == AD_ST_TRANSITIVELY_KNOWN || B.st[i] == AD_ST_INVALID) continue;
+            for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
+                auto it = t.find(B.keys[p]);
+                if (it == t.end()) t[B.keys[p]] = B.ex[i];
+                else if (ts_cmp(B.ex[i], it->second) > 0) it->second = B.ex[i];
+            }
+        }
+        *count = t.size();
+        if (!ok) return AD_OK;
+        size_t x = 0;
+        for (auto& e : t) { ok[x] = e.first; om[x] = e.second.msb; ol[x] = e.second.lsb; on[x] = e.second.node; ++x; }
+        return AD_OK;
+    } catch (const std::exception&) {
+        return AD_ERR_ARGUMENT;
+    }
+}
+
 static const Flat* pick(const oracle_result* r, int stage, uint32_t view, uint32_t cls) {
     if (cls >= AD_NUM_CLASSES) return nullptr;
     if (stage == 0) { if (view >= r->replicas || r->deps.empty()) return nullptr; return &r->deps[view * 3 + cls]; }

@@ -39,6 +39,11 @@ def lib():
         L.oracle_free.argtypes = [C.c_void_p]
         L.oracle_max_conflicts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.POINTER(C.c_uint32),
                                            C.POINTER(C.c_uint8)]
+        vp = C.c_void_p
+        L.oracle_max_conflicts_ts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_size_t, vp, vp, vp, vp,
+                                              vp, vp, vp, vp]
+        L.oracle_max_conflicts_export.argtypes = [C.POINTER(abi.AdBatch), C.c_size_t, vp, vp, vp, vp, C.POINTER(C.c_size_t),
+                                                  vp, vp, vp, vp]
         L.oracle_build.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_size_t,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]
@@ -114,6 +119,47 @@ def max_conflicts(batch, cfg):
     if rc != abi.AD_OK:
         raise ValueError("oracle_max_conflicts rc=%d" % rc)
     return rank[:, :n].copy(), fast[:, :n].copy()
+
+
+EMPTY_CARRY = (np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.int32))
+
+
+def _carry(table):
+    table = EMPTY_CARRY if table is None else table
+    return tuple(np.ascontiguousarray(a, dt) for a, dt in zip(table, (np.uint64, np.uint64, np.uint64, np.int32)))
+
+
+def max_conflicts_ts(batch, cfg, carry=None):
+    """maxConflicts.get(keys) over a carried MaxConflicts table + the batch, as timestamps:
+    (msb [R, n], lsb [R, n], node [R, n], fast [R, n])."""
+    b = abi.make_batch(batch)
+    n, R = batch["n"], cfg.replicas
+    ck, cm, cl, cn = _carry(carry)
+    om = np.zeros((R, max(n, 1)), np.uint64)
+    ol = np.zeros((R, max(n, 1)), np.uint64)
+    on = np.zeros((R, max(n, 1)), np.int32)
+    fa = np.zeros((R, max(n, 1)), np.uint8)
+    rc = lib().oracle_max_conflicts_ts(C.byref(b), C.byref(cfg), len(ck), ck.ctypes.data, cm.ctypes.data, cl.ctypes.data,
+                                       cn.ctypes.data, om.ctypes.data, ol.ctypes.data, on.ctypes.data, fa.ctypes.data)
+    if rc != abi.AD_OK:
+        raise ValueError("oracle_max_conflicts_ts rc=%d" % rc)
+    return om[:, :n].copy(), ol[:, :n].copy(), on[:, :n].copy(), fa[:, :n].copy()
+
+
+def max_conflicts_export(batch, carry=None):
+    """The MaxConflicts table after the batch: (keys, msb, lsb, node)."""
+    b = abi.make_batch(batch)
+    ck, cm, cl, cn = _carry(carry)
+    m = C.c_size_t()
+    rc = lib().oracle_max_conflicts_export(C.byref(b), len(ck), ck.ctypes.data, cm.ctypes.data, cl.ctypes.data,
+                                           cn.ctypes.data, C.byref(m), None, None, None, None)
+    if rc != abi.AD_OK:
+        raise ValueError("oracle_max_conflicts_export rc=%d" % rc)
+    out = (np.zeros(max(m.value, 1), np.uint64), np.zeros(max(m.value, 1), np.uint64), np.zeros(max(m.value, 1), np.uint64),
+           np.zeros(max(m.value, 1), np.int32))
+    lib().oracle_max_conflicts_export(C.byref(b), len(ck), ck.ctypes.data, cm.ctypes.data, cl.ctypes.data, cn.ctypes.data,
+                                      C.byref(m), *(a.ctypes.data for a in out))
+    return tuple(a[:m.value].copy() for a in out)
 
 
 def build_relation(keys, vals):

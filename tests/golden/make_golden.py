@@ -17,8 +17,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import oracle as O  # noqa: E402
+import refgen as R  # noqa: E402
 from accord_amd import abi, workload  # noqa: E402
 
 CSR_FIELDS = ("key_off", "keys", "k2t_off", "k2t", "txn_off", "txns")
@@ -43,7 +45,90 @@ CASES = {
     "hot_keys": (lambda: workload.generate(2000, keys_per_txn=2, keyspace=5, slow_frac=0.5, bump_max=300, seed=11),
                  (4, 2, 0.3, 11), True),
     "mixed_kinds": (lambda: mixed_kinds(1500, 12), (8, 3, 0.2, 12), False),
+    # the reference's own seeded RangeDepsTest inputs (tests/refgen.py; tests/test_oracle_rangedeps.py checks the
+    # oracle on them against RangeDepsTest.Validate's model): testRandom's first recorded seed and the first
+    # nemesis layout of testNemesisRanges' recorded seed, as engine batches of range Writes + Validate's queries
+    "rangedeps_random": (lambda: rangedeps_case("random"), (0, 1, 0.0, 1), True),
+    "rangedeps_nemesis": (lambda: rangedeps_case("nemesis"), (0, 1, 0.0, 1), True),
 }
+
+
+def rangedeps_case(which):
+    if which == "random":
+        r = R.JavaRandom(R.RANGEDEPS_RANDOM_SEEDS[0])
+        gen = R.GenerateRanges(1000, 0.01, 0.3, 0.1, 1.0)
+        canonical = R.rangedeps_generate(r, gen, 100, 1000)
+    else:
+        r = R.JavaRandom(R.RANGEDEPS_NEMESIS_SEED)
+        width, count = 1 + r.nextInt(511), 1 + r.nextInt(99)
+        canonical, gen = R.rangedeps_nemesis(width, count, 1000, 1)
+    queries = R.rangedeps_validate_queries(r, gen, canonical)
+    if which == "random":
+        queries = queries[:1500] + queries[-10:]     # a prefix of Validate's queries + its 10 slices (fixture size)
+    return R.rangedeps_batch(canonical, queries)
+
+
+KEYDEPS_MERGE_SEEDS = range(64)
+KEYDEPS_MERGE_R = 4
+
+
+def keydeps_merge_case():
+    """KeyDepsTest.testMerge (test/primitives/KeyDepsTest.java:115-126) inputs for seeds 0..63 (tests/refgen.py)
+    as ONE batch for ad_merge_host: the batch rows are every TxnId of the cases (TxnId order, so a TxnId's rank
+    is its row); row c holds case c's list of Deps as its R = 4 replies (empty replies pad shorter lists).
+    Expected: row c of the merged Deps = the oracle's LinearMerger fold, which tests/test_oracle_keydeps.py pins
+    to KeyDepsTest's canonical TreeMap model (testMergedProperty)."""
+    cases = [R.testmerge_inputs(seed) for seed in KEYDEPS_MERGE_SEEDS]
+    allt = sorted({t for deps in cases for d in deps for st in d.canonical.values() for t in st}, key=R.txn_order_key)
+    rank = {t: i for i, t in enumerate(allt)}
+    n = len(allt)
+    assert n >= len(cases)
+    msb = np.array([t[0] for t in allt], np.uint64)
+    lsb = np.array([t[1] for t in allt], np.uint64)
+    node = np.array([t[2] for t in allt], np.int32)
+    batch = {"n": n, "txn_msb": msb, "txn_lsb": lsb, "txn_node": node, "exec_msb": msb.copy(), "exec_lsb": lsb.copy(),
+             "exec_node": node.copy(), "status": np.full(n, abi.ST_APPLIED, np.uint8),
+             "key_off": np.zeros(n + 1, np.uint32), "keys": np.zeros(0, np.uint64),
+             "range_off": None, "range_start": None, "range_end": None}
+    rows = [[O.EMPTY_RELATION] * n for _ in range(KEYDEPS_MERGE_R)]
+    merged = [O.EMPTY_RELATION] * n
+    for c, deps in enumerate(cases):
+        acc = O.EMPTY_RELATION
+        for v, d in enumerate(deps):
+            if d.canonical:
+                pairs = d.add_order()
+                rel = O.build_relation(np.array([k for k, _ in pairs], np.uint64),
+                                       np.array([rank[t] for _, t in pairs], np.uint32))
+            else:
+                rel = O.EMPTY_RELATION
+            rows[v][c] = rel
+            acc = O.union_relation(acc, rel)
+        merged[c] = acc
+    return batch, [relations_to_csr(rs) for rs in rows], relations_to_csr(merged)
+
+
+def relations_to_csr(rels):
+    """Per-row canonical relations (keys, txn ranks, keysToTxnIds) -> one batched abi.Csr."""
+    ko, mo, to = [0], [0], [0]
+    for k, v, m in rels:
+        ko.append(ko[-1] + len(k)); mo.append(mo[-1] + len(m)); to.append(to[-1] + len(v))
+    cat = lambda xs, dt: np.concatenate([np.asarray(x, dt) for x in xs]) if rels else np.zeros(0, dt)  # noqa: E731
+    return abi.Csr(np.array(ko, np.uint32), cat([r[0] for r in rels], np.uint64), np.array(mo, np.uint32),
+                   cat([r[2] for r in rels], np.int32), np.array(to, np.uint32), cat([r[1] for r in rels], np.uint32))
+
+
+def save_keydeps_merge():
+    batch, replies, merged = keydeps_merge_case()
+    out = {"cfg": np.array([0, KEYDEPS_MERGE_R, 0], np.uint64), "drop_p": np.array([0.0], np.float32)}
+    for f in abi.BATCH_FIELDS:
+        if batch.get(f) is not None:
+            out["in_" + f] = np.asarray(batch[f], abi.BATCH_FIELDS[f])
+    for v, csr in enumerate(replies):
+        for f in CSR_FIELDS:
+            out["reply_%d_%s" % (v, f)] = getattr(csr, f)
+    for f in CSR_FIELDS:
+        out["merged_0_" + f] = getattr(merged, f)
+    np.savez_compressed(os.path.join(HERE, "keydeps_merge.npz"), **out)
 
 
 def save(name):
@@ -85,6 +170,12 @@ def csr_from(z, prefix, is_range):
 
 
 if __name__ == "__main__":
+    only = sys.argv[1:]
     for name in CASES:
+        if only and name not in only:
+            continue
         save(name)
         print("wrote", name, os.path.getsize(os.path.join(HERE, name + ".npz")), "bytes")
+    if not only or "keydeps_merge" in only:
+        save_keydeps_merge()
+        print("wrote keydeps_merge", os.path.getsize(os.path.join(HERE, "keydeps_merge.npz")), "bytes")

@@ -165,3 +165,188 @@ def testmerge_inputs(seed, unique_txn_ids_range=100, epoch_range=3, hlc_range=50
                            empty_keys_range, key_range, total_count_range)
     count = 1 + r.nextInt(merge_count_range)
     return [sup() for _ in range(count)]
+
+
+# ---------------------------------------------------------------------------------------------------------
+# RangeDepsTest (test/primitives/RangeDepsTest.java) — seeded inputs and its Validate queries
+# ---------------------------------------------------------------------------------------------------------
+def _f32(x):
+    import numpy as np
+    return np.float32(x)
+
+
+def next_float(r):
+    """java.util.Random.nextFloat(): next(24) / (float)(1 << 24), an IEEE single."""
+    return _f32(r.next(24)) / _f32(1 << 24)
+
+
+def _java_int(x):
+    """(int) cast of a float: truncation toward zero (values here are small and finite)."""
+    return int(x)
+
+
+class GenerateRanges:
+    """RangeDepsTest.GenerateRanges (:43-81): float arithmetic in IEEE single precision, as Java evaluates it."""
+
+    def __init__(self, range_domain, min_dom, max_dom, min_span, max_span):
+        self.range_domain = range_domain
+        self.min_dom, self.max_dom = _f32(min_dom), _f32(max_dom)
+        self.min_span, self.max_span = _f32(min_span), _f32(max_span)
+
+    def generate(self, r, count):
+        """generateRanges(random, rangeCount) -> list of (start, end] int pairs."""
+        dom = _f32(self.range_domain)
+        txn_domain = max(count, _java_int(((next_float(r) * (self.max_dom - self.min_dom)) + self.min_dom) * dom))
+        txn_span = max(txn_domain, _java_int(((next_float(r) * (self.max_span - self.min_span)) + self.min_span) * dom))
+        gap_span = txn_span - txn_domain
+        start = 0 if self.range_domain == txn_span else r.nextInt(self.range_domain - txn_span)
+        end = start + txn_span
+        gaps, gap_spans = [], []
+        for i in range(count):
+            gaps.append(start + r.nextInt(end - start))
+            if i == count - 1 or gap_span <= 1:
+                gap_spans.append(gap_span)
+            else:
+                gap_spans.append(1 + r.nextInt(max(1, _java_div(2 * gap_span, count - i))))
+        gaps.sort()
+        out = []
+        for i in range(count):
+            end = max(start + 1, gaps[i])
+            out.append((start, end))
+            start = end + gap_spans[i]
+        return out
+
+
+def _java_div(a, b):
+    """Java int division (truncates toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def ranges_of(ranges):
+    """Ranges.of (AbstractRanges.of :678-684): sort by Range::compare (start, end), then merge ranges that
+    overlap (MERGE_OVERLAPPING: prev.end > next.start; touching ranges stay apart)."""
+    rs = sorted(ranges)
+    out = []
+    for s, e in rs:
+        if out and out[-1][1] > s:
+            out[-1] = (out[-1][0], max(out[-1][1], e))
+        else:
+            out.append((s, e))
+    return out
+
+
+def rangedeps_generate(r, gen, txn_count, range_count):
+    """RangeDepsTest.generate (:197-207): {txn index: Ranges}."""
+    out = {}
+    for t in range(txn_count):
+        this = range_count if txn_count == 1 else 1 + r.nextInt(_java_div(2 * range_count, txn_count) - 1)
+        out[t] = ranges_of(gen.generate(r, this))
+    return out
+
+
+def rangedeps_identical(r, gen, txn_count, range_count):
+    """RangeDepsTest.generateIdenticalTxns (:209-216)."""
+    rs = ranges_of(gen.generate(r, _java_div(range_count, txn_count)))
+    return {t: list(rs) for t in range(txn_count)}
+
+
+def rangedeps_nemesis(width, nemesis_count, range_count, non_nemesis_per_nemesis):
+    """RangeDepsTest.generateNemesisRanges (:218-233) -> ({txn: Ranges}, its GenerateRanges)."""
+    build = {}
+    non_count = nemesis_count * non_nemesis_per_nemesis
+    range_count = _java_div(range_count, 1 + non_nemesis_per_nemesis)
+    domain = 0
+    for i in range(range_count):
+        build.setdefault(i % nemesis_count, []).append((i, i + width))
+        for _ in range(non_nemesis_per_nemesis):
+            build.setdefault(nemesis_count + (i % non_count), []).append((i, i + 1))
+        domain = i + width
+    return {t: ranges_of(build[t]) for t in range(nemesis_count + non_count)}, GenerateRanges(domain, 0.0, 1.0, 0.0, 1.0)
+
+
+def rangedeps_validate_queries(r, gen, canonical):
+    """The queries Validate.validate(random) (:171-193) issues, in order, drawing from the same Random:
+    ('range', (s, e)), ('key', k) and ('slice', [(s, e), ...]).  test.range(i) iterates RangeDeps' sorted
+    unique ranges."""
+    uniq = sorted({rg for rs in canonical.values() for rg in rs})
+    q = []
+    for rg in uniq:
+        q += [("range", rg), ("key", rg[0]), ("key", rg[1])]
+    for _ in range(len(uniq)):
+        rg = gen.generate(r, 1)[0]
+        q += [("range", rg), ("key", rg[0]), ("key", rg[1])]
+    for _ in range(10):
+        q.append(("slice", ranges_of(gen.generate(r, r.nextInt(10) + 1))))
+    return q
+
+
+# RangeDepsTest's own recorded seeds (the commented reproduction seeds in the test source)
+RANGEDEPS_RANDOM_SEEDS = (-6268194734307361517, -1531261279965735959, 1953755836248097851)   # testRandom :262-268
+RANGEDEPS_IDENTICAL_SEED = -4951029115911714505                                             # testIdenticalTransactions :278
+RANGEDEPS_NEMESIS_SEED = 2005526220972215410                                                # testNemesisRanges :301
+
+
+def rangedeps_batch(canonical, queries):
+    """An engine batch whose PreAccept RangeDeps answer RangeDepsTest's Validate queries: the test's TxnIds
+    become range-domain Writes (hlc = 1 + t, in TxnId order) holding their Ranges, followed by one Read per query
+    (a range / slice query: range domain with its ranges; a key query: key domain with the one key).  Reads
+    witness Writes only (Txn.java:221-245), so each query's RangeDeps are exactly the stored txns its footprint
+    intersects (InMemoryCommandStore.mapReduceRangesInternal, :884-1017)."""
+    import numpy as np
+    from accord_amd import abi
+    N = len(canonical)
+    n = N + len(queries)
+    hlc = np.arange(1, n + 1, dtype=np.int64)
+    kinds = np.array([abi.KIND_WRITE] * N + [abi.KIND_READ] * len(queries), np.int64)
+    domain = np.array([1] * N + [0 if q[0] == "key" else 1 for q in queries], np.int64)
+    flags = (kinds << 1) | domain
+    msb = (np.uint64(1) << np.uint64(15)) | (hlc.astype(np.uint64) >> np.uint64(48))
+    lsb = (hlc.astype(np.uint64) << np.uint64(16)) | flags.astype(np.uint64)
+    key_off, keys, range_off, rs, re_ = [0], [], [0], [], []
+    for t in range(N):
+        for s, e in canonical[t]:
+            rs.append(s); re_.append(e)
+        key_off.append(len(keys)); range_off.append(len(rs))
+    for kind, v in queries:
+        if kind == "key":
+            keys.append(v)
+        else:
+            for s, e in ([v] if kind == "range" else v):
+                rs.append(s); re_.append(e)
+        key_off.append(len(keys)); range_off.append(len(rs))
+    node = np.ones(n, np.int32)
+    return {"n": n, "txn_msb": msb, "txn_lsb": lsb, "txn_node": node, "exec_msb": msb.copy(), "exec_lsb": lsb.copy(),
+            "exec_node": node.copy(), "status": np.full(n, abi.ST_APPLIED, np.uint8),
+            "key_off": np.array(key_off, np.uint32), "keys": np.array(keys, np.uint64),
+            "range_off": np.array(range_off, np.uint32), "range_start": np.array(rs, np.uint64),
+            "range_end": np.array(re_, np.uint64)}
+
+
+def rangedeps_expected(canonical, queries):
+    """Per batch txn, the canonical RangeDeps (sorted unique ranges, sorted unique dependency ranks, and
+    rangesToTxnIds = per-range end offsets then indices) from RangeDepsTest.Validate's model: a stored txn i is
+    a dependency on each of its ranges that intersects the query's footprint ((s, e] semantics,
+    Range.EndInclusive) or contains the query key."""
+    def inter(a, b):
+        return max(a[0], b[0]) < min(a[1], b[1])
+    N = len(canonical)
+    foot = [("ranges", canonical[t]) for t in range(N)]
+    foot += [("key", q[1]) if q[0] == "key" else ("ranges", [q[1]] if q[0] == "range" else q[1]) for q in queries]
+    out = []
+    for t, (kind, v) in enumerate(foot):
+        pairs = set()
+        for i in range(min(t, N)):
+            for r in canonical[i]:
+                if (kind == "key" and r[0] < v <= r[1]) or (kind == "ranges" and any(inter(r, q) for q in v)):
+                    pairs.add((r, i))
+        ks = sorted({p[0] for p in pairs})
+        tx = sorted({p[1] for p in pairs})
+        pos = {x: j for j, x in enumerate(tx)}
+        ends, idx = [], []
+        for k in ks:
+            lst = sorted(pos[i] for (r, i) in pairs if r == k)
+            idx += lst
+            ends.append(len(ks) + len(idx))
+        out.append((ks, tx, ends + idx))
+    return out

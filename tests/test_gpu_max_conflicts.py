@@ -8,6 +8,7 @@ import pytest
 
 import oracle as O
 from accord_amd import abi, engine, workload
+from batchkit import T, make_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -113,3 +114,52 @@ def test_full_size_prefix(engine_factory, name):
         assert np.array_equal(fast[v, i].astype(bool), gt | eq)
         assert fast[v, ~has[v]].all()
     assert n == 1 << 20
+
+
+# ---- MaxConflicts carried across batches (ad_max_conflicts_carry / _ts / _export) -------------------------------
+def _engine_store(engine_factory, batches, window, replicas, drop_p, seed):
+    eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
+    carry = None
+    out = []
+    for b in batches:
+        eng.load(b)
+        eng.preaccept_deps()
+        if carry is not None:
+            eng.max_conflicts_carry(carry)
+        else:
+            eng.max_conflicts_carry(O.EMPTY_CARRY)
+        out.append(eng.max_conflicts_ts())
+        carry = eng.max_conflicts_export()
+        out[-1] = out[-1] + (carry,)
+    return out
+
+
+def test_gpu_preaccept_kat_multi_key(engine_factory):
+    # PreAcceptTest.multiKeyTimestampUpdate through the engine: the later-arriving smaller TxnId sees (1, 100, ID2)
+    from accord_amd import witness as Wt
+    first = make_batch([T(100, abi.KIND_WRITE, [10], node=2)])
+    second = make_batch([T(50, abi.KIND_WRITE, [10, 11], node=3)])
+    (m1, l1, n1, f1, c1), (m2, l2, n2, f2, c2) = _engine_store(engine_factory, [first, second], 0, 1, 0.0, 1)
+    assert f1[0, 0] == 1 and f2[0, 0] == 0
+    assert (int(m2[0, 0]), int(l2[0, 0]), int(n2[0, 0])) == Wt.from_values(1, 100, abi.KIND_WRITE << 1, 2)
+    clock = Wt.NodeClock(1, 1, 110)
+    clock.now = Wt.from_values(1, 100, 0, 1)
+    w = Wt.preaccept_witnessed_at(Wt.from_values(1, 50, abi.KIND_WRITE << 1, 3), (int(m2[0, 0]), int(l2[0, 0]), int(n2[0, 0])), clock)
+    assert (Wt.epoch(w), Wt.hlc(w), w[2]) == (1, 110, 1)
+
+
+@pytest.mark.parametrize("keyspace,window,replicas,drop", [(40, 0, 1, 0.0), (300, 16, 3, 0.2), (5000, 32, 2, 0.1)])
+def test_gpu_carry_chain_equals_oracle(engine_factory, keyspace, window, replicas, drop):
+    # five consecutive batches of one store: every batch's maxConflicts timestamps / fast flags and the carried map
+    # after it equal the oracle's, bit for bit
+    batches = [workload.generate(3000, keys_per_txn=3, keyspace=keyspace, seed=100 + k, slow_frac=0.3, bump_max=50,
+                                 hlc_start=1_000_000 + 40_000 * k) for k in range(5)]
+    got = _engine_store(engine_factory, batches, window, replicas, drop, 0xC0FFEE)
+    cfg = abi.make_config(window, replicas, drop, 0xC0FFEE)
+    carry = None
+    for b, (m, l, n_, f, exp) in zip(batches, got):
+        om, ol, on, fast = O.max_conflicts_ts(b, cfg, carry)
+        assert np.array_equal(m, om) and np.array_equal(l, ol) and np.array_equal(n_, on) and np.array_equal(f, fast)
+        carry = O.max_conflicts_export(b, carry)
+        assert all(np.array_equal(x, y) for x, y in zip(exp, carry))
+    assert carry[0].size > 0

@@ -2,8 +2,9 @@
 Deps.Builder routing) on hand-built batches, and the CommandsForKeyTest.Canon execution-order
 invariant on its execution levels.
 
-Each expected answer is derived by hand from the reference code cited in the test; the PreAcceptTest
-known answers (test/messages/PreAcceptTest.java:85-290) are the first two cases.
+Each expected answer is derived by hand from the reference code cited in the test.  The PreAcceptTest known
+answers themselves (test/messages/PreAcceptTest.java:85-290), witnessedAt included, are restated exactly in
+tests/test_oracle_preaccept_kats.py; the first two cases here only check the deps part of two of them.
 """
 import numpy as np
 import pytest
@@ -35,7 +36,7 @@ def test_initial_command_no_deps():
 
 
 def test_later_txn_not_a_dependency():
-    # PreAcceptTest.multiKeyTimestampUpdate: txnId2 (hlc 50) < txn1 (hlc 110) -> no deps for txnId2
+    # deps part of PreAcceptTest.multiKeyTimestampUpdate in one batch: txnId2 (hlc 50) < txn1 (hlc 110) -> no deps
     # (CommandsForKey.mapReduceActive only visits byId[0, insertPos(startedBefore)), :929)
     res, _ = run([T(110, W, [10], node=2), T(50, W, [10, 11], node=3)])
     assert d(res, KEY, 0) == {}            # rank 0 = hlc 50
