@@ -72,6 +72,7 @@ def lib():
         L.ad_kernel_units.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64)]
         L.ad_shard_bounds.argtypes = [C.POINTER(C.c_uint64), C.c_size_t, C.c_uint32, C.POINTER(C.c_uint64)]
         L.ad_max_conflicts_carry.argtypes = [vp, C.c_size_t, vp, vp, vp, vp]
+        L.ad_merge_deps_fast.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_max_conflicts_ts.argtypes = [vp, vp, vp, vp, vp]
         L.ad_max_conflicts_export.argtypes = [vp, C.POINTER(C.c_size_t), vp, vp, vp, vp]
         _LIB = L
@@ -79,7 +80,7 @@ def lib():
 
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
-            "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export",
+            "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_merge_deps_fast",
             "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
@@ -156,6 +157,14 @@ class DepsEngine:
     def merge(self):
         sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
         self._check(lib().ad_merge_deps(self.h, sizes), "ad_merge_deps")
+        self._merge_sizes = sizes
+        return sizes
+
+    def merge_fast(self):
+        """The coordinator's fast-path Deps.merge: per txn only the views whose proposal is witnessedAt == TxnId
+        (the fast flags of the last max_conflicts / max_conflicts_ts).  Fetch with fetch_merged()."""
+        sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
+        self._check(lib().ad_merge_deps_fast(self.h, sizes), "ad_merge_deps_fast")
         self._merge_sizes = sizes
         return sizes
 

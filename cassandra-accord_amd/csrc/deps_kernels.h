@@ -220,6 +220,14 @@ __global__ __launch_bounds__(256) void k_gather_entries(size_t P, const uint32_t
 }
 
 // Segmented prefix state of CommandsForKey.mapReduceActive over the (key, TxnId)-sorted entries.
+// Wide key spreads: the sort key of pass `shift` (0: low 32 bits, 32: high bits) of the pairs in their current
+// order (val = pair index), for an LSD sort of the full 64-bit (key - key_min) by 32-bit halves.
+__global__ __launch_bounds__(256) void k_pair_key_half(size_t P, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ val,
+                                                       uint64_t key_min, int shift, uint32_t* __restrict__ out) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < P) out[x] = (uint32_t)((keys[val[x]] - key_min) >> shift);
+}
+
 struct ElideOp {
     struct S {
         uint32_t head;
@@ -242,10 +250,14 @@ struct ElideOp {
     uint64_t key_min;
     size_t n;
     Params* prm;
+    const uint64_t* keys64;  // wide key spreads (> 32 bits): raw keys through sval (skey holds only low bits)
+    const uint32_t* sval;
 
+    __device__ uint64_t key_at(size_t i) const { return keys64 ? keys64[sval[i]] : (uint64_t)skey[i] + key_min; }
     __device__ S load(size_t i) const {
         S s;
-        s.head = (i == 0 || skey[i] != skey[i - 1]) ? 1u : 0u;
+        if (keys64) s.head = (i == 0 || keys64[sval[i]] != keys64[sval[i - 1]]) ? 1u : 0u;
+        else s.head = (i == 0 || skey[i] != skey[i - 1]) ? 1u : 0u;
         s.ss = s.head ? (int32_t)i : -1;
         uint32_t m = e_meta[i];
         uint32_t cat = category(m);
@@ -274,7 +286,7 @@ struct ElideOp {
         pm_c[i] = inc.pc;
         const uint32_t u = inc.hc - 1;
         if (el.head) {
-            ukey[u] = (uint64_t)skey[i] + key_min;
+            ukey[u] = key_at(i);
             useg[u] = (uint32_t)i;
         } else {
             nh[i - inc.hc] = (uint32_t)i;     // (i + 1 - hc) non-heads so far, this one included

@@ -24,6 +24,7 @@
 #include "merge_kernels.h"
 #include "radix_sort.h"
 #include "shard_kernels.h"
+#include "validate.h"
 
 using namespace ad;
 
@@ -118,6 +119,7 @@ struct ad_handle {
     uint64_t *mc_ck = nullptr, *mc_cm = nullptr, *mc_cl = nullptr;
     int32_t* mc_cn = nullptr;
     bool mc_ready = false;           // the MaxConflicts scan of the current batch is on the device (export)
+    const uint8_t* mc_fast = nullptr;  // [replicas * n] fast-path flags of the last ad_max_conflicts(_ts)
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
@@ -202,6 +204,7 @@ enum Slot : size_t {
     S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
     S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST, S_MCLOCAL, S_MCCK, S_MCCM, S_MCCL, S_MCCN,
     S_MCOM, S_MCOL, S_MCON, S_MCOF, S_MCSK, S_MCSM, S_MCSL, S_MCSN, S_MCSU, S_MCSP,
+    S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS,
     S_CSR0 = 100
 };
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -331,13 +334,11 @@ int stage_prepare(ad_handle* h) {
     h->pack.sh_hlc = NB + 4;
     h->pack.sh_msb = NB + 4 + HB;
     h->pack.total_bits = NB + 4 + HB + MB;
-    h->key_bits = P ? bits_of(p.key_max - p.key_min) : 0;
-    if (h->key_bits > 32) return set_err(h, AD_ERR_UNSUPPORTED, "key spread exceeds 32 bits");
+    h->key_bits = P ? bits_of(p.key_max - p.key_min) : 0;      // > 32: sorted in two 32-bit LSD halves
     h->n_large = p.n_large;
     h->rbase = Q ? p.rs_min : 0;
     h->wmax = Q ? p.rw_max : 0;
-    h->range_bits = Q ? bits_of(p.re_max - p.rs_min) : 0;
-    if (h->range_bits > 32) return set_err(h, AD_ERR_UNSUPPORTED, "range spread exceeds 32 bits");
+    h->range_bits = Q ? bits_of(p.re_max - p.rs_min) : 0;    // > 32: each endpoint sorted in two 32-bit halves
     KScope ks(K_PACK, n);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
@@ -359,19 +360,34 @@ int stage_sort(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     hipStream_t st = h->st;
     if (P > 0) {
-        bool flip = radix_sort_pairs(h->ka, h->va, h->kb, h->vb, P, h->key_bits, radix_scratch(h, P), st);
-        h->skey = flip ? h->kb : h->ka;
-        h->sval = flip ? h->vb : h->va;
+        uint32_t *k = h->ka, *v = h->va, *ko = h->kb, *vo = h->vb;
+        if (radix_sort_pairs(k, v, ko, vo, P, std::min(h->key_bits, 32), radix_scratch(h, P), st)) { std::swap(k, ko); std::swap(v, vo); }
+        if (h->key_bits > 32) {
+            // wide key spread: stable second pass on the high half (LSD over the full 64-bit key)
+            k_pair_key_half<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->keys, v, h->hprm.key_min, 32, k);
+            if (radix_sort_pairs(k, v, ko, vo, P, h->key_bits - 32, radix_scratch(h, P), st)) { std::swap(k, ko); std::swap(v, vo); }
+        }
+        h->skey = k;
+        h->sval = v;
     }
     if (Q > 0) {
-        // (start, end, owner): stable by end, then stable by start, over the owner-ordered input
+        // (start, end, owner): stable by end, then stable by start, over the owner-ordered input; each endpoint
+        // in one pass, or in two 32-bit halves (low, then high) for a spread beyond 32 bits
         k_range_prep<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->meta, h->range_off, h->range_s, h->range_e, h->rbase,
                                                               h->rowner, h->rk0, h->rv0);
         uint32_t *k = h->rk0, *v = h->rv0, *ko = h->rk1, *vo = h->rv1;
-        if (radix_sort_pairs(k, v, ko, vo, Q, h->range_bits, radix_scratch(h, Q), st)) { std::swap(k, ko); std::swap(v, vo); }
-        k_range_startkey<<<ceil_div((long)Q, 256), 256, 0, st>>>(Q, h->range_s, v, h->rbase, k);
-        if (radix_sort_pairs(k, v, ko, vo, Q, h->range_bits, radix_scratch(h, Q), st)) { std::swap(k, ko); std::swap(v, vo); }
-        k_range_gather<<<ceil_div((long)Q, 256), 256, 0, st>>>(Q, v, h->range_s, h->range_e, h->rowner, h->es, h->ee, h->eown);
+        const int rb = h->range_bits, lo_bits = std::min(rb, 32);
+        const int gq = ceil_div((long)Q, 256);
+        auto pass = [&](int bits) {
+            if (radix_sort_pairs(k, v, ko, vo, Q, bits, radix_scratch(h, Q), st)) { std::swap(k, ko); std::swap(v, vo); }
+        };
+        if (rb > 32) k_range_key_half<<<gq, 256, 0, st>>>(Q, h->range_e, v, h->rbase, 0, k);
+        pass(lo_bits);
+        if (rb > 32) { k_range_key_half<<<gq, 256, 0, st>>>(Q, h->range_e, v, h->rbase, 32, k); pass(rb - 32); }
+        k_range_key_half<<<gq, 256, 0, st>>>(Q, h->range_s, v, h->rbase, 0, k);
+        pass(lo_bits);
+        if (rb > 32) { k_range_key_half<<<gq, 256, 0, st>>>(Q, h->range_s, v, h->rbase, 32, k); pass(rb - 32); }
+        k_range_gather<<<gq, 256, 0, st>>>(Q, v, h->range_s, h->range_e, h->rowner, h->es, h->ee, h->eown);
     }
     return AD_OK;
 }
@@ -537,7 +553,8 @@ int stage_deps(ad_handle* h) {
     if (P > 0) {
         { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->e_txn, h->e_meta, h->e_exec1); }
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
-                    h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm};
+                    h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm,
+                    h->key_bits > 32 ? h->keys : nullptr, h->sval};
         KScope ks(K_SCAN_ELIDE, P);
         device_scan(eop, P, (ElideOp::S*)h->scratch, st);
     }
@@ -775,14 +792,16 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
     return AD_OK;
 }
 
-// Deps.merge of `np` parts per class into h->merged.  parts[cls][v] are batched per-txn CSRs over the loaded batch.
-int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_range) {
+// Deps.merge of `np` parts per class into h->merged.  parts[cls][v] are batched per-txn CSRs over the loaded batch;
+// view_rows[v] (nullable) maps txn -> row of part v, -1 = leave that reply out for the txn.
+int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_range, const int32_t* const* view_rows = nullptr) {
     const size_t n = h->n;
     h->merged_entries = 0;
     Csr* out[3];
     size_t blocks[3];
     int kw[3];
     const Csr* in[3][MAXV] = {};
+    const int32_t* rows[3][MAXV] = {};
     int K = 0;
     for (int cls = 0; cls < 3; ++cls) {
         if (cls == AD_CLASS_RANGE && !has_range) {
@@ -803,10 +822,10 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
         out[K] = &h->merged[cls];
         blocks[K] = CSR_MERGED0 + cls;
         kw[K] = cls == AD_CLASS_RANGE ? 2 : 1;
-        for (int v = 0; v < np; ++v) in[K][v] = parts[cls][v];
+        for (int v = 0; v < np; ++v) { in[K][v] = parts[cls][v]; rows[K][v] = view_rows ? view_rows[v] : nullptr; }
         ++K;
     }
-    CK(merge_multi(h, n, K, out, blocks, kw, in, nullptr, np, &h->merged_entries));
+    CK(merge_multi(h, n, K, out, blocks, kw, in, view_rows ? rows : nullptr, np, &h->merged_entries));
     h->have_merged = true;
     return AD_OK;
 }
@@ -822,42 +841,6 @@ int stage_merge(ad_handle* h) {
         parts[2][v] = &h->rdeps[v];
     }
     return merge_parts(h, parts, nv, h->Q > 0);
-}
-
-// Validates one caller-supplied canonical CSR over n txns (host side: a malformed reply must never reach a
-// kernel as an out-of-range index).  Returns the three lengths via *keys/*k2t/*txns.
-bool valid_part(const ad_csr_in& c, size_t n, int kw, size_t* nkeys, size_t* nk2t, size_t* ntx, std::string& why) {
-    if (!c.key_off || !c.k2t_off || !c.txn_off) { why = "null offsets"; return false; }
-    if (c.key_off[0] != 0 || c.k2t_off[0] != 0 || c.txn_off[0] != 0) { why = "offsets must start at 0"; return false; }
-    for (size_t i = 0; i < n; ++i) {
-        const uint32_t k0 = c.key_off[i], k1 = c.key_off[i + 1], m0 = c.k2t_off[i], m1 = c.k2t_off[i + 1];
-        const uint32_t t0 = c.txn_off[i], t1 = c.txn_off[i + 1];
-        if (k1 < k0 || m1 < m0 || t1 < t0) { why = "offsets not monotone at txn " + std::to_string(i); return false; }
-        const uint32_t nk = k1 - k0, len = m1 - m0, nt = t1 - t0;
-        if ((nk == 0) != (len == 0) || (nk == 0) != (nt == 0) || len < nk) { why = "inconsistent CSR at txn " + std::to_string(i); return false; }
-        // keys strictly ascending (Range::compare for ranges)
-        for (uint32_t k = k0 + 1; k < k1; ++k) {
-            const uint64_t* a = c.keys + (size_t)kw * (k - 1);
-            const uint64_t* b = c.keys + (size_t)kw * k;
-            const bool lt = kw == 1 ? a[0] < b[0] : (a[0] < b[0] || (a[0] == b[0] && a[1] < b[1]));
-            if (!lt) { why = "keys not strictly ascending at txn " + std::to_string(i); return false; }
-        }
-        for (uint32_t x = t0; x < t1; ++x)
-            if (c.txns[x] >= n || (x > t0 && c.txns[x] <= c.txns[x - 1])) { why = "TxnIds not sorted unique ranks at txn " + std::to_string(i); return false; }
-        uint32_t prev = nk;
-        for (uint32_t k = 0; k < nk; ++k) {
-            const uint32_t end = (uint32_t)c.k2t[m0 + k];
-            if (end < prev || end > len || (end == prev)) { why = "keysToTxnIds header invalid at txn " + std::to_string(i); return false; }
-            for (uint32_t x = prev; x < end; ++x) {
-                const int32_t ix = c.k2t[m0 + x];
-                if (ix < 0 || (uint32_t)ix >= nt || (x > prev && ix <= c.k2t[m0 + x - 1])) { why = "keysToTxnIds index invalid at txn " + std::to_string(i); return false; }
-            }
-            prev = end;
-        }
-        if (prev != len) { why = "keysToTxnIds length mismatch at txn " + std::to_string(i); return false; }
-    }
-    *nkeys = c.key_off[n]; *nk2t = c.k2t_off[n]; *ntx = c.txn_off[n];
-    return true;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -911,7 +894,7 @@ int fetch_csr(ad_handle* h, const Csr& c, int kw, ad_csr_out* out) {
     uint32_t o = 0;
     out->txn_off[0] = 0;
     for (size_t i = 0; i < n; ++i) {
-        std::memcpy(out->txns + o, tx.data() + ent[i], cnt[i] * 4);
+        if (cnt[i]) std::memcpy(out->txns + o, tx.data() + ent[i], cnt[i] * 4);
         o += cnt[i];
         out->txn_off[i + 1] = o;
     }
@@ -954,7 +937,7 @@ int fetch_rows(ad_handle* h, const Csr& c, int kw, size_t lo, size_t hi, ad_csr_
     uint32_t o = 0;
     out->txn_off[0] = 0;
     for (size_t i = 0; i < m; ++i) {
-        std::memcpy(out->txns + o, tx.data() + (eo[i] - eo[0]), cnt[i] * 4);
+        if (cnt[i]) std::memcpy(out->txns + o, tx.data() + (eo[i] - eo[0]), cnt[i] * 4);
         o += cnt[i];
         out->txn_off[i + 1] = o;
     }
@@ -1019,6 +1002,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     h->loaded = false;
     h->have_deps = h->have_merged = h->have_levels = false;
     h->mc_ready = false;
+    h->mc_fast = nullptr;
     CK(dalloc(h, S_TM, &h->tm, n)); CK(dalloc(h, S_TL, &h->tl, n)); CK(dalloc(h, S_TN, &h->tn, n));
     CK(dalloc(h, S_EM, &h->em, n)); CK(dalloc(h, S_EL, &h->el, n)); CK(dalloc(h, S_EN, &h->en, n));
     CK(dalloc(h, S_ST, &h->status, n)); CK(dalloc(h, S_KOFF, &h->key_off, n + 1)); CK(dalloc(h, S_KEYS, &h->keys, P));
@@ -1134,6 +1118,7 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
     }
     HIPCHK(h, hipGetLastError());
     h->mc_ready = true;
+    h->mc_fast = fst;
     *rank_out = rank; *fast_out = fst;
     if (local_out) *local_out = local;
     return AD_OK;
@@ -1193,6 +1178,7 @@ int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* nod
         KScope ks(K_MAX_CONFLICTS);
         k_mc_carry<<<ceil_div((long)n, 256), 256, 0, st>>>(c);
         HIPCHK(h, hipGetLastError());
+        h->mc_fast = of;
         if (msb) HIPCHK(h, hipMemcpyAsync(msb, om, n * nv * 8, hipMemcpyDeviceToHost, st));
         if (lsb) HIPCHK(h, hipMemcpyAsync(lsb, ol, n * nv * 8, hipMemcpyDeviceToHost, st));
         if (node) HIPCHK(h, hipMemcpyAsync(node, on, n * nv * 4, hipMemcpyDeviceToHost, st));
@@ -1217,8 +1203,8 @@ int ad_max_conflicts_export(ad_handle* h, size_t* m_out, uint64_t* keys, uint64_
     CK(dalloc(h, S_MCSK, &sk, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCSM, &sm, std::max<size_t>(S, 1)));
     CK(dalloc(h, S_MCSL, &sl, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCSN, &sn, std::max<size_t>(S, 1)));
     CK(dalloc(h, S_MCSU, &su, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCSP, &sp, std::max<size_t>(S, 1) + 16));
-    CK(dalloc(h, S_MCOM, &ok_, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCOL, &om_, std::max<size_t>(S, 1)));
-    CK(dalloc(h, S_MCON, &on_, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCOF, &ol_, std::max<size_t>(S, 1)));
+    CK(dalloc(h, S_MCEK, &ok_, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCEM, &om_, std::max<size_t>(S, 1)));
+    CK(dalloc(h, S_MCEN, &on_, std::max<size_t>(S, 1))); CK(dalloc(h, S_MCEL, &ol_, std::max<size_t>(S, 1)));
     tot = sp + std::max<size_t>(S, 1);
     uint32_t count = 0;
     if (S) {
@@ -1259,6 +1245,45 @@ int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
     g_tracer = &h->tracer;
     hipSetDevice(h->device);
     CK(stage_merge(h));
+    h->merged_has_range = h->Q > 0;
+    if (sizes) {
+        CK(csr_sizes(h, h->merged[0], &sizes[0]));
+        CK(csr_sizes(h, h->merged[1], &sizes[1]));
+        if (h->Q) CK(csr_sizes(h, h->merged[2], &sizes[2]));
+        else sizes[2] = ad_csr_sizes{h->n, 0, 0, 0, 0};
+    }
+    return AD_OK;
+}
+
+__global__ void k_fast_rows(size_t n, int nv, const uint8_t* __restrict__ fast, int32_t* __restrict__ rows) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < n * (size_t)nv) rows[x] = fast[x] ? (int32_t)(x % n) : -1;
+}
+
+// The coordinator's fast-path merge (CoordinateTransaction.onPreAccepted :75): per txn, only the replies whose
+// witnessedAt == TxnId — the fast flags of the last ad_max_conflicts(_ts) on this batch.
+int ad_merge_deps_fast(ad_handle* h, ad_csr_sizes* sizes) {
+    if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps_fast before ad_preaccept_deps");
+    if (!h->mc_fast) return set_err(h, AD_ERR_STATE, "ad_merge_deps_fast: run ad_max_conflicts(_ts) on this batch first");
+    hipSetDevice(h->device);
+    StageScope sc(h, STAGE_MERGE);
+    const size_t n = h->n;
+    const int nv = (int)h->cfg.replicas;
+    int32_t* rows = nullptr;
+    CK(dalloc(h, S_FASTROWS, &rows, std::max<size_t>(n * nv, 1)));
+    if (n) k_fast_rows<<<ceil_div((long)(n * nv), 256), 256, 0, h->st>>>(n, nv, h->mc_fast, rows);
+    const Csr* parts[3][MAXV] = {};
+    const int32_t* vr[MAXV] = {};
+    for (int v = 0; v < nv; ++v) {
+        parts[0][v] = &h->deps[2 * v];
+        parts[1][v] = &h->deps[2 * v + 1];
+        parts[2][v] = &h->rdeps[v];
+        vr[v] = rows + (size_t)v * n;
+    }
+    h->merge_heavy = true;
+    CK(merge_parts(h, parts, nv, h->Q > 0, vr));
     h->merged_has_range = h->Q > 0;
     if (sizes) {
         CK(csr_sizes(h, h->merged[0], &sizes[0]));

@@ -48,6 +48,13 @@ __global__ __launch_bounds__(256) void k_range_startkey(size_t Q, const uint64_t
     if (x < Q) k_start[x] = (uint32_t)(rs[idx[x]] - rbase);
 }
 
+// 64-bit range spreads: sort key = (src[idx[x]] - rbase) >> shift, truncated to 32 bits (one LSD half)
+__global__ __launch_bounds__(256) void k_range_key_half(size_t Q, const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx,
+                                                        uint64_t rbase, int shift, uint32_t* __restrict__ k_out) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < Q) k_out[x] = (uint32_t)((src[idx[x]] - rbase) >> shift);
+}
+
 __global__ __launch_bounds__(256) void k_range_gather(size_t Q, const uint32_t* __restrict__ idx, const uint64_t* __restrict__ rs,
                                                       const uint64_t* __restrict__ re, const uint32_t* __restrict__ rowner,
                                                       uint64_t* __restrict__ es, uint64_t* __restrict__ ee,

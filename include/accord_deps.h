@@ -176,6 +176,13 @@ int  ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out);
 int  ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
 int  ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out);
 
+/* Stage 2 on the fast path — CoordinateTransaction.onPreAccepted (coordinate/CoordinateTransaction.java:71-101):
+ * when the coordinator takes the fast path it merges only the replies whose witnessedAt == TxnId (:75); the slow
+ * path merges all (:81, ad_merge_deps).  Per txn, view v's reply is folded iff the fast flag of the last
+ * ad_max_conflicts / ad_max_conflicts_ts on this batch is set for (v, txn).  Result as ad_merge_deps
+ * (ad_fetch_merged / ad_fetch_rows with view == replicas). */
+int  ad_merge_deps_fast(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
+
 /* Paged fetch: rows [lo, hi) of replica view `view`'s CSR of class `cls` (view == replicas: the merged
  * Deps), offsets rebased to 0.  Two calls: out == NULL fills *sizes (n = hi - lo), then the caller
  * allocates and passes out.  Lets a host stream a full-size batch's Deps (C4: ~10^9 entries per view)

@@ -590,7 +590,17 @@ extern "C" {
 
 /* flags: bit0 = pruning (baseline mode), bit1 = merge, bit2 = levels; threads: key-range shards
  * for the deps stage (InMemoryCommandStore.SingleThread per shard + PreAccept.reduce). */
+oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+                                 const uint8_t* view_mask);
 oracle_result* oracle_run(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads) {
+    return oracle_run_masked(b, c, flags, threads, nullptr);
+}
+
+/* As oracle_run; view_mask (nullable, [replicas * n]) selects, per txn, the replies the merge folds: the
+ * coordinator's fast-path merge takes only the replies whose witnessedAt == TxnId
+ * (CoordinateTransaction.onPreAccepted, coordinate/CoordinateTransaction.java:71-101, :75). */
+oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+                                 const uint8_t* view_mask) {
     oracle_result* res = new oracle_result();
     try {
         Batch B(b);
@@ -671,6 +681,7 @@ oracle_result* oracle_run(const ad_batch* b, const ad_config* c, uint32_t flags,
             for (uint32_t i = 0; i < n; ++i) {
                 TxnDeps acc;
                 for (uint32_t v = 0; v < R; ++v) {
+                    if (view_mask && !view_mask[(size_t)v * n + i]) continue;
                     acc.key = linear_union(acc.key, all[v][i].key);
                     acc.direct = linear_union(acc.direct, all[v][i].direct);
                     acc.range = linear_union(acc.range, all[v][i].range);
@@ -819,12 +830,14 @@ int oracle_sizes(const oracle_result* r, int stage, uint32_t view, uint32_t cls,
 int oracle_fetch(const oracle_result* r, int stage, uint32_t view, uint32_t cls, ad_csr_out* out) {
     const Flat* f = pick(r, stage, view, cls);
     if (!f) return AD_ERR_ARGUMENT;
-    std::memcpy(out->key_off, f->key_off.data(), f->key_off.size() * 4);
-    std::memcpy(out->keys, f->keys.data(), f->keys.size() * 8);
-    std::memcpy(out->k2t_off, f->k2t_off.data(), f->k2t_off.size() * 4);
-    std::memcpy(out->k2t, f->k2t.data(), f->k2t.size() * 4);
-    std::memcpy(out->txn_off, f->txn_off.data(), f->txn_off.size() * 4);
-    std::memcpy(out->txns, f->txns.data(), f->txns.size() * 4);
+    // (memcpy of an empty vector's null data() is undefined even for 0 bytes: UBSan, tests/native/oracle_asan.cpp)
+    auto cp = [](void* dst, const void* src, size_t bytes) { if (bytes) std::memcpy(dst, src, bytes); };
+    cp(out->key_off, f->key_off.data(), f->key_off.size() * 4);
+    cp(out->keys, f->keys.data(), f->keys.size() * 8);
+    cp(out->k2t_off, f->k2t_off.data(), f->k2t_off.size() * 4);
+    cp(out->k2t, f->k2t.data(), f->k2t.size() * 4);
+    cp(out->txn_off, f->txn_off.data(), f->txn_off.size() * 4);
+    cp(out->txns, f->txns.data(), f->txns.size() * 4);
     return AD_OK;
 }
 

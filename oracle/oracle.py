@@ -30,6 +30,8 @@ def lib():
         L = C.CDLL(path)
         L.oracle_run.restype = C.c_void_p
         L.oracle_run.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_uint32]
+        L.oracle_run_masked.restype = C.c_void_p
+        L.oracle_run_masked.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_uint32, C.c_void_p]
         L.oracle_error.restype = C.c_char_p
         L.oracle_error.argtypes = [C.c_void_p]
         L.oracle_sizes.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrSizes)]
@@ -59,12 +61,18 @@ FLAG_PRUNE, FLAG_MERGE, FLAG_LEVELS = 1, 2, 4
 
 
 class OracleResult:
-    def __init__(self, batch, cfg, flags=FLAG_MERGE | FLAG_LEVELS, threads=1):
+    def __init__(self, batch, cfg, flags=FLAG_MERGE | FLAG_LEVELS, threads=1, view_mask=None):
+        """view_mask ([replicas, n] uint8, optional): per txn, the replies the merge folds (the coordinator's
+        fast-path merge: only replies with witnessedAt == TxnId)."""
         self._b = abi.make_batch(batch)
         self._cfg = cfg
         self.n = batch["n"]
         self.replicas = cfg.replicas
-        self.h = lib().oracle_run(C.byref(self._b), C.byref(cfg), flags, threads)
+        if view_mask is None:
+            self.h = lib().oracle_run(C.byref(self._b), C.byref(cfg), flags, threads)
+        else:
+            self._mask = np.ascontiguousarray(view_mask, np.uint8)
+            self.h = lib().oracle_run_masked(C.byref(self._b), C.byref(cfg), flags, threads, self._mask.ctypes.data)
         err = lib().oracle_error(self.h)
         if err:
             msg = err.decode()

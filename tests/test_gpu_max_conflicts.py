@@ -163,3 +163,25 @@ def test_gpu_carry_chain_equals_oracle(engine_factory, keyspace, window, replica
         carry = O.max_conflicts_export(b, carry)
         assert all(np.array_equal(x, y) for x, y in zip(exp, carry))
     assert carry[0].size > 0
+
+
+@pytest.mark.parametrize("name,window,drop", [("C3", 32, 0.2), ("C2", 32, 0.1), ("C3", 0, 0.0)])
+def test_gpu_fast_path_merge(engine_factory, name, window, drop):
+    # CoordinateTransaction.onPreAccepted :75 — the fast-path merge folds only the replies with witnessedAt == TxnId:
+    # ad_merge_deps_fast with the fast flags of ad_max_conflicts equals the oracle's merge under the same mask
+    b = workload.config(name, n=20000)
+    R = 3
+    eng = engine_factory(window=window, replicas=R, drop_p=drop, seed=0x51DE)
+    eng.load(b)
+    eng.preaccept_deps()
+    _, fast = eng.max_conflicts()
+    eng.merge_fast()
+    ref = O.OracleResult(b, abi.make_config(window, R, drop, 0x51DE), O.FLAG_MERGE, view_mask=fast)
+    for c in range(abi.NUM_CLASSES):
+        assert eng.fetch_merged(c).equal(ref.merged(c)), "class %d" % c
+    if name == "C3":
+        assert fast.min() == 0 and fast.max() == 1        # both outcomes exercised
+    # the slow path (all replies) on the same handle afterwards
+    eng.merge()
+    full = O.OracleResult(b, abi.make_config(window, R, drop, 0x51DE), O.FLAG_MERGE)
+    assert eng.fetch_merged(abi.CLASS_KEY).equal(full.merged(abi.CLASS_KEY))

@@ -296,3 +296,25 @@ def test_merge_host_rejects_malformed(engine_factory):
     bad.k2t[bad.k2t_off[i] + (bad.key_off[i + 1] - bad.key_off[i])] = 10 ** 6      # index out of range
     with pytest.raises(engine.IllegalArgumentException):
         eng.merge_host([[bad, rep[1], rep[2]]])
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_wide_64bit_keys(engine_factory, hot):
+    # Murmur3-style 64-bit key tokens (the full u64 range): sorted in two 32-bit LSD halves, key segments by full
+    # 64-bit equality; deps, merge and levels equal the oracle
+    b = workload.generate(20000, keys_per_txn=4, keyspace=300 if hot else 10_000_000, seed=31 + hot)
+    rng = np.random.default_rng(7)
+    uniq = np.unique(b["keys"])
+    tok = np.sort(rng.choice(np.iinfo(np.uint64).max, size=len(uniq), replace=False).astype(np.uint64))
+    b["keys"] = tok[np.searchsorted(uniq, b["keys"])]      # order-preserving remap onto 64-bit tokens
+    check(engine_factory, b)
+
+
+def test_wide_64bit_ranges(engine_factory):
+    # range endpoints spread over ~2^62: each endpoint sorted in two 32-bit halves; keys scaled the same way
+    b = workload.generate(4000, 4, 20000, "uniform", range_frac=0.1, range_width_max=400, seed=33)
+    scale = np.uint64(1 << 44)
+    b["keys"] = b["keys"] * scale + np.uint64(12345)
+    b["range_start"] = b["range_start"] * scale + np.uint64(12345)
+    b["range_end"] = b["range_end"] * scale + np.uint64(12345)
+    check(engine_factory, b, window=8)
