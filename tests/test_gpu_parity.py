@@ -305,7 +305,8 @@ def test_wide_64bit_keys(engine_factory, hot):
     b = workload.generate(20000, keys_per_txn=4, keyspace=300 if hot else 10_000_000, seed=31 + hot)
     rng = np.random.default_rng(7)
     uniq = np.unique(b["keys"])
-    tok = np.sort(rng.choice(np.iinfo(np.uint64).max, size=len(uniq), replace=False).astype(np.uint64))
+    tok = np.unique(rng.integers(0, np.iinfo(np.uint64).max, size=2 * len(uniq), dtype=np.uint64, endpoint=True))
+    tok = np.sort(rng.choice(tok, size=len(uniq), replace=False))
     b["keys"] = tok[np.searchsorted(uniq, b["keys"])]      # order-preserving remap onto 64-bit tokens
     check(engine_factory, b)
 
