@@ -72,13 +72,11 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
         # write pass also writes the merged rows (16 B/txn + 8 B/entry)
         "k_merge<count>": units * 16 * R + 8 * D,
         "k_merge<write>": units * (16 * R + 16) + 8 * D + 8 * M,
-        # Kahn region per pair: the entry read by the chain build (17 B), its executeAt-ordered txn + successor
-        # run written (12 B), the release (successor run, txn, remaining-count RMW, level: 24 B); per txn the
-        # in-degree, remaining count and level (16 B)
-        "kahn_levels": units * (17 + 12 + 24) + calls * n * 16,
-        # executeAt blocks per pair: chain order (17 B in, 17 B out), block sort (2 x 16 B), record (16 B in,
-        # 8 B out), the walk's record read (8 B); per txn executeAt rank, block prefix, order and level (20 B)
-        "block_levels": units * (34 + 32 + 24 + 8) + calls * n * 20,
+        # the level stage priced as SURVEY §8(d) B_level: per pair its u64 entry (8 B), per predecessor edge
+        # (the walk items: entries with an earlier entry of their key) 8 B, per txn in-degree + level (8 B);
+        # the same figure for the Kahn region and for the executeAt-block path
+        "kahn_levels": calls * (P * 8 + W * 8 + n * 8),
+        "block_levels": calls * (P * 8 + W * 8 + n * 8),
         # window rank (12 B in, 16 B out), check (16 B), one level radix pass (4 + 16 B), order out (4 B)
         "order_sort": units * 68,
     }
@@ -104,7 +102,7 @@ def pipeline_alg_bytes(n, P, R, st, Q=0):
     b_scan = P * (8 + 24)
     b_out = n * 4 * 3 * R + D * 8
     b_merge = (n * 12 * R + D * 8) + (n * 12 + M * 8)
-    b_level = P * 8 + P * 8 + n * 4 * 2
+    b_level = P * 8 + st["walk_items"] * 8 + n * 4 * 2       # E = predecessor edges (walk items)
     return b_in + b_sort + b_scan + b_out + b_merge + b_level
 
 
@@ -302,10 +300,11 @@ def main_sharded(args, rank, world, local, dist):
     bounds = sharding.even_bounds(0, KEYSPACE * world, world)
     lb, gid, home = sharding.slice_for_shard(batch, bounds[rank], bounds[rank + 1])
     hs = sharding.home_stores(batch, bounds)[gid]
+    holders = sharding.holder_masks(batch, bounds)[gid]
     del batch
     device = local % max(1, engine.device_count())
     store = sharding.ShardStore(device, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C5"])
-    store.load(lb, gid, hs, n_total, rank, world)
+    store.load(lb, gid, hs, n_total, rank, world, holders=holders)     # delta level exchange
     tr = None
     if args.transport == "rccl":
         try:
@@ -357,6 +356,8 @@ def main_sharded(args, rank, world, local, dist):
                    "txns_total": n_total, "txns_per_gpu": args.n, "local_txns_rank0": n_loc, "local_pairs_rank0": P_loc,
                    "keys_per_txn": 4, "keyspace": KEYSPACE * world, "replicas": REPLICAS, "window": WINDOW,
                    "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds,
+                   "level_exchange_bytes_rank0": 8 * store.pairs_sent,
+                   "level_exchange_bytes_dense": 4 * (n_total + 1) * rounds,
                    "phase_ms_rank0": {k: round(v * 1e3 / args.steps, 3) for k, v in phases.items()}},
         "roofline": roof,
         "cpu_baseline": None,

@@ -86,7 +86,8 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_alltoall", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
-            "ad_shard_levels_allreduce", "ad_shard_order")
+            "ad_shard_levels_allreduce", "ad_shard_order", "ad_shard_set_holders", "ad_shard_levels_deltas",
+            "ad_shard_levels_apply", "ad_shard_levels_exchange")
 
 
 class DepsEngine:

@@ -71,6 +71,24 @@ def home_stores(batch, bounds):
     return np.clip(hs, 0, len(bounds) - 2).astype(np.uint8)
 
 
+def holder_masks(batch, bounds):
+    """Per global txn: bitmask of the stores holding it (the stores owning any of its keys).  A store's
+    chains hold only its own txns, so in the level rounds a raised level travels only to the other holders
+    (ShardStore.set_holders, the delta exchange)."""
+    n = batch["n"]
+    ko = batch["key_off"].astype(np.int64)
+    keys = batch["keys"]
+    b = np.asarray(bounds, np.uint64)
+    st = np.clip(np.searchsorted(b, keys, side="right") - 1, 0, len(b) - 2)
+    bits = (np.uint16(1) << st.astype(np.uint16)).astype(np.uint16)
+    out = np.zeros(n, np.uint16)
+    nz = ko[1:] > ko[:-1]
+    if len(keys):
+        red = np.bitwise_or.reduceat(bits, ko[:-1][nz])
+        out[nz] = red
+    return out.astype(np.uint8)
+
+
 def reduce_witnessed(batch, parts):
     """PreAccept.reduce of the stores' witnessedAt proposals (messages/PreAccept.java:141-156: witnessedAt =
     Timestamp.mergeMax, Timestamp.java:273-279) for the global batch: parts = [(gid, max_rank, fast)] per
@@ -139,6 +157,12 @@ class ShardStore:
         L.ad_shard_levels_set.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.ad_shard_levels_allreduce.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.ad_shard_order.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ad_shard_set_holders.argtypes = [vp, C.POINTER(C.c_uint8)]
+        L.ad_shard_levels_deltas.argtypes = [vp, C.POINTER(C.c_uint32), u64p]
+        L.ad_shard_levels_apply.argtypes = [vp, u64p, C.c_size_t]
+        L.ad_shard_levels_exchange.argtypes = [vp, C.POINTER(C.c_uint32)]
+        self.delta = False
+        self.pairs_sent = 0
 
     def close(self):
         self.eng.close()
@@ -147,8 +171,11 @@ class ShardStore:
         self.eng._check(rc, what)
 
     # ---- protocol steps
-    def load(self, local_batch, gid, home_store, n_global, rank, world):
-        """home_store: per local row, the store of the txn's first key (home_stores(global)[gid])."""
+    def load(self, local_batch, gid, home_store, n_global, rank, world, holders=None):
+        """home_store: per local row, the store of the txn's first key (home_stores(global)[gid]); holders
+        (optional): per local row, the bitmask of stores holding the txn (holder_masks(global)[gid]) —
+        given, the level rounds exchange only raised levels of shared txns (delta mode), else the whole
+        global level array is all-reduced each round (dense mode)."""
         self.eng.load(local_batch)
         self.gid = np.ascontiguousarray(gid, np.uint32)
         self.home_store = np.ascontiguousarray(home_store, np.uint8)
@@ -156,6 +183,11 @@ class ShardStore:
         self.rank, self.world = rank, world
         self._check(self.L.ad_shard_setup(self.eng.h, _u32p(self.gid), self.home_store.ctypes.data_as(C.POINTER(C.c_uint8)),
                                           rank, world, n_global), "ad_shard_setup")
+        self.delta = holders is not None
+        if self.delta:
+            self.holders = np.ascontiguousarray(holders, np.uint8)
+            self._check(self.L.ad_shard_set_holders(self.eng.h, self.holders.ctypes.data_as(C.POINTER(C.c_uint8))),
+                        "ad_shard_set_holders")
 
     def preaccept(self):
         self._check(self.L.ad_preaccept_deps(self.eng.h, None), "ad_preaccept_deps")
@@ -216,6 +248,12 @@ class ShardStore:
     def levels_round(self, first):
         ch = C.c_uint32()
         self._check(self.L.ad_shard_levels_round(self.eng.h, 1 if first else 0, C.byref(ch)), "ad_shard_levels_round")
+        if self.delta:
+            if first:
+                self.pairs_sent = 0
+            cnt = np.zeros(self.world, np.uint32)
+            self._check(self.L.ad_shard_levels_deltas(self.eng.h, _u32p(cnt), None), "ad_shard_levels_deltas")
+            self.pairs_sent += int(cnt.sum())       # level exchange volume of this batch: 8 B per pair
         return bool(ch.value)
 
     def levels_get(self):
@@ -231,6 +269,28 @@ class ShardStore:
         """RCCL all-reduce(max) of the level array; returns whether any store raised a level this round."""
         ch = C.c_uint32()
         self._check(self.L.ad_shard_levels_allreduce(self.eng.h, C.byref(ch)), "ad_shard_levels_allreduce")
+        return bool(ch.value)
+
+    def level_deltas(self):
+        """Delta mode: the last round's (gid << 32 | level) pairs per destination: (counts[world], pairs)."""
+        cnt = np.zeros(self.world, np.uint32)
+        self._check(self.L.ad_shard_levels_deltas(self.eng.h, _u32p(cnt), None), "ad_shard_levels_deltas")
+        pairs = np.zeros(max(int(cnt.sum()), 1), np.uint64)
+        self._check(self.L.ad_shard_levels_deltas(self.eng.h, _u32p(cnt), pairs.ctypes.data_as(C.POINTER(C.c_uint64))),
+                    "ad_shard_levels_deltas")
+        return cnt, pairs[:int(cnt.sum())]
+
+    def levels_apply(self, pairs):
+        p = np.ascontiguousarray(pairs, np.uint64)
+        if p.size == 0:
+            return
+        self._check(self.L.ad_shard_levels_apply(self.eng.h, p.ctypes.data_as(C.POINTER(C.c_uint64)), p.size),
+                    "ad_shard_levels_apply")
+
+    def levels_exchange(self):
+        """RCCL delta exchange; returns whether any store sent a pair this round."""
+        ch = C.c_uint32()
+        self._check(self.L.ad_shard_levels_exchange(self.eng.h, C.byref(ch)), "ad_shard_levels_exchange")
         return bool(ch.value)
 
     def order(self):
@@ -285,7 +345,18 @@ class GlooTransport:
         store.import_host(recv.numpy(), rsz)
 
     def allreduce_levels(self, store, changed):
-        """All-reduce(max) of the level array; returns whether any store raised a level this round."""
+        """Delta mode: all-to-all of the raised levels of shared txns; dense mode: all-reduce(max) of the level
+        array.  Returns whether any store raised a level another store needs (dense: raised any level)."""
+        if store.delta:
+            cnt, pairs = store.level_deltas()
+            if not self.any(int(cnt.sum()) > 0):
+                return False
+            rcnt = self.recv_sizes(cnt.astype(np.uint64))
+            recv = self.torch.zeros(int(rcnt.sum()), dtype=self.torch.int64)
+            self.dist.all_to_all_single(recv, self.torch.from_numpy(pairs.view(np.int64).copy()),
+                                        output_split_sizes=[int(x) for x in rcnt], input_split_sizes=[int(x) for x in cnt])
+            store.levels_apply(recv.numpy().view(np.uint64))
+            return True
         g = self.torch.from_numpy(store.levels_get().astype(np.int32))
         self.dist.all_reduce(g, op=self.dist.ReduceOp.MAX)
         store.levels_set(g.numpy().astype(np.uint32))
@@ -344,6 +415,8 @@ class RcclTransport(GlooTransport):
         store.alltoall(self.recv_sizes(sizes))
 
     def allreduce_levels(self, store, changed):
+        if store.delta:
+            return store.levels_exchange()   # counts all-gather + pair send/recv, all over RCCL
         return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
 
@@ -372,6 +445,14 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None):
     lap("exchange")
     store.merge()
     lap("merge")
+    return run_levels(store, transport, max_rounds, lap)
+
+
+def run_levels(store, transport, max_rounds=1 << 16, lap=None):
+    """The distributed level fixpoint: local rounds over the store's own key chains, then the
+    transport's exchange (delta pairs to the peers holding each raised txn, or the dense all-reduce), until no
+    store has anything left to tell another.  Returns the number of rounds."""
+    lap = lap or (lambda name: None)
     changed = store.levels_round(True)
     lap("levels_local")
     rounds = 1
@@ -406,11 +487,22 @@ class LocalTransport:
         changed = [s.levels_round(True) for s in stores]
         rounds = 1
         while True:
-            g = np.maximum.reduce([s.levels_get() for s in stores])
-            for s in stores:
-                s.levels_set(g)
-            if not any(changed):
-                break
+            if all(s.delta for s in stores):
+                out = [s.level_deltas() for s in stores]
+                for d, s in enumerate(stores):
+                    parts = []
+                    for k, (cnt, pairs) in enumerate(out):
+                        o = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
+                        parts.append(pairs[o[d]:o[d + 1]])
+                    s.levels_apply(np.concatenate(parts))
+                if not any(int(c.sum()) for c, _ in out):
+                    break
+            else:
+                g = np.maximum.reduce([s.levels_get() for s in stores])
+                for s in stores:
+                    s.levels_set(g)
+                if not any(changed):
+                    break
             if rounds >= max_rounds:
                 raise LevelsNotConverged("distributed execution levels still changing after %d rounds" % rounds)
             changed = [s.levels_round(False) for s in stores]

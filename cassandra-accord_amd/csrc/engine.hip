@@ -114,6 +114,11 @@ struct ad_handle {
     std::vector<Csr> sdeps;          // home-indexed per (view, class)
     Csr smerged[3];
     ncclComm_t comm = nullptr;
+    // delta level exchange (ad_shard_set_holders): per-row holder masks, per-destination send regions
+    uint8_t* holders = nullptr;
+    uint32_t *dbase_dev = nullptr, *dcnt_dev = nullptr;
+    uint64_t* dout = nullptr;
+    std::vector<uint32_t> dbase, dcnt;   // [world + 1] region starts; [world] last round's pair counts
     // MaxConflicts carried from earlier batches (ad_max_conflicts_carry): sorted keys + timestamps on the device
     size_t mc_m = 0;
     uint64_t *mc_ck = nullptr, *mc_cm = nullptr, *mc_cl = nullptr;
@@ -204,7 +209,7 @@ enum Slot : size_t {
     S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
     S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST, S_MCLOCAL, S_MCCK, S_MCCM, S_MCCL, S_MCCN,
     S_MCOM, S_MCOL, S_MCON, S_MCOF, S_MCSK, S_MCSM, S_MCSL, S_MCSN, S_MCSU, S_MCSP,
-    S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS,
+    S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV,
     S_NUM_FIXED,
     S_CSR0 = 160
 };
@@ -1529,6 +1534,8 @@ int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home_store,
     h->n_global = n_global;
     h->self = self;
     h->world = world;
+    h->holders = nullptr;
+    h->dcnt.assign(world, 0);
     h->have_deps = h->have_merged = h->have_levels = false;
     return AD_OK;
 }
@@ -1889,12 +1896,131 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     CK(run_levels(h->ls, li, false, st, &iters, h->err));
     if (first) h->ls.chains_ready = true;
     HIPCHK(h, hipMemsetAsync(flag, 0, 4, st));
-    if (n) k_levels_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl, flag);
-    // the flag also rides in G[n_global], so the RCCL all-reduce(max) returns "any store changed"
-    HIPCHK(h, hipMemcpyAsync(h->G + h->n_global, flag, 4, hipMemcpyDeviceToDevice, st));
+    if (h->holders) {
+        const uint32_t W = h->world;
+        HIPCHK(h, hipMemsetAsync(h->dcnt_dev, 0, W * 4, st));
+        const uint32_t others = ((1u << W) - 1u) & ~(1u << h->self);
+        if (n) k_level_deltas<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->holders, others, h->G, h->lvl,
+                                                                     h->dbase_dev, h->dcnt_dev, h->dout, flag);
+        HIPCHK(h, hipMemcpyAsync(h->dcnt.data(), h->dcnt_dev, W * 4, hipMemcpyDeviceToHost, st));
+    } else {
+        if (n) k_levels_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl, flag);
+        // the flag also rides in G[n_global], so the RCCL all-reduce(max) returns "any store changed"
+        HIPCHK(h, hipMemcpyAsync(h->G + h->n_global, flag, 4, hipMemcpyDeviceToDevice, st));
+    }
     HIPCHK(h, hipMemcpyAsync(changed, flag, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     h->level_iters += (uint32_t)iters;
+    return AD_OK;
+}
+
+int ad_shard_set_holders(ad_handle* h, const uint8_t* holders) {
+    if (!h || (!holders && h->n)) return AD_ERR_ARGUMENT;
+    if (!h->sharded) return set_err(h, AD_ERR_STATE, "ad_shard_set_holders: ad_shard_setup first");
+    hipSetDevice(h->device);
+    const size_t n = h->n;
+    const uint32_t W = h->world, self_bit = 1u << h->self, all = (1u << W) - 1u;
+    std::vector<uint64_t> cap(W, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t m = holders[i];
+        if (!(m & self_bit) || (m & ~all)) return set_err(h, AD_ERR_ARGUMENT, "holders: every mask holds this store and only stores < world");
+        for (uint32_t d = 0; d < W; ++d) cap[d] += (d != h->self) && ((m >> d) & 1u);
+    }
+    h->dbase.assign(W + 1, 0);
+    for (uint32_t d = 0; d < W; ++d) {
+        if (h->dbase[d] + cap[d] > 0xFFFFFFFFull) return set_err(h, AD_ERR_UNSUPPORTED, "holders: more than 2^32 shared rows");
+        h->dbase[d + 1] = h->dbase[d] + (uint32_t)cap[d];
+    }
+    CK(dalloc(h, S_HOLD, &h->holders, std::max<size_t>(n, 1)));
+    CK(dalloc(h, S_DBASE, &h->dbase_dev, MAX_STORES + 1));
+    CK(dalloc(h, S_DCNT, &h->dcnt_dev, MAX_STORES));
+    CK(dalloc(h, S_DOUT, &h->dout, std::max<size_t>(h->dbase[W], 1)));
+    if (n) HIPCHK(h, hipMemcpyAsync(h->holders, holders, n, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipMemcpyAsync(h->dbase_dev, h->dbase.data(), (W + 1) * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->dcnt.assign(W, 0);
+    return AD_OK;
+}
+
+int ad_shard_levels_deltas(ad_handle* h, uint32_t* counts, uint64_t* pairs) {
+    if (!h || !counts) return AD_ERR_ARGUMENT;
+    if (!h->holders) return set_err(h, AD_ERR_STATE, "ad_shard_levels_deltas: ad_shard_set_holders + a round first");
+    hipSetDevice(h->device);
+    size_t at = 0;
+    for (uint32_t d = 0; d < h->world; ++d) {
+        counts[d] = h->dcnt[d];
+        if (pairs && h->dcnt[d])
+            HIPCHK(h, hipMemcpyAsync(pairs + at, h->dout + h->dbase[d], (size_t)h->dcnt[d] * 8, hipMemcpyDeviceToHost, h->st));
+        at += h->dcnt[d];
+    }
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
+static int apply_level_pairs(ad_handle* h, const uint64_t* dev_pairs, size_t m) {
+    if (m) k_level_apply<<<ceil_div((long)m, 256), 256, 0, h->st>>>(m, dev_pairs, h->G);
+    HIPCHK(h, hipGetLastError());
+    return AD_OK;
+}
+
+int ad_shard_levels_apply(ad_handle* h, const uint64_t* pairs, size_t m) {
+    if (!h || (m && !pairs)) return AD_ERR_ARGUMENT;
+    if (!h->G) return set_err(h, AD_ERR_STATE, "ad_shard_levels_apply: a level round first");
+    hipSetDevice(h->device);
+    for (size_t i = 0; i < m; ++i)
+        if ((pairs[i] >> 32) >= h->n_global) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_levels_apply: global rank out of range");
+    uint64_t* buf = nullptr;
+    CK(dalloc(h, S_DRECV, &buf, std::max<size_t>(m, 1)));
+    if (m) HIPCHK(h, hipMemcpyAsync(buf, pairs, m * 8, hipMemcpyHostToDevice, h->st));
+    CK(apply_level_pairs(h, buf, m));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return AD_OK;
+}
+
+// RCCL: every store all-gathers the per-destination pair counts (a world x world matrix: row s = what store s
+// sends), then the pairs move by grouped point-to-point send/recv and are max-folded into G.
+int ad_shard_levels_exchange(ad_handle* h, uint32_t* any_sent) {
+    if (!h || !any_sent) return AD_ERR_ARGUMENT;
+    if (!h->comm || !h->holders || !h->G) return set_err(h, AD_ERR_STATE, "ad_shard_levels_exchange: ad_comm_init + ad_shard_set_holders + a round first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const uint32_t W = h->world;
+    uint32_t* mat = nullptr;
+    CK(dalloc(h, S_DMAT, &mat, (size_t)MAX_STORES * MAX_STORES));
+    ncclResult_t r = ncclAllGather(h->dcnt_dev, mat, W, ncclUint32, h->comm, st);
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllGather (level counts): ") + ncclGetErrorString(r));
+    std::vector<uint32_t> M((size_t)W * W);
+    HIPCHK(h, hipMemcpyAsync(M.data(), mat, (size_t)W * W * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    uint64_t total_sent = 0, recv_total = 0;
+    for (uint32_t s = 0; s < W; ++s)
+        for (uint32_t d = 0; d < W; ++d) total_sent += M[(size_t)s * W + d];
+    for (uint32_t s = 0; s < W; ++s) recv_total += M[(size_t)s * W + h->self];
+    *any_sent = total_sent ? 1u : 0u;
+    if (!total_sent) return AD_OK;
+    uint64_t* buf = nullptr;
+    CK(dalloc(h, S_DRECV, &buf, std::max<size_t>(recv_total, 1)));
+    if (ncclGroupStart() != ncclSuccess) return set_err(h, AD_ERR_DEVICE, "ncclGroupStart");
+    ncclResult_t first = ncclSuccess;
+    std::string what;
+    size_t ro = 0;
+    for (uint32_t p = 0; p < W && first == ncclSuccess; ++p) {
+        const uint32_t sn = h->dcnt[p], rn = M[(size_t)p * W + h->self];
+        if (sn) {
+            ncclResult_t e = ncclSend(h->dout + h->dbase[p], (size_t)sn * 8, ncclUint8, (int)p, h->comm, st);
+            if (e != ncclSuccess) { first = e; what = "ncclSend (levels) to " + std::to_string(p); }
+        }
+        if (first == ncclSuccess && rn) {
+            ncclResult_t e = ncclRecv(buf + ro, (size_t)rn * 8, ncclUint8, (int)p, h->comm, st);
+            if (e != ncclSuccess) { first = e; what = "ncclRecv (levels) from " + std::to_string(p); }
+        }
+        ro += rn;
+    }
+    r = ncclGroupEnd();
+    if (first != ncclSuccess) return set_err(h, AD_ERR_DEVICE, what + ": " + ncclGetErrorString(first));
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclGroupEnd (levels): ") + ncclGetErrorString(r));
+    CK(apply_level_pairs(h, buf, recv_total));
+    HIPCHK(h, hipStreamSynchronize(st));
     return AD_OK;
 }
 

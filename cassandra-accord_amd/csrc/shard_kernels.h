@@ -216,4 +216,49 @@ __global__ __launch_bounds__(256) void k_levels_scatter(size_t n, const uint32_t
     wave_set_flag(up, changed);
 }
 
+// Delta level exchange: a store's chains hold only the txns that touch its keys, so the only
+// levels another store needs are those of the txns both hold.  Per round, every level this store raised is
+// folded into its own G and, for a txn other stores hold too (holders[r]: bitmask of the stores holding row
+// r), appended as (gid << 32 | level) to each of those stores' regions of `out` (region d starts at base[d]
+// and holds at most the rows shared with d: no overflow).  Order inside a region is free: the receiver folds
+// with max.  *sent: some pair was appended.
+__global__ __launch_bounds__(256) void k_level_deltas(size_t n, const uint32_t* __restrict__ gid, const uint8_t* __restrict__ holders,
+                                                      uint32_t others, uint32_t* __restrict__ G, const uint32_t* __restrict__ L,
+                                                      const uint32_t* __restrict__ base, uint32_t* __restrict__ cnt,
+                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ sent) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t m = 0;
+    uint64_t pair = 0;
+    if (i < n) {
+        const uint32_t g = gid[i], l = L[i];
+        if (l > G[g]) {
+            G[g] = l;
+            m = holders[i] & others;
+            pair = ((uint64_t)g << 32) | l;
+        }
+    }
+    const int lane = (int)__lane_id();
+#pragma unroll
+    for (int d = 0; d < MAX_STORES; ++d) {
+        const bool want = (m >> d) & 1u;
+        const uint64_t b = __ballot(want);
+        if (!b) continue;
+        const int leader = __ffsll((unsigned long long)b) - 1;
+        uint32_t at = 0;
+        if (lane == leader) at = atomicAdd(cnt + d, (uint32_t)__popcll(b));
+        at = __builtin_amdgcn_readlane(at, leader);
+        if (want) out[base[d] + at + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = pair;
+    }
+    wave_set_flag(m != 0, sent);
+}
+
+// Received (gid << 32 | level) pairs folded into G (several stores may raise one txn: max).
+__global__ __launch_bounds__(256) void k_level_apply(size_t m, const uint64_t* __restrict__ pairs, uint32_t* __restrict__ G) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) {
+        const uint64_t p = pairs[i];
+        atomicMax(G + (uint32_t)(p >> 32), (uint32_t)p);
+    }
+}
+
 }  // namespace ad

@@ -295,9 +295,12 @@ int  ad_kernel_units(ad_handle* h, int kid, uint64_t* units);
 /*   exchange: all-to-all (the peers' byte counts give recv_sizes): ad_comm_init +              */
 /*   ad_shard_alltoall over RCCL/xGMI, or ad_shard_send_to_host / ad_shard_import_host over a   */
 /*   host transport -> ad_shard_merge                                                          */
-/*   levels: ad_shard_levels_round, all-reduce(max) of the global level array                  */
-/*   (ad_shard_levels_allreduce over RCCL, or _get/_set), repeat until no store raised a level; */
-/*   ad_shard_order.                                                                           */
+/*   levels, delta exchange (after ad_shard_set_holders): ad_shard_levels_round appends, per     */
+/*   peer store, the levels it raised for txns that peer also holds; ad_shard_levels_exchange   */
+/*   (RCCL: all-gather of the per-peer counts + grouped send/recv of the pairs) or              */
+/*   ad_shard_levels_deltas / ad_shard_levels_apply over a host transport; repeat until no      */
+/*   store sent a pair.  Dense variant (no holders set): all-reduce(max) of the whole global    */
+/*   level array (ad_shard_levels_allreduce, or _get/_set).  Then ad_shard_order.               */
 /* Home txn = its first key lies in this store's range; results are per home txn, TxnIds as    */
 /* global ranks.  Range txns are not supported in sharded mode (AD_ERR_UNSUPPORTED).  At most 8 */
 /* stores.                                                                                     */
@@ -314,7 +317,18 @@ int  ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id
 int  ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world]: peers' bytes[this store] */);
 int  ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes /* [(replicas+1)*3]; view == replicas: merged */, size_t* n_home);
 int  ad_shard_fetch(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out, uint32_t* home_gid /* [n_home] or NULL */);
-int  ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed);
+/* holders[r]: bitmask of the stores that hold local row r's txn (bit self set; < 1 << world).  Switches
+ * the level rounds to the delta exchange: per round only the raised levels of txns shared with a peer
+ * travel to that peer, as u64 (global rank << 32 | level) pairs. */
+int  ad_shard_set_holders(ad_handle* h, const uint8_t* holders /* [n] */);
+int  ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed /* delta mode: this store sent a pair */);
+/* The pairs of the last round per destination store: counts[world]; pairs (nullable) receives them
+ * concatenated in destination order. */
+int  ad_shard_levels_deltas(ad_handle* h, uint32_t* counts /* [world] */, uint64_t* pairs);
+int  ad_shard_levels_apply(ad_handle* h, const uint64_t* pairs, size_t m);      /* received pairs, max-folded */
+/* RCCL: exchange the last round's pairs with every peer; *any_sent = some store sent a pair this round
+ * (0: the levels are final on every store). */
+int  ad_shard_levels_exchange(ad_handle* h, uint32_t* any_sent);
 int  ad_shard_levels_get(ad_handle* h, uint32_t* G /* [n_global] */);
 int  ad_shard_levels_set(ad_handle* h, const uint32_t* G);
 int  ad_shard_levels_allreduce(ad_handle* h, uint32_t* any_changed /* out: max of the stores' round flags, or NULL */);

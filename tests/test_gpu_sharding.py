@@ -26,13 +26,17 @@ def same_txn(got, h, want, g):
     return all(np.array_equal(x, y) for x, y in zip(a, b))
 
 
-@pytest.mark.parametrize("name,shards", [("C2", 2), ("C2", 4), ("C3", 3)])
-def test_sharded_equals_unsharded(engine_factory, name, shards):
+@pytest.mark.parametrize("name,shards,delta", [("C2", 2, True), ("C2", 4, True), ("C3", 3, True), ("C3", 3, False),
+                                                ("C2", 4, False)])
+def test_sharded_equals_unsharded(engine_factory, name, shards, delta):
+    # delta: level rounds exchange only raised levels of shared txns (ad_shard_set_holders); else the dense
+    # all-reduce of the whole level array
     w, r, p, s = 32, 3, 0.1, 0xACC0D1
     b = workload.config(name, n=30000)
     views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
     bounds = sharding.even_bounds(0, 10_000_000, shards)
     hs = sharding.home_stores(b, bounds)
+    masks = sharding.holder_masks(b, bounds)
     stores = []
     try:
         for k in range(shards):
@@ -40,7 +44,7 @@ def test_sharded_equals_unsharded(engine_factory, name, shards):
             assert np.array_equal(home, (hs[gid] == k).astype(np.uint8))
             st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
             stores.append(st)
-            st.load(local, gid, hs[gid], b["n"], k, shards)
+            st.load(local, gid, hs[gid], b["n"], k, shards, holders=masks[gid] if delta else None)
         rounds = sharding.LocalTransport.run(stores)
         assert rounds >= 1
         seen = np.zeros(b["n"], bool)
@@ -96,15 +100,16 @@ def test_sharded_witnessed_at(engine_factory, name, shards):
             st.close()
 
 
-def _make_stores(b, shards, w, r, p, s, keyspace):
+def _make_stores(b, shards, w, r, p, s, keyspace, delta=True):
     bounds = sharding.even_bounds(0, keyspace, shards)
     hs = sharding.home_stores(b, bounds)
+    masks = sharding.holder_masks(b, bounds)
     stores = []
     for k in range(shards):
         local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
         st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
         stores.append(st)
-        st.load(local, gid, hs[gid], b["n"], k, shards)
+        st.load(local, gid, hs[gid], b["n"], k, shards, holders=masks[gid] if delta else None)
     return stores, bounds, hs
 
 
@@ -180,10 +185,12 @@ def test_host_fragments_import(engine_factory):
             st.close()
 
 
-def test_rccl_world1_run_store(engine_factory, tmp_path):
+@pytest.mark.parametrize("delta", [True, False])
+def test_rccl_world1_run_store(engine_factory, tmp_path, delta):
     # the RCCL transport end to end on the one GPU: a world = 1 communicator (ad_comm_init), the grouped
-    # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and ncclAllReduce level rounds
-    # (ad_shard_levels_allreduce), driven by the same run_store the N>1 bench uses; equal to the unsharded engine
+    # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and the level rounds — delta: ncclAllGather of
+    # the pair counts (ad_shard_levels_exchange); dense: ncclAllReduce of the level array
+    # (ad_shard_levels_allreduce) — driven by the same run_store the N>1 bench uses; equal to the unsharded engine
     import torch.distributed as dist
     w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
     b = workload.generate(200_000, 4, 10_000_000, "uniform", seed=s)
@@ -191,7 +198,7 @@ def test_rccl_world1_run_store(engine_factory, tmp_path):
     dist.init_process_group("gloo", init_method="file://%s" % (tmp_path / "rdv"), rank=0, world_size=1)
     stores = []
     try:
-        stores, _, _ = _make_stores(b, 1, w, r, p, s, 10_000_000)
+        stores, _, _ = _make_stores(b, 1, w, r, p, s, 10_000_000, delta=delta)
         tr = sharding.RcclTransport(dist, stores[0], 0, 1)
         assert tr.name == "rccl"
         rounds = sharding.run_store(stores[0], tr)
@@ -233,6 +240,8 @@ def test_c5_four_stores_1m_each(engine_factory):
     try:
         rounds = sharding.LocalTransport.run(stores)
         assert rounds >= 1
+        # delta exchange: the last round raised nothing another store needs
+        assert all(int(st.level_deltas()[0].sum()) == 0 for st in stores)
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all(), "every txn has exactly one home store"
     finally:

@@ -1,0 +1,127 @@
+"""The distributed level fixpoint's delta exchange on CPU: two processes over gloo (world_size 2, 127.0.0.1).
+
+Each rank holds the key chains of its key range only (a store's CommandsForKey); per round it resolves the
+levels of its local txns from its chains with the levels it knows as lower bounds, and sends each peer that
+also holds a txn the levels it raised (u64 global rank << 32 | level pairs) — the product path
+sharding.run_levels + GlooTransport.allreduce_levels in delta mode, with the store's local round played by a
+host model of the engine's round (HostLevelStore: the notifyManaged DP over the store's own chains, oracle.cpp
+exec_levels restricted to the store's keys).  The fixpoint must equal the oracle's levels of the unsharded
+batch for every txn, and pairs travel only between holders.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class HostLevelStore:
+    """Host model of ad_shard_levels_round / _deltas / _apply (csrc/shard_kernels.h k_level_deltas,
+    k_level_apply) for pure key batches of Reads and Writes."""
+
+    delta = True
+
+    def __init__(self, local, gid, holders, n_global, rank, world):
+        self.b, self.gid, self.holders = local, gid, holders.astype(np.int64)
+        self.rank, self.world = rank, world
+        self.G = np.zeros(n_global, np.uint64)
+        lsb, msb = local["exec_lsb"], local["exec_msb"]
+        self.by_exec = np.lexsort((local["exec_node"].astype(np.int64), lsb & np.uint64(0x1E), lsb >> np.uint64(16), msb))
+        self.write = ((local["txn_lsb"] >> np.uint64(1)) & np.uint64(7)) == 1
+        self.sent = []
+
+    def levels_round(self, first):
+        n = self.b["n"]
+        lo = np.zeros(n, np.int64) if first else self.G[self.gid].astype(np.int64)
+        lvl = np.zeros(n, np.int64)
+        max_all, max_w = {}, {}
+        ko, keys = self.b["key_off"], self.b["keys"]
+        for t in self.by_exec:
+            lv = -1
+            ks = [int(k) for k in keys[ko[t]:ko[t + 1]]]
+            for k in ks:
+                lv = max(lv, max_all.get(k, -1) if self.write[t] else max_w.get(k, -1))
+            lvl[t] = max(lv + 1, lo[t])
+            for k in ks:
+                max_all[k] = max(max_all.get(k, -1), lvl[t])
+                if self.write[t]:
+                    max_w[k] = max(max_w.get(k, -1), lvl[t])
+        up = lvl > self.G[self.gid].astype(np.int64)
+        self.G[self.gid[up]] = lvl[up].astype(np.uint64)
+        others = ((1 << self.world) - 1) & ~(1 << self.rank)
+        self.cnt = np.zeros(self.world, np.uint32)
+        parts = []
+        for d in range(self.world):
+            sel = up & ((self.holders & others & (1 << d)) != 0)
+            self.cnt[d] = sel.sum()
+            parts.append((self.gid[sel].astype(np.uint64) << np.uint64(32)) | lvl[sel].astype(np.uint64))
+        self.pairs = np.concatenate(parts) if parts else np.zeros(0, np.uint64)
+        self.sent.append(int(self.cnt.sum()))
+        return bool(self.cnt.sum())
+
+    def level_deltas(self):
+        return self.cnt, self.pairs
+
+    def levels_apply(self, pairs):
+        g = (pairs >> np.uint64(32)).astype(np.int64)
+        lv = pairs & np.uint64(0xFFFFFFFF)
+        np.maximum.at(self.G, g, lv)
+
+
+def _worker(rank, world, port, n):
+    sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import torch
+    from accord_amd import abi, sharding, workload
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = workload.generate(n, 3, 3000, "zipf", seed=11)           # deep chains crossing both stores
+        bounds = sharding.even_bounds(0, 3000, world)
+        masks = sharding.holder_masks(b, bounds)
+        local, gid, _ = sharding.slice_for_shard(b, bounds[rank], bounds[rank + 1])
+        assert (masks[gid] & (1 << rank)).all()
+        store = HostLevelStore(local, gid, masks[gid], n, rank, world)
+        tr = sharding.GlooTransport(dist)
+        rounds = sharding.run_levels(store, tr)
+        assert rounds >= 2                                           # the chains really couple across stores
+        want, _ = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_LEVELS).levels()
+        got = store.G[gid].astype(np.uint32)
+        assert np.array_equal(got, want[gid]), "rank %d: levels differ at %s" % (rank, np.nonzero(got != want[gid])[0][:8])
+        # only levels of txns the peer also holds travel, never more than once per raise
+        shared = int(((masks[gid] & ~np.uint8(1 << rank)) != 0).sum())
+        assert store.sent[0] <= shared
+        tot = torch.tensor([sum(store.sent)], dtype=torch.int64)
+        dist.all_reduce(tot)
+        assert tot.item() > 0
+    finally:
+        dist.destroy_process_group()
+
+
+def test_delta_level_exchange_over_gloo():
+    mp.spawn(_worker, args=(2, _free_port(), 3000), nprocs=2, join=True)
+
+
+def test_holder_masks():
+    sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+    from accord_amd import sharding
+    b = {"n": 4, "key_off": np.array([0, 2, 2, 3, 5], np.uint32),
+         "keys": np.array([1, 9, 5, 2, 8], np.uint64)}
+    m = sharding.holder_masks(b, sharding.even_bounds(0, 10, 2))
+    assert m.tolist() == [3, 0, 2, 3]
