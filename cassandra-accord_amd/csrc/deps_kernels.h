@@ -39,6 +39,8 @@ struct Params {                // device-side batch statistics (filled by k_minm
     unsigned int max_keys, err;                  // err bits below
     unsigned int n_large, n_keys_u;              // large txns; distinct keys (after sort)
     unsigned long long n_vitems;                 // virtual items
+    unsigned int n_special, pad_;                // key-domain txns that are not Read/Write (sync points,
+                                                 // ephemeral reads, local-only): unmanaged execution
 };
 enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
                   ERR_RANGEBITS = 32, ERR_CAP = 64 };
@@ -47,7 +49,7 @@ __global__ void k_params_init(Params* p) {
     p->msb_min = ~0ull; p->msb_max = 0; p->hlc_min = ~0ull; p->hlc_max = 0;
     p->key_min = ~0ull; p->key_max = 0; p->rs_min = ~0ull; p->re_max = 0; p->rw_max = 0;
     p->node_min_b = ~0u; p->node_max_b = 0; p->max_keys = 0; p->err = 0;
-    p->n_large = 0; p->n_keys_u = 0; p->n_vitems = 0;
+    p->n_large = 0; p->n_keys_u = 0; p->n_vitems = 0; p->n_special = 0; p->pad_ = 0;
 }
 
 __device__ inline unsigned long long wmin64(unsigned long long v) {
@@ -69,11 +71,11 @@ __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __rest
                                                 const uint32_t* __restrict__ key_off, const uint64_t* __restrict__ keys,
                                                 size_t P, const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
                                                 size_t Q, unsigned long long* __restrict__ partial) {
-    constexpr int NF = 13;
+    constexpr int NF = 14, NSUM = 12;
     // fields: 0 msb_min 1 msb_max 2 hlc_min 3 hlc_max 4 node_min 5 node_max 6 key_min 7 key_max 8 max_keys
     //         9 rs_min 10 re_max 11 rw_max ; *_min are stored complemented so every field is a max
-    //         12 large txns (a sum)
-    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    //         12 large txns, 13 special key-domain txns (sums, fields >= NSUM)
+    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         unsigned long long a = tm[i], b = em[i], ha = tl[i] >> 16, hb = el[i] >> 16;
@@ -84,6 +86,8 @@ __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __rest
         const unsigned kc = key_off[i + 1] - key_off[i];
         f[8] = max(f[8], (unsigned long long)kc);
         f[12] += ((tl[i] & 1) == AD_DOMAIN_RANGE || kc > (unsigned)KMAX) ? 1ull : 0ull;
+        const unsigned kind = (unsigned)((tl[i] >> 1) & 7);
+        f[13] += ((tl[i] & 1) == AD_DOMAIN_KEY && kind != AD_KIND_READ && kind != AD_KIND_WRITE) ? 1ull : 0ull;
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
         unsigned long long k = keys[i];
@@ -96,39 +100,40 @@ __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __rest
     __shared__ unsigned long long red[4][NF];
     const int w = threadIdx.x / WAVE;
 #pragma unroll
-    for (int k = 0; k < NF - 1; ++k) {
+    for (int k = 0; k < NSUM; ++k) {
         unsigned long long v = wmax64(f[k]);
         if (__lane_id() == 0) red[w][k] = v;
     }
-    {
-        unsigned long long v = f[NF - 1];
+#pragma unroll
+    for (int k = NSUM; k < NF; ++k) {
+        unsigned long long v = f[k];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (__lane_id() == 0) red[w][NF - 1] = v;
+        if (__lane_id() == 0) red[w][k] = v;
     }
     __syncthreads();
     if (threadIdx.x < NF) {
         const int k = threadIdx.x;
-        unsigned long long v = k == NF - 1 ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
-                                           : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
+        unsigned long long v = k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
+                                         : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
         partial[(size_t)blockIdx.x * NF + k] = v;
     }
 }
 
 // second level of k_minmax: one block folds the per-block partials into Params (no contended atomics)
 __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out) {
-    constexpr int NF = 13;
+    constexpr int NF = 14, NSUM = 12;
     __shared__ unsigned long long red[4][NF];
-    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = threadIdx.x; b < nblk; b += blockDim.x)
         for (int k = 0; k < NF; ++k) {
             const unsigned long long v = partial[(size_t)b * NF + k];
-            f[k] = k == NF - 1 ? f[k] + v : max(f[k], v);
+            f[k] = k >= NSUM ? f[k] + v : max(f[k], v);
         }
     const int w = threadIdx.x / WAVE;
     for (int k = 0; k < NF; ++k) {
         unsigned long long v = f[k];
-        if (k == NF - 1) {
+        if (k >= NSUM) {
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         } else {
             v = wmax64(v);
@@ -138,8 +143,8 @@ __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned l
     __syncthreads();
     if (threadIdx.x < NF) {
         const int k = threadIdx.x;
-        unsigned long long v = k == NF - 1 ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
-                                           : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
+        unsigned long long v = k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
+                                         : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
         switch (k) {
             case 0: atomicMin(&out->msb_min, ~v); break;
             case 1: atomicMax(&out->msb_max, v); break;
@@ -154,6 +159,7 @@ __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned l
             case 10: atomicMax(&out->re_max, v); break;
             case 11: atomicMax(&out->rw_max, v); break;
             case 12: if (v) atomicAdd(&out->n_large, (unsigned)v); break;
+            case 13: if (v) atomicAdd(&out->n_special, (unsigned)v); break;
         }
     }
 }

@@ -290,15 +290,23 @@ __global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __
     }
 }
 
-// Rejects kinds the batch execution order does not model (sync points, ephemeral reads, local-only).
+// Rejects kinds the batch execution order does not model (local-only txns are not globally visible).
 __global__ __launch_bounds__(256) void k_level_kinds(size_t n, const uint8_t* __restrict__ meta, uint32_t* __restrict__ flag) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool bad = false;
-    if (t < n) {
-        const uint32_t k = meta_kind(meta[t]);
-        bad = !(k == AD_KIND_READ || k == AD_KIND_WRITE);
-    }
+    if (t < n) bad = meta_kind(meta[t]) == AD_KIND_LOCAL_ONLY;
     wave_set_flag(bad, flag);
+}
+
+// Txn.Kind.awaitsOnlyDeps (Txn.java:211-214): ExclusiveSyncPoint and EphemeralRead wait for every dependency,
+// whatever its executeAt (Commands.initialiseWaitingOn :690-691 waits at maxForEpoch).
+__device__ inline bool awaits_only_deps(uint32_t m) {
+    const uint32_t k = meta_kind(m);
+    return k == AD_KIND_EXCLUSIVE_SYNC_POINT || k == AD_KIND_EPHEMERAL_READ;
+}
+__device__ inline bool is_sync_point(uint32_t m) {
+    const uint32_t k = meta_kind(m);
+    return k == AD_KIND_SYNC_POINT || k == AD_KIND_EXCLUSIVE_SYNC_POINT;
 }
 
 struct EdgeArgs {
@@ -325,19 +333,29 @@ struct EdgeArgs {
     const uint64_t* c_exec1;
     const uint32_t* c_txn;
     const int32_t* seg_start;
+    // sync points: the key's entries in TxnId order (CommandsForKey.byId)
+    const uint32_t* e_txn;
+    const uint8_t* e_meta;
+    const uint64_t* e_exec1;
     PushCtx push;
     uint32_t* changed;           // any edge raised a level this iteration
     uint32_t* work_left;
 };
 
 // (c) preparation: for unmanaged T and each key of its merged KeyDeps, the last chain position (in
-// executeAt order) whose executeAt <= bnd = max executeAt of T's deps on that key below T's own.
+// executeAt order) whose executeAt <= bnd = max executeAt of T's qualifying deps on that key
+// (Updating.updateUnmanaged :740-792): below T's own executeAt, any for an EphemeralRead, any earlier TxnId
+// for an ExclusiveSyncPoint; sync points also fold the key's managed-execution entries between their first
+// and last dependency in TxnId order (:760-777; a loop over that byId range).
 // One wave per txn, one lane per key of its merged KeyDeps (a C4 range txn has ~3*10^3 of them).
 __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n) return;
     const uint32_t kb = a.mk_key_off[t], ke = a.mk_key_off[t + 1];
-    const bool unmanaged = !manages_execution(a.meta[t]);
+    const uint32_t mt = a.meta[t];
+    const bool unmanaged = !manages_execution(mt);
+    const bool any_exec = awaits_only_deps(mt);            // ESP deps all have earlier TxnIds
+    const bool sync = is_sync_point(mt);
     const uint32_t nk = ke - kb;
     const uint32_t mb = a.mk_k2t_off[t];
     const uint32_t tb = a.mk_ent_off[t];
@@ -350,16 +368,27 @@ __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
             uint64_t bnd = 0;
             for (uint32_t x = from; x < to; ++x) {
                 const uint64_t e = a.ex1[a.mk_txns[tb + (uint32_t)a.mk_k2t[x]]];
-                if (e < my && e > bnd) bnd = e;
+                if ((any_exec || e < my) && e > bnd) bnd = e;
             }
-            if (bnd != 0) {
-                const uint64_t key = a.mk_keys[kb + ki];
-                const uint32_t u = lb_u64(a.ukey, 0, a.U, key);
-                if (u < a.U && a.ukey[u] == key) {
-                    const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
-                    const uint32_t p = ub_u64(a.c_exec1, s0, s1, bnd);     // first executeAt+1 > bnd
-                    pos = p > s0 ? (int32_t)(p - 1) : -1;
+            const uint64_t key = a.mk_keys[kb + ki];
+            const uint32_t u = from < to ? lb_u64(a.ukey, 0, a.U, key) : a.U;
+            const bool found = u < a.U && a.ukey[u] == key;
+            if (sync && found) {
+                // per-key lists are ascending: first and last dependency (batch ranks = TxnId order)
+                const uint32_t f = a.mk_txns[tb + (uint32_t)a.mk_k2t[from]], l = a.mk_txns[tb + (uint32_t)a.mk_k2t[to - 1]];
+                const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+                uint32_t lo = s0, hi = s1;
+                while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (a.e_txn[m] < f) lo = m + 1; else hi = m; }
+                for (uint32_t x = lo; x < s1 && a.e_txn[x] <= l; ++x) {
+                    const uint32_t em = a.e_meta[x];
+                    const uint64_t e = a.e_exec1[x];
+                    if (manages_execution(em) && (any_exec || e < my) && e > bnd) bnd = e;
                 }
+            }
+            if (bnd != 0 && found) {
+                const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+                const uint32_t p = ub_u64(a.c_exec1, s0, s1, bnd);     // first executeAt+1 > bnd
+                pos = p > s0 ? (int32_t)(p - 1) : -1;
             }
         }
         a.cons_pos[kb + ki] = pos;
@@ -375,13 +404,14 @@ __global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int d
         const uint64_t my = a.ex1[t];
         int best = -1;
         if (do_b) {
+            const bool all = awaits_only_deps(a.meta[t]);
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 if (!a.txns[c]) continue;
                 const uint32_t b = a.ent_off[c][t], e = b + a.tcnt[c][t];
                 for (uint32_t x = b; x < e; ++x) {
                     const uint32_t d = a.txns[c][x];
-                    if (a.ex1[d] < my) best = max(best, (int)a.L[d]);
+                    if (all || a.ex1[d] < my) best = max(best, (int)a.L[d]);
                 }
             }
         }
@@ -593,9 +623,6 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
 // keys the first successor of every pair is released with all loads and atomics issued together (the
 // returning atomics are the latency of this kernel); longer runs and wider txns go serially.
 constexpr int KAHN_GRID = 2048;
-__device__ inline void kahn_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
-    if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
-}
 // ---------------------------------------------------------------------------------------------------
 // Kahn chain build for batches with long chains (C3's Zipf hot keys: ~10^5 entries on one key), all
 // positions in parallel instead of one thread per segment:
@@ -716,18 +743,50 @@ __global__ __launch_bounds__(256) void k_chain_links(size_t P, const int32_t* __
 // them itself; heavier ones (a range txn can have thousands of dependants) are released by the whole wave,
 // 64 lanes per edge run.
 constexpr uint64_t XLIGHT = 8;
-__global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
-                                                   uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
-                                                   const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
-                                                   const uint32_t* __restrict__ c_txn, const uint32_t* gate, int gate_is_abort,
-                                                   uint32_t* __restrict__ work, const uint64_t* __restrict__ xoff,
-                                                   const uint32_t* __restrict__ xs) {
-    if (gate_is_abort ? *gate != 0u : *gate == 0u) return;
-    bool released = false;
+
+// Frontier-list wavefronts: the txns of level `lvl` release their successors; a successor whose remaining count
+// reaches zero gets level lvl + 1 and is appended to the next frontier list.  SWEEP (a batch's first launch: level
+// 0, or a level resumed after k_kahn_small) finds its frontier by scanning all n txns; list launches walk only
+// the frontier (*cin entries of fin), so the narrow tail levels of a shallow graph cost a near-empty launch
+// instead of a sweep over n.  Appends go to a per-workgroup LDS buffer (LDS atomics), flushed with one global
+// atomicAdd per workgroup; a buffer overflow appends directly.
+constexpr uint32_t KF_BUF = 4096;
+__device__ inline void kf_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
+                                  uint32_t* sbuf, uint32_t* scnt, uint32_t* __restrict__ fout, uint32_t* __restrict__ cout) {
+    if (atomicSub(&rem[s], 1u) == 1u) {
+        L[s] = lvl + 1;
+        const uint32_t at = atomicAdd(scnt, 1u);
+        if (at < KF_BUF) sbuf[at] = s;
+        else fout[atomicAdd(cout, 1u)] = s;
+    }
+}
+template <bool SWEEP>
+__global__ __launch_bounds__(256) void k_kahn_front(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
+                                                    uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
+                                                    const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
+                                                    const uint32_t* __restrict__ c_txn, const uint32_t* abort_gate,
+                                                    const uint32_t* __restrict__ fin, const uint32_t* cin,
+                                                    uint32_t* __restrict__ fout, uint32_t* cout,
+                                                    const uint64_t* __restrict__ xoff, const uint32_t* __restrict__ xs) {
+    __shared__ uint32_t sbuf[KF_BUF];
+    __shared__ uint32_t scnt, sbase;
+    if (abort_gate && *abort_gate != 0u) return;
+    const size_t m = SWEEP ? n : (size_t)*cin;
+    if (m == 0) return;
+    if (threadIdx.x == 0) scnt = 0;
+    __syncthreads();
     // block-aligned stride: every lane of a wave runs the same iterations (the heavy-run ballot below)
-    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
-        const size_t t = base + threadIdx.x;
-        const bool mine = t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < m; base += (size_t)gridDim.x * blockDim.x) {
+        const size_t idx = base + threadIdx.x;
+        uint32_t t = 0;
+        bool mine;
+        if (SWEEP) {
+            t = (uint32_t)idx;
+            mine = idx < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
+        } else {
+            mine = idx < m;
+            if (mine) t = fin[idx];
+        }
         if (mine) {
             const uint32_t b = key_off[t], e = key_off[t + 1];
             if (e - b <= 4) {
@@ -741,14 +800,19 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
                 for (int j = 0; j < 4; ++j) rr[j] = sc[j].y ? atomicSub(&rem[sx[j]], 1u) : 0u;
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if (sc[j].y && rr[j] == 1u) { L[sx[j]] = lvl + 1; released = true; }
+                    if (sc[j].y && rr[j] == 1u) {
+                        L[sx[j]] = lvl + 1;
+                        const uint32_t at = atomicAdd(&scnt, 1u);
+                        if (at < KF_BUF) sbuf[at] = sx[j];
+                        else fout[atomicAdd(cout, 1u)] = sx[j];
+                    }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kf_release(c_txn[x], lvl, rem, L, sbuf, &scnt, fout, cout);
             } else {
                 for (uint32_t p = b; p < e; ++p) {
                     const uint2 sc = succ[p];
-                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kf_release(c_txn[x], lvl, rem, L, sbuf, &scnt, fout, cout);
                 }
             }
         }
@@ -757,7 +821,7 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
             if (mine) { xb = xoff[t]; xe = xoff[t + 1]; }
             const bool heavy = xe - xb > XLIGHT;
             if (mine && !heavy)
-                for (uint64_t j = xb; j < xe; ++j) kahn_release(xs[j], lvl, rem, L, released);
+                for (uint64_t j = xb; j < xe; ++j) kf_release(xs[j], lvl, rem, L, sbuf, &scnt, fout, cout);
             uint64_t hm = __ballot(heavy);
             while (hm) {
                 const int l = __ffsll((unsigned long long)hm) - 1;
@@ -766,18 +830,22 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)xb, l);
                 const uint64_t e0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(xe >> 32), l) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)xe, l);
-                for (uint64_t j = b0 + __lane_id(); j < e0; j += WAVE) kahn_release(xs[j], lvl, rem, L, released);
+                for (uint64_t j = b0 + __lane_id(); j < e0; j += WAVE) kf_release(xs[j], lvl, rem, L, sbuf, &scnt, fout, cout);
             }
         }
     }
-    wave_set_flag(released, work);
+    __syncthreads();
+    const uint32_t k = min(scnt, KF_BUF);
+    if (threadIdx.x == 0) sbase = k ? atomicAdd(cout, k) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) fout[sbase + i] = sbuf[i];
 }
 
 // Deep graphs (C3: the hot key's ~10^5 Writes make ~10^5 levels, a handful of txns each): one launch per
 // wavefront costs more than the wavefront.  k_kahn_small runs consecutive wavefronts inside ONE workgroup:
 // the frontier is an explicit list (LDS counter, global slots), released successors are appended to the
 // next list, a workgroup barrier separates levels.  It stops when a frontier exceeds KS_MAX (the
-// grid-wide k_kahn_step takes over from that level: its L == lvl test needs no list) or is empty.
+// grid-wide k_kahn_front sweep takes over from that level: its L == lvl test needs no list) or is empty.
 // k_frontier_collect builds the list of the txns at level lvl for the switch.
 constexpr int KS_T = 1024;
 constexpr uint32_t KS_MAX = 4096;
@@ -865,7 +933,8 @@ __global__ __launch_bounds__(KS_T) void k_kahn_small(uint32_t lvl0, uint32_t* __
 
 // (b) and (c) as explicit Kahn edges, one thread per txn T (count pass: per-source out-degrees and T's
 // in-degree; fill pass: T appended to each source's successor run):
-//   (b) every merged direct-key / range dependency D of T with executeAt(D) < executeAt(T);
+//   (b) every merged direct-key / range dependency D of T with executeAt(D) < executeAt(T) (every D when T
+//       awaits only its deps);
 //   (c) unmanaged T, per key of its merged KeyDeps with a constraint position p (k_unmanaged_prep): every
 //       managed entry of that key's chain at positions <= p.  The chain rule already orders the prefix, so
 //       its maximum level sits on the last Write at or before p or on a Read after it: the edges come from
@@ -892,13 +961,14 @@ __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
     };
     if (a.do_b) {
         const uint64_t my = e.ex1[t];
+        const bool all = awaits_only_deps(e.meta[t]);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             if (!e.txns[c]) continue;
             const uint32_t b = e.ent_off[c][t], end = b + e.tcnt[c][t];
             for (uint32_t x = b; x < end; ++x) {
                 const uint32_t d = e.txns[c][x];
-                if (e.ex1[d] < my) emit(d);
+                if (all || e.ex1[d] < my) emit(d);
             }
         }
     }
@@ -918,6 +988,9 @@ __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
 
 struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
+    int kb_hint = 0;                    // wavefronts in the first Kahn launch batch (previous depth + 1)
+    uint32_t* front = nullptr;          // k_kahn_front: two frontier lists of capFront txns
+    size_t capFront = 0;
     uint32_t* c_txn = nullptr;
     uint8_t* c_meta = nullptr;
     uint64_t* c_exec1 = nullptr;
@@ -950,7 +1023,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront, s.front};
     for (void* p : ps) if (p) hipFree(p);
     free_block_bufs(s.bl);
     s = LevelState{};
@@ -979,6 +1052,7 @@ struct LevelInputs {
     const uint32_t* useg;
     uint32_t U;
     uint32_t n_large;
+    uint32_t n_special;                  // key-domain sync points / ephemeral reads (unmanaged execution)
     uint32_t exec_bits;
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
@@ -1296,7 +1370,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // ---- chain order, segment table, pair -> segment, long-segment positions, (c) constraints
         const int gP = ceil_div((long)std::max<size_t>(P, 1), 256);
         const bool has_b = (in.merged_direct && in.merged_direct->ncap > 0) || (in.merged_range && in.merged_range->ncap > 0);
-        const bool has_c = in.n_large > 0 && nkm > 0 && P > 0;
+        const bool has_c = (in.n_large > 0 || in.n_special > 0) && nkm > 0 && P > 0;
         PushCtx push{};
         push.key_off = in.key_off; push.pair_seg = ls.pair_seg; push.seg_len = ls.seg_len; push.stamp = ls.stamp;
         push.long_dirty = ls.flags + 2;
@@ -1312,10 +1386,11 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         }
         ea.cons_pos = ls.cons_pos; ea.pm_all = ls.pm_all; ea.ukey = in.ukey; ea.useg = in.useg; ea.U = in.U;
         ea.c_exec1 = ls.c_exec1; ea.c_txn = ls.c_txn; ea.seg_start = in.seg_start;
+        ea.e_txn = in.e_txn; ea.e_meta = in.e_meta; ea.e_exec1 = in.e_exec1;
         uint32_t host[8] = {0};
         // ---- executeAt blocks (block_levels.h): pure key-chain batches whose chains are long (found by the
         // Kahn chain build below), or always when forced
-        const bool pure = !has_b && !has_c && in.n_large == 0;
+        const bool pure = !has_b && !has_c && in.n_large == 0 && in.n_special == 0;
         auto block_path = [&]() -> int {
             int depth = 0;
             uint32_t rounds = 0;
@@ -1341,7 +1416,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 return AD_ERR_DEVICE;
             }
             if (host[5]) {
-                err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                err = "exec levels: local-only txns are not part of the batch execution order";
                 return AD_ERR_UNSUPPORTED;
             }
             return block_path();
@@ -1349,7 +1424,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // ---- Kahn wavefront (short-chain key batches): chain build + wavefronts with no decision sync;
         // the first batch's readback also carries the kinds / long-chain flags, and a long chain found by
         // the build sends the batch to the fixpoint below
-        if (in.kahn_ok && !in.keep_levels && P > 0) {
+        // key-domain sync points / ephemeral reads sit in the key segments but not in the execution chains:
+        // the chain build of this path treats every key entry as a Read or Write, so such batches resolve on
+        // the relaxation path below (its chain scans skip unmanaged entries)
+        if (in.kahn_ok && !in.keep_levels && P > 0 && in.n_special == 0) {
             ls.chains_ready = false;
             int lv = 0;
             bool fallback = false;
@@ -1404,7 +1482,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                         return AD_ERR_DEVICE;
                     }
                     if (host[5]) {
-                        err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                        err = "exec levels: local-only txns are not part of the batch execution order";
                         return AD_ERR_UNSUPPORTED;
                     }
                     if (host[7] && !long_build()) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
@@ -1438,16 +1516,38 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 // batches double while every wavefront keeps releasing (mixed batches: thousands of levels)
                 constexpr int KB_MAX = 64;
                 const int gn = std::min(ceil_div((long)n, 256), KAHN_GRID);
+                if (ls.capFront < n || !ls.front) {
+                    if (!grow((void**)&ls.front, 2 * std::max<size_t>(n, 1) * 4)) goto oom;
+                    ls.capFront = n;
+                }
                 bool more = !fallback;
-                int KB = 16;
+                // the first batch: the previous batch's depth (+1) on this handle, else 16 (a gated wavefront
+                // still costs a ~5 us launch of the whole grid)
+                int KB = ls.kb_hint > 0 ? ls.kb_hint : 16;
+                // frontier counts: two regions of KB_MAX + 1 (region[k + 1] = txns appended by launch k); a batch
+                // continuing from the previous one reads its input count from the other region's last slot
+                bool sweep_first = true;
+                int region = 0, par = 0;
+                const uint32_t* carried = nullptr;
                 while (more && lv < (1 << 24)) {
-                    hipMemsetAsync(ls.iflags, 0, KB * 4, st);
-                    for (int k = 0; k < KB; ++k)
-                        k_kahn_step<<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ, ls.c_txn,
-                                                        k == 0 ? ls.flags + 7 : ls.iflags + (k - 1), k == 0, ls.iflags + k,
-                                                        xedges ? (const uint64_t*)ls.xoff : nullptr, xedges ? ls.xs : nullptr);
+                    uint32_t* cnt = ls.iflags + region * (KB_MAX + 1);
+                    hipMemsetAsync(cnt + 1, 0, KB * 4, st);
+                    for (int k = 0; k < KB; ++k) {
+                        uint32_t* fin = ls.front + (size_t)((par + k) & 1) * ls.capFront;
+                        uint32_t* fout = ls.front + (size_t)((par + k + 1) & 1) * ls.capFront;
+                        const uint32_t* cin = k == 0 ? carried : cnt + k;
+                        const uint32_t* gate = k == 0 && lv == 0 ? ls.flags + 7 : nullptr;
+                        const uint64_t* xo = xedges ? (const uint64_t*)ls.xoff : nullptr;
+                        const uint32_t* xv = xedges ? ls.xs : nullptr;
+                        if (k == 0 && sweep_first)
+                            k_kahn_front<true><<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ,
+                                                                   ls.c_txn, gate, fin, cin, fout, cnt + k + 1, xo, xv);
+                        else
+                            k_kahn_front<false><<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ,
+                                                                    ls.c_txn, gate, fin, cin, fout, cnt + k + 1, xo, xv);
+                    }
                     uint32_t fh[KB_MAX];
-                    if (hipMemcpyAsync(fh, ls.iflags, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    if (hipMemcpyAsync(fh, cnt + 1, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         (lv == 0 && hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess) ||
                         hipStreamSynchronize(st) != hipSuccess) {
                         err = "exec levels: device error";
@@ -1455,7 +1555,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     }
                     if (lv == 0) {
                         if (host[5]) {
-                            err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+                            err = "exec levels: local-only txns are not part of the batch execution order";
                             return AD_ERR_UNSUPPORTED;
                         }
                         if (host[7] && !long_done) {      // the batch's wavefronts were gated off: rebuild, restart
@@ -1470,6 +1570,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     int k = 0;
                     while (k < KB && fh[k]) ++k;
                     if (k == KB) {                   // all released more: next batch
+                        carried = cnt + KB;
+                        region ^= 1;
+                        par = (par + KB) & 1;
+                        sweep_first = false;
                         lv += KB;
                         KB = std::min(KB_MAX, 2 * KB);
                         if (!xedges) {
@@ -1488,11 +1592,13 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                             if (ks[0] == 0) { lv = (int)ks[1] + 1; more = false; break; }
                             if ((int)ks[1] != lv) KB = 16;     // resumed at a new wide level
                             lv = (int)ks[1];
+                            sweep_first = true;                // its frontier: the txns at level lv (sweep)
                         }
                         continue;
                     }
                     lv += k + 1;
                     more = false;
+                    ls.kb_hint = std::min(KB_MAX, std::max(4, lv + 1));
                 }
             }
             if (go_blocks) return block_path();
@@ -1527,7 +1633,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess) { err = "exec levels: device error"; return AD_ERR_DEVICE; }
         if (host[5]) {
-            err = "exec levels: sync points / ephemeral reads are not modelled by the batch execution order";
+            err = "exec levels: local-only txns are not part of the batch execution order";
             return AD_ERR_UNSUPPORTED;
         }
         if (!reuse) { ls.nheads = host[0]; ls.nlong = host[1]; ls.chains_ready = true; }

@@ -114,18 +114,30 @@ __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename
     }
 }
 
-// Exclusive scan of nblk aggregates in place by one workgroup (chunks of BLOCK with a carry).
-template <class Op, int BLOCK>
+// Exclusive scan of nblk aggregates in place by one workgroup: chunks of BLOCK x AI, each thread folding
+// AI consecutive aggregates serially before one block scan (4096 aggregates = one chunk: the 4M-entry
+// elision scan spent 19 us here with one aggregate per thread and four chunk rounds).
+template <class Op, int BLOCK, int AI = 4>
 __global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, typename Op::S* agg) {
     using S = typename Op::S;
     __shared__ S lds[BLOCK / WAVE];
     S carry = op.identity();
-    for (int c0 = 0; c0 < nblk; c0 += BLOCK) {
-        int i = c0 + threadIdx.x;
-        S v = i < nblk ? agg[i] : op.identity();
+    for (int c0 = 0; c0 < nblk; c0 += BLOCK * AI) {
+        const int b = c0 + (int)threadIdx.x * AI;
+        S v[AI];
+        S t = op.identity();
+#pragma unroll
+        for (int k = 0; k < AI; ++k) {
+            v[k] = b + k < nblk ? agg[b + k] : op.identity();
+            t = op.combine(t, v[k]);
+        }
         S total;
-        S ex = block_exclusive_scan<Op, BLOCK>(op, v, lds, &total);
-        if (i < nblk) agg[i] = op.combine(carry, ex);
+        S ex = op.combine(carry, block_exclusive_scan<Op, BLOCK>(op, t, lds, &total));
+#pragma unroll
+        for (int k = 0; k < AI; ++k) {
+            if (b + k < nblk) agg[b + k] = ex;
+            ex = op.combine(ex, v[k]);
+        }
         carry = op.combine(carry, total);
         __syncthreads();
     }

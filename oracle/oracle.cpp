@@ -495,54 +495,82 @@ struct Flat {
 /* ---------------------------------------------------------------------------------------------- */
 namespace {
 
-// Execution order over the committed batch.  Every edge D -> T increases executeAt, so processing in
-// executeAt order is a topological order and level[T] = 1 + max level over predecessors (0 if none):
+// Execution order over the committed batch.  level[T] = 1 + max level over T's predecessors (0 if none):
 //  * managed T (key Read/Write): per key, every earlier-executeAt managed txn T witnesses
 //    (CommandsForKey.notifyManaged :1208-1289 with unappliedCounters :1291-1330: a Write waits for
 //    all earlier Reads+Writes, a Read for earlier Writes; CommandsForKeyTest.Canon.readyToExecute :169-174),
-//  * every T: direct-key and range deps with executeAt < T's (Commands.updateWaitingOn :740-755),
-//  * unmanaged T (range domain): per key of its keyDeps, every managed txn with executeAt <= the
-//    greatest executeAt among its deps on that key below its own (Updating.updateUnmanaged :740-757
-//    -> Unmanaged APPLY "wait for it and all earlier txn to Apply", CommandsForKey.java:437-445).
+//  * every T: direct-key and range deps with executeAt < T's (Commands.updateWaitingOn :749-755 drops a
+//    dependency that executes later) — all of them when T.kind.awaitsOnlyDeps (ExclusiveSyncPoint,
+//    EphemeralRead: Commands.initialiseWaitingOn :690-691 waits at maxForEpoch, Txn.java:211-214),
+//  * unmanaged T (range domain; key-domain SyncPoint / ExclusiveSyncPoint / EphemeralRead): per key of its
+//    keyDeps, every managed txn with executeAt <= the bound = greatest executeAt among its qualifying deps
+//    there (Updating.updateUnmanaged :740-792 -> Unmanaged APPLY "wait for it and all earlier txn to
+//    Apply", CommandsForKey.java:437-445).  Qualifying: executeAt below T's own; any for EphemeralRead;
+//    TxnId below T's for ExclusiveSyncPoint.  Sync points (SyncPoint, ExclusiveSyncPoint) also fold every
+//    managed-execution txn of the key's byId between their first and last dependency (:760-777).
+// Every edge into a txn that does not await only its deps increases executeAt, so those are resolved in
+// executeAt order (phase 1).  Only ExclusiveSyncPoints witness ExclusiveSyncPoints and nothing witnesses an
+// EphemeralRead, and their deps precede them in TxnId order: phase 2 resolves them in TxnId order.
 static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDeps>& merged, std::vector<uint32_t>& order) {
     const uint32_t n = (uint32_t)B.n;
-    for (uint32_t i = 0; i < n; ++i) {
-        int k = kind_of(B.tx[i]);
-        if (awaits_only_deps(k) || k == AD_KIND_SYNC_POINT || k == AD_KIND_LOCAL_ONLY)
-            throw std::invalid_argument("exec levels: sync points / ephemeral reads not supported in batch execution order");
-    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (kind_of(B.tx[i]) == AD_KIND_LOCAL_ONLY)
+            throw std::invalid_argument("exec levels: local-only txns are not part of the batch execution order");
     std::vector<uint32_t> byExec(n);
     for (uint32_t i = 0; i < n; ++i) byExec[i] = i;
     std::sort(byExec.begin(), byExec.end(), [&](uint32_t a, uint32_t b) { return ts_cmp(B.ex[a], B.ex[b]) < 0; });
     std::vector<int64_t> level(n, -1);
     struct Chain { std::vector<Ts> exec; std::vector<int64_t> pmAll; int64_t maxAll = -1, maxW = -1; };
     std::map<uint64_t, Chain> chains;
-    for (uint32_t t : byExec) {
+    // per key: the managed-execution txns in TxnId (= batch) order (CommandsForKey.byId restricted to them)
+    std::map<uint64_t, std::vector<uint32_t>> byId;
+    for (uint32_t t = 0; t < n; ++t)
+        if (manages_execution(B.tx[t]))
+            for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) byId[B.keys[p]].push_back(t);
+    auto resolve = [&](uint32_t t) {
         int64_t lv = -1;
         const Ts& me = B.tx[t];
         const Ts& myExec = B.ex[t];
+        const int kind = kind_of(me);
+        const bool awaits = awaits_only_deps(kind);
+        const bool sync_point = kind == AD_KIND_SYNC_POINT || kind == AD_KIND_EXCLUSIVE_SYNC_POINT;
         const TxnDeps& d = merged[t];
         auto dep_pred = [&](uint32_t dep) {
-            if (ts_cmp(B.ex[dep], myExec) < 0) lv = std::max(lv, level[dep]);
+            if (awaits || ts_cmp(B.ex[dep], myExec) < 0) lv = std::max(lv, level[dep]);
         };
         for (uint32_t v : d.direct.vals) dep_pred(v);
         for (uint32_t v : d.range.vals) dep_pred(v);
+        // updateUnmanaged's qualification of a committed managed txn j as one T waits for
+        auto qualifies = [&](uint32_t j) {
+            return ts_cmp(B.ex[j], myExec) < 0 || kind == AD_KIND_EPHEMERAL_READ ||
+                   (kind == AD_KIND_EXCLUSIVE_SYNC_POINT && j < t);
+        };
         if (manages_execution(me)) {
-            bool w = kind_of(me) == AD_KIND_WRITE;
+            bool w = kind == AD_KIND_WRITE;
             for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
                 auto it = chains.find(B.keys[p]);
                 if (it == chains.end()) continue;
                 lv = std::max(lv, w ? it->second.maxAll : it->second.maxW);
             }
         } else {
-            // unmanaged: per key of keyDeps, bound = max executeAt of its deps there below its own
+            // unmanaged: per key of keyDeps, bound = max executeAt of its qualifying deps (+ byId between them)
             const Csr<uint64_t>& kd = d.key;
             for (size_t ki = 0; ki < kd.keys.size(); ++ki) {
                 int from = ki == 0 ? (int)kd.keys.size() : kd.k2t[ki - 1];
                 bool has = false; Ts bnd{0, 0, 0};
+                auto fold = [&](uint32_t j) {
+                    if (qualifies(j) && (!has || ts_cmp(B.ex[j], bnd) > 0)) { bnd = B.ex[j]; has = true; }
+                };
+                uint32_t first = UINT32_MAX, last = 0;
                 for (int x = from; x < kd.k2t[ki]; ++x) {
                     uint32_t dep = kd.vals[kd.k2t[x]];
-                    if (ts_cmp(B.ex[dep], myExec) < 0 && (!has || ts_cmp(B.ex[dep], bnd) > 0)) { bnd = B.ex[dep]; has = true; }
+                    fold(dep);
+                    first = std::min(first, dep); last = std::max(last, dep);
+                }
+                auto bit = byId.find(kd.keys[ki]);
+                if (sync_point && first != UINT32_MAX && bit != byId.end()) {
+                    const std::vector<uint32_t>& ids = bit->second;
+                    for (auto q = std::lower_bound(ids.begin(), ids.end(), first); q != ids.end() && *q <= last; ++q) fold(*q);
                 }
                 if (!has) continue;
                 auto it = chains.find(kd.keys[ki]);
@@ -554,7 +582,7 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
         }
         level[t] = lv + 1;
         if (manages_execution(me)) {
-            bool w = kind_of(me) == AD_KIND_WRITE;
+            bool w = kind == AD_KIND_WRITE;
             for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
                 Chain& c = chains[B.keys[p]];
                 c.maxAll = std::max(c.maxAll, level[t]);
@@ -563,7 +591,11 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
                 c.pmAll.push_back(c.maxAll);
             }
         }
-    }
+    };
+    for (uint32_t t : byExec)                       // phase 1
+        if (!awaits_only_deps(kind_of(B.tx[t]))) resolve(t);
+    for (uint32_t t = 0; t < n; ++t)                // phase 2
+        if (awaits_only_deps(kind_of(B.tx[t]))) resolve(t);
     std::vector<uint32_t> out(n);
     for (uint32_t i = 0; i < n; ++i) out[i] = (uint32_t)level[i];
     order = byExec;

@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 BLOCKS = engine.DepsEngine.LEVELS_BLOCKS
 
 
-def check_levels(engine_factory, b, mode=BLOCKS, window=32, replicas=2, drop_p=0.1, seed=0xACC0D1, expect_blocks=True):
+def check_levels(engine_factory, b, mode=BLOCKS, window=32, replicas=2, drop_p=0.1, seed=0xACC0D1, expect_blocks=True,
+                 check_depth=True):
     ref = O.OracleResult(b, abi.make_config(window, replicas, drop_p, seed), O.FLAG_MERGE | O.FLAG_LEVELS)
     eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
     eng.set_level_mode(mode)
@@ -29,7 +30,7 @@ def check_levels(engine_factory, b, mode=BLOCKS, window=32, replicas=2, drop_p=0
     bad = np.nonzero(lv != rlv)[0]
     assert len(bad) == 0, "levels differ at %s (gpu %s, oracle %s)" % (bad[:8], lv[bad[:8]], rlv[bad[:8]])
     assert np.array_equal(order, rorder), "order differs"
-    if len(lv):
+    if len(lv) and check_depth:
         assert depth == int(lv.max()) + 1
     st = eng.last_times()
     if expect_blocks:
@@ -110,14 +111,11 @@ def test_blocks_pipeline_repeat(engine_factory):
         assert eng.last_times()["level_blocks"] > 0
 
 
-def test_blocks_reject_sync_points(engine_factory):
+def test_blocks_mode_with_sync_points_takes_relaxation(engine_factory):
+    # the block path covers pure Read/Write key batches only: with sync points a forced BLOCKS run resolves the
+    # unmanaged waits on the relaxation path (its iteration count is not the depth) and still equals the oracle
     n = 2000
     kinds = np.where(np.arange(n) % 7 == 3, abi.KIND_SYNC_POINT, abi.KIND_WRITE)
     b = workload.generate(n, keyspace=100, kinds=kinds, seed=6)
-    eng = engine_factory(window=8, replicas=1, drop_p=0.0)
-    eng.set_level_mode(BLOCKS)
-    eng.load(b)
-    eng.preaccept_deps()
-    eng.merge()
-    with pytest.raises(engine.AccordDepsError):
-        eng.exec_levels()
+    eng = check_levels(engine_factory, b, window=8, replicas=1, drop_p=0.0, expect_blocks=False, check_depth=False)
+    assert eng.last_times()["level_blocks"] == 0

@@ -122,7 +122,7 @@ def test_mixed_kinds_and_statuses(engine_factory):
                          abi.ST_INVALID, abi.ST_TRANSITIVELY_KNOWN, abi.ST_HISTORICAL], size=n,
                         p=[0.5, 0.1, 0.1, 0.05, 0.05, 0.1, 0.05, 0.05]).astype(np.uint8)
     b = workload.generate(n, keys_per_txn=3, keyspace=200, kinds=kinds, status=status, seed=12)
-    check(engine_factory, b, window=8, levels=False)
+    check(engine_factory, b, window=8)
 
 
 def test_ragged_keys(engine_factory):
@@ -204,7 +204,7 @@ def test_range_txns_writes_and_sync_points(engine_factory):
                        p=[0.4, 0.4, 0.1, 0.1])
     status = rng.choice([abi.ST_APPLIED, abi.ST_INVALID, abi.ST_COMMITTED], size=n, p=[0.8, 0.1, 0.1]).astype(np.uint8)
     b = workload.generate(n, 2, 3000, "uniform", range_frac=0.3, range_width_max=200, kinds=kinds, status=status, seed=31)
-    check(engine_factory, b, window=8, levels=False, replicas=4, drop_p=0.25)
+    check(engine_factory, b, window=8, replicas=4, drop_p=0.25)
 
 
 def test_many_keys_large_path(engine_factory):
@@ -233,10 +233,22 @@ def test_unsorted_keys_rejected(engine_factory):
         eng.preaccept_deps()
 
 
-def test_levels_reject_sync_points(engine_factory):
+def test_levels_sync_points_and_ephemeral_reads(engine_factory):
+    # key-domain SyncPoint / ExclusiveSyncPoint / EphemeralRead are unmanaged: per-key bounds over their deps
+    # (+ the byId range between them for sync points), and awaitsOnlyDeps kinds wait for every dependency
+    rng = np.random.default_rng(41)
+    for n, keyspace, slow in ((3000, 40, 0.3), (20000, 2000, 0.1)):
+        kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT,
+                            abi.KIND_EXCLUSIVE_SYNC_POINT], size=n, p=[0.3, 0.3, 0.14, 0.13, 0.13])
+        b = workload.generate(n, 3, keyspace, kinds=kinds, slow_frac=slow, bump_max=60, seed=n)
+        check(engine_factory, b, window=16)
+        check(engine_factory, b, window=16, fixpoint=True)      # the relaxation path (b)/(c) edges too
+
+
+def test_levels_reject_local_only(engine_factory):
     from accord_amd import engine
 
-    kinds = np.array([abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_READ] * 10)
+    kinds = np.array([abi.KIND_WRITE, abi.KIND_LOCAL_ONLY, abi.KIND_READ] * 10)
     b = workload.generate(30, 2, 50, kinds=kinds, seed=3)
     eng = engine_factory()
     eng.load(b)

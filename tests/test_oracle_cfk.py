@@ -146,34 +146,50 @@ def _exec_key(b, i):
 
 
 def canon_check(b, res):
+    """Brute-force restatement of the level rules (independent of oracle.cpp's executeAt-order DP): per txn T
+    the predecessor set, then level[T] = 1 + max level over it.
+      managed T (key Read/Write): the managed txns on a shared key executing earlier that T witnesses;
+      unmanaged T (range domain, key sync points, ephemeral reads): per key of its KeyDeps, the managed txns
+        executing at or before bnd = the latest executeAt among its qualifying deps there (Updating.
+        updateUnmanaged :740-792: below T's executeAt, any for EphemeralRead, an earlier TxnId for
+        ExclusiveSyncPoint; sync points also fold the key's managed txns between their first and last dep);
+      every T: direct / range deps executing earlier, all of them when T awaits only its deps (Commands.
+        initialiseWaitingOn :690-691, updateWaitingOn :749-755)."""
     lv, order = res.levels()
     n = b["n"]
-    kind = (b["txn_lsb"] >> np.uint64(1)) & np.uint64(7)
+    kind = [int(x) for x in (b["txn_lsb"] >> np.uint64(1)) & np.uint64(7)]
+    is_range = [bool(x) for x in (b["txn_lsb"] & np.uint64(1))]
     ex = [_exec_key(b, i) for i in range(n)]
     keys_of = [set(int(k) for k in b["keys"][b["key_off"][i]:b["key_off"][i + 1]]) for i in range(n)]
+    managed = [not is_range[i] and kind[i] in (R, W) for i in range(n)]
     by_key = {}
     for i in range(n):
-        for k in keys_of[i]:
-            by_key.setdefault(k, []).append(i)
+        if managed[i]:
+            for k in keys_of[i]:
+                by_key.setdefault(k, []).append(i)
     direct, rng, keyd = res.merged(DIRECT), res.merged(RANGE), res.merged(KEY)
-    is_range = (b["txn_lsb"] & np.uint64(1)).astype(bool)
     for t in range(n):
+        awaits = kind[t] in (ESP, EPH)
+        sync = kind[t] in (SP, ESP)
         preds = set()
-        for k in keys_of[t]:
-            for dd in by_key[k]:
-                if ex[dd] < ex[t] and (kind[t] == W or kind[dd] == W):
-                    preds.add(dd)
-        if is_range[t]:
-            # unmanaged (Updating.updateUnmanaged): per key of its KeyDeps, every managed txn executing at or
-            # before the latest of its deps there that executes before it
+        if managed[t]:
+            for k in keys_of[t]:
+                for dd in by_key.get(k, []):
+                    if ex[dd] < ex[t] and (kind[t] == W or kind[dd] == W):
+                        preds.add(dd)
+        else:
+            def qualifies(x):
+                return ex[x] < ex[t] or kind[t] == EPH or (kind[t] == ESP and x < t)
             for k, deps in deps_of(keyd, t).items():
-                below = [ex[x] for x in deps if ex[x] < ex[t]]
-                if below:
-                    bnd = max(below)
+                cand = [x for x in deps if qualifies(x)]
+                if sync and deps:
+                    cand += [x for x in by_key.get(k, []) if min(deps) <= x <= max(deps) and qualifies(x)]
+                if cand:
+                    bnd = max(ex[x] for x in cand)
                     preds.update(dd for dd in by_key.get(k, []) if ex[dd] <= bnd)
         for csr in (direct, rng):
             for deps in deps_of(csr, t).values():
-                preds.update(x for x in deps if ex[x] < ex[t])
+                preds.update(x for x in deps if awaits or ex[x] < ex[t])
         want = 1 + max((int(lv[p]) for p in preds), default=-1)
         assert int(lv[t]) == want, "txn %d level %d, Canon-minimal %d" % (t, lv[t], want)
     # order = txns sorted by (level, executeAt)
@@ -225,3 +241,59 @@ def test_threaded_oracle_equals_single_store():
     for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
         assert one.merged(c).equal(four.merged(c))
     assert all(np.array_equal(x, y) for x, y in zip(one.levels(), four.levels()))
+
+
+# ------------------------------------------------------------------------------------------------
+# Sync points and ephemeral reads (Txn.Kind.awaitsOnlyDeps, Txn.java:211-214; Updating.updateUnmanaged)
+# ------------------------------------------------------------------------------------------------
+def test_levels_sync_points_hand_derived():
+    # key 10, every earlier txn applied (window 0: final statuses, committed-write elision on)
+    #   W1 -> 0;  R2 waits W1 -> 1
+    #   SP3 (unmanaged): keyDeps {W1, R2}, bound = executeAt(R2) -> waits W1, R2 -> 2
+    #   W4 waits W1, R2 (a SyncPoint is not managed execution) -> 2
+    #   ESP5 (awaits only deps): keyDeps {W4} + direct {SP3}; byId between W4 and W4 -> bound = W4 -> 3
+    #   E6 (EphemeralRead, witnesses Writes): keyDeps {W4} -> 3
+    res, b = run([T(1, W, [10]), T(2, R, [10]), T(3, SP, [10]), T(4, W, [10]), T(5, ESP, [10]), T(6, EPH, [10])],
+                 window=0, levels=True)
+    lv, _ = res.levels()
+    assert d(res, DIRECT, 4) == {10: [2]}
+    assert list(lv) == [0, 1, 2, 2, 3, 3]
+    canon_check(b, res)
+
+
+def test_levels_awaits_only_deps_ignores_executeat():
+    # W2's slow path moves its executeAt past everyone's: a SyncPoint executing earlier does not wait for it
+    # (Commands.updateWaitingOn :749-755), an ExclusiveSyncPoint and an EphemeralRead wait for it anyway
+    res, b = run([T(1, W, [10]), T(2, W, [10], exec_hlc=100), T(3, SP, [10]), T(4, ESP, [10]), T(5, EPH, [10])],
+                 window=8, levels=True)
+    lv, _ = res.levels()
+    # W1 0; W2 (exec 100) after W1 -> 1; SP3 (exec 3): deps W1, W2 -> bound W1 -> 1; ESP4: bound W2 -> 2;
+    # EPH5 (witnesses Writes W1, W2): bound W2 -> 2
+    assert list(lv) == [0, 1, 1, 2, 2]
+    canon_check(b, res)
+
+
+@pytest.mark.parametrize("seed", [6, 7, 8])
+def test_levels_canon_invariant_all_kinds(seed):
+    rng = np.random.default_rng(seed)
+    n = 1200
+    kinds = rng.choice([R, W, EPH, SP, ESP], size=n, p=[0.35, 0.35, 0.1, 0.1, 0.1])
+    b = workload.generate(n, keys_per_txn=2, keyspace=80, kinds=kinds, slow_frac=0.3, bump_max=40, seed=seed)
+    res = O.OracleResult(b, abi.make_config(8, 3, 0.2, seed), O.FLAG_MERGE | O.FLAG_LEVELS)
+    canon_check(b, res)
+
+
+@pytest.mark.parametrize("seed", [9, 10])
+def test_levels_canon_invariant_all_kinds_with_ranges(seed):
+    rng = np.random.default_rng(seed)
+    n = 1000
+    kinds = rng.choice([R, W, EPH, SP, ESP], size=n, p=[0.35, 0.35, 0.1, 0.1, 0.1])
+    b = workload.generate(n, keys_per_txn=2, keyspace=300, range_frac=0.2, range_width_max=60, kinds=kinds,
+                          slow_frac=0.3, bump_max=40, seed=seed)
+    res = O.OracleResult(b, abi.make_config(8, 3, 0.2, seed), O.FLAG_MERGE | O.FLAG_LEVELS)
+    canon_check(b, res)
+
+
+def test_levels_reject_local_only():
+    with pytest.raises(ValueError):
+        run([T(1, W, [10]), T(2, abi.KIND_LOCAL_ONLY, [10])], levels=True)
