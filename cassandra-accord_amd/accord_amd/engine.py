@@ -51,6 +51,7 @@ def lib():
         L.ad_device_count.restype = C.c_int
         L.ad_load_batch.argtypes = [vp, C.POINTER(abi.AdBatch)]
         L.ad_preaccept_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
+        L.ad_accept_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_deps.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut)]
         L.ad_merge_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
@@ -79,7 +80,7 @@ def lib():
     return _LIB
 
 
-EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps",
+EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_merge_deps_fast",
             "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
@@ -135,6 +136,13 @@ class DepsEngine:
     def preaccept_deps(self):
         sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
         self._check(lib().ad_preaccept_deps(self.h, sizes), "ad_preaccept_deps")
+        self._dep_sizes = sizes
+        return sizes
+
+    def accept_deps(self):
+        """Deps with bound = executeAt (Accept.calculatePartialDeps / GetDeps): fetch with fetch_deps."""
+        sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
+        self._check(lib().ad_accept_deps(self.h, sizes), "ad_accept_deps")
         self._dep_sizes = sizes
         return sizes
 

@@ -332,6 +332,10 @@ struct WalkArgs {
     const uint32_t* vi_seg0;
     uint32_t* vcnt;           // [x * nvc + vc]
     const uint32_t* vdst;     // [x * nvc + vc]
+    // executeAt-bound queries (Accept / GetDeps; nullable = PreAccept, bound TxnId): per txn the arrival position
+    // of its bound, q = #{j : TxnId_j < executeAt_i}; ex1 = executeAt + 1
+    const uint32_t* qpos;
+    const uint64_t* ex1;
 };
 
 // Next emitted "elidable" (committed Read/Write) entry at or before q, or seg0-1.
@@ -344,20 +348,24 @@ __device__ inline int next_elidable(const WalkArgs& a, int q, int seg0, uint64_t
     return seg0 - 1;
 }
 
-// CommandsForKey.mapReduceActive(startedBefore = TxnId_i) for one key segment, over the entries
-// [seg0, s) (all with TxnId < i), every replica view at once.  emit(v, direct, j) in descending order.
+// CommandsForKey.mapReduceActive(startedBefore) for one key segment, over the entries [seg0, s) (all with
+// TxnId below the bound), every replica view at once.  emit(v, direct, j) in descending order.  gq: the arrival
+// position the query is answered at (PreAccept: i's own; Accept: its executeAt's), which places the in-flight
+// window; b1 = bound + 1.  The txn's own entry is never emitted (PreAccept.calculatePartialDeps :258-260).
 template <int NV, class Emit>
-__device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, int s, int seg0, Emit&& emit) {
+__device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t gq, uint64_t b1, uint32_t qk, int s, int seg0,
+                                  Emit&& emit) {
     // window and drop decisions use global arrival ranks (shard-invariant); emitted ids stay local rows
     const uint32_t gi = a.gid ? a.gid[i] : i;
-    const uint32_t lo = a.window == 0 ? gi : (gi > a.window ? gi - a.window : 0u);
-    // 1. in-flight window: txns j in [i - W, i) are PREACCEPTED from i's viewpoint; replica view v has
+    const uint32_t lo = a.window == 0 ? gq : (gq > a.window ? gq - a.window : 0u);
+    // 1. in-flight window: txns j in [q - W, q) are PREACCEPTED from i's viewpoint; replica view v has
     //    not witnessed j with probability drop_p (ad_drop_hash).
     int q = s - 1;
     for (; q >= seg0; --q) {
         const uint32_t j = a.e_txn[q];
         const uint32_t gj = a.gid ? a.gid[j] : j;
         if (gj < lo) break;
+        if (j == i) continue;
         const uint32_t mj = a.e_meta[q];
         if (!manages(mj) || !witnesses(qk, meta_kind(mj))) continue;
         const bool direct = !manages_execution(mj);
@@ -369,7 +377,6 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, in
     const int p = q;
     if (p < seg0) return;
     uint64_t M1 = a.pm_w[p];
-    const uint64_t b1 = a.tx_ts[i] + 1;
     if (M1 >= b1) {   // a bumped executeAt beyond the bound: exact maxCommittedWriteBefore
         M1 = 0;
         for (int x = p; x >= seg0; --x) {
@@ -384,8 +391,8 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, in
     while (qe >= seg0 || qa >= 0) {
         if (qa > qe) {
             const uint32_t mj = a.e_meta[qa];
-            if (witnesses(qk, meta_kind(mj))) {
-                const uint32_t j = a.e_txn[qa];
+            const uint32_t j = a.e_txn[qa];
+            if (witnesses(qk, meta_kind(mj)) && j != i) {
                 const bool direct = !manages_execution(mj);
 #pragma unroll
                 for (int v = 0; v < NV; ++v) emit(v, direct, j);
@@ -395,9 +402,11 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, in
             if (qa < seg0) qa = -1;
         } else {
             const uint32_t j = a.e_txn[qe];
-            const bool direct = !manages_execution(a.e_meta[qe]);
+            if (j != i) {
+                const bool direct = !manages_execution(a.e_meta[qe]);
 #pragma unroll
-            for (int v = 0; v < NV; ++v) emit(v, direct, j);
+                for (int v = 0; v < NV; ++v) emit(v, direct, j);
+            }
             qe = next_elidable(a, qe - 1, seg0, M1, qk);
         }
     }
@@ -407,11 +416,13 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t qk, in
 // One thread per non-head entry (a key segment's first entry has nothing before it: no deps, and its
 // counts stay at the zeros the caller cleared).  The list is dense, so the active threads fill whole
 // waves (a grid over all P entries left ~5 of 6 lanes idle in every wave of this latency-bound walk).
+// Executeat-bound queries (a.qpos): one thread per entry (a segment head can have deps that arrived after it),
+// walking from the first entry of the segment whose TxnId reaches the bound.
 template <int NV, bool FILL>
 __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= a.P - a.prm->n_keys_u) return;
-    const size_t s = a.nh[x];
+    if (x >= (a.qpos ? a.P : a.P - a.prm->n_keys_u)) return;
+    const size_t s = a.qpos ? x : (size_t)a.nh[x];
     const int seg0 = a.seg_start[s];
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
@@ -438,7 +449,21 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     };
     // small key-domain query txns only (large ones are virtual items)
     const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE);
-    if (query) walk_query<NV>(a, i, qk, (int)s, seg0, emit);
+    if (query) {
+        if (a.qpos) {
+            // first entry of the segment at or past the bound: ranks ascend inside a segment
+            const uint32_t qi = a.qpos[i];
+            size_t lo = s + 1, hi = a.P;
+            while (lo < hi) {
+                const size_t m = (lo + hi) >> 1;
+                if (a.seg_start[m] == seg0 && a.e_txn[m] < qi) lo = m + 1; else hi = m;
+            }
+            walk_query<NV>(a, i, a.gid ? a.gid[i] : qi, a.ex1[i], qk, (int)lo, seg0, emit);
+        } else {
+            const uint32_t gi = a.gid ? a.gid[i] : i;
+            walk_query<NV>(a, i, gi, a.tx_ts[i] + 1, qk, (int)s, seg0, emit);
+        }
+    }
     if (!FILL) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -465,7 +490,10 @@ __global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
         if (FILL) a.k2t[vc][c[vc]--] = (int32_t)j;
         else c[vc]++;
     };
-    if (qk <= AD_KIND_EXCLUSIVE_SYNC_POINT) walk_query<NV>(a, i, qk, (int)a.vi_pos[x], (int)a.vi_seg0[x], emit);
+    if (qk <= AD_KIND_EXCLUSIVE_SYNC_POINT) {
+        const uint32_t gq = a.qpos ? a.qpos[i] : (a.gid ? a.gid[i] : i);
+        walk_query<NV>(a, i, gq, a.qpos ? a.ex1[i] : a.tx_ts[i] + 1, qk, (int)a.vi_pos[x], (int)a.vi_seg0[x], emit);
+    }
     if (!FILL) {
 #pragma unroll
         for (int vc = 0; vc < 2 * NV; ++vc) a.vcnt[x * (2 * NV) + vc] = c[vc];

@@ -130,6 +130,8 @@ struct ad_handle {
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
     bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
+    bool accept = false;             // the deps stage runs with bound = executeAt (ad_accept_deps)
+    uint32_t* qpos = nullptr;        // [n] arrival position of each txn's executeAt (accept bound)
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -210,7 +212,7 @@ enum Slot : size_t {
     S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
     S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST, S_MCLOCAL, S_MCCK, S_MCCM, S_MCCL, S_MCCN,
     S_MCOM, S_MCOL, S_MCON, S_MCOF, S_MCSK, S_MCSM, S_MCSL, S_MCSN, S_MCSU, S_MCSP,
-    S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV,
+    S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
     S_NUM_FIXED,
     S_CSR0 = 160
 };
@@ -560,6 +562,18 @@ struct StageScope {
     ~StageScope() { h->stage = STAGE_NONE; }
 };
 
+// Accept / GetDeps bound: per txn the number of batch TxnIds below its executeAt (TxnIds and executeAts share
+// one packed order; tx_ts ascends with the batch).
+__global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64_t* __restrict__ tx_ts, const uint64_t* __restrict__ ex1,
+                                                   uint32_t* __restrict__ qpos) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t e = ex1[i] - 1;
+    size_t lo = i, hi = n;              // executeAt >= TxnId
+    while (lo < hi) { const size_t m = (lo + hi) >> 1; if (tx_ts[m] < e) lo = m + 1; else hi = m; }
+    qpos[i] = (uint32_t)lo;
+}
+
 int stage_deps(ad_handle* h) {
     StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
@@ -576,12 +590,19 @@ int stage_deps(ad_handle* h) {
         KScope ks(K_SCAN_ELIDE, P);
         scan_any(h, eop, P);
     }
+    // ---- executeAt-bound queries: the arrival position of each bound (first TxnId >= executeAt)
+    const uint32_t* qpos = nullptr;
+    if (h->accept) {
+        CK(dalloc(h, S_QPOS, &h->qpos, std::max<size_t>(n, 1)));
+        if (n) k_query_pos<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->tx_ts, h->ex1, h->qpos);
+        qpos = h->qpos;
+    }
     // ---- virtual items of large txns
     h->V = 0;
     VItemArgs va{};
     va.n = n; va.meta = h->meta; va.key_off = h->key_off; va.keys = h->keys; va.range_off = h->range_off;
     va.rs = h->range_s; va.re = h->range_e; va.e_txn = h->e_txn;
-    va.ukey = h->ukey; va.useg = h->useg; va.prm = h->prm; va.vn = h->vn; va.voff = h->voff;
+    va.ukey = h->ukey; va.useg = h->useg; va.prm = h->prm; va.vn = h->vn; va.voff = h->voff; va.qpos = qpos;
     if (h->n_large > 0) {
         KScope ks(K_VITEMS);
         k_vitems<false><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
@@ -605,6 +626,7 @@ int stage_deps(ad_handle* h) {
     wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
+    wa.qpos = qpos; wa.ex1 = h->ex1;
     if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt, 0, (size_t)nvc * P * 4, st));   // segment heads keep zero counts
     NV_DISPATCH(nv, launch_walk, wa, false, st);
     TxnArgs ta{};
@@ -628,6 +650,7 @@ int stage_deps(ad_handle* h) {
     ra.n = n; ra.Q = Q; ra.key_off = h->key_off; ra.keys = h->keys; ra.range_off = h->range_off; ra.rs = h->range_s;
     ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.wmax = h->wmax;
     ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
+    ra.qpos = qpos;
     if (Q > 0 && n > 0) {
         NV_DISPATCH(nv, launch_range, ra, false, st);
         for (int v = 0; v < nv; ++v) csr_offsets(h, h->rdeps[v], h->rnk + (size_t)v * n, h->rne + (size_t)v * n);
@@ -1075,14 +1098,18 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     return AD_OK;
 }
 
-int ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes) {
+static int run_deps(ad_handle* h, ad_csr_sizes* sizes, bool accept) {
     if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
+    if (accept && h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_accept_deps: sharded stores answer PreAccept deps only");
     hipSetDevice(h->device);
-    CK(stage_prepare(h));
-    CK(stage_sort(h));
-    CK(stage_deps(h));
+    h->accept = accept;
+    int rc = stage_prepare(h);
+    if (rc == AD_OK) rc = stage_sort(h);
+    if (rc == AD_OK) rc = stage_deps(h);
+    h->accept = false;
+    CK(rc);
     CK(read_params(h));
     CK(check_params(h));
     if (sizes) {
@@ -1096,6 +1123,9 @@ int ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes) {
     }
     return AD_OK;
 }
+
+int ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes) { return run_deps(h, sizes, false); }
+int ad_accept_deps(ad_handle* h, ad_csr_sizes* sizes) { return run_deps(h, sizes, true); }
 
 static int fetch_empty(ad_handle* h, ad_csr_out* out) {
     for (size_t i = 0; i <= h->n; ++i) { out->key_off[i] = 0; out->k2t_off[i] = 0; out->txn_off[i] = 0; }

@@ -188,10 +188,6 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 // per-key lists, whose TxnIds are remapped by binary search in the txn's merged TxnId list.
 constexpr int MCH = 32, MH_T = 64, MH_GRID = 8192;
 
-__device__ inline uint32_t lb_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {   // first a[x] >= v
-    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (a[m] < v) lo = m + 1; else hi = m; }
-    return lo;
-}
 template <int KW>
 __device__ inline uint32_t lb_key(const uint64_t* k, uint32_t lo, uint32_t hi, const MKey<KW>& v) {
     while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (MKey<KW>::load(k, m) < v) lo = m + 1; else hi = m; }

@@ -87,6 +87,7 @@ struct RangeArgs {
     const uint32_t* k2t_off_v[MAXV];
     uint64_t* keys_v[MAXV];      // (start, end) interleaved
     int32_t* k2t_v[MAXV];
+    const uint32_t* qpos;        // executeAt-bound queries: per txn the bound's arrival position (nullable)
 };
 
 // does entry [s, e) intersect txn t's footprint (sorted keys, or sorted disjoint ranges)?
@@ -117,7 +118,9 @@ __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
     const bool key_dom = meta_domain(mi) == AD_DOMAIN_KEY;
     const uint32_t fb = key_dom ? a.key_off[i] : a.range_off[i];
     const uint32_t fe = key_dom ? a.key_off[i + 1] : a.range_off[i + 1];
-    const uint32_t lo_w = a.window == 0 ? i : (i > a.window ? i - a.window : 0u);
+    // the arrival position the query is answered at (PreAccept: i; Accept: its executeAt's), the window below it
+    const uint32_t qi = a.qpos ? a.qpos[i] : i;
+    const uint32_t lo_w = a.window == 0 ? qi : (qi > a.window ? qi - a.window : 0u);
     uint32_t ecount[NV], kcount[NV];
     uint64_t cs[NV], ce[NV];
     bool chas[NV];
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
                     bool cond = false;
                     if (valid) {
                         j = a.eown[x];
-                        if (j < i) {
+                        if (j < qi && j != i) {
                             const uint32_t mj = a.meta[j];
                             const bool inw = j >= lo_w;
                             cond = witnesses(qk, meta_kind(mj)) && (inw || meta_status(mj) != AD_ST_INVALID);

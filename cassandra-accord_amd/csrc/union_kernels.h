@@ -29,6 +29,10 @@ __device__ inline uint32_t ub_u64(const uint64_t* a, uint32_t lo, uint32_t hi, u
     }
     return lo;
 }
+__device__ inline uint32_t lb_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {   // first a[x] >= v
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (a[m] < v) lo = m + 1; else hi = m; }
+    return lo;
+}
 __device__ inline uint32_t ub_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {   // first a[x] > v
     while (lo < hi) {
         uint32_t m = (lo + hi) >> 1;
@@ -55,6 +59,7 @@ struct VItemArgs {
     uint32_t* vi_pos;
     uint32_t* vi_seg0;
     uint64_t* vi_key;
+    const uint32_t* qpos;        // executeAt-bound queries: per txn the bound's arrival position (nullable)
 };
 
 // CFK keys inside (s, e]  (EndInclusive: start excluded, end included)
@@ -82,9 +87,11 @@ __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
             const uint64_t k = a.keys[p];
             const uint32_t u = lb_u64(a.ukey, 0, U, k);
             const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
-            const uint32_t s = ub_u32(a.e_txn, s0, s1, (uint32_t)t) - 1;
+            // PreAccept: the pair itself, walk [seg0, s); Accept: walk up to the bound's position (the txn's own
+            // entry inside is skipped by the walk)
+            const uint32_t s = a.qpos ? lb_u32(a.e_txn, s0, s1, a.qpos[t]) : ub_u32(a.e_txn, s0, s1, (uint32_t)t) - 1;
             a.vi_txn[x] = (uint32_t)t;
-            a.vi_pos[x] = s;                       // the pair itself: walk [seg0, s)
+            a.vi_pos[x] = s;
             a.vi_seg0[x] = s0;
             a.vi_key[x] = k;
         }
@@ -100,7 +107,8 @@ __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
         for (uint32_t u = lo; u < hi; ++u, ++x) {
             const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
             a.vi_txn[x] = (uint32_t)t;
-            a.vi_pos[x] = ub_u32(a.e_txn, s0, s1, (uint32_t)t);   // insertPos(TxnId t): first entry with txn > t
+            // insertPos(bound): first entry with txn > t (PreAccept) / at or past the bound's position (Accept)
+            a.vi_pos[x] = a.qpos ? lb_u32(a.e_txn, s0, s1, a.qpos[t]) : ub_u32(a.e_txn, s0, s1, (uint32_t)t);
             a.vi_seg0[x] = s0;
             a.vi_key[x] = a.ukey[u];
         }

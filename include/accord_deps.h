@@ -170,6 +170,13 @@ int  ad_load_batch(ad_handle* h, const ad_batch* batch);
 /* Runs on the device; sizes[v * AD_NUM_CLASSES + c] receives the CSR sizes of view v class c. */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes /* [replicas*AD_NUM_CLASSES] */);
+/* The same deps with bound = executeAt instead of TxnId: Accept.calculatePartialDeps (messages/Accept.java
+ * :113-116) and GetDeps.apply (messages/GetDeps.java:76) call PreAccept.calculatePartialDeps with the
+ * proposed executeAt, so every txn with TxnId < executeAt (later arrivals included) is a candidate and the
+ * txn itself is left out (PreAccept.java:256-261).  Each query is answered at the arrival position of its
+ * executeAt (the window / status model applies from there).  Fetch with ad_fetch_deps; ad_merge_deps and the
+ * later stages use the last deps computed.  Not in sharded mode (AD_ERR_UNSUPPORTED). */
+int  ad_accept_deps(ad_handle* h, ad_csr_sizes* sizes /* [replicas*AD_NUM_CLASSES] */);
 int  ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out);
 
 /* Stage 2 — Deps.merge of the R replica replies produced by stage 1 (device-resident). */

@@ -309,10 +309,12 @@ struct Oracle {
     const Batch& B;
     Config cfg;
     bool prune;
+    bool accept;                        // bound = executeAt (Accept / GetDeps) instead of TxnId (PreAccept)
     std::vector<Cfk> cfks;              // sorted by key
     std::vector<uint32_t> rangeTxns;    // ranks of range-domain txns (rangeCommands registry)
 
-    Oracle(const Batch& b, const Config& c, bool prune_) : B(b), cfg(c), prune(prune_) {
+    Oracle(const Batch& b, const Config& c, bool prune_, bool accept_ = false)
+        : B(b), cfg(c), prune(prune_ && !accept_), accept(accept_) {
         std::map<uint64_t, std::vector<uint32_t>> m;
         for (uint32_t i = 0; i < B.n; ++i) {
             if (domain_of(B.tx[i]) == AD_DOMAIN_RANGE) { rangeTxns.push_back(i); continue; }
@@ -328,14 +330,30 @@ struct Oracle {
     bool dropped(uint32_t view, uint32_t i, uint32_t j) const {
         return in_window(i, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, i, j) < cfg.drop_thresh;
     }
+    // The query of txn i: its bound (startedBefore) and the arrival position it is answered at.  PreAccept:
+    // TxnId_i at position i.  Accept / GetDeps (Accept.calculatePartialDeps :113-116, GetDeps.apply :76 ->
+    // PreAccept.calculatePartialDeps with executeAt): executeAt_i, answered once every txn with a smaller
+    // TxnId has arrived — position q = #{j : TxnId_j < executeAt_i}; the status model and window apply from q.
+    const Ts& bound_of(uint32_t i) const { return accept ? B.ex[i] : B.tx[i]; }
+    uint32_t query_pos(uint32_t i) const {
+        if (!accept) return i;
+        const Ts& b = B.ex[i];
+        return (uint32_t)(std::lower_bound(B.tx.begin(), B.tx.end(), b, [](const Ts& x, const Ts& y) { return ts_cmp(x, y) < 0; }) - B.tx.begin());
+    }
+    int seen_status_q(uint32_t q, uint32_t j) const { return in_window(q, j) ? (int)AD_ST_PREACCEPTED : (int)B.st[j]; }
+    bool dropped_q(uint32_t view, uint32_t q, uint32_t i, uint32_t j) const {
+        return in_window(q, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, i, j) < cfg.drop_thresh;
+    }
 
-    // CommandsForKey.mapReduceActive(startedBefore = TxnId_i, testKind = kind_i.witnesses()) — CommandsForKey.java:925-983
+    // CommandsForKey.mapReduceActive(startedBefore = bound, testKind = kind_i.witnesses()) — CommandsForKey.java:925-983;
+    // PreAccept.calculatePartialDeps' fn leaves out the txn itself (:258-260: p1 = txnId when executeAt != txnId)
     template <class F>
     void map_reduce_active(Cfk& cfk, uint32_t i, uint32_t view, F&& emit) {
-        const Ts& bound = B.tx[i];
-        const int qkind = kind_of(bound);
+        const Ts& bound = bound_of(i);
+        const uint32_t qp = query_pos(i);
+        const int qkind = kind_of(B.tx[i]);
         // int end = insertPos(startedBefore)  (:929, :1373-1378); byId is rank-ordered
-        size_t end = std::lower_bound(cfk.byId.begin(), cfk.byId.end(), i) - cfk.byId.begin();
+        size_t end = std::lower_bound(cfk.byId.begin(), cfk.byId.end(), qp) - cfk.byId.begin();
         // maxCommittedWriteBefore (:930-943): the greatest executeAt of a committed Write in
         // committedByExecuteAt with executeAt < startedBefore.  committedByExecuteAt holds the byId
         // entries (all have TxnId < bound here) whose status >= COMMITTED and != INVALID.
@@ -343,16 +361,18 @@ struct Oracle {
         Ts M = cfk.prunedMaxWrite;
         for (size_t x = cfk.prunedBefore; x < end; ++x) {
             uint32_t j = cfk.byId[x];
-            if (!in_committed_by_execute_at(seen_status(i, j))) continue;
+            if (j == i) continue;
+            if (!in_committed_by_execute_at(seen_status_q(qp, j))) continue;
             if (kind_of(B.tx[j]) != AD_KIND_WRITE) continue;
             if (ts_cmp(B.ex[j], bound) >= 0) continue;
             if (!hasM || ts_cmp(B.ex[j], M) > 0) { M = B.ex[j]; hasM = true; }
         }
         for (size_t x = cfk.prunedBefore; x < end; ++x) {                       // :945-965
             uint32_t j = cfk.byId[x];
+            if (j == i) continue;
             const Ts& txn = B.tx[j];
             if (!witnesses(qkind, kind_of(txn))) continue;
-            switch (seen_status(i, j)) {
+            switch (seen_status_q(qp, j)) {
                 case AD_ST_COMMITTED: case AD_ST_STABLE: case AD_ST_APPLIED:
                     if (!hasM || ts_cmp(B.ex[j], M) >= 0 || !witnesses(AD_KIND_WRITE, kind_of(txn))) break;
                     continue;                                                    // elided (falls into :959-961)
@@ -360,7 +380,7 @@ struct Oracle {
                     continue;
                 default: break;
             }
-            if (dropped(view, i, j)) continue;
+            if (dropped_q(view, qp, i, j)) continue;
             emit(cfk.key, j);
         }
         // prunedBefore future-dependency branch (:967-980) never fires: queries arrive in TxnId
@@ -416,11 +436,13 @@ struct Oracle {
         }
         // mapReduceRangesInternal(STARTED_BEFORE, ANY_DEPS, ANY_STATUS) — InMemoryCommandStore.java:884-1017
         std::vector<std::pair<RangeK, std::vector<uint32_t>>> collect;   // TreeMap<Range, List> by Range::compare
+        const uint32_t qp = query_pos(i);
         for (uint32_t j : rangeTxns) {
-            if (j >= i) break;                                       // txnId.compareTo(testTimestamp) >= 0 -> return
-            if (seen_status(i, j) == AD_ST_INVALID) continue;        // saveStatus >= Erased
+            if (j >= qp) break;                                      // txnId.compareTo(testTimestamp) >= 0 -> return
+            if (j == i) continue;
+            if (seen_status_q(qp, j) == AD_ST_INVALID) continue;     // saveStatus >= Erased
             if (!witnesses(qkind, kind_of(B.tx[j]))) continue;
-            if (dropped(view, i, j)) continue;
+            if (dropped_q(view, qp, i, j)) continue;
             for (uint32_t q = B.range_off[j]; q < B.range_off[j + 1]; ++q) {
                 const RangeK& r = B.ranges[q];
                 bool hit = false;
@@ -620,7 +642,8 @@ struct oracle_result {
 
 extern "C" {
 
-/* flags: bit0 = pruning (baseline mode), bit1 = merge, bit2 = levels; threads: key-range shards
+/* flags: bit0 = pruning (baseline mode), bit1 = merge, bit2 = levels, bit3 = executeAt-bound deps (Accept /
+ * GetDeps; no pruning); threads: key-range shards
  * for the deps stage (InMemoryCommandStore.SingleThread per shard + PreAccept.reduce). */
 oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
                                  const uint8_t* view_mask);
@@ -646,10 +669,11 @@ oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t
         auto t0 = std::chrono::steady_clock::now();
         if (threads <= 1) {
             for (uint32_t v = 0; v < R; ++v) {
-                Oracle o(B, cfg, flags & 1);
+                Oracle o(B, cfg, flags & 1, (flags & 8) != 0);
                 for (uint32_t i = 0; i < n; ++i) all[v][i] = o.preaccept(i, v);
             }
         } else {
+            if (flags & 8) throw std::invalid_argument("threaded oracle: executeAt-bound deps unsupported");
             // Shard the key space into `threads` contiguous ranges of the batch's distinct keys
             // (ShardDistributor.EvenSplit, local/ShardDistributor.java:32-80), one single-threaded
             // store per shard; each store answers the part of every query that falls in its range;

@@ -57,7 +57,7 @@ def lib():
     return _LIB
 
 
-FLAG_PRUNE, FLAG_MERGE, FLAG_LEVELS = 1, 2, 4
+FLAG_PRUNE, FLAG_MERGE, FLAG_LEVELS, FLAG_ACCEPT = 1, 2, 4, 8
 
 
 class OracleResult:

@@ -297,3 +297,41 @@ def test_levels_canon_invariant_all_kinds_with_ranges(seed):
 def test_levels_reject_local_only():
     with pytest.raises(ValueError):
         run([T(1, W, [10]), T(2, abi.KIND_LOCAL_ONLY, [10])], levels=True)
+
+
+# ------------------------------------------------------------------------------------------------
+# Accept / GetDeps: PreAccept.calculatePartialDeps with bound = executeAt (Accept.java:113-116, GetDeps.java:76)
+# ------------------------------------------------------------------------------------------------
+def run_accept(txns, window=32):
+    b = make_batch(txns)
+    return O.OracleResult(b, abi.make_config(window, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_ACCEPT), b
+
+
+def test_accept_bound_sees_later_arrivals():
+    # W1's slow path proposes executeAt 50: every txn with TxnId < 50 on its key is a candidate, W2 (hlc 20)
+    # and R3 (hlc 30) included, R4 (hlc 60) not; W1 itself never (:258-260)
+    txns = [T(10, W, [10], exec_hlc=50), T(20, W, [10]), T(30, R, [10]), T(60, R, [10])]
+    res, _ = run_accept(txns)
+    assert d(res, KEY, 0) == {10: [1, 2]}
+    pre, _ = run(txns)
+    assert d(pre, KEY, 0) == {}                         # PreAccept (bound = TxnId): nothing earlier
+    # fast-path txns (executeAt == TxnId) answer exactly their PreAccept deps
+    for i in (1, 2, 3):
+        assert d(res, KEY, i) == d(pre, KEY, i)
+
+
+def test_accept_equals_preaccept_without_slow_paths():
+    b = workload.generate(2500, keys_per_txn=3, keyspace=200, slow_frac=0.0, range_frac=0.1, range_width_max=40, seed=13)
+    cfg = abi.make_config(12, 3, 0.2, 5)
+    a = O.OracleResult(b, cfg, O.FLAG_MERGE)
+    c = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_ACCEPT)
+    for v in range(3):
+        for k in (KEY, DIRECT, RANGE):
+            assert a.deps(v, k).equal(c.deps(v, k))
+
+
+def test_accept_range_bound():
+    # range txns: mapReduceRangesInternal stops at TxnIds >= the bound (executeAt here)
+    txns = [T(10, W, [15], exec_hlc=50), T(20, R, ranges=[(10, 20)]), T(70, R, ranges=[(10, 20)])]
+    res, _ = run_accept(txns)
+    assert d(res, RANGE, 0) == {(10, 20): [1]}
