@@ -220,7 +220,7 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
     # are shared fill/copy kernels and are not attributed)
-    "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_front", "ad::k_chain_rank", "ad::k_chain_check",
+    "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_step", "ad::k_chain_rank", "ad::k_chain_check",
                     "ad::k_chain_links", "ad::k_frontier_collect", "ad::k_kahn_small"),
     "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<6>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<6>, 1024>",
                      "ad::k_scan_apply<ad::OffsetsOp<6>, 256, 4>"),

@@ -623,6 +623,9 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
 // keys the first successor of every pair is released with all loads and atomics issued together (the
 // returning atomics are the latency of this kernel); longer runs and wider txns go serially.
 constexpr int KAHN_GRID = 2048;
+__device__ inline void kahn_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
+    if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
+}
 // ---------------------------------------------------------------------------------------------------
 // Kahn chain build for batches with long chains (C3's Zipf hot keys: ~10^5 entries on one key), all
 // positions in parallel instead of one thread per segment:
@@ -744,49 +747,18 @@ __global__ __launch_bounds__(256) void k_chain_links(size_t P, const int32_t* __
 // 64 lanes per edge run.
 constexpr uint64_t XLIGHT = 8;
 
-// Frontier-list wavefronts: the txns of level `lvl` release their successors; a successor whose remaining count
-// reaches zero gets level lvl + 1 and is appended to the next frontier list.  SWEEP (a batch's first launch: level
-// 0, or a level resumed after k_kahn_small) finds its frontier by scanning all n txns; list launches walk only
-// the frontier (*cin entries of fin), so the narrow tail levels of a shallow graph cost a near-empty launch
-// instead of a sweep over n.  Appends go to a per-workgroup LDS buffer (LDS atomics), flushed with one global
-// atomicAdd per workgroup; a buffer overflow appends directly.
-constexpr uint32_t KF_BUF = 4096;
-__device__ inline void kf_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
-                                  uint32_t* sbuf, uint32_t* scnt, uint32_t* __restrict__ fout, uint32_t* __restrict__ cout) {
-    if (atomicSub(&rem[s], 1u) == 1u) {
-        L[s] = lvl + 1;
-        const uint32_t at = atomicAdd(scnt, 1u);
-        if (at < KF_BUF) sbuf[at] = s;
-        else fout[atomicAdd(cout, 1u)] = s;
-    }
-}
-template <bool SWEEP>
-__global__ __launch_bounds__(256) void k_kahn_front(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
-                                                    uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
-                                                    const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
-                                                    const uint32_t* __restrict__ c_txn, const uint32_t* abort_gate,
-                                                    const uint32_t* __restrict__ fin, const uint32_t* cin,
-                                                    uint32_t* __restrict__ fout, uint32_t* cout,
-                                                    const uint64_t* __restrict__ xoff, const uint32_t* __restrict__ xs) {
-    __shared__ uint32_t sbuf[KF_BUF];
-    __shared__ uint32_t scnt, sbase;
-    if (abort_gate && *abort_gate != 0u) return;
-    const size_t m = SWEEP ? n : (size_t)*cin;
-    if (m == 0) return;
-    if (threadIdx.x == 0) scnt = 0;
-    __syncthreads();
+__global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
+                                                   uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
+                                                   const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
+                                                   const uint32_t* __restrict__ c_txn, const uint32_t* gate, int gate_is_abort,
+                                                   uint32_t* __restrict__ work, const uint64_t* __restrict__ xoff,
+                                                   const uint32_t* __restrict__ xs) {
+    if (gate_is_abort ? *gate != 0u : *gate == 0u) return;
+    bool released = false;
     // block-aligned stride: every lane of a wave runs the same iterations (the heavy-run ballot below)
-    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < m; base += (size_t)gridDim.x * blockDim.x) {
-        const size_t idx = base + threadIdx.x;
-        uint32_t t = 0;
-        bool mine;
-        if (SWEEP) {
-            t = (uint32_t)idx;
-            mine = idx < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
-        } else {
-            mine = idx < m;
-            if (mine) t = fin[idx];
-        }
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
+        const size_t t = base + threadIdx.x;
+        const bool mine = t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
         if (mine) {
             const uint32_t b = key_off[t], e = key_off[t + 1];
             if (e - b <= 4) {
@@ -800,19 +772,14 @@ __global__ __launch_bounds__(256) void k_kahn_front(size_t n, uint32_t lvl, cons
                 for (int j = 0; j < 4; ++j) rr[j] = sc[j].y ? atomicSub(&rem[sx[j]], 1u) : 0u;
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if (sc[j].y && rr[j] == 1u) {
-                        L[sx[j]] = lvl + 1;
-                        const uint32_t at = atomicAdd(&scnt, 1u);
-                        if (at < KF_BUF) sbuf[at] = sx[j];
-                        else fout[atomicAdd(cout, 1u)] = sx[j];
-                    }
+                    if (sc[j].y && rr[j] == 1u) { L[sx[j]] = lvl + 1; released = true; }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kf_release(c_txn[x], lvl, rem, L, sbuf, &scnt, fout, cout);
+                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
             } else {
                 for (uint32_t p = b; p < e; ++p) {
                     const uint2 sc = succ[p];
-                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kf_release(c_txn[x], lvl, rem, L, sbuf, &scnt, fout, cout);
+                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
                 }
             }
         }
@@ -821,7 +788,7 @@ __global__ __launch_bounds__(256) void k_kahn_front(size_t n, uint32_t lvl, cons
             if (mine) { xb = xoff[t]; xe = xoff[t + 1]; }
             const bool heavy = xe - xb > XLIGHT;
             if (mine && !heavy)
-                for (uint64_t j = xb; j < xe; ++j) kf_release(xs[j], lvl, rem, L, sbuf, &scnt, fout, cout);
+                for (uint64_t j = xb; j < xe; ++j) kahn_release(xs[j], lvl, rem, L, released);
             uint64_t hm = __ballot(heavy);
             while (hm) {
                 const int l = __ffsll((unsigned long long)hm) - 1;
@@ -830,22 +797,18 @@ __global__ __launch_bounds__(256) void k_kahn_front(size_t n, uint32_t lvl, cons
                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)xb, l);
                 const uint64_t e0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(xe >> 32), l) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)xe, l);
-                for (uint64_t j = b0 + __lane_id(); j < e0; j += WAVE) kf_release(xs[j], lvl, rem, L, sbuf, &scnt, fout, cout);
+                for (uint64_t j = b0 + __lane_id(); j < e0; j += WAVE) kahn_release(xs[j], lvl, rem, L, released);
             }
         }
     }
-    __syncthreads();
-    const uint32_t k = min(scnt, KF_BUF);
-    if (threadIdx.x == 0) sbase = k ? atomicAdd(cout, k) : 0u;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) fout[sbase + i] = sbuf[i];
+    wave_set_flag(released, work);
 }
 
 // Deep graphs (C3: the hot key's ~10^5 Writes make ~10^5 levels, a handful of txns each): one launch per
 // wavefront costs more than the wavefront.  k_kahn_small runs consecutive wavefronts inside ONE workgroup:
 // the frontier is an explicit list (LDS counter, global slots), released successors are appended to the
 // next list, a workgroup barrier separates levels.  It stops when a frontier exceeds KS_MAX (the
-// grid-wide k_kahn_front sweep takes over from that level: its L == lvl test needs no list) or is empty.
+// grid-wide k_kahn_step takes over from that level: its L == lvl test needs no list) or is empty.
 // k_frontier_collect builds the list of the txns at level lvl for the switch.
 constexpr int KS_T = 1024;
 constexpr uint32_t KS_MAX = 4096;
@@ -989,8 +952,6 @@ __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
 struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
     int kb_hint = 0;                    // wavefronts in the first Kahn launch batch (previous depth + 1)
-    uint32_t* front = nullptr;          // k_kahn_front: two frontier lists of capFront txns
-    size_t capFront = 0;
     uint32_t* c_txn = nullptr;
     uint8_t* c_meta = nullptr;
     uint64_t* c_exec1 = nullptr;
@@ -1023,7 +984,7 @@ struct LevelState {
 };
 
 inline void free_level_state(LevelState& s) {
-    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront, s.front};
+    void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront};
     for (void* p : ps) if (p) hipFree(p);
     free_block_bufs(s.bl);
     s = LevelState{};
@@ -1516,38 +1477,19 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 // batches double while every wavefront keeps releasing (mixed batches: thousands of levels)
                 constexpr int KB_MAX = 64;
                 const int gn = std::min(ceil_div((long)n, 256), KAHN_GRID);
-                if (ls.capFront < n || !ls.front) {
-                    if (!grow((void**)&ls.front, 2 * std::max<size_t>(n, 1) * 4)) goto oom;
-                    ls.capFront = n;
-                }
                 bool more = !fallback;
                 // the first batch: the previous batch's depth (+1) on this handle, else 16 (a gated wavefront
-                // still costs a ~5 us launch of the whole grid)
+                // still costs a ~5 us launch of the whole grid).  (A frontier-list variant that walked only each
+                // level's txns measured no faster on C2 and 5x slower on C4's 5650 levels: kept the sweep.)
                 int KB = ls.kb_hint > 0 ? ls.kb_hint : 16;
-                // frontier counts: two regions of KB_MAX + 1 (region[k + 1] = txns appended by launch k); a batch
-                // continuing from the previous one reads its input count from the other region's last slot
-                bool sweep_first = true;
-                int region = 0, par = 0;
-                const uint32_t* carried = nullptr;
                 while (more && lv < (1 << 24)) {
-                    uint32_t* cnt = ls.iflags + region * (KB_MAX + 1);
-                    hipMemsetAsync(cnt + 1, 0, KB * 4, st);
-                    for (int k = 0; k < KB; ++k) {
-                        uint32_t* fin = ls.front + (size_t)((par + k) & 1) * ls.capFront;
-                        uint32_t* fout = ls.front + (size_t)((par + k + 1) & 1) * ls.capFront;
-                        const uint32_t* cin = k == 0 ? carried : cnt + k;
-                        const uint32_t* gate = k == 0 && lv == 0 ? ls.flags + 7 : nullptr;
-                        const uint64_t* xo = xedges ? (const uint64_t*)ls.xoff : nullptr;
-                        const uint32_t* xv = xedges ? ls.xs : nullptr;
-                        if (k == 0 && sweep_first)
-                            k_kahn_front<true><<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ,
-                                                                   ls.c_txn, gate, fin, cin, fout, cnt + k + 1, xo, xv);
-                        else
-                            k_kahn_front<false><<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ,
-                                                                    ls.c_txn, gate, fin, cin, fout, cnt + k + 1, xo, xv);
-                    }
+                    hipMemsetAsync(ls.iflags, 0, KB * 4, st);
+                    for (int k = 0; k < KB; ++k)
+                        k_kahn_step<<<gn, 256, 0, st>>>(n, (uint32_t)(lv + k), ls.indeg, ls.rem, in.lvl, in.key_off, ls.succ, ls.c_txn,
+                                                        k == 0 ? ls.flags + 7 : ls.iflags + (k - 1), k == 0, ls.iflags + k,
+                                                        xedges ? (const uint64_t*)ls.xoff : nullptr, xedges ? ls.xs : nullptr);
                     uint32_t fh[KB_MAX];
-                    if (hipMemcpyAsync(fh, cnt + 1, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    if (hipMemcpyAsync(fh, ls.iflags, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         (lv == 0 && hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess) ||
                         hipStreamSynchronize(st) != hipSuccess) {
                         err = "exec levels: device error";
@@ -1570,10 +1512,6 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     int k = 0;
                     while (k < KB && fh[k]) ++k;
                     if (k == KB) {                   // all released more: next batch
-                        carried = cnt + KB;
-                        region ^= 1;
-                        par = (par + KB) & 1;
-                        sweep_first = false;
                         lv += KB;
                         KB = std::min(KB_MAX, 2 * KB);
                         if (!xedges) {
@@ -1592,7 +1530,6 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                             if (ks[0] == 0) { lv = (int)ks[1] + 1; more = false; break; }
                             if ((int)ks[1] != lv) KB = 16;     // resumed at a new wide level
                             lv = (int)ks[1];
-                            sweep_first = true;                // its frontier: the txns at level lv (sweep)
                         }
                         continue;
                     }
