@@ -12,7 +12,7 @@
 //   walk<count|fill>    per query item (txn i, key segment, insert position) and replica view: the
 //                       dependencies mapReduceActive emits (CommandsForKey.java:945-965)
 //   small txns (key txns with <= KMAX keys): one thread per txn builds the per-txn KeyDeps layout and
-//   the TxnId union in registers (k_txn_counts / k_txn_layout / k_txn_union)
+//   the TxnId union in registers (OffsetsOp's fused layout or k_txn_layout / k_txn_union)
 //   large txns (range-domain txns querying every CFK key inside their ranges, and key txns with more
 //   than KMAX keys) go through "virtual items" (vitem_kernels in engine.hip) and union_kernels.h.
 #pragma once
@@ -325,13 +325,14 @@ struct WalkArgs {
     uint32_t* cnt;            // real pairs, AoS by pair: [p * 2NV + vc], vc = view * 2 + class
     const uint32_t* dst;      // real pairs, AoS by pair: absolute k2t slot of the last entry (fill)
     int32_t* k2t[NVC_MAX];    // per-vc keysToTxnIds (fill)
-    // virtual items (large txns): item x queries key segment [vi_seg0[x], ...) before position vi_pos[x]
+    // virtual items (large txns): item x queries key segment u = vi_u[x] ([useg[u], ...)) before position vi_pos[x]
     size_t V;
     const uint32_t* vi_txn;
     const uint32_t* vi_pos;
-    const uint32_t* vi_seg0;
+    const uint32_t* vi_u;     // distinct-key index of the item
+    const uint32_t* useg;     // [U+1] segment starts
     uint32_t* vcnt;           // [x * nvc + vc]
-    const uint32_t* vdst;     // [x * nvc + vc]
+    const uint32_t* vdst;     // [x * nvc + vc] (the same buffer: k_large_layout rewrites counts into slots)
     // executeAt-bound queries (Accept / GetDeps; nullable = PreAccept, bound TxnId): per txn the arrival position
     // of its bound, q = #{j : TxnId_j < executeAt_i}; ex1 = executeAt + 1
     const uint32_t* qpos;
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
     };
     if (qk <= AD_KIND_EXCLUSIVE_SYNC_POINT) {
         const uint32_t gq = a.qpos ? a.qpos[i] : (a.gid ? a.gid[i] : i);
-        walk_query<NV>(a, i, gq, a.qpos ? a.ex1[i] : a.tx_ts[i] + 1, qk, (int)a.vi_pos[x], (int)a.vi_seg0[x], emit);
+        walk_query<NV>(a, i, gq, a.qpos ? a.ex1[i] : a.tx_ts[i] + 1, qk, (int)a.vi_pos[x], (int)a.useg[a.vi_u[x]], emit);
     }
     if (!FILL) {
 #pragma unroll
@@ -518,47 +519,17 @@ struct TxnArgs {
     // large txns (virtual items, in (txn, key) order): items [voff[t], voff[t+1])
     const uint32_t* voff;
     const uint32_t* vcnt;         // [x * nvc + vc]
-    uint32_t* vdst;               // [x * nvc + vc]
-    const uint64_t* vi_key;
+    uint32_t* vdst;               // [x * nvc + vc] (aliases vcnt: each slot is read, then rewritten, once)
+    const uint32_t* vi_u;         // item -> distinct-key index (its key = ukey[u])
+    const uint64_t* ukey;
 };
-
-__global__ __launch_bounds__(256) void k_txn_counts(TxnArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    if (a.meta[t] & META_LARGE) {
-        const uint32_t b = a.voff[t], e = a.voff[t + 1];
-        for (int vc = 0; vc < a.nvc; ++vc) {
-            uint32_t nk = 0, ne = 0;
-            for (uint32_t x = b; x < e; ++x) {
-                uint32_t c = a.vcnt[(size_t)x * a.nvc + vc];
-                nk += c > 0;
-                ne += c;
-            }
-            a.nk[(size_t)vc * a.n + t] = nk;
-            a.ne[(size_t)vc * a.n + t] = ne;
-        }
-        return;
-    }
-    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
-    for (int vc = 0; vc < a.nvc; ++vc) {
-        uint32_t nk = 0, ne = 0;
-        for (uint32_t p = b; p < e; ++p) {
-            uint32_t c = a.cnt[(size_t)p * a.nvc + vc];
-            nk += c > 0;
-            ne += c;
-        }
-        a.nk[(size_t)vc * a.n + t] = nk;
-        a.ne[(size_t)vc * a.n + t] = ne;
-    }
-}
 
 // Per txn: keys in ascending order (Keys are sorted), KeyDeps header offsets, per-item first-entry slot.
 __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
-    const bool large = a.meta[t] & META_LARGE;
-    if (large) return;            // k_large_layout
-    const uint32_t b = large ? a.voff[t] : a.key_off[t], e = large ? a.voff[t + 1] : a.key_off[t + 1];
+    if (a.meta[t] & META_LARGE) return;            // k_large_layout
+    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
     for (int vc = 0; vc < a.nvc; ++vc) {
         const uint32_t kb = a.out_key_off[vc][t];
         const uint32_t nk = a.out_key_off[vc][t + 1] - kb;
@@ -566,14 +537,10 @@ __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
         const uint32_t mb = a.out_k2t_off[vc][t];
         uint32_t run = nk, kk = 0;
         for (uint32_t x = b; x < e; ++x) {
-            uint32_t c;
-            if (large) c = a.vcnt[(size_t)x * a.nvc + vc];
-            else c = a.cnt[(size_t)x * a.nvc + vc];
+            const uint32_t c = a.cnt[(size_t)x * a.nvc + vc];
             if (c == 0) continue;
-            a.out_keys[vc][kb + kk] = large ? a.vi_key[x] : a.keys[x];
-            // the fill walk emits descending from the run's last slot
-            if (large) a.vdst[(size_t)x * a.nvc + vc] = mb + run + c - 1;
-            else a.dst[(size_t)x * a.nvc + vc] = mb + run + c - 1;
+            a.out_keys[vc][kb + kk] = a.keys[x];
+            a.dst[(size_t)x * a.nvc + vc] = mb + run + c - 1;      // the fill walk emits descending from here
             run += c;
             a.out_k2t[vc][mb + kk] = (int32_t)run;
             ++kk;
@@ -637,7 +604,7 @@ __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
             if (v > 0) {
                 const uint32_t r = kk + (uint32_t)__popcll(nz & below);
                 const uint32_t before = run + incl - v;
-                a.out_keys[c][kb + r] = a.vi_key[x];
+                a.out_keys[c][kb + r] = a.ukey[a.vi_u[x]];
                 a.vdst[(size_t)x * NVC + c] = mb + before + v - 1;
                 a.out_k2t[c][mb + r] = (int32_t)(before + v);
             }
@@ -661,8 +628,6 @@ struct OffsetsOp {
     const uint8_t* meta;
     const uint32_t* key_off;
     const uint32_t* cnt;          // AoS by pair
-    const uint32_t* voff;
-    const uint32_t* vcnt;         // AoS by virtual item
     uint32_t* o_key_off[NVC];
     uint32_t* o_ent_off[NVC];
     uint32_t* o_k2t_off[NVC];
@@ -671,12 +636,10 @@ struct OffsetsOp {
     // caller runs k_txn_layout after sizing the buffers (layout == 0: offsets only)
     int layout;
     const uint64_t* keys;
-    const uint64_t* vi_key;
     uint64_t* out_keys[NVC];
     int32_t* out_k2t[NVC];
     uint32_t cap_keys[NVC], cap_k2t[NVC];
     uint32_t* dst;                // AoS by pair: last k2t slot of the pair's run
-    uint32_t* vdst;
     uint32_t* overflow;
     const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
     const uint32_t* lsum_e;
@@ -731,11 +694,10 @@ struct OffsetsOp {
             }
         }
         if (!layout) return;
-        const bool large = meta[t] & META_LARGE;
-        if (large) return;        // k_large_layout
-        const uint32_t b = large ? voff[t] : key_off[t], e = large ? voff[t + 1] : key_off[t + 1];
-        const uint32_t* src = large ? vcnt : cnt;
-        uint32_t* d = large ? vdst : dst;
+        if (meta[t] & META_LARGE) return;     // k_large_layout
+        const uint32_t b = key_off[t], e = key_off[t + 1];
+        const uint32_t* src = cnt;
+        uint32_t* d = dst;
         for (int c = 0; c < NVC; ++c) {
             const uint32_t nk = el.k[c];
             if (nk == 0) continue;
@@ -748,7 +710,7 @@ struct OffsetsOp {
             for (uint32_t x = b; x < e; ++x) {
                 const uint32_t cc = src[(size_t)x * NVC + c];
                 if (cc == 0) continue;
-                out_keys[c][kb + kk] = large ? vi_key[x] : keys[x];
+                out_keys[c][kb + kk] = keys[x];
                 d[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
                 run += cc;
                 out_k2t[c][mb + kk] = (int32_t)run;

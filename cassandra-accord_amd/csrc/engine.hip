@@ -80,9 +80,8 @@ struct ad_handle {
     uint32_t *cnt = nullptr, *dst = nullptr, *nk = nullptr, *ne = nullptr;
     // virtual items (large txns)
     size_t V = 0;
-    uint32_t *vn = nullptr, *voff = nullptr, *vi_txn = nullptr, *vi_pos = nullptr, *vi_seg0 = nullptr;
-    uint32_t *vcnt = nullptr, *vdst = nullptr;
-    uint64_t* vi_key = nullptr;
+    uint32_t *vn = nullptr, *voff = nullptr, *vi_txn = nullptr, *vi_pos = nullptr, *vi_u = nullptr;
+    uint32_t* vcnt = nullptr;        // per (item, view x class): counts, rewritten in place into fill slots
     // range entries sorted by (start, end, owner)
     uint32_t *rowner = nullptr, *rk0 = nullptr, *rv0 = nullptr, *rk1 = nullptr, *rv1 = nullptr, *eown = nullptr;
     uint64_t *es = nullptr, *ee = nullptr;
@@ -206,7 +205,7 @@ enum Slot : size_t {
     S_TM, S_TL, S_TN, S_EM, S_EL, S_EN, S_ST, S_KOFF, S_KEYS, S_ROFF, S_RS, S_RE,
     S_PRM, S_TXTS, S_EX1, S_META, S_PTXN, S_KA, S_VA, S_KB, S_VB, S_ETXN, S_SPOS, S_EMETA, S_EEXEC,
     S_PMW, S_PMC, S_SEG, S_UD, S_CNT, S_DST, S_NK, S_NE, S_SCRATCH,
-    S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST,
+    S_LVL, S_ORDER, S_UIDX, S_UKEY, S_USEG, S_VN, S_VOFF, S_VTXN, S_VPOS, S_VSEG, S_VCNT,
     S_ROWN, S_RK0, S_RV0, S_RK1, S_RV1, S_ES, S_EE, S_EOWN, S_RNK, S_RNE, S_MSCR,
     S_GID, S_HOME, S_SEND, S_RECV, S_HROWS, S_HGID, S_G, S_SROWS, S_TOT, S_HSTORE, S_XRANK, S_XLIST, S_XOFF,
     S_XBND, S_XSEC, S_OVF, S_OVFL, S_OVFT, S_OVFN, S_OVFG, S_OVFO, S_MHL,
@@ -233,6 +232,10 @@ void release_dead(ad_handle* h) {
     auto rel = [&](size_t slot) {
         if (slot < h->bufs.size() && h->bufs[slot].p) { (void)hipFree(h->bufs[slot].p); h->bufs[slot] = DBuf{}; }
     };
+    if (h->stage == STAGE_MERGE) {
+        for (size_t sl : {S_VTXN, S_VPOS, S_VSEG, S_VCNT}) rel(sl);
+        h->vi_txn = h->vi_pos = h->vi_u = h->vcnt = nullptr;
+    }
     if (h->stage == STAGE_DEPS) {
         for (size_t blk = CSR_MERGED0; blk < CSR_HOST0 + 3 * MAXV; ++blk)
             for (size_t k = 0; k < 10; ++k) rel(S_CSR0 + 10 * blk + k);
@@ -460,9 +463,9 @@ size_t csr_cap(ad_handle* h, size_t block, int which, size_t elem) {
 template <int NV>
 void launch_offsets(ad_handle* h, const TxnArgs& ta, uint32_t* overflow) {
     OffsetsOp<2 * NV> op{};
-    op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt; op.voff = h->voff; op.vcnt = h->vcnt;
+    op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt;
     op.layout = 1;
-    op.keys = h->keys; op.vi_key = h->vi_key; op.dst = h->dst; op.vdst = h->vdst; op.overflow = overflow;
+    op.keys = h->keys; op.dst = h->dst; op.overflow = overflow;
     op.lsum_k = h->nk; op.lsum_e = h->ne; op.heavy = overflow - 1;
     for (int c = 0; c < 2 * NV; ++c) {
         op.o_key_off[c] = h->deps[c].key_off; op.o_ent_off[c] = h->deps[c].ent_off; op.o_k2t_off[c] = h->deps[c].k2t_off;
@@ -611,10 +614,11 @@ int stage_deps(ad_handle* h) {
         HIPCHK(h, hipMemcpyAsync(&V, h->voff + n, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipStreamSynchronize(st));
         h->V = V;
-        CK(dalloc(h, S_VTXN, &h->vi_txn, V)); CK(dalloc(h, S_VPOS, &h->vi_pos, V)); CK(dalloc(h, S_VSEG, &h->vi_seg0, V));
-        CK(dalloc(h, S_VKEY, &h->vi_key, V));
-        CK(dalloc(h, S_VCNT, &h->vcnt, (size_t)V * nvc)); CK(dalloc(h, S_VDST, &h->vdst, (size_t)V * nvc));
-        va.vi_txn = h->vi_txn; va.vi_pos = h->vi_pos; va.vi_seg0 = h->vi_seg0; va.vi_key = h->vi_key;
+        // 12 B + 4 B per (view, class) per item (C4: ~2.5 * 10^9 items): the item's key and segment come from
+        // its distinct-key index, the fill slots overwrite the counts in place
+        CK(dalloc(h, S_VTXN, &h->vi_txn, V)); CK(dalloc(h, S_VPOS, &h->vi_pos, V)); CK(dalloc(h, S_VSEG, &h->vi_u, V));
+        CK(dalloc(h, S_VCNT, &h->vcnt, (size_t)V * nvc));
+        va.vi_txn = h->vi_txn; va.vi_pos = h->vi_pos; va.vi_u = h->vi_u;
         if (V > 0) k_vitems<true><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
     }
     // ---- walk (count)
@@ -625,14 +629,15 @@ int stage_deps(ad_handle* h) {
     wa.gid = h->sharded ? h->gid : nullptr;
     wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
-    wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_seg0 = h->vi_seg0; wa.vcnt = h->vcnt; wa.vdst = h->vdst;
+    wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
+    wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
     wa.qpos = qpos; wa.ex1 = h->ex1;
     if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt, 0, (size_t)nvc * P * 4, st));   // segment heads keep zero counts
     NV_DISPATCH(nv, launch_walk, wa, false, st);
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nvc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt = h->cnt;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
-    ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vdst; ta.vi_key = h->vi_key;
+    ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
     uint32_t* overflow = h->totd + MAX_TOTALS - 1;       // fused-layout overflow flag (read with the totals)
     if (n > 0 && h->V > 0) {
         KScope ks(K_VITEMS);
@@ -734,14 +739,9 @@ int stage_deps(ad_handle* h) {
         }
         CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
     }
-    // Virtual-item work arrays are dead once the CSRs are filled.  Range-domain txns query every CFK key
-    // of their ranges, so for wide-range batches (C4: ~10^9 items x 2R counts and slots) they are the
-    // largest allocation of the handle: give them back before the merge allocates its outputs.
-    if ((size_t)h->V * nvc * 8 > ((size_t)1 << 30)) {
-        for (size_t sl : {S_VTXN, S_VPOS, S_VSEG, S_VKEY, S_VCNT, S_VDST}) CK(drelease(h, sl));
-        h->vi_txn = h->vi_pos = h->vi_seg0 = h->vcnt = h->vdst = nullptr;
-        h->vi_key = nullptr;
-    }
+    // Virtual-item work arrays are dead once the CSRs are filled; they stay allocated for the next batch
+    // (re-allocating C4's ~90 GB of them every batch cost more than the walks) unless the merge runs out of
+    // HBM, when release_dead gives them back (STAGE_MERGE).
     h->have_deps = true;
     h->ls.chains_ready = false;
     h->times.deps_entries = h->deps_entries;

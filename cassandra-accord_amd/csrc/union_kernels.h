@@ -57,8 +57,7 @@ struct VItemArgs {
     const uint32_t* voff;        // [n+1] (fill pass)
     uint32_t* vi_txn;
     uint32_t* vi_pos;
-    uint32_t* vi_seg0;
-    uint64_t* vi_key;
+    uint32_t* vi_u;              // item -> distinct-key index (segment useg[u], key ukey[u])
     const uint32_t* qpos;        // executeAt-bound queries: per txn the bound's arrival position (nullable)
 };
 
@@ -92,8 +91,7 @@ __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
             const uint32_t s = a.qpos ? lb_u32(a.e_txn, s0, s1, a.qpos[t]) : ub_u32(a.e_txn, s0, s1, (uint32_t)t) - 1;
             a.vi_txn[x] = (uint32_t)t;
             a.vi_pos[x] = s;
-            a.vi_seg0[x] = s0;
-            a.vi_key[x] = k;
+            a.vi_u[x] = u;
         }
         return;
     }
@@ -109,8 +107,7 @@ __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
             a.vi_txn[x] = (uint32_t)t;
             // insertPos(bound): first entry with txn > t (PreAccept) / at or past the bound's position (Accept)
             a.vi_pos[x] = a.qpos ? lb_u32(a.e_txn, s0, s1, a.qpos[t]) : ub_u32(a.e_txn, s0, s1, (uint32_t)t);
-            a.vi_seg0[x] = s0;
-            a.vi_key[x] = a.ukey[u];
+            a.vi_u[x] = u;
         }
     }
     if (!FILL) a.vn[t] = c;
