@@ -180,13 +180,16 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Heavy txns: one 64-lane workgroup (a wave) per txn (grid-stride over the heavy list).  The txn's TxnId lists
+// Heavy txns: one 256-thread workgroup per txn (grid-stride over the heavy list).  The txn's TxnId lists
 // are cut into chunks at every MCH-th TxnId of the reply holding the most, its key lists likewise by keys;
 // each chunk is a value interval, so the R-way merge of one chunk (the same loops as k_merge) is
 // independent of the others.  Thread j takes a contiguous run of chunks; a block scan of the per-thread
 // totals gives each thread its output offsets.  Write pass: TxnIds first (a barrier), then keys and
 // per-key lists, whose TxnIds are remapped by binary search in the txn's merged TxnId list.
-constexpr int MCH = 32, MH_T = 64, MH_GRID = 8192;
+constexpr int MCH = 32, MH_T = 256, MH_GRID = 8192;
+// write pass: the txn's merged TxnId list is staged in LDS for the per-entry remap (binary searches in LDS
+// instead of HBM round trips) when it fits
+constexpr uint32_t MH_LDS = 12288;
 
 template <int KW>
 __device__ inline uint32_t lb_key(const uint64_t* k, uint32_t lo, uint32_t hi, const MKey<KW>& v) {
@@ -223,6 +226,7 @@ __device__ inline void block_scan3(uint32_t x[3], uint32_t tot[3]) {
 template <int NV, bool WRITE, int KW>
 __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
     constexpr uint32_t INF = 0xFFFFFFFFu;
+    __shared__ uint32_t sU[WRITE ? MH_LDS : 1];
     const uint32_t H = *a.hcount;
     for (uint32_t hi = blockIdx.x; hi < H; hi += gridDim.x) {
         const uint32_t t = a.hlist[hi];
@@ -327,7 +331,7 @@ __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
                     for (int v = 0; v < NV; ++v) mn = lh[v] < mn ? lh[v] : mn;
                     if (mn == INF) break;
                     if (wr) {
-                        x = lb_u32(U, x, mu, mn);
+                        x = lb_u32(U, x, mu, mn);       // U: the LDS copy when it fits
                         a.o_k2t[ep++] = (int32_t)x;
                     }
                     ++me;
@@ -357,14 +361,20 @@ __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
             block_scan3(x, tot);
             if (threadIdx.x == 0) { a.mk[t] = tot[0]; a.me[t] = tot[1]; a.mu[t] = tot[2]; }
         } else {
-            uint32_t* U = a.o_txns + a.o_ent_off[t];
+            uint32_t* Ug = a.o_txns + a.o_ent_off[t];
             for (uint32_t c = c0; c < c1; ++c) x[2] += t_union(c, nullptr);
             block_scan3(x, tot);
             uint32_t pos = x[2];
-            for (uint32_t c = c0; c < c1; ++c) pos += t_union(c, U + pos);
+            for (uint32_t c = c0; c < c1; ++c) pos += t_union(c, Ug + pos);
             const uint32_t mu = tot[2];
             __threadfence_block();
             __syncthreads();
+            const uint32_t* U = Ug;
+            if (mu <= MH_LDS) {
+                for (uint32_t i = threadIdx.x; i < mu; i += MH_T) sU[i] = Ug[i];
+                __syncthreads();
+                U = sU;
+            }
             // keys: per-thread (keys, entries) totals, then the writes
             x[0] = x[1] = x[2] = 0;
             for (uint32_t c = c0; c < c1; ++c) {
