@@ -52,6 +52,9 @@ def lib():
         L.ad_load_batch.argtypes = [vp, C.POINTER(abi.AdBatch)]
         L.ad_preaccept_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_accept_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
+        L.ad_cfk_retain.argtypes = [vp, C.POINTER(C.c_size_t)]
+        L.ad_cfk_reset.argtypes = [vp]
+        L.ad_cfk_rows.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_uint32)]
         L.ad_fetch_deps.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut)]
         L.ad_merge_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
@@ -88,7 +91,7 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_alltoall", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
             "ad_shard_levels_allreduce", "ad_shard_order", "ad_shard_set_holders", "ad_shard_levels_deltas",
-            "ad_shard_levels_apply", "ad_shard_levels_exchange")
+            "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows")
 
 
 class DepsEngine:
@@ -130,8 +133,12 @@ class DepsEngine:
 
     def load(self, batch):
         self._batch = abi.make_batch(batch)
-        self.n = batch["n"]
         self._check(lib().ad_load_batch(self.h, C.byref(self._batch)), "ad_load_batch")
+        # rows on the device: the batch, after any CFK history rows kept from the previous batch (ad_cfk_retain)
+        hr = C.c_size_t()
+        self._check(lib().ad_cfk_rows(self.h, C.byref(hr), None), "ad_cfk_rows")
+        self.hist_rows = hr.value
+        self.n = self.n_rows = batch["n"] + hr.value
 
     def preaccept_deps(self):
         sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
@@ -145,6 +152,22 @@ class DepsEngine:
         self._check(lib().ad_accept_deps(self.h, sizes), "ad_accept_deps")
         self._dep_sizes = sizes
         return sizes
+
+    def cfk_retain(self):
+        """Keep this batch's still-visible CFK rows on the device for the next load (returns the kept row count)."""
+        k = C.c_size_t()
+        self._check(lib().ad_cfk_retain(self.h, C.byref(k)), "ad_cfk_retain")
+        return k.value
+
+    def cfk_reset(self):
+        self._check(lib().ad_cfk_reset(self.h), "ad_cfk_reset")
+
+    def cfk_rows(self):
+        """(history rows H, gid[n]: global arrival rank of every row of the loaded batch)."""
+        hr = C.c_size_t()
+        g = np.zeros(max(self.n_rows, 1), np.uint32)
+        self._check(lib().ad_cfk_rows(self.h, C.byref(hr), g.ctypes.data_as(C.POINTER(C.c_uint32))), "ad_cfk_rows")
+        return hr.value, g[:self.n_rows]
 
     def fetch_deps(self, view, cls):
         s = self._dep_sizes[view * abi.NUM_CLASSES + cls]

@@ -14,8 +14,13 @@
 //   k_mc_txns<NV>        one thread per txn: per pair, the in-flight window walk per view from the pair's
 //                        sorted position, then the prefix max of the entry just below the window; max over
 //                        the txn's pairs per view, fast-path test (no per-pair intermediate in HBM)
+//   k_mc_range_keys<NV>  range-domain txns: the same per CFK key inside their ranges (MaxConflicts is a
+//                        ReducingRangeMap: get(ranges) folds every key inside), one wave per txn
+//   k_mc_range_entries<NV> every txn vs the batch's range txns: ranges containing one of its keys /
+//                        intersecting one of its ranges (the windowed join of k_range_deps), one wave per txn
 #pragma once
 #include "deps_kernels.h"
+#include "union_kernels.h"
 
 namespace ad {
 
@@ -121,6 +126,146 @@ __global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
         if (a.local_rank) a.local_rank[(size_t)v * a.n + t] = be[v] ? br[v] : AD_RANK_NONE;
         a.fast[(size_t)v * a.n + t] = (be[v] == 0 || t1 >= be[v]) ? 1 : 0;   // TxnId.compareTo(max) >= 0
     }
+}
+
+// ---- range footprints ---------------------------------------------------------------------------------------
+struct McRangeArgs {
+    size_t n;
+    const uint8_t* meta;
+    const uint64_t* ex1;       // [n] executeAt + 1 (packed)
+    const uint64_t* tx_ts;     // [n] packed TxnId
+    const uint32_t* key_off;
+    const uint64_t* keys;
+    const uint32_t* range_off;
+    const uint64_t* rs;
+    const uint64_t* re;
+    // CFK entries (k_mc_range_keys)
+    const uint64_t* ukey;
+    const uint32_t* useg;
+    uint32_t U;
+    const uint32_t* e_txn;
+    const uint8_t* e_meta;
+    const uint64_t* e_exec1;
+    const uint64_t* pm_e;
+    const uint32_t* pm_r;
+    // range entries sorted by (start, end, owner) (k_mc_range_entries)
+    size_t Q;
+    const uint64_t* es;
+    const uint64_t* ee;
+    const uint32_t* eown;
+    uint64_t wmax;
+    uint32_t window, thresh;
+    uint64_t seed;
+    uint32_t* max_rank;        // [v * n + t] folded in place (batch rows: range batches are not sharded)
+    uint8_t* fast;
+};
+
+// wave max of (e, r) per view; lane 0 folds it into the txn's answer and redoes the fast-path test
+template <int NV>
+__device__ inline void mc_fold_wave(const McRangeArgs& a, size_t t, uint64_t* be, uint32_t* br) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        uint64_t e = be[v];
+        uint32_t r = br[v];
+#pragma unroll
+        for (int o = WAVE / 2; o > 0; o >>= 1) {
+            const uint64_t e2 = __shfl_xor(e, o);
+            const uint32_t r2 = __shfl_xor(r, o);
+            if (mc_less(e, r, e2, r2)) { e = e2; r = r2; }
+        }
+        if (__lane_id() == 0 && e != 0) {
+            const size_t x = (size_t)v * a.n + t;
+            const uint32_t cur = a.max_rank[x];
+            const uint64_t ce = cur == AD_RANK_NONE ? 0ull : a.ex1[cur];
+            if (cur == AD_RANK_NONE || mc_less(ce, cur, e, r)) {
+                a.max_rank[x] = r;
+                a.fast[x] = a.tx_ts[t] + 1 >= e ? 1 : 0;          // TxnId.compareTo(max) >= 0
+            }
+        }
+    }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void k_mc_range_keys(McRangeArgs a) {
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (t >= a.n || meta_domain(a.meta[t]) != AD_DOMAIN_RANGE) return;
+    const uint32_t lo_w = a.window == 0 ? (uint32_t)t : ((uint32_t)t > a.window ? (uint32_t)t - a.window : 0u);
+    uint64_t be[NV];
+    uint32_t br[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) { be[v] = 0; br[v] = 0; }
+    for (uint32_t q = a.range_off[t]; q < a.range_off[t + 1]; ++q) {
+        // CFK keys inside (start, end]
+        const uint32_t ulo = ub_u64(a.ukey, 0, a.U, a.rs[q]), uhi = ub_u64(a.ukey, ulo, a.U, a.re[q]);
+        for (uint32_t u = ulo + __lane_id(); u < uhi; u += WAVE) {
+            const int s0 = (int)a.useg[u];
+            const int pos = (int)ub_u32(a.e_txn, a.useg[u], a.useg[u + 1], (uint32_t)t);   // insertPos(TxnId t)
+            int x = pos - 1;
+            for (; x >= s0; --x) {                 // in-flight window: per view unless dropped
+                const uint32_t j = a.e_txn[x];
+                if (j < lo_w) break;
+                if (!manages(a.e_meta[x])) continue;
+                const uint64_t e = a.e_exec1[x];
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, (uint32_t)t, j) < a.thresh) && mc_less(be[v], br[v], e, j)) {
+                        be[v] = e; br[v] = j;
+                    }
+            }
+            if (x >= s0) {                         // recorded prefix: one scan value for every view
+                const uint64_t e = a.pm_e[x];
+                const uint32_t r = a.pm_r[x];
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    if (mc_less(be[v], br[v], e, r)) { be[v] = e; br[v] = r; }
+            }
+        }
+    }
+    mc_fold_wave<NV>(a, t, be, br);
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void k_mc_range_entries(McRangeArgs a) {
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (t >= a.n) return;
+    const uint32_t i = (uint32_t)t;
+    const bool key_dom = meta_domain(a.meta[i]) == AD_DOMAIN_KEY;
+    const uint32_t fb = key_dom ? a.key_off[i] : a.range_off[i];
+    const uint32_t fe = key_dom ? a.key_off[i + 1] : a.range_off[i + 1];
+    const uint32_t lo_w = a.window == 0 ? i : (i > a.window ? i - a.window : 0u);
+    const uint32_t Q = (uint32_t)a.Q;
+    uint64_t be[NV];
+    uint32_t br[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) { be[v] = 0; br[v] = 0; }
+    for (uint32_t f = fb; f < fe; ++f) {
+        // entries that can intersect the element: start within the widest range below it
+        uint64_t qs, qe;
+        if (key_dom) { qe = a.keys[f]; qs = qe; } else { qs = a.rs[f]; qe = a.re[f]; }
+        const uint64_t vlo = key_dom ? (qe > a.wmax ? qe - a.wmax : 0ull) : (qs >= a.wmax ? qs - a.wmax + 1 : 0ull);
+        const uint32_t lo = lb_u64(a.es, 0, Q, vlo), hi = lb_u64(a.es, lo, Q, qe);
+        for (uint32_t x = lo + __lane_id(); x < hi; x += WAVE) {
+            const uint32_t j = a.eown[x];
+            if (j >= i) continue;
+            const uint32_t mj = a.meta[j];
+            const uint32_t kj = meta_kind(mj);
+            if (!(kj == AD_KIND_READ || kj == AD_KIND_WRITE || kj == AD_KIND_SYNC_POINT || kj == AD_KIND_EXCLUSIVE_SYNC_POINT))
+                continue;                          // globally visible kinds only
+            const uint64_t s = a.es[x], e = a.ee[x];
+            const bool hit = key_dom ? (s < qe && qe <= e) : (s < qe && e > qs);
+            if (!hit) continue;
+            const bool inw = j >= lo_w;
+            const uint32_t st = meta_status(mj);
+            if (!inw && (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID)) continue;
+            const uint64_t ej = a.ex1[j];
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (!(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh) && mc_less(be[v], br[v], ej, j)) {
+                    be[v] = ej; br[v] = j;
+                }
+        }
+    }
+    mc_fold_wave<NV>(a, t, be, br);
 }
 
 // ---- MaxConflicts carried across batches (the store's state from its earlier batches) ----------------------

@@ -21,6 +21,7 @@
 
 #include "conflict_kernels.h"
 #include "level_kernels.h"
+#include "history_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
 #include "shard_kernels.h"
@@ -130,6 +131,12 @@ struct ad_handle {
     bool evicting = false;
     bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
     bool accept = false;             // the deps stage runs with bound = executeAt (ad_accept_deps)
+    // CFK history (history_kernels.h): kept rows of earlier batches, prepended to the next loaded batch
+    bool hist_valid = false;         // ad_cfk_retain ran: the next ad_load_batch prepends hist_n rows
+    size_t hist_n = 0, hist_p = 0;   // kept rows / their keys
+    uint64_t hist_next = 0;          // global arrival rank of the next batch's first txn
+    bool hist_active = false;        // the loaded batch's rows [0, hist_rows) are history; gid = global ranks
+    size_t hist_rows = 0;
     uint32_t* qpos = nullptr;        // [n] arrival position of each txn's executeAt (accept bound)
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
@@ -212,6 +219,7 @@ enum Slot : size_t {
     S_MCPE, S_MCPR, S_MCINV, S_MCRANK, S_MCFAST, S_MCLOCAL, S_MCCK, S_MCCM, S_MCCL, S_MCCN,
     S_MCOM, S_MCOL, S_MCON, S_MCOF, S_MCSK, S_MCSM, S_MCSL, S_MCSN, S_MCSU, S_MCSP,
     S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
+    S_HTM, S_HTL, S_HTN, S_HEM, S_HEL, S_HEN, S_HST, S_HKOFF, S_HKEYS, S_HGIDS, S_HSEGM, S_HKEEP, S_HROWS2, S_HCNT,
     S_NUM_FIXED,
     S_CSR0 = 160
 };
@@ -558,6 +566,12 @@ template <int NV>
 void launch_mc(const McArgs& a, hipStream_t st) {
     k_mc_txns<NV><<<ceil_div((long)a.n, 256), 256, 0, st>>>(a);
 }
+template <int NV>
+void launch_mc_ranges(const McRangeArgs& a, hipStream_t st) {
+    const int g = ceil_div((long)a.n * WAVE, 256);
+    if (a.U > 0) k_mc_range_keys<NV><<<g, 256, 0, st>>>(a);
+    k_mc_range_entries<NV><<<g, 256, 0, st>>>(a);
+}
 
 struct StageScope {
     ad_handle* h;
@@ -626,7 +640,7 @@ int stage_deps(ad_handle* h) {
     wa.e_txn = h->e_txn; wa.e_meta = h->e_meta; wa.e_exec1 = h->e_exec1; wa.seg_start = h->seg_start;
     wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
-    wa.gid = h->sharded ? h->gid : nullptr;
+    wa.gid = (h->sharded || h->hist_active) ? h->gid : nullptr;
     wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
@@ -889,6 +903,8 @@ int stage_merge(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_exec_levels before ad_merge_deps");
+    if (h->hist_active)
+        return set_err(h, AD_ERR_UNSUPPORTED, "ad_exec_levels: the batch carries CFK history rows (already ordered in their own batch)");
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_exec_levels needs ad_preaccept_deps on this batch (its key chains)");
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
@@ -1035,33 +1051,63 @@ const char* ad_last_error(const ad_handle* h) { return h ? h->err.c_str() : "nul
 int ad_load_batch(ad_handle* h, const ad_batch* b) {
     if (!h || !b) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    const size_t n = b->n;
-    if (n >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
-    const size_t P = n ? b->key_off[n] : 0;
-    const size_t Q = (n && b->range_off) ? b->range_off[n] : 0;
-    if (P >= (1ull << 31) || Q >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
+    const size_t nb = b->n;
+    if (nb >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
+    const size_t Pb = nb ? b->key_off[nb] : 0;
+    const size_t Q = (nb && b->range_off) ? b->range_off[nb] : 0;
+    if (Pb >= (1ull << 31) || Q >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
+    // CFK history from the previous batch (ad_cfk_retain): its kept rows go first, then the new txns
+    const bool hist = h->hist_valid;
+    if (hist && Q) return set_err(h, AD_ERR_UNSUPPORTED, "CFK history: key batches only (no range txns)");
+    if (hist && h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "CFK history: not in sharded mode");
+    const size_t H = hist ? h->hist_n : 0, HP = hist ? h->hist_p : 0;
+    const size_t n = H + nb, P = HP + Pb;
+    if (n >= (1ull << 31) || P >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
     h->n = n; h->P = P; h->Q = Q;
     h->loaded = false;
     h->have_deps = h->have_merged = h->have_levels = false;
     h->mc_ready = false;
     h->mc_fast = nullptr;
+    h->hist_active = hist;
+    h->hist_rows = H;
+    h->hist_valid = false;           // consumed: ad_cfk_retain on this batch carries the state on
     CK(dalloc(h, S_TM, &h->tm, n)); CK(dalloc(h, S_TL, &h->tl, n)); CK(dalloc(h, S_TN, &h->tn, n));
     CK(dalloc(h, S_EM, &h->em, n)); CK(dalloc(h, S_EL, &h->el, n)); CK(dalloc(h, S_EN, &h->en, n));
     CK(dalloc(h, S_ST, &h->status, n)); CK(dalloc(h, S_KOFF, &h->key_off, n + 1)); CK(dalloc(h, S_KEYS, &h->keys, P));
     CK(dalloc(h, S_ROFF, &h->range_off, n + 1)); CK(dalloc(h, S_RS, &h->range_s, Q)); CK(dalloc(h, S_RE, &h->range_e, Q));
     hipStream_t st = h->st;
-    if (n) {
-        HIPCHK(h, hipMemcpyAsync(h->tm, b->txn_msb, n * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->tl, b->txn_lsb, n * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->tn, b->txn_node, n * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->em, b->exec_msb, n * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->el, b->exec_lsb, n * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->en, b->exec_node, n * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->status, b->status, n, hipMemcpyHostToDevice, st));
-        HIPCHK(h, hipMemcpyAsync(h->key_off, b->key_off, (n + 1) * 4, hipMemcpyHostToDevice, st));
-        if (P) HIPCHK(h, hipMemcpyAsync(h->keys, b->keys, P * 8, hipMemcpyHostToDevice, st));
-    } else {
+    if (H) {
+        auto d2d = [&](void* dst, size_t slot, size_t bytes) {
+            return hipMemcpyAsync(dst, h->bufs[slot].p, bytes, hipMemcpyDeviceToDevice, st);
+        };
+        HIPCHK(h, d2d(h->tm, S_HTM, H * 8)); HIPCHK(h, d2d(h->tl, S_HTL, H * 8)); HIPCHK(h, d2d(h->tn, S_HTN, H * 4));
+        HIPCHK(h, d2d(h->em, S_HEM, H * 8)); HIPCHK(h, d2d(h->el, S_HEL, H * 8)); HIPCHK(h, d2d(h->en, S_HEN, H * 4));
+        HIPCHK(h, d2d(h->status, S_HST, H)); HIPCHK(h, d2d(h->key_off, S_HKOFF, H * 4));
+        if (HP) HIPCHK(h, d2d(h->keys, S_HKEYS, HP * 8));
+    }
+    if (nb) {
+        HIPCHK(h, hipMemcpyAsync(h->tm + H, b->txn_msb, nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->tl + H, b->txn_lsb, nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->tn + H, b->txn_node, nb * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->em + H, b->exec_msb, nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->el + H, b->exec_lsb, nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->en + H, b->exec_node, nb * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->status + H, b->status, nb, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(h->key_off + H, b->key_off, (nb + 1) * 4, hipMemcpyHostToDevice, st));
+        if (Pb) HIPCHK(h, hipMemcpyAsync(h->keys + HP, b->keys, Pb * 8, hipMemcpyHostToDevice, st));
+    } else if (!H) {
         HIPCHK(h, hipMemsetAsync(h->key_off, 0, 4, st));
+    } else {
+        const uint32_t end = (uint32_t)HP;                                           // empty batch: end offset
+        HIPCHK(h, hipMemcpyAsync(h->key_off + H, &end, 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    if (hist) {
+        // global arrival ranks: the kept rows' own, then next + i; the new key offsets follow the kept keys
+        CK(dalloc(h, S_GID, &h->gid, std::max<size_t>(n, 1)));
+        if (H) HIPCHK(h, hipMemcpyAsync(h->gid, h->bufs[S_HGIDS].p, H * 4, hipMemcpyDeviceToDevice, st));
+        if (nb) k_hist_new_rows<<<ceil_div((long)nb + 1, 256), 256, 0, st>>>(H, nb, h->hist_next, (uint32_t)HP, h->gid, h->key_off);
+        HIPCHK(h, hipGetLastError());
     }
     if (Q) {
         HIPCHK(h, hipMemcpyAsync(h->range_off, b->range_off, (n + 1) * 4, hipMemcpyHostToDevice, st));
@@ -1103,6 +1149,7 @@ static int run_deps(ad_handle* h, ad_csr_sizes* sizes, bool accept) {
     g_tracer = &h->tracer;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
     if (accept && h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_accept_deps: sharded stores answer PreAccept deps only");
+    if (accept && h->hist_active) return set_err(h, AD_ERR_UNSUPPORTED, "ad_accept_deps: not over a CFK history batch");
     hipSetDevice(h->device);
     h->accept = accept;
     int rc = stage_prepare(h);
@@ -1136,7 +1183,6 @@ static int fetch_empty(ad_handle* h, ad_csr_out* out) {
 // deps stage left on the device: leaves max_rank / fast (and the batch-local rank) in their slots.
 static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_out, uint32_t** local_out) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
-    if (h->Q > 0) return set_err(h, AD_ERR_UNSUPPORTED, "max conflicts: range txns are not supported");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     const size_t n = h->n, P = h->P;
@@ -1145,7 +1191,7 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
     McArgs a{};
     a.n = n; a.P = P;
     a.e_txn = h->e_txn; a.e_meta = h->e_meta; a.e_exec1 = h->e_exec1; a.seg_start = h->seg_start;
-    a.gid = h->sharded ? h->gid : nullptr;
+    a.gid = (h->sharded || h->hist_active) ? h->gid : nullptr;
     a.window = h->cfg.window; a.thresh = ad_drop_threshold(h->cfg.drop_p); a.seed = h->cfg.seed;
     a.key_off = h->key_off; a.tx_ts = h->tx_ts;
     uint64_t* pm_e = nullptr;
@@ -1164,6 +1210,17 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
             scan_any(h, op, P);
         }
         NV_DISPATCH(nv, launch_mc, a, st);
+        if (h->Q > 0) {
+            // range footprints: range txns' CFK keys, and every txn against the range entries
+            McRangeArgs ra{};
+            ra.n = n; ra.meta = h->meta; ra.ex1 = h->ex1; ra.tx_ts = h->tx_ts; ra.key_off = h->key_off; ra.keys = h->keys;
+            ra.range_off = h->range_off; ra.rs = h->range_s; ra.re = h->range_e;
+            ra.ukey = h->ukey; ra.useg = h->useg; ra.U = P ? h->hprm.n_keys_u : 0;
+            ra.e_txn = h->e_txn; ra.e_meta = h->e_meta; ra.e_exec1 = h->e_exec1; ra.pm_e = pm_e; ra.pm_r = pm_r;
+            ra.Q = h->Q; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.wmax = h->wmax;
+            ra.window = a.window; ra.thresh = a.thresh; ra.seed = a.seed; ra.max_rank = rank; ra.fast = fst;
+            NV_DISPATCH(nv, launch_mc_ranges, ra, st);
+        }
     }
     HIPCHK(h, hipGetLastError());
     h->mc_ready = true;
@@ -1208,6 +1265,7 @@ int ad_max_conflicts_carry(ad_handle* h, size_t m, const uint64_t* keys, const u
 
 int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast) {
     if (!h) return AD_ERR_ARGUMENT;
+    if (h->Q > 0) return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts_ts: the carried MaxConflicts map is per key (key batches)");
     uint32_t *rank = nullptr, *local = nullptr;
     uint8_t* fst = nullptr;
     CK(run_max_conflicts(h, &rank, &fst, &local));
@@ -1241,6 +1299,7 @@ int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* nod
 int ad_max_conflicts_export(ad_handle* h, size_t* m_out, uint64_t* keys, uint64_t* msb, uint64_t* lsb, int32_t* node) {
     if (!h || !m_out) return AD_ERR_ARGUMENT;
     if (!h->mc_ready) return set_err(h, AD_ERR_STATE, "ad_max_conflicts_export: run ad_max_conflicts(_ts) on this batch first");
+    if (h->Q > 0) return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts_export: the carried MaxConflicts map is per key (key batches)");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
     const uint32_t U = h->P ? h->hprm.n_keys_u : 0;
@@ -1552,10 +1611,109 @@ int ad_reset_kernel_stats(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 static size_t align8(size_t x) { return (x + 7) & ~(size_t)7; }
 
+int ad_cfk_retain(ad_handle* h, size_t* retained) {
+    if (!h) return AD_ERR_ARGUMENT;
+    if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_cfk_retain: run ad_preaccept_deps on the batch first");
+    if (h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_retain: not in sharded mode");
+    if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_retain: key batches only (no range txns)");
+    hipSetDevice(h->device);
+    g_tracer = &h->tracer;
+    hipStream_t st = h->st;
+    const size_t n = h->n, P = h->P;
+    const uint32_t* gid = h->hist_active ? h->gid : nullptr;
+    // the next batch's first global rank; every later query's window starts at or above next - W
+    uint64_t last_g = 0, last_ts = 0;
+    if (n) {
+        uint32_t lg = (uint32_t)(n - 1);
+        if (gid) HIPCHK(h, hipMemcpyAsync(&lg, gid + n - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&last_ts, h->tx_ts + n - 1, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        last_g = lg;
+    }
+    const uint64_t next = n ? last_g + 1 : h->hist_next;
+    const uint64_t wlo = h->cfg.window == 0 ? next : (next > h->cfg.window ? next - h->cfg.window : 0);
+    uint8_t* keep = nullptr;
+    unsigned long long* segmax = nullptr;
+    uint32_t *rows = nullptr, *tot = nullptr;
+    CK(dalloc(h, S_HKEEP, &keep, std::max<size_t>(n, 1)));
+    CK(dalloc(h, S_HSEGM, &segmax, std::max<size_t>(P, 1)));
+    CK(dalloc(h, S_HROWS2, &rows, std::max<size_t>(n, 1) + 16));
+    tot = rows + std::max<size_t>(n, 1);
+    uint32_t H = 0;
+    if (n) {
+        HIPCHK(h, hipMemsetAsync(keep, 0, n, st));
+        if (P) {
+            HIPCHK(h, hipMemsetAsync(segmax, 0, P * 8, st));
+            const int g = ceil_div((long)P, 256);
+            k_hist_seg_wmax<<<g, 256, 0, st>>>(P, h->seg_start, h->e_meta, h->e_exec1, last_ts + 1, segmax);
+            k_hist_keep<<<g, 256, 0, st>>>(P, h->seg_start, h->e_txn, h->e_meta, h->e_exec1, segmax, gid, wlo, keep);
+        }
+        device_scan(CompactFlagOp{keep, rows, tot, n}, n, (uint32_t*)h->scratch, st);
+        HIPCHK(h, hipMemcpyAsync(&H, tot, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    // the kept rows (own slots: the next load overwrites the batch arrays)
+    uint64_t *otm, *otl, *oem, *oel, *okeys;
+    int32_t *otn, *oen;
+    uint8_t* ost;
+    uint32_t *okoff, *ogid, *ocnt;
+    const size_t H1 = std::max<size_t>(H, 1);
+    CK(dalloc(h, S_HTM, &otm, H1)); CK(dalloc(h, S_HTL, &otl, H1)); CK(dalloc(h, S_HTN, &otn, H1));
+    CK(dalloc(h, S_HEM, &oem, H1)); CK(dalloc(h, S_HEL, &oel, H1)); CK(dalloc(h, S_HEN, &oen, H1));
+    CK(dalloc(h, S_HST, &ost, H1)); CK(dalloc(h, S_HKOFF, &okoff, H1 + 1)); CK(dalloc(h, S_HGIDS, &ogid, H1));
+    CK(dalloc(h, S_HCNT, &ocnt, H1 + 16));
+    uint32_t HP = 0;
+    if (H) {
+        HistGather g{};
+        g.H = H; g.rows = rows; g.tm = h->tm; g.tl = h->tl; g.em = h->em; g.el = h->el; g.tn = h->tn; g.en = h->en;
+        g.st = h->status; g.key_off = h->key_off; g.gid = gid;
+        g.otm = otm; g.otl = otl; g.oem = oem; g.oel = oel; g.otn = otn; g.oen = oen; g.ost = ost; g.ocnt = ocnt; g.ogid = ogid;
+        k_hist_gather_rows<<<ceil_div((long)H, 256), 256, 0, st>>>(g);
+        scan_offsets(h, ocnt, okoff, H);
+        HIPCHK(h, hipMemcpyAsync(&HP, okoff + H, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        CK(dalloc(h, S_HKEYS, &okeys, std::max<size_t>(HP, 1)));
+        k_hist_gather_keys<<<ceil_div((long)H, 256), 256, 0, st>>>(H, rows, h->key_off, h->keys, okoff, okeys);
+    }
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(st));
+    h->hist_n = H;
+    h->hist_p = HP;
+    h->hist_next = next;
+    h->hist_valid = true;
+    if (retained) *retained = H;
+    return AD_OK;
+}
+
+int ad_cfk_reset(ad_handle* h) {
+    if (!h) return AD_ERR_ARGUMENT;
+    h->hist_valid = false;
+    h->hist_n = h->hist_p = 0;
+    h->hist_next = 0;
+    return AD_OK;
+}
+
+int ad_cfk_rows(ad_handle* h, size_t* hist_rows, uint32_t* gid) {
+    if (!h || !hist_rows) return AD_ERR_ARGUMENT;
+    if (!h->loaded) return set_err(h, AD_ERR_STATE, "ad_cfk_rows: no batch loaded");
+    hipSetDevice(h->device);
+    *hist_rows = h->hist_active ? h->hist_rows : 0;
+    if (gid && h->n) {
+        if (h->hist_active) {
+            HIPCHK(h, hipMemcpyAsync(gid, h->gid, h->n * 4, hipMemcpyDeviceToHost, h->st));
+            HIPCHK(h, hipStreamSynchronize(h->st));
+        } else {
+            for (size_t i = 0; i < h->n; ++i) gid[i] = (uint32_t)i;
+        }
+    }
+    return AD_OK;
+}
+
 int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home_store, uint32_t self, uint32_t world, size_t n_global) {
     if (!h || (!gid && h->n) || (!home_store && h->n) || world == 0 || world > (uint32_t)MAX_STORES || self >= world)
         return AD_ERR_ARGUMENT;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "ad_shard_setup: load the store's batch first");
+    if (h->hist_active) return set_err(h, AD_ERR_UNSUPPORTED, "ad_shard_setup: the batch carries CFK history rows");
     if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "sharded mode: range txns are not supported in this build");
     hipSetDevice(h->device);
     const size_t n = h->n;

@@ -211,18 +211,19 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
  *   CommandStore.preaccept            local/CommandStore.java:322-347   (maxConflicts.get(keys), fast-path test :342-344)
  *   MaxConflicts.get / update         local/MaxConflicts.java:46-59
  *   CommandStore.updateMaxConflicts   local/CommandStore.java:282-291, SafeCommandStore.java:210-222 (globally visible kinds)
- * max_rank[v*n + i] = the batch rank of the txn whose executeAt is maxConflicts.get(keys of i) in view v — the greatest
- * executeAt (Timestamp.compareTo; ties to the larger rank) over the txns j < i sharing a key with i that the view has
- * stored (CommandsForKey entries not TRANSITIVELY_KNOWN/INVALID; in-flight j unless the view dropped it) — or
- * AD_RANK_NONE (Timestamp.NONE).  fast[v*n + i] = 1 when TxnId_i >= that timestamp (or NONE): the replica answers
+ * max_rank[v*n + i] = the batch rank of the txn whose executeAt is maxConflicts.get(keysOrRanges of i) in view v — the
+ * greatest executeAt (Timestamp.compareTo; ties to the larger rank) over the globally visible txns j < i whose footprint
+ * meets i's that the view has stored (not TRANSITIVELY_KNOWN/INVALID; in-flight j unless the view dropped it) — or
+ * AD_RANK_NONE (Timestamp.NONE).  MaxConflicts is a ReducingRangeMap (keys are points, ranges (start, end] intervals):
+ * a key txn meets the txns on its keys and the range txns covering one; a range txn the key txns inside its ranges
+ * and the range txns crossing them.  fast[v*n + i] = 1 when TxnId_i >= that timestamp (or NONE): the replica answers
  * witnessedAt = TxnId (fast path), else time.uniqueNow(maxConflict), which the host clock supplies.
  * Model assumption (stated, not pinned by the reference): an in-flight j the view holds contributes its batch
  * executeAt — the value MaxConflicts holds once j commits.  In the reference a PreAccepted j contributes the
  * view's own earlier witnessedAt proposal for j (<= its final executeAt for slow-path txns) until it commits,
  * so for views holding slow-path j in flight max_rank / fast may be higher / lower than a live replica's.
  * The oracle (oracle.cpp Oracle::max_conflict) makes the same assumption.
- * Key-domain batches (AD_ERR_UNSUPPORTED when the batch has range txns).  Either pointer may be NULL.
- * Sharded stores (ad_shard_setup): rows are local, max_rank holds global arrival ranks; PreAccept.reduce's
+ * Either pointer may be NULL.  Sharded stores (ad_shard_setup): rows are local, max_rank holds global arrival ranks; PreAccept.reduce's
  * mergeMax across stores (messages/PreAccept.java:141-156) is then a per-txn max over the stores' answers. */
 #define AD_RANK_NONE 0xFFFFFFFFu
 int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8_t* fast /* [replicas*n] */);
@@ -238,7 +239,8 @@ int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8
  *                            executeAt in the batch (final statuses; TRANSITIVELY_KNOWN / INVALID unrecorded).
  *                            Two calls: keys == NULL returns *m only.  Needs ad_max_conflicts(_ts) on the batch.
  * A txn that PreAccepts in a later batch than a larger-TxnId txn (arrival order != TxnId order,
- * PreAcceptTest.multiKeyTimestampUpdate) sees it through the carry. */
+ * PreAcceptTest.multiKeyTimestampUpdate) sees it through the carry.  The carried table is per key: key batches only
+ * (AD_ERR_UNSUPPORTED for _ts / _export when the batch has range txns). */
 int  ad_max_conflicts_carry(ad_handle* h, size_t m, const uint64_t* keys, const uint64_t* msb, const uint64_t* lsb,
                             const int32_t* node);
 int  ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast);
@@ -288,6 +290,22 @@ int  ad_kernel_stats(ad_handle* h, int kid, const char** name, uint64_t* calls, 
 int  ad_reset_kernel_stats(ad_handle* h);
 /* elements the traced launches of kernel kid processed (its algorithmic unit: pairs, txns, sort items) */
 int  ad_kernel_units(ad_handle* h, int kid, uint64_t* units);
+
+/* ------------------------------------------------------------------------------------------ */
+/* CommandsForKey state across batches.  A store's batches continue one TxnId order; instead  */
+/* of a closed world per batch, ad_cfk_retain (after ad_preaccept_deps on a batch) keeps on the device every txn */
+/* whose CFK entries a later query can still see — in flight for a later query (global rank >= next - W), or on  */
+/* some key not prunable (Pruning.java:164-233: TRANSITIVELY_KNOWN / INVALID / unmanaged entries, and committed  */
+/* Reads/Writes executing before the key's greatest committed Write below every later TxnId, are never emitted  */
+/* again by mapReduceActive, CommandsForKey.java:925-983).  The next ad_load_batch puts those rows first: the    */
+/* loaded batch is [kept rows | new txns], window / drop decisions and MaxConflicts use global arrival ranks,    */
+/* and every output row / TxnId is a combined row (ad_cfk_rows maps rows to global ranks).  The new txns'      */
+/* deps equal those of the whole stream resolved at once.  Key batches only; ad_exec_levels, ad_accept_deps and  */
+/* sharded mode are refused over a batch with history rows (AD_ERR_UNSUPPORTED).                               */
+/* ------------------------------------------------------------------------------------------ */
+int  ad_cfk_retain(ad_handle* h, size_t* retained /* out: kept rows, or NULL */);
+int  ad_cfk_reset(ad_handle* h);                        /* forget the kept rows: the next batch starts afresh */
+int  ad_cfk_rows(ad_handle* h, size_t* hist_rows /* out */, uint32_t* gid /* [n] global rank per row, or NULL */);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU key-range sharding (one handle = one CommandStore = one GPU).                     */

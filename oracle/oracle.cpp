@@ -324,11 +324,14 @@ struct Oracle {
         for (auto& e : m) { Cfk c2; c2.key = e.first; c2.byId = std::move(e.second); cfks.push_back(std::move(c2)); }
     }
 
-    bool in_window(uint32_t i, uint32_t j) const { return cfg.window > 0 && (uint64_t)j + cfg.window >= i; }
+    // rows -> global arrival ranks (a batch that carries earlier batches' kept rows first; nullptr = identity)
+    const uint32_t* gid = nullptr;
+    uint32_t g(uint32_t x) const { return gid ? gid[x] : x; }
+    bool in_window(uint32_t i, uint32_t j) const { return cfg.window > 0 && (uint64_t)g(j) + cfg.window >= g(i); }
     // status of j as seen when i is PreAccepted (SURVEY §8d status model)
     int seen_status(uint32_t i, uint32_t j) const { return in_window(i, j) ? (int)AD_ST_PREACCEPTED : (int)B.st[j]; }
     bool dropped(uint32_t view, uint32_t i, uint32_t j) const {
-        return in_window(i, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, i, j) < cfg.drop_thresh;
+        return in_window(i, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, g(i), g(j)) < cfg.drop_thresh;
     }
     // The query of txn i: its bound (startedBefore) and the arrival position it is answered at.  PreAccept:
     // TxnId_i at position i.  Accept / GetDeps (Accept.calculatePartialDeps :113-116, GetDeps.apply :76 ->
@@ -342,7 +345,7 @@ struct Oracle {
     }
     int seen_status_q(uint32_t q, uint32_t j) const { return in_window(q, j) ? (int)AD_ST_PREACCEPTED : (int)B.st[j]; }
     bool dropped_q(uint32_t view, uint32_t q, uint32_t i, uint32_t j) const {
-        return in_window(q, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, i, j) < cfg.drop_thresh;
+        return in_window(q, j) && cfg.drop_thresh && ad_drop_hash(cfg.seed, view, g(i), g(j)) < cfg.drop_thresh;
     }
 
     // CommandsForKey.mapReduceActive(startedBefore = bound, testKind = kind_i.witnesses()) — CommandsForKey.java:925-983;
@@ -463,25 +466,55 @@ struct Oracle {
         return d;
     }
 
-    // CommandStore.preaccept's maxConflicts.get(keys) (local/CommandStore.java:342) as replica view `view`
+    // CommandStore.preaccept's maxConflicts.get(keysOrRanges) (local/CommandStore.java:342) as replica view `view`
     // holds it when txn i arrives: MaxConflicts.update (local/MaxConflicts.java:56-59) has folded in the
-    // executeAt of every globally visible txn the store holds on each key (CommandStore.updateMaxConflicts
-    // :282-291, SafeCommandStore.updateMaxConflicts :210-222) — the CFK byId entries j < i that are not
-    // TRANSITIVELY_KNOWN/INVALID, in-flight ones unless the view dropped them.  Returns the rank of the
+    // executeAt of every globally visible txn the store holds over its keys or ranges (CommandStore.
+    // updateMaxConflicts :282-291; MaxConflicts is a ReducingRangeMap: a key is a point, get() folds every
+    // interval intersecting the query) — txns j < i that are not TRANSITIVELY_KNOWN/INVALID, in-flight ones
+    // unless the view dropped them: the key txns on i's keys (CFK byId) or on keys inside i's ranges, and the
+    // range txns whose ranges contain one of i's keys / intersect one of i's ranges.  Returns the rank of the
     // greatest executeAt (Timestamp::max, ties to the larger rank) or UINT32_MAX for Timestamp.NONE.
     uint32_t max_conflict(uint32_t i, uint32_t view) {
         uint32_t best = UINT32_MAX;
-        for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
-            Cfk* c = find_cfk(B.keys[p]);
-            if (!c) continue;
-            for (uint32_t j : c->byId) {
+        auto consider = [&](uint32_t j) {
+            int st = seen_status(i, j);
+            if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID) return;
+            if (dropped(view, i, j)) return;
+            int cmp = best == UINT32_MAX ? 1 : ts_cmp(B.ex[j], B.ex[best]);
+            if (cmp > 0 || (cmp == 0 && j > best)) best = j;
+        };
+        auto cfk_prefix = [&](const Cfk& c) {
+            for (uint32_t j : c.byId) {
                 if (j >= i) break;
-                int st = seen_status(i, j);
-                if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID) continue;
-                if (dropped(view, i, j)) continue;
-                int cmp = best == UINT32_MAX ? 1 : ts_cmp(B.ex[j], B.ex[best]);
-                if (cmp > 0 || (cmp == 0 && j > best)) best = j;
+                consider(j);
             }
+        };
+        const bool key_dom = domain_of(B.tx[i]) == AD_DOMAIN_KEY;
+        if (key_dom) {
+            for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
+                Cfk* c = find_cfk(B.keys[p]);
+                if (c) cfk_prefix(*c);
+            }
+        } else {
+            for (uint32_t q = B.range_off[i]; q < B.range_off[i + 1]; ++q) {
+                const RangeK& r = B.ranges[q];
+                auto it = std::upper_bound(cfks.begin(), cfks.end(), r.s, [](uint64_t k, const Cfk& c) { return k < c.key; });
+                for (; it != cfks.end() && it->key <= r.e; ++it) cfk_prefix(*it);
+            }
+        }
+        for (uint32_t j : rangeTxns) {
+            if (j >= i) break;
+            if (!globally_visible(kind_of(B.tx[j]))) continue;
+            bool hit = false;
+            for (uint32_t q = B.range_off[j]; q < B.range_off[j + 1] && !hit; ++q) {
+                const RangeK& r = B.ranges[q];
+                if (key_dom) {
+                    for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1] && !hit; ++p) hit = range_contains(r, B.keys[p]);
+                } else {
+                    for (uint32_t x = B.range_off[i]; x < B.range_off[i + 1] && !hit; ++x) hit = ranges_intersect(r, B.ranges[x]);
+                }
+            }
+            if (hit) consider(j);
         }
         return best;
     }
@@ -654,8 +687,20 @@ oracle_result* oracle_run(const ad_batch* b, const ad_config* c, uint32_t flags,
 /* As oracle_run; view_mask (nullable, [replicas * n]) selects, per txn, the replies the merge folds: the
  * coordinator's fast-path merge takes only the replies whose witnessedAt == TxnId
  * (CoordinateTransaction.onPreAccepted, coordinate/CoordinateTransaction.java:71-101, :75). */
+static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+                                      const uint8_t* view_mask, const uint32_t* gid);
 oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
                                  const uint8_t* view_mask) {
+    return oracle_run_impl(b, c, flags, threads, view_mask, nullptr);
+}
+/* As oracle_run over a batch whose rows carry global arrival ranks gid[n] (the engine's CFK history layout:
+ * kept rows of earlier batches, then the new txns); window and drop decisions use gid.  Single-threaded,
+ * PreAccept bound. */
+oracle_result* oracle_run_gid(const ad_batch* b, const ad_config* c, uint32_t flags, const uint32_t* gid) {
+    return oracle_run_impl(b, c, flags & ~8u, 1, nullptr, gid);
+}
+static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+                                      const uint8_t* view_mask, const uint32_t* gid) {
     oracle_result* res = new oracle_result();
     try {
         Batch B(b);
@@ -669,7 +714,8 @@ oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t
         auto t0 = std::chrono::steady_clock::now();
         if (threads <= 1) {
             for (uint32_t v = 0; v < R; ++v) {
-                Oracle o(B, cfg, flags & 1, (flags & 8) != 0);
+                Oracle o(B, cfg, (flags & 1) && !gid, (flags & 8) != 0);
+                o.gid = gid;
                 for (uint32_t i = 0; i < n; ++i) all[v][i] = o.preaccept(i, v);
             }
         } else {
@@ -771,12 +817,11 @@ oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t
 const char* oracle_error(const oracle_result* r) { return r->error.empty() ? nullptr : r->error.c_str(); }
 
 /* witnessedAt proposal per view (CommandStore.preaccept, local/CommandStore.java:322-347): max_rank[v*n+i] =
- * Oracle::max_conflict, fast[v*n+i] = TxnId_i >= that executeAt (or none) — the fast-path test :343.
- * Key-domain batches only (returns -4 = AD_ERR_UNSUPPORTED with range txns), -1 on invalid input. */
+ * Oracle::max_conflict (key and range footprints), fast[v*n+i] = TxnId_i >= that executeAt (or none) — the
+ * fast-path test :343.  -1 on invalid input. */
 int oracle_max_conflicts(const ad_batch* b, const ad_config* c, uint32_t* max_rank, uint8_t* fast) {
     try {
         Batch B(b);
-        if (B.range_off[B.n] > 0) return AD_ERR_UNSUPPORTED;
         Config cfg;
         cfg.window = c->window; cfg.replicas = c->replicas ? c->replicas : 1; cfg.seed = c->seed;
         cfg.drop_thresh = ad_drop_threshold(c->drop_p);

@@ -32,6 +32,8 @@ def lib():
         L.oracle_run.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_uint32]
         L.oracle_run_masked.restype = C.c_void_p
         L.oracle_run_masked.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_uint32, C.c_void_p]
+        L.oracle_run_gid.restype = C.c_void_p
+        L.oracle_run_gid.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_void_p]
         L.oracle_error.restype = C.c_char_p
         L.oracle_error.argtypes = [C.c_void_p]
         L.oracle_sizes.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrSizes)]
@@ -61,14 +63,18 @@ FLAG_PRUNE, FLAG_MERGE, FLAG_LEVELS, FLAG_ACCEPT = 1, 2, 4, 8
 
 
 class OracleResult:
-    def __init__(self, batch, cfg, flags=FLAG_MERGE | FLAG_LEVELS, threads=1, view_mask=None):
+    def __init__(self, batch, cfg, flags=FLAG_MERGE | FLAG_LEVELS, threads=1, view_mask=None, gid=None):
         """view_mask ([replicas, n] uint8, optional): per txn, the replies the merge folds (the coordinator's
-        fast-path merge: only replies with witnessedAt == TxnId)."""
+        fast-path merge: only replies with witnessedAt == TxnId).  gid ([n] uint32, optional): global arrival rank
+        of every row (a batch carrying earlier batches' kept CFK rows first); window and drops use it."""
         self._b = abi.make_batch(batch)
         self._cfg = cfg
         self.n = batch["n"]
         self.replicas = cfg.replicas
-        if view_mask is None:
+        if gid is not None:
+            self._gid = np.ascontiguousarray(gid, np.uint32)
+            self.h = lib().oracle_run_gid(C.byref(self._b), C.byref(cfg), flags, self._gid.ctypes.data)
+        elif view_mask is None:
             self.h = lib().oracle_run(C.byref(self._b), C.byref(cfg), flags, threads)
         else:
             self._mask = np.ascontiguousarray(view_mask, np.uint8)

@@ -81,16 +81,36 @@ def test_after_merge_and_levels(engine_factory):
     assert np.array_equal(r0, r1) and np.array_equal(f0, f1)
 
 
-def test_rejects_range_batches_and_call_order(engine_factory):
+def test_call_order_and_range_carry_rejected(engine_factory):
     eng = engine_factory()
     b = workload.generate(2000, range_frac=0.1, seed=3)
     eng.load(b)
     with pytest.raises(engine.IllegalStateException):
         eng.max_conflicts()                            # before ad_preaccept_deps
     eng.preaccept_deps()
+    eng.max_conflicts()
     with pytest.raises(engine.AccordDepsError) as e:
-        eng.max_conflicts()
+        eng.max_conflicts_ts()                         # the carried map is per key
     assert e.value.rc == abi.AD_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("n,keyspace,rf,width,window,replicas,drop", [(3000, 3000, 0.2, 200, 16, 3, 0.2),
+                                                                      (20000, 40000, 0.1, 400, 32, 2, 0.1),
+                                                                      (4000, 500, 0.3, 50, 0, 1, 0.0)])
+def test_range_footprints(engine_factory, n, keyspace, rf, width, window, replicas, drop):
+    # MaxConflicts as a ReducingRangeMap: key txns vs range txns covering their keys, range txns vs the keys inside
+    # and the ranges crossing them (k_mc_range_keys / k_mc_range_entries) — vs Oracle::max_conflict
+    b = workload.generate(n, 3, keyspace, "uniform", range_frac=rf, range_width_max=width, slow_frac=0.3, bump_max=40,
+                          seed=n + keyspace)
+    eng = engine_factory(window=window, replicas=replicas, drop_p=drop, seed=0xC0DE)
+    eng.load(b)
+    eng.preaccept_deps()
+    rank, fast = eng.max_conflicts()
+    orank, ofast = O.max_conflicts(b, abi.make_config(window, replicas, drop, 0xC0DE))
+    bad = np.nonzero((rank != orank).any(axis=0) | (fast != ofast).any(axis=0))[0]
+    assert len(bad) == 0, "txns %s: gpu %s oracle %s" % (bad[:6], rank[:, bad[:6]], orank[:, bad[:6]])
+    is_range = (b["txn_lsb"] & np.uint64(1)).astype(bool)
+    assert (rank[:, is_range] != abi.AD_RANK_NONE).any()
 
 
 @pytest.mark.parametrize("name", ["C2", "C3"])

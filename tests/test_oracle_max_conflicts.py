@@ -101,6 +101,20 @@ def _model(b, cfg):
     ex = [ts(b["exec_msb"][i], b["exec_lsb"][i], b["exec_node"][i]) for i in range(n)]
     kind = [(int(b["txn_lsb"][i]) >> 1) & 7 for i in range(n)]
     keys = [set(int(k) for k in b["keys"][b["key_off"][i]:b["key_off"][i + 1]]) for i in range(n)]
+    ranges = [[] for _ in range(n)]
+    if b.get("range_off") is not None:
+        ro = b["range_off"]
+        ranges = [[(int(b["range_start"][q]), int(b["range_end"][q])) for q in range(ro[i], ro[i + 1])] for i in range(n)]
+
+    def overlaps(i, j):
+        # MaxConflicts is a ReducingRangeMap: keys are points, ranges (start, end] intervals
+        if keys[i] & keys[j]:
+            return True
+        if any(s < k <= e for (s, e) in ranges[j] for k in keys[i]):
+            return True
+        if any(s < k <= e for (s, e) in ranges[i] for k in keys[j]):
+            return True
+        return any(not (a1 >= b2 or b1 <= a2) for (a1, b1) in ranges[i] for (a2, b2) in ranges[j])
     thresh = _drop_threshold(cfg.drop_p)
     R_ = cfg.replicas
     rank = np.full((R_, n), NONE, np.uint32)
@@ -111,7 +125,7 @@ def _model(b, cfg):
             for j in range(i):
                 if kind[j] not in (abi.KIND_READ, abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT):
                     continue
-                if not (keys[i] & keys[j]):
+                if not overlaps(i, j):
                     continue
                 in_flight = cfg.window > 0 and j + cfg.window >= i
                 if in_flight:
@@ -135,6 +149,19 @@ def test_oracle_equals_independent_model():
         mr, mf = _model(b, cfg)
         assert np.array_equal(rank, mr) and np.array_equal(fast, mf)
         assert fast.min() == 0 and (rank != NONE).any()     # both outcomes exercised
+
+
+def test_oracle_equals_independent_model_with_ranges():
+    # range footprints: key txns vs range txns covering their keys, range txns vs keys inside / ranges crossing
+    for seed in (6, 7):
+        b = workload.generate(300, keys_per_txn=2, keyspace=400, range_frac=0.25, range_width_max=60, seed=seed,
+                              slow_frac=0.3, bump_max=40)
+        cfg = abi.make_config(8, 2, 0.3, 0xBEEF + seed)
+        rank, fast = O.max_conflicts(b, cfg)
+        mr, mf = _model(b, cfg)
+        assert np.array_equal(rank, mr) and np.array_equal(fast, mf)
+        is_range = (b["txn_lsb"] & np.uint64(1)).astype(bool)
+        assert (rank[:, is_range] != NONE).any() and fast.min() == 0
 
 
 def test_reduce_witnessed_across_stores():
