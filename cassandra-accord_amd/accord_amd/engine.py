@@ -79,6 +79,9 @@ def lib():
         L.ad_merge_deps_fast.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_max_conflicts_ts.argtypes = [vp, vp, vp, vp, vp]
         L.ad_max_conflicts_export.argtypes = [vp, C.POINTER(C.c_size_t), vp, vp, vp, vp]
+        L.ad_recover.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.ad_fetch_recovery.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp]
+        L.ad_fetch_recovery_flags.argtypes = [vp, vp]
         _LIB = L
     return _LIB
 
@@ -91,7 +94,8 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_alltoall", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
             "ad_shard_levels_allreduce", "ad_shard_order", "ad_shard_set_holders", "ad_shard_levels_deltas",
-            "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows")
+            "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows",
+            "ad_recover", "ad_fetch_recovery", "ad_fetch_recovery_flags")
 
 
 class DepsEngine:
@@ -161,6 +165,34 @@ class DepsEngine:
 
     def cfk_reset(self):
         self._check(lib().ad_cfk_reset(self.h), "ad_cfk_reset")
+
+    def recover(self, rows):
+        """BeginRecovery's store queries for the recovering rows (ad_recover, after a merge on this batch) ->
+        (out, reject): out[which][cls] = (off [nq+1], keys [E] or [E, 2], txns [E]) — which 0 =
+        earlierCommittedWitness, 1 = earlierAcceptedNoWitness, each Deps as its entries in Deps order (the
+        Deps.Builder stream; wire.relations_to_csr / KeyDeps.Builder build the SerializerSupport arrays);
+        reject [nq] uint8 = rejectsFastPath."""
+        rows = np.ascontiguousarray(rows, np.uint32)
+        nq = len(rows)
+        ent = (C.c_size_t * 6)()
+        self._check(lib().ad_recover(self.h, rows.ctypes.data, nq, ent), "ad_recover")
+        out = []
+        for w in range(2):
+            cl = []
+            for c in range(abi.NUM_CLASSES):
+                e = ent[w * 3 + c]
+                kw = 2 if c == abi.CLASS_RANGE else 1
+                off = np.zeros(nq + 1, np.uint32)
+                keys = np.zeros(max(e * kw, 1), np.uint64)
+                txns = np.zeros(max(e, 1), np.uint32)
+                self._check(lib().ad_fetch_recovery(self.h, w, c, off.ctypes.data, keys.ctypes.data, txns.ctypes.data),
+                            "ad_fetch_recovery")
+                keys = keys[:e * kw].reshape(-1, 2) if kw == 2 else keys[:e]
+                cl.append((off, keys, txns[:e]))
+            out.append(cl)
+        rej = np.zeros(max(nq, 1), np.uint8)
+        self._check(lib().ad_fetch_recovery_flags(self.h, rej.ctypes.data), "ad_fetch_recovery_flags")
+        return out, rej[:nq]
 
     def cfk_rows(self):
         """(history rows H, gid[n]: global arrival rank of every row of the loaded batch)."""

@@ -22,6 +22,7 @@
 #include "conflict_kernels.h"
 #include "level_kernels.h"
 #include "history_kernels.h"
+#include "recovery_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
 #include "shard_kernels.h"
@@ -138,6 +139,13 @@ struct ad_handle {
     bool hist_active = false;        // the loaded batch's rows [0, hist_rows) are history; gid = global ranks
     size_t hist_rows = 0;
     uint32_t* qpos = nullptr;        // [n] arrival position of each txn's executeAt (accept bound)
+    // BeginRecovery queries (recovery_kernels.h): outputs of the last ad_recover
+    size_t rc_nq = 0;
+    bool rc_ready = false;
+    uint32_t* rc_off = nullptr;      // [RC_OUT][nq + 1]
+    uint8_t* rc_rej = nullptr;
+    uint64_t* rc_keys[RC_OUT] = {};
+    uint32_t* rc_txn[RC_OUT] = {};
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -220,7 +228,8 @@ enum Slot : size_t {
     S_MCOM, S_MCOL, S_MCON, S_MCOF, S_MCSK, S_MCSM, S_MCSL, S_MCSN, S_MCSU, S_MCSP,
     S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
     S_HTM, S_HTL, S_HTN, S_HEM, S_HEL, S_HEN, S_HST, S_HKOFF, S_HKEYS, S_HGIDS, S_HSEGM, S_HKEEP, S_HROWS2, S_HCNT,
-    S_NUM_FIXED,
+    S_RCROWS, S_RCCNT, S_RCOFF, S_RCREJ, S_RCK0, S_RCT0 = S_RCK0 + RC_OUT, S_RCEND = S_RCT0 + RC_OUT,
+    S_NUM_FIXED = S_RCEND,
     S_CSR0 = 160
 };
 static_assert(S_NUM_FIXED <= S_CSR0, "fixed device slots overlap the CSR slot blocks");
@@ -1068,6 +1077,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     h->have_deps = h->have_merged = h->have_levels = false;
     h->mc_ready = false;
     h->mc_fast = nullptr;
+    h->rc_ready = false;
     h->hist_active = hist;
     h->hist_rows = H;
     h->hist_valid = false;           // consumed: ad_cfk_retain on this batch carries the state on
@@ -1336,6 +1346,100 @@ int ad_max_conflicts_export(ad_handle* h, size_t* m_out, uint64_t* keys, uint64_
         if (node) HIPCHK(h, hipMemcpyAsync(node, on_, count * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(h, hipStreamSynchronize(st));
+    return AD_OK;
+}
+
+// BeginRecovery's store queries (recovery_kernels.h) for nq recovering rows, over the merged Deps on the handle:
+// count pass, one scan for the six outputs' offsets, fill pass.  The outputs stay on the device for
+// ad_fetch_recovery / ad_fetch_recovery_flags.
+int ad_recover(ad_handle* h, const uint32_t* rows, size_t nq, size_t* entries) {
+    if (!h || (nq && !rows)) return AD_ERR_ARGUMENT;
+    if (!h->have_deps || !h->have_merged)
+        return set_err(h, AD_ERR_STATE, "ad_recover needs the batch's deps and merged Deps (ad_merge_deps / _fast / ad_merge_host)");
+    if (h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_recover: not in sharded mode");
+    for (size_t q = 0; q < nq; ++q)
+        if (rows[q] >= h->n) return set_err(h, AD_ERR_ARGUMENT, "ad_recover: row " + std::to_string(rows[q]) + " out of range");
+    hipSetDevice(h->device);
+    g_tracer = &h->tracer;
+    hipStream_t st = h->st;
+    h->rc_ready = false;
+    uint32_t *drows = nullptr, *cnt = nullptr, *off = nullptr;
+    CK(dalloc(h, S_RCROWS, &drows, std::max<size_t>(nq, 1)));
+    CK(dalloc(h, S_RCCNT, &cnt, std::max<size_t>(RC_OUT * nq, 1)));
+    CK(dalloc(h, S_RCOFF, &off, RC_OUT * (nq + 1)));
+    CK(dalloc(h, S_RCREJ, &h->rc_rej, std::max<size_t>(nq, 1)));
+    h->rc_off = off;
+    h->rc_nq = nq;
+    RecoverArgs a{};
+    a.nq = nq; a.rows = drows;
+    a.meta = h->meta; a.tx_ts = h->tx_ts; a.ex1 = h->ex1; a.key_off = h->key_off; a.keys = h->keys;
+    a.range_off = h->range_off; a.rs = h->range_s; a.re = h->range_e;
+    a.ukey = h->ukey; a.useg = h->useg; a.U = h->P ? h->hprm.n_keys_u : 0;
+    a.e_txn = h->e_txn; a.e_meta = h->e_meta; a.e_exec1 = h->e_exec1; a.sval = h->sval;
+    a.Q = h->Q; a.es = h->es; a.ee = h->ee; a.eown = h->eown; a.wmax = h->wmax;
+    const int ncls = (h->Q > 0 && h->merged_has_range) ? 3 : 2;
+    for (int c = 0; c < ncls; ++c) {
+        const Csr& m = h->merged[c];
+        a.m_key_off[c] = m.key_off; a.m_keys[c] = m.keys; a.m_k2t_off[c] = m.k2t_off; a.m_k2t[c] = m.k2t;
+        a.m_ent_off[c] = m.ent_off; a.m_tcnt[c] = m.tcnt; a.m_txns[c] = m.txns;
+    }
+    a.cnt = cnt; a.off = off; a.reject = h->rc_rej;
+    std::array<uint32_t, RC_OUT> tot{};
+    if (nq) {
+        HIPCHK(h, hipMemcpyAsync(drows, rows, nq * 4, hipMemcpyHostToDevice, st));
+        const int grid = ceil_div((long)nq * WAVE, 256);
+        KScope ks(K_RECOVER, nq);
+        k_recover<false><<<grid, 256, 0, st>>>(a);
+        CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<RecoverOffsetsOp>(nq))));
+        device_scan(RecoverOffsetsOp{cnt, off, nq}, nq, (RecoverOffsetsOp::S*)h->scratch, st);
+        for (int o = 0; o < RC_OUT; ++o)
+            HIPCHK(h, hipMemcpyAsync(&tot[o], off + (size_t)o * (nq + 1) + nq, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        for (int o = 0; o < RC_OUT; ++o) {
+            const int kw = o % 3 == AD_CLASS_RANGE ? 2 : 1;
+            CK(dalloc(h, S_RCK0 + o, &h->rc_keys[o], std::max<size_t>((size_t)tot[o] * kw, 1)));
+            CK(dalloc(h, S_RCT0 + o, &h->rc_txn[o], std::max<size_t>(tot[o], 1)));
+            a.okeys[o] = h->rc_keys[o]; a.otxn[o] = h->rc_txn[o];
+        }
+        k_recover<true><<<grid, 256, 0, st>>>(a);
+        HIPCHK(h, hipGetLastError());
+    } else {
+        HIPCHK(h, hipMemsetAsync(off, 0, RC_OUT * 4, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    h->tracer.resolve();
+    if (entries)
+        for (int o = 0; o < RC_OUT; ++o) entries[o] = tot[o];
+    h->rc_ready = true;
+    return AD_OK;
+}
+
+int ad_fetch_recovery(ad_handle* h, uint32_t which, uint32_t cls, uint32_t* off, uint64_t* keys, uint32_t* txns) {
+    if (!h || which > 1 || cls >= AD_NUM_CLASSES) return AD_ERR_ARGUMENT;
+    if (!h->rc_ready) return set_err(h, AD_ERR_STATE, "no ad_recover result for this batch");
+    hipSetDevice(h->device);
+    const int o = (int)(which * 3 + cls);
+    const size_t nq = h->rc_nq;
+    hipStream_t st = h->st;
+    uint32_t total = 0;
+    HIPCHK(h, hipMemcpyAsync(&total, h->rc_off + (size_t)o * (nq + 1) + nq, 4, hipMemcpyDeviceToHost, st));
+    if (off) HIPCHK(h, hipMemcpyAsync(off, h->rc_off + (size_t)o * (nq + 1), (nq + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    const int kw = cls == AD_CLASS_RANGE ? 2 : 1;
+    if (total && keys) HIPCHK(h, hipMemcpyAsync(keys, h->rc_keys[o], (size_t)total * kw * 8, hipMemcpyDeviceToHost, st));
+    if (total && txns) HIPCHK(h, hipMemcpyAsync(txns, h->rc_txn[o], (size_t)total * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    return AD_OK;
+}
+
+int ad_fetch_recovery_flags(ad_handle* h, uint8_t* reject_fast_path) {
+    if (!h) return AD_ERR_ARGUMENT;
+    if (!h->rc_ready) return set_err(h, AD_ERR_STATE, "no ad_recover result for this batch");
+    hipSetDevice(h->device);
+    if (h->rc_nq && reject_fast_path) {
+        HIPCHK(h, hipMemcpyAsync(reject_fast_path, h->rc_rej, h->rc_nq, hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipStreamSynchronize(h->st));
+    }
     return AD_OK;
 }
 

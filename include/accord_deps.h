@@ -292,6 +292,28 @@ int  ad_reset_kernel_stats(ad_handle* h);
 int  ad_kernel_units(ad_handle* h, int kid, uint64_t* units);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Recovery — BeginRecovery's store queries (messages/BeginRecovery.java:126-145) for the   */
+/* recovering txns rows[nq] of the loaded batch, each a SafeCommandStore.mapReduceFull over its footprint     */
+/* (CommandsForKey.mapReduceFull local/cfk/CommandsForKey.java:824-923 per key, mapReduceRangesInternal        */
+/* impl/InMemoryCommandStore.java:884-1017 over the range commands):                                         */
+/*   which 0  earlierCommittedWitness  = stableStartedBeforeAndWitnessed :344-352                              */
+/*   which 1  earlierAcceptedNoWitness = acceptedOrCommittedStartedBeforeWithoutWitnessing :329-342            */
+/*   flags    rejectsFastPath = hasAcceptedOrCommittedStartedAfterWithoutWitnessing :354-367                   */
+/*                              || hasStableExecutesAfterWithoutWitnessing :369-380                            */
+/* The store is the loaded batch with its statuses and executeAts (every txn known, nothing pruned); each      */
+/* txn's Deps are the merged Deps on the handle (ad_merge_deps / _fast / ad_merge_host: what it was accepted   */
+/* or committed with); a CFK entry's missing() follows the CommandsForKey invariant (Updating.java:194-287,    */
+/* :340-352).  Rows already PreCommitted (status >= COMMITTED) answer Deps.NONE and false (:126-130).         */
+/* entries[which * 3 + class] receives the entry counts.  ad_fetch_recovery returns one (Deps, class) as the   */
+/* built Deps flattened to its (key or range, TxnId rank) entries in Deps order: off[nq + 1] per recovering    */
+/* txn, keys[entries] (range class: [2 * entries] start, end), txns[entries]; any pointer may be NULL.        */
+/* Not in sharded mode.                                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+int  ad_recover(ad_handle* h, const uint32_t* rows, size_t nq, size_t* entries /* [6], or NULL */);
+int  ad_fetch_recovery(ad_handle* h, uint32_t which, uint32_t cls, uint32_t* off, uint64_t* keys, uint32_t* txns);
+int  ad_fetch_recovery_flags(ad_handle* h, uint8_t* reject_fast_path /* [nq] */);
+
+/* ------------------------------------------------------------------------------------------ */
 /* CommandsForKey state across batches.  A store's batches continue one TxnId order; instead  */
 /* of a closed world per batch, ad_cfk_retain (after ad_preaccept_deps on a batch) keeps on the device every txn */
 /* whose CFK entries a later query can still see — in flight for a later query (global rank >= next - W), or on  */

@@ -988,3 +988,276 @@ int oracle_union(const uint64_t* lk, size_t nlk, const uint32_t* lv, size_t nlv,
 }
 
 }  // extern "C"
+
+/* ---------------------------------------------------------------------------------------------- */
+/* BeginRecovery's store queries                                                */
+/*                                                                                                 */
+/*   BeginRecovery.apply .............................. messages/BeginRecovery.java:126-145         */
+/*   acceptedOrCommittedStartedBeforeWithoutWitnessing  :329-342  (STARTED_BEFORE, WITHOUT, IS_PROPOSED) */
+/*   stableStartedBeforeAndWitnessed .................. :344-352  (STARTED_BEFORE, WITH, IS_STABLE)   */
+/*   hasAcceptedOrCommittedStartedAfterWithout... ..... :354-367  (STARTED_AFTER, WITHOUT, IS_PROPOSED) */
+/*   hasStableExecutesAfterWithoutWitnessing .......... :369-380  (ANY, WITHOUT, IS_STABLE)           */
+/*   CommandsForKey.mapReduceFull ..................... local/cfk/CommandsForKey.java:824-923        */
+/*   InMemorySafeStore.mapReduceFull / RangesInternal . impl/InMemoryCommandStore.java:875-1017     */
+/*   TxnInfo.missing (the CFK invariant) .............. Updating.computeInfoAndAdditions :194-287,   */
+/*                                                      Updating.java:340-352 (remove/addToMissingArrays) */
+/*                                                                                                 */
+/* The store: every txn of the batch with its status and executeAt; each txn's deps = `merged` (the */
+/* Deps it was accepted / committed with); nothing pruned (prunedBefore = none).  A managed txn j's   */
+/* missing() on key k holds the TxnIds t of byId_k with t < depsKnownBefore(j) (executeAt when       */
+/* COMMITTED/STABLE/APPLIED, else TxnId, InternalStatus.depsKnownBefore :561-580), t != j, witnessed */
+/* by j's kind, not yet COMMITTED (committed / invalidated txns leave every missing array), and not */
+/* in j's Deps.txnIds(k) (Deps.java:188-203: keyDeps, covering rangeDeps, directKeyDeps).            */
+/* ---------------------------------------------------------------------------------------------- */
+namespace {
+
+struct DepsIn {
+    const ad_csr_in* c;      // [3]
+    bool key_list_has(int cls, uint32_t j, uint64_t key, uint32_t t) const {   // t in class cls's txnIds(key) of j
+        const ad_csr_in& x = c[cls];
+        const uint32_t kb = x.key_off[j], ke = x.key_off[j + 1];
+        const uint64_t* it = std::lower_bound(x.keys + kb, x.keys + ke, key);
+        if (it == x.keys + ke || *it != key) return false;
+        return list_has(x, j, (uint32_t)(it - (x.keys + kb)), t);
+    }
+    static bool list_has(const ad_csr_in& x, uint32_t j, uint32_t ki, uint32_t t) {
+        const uint32_t nk = x.key_off[j + 1] - x.key_off[j];
+        const int32_t* m = x.k2t + x.k2t_off[j];
+        const uint32_t* v = x.txns + x.txn_off[j];
+        for (int32_t p = ki == 0 ? (int32_t)nk : m[ki - 1]; p < m[ki]; ++p)
+            if (v[m[p]] == t) return true;
+        return false;
+    }
+    // Deps.txnIds(key) contains t (Deps.java:188-203)
+    bool txn_ids_has(uint32_t j, uint64_t key, uint32_t t) const {
+        if (key_list_has(AD_CLASS_KEY, j, key, t) || key_list_has(AD_CLASS_DIRECT_KEY, j, key, t)) return true;
+        const ad_csr_in& r = c[AD_CLASS_RANGE];
+        if (!r.key_off) return false;
+        for (uint32_t q = r.key_off[j]; q < r.key_off[j + 1]; ++q)
+            if (range_contains(RangeK{r.keys[2 * q], r.keys[2 * q + 1]}, key) && list_has(r, j, q - r.key_off[j], t)) return true;
+        return false;
+    }
+    // Deps.intersects(txnId, ranges) (Deps.java:176-186, KeyDeps.java:278-300, RangeDeps.java:507-534)
+    bool intersects(uint32_t j, const Ts& tid, uint32_t t, const std::vector<RangeK>& ranges) const {
+        const int cls = domain_of(tid) == AD_DOMAIN_RANGE ? AD_CLASS_RANGE : manages_execution(tid) ? AD_CLASS_KEY : AD_CLASS_DIRECT_KEY;
+        const ad_csr_in& x = c[cls];
+        if (!x.key_off) return false;
+        const uint32_t kb = x.key_off[j], ke = x.key_off[j + 1];
+        for (uint32_t q = kb; q < ke; ++q) {
+            if (!list_has(x, j, q - kb, t)) continue;
+            for (const RangeK& r : ranges) {
+                if (cls == AD_CLASS_RANGE ? ranges_intersect(RangeK{x.keys[2 * q], x.keys[2 * q + 1]}, r) : range_contains(r, x.keys[q]))
+                    return true;
+            }
+        }
+        return false;
+    }
+};
+
+enum TestStartedAt { STARTED_BEFORE, STARTED_AFTER, ANY };
+enum TestDep { WITH, WITHOUT, ANY_DEPS };
+enum TestStatus { IS_PROPOSED, IS_STABLE, ANY_STATUS };
+
+struct Recovery {
+    const Batch& B;
+    const Oracle& O;
+    DepsIn deps;
+
+    static bool has_execute_at_or_deps(int st) { return st == AD_ST_ACCEPTED || st == AD_ST_COMMITTED || st == AD_ST_STABLE || st == AD_ST_APPLIED; }
+
+    bool missing_has(uint32_t j, uint64_t key, uint32_t t) const {       // TxnInfo.missing() of j on key contains t
+        const int sj = B.st[j];
+        if (!has_execute_at_or_deps(sj) || t == j) return false;
+        const Ts& dkb = (sj >= AD_ST_COMMITTED) ? B.ex[j] : B.tx[j];
+        if (ts_cmp(B.tx[t], dkb) >= 0) return false;
+        if (!witnesses(kind_of(B.tx[j]), kind_of(B.tx[t]))) return false;
+        if (B.st[t] >= AD_ST_COMMITTED) return false;
+        return !deps.txn_ids_has(j, key, t);
+    }
+
+    // CommandsForKey.mapReduceFull (CommandsForKey.java:824-923); fn(j) per visited entry
+    template <class F>
+    void cfk_full(const Cfk& c, uint32_t t, TestStartedAt sa, TestDep td, TestStatus ts, F fn) const {
+        const Ts& tid = B.tx[t];
+        auto it = std::lower_bound(c.byId.begin(), c.byId.end(), t);
+        const bool known = it != c.byId.end() && *it == t;
+        const size_t insertPos = (size_t)(it - c.byId.begin());
+        // loadingFor: known -> null; unknown -> NO_TXNIDS (nothing is pruned: WITH returns the initial value)
+        if (!known && td == WITH) return;
+        size_t start = 0, end = c.byId.size();
+        if (sa == STARTED_BEFORE) end = insertPos;
+        else if (sa == STARTED_AFTER) start = known ? insertPos + 1 : insertPos;   // byId order: known t sits at insertPos
+        for (size_t i = start; i < end; ++i) {
+            const uint32_t j = c.byId[i];
+            if (sa == STARTED_AFTER && j == t) continue;
+            if (!witnesses(kind_of(B.tx[j]), kind_of(tid))) continue;      // testKind = kind.witnessedBy()
+            const int st = B.st[j];
+            if (ts == IS_PROPOSED && !(st == AD_ST_ACCEPTED || st == AD_ST_COMMITTED)) continue;
+            if (ts == IS_STABLE && !(st == AD_ST_STABLE || st == AD_ST_APPLIED)) continue;
+            if (ts == ANY_STATUS && st == AD_ST_TRANSITIVELY_KNOWN) continue;
+            if (td != ANY_DEPS) {
+                if (!has_execute_at_or_deps(st)) continue;
+                if (ts_cmp(B.ex[j], tid) <= 0) continue;
+                const bool hasAsDep = known ? !missing_has(j, c.key, t) : false;
+                if (hasAsDep != (td == WITH)) continue;
+            }
+            fn(c.key, j);
+        }
+    }
+
+    // the store's CFKs the footprint of t visits (mapReduceForKey: its keys, or every CFK key in its ranges)
+    template <class F>
+    void for_cfks(uint32_t t, F fn) const {
+        if (domain_of(B.tx[t]) == AD_DOMAIN_KEY) {
+            for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
+                auto it = std::lower_bound(O.cfks.begin(), O.cfks.end(), B.keys[p], [](const Cfk& c, uint64_t k) { return c.key < k; });
+                if (it != O.cfks.end() && it->key == B.keys[p]) fn(*it);
+            }
+        } else {
+            for (const Cfk& c : O.cfks) {
+                bool in = false;
+                for (uint32_t q = B.range_off[t]; q < B.range_off[t + 1] && !in; ++q) in = range_contains(B.ranges[q], c.key);
+                if (in) fn(c);
+            }
+        }
+    }
+
+    // mapReduceRangesInternal (InMemoryCommandStore.java:884-1017) over the range commands
+    template <class F>
+    void ranges_full(uint32_t t, TestStartedAt sa, TestDep td, TestStatus ts, F fn) const {
+        const Ts& tid = B.tx[t];
+        const bool key_dom = domain_of(tid) == AD_DOMAIN_KEY;
+        for (uint32_t j : O.rangeTxns) {
+            if (sa == STARTED_AFTER && ts_cmp(B.tx[j], tid) <= 0) continue;
+            if (sa == STARTED_BEFORE && ts_cmp(B.tx[j], tid) >= 0) continue;
+            if (sa != STARTED_AFTER && td != ANY_DEPS && ts_cmp(B.ex[j], tid) < 0) continue;
+            const int st = B.st[j];
+            if (ts == IS_PROPOSED && !(st == AD_ST_ACCEPTED || st == AD_ST_COMMITTED)) continue;
+            if (ts == IS_STABLE && !(st == AD_ST_STABLE || st == AD_ST_APPLIED)) continue;
+            if (!witnesses(kind_of(B.tx[j]), kind_of(tid))) continue;
+            std::vector<RangeK> jr(B.ranges.begin() + B.range_off[j], B.ranges.begin() + B.range_off[j + 1]);
+            if (td != ANY_DEPS) {
+                if (!has_execute_at_or_deps(st)) continue;
+                if ((td == WITH) == !deps.intersects(j, tid, t, jr)) continue;
+            }
+            for (const RangeK& r : jr) {        // Routables.foldl(rangeCommand.ranges, sliced): ranges meeting t's footprint
+                bool hit = false;
+                if (key_dom) for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1] && !hit; ++p) hit = range_contains(r, B.keys[p]);
+                else for (uint32_t q = B.range_off[t]; q < B.range_off[t + 1] && !hit; ++q) hit = ranges_intersect(r, B.ranges[q]);
+                if (hit) fn(r, j);
+            }
+        }
+    }
+};
+
+struct RecoveryDeps {             // Deps.Builder: key, direct, range builders (Deps.java:80-106)
+    Builder<uint64_t> key, direct;
+    Builder<RangeK> range;
+};
+
+}  // namespace
+
+struct oracle_recovery {
+    std::vector<uint32_t> off[2][3];
+    std::vector<uint64_t> keys[2][3];
+    std::vector<uint32_t> txns[2][3];
+    std::vector<uint8_t> reject;
+    std::string error;
+};
+
+extern "C" {
+
+/* rows[nq]: the recovering txns (batch rows).  merged[3]: each txn's Deps (ad_csr_in per class; range may have
+ * NULL arrays for key batches).  Outputs per which (0 = earlierCommittedWitness, 1 = earlierAcceptedNoWitness)
+ * and class: the built Deps flattened to its (key or range, TxnId) entries in Deps order; reject[q] =
+ * rejectsFastPath.  Txns already PreCommitted (status COMMITTED / STABLE / APPLIED / INVALID) answer
+ * Deps.NONE and false (:126-130). */
+oracle_recovery* oracle_recover(const ad_batch* b, const ad_csr_in* merged, const uint32_t* rows, size_t nq) {
+    oracle_recovery* res = new oracle_recovery();
+    try {
+        Batch B(b);
+        Config cfg;
+        cfg.window = 0; cfg.replicas = 1;
+        Oracle O(B, cfg, false);
+        Recovery R{B, O, DepsIn{merged}};
+        for (int w = 0; w < 2; ++w)
+            for (int c = 0; c < 3; ++c) res->off[w][c].assign(1, 0);
+        res->reject.assign(nq, 0);
+        for (size_t q = 0; q < nq; ++q) {
+            const uint32_t t = rows[q];
+            if (t >= B.n) throw std::invalid_argument("recovery row out of range");
+            RecoveryDeps out[2];
+            if (B.st[t] < AD_ST_COMMITTED) {
+                bool reject = false;
+                auto any = [&](uint64_t, uint32_t) { reject = true; };
+                auto anyr = [&](const RangeK&, uint32_t) { reject = true; };
+                R.for_cfks(t, [&](const Cfk& c) { R.cfk_full(c, t, STARTED_AFTER, WITHOUT, IS_PROPOSED, any); });
+                R.ranges_full(t, STARTED_AFTER, WITHOUT, IS_PROPOSED, anyr);
+                if (!reject) {
+                    R.for_cfks(t, [&](const Cfk& c) { R.cfk_full(c, t, ANY, WITHOUT, IS_STABLE, any); });
+                    R.ranges_full(t, ANY, WITHOUT, IS_STABLE, anyr);
+                }
+                res->reject[q] = reject ? 1 : 0;
+                auto add_key = [&](RecoveryDeps& d, uint64_t k, uint32_t j) {
+                    if (manages_execution(B.tx[j])) d.key.add(k, j); else d.direct.add(k, j);
+                };
+                // stableStartedBeforeAndWitnessed
+                R.for_cfks(t, [&](const Cfk& c) { R.cfk_full(c, t, STARTED_BEFORE, WITH, IS_STABLE,
+                                                             [&](uint64_t k, uint32_t j) { add_key(out[0], k, j); }); });
+                R.ranges_full(t, STARTED_BEFORE, WITH, IS_STABLE, [&](const RangeK& r, uint32_t j) { out[0].range.add(r, j); });
+                // acceptedOrCommittedStartedBeforeWithoutWitnessing (the map adds only executeAt > startedBefore)
+                R.for_cfks(t, [&](const Cfk& c) { R.cfk_full(c, t, STARTED_BEFORE, WITHOUT, IS_PROPOSED, [&](uint64_t k, uint32_t j) {
+                    if (ts_cmp(B.ex[j], B.tx[t]) > 0) add_key(out[1], k, j); }); });
+                R.ranges_full(t, STARTED_BEFORE, WITHOUT, IS_PROPOSED, [&](const RangeK& r, uint32_t j) {
+                    if (ts_cmp(B.ex[j], B.tx[t]) > 0) out[1].range.add(r, j); });
+            }
+            for (int w = 0; w < 2; ++w) {
+                auto flat_key = [&](Csr<uint64_t> c, int cls) {
+                    for (size_t k = 0; k < c.keys.size(); ++k)
+                        for (int32_t p = k == 0 ? (int32_t)c.keys.size() : c.k2t[k - 1]; p < c.k2t[k]; ++p) {
+                            res->keys[w][cls].push_back(c.keys[k]);
+                            res->txns[w][cls].push_back(c.vals[c.k2t[p]]);
+                        }
+                    res->off[w][cls].push_back((uint32_t)res->txns[w][cls].size());
+                };
+                flat_key(out[w].key.build(), AD_CLASS_KEY);
+                flat_key(out[w].direct.build(), AD_CLASS_DIRECT_KEY);
+                Csr<RangeK> rc = out[w].range.build();
+                for (size_t k = 0; k < rc.keys.size(); ++k)
+                    for (int32_t p = k == 0 ? (int32_t)rc.keys.size() : rc.k2t[k - 1]; p < rc.k2t[k]; ++p) {
+                        res->keys[w][AD_CLASS_RANGE].push_back(rc.keys[k].s);
+                        res->keys[w][AD_CLASS_RANGE].push_back(rc.keys[k].e);
+                        res->txns[w][AD_CLASS_RANGE].push_back(rc.vals[rc.k2t[p]]);
+                    }
+                res->off[w][AD_CLASS_RANGE].push_back((uint32_t)res->txns[w][AD_CLASS_RANGE].size());
+            }
+        }
+    } catch (const std::exception& e) {
+        res->error = e.what();
+    }
+    return res;
+}
+
+const char* oracle_recovery_error(const oracle_recovery* r) { return r->error.empty() ? nullptr : r->error.c_str(); }
+
+size_t oracle_recovery_entries(const oracle_recovery* r, uint32_t which, uint32_t cls) {
+    return which < 2 && cls < 3 ? r->txns[which][cls].size() : 0;
+}
+
+int oracle_recovery_fetch(const oracle_recovery* r, uint32_t which, uint32_t cls, uint32_t* off, uint64_t* keys, uint32_t* txns) {
+    if (which >= 2 || cls >= 3) return AD_ERR_ARGUMENT;
+    auto cp = [](void* dst, const void* src, size_t bytes) { if (bytes) std::memcpy(dst, src, bytes); };
+    cp(off, r->off[which][cls].data(), r->off[which][cls].size() * 4);
+    cp(keys, r->keys[which][cls].data(), r->keys[which][cls].size() * 8);
+    cp(txns, r->txns[which][cls].data(), r->txns[which][cls].size() * 4);
+    return AD_OK;
+}
+
+int oracle_recovery_flags(const oracle_recovery* r, uint8_t* reject) {
+    if (!r->reject.empty()) std::memcpy(reject, r->reject.data(), r->reject.size());
+    return AD_OK;
+}
+
+void oracle_recovery_free(oracle_recovery* r) { delete r; }
+
+}  // extern "C"

@@ -55,6 +55,15 @@ def lib():
         L.oracle_union.argtypes = [u64p, C.c_size_t, u32p, C.c_size_t, i32p, C.c_size_t,
                                    u64p, C.c_size_t, u32p, C.c_size_t, i32p, C.c_size_t,
                                    u64p, szp, u32p, szp, i32p, szp]
+        L.oracle_recover.restype = C.c_void_p
+        L.oracle_recover.argtypes = [C.POINTER(abi.AdBatch), C.c_void_p, C.c_void_p, C.c_size_t]
+        L.oracle_recovery_error.restype = C.c_char_p
+        L.oracle_recovery_error.argtypes = [C.c_void_p]
+        L.oracle_recovery_entries.restype = C.c_size_t
+        L.oracle_recovery_entries.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.oracle_recovery_fetch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, vp, vp, vp]
+        L.oracle_recovery_flags.argtypes = [C.c_void_p, vp]
+        L.oracle_recovery_free.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -216,3 +225,38 @@ def union_relation(left, right):
 
 
 EMPTY_RELATION = (np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int32))
+
+
+def recover(batch, merged, rows):
+    """BeginRecovery's store queries (oracle.cpp oracle_recover) for the recovering rows, over the batch whose txns hold
+    the Deps `merged` ([key, direct, range] abi.Csr) -> (out, reject): out[which][cls] = (off [nq+1], keys [E] or
+    [E, 2], txns [E]) with which 0 = earlierCommittedWitness, 1 = earlierAcceptedNoWitness; reject [nq] uint8 =
+    rejectsFastPath."""
+    b = abi.make_batch(batch)
+    rows = np.ascontiguousarray(rows, np.uint32)
+    parts = (abi.AdCsrIn * 3)()
+    for c in range(3):
+        parts[c] = merged[c].as_in()
+    h = lib().oracle_recover(C.byref(b), C.cast(parts, C.c_void_p), rows.ctypes.data, len(rows))
+    try:
+        err = lib().oracle_recovery_error(h)
+        if err:
+            raise ValueError(err.decode())
+        out = []
+        for w in range(2):
+            cl = []
+            for c in range(3):
+                e = lib().oracle_recovery_entries(h, w, c)
+                w2 = 2 if c == abi.CLASS_RANGE else 1
+                off = np.zeros(len(rows) + 1, np.uint32)
+                keys = np.zeros(max(e * w2, 1), np.uint64)
+                txns = np.zeros(max(e, 1), np.uint32)
+                lib().oracle_recovery_fetch(h, w, c, off.ctypes.data, keys.ctypes.data, txns.ctypes.data)
+                keys = keys[:e * w2].reshape(-1, 2) if w2 == 2 else keys[:e]
+                cl.append((off, keys.copy(), txns[:e].copy()))
+            out.append(cl)
+        rej = np.zeros(max(len(rows), 1), np.uint8)
+        lib().oracle_recovery_flags(h, rej.ctypes.data)
+        return out, rej[:len(rows)].copy()
+    finally:
+        lib().oracle_recovery_free(h)
