@@ -20,6 +20,7 @@
 //                        intersecting one of its ranges (the windowed join of k_range_deps), one wave per txn
 #pragma once
 #include "deps_kernels.h"
+#include "range_kernels.h"
 #include "union_kernels.h"
 
 namespace ad {
@@ -153,7 +154,7 @@ struct McRangeArgs {
     const uint64_t* es;
     const uint64_t* ee;
     const uint32_t* eown;
-    uint64_t wmax;
+    RangeIndex ix;
     uint32_t window, thresh;
     uint64_t seed;
     uint32_t* max_rank;        // [v * n + t] folded in place (batch rows: range batches are not sharded)
@@ -238,33 +239,29 @@ __global__ __launch_bounds__(256) void k_mc_range_entries(McRangeArgs a) {
     uint32_t br[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) { be[v] = 0; br[v] = 0; }
-    for (uint32_t f = fb; f < fe; ++f) {
-        // entries that can intersect the element: start within the widest range below it
-        uint64_t qs, qe;
-        if (key_dom) { qe = a.keys[f]; qs = qe; } else { qs = a.rs[f]; qe = a.re[f]; }
-        const uint64_t vlo = key_dom ? (qe > a.wmax ? qe - a.wmax : 0ull) : (qs >= a.wmax ? qs - a.wmax + 1 : 0ull);
-        const uint32_t lo = lb_u64(a.es, 0, Q, vlo), hi = lb_u64(a.es, lo, Q, qe);
-        for (uint32_t x = lo + __lane_id(); x < hi; x += WAVE) {
-            const uint32_t j = a.eown[x];
-            if (j >= i) continue;
-            const uint32_t mj = a.meta[j];
-            const uint32_t kj = meta_kind(mj);
-            if (!(kj == AD_KIND_READ || kj == AD_KIND_WRITE || kj == AD_KIND_SYNC_POINT || kj == AD_KIND_EXCLUSIVE_SYNC_POINT))
-                continue;                          // globally visible kinds only
-            const uint64_t s = a.es[x], e = a.ee[x];
-            const bool hit = key_dom ? (s < qe && qe <= e) : (s < qe && e > qs);
-            if (!hit) continue;
-            const bool inw = j >= lo_w;
-            const uint32_t st = meta_status(mj);
-            if (!inw && (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID)) continue;
-            const uint64_t ej = a.ex1[j];
+    ri_walk(a.ix, a.es, Q, key_dom, a.keys, a.rs, a.re, fb, fe, [&](uint32_t clo, uint32_t chi) {
+        const uint32_t x = clo + __lane_id();
+        if (x >= chi) return;
+        const uint32_t j = a.eown[x];
+        if (j >= i) return;
+        const uint32_t mj = a.meta[j];
+        const uint32_t kj = meta_kind(mj);
+        if (!(kj == AD_KIND_READ || kj == AD_KIND_WRITE || kj == AD_KIND_SYNC_POINT || kj == AD_KIND_EXCLUSIVE_SYNC_POINT))
+            return;                                // globally visible kinds only
+        // the chunk can hold entries of no footprint element: the exact intersection test
+        RangeArgs ra{};
+        ra.keys = a.keys; ra.rs = a.rs; ra.re = a.re;
+        if (!range_hits(ra, key_dom, fb, fe, a.es[x], a.ee[x])) return;
+        const bool inw = j >= lo_w;
+        const uint32_t st = meta_status(mj);
+        if (!inw && (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID)) return;
+        const uint64_t ej = a.ex1[j];
 #pragma unroll
-            for (int v = 0; v < NV; ++v)
-                if (!(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh) && mc_less(be[v], br[v], ej, j)) {
-                    be[v] = ej; br[v] = j;
-                }
-        }
-    }
+        for (int v = 0; v < NV; ++v)
+            if (!(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh) && mc_less(be[v], br[v], ej, j)) {
+                be[v] = ej; br[v] = j;
+            }
+    });
     mc_fold_wave<NV>(a, t, be, br);
 }
 

@@ -87,6 +87,8 @@ struct ad_handle {
     // range entries sorted by (start, end, owner)
     uint32_t *rowner = nullptr, *rk0 = nullptr, *rv0 = nullptr, *rk1 = nullptr, *rv1 = nullptr, *eown = nullptr;
     uint64_t *es = nullptr, *ee = nullptr;
+    uint64_t* ri_nodes = nullptr;    // upper levels of the range index (range_index.h)
+    RangeIndex ix{};
     uint32_t *rnk = nullptr, *rne = nullptr;
     void* scratch = nullptr;
     size_t scratch_cap = 0;
@@ -229,7 +231,8 @@ enum Slot : size_t {
     S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
     S_HTM, S_HTL, S_HTN, S_HEM, S_HEL, S_HEN, S_HST, S_HKOFF, S_HKEYS, S_HGIDS, S_HSEGM, S_HKEEP, S_HROWS2, S_HCNT,
     S_RCROWS, S_RCCNT, S_RCOFF, S_RCREJ, S_RCK0, S_RCT0 = S_RCK0 + RC_OUT, S_RCEND = S_RCT0 + RC_OUT,
-    S_NUM_FIXED = S_RCEND,
+    S_RIDX = S_RCEND,
+    S_NUM_FIXED,
     S_CSR0 = 160
 };
 static_assert(S_NUM_FIXED <= S_CSR0, "fixed device slots overlap the CSR slot blocks");
@@ -429,6 +432,22 @@ int stage_sort(ad_handle* h) {
         if (rb > 32) { k_range_key_half<<<gq, 256, 0, st>>>(Q, h->range_s, v, h->rbase, 32, k); pass(rb - 32); }
         k_range_gather<<<gq, 256, 0, st>>>(Q, v, h->range_s, h->range_e, h->rowner, h->es, h->ee, h->eown);
     }
+    // the interval index over the sorted entries: a 64-ary tree of maximum ends
+    RangeIndex ix{};
+    size_t nodes = 0;
+    ix.top = ri_levels(Q, ix.cnt, &nodes);
+    ix.lv[0] = h->ee;
+    if (ix.top > 0) {
+        CK(dalloc(h, S_RIDX, &h->ri_nodes, nodes));
+        size_t off = 0;
+        for (int l = 1; l <= ix.top; ++l) {
+            uint64_t* out = h->ri_nodes + off;
+            k_ri_level<<<ceil_div((long)ix.cnt[l] * WAVE, 256), 256, 0, st>>>(ix.cnt[l], ix.cnt[l - 1], ix.lv[l - 1], out);
+            ix.lv[l] = out;
+            off += ix.cnt[l];
+        }
+    }
+    h->ix = ix;
     return AD_OK;
 }
 
@@ -676,7 +695,7 @@ int stage_deps(ad_handle* h) {
     // ---- RangeDeps (count)
     RangeArgs ra{};
     ra.n = n; ra.Q = Q; ra.key_off = h->key_off; ra.keys = h->keys; ra.range_off = h->range_off; ra.rs = h->range_s;
-    ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.wmax = h->wmax;
+    ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
     ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
     ra.qpos = qpos;
     if (Q > 0 && n > 0) {
@@ -1227,7 +1246,7 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
             ra.range_off = h->range_off; ra.rs = h->range_s; ra.re = h->range_e;
             ra.ukey = h->ukey; ra.useg = h->useg; ra.U = P ? h->hprm.n_keys_u : 0;
             ra.e_txn = h->e_txn; ra.e_meta = h->e_meta; ra.e_exec1 = h->e_exec1; ra.pm_e = pm_e; ra.pm_r = pm_r;
-            ra.Q = h->Q; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.wmax = h->wmax;
+            ra.Q = h->Q; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
             ra.window = a.window; ra.thresh = a.thresh; ra.seed = a.seed; ra.max_rank = rank; ra.fast = fst;
             NV_DISPATCH(nv, launch_mc_ranges, ra, st);
         }
@@ -1376,7 +1395,7 @@ int ad_recover(ad_handle* h, const uint32_t* rows, size_t nq, size_t* entries) {
     a.range_off = h->range_off; a.rs = h->range_s; a.re = h->range_e;
     a.ukey = h->ukey; a.useg = h->useg; a.U = h->P ? h->hprm.n_keys_u : 0;
     a.e_txn = h->e_txn; a.e_meta = h->e_meta; a.e_exec1 = h->e_exec1; a.sval = h->sval;
-    a.Q = h->Q; a.es = h->es; a.ee = h->ee; a.eown = h->eown; a.wmax = h->wmax;
+    a.Q = h->Q; a.es = h->es; a.ee = h->ee; a.eown = h->eown; a.ix = h->ix;
     const int ncls = (h->Q > 0 && h->merged_has_range) ? 3 : 2;
     for (int c = 0; c < ncls; ++c) {
         const Csr& m = h->merged[c];

@@ -11,19 +11,20 @@
 // Device algorithm:
 //   * range entries (start, end, owner) of all range txns are radix-sorted by (start, end, owner) once
 //     per batch (stable LSD on end then start over the input order, which is owner order);
-//   * every entry is at most Wmax = max(end - start) wide, so the entries that can contain key k have
-//     start in [k - Wmax, k), and those that can intersect (qs, qe] have start in (qs - Wmax, qe): each
-//     footprint element maps to one contiguous window of the sorted entries (two binary searches);
-//   * one wave per query txn walks the union of its (sorted, hence mergeable) windows 64 entries at a
+//   * a 64-ary max-end tree over the sorted entries (range_index.h, the device form of CINTIA's
+//     checkpoints) gives, per footprint element, the entries below its bound whose end reaches it:
+//     O(log Q + hits) per query whatever the width distribution (one very wide range no longer widens
+//     every query's window);
+//   * one wave per query txn walks the chunks the index yields for its whole footprint 64 entries at a
 //     time, evaluates the predicate per lane, and ballots per replica view: popcounts give the counts,
 //     prefix popcounts the output slots, and the matched entries come out already in (start, end,
 //     owner) order — the RangeDeps key order — so equal ranges are adjacent and the distinct-range
 //     count falls out of a lane-to-previous-match comparison (shuffle from the highest lower match).
 //   * the per-txn TxnId union/remap is k_union_lds.
-// Bytes per query: the window entries (16 B range + 4 B owner + 1 B meta); per emitted entry 4 B (+16 B
-// per distinct range).  Degenerate width distributions (one very wide range) widen every window: the
-// next step is CINTIA's checkpoint lists (utils/CheckpointIntervalArray.java:28-219) for the wide tail.
+// Bytes per query: the visited entries (16 B range + 4 B owner + 1 B meta) + 512 B per index step; per
+// emitted entry 4 B (+16 B per distinct range).
 #pragma once
+#include "range_index.h"
 #include "union_kernels.h"
 
 namespace ad {
@@ -78,7 +79,7 @@ struct RangeArgs {
     const uint64_t* es;          // sorted entries
     const uint64_t* ee;
     const uint32_t* eown;
-    uint64_t wmax;
+    RangeIndex ix;               // max-end tree over the sorted entries (range_index.h)
     uint32_t window, thresh;
     uint64_t seed;
     uint32_t* rnk;               // [v * n + t]  distinct ranges (count pass)
@@ -136,83 +137,57 @@ __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
     }
     const bool query = qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && fe > fb && a.Q > 0;
     if (query) {
-        const uint32_t Q = (uint32_t)a.Q;
-        // windows of the footprint elements, merged on the fly (both bounds are non-decreasing in f)
-        uint32_t clo = 0, chi = 0;
-        bool open = false;
-        for (uint32_t f = fb; f <= fe; ++f) {
-            uint32_t lo = 0, hi = 0;
-            if (f < fe) {
-                uint64_t vlo, vhi;
-                if (key_dom) {
-                    const uint64_t k = a.keys[f];
-                    vlo = k > a.wmax ? k - a.wmax : 0ull;
-                    vhi = k;
-                } else {
-                    const uint64_t qs = a.rs[f], qe = a.re[f];
-                    vlo = qs >= a.wmax ? qs - a.wmax + 1 : 0ull;
-                    vhi = qe;
-                }
-                lo = lb_u64(a.es, 0, Q, vlo);
-                hi = lb_u64(a.es, lo, Q, vhi);
-                if (lo >= hi) continue;
-                if (open && lo <= chi) { chi = max(chi, hi); continue; }
-            }
-            if (open) {
-                // process [clo, chi)
-                for (uint32_t base = clo; base < chi; base += WAVE) {
-                    const uint32_t x = base + lane;
-                    const bool valid = x < chi;
-                    uint64_t s = 0, e = 0;
-                    uint32_t j = 0xFFFFFFFFu;
-                    bool cond = false;
-                    if (valid) {
-                        j = a.eown[x];
-                        if (j < qi && j != i) {
-                            const uint32_t mj = a.meta[j];
-                            const bool inw = j >= lo_w;
-                            cond = witnesses(qk, meta_kind(mj)) && (inw || meta_status(mj) != AD_ST_INVALID);
-                            if (cond) {
-                                s = a.es[x];
-                                e = a.ee[x];
-                                cond = range_hits(a, key_dom, fb, fe, s, e);
-                            }
-                        }
-                    }
+        // the index walk visits, in entry order, the chunks that can hold a hit; the predicate is exact
+        ri_walk(a.ix, a.es, (uint32_t)a.Q, key_dom, a.keys, a.rs, a.re, fb, fe, [&](uint32_t clo, uint32_t chi) {
+            const uint32_t x = clo + lane;
+            const bool valid = x < chi;
+            uint64_t s = 0, e = 0;
+            uint32_t j = 0xFFFFFFFFu;
+            bool cond = false;
+            if (valid) {
+                j = a.eown[x];
+                if (j < qi && j != i) {
+                    const uint32_t mj = a.meta[j];
                     const bool inw = j >= lo_w;
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        const bool ok = cond && !(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh);
-                        const uint64_t mask = __ballot(ok);
-                        if (mask == 0) continue;
-                        const uint64_t lower = mask & below;
-                        const int pl = lower ? 63 - __clzll(lower) : lane;
-                        const uint64_t ps = __shfl(s, pl), pe = __shfl(e, pl);
-                        const bool has_prev = lower ? true : chas[v];
-                        const uint64_t prs = lower ? ps : cs[v], pre = lower ? pe : ce[v];
-                        const bool newkey = ok && !(has_prev && prs == s && pre == e);
-                        const uint64_t nmask = __ballot(newkey);
-                        if (FILL) {
-                            const uint32_t epos = ecount[v] + (uint32_t)__popcll(lower);
-                            if (ok) a.k2t_v[v][mb[v] + nkt[v] + epos] = (int32_t)j;
-                            if (newkey) {
-                                const uint32_t kpos = kcount[v] + (uint32_t)__popcll(nmask & below);
-                                a.keys_v[v][2 * (size_t)(kb[v] + kpos)] = s;
-                                a.keys_v[v][2 * (size_t)(kb[v] + kpos) + 1] = e;
-                                if (kpos > 0) a.k2t_v[v][mb[v] + kpos - 1] = (int32_t)(nkt[v] + epos);
-                            }
-                        }
-                        ecount[v] += (uint32_t)__popcll(mask);
-                        kcount[v] += (uint32_t)__popcll(nmask);
-                        const int hl = 63 - __clzll(mask);
-                        cs[v] = __shfl(s, hl);
-                        ce[v] = __shfl(e, hl);
-                        chas[v] = true;
+                    cond = witnesses(qk, meta_kind(mj)) && (inw || meta_status(mj) != AD_ST_INVALID);
+                    if (cond) {
+                        s = a.es[x];
+                        e = a.ee[x];
+                        cond = range_hits(a, key_dom, fb, fe, s, e);
                     }
                 }
             }
-            if (f < fe) { clo = lo; chi = hi; open = true; }
-        }
+            const bool inw = j >= lo_w;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const bool ok = cond && !(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh);
+                const uint64_t mask = __ballot(ok);
+                if (mask == 0) continue;
+                const uint64_t lower = mask & below;
+                const int pl = lower ? 63 - __clzll(lower) : lane;
+                const uint64_t ps = __shfl(s, pl), pe = __shfl(e, pl);
+                const bool has_prev = lower ? true : chas[v];
+                const uint64_t prs = lower ? ps : cs[v], pre = lower ? pe : ce[v];
+                const bool newkey = ok && !(has_prev && prs == s && pre == e);
+                const uint64_t nmask = __ballot(newkey);
+                if (FILL) {
+                    const uint32_t epos = ecount[v] + (uint32_t)__popcll(lower);
+                    if (ok) a.k2t_v[v][mb[v] + nkt[v] + epos] = (int32_t)j;
+                    if (newkey) {
+                        const uint32_t kpos = kcount[v] + (uint32_t)__popcll(nmask & below);
+                        a.keys_v[v][2 * (size_t)(kb[v] + kpos)] = s;
+                        a.keys_v[v][2 * (size_t)(kb[v] + kpos) + 1] = e;
+                        if (kpos > 0) a.k2t_v[v][mb[v] + kpos - 1] = (int32_t)(nkt[v] + epos);
+                    }
+                }
+                ecount[v] += (uint32_t)__popcll(mask);
+                kcount[v] += (uint32_t)__popcll(nmask);
+                const int hl = 63 - __clzll(mask);
+                cs[v] = __shfl(s, hl);
+                ce[v] = __shfl(e, hl);
+                chas[v] = true;
+            }
+        });
     }
     if (lane == 0) {
 #pragma unroll

@@ -61,7 +61,7 @@ struct RecoverArgs {
     const uint64_t* es;
     const uint64_t* ee;
     const uint32_t* eown;
-    uint64_t wmax;
+    RangeIndex ix;
     // each txn's Deps (merged), per class
     const uint32_t* m_key_off[3];
     const uint64_t* m_keys[3];
@@ -216,52 +216,34 @@ __global__ __launch_bounds__(256) void k_recover(RecoverArgs a) {
         }
         // ---- range commands ----
         if (a.Q > 0) {
-            const uint32_t Q = (uint32_t)a.Q;
-            uint32_t clo = 0, chi = 0;
-            bool open = false;
-            for (uint32_t f = fb; f <= fe; ++f) {
-                uint32_t lo = 0, hi = 0;
-                if (f < fe) {
-                    uint64_t vlo, vhi;
-                    if (key_dom) { const uint64_t k = a.keys[f]; vlo = k > a.wmax ? k - a.wmax : 0ull; vhi = k; }
-                    else { vlo = a.rs[f] >= a.wmax ? a.rs[f] - a.wmax + 1 : 0ull; vhi = a.re[f]; }
-                    lo = lb_u64(a.es, 0, Q, vlo);
-                    hi = lb_u64(a.es, lo, Q, vhi);
-                    if (lo >= hi) continue;
-                    if (open && lo <= chi) { chi = max(chi, hi); continue; }
-                }
-                if (open) {
-                    for (uint32_t base = clo; base < chi; base += WAVE) {
-                        const uint32_t x = base + lane;
-                        int o = -1;
-                        uint64_t s = 0, e = 0;
-                        uint32_t j = 0;
-                        if (x < chi) {
-                            j = a.eown[x];
-                            const uint32_t mj = a.meta[j];
-                            const uint32_t sj = meta_status(mj);
-                            const bool proposed = sj == AD_ST_ACCEPTED || sj == AD_ST_COMMITTED;
-                            const bool stable = sj == AD_ST_STABLE || sj == AD_ST_APPLIED;
-                            s = a.es[x]; e = a.ee[x];
-                            RangeArgs ra{};
-                            ra.keys = a.keys; ra.rs = a.rs; ra.re = a.re;
-                            if (j != t && (proposed || stable) && witnesses(meta_kind(mj), kt) &&
-                                range_hits(ra, key_dom, fb, fe, s, e)) {
-                                const uint64_t ej = a.ex1[j];                   // executeAt + 1
-                                const bool exec_ge = ej > tt;                   // executeAt >= t
-                                const bool has = rc_intersects(a, j, t, mt);
-                                if (j < t && exec_ge) {
-                                    if (stable && has) o = 0 * 3 + AD_CLASS_RANGE;
-                                    else if (proposed && !has && ej > tt + 1) o = 1 * 3 + AD_CLASS_RANGE;
-                                }
-                                if (!has && ((j > t && proposed) || (stable && exec_ge))) reject = true;
-                            }
+            ri_walk(a.ix, a.es, (uint32_t)a.Q, key_dom, a.keys, a.rs, a.re, fb, fe, [&](uint32_t clo, uint32_t chi) {
+                const uint32_t x = clo + lane;
+                int o = -1;
+                uint64_t s = 0, e = 0;
+                uint32_t j = 0;
+                if (x < chi) {
+                    j = a.eown[x];
+                    const uint32_t mj = a.meta[j];
+                    const uint32_t sj = meta_status(mj);
+                    const bool proposed = sj == AD_ST_ACCEPTED || sj == AD_ST_COMMITTED;
+                    const bool stable = sj == AD_ST_STABLE || sj == AD_ST_APPLIED;
+                    s = a.es[x]; e = a.ee[x];
+                    RangeArgs ra{};
+                    ra.keys = a.keys; ra.rs = a.rs; ra.re = a.re;
+                    if (j != t && (proposed || stable) && witnesses(meta_kind(mj), kt) &&
+                        range_hits(ra, key_dom, fb, fe, s, e)) {
+                        const uint64_t ej = a.ex1[j];                   // executeAt + 1
+                        const bool exec_ge = ej > tt;                   // executeAt >= t
+                        const bool has = rc_intersects(a, j, t, mt);
+                        if (j < t && exec_ge) {
+                            if (stable && has) o = 0 * 3 + AD_CLASS_RANGE;
+                            else if (proposed && !has && ej > tt + 1) o = 1 * 3 + AD_CLASS_RANGE;
                         }
-                        em.emit(a, o, s, e, j);
+                        if (!has && ((j > t && proposed) || (stable && exec_ge))) reject = true;
                     }
                 }
-                if (f < fe) { clo = lo; chi = hi; open = true; }
-            }
+                em.emit(a, o, s, e, j);
+            });
         }
     }
     const bool any = __ballot(reject) != 0ull;
