@@ -5,11 +5,13 @@ PreAccept.reduce across CommandStores (messages/PreAccept.java:141-156) needs, a
 PartialDeps every other store computed for it.  A store packs, per destination store, the rows of the local
 txns homed there that have any deps, with TxnIds rewritten to global arrival ranks.  One blob per destination:
 
-    u64 header[3 + 3*nvc] = {MAGIC, rows, nvc, per (view, class) vc: (keys, keysToTxnIds, TxnIds) counts}
+    u64 header[3 + 3*nvc] = {MAGIC, rows, nvc | nr << 16, per (view, class) vc: (keys, keysToTxnIds, TxnIds) counts}
     u32 gid[rows]                                      global rank of each row (ascending)
     per vc:  u32 key_off[rows+1]  u32 k2t_off[rows+1]  u32 ent_off[rows+1]  u32 tcnt[rows]
-             u64 keys[keys]       i32 k2t[k2t]         u32 txns[TxnIds]
-    every section 8-byte aligned, padding zero; vc = view * 2 + class (keyDeps, directKeyDeps)
+             u64 keys[keys * w]   i32 k2t[k2t]         u32 txns[TxnIds]
+    every section 8-byte aligned, padding zero; vc = view * 2 + class (keyDeps, directKeyDeps) for vc < 2R, then,
+    when the store holds range txns, nr = R RangeDeps classes (one per view) whose keys are (start, end] ranges
+    (w = 2 words; RangeDeps.SerializerSupport.create's Range[], primitives/RangeDeps.java:100-103)
 
 The per-row arrays are exactly KeyDeps.SerializerSupport.create's arguments (primitives/KeyDeps.java:69-72)
 per txn; ent_off is compact (ent_off[i+1] - ent_off[i] == tcnt[i]).  A host that resolves a store's fragments
@@ -27,16 +29,18 @@ def _align8(x):
     return (x + 7) & ~7
 
 
-def layout(rows, nvc, counts):
-    """Byte offsets of the sections of one blob and its total size.  counts[vc] = (keys, k2t, txns).
-    Returns (gid offset, [vc][7] section offsets, total bytes) — engine.hip blob_layout."""
+def layout(rows, nvc, counts, nr=0):
+    """Byte offsets of the sections of one blob and its total size.  counts[vc] = (keys, k2t, txns); the last nr
+    classes are RangeDeps (two words per key).  Returns (gid offset, [vc][7] section offsets, total bytes) —
+    engine.hip blob_layout."""
     off = _align8((3 + 3 * nvc) * 8)
     gid_off = off
     off = _align8(off + rows * 4)
     secs = []
     for c in range(nvc):
         nk, nm, nt = counts[c]
-        sizes = ((rows + 1) * 4, (rows + 1) * 4, (rows + 1) * 4, rows * 4, nk * 8, nm * 4, nt * 4)
+        w = 2 if c >= nvc - nr else 1
+        sizes = ((rows + 1) * 4, (rows + 1) * 4, (rows + 1) * 4, rows * 4, nk * 8 * w, nm * 4, nt * 4)
         s = []
         for z in sizes:
             s.append(off)
@@ -73,11 +77,14 @@ def encode(gid, csrs):
     TxnIds already global.  Returns np.uint8 bytes (zero padding, as the engine's memset send buffer)."""
     gid = np.ascontiguousarray(gid, np.uint32)
     rows, nvc = len(gid), len(csrs)
+    nr = sum(1 for c in csrs if c.is_range)
+    if any(c.is_range for c in csrs[:nvc - nr]):
+        raise ValueError("RangeDeps classes go last")
     counts = [(int(c.key_off[-1]), int(c.k2t_off[-1]), int(c.txn_off[-1])) for c in csrs]
-    gid_off, secs, total = layout(rows, nvc, counts)
+    gid_off, secs, total = layout(rows, nvc, counts, nr)
     buf = np.zeros(total, np.uint8)
     hdr = np.zeros(3 + 3 * nvc, np.uint64)
-    hdr[0], hdr[1], hdr[2] = MAGIC, rows, nvc
+    hdr[0], hdr[1], hdr[2] = MAGIC, rows, nvc | (nr << 16)
     for c, (nk, nm, nt) in enumerate(counts):
         hdr[3 + 3 * c:6 + 3 * c] = (nk, nm, nt)
     buf[:hdr.nbytes] = hdr.view(np.uint8)
@@ -109,12 +116,14 @@ def decode(buf):
     h0 = buf[:24].view(np.uint64)
     if int(h0[0]) != MAGIC:
         raise ValueError("shard blob: bad magic")
-    rows, nvc = int(h0[1]), int(h0[2])
+    rows, nvc, nr = int(h0[1]), int(h0[2]) & 0xFFFF, int(h0[2]) >> 16
+    if nr > nvc:
+        raise ValueError("shard blob: bad class counts")
     if buf.nbytes < (3 + 3 * nvc) * 8:
         raise ValueError("shard blob truncated")
     hdr = buf[:(3 + 3 * nvc) * 8].view(np.uint64)
     counts = [tuple(int(x) for x in hdr[3 + 3 * c:6 + 3 * c]) for c in range(nvc)]
-    gid_off, secs, total = layout(rows, nvc, counts)
+    gid_off, secs, total = layout(rows, nvc, counts, nr)
     if total > buf.nbytes:
         raise ValueError("shard blob exceeds its size")
 
@@ -126,8 +135,9 @@ def decode(buf):
     for c in range(nvc):
         nk, nm, nt = counts[c]
         s = secs[c]
-        out.append(abi.Csr(get(s[0], rows + 1, np.uint32), get(s[4], nk, np.uint64), get(s[1], rows + 1, np.uint32),
-                           get(s[5], nm, np.int32), get(s[2], rows + 1, np.uint32), get(s[6], nt, np.uint32)))
+        w = 2 if c >= nvc - nr else 1
+        out.append(abi.Csr(get(s[0], rows + 1, np.uint32), get(s[4], nk * w, np.uint64), get(s[1], rows + 1, np.uint32),
+                           get(s[5], nm, np.int32), get(s[2], rows + 1, np.uint32), get(s[6], nt, np.uint32), w == 2))
     return gid, out
 
 

@@ -32,22 +32,43 @@ def even_bounds(key_lo, key_hi, shards):
     return np.array(b + [np.iinfo(np.uint64).max], np.uint64)
 
 
+def _ranges(batch):
+    ro = batch.get("range_off")
+    if ro is None or int(ro[-1]) == 0:
+        return None
+    return (np.asarray(ro, np.int64), np.asarray(batch["range_start"], np.uint64), np.asarray(batch["range_end"], np.uint64))
+
+
+def _clip_ranges(rs, re, lo, hi):
+    """(start, end] ranges cut to the store owning keys [lo, hi): (max(start, lo - 1), min(end, hi - 1)] — the
+    range commands' slice to the store's ranges (impl/InMemoryCommandStore.java:758-761, Ranges.slice)."""
+    lo, hi = int(lo), int(hi)
+    s = np.maximum(rs, np.uint64(lo - 1)) if lo > 0 else rs.copy()
+    e = np.minimum(re, np.uint64(hi - 1))
+    return s, e, s < e
+
+
 def slice_for_shard(batch, lo, hi):
-    """(local batch, gid, home) of the store owning keys in [lo, hi)."""
-    if batch.get("range_off") is not None and int(batch["range_off"][-1]) > 0:
-        raise ValueError("sharded mode: range txns are not supported")
+    """(local batch, gid, home) of the store owning keys [lo, hi): every txn with a key in range or a range
+    meeting it, keys cut to the range and ranges sliced to it (_clip_ranges), TxnId order kept."""
     n = batch["n"]
     ko = batch["key_off"].astype(np.int64)
     keys = batch["keys"]
     inr = (keys >= np.uint64(lo)) & (keys < np.uint64(hi))
     owner = np.repeat(np.arange(n, dtype=np.int64), np.diff(ko))
     cnt = np.bincount(owner[inr], minlength=n)
-    touch = cnt > 0
+    rg = _ranges(batch)
+    if rg is not None:
+        ro, rs, re = rg
+        cs, ce, keep = _clip_ranges(rs, re, lo, hi)
+        rowner = np.repeat(np.arange(n, dtype=np.int64), np.diff(ro))
+        rcnt = np.bincount(rowner[keep], minlength=n)
+    else:
+        rcnt = np.zeros(n, np.int64)
+    touch = (cnt > 0) | (rcnt > 0)
     gid = np.nonzero(touch)[0].astype(np.uint32)
-    first = np.full(n, np.iinfo(np.uint64).max, np.uint64)
-    nz = ko[1:] > ko[:-1]
-    first[nz] = keys[ko[:-1][nz]]
-    home = ((first >= np.uint64(lo)) & (first < np.uint64(hi)))[gid].astype(np.uint8)
+    hs = home_stores(batch, np.array([lo, hi], np.uint64), clip=False)
+    home = (hs[gid] == 0).astype(np.uint8)
     local = {"n": int(len(gid))}
     for f in ("txn_msb", "txn_lsb", "txn_node", "exec_msb", "exec_lsb", "exec_node", "status"):
         local[f] = np.ascontiguousarray(batch[f][gid])
@@ -55,38 +76,92 @@ def slice_for_shard(batch, lo, hi):
     lk[1:] = np.cumsum(cnt[gid])
     local["key_off"] = lk
     local["keys"] = np.ascontiguousarray(keys[inr])
-    local["range_off"] = local["range_start"] = local["range_end"] = None
+    if rg is not None and int(rcnt.sum()) > 0:
+        lr = np.zeros(len(gid) + 1, np.uint32)
+        lr[1:] = np.cumsum(rcnt[gid])
+        local["range_off"] = lr
+        local["range_start"] = np.ascontiguousarray(cs[keep])
+        local["range_end"] = np.ascontiguousarray(ce[keep])
+    else:
+        local["range_off"] = local["range_start"] = local["range_end"] = None
     return local, gid, home
 
 
-def home_stores(batch, bounds):
-    """Per global txn: the store owning its first key (its home; merges its deps)."""
+def home_stores(batch, bounds, clip=True):
+    """Per global txn: the store owning its first key — for a range txn the first key its first range covers,
+    start + 1 — (its home; merges its deps).  clip=False: -1 / len(bounds) - 1 outside the bounds."""
     ko = batch["key_off"].astype(np.int64)
     keys = batch["keys"]
     n = batch["n"]
     first = np.zeros(n, np.uint64)
     nz = ko[1:] > ko[:-1]
     first[nz] = keys[ko[:-1][nz]]
+    rg = _ranges(batch)
+    if rg is not None:
+        ro, rs, _ = rg
+        has = ro[1:] > ro[:-1]
+        first[has & ~nz] = rs[ro[:-1][has & ~nz]] + np.uint64(1)
     hs = np.searchsorted(np.asarray(bounds, np.uint64), first, side="right") - 1
+    if not clip:
+        return hs
     return np.clip(hs, 0, len(bounds) - 2).astype(np.uint8)
 
 
 def holder_masks(batch, bounds):
-    """Per global txn: bitmask of the stores holding it (the stores owning any of its keys).  A store's
-    chains hold only its own txns, so in the level rounds a raised level travels only to the other holders
-    (ShardStore.set_holders, the delta exchange)."""
+    """Per global txn: bitmask of the stores holding it (the stores owning any of its keys, or meeting any of
+    its ranges).  A store's chains hold only its own txns, so in the level rounds a raised level travels only
+    to the other holders (ShardStore.set_holders, the delta exchange)."""
     n = batch["n"]
     ko = batch["key_off"].astype(np.int64)
     keys = batch["keys"]
     b = np.asarray(bounds, np.uint64)
-    st = np.clip(np.searchsorted(b, keys, side="right") - 1, 0, len(b) - 2)
+    S = len(b) - 1
+    st = np.clip(np.searchsorted(b, keys, side="right") - 1, 0, S - 1)
     bits = (np.uint16(1) << st.astype(np.uint16)).astype(np.uint16)
     out = np.zeros(n, np.uint16)
     nz = ko[1:] > ko[:-1]
     if len(keys):
         red = np.bitwise_or.reduceat(bits, ko[:-1][nz])
         out[nz] = red
+    rg = _ranges(batch)
+    if rg is not None:
+        ro, rs, re = rg
+        first = np.clip(np.searchsorted(b, rs + np.uint64(1), side="right") - 1, 0, S - 1)
+        last = np.clip(np.searchsorted(b, re, side="right") - 1, 0, S - 1)
+        rb = np.zeros(len(rs), np.uint16)
+        for k in range(S):
+            rb |= (((first <= k) & (k <= last)).astype(np.uint16) << np.uint16(k)).astype(np.uint16)
+        has = ro[1:] > ro[:-1]
+        out[has] |= np.bitwise_or.reduceat(rb, ro[:-1][has])
     return out.astype(np.uint8)
+
+
+def presplit(batch, bounds):
+    """The global batch with every range cut at the store boundaries (each piece = one store's slice,
+    _clip_ranges).  Its unsharded deps are what the sharded stores produce together: RangeDeps are keyed by
+    the store-sliced ranges, while KeyDeps, TxnId sets, witnessedAt and levels do not depend on
+    the split."""
+    rg = _ranges(batch)
+    if rg is None:
+        return batch
+    ro, rs, re = rg
+    b = np.asarray(bounds, np.uint64)
+    S = len(b) - 1
+    n = batch["n"]
+    rowner = np.repeat(np.arange(n, dtype=np.int64), np.diff(ro))
+    ps, pe, po, pk = [], [], [], []
+    for k in range(S):
+        s, e, keep = _clip_ranges(rs, re, b[k], b[k + 1])
+        idx = np.nonzero(keep)[0]
+        ps.append(s[idx]); pe.append(e[idx]); po.append(rowner[idx]); pk.append(idx * (S + 1) + k)
+    ps, pe, po, pk = (np.concatenate(x) for x in (ps, pe, po, pk))
+    order = np.argsort(pk, kind="stable")                 # by (original range, store): ascending per txn
+    out = dict(batch)
+    out["range_start"] = np.ascontiguousarray(ps[order])
+    out["range_end"] = np.ascontiguousarray(pe[order])
+    cnt = np.bincount(po, minlength=n)
+    out["range_off"] = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32)
+    return out
 
 
 def reduce_witnessed(batch, parts):

@@ -116,7 +116,11 @@ struct ad_handle {
     std::vector<uint32_t*> src_gid;
     std::vector<uint32_t> src_n;
     std::vector<Csr> sdeps;          // home-indexed per (view, class)
+    Csr srdeps[MAXV];                // home-indexed RangeDeps per view (sources with range classes)
     Csr smerged[3];
+    std::vector<uint8_t> src_ranges; // per source: its blob carries RangeDeps classes
+    bool shard_ranges = false;       // the home merge produced RangeDeps (some source carried them)
+    int32_t* none_rows = nullptr;    // [H] all -1: a source without RangeDeps classes
     ncclComm_t comm = nullptr;
     // delta level exchange (ad_shard_set_holders): per-row holder masks, per-destination send regions
     uint8_t* holders = nullptr;
@@ -231,7 +235,7 @@ enum Slot : size_t {
     S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
     S_HTM, S_HTL, S_HTN, S_HEM, S_HEL, S_HEN, S_HST, S_HKOFF, S_HKEYS, S_HGIDS, S_HSEGM, S_HKEEP, S_HROWS2, S_HCNT,
     S_RCROWS, S_RCCNT, S_RCOFF, S_RCREJ, S_RCK0, S_RCT0 = S_RCK0 + RC_OUT, S_RCEND = S_RCT0 + RC_OUT,
-    S_RIDX = S_RCEND,
+    S_RIDX = S_RCEND, S_NONEROWS,
     S_NUM_FIXED,
     S_CSR0 = 160
 };
@@ -239,7 +243,7 @@ static_assert(S_NUM_FIXED <= S_CSR0, "fixed device slots overlap the CSR slot bl
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
 // merged [NVC_MAX + MAXV, +3)
 constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV, CSR_HOST0 = CSR_MERGED0 + 3;
-constexpr size_t CSR_SHARD0 = CSR_HOST0 + 3 * MAXV, CSR_SMERGED0 = CSR_SHARD0 + NVC_MAX;
+constexpr size_t CSR_SHARD0 = CSR_HOST0 + 3 * MAXV, CSR_SMERGED0 = CSR_SHARD0 + NVC_MAX, CSR_SRANGE0 = CSR_SMERGED0 + 3;
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
 
@@ -698,6 +702,7 @@ int stage_deps(ad_handle* h) {
     ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
     ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
     ra.qpos = qpos;
+    ra.gid = wa.gid;
     if (Q > 0 && n > 0) {
         NV_DISPATCH(nv, launch_range, ra, false, st);
         for (int v = 0; v < nv; ++v) csr_offsets(h, h->rdeps[v], h->rnk + (size_t)v * n, h->rne + (size_t)v * n);
@@ -839,7 +844,9 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
             case 2: launch_multi_offsets<2>(h, n, mk, me, mu, out); break;
             case 3: launch_multi_offsets<3>(h, n, mk, me, mu, out); break;
             case 4: launch_multi_offsets<4>(h, n, mk, me, mu, out); break;
+            case 5: launch_multi_offsets<5>(h, n, mk, me, mu, out); break;
             case 6: launch_multi_offsets<6>(h, n, mk, me, mu, out); break;
+            case 7: launch_multi_offsets<7>(h, n, mk, me, mu, out); break;
             case 8: launch_multi_offsets<8>(h, n, mk, me, mu, out); break;
             case 10: launch_multi_offsets<10>(h, n, mk, me, mu, out); break;
             case 12: launch_multi_offsets<12>(h, n, mk, me, mu, out); break;
@@ -1212,6 +1219,8 @@ static int fetch_empty(ad_handle* h, ad_csr_out* out) {
 // deps stage left on the device: leaves max_rank / fast (and the batch-local rank) in their slots.
 static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_out, uint32_t** local_out) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
+    if (h->sharded && h->Q > 0)
+        return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts: range footprints answer in batch rows (not in sharded mode)");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     const size_t n = h->n, P = h->P;
@@ -1837,7 +1846,6 @@ int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home_store,
         return AD_ERR_ARGUMENT;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "ad_shard_setup: load the store's batch first");
     if (h->hist_active) return set_err(h, AD_ERR_UNSUPPORTED, "ad_shard_setup: the batch carries CFK history rows");
-    if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "sharded mode: range txns are not supported in this build");
     hipSetDevice(h->device);
     const size_t n = h->n;
     for (size_t i = 0; i < n; ++i) {
@@ -1865,13 +1873,16 @@ int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home_store,
 
 // Blob of one destination: header u64[3 + 3 nvc] = {magic, rows, nvc, per vc (keys, k2t, txns)}, then
 // gid[rows], then per vc key_off[rows+1] k2t_off[rows+1] ent_off[rows+1] tcnt[rows] keys k2t txns (8-aligned).
-static size_t blob_layout(size_t rows, int nvc, const uint32_t* cnt /* [nvc*3] */, uint64_t* sec /* [SEC_PER_DEST] or null */) {
+// nvc = 2R (key, direct per view) or 3R (then RangeDeps per view follow: vc >= 2R, keys = (start, end) pairs);
+// the header word holds nvc | (number of RangeDeps classes) << 16.
+static size_t blob_layout(size_t rows, int nvc, int nv, const uint32_t* cnt /* [nvc*3] */, uint64_t* sec /* [SEC_PER_DEST] or null */) {
     size_t off = align8((3 + 3 * (size_t)nvc) * 8);
     if (sec) sec[0] = off;
     off = align8(off + rows * 4);
     for (int c = 0; c < nvc; ++c) {
         const size_t nk = cnt[3 * c], nm = cnt[3 * c + 1], nt = cnt[3 * c + 2];
-        const size_t sz[7] = {(rows + 1) * 4, (rows + 1) * 4, (rows + 1) * 4, rows * 4, nk * 8, nm * 4, nt * 4};
+        const size_t kw = c >= 2 * nv ? 2 : 1;
+        const size_t sz[7] = {(rows + 1) * 4, (rows + 1) * 4, (rows + 1) * 4, rows * 4, nk * 8 * kw, nm * 4, nt * 4};
         for (int k = 0; k < 7; ++k) {
             if (sec) sec[1 + 7 * c + k] = off;
             off = align8(off + sz[k]);
@@ -1882,12 +1893,18 @@ static size_t blob_layout(size_t rows, int nvc, const uint32_t* cnt /* [nvc*3] *
 
 }  // extern "C"
 
+// exported CSR vc of the store: key / direct per view, then RangeDeps per view
+static const Csr& export_csr(ad_handle* h, int vc) {
+    const int nvc2 = 2 * (int)h->cfg.replicas;
+    return vc < nvc2 ? h->deps[vc] : h->rdeps[vc - nvc2];
+}
+
 template <int NVC>
 void launch_export_offsets(ad_handle* h, size_t K, const uint32_t* list, const ExportOffs& o) {
     ExportOffsetsOp<NVC> op{};
     op.list = list; op.n = K;
     for (int c = 0; c < NVC; ++c) {
-        const Csr& x = h->deps[c];
+        const Csr& x = export_csr(h, c);
         op.key_off[c] = x.key_off; op.k2t_off[c] = x.k2t_off; op.tcnt[c] = x.tcnt;
         op.ok[c] = o.ok[c]; op.om[c] = o.om[c]; op.ot[c] = o.ot[c];
     }
@@ -1896,20 +1913,23 @@ void launch_export_offsets(ad_handle* h, size_t K, const uint32_t* list, const E
 
 template <int NV>
 void launch_export_offsets_nv(ad_handle* h, size_t K, const uint32_t* list, const ExportOffs& o) {
-    launch_export_offsets<2 * NV>(h, K, list, o);
+    if (h->Q > 0) launch_export_offsets<3 * NV>(h, K, list, o);
+    else launch_export_offsets<2 * NV>(h, K, list, o);
 }
 
 extern "C" {
 
-// Pack this store's deps rows (every view, key + direct class) per destination store: the local txns
-// homed at destination d that have deps here, TxnIds as global ranks.  bytes[d] = blob size for d.
+// Pack this store's deps rows (every view, key + direct class, and RangeDeps when the store holds range
+// txns) per destination store: the local txns homed at destination d that have deps here, TxnIds as global
+// ranks.  bytes[d] = blob size for d.
 int ad_shard_export(ad_handle* h, uint64_t* bytes /* [world] */) {
     if (!h || !bytes) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_export: ad_shard_setup + ad_preaccept_deps first");
     hipSetDevice(h->device);
     const size_t n = h->n;
-    const int nvc = 2 * (int)h->cfg.replicas;
+    const int nv = (int)h->cfg.replicas;
+    const int nvc = (h->Q > 0 ? 3 : 2) * nv;
     const uint32_t W = h->world;
     hipStream_t st = h->st;
     // 1. rows with deps, partitioned by destination
@@ -1919,7 +1939,7 @@ int ad_shard_export(ad_handle* h, uint64_t* bytes /* [world] */) {
     if (n) {
         DestOp op{};
         op.dest = h->hstore; op.nvc = nvc; op.rank = rank; op.totals = xtot; op.n = n;
-        for (int c = 0; c < nvc; ++c) op.tcnt[c] = h->deps[c].tcnt;
+        for (int c = 0; c < nvc; ++c) op.tcnt[c] = export_csr(h, c).tcnt;
         device_scan(op, n, (DestOp::S*)h->scratch, st);
         k_export_list<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->hstore, rank, xtot, list);
         HIPCHK(h, hipMemcpyAsync(tot.data(), xtot, MAX_STORES * 4, hipMemcpyDeviceToHost, st));
@@ -1937,7 +1957,7 @@ int ad_shard_export(ad_handle* h, uint64_t* bytes /* [world] */) {
         o.ot[c] = xoff + (size_t)(3 * c + 2) * (K + 1);
     }
     uint32_t* bnd = nullptr;
-    CK(dalloc(h, S_XBND, &bnd, (size_t)(MAX_STORES + 1) * NVC_MAX * 3));
+    CK(dalloc(h, S_XBND, &bnd, (size_t)(MAX_STORES + 1) * NVX_MAX * 3));
     std::vector<uint32_t> hb((size_t)(W + 1) * nvc * 3, 0);
     if (K) {
         NV_DISPATCH((int)h->cfg.replicas, launch_export_offsets_nv, h, K, list, o);
@@ -1956,10 +1976,10 @@ int ad_shard_export(ad_handle* h, uint64_t* bytes /* [world] */) {
         std::vector<uint32_t> cnt((size_t)3 * nvc, 0);
         for (int c = 0; c < nvc; ++c)
             for (int k = 0; k < 3; ++k) cnt[3 * c + k] = hb[((size_t)(d + 1) * nvc + c) * 3 + k] - hb[((size_t)d * nvc + c) * 3 + k];
-        const size_t sz = blob_layout(tot[d], nvc, cnt.data(), sec.data() + (size_t)d * SEC_PER_DEST);
+        const size_t sz = blob_layout(tot[d], nvc, nv, cnt.data(), sec.data() + (size_t)d * SEC_PER_DEST);
         for (int k = 0; k < SEC_PER_DEST; ++k) sec[(size_t)d * SEC_PER_DEST + k] += total;
         uint64_t* hd = h->send_hdr.data() + (size_t)d * hdr_words;
-        hd[0] = 0xAD5EC0DFull; hd[1] = tot[d]; hd[2] = (uint64_t)nvc;
+        hd[0] = 0xAD5EC0DFull; hd[1] = tot[d]; hd[2] = (uint64_t)nvc | ((uint64_t)(nvc - 2 * nv) << 16);
         for (int c = 0; c < 3 * nvc; ++c) hd[3 + c] = cnt[c];
         base[d] = total;
         h->send_sizes[d] = sz;
@@ -1978,9 +1998,10 @@ int ad_shard_export(ad_handle* h, uint64_t* bytes /* [world] */) {
         fa.K = K; fa.nvc = nvc; fa.list = list; fa.dest = h->hstore; fa.totals = xtot; fa.gid = h->gid; fa.bnd = bnd;
         fa.sec = dsec; fa.send = h->send; fa.o = o;
         for (int c = 0; c < nvc; ++c) {
-            const Csr& x = h->deps[c];
+            const Csr& x = export_csr(h, c);
             fa.key_off[c] = x.key_off; fa.keys[c] = x.keys; fa.k2t_off[c] = x.k2t_off; fa.k2t[c] = x.k2t;
             fa.ent_off[c] = x.ent_off; fa.tcnt[c] = x.tcnt; fa.txns[c] = x.txns;
+            fa.kw[c] = c >= 2 * nv ? 2 : 1;
         }
         k_export_fill<<<ceil_div((long)K, 256), 256, 0, st>>>(fa);
     }
@@ -1999,35 +2020,41 @@ int ad_shard_send_to_host(ad_handle* h, void* dst) {
 
 // Views into the received per-source blobs (concatenated in source order, sizes[s] bytes each).
 static int parse_recv(ad_handle* h, const uint64_t* sizes) {
-    const int nvc = 2 * (int)h->cfg.replicas;
-    const size_t hdr_words = 3 + 3 * (size_t)nvc;
+    const int nv = (int)h->cfg.replicas, nvc2 = 2 * nv, nvc3 = 3 * nv;
     const uint32_t W = h->world;
     std::vector<size_t> off(W, 0);
     for (uint32_t s = 1; s < W; ++s) off[s] = off[s - 1] + sizes[s - 1];
-    std::vector<uint64_t> hdr(hdr_words * W, 0);
+    // the header's first three words (magic, rows, nvc), then the per-vc counts of its nvc classes
+    const size_t hdr_max = 3 + 3 * (size_t)nvc3;
+    std::vector<uint64_t> hdr(hdr_max * W, 0);
     for (uint32_t s = 0; s < W; ++s) {
-        if (sizes[s] < hdr_words * 8) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": truncated");
-        HIPCHK(h, hipMemcpyAsync(hdr.data() + s * hdr_words, h->recv + off[s], hdr_words * 8, hipMemcpyDeviceToHost, h->st));
+        if (sizes[s] < (3 + 3 * (size_t)nvc2) * 8) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": truncated");
+        HIPCHK(h, hipMemcpyAsync(hdr.data() + s * hdr_max, h->recv + off[s], std::min<size_t>(hdr_max * 8, sizes[s]),
+                                 hipMemcpyDeviceToHost, h->st));
     }
     HIPCHK(h, hipStreamSynchronize(h->st));
-    h->src_csr.assign((size_t)W * nvc, Csr{});
+    h->src_csr.assign((size_t)W * nvc3, Csr{});
     h->src_gid.assign(W, nullptr);
     h->src_n.assign(W, 0);
+    h->src_ranges.assign(W, 0);
     for (uint32_t s = 0; s < W; ++s) {
-        const uint64_t* hd = hdr.data() + s * hdr_words;
-        if (hd[0] != 0xAD5EC0DFull || hd[2] != (uint64_t)nvc)
+        const uint64_t* hd = hdr.data() + s * hdr_max;
+        const int nvc = (int)(hd[2] & 0xFFFF);
+        if (hd[0] != 0xAD5EC0DFull || (hd[2] != (uint64_t)nvc2 && hd[2] != ((uint64_t)nvc3 | ((uint64_t)nv << 16))))
             return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": bad header (replicas must match)");
+        if (sizes[s] < (3 + 3 * (size_t)nvc) * 8) return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + ": truncated");
+        h->src_ranges[s] = nvc == nvc3 ? 1 : 0;
         const size_t rows = hd[1];
         std::vector<uint32_t> cnt((size_t)3 * nvc);
         for (int c = 0; c < 3 * nvc; ++c) cnt[c] = (uint32_t)hd[3 + c];
         std::vector<uint64_t> sec(SEC_PER_DEST, 0);
-        if (blob_layout(rows, nvc, cnt.data(), sec.data()) > sizes[s])
+        if (blob_layout(rows, nvc, nv, cnt.data(), sec.data()) > sizes[s])
             return set_err(h, AD_ERR_ARGUMENT, "shard blob " + std::to_string(s) + " exceeds its size");
         uint8_t* b = h->recv + off[s];
         h->src_gid[s] = (uint32_t*)(b + sec[0]);
         h->src_n[s] = (uint32_t)rows;
         for (int c = 0; c < nvc; ++c) {
-            Csr& x = h->src_csr[(size_t)s * nvc + c];
+            Csr& x = h->src_csr[(size_t)s * nvc3 + c];
             x.nkeys = cnt[3 * c]; x.nk2t = cnt[3 * c + 1]; x.ncap = cnt[3 * c + 2];
             x.key_off = (uint32_t*)(b + sec[1 + 7 * c]); x.k2t_off = (uint32_t*)(b + sec[2 + 7 * c]);
             x.ent_off = (uint32_t*)(b + sec[3 + 7 * c]); x.tcnt = (uint32_t*)(b + sec[4 + 7 * c]);
@@ -2115,7 +2142,9 @@ int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
     const size_t n = h->n;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     if (h->world > (uint32_t)MAXV) return set_err(h, AD_ERR_UNSUPPORTED, "more than 8 shards");
-    if (h->src_csr.size() != (size_t)h->world * nvc) return set_err(h, AD_ERR_STATE, "ad_shard_merge: exchange the blobs first");
+    if (h->src_csr.size() != (size_t)h->world * 3 * nv) return set_err(h, AD_ERR_STATE, "ad_shard_merge: exchange the blobs first");
+    bool ranges = false;
+    for (uint32_t s = 0; s < h->world; ++s) ranges |= h->src_ranges[s] != 0;
     // home rows + global ids
     CK(dalloc(h, S_HROWS, &h->home_rows, n + 1));
     uint32_t* tot = nullptr;
@@ -2129,37 +2158,48 @@ int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
     h->H = H;
     CK(dalloc(h, S_HGID, &h->home_gid, H));
     CK(dalloc(h, S_SROWS, &h->src_rows, H * h->world));
+    if (ranges) {
+        CK(dalloc(h, S_NONEROWS, &h->none_rows, std::max<size_t>(H, 1)));
+        if (H) HIPCHK(h, hipMemsetAsync(h->none_rows, 0xFF, H * 4, st));
+    }
     if (H) {
         k_home_gid<<<ceil_div((long)H, 256), 256, 0, st>>>(H, h->home_rows, h->gid, h->home_gid);
         for (uint32_t s = 0; s < h->world; ++s)
             k_source_rows<<<ceil_div((long)H, 256), 256, 0, st>>>(H, h->home_gid, h->src_gid[s], h->src_n[s], h->src_rows + s * H);
     }
-    // per (view, class): union over sources
+    // per (view, class): union over sources (PartialDeps.with); RangeDeps from the sources that carry them
+    // (a source without range classes holds no range dependency: its rows are all absent)
     h->sdeps.resize(nvc);
-    std::vector<Csr*> out(nvc);
-    std::vector<size_t> blocks(nvc);
-    std::vector<int> kw(nvc, 1);
-    std::vector<std::array<const Csr*, MAXV>> in(nvc);
-    std::vector<std::array<const int32_t*, MAXV>> rows(nvc);
-    for (int vc = 0; vc < nvc; ++vc) {
-        out[vc] = &h->sdeps[vc];
-        blocks[vc] = CSR_SHARD0 + vc;
-        for (uint32_t s = 0; s < h->world; ++s) {
-            in[vc][s] = &h->src_csr[(size_t)s * nvc + vc];
-            rows[vc][s] = h->src_rows + s * H;
+    for (int pass = 0; pass < (ranges ? 2 : 1); ++pass) {
+        const int nx = pass == 0 ? nvc : nv, v0 = pass == 0 ? 0 : nvc;
+        std::vector<Csr*> out(nx);
+        std::vector<size_t> blocks(nx);
+        std::vector<int> kw(nx, pass == 0 ? 1 : 2);
+        std::vector<std::array<const Csr*, MAXV>> in(nx);
+        std::vector<std::array<const int32_t*, MAXV>> rows(nx);
+        for (int k = 0; k < nx; ++k) {
+            const int vc = v0 + k;
+            out[k] = pass == 0 ? &h->sdeps[vc] : &h->srdeps[k];
+            blocks[k] = pass == 0 ? CSR_SHARD0 + vc : CSR_SRANGE0 + k;
+            for (uint32_t s = 0; s < h->world; ++s) {
+                in[k][s] = &h->src_csr[(size_t)s * 3 * nv + vc];
+                rows[k][s] = (pass == 0 || h->src_ranges[s]) ? h->src_rows + s * H : h->none_rows;
+            }
         }
+        CK(merge_multi(h, H, nx, out.data(), blocks.data(), kw.data(),
+                       reinterpret_cast<const Csr* const (*)[MAXV]>(in.data()),
+                       reinterpret_cast<const int32_t* const (*)[MAXV]>(rows.data()), (int)h->world, nullptr));
     }
-    CK(merge_multi(h, H, nvc, out.data(), blocks.data(), kw.data(),
-                   reinterpret_cast<const Csr* const (*)[MAXV]>(in.data()),
-                   reinterpret_cast<const int32_t* const (*)[MAXV]>(rows.data()), (int)h->world, nullptr));
-    // Deps.merge across views (key, direct); RangeDeps are empty in sharded mode
-    Csr* mout[2] = {&h->smerged[0], &h->smerged[1]};
-    size_t mblocks[2] = {CSR_SMERGED0, CSR_SMERGED0 + 1};
-    int mkw[2] = {1, 1};
-    const Csr* min_[2][MAXV] = {};
-    for (int v = 0; v < nv; ++v) { min_[0][v] = &h->sdeps[2 * v]; min_[1][v] = &h->sdeps[2 * v + 1]; }
+    // Deps.merge across views (key, direct, and range when any store held range txns)
+    const int mc = ranges ? 3 : 2;
+    Csr* mout[3] = {&h->smerged[0], &h->smerged[1], &h->smerged[2]};
+    size_t mblocks[3] = {CSR_SMERGED0, CSR_SMERGED0 + 1, CSR_SMERGED0 + 2};
+    int mkw[3] = {1, 1, 2};
+    const Csr* min_[3][MAXV] = {};
+    for (int v = 0; v < nv; ++v) { min_[0][v] = &h->sdeps[2 * v]; min_[1][v] = &h->sdeps[2 * v + 1]; min_[2][v] = &h->srdeps[v]; }
     uint64_t ent = 0;
-    CK(merge_multi(h, H, 2, mout, mblocks, mkw, min_, nullptr, nv, &ent));
+    CK(merge_multi(h, H, mc, mout, mblocks, mkw, min_, nullptr, nv, &ent));
+    h->shard_ranges = ranges;
     h->merged_entries = ent;
     h->times.merged_entries = ent;
     if (n_home) *n_home = H;
@@ -2170,7 +2210,12 @@ int ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes, size_t* n_home) {
                 const Csr& x = v < nv ? h->sdeps[2 * v + c] : h->smerged[c];
                 sizes[v * 3 + c] = ad_csr_sizes{H, x.nkeys, x.nk2t, x.ncap, x.ncap};
             }
-            sizes[v * 3 + 2] = ad_csr_sizes{H, 0, 0, 0, 0};
+            if (ranges) {
+                const Csr& x = v < nv ? h->srdeps[v] : h->smerged[2];
+                sizes[v * 3 + 2] = ad_csr_sizes{H, x.nkeys, x.nk2t, x.ncap, x.ncap};
+            } else {
+                sizes[v * 3 + 2] = ad_csr_sizes{H, 0, 0, 0, 0};
+            }
         }
     }
     return AD_OK;
@@ -2183,7 +2228,8 @@ int ad_shard_fetch(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out, u
     const size_t n_saved = h->n;
     h->n = h->H;                          // fetch_csr / fetch_empty work over the home txns
     int rc;
-    if (cls == AD_CLASS_RANGE) rc = fetch_empty(h, out);
+    if (cls == AD_CLASS_RANGE && !h->shard_ranges) rc = fetch_empty(h, out);
+    else if (cls == AD_CLASS_RANGE) rc = fetch_csr(h, view < h->cfg.replicas ? h->srdeps[view] : h->smerged[2], 2, out);
     else rc = fetch_csr(h, view < h->cfg.replicas ? h->sdeps[2 * view + cls] : h->smerged[cls], 1, out);
     h->n = n_saved;
     if (rc == AD_OK && home_gid && h->H) {
@@ -2199,11 +2245,16 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     if (!h || !changed) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_levels_round: sharded deps first");
-    if (h->n_special)
-        return set_err(h, AD_ERR_UNSUPPORTED, "sharded levels: sync points / ephemeral reads wait on merged deps homed elsewhere");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
     const size_t n = h->n;
+    // Unmanaged txns (range txns, key-domain sync points / ephemeral reads) and the key txns depending on range
+    // txns also wait on their merged deps: rules (b) and (c).  Every such constraint is local to one store — a
+    // dependency edge T -> D comes from a key or range slice both hold, a (c) bound from one key's chain — so
+    // each store applies the ones it holds from the Deps.merge of its own replica views (the global merged
+    // deps restricted to its keys), computed once per batch.
+    const bool mixed = h->Q > 0 || h->n_special > 0 || h->n_large > 0;
+    if (first && mixed) CK(stage_merge(h));
     CK(dalloc(h, S_G, &h->G, h->n_global + 1));
     uint32_t* flag = nullptr;
     CK(dalloc(h, S_NE, &flag, 16));
@@ -2214,8 +2265,14 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     li.seg_start = h->seg_start; li.sval = h->sval; li.nh = h->nh; li.prm = h->prm; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;
-    li.n_large = 0;
-    li.n_special = 0;
+    if (mixed) {
+        if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_shard_levels_round: first round missing");
+        li.merged_key = &h->merged[AD_CLASS_KEY];
+        li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
+        li.merged_range = &h->merged[AD_CLASS_RANGE];
+    }
+    li.n_large = mixed ? h->n_large : 0;
+    li.n_special = mixed ? h->n_special : 0;
     li.exec_bits = h->pack.total_bits;
     li.keep_levels = first ? 0 : 1;
     int iters = 0;

@@ -89,6 +89,7 @@ struct RangeArgs {
     uint64_t* keys_v[MAXV];      // (start, end) interleaved
     int32_t* k2t_v[MAXV];
     const uint32_t* qpos;        // executeAt-bound queries: per txn the bound's arrival position (nullable)
+    const uint32_t* gid;         // sharded stores: local row -> global arrival rank (window, drops; nullable)
 };
 
 // does entry [s, e) intersect txn t's footprint (sorted keys, or sorted disjoint ranges)?
@@ -121,7 +122,10 @@ __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
     const uint32_t fe = key_dom ? a.key_off[i + 1] : a.range_off[i + 1];
     // the arrival position the query is answered at (PreAccept: i; Accept: its executeAt's), the window below it
     const uint32_t qi = a.qpos ? a.qpos[i] : i;
-    const uint32_t lo_w = a.window == 0 ? qi : (qi > a.window ? qi - a.window : 0u);
+    // window and drop decisions use global arrival ranks (shard-invariant); emitted ids stay local rows
+    const uint32_t gi = a.gid ? a.gid[i] : i;
+    const uint32_t gq = a.qpos ? qi : gi;
+    const uint32_t lo_w = a.window == 0 ? gq : (gq > a.window ? gq - a.window : 0u);
     uint32_t ecount[NV], kcount[NV];
     uint64_t cs[NV], ce[NV];
     bool chas[NV];
@@ -142,13 +146,14 @@ __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
             const uint32_t x = clo + lane;
             const bool valid = x < chi;
             uint64_t s = 0, e = 0;
-            uint32_t j = 0xFFFFFFFFu;
+            uint32_t j = 0xFFFFFFFFu, gj = 0xFFFFFFFFu;
             bool cond = false;
             if (valid) {
                 j = a.eown[x];
                 if (j < qi && j != i) {
                     const uint32_t mj = a.meta[j];
-                    const bool inw = j >= lo_w;
+                    gj = a.gid ? a.gid[j] : j;
+                    const bool inw = gj >= lo_w;
                     cond = witnesses(qk, meta_kind(mj)) && (inw || meta_status(mj) != AD_ST_INVALID);
                     if (cond) {
                         s = a.es[x];
@@ -157,10 +162,10 @@ __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
                     }
                 }
             }
-            const bool inw = j >= lo_w;
+            const bool inw = gj >= lo_w;
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                const bool ok = cond && !(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh);
+                const bool ok = cond && !(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh);
                 const uint64_t mask = __ballot(ok);
                 if (mask == 0) continue;
                 const uint64_t lower = mask & below;

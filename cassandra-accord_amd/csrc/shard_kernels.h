@@ -36,10 +36,12 @@ struct CompactFlagOp {            // rows with flag -> out[] (exclusive-scan sca
 
 // ---- export: rows with deps, partitioned by destination store ----------------------------------------
 constexpr int MAX_STORES = 8;
+// CSRs per exported row: per view key + direct (2R), and with range txns RangeDeps per view (R more)
+constexpr int NVX_MAX = 3 * MAXV;
 struct DestOp {                       // per row: rank among the kept rows of its destination
     struct S { uint32_t c[MAX_STORES]; };
     const uint8_t* dest;
-    const uint32_t* tcnt[NVC_MAX];    // per (view, class): per-row unique TxnId counts
+    const uint32_t* tcnt[NVX_MAX];    // per (view, class): per-row unique TxnId counts
     int nvc;
     uint32_t* rank;                   // [n] rank within destination, or ~0u (no deps: not exported)
     uint32_t* totals;                 // [MAX_STORES]
@@ -111,7 +113,7 @@ struct ExportOffsetsOp {
     }
 };
 // the global offsets at every destination boundary: out[(d * nvc + c) * 3 + {0,1,2}], d = 0..world
-struct ExportOffs { uint32_t* ok[NVC_MAX]; uint32_t* om[NVC_MAX]; uint32_t* ot[NVC_MAX]; };
+struct ExportOffs { uint32_t* ok[NVX_MAX]; uint32_t* om[NVX_MAX]; uint32_t* ot[NVX_MAX]; };
 __global__ void k_export_bounds(int world, int nvc, const uint32_t* __restrict__ totals, ExportOffs o, uint32_t* __restrict__ out) {
     const int i = threadIdx.x;
     if (i >= (world + 1) * nvc) return;
@@ -124,7 +126,8 @@ __global__ void k_export_bounds(int world, int nvc, const uint32_t* __restrict__
 }
 // Destination blob sections (byte offsets from the send buffer base), per destination:
 // [0] gid, then per vc: [1+7c] key_off [2+7c] k2t_off [3+7c] ent_off [4+7c] tcnt [5+7c] keys [6+7c] k2t [7+7c] txns
-constexpr int SEC_PER_DEST = 1 + 7 * NVC_MAX;
+// (vc < 2R: key / direct class of view vc/2, keys 8 B; vc >= 2R: RangeDeps of view vc-2R, ranges 16 B)
+constexpr int SEC_PER_DEST = 1 + 7 * NVX_MAX;
 struct ExportFillArgs {
     size_t K;
     int nvc;
@@ -135,13 +138,14 @@ struct ExportFillArgs {
     const uint32_t* bnd;              // k_export_bounds output
     const uint64_t* sec;              // [MAX_STORES * SEC_PER_DEST]
     uint8_t* send;
-    const uint32_t* key_off[NVC_MAX];
-    const uint64_t* keys[NVC_MAX];
-    const uint32_t* k2t_off[NVC_MAX];
-    const int32_t* k2t[NVC_MAX];
-    const uint32_t* ent_off[NVC_MAX];
-    const uint32_t* tcnt[NVC_MAX];
-    const uint32_t* txns[NVC_MAX];
+    const uint32_t* key_off[NVX_MAX];
+    const uint64_t* keys[NVX_MAX];
+    const uint32_t* k2t_off[NVX_MAX];
+    const int32_t* k2t[NVX_MAX];
+    const uint32_t* ent_off[NVX_MAX];
+    const uint32_t* tcnt[NVX_MAX];
+    const uint32_t* txns[NVX_MAX];
+    int kw[NVX_MAX];                  // u64 words per key (2: a range)
     ExportOffs o;
 };
 // one thread per exported row: its gid, rebased offsets, and its keys / keysToTxnIds / TxnIds (as global
@@ -172,7 +176,8 @@ __global__ __launch_bounds__(256) void k_export_fill(ExportFillArgs a) {
         const uint32_t st = a.ent_off[c][r], nt = a.tcnt[c][r];
         key_off[i] = kb; k2t_off[i] = mb; ent_off[i] = tb; tcnt[i] = nt;
         if (last) { key_off[i + 1] = kb + nk; k2t_off[i + 1] = mb + nm; ent_off[i + 1] = tb + nt; }
-        for (uint32_t x = 0; x < nk; ++x) keys[kb + x] = a.keys[c][sk + x];
+        const uint32_t w = (uint32_t)a.kw[c];
+        for (uint32_t x = 0; x < nk * w; ++x) keys[(size_t)kb * w + x] = a.keys[c][(size_t)sk * w + x];
         for (uint32_t x = 0; x < nm; ++x) k2t[mb + x] = a.k2t[c][sm + x];
         for (uint32_t x = 0; x < nt; ++x) txns[tb + x] = a.gid[a.txns[c][st + x]];
     }
