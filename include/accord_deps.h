@@ -348,9 +348,14 @@ int  ad_cfk_rows(ad_handle* h, size_t* hist_rows /* out */, uint32_t* gid /* [n]
 /*   ad_shard_levels_deltas / ad_shard_levels_apply over a host transport; repeat until no      */
 /*   store sent a pair.  Dense variant (no holders set): all-reduce(max) of the whole global    */
 /*   level array (ad_shard_levels_allreduce, or _get/_set).  Then ad_shard_order.               */
-/* Home txn = its first key lies in this store's range; results are per home txn, TxnIds as    */
-/* global ranks.  Range txns are not supported in sharded mode (AD_ERR_UNSUPPORTED).  At most 8 */
-/* stores.                                                                                     */
+/* Home txn = its first key (a range txn: its first range's first key, start + 1) lies in this  */
+/* store's range; results are per home txn, TxnIds as global ranks.  Range txns: the host       */
+/* slices each range to the store, (max(start, lo-1), min(end, hi-1)] for keys [lo, hi)         */
+/* (InMemoryCommandStore.java:758-761); blobs then carry RangeDeps per view (header word         */
+/* nvc | nr << 16), and ad_shard_fetch(AD_CLASS_RANGE) returns the store-sliced RangeDeps.      */
+/* Range txns, sync points and ephemeral reads take their (b)/(c) level constraints from the    */
+/* store's own Deps.merge of its views (first level round).  ad_max_conflicts is refused on a   */
+/* sharded batch with range txns (AD_ERR_UNSUPPORTED).  At most 8 stores.                       */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_shard_bounds(const uint64_t* keys, size_t nkeys, uint32_t shards, uint64_t* bounds_out /* [shards+1] */);
 int  ad_shard_setup(ad_handle* h, const uint32_t* gid /* [n] ascending */, const uint8_t* home_store /* [n] */,
