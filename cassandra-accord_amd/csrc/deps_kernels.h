@@ -623,6 +623,7 @@ __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
 constexpr uint32_t MERGE_HEAVY_HINT = 256;
 template <int NVC>
 struct OffsetsOp {
+    static_assert(NVC % 2 == 0, "key + direct class per view: NVC = 2R");
     struct S { uint32_t k[NVC], e[NVC]; };
     size_t n;
     const uint8_t* meta;
@@ -660,13 +661,16 @@ struct OffsetsOp {
             return s;
         }
         const uint32_t b = key_off[t], e = key_off[t + 1];
-        const uint32_t* src = cnt;
+        // a pair's NVC counts are contiguous and 8-byte aligned (NVC = 2R): dwordx2 loads
         for (uint32_t x = b; x < e; ++x) {
+            const uint2* p = reinterpret_cast<const uint2*>(cnt + (size_t)x * NVC);
 #pragma unroll
-            for (int c = 0; c < NVC; ++c) {
-                const uint32_t v = src[(size_t)x * NVC + c];
-                s.k[c] += v > 0 ? 1u : 0u;
-                s.e[c] += v;
+            for (int c2 = 0; c2 < NVC / 2; ++c2) {
+                const uint2 v = p[c2];
+                s.k[2 * c2] += v.x > 0 ? 1u : 0u;
+                s.e[2 * c2] += v.x;
+                s.k[2 * c2 + 1] += v.y > 0 ? 1u : 0u;
+                s.e[2 * c2 + 1] += v.y;
             }
         }
         return s;
@@ -698,6 +702,43 @@ struct OffsetsOp {
         const uint32_t b = key_off[t], e = key_off[t + 1];
         const uint32_t* src = cnt;
         uint32_t* d = dst;
+        if (e - b <= 4) {                 // the counts of up to 4 pairs in registers (dwordx2 loads), one pass
+            uint32_t cv[4][NVC];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint2* p = reinterpret_cast<const uint2*>(src + (size_t)(b + j) * NVC);
+#pragma unroll
+                for (int c2 = 0; c2 < NVC / 2; ++c2) {
+                    const uint2 v = b + j < e ? p[c2] : make_uint2(0u, 0u);
+                    cv[j][2 * c2] = v.x; cv[j][2 * c2 + 1] = v.y;
+                }
+            }
+            uint64_t kx[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) kx[j] = b + j < e ? keys[b + j] : 0ull;
+#pragma unroll
+            for (int c = 0; c < NVC; ++c) {
+                const uint32_t nk = el.k[c];
+                if (nk == 0) continue;
+                const uint32_t kb = ex.k[c], mb = ex.k[c] + ex.e[c];
+                if (kb + nk > cap_keys[c] || mb + nk + el.e[c] > cap_k2t[c]) {
+                    if (*(volatile uint32_t*)overflow == 0u) *(volatile uint32_t*)overflow = 1u;
+                    continue;
+                }
+                uint32_t run = nk, kk = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t cc = cv[j][c];
+                    if (cc == 0) continue;
+                    out_keys[c][kb + kk] = kx[j];
+                    d[(size_t)(b + j) * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
+                    run += cc;
+                    out_k2t[c][mb + kk] = (int32_t)run;
+                    ++kk;
+                }
+            }
+            return;
+        }
         for (int c = 0; c < NVC; ++c) {
             const uint32_t nk = el.k[c];
             if (nk == 0) continue;

@@ -626,6 +626,25 @@ constexpr int KAHN_GRID = 2048;
 __device__ inline void kahn_release(uint32_t s, uint32_t lvl, uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
     if (atomicSub(&rem[s], 1u) == 1u) { L[s] = lvl + 1; released = true; }
 }
+// Release ids[x] for x = b, b + stride, ... < e, KR_ILP at a time: the id loads, then the returning atomics, then
+// the checks, so a lane keeps KR_ILP memory round trips in flight instead of one.  A wavefront lasts as long as
+// its longest serial release chain (a Write followed by several Reads, a range txn's thousands of dependants):
+// one atomic round trip per successor made those chains the kernel time.
+constexpr int KR_ILP = 8;
+template <class I>
+__device__ inline void kahn_release_run(const uint32_t* __restrict__ ids, I b, I e, I stride, uint32_t lvl,
+                                        uint32_t* __restrict__ rem, uint32_t* __restrict__ L, bool& released) {
+    for (I x = b; x < e; x += stride * (I)KR_ILP) {
+        uint32_t sv[KR_ILP], rv[KR_ILP];
+#pragma unroll
+        for (int u = 0; u < KR_ILP; ++u) { const I y = x + (I)u * stride; sv[u] = y < e ? ids[y] : 0u; }
+#pragma unroll
+        for (int u = 0; u < KR_ILP; ++u) { const I y = x + (I)u * stride; rv[u] = y < e ? atomicSub(&rem[sv[u]], 1u) : 0u; }
+#pragma unroll
+        for (int u = 0; u < KR_ILP; ++u)
+            if (rv[u] == 1u) { L[sv[u]] = lvl + 1; released = true; }
+    }
+}
 // ---------------------------------------------------------------------------------------------------
 // Kahn chain build for batches with long chains (C3's Zipf hot keys: ~10^5 entries on one key), all
 // positions in parallel instead of one thread per segment:
@@ -775,11 +794,11 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
                     if (sc[j].y && rr[j] == 1u) { L[sx[j]] = lvl + 1; released = true; }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    for (uint32_t x = sc[j].x + 1; x < sc[j].x + sc[j].y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+                    if (sc[j].y > 1) kahn_release_run<uint32_t>(c_txn, sc[j].x + 1, sc[j].x + sc[j].y, 1u, lvl, rem, L, released);
             } else {
                 for (uint32_t p = b; p < e; ++p) {
                     const uint2 sc = succ[p];
-                    for (uint32_t x = sc.x; x < sc.x + sc.y; ++x) kahn_release(c_txn[x], lvl, rem, L, released);
+                    if (sc.y) kahn_release_run<uint32_t>(c_txn, sc.x, sc.x + sc.y, 1u, lvl, rem, L, released);
                 }
             }
         }
@@ -788,7 +807,7 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
             if (mine) { xb = xoff[t]; xe = xoff[t + 1]; }
             const bool heavy = xe - xb > XLIGHT;
             if (mine && !heavy)
-                for (uint64_t j = xb; j < xe; ++j) kahn_release(xs[j], lvl, rem, L, released);
+                kahn_release_run<uint64_t>(xs, xb, xe, 1ull, lvl, rem, L, released);
             uint64_t hm = __ballot(heavy);
             while (hm) {
                 const int l = __ffsll((unsigned long long)hm) - 1;
@@ -797,7 +816,7 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)xb, l);
                 const uint64_t e0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(xe >> 32), l) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)xe, l);
-                for (uint64_t j = b0 + __lane_id(); j < e0; j += WAVE) kahn_release(xs[j], lvl, rem, L, released);
+                kahn_release_run<uint64_t>(xs, b0 + __lane_id(), e0, (uint64_t)WAVE, lvl, rem, L, released);
             }
         }
     }
