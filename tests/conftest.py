@@ -13,8 +13,10 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
 
 
-@pytest.fixture(scope="session")
+@pytest.fixture
 def engine_factory():
+    """Engines made by one test, closed when it ends: a session-long handle keeps its device arena (the full-size
+    tests hold tens of GB each), so later tests would run out of HBM."""
     from accord_amd import engine
 
     made = []
