@@ -434,8 +434,9 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         if (FILL) {
-            c0[v] = a.dst[pb + 2 * v];          // last slot of the pair's run (filled descending)
-            c1[v] = a.dst[pb + 2 * v + 1];
+            const uint2 d = reinterpret_cast<const uint2*>(a.dst + pb)[v];   // last slots of the pair's runs (filled descending)
+            c0[v] = d.x;
+            c1[v] = d.y;
         } else {
             c0[v] = 0; c1[v] = 0;
         }
@@ -467,10 +468,7 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     }
     if (!FILL) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            a.cnt[pb + 2 * v] = c0[v];
-            a.cnt[pb + 2 * v + 1] = c1[v];
-        }
+        for (int v = 0; v < NV; ++v) reinterpret_cast<uint2*>(a.cnt + pb)[v] = make_uint2(c0[v], c1[v]);
     }
 }
 

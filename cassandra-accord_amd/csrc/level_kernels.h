@@ -25,6 +25,9 @@
 //      the critical path (C2: ~9).
 //   5. order: LSD radix sorts by executeAt (64-bit, two 32-bit halves) then stably by level.
 #pragma once
+#include <chrono>
+#include <cstring>
+
 #include "radix_sort.h"
 #include "union_kernels.h"
 #include "block_levels.h"
@@ -968,8 +971,56 @@ __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
     if (!FILL && local) atomicAdd(&a.indeg[t], local);
 }
 
+// Small device results to the host without a stream sync (the engine's host-mapped coherent buffer, see
+// engine.hip read_totals_params): copy a[0..na) and b[0..nb) to pub[off..], fence, bump pub[0] = seq.
+__global__ __launch_bounds__(128) void k_publish2(const uint32_t* __restrict__ a, int na, const uint32_t* __restrict__ b, int nb,
+                                                  uint32_t* pub, int off, uint32_t seq) {
+    const int i = threadIdx.x;
+    if (i < na) pub[off + i] = a[i];
+    if (i < nb) pub[off + na + i] = b[i];
+    __syncthreads();
+    if (i == 0) {
+        __threadfence_system();
+        __hip_atomic_store(pub, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+struct Publisher {
+    uint32_t* host = nullptr;           // mapped coherent host words ([0] = sequence)
+    uint32_t* dev = nullptr;
+    uint32_t* seq = nullptr;            // the owner's sequence counter
+    int off = 0, cap = 0;               // the words this user may write: [off, off + cap)
+};
+// a[0..na) -> ha, b[0..nb) -> hb, waiting on the mapped buffer (else a copy + stream sync)
+inline bool publish_read(const Publisher& p, hipStream_t st, const uint32_t* a, int na, uint32_t* ha,
+                         const uint32_t* b, int nb, uint32_t* hb) {
+    if (!p.host || na + nb > p.cap || na > 128 || nb > 128) {
+        if (na && hipMemcpyAsync(ha, a, (size_t)na * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+        if (nb && hipMemcpyAsync(hb, b, (size_t)nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+        return hipStreamSynchronize(st) == hipSuccess;
+    }
+    const uint32_t seq = ++*p.seq;
+    k_publish2<<<1, 128, 0, st>>>(a, na, b, nb, p.dev, p.off, seq);
+    uint64_t spins = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(p.host, __ATOMIC_ACQUIRE) != seq) {
+        if ((++spins & 0x3FF) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q != hipSuccess && q != hipErrorNotReady) return false;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                if (hipStreamSynchronize(st) != hipSuccess) return false;
+                if (__atomic_load_n(p.host, __ATOMIC_ACQUIRE) != seq) return false;
+                break;
+            }
+        }
+    }
+    if (na) std::memcpy(ha, p.host + p.off, (size_t)na * 4);
+    if (nb) std::memcpy(hb, p.host + p.off + na, (size_t)nb * 4);
+    return true;
+}
+
 struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
+    Publisher pub;                      // set by the engine: flag read-backs without a stream sync
     int kb_hint = 0;                    // wavefronts in the first Kahn launch batch (previous depth + 1)
     uint32_t* c_txn = nullptr;
     uint8_t* c_meta = nullptr;
@@ -1508,9 +1559,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                                                         k == 0 ? ls.flags + 7 : ls.iflags + (k - 1), k == 0, ls.iflags + k,
                                                         xedges ? (const uint64_t*)ls.xoff : nullptr, xedges ? ls.xs : nullptr);
                     uint32_t fh[KB_MAX];
-                    if (hipMemcpyAsync(fh, ls.iflags, KB * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        (lv == 0 && hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-                        hipStreamSynchronize(st) != hipSuccess) {
+                    if (!publish_read(ls.pub, st, ls.iflags, KB, fh, ls.flags, lv == 0 ? 8 : 0, host)) {
                         err = "exec levels: device error";
                         return AD_ERR_DEVICE;
                     }
