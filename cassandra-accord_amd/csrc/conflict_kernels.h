@@ -157,9 +157,18 @@ struct McRangeArgs {
     RangeIndex ix;
     uint32_t window, thresh;
     uint64_t seed;
-    uint32_t* max_rank;        // [v * n + t] folded in place (batch rows: range batches are not sharded)
+    uint32_t* max_rank;        // [v * n + t] batch rows, folded in place (sharded: the local-row answers,
+                               // turned into global ranks by k_mc_globalize afterwards)
     uint8_t* fast;
+    const uint32_t* gid;       // sharded stores: local row -> global arrival rank (window, drops; nullable)
 };
+
+// sharded stores: the folded local-row answers -> global ranks
+__global__ __launch_bounds__(256) void k_mc_globalize(size_t m, const uint32_t* __restrict__ local,
+                                                      const uint32_t* __restrict__ gid, uint32_t* __restrict__ rank) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < m) rank[x] = local[x] == AD_RANK_NONE ? AD_RANK_NONE : gid[local[x]];
+}
 
 // wave max of (e, r) per view; lane 0 folds it into the txn's answer and redoes the fast-path test
 template <int NV>
@@ -190,7 +199,8 @@ template <int NV>
 __global__ __launch_bounds__(256) void k_mc_range_keys(McRangeArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n || meta_domain(a.meta[t]) != AD_DOMAIN_RANGE) return;
-    const uint32_t lo_w = a.window == 0 ? (uint32_t)t : ((uint32_t)t > a.window ? (uint32_t)t - a.window : 0u);
+    const uint32_t gi = a.gid ? a.gid[t] : (uint32_t)t;     // window and drops: global arrival ranks
+    const uint32_t lo_w = a.window == 0 ? gi : (gi > a.window ? gi - a.window : 0u);
     uint64_t be[NV];
     uint32_t br[NV];
 #pragma unroll
@@ -204,12 +214,13 @@ __global__ __launch_bounds__(256) void k_mc_range_keys(McRangeArgs a) {
             int x = pos - 1;
             for (; x >= s0; --x) {                 // in-flight window: per view unless dropped
                 const uint32_t j = a.e_txn[x];
-                if (j < lo_w) break;
+                const uint32_t gj = a.gid ? a.gid[j] : j;
+                if (gj < lo_w) break;
                 if (!manages(a.e_meta[x])) continue;
                 const uint64_t e = a.e_exec1[x];
 #pragma unroll
                 for (int v = 0; v < NV; ++v)
-                    if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, (uint32_t)t, j) < a.thresh) && mc_less(be[v], br[v], e, j)) {
+                    if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh) && mc_less(be[v], br[v], e, j)) {
                         be[v] = e; br[v] = j;
                     }
             }
@@ -233,7 +244,8 @@ __global__ __launch_bounds__(256) void k_mc_range_entries(McRangeArgs a) {
     const bool key_dom = meta_domain(a.meta[i]) == AD_DOMAIN_KEY;
     const uint32_t fb = key_dom ? a.key_off[i] : a.range_off[i];
     const uint32_t fe = key_dom ? a.key_off[i + 1] : a.range_off[i + 1];
-    const uint32_t lo_w = a.window == 0 ? i : (i > a.window ? i - a.window : 0u);
+    const uint32_t gi = a.gid ? a.gid[i] : i;
+    const uint32_t lo_w = a.window == 0 ? gi : (gi > a.window ? gi - a.window : 0u);
     const uint32_t Q = (uint32_t)a.Q;
     uint64_t be[NV];
     uint32_t br[NV];
@@ -252,13 +264,14 @@ __global__ __launch_bounds__(256) void k_mc_range_entries(McRangeArgs a) {
         RangeArgs ra{};
         ra.keys = a.keys; ra.rs = a.rs; ra.re = a.re;
         if (!range_hits(ra, key_dom, fb, fe, a.es[x], a.ee[x])) return;
-        const bool inw = j >= lo_w;
+        const uint32_t gj = a.gid ? a.gid[j] : j;
+        const bool inw = gj >= lo_w;
         const uint32_t st = meta_status(mj);
         if (!inw && (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID)) return;
         const uint64_t ej = a.ex1[j];
 #pragma unroll
         for (int v = 0; v < NV; ++v)
-            if (!(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, i, j) < a.thresh) && mc_less(be[v], br[v], ej, j)) {
+            if (!(inw && a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh) && mc_less(be[v], br[v], ej, j)) {
                 be[v] = ej; br[v] = j;
             }
     });

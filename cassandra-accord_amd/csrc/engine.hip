@@ -1297,8 +1297,6 @@ static int fetch_empty(ad_handle* h, ad_csr_out* out) {
 // deps stage left on the device: leaves max_rank / fast (and the batch-local rank) in their slots.
 static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_out, uint32_t** local_out) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
-    if (h->sharded && h->Q > 0)
-        return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts: range footprints answer in batch rows (not in sharded mode)");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     const size_t n = h->n, P = h->P;
@@ -1316,7 +1314,9 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
     CK(dalloc(h, S_MCPE, &pm_e, std::max<size_t>(P, 1))); CK(dalloc(h, S_MCPR, &pm_r, std::max<size_t>(P, 1)));
     CK(dalloc(h, S_MCINV, &inv, std::max<size_t>(P, 1)));
     CK(dalloc(h, S_MCRANK, &rank, std::max<size_t>(n * nv, 1))); CK(dalloc(h, S_MCFAST, &fst, std::max<size_t>(n * nv, 1)));
-    if (local_out) CK(dalloc(h, S_MCLOCAL, &local, std::max<size_t>(n * nv, 1)));
+    // sharded stores with range txns: the range kernels fold local rows, globalised afterwards
+    const bool fold_local = h->Q > 0 && a.gid != nullptr;
+    if (local_out || fold_local) CK(dalloc(h, S_MCLOCAL, &local, std::max<size_t>(n * nv, 1)));
     a.pm_e = pm_e; a.pm_r = pm_r; a.inv = inv; a.max_rank = rank; a.fast = fst; a.local_rank = local;
     if (P > 0) CK(ensure_scratch(h, std::max(h->scratch_cap, device_scan_scratch<MaxConflictOp>(P))));
     if (n > 0) {
@@ -1334,8 +1334,12 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
             ra.ukey = h->ukey; ra.useg = h->useg; ra.U = P ? h->hprm.n_keys_u : 0;
             ra.e_txn = h->e_txn; ra.e_meta = h->e_meta; ra.e_exec1 = h->e_exec1; ra.pm_e = pm_e; ra.pm_r = pm_r;
             ra.Q = h->Q; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
-            ra.window = a.window; ra.thresh = a.thresh; ra.seed = a.seed; ra.max_rank = rank; ra.fast = fst;
+            ra.window = a.window; ra.thresh = a.thresh; ra.seed = a.seed; ra.fast = fst;
+            ra.gid = a.gid;
+            ra.max_rank = fold_local ? local : rank;
             NV_DISPATCH(nv, launch_mc_ranges, ra, st);
+            if (fold_local)
+                k_mc_globalize<<<ceil_div((long)(n * nv), 256), 256, 0, st>>>(n * nv, local, a.gid, rank);
         }
     }
     HIPCHK(h, hipGetLastError());

@@ -354,8 +354,8 @@ int  ad_cfk_rows(ad_handle* h, size_t* hist_rows /* out */, uint32_t* gid /* [n]
 /* (InMemoryCommandStore.java:758-761); blobs then carry RangeDeps per view (header word         */
 /* nvc | nr << 16), and ad_shard_fetch(AD_CLASS_RANGE) returns the store-sliced RangeDeps.      */
 /* Range txns, sync points and ephemeral reads take their (b)/(c) level constraints from the    */
-/* store's own Deps.merge of its views (first level round).  ad_max_conflicts is refused on a   */
-/* sharded batch with range txns (AD_ERR_UNSUPPORTED).  At most 8 stores.                       */
+/* store's own Deps.merge of its views (first level round); ad_max_conflicts answers range      */
+/* footprints per store in global ranks too (fold: sharding.reduce_witnessed).  At most 8 stores.*/
 /* ------------------------------------------------------------------------------------------ */
 int  ad_shard_bounds(const uint64_t* keys, size_t nkeys, uint32_t shards, uint64_t* bounds_out /* [shards+1] */);
 int  ad_shard_setup(ad_handle* h, const uint32_t* gid /* [n] ascending */, const uint8_t* home_store /* [n] */,

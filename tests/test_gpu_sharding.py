@@ -100,6 +100,36 @@ def test_sharded_witnessed_at(engine_factory, name, shards):
             st.close()
 
 
+@pytest.mark.parametrize("shards,window,drop", [(2, 32, 0.1), (3, 8, 0.3), (4, 0, 0.0)])
+def test_sharded_witnessed_at_range_txns(engine_factory, shards, window, drop):
+    # range footprints too (MaxConflicts as a ReducingRangeMap, k_mc_range_keys / k_mc_range_entries): each store
+    # answers for its slices with global-rank windows and drops, the fold equals the unsharded store's answer
+    r, s = 3, 0xC0DE
+    b = workload.generate(20000, 4, 200_000, "uniform", range_frac=0.1, range_width_max=1 << 14, seed=60 + shards)
+    eng = engine_factory(window=window, replicas=r, drop_p=drop, seed=s)
+    eng.load(b)
+    eng.preaccept_deps()
+    want_rank, want_fast = eng.max_conflicts()
+    bounds = sharding.even_bounds(0, 200_000, shards)
+    hs = sharding.home_stores(b, bounds)
+    stores, parts = [], []
+    try:
+        for k in range(shards):
+            local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+            st = sharding.ShardStore(0, window=window, replicas=r, drop_p=drop, seed=s)
+            stores.append(st)
+            st.load(local, gid, hs[gid], b["n"], k, shards)
+            st.preaccept()
+            rank, fast = st.max_conflicts()
+            parts.append((gid, rank.copy(), fast.copy()))
+        got_rank, got_fast, _ = sharding.reduce_witnessed(b, parts)
+        assert np.array_equal(got_rank, want_rank) and np.array_equal(got_fast, want_fast)
+        assert want_fast.min() == 0
+    finally:
+        for st in stores:
+            st.close()
+
+
 def _make_stores(b, shards, w, r, p, s, keyspace, delta=True):
     bounds = sharding.even_bounds(0, keyspace, shards)
     hs = sharding.home_stores(b, bounds)
