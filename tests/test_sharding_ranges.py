@@ -121,3 +121,33 @@ def test_blob_codec_carries_range_classes():
     # header word: nvc | nr << 16
     h = buf[:24].view(np.uint64)
     assert int(h[2]) == 6 | (2 << 16)
+
+
+def test_clip_edges():
+    # (start, end] against the store owning keys [lo, hi): boundary keys belong to exactly one store
+    rs = np.array([0, 9, 10, 5, 19, 0], np.uint64)
+    re = np.array([10, 10, 11, 25, 20, 2**64 - 2], np.uint64)
+    bounds = np.array([0, 10, 20, 2**64 - 1], np.uint64)
+    pieces = []
+    for k in range(3):
+        s, e, keep = sharding._clip_ranges(rs, re, bounds[k], bounds[k + 1])
+        pieces.append([(int(a), int(b)) if m else None for a, b, m in zip(s, e, keep)])
+    # keys 1..10 of (0, 10]: 1..9 in store 0, 10 in store 1
+    assert pieces[0][0] == (0, 9) and pieces[1][0] == (9, 10) and pieces[2][0] is None
+    assert pieces[0][1] is None and pieces[1][1] == (9, 10)           # (9, 10] = key 10 only
+    assert pieces[1][2] == (10, 11) and pieces[0][2] is None
+    assert pieces[0][3] == (5, 9) and pieces[1][3] == (9, 19) and pieces[2][3] == (19, 25)
+    assert pieces[1][4] is None and pieces[2][4] == (19, 20)          # (19, 20] = key 20, store 2
+    assert pieces[2][5] == (19, 2**64 - 2)
+    # every covered key lands in exactly one piece
+    for t in range(5):
+        keys = set(range(int(rs[t]) + 1, int(re[t]) + 1))
+        got = set()
+        for k in range(3):
+            if pieces[k][t]:
+                a, b = pieces[k][t]
+                part = set(range(a + 1, b + 1))
+                assert not (got & part)
+                assert all(int(bounds[k]) <= x < int(bounds[k + 1]) for x in part)
+                got |= part
+        assert got == keys
