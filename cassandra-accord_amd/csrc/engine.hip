@@ -1030,6 +1030,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.exec_bits = h->pack.total_bits;
     li.kahn_ok = h->level_mode != AD_LEVELS_FIXPOINT ? 1 : 0;
     li.force_blocks = h->level_mode == AD_LEVELS_BLOCKS ? 1 : 0;
+    h->ls.pull_off = h->level_mode == AD_LEVELS_KAHN;
     h->ls.bl_rounds = 0;
     h->ls.bl_used = false;
     h->order_pending = false;
@@ -1780,7 +1781,8 @@ int ad_kernel_count(void) { return K_COUNT; }
 const char* ad_kernel_name(int kid) { return kernel_name(kid); }
 
 int ad_set_level_mode(ad_handle* h, int mode) {
-    if (!h || (mode != AD_LEVELS_AUTO && mode != AD_LEVELS_FIXPOINT && mode != AD_LEVELS_BLOCKS)) return AD_ERR_ARGUMENT;
+    if (!h || (mode != AD_LEVELS_AUTO && mode != AD_LEVELS_FIXPOINT && mode != AD_LEVELS_BLOCKS && mode != AD_LEVELS_KAHN))
+        return AD_ERR_ARGUMENT;
     h->level_mode = mode;
     return AD_OK;
 }

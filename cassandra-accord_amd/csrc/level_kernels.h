@@ -487,7 +487,7 @@ constexpr int CB_REG = 8;
 __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                         const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
                                         uint32_t* __restrict__ c_txn, uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
-                                        uint8_t* __restrict__ c_meta, uint64_t* __restrict__ c_exec1) {
+                                        uint8_t* __restrict__ c_meta, uint64_t* __restrict__ c_exec1, bool pred_mode) {
     uint64_t k[CB_REG];
     uint32_t t[CB_REG], pr[CB_REG], wr[CB_REG], ord[CB_REG];
 #pragma unroll
@@ -521,16 +521,26 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
 #pragma unroll
     for (int q = 0; q < CB_REG; ++q) wr[q] = meta_kind((uint8_t)wr[q]) == AD_KIND_WRITE ? 1u : 0u;
     bool seen_w = false;
-    uint32_t reads = 0;
+    uint32_t reads = 0, lw = 0;
 #pragma unroll
     for (int q = 0; q < CB_REG; ++q) {
         if (q < len) {
             c_txn[s + q] = t[q];
-            const uint32_t pc = wr[q] ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
-            if (pc) atomicAdd(&indeg[t[q]], pc);
-            if (wr[q]) { seen_w = true; reads = 0; } else ++reads;
+            if (pred_mode) {
+                // the same reduced edges as predecessor runs: a Read's last Write before it; a Write's Reads
+                // since the last Write, else that Write
+                uint2 pe = make_uint2(0u, 0u);
+                if (wr[q] && reads > 0) pe = make_uint2((uint32_t)(s + q) - reads, reads);
+                else if (seen_w) pe = make_uint2((uint32_t)s + lw, 1u);
+                if (pe.y) succ[pr[q]] = pe;
+            } else {
+                const uint32_t pc = wr[q] ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
+                if (pc) atomicAdd(&indeg[t[q]], pc);
+            }
+            if (wr[q]) { seen_w = true; reads = 0; lw = (uint32_t)q; } else ++reads;
         }
     }
+    if (pred_mode) return;
     int next_w = len;
 #pragma unroll
     for (int q = CB_REG - 1; q >= 0; --q) {
@@ -562,7 +572,7 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
                                                      uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
                                                      uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
                                                      uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
-                                                     uint32_t* __restrict__ any_long, int full) {
+                                                     uint32_t* __restrict__ any_long, int full, int pred_mode = 0) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool lng = false;
     const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
@@ -574,7 +584,7 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
             lng = true;
         } else if (end - s <= CB_REG) {
             chain_build_regs(s, (int)(end - s), e_txn, e_meta, e_exec1, sval, c_txn, indeg, succ, full ? c_meta : nullptr,
-                             full ? c_exec1 : nullptr);
+                             full ? c_exec1 : nullptr, pred_mode != 0);
         } else {
             for (size_t x = s; x < end; ++x) {
                 const uint64_t kx = e_exec1[x];
@@ -591,16 +601,24 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
             // Write, else for that Write (k_kahn_prep states the reduction)
             bool seen_w = false;
             uint32_t reads = 0;
+            size_t lw = s;
             for (size_t q = s; q < end; ++q) {
                 const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
-                const uint32_t pc = wr ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
-                if (pc) atomicAdd(&indeg[c_txn[q]], pc);
-                if (wr) { seen_w = true; reads = 0; } else ++reads;
+                if (pred_mode) {
+                    uint2 pe = make_uint2(0u, 0u);
+                    if (wr && reads > 0) pe = make_uint2((uint32_t)(q - reads), reads);
+                    else if (seen_w) pe = make_uint2((uint32_t)lw, 1u);
+                    if (pe.y) succ[c_pair[q]] = pe;
+                } else {
+                    const uint32_t pc = wr ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
+                    if (pc) atomicAdd(&indeg[c_txn[q]], pc);
+                }
+                if (wr) { seen_w = true; reads = 0; lw = q; } else ++reads;
             }
             // successors: after a Write the Reads that follow it (or the next Write if one follows
             // directly); after a Read the next Write
             size_t next_w = end;
-            for (size_t q = end; q-- > s;) {
+            for (size_t q = end; !pred_mode && q-- > s;) {
                 const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
                 uint2 sc = make_uint2(0u, 0u);
                 if (wr) {
@@ -826,6 +844,86 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
     wave_set_flag(released, work);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// One-pass levels for shallow key-chain batches (C2: 10 levels, chains of a few entries).  Kahn pays one grid
+// launch plus the slowest lane's chain of returning atomics per level.  Here every txn pulls instead: its
+// level = 1 + the maximum level of its predecessor runs (the same reduced (a) edges, written by the chain
+// build in pred mode), 0 without predecessors, and it publishes the level with LV_FINAL once every
+// predecessor's is final.  One launch: a wave retries its unfinished lanes until all have published (a lane
+// never blocks inside the wave, so a predecessor in the same wave is never starved).  Predecessors have a
+// smaller executeAt, i.e. almost always a smaller TxnId, so the txns a lane waits for sit in the same or an
+// earlier workgroup; a slow-path bump points at most a few workgroups ahead, and those are dispatched as
+// earlier ones retire.  A lane that has retried PULL_CAP times raises *abort and publishes a placeholder (so no
+// lane waits for ever); the caller then recomputes the batch with the Kahn wavefronts.  Levels are read and
+// written with agent-scope atomics: the 8 XCDs' L2s are not coherent with each other.
+constexpr uint32_t LV_FINAL = 0x80000000u;
+constexpr uint32_t PULL_CAP = 1u << 16;
+__global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __restrict__ key_off, const uint2* __restrict__ pred,
+                                                    const uint32_t* __restrict__ c_txn, uint32_t* L, const uint32_t* gate,
+                                                    uint32_t* abort_flag, uint32_t* __restrict__ bmax) {
+    __shared__ uint32_t wm[256 / WAVE];
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool gated = *gate != 0u;                     // long chains: the caller takes another path
+    bool done = t >= n || gated;
+    uint32_t b = 0, e = 0, m = 0, tries = 0;
+    if (!done) { b = key_off[t]; e = key_off[t + 1]; }
+    while (__ballot(!done)) {
+        if (!done) {
+            bool ready = true;
+            uint32_t mm = 0;
+            for (uint32_t p = b; p < e && ready; ++p) {
+                const uint2 r = pred[p];
+                for (uint32_t x = r.x; x < r.x + r.y; ++x) {
+                    const uint32_t v = __hip_atomic_load(&L[c_txn[x]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!(v & LV_FINAL)) { ready = false; break; }
+                    const uint32_t lv = (v & ~LV_FINAL) + 1u;
+                    mm = lv > mm ? lv : mm;
+                }
+            }
+            if (ready) {
+                __hip_atomic_store(&L[t], mm | LV_FINAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                m = mm;
+                done = true;
+            } else if (++tries >= PULL_CAP ||
+                       ((tries & 63u) == 0u && __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                if (tries >= PULL_CAP) __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&L[t], LV_FINAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                done = true;
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(m, o); m = y > m ? y : m; }
+    if (__lane_id() == 0) wm[threadIdx.x / WAVE] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = 0;
+        for (int w = 0; w < 256 / WAVE; ++w) x = wm[w] > x ? wm[w] : x;
+        bmax[blockIdx.x] = x;
+    }
+}
+// max of the per-workgroup maxima (one workgroup); strips LV_FINAL from the levels afterwards
+__global__ __launch_bounds__(1024) void k_level_pull_max(uint32_t nb, const uint32_t* __restrict__ bmax, uint32_t* out) {
+    __shared__ uint32_t wm[1024 / WAVE];
+    uint32_t m = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) m = bmax[i] > m ? bmax[i] : m;
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(m, o); m = y > m ? y : m; }
+    if (__lane_id() == 0) wm[threadIdx.x / WAVE] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = 0;
+        for (int w = 0; w < 1024 / WAVE; ++w) x = wm[w] > x ? wm[w] : x;
+        *out = x;
+    }
+}
+__global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) L[t] &= ~LV_FINAL;
+}
+
 // Deep graphs (C3: the hot key's ~10^5 Writes make ~10^5 levels, a handful of txns each): one launch per
 // wavefront costs more than the wavefront.  k_kahn_small runs consecutive wavefronts inside ONE workgroup:
 // the frontier is an explicit list (LDS counter, global slots), released successors are appended to the
@@ -1021,6 +1119,7 @@ inline bool publish_read(const Publisher& p, hipStream_t st, const uint32_t* a, 
 struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
     Publisher pub;                      // set by the engine: flag read-backs without a stream sync
+    bool pull_off = false;              // AD_LEVELS_KAHN: skip the one-pass pull levels
     int kb_hint = 0;                    // wavefronts in the first Kahn launch batch (previous depth + 1)
     uint32_t* c_txn = nullptr;
     uint8_t* c_meta = nullptr;
@@ -1458,6 +1557,38 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // key-domain sync points / ephemeral reads sit in the key segments but not in the execution chains:
         // the chain build of this path treats every key entry as a Read or Write, so such batches resolve on
         // the relaxation path below (its chain scans skip unmanaged entries)
+        // ---- one-pass pull levels: pure key batches (no (b)/(c) edges); long chains go to the block path,
+        // an abort (a lane waited PULL_CAP retries) to the Kahn wavefronts below
+        if (in.kahn_ok && !in.keep_levels && P > 0 && pure && !ls.pull_off) {
+            ls.chains_ready = false;
+            uint32_t lng = 0, res[2] = {0, 0};
+            {
+                KScope ks(K_KAHN, P);
+                const int gn = ceil_div((long)n, 256);
+                hipMemsetAsync(ls.succ, 0, P * 8, st);                    // predecessor runs (zero: none)
+                hipMemsetAsync(ls.flags + 16, 0, 8, st);                  // [16] abort, [17] max level
+                k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1);
+                k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 16, ls.sk1);
+                k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
+                k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
+                if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 2, res)) {
+                    err = "exec levels: device error";
+                    return AD_ERR_DEVICE;
+                }
+            }
+            if (lng) return block_path();                                  // deep key chains: executeAt blocks
+            if (!res[0]) {
+                const int lv = (int)res[1] + 1;
+                *iters = lv;
+                if (want_order && n > 0 && in.order_verify)
+                    *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, lv - 1, in.order_verify);
+                else if (want_order && n > 0)
+                    order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
+                return AD_OK;
+            }
+            hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);     // aborted: the wavefronts below
+        }
         if (in.kahn_ok && !in.keep_levels && P > 0 && in.n_special == 0) {
             ls.chains_ready = false;
             int lv = 0;

@@ -27,7 +27,7 @@ def check(engine_factory, batch, window=32, replicas=3, drop_p=0.1, seed=0xACC0D
     if eng is None:
         eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
     if fixpoint:
-        eng.set_level_mode(True)
+        eng.set_level_mode(fixpoint)          # True: the chain fixpoint; an int: that AD_LEVELS_* mode
     eng.load(batch)
     eng.preaccept_deps()
     for v in range(replicas):
@@ -49,13 +49,24 @@ def test_configs_small(engine_factory, name, n):
     check(engine_factory, workload.config(name, n=n))
 
 
-@pytest.mark.parametrize("fixpoint", [False, True])
+@pytest.mark.parametrize("fixpoint", [False, True, 3])
 @pytest.mark.parametrize("keyspace,n", [(10_000_000, 200000), (40000, 20000), (4000, 6000), (300, 2000)])
 def test_levels_kahn_and_fixpoint(engine_factory, keyspace, n, fixpoint):
-    # short key chains and no range txns: AUTO takes the Kahn wavefront, FIXPOINT the chain fixpoint; both
-    # must give the oracle's levels and order (the denser keyspaces give deeper graphs, up to long chains)
+    # short key chains and no range txns: AUTO takes the one-pass pull levels, 3 (AD_LEVELS_KAHN) the Kahn
+    # wavefront, FIXPOINT the chain fixpoint; all must give the oracle's levels and order (the denser keyspaces
+    # give deeper graphs, up to long chains)
     b = workload.generate(n, keys_per_txn=4, keyspace=keyspace, seed=keyspace % 97 + n)
     check(engine_factory, b, fixpoint=fixpoint)
+
+
+@pytest.mark.parametrize("bump", [5000, 10 ** 7])
+def test_pull_levels_far_bumps(engine_factory, bump):
+    # the pull levels wait for predecessors with a smaller executeAt; a slow-path bump makes some of them later
+    # TxnIds (later workgroups): near ones are dispatched as earlier workgroups retire, and if lanes wait too
+    # long the pass aborts into the Kahn wavefronts — the levels are the oracle's either way
+    b = workload.generate(30000, keys_per_txn=4, keyspace=20000, slow_frac=0.3, bump_max=bump, seed=bump % 1000 + 7)
+    check(engine_factory, b)
+    check(engine_factory, b, fixpoint=3)
 
 
 @pytest.mark.parametrize("fixpoint", [False, True])
