@@ -484,6 +484,7 @@ __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __
 // segments): odd-even transposition sort on (executeAt, arrival) in registers, both passes unrolled, and
 // only c_txn (what the wavefronts read) is written back.
 constexpr int CB_REG = 8;
+constexpr uint32_t PRED_TXN = 0x80000000u;   // pred mode: the run is one txn, stored in .x
 __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                         const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
                                         uint32_t* __restrict__ c_txn, uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
@@ -521,23 +522,25 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
 #pragma unroll
     for (int q = 0; q < CB_REG; ++q) wr[q] = meta_kind((uint8_t)wr[q]) == AD_KIND_WRITE ? 1u : 0u;
     bool seen_w = false;
-    uint32_t reads = 0, lw = 0;
+    uint32_t reads = 0, lw_txn = 0;
 #pragma unroll
     for (int q = 0; q < CB_REG; ++q) {
         if (q < len) {
             c_txn[s + q] = t[q];
             if (pred_mode) {
                 // the same reduced edges as predecessor runs: a Read's last Write before it; a Write's Reads
-                // since the last Write, else that Write
+                // since the last Write, else that Write.  A single predecessor is stored as its txn
+                // (PRED_TXN): the pull pass then needs no c_txn hop.
                 uint2 pe = make_uint2(0u, 0u);
-                if (wr[q] && reads > 0) pe = make_uint2((uint32_t)(s + q) - reads, reads);
-                else if (seen_w) pe = make_uint2((uint32_t)s + lw, 1u);
+                if (wr[q] && reads > 1) pe = make_uint2((uint32_t)(s + q) - reads, reads);
+                else if (wr[q] && reads == 1) pe = make_uint2(t[q > 0 ? q - 1 : 0], 1u | PRED_TXN);
+                else if (seen_w) pe = make_uint2(lw_txn, 1u | PRED_TXN);
                 if (pe.y) succ[pr[q]] = pe;
             } else {
                 const uint32_t pc = wr[q] ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
                 if (pc) atomicAdd(&indeg[t[q]], pc);
             }
-            if (wr[q]) { seen_w = true; reads = 0; lw = (uint32_t)q; } else ++reads;
+            if (wr[q]) { seen_w = true; reads = 0; lw_txn = t[q]; } else ++reads;
         }
     }
     if (pred_mode) return;
@@ -606,8 +609,9 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
                 const bool wr = meta_kind(c_meta[q]) == AD_KIND_WRITE;
                 if (pred_mode) {
                     uint2 pe = make_uint2(0u, 0u);
-                    if (wr && reads > 0) pe = make_uint2((uint32_t)(q - reads), reads);
-                    else if (seen_w) pe = make_uint2((uint32_t)lw, 1u);
+                    if (wr && reads > 1) pe = make_uint2((uint32_t)(q - reads), reads);
+                    else if (wr && reads == 1) pe = make_uint2(c_txn[q - 1], 1u | PRED_TXN);
+                    else if (seen_w) pe = make_uint2(c_txn[lw], 1u | PRED_TXN);
                     if (pe.y) succ[c_pair[q]] = pe;
                 } else {
                     const uint32_t pc = wr ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
@@ -873,8 +877,11 @@ __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __
             uint32_t mm = 0;
             for (uint32_t p = b; p < e && ready; ++p) {
                 const uint2 r = pred[p];
-                for (uint32_t x = r.x; x < r.x + r.y; ++x) {
-                    const uint32_t v = __hip_atomic_load(&L[c_txn[x]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool one = (r.y & PRED_TXN) != 0u;
+                const uint32_t len = r.y & ~PRED_TXN;
+                for (uint32_t x = 0; x < len; ++x) {
+                    const uint32_t j = one ? r.x : c_txn[r.x + x];
+                    const uint32_t v = __hip_atomic_load(&L[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (!(v & LV_FINAL)) { ready = false; break; }
                     const uint32_t lv = (v & ~LV_FINAL) + 1u;
                     mm = lv > mm ? lv : mm;
