@@ -849,7 +849,10 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
 }
 
 // ---------------------------------------------------------------------------------------------------
-// One-pass levels for shallow key-chain batches (C2: 10 levels, chains of a few entries).  Kahn pays one grid
+// One-pass levels for shallow key-chain batches (C2: 10 levels, chains of a few entries).  (Tried for mixed key +
+// range batches with the (b)/(c) sources read per txn from its merged deps: on C4's 5,650 levels ~10^6 lanes
+// wait at once and their polling swamps the memory side, so the pass hit its cap; mixed batches stay on the
+// Kahn wavefronts.)  Kahn pays one grid
 // launch plus the slowest lane's chain of returning atomics per level.  Here every txn pulls instead: its
 // level = 1 + the maximum level of its predecessor runs (the same reduced (a) edges, written by the chain
 // build in pred mode), 0 without predecessors, and it publishes the level with LV_FINAL once every
@@ -857,11 +860,11 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
 // never blocks inside the wave, so a predecessor in the same wave is never starved).  Predecessors have a
 // smaller executeAt, i.e. almost always a smaller TxnId, so the txns a lane waits for sit in the same or an
 // earlier workgroup; a slow-path bump points at most a few workgroups ahead, and those are dispatched as
-// earlier ones retire.  A lane that has retried PULL_CAP times raises *abort and publishes a placeholder (so no
+// earlier ones retire.  A lane that has waited ~1 s raises *abort and publishes a placeholder (so no
 // lane waits for ever); the caller then recomputes the batch with the Kahn wavefronts.  Levels are read and
 // written with agent-scope atomics: the 8 XCDs' L2s are not coherent with each other.
 constexpr uint32_t LV_FINAL = 0x80000000u;
-constexpr uint32_t PULL_CAP = 1u << 16;
+constexpr uint64_t PULL_CAP_TICKS = 100000000ull;    // wall_clock64 at 100 MHz: a lane gives up after ~1 s
 __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __restrict__ key_off, const uint2* __restrict__ pred,
                                                     const uint32_t* __restrict__ c_txn, uint32_t* L, const uint32_t* gate,
                                                     uint32_t* abort_flag, uint32_t* __restrict__ bmax) {
@@ -871,6 +874,7 @@ __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __
     bool done = t >= n || gated;
     uint32_t b = 0, e = 0, m = 0, tries = 0;
     if (!done) { b = key_off[t]; e = key_off[t + 1]; }
+    const uint64_t t0 = wall_clock64();
     while (__ballot(!done)) {
         if (!done) {
             bool ready = true;
@@ -891,13 +895,16 @@ __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __
                 __hip_atomic_store(&L[t], mm | LV_FINAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 m = mm;
                 done = true;
-            } else if (++tries >= PULL_CAP ||
-                       ((tries & 63u) == 0u && __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                if (tries >= PULL_CAP) __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if ((++tries & 63u) == 0u &&
+                       (wall_clock64() - t0 > PULL_CAP_TICKS ||
+                        __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                // waited too long (or another lane did): placeholder, and the caller redoes the batch
+                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&L[t], LV_FINAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 done = true;
             } else {
                 __builtin_amdgcn_s_sleep(1);
+                if (tries > 64) __builtin_amdgcn_s_sleep(8);      // back off as the wait grows
             }
         }
     }
@@ -1565,7 +1572,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // the chain build of this path treats every key entry as a Read or Write, so such batches resolve on
         // the relaxation path below (its chain scans skip unmanaged entries)
         // ---- one-pass pull levels: pure key batches (no (b)/(c) edges); long chains go to the block path,
-        // an abort (a lane waited PULL_CAP retries) to the Kahn wavefronts below
+        // an abort (a lane waited ~1 s) to the Kahn wavefronts below
         if (in.kahn_ok && !in.keep_levels && P > 0 && pure && !ls.pull_off) {
             ls.chains_ready = false;
             uint32_t lng = 0, res[2] = {0, 0};
