@@ -181,12 +181,13 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 
 // ---------------------------------------------------------------------------------------------------
 // Heavy txns: one 256-thread workgroup per txn (grid-stride over the heavy list).  The txn's TxnId lists
-// are cut into chunks at every MCH-th TxnId of the reply holding the most, its key lists likewise by keys;
+// are cut into chunks at every mch-th TxnId of the reply holding the most (mch: the longer list over the
+// workgroup, at least MCH_MIN), its key lists likewise by keys;
 // each chunk is a value interval, so the R-way merge of one chunk (the same loops as k_merge) is
 // independent of the others.  Thread j takes a contiguous run of chunks; a block scan of the per-thread
 // totals gives each thread its output offsets.  Write pass: TxnIds first (a barrier), then keys and
 // per-key lists, whose TxnIds are remapped by binary search in the txn's merged TxnId list.
-constexpr int MCH = 32, MH_T = 256, MH_GRID = 8192;
+constexpr int MCH_MIN = 4, MH_T = 256, MH_GRID = 8192;
 // write pass: the txn's merged TxnId list is staged in LDS for the per-entry remap (binary searches in LDS
 // instead of HBM round trips) when it fits
 constexpr uint32_t MH_LDS = 12288;
@@ -245,14 +246,18 @@ __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
             if (tc[v] > tc[pv]) pv = v;
             if (nk[v] > nk[pk]) pk = v;
         }
-        const uint32_t nT = (tc[pv] + MCH - 1) / MCH, nK = (nk[pk] + MCH - 1) / MCH;
+        // chunk size: spread the larger of the two lists over the whole workgroup (a key Write's ~10^2-10^3 RangeDeps
+        // used to keep 19 of 256 threads busy with fixed 32-item chunks), at least MCH_MIN items per chunk
+        const uint32_t big = tc[pv] > nk[pk] ? tc[pv] : nk[pk];
+        const uint32_t mch = max((uint32_t)MCH_MIN, (big + MH_T - 1) / MH_T);
+        const uint32_t nT = (tc[pv] + mch - 1) / mch, nK = (nk[pk] + mch - 1) / mch;
         const uint32_t nch = nT > nK ? nT : nK;
         const uint32_t cpt = (nch + MH_T - 1) / MH_T;
         const uint32_t c0 = threadIdx.x * cpt, c1 = min(nch, c0 + cpt);
-        // chunk c of the TxnIds: [T_pv[c*MCH], T_pv[(c+1)*MCH]) in every reply
+        // chunk c of the TxnIds: [T_pv[c*mch], T_pv[(c+1)*mch]) in every reply
         auto t_bounds = [&](uint32_t c, uint32_t* cur, uint32_t* end) {
-            const uint32_t lo = c == 0 ? 0u : a.txns[pv][tb[pv] + c * MCH];
-            const uint32_t hiv = (c + 1) * MCH < tc[pv] ? a.txns[pv][tb[pv] + (c + 1) * MCH] : INF;
+            const uint32_t lo = c == 0 ? 0u : a.txns[pv][tb[pv] + c * mch];
+            const uint32_t hiv = (c + 1) * mch < tc[pv] ? a.txns[pv][tb[pv] + (c + 1) * mch] : INF;
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 const uint32_t b = tb[v], e = tb[v] + tc[v];
@@ -261,9 +266,9 @@ __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
             }
         };
         auto k_bounds = [&](uint32_t c, uint32_t* kc, uint32_t* ke) {
-            const bool first = c == 0, last = (c + 1) * MCH >= nk[pk];
-            const MKey<KW> lo = first ? MKey<KW>{0ull, 0ull} : MKey<KW>::load(a.keys[pk], kb[pk] + c * MCH);
-            const MKey<KW> hv = last ? MKey<KW>{0ull, 0ull} : MKey<KW>::load(a.keys[pk], kb[pk] + (c + 1) * MCH);
+            const bool first = c == 0, last = (c + 1) * mch >= nk[pk];
+            const MKey<KW> lo = first ? MKey<KW>{0ull, 0ull} : MKey<KW>::load(a.keys[pk], kb[pk] + c * mch);
+            const MKey<KW> hv = last ? MKey<KW>{0ull, 0ull} : MKey<KW>::load(a.keys[pk], kb[pk] + (c + 1) * mch);
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 const uint32_t b = kb[v], e = kb[v] + nk[v];
