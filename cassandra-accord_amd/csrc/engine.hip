@@ -240,7 +240,7 @@ enum Slot : size_t {
     S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
     S_HTM, S_HTL, S_HTN, S_HEM, S_HEL, S_HEN, S_HST, S_HKOFF, S_HKEYS, S_HGIDS, S_HSEGM, S_HKEEP, S_HROWS2, S_HCNT,
     S_RCROWS, S_RCCNT, S_RCOFF, S_RCREJ, S_RCK0, S_RCT0 = S_RCK0 + RC_OUT, S_RCEND = S_RCT0 + RC_OUT,
-    S_RIDX = S_RCEND, S_NONEROWS,
+    S_RIDX = S_RCEND, S_NONEROWS, S_LROWS,
     S_NUM_FIXED,
     S_CSR0 = 160
 };
@@ -849,7 +849,13 @@ int stage_deps(ad_handle* h) {
                 la.key_off[vc] = c.key_off; la.k2t_off[vc] = c.k2t_off; la.ent_off[vc] = c.ent_off; la.k2t[vc] = c.k2t;
                 la.txns[vc] = c.txns; la.tcnt[vc] = c.tcnt;
             }
-            k_union_lds<<<dim3((unsigned)n, (unsigned)nvc), UB, 0, st>>>(la);
+            // one workgroup per (large txn, CSR), not per (txn, CSR)
+            uint32_t* lrows = nullptr;
+            CK(dalloc(h, S_LROWS, &lrows, n + 64));
+            device_scan(LargeRowsOp{h->meta, lrows, lrows + n, n}, n, (uint32_t*)h->scratch, st);
+            la.rows = lrows; la.rows_total = lrows + n;
+            k_union_lds<<<dim3((unsigned)h->n_large, (unsigned)nvc), UB, 0, st>>>(la);
+            la.rows = nullptr; la.rows_total = nullptr;
         }
         if (Q > 0) {
             la.ncsr = nv; la.csr_base = nvc; la.only_large = 0;

@@ -171,6 +171,8 @@ struct LdsUnionArgs {
     int ncsr;
     int csr_base;                      // this launch's CSRs are [csr_base, csr_base + ncsr) of the tables
     int only_large;
+    const uint32_t* rows;              // only_large: the large txns' rows (grid x = their count), or null
+    const uint32_t* rows_total;        //   their device-side count (guard)
     const uint8_t* meta;
     const uint32_t* key_off[UNION_CSRS];
     const uint32_t* k2t_off[UNION_CSRS];
@@ -223,9 +225,27 @@ __device__ inline void union_body(uint32_t* buf, uint32_t* wsum, int32_t* body, 
     if (threadIdx.x == 0) *tcnt = total;
 }
 
-// grid (n, ncsr): one workgroup per (txn, CSR); CSRs above UNION_CAP entries are queued for k_union_big
+// the rows of the large txns (the key-CSR launch only has work there: C4's 4M-row grid x 6 CSRs launched
+// 24M mostly empty workgroups for ~4*10^5 range txns)
+struct LargeRowsOp {
+    using S = uint32_t;
+    const uint8_t* meta;
+    uint32_t* out;
+    uint32_t* total;
+    size_t n;
+    __device__ S load(size_t i) const { return (meta[i] & META_LARGE) ? 1u : 0u; }
+    __device__ S identity() const { return 0u; }
+    __device__ S combine(S a, S b) const { return a + b; }
+    __device__ void store(size_t i, S ex, S inc, S el) const {
+        if (el) out[ex] = (uint32_t)i;
+        if (i + 1 == n) *total = inc;
+    }
+};
+
+// grid (n or #large rows, ncsr): one workgroup per (txn, CSR); CSRs above UNION_CAP entries are queued for k_union_big
 __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
-    const size_t t = blockIdx.x;
+    if (a.rows && blockIdx.x >= *a.rows_total) return;
+    const size_t t = a.rows ? (size_t)a.rows[blockIdx.x] : (size_t)blockIdx.x;
     const int c = a.csr_base + (int)blockIdx.y;
     if (t >= a.n) return;
     if (a.only_large && !(a.meta[t] & META_LARGE)) return;
