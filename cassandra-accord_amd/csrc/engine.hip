@@ -240,7 +240,7 @@ enum Slot : size_t {
     S_MCEK, S_MCEM, S_MCEL, S_MCEN, S_FASTROWS, S_HOLD, S_DBASE, S_DCNT, S_DOUT, S_DMAT, S_DRECV, S_QPOS,
     S_HTM, S_HTL, S_HTN, S_HEM, S_HEL, S_HEN, S_HST, S_HKOFF, S_HKEYS, S_HGIDS, S_HSEGM, S_HKEEP, S_HROWS2, S_HCNT,
     S_RCROWS, S_RCCNT, S_RCOFF, S_RCREJ, S_RCK0, S_RCT0 = S_RCK0 + RC_OUT, S_RCEND = S_RCT0 + RC_OUT,
-    S_RIDX = S_RCEND, S_NONEROWS, S_LROWS,
+    S_RIDX = S_RCEND, S_NONEROWS, S_LROWS, S_UMEDC, S_UMED,
     S_NUM_FIXED,
     S_CSR0 = 160
 };
@@ -864,7 +864,15 @@ int stage_deps(ad_handle* h) {
                 la.key_off[nvc + v] = c.key_off; la.k2t_off[nvc + v] = c.k2t_off; la.ent_off[nvc + v] = c.ent_off;
                 la.k2t[nvc + v] = c.k2t; la.txns[nvc + v] = c.txns; la.tcnt[nvc + v] = c.tcnt;
             }
-            k_union_lds<<<dim3((unsigned)n, (unsigned)nv), UB, 0, st>>>(la);
+            // small lists by single-wave workgroups, the rest queued for 256-thread workgroups
+            uint32_t* med_count = nullptr;
+            uint2* med = nullptr;
+            CK(dalloc(h, S_UMEDC, &med_count, 64));
+            CK(dalloc(h, S_UMED, &med, (size_t)n * nv + 1));
+            HIPCHK(h, hipMemsetAsync(med_count, 0, 4, st));
+            la.med_count = med_count; la.med = med;
+            k_union_lds_small<<<dim3((unsigned)n, (unsigned)nv), US_T, 0, st>>>(la);
+            k_union_lds_list<<<8192, UB, 0, st>>>(la);
         }
         CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
     }

@@ -185,6 +185,9 @@ struct LdsUnionArgs {
     uint32_t* ovf_count;
     uint2* ovf;                        // {txn, csr}
     uint32_t ovf_cap;
+    // small/medium split (RangeDeps launch): items above UNION_SMALL entries queued for the 256-thread pass
+    uint32_t* med_count;
+    uint2* med;                        // {txn, csr}
     // big pass
     const uint2* items;                // overflow items
     uint32_t* gbuf;                    // global sort space for items above UNION_CAP_BIG
@@ -268,6 +271,55 @@ __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
         return;
     }
     union_body<UB>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
+}
+
+// RangeDeps of every txn (C4: ~10^7 (txn, view) lists of a few hundred entries): one 64-thread workgroup with a
+// 2 KiB LDS buffer per (txn, CSR).  The 256-thread kernel's 32 KiB buffer held a CU to 5 workgroups, i.e. 5
+// unions in flight per CU, each a chain of ~40 barrier-separated bitonic stages; single-wave workgroups fit 32
+// per CU and their barriers are cheap.  Lists above UNION_SMALL go to the medium queue (k_union_lds_list).
+constexpr int UNION_SMALL = 512, US_T = 64;
+__global__ __launch_bounds__(US_T) void k_union_lds_small(LdsUnionArgs a) {
+    const size_t t = blockIdx.x;
+    const int c = a.csr_base + (int)blockIdx.y;
+    if (t >= a.n) return;
+    __shared__ uint32_t buf[UNION_SMALL];
+    __shared__ uint32_t wsum[1];
+    const uint32_t nk = a.key_off[c][t + 1] - a.key_off[c][t];
+    if (nk == 0) {
+        if (threadIdx.x == 0) a.tcnt[c][t] = 0;
+        return;
+    }
+    const uint32_t mb = a.k2t_off[c][t];
+    const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
+    if (ne > (uint32_t)UNION_SMALL) {
+        if (threadIdx.x == 0) a.med[atomicAdd(a.med_count, 1u)] = make_uint2((uint32_t)t, (uint32_t)c);
+        return;
+    }
+    union_body<US_T>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
+}
+// the medium queue: grid-stride over the device-side count, one 256-thread workgroup per item (LDS up to
+// UNION_CAP; above it the overflow queue as in k_union_lds)
+__global__ __launch_bounds__(UB) void k_union_lds_list(LdsUnionArgs a) {
+    __shared__ uint32_t buf[UNION_CAP];
+    __shared__ uint32_t wsum[UB / WAVE];
+    const uint32_t count = *a.med_count;
+    for (uint32_t it = blockIdx.x; it < count; it += gridDim.x) {
+        const uint32_t t = a.med[it].x, c = a.med[it].y;
+        const uint32_t nk = a.key_off[c][t + 1] - a.key_off[c][t];
+        const uint32_t mb = a.k2t_off[c][t];
+        const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
+        if (ne > (uint32_t)UNION_CAP) {
+            if (threadIdx.x == 0) {
+                const uint32_t k = atomicAdd(a.ovf_count, 1u);
+                if (k < a.ovf_cap) a.ovf[k] = make_uint2(t, c);
+                else atomicOr(&a.prm->err, ERR_CAP);
+                a.tcnt[c][t] = 0;
+            }
+            continue;
+        }
+        union_body<UB>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
+        __syncthreads();
+    }
 }
 
 // overflow pass, one 1024-thread workgroup per queued (txn, CSR): LDS up to UNION_CAP_BIG entries, beyond
