@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 // independent of the others.  Thread j takes a contiguous run of chunks; a block scan of the per-thread
 // totals gives each thread its output offsets.  Write pass: TxnIds first (a barrier), then keys and
 // per-key lists, whose TxnIds are remapped by binary search in the txn's merged TxnId list.
-constexpr int MCH_MIN = 4, MH_T = 256, MH_GRID = 8192;
+constexpr int MCH_MIN = 2, MH_T = 256, MH_GRID = 8192;
 // write pass: the txn's merged TxnId list is staged in LDS for the per-entry remap (binary searches in LDS
 // instead of HBM round trips) when it fits
 constexpr uint32_t MH_LDS = 12288;
