@@ -1,4 +1,5 @@
 set -eo pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_sharding.py -m gpu -x -v --timeout 170 --timeout-method thread --durations=0 > gpurun_out/t_shr.log 2>&1
-echo tests ok
+export TMPDIR=/tmp
+timeout -k 10 300 python3 -u bench.py > gpurun_out/final_bench.json 2> gpurun_out/final_bench.err
+echo bench ok
