@@ -49,6 +49,7 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
     D = st["deps_entries"]           # emitted dependency entries over all views/classes
     M = st["merged_entries"]         # entries of the merged Deps
     W = st["walk_items"]             # entries the deps walks visit
+    C = st.get("key_classes") or 2 * R   # key-footprint CSRs computed: 2R, or R without directKeyDeps
     per = {
         "k_minmax": calls * (n * 44 + P * 8),                    # TxnId/executeAt SoA + key_off; keys
         "k_pack": calls * (n * 62 + P * 20),                     # read 45 B/txn, write 17 B/txn; 8+12 B/pair
@@ -58,16 +59,16 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
         "k_gather_entries": units * 34,                          # sval, pair_txn, meta, ex1 -> e_txn, e_meta, e_exec1, spos
         "scan_elide": units * 37,                                # skey, e_meta, e_exec1 -> seg, ud, pm_w, pm_c
         # the walks visit only entries with an earlier entry of their key (ad_stage_times.walk_items):
-        # list index, entry state, own txn's TxnId, predecessor entry, prefix state; 2R counts out
-        "k_deps_walk<count>": calls * W * (46 + 8 * R),
-        "k_deps_walk<fill>": calls * (W * (46 + 8 * R) + 4 * D),  # 2R end slots in, the entries out
-        "k_txn_layout": units * (8 + 16 * R),                    # key + 2R counts in, 2R slots out
-        # OffsetsOp: per pair the key + 2R counts in and 2R slots out; per txn 3 offsets x 2R CSRs out
-        "scan_offsets": calls * (P * (8 + 16 * R)) + units * 24 * R,
+        # list index, entry state, own txn's TxnId, predecessor entry, prefix state; C counts out
+        "k_deps_walk<count>": calls * W * (46 + 4 * C),
+        "k_deps_walk<fill>": calls * (W * (46 + 4 * C) + 4 * D),  # C end slots in, the entries out
+        "k_txn_layout": units * (8 + 8 * C),                     # key + C counts in, C slots out
+        # OffsetsOp: per pair the key + C counts in and C slots out; per txn 3 offsets x C CSRs out
+        "scan_offsets": calls * (P * (8 + 8 * C)) + units * 12 * C,
         "csr_offsets": units * 24,                               # 3 exclusive scans of one count array
         "merge_offsets": units * 24,                             # per (txn, output): 3 counts in, 3 offsets out
-        # per txn: 3 offsets x 2R CSRs, the per-key lists in, unique TxnIds + remapped lists out
-        "k_txn_union": calls * (n * (12 * 2 * R + 4 * 2 * R) + 12 * D),
+        # per txn: 3 offsets x C CSRs, the per-key lists in, unique TxnIds + remapped lists out
+        "k_txn_union": calls * (n * (12 * C + 4 * C) + 12 * D),
         # R-way merge: every reply's per-txn offsets (16 B) and TxnIds + keysToTxnIds (8 B/entry) in; the
         # write pass also writes the merged rows (16 B/txn + 8 B/entry)
         "k_merge<count>": units * 16 * R + 8 * D,

@@ -15,6 +15,7 @@ AD_ERR_UNSUPPORTED = -4
 AD_ERR_DEVICE = -5
 AD_ERR_NOMEM = -6
 AD_RANK_NONE = 0xFFFFFFFF   # ad_max_conflicts: Timestamp.NONE
+AD_LEVEL_DONE = 0xFFFFFFFF  # ad_exec_levels over a CFK history batch: an APPLIED / INVALID row
 
 # Txn.Kind ordinals (primitives/Txn.java:53-113)
 KIND_READ, KIND_WRITE, KIND_EPHEMERAL_READ, KIND_SYNC_POINT, KIND_EXCLUSIVE_SYNC_POINT, KIND_LOCAL_ONLY = range(6)
@@ -66,7 +67,8 @@ class AdStageTimes(C.Structure):
                 ("levels", C.c_float), ("total", C.c_float),
                 ("deps_entries", C.c_uint64), ("merged_entries", C.c_uint64), ("level_edges", C.c_uint64),
                 ("level_iterations", C.c_uint32), ("walk_items", C.c_uint32),
-                ("level_blocks", C.c_uint32), ("level_rounds", C.c_uint32)]
+                ("level_blocks", C.c_uint32), ("level_rounds", C.c_uint32),
+                ("key_classes", C.c_uint32), ("level_path", C.c_uint32)]
 
 
 def ptr(a, ctype):

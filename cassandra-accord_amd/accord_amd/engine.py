@@ -55,6 +55,8 @@ def lib():
         L.ad_cfk_retain.argtypes = [vp, C.POINTER(C.c_size_t)]
         L.ad_cfk_reset.argtypes = [vp]
         L.ad_cfk_rows.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_uint32)]
+        L.ad_cfk_update.argtypes = [vp, C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
         L.ad_fetch_deps.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut)]
         L.ad_merge_deps.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
@@ -94,8 +96,9 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_shard_alltoall", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
             "ad_shard_levels_allreduce", "ad_shard_order", "ad_shard_set_holders", "ad_shard_levels_deltas",
-            "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows",
-            "ad_recover", "ad_fetch_recovery", "ad_fetch_recovery_flags")
+            "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows", "ad_cfk_update",
+            "ad_recover", "ad_fetch_recovery", "ad_fetch_recovery_flags", "ad_shard_level_edges", "ad_shard_levels_solve",
+            "ad_shard_levels_gather", "ad_ephemeral_read_deps")
 
 
 class DepsEngine:
@@ -150,6 +153,13 @@ class DepsEngine:
         self._dep_sizes = sizes
         return sizes
 
+    def ephemeral_read_deps(self):
+        """Deps with bound = Timestamp.MAX (GetEphemeralReadDeps.java:76): fetch with fetch_deps."""
+        sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
+        self._check(lib().ad_ephemeral_read_deps(self.h, sizes), "ad_ephemeral_read_deps")
+        self._dep_sizes = sizes
+        return sizes
+
     def accept_deps(self):
         """Deps with bound = executeAt (Accept.calculatePartialDeps / GetDeps): fetch with fetch_deps."""
         sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
@@ -193,6 +203,22 @@ class DepsEngine:
         rej = np.zeros(max(nq, 1), np.uint8)
         self._check(lib().ad_fetch_recovery_flags(self.h, rej.ctypes.data), "ad_fetch_recovery_flags")
         return out, rej[:nq]
+
+    def cfk_update(self, gid, status, exec_msb=None, exec_lsb=None, exec_node=None):
+        """Status transitions of kept rows between batches (after cfk_retain, before the next load): gid[m]
+        ascending global ranks, status[m] InternalStatus, optional executeAt arrays (CommandsForKeyTest's
+        transition table; a refused update applies none)."""
+        g = np.ascontiguousarray(gid, np.uint32)
+        s = np.ascontiguousarray(status, np.uint8)
+        u64p, i32p = C.POINTER(C.c_uint64), C.POINTER(C.c_int32)
+        ex = None
+        if exec_msb is not None:
+            ex = (np.ascontiguousarray(exec_msb, np.uint64), np.ascontiguousarray(exec_lsb, np.uint64),
+                  np.ascontiguousarray(exec_node, np.int32))
+        self._check(lib().ad_cfk_update(self.h, len(g), g.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        s.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                        ex[0].ctypes.data_as(u64p) if ex else None, ex[1].ctypes.data_as(u64p) if ex else None,
+                                        ex[2].ctypes.data_as(i32p) if ex else None), "ad_cfk_update")
 
     def cfk_rows(self):
         """(history rows H, gid[n]: global arrival rank of every row of the loaded batch)."""
@@ -323,13 +349,14 @@ class DepsEngine:
         self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
         return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_}
 
-    LEVELS_AUTO, LEVELS_FIXPOINT, LEVELS_BLOCKS, LEVELS_KAHN = 0, 1, 2, 3
+    LEVELS_AUTO, LEVELS_FIXPOINT, LEVELS_BLOCKS, LEVELS_KAHN, LEVELS_PULL_ABORT = 0, 1, 2, 3, 4
 
     def set_level_mode(self, mode):
         """LEVELS_AUTO (default; False): one-pass pull levels for short key chains, executeAt blocks for deep
         key-only batches, Kahn with explicit edges for mixed batches; LEVELS_FIXPOINT (True): always the chain
         fixpoint; LEVELS_BLOCKS: executeAt blocks for every key-only batch; LEVELS_KAHN: the Kahn wavefront
-        instead of the pull levels."""
+        instead of the pull levels; LEVELS_PULL_ABORT (tests): the pull levels abort at once and the Kahn
+        wavefronts recompute the batch (the abort path of AUTO)."""
         mode = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
         self._check(lib().ad_set_level_mode(self.h, mode), "ad_set_level_mode")
 

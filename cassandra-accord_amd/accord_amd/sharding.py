@@ -236,6 +236,9 @@ class ShardStore:
         L.ad_shard_levels_deltas.argtypes = [vp, C.POINTER(C.c_uint32), u64p]
         L.ad_shard_levels_apply.argtypes = [vp, u64p, C.c_size_t]
         L.ad_shard_levels_exchange.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.ad_shard_level_edges.argtypes = [vp, C.POINTER(C.c_size_t), u64p]
+        L.ad_shard_levels_solve.argtypes = [vp, u64p, C.c_size_t, C.POINTER(C.c_uint32)]
+        L.ad_shard_levels_gather.argtypes = [vp, C.POINTER(C.c_uint32)]
         self.delta = False
         self.pairs_sent = 0
 
@@ -368,6 +371,37 @@ class ShardStore:
         self._check(self.L.ad_shard_levels_exchange(self.eng.h, C.byref(ch)), "ad_shard_levels_exchange")
         return bool(ch.value)
 
+    # ---- one-exchange levels (the default): this store's constraint edges, every store's edges solved
+    def level_edges_compute(self):
+        """This store's execution constraints as global-rank edges, kept on the device; returns their count."""
+        m = C.c_size_t(0)
+        self._check(self.L.ad_shard_level_edges(self.eng.h, C.byref(m), None), "ad_shard_level_edges")
+        self.n_edges = m.value
+        return m.value
+
+    def level_edges(self):
+        """The constraint edges as np.uint64 (global src << 32 | global dst), computed on the device."""
+        m = self.level_edges_compute()
+        out = np.zeros(max(m, 1), np.uint64)
+        mm = C.c_size_t(m)
+        self._check(self.L.ad_shard_level_edges(self.eng.h, C.byref(mm), out.ctypes.data_as(C.POINTER(C.c_uint64))),
+                    "ad_shard_level_edges")
+        return out[:m]
+
+    def levels_solve(self, edges):
+        """Levels of the whole batch from every store's edges (host array); returns the level count."""
+        e = np.ascontiguousarray(edges, np.uint64)
+        d = C.c_uint32()
+        self._check(self.L.ad_shard_levels_solve(self.eng.h, e.ctypes.data_as(C.POINTER(C.c_uint64)) if e.size else None,
+                                                 e.size, C.byref(d)), "ad_shard_levels_solve")
+        return d.value
+
+    def levels_gather(self):
+        """RCCL: gather every store's edges (after level_edges_compute) and solve; returns the level count."""
+        d = C.c_uint32()
+        self._check(self.L.ad_shard_levels_gather(self.eng.h, C.byref(d)), "ad_shard_levels_gather")
+        return d.value
+
     def order(self):
         lv = np.zeros(max(self.n_home, 1), np.uint32)
         od = np.zeros(max(self.n_home, 1), np.uint32)
@@ -418,6 +452,22 @@ class GlooTransport:
         self.dist.all_to_all_single(recv, send, output_split_sizes=[int(x) for x in rsz],
                                     input_split_sizes=[int(x) for x in sizes])
         store.import_host(recv.numpy(), rsz)
+
+    def gather_levels(self, store):
+        """One-exchange levels: all-gather every store's constraint edges (padded to the largest count), then
+        the store solves their union.  Returns the level count."""
+        edges = store.level_edges()
+        cnt = self.torch.tensor([edges.size], dtype=self.torch.int64)
+        counts = [self.torch.zeros(1, dtype=self.torch.int64) for _ in range(self.dist.get_world_size())]
+        self.dist.all_gather(counts, cnt)
+        counts = [int(c.item()) for c in counts]
+        top = max(max(counts), 1)
+        mine = self.torch.zeros(top, dtype=self.torch.int64)
+        mine[:edges.size] = self.torch.from_numpy(edges.view(np.int64).copy())
+        parts = [self.torch.zeros(top, dtype=self.torch.int64) for _ in counts]
+        self.dist.all_gather(parts, mine)
+        allv = np.concatenate([p.numpy()[:c] for p, c in zip(parts, counts)]).view(np.uint64)
+        return store.levels_solve(allv)
 
     def allreduce_levels(self, store, changed):
         """Delta mode: all-to-all of the raised levels of shared txns; dense mode: all-reduce(max) of the level
@@ -489,6 +539,10 @@ class RcclTransport(GlooTransport):
         sizes = store.export()
         store.alltoall(self.recv_sizes(sizes))
 
+    def gather_levels(self, store):
+        store.level_edges_compute()
+        return store.levels_gather()       # counts all-gather + grouped edge send/recv over RCCL, then the solve
+
     def allreduce_levels(self, store, changed):
         if store.delta:
             return store.levels_exchange()   # counts all-gather + pair send/recv, all over RCCL
@@ -500,9 +554,10 @@ class LevelsNotConverged(RuntimeError):
     final and must not be reported (every store raises it in the same round: the flag is all-reduced)."""
 
 
-def run_store(store, transport, max_rounds=1 << 16, timings=None):
-    """The per-store protocol after load(): returns the number of distributed level rounds.  Raises
-    LevelsNotConverged if the rounds reach max_rounds while levels are still changing.
+def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="gather"):
+    """The per-store protocol after load(): returns the number of level exchanges (1 with levels="gather",
+    the default; the round count with levels="rounds", the per-round delta / dense exchange, which raises
+    LevelsNotConverged if the rounds reach max_rounds while levels are still changing).
     timings (dict, optional) accumulates wall seconds per phase (each phase ends synchronised)."""
     import time
     clock = time.perf_counter
@@ -520,6 +575,10 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None):
     lap("exchange")
     store.merge()
     lap("merge")
+    if levels == "gather":
+        store.depth = transport.gather_levels(store)
+        lap("levels")
+        return 1
     return run_levels(store, transport, max_rounds, lap)
 
 
@@ -548,7 +607,7 @@ class LocalTransport:
     """Several stores in one process (tests): the same protocol with in-process exchange."""
 
     @staticmethod
-    def run(stores, max_rounds=1 << 16):
+    def run(stores, max_rounds=1 << 16, levels="gather"):
         for s in stores:
             s.preaccept()
         sizes = [s.export() for s in stores]
@@ -559,6 +618,11 @@ class LocalTransport:
             s.import_host(np.concatenate(parts) if parts else np.zeros(0, np.uint8),
                           np.array([sizes[k][d] for k in range(len(stores))], np.uint64))
             s.merge()
+        if levels == "gather":
+            edges = np.concatenate([s.level_edges() for s in stores])
+            for s in stores:
+                s.depth = s.levels_solve(edges)
+            return 1
         changed = [s.levels_round(True) for s in stores]
         rounds = 1
         while True:

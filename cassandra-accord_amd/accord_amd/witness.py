@@ -38,6 +38,15 @@ def order_key(t):
     return (t[0], t[1] >> 16, t[1] & IDENTITY_FLAGS, t[2])
 
 
+IDENTITY_LSB = 0xFFFFFFFFFFFF001E
+
+
+def equals(a, b):
+    """Timestamp.equals (:244-249): msb, the identity bits of lsb (hlc and kind flags; not the domain bit or
+    REJECTED) and node."""
+    return a[0] == b[0] and (a[1] & IDENTITY_LSB) == (b[1] & IDENTITY_LSB) and a[2] == b[2]
+
+
 def compare(a, b):
     ka, kb = order_key(a), order_key(b)
     return (ka > kb) - (ka < kb)
@@ -60,11 +69,13 @@ def with_hlc_at_least(t, min_hlc):
 class NodeClock:
     """Node.now + nowSupplier + topology epoch (local/Node.java:161, 188, 335-375)."""
 
-    def __init__(self, node, epoch_, hlc_now):
+    def __init__(self, node, epoch_, hlc_now, now_epoch=None):
+        """now_epoch: the topology epoch when the node was built (Node.java:188 builds `now` from topology.epoch()
+        then: 0 before the configuration service has reported any topology); default epoch_."""
         self.node = node
         self.topology_epoch = epoch_
         self.clock = hlc_now                                      # nowSupplier.getAsLong()
-        self.now = from_values(epoch_, hlc_now, 0, node)         # Timestamp.fromValues(epoch, now, id)
+        self.now = from_values(epoch_ if now_epoch is None else now_epoch, hlc_now, 0, node)
 
     def unique_now(self, at_least=None):
         if at_least is not None and compare(self.now, at_least) < 0:

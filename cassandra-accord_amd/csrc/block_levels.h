@@ -58,7 +58,7 @@ struct BlOp {                                 // adaptor for the DPP wave scan (
 };
 
 // executeAt rank of every txn (order[k] = txn at rank k)
-__global__ __launch_bounds__(256) void k_bl_erank(size_t n, const uint32_t* __restrict__ order, uint32_t* __restrict__ erank) {
+static __global__ __launch_bounds__(256) void k_bl_erank(size_t n, const uint32_t* __restrict__ order, uint32_t* __restrict__ erank) {
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) erank[order[k]] = (uint32_t)k;
 }
@@ -83,7 +83,7 @@ struct BlCntOp {
 };
 // block of every chain position (blocks cut the entry prefix every bcap; a txn belongs to the block its
 // first entry falls in, so a block holds < bcap + max keys per txn entries)
-__global__ __launch_bounds__(256) void k_bl_chain_block(size_t P, const uint32_t* __restrict__ c_txn, const uint32_t* __restrict__ erank,
+static __global__ __launch_bounds__(256) void k_bl_chain_block(size_t P, const uint32_t* __restrict__ c_txn, const uint32_t* __restrict__ erank,
                                                         const uint32_t* __restrict__ epre, uint32_t bcap, uint32_t* __restrict__ bk,
                                                         uint32_t* __restrict__ bv) {
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_bl_chain_block(size_t P, const uint32_t
     bv[q] = (uint32_t)q;
 }
 // tb[b] = first executeAt rank of block b, boff[b] = first slot of block b (b = 0..B)
-__global__ __launch_bounds__(256) void k_bl_bounds(uint32_t B, size_t n, size_t P, const uint32_t* __restrict__ epre, uint32_t bcap,
+static __global__ __launch_bounds__(256) void k_bl_bounds(uint32_t B, size_t n, size_t P, const uint32_t* __restrict__ epre, uint32_t bcap,
                                                    const uint32_t* __restrict__ sk, uint32_t* __restrict__ tb, uint32_t* __restrict__ boff) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b > B) return;
@@ -117,11 +117,11 @@ constexpr uint32_t BL_NONE = 0xFFFFFFFFu;
 __device__ inline uint32_t bl_block_of(uint32_t q, const uint32_t* c_txn, const uint32_t* erank, const uint32_t* epre, uint32_t bcap) {
     return epre[erank[c_txn[q]]] / bcap;
 }
-__global__ __launch_bounds__(256) void k_bl_inverse(size_t P, const uint32_t* __restrict__ sv, uint32_t* __restrict__ inv) {
+static __global__ __launch_bounds__(256) void k_bl_inverse(size_t P, const uint32_t* __restrict__ sv, uint32_t* __restrict__ inv) {
     const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < P) inv[sv[j]] = (uint32_t)j;
 }
-__global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                     const uint32_t* __restrict__ inv, const uint32_t* __restrict__ c_txn,
                                                     const uint8_t* __restrict__ c_meta, const int32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ erank, const uint32_t* __restrict__ epre, uint32_t bcap,
@@ -282,7 +282,7 @@ __device__ inline void bl_stage(uint32_t b, uint32_t B, int t, int nthr, const u
     if (t == 0) { sbnd[0] = j0; sbnd[1] = j1; sbnd[2] = t0; sbnd[3] = t1; }
 }
 
-__global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const uint32_t* __restrict__ boff, const uint32_t* __restrict__ tb,
+static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const uint32_t* __restrict__ boff, const uint32_t* __restrict__ tb,
                                                        const uint64_t* __restrict__ rec, int2* carry,
                                                        const uint32_t* __restrict__ order, uint32_t* __restrict__ L,
                                                        uint32_t* __restrict__ stats) {

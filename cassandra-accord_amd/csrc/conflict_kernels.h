@@ -84,7 +84,7 @@ struct McArgs {
 };
 
 template <int NV>
-__global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
+static __global__ __launch_bounds__(256) void k_mc_txns(McArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     const uint32_t gi = a.gid ? a.gid[t] : (uint32_t)t;
@@ -164,7 +164,7 @@ struct McRangeArgs {
 };
 
 // sharded stores: the folded local-row answers -> global ranks
-__global__ __launch_bounds__(256) void k_mc_globalize(size_t m, const uint32_t* __restrict__ local,
+static __global__ __launch_bounds__(256) void k_mc_globalize(size_t m, const uint32_t* __restrict__ local,
                                                       const uint32_t* __restrict__ gid, uint32_t* __restrict__ rank) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x < m) rank[x] = local[x] == AD_RANK_NONE ? AD_RANK_NONE : gid[local[x]];
@@ -196,7 +196,7 @@ __device__ inline void mc_fold_wave(const McRangeArgs& a, size_t t, uint64_t* be
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void k_mc_range_keys(McRangeArgs a) {
+static __global__ __launch_bounds__(256) void k_mc_range_keys(McRangeArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n || meta_domain(a.meta[t]) != AD_DOMAIN_RANGE) return;
     const uint32_t gi = a.gid ? a.gid[t] : (uint32_t)t;     // window and drops: global arrival ranks
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_mc_range_keys(McRangeArgs a) {
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void k_mc_range_entries(McRangeArgs a) {
+static __global__ __launch_bounds__(256) void k_mc_range_entries(McRangeArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n) return;
     const uint32_t i = (uint32_t)t;
@@ -307,7 +307,7 @@ struct McCarryArgs {
     int32_t* on;
     uint8_t* fast;                           // [v * n + t]
 };
-__global__ __launch_bounds__(256) void k_mc_carry(McCarryArgs a) {
+static __global__ __launch_bounds__(256) void k_mc_carry(McCarryArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     Ts3 cb{0, 0, 0};
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void k_mc_carry(McCarryArgs a) {
 // Export: the union of the carry table and the batch's per-key maxima (the recorded-entry prefix max at each
 // key segment's end), merged by key ranks into slots with gaps (a key in both lands on one slot), then
 // compacted.  slot[i] of a batch key = i + #carry keys below it; of a carry key = j + #batch keys below it.
-__global__ __launch_bounds__(256) void k_mc_export_slots(uint32_t U, const uint64_t* __restrict__ ukey, const uint32_t* __restrict__ useg,
+static __global__ __launch_bounds__(256) void k_mc_export_slots(uint32_t U, const uint64_t* __restrict__ ukey, const uint32_t* __restrict__ useg,
                                                          const uint64_t* __restrict__ pm_e, const uint32_t* __restrict__ pm_r,
                                                          const uint64_t* __restrict__ em, const uint64_t* __restrict__ el,
                                                          const int32_t* __restrict__ en, size_t m, const uint64_t* __restrict__ ck,
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void k_mc_export_slots(uint32_t U, const uint6
     }
 }
 // CompactFlagOp gives out[k] = the k-th used slot: gather them in slot (= key) order
-__global__ __launch_bounds__(256) void k_mc_export_gather(uint32_t count, const uint32_t* __restrict__ slot,
+static __global__ __launch_bounds__(256) void k_mc_export_gather(uint32_t count, const uint32_t* __restrict__ slot,
                                                           const uint64_t* __restrict__ sk, const uint64_t* __restrict__ sm,
                                                           const uint64_t* __restrict__ sl, const int32_t* __restrict__ sn,
                                                           uint64_t* __restrict__ ok, uint64_t* __restrict__ om,

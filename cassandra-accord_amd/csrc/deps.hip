@@ -1,0 +1,285 @@
+// deps.hip — the deps stage: CFK elision scan, walks, per-txn KeyDeps layout and unions, RangeDeps join.
+#include "engine_internal.h"
+
+// ---------------------------------------------------------------------------------------------------
+// deps
+// ---------------------------------------------------------------------------------------------------
+// Capacity (elements) of CSR block `block`'s data buffers as currently allocated (0 if none).
+size_t csr_cap(ad_handle* h, size_t block, int which, size_t elem) {
+    const size_t slot = S_CSR0 + 10 * block + which;
+    return slot < h->bufs.size() ? h->bufs[slot].cap / elem : 0;
+}
+
+static __global__ void k_ovf_sizes(uint32_t count, const uint2* items, const uint32_t* const* key_off, const uint32_t* const* k2t_off,
+                            uint32_t* ne) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t t = items[i].x, c = items[i].y;
+    ne[i] = k2t_off[c][t + 1] - k2t_off[c][t] - (key_off[c][t + 1] - key_off[c][t]);
+}
+
+// CSRs that overflowed the LDS union: one sync to learn how many; each gets a 1024-thread workgroup with
+// 128 KiB of LDS, or a slice of global memory above UNION_CAP_BIG entries.  The CSR blocks are the key
+// classes (large txns) and, when the batch has ranges, the RangeDeps views (item.y >= 2R: range view).
+int union_overflow(ad_handle* h, LdsUnionArgs la, uint32_t* ovf_count, uint2* ovf, bool has_range) {
+    hipStream_t st = h->st;
+    uint32_t count = 0;
+    HIPCHK(h, hipMemcpyAsync(&count, ovf_count, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (count == 0) return AD_OK;
+    count = std::min<uint32_t>(count, 1u << 20);
+    (void)has_range;
+    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
+    // tables of all CSRs the first pass may have queued: key classes [0, nvc), range views [nvc, nvc+nv)
+    LdsUnionArgs b = la;
+    std::vector<const uint32_t*> ko(nvc + nv), mo(nvc + nv);
+    for (int c = 0; c < nvc + nv; ++c) {
+        const Csr& x = c < nvc ? h->deps[c] : h->rdeps[c - nvc];
+        ko[c] = x.key_off; mo[c] = x.k2t_off;
+        b.key_off[c] = x.key_off; b.k2t_off[c] = x.k2t_off; b.ent_off[c] = x.ent_off; b.k2t[c] = x.k2t;
+        b.txns[c] = x.txns; b.tcnt[c] = x.tcnt;
+    }
+    const uint32_t** dko = nullptr;
+    uint32_t* ne = nullptr;
+    CK(dalloc(h, S_OVFT, (uint64_t**)&dko, 2 * (nvc + nv)));
+    CK(dalloc(h, S_OVFN, &ne, count));
+    HIPCHK(h, hipMemcpyAsync(dko, ko.data(), (nvc + nv) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(dko + nvc + nv, mo.data(), (nvc + nv) * 8, hipMemcpyHostToDevice, st));
+    k_ovf_sizes<<<ceil_div((long)count, 256), 256, 0, st>>>(count, ovf, dko, dko + nvc + nv, ne);
+    std::vector<uint32_t> hne(count);
+    HIPCHK(h, hipMemcpyAsync(hne.data(), ne, count * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    std::vector<uint64_t> goff(count, 0);
+    uint64_t gtot = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        if (hne[i] > (uint32_t)UNION_CAP_BIG) {
+            uint64_t n2 = 1;
+            while (n2 < hne[i]) n2 <<= 1;
+            goff[i] = gtot;
+            gtot += n2;
+        }
+    }
+    uint32_t* gbuf = nullptr;
+    uint64_t* dgoff = nullptr;
+    CK(dalloc(h, S_OVFG, &gbuf, std::max<uint64_t>(gtot, 1)));
+    CK(dalloc(h, S_OVFO, &dgoff, count));
+    HIPCHK(h, hipMemcpyAsync(dgoff, goff.data(), count * 8, hipMemcpyHostToDevice, st));
+    b.items = ovf; b.gbuf = gbuf; b.gbuf_off = dgoff;
+    k_union_big<<<count, UB_BIG, 0, st>>>(b, count);
+    HIPCHK(h, hipStreamSynchronize(st));    // host tables
+    return AD_OK;
+}
+
+// Accept / GetDeps bound: per txn the number of batch TxnIds below its executeAt (TxnIds and executeAts share
+// one packed order; tx_ts ascends with the batch).
+static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64_t* __restrict__ tx_ts, const uint64_t* __restrict__ ex1,
+                                                   uint32_t* __restrict__ qpos, int bound_max) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (bound_max) { qpos[i] = (uint32_t)n; return; }   // Timestamp.MAX: every TxnId is below it
+    const uint64_t e = ex1[i] - 1;
+    size_t lo = i, hi = n;              // executeAt >= TxnId
+    while (lo < hi) { const size_t m = (lo + hi) >> 1; if (tx_ts[m] < e) lo = m + 1; else hi = m; }
+    qpos[i] = (uint32_t)lo;
+}
+
+int stage_deps(ad_handle* h) {
+    StageScope sc(h, STAGE_DEPS);
+    const size_t n = h->n, P = h->P, Q = h->Q;
+    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
+    hipStream_t st = h->st;
+    // directKeyDeps entries come only from key-domain sync points (CommandsForKey.managesExecution is false
+    // for them, Deps.java:80-106); without any in the batch every directKeyDeps CSR is empty, so only the R
+    // keyDeps classes are computed (computed class k = CSR cls[k]) and the direct CSRs are zero offsets.
+    const bool direct = h->n_special > 0;
+    const int nc = direct ? nvc : nv;
+    int cls[NVC_MAX];
+    for (int k = 0; k < nc; ++k) cls[k] = direct ? k : 2 * k;
+    h->deps_direct = direct;
+    h->deps.resize(nvc);
+    for (int vc = 0; vc < nvc; ++vc) CK(alloc_csr(h, vc, h->deps[vc], n));
+    for (int v = 0; v < nv; ++v) CK(alloc_csr(h, CSR_RANGE0 + v, h->rdeps[v], n));
+    for (int k = 0; k < nc; ++k) dirty_csr(h, cls[k]);
+    for (int v = 0; v < nv; ++v) dirty_csr(h, CSR_RANGE0 + v);
+    if (P > 0) {
+        { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->e_txn, h->e_meta, h->e_exec1); }
+        ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
+                    h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm,
+                    h->key_bits > 32 ? h->keys : nullptr, h->sval};
+        KScope ks(K_SCAN_ELIDE, P);
+        scan_any(h, eop, P);
+    }
+    // ---- executeAt-bound queries: the arrival position of each bound (first TxnId >= executeAt)
+    const uint32_t* qpos = nullptr;
+    if (h->accept) {
+        CK(dalloc(h, S_QPOS, &h->qpos, std::max<size_t>(n, 1)));
+        if (n) k_query_pos<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->tx_ts, h->ex1, h->qpos, h->bound_max ? 1 : 0);
+        qpos = h->qpos;
+    }
+    // ---- virtual items of large txns
+    h->V = 0;
+    VItemArgs va{};
+    va.n = n; va.meta = h->meta; va.key_off = h->key_off; va.keys = h->keys; va.range_off = h->range_off;
+    va.rs = h->range_s; va.re = h->range_e; va.e_txn = h->e_txn;
+    va.ukey = h->ukey; va.useg = h->useg; va.prm = h->prm; va.vn = h->vn; va.voff = h->voff; va.qpos = qpos;
+    if (h->n_large > 0) {
+        KScope ks(K_VITEMS);
+        k_vitems<false><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
+        scan_offsets(h, h->vn, h->voff, n);
+        uint32_t V = 0;
+        HIPCHK(h, hipMemcpyAsync(&V, h->voff + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        h->V = V;
+        // 12 B + 4 B per (view, class) per item (C4: ~2.5 * 10^9 items): the item's key and segment come from
+        // its distinct-key index, the fill slots overwrite the counts in place
+        CK(dalloc(h, S_VTXN, &h->vi_txn, V)); CK(dalloc(h, S_VPOS, &h->vi_pos, V)); CK(dalloc(h, S_VSEG, &h->vi_u, V));
+        CK(dalloc(h, S_VCNT, &h->vcnt, (size_t)V * nc));
+        va.vi_txn = h->vi_txn; va.vi_pos = h->vi_pos; va.vi_u = h->vi_u;
+        if (V > 0) k_vitems<true><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
+    }
+    // ---- walk (count)
+    WalkArgs wa{};
+    wa.e_txn = h->e_txn; wa.e_meta = h->e_meta; wa.e_exec1 = h->e_exec1; wa.seg_start = h->seg_start;
+    wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
+    wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
+    wa.gid = (h->sharded || h->hist_active) ? h->gid : nullptr;
+    wa.nh = h->nh; wa.prm = h->prm;
+    wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
+    wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
+    wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
+    wa.qpos = qpos; wa.ex1 = h->ex1; wa.bound_max = h->bound_max ? 1 : 0;
+    if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt, 0, (size_t)nc * P * 4, st));   // segment heads keep zero counts
+    launch_walk_nv(nv, wa, false, direct, st);
+    TxnArgs ta{};
+    ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt = h->cnt;
+    ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
+    ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
+    uint32_t* overflow = h->totd + MAX_TOTALS - 1;       // fused-layout overflow flag (read with the totals)
+    if (n > 0 && h->V > 0) {
+        KScope ks(K_VITEMS);
+        launch_large_sums_nv(nv, ta, direct, st);
+    }
+    if (n > 0) {
+        HIPCHK(h, hipMemsetAsync(overflow - 1, 0, 8, st));     // [heavy-merge hint, layout overflow]
+        KScope ks(K_SCAN_OFFSETS, n);
+        launch_offsets_nv(h, nv, direct, cls, overflow);
+    } else {
+        for (int k = 0; k < nc; ++k) csr_offsets(h, h->deps[cls[k]], h->nk, h->ne);
+    }
+    if (!direct)
+        for (int v = 0; v < nv; ++v) CK(zero_csr(h, 2 * v + 1, h->deps[2 * v + 1], n));
+    // ---- RangeDeps (count)
+    RangeArgs ra{};
+    ra.n = n; ra.Q = Q; ra.key_off = h->key_off; ra.keys = h->keys; ra.range_off = h->range_off; ra.rs = h->range_s;
+    ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
+    ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
+    ra.qpos = qpos;
+    ra.gid = wa.gid;
+    if (Q > 0 && n > 0) {
+        launch_range_nv(nv, ra, false, st);
+        for (int v = 0; v < nv; ++v) csr_offsets(h, h->rdeps[v], h->rnk + (size_t)v * n, h->rne + (size_t)v * n);
+    }
+    // ---- sizes -> host (one sync), allocate outputs
+    const int ncsr = nc + nv;
+    std::vector<uint32_t> tot(3 * ncsr, 0);
+    auto csr_at = [&](int c) -> Csr& { return c < nc ? h->deps[cls[c]] : h->rdeps[c - nc]; };
+    TotTable tt{};
+    for (int c = 0; c < (Q > 0 ? ncsr : nc); ++c) {
+        Csr& x = csr_at(c);
+        tt.src[3 * c + 0] = x.key_off + n; tt.src[3 * c + 1] = x.k2t_off + n; tt.src[3 * c + 2] = x.ent_off + n;
+        tt.count = 3 * c + 3;
+    }
+    const int ncol = tt.count;
+    tt.src[tt.count++] = overflow;
+    tt.src[tt.count++] = overflow - 1;
+    std::vector<uint32_t> got(tt.count, 0);
+    CK(read_totals_params(h, tt, got.data()));
+    std::copy(got.begin(), got.begin() + ncol, tot.begin());
+    const bool fused_layout = n > 0 && got[ncol] == 0;
+    h->merge_heavy = n == 0 || got[ncol + 1] != 0 || h->n_large > 0 || Q > 0;
+    CK(check_params(h));
+    h->deps_entries = 0;
+    for (int c = 0; c < ncsr; ++c) {
+        Csr& x = csr_at(c);
+        x.nkeys = tot[3 * c]; x.nk2t = tot[3 * c + 1]; x.ncap = tot[3 * c + 2];
+        h->deps_entries += x.ncap;
+        if (c < nc) {
+            CK(alloc_csr_data(h, cls[c], x, 1));
+            ta.out_key_off[c] = x.key_off; ta.out_k2t_off[c] = x.k2t_off; ta.out_keys[c] = x.keys; ta.out_k2t[c] = x.k2t;
+            wa.k2t[c] = x.k2t;
+        } else {
+            CK(alloc_csr_data(h, CSR_RANGE0 + (c - nc), x, 2));
+            const int v = c - nc;
+            ra.key_off_v[v] = x.key_off; ra.k2t_off_v[v] = x.k2t_off; ra.keys_v[v] = x.keys; ra.k2t_v[v] = x.k2t;
+        }
+    }
+    // ---- fill
+    if (n > 0 && !fused_layout) { KScope ks(K_TXN_LAYOUT, P); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
+    if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
+    launch_walk_nv(nv, wa, true, direct, st);
+    if (Q > 0 && n > 0) launch_range_nv(nv, ra, true, st);
+    UnionArgs ua{};
+    ua.n = n; ua.nvc = nc; ua.meta = h->meta;
+    for (int vc = 0; vc < nc; ++vc) {
+        Csr& c = h->deps[cls[vc]];
+        ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
+        ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
+    }
+    if (n > 0) { KScope ks(K_TXN_UNION, n); launch_union_nv(nv, ua, direct, st); }
+    // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
+    if (n > 0 && (h->n_large > 0 || Q > 0)) {
+        KScope ks(K_UNION_LDS);
+        LdsUnionArgs la{};
+        la.n = n; la.meta = h->meta; la.prm = h->prm;
+        constexpr uint32_t OVF_CAP = 1u << 20;
+        uint32_t* ovf_count = nullptr;
+        uint2* ovf = nullptr;
+        CK(dalloc(h, S_OVF, &ovf_count, 64));
+        CK(dalloc(h, S_OVFL, &ovf, OVF_CAP));
+        HIPCHK(h, hipMemsetAsync(ovf_count, 0, 4, st));
+        la.ovf_count = ovf_count; la.ovf = ovf; la.ovf_cap = OVF_CAP;
+        if (h->n_large > 0) {
+            la.ncsr = nc; la.csr_base = 0; la.csr_step = direct ? 1 : 2; la.only_large = 1;
+            for (int vc = 0; vc < nvc; ++vc) {
+                Csr& c = h->deps[vc];
+                la.key_off[vc] = c.key_off; la.k2t_off[vc] = c.k2t_off; la.ent_off[vc] = c.ent_off; la.k2t[vc] = c.k2t;
+                la.txns[vc] = c.txns; la.tcnt[vc] = c.tcnt;
+            }
+            // one workgroup per (large txn, CSR), not per (txn, CSR)
+            uint32_t* lrows = nullptr;
+            CK(dalloc(h, S_LROWS, &lrows, n + 64));
+            device_scan(LargeRowsOp{h->meta, lrows, lrows + n, n}, n, (uint32_t*)h->scratch, st);
+            la.rows = lrows; la.rows_total = lrows + n;
+            k_union_lds<<<dim3((unsigned)h->n_large, (unsigned)nc), UB, 0, st>>>(la);
+            la.rows = nullptr; la.rows_total = nullptr;
+        }
+        if (Q > 0) {
+            la.ncsr = nv; la.csr_base = nvc; la.csr_step = 1; la.only_large = 0;
+            for (int v = 0; v < nv; ++v) {
+                Csr& c = h->rdeps[v];
+                la.key_off[nvc + v] = c.key_off; la.k2t_off[nvc + v] = c.k2t_off; la.ent_off[nvc + v] = c.ent_off;
+                la.k2t[nvc + v] = c.k2t; la.txns[nvc + v] = c.txns; la.tcnt[nvc + v] = c.tcnt;
+            }
+            // small lists by single-wave workgroups, the rest queued for 256-thread workgroups
+            uint32_t* med_count = nullptr;
+            uint2* med = nullptr;
+            CK(dalloc(h, S_UMEDC, &med_count, 64));
+            CK(dalloc(h, S_UMED, &med, (size_t)n * nv + 1));
+            HIPCHK(h, hipMemsetAsync(med_count, 0, 4, st));
+            la.med_count = med_count; la.med = med;
+            k_union_lds_small<<<dim3((unsigned)n, (unsigned)nv), US_T, 0, st>>>(la);
+            k_union_lds_list<<<8192, UB, 0, st>>>(la);
+        }
+        CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
+    }
+    // Virtual-item work arrays are dead once the CSRs are filled; they stay allocated for the next batch
+    // (re-allocating C4's ~90 GB of them every batch cost more than the walks) unless the merge runs out of
+    // HBM, when release_dead gives them back (STAGE_MERGE).
+    h->have_deps = true;
+    h->ls.chains_ready = false;
+    h->times.deps_entries = h->deps_entries;
+    h->times.key_classes = (uint32_t)nc;
+    h->times.level_edges = h->P;
+    h->times.walk_items = (uint32_t)(h->P - (h->P ? h->hprm.n_keys_u : 0));
+    return AD_OK;
+}

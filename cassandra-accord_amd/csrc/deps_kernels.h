@@ -45,7 +45,7 @@ struct Params {                // device-side batch statistics (filled by k_minm
 enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
                   ERR_RANGEBITS = 32, ERR_CAP = 64 };
 
-__global__ void k_params_init(Params* p) {
+static __global__ void k_params_init(Params* p) {
     p->msb_min = ~0ull; p->msb_max = 0; p->hlc_min = ~0ull; p->hlc_max = 0;
     p->key_min = ~0ull; p->key_max = 0; p->rs_min = ~0ull; p->re_max = 0; p->rw_max = 0;
     p->node_min_b = ~0u; p->node_max_b = 0; p->max_keys = 0; p->err = 0;
@@ -65,7 +65,7 @@ __device__ inline unsigned long long wmax64(unsigned long long v) {
 
 // Batch statistics: per-thread accumulation, wave shuffles, one LDS combine per block, one atomic per
 // block and field (per-wave atomics on one address serialise: the first version spent 0.44 ms here).
-__global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __restrict__ tm, const uint64_t* __restrict__ tl,
+static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __restrict__ tm, const uint64_t* __restrict__ tl,
                                                 const int32_t* __restrict__ tn, const uint64_t* __restrict__ em,
                                                 const uint64_t* __restrict__ el, const int32_t* __restrict__ en,
                                                 const uint32_t* __restrict__ key_off, const uint64_t* __restrict__ keys,
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t* __rest
 }
 
 // second level of k_minmax: one block folds the per-block partials into Params (no contended atomics)
-__global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out) {
+static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out) {
     constexpr int NF = 14, NSUM = 12;
     __shared__ unsigned long long red[4][NF];
     unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned l
 }
 
 // Packs timestamps, builds per-txn meta, the sort input and validates footprints.  One thread per txn.
-__global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_min,
+static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_min,
                                               const uint64_t* __restrict__ tm, const uint64_t* __restrict__ tl,
                                               const int32_t* __restrict__ tn, const uint64_t* __restrict__ em,
                                               const uint64_t* __restrict__ el, const int32_t* __restrict__ en,
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_
 
 // Sorted entry SoA: one random 16-byte record read per entry (the pair's txn, meta and executeAt were
 // packed per pair by k_pack in pair order, i.e. coalesced), instead of three dependent random loads.
-__global__ __launch_bounds__(256) void k_gather_entries(size_t P, const uint32_t* __restrict__ sval,
+static __global__ __launch_bounds__(256) void k_gather_entries(size_t P, const uint32_t* __restrict__ sval,
                                                         const PairRec* __restrict__ prec,
                                                         uint32_t* __restrict__ e_txn, uint8_t* __restrict__ e_meta,
                                                         uint64_t* __restrict__ e_exec1) {
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void k_gather_entries(size_t P, const uint32_t
 // Segmented prefix state of CommandsForKey.mapReduceActive over the (key, TxnId)-sorted entries.
 // Wide key spreads: the sort key of pass `shift` (0: low 32 bits, 32: high bits) of the pairs in their current
 // order (val = pair index), for an LSD sort of the full 64-bit (key - key_min) by 32-bit halves.
-__global__ __launch_bounds__(256) void k_pair_key_half(size_t P, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ val,
+static __global__ __launch_bounds__(256) void k_pair_key_half(size_t P, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ val,
                                                        uint64_t key_min, int shift, uint32_t* __restrict__ out) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x < P) out[x] = (uint32_t)((keys[val[x]] - key_min) >> shift);
@@ -337,6 +337,8 @@ struct WalkArgs {
     // of its bound, q = #{j : TxnId_j < executeAt_i}; ex1 = executeAt + 1
     const uint32_t* qpos;
     const uint64_t* ex1;
+    int bound_max;            // GetEphemeralReadDeps: bound Timestamp.MAX (qpos = n; no executeAt bound)
+    __device__ uint64_t bound1(uint32_t i) const { return bound_max ? ~0ull : ex1[i]; }
 };
 
 // Next emitted "elidable" (committed Read/Write) entry at or before q, or seg0-1.
@@ -419,8 +421,15 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t gq, ui
 // waves (a grid over all P entries left ~5 of 6 lanes idle in every wave of this latency-bound walk).
 // Executeat-bound queries (a.qpos): one thread per entry (a segment head can have deps that arrived after it),
 // walking from the first entry of the segment whose TxnId reaches the bound.
-template <int NV, bool FILL>
-__global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
+// DIRECT: the batch holds key-domain sync points (n_special > 0), so entries split into keyDeps and
+// directKeyDeps (class vc = 2 view + direct); otherwise every emitted entry is a keyDeps entry (vc = view) and
+// the per-pair count / slot words are R instead of 2R.
+template <int NV, bool DIRECT>
+__device__ inline int walk_class(int v, bool direct) { return DIRECT ? 2 * v + (direct ? 1 : 0) : v; }
+
+template <int NV, bool FILL, bool DIRECT>
+static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
+    constexpr int NC = DIRECT ? 2 * NV : NV;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= (a.qpos ? a.P : a.P - a.prm->n_keys_u)) return;
     const size_t s = a.qpos ? x : (size_t)a.nh[x];
@@ -429,25 +438,14 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     const uint32_t mi = a.e_meta[s];
     const uint32_t qk = meta_kind(mi);
     // the pair's counts / slots live AoS by pair index (the per-txn kernels read them contiguously)
-    const size_t pb = (size_t)a.sval[s] * (2 * NV);
-    uint32_t c0[NV], c1[NV];   // count mode: counts; fill mode: next write slot (descending)
+    const size_t pb = (size_t)a.sval[s] * NC;
+    uint32_t c[NC];            // count mode: counts; fill mode: next write slot (descending)
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        if (FILL) {
-            const uint2 d = reinterpret_cast<const uint2*>(a.dst + pb)[v];   // last slots of the pair's runs (filled descending)
-            c0[v] = d.x;
-            c1[v] = d.y;
-        } else {
-            c0[v] = 0; c1[v] = 0;
-        }
-    }
+    for (int k = 0; k < NC; ++k) c[k] = FILL ? a.dst[pb + k] : 0u;
     auto emit = [&](int v, bool direct, uint32_t j) {
-        if (FILL) {
-            if (direct) a.k2t[2 * v + 1][c1[v]--] = (int32_t)j;
-            else a.k2t[2 * v][c0[v]--] = (int32_t)j;
-        } else {
-            if (direct) c1[v]++; else c0[v]++;
-        }
+        const int k = walk_class<NV, DIRECT>(v, direct);
+        if (FILL) a.k2t[k][c[k]--] = (int32_t)j;
+        else c[k]++;
     };
     // small key-domain query txns only (large ones are virtual items)
     const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE);
@@ -460,7 +458,7 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
                 const size_t m = (lo + hi) >> 1;
                 if (a.seg_start[m] == seg0 && a.e_txn[m] < qi) lo = m + 1; else hi = m;
             }
-            walk_query<NV>(a, i, a.gid ? a.gid[i] : qi, a.ex1[i], qk, (int)lo, seg0, emit);
+            walk_query<NV>(a, i, a.gid ? a.gid[i] : qi, a.bound1(i), qk, (int)lo, seg0, emit);
         } else {
             const uint32_t gi = a.gid ? a.gid[i] : i;
             walk_query<NV>(a, i, gi, a.tx_ts[i] + 1, qk, (int)s, seg0, emit);
@@ -468,34 +466,35 @@ __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     }
     if (!FILL) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) reinterpret_cast<uint2*>(a.cnt + pb)[v] = make_uint2(c0[v], c1[v]);
+        for (int k = 0; k < NC; ++k) a.cnt[pb + k] = c[k];
     }
 }
 
-// Virtual items (large txns), one thread per item; counts/slots AoS [x * 2NV + vc].
-template <int NV, bool FILL>
-__global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
+// Virtual items (large txns), one thread per item; counts/slots AoS [x * NC + vc].
+template <int NV, bool FILL, bool DIRECT>
+static __global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
+    constexpr int NC = DIRECT ? 2 * NV : NV;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= a.V) return;
     const uint32_t i = a.vi_txn[x];
     const uint32_t mi = a.meta[i];
     const uint32_t qk = meta_kind(mi);
-    uint32_t c[2 * NV];
+    uint32_t c[NC];
 #pragma unroll
-    for (int vc = 0; vc < 2 * NV; ++vc)
-        c[vc] = FILL ? a.vdst[x * (2 * NV) + vc] : 0u;
+    for (int vc = 0; vc < NC; ++vc)
+        c[vc] = FILL ? a.vdst[x * NC + vc] : 0u;
     auto emit = [&](int v, bool direct, uint32_t j) {
-        const int vc = 2 * v + (direct ? 1 : 0);
+        const int vc = walk_class<NV, DIRECT>(v, direct);
         if (FILL) a.k2t[vc][c[vc]--] = (int32_t)j;
         else c[vc]++;
     };
     if (qk <= AD_KIND_EXCLUSIVE_SYNC_POINT) {
         const uint32_t gq = a.qpos ? a.qpos[i] : (a.gid ? a.gid[i] : i);
-        walk_query<NV>(a, i, gq, a.qpos ? a.ex1[i] : a.tx_ts[i] + 1, qk, (int)a.vi_pos[x], (int)a.useg[a.vi_u[x]], emit);
+        walk_query<NV>(a, i, gq, a.qpos ? a.bound1(i) : a.tx_ts[i] + 1, qk, (int)a.vi_pos[x], (int)a.useg[a.vi_u[x]], emit);
     }
     if (!FILL) {
 #pragma unroll
-        for (int vc = 0; vc < 2 * NV; ++vc) a.vcnt[x * (2 * NV) + vc] = c[vc];
+        for (int vc = 0; vc < NC; ++vc) a.vcnt[x * NC + vc] = c[vc];
     }
 }
 
@@ -523,7 +522,7 @@ struct TxnArgs {
 };
 
 // Per txn: keys in ascending order (Keys are sorted), KeyDeps header offsets, per-item first-entry slot.
-__global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
+static __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     if (a.meta[t] & META_LARGE) return;            // k_large_layout
@@ -560,7 +559,7 @@ __device__ inline uint32_t wave_incl_sum(uint32_t v) {
     return v;
 }
 template <int NVC>
-__global__ __launch_bounds__(256) void k_large_sums(TxnArgs a) {
+static __global__ __launch_bounds__(256) void k_large_sums(TxnArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n || !(a.meta[t] & META_LARGE)) return;
     const uint32_t b = a.voff[t], e = a.voff[t + 1];
@@ -582,7 +581,7 @@ __global__ __launch_bounds__(256) void k_large_sums(TxnArgs a) {
     }
 }
 template <int NVC>
-__global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
+static __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n || !(a.meta[t] & META_LARGE)) return;
     const uint32_t b = a.voff[t], e = a.voff[t + 1];
@@ -621,7 +620,6 @@ __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
 constexpr uint32_t MERGE_HEAVY_HINT = 256;
 template <int NVC>
 struct OffsetsOp {
-    static_assert(NVC % 2 == 0, "key + direct class per view: NVC = 2R");
     struct S { uint32_t k[NVC], e[NVC]; };
     size_t n;
     const uint8_t* meta;
@@ -650,6 +648,17 @@ struct OffsetsOp {
         for (int c = 0; c < NVC; ++c) { s.k[c] = 0; s.e[c] = 0; }
         return s;
     }
+    // the NVC count words of pair x (dwordx2 loads when the pair's words are 8-byte aligned: NVC even)
+    __device__ void load_counts(uint32_t x, uint32_t* v) const {
+        if (NVC % 2 == 0) {
+            const uint2* p = reinterpret_cast<const uint2*>(cnt + (size_t)x * NVC);
+#pragma unroll
+            for (int c2 = 0; c2 < NVC / 2; ++c2) { const uint2 w = p[c2]; v[2 * c2] = w.x; v[2 * c2 + 1] = w.y; }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NVC; ++c) v[c] = cnt[(size_t)x * NVC + c];
+        }
+    }
     __device__ S load(size_t t) const {
         S s = identity();
         const bool large = meta[t] & META_LARGE;
@@ -659,17 +668,12 @@ struct OffsetsOp {
             return s;
         }
         const uint32_t b = key_off[t], e = key_off[t + 1];
-        // a pair's NVC counts are contiguous and 8-byte aligned (NVC = 2R): dwordx2 loads
+        // a pair's NVC counts are contiguous
         for (uint32_t x = b; x < e; ++x) {
-            const uint2* p = reinterpret_cast<const uint2*>(cnt + (size_t)x * NVC);
+            uint32_t v[NVC];
+            load_counts(x, v);
 #pragma unroll
-            for (int c2 = 0; c2 < NVC / 2; ++c2) {
-                const uint2 v = p[c2];
-                s.k[2 * c2] += v.x > 0 ? 1u : 0u;
-                s.e[2 * c2] += v.x;
-                s.k[2 * c2 + 1] += v.y > 0 ? 1u : 0u;
-                s.e[2 * c2 + 1] += v.y;
-            }
+            for (int c = 0; c < NVC; ++c) { s.k[c] += v[c] > 0 ? 1u : 0u; s.e[c] += v[c]; }
         }
         return s;
     }
@@ -704,11 +708,10 @@ struct OffsetsOp {
             uint32_t cv[4][NVC];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint2* p = reinterpret_cast<const uint2*>(src + (size_t)(b + j) * NVC);
+                if (b + j < e) load_counts(b + j, cv[j]);
+                else {
 #pragma unroll
-                for (int c2 = 0; c2 < NVC / 2; ++c2) {
-                    const uint2 v = b + j < e ? p[c2] : make_uint2(0u, 0u);
-                    cv[j][2 * c2] = v.x; cv[j][2 * c2 + 1] = v.y;
+                    for (int c = 0; c < NVC; ++c) cv[j][c] = 0u;
                 }
             }
             uint64_t kx[4];
@@ -828,7 +831,7 @@ struct UnionArgs {
 
 // Small txns: register K-way merge of the per-key lists (large txns: k_union_lds).
 template <int NVC>
-__global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
+static __global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     if (a.meta[t] & META_LARGE) return;

@@ -150,7 +150,7 @@ struct ChainOp {
 
 // Short chains: one thread per short multi-entry segment; segments not queued for this iteration
 // (stamp != it) exit at once.  Walks the chain in executeAt order with the same recurrence.
-__global__ __launch_bounds__(256) void k_seg_short(const uint32_t* __restrict__ heads, uint32_t count, uint32_t it,
+static __global__ __launch_bounds__(256) void k_seg_short(const uint32_t* __restrict__ heads, uint32_t count, uint32_t it,
                                                    const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
                                                    uint32_t* L, int32_t* __restrict__ pm_all, PushCtx push,
                                                    uint32_t* __restrict__ work_left) {
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_seg_short(const uint32_t* __restrict__ 
 
 // Segment table: length and stamp at each head; per position: is it the head of a short multi-entry
 // segment (-> heads list), is it inside a long segment (-> long positions list).
-__global__ __launch_bounds__(256) void k_seg_table(size_t P, const int32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_len,
+static __global__ __launch_bounds__(256) void k_seg_table(size_t P, const int32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_len,
                                                    uint32_t* __restrict__ stamp, uint32_t* __restrict__ any_long) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool lng = false;
@@ -220,7 +220,7 @@ struct SegListOp {                 // two compactions in one scan: short multi h
         if (i + 1 == n) { totals[0] = inc.a; totals[1] = inc.b; }
     }
 };
-__global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict__ heads, uint32_t count, uint32_t* __restrict__ stamp) {
+static __global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict__ heads, uint32_t count, uint32_t* __restrict__ stamp) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) stamp[heads[i]] = 0u;
 }
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_stamp_reset(const uint32_t* __restrict_
 // has dependants iff it is not the chain's last entry, a Read iff a Write follows it.  A pair with no
 // dependants gets -1, so raising T does not re-walk that chain.  With (c), every position's prefix max
 // (pm_all) is read by unmanaged txns, so every chain containing T is re-walked.
-__global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ c_pair, const uint8_t* __restrict__ c_meta,
+static __global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __restrict__ c_pair, const uint8_t* __restrict__ c_meta,
                                                   const int32_t* __restrict__ seg_start, const uint32_t* __restrict__ seg_len,
                                                   int32_t* __restrict__ pair_seg, int prune) {
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void k_pair_seg(size_t P, const uint32_t* __re
     pair_seg[c_pair[q]] = tgt;
 }
 
-__global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+static __global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                                     const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
                                                     uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
                                                     uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair) {
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_chain_copy(size_t P, const uint32_t* __
 }
 
 // Per-segment fix-up: entries of one key ordered by executeAt (insertion sort; one thread per segment).
-__global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __restrict__ seg_start,
+static __global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __restrict__ seg_start,
                                                      uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
                                                      uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void k_chain_order(size_t P, const int32_t* __
 }
 
 // Rejects kinds the batch execution order does not model (local-only txns are not globally visible).
-__global__ __launch_bounds__(256) void k_level_kinds(size_t n, const uint8_t* __restrict__ meta, uint32_t* __restrict__ flag) {
+static __global__ __launch_bounds__(256) void k_level_kinds(size_t n, const uint8_t* __restrict__ meta, uint32_t* __restrict__ flag) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool bad = false;
     if (t < n) bad = meta_kind(meta[t]) == AD_KIND_LOCAL_ONLY;
@@ -351,7 +351,7 @@ struct EdgeArgs {
 // for an ExclusiveSyncPoint; sync points also fold the key's managed-execution entries between their first
 // and last dependency in TxnId order (:760-777; a loop over that byId range).
 // One wave per txn, one lane per key of its merged KeyDeps (a C4 range txn has ~3*10^3 of them).
-__global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
+static __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n) return;
     const uint32_t kb = a.mk_key_off[t], ke = a.mk_key_off[t + 1];
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
 }
 
 // (b) + (c) relaxation, one thread per txn.
-__global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int do_c, const uint32_t* prev) {
+static __global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int do_c, const uint32_t* prev) {
     if (prev && !(prev[0] | prev[1] | prev[2])) return;     // nothing changed in the previous iteration
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool raised = false, queued = false;
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(256) void k_level_edges(EdgeArgs a, int do_b, int d
     wave_set_flag(queued, a.work_left);
 }
 
-__global__ __launch_bounds__(256) void k_exec_split(size_t n, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ idx,
+static __global__ __launch_bounds__(256) void k_exec_split(size_t n, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ idx,
                                                     uint32_t* __restrict__ key, int hi) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -448,12 +448,12 @@ __global__ __launch_bounds__(256) void k_exec_split(size_t n, const uint64_t* __
     const uint64_t e = ex1[t] - 1;
     key[i] = hi ? (uint32_t)(e >> 32) : (uint32_t)e;
 }
-__global__ __launch_bounds__(256) void k_iota(size_t n, uint32_t* __restrict__ v) {
+static __global__ __launch_bounds__(256) void k_iota(size_t n, uint32_t* __restrict__ v) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
 }
 // gather + block-reduced max (one atomic per block)
-__global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx,
+static __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx,
                                                     uint32_t* __restrict__ dst, uint32_t* __restrict__ maxv) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t v = 0;
@@ -485,10 +485,14 @@ __global__ __launch_bounds__(256) void k_gather_u32(size_t n, const uint32_t* __
 // only c_txn (what the wavefronts read) is written back.
 constexpr int CB_REG = 8;
 constexpr uint32_t PRED_TXN = 0x80000000u;   // pred mode: the run is one txn, stored in .x
+// pred mode feeds the one-pass pull levels, whose lanes wait for their predecessors' lanes: a predecessor more
+// than PULL_FAR rows AFTER its dependant (a slow-path bump moved its executeAt far back) may sit in a workgroup
+// not yet resident while the waiting ones occupy the chip, so such batches take the Kahn wavefronts instead
+constexpr uint32_t PULL_FAR = 1u << 16;
 __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                         const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
                                         uint32_t* __restrict__ c_txn, uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
-                                        uint8_t* __restrict__ c_meta, uint64_t* __restrict__ c_exec1, bool pred_mode) {
+                                        uint8_t* __restrict__ c_meta, uint64_t* __restrict__ c_exec1, bool pred_mode, bool& far) {
     uint64_t k[CB_REG];
     uint32_t t[CB_REG], pr[CB_REG], wr[CB_REG], ord[CB_REG];
 #pragma unroll
@@ -536,6 +540,13 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
                 else if (wr[q] && reads == 1) pe = make_uint2(t[q > 0 ? q - 1 : 0], 1u | PRED_TXN);
                 else if (seen_w) pe = make_uint2(lw_txn, 1u | PRED_TXN);
                 if (pe.y) succ[pr[q]] = pe;
+                // the latest predecessor row: a Write's Reads since the last Write, or that Write
+                uint32_t pmax = 0;
+#pragma unroll
+                for (int x = 0; x < CB_REG; ++x)
+                    if (wr[q] && reads > 1 && x < q && x >= q - (int)reads) pmax = t[x] > pmax ? t[x] : pmax;
+                if (pe.y & PRED_TXN) pmax = pe.x;
+                if (pmax > t[q] + PULL_FAR) far = true;
             } else {
                 const uint32_t pc = wr[q] ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
                 if (pc) atomicAdd(&indeg[t[q]], pc);
@@ -568,16 +579,17 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
 // have no edges and are skipped; a segment longer than SHORT_SEG raises *any_long and the caller falls
 // back to the fixpoint (whose chain preparation handles long chains).
 // One thread per non-head entry (ElideOp's dense list); the second entry of each segment builds it.
-__global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
+static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
                                                      const int32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                                      const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
                                                      uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
                                                      uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
                                                      uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
-                                                     uint32_t* __restrict__ any_long, int full, int pred_mode = 0) {
+                                                     uint32_t* __restrict__ any_long, int full, int pred_mode = 0,
+                                                     uint32_t* __restrict__ any_far = nullptr) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool lng = false;
+    bool lng = false, far = false;
     const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
     const size_t s = s2 - 1;
     if (s2 > 0 && seg_start[s2] == (int32_t)s) {
@@ -587,7 +599,7 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
             lng = true;
         } else if (end - s <= CB_REG) {
             chain_build_regs(s, (int)(end - s), e_txn, e_meta, e_exec1, sval, c_txn, indeg, succ, full ? c_meta : nullptr,
-                             full ? c_exec1 : nullptr, pred_mode != 0);
+                             full ? c_exec1 : nullptr, pred_mode != 0, far);
         } else {
             for (size_t x = s; x < end; ++x) {
                 const uint64_t kx = e_exec1[x];
@@ -613,6 +625,10 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
                     else if (wr && reads == 1) pe = make_uint2(c_txn[q - 1], 1u | PRED_TXN);
                     else if (seen_w) pe = make_uint2(c_txn[lw], 1u | PRED_TXN);
                     if (pe.y) succ[c_pair[q]] = pe;
+                    uint32_t pmax = (pe.y & PRED_TXN) ? pe.x : 0u;
+                    if (wr && reads > 1)
+                        for (size_t y = q - reads; y < q; ++y) pmax = c_txn[y] > pmax ? c_txn[y] : pmax;
+                    if (pmax > c_txn[q] + PULL_FAR) far = true;
                 } else {
                     const uint32_t pc = wr ? (reads > 0 ? reads : (seen_w ? 1u : 0u)) : (seen_w ? 1u : 0u);
                     if (pc) atomicAdd(&indeg[c_txn[q]], pc);
@@ -637,6 +653,7 @@ __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* _
         }
     }
     wave_set_flag(lng, any_long);
+    if (any_far) wave_set_flag(far, any_far);
 }
 
 // One wavefront: the txns released at level `lvl` (level 0: indeg == 0 in the snapshot; later levels:
@@ -682,7 +699,7 @@ __device__ inline void kahn_release_run(const uint32_t* __restrict__ ids, I b, I
 //   3. k_chain_links: the transitive reduction of the (a) rule from those two positions: in-degree per
 //      txn and the successor run per pair, the same edges k_chain_build derives serially.
 constexpr int CR_N = 1024, CR_D = 64, CR_T = 256;
-__global__ __launch_bounds__(CR_T) void k_chain_rank(size_t P, const int32_t* __restrict__ seg_start,
+static __global__ __launch_bounds__(CR_T) void k_chain_rank(size_t P, const int32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
                                                      const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
                                                      uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
@@ -716,7 +733,7 @@ __global__ __launch_bounds__(CR_T) void k_chain_rank(size_t P, const int32_t* __
         c_pair[q] = sval[i];
     }
 }
-__global__ __launch_bounds__(256) void k_chain_check(size_t P, const int32_t* __restrict__ seg_start,
+static __global__ __launch_bounds__(256) void k_chain_check(size_t P, const int32_t* __restrict__ seg_start,
                                                      const uint64_t* __restrict__ c_exec1, const uint32_t* __restrict__ c_pair,
                                                      uint32_t* __restrict__ bad) {
     bool b = false;
@@ -761,7 +778,7 @@ struct WriteLinkOp {
         out[q] = el.f ? (MIN ? (int32_t)(q + 1) : -1) : ex.v;
     }
 };
-__global__ __launch_bounds__(256) void k_chain_links(size_t P, const int32_t* __restrict__ seg_start,
+static __global__ __launch_bounds__(256) void k_chain_links(size_t P, const int32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
                                                      const uint32_t* __restrict__ c_pair, const int32_t* __restrict__ last_w,
                                                      const int32_t* __restrict__ next_w, uint32_t* __restrict__ indeg,
@@ -791,7 +808,7 @@ __global__ __launch_bounds__(256) void k_chain_links(size_t P, const int32_t* __
 // 64 lanes per edge run.
 constexpr uint64_t XLIGHT = 8;
 
-__global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
+static __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
                                                    uint32_t* __restrict__ rem, uint32_t* __restrict__ L,
                                                    const uint32_t* __restrict__ key_off, const uint2* __restrict__ succ,
                                                    const uint32_t* __restrict__ c_txn, const uint32_t* gate, int gate_is_abort,
@@ -803,7 +820,7 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
     for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
         const size_t t = base + threadIdx.x;
         const bool mine = t < n && (lvl == 0 ? indeg0[t] == 0u : L[t] == lvl);
-        if (mine) {
+        if (mine && key_off) {                 // key_off == nullptr: an explicit edge graph (xoff / xs) only
             const uint32_t b = key_off[t], e = key_off[t + 1];
             if (e - b <= 4) {
                 uint2 sc[4];
@@ -865,13 +882,20 @@ __global__ __launch_bounds__(256) void k_kahn_step(size_t n, uint32_t lvl, const
 // written with agent-scope atomics: the 8 XCDs' L2s are not coherent with each other.
 constexpr uint32_t LV_FINAL = 0x80000000u;
 constexpr uint64_t PULL_CAP_TICKS = 100000000ull;    // wall_clock64 at 100 MHz: a lane gives up after ~1 s
-__global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __restrict__ key_off, const uint2* __restrict__ pred,
+static __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __restrict__ key_off, const uint2* __restrict__ pred,
                                                     const uint32_t* __restrict__ c_txn, uint32_t* L, const uint32_t* gate,
-                                                    uint32_t* abort_flag, uint32_t* __restrict__ bmax) {
+                                                    const uint32_t* gate_far, uint32_t* abort_flag, uint32_t* __restrict__ bmax,
+                                                    int force_abort) {
     __shared__ uint32_t wm[256 / WAVE];
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool gated = *gate != 0u;                     // long chains: the caller takes another path
+    // long chains (block path) or far predecessors (Kahn): the caller takes another path
+    const bool gated = *gate != 0u || *gate_far != 0u;
     bool done = t >= n || gated;
+    if (!done && force_abort) {                         // tests: every lane takes the abort path at once
+        __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&L[t], LV_FINAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done = true;
+    }
     uint32_t b = 0, e = 0, m = 0, tries = 0;
     if (!done) { b = key_off[t]; e = key_off[t + 1]; }
     const uint64_t t0 = wall_clock64();
@@ -919,7 +943,7 @@ __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint32_t* __
     }
 }
 // max of the per-workgroup maxima (one workgroup); strips LV_FINAL from the levels afterwards
-__global__ __launch_bounds__(1024) void k_level_pull_max(uint32_t nb, const uint32_t* __restrict__ bmax, uint32_t* out) {
+static __global__ __launch_bounds__(1024) void k_level_pull_max(uint32_t nb, const uint32_t* __restrict__ bmax, uint32_t* out) {
     __shared__ uint32_t wm[1024 / WAVE];
     uint32_t m = 0;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) m = bmax[i] > m ? bmax[i] : m;
@@ -933,7 +957,7 @@ __global__ __launch_bounds__(1024) void k_level_pull_max(uint32_t nb, const uint
         *out = x;
     }
 }
-__global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L) {
+static __global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) L[t] &= ~LV_FINAL;
 }
@@ -946,7 +970,7 @@ __global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restr
 // k_frontier_collect builds the list of the txns at level lvl for the switch.
 constexpr int KS_T = 1024;
 constexpr uint32_t KS_MAX = 4096;
-__global__ __launch_bounds__(256) void k_frontier_collect(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
+static __global__ __launch_bounds__(256) void k_frontier_collect(size_t n, uint32_t lvl, const uint32_t* __restrict__ indeg0,
                                                           const uint32_t* __restrict__ L, uint32_t* __restrict__ F,
                                                           uint32_t* __restrict__ count) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -962,10 +986,12 @@ __global__ __launch_bounds__(256) void k_frontier_collect(size_t n, uint32_t lvl
 }
 // state[0] = frontier size in (level lvl0, list in F0); out: [0] = the size of the frontier left (0 = done,
 // all levels final), [1] = its level (the grid-wide steps resume there through L == lvl).
-__global__ __launch_bounds__(KS_T) void k_kahn_small(uint32_t lvl0, uint32_t* __restrict__ state, uint32_t* __restrict__ F0,
+static __global__ __launch_bounds__(KS_T) void k_kahn_small(uint32_t lvl0, uint32_t* __restrict__ state, uint32_t* __restrict__ F0,
                                                       uint32_t* __restrict__ F1, uint32_t* __restrict__ rem,
                                                       uint32_t* __restrict__ L, const uint32_t* __restrict__ key_off,
-                                                      const uint2* __restrict__ succ, const uint32_t* __restrict__ c_txn) {
+                                                      const uint2* __restrict__ succ, const uint32_t* __restrict__ c_txn,
+                                                      const uint64_t* __restrict__ xoff = nullptr,
+                                                      const uint32_t* __restrict__ xs = nullptr) {
     __shared__ uint32_t nf;
     __shared__ uint32_t fa[KS_MAX], fb[KS_MAX];      // frontier lists live in LDS
     uint32_t count = state[0], lvl = lvl0;
@@ -985,6 +1011,12 @@ __global__ __launch_bounds__(KS_T) void k_kahn_small(uint32_t lvl0, uint32_t* __
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < count; i += KS_T) {
             const uint32_t t = cur[i];
+            if (xoff)
+                for (uint64_t x = xoff[t]; x < xoff[t + 1]; ++x) {
+                    const uint32_t y = xs[x];
+                    release(y, atomicSub(&rem[y], 1u));
+                }
+            if (!key_off) continue;
             const uint32_t b = key_off[t], e = key_off[t + 1];
             if (e - b <= 4) {
                 // every key's first successor: loads and atomics issued together (one dependent chain)
@@ -1040,22 +1072,23 @@ struct XEdgeArgs {
     EdgeArgs e;
     const uint8_t* c_meta;
     int do_b, do_c;
+    int done_aware;                      // CFK history batches: no edge into or out of an APPLIED / INVALID txn
     uint32_t* indeg;
     unsigned long long* outcnt;          // count pass: [n] per-source out-degree
     unsigned long long* cur;             // fill pass: [n] per-source write cursor (starts at xoff)
     uint32_t* xs;
 };
-template <bool FILL>
-__global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.e.n) return;
+// The (b) / (c) sources of txn t, emit(src) each (an edge src -> t).  (c) walks the executeAt chain down from
+// the constraint position over the managed entries only (key-domain sync points / ephemeral reads sit in the
+// key segments but not in the execution chains).
+__device__ inline bool status_done(uint32_t m) {
+    const uint32_t s = meta_status(m);
+    return s == AD_ST_APPLIED || s == AD_ST_INVALID;
+}
+template <class Emit>
+__device__ inline void xedges_visit(const XEdgeArgs& a, size_t t, Emit&& emit) {
     const EdgeArgs& e = a.e;
-    uint32_t local = 0;
-    auto emit = [&](uint32_t src) {
-        if (FILL) a.xs[atomicAdd(&a.cur[src], 1ull)] = (uint32_t)t;
-        else atomicAdd(&a.outcnt[src], 1ull);
-        ++local;
-    };
+    if (a.done_aware && status_done(e.meta[t])) return;
     if (a.do_b) {
         const uint64_t my = e.ex1[t];
         const bool all = awaits_only_deps(e.meta[t]);
@@ -1065,7 +1098,7 @@ __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
             const uint32_t b = e.ent_off[c][t], end = b + e.tcnt[c][t];
             for (uint32_t x = b; x < end; ++x) {
                 const uint32_t d = e.txns[c][x];
-                if (all || e.ex1[d] < my) emit(d);
+                if ((all || e.ex1[d] < my) && !(a.done_aware && status_done(e.meta[d]))) emit(d);
             }
         }
     }
@@ -1075,17 +1108,32 @@ __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
             if (p < 0) continue;
             const int32_t s0 = e.seg_start[p];
             for (int32_t q = p;; --q) {
-                emit(e.c_txn[q]);
-                if (meta_kind(a.c_meta[q]) == AD_KIND_WRITE || q == s0) break;
+                const uint32_t mq = a.c_meta[q];
+                if (manages_execution(mq)) {
+                    if (!(a.done_aware && status_done(mq))) emit(e.c_txn[q]);
+                    if (meta_kind(mq) == AD_KIND_WRITE) break;
+                }
+                if (q == s0) break;
             }
         }
     }
+}
+template <bool FILL>
+static __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.e.n) return;
+    uint32_t local = 0;
+    xedges_visit(a, t, [&](uint32_t src) {
+        if (FILL) a.xs[atomicAdd(&a.cur[src], 1ull)] = (uint32_t)t;
+        else atomicAdd(&a.outcnt[src], 1ull);
+        ++local;
+    });
     if (!FILL && local) atomicAdd(&a.indeg[t], local);
 }
 
 // Small device results to the host without a stream sync (the engine's host-mapped coherent buffer, see
 // engine.hip read_totals_params): copy a[0..na) and b[0..nb) to pub[off..], fence, bump pub[0] = seq.
-__global__ __launch_bounds__(128) void k_publish2(const uint32_t* __restrict__ a, int na, const uint32_t* __restrict__ b, int nb,
+static __global__ __launch_bounds__(128) void k_publish2(const uint32_t* __restrict__ a, int na, const uint32_t* __restrict__ b, int nb,
                                                   uint32_t* pub, int off, uint32_t seq) {
     const int i = threadIdx.x;
     if (i < na) pub[off + i] = a[i];
@@ -1134,6 +1182,8 @@ struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
     Publisher pub;                      // set by the engine: flag read-backs without a stream sync
     bool pull_off = false;              // AD_LEVELS_KAHN: skip the one-pass pull levels
+    bool pull_force_abort = false;      // AD_LEVELS_PULL_ABORT (tests): every pull lane aborts, Kahn recomputes
+    int pull_path = 0;                  // last pull attempt: 0 none, 1 pulled, 2 far predecessors -> Kahn, 3 aborted -> Kahn
     int kb_hint = 0;                    // wavefronts in the first Kahn launch batch (previous depth + 1)
     uint32_t* c_txn = nullptr;
     uint8_t* c_meta = nullptr;
@@ -1165,6 +1215,30 @@ struct LevelState {
     uint32_t bl_rounds = 0;              // block scan rounds of the last block-path run
     bool bl_used = false;                // the last run_levels took the block path
 };
+
+// The buffers order_rows needs for m rows (run_levels sizes them too; callers ordering rows without a
+// run_levels pass on the handle reserve them here).
+inline bool ls_reserve_order(LevelState& ls, size_t m, hipStream_t st) {
+    auto grow = [&](void** p, size_t bytes) -> bool {
+        if (*p) { hipStreamSynchronize(st); hipFree(*p); *p = nullptr; }
+        return hipMalloc(p, bytes) == hipSuccess;
+    };
+    if (ls.capN < m || !ls.sk0) {
+        const size_t c = std::max<size_t>(m, 1);
+        if (!grow((void**)&ls.sk0, c * 4) || !grow((void**)&ls.sv0, c * 4) || !grow((void**)&ls.sk1, c * 4) ||
+            !grow((void**)&ls.sv1, c * 4) || !grow((void**)&ls.key64, c * 8) || !grow((void**)&ls.indeg, c * 4) ||
+            !grow((void**)&ls.rem, c * 4))
+            return false;
+        ls.capN = c;
+    }
+    if (!ls.flags && !grow((void**)&ls.flags, 256)) return false;
+    const size_t rneed = (3 * (radix_hist_len(std::max<size_t>(m, 1)) + 128) + 64 * 1024) * 4;
+    if (ls.rs_cap < rneed) {
+        if (!grow((void**)&ls.rs, rneed)) return false;
+        ls.rs_cap = rneed;
+    }
+    return true;
+}
 
 inline void free_level_state(LevelState& s) {
     void* ps[] = {s.c_txn, s.c_meta, s.c_pair, s.c_exec1, s.indeg, s.rem, s.succ, s.pm_all, s.pair_seg, s.seg_len, s.stamp, s.heads, s.long_pos, s.iflags, s.cons_pos, s.flags, s.agg, s.sk0, s.sv0, s.sk1, s.sv1, s.key64, s.rs, s.xcnt, s.xoff, s.xcur, s.xs, s.kfront};
@@ -1207,7 +1281,7 @@ struct LevelInputs {
 
 // Execution order over m txns (rows[k], or k when rows is null): LSD radix sort by executeAt (two 32-bit
 // halves) then stably by level; order_out[k'] = k of the k'-th txn.  ls.sk*/sv*/rs must hold m entries.
-__global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
+static __global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
                                                          const uint32_t* __restrict__ perm, uint32_t* __restrict__ key, int hi) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
@@ -1225,7 +1299,7 @@ __global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const uint64_
 // (no collision, via a sentinel) and that the keys ascend; otherwise the full LSD radix sort runs.
 constexpr int WR_N = 1024, WR_D = 64, WR_T = 256;
 constexpr uint32_t WR_EMPTY = 0xFFFFFFFFu;
-__global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
+static __global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
                                                       const uint32_t* __restrict__ lvl, uint64_t* __restrict__ okey,
                                                       uint32_t* __restrict__ oidx, uint32_t* __restrict__ olvl,
                                                       uint32_t* __restrict__ bad) {
@@ -1257,7 +1331,7 @@ __global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uint64_t* 
     wave_set_flag(oob, bad);
 }
 // flags[0] = max level, flags[1] |= 1 unless okey ascends and every slot is filled
-__global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ oidx,
+static __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ oidx,
                                                     const uint32_t* __restrict__ olvl, uint32_t* __restrict__ flags) {
     uint32_t v = 0;
     bool bad = false;
@@ -1282,7 +1356,7 @@ __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint64_t* __
 // level of each txn in `perm` order (dst) + max level (fallback path).  Grid-stride over a bounded grid:
 // one atomic per block.
 constexpr int ORDER_GRID = 1024;
-__global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint32_t* __restrict__ lvl, const uint32_t* __restrict__ rows,
+static __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, const uint32_t* __restrict__ lvl, const uint32_t* __restrict__ rows,
                                                            const uint32_t* __restrict__ perm, uint32_t* __restrict__ dst,
                                                            uint32_t* __restrict__ flags) {
     uint32_t v = 0;
@@ -1506,6 +1580,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         if (ls.rs_cap < rneed) { if (!grow((void**)&ls.rs, rneed)) goto oom; ls.rs_cap = rneed; }
     }
 
+    ls.pull_path = 0;
     hipMemsetAsync(ls.flags, 0, 64, st);
     if (n > 0) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
     if (!in.keep_levels) hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
@@ -1575,24 +1650,27 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // an abort (a lane waited ~1 s) to the Kahn wavefronts below
         if (in.kahn_ok && !in.keep_levels && P > 0 && pure && !ls.pull_off) {
             ls.chains_ready = false;
-            uint32_t lng = 0, res[2] = {0, 0};
+            uint32_t lng = 0, res[3] = {0, 0, 0};
             {
                 KScope ks(K_KAHN, P);
                 const int gn = ceil_div((long)n, 256);
                 hipMemsetAsync(ls.succ, 0, P * 8, st);                    // predecessor runs (zero: none)
-                hipMemsetAsync(ls.flags + 16, 0, 8, st);                  // [16] abort, [17] max level
+                hipMemsetAsync(ls.flags + 16, 0, 12, st);                 // [16] abort, [17] max level, [18] far pred
                 k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
-                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1);
-                k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 16, ls.sk1);
+                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1,
+                                                  ls.flags + 18);
+                k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
+                                                 ls.sk1, ls.pull_force_abort ? 1 : 0);
                 k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
                 k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
-                if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 2, res)) {
+                if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 3, res)) {
                     err = "exec levels: device error";
                     return AD_ERR_DEVICE;
                 }
             }
             if (lng) return block_path();                                  // deep key chains: executeAt blocks
-            if (!res[0]) {
+            ls.pull_path = res[2] ? 2 : (res[0] ? 3 : 1);                   // 1 pulled, 2 far predecessors, 3 aborted
+            if (!res[0] && !res[2]) {
                 const int lv = (int)res[1] + 1;
                 *iters = lv;
                 if (want_order && n > 0 && in.order_verify)
@@ -1601,7 +1679,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
                 return AD_OK;
             }
-            hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);     // aborted: the wavefronts below
+            hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);     // aborted / far: the wavefronts below
         }
         if (in.kahn_ok && !in.keep_levels && P > 0 && in.n_special == 0) {
             ls.chains_ready = false;

@@ -1,0 +1,131 @@
+// merge.hip — Deps.merge of the replica views (and of host / shard parts) on the device.
+#include "engine_internal.h"
+
+// ---------------------------------------------------------------------------------------------------
+// merge
+// ---------------------------------------------------------------------------------------------------
+template <int K>
+void launch_multi_offsets(ad_handle* h, size_t n, const uint32_t* mk, const uint32_t* me, const uint32_t* mu, Csr* const* out) {
+    MultiOffsetsOp<K> op{};
+    op.n = n; op.mk = mk; op.me = me; op.mu = mu;
+    for (int c = 0; c < K; ++c) { op.key_off[c] = out[c]->key_off; op.ent_off[c] = out[c]->ent_off; op.k2t_off[c] = out[c]->k2t_off; }
+    scan_any(h, op, n);
+}
+
+// K unions computed together (count, one fused offsets scan, ONE host sync, allocation, write):
+// out[k] = Deps.merge over in[k][0..np) per output txn; rows[k][v] (nullable) maps output txn -> input row.
+int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* out_block, const int* kw,
+                const Csr* const (*in)[MAXV], const int32_t* const (*rows)[MAXV], int np, uint64_t* entries) {
+    hipStream_t st = h->st;
+    uint32_t *mk, *me, *mu;
+    CK(dalloc(h, S_MSCR, &mk, 3 * (size_t)K * n + 3));
+    me = mk + (size_t)K * n;
+    mu = me + (size_t)K * n;
+    uint32_t* hl;                                   // heavy-txn lists [K * n] + counters [K]
+    CK(dalloc(h, S_MHL, &hl, (size_t)K * n + 64));
+    uint32_t* hc = hl + (size_t)K * n;
+    if (n > 0) HIPCHK(h, hipMemsetAsync(hc, 0, (size_t)K * 4, st));
+    std::vector<MergeArgs> ma(K);
+    for (int k = 0; k < K; ++k) {
+        CK(alloc_csr(h, out_block[k], *out[k], n));
+        dirty_csr(h, out_block[k]);
+        MergeArgs& a = ma[k];
+        a = MergeArgs{};
+        a.n = n; a.nv = np;
+        for (int v = 0; v < np; ++v) {
+            const Csr& c = *in[k][v];
+            a.key_off[v] = c.key_off; a.keys[v] = c.keys; a.k2t_off[v] = c.k2t_off; a.k2t[v] = c.k2t;
+            a.ent_off[v] = c.ent_off; a.txns[v] = c.txns; a.tcnt[v] = c.tcnt;
+            a.row[v] = rows ? rows[k][v] : nullptr;
+        }
+        a.mk = mk + (size_t)k * n; a.me = me + (size_t)k * n; a.mu = mu + (size_t)k * n;
+        if (h->merge_heavy) { a.hlist = hl + (size_t)k * n; a.hcount = hc + k; }
+        if (n > 0) merge_launch(a, np, false, kw[k], st);
+    }
+    if (n > 0) {
+        KScope ks(K_MERGE_OFFSETS, n * (size_t)K);
+        switch (K) {
+            case 1: launch_multi_offsets<1>(h, n, mk, me, mu, out); break;
+            case 2: launch_multi_offsets<2>(h, n, mk, me, mu, out); break;
+            case 3: launch_multi_offsets<3>(h, n, mk, me, mu, out); break;
+            case 4: launch_multi_offsets<4>(h, n, mk, me, mu, out); break;
+            case 5: launch_multi_offsets<5>(h, n, mk, me, mu, out); break;
+            case 6: launch_multi_offsets<6>(h, n, mk, me, mu, out); break;
+            case 7: launch_multi_offsets<7>(h, n, mk, me, mu, out); break;
+            case 8: launch_multi_offsets<8>(h, n, mk, me, mu, out); break;
+            case 10: launch_multi_offsets<10>(h, n, mk, me, mu, out); break;
+            case 12: launch_multi_offsets<12>(h, n, mk, me, mu, out); break;
+            case 14: launch_multi_offsets<14>(h, n, mk, me, mu, out); break;
+            case 16: launch_multi_offsets<16>(h, n, mk, me, mu, out); break;
+            default: return set_err(h, AD_ERR_UNSUPPORTED, "merge_multi: unsupported output count");
+        }
+    } else {
+        for (int k = 0; k < K; ++k) {
+            HIPCHK(h, hipMemsetAsync(out[k]->key_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(out[k]->ent_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(out[k]->k2t_off, 0, 4, st));
+        }
+    }
+    std::vector<uint32_t> tot(3 * K, 0);
+    TotTable tt{};
+    for (int k = 0; k < K; ++k) {
+        tt.src[3 * k + 0] = out[k]->key_off + n; tt.src[3 * k + 1] = out[k]->k2t_off + n; tt.src[3 * k + 2] = out[k]->ent_off + n;
+    }
+    tt.count = 3 * K;
+    CK(read_totals_params(h, tt, tot.data()));
+    CK(check_params(h));
+    for (int k = 0; k < K; ++k) {
+        Csr& m = *out[k];
+        m.nkeys = tot[3 * k]; m.nk2t = tot[3 * k + 1]; m.ncap = tot[3 * k + 2];
+        if (entries) *entries += m.nk2t - m.nkeys;
+        CK(alloc_csr_data(h, out_block[k], m, kw[k]));
+        MergeArgs& a = ma[k];
+        a.o_key_off = m.key_off; a.o_keys = m.keys; a.o_k2t_off = m.k2t_off; a.o_k2t = m.k2t;
+        a.o_ent_off = m.ent_off; a.o_txns = m.txns; a.o_tcnt = m.tcnt;
+        if (n > 0) merge_launch(a, np, true, kw[k], st);
+    }
+    return AD_OK;
+}
+
+// Deps.merge of `np` parts per class into h->merged.  parts[cls][v] are batched per-txn CSRs over the loaded batch;
+// view_rows[v] (nullable) maps txn -> row of part v, -1 = leave that reply out for the txn.
+int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_range, const int32_t* const* view_rows,
+                bool has_direct) {
+    const size_t n = h->n;
+    h->merged_entries = 0;
+    Csr* out[3];
+    size_t blocks[3];
+    int kw[3];
+    const Csr* in[3][MAXV] = {};
+    const int32_t* rows[3][MAXV] = {};
+    int K = 0;
+    for (int cls = 0; cls < 3; ++cls) {
+        if ((cls == AD_CLASS_RANGE && !has_range) || (cls == AD_CLASS_DIRECT_KEY && !has_direct)) {
+            // an empty class in every part: an empty merged class (zero offsets, kept from the previous batch
+            // when still valid)
+            CK(zero_csr(h, CSR_MERGED0 + cls, h->merged[cls], n));
+            continue;
+        }
+        out[K] = &h->merged[cls];
+        blocks[K] = CSR_MERGED0 + cls;
+        kw[K] = cls == AD_CLASS_RANGE ? 2 : 1;
+        for (int v = 0; v < np; ++v) { in[K][v] = parts[cls][v]; rows[K][v] = view_rows ? view_rows[v] : nullptr; }
+        ++K;
+    }
+    CK(merge_multi(h, n, K, out, blocks, kw, in, view_rows ? rows : nullptr, np, &h->merged_entries));
+    h->have_merged = true;
+    return AD_OK;
+}
+
+int stage_merge(ad_handle* h) {
+    StageScope sc(h, STAGE_MERGE);
+    if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps before ad_preaccept_deps");
+    const int nv = (int)h->cfg.replicas;
+    const Csr* parts[3][MAXV] = {};
+    for (int v = 0; v < nv; ++v) {
+        parts[0][v] = &h->deps[2 * v];
+        parts[1][v] = &h->deps[2 * v + 1];
+        parts[2][v] = &h->rdeps[v];
+    }
+    return merge_parts(h, parts, nv, h->Q > 0, nullptr, h->deps_direct);
+}

@@ -57,7 +57,7 @@ struct MKey {
 };
 
 template <int NV, bool WRITE, int KW>
-__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+static __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     constexpr uint32_t INF = 0xFFFFFFFFu;
@@ -225,7 +225,7 @@ __device__ inline void block_scan3(uint32_t x[3], uint32_t tot[3]) {
 }
 
 template <int NV, bool WRITE, int KW>
-__global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
+static __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
     constexpr uint32_t INF = 0xFFFFFFFFu;
     __shared__ uint32_t sU[WRITE ? MH_LDS : 1];
     const uint32_t H = *a.hcount;
@@ -443,7 +443,7 @@ struct MultiOffsetsOp {
 };
 
 // Uploaded replies (ad_merge_host): per-txn unique-TxnId counts from the compacted txn_off.
-__global__ __launch_bounds__(256) void k_tcnt_from_off(size_t n, const uint32_t* __restrict__ off, uint32_t* __restrict__ tcnt) {
+static __global__ __launch_bounds__(256) void k_tcnt_from_off(size_t n, const uint32_t* __restrict__ off, uint32_t* __restrict__ tcnt) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) tcnt[t] = off[t + 1] - off[t];
 }

@@ -21,7 +21,7 @@ constexpr int RS_TILE = RS_BLOCK * RS_ITEMS;
 constexpr int RS_WAVES = RS_BLOCK / WAVE;
 constexpr int RS_ROUNDS = RS_TILE / RS_WAVES / WAVE;   // 16
 
-__global__ __launch_bounds__(RS_BLOCK) void k_radix_hist(const uint32_t* __restrict__ keys, size_t n, int shift,
+static __global__ __launch_bounds__(RS_BLOCK) void k_radix_hist(const uint32_t* __restrict__ keys, size_t n, int shift,
                                                          int ntiles, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[RS_WAVES][256];
     const int w = threadIdx.x / WAVE;
@@ -57,7 +57,7 @@ __device__ inline uint64_t match_digit(uint32_t d, bool valid) {
 // per-wave ballot ranks, the tile's (key, value) pairs are written to LDS in that order, and then read
 // back sequentially: consecutive threads write consecutive global slots of one digit's run, so the global
 // stores are coalesced bursts instead of 4-byte scatters (measured: 3.6x write amplification before).
-__global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+static __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             size_t n, int shift, int ntiles,
                                                             const uint32_t* __restrict__ offs) {

@@ -45,7 +45,7 @@ inline int ri_levels(size_t Q, uint32_t* cnt, size_t* total) {
 }
 
 // one wave per output node: max of its 64 children
-__global__ __launch_bounds__(256) void k_ri_level(size_t nout, uint32_t nin, const uint64_t* __restrict__ in, uint64_t* __restrict__ out) {
+static __global__ __launch_bounds__(256) void k_ri_level(size_t nout, uint32_t nin, const uint64_t* __restrict__ in, uint64_t* __restrict__ out) {
     const size_t x = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (x >= nout) return;
     const size_t c = x * WAVE + __lane_id();

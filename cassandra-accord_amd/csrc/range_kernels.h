@@ -30,7 +30,7 @@
 namespace ad {
 
 // per range entry: owner txn + sort keys (end, start relative to rbase)
-__global__ __launch_bounds__(256) void k_range_prep(size_t n, const uint8_t* __restrict__ meta, const uint32_t* __restrict__ range_off,
+static __global__ __launch_bounds__(256) void k_range_prep(size_t n, const uint8_t* __restrict__ meta, const uint32_t* __restrict__ range_off,
                                                     const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
                                                     uint64_t rbase, uint32_t* __restrict__ rowner,
                                                     uint32_t* __restrict__ k_end, uint32_t* __restrict__ v_idx) {
@@ -43,20 +43,20 @@ __global__ __launch_bounds__(256) void k_range_prep(size_t n, const uint8_t* __r
     }
 }
 
-__global__ __launch_bounds__(256) void k_range_startkey(size_t Q, const uint64_t* __restrict__ rs, const uint32_t* __restrict__ idx,
+static __global__ __launch_bounds__(256) void k_range_startkey(size_t Q, const uint64_t* __restrict__ rs, const uint32_t* __restrict__ idx,
                                                         uint64_t rbase, uint32_t* __restrict__ k_start) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x < Q) k_start[x] = (uint32_t)(rs[idx[x]] - rbase);
 }
 
 // 64-bit range spreads: sort key = (src[idx[x]] - rbase) >> shift, truncated to 32 bits (one LSD half)
-__global__ __launch_bounds__(256) void k_range_key_half(size_t Q, const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx,
+static __global__ __launch_bounds__(256) void k_range_key_half(size_t Q, const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx,
                                                         uint64_t rbase, int shift, uint32_t* __restrict__ k_out) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x < Q) k_out[x] = (uint32_t)((src[idx[x]] - rbase) >> shift);
 }
 
-__global__ __launch_bounds__(256) void k_range_gather(size_t Q, const uint32_t* __restrict__ idx, const uint64_t* __restrict__ rs,
+static __global__ __launch_bounds__(256) void k_range_gather(size_t Q, const uint32_t* __restrict__ idx, const uint64_t* __restrict__ rs,
                                                       const uint64_t* __restrict__ re, const uint32_t* __restrict__ rowner,
                                                       uint64_t* __restrict__ es, uint64_t* __restrict__ ee,
                                                       uint32_t* __restrict__ eown) {
@@ -109,7 +109,7 @@ __device__ inline bool range_hits(const RangeArgs& a, bool key_dom, uint32_t fb,
 }
 
 template <int NV, bool FILL>
-__global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
+static __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
     const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (t >= a.n) return;
     const int lane = __lane_id();

@@ -160,7 +160,7 @@ struct RcEmit {
 };
 
 template <bool FILL>
-__global__ __launch_bounds__(256) void k_recover(RecoverArgs a) {
+static __global__ __launch_bounds__(256) void k_recover(RecoverArgs a) {
     const size_t q = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (q >= a.nq) return;
     const int lane = __lane_id();

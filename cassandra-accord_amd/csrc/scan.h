@@ -92,7 +92,7 @@ __device__ inline typename Op::S block_exclusive_scan(const Op& op, typename Op:
 // (coalesced).  Order is preserved: each round is an ordered 64-lane scan, rounds are folded in order,
 // waves in wave order (the ops are associative, not commutative).
 template <class Op, int BLOCK, int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename Op::S* agg) {
+static __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename Op::S* agg) {
     using S = typename Op::S;
     constexpr int NW = BLOCK / WAVE;
     __shared__ S lds[NW];
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_reduce(Op op, size_t n, typename
 // AI consecutive aggregates serially before one block scan (4096 aggregates = one chunk: the 4M-entry
 // elision scan spent 19 us here with one aggregate per thread and four chunk rounds).
 template <class Op, int BLOCK, int AI = 4>
-__global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, typename Op::S* agg) {
+static __global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, typename Op::S* agg) {
     using S = typename Op::S;
     __shared__ S lds[BLOCK / WAVE];
     S carry = op.identity();
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_aggregates(Op op, int nblk, type
 }
 
 template <class Op, int BLOCK, int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_scan_apply(Op op, size_t n, const typename Op::S* agg) {
+static __global__ __launch_bounds__(BLOCK) void k_scan_apply(Op op, size_t n, const typename Op::S* agg) {
     using S = typename Op::S;
     constexpr int NW = BLOCK / WAVE;
     __shared__ S lds[NW];

@@ -65,7 +65,7 @@ struct DestOp {                       // per row: rank among the kept rows of it
     }
 };
 // list[base[d] + rank] = r  (base = exclusive prefix of the destination totals, computed in-kernel)
-__global__ __launch_bounds__(256) void k_export_list(size_t n, const uint8_t* __restrict__ dest, const uint32_t* __restrict__ rank,
+static __global__ __launch_bounds__(256) void k_export_list(size_t n, const uint8_t* __restrict__ dest, const uint32_t* __restrict__ rank,
                                                      const uint32_t* __restrict__ totals, uint32_t* __restrict__ list) {
     const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n || rank[r] == ~0u) return;
@@ -114,7 +114,7 @@ struct ExportOffsetsOp {
 };
 // the global offsets at every destination boundary: out[(d * nvc + c) * 3 + {0,1,2}], d = 0..world
 struct ExportOffs { uint32_t* ok[NVX_MAX]; uint32_t* om[NVX_MAX]; uint32_t* ot[NVX_MAX]; };
-__global__ void k_export_bounds(int world, int nvc, const uint32_t* __restrict__ totals, ExportOffs o, uint32_t* __restrict__ out) {
+static __global__ void k_export_bounds(int world, int nvc, const uint32_t* __restrict__ totals, ExportOffs o, uint32_t* __restrict__ out) {
     const int i = threadIdx.x;
     if (i >= (world + 1) * nvc) return;
     const int d = i / nvc, c = i % nvc;
@@ -150,7 +150,7 @@ struct ExportFillArgs {
 };
 // one thread per exported row: its gid, rebased offsets, and its keys / keysToTxnIds / TxnIds (as global
 // ranks) copied into its destination's blob; the destination's last row writes the closing offsets
-__global__ __launch_bounds__(256) void k_export_fill(ExportFillArgs a) {
+static __global__ __launch_bounds__(256) void k_export_fill(ExportFillArgs a) {
     const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.K) return;
     const uint32_t r = a.list[j];
@@ -184,14 +184,14 @@ __global__ __launch_bounds__(256) void k_export_fill(ExportFillArgs a) {
 }
 
 // home txns: global ids
-__global__ __launch_bounds__(256) void k_home_gid(size_t H, const uint32_t* __restrict__ rows, const uint32_t* __restrict__ gid,
+static __global__ __launch_bounds__(256) void k_home_gid(size_t H, const uint32_t* __restrict__ rows, const uint32_t* __restrict__ gid,
                                                   uint32_t* __restrict__ hg) {
     const size_t h = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h < H) hg[h] = gid[rows[h]];
 }
 
 // row of each home txn in source s (binary search over the source's ascending global ids; -1 = absent)
-__global__ __launch_bounds__(256) void k_source_rows(size_t H, const uint32_t* __restrict__ hg, const uint32_t* __restrict__ sgid,
+static __global__ __launch_bounds__(256) void k_source_rows(size_t H, const uint32_t* __restrict__ hg, const uint32_t* __restrict__ sgid,
                                                      uint32_t ns, int32_t* __restrict__ row) {
     const size_t h = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= H) return;
@@ -205,12 +205,12 @@ __global__ __launch_bounds__(256) void k_source_rows(size_t H, const uint32_t* _
 }
 
 // levels: local rows <- replicated global array; and back (max), flagging any raise
-__global__ __launch_bounds__(256) void k_levels_gather(size_t n, const uint32_t* __restrict__ gid, const uint32_t* __restrict__ G,
+static __global__ __launch_bounds__(256) void k_levels_gather(size_t n, const uint32_t* __restrict__ gid, const uint32_t* __restrict__ G,
                                                        uint32_t* __restrict__ L) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) L[i] = G[gid[i]];
 }
-__global__ __launch_bounds__(256) void k_levels_scatter(size_t n, const uint32_t* __restrict__ gid, uint32_t* __restrict__ G,
+static __global__ __launch_bounds__(256) void k_levels_scatter(size_t n, const uint32_t* __restrict__ gid, uint32_t* __restrict__ G,
                                                         const uint32_t* __restrict__ L, uint32_t* __restrict__ changed) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool up = false;
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void k_levels_scatter(size_t n, const uint32_t
 // r), appended as (gid << 32 | level) to each of those stores' regions of `out` (region d starts at base[d]
 // and holds at most the rows shared with d: no overflow).  Order inside a region is free: the receiver folds
 // with max.  *sent: some pair was appended.
-__global__ __launch_bounds__(256) void k_level_deltas(size_t n, const uint32_t* __restrict__ gid, const uint8_t* __restrict__ holders,
+static __global__ __launch_bounds__(256) void k_level_deltas(size_t n, const uint32_t* __restrict__ gid, const uint8_t* __restrict__ holders,
                                                       uint32_t others, uint32_t* __restrict__ G, const uint32_t* __restrict__ L,
                                                       const uint32_t* __restrict__ base, uint32_t* __restrict__ cnt,
                                                       uint64_t* __restrict__ out, uint32_t* __restrict__ sent) {
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void k_level_deltas(size_t n, const uint32_t* 
 }
 
 // Received (gid << 32 | level) pairs folded into G (several stores may raise one txn: max).
-__global__ __launch_bounds__(256) void k_level_apply(size_t m, const uint64_t* __restrict__ pairs, uint32_t* __restrict__ G) {
+static __global__ __launch_bounds__(256) void k_level_apply(size_t m, const uint64_t* __restrict__ pairs, uint32_t* __restrict__ G) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) {
         const uint64_t p = pairs[i];

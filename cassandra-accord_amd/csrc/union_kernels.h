@@ -68,7 +68,7 @@ __device__ inline void keys_in_range(const VItemArgs& a, uint32_t U, uint64_t s,
 }
 
 template <bool FILL>
-__global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
+static __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     const uint32_t m = a.meta[t];
@@ -169,7 +169,8 @@ constexpr int UNION_CSRS = NVC_MAX + MAXV;   // key classes of every view, then 
 struct LdsUnionArgs {
     size_t n;
     int ncsr;
-    int csr_base;                      // this launch's CSRs are [csr_base, csr_base + ncsr) of the tables
+    int csr_base;                      // this launch's CSRs are csr_base + k * csr_step, k < ncsr, of the tables
+    int csr_step;                      //   (2: keyDeps classes only, the batch has no directKeyDeps)
     int only_large;
     const uint32_t* rows;              // only_large: the large txns' rows (grid x = their count), or null
     const uint32_t* rows_total;        //   their device-side count (guard)
@@ -246,10 +247,10 @@ struct LargeRowsOp {
 };
 
 // grid (n or #large rows, ncsr): one workgroup per (txn, CSR); CSRs above UNION_CAP entries are queued for k_union_big
-__global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
+static __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
     if (a.rows && blockIdx.x >= *a.rows_total) return;
     const size_t t = a.rows ? (size_t)a.rows[blockIdx.x] : (size_t)blockIdx.x;
-    const int c = a.csr_base + (int)blockIdx.y;
+    const int c = a.csr_base + (int)blockIdx.y * a.csr_step;
     if (t >= a.n) return;
     if (a.only_large && !(a.meta[t] & META_LARGE)) return;
     __shared__ uint32_t buf[UNION_CAP];
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
 // unions in flight per CU, each a chain of ~40 barrier-separated bitonic stages; single-wave workgroups fit 32
 // per CU and their barriers are cheap.  Lists above UNION_SMALL go to the medium queue (k_union_lds_list).
 constexpr int UNION_SMALL = 512, US_T = 64;
-__global__ __launch_bounds__(US_T) void k_union_lds_small(LdsUnionArgs a) {
+static __global__ __launch_bounds__(US_T) void k_union_lds_small(LdsUnionArgs a) {
     const size_t t = blockIdx.x;
     const int c = a.csr_base + (int)blockIdx.y;
     if (t >= a.n) return;
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(US_T) void k_union_lds_small(LdsUnionArgs a) {
 }
 // the medium queue: grid-stride over the device-side count, one 256-thread workgroup per item (LDS up to
 // UNION_CAP; above it the overflow queue as in k_union_lds)
-__global__ __launch_bounds__(UB) void k_union_lds_list(LdsUnionArgs a) {
+static __global__ __launch_bounds__(UB) void k_union_lds_list(LdsUnionArgs a) {
     __shared__ uint32_t buf[UNION_CAP];
     __shared__ uint32_t wsum[UB / WAVE];
     const uint32_t count = *a.med_count;
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(UB) void k_union_lds_list(LdsUnionArgs a) {
 
 // overflow pass, one 1024-thread workgroup per queued (txn, CSR): LDS up to UNION_CAP_BIG entries, beyond
 // that a bitonic sort in this item's slice of global memory
-__global__ __launch_bounds__(UB_BIG) void k_union_big(LdsUnionArgs a, uint32_t count) {
+static __global__ __launch_bounds__(UB_BIG) void k_union_big(LdsUnionArgs a, uint32_t count) {
     const uint32_t it = blockIdx.x;
     if (it >= count) return;
     __shared__ uint32_t buf[UNION_CAP_BIG];

@@ -177,6 +177,11 @@ int  ad_preaccept_deps(ad_handle* h, ad_csr_sizes* sizes /* [replicas*AD_NUM_CLA
  * executeAt (the window / status model applies from there).  Fetch with ad_fetch_deps; ad_merge_deps and the
  * later stages use the last deps computed.  Not in sharded mode (AD_ERR_UNSUPPORTED). */
 int  ad_accept_deps(ad_handle* h, ad_csr_sizes* sizes /* [replicas*AD_NUM_CLASSES] */);
+/* GetEphemeralReadDeps (messages/GetEphemeralReadDeps.java:76): PreAccept.calculatePartialDeps with bound
+ * Timestamp.MAX — every txn of the batch's CFKs and range commands the query kind witnesses (the txn itself
+ * left out), answered after every arrival (the in-flight window is the batch's last W txns).  Same outputs as
+ * ad_preaccept_deps; not over CFK history batches or sharded stores. */
+int  ad_ephemeral_read_deps(ad_handle* h, ad_csr_sizes* sizes /* [replicas*3] */);
 int  ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out);
 
 /* Stage 2 — Deps.merge of the R replica replies produced by stage 1 (device-resident). */
@@ -226,6 +231,8 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
  * Either pointer may be NULL.  Sharded stores (ad_shard_setup): rows are local, max_rank holds global arrival ranks; PreAccept.reduce's
  * mergeMax across stores (messages/PreAccept.java:141-156) is then a per-txn max over the stores' answers. */
 #define AD_RANK_NONE 0xFFFFFFFFu
+/* ad_exec_levels over a batch carrying CFK history: the level of a row already APPLIED or INVALID (done) */
+#define AD_LEVEL_DONE 0xFFFFFFFFu
 int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8_t* fast /* [replicas*n] */);
 
 /* Stage 1b across batches — the store's MaxConflicts map outlives a batch (local/MaxConflicts.java:32-96,
@@ -264,6 +271,10 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
                                     /* ones the deps walks visit (P - distinct keys)             */
     uint32_t level_blocks;          /* executeAt blocks walked by the block level path (0: Kahn)  */
     uint32_t level_rounds;          /* block-scan rounds over those blocks                        */
+    uint32_t key_classes;           /* key-footprint CSRs the deps stage computed per batch: 2R, or */
+                                    /* R when the batch has no directKeyDeps (no key sync points)   */
+    uint32_t level_path;            /* the pull levels' outcome: 0 not tried, 1 pulled, 2 a far    */
+                                    /* predecessor (> 65536 rows ahead) -> Kahn, 3 aborted -> Kahn   */
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
@@ -280,6 +291,7 @@ int  ad_last_times(ad_handle* h, ad_stage_times* out);
 #define AD_LEVELS_FIXPOINT 1
 #define AD_LEVELS_BLOCKS 2
 #define AD_LEVELS_KAHN 3
+#define AD_LEVELS_PULL_ABORT 4      /* tests: the pull levels abort at once, the Kahn wavefronts recompute the batch */
 int  ad_set_level_mode(ad_handle* h, int mode);
 
 /* Per-kernel HIP-event timing (trace mode).  mask bit k enables kernel id k (0 <= k < ad_kernel_count()); the
@@ -325,11 +337,24 @@ int  ad_fetch_recovery_flags(ad_handle* h, uint8_t* reject_fast_path /* [nq] */)
 /* again by mapReduceActive, CommandsForKey.java:925-983).  The next ad_load_batch puts those rows first: the    */
 /* loaded batch is [kept rows | new txns], window / drop decisions and MaxConflicts use global arrival ranks,    */
 /* and every output row / TxnId is a combined row (ad_cfk_rows maps rows to global ranks).  The new txns'      */
-/* deps equal those of the whole stream resolved at once.  Key batches only; ad_exec_levels, ad_accept_deps and  */
-/* sharded mode are refused over a batch with history rows (AD_ERR_UNSUPPORTED).                               */
+/* deps equal those of the whole stream resolved at once.  Statuses of kept rows are current (ad_cfk_update);  */
+/* ad_exec_levels orders the combined rows with APPLIED / INVALID rows done.  Key batches only; ad_accept_deps   */
+/* and sharded mode are refused over a batch with history rows (AD_ERR_UNSUPPORTED).                            */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_cfk_retain(ad_handle* h, size_t* retained /* out: kept rows, or NULL */);
 int  ad_cfk_reset(ad_handle* h);                        /* forget the kept rows: the next batch starts afresh */
+/* State transitions between batches (after ad_cfk_retain, before the next ad_load_batch): the kept rows with
+ * global ranks gid[m] (strictly ascending) move to status[m] (InternalStatus), with executeAt (three arrays, or
+ * all NULL to keep it).  Replaces CommandsForKey.update on Commit / Stable / Apply / Invalidate
+ * (CommandsForKey.java:987-1057, Updating.java:99-358).  Legal moves are CommandsForKeyTest's TRANSITIONS
+ * (CommandsForKeyTest.java:235-246): TRANSITIVELY_KNOWN / PREACCEPTED -> PREACCEPTED, ACCEPTED, COMMITTED,
+ * STABLE, INVALID; ACCEPTED -> COMMITTED, STABLE, INVALID; COMMITTED -> STABLE; STABLE -> APPLIED.  executeAt
+ * >= TxnId once decided and fixed from COMMITTED on.  Every update is checked first; AD_ERR_ARGUMENT (none
+ * applied) names the first refused one (not a kept row, illegal move, executeAt rule).  The next ad_cfk_retain
+ * prunes rows that became APPLIED below an applied Write's executeAt (Pruning.java:164-233) or INVALID, and
+ * ad_exec_levels over the next batch treats APPLIED / INVALID rows as done (AD_LEVEL_DONE). */
+int  ad_cfk_update(ad_handle* h, size_t m, const uint32_t* gid, const uint8_t* status, const uint64_t* exec_msb,
+                   const uint64_t* exec_lsb, const int32_t* exec_node);
 int  ad_cfk_rows(ad_handle* h, size_t* hist_rows /* out */, uint32_t* gid /* [n] global rank per row, or NULL */);
 
 /* ------------------------------------------------------------------------------------------ */
@@ -388,6 +413,19 @@ int  ad_shard_levels_get(ad_handle* h, uint32_t* G /* [n_global] */);
 int  ad_shard_levels_set(ad_handle* h, const uint32_t* G);
 int  ad_shard_levels_allreduce(ad_handle* h, uint32_t* any_changed /* out: max of the stores' round flags, or NULL */);
 int  ad_shard_order(ad_handle* h, uint32_t* level_out /* [n_home] */, uint32_t* order_out /* [n_home] global ranks */);
+/* One-exchange levels (the default protocol): every execution constraint is local to one store, so the
+ * batch's level DAG is the union of the stores' constraint graphs.  ad_shard_level_edges gives this store's
+ * constraints as explicit edges over global ranks, (src << 32 | dst): the transitive reduction of its key
+ * chains (CommandsForKey.notifyManaged's Read/Write rule, CommandsForKey.java:1208-1289) plus its direct /
+ * range dependency edges and unmanaged chain bounds (Commands.updateWaitingOn, Commands.java:700-775;
+ * Updating.updateUnmanaged, Updating.java:715-800) from the Deps.merge of its own views.  out == NULL: compute
+ * and return the count; then again with out[m] to copy them.  Every store gathers every store's edges and
+ * solves the union (Kahn wavefronts; deep graphs inside one workgroup): ad_shard_levels_solve from host
+ * edges, or ad_shard_levels_gather over RCCL (counts all-gather + grouped send/recv of the edges).  *depth =
+ * number of levels.  Then ad_shard_order.  No round count depends on the depth of the graph. */
+int  ad_shard_level_edges(ad_handle* h, size_t* m, uint64_t* out);
+int  ad_shard_levels_solve(ad_handle* h, const uint64_t* edges, size_t m, uint32_t* depth);
+int  ad_shard_levels_gather(ad_handle* h, uint32_t* depth);
 
 #ifdef __cplusplus
 }

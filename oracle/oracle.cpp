@@ -310,6 +310,7 @@ struct Oracle {
     Config cfg;
     bool prune;
     bool accept;                        // bound = executeAt (Accept / GetDeps) instead of TxnId (PreAccept)
+    bool bound_max = false;             // bound = Timestamp.MAX (GetEphemeralReadDeps.java:76)
     std::vector<Cfk> cfks;              // sorted by key
     std::vector<uint32_t> rangeTxns;    // ranks of range-domain txns (rangeCommands registry)
 
@@ -337,8 +338,10 @@ struct Oracle {
     // TxnId_i at position i.  Accept / GetDeps (Accept.calculatePartialDeps :113-116, GetDeps.apply :76 ->
     // PreAccept.calculatePartialDeps with executeAt): executeAt_i, answered once every txn with a smaller
     // TxnId has arrived — position q = #{j : TxnId_j < executeAt_i}; the status model and window apply from q.
-    const Ts& bound_of(uint32_t i) const { return accept ? B.ex[i] : B.tx[i]; }
+    Ts ts_max{~0ull, ~0ull, INT32_MAX};  // Timestamp.MAX
+    const Ts& bound_of(uint32_t i) const { return bound_max ? ts_max : (accept ? B.ex[i] : B.tx[i]); }
     uint32_t query_pos(uint32_t i) const {
+        if (bound_max) return (uint32_t)B.n;     // answered after every arrival
         if (!accept) return i;
         const Ts& b = B.ex[i];
         return (uint32_t)(std::lower_bound(B.tx.begin(), B.tx.end(), b, [](const Ts& x, const Ts& y) { return ts_cmp(x, y) < 0; }) - B.tx.begin());
@@ -566,8 +569,15 @@ namespace {
 // Every edge into a txn that does not await only its deps increases executeAt, so those are resolved in
 // executeAt order (phase 1).  Only ExclusiveSyncPoints witness ExclusiveSyncPoints and nothing witnesses an
 // EphemeralRead, and their deps precede them in TxnId order: phase 2 resolves them in TxnId order.
-static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDeps>& merged, std::vector<uint32_t>& order) {
+// done_aware (a batch carrying CFK history, statuses current): an APPLIED or INVALID txn is done — it waits for
+// nothing and nothing waits for it (Commands.updateWaitingOn drops applied / invalidated deps, Commands.java:
+// 700-775; CommandsForKey's unapplied counters skip them, :1291-1330): its level is -1 inside the recurrence,
+// AD_LEVEL_DONE outside, and the order lists the done txns first (executeAt order), then the rest by (level,
+// executeAt).
+static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDeps>& merged, std::vector<uint32_t>& order,
+                                         bool done_aware = false) {
     const uint32_t n = (uint32_t)B.n;
+    auto done = [&](uint32_t t) { return done_aware && (B.st[t] == AD_ST_APPLIED || B.st[t] == AD_ST_INVALID); };
     for (uint32_t i = 0; i < n; ++i)
         if (kind_of(B.tx[i]) == AD_KIND_LOCAL_ONLY)
             throw std::invalid_argument("exec levels: local-only txns are not part of the batch execution order");
@@ -635,7 +645,7 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
                 if (pos > 0) lv = std::max(lv, c.pmAll[pos - 1]);
             }
         }
-        level[t] = lv + 1;
+        level[t] = done(t) ? -1 : lv + 1;
         if (manages_execution(me)) {
             bool w = kind == AD_KIND_WRITE;
             for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
@@ -652,9 +662,9 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
     for (uint32_t t = 0; t < n; ++t)                // phase 2
         if (awaits_only_deps(kind_of(B.tx[t]))) resolve(t);
     std::vector<uint32_t> out(n);
-    for (uint32_t i = 0; i < n; ++i) out[i] = (uint32_t)level[i];
+    for (uint32_t i = 0; i < n; ++i) out[i] = done(i) ? AD_LEVEL_DONE : (uint32_t)level[i];
     order = byExec;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return out[a] < out[b]; });
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return out[a] + 1u < out[b] + 1u; });
     return out;
 }
 
@@ -676,7 +686,8 @@ struct oracle_result {
 extern "C" {
 
 /* flags: bit0 = pruning (baseline mode), bit1 = merge, bit2 = levels, bit3 = executeAt-bound deps (Accept /
- * GetDeps; no pruning); threads: key-range shards
+ * GetDeps; no pruning), bit4 = levels with APPLIED / INVALID txns done (CFK history batches), bit5 = bound
+ * Timestamp.MAX (GetEphemeralReadDeps); threads: key-range shards
  * for the deps stage (InMemoryCommandStore.SingleThread per shard + PreAccept.reduce). */
 oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
                                  const uint8_t* view_mask);
@@ -714,12 +725,13 @@ static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uin
         auto t0 = std::chrono::steady_clock::now();
         if (threads <= 1) {
             for (uint32_t v = 0; v < R; ++v) {
-                Oracle o(B, cfg, (flags & 1) && !gid, (flags & 8) != 0);
+                Oracle o(B, cfg, (flags & 1) && !gid, (flags & 40) != 0);
+                o.bound_max = (flags & 32) != 0;
                 o.gid = gid;
                 for (uint32_t i = 0; i < n; ++i) all[v][i] = o.preaccept(i, v);
             }
         } else {
-            if (flags & 8) throw std::invalid_argument("threaded oracle: executeAt-bound deps unsupported");
+            if (flags & 40) throw std::invalid_argument("threaded oracle: executeAt / MAX-bound deps unsupported");
             // Shard the key space into `threads` contiguous ranges of the batch's distinct keys
             // (ShardDistributor.EvenSplit, local/ShardDistributor.java:32-80), one single-threaded
             // store per shard; each store answers the part of every query that falls in its range;
@@ -804,7 +816,7 @@ static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uin
         }
         if (flags & 4) {
             auto t4 = std::chrono::steady_clock::now();
-            res->level = exec_levels(B, merged, res->order);
+            res->level = exec_levels(B, merged, res->order, (flags & 16) != 0);
             auto t5 = std::chrono::steady_clock::now();
             res->t_levels = std::chrono::duration<double>(t5 - t4).count();
         }

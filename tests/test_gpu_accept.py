@@ -11,12 +11,16 @@ from accord_amd import abi, workload
 pytestmark = pytest.mark.gpu
 
 
-def check_accept(engine_factory, b, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1):
+def check_accept(engine_factory, b, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1, bound_max=False):
+    # bound_max: GetEphemeralReadDeps (bound Timestamp.MAX, GetEphemeralReadDeps.java:76) vs the oracle's MAX bound
     cfg = abi.make_config(window, replicas, drop_p, seed)
-    ref = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_ACCEPT)
+    ref = O.OracleResult(b, cfg, O.FLAG_MERGE | (O.FLAG_BOUND_MAX if bound_max else O.FLAG_ACCEPT))
     eng = engine_factory(window=window, replicas=replicas, drop_p=drop_p, seed=seed)
     eng.load(b)
-    eng.accept_deps()
+    if bound_max:
+        eng.ephemeral_read_deps()
+    else:
+        eng.accept_deps()
     for v in range(replicas):
         for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY, abi.CLASS_RANGE):
             got, want = eng.fetch_deps(v, c), ref.deps(v, c)
@@ -84,3 +88,33 @@ def test_accept_then_preaccept_on_one_handle(engine_factory):
     eng.preaccept_deps()
     for v in range(3):
         assert eng.fetch_deps(v, abi.CLASS_KEY).equal(ref.deps(v, abi.CLASS_KEY))
+
+
+@pytest.mark.parametrize("case", ["C2", "C3", "hot", "mixed", "large", "ranges"])
+def test_ephemeral_read_deps_bound_max(engine_factory, case):
+    # GetEphemeralReadDeps: every witnessed txn of the txn's keys / ranges, later TxnIds included, the window at the
+    # batch's end; every view and class and the merged Deps vs the oracle
+    rng = np.random.default_rng(41)
+    if case in ("C2", "C3"):
+        b, w = workload.config(case, n=20000), 32
+    elif case == "hot":
+        b, w = workload.generate(6000, keys_per_txn=2, keyspace=5, slow_frac=0.4, bump_max=200, seed=42), 0
+    elif case == "mixed":
+        n = 6000
+        kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT,
+                            abi.KIND_EXCLUSIVE_SYNC_POINT], size=n, p=[0.35, 0.35, 0.1, 0.1, 0.1])
+        status = rng.choice([abi.ST_APPLIED, abi.ST_COMMITTED, abi.ST_INVALID, abi.ST_TRANSITIVELY_KNOWN], size=n,
+                            p=[0.7, 0.1, 0.1, 0.1]).astype(np.uint8)
+        b, w = workload.generate(n, keys_per_txn=3, keyspace=150, kinds=kinds, status=status, slow_frac=0.3,
+                                 bump_max=100, seed=43), 8
+    elif case == "large":
+        b, w = workload.generate(3000, keys_per_txn=24, keyspace=2000, seed=44), 16
+    else:
+        b, w = workload.generate(8000, keys_per_txn=3, keyspace=20000, range_frac=0.15, range_width_max=3000, seed=45), 16
+    eng, ref = check_accept(engine_factory, b, window=w, bound_max=True)
+    # later TxnIds do appear (the PreAccept bound would leave them out)
+    got = eng.fetch_deps(0, abi.CLASS_KEY)
+    later = 0
+    for i in range(0, b["n"], 97):
+        later += int((got.txn(i)[1] > i).sum())
+    assert later > 0

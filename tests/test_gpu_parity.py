@@ -69,6 +69,50 @@ def test_pull_levels_far_bumps(engine_factory, bump):
     check(engine_factory, b, fixpoint=3)
 
 
+@pytest.mark.parametrize("name,bump", [("C2", 16), ("bumps", 5000), ("hot", 60)])
+def test_pull_levels_forced_abort(engine_factory, name, bump):
+    # the pull levels' abort path (placeholder levels, the abort flag, levels re-zeroed, chains rebuilt in
+    # successor mode, Kahn wavefronts) forced on every lane (AD_LEVELS_PULL_ABORT): the oracle's levels and order
+    if name == "C2":
+        b = workload.config("C2", n=60000, seed=31)
+    else:
+        b = workload.generate(30000, keys_per_txn=4, keyspace=20000 if name == "bumps" else 3000, slow_frac=0.3,
+                              bump_max=bump, seed=bump + 3)
+    eng = engine_factory()
+    check(engine_factory, b, fixpoint=4, eng=eng)
+    assert eng.last_times()["level_path"] == 3, "the pull pass must have aborted into the Kahn wavefronts"
+
+
+def test_pull_levels_far_predecessors_full_size(engine_factory):
+    # 1,048,576 txns where slow-path bumps move executeAt millions of ranks ahead, so a txn's
+    # predecessor can be a TxnId far after it, in a workgroup not resident while the waiting lanes occupy the
+    # chip.  The chain build flags predecessors more than 65536 rows ahead and the batch takes the Kahn
+    # wavefronts directly (no ~1 s spin until the abort cap): levels / order equal the Kahn mode's (which is
+    # oracle-checked at every smaller size), in well under a second.
+    import time
+    b = workload.generate(1 << 20, keys_per_txn=4, keyspace=10_000_000, slow_frac=0.2, bump_max=10 ** 7, seed=77)
+    eng = engine_factory()
+    eng.load(b)
+    eng.preaccept_deps()
+    eng.merge()
+    eng.exec_levels()                                   # warm-up (allocations)
+    t0 = time.perf_counter()
+    lv, order, _ = eng.exec_levels()
+    dt = time.perf_counter() - t0
+    assert eng.last_times()["level_path"] == 2, "far predecessors must send the batch to the Kahn wavefronts"
+    assert dt < 0.5, "levels took %.3f s" % dt
+    eng.set_level_mode(3)
+    klv, korder, _ = eng.exec_levels()
+    assert np.array_equal(lv, klv) and np.array_equal(order, korder)
+    # and the near case stays on the pull pass
+    c2 = engine_factory()
+    c2.load(workload.config("C2", n=1 << 20))
+    c2.preaccept_deps()
+    c2.merge()
+    c2.exec_levels()
+    assert c2.last_times()["level_path"] == 1
+
+
 @pytest.mark.parametrize("fixpoint", [False, True])
 def test_order_far_bumps(engine_factory, fixpoint):
     # slow-path bumps that move executeAt hundreds of ranks: the windowed-rank order fast path fails its

@@ -1,7 +1,9 @@
 """Key-range sharding (SURVEY §8e / BASELINE C5) on one GPU: S stores (handles) in one process run the full
-protocol (deps on sliced local batches, export, exchange, home merge, distributed level rounds, order) and must
-reproduce the unsharded engine bit for bit: KeyDeps are shard-invariant, and window/drop decisions use global
-arrival ranks."""
+protocol (deps on sliced local batches, export, exchange, home merge, levels, order) and must reproduce the
+unsharded engine bit for bit: KeyDeps are shard-invariant, and window/drop decisions use global arrival ranks.
+Levels: levels="gather" (the default: every store's constraint edges gathered once and solved,
+ad_shard_level_edges / ad_shard_levels_solve / ad_shard_levels_gather) and levels="rounds" (the per-round
+delta / dense exchange, rounds = graph depth)."""
 import numpy as np
 import pytest
 
@@ -26,11 +28,13 @@ def same_txn(got, h, want, g):
     return all(np.array_equal(x, y) for x, y in zip(a, b))
 
 
-@pytest.mark.parametrize("name,shards,delta", [("C2", 2, True), ("C2", 4, True), ("C3", 3, True), ("C3", 3, False),
-                                                ("C2", 4, False)])
-def test_sharded_equals_unsharded(engine_factory, name, shards, delta):
-    # delta: level rounds exchange only raised levels of shared txns (ad_shard_set_holders); else the dense
-    # all-reduce of the whole level array
+@pytest.mark.parametrize("name,shards,levels,delta", [("C2", 2, "gather", False), ("C2", 4, "gather", True),
+                                                       ("C3", 3, "gather", False), ("C2", 2, "rounds", True),
+                                                       ("C3", 3, "rounds", True), ("C3", 3, "rounds", False),
+                                                       ("C2", 4, "rounds", False)])
+def test_sharded_equals_unsharded(engine_factory, name, shards, levels, delta):
+    # levels="rounds" + delta: level rounds exchange only raised levels of shared txns (ad_shard_set_holders);
+    # rounds without delta: the dense all-reduce of the whole level array; "gather": one edge exchange
     w, r, p, s = 32, 3, 0.1, 0xACC0D1
     b = workload.config(name, n=30000)
     views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
@@ -45,8 +49,8 @@ def test_sharded_equals_unsharded(engine_factory, name, shards, delta):
             st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
             stores.append(st)
             st.load(local, gid, hs[gid], b["n"], k, shards, holders=masks[gid] if delta else None)
-        rounds = sharding.LocalTransport.run(stores)
-        assert rounds >= 1
+        rounds = sharding.LocalTransport.run(stores, levels=levels)
+        assert rounds >= 1 and (levels == "rounds" or rounds == 1)
         seen = np.zeros(b["n"], bool)
         pos = {int(t): i for i, t in enumerate(order)}
         for st in stores:
@@ -215,12 +219,13 @@ def test_host_fragments_import(engine_factory):
             st.close()
 
 
-@pytest.mark.parametrize("delta", [True, False])
-def test_rccl_world1_run_store(engine_factory, tmp_path, delta):
+@pytest.mark.parametrize("levels,delta", [("gather", False), ("rounds", True), ("rounds", False)])
+def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta):
     # the RCCL transport end to end on the one GPU: a world = 1 communicator (ad_comm_init), the grouped
-    # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and the level rounds — delta: ncclAllGather of
-    # the pair counts (ad_shard_levels_exchange); dense: ncclAllReduce of the level array
-    # (ad_shard_levels_allreduce) — driven by the same run_store the N>1 bench uses; equal to the unsharded engine
+    # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and the levels — gather: ncclAllGather of the
+    # edge counts + the edge send/recv (ad_shard_levels_gather); rounds + delta: ncclAllGather of the pair counts
+    # (ad_shard_levels_exchange); rounds, dense: ncclAllReduce of the level array (ad_shard_levels_allreduce) —
+    # driven by the same run_store the N>1 bench uses; equal to the unsharded engine
     import torch.distributed as dist
     w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
     b = workload.generate(200_000, 4, 10_000_000, "uniform", seed=s)
@@ -231,8 +236,8 @@ def test_rccl_world1_run_store(engine_factory, tmp_path, delta):
         stores, _, _ = _make_stores(b, 1, w, r, p, s, 10_000_000, delta=delta)
         tr = sharding.RcclTransport(dist, stores[0], 0, 1)
         assert tr.name == "rccl"
-        rounds = sharding.run_store(stores[0], tr)
-        assert rounds >= 1
+        rounds = sharding.run_store(stores[0], tr, levels=levels)
+        assert rounds >= 1 and (levels == "rounds" or rounds == 1)
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all()
         # a second communicator on the same handle is refused (no leak of the first)
@@ -252,7 +257,7 @@ def test_levels_round_cap_raises(engine_factory):
     stores, _, _ = _make_stores(b, 3, w, r, p, s, 10_000_000)
     try:
         with pytest.raises(sharding.LevelsNotConverged):
-            sharding.LocalTransport.run(stores, max_rounds=1)
+            sharding.LocalTransport.run(stores, max_rounds=1, levels="rounds")
     finally:
         for st in stores:
             st.close()
@@ -260,7 +265,7 @@ def test_levels_round_cap_raises(engine_factory):
 
 def test_c5_four_stores_1m_each(engine_factory):
     # C5's generator at 1,048,576 txns per store over S = 4 key-range stores (4,194,304 txns, 40M keys): the full
-    # cross-store protocol (local deps, export, exchange, home merge, distributed level rounds, order) equals the
+    # cross-store protocol (local deps, export, exchange, home merge, one level-edge exchange, order) equals the
     # unsharded engine on the whole batch, bit for bit, for every home txn of every store
     w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
     shards, per = 4, 1 << 20
@@ -269,9 +274,7 @@ def test_c5_four_stores_1m_each(engine_factory):
     stores, _, _ = _make_stores(b, shards, w, r, p, s, 10_000_000 * shards)
     try:
         rounds = sharding.LocalTransport.run(stores)
-        assert rounds >= 1
-        # delta exchange: the last round raised nothing another store needs
-        assert all(int(st.level_deltas()[0].sum()) == 0 for st in stores)
+        assert rounds == 1
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all(), "every txn has exactly one home store"
     finally:
@@ -290,13 +293,16 @@ def unsharded3(engine_factory, b, w, r, p, s):
     return views, merged, lv, order
 
 
-@pytest.mark.parametrize("shards,delta,special", [(2, True, False), (3, True, True), (4, False, True), (4, True, False)])
-def test_sharded_range_txns_equal_presplit_unsharded(engine_factory, shards, delta, special):
+@pytest.mark.parametrize("shards,levels,delta,special", [(2, "gather", True, False), (3, "gather", True, True),
+                                                          (4, "gather", False, True), (4, "rounds", True, False),
+                                                          (3, "rounds", False, False)])
+def test_sharded_range_txns_equal_presplit_unsharded(engine_factory, shards, levels, delta, special):
     # range txns sliced at the store bounds; the stores together must equal the unsharded engine on
     # the batch whose ranges are cut at the same bounds (sharding.presplit; the CPU test
     # test_sharding_ranges.py pins that claim with the oracle): every view and class incl. RangeDeps, the merged
     # Deps, levels (rules (b)/(c) applied per store from its own views' Deps.merge) and the order.  special:
-    # key-domain sync points / ephemeral reads too.
+    # key-domain sync points / ephemeral reads too, and range sync points / exclusive sync points (their levels
+    # run ~10^3 deep: one edge exchange, not one round per level).
     w, r, p, s = 32, 3, 0.1, 0xACC0D1
     n, ks = 12000, 160_000
     kinds = None
@@ -305,13 +311,6 @@ def test_sharded_range_txns_equal_presplit_unsharded(engine_factory, shards, del
             [abi.KIND_READ, abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT, abi.KIND_EPHEMERAL_READ],
             size=n, p=[0.4, 0.4, 0.07, 0.07, 0.06])
     b = workload.generate(n, 4, ks, "uniform", range_frac=0.1, range_width_max=1 << 13, kinds=kinds, seed=40 + shards)
-    if special:
-        # range txns stay Reads: wide range sync points chain the txns they cover into levels ~2000 deep (30k txns,
-        # widths up to 2^15 of 4*10^5 keys), and the distributed rounds (one level exchange each) then run into the
-        # hundreds — correct, but not a unit test
-        dom = (b["txn_lsb"] & np.uint64(1)).astype(bool)
-        for f in ("txn_lsb", "exec_lsb"):
-            b[f] = np.where(dom, (b[f] & ~np.uint64(0xE)) | np.uint64(abi.KIND_READ << 1), b[f]).astype(np.uint64)
     bounds = sharding.even_bounds(0, ks, shards)
     views, merged, lv, order = unsharded3(engine_factory, sharding.presplit(b, bounds), w, r, p, s)
     hs = sharding.home_stores(b, bounds)
@@ -323,7 +322,7 @@ def test_sharded_range_txns_equal_presplit_unsharded(engine_factory, shards, del
             st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
             stores.append(st)
             st.load(local, gid, hs[gid], b["n"], k, shards, holders=masks[gid] if delta else None)
-        sharding.LocalTransport.run(stores)
+        assert sharding.LocalTransport.run(stores, levels=levels) >= 1
         seen = np.zeros(b["n"], bool)
         pos = {int(t): i for i, t in enumerate(order)}
         ranged = 0
@@ -370,3 +369,98 @@ def test_sharded_range_blob_bytes_equal_host_codec(engine_factory):
         assert np.array_equal(sizes, hsizes) and np.array_equal(buf, hbuf)
     finally:
         st.close()
+
+
+def _range_batch_check(stores, views, merged, lv, order, r, b):
+    """Every store's home txns against the unsharded (presplit) engine, all three classes, vectorised."""
+    pos = np.empty(len(order), np.int64)
+    pos[order] = np.arange(len(order))
+    seen = np.zeros(b["n"], bool)
+    for st in stores:
+        for v in range(r + 1):
+            for c in range(3):
+                got, hg = st.fetch(v, c)
+                want = merged[c] if v == r else views[v][c]
+                assert blob._rows_of(want, hg).equal(got), "store view %d class %d differs" % (v, c)
+        hl, ho = st.order()
+        _, hg = st.fetch(r, abi.CLASS_KEY)
+        assert np.array_equal(hl, lv[hg]), "levels differ"
+        assert np.all(np.diff(pos[ho]) > 0)
+        assert not seen[hg].any()
+        seen[hg] = True
+    touched = (np.diff(b["key_off"]) > 0) | (np.diff(b["range_off"]) > 0)
+    assert seen[touched].all(), "every txn has exactly one home store"
+
+
+def test_sharded_deep_range_sync_points(engine_factory):
+    # the configuration that did not converge under the per-round exchange (round 2: still raising levels after
+    # 68 rounds at 0.5 s each): 30k txns, 3 stores, 10 % range txns of every kind incl. range sync points and
+    # exclusive sync points up to 2^15 wide over 4*10^5 keys, key-domain sync points / ephemeral reads.  One edge
+    # exchange; levels ~10^3 deep; every class, merged Deps, levels and order equal the presplit unsharded engine.
+    shards = 3
+    w, r, p, s = 32, 3, 0.1, 0xACC0D1
+    n, ks = 30000, 400_000
+    kinds = np.random.default_rng(shards).choice(
+        [abi.KIND_READ, abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT, abi.KIND_EPHEMERAL_READ],
+        size=n, p=[0.4, 0.4, 0.07, 0.07, 0.06])
+    b = workload.generate(n, 4, ks, "uniform", range_frac=0.1, range_width_max=1 << 15, kinds=kinds, seed=40 + shards)
+    bounds = sharding.even_bounds(0, ks, shards)
+    views, merged, lv, order = unsharded3(engine_factory, sharding.presplit(b, bounds), w, r, p, s)
+    assert lv.max() > 500, "the configuration is meant to be deep"
+    hs = sharding.home_stores(b, bounds)
+    stores = []
+    try:
+        for k in range(shards):
+            local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+            st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
+            stores.append(st)
+            st.load(local, gid, hs[gid], b["n"], k, shards)
+        assert sharding.LocalTransport.run(stores) == 1
+        assert all(st.depth == lv.max() + 1 for st in stores)
+        _range_batch_check(stores, views, merged, lv, order, r, b)
+    finally:
+        for st in stores:
+            st.close()
+
+
+def test_sharded_c3_full_size_8_stores(engine_factory):
+    # BASELINE C3 at its full 1,048,576 txns (Zipf 0.99: the hot keys chain ~1.6*10^5 levels) over 8 key-range
+    # stores: one edge exchange, levels and order equal the unsharded engine's (deep narrow frontiers solved
+    # inside one workgroup), and every view / merged Deps of every home txn
+    w, r, p, s = 32, 3, 0.1, workload.SEEDS["C3"]
+    b = workload.config("C3")
+    views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
+    stores, _, _ = _make_stores(b, 8, w, r, p, s, 10_000_000, delta=False)
+    try:
+        assert sharding.LocalTransport.run(stores) == 1
+        assert all(st.depth == lv.max() + 1 for st in stores)
+        seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
+        assert seen[np.diff(b["key_off"]) > 0].all()
+    finally:
+        for st in stores:
+            st.close()
+
+
+def test_c5_full_shape_8_stores(engine_factory):
+    # BASELINE C5 at its shape, in one process: 16,777,216 txns (4 uniform keys over 10^7) over 8 key-range stores
+    # through LocalTransport (export, exchange, home merge, one level-edge exchange, order), against the unsharded
+    # engine on the same batch: every view and the merged Deps of every home txn of every store, levels and order
+    import time
+    w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
+    t0 = time.perf_counter()
+    b = workload.config("C5")
+    views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
+    t1 = time.perf_counter()
+    stores, _, _ = _make_stores(b, 8, w, r, p, s, 10_000_000, delta=False)
+    try:
+        timings = {}
+        assert sharding.LocalTransport.run(stores) == 1
+        t2 = time.perf_counter()
+        assert all(st.depth == lv.max() + 1 for st in stores)
+        seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
+        assert seen[np.diff(b["key_off"]) > 0].all(), "every txn has exactly one home store"
+        print("C5 16M x 8 stores: unsharded %.1f s, 8-store protocol %.1f s, check %.1f s"
+              % (t1 - t0, t2 - t1, time.perf_counter() - t2))
+    finally:
+        for st in stores:
+            st.close()

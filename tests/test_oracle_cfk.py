@@ -335,3 +335,38 @@ def test_accept_range_bound():
     txns = [T(10, W, [15], exec_hlc=50), T(20, R, ranges=[(10, 20)]), T(70, R, ranges=[(10, 20)])]
     res, _ = run_accept(txns)
     assert d(res, RANGE, 0) == {(10, 20): [1]}
+
+
+# ------------------------------------------------------------------------------------------------
+# GetEphemeralReadDeps: PreAccept.calculatePartialDeps with bound = Timestamp.MAX (GetEphemeralReadDeps.java:76)
+# ------------------------------------------------------------------------------------------------
+def run_max(txns, window=0):
+    b = make_batch(txns)
+    return O.OracleResult(b, abi.make_config(window, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_BOUND_MAX), b
+
+
+def test_bound_max_sees_every_witnessed_txn():
+    # key 7: W0 applied, R1 / W2 / R3 preaccepted (window 0: statuses as given).  Bound MAX: every byId entry is
+    # before the bound (insertPos = the end, CommandsForKey.java:929); maxCommittedWriteBefore(MAX) = executeAt(W0),
+    # so W0 (executeAt == M) is not elided (:951-962); later TxnIds are candidates; the txn itself never
+    txns = [T(10, W, [7], status=abi.ST_APPLIED), T(20, R, [7], status=abi.ST_PREACCEPTED),
+            T(30, W, [7], status=abi.ST_PREACCEPTED), T(40, R, [7], status=abi.ST_PREACCEPTED)]
+    res, _ = run_max(txns)
+    assert d(res, KEY, 1) == {7: [0, 2]}              # the Read witnesses Writes only, W2 after it included
+    assert d(res, KEY, 0) == {7: [1, 2, 3]}           # the Write witnesses Reads and Writes, all later
+    pre, _ = run(txns, window=0)
+    assert d(pre, KEY, 1) == {7: [0]}                 # PreAccept: only earlier TxnIds
+    # a committed Write executing before a later committed Write is elided under the MAX bound too
+    txns2 = [T(10, W, [7], status=abi.ST_APPLIED), T(20, W, [7], status=abi.ST_APPLIED), T(30, R, [7], status=abi.ST_PREACCEPTED)]
+    res2, _ = run_max(txns2)
+    assert d(res2, KEY, 2) == {7: [1]}
+
+
+def test_bound_max_range_txns_and_window():
+    # range commands: every range txn meeting the footprint, later ones included; with a window the last W
+    # arrivals of the batch are in flight (PREACCEPTED) — an INVALID range txn in it is still reported
+    txns = [T(10, W, [15]), T(20, R, ranges=[(10, 20)]), T(70, R, ranges=[(12, 18)], status=abi.ST_INVALID)]
+    res, _ = run_max(txns, window=0)
+    assert d(res, RANGE, 0) == {(10, 20): [1]}
+    res_w, _ = run_max(txns, window=2)
+    assert d(res_w, RANGE, 0) == {(10, 20): [1], (12, 18): [2]}

@@ -40,7 +40,8 @@ def _concat(a, b):
 
 
 def keep_rows(b, gid, window):
-    """history_kernels.h k_hist_seg_wmax + k_hist_keep: rows a later query can still see."""
+    """history_kernels.h k_hist_seg_wmax + k_hist_keep: rows a later query or the execution order can still need
+    (statuses are current: only INVALID rows and APPLIED rows no later mapReduceActive sees are dropped)."""
     n = b["n"]
     kind = (b["txn_lsb"] >> np.uint64(1)) & np.uint64(7)
     ex = [_ts(b["exec_msb"][i], b["exec_lsb"][i], b["exec_node"][i]) for i in range(n)]
@@ -64,8 +65,8 @@ def keep_rows(b, gid, window):
         st = b["status"][i]
         for k in b["keys"][ko[i]:ko[i + 1]]:
             k = int(k)
-            prunable = (not managed or st in (abi.ST_TRANSITIVELY_KNOWN, abi.ST_INVALID) or
-                        (st in COMMITTED and kind[i] in (R, W) and k in mk and ex[i] < mk[k]))
+            prunable = st == abi.ST_INVALID or (
+                st == abi.ST_APPLIED and (not managed or (kind[i] in (R, W) and k in mk and ex[i] < mk[k])))
             if not prunable:
                 keep.append(i)
                 break
@@ -106,10 +107,14 @@ def test_history_batches_equal_whole_stream(window, drop, keyspace):
                         "batch %d view %d class %d txn %d" % (k, v, c, k * nb + x)
         keep = keep_rows(comb, gid, window)
         hist, hgid = _take(comb, keep), gid[keep]
-        kept_sizes.append(len(keep))
-    # the kept state is what a later query can see (in flight, undecided, each key's last committed Write and what
-    # executes after it): bounded on dense keyspaces; on a sparse one every once-touched key keeps its entry, as a
-    # live CommandsForKey does until a committed Write there lets Pruning drop it
+        done = np.isin(comb["status"][keep], (abi.ST_APPLIED, abi.ST_INVALID))
+        kept_sizes.append(int(done.sum()))
+        # every row that still executes or may still be preaccepted stays (statuses are current between batches)
+        live = ~np.isin(comb["status"], (abi.ST_APPLIED, abi.ST_INVALID))
+        assert np.isin(np.nonzero(live)[0], keep).all()
+    # the applied rows kept are what a later query can still see (in flight, each key's last applied Write and
+    # what executes after it): bounded on dense keyspaces; on a sparse one every once-touched key keeps its
+    # entry, as a live CommandsForKey does until a committed Write there lets Pruning drop it
     assert all(s < (k + 1) * nb for k, s in enumerate(kept_sizes))
     if keyspace <= 300:
         assert max(kept_sizes) < 2 * nb

@@ -58,8 +58,9 @@ def test_initial_command():
 def test_multi_key_timestamp_update():
     # multiKeyTimestampUpdate (:187-222): (1, 100, ID2) on key 10 arrives first; then txnId2 = (1, 50, ID3) on keys
     # {10, 11}: no deps (the earlier arrival has the larger TxnId), maxConflict = (1, 100, ID2) > txnId2 -> slow path,
-    # witnessedAt = uniqueNow(maxConflict) = (epoch 1, hlc 110, ID1)
-    clock = Wt.NodeClock(ID1, 1, 100)
+    # witnessedAt = uniqueNow(maxConflict) = (epoch 1, hlc 110, ID1).  Node.now was built at epoch 0 (Node.java:188,
+    # before the test topology was reported), so nowAtLeast (:368-375) takes the max conflict's bits, flags included
+    clock = Wt.NodeClock(ID1, 1, 100, now_epoch=0)
     first = make_batch([T(100, abi.KIND_WRITE, [10], node=ID2)])
     second = make_batch([T(50, abi.KIND_WRITE, [10, 11], node=ID3)])
     (_, mc1, f1), (deps2, mc2, f2) = store_process([first, second])
@@ -68,9 +69,12 @@ def test_multi_key_timestamp_update():
     assert max_conflict(mc2, 0) == Wt.from_values(1, 100, WRITE_KEY_FLAGS, ID2) and f2[0] == 0
     clock.clock += 10
     w = Wt.preaccept_witnessed_at(Wt.from_values(1, 50, WRITE_KEY_FLAGS, ID3), max_conflict(mc2, 0), clock)
-    # Timestamp.fromValues(1, 110, ID1).withExtraFlags(txnId2.flags()): epoch, hlc and node; the kind flag bits of
-    # the expected value come from the test's withExtraFlags (Node.uniqueNow keeps Node.now's own flags)
-    assert (Wt.epoch(w), Wt.hlc(w), w[2]) == (1, 110, ID1)
+    # expectedTs = Timestamp.fromValues(1, 110, ID1).withExtraFlags(txnId2.flags()), compared by PreAcceptOk.equals
+    # -> Timestamp.equals (Timestamp.java:244-249: IDENTITY_LSB includes the kind flags): Node.nowAtLeast takes the
+    # max conflict's bits (its flags: Write, Key — txnId2's too) with Node.now's hlc and node, and uniqueNow keeps
+    # them (withNextHlc / withEpochAtLeast carry flags())
+    assert Wt.equals(w, Wt.from_values(1, 110, WRITE_KEY_FLAGS, ID1))
+    assert not Wt.equals(w, Wt.from_values(1, 110, 0, ID1))            # the flags are part of the identity
 
 
 def test_single_key_newer_timestamp():
