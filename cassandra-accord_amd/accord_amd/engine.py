@@ -84,6 +84,14 @@ def lib():
         L.ad_recover.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.ad_fetch_recovery.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.ad_fetch_recovery_flags.argtypes = [vp, vp]
+        L.ad_load_batch_async.argtypes = [vp, C.POINTER(abi.AdBatch)]
+        L.ad_load_batch_commit.argtypes = [vp]
+        L.ad_host_alloc.argtypes = [C.c_size_t]
+        L.ad_host_alloc.restype = vp
+        L.ad_host_free.argtypes = [vp]
+        L.ad_host_free.restype = None
+        L.ad_merged_sizes.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
+        L.ad_fetch_merged_all.argtypes = [vp, C.POINTER(abi.AdCsrOut)]
         _LIB = L
     return _LIB
 
@@ -98,7 +106,47 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_shard_levels_allreduce", "ad_shard_order", "ad_shard_set_holders", "ad_shard_levels_deltas",
             "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows", "ad_cfk_update",
             "ad_recover", "ad_fetch_recovery", "ad_fetch_recovery_flags", "ad_shard_level_edges", "ad_shard_levels_solve",
-            "ad_shard_levels_gather", "ad_ephemeral_read_deps")
+            "ad_shard_levels_gather", "ad_ephemeral_read_deps", "ad_load_batch_async", "ad_load_batch_commit",
+            "ad_host_alloc", "ad_host_free", "ad_merged_sizes", "ad_fetch_merged_all")
+
+
+class PinnedArena:
+    """Page-locked host arrays (ad_host_alloc): batches and fetched Deps whose H2D / D2H copies are DMA
+    transfers.  Arrays are numpy views; they live until close()."""
+
+    def __init__(self):
+        self._blocks = []
+
+    def empty(self, count, dtype):
+        dt = np.dtype(dtype)
+        nbytes = max(int(count) * dt.itemsize, 64)
+        p = lib().ad_host_alloc(nbytes)
+        if not p:
+            raise MemoryError("ad_host_alloc(%d) failed" % nbytes)
+        self._blocks.append(p)
+        buf = (C.c_uint8 * nbytes).from_address(p)
+        return np.frombuffer(buf, dtype=dt, count=int(count))
+
+    def copy(self, a):
+        out = self.empty(a.size, a.dtype)
+        out[:] = a.reshape(-1)
+        return out
+
+    def batch(self, b):
+        """A pinned copy of a workload batch dict (numpy arrays copied, scalars kept)."""
+        return {k: (self.copy(v) if isinstance(v, np.ndarray) else v) for k, v in b.items()}
+
+    def csr(self, s, is_range=False):
+        """An abi.Csr sized by ad_csr_sizes `s`, in pinned memory."""
+        n = s.n
+        return abi.Csr(self.empty(n + 1, np.uint32), self.empty(s.keys * (2 if is_range else 1), np.uint64),
+                       self.empty(n + 1, np.uint32), self.empty(s.k2t, np.int32),
+                       self.empty(n + 1, np.uint32), self.empty(s.txns, np.uint32), is_range=is_range)
+
+    def close(self):
+        for p in self._blocks:
+            lib().ad_host_free(p)
+        self._blocks = []
 
 
 class DepsEngine:
@@ -146,6 +194,35 @@ class DepsEngine:
         self._check(lib().ad_cfk_rows(self.h, C.byref(hr), None), "ad_cfk_rows")
         self.hist_rows = hr.value
         self.n = self.n_rows = batch["n"] + hr.value
+
+    def load_async(self, batch):
+        """Stage the next batch on the copy stream (ad_load_batch_async); the loaded batch keeps running.
+        `batch` must stay alive until load_commit()."""
+        self._staged = abi.make_batch(batch)
+        self._staged_n = batch["n"]
+        self._check(lib().ad_load_batch_async(self.h, C.byref(self._staged)), "ad_load_batch_async")
+
+    def load_commit(self):
+        self._check(lib().ad_load_batch_commit(self.h), "ad_load_batch_commit")
+        self._batch = self._staged
+        self._staged = None
+        self.hist_rows = 0
+        self.n = self.n_rows = self._staged_n
+
+    def merged_sizes(self):
+        sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
+        self._check(lib().ad_merged_sizes(self.h, sizes), "ad_merged_sizes")
+        return sizes
+
+    def fetch_merged_all(self, outs=None):
+        """The merged Deps of all three classes in one call (ad_fetch_merged_all); `outs` optional
+        preallocated abi.Csr per class (e.g. PinnedArena.csr of merged_sizes())."""
+        if outs is None:
+            s = self.merged_sizes()
+            outs = [abi.Csr.alloc(s[c], is_range=(c == abi.CLASS_RANGE)) for c in range(abi.NUM_CLASSES)]
+        arr = (abi.AdCsrOut * abi.NUM_CLASSES)(*[o.as_out() for o in outs])
+        self._check(lib().ad_fetch_merged_all(self.h, arr), "ad_fetch_merged_all")
+        return outs
 
     def preaccept_deps(self):
         sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()
@@ -337,10 +414,12 @@ class DepsEngine:
     def run_pipeline(self):
         self._check(lib().ad_run_pipeline(self.h), "ad_run_pipeline")
 
-    def fetch_levels(self):
-        """(levels, order) left on the device by the last run_pipeline / exec_levels."""
-        lv = np.zeros(max(self.n, 1), np.uint32)
-        order = np.zeros(max(self.n, 1), np.uint32)
+    def fetch_levels(self, out=None):
+        """(levels, order) left on the device by the last run_pipeline / exec_levels; `out` an optional
+        preallocated (levels, order) pair of uint32 arrays with at least n entries (e.g. pinned)."""
+        lv, order = out if out is not None else (np.zeros(max(self.n, 1), np.uint32), np.zeros(max(self.n, 1), np.uint32))
+        if len(lv) < self.n or len(order) < self.n or lv.dtype != np.uint32 or order.dtype != np.uint32:
+            raise ValueError("fetch_levels: out arrays too small or not uint32")
         self._check(lib().ad_fetch_levels(self.h, lv.ctypes.data, order.ctypes.data), "ad_fetch_levels")
         return lv[:self.n], order[:self.n]
 

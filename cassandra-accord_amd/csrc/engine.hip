@@ -376,6 +376,47 @@ void launch_mc_ranges(const McRangeArgs& a, hipStream_t st) {
 // =====================================================================================================
 // C-ABI
 // =====================================================================================================
+// The working buffers of a loaded batch of h->n rows, h->P pairs, h->Q ranges (grow-only slots).
+static int load_working(ad_handle* h) {
+    const size_t n = h->n, P = h->P, Q = h->Q;
+    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
+    CK(dalloc(h, S_PRM, &h->prm, 1)); CK(dalloc(h, S_TOT, &h->totd, MAX_TOTALS));
+    CK(dalloc(h, S_TXTS, &h->tx_ts, n)); CK(dalloc(h, S_EX1, &h->ex1, n)); CK(dalloc(h, S_META, &h->meta, n));
+    CK(dalloc(h, S_PTXN, &h->prec, P));
+    CK(dalloc(h, S_KA, &h->ka, P)); CK(dalloc(h, S_VA, &h->va, P)); CK(dalloc(h, S_KB, &h->kb, P)); CK(dalloc(h, S_VB, &h->vb, P));
+    CK(dalloc(h, S_ETXN, &h->e_txn, P)); CK(dalloc(h, S_EMETA, &h->e_meta, P));
+    CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
+    CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
+    CK(dalloc(h, S_UIDX, &h->nh, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
+    CK(dalloc(h, S_CNT, &h->cnt, (size_t)nvc * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
+    CK(dalloc(h, S_NK, &h->nk, (size_t)nvc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nvc * n + n));
+    CK(dalloc(h, S_VN, &h->vn, n)); CK(dalloc(h, S_VOFF, &h->voff, n + 1));
+    CK(dalloc(h, S_LVL, &h->lvl, n + 1)); CK(dalloc(h, S_ORDER, &h->order, n + 1));
+    CK(dalloc(h, S_ROWN, &h->rowner, Q)); CK(dalloc(h, S_RK0, &h->rk0, Q)); CK(dalloc(h, S_RV0, &h->rv0, Q));
+    CK(dalloc(h, S_RK1, &h->rk1, Q)); CK(dalloc(h, S_RV1, &h->rv1, Q));
+    CK(dalloc(h, S_ES, &h->es, Q)); CK(dalloc(h, S_EE, &h->ee, Q)); CK(dalloc(h, S_EOWN, &h->eown, Q));
+    CK(dalloc(h, S_RNK, &h->rnk, (size_t)nv * n)); CK(dalloc(h, S_RNE, &h->rne, (size_t)nv * n));
+    const size_t big = std::max(std::max(P, n), Q);
+    size_t sc = std::max<size_t>(1 << 20, 3 * (radix_hist_len(big) + 128) * 4 + 64 * 1024);
+    sc = std::max(sc, device_scan_scratch<ElideOp>(big) + 4096);
+    sc = std::max(sc, level_scratch_bytes(n, P));
+    CK(ensure_scratch(h, sc));
+    return AD_OK;
+}
+
+// ---- asynchronous batch upload (ad_load_batch_async / ad_load_batch_commit): the input SoA of the next batch
+// is copied on a copy stream into a second set of input slots while the current batch runs; the commit swaps
+// the two sets.  With pinned host buffers (ad_host_alloc) the copies are DMA transfers over PCIe that overlap
+// the pipeline and the previous batch's paged-out results.
+static const size_t IN_SLOTS[12] = {S_TM, S_TL, S_TN, S_EM, S_EL, S_EN, S_ST, S_KOFF, S_KEYS, S_ROFF, S_RS, S_RE};
+
+static void bind_inputs(ad_handle* h) {
+    h->tm = (uint64_t*)h->bufs[S_TM].p; h->tl = (uint64_t*)h->bufs[S_TL].p; h->tn = (int32_t*)h->bufs[S_TN].p;
+    h->em = (uint64_t*)h->bufs[S_EM].p; h->el = (uint64_t*)h->bufs[S_EL].p; h->en = (int32_t*)h->bufs[S_EN].p;
+    h->status = (uint8_t*)h->bufs[S_ST].p; h->key_off = (uint32_t*)h->bufs[S_KOFF].p; h->keys = (uint64_t*)h->bufs[S_KEYS].p;
+    h->range_off = (uint32_t*)h->bufs[S_ROFF].p; h->range_s = (uint64_t*)h->bufs[S_RS].p; h->range_e = (uint64_t*)h->bufs[S_RE].p;
+}
+
 extern "C" {
 
 int ad_device_count(void) {
@@ -408,6 +449,9 @@ void ad_close(ad_handle* h) {
     hipSetDevice(h->device);
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->st) hipStreamSynchronize(h->st);
+    if (h->cst) { hipStreamSynchronize(h->cst); hipStreamDestroy(h->cst); }
+    if (h->cev) hipEventDestroy(h->cev);
+    if (h->sev) hipEventDestroy(h->sev);
     if (h->pub_host) hipHostFree(h->pub_host);
     for (auto& b : h->bufs) if (b.p) hipFree(b.p);
     for (auto& e : h->ev) if (e) hipEventDestroy(e);
@@ -487,32 +531,79 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     } else {
         HIPCHK(h, hipMemsetAsync(h->range_off, 0, (n + 1) * 4, st));
     }
-    // working buffers
-    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
-    CK(dalloc(h, S_PRM, &h->prm, 1)); CK(dalloc(h, S_TOT, &h->totd, MAX_TOTALS));
-    CK(dalloc(h, S_TXTS, &h->tx_ts, n)); CK(dalloc(h, S_EX1, &h->ex1, n)); CK(dalloc(h, S_META, &h->meta, n));
-    CK(dalloc(h, S_PTXN, &h->prec, P));
-    CK(dalloc(h, S_KA, &h->ka, P)); CK(dalloc(h, S_VA, &h->va, P)); CK(dalloc(h, S_KB, &h->kb, P)); CK(dalloc(h, S_VB, &h->vb, P));
-    CK(dalloc(h, S_ETXN, &h->e_txn, P)); CK(dalloc(h, S_EMETA, &h->e_meta, P));
-    CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
-    CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
-    CK(dalloc(h, S_UIDX, &h->nh, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
-    CK(dalloc(h, S_CNT, &h->cnt, (size_t)nvc * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
-    CK(dalloc(h, S_NK, &h->nk, (size_t)nvc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nvc * n + n));
-    CK(dalloc(h, S_VN, &h->vn, n)); CK(dalloc(h, S_VOFF, &h->voff, n + 1));
-    CK(dalloc(h, S_LVL, &h->lvl, n + 1)); CK(dalloc(h, S_ORDER, &h->order, n + 1));
-    CK(dalloc(h, S_ROWN, &h->rowner, Q)); CK(dalloc(h, S_RK0, &h->rk0, Q)); CK(dalloc(h, S_RV0, &h->rv0, Q));
-    CK(dalloc(h, S_RK1, &h->rk1, Q)); CK(dalloc(h, S_RV1, &h->rv1, Q));
-    CK(dalloc(h, S_ES, &h->es, Q)); CK(dalloc(h, S_EE, &h->ee, Q)); CK(dalloc(h, S_EOWN, &h->eown, Q));
-    CK(dalloc(h, S_RNK, &h->rnk, (size_t)nv * n)); CK(dalloc(h, S_RNE, &h->rne, (size_t)nv * n));
-    const size_t big = std::max(std::max(P, n), Q);
-    size_t sc = std::max<size_t>(1 << 20, 3 * (radix_hist_len(big) + 128) * 4 + 64 * 1024);
-    sc = std::max(sc, device_scan_scratch<ElideOp>(big) + 4096);
-    sc = std::max(sc, level_scratch_bytes(n, P));
-    CK(ensure_scratch(h, sc));
+    CK(load_working(h));
     HIPCHK(h, hipStreamSynchronize(st));
     h->loaded = true;
     return AD_OK;
+}
+
+int ad_load_batch_async(ad_handle* h, const ad_batch* b) {
+    if (!h || !b) return AD_ERR_ARGUMENT;
+    if (h->hist_valid) return set_err(h, AD_ERR_UNSUPPORTED, "ad_load_batch_async: the next batch carries CFK history (ad_load_batch)");
+    if (h->stage_pending) return set_err(h, AD_ERR_STATE, "ad_load_batch_async: commit the staged batch first");
+    hipSetDevice(h->device);
+    const size_t n = b->n;
+    if (n >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
+    const size_t P = n ? b->key_off[n] : 0;
+    const size_t Q = (n && b->range_off) ? b->range_off[n] : 0;
+    if (P >= (1ull << 31) || Q >= (1ull << 31)) return set_err(h, AD_ERR_ARGUMENT, "batch too large");
+    if (!h->cst) {
+        HIPCHK(h, hipStreamCreateWithFlags(&h->cst, hipStreamNonBlocking));
+        HIPCHK(h, hipEventCreateWithFlags(&h->cev, hipEventDisableTiming));
+        HIPCHK(h, hipEventCreateWithFlags(&h->sev, hipEventDisableTiming));
+    }
+    const size_t cnt[12] = {n * 8, n * 8, n * 4, n * 8, n * 8, n * 4, n, (n + 1) * 4, P * 8, (n + 1) * 4, Q * 8, Q * 8};
+    uint8_t* d[12];
+    for (int k = 0; k < 12; ++k) CK(dalloc(h, S_STG0 + k, &d[k], cnt[k]));
+    // the staging slots held an earlier batch: copy only after the handle's stream is past its last use
+    HIPCHK(h, hipEventRecord(h->sev, h->st));
+    HIPCHK(h, hipStreamWaitEvent(h->cst, h->sev, 0));
+    const void* src[12] = {b->txn_msb, b->txn_lsb, b->txn_node, b->exec_msb, b->exec_lsb, b->exec_node, b->status,
+                           b->key_off, b->keys, b->range_off, b->range_start, b->range_end};
+    for (int k = 0; k < 12; ++k) {
+        if (k == 9 && !Q) { HIPCHK(h, hipMemsetAsync(d[k], 0, (n + 1) * 4, h->cst)); continue; }
+        if (k == 7 && !n) { HIPCHK(h, hipMemsetAsync(d[k], 0, 4, h->cst)); continue; }
+        if (cnt[k] && src[k]) HIPCHK(h, hipMemcpyAsync(d[k], src[k], cnt[k], hipMemcpyHostToDevice, h->cst));
+    }
+    HIPCHK(h, hipEventRecord(h->cev, h->cst));
+    h->stg_n = n; h->stg_p = P; h->stg_q = Q;
+    h->stage_pending = true;
+    return AD_OK;
+}
+
+int ad_load_batch_commit(ad_handle* h) {
+    if (!h) return AD_ERR_ARGUMENT;
+    if (!h->stage_pending) return set_err(h, AD_ERR_STATE, "ad_load_batch_commit: no staged batch (ad_load_batch_async)");
+    hipSetDevice(h->device);
+    HIPCHK(h, hipEventSynchronize(h->cev));          // the host batch may be reused once this returns
+    h->stage_pending = false;
+    if (h->hist_valid) return set_err(h, AD_ERR_UNSUPPORTED, "ad_load_batch_commit: CFK history was retained after the async load (ad_load_batch)");
+    for (int k = 0; k < 12; ++k) std::swap(h->bufs[IN_SLOTS[k]], h->bufs[S_STG0 + k]);
+    bind_inputs(h);
+    h->n = h->stg_n; h->P = h->stg_p; h->Q = h->stg_q;
+    h->loaded = false;
+    h->have_deps = h->have_merged = h->have_levels = false;
+    h->mc_ready = false;
+    h->mc_fast = nullptr;
+    h->rc_ready = false;
+    h->hist_active = false;
+    h->hist_rows = 0;
+    CK(load_working(h));
+    h->loaded = true;
+    return AD_OK;
+}
+
+void* ad_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 64), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void ad_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 static int run_deps(ad_handle* h, ad_csr_sizes* sizes, bool accept, bool bound_max = false) {
@@ -885,6 +976,45 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
     hipSetDevice(h->device);
     if (cls == AD_CLASS_RANGE) return h->merged_has_range ? fetch_csr(h, h->merged[2], 2, out) : fetch_empty(h, out);
     return fetch_csr(h, h->merged[cls], 1, out);
+}
+
+// The merged Deps of every class in one call: Deps.merge's outputs carry exact per-txn TxnId offsets
+// (MultiOffsetsOp), so every array goes straight from HBM into the caller's buffers (pinned: DMA) with one stream
+// sync and no host-side compaction.  out[c] sized by ad_merged_sizes.
+int ad_merged_sizes(ad_handle* h, ad_csr_sizes* sizes /* [3] */) {
+    if (!h || !sizes) return AD_ERR_ARGUMENT;
+    if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
+    for (int c = 0; c < 3; ++c) {
+        const Csr& m = h->merged[c];
+        const bool empty = c == AD_CLASS_RANGE && !h->merged_has_range;
+        sizes[c] = empty ? ad_csr_sizes{h->n, 0, 0, 0, 0} : ad_csr_sizes{h->n, m.nkeys, m.nk2t, m.ncap, m.ncap};
+    }
+    return AD_OK;
+}
+
+int ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [3] */) {
+    if (!h || !out) return AD_ERR_ARGUMENT;
+    if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const size_t n = h->n;
+    for (int c = 0; c < 3; ++c) {
+        const Csr& m = h->merged[c];
+        ad_csr_out& o = out[c];
+        if (c == AD_CLASS_RANGE && !h->merged_has_range) {
+            for (size_t i = 0; i <= n; ++i) { o.key_off[i] = 0; o.k2t_off[i] = 0; o.txn_off[i] = 0; }
+            continue;
+        }
+        const int kw = c == AD_CLASS_RANGE ? 2 : 1;
+        HIPCHK(h, hipMemcpyAsync(o.key_off, m.key_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(o.k2t_off, m.k2t_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(o.txn_off, m.ent_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+        if (m.nkeys) HIPCHK(h, hipMemcpyAsync(o.keys, m.keys, m.nkeys * 8 * kw, hipMemcpyDeviceToHost, st));
+        if (m.nk2t) HIPCHK(h, hipMemcpyAsync(o.k2t, m.k2t, m.nk2t * 4, hipMemcpyDeviceToHost, st));
+        if (m.ncap) HIPCHK(h, hipMemcpyAsync(o.txns, m.txns, m.ncap * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    return AD_OK;
 }
 
 int ad_fetch_rows(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t hi, ad_csr_sizes* sizes, ad_csr_out* out) {

@@ -150,6 +150,11 @@ struct ad_handle {
     bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
     bool accept = false;             // the deps stage runs with bound = executeAt (ad_accept_deps)
     bool bound_max = false;          // ... with bound = Timestamp.MAX (ad_ephemeral_read_deps)
+    // ad_load_batch_async: the next batch's inputs on a copy stream into the staging slots
+    hipStream_t cst = nullptr;
+    hipEvent_t cev = nullptr, sev = nullptr;
+    bool stage_pending = false;
+    size_t stg_n = 0, stg_p = 0, stg_q = 0;
     // CFK history (history_kernels.h): kept rows of earlier batches, prepended to the next loaded batch
     bool hist_valid = false;         // ad_cfk_retain ran: the next ad_load_batch prepends hist_n rows
     size_t hist_n = 0, hist_p = 0;   // kept rows / their keys
@@ -242,6 +247,7 @@ enum Slot : size_t {
     S_RIDX = S_RCEND, S_NONEROWS, S_LROWS, S_UMEDC, S_UMED,
     S_GLCT, S_GLCM, S_GLCE, S_GLCP, S_GLLW, S_GLEC, S_GLEO, S_GLXC, S_GLXO, S_GLCONS, S_GLE, S_GLIN,
     S_GLSRC, S_GLDST, S_GLSRC2, S_GLDST2, S_GLDEG, S_GLREM, S_GLXOFF, S_GLFL, S_GLFRONT, S_GLKEY, S_CFKU,
+    S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 192
 };

@@ -165,6 +165,20 @@ int  ad_device_count(void);
 /* Copy one batch host->device (the only PCIe transfer of the inputs).  Replaces the previous batch. */
 int  ad_load_batch(ad_handle* h, const ad_batch* batch);
 
+/* Double-buffered upload for a stream of batches (the CommandStore's next batch while this one runs):
+ * ad_load_batch_async enqueues the H2D copies of `batch` on the handle's copy stream into a second set of
+ * input buffers and returns at once; the loaded batch and its results stay untouched.  ad_load_batch_commit
+ * waits for those copies (the host arrays may be reused after it returns) and makes the staged batch the
+ * loaded one, as ad_load_batch would.  The host arrays must stay valid until the commit; from pinned memory
+ * (ad_host_alloc) the copies are DMA transfers that overlap the device work of the loaded batch.  Not for
+ * batches after ad_cfk_retain (AD_ERR_UNSUPPORTED: the kept rows are prepended by ad_load_batch). */
+int  ad_load_batch_async(ad_handle* h, const ad_batch* batch);
+int  ad_load_batch_commit(ad_handle* h);
+
+/* Page-locked host memory for batches and fetched Deps (hipHostMalloc); NULL on failure. */
+void* ad_host_alloc(size_t bytes);
+void  ad_host_free(void* p);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Stage 1 — PreAccept deps for every txn of the loaded batch under cfg->replicas views.       */
 /* Runs on the device; sizes[v * AD_NUM_CLASSES + c] receives the CSR sizes of view v class c. */
@@ -187,6 +201,11 @@ int  ad_fetch_deps(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out);
 /* Stage 2 — Deps.merge of the R replica replies produced by stage 1 (device-resident). */
 int  ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
 int  ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out);
+/* All three merged classes in one call: sizes[3] (txns == txn_cap: the merged TxnId lists are exact) and the
+ * arrays straight from HBM into out[3] with one stream sync (no host-side compaction) — with pinned buffers
+ * the whole page-out is three DMA streams.  An empty range class gets zero offsets. */
+int  ad_merged_sizes(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
+int  ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [AD_NUM_CLASSES] */);
 
 /* Stage 2 on the fast path — CoordinateTransaction.onPreAccepted (coordinate/CoordinateTransaction.java:71-101):
  * when the coordinator takes the fast path it merges only the replies whose witnessedAt == TxnId (:75); the slow
