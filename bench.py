@@ -50,6 +50,7 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
     M = st["merged_entries"]         # entries of the merged Deps
     W = st["walk_items"]             # entries the deps walks visit
     C = st.get("key_classes") or 2 * R   # key-footprint CSRs computed: 2R, or R without directKeyDeps
+    ncb = (C + 3) & ~3                   # count bytes per pair
     per = {
         "k_minmax": calls * (n * 44 + P * 8),                    # TxnId/executeAt SoA + key_off; keys
         "k_pack": calls * (n * 62 + P * 20),                     # read 45 B/txn, write 17 B/txn; 8+12 B/pair
@@ -60,11 +61,15 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
         "scan_elide": units * 37,                                # skey, e_meta, e_exec1 -> seg, ud, pm_w, pm_c
         # the walks visit only entries with an earlier entry of their key (ad_stage_times.walk_items):
         # list index, entry state, own txn's TxnId, predecessor entry, prefix state; C counts out
-        "k_deps_walk<count>": calls * W * (46 + 4 * C),
+        # (count: one byte per class out, the first WALK_INL emitted ids per class kept inline: 4 B per entry)
+        "k_deps_walk<count>": calls * (W * (46 + C) + 4 * D),
         "k_deps_walk<fill>": calls * (W * (46 + 4 * C) + 4 * D),  # C end slots in, the entries out
-        "k_txn_layout": units * (8 + 8 * C),                     # key + C counts in, C slots out
-        # OffsetsOp: per pair the key + C counts in and C slots out; per txn 3 offsets x C CSRs out
-        "scan_offsets": calls * (P * (8 + 8 * C)) + units * 12 * C,
+        # per txn: key_off, 4 offsets in + tcnt out per class; per pair key + count bytes; per entry the inline id
+        # in, k2t entry + TxnId out
+        "k_txn_finish": units * (8 + 20 * C) + calls * (P * (8 + ncb) + 12 * D),
+        # OffsetsOp: per pair one count dword (C <= 4 byte counts), per txn key_off + meta + deferred flag in and
+        # 3 offsets x C CSRs out
+        "scan_offsets": calls * (P * ncb) + units * (10 + 12 * C),
         "csr_offsets": units * 24,                               # 3 exclusive scans of one count array
         "merge_offsets": units * 24,                             # per (txn, output): 3 counts in, 3 offsets out
         # per txn: 3 offsets x C CSRs, the per-key lists in, unique TxnIds + remapped lists out
@@ -242,17 +247,17 @@ def roofline_of(eng, dom, n, P, st, large=False, pmc=True):
 
 
 ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profiles/*_pmc.json keys)
-    "k_deps_walk<fill>": "ad::k_deps_walk<3, true>", "k_deps_walk<count>": "ad::k_deps_walk<3, false>",
+    "k_deps_walk<fill>": "ad::k_deps_walk<3, true, false>", "k_deps_walk<count>": "ad::k_deps_walk<3, false, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
-    "k_gather_entries": "ad::k_gather_entries", "k_txn_layout": "ad::k_txn_layout",
-    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<6>",
+    "k_gather_entries": "ad::k_gather_entries", "k_txn_finish": "ad::k_txn_finish<3>",
+    "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<3>",
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
     # are shared fill/copy kernels and are not attributed)
     "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_step", "ad::k_chain_rank", "ad::k_chain_check",
                     "ad::k_chain_links", "ad::k_frontier_collect", "ad::k_kahn_small"),
-    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<6>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<6>, 1024>",
-                     "ad::k_scan_apply<ad::OffsetsOp<6>, 256, 4>"),
+    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<3>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<3>, 1024, 4>",
+                     "ad::k_scan_apply<ad::OffsetsOp<3>, 256, 4>"),
     "order_sort": ("ad::k_window_rank", "ad::k_rank_check"),
 }
 

@@ -68,7 +68,8 @@ class AdStageTimes(C.Structure):
                 ("deps_entries", C.c_uint64), ("merged_entries", C.c_uint64), ("level_edges", C.c_uint64),
                 ("level_iterations", C.c_uint32), ("walk_items", C.c_uint32),
                 ("level_blocks", C.c_uint32), ("level_rounds", C.c_uint32),
-                ("key_classes", C.c_uint32), ("level_path", C.c_uint32)]
+                ("key_classes", C.c_uint32), ("level_path", C.c_uint32),
+                ("deps_path", C.c_uint32)]
 
 
 def ptr(a, ctype):

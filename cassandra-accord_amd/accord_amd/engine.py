@@ -198,9 +198,9 @@ class DepsEngine:
     def load_async(self, batch):
         """Stage the next batch on the copy stream (ad_load_batch_async); the loaded batch keeps running.
         `batch` must stay alive until load_commit()."""
-        self._staged = abi.make_batch(batch)
-        self._staged_n = batch["n"]
-        self._check(lib().ad_load_batch_async(self.h, C.byref(self._staged)), "ad_load_batch_async")
+        staged = abi.make_batch(batch)
+        self._check(lib().ad_load_batch_async(self.h, C.byref(staged)), "ad_load_batch_async")
+        self._staged, self._staged_n = staged, batch["n"]      # a refused call leaves the staged batch as it was
 
     def load_commit(self):
         self._check(lib().ad_load_batch_commit(self.h), "ad_load_batch_commit")

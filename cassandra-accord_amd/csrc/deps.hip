@@ -144,25 +144,27 @@ int stage_deps(ad_handle* h) {
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
     wa.gid = (h->sharded || h->hist_active) ? h->gid : nullptr;
     wa.nh = h->nh; wa.prm = h->prm;
-    wa.sval = h->sval; wa.cnt = h->cnt; wa.dst = h->dst;
+    wa.sval = h->sval; wa.cnt8 = h->cnt8; wa.cntx = h->cntx; wa.inl = h->inl; wa.dfr = h->dfr; wa.dst = h->dst;
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
     wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
     wa.qpos = qpos; wa.ex1 = h->ex1; wa.bound_max = h->bound_max ? 1 : 0;
-    if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt, 0, (size_t)nc * P * 4, st));   // segment heads keep zero counts
-    launch_walk_nv(nv, wa, false, direct, st);
+    if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt8, 0, (size_t)ncb_of(nc) * P, st));   // segment heads keep zero counts
+    if (n > 0) HIPCHK(h, hipMemsetAsync(h->dfr, 0, n, st));
+    launch_walk_nv(nv, wa, false, direct, true, st);
     TxnArgs ta{};
-    ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt = h->cnt;
+    ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
-    uint32_t* overflow = h->totd + MAX_TOTALS - 1;       // fused-layout overflow flag (read with the totals)
+    uint32_t* heavy = h->totd + MAX_TOTALS - 1;          // heavy-merge hint (read with the totals)
+    uint32_t* any_dfr = heavy - 1;                        // some small txn deferred to the fill walk + union
     if (n > 0 && h->V > 0) {
         KScope ks(K_VITEMS);
         launch_large_sums_nv(nv, ta, direct, st);
     }
     if (n > 0) {
-        HIPCHK(h, hipMemsetAsync(overflow - 1, 0, 8, st));     // [heavy-merge hint, layout overflow]
+        HIPCHK(h, hipMemsetAsync(any_dfr, 0, 8, st));          // [deferred, heavy-merge hint]
         KScope ks(K_SCAN_OFFSETS, n);
-        launch_offsets_nv(h, nv, direct, cls, overflow);
+        launch_offsets_nv(h, nv, direct, cls, heavy);
     } else {
         for (int k = 0; k < nc; ++k) csr_offsets(h, h->deps[cls[k]], h->nk, h->ne);
     }
@@ -190,13 +192,16 @@ int stage_deps(ad_handle* h) {
         tt.count = 3 * c + 3;
     }
     const int ncol = tt.count;
-    tt.src[tt.count++] = overflow;
-    tt.src[tt.count++] = overflow - 1;
+    tt.src[tt.count++] = heavy;
+    tt.src[tt.count++] = any_dfr;
     std::vector<uint32_t> got(tt.count, 0);
     CK(read_totals_params(h, tt, got.data()));
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
-    const bool fused_layout = n > 0 && got[ncol] == 0;
-    h->merge_heavy = n == 0 || got[ncol + 1] != 0 || h->n_large > 0 || Q > 0;
+    // k_txn_finish completes every small txn whose pairs kept all their ids inline; only the deferred ones need
+    // the fill walk and the union (none on most C2 batches)
+    const bool deferred = n > 0 && got[ncol + 1] != 0;
+    h->times.deps_path = deferred ? 2u : 1u;
+    h->merge_heavy = n == 0 || got[ncol] != 0 || h->n_large > 0 || Q > 0;
     CK(check_params(h));
     h->deps_entries = 0;
     for (int c = 0; c < ncsr; ++c) {
@@ -206,6 +211,7 @@ int stage_deps(ad_handle* h) {
         if (c < nc) {
             CK(alloc_csr_data(h, cls[c], x, 1));
             ta.out_key_off[c] = x.key_off; ta.out_k2t_off[c] = x.k2t_off; ta.out_keys[c] = x.keys; ta.out_k2t[c] = x.k2t;
+            ta.out_ent_off[c] = x.ent_off; ta.out_txns[c] = x.txns; ta.out_tcnt[c] = x.tcnt;
             wa.k2t[c] = x.k2t;
         } else {
             CK(alloc_csr_data(h, CSR_RANGE0 + (c - nc), x, 2));
@@ -214,18 +220,20 @@ int stage_deps(ad_handle* h) {
         }
     }
     // ---- fill
-    if (n > 0 && !fused_layout) { KScope ks(K_TXN_LAYOUT, P); k_txn_layout<<<ceil_div((long)n, 256), 256, 0, st>>>(ta); }
+    ta.inl = h->inl; ta.dfr = h->dfr;
+    if (n > 0) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
-    launch_walk_nv(nv, wa, true, direct, st);
+    wa.only_dfr = 1;
+    launch_walk_nv(nv, wa, true, direct, deferred, st);
     if (Q > 0 && n > 0) launch_range_nv(nv, ra, true, st);
     UnionArgs ua{};
-    ua.n = n; ua.nvc = nc; ua.meta = h->meta;
+    ua.n = n; ua.nvc = nc; ua.meta = h->meta; ua.dfr = h->dfr;
     for (int vc = 0; vc < nc; ++vc) {
         Csr& c = h->deps[cls[vc]];
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    if (n > 0) { KScope ks(K_TXN_UNION, n); launch_union_nv(nv, ua, direct, st); }
+    if (n > 0 && deferred) { KScope ks(K_TXN_UNION, n); launch_union_nv(nv, ua, direct, st); }
     // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
         KScope ks(K_UNION_LDS);

@@ -9,10 +9,13 @@
 //                       writes (maxCommittedWriteBefore), prefix max executeAt of elidable entries, last
 //                       "always emitted" entry — CommandsForKey.mapReduceActive's state
 //                       (CommandsForKey.java:925-983) as one segmented scan
-//   walk<count|fill>    per query item (txn i, key segment, insert position) and replica view: the
-//                       dependencies mapReduceActive emits (CommandsForKey.java:945-965)
-//   small txns (key txns with <= KMAX keys): one thread per txn builds the per-txn KeyDeps layout and
-//   the TxnId union in registers (OffsetsOp's fused layout or k_txn_layout / k_txn_union)
+//   walk<count>         per query item (txn i, key segment, insert position) and replica view: the
+//                       dependencies mapReduceActive emits (CommandsForKey.java:945-965), counted per (pair,
+//                       class) in one byte, the first WALK_INL ids kept inline
+//   OffsetsOp scan      per-txn CSR offsets of every class
+//   k_txn_finish        small txns (key txns with <= 4 keys whose pairs kept every id inline): KeyDeps layout,
+//                       per-key lists and TxnId union in registers; the rest (deferred) get their layout here
+//                       and their lists from walk<fill> + k_txn_union (<= KMAX keys)
 //   large txns (range-domain txns querying every CFK key inside their ranges, and key txns with more
 //   than KMAX keys) go through "virtual items" (vitem_kernels in engine.hip) and union_kernels.h.
 #pragma once
@@ -24,6 +27,30 @@ constexpr int MAXV = 8;       // replica views
 constexpr int KMAX = 16;      // keys per key-domain txn handled by the per-txn register kernels
 constexpr int NVC_MAX = MAXV * 2;
 constexpr uint32_t META_LARGE = 0x80u;   // meta bit 7: txn takes the large (virtual item) path
+// The count walk keeps the first WALK_INL dependencies of every (pair, class) inline, so a txn whose pairs stay
+// within it gets its KeyDeps lists and TxnId union written by the offsets scan's store: no fill walk and no union
+// pass over it.  Counts are one byte per (pair, class), NCB bytes per pair (one dword for NC <= 4).
+constexpr int WALK_INL = 4;
+constexpr int ncb_of(int nc) { return (nc + 3) & ~3; }
+__device__ inline uint32_t pair_count(const uint8_t* __restrict__ cnt8, const uint32_t* __restrict__ cntx, int ncb, int nc,
+                                      size_t x, int c) {
+    const uint32_t b = cnt8[x * ncb + c];
+    return b == 255u ? cntx[x * nc + c] : b;
+}
+// all NC counts of pair x (dword loads: NCB is a multiple of 4)
+template <int NC>
+__device__ inline void pair_counts(const uint8_t* __restrict__ cnt8, const uint32_t* __restrict__ cntx, size_t x, uint32_t* v) {
+    constexpr int NCB = ncb_of(NC);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(cnt8 + x * NCB);
+    uint32_t d[NCB / 4];
+#pragma unroll
+    for (int q = 0; q < NCB / 4; ++q) d[q] = w[q];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t b = (d[c >> 2] >> (8 * (c & 3))) & 0xFFu;
+        v[c] = b == 255u ? cntx[x * NC + c] : b;
+    }
+}
 
 struct alignas(16) PairRec {  // per (txn, key) pair, in pair order: what the sorted entries gather
     uint64_t ex1;             // the txn's executeAt + 1 (packed)
@@ -322,7 +349,12 @@ struct WalkArgs {
     uint32_t thresh;
     uint64_t seed;
     const uint32_t* sval;     // sorted position -> pair index p
-    uint32_t* cnt;            // real pairs, AoS by pair: [p * 2NV + vc], vc = view * 2 + class
+    uint8_t* cnt8;            // real pairs, AoS by pair: [p * NCB + k] count of class k, 255 = see cntx
+    uint32_t* cntx;           // [p * NC + k] exact count where cnt8 saturated (>= 255)
+    uint32_t* inl;            // [(p * NC + k) * WALK_INL + q]: the first WALK_INL ids the walk emits (descending)
+    uint8_t* dfr;             // [txn] 1: a pair of the txn emits more than WALK_INL ids in some class, or the offsets
+                              // scan could not finish the txn (fill walk + union needed); count walk / scan write it
+    int only_dfr;             // fill walk: only the entries of deferred txns (0: every entry)
     const uint32_t* dst;      // real pairs, AoS by pair: absolute k2t slot of the last entry (fill)
     int32_t* k2t[NVC_MAX];    // per-vc keysToTxnIds (fill)
     // virtual items (large txns): item x queries key segment u = vi_u[x] ([useg[u], ...)) before position vi_pos[x]
@@ -380,12 +412,20 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t gq, ui
     const int p = q;
     if (p < seg0) return;
     uint64_t M1 = a.pm_w[p];
-    if (M1 >= b1) {   // a bumped executeAt beyond the bound: exact maxCommittedWriteBefore
+    bool exact = M1 >= b1;   // a bumped executeAt beyond the bound: exact maxCommittedWriteBefore
+    if (!exact && a.qpos && M1 != 0) {
+        // bound-position queries (Accept, GetEphemeralReadDeps) keep the txn's own entry inside [seg0, p]: it
+        // must not set maxCommittedWriteBefore (the oracle leaves the querying txn out, oracle.cpp map_reduce_active)
+        int l = seg0, r = p + 1;
+        while (l < r) { const int m = (l + r) >> 1; if (a.e_txn[m] < i) l = m + 1; else r = m; }
+        exact = l <= p && a.e_txn[l] == i && a.e_exec1[l] == M1;
+    }
+    if (exact) {
         M1 = 0;
         for (int x = p; x >= seg0; --x) {
             uint32_t m = a.e_meta[x];
             uint64_t e = a.e_exec1[x];
-            if (category(m) == CAT_ELIDABLE && meta_kind(m) == AD_KIND_WRITE && e < b1 && e > M1) M1 = e;
+            if (category(m) == CAT_ELIDABLE && meta_kind(m) == AD_KIND_WRITE && e < b1 && e > M1 && a.e_txn[x] != i) M1 = e;
         }
     }
     int qe = next_elidable(a, p, seg0, M1, qk);
@@ -437,15 +477,22 @@ static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
     const uint32_t qk = meta_kind(mi);
+    if (FILL && a.only_dfr && !a.dfr[i]) return;      // finished by the offsets scan from the inline ids
     // the pair's counts / slots live AoS by pair index (the per-txn kernels read them contiguously)
-    const size_t pb = (size_t)a.sval[s] * NC;
+    const size_t p = a.sval[s];
+    const size_t pb = p * NC;
     uint32_t c[NC];            // count mode: counts; fill mode: next write slot (descending)
 #pragma unroll
     for (int k = 0; k < NC; ++k) c[k] = FILL ? a.dst[pb + k] : 0u;
+    uint32_t* inl = a.inl + pb * WALK_INL;
     auto emit = [&](int v, bool direct, uint32_t j) {
         const int k = walk_class<NV, DIRECT>(v, direct);
-        if (FILL) a.k2t[k][c[k]--] = (int32_t)j;
-        else c[k]++;
+        if (FILL) {
+            a.k2t[k][c[k]--] = (int32_t)j;
+        } else {
+            if (c[k] < (uint32_t)WALK_INL) inl[k * WALK_INL + c[k]] = j;
+            c[k]++;
+        }
     };
     // small key-domain query txns only (large ones are virtual items)
     const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE);
@@ -465,8 +512,21 @@ static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
         }
     }
     if (!FILL) {
+        constexpr int NCB = ncb_of(NC);
+        uint32_t w[NCB / 4];
 #pragma unroll
-        for (int k = 0; k < NC; ++k) a.cnt[pb + k] = c[k];
+        for (int q = 0; q < NCB / 4; ++q) w[q] = 0;
+        bool over = false;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            w[k >> 2] |= (c[k] < 255u ? c[k] : 255u) << (8 * (k & 3));
+            if (c[k] >= 255u) a.cntx[pb + k] = c[k];
+            over |= c[k] > (uint32_t)WALK_INL;
+        }
+        uint32_t* d = reinterpret_cast<uint32_t*>(a.cnt8 + p * NCB);
+#pragma unroll
+        for (int q = 0; q < NCB / 4; ++q) d[q] = w[q];
+        if (over) a.dfr[i] = 1;
     }
 }
 
@@ -504,13 +564,19 @@ struct TxnArgs {
     const uint32_t* key_off;
     const uint64_t* keys;
     const uint8_t* meta;
-    const uint32_t* cnt;          // AoS by pair [p * nvc + vc]
+    const uint8_t* cnt8;          // AoS by pair [p * ncb + vc] (pair_count)
+    const uint32_t* cntx;
     uint32_t* nk;                 // [vc * n + t]
     uint32_t* ne;                 // [vc * n + t]
     const uint32_t* out_key_off[NVC_MAX];
     const uint32_t* out_k2t_off[NVC_MAX];
+    const uint32_t* out_ent_off[NVC_MAX];
     uint64_t* out_keys[NVC_MAX];
     int32_t* out_k2t[NVC_MAX];
+    uint32_t* out_txns[NVC_MAX];
+    uint32_t* out_tcnt[NVC_MAX];
+    const uint32_t* inl;          // the count walk's inline ids [(p * nvc + vc) * WALK_INL + q], descending
+    const uint8_t* dfr;           // [txn] deferred to the fill walk + k_txn_union
     uint32_t* dst;                // AoS by pair [p * nvc + vc]
     Params* prm;
     // large txns (virtual items, in (txn, key) order): items [voff[t], voff[t+1])
@@ -520,30 +586,6 @@ struct TxnArgs {
     const uint32_t* vi_u;         // item -> distinct-key index (its key = ukey[u])
     const uint64_t* ukey;
 };
-
-// Per txn: keys in ascending order (Keys are sorted), KeyDeps header offsets, per-item first-entry slot.
-static __global__ __launch_bounds__(256) void k_txn_layout(TxnArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    if (a.meta[t] & META_LARGE) return;            // k_large_layout
-    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
-    for (int vc = 0; vc < a.nvc; ++vc) {
-        const uint32_t kb = a.out_key_off[vc][t];
-        const uint32_t nk = a.out_key_off[vc][t + 1] - kb;
-        if (nk == 0) continue;
-        const uint32_t mb = a.out_k2t_off[vc][t];
-        uint32_t run = nk, kk = 0;
-        for (uint32_t x = b; x < e; ++x) {
-            const uint32_t c = a.cnt[(size_t)x * a.nvc + vc];
-            if (c == 0) continue;
-            a.out_keys[vc][kb + kk] = a.keys[x];
-            a.dst[(size_t)x * a.nvc + vc] = mb + run + c - 1;      // the fill walk emits descending from here
-            run += c;
-            a.out_k2t[vc][mb + kk] = (int32_t)run;
-            ++kk;
-        }
-    }
-}
 
 // Large txns (virtual items: range-domain txns, >16-key txns), one wave per txn: per-CSR key and entry
 // totals (k_large_sums, read by OffsetsOp's load) and the layout (k_large_layout, after the CSRs are
@@ -624,20 +666,13 @@ struct OffsetsOp {
     size_t n;
     const uint8_t* meta;
     const uint32_t* key_off;
-    const uint32_t* cnt;          // AoS by pair
+    const uint8_t* cnt8;          // AoS by pair, one byte per class (pair_counts)
+    const uint32_t* cntx;
     uint32_t* o_key_off[NVC];
     uint32_t* o_ent_off[NVC];
     uint32_t* o_k2t_off[NVC];
-    // fused per-txn layout (k_txn_layout's work) into output buffers allocated by an earlier batch:
-    // written only where the txn's rows fit the current capacities, else *overflow is raised and the
-    // caller runs k_txn_layout after sizing the buffers (layout == 0: offsets only)
-    int layout;
-    const uint64_t* keys;
-    uint64_t* out_keys[NVC];
-    int32_t* out_k2t[NVC];
-    uint32_t cap_keys[NVC], cap_k2t[NVC];
-    uint32_t* dst;                // AoS by pair: last k2t slot of the pair's run
-    uint32_t* overflow;
+    uint8_t* dfr;                 // [txn] deferred to the fill walk + union (set by the walk, or here)
+    uint32_t* any_dfr;            // some deferred txn has entries
     const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
     const uint32_t* lsum_e;
     uint32_t* heavy;              // set when some txn's CSRs total more than MERGE_HEAVY keys + entries
@@ -648,17 +683,6 @@ struct OffsetsOp {
         for (int c = 0; c < NVC; ++c) { s.k[c] = 0; s.e[c] = 0; }
         return s;
     }
-    // the NVC count words of pair x (dwordx2 loads when the pair's words are 8-byte aligned: NVC even)
-    __device__ void load_counts(uint32_t x, uint32_t* v) const {
-        if (NVC % 2 == 0) {
-            const uint2* p = reinterpret_cast<const uint2*>(cnt + (size_t)x * NVC);
-#pragma unroll
-            for (int c2 = 0; c2 < NVC / 2; ++c2) { const uint2 w = p[c2]; v[2 * c2] = w.x; v[2 * c2 + 1] = w.y; }
-        } else {
-#pragma unroll
-            for (int c = 0; c < NVC; ++c) v[c] = cnt[(size_t)x * NVC + c];
-        }
-    }
     __device__ S load(size_t t) const {
         S s = identity();
         const bool large = meta[t] & META_LARGE;
@@ -668,10 +692,10 @@ struct OffsetsOp {
             return s;
         }
         const uint32_t b = key_off[t], e = key_off[t + 1];
-        // a pair's NVC counts are contiguous
+        // a pair's NVC counts are contiguous bytes (one dword per pair for NVC <= 4)
         for (uint32_t x = b; x < e; ++x) {
             uint32_t v[NVC];
-            load_counts(x, v);
+            pair_counts<NVC>(cnt8, cntx, x, v);
 #pragma unroll
             for (int c = 0; c < NVC; ++c) { s.k[c] += v[c] > 0 ? 1u : 0u; s.e[c] += v[c]; }
         }
@@ -684,9 +708,9 @@ struct OffsetsOp {
         return r;
     }
     __device__ void store(size_t t, const S& ex, const S& inc, const S& el) const {
-        uint32_t w = 0;
+        uint32_t w = 0, ents = 0;
 #pragma unroll
-        for (int c = 0; c < NVC; ++c) w += el.k[c] + el.e[c];
+        for (int c = 0; c < NVC; ++c) { w += el.k[c] + el.e[c]; ents += el.e[c]; }
         if (w > MERGE_HEAVY_HINT && *(volatile uint32_t*)heavy == 0u) *(volatile uint32_t*)heavy = 1u;
 #pragma unroll
         for (int c = 0; c < NVC; ++c) {
@@ -699,68 +723,135 @@ struct OffsetsOp {
                 o_k2t_off[c][n] = inc.k[c] + inc.e[c];
             }
         }
-        if (!layout) return;
-        if (meta[t] & META_LARGE) return;     // k_large_layout
-        const uint32_t b = key_off[t], e = key_off[t + 1];
-        const uint32_t* src = cnt;
-        uint32_t* d = dst;
-        if (e - b <= 4) {                 // the counts of up to 4 pairs in registers (dwordx2 loads), one pass
-            uint32_t cv[4][NVC];
+        // small txns k_txn_finish cannot finish from the inline ids: a pair overflowed them (the walk set
+        // dfr), or more than 4 keys carry entries
+        if (meta[t] & META_LARGE) return;
+        bool d = dfr[t] != 0;
+        if (!d && ents > 0 && key_off[t + 1] - key_off[t] > 4) { dfr[t] = 1; d = true; }
+        if (d && *(volatile uint32_t*)any_dfr == 0u) *(volatile uint32_t*)any_dfr = 1u;
+    }
+};
+
+// Sorts 16 keys ascending in registers (bitonic network, compile-time indices only).
+__device__ inline void sort16(uint64_t* v) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (b + j < e) load_counts(b + j, cv[j]);
-                else {
+    for (int k = 2; k <= 16; k <<= 1) {
 #pragma unroll
-                    for (int c = 0; c < NVC; ++c) cv[j][c] = 0u;
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = v[i], y = v[l];
+                    const bool up = (i & k) == 0;
+                    const bool sw = up ? x > y : x < y;
+                    v[i] = sw ? y : x;
+                    v[l] = sw ? x : y;
                 }
-            }
-            uint64_t kx[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) kx[j] = b + j < e ? keys[b + j] : 0ull;
-#pragma unroll
-            for (int c = 0; c < NVC; ++c) {
-                const uint32_t nk = el.k[c];
-                if (nk == 0) continue;
-                const uint32_t kb = ex.k[c], mb = ex.k[c] + ex.e[c];
-                if (kb + nk > cap_keys[c] || mb + nk + el.e[c] > cap_k2t[c]) {
-                    if (*(volatile uint32_t*)overflow == 0u) *(volatile uint32_t*)overflow = 1u;
-                    continue;
-                }
-                uint32_t run = nk, kk = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t cc = cv[j][c];
-                    if (cc == 0) continue;
-                    out_keys[c][kb + kk] = kx[j];
-                    d[(size_t)(b + j) * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
-                    run += cc;
-                    out_k2t[c][mb + kk] = (int32_t)run;
-                    ++kk;
-                }
-            }
-            return;
-        }
-        for (int c = 0; c < NVC; ++c) {
-            const uint32_t nk = el.k[c];
-            if (nk == 0) continue;
-            const uint32_t kb = ex.k[c], mb = ex.k[c] + ex.e[c];
-            if (kb + nk > cap_keys[c] || mb + nk + el.e[c] > cap_k2t[c]) {
-                if (*(volatile uint32_t*)overflow == 0u) *(volatile uint32_t*)overflow = 1u;
-                continue;
-            }
-            uint32_t run = nk, kk = 0;
-            for (uint32_t x = b; x < e; ++x) {
-                const uint32_t cc = src[(size_t)x * NVC + c];
-                if (cc == 0) continue;
-                out_keys[c][kb + kk] = keys[x];
-                d[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
-                run += cc;
-                out_k2t[c][mb + kk] = (int32_t)run;
-                ++kk;
             }
         }
     }
-};
+}
+
+// Per small txn, after the CSRs are sized: the KeyDeps layout of every computed class (keys in ascending order,
+// keysToTxnIds header), then, unless the txn is deferred, the per-key lists from the count walk's inline ids
+// (emitted descending, laid out ascending) and the TxnId union with every entry remapped to its index
+// (RelationMultiMap.AbstractBuilder's finishKey/build, utils/RelationMultiMap.java:201-260) -- the fill walk and
+// k_txn_union then run only for the deferred txns (dst: their pairs' last k2t slots).  One thread per txn;
+// the classes in a runtime loop, the <= 4 pairs and <= WALK_INL ids per pair at compile-time indices, so the
+// union of up to 16 (TxnId, slot) pairs is one register sorting network.
+template <int NVC>
+static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    if (a.meta[t] & META_LARGE) return;            // k_large_layout
+    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
+    const bool defer = a.dfr[t] != 0;
+    constexpr int NCB = ncb_of(NVC);
+    if (e - b > 4) {                                // deferred whenever it has entries (OffsetsOp::store)
+#pragma unroll 1
+        for (int c = 0; c < NVC; ++c) {
+            const uint32_t kb = a.out_key_off[c][t], nk = a.out_key_off[c][t + 1] - kb;
+            if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; continue; }
+            const uint32_t mb = a.out_k2t_off[c][t];
+            uint32_t run = nk, kk = 0;
+            for (uint32_t x = b; x < e; ++x) {
+                const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, x, c);
+                if (cc == 0) continue;
+                a.out_keys[c][kb + kk] = a.keys[x];
+                a.dst[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
+                run += cc;
+                a.out_k2t[c][mb + kk] = (int32_t)run;
+                ++kk;
+            }
+        }
+        return;
+    }
+    uint64_t kx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kx[j] = b + j < e ? a.keys[b + j] : 0ull;
+#pragma unroll 1
+    for (int c = 0; c < NVC; ++c) {
+        const uint32_t kb = a.out_key_off[c][t], nk = a.out_key_off[c][t + 1] - kb;
+        if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; continue; }
+        const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
+        uint32_t cc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cc[j] = b + j < e ? pair_count(a.cnt8, a.cntx, NCB, NVC, b + j, c) : 0u;
+        uint32_t run = nk, kk = 0, rb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            rb[j] = run;
+            if (cc[j] == 0) continue;
+            a.out_keys[c][kb + kk] = kx[j];
+            if (defer) a.dst[(size_t)(b + j) * NVC + c] = mb + run + cc[j] - 1;
+            run += cc[j];
+            a.out_k2t[c][mb + kk] = (int32_t)run;
+            ++kk;
+        }
+        if (defer) continue;
+        int32_t* k2t = a.out_k2t[c];
+        uint32_t* tx = a.out_txns[c] + ob;
+        if (nk == 1) {                              // one key: its list is the union, indices 0..cc-1
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (cc[j] == 0) continue;
+                const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
+#pragma unroll
+                for (int q = 0; q < WALK_INL; ++q) {
+                    if ((uint32_t)q < cc[j]) {
+                        const uint32_t pos = cc[j] - 1 - (uint32_t)q;
+                        tx[pos] = src[q];
+                        k2t[mb + rb[j] + pos] = (int32_t)pos;
+                    }
+                }
+                a.out_tcnt[c][t] = cc[j];
+            }
+            continue;
+        }
+        // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index
+        uint64_t v[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
+#pragma unroll
+            for (int q = 0; q < WALK_INL; ++q)
+                v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)src[q] << 32) | (uint64_t)(mb + rb[j] + cc[j] - 1 - (uint32_t)q) : ~0ull;
+        }
+        sort16(v);
+        uint32_t u = 0, prev = 0xFFFFFFFFu;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (v[r] != ~0ull) {
+                const uint32_t id = (uint32_t)(v[r] >> 32);
+                if (id != prev) { tx[u++] = id; prev = id; }
+                k2t[(uint32_t)v[r]] = (int32_t)(u - 1);
+            }
+        }
+        a.out_tcnt[c][t] = u;
+    }
+}
+static_assert(WALK_INL == 4, "k_txn_finish's sorting network holds 4 pairs x 4 ids");
 
 // Union of up to KMAX sorted lists living in k2t[lo[k] .. hi[k]) -> out (unique, ascending); then
 // every entry is rewritten as its index in out.  Returns |out|.
@@ -827,6 +918,7 @@ struct UnionArgs {
     int32_t* k2t[NVC_MAX];
     uint32_t* txns[NVC_MAX];
     uint32_t* tcnt[NVC_MAX];
+    const uint8_t* dfr;           // nullable: every small txn; else only the deferred ones
 };
 
 // Small txns: register K-way merge of the per-key lists (large txns: k_union_lds).
@@ -835,6 +927,7 @@ static __global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
     if (a.meta[t] & META_LARGE) return;
+    if (a.dfr && !a.dfr[t]) return;          // finished by the offsets scan
     // every CSR's key range up front: the loads issue together instead of behind each CSR's stores
     uint32_t kb[NVC], ke[NVC];
 #pragma unroll

@@ -2,33 +2,30 @@
 // sums and layout, TxnId unions), one instantiation per class count; compiled in parallel with deps.hip.
 #include "engine_internal.h"
 
-// Offsets of every computed key-class CSR in one scan; with buffers left by an earlier batch, also the
-// per-txn layout (fused; *overflow reports rows that did not fit, then k_txn_layout runs after sizing).
-// Computed class k is CSR cls[k] (every class, or the keyDeps class of each view when the batch has no
-// directKeyDeps).
+// Offsets of every computed key-class CSR in one scan (OffsetsOp: one count dword per pair for <= 4 classes);
+// the scan also marks the small txns k_txn_finish cannot finish from the walk's inline ids.  Computed class k
+// is CSR cls[k] (every class, or the keyDeps class of each view when the batch has no directKeyDeps).
 template <int NC>
-void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* overflow) {
+void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* heavy) {
     OffsetsOp<NC> op{};
-    op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt = h->cnt;
-    op.layout = 1;
-    op.keys = h->keys; op.dst = h->dst; op.overflow = overflow;
-    op.lsum_k = h->nk; op.lsum_e = h->ne; op.heavy = overflow - 1;
+    op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt8 = h->cnt8; op.cntx = h->cntx;
+    op.dfr = h->dfr; op.any_dfr = heavy - 1;
+    op.lsum_k = h->nk; op.lsum_e = h->ne; op.heavy = heavy;
     for (int k = 0; k < NC; ++k) {
         const int c = cls[k];
         op.o_key_off[k] = h->deps[c].key_off; op.o_ent_off[k] = h->deps[c].ent_off; op.o_k2t_off[k] = h->deps[c].k2t_off;
-        const size_t base = S_CSR0 + 10 * (size_t)c;
-        const size_t ck = csr_cap(h, c, 4, 8), cm = csr_cap(h, c, 5, 4);
-        op.out_keys[k] = ck ? (uint64_t*)h->bufs[base + 4].p : nullptr;
-        op.out_k2t[k] = cm ? (int32_t*)h->bufs[base + 5].p : nullptr;
-        op.cap_keys[k] = (uint32_t)std::min<size_t>(ck, 0xFFFFFFFFu);
-        op.cap_k2t[k] = (uint32_t)std::min<size_t>(cm, 0xFFFFFFFFu);
     }
     scan_any(h, op, h->n);
 }
 template <int NV>
-void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* overflow) {
-    if (direct) launch_offsets_nc<2 * NV>(h, cls, overflow);
-    else launch_offsets_nc<NV>(h, cls, overflow);
+void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy) {
+    if (direct) launch_offsets_nc<2 * NV>(h, cls, heavy);
+    else launch_offsets_nc<NV>(h, cls, heavy);
+}
+template <int NV>
+void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
+    if (direct) k_txn_finish<2 * NV><<<ceil_div((long)ta.n, 256), 256, 0, st>>>(ta);
+    else k_txn_finish<NV><<<ceil_div((long)ta.n, 256), 256, 0, st>>>(ta);
 }
 
 template <int NV>
@@ -50,9 +47,10 @@ void launch_union(const UnionArgs& ua, bool direct, hipStream_t st) {
     else k_txn_union<NV><<<ceil_div((long)ua.n, 256), 256, 0, st>>>(ua);
 }
 
-void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* overflow) {
-    NV_DISPATCH(nv, launch_offsets, h, direct, cls, overflow);
+void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy) {
+    NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy);
 }
+void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_finish, ta, direct, st); }
 void launch_large_sums_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_large_sums, ta, direct, st); }
 void launch_large_layout_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_large_layout, ta, direct, st); }
 void launch_union_nv(int nv, const UnionArgs& ua, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_union, ua, direct, st); }

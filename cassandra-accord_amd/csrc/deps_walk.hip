@@ -4,8 +4,8 @@
 #include "engine_internal.h"
 
 template <int NV, bool DIRECT>
-void launch_walk_d(const WalkArgs& a, bool fill, hipStream_t st) {
-    if (a.P > 0) {
+void launch_walk_d(const WalkArgs& a, bool fill, bool pairs, hipStream_t st) {
+    if (a.P > 0 && pairs) {
         const int g = ceil_div((long)a.P, 256);
         KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT, a.P);
         if (fill) k_deps_walk<NV, true, DIRECT><<<g, 256, 0, st>>>(a);
@@ -19,9 +19,9 @@ void launch_walk_d(const WalkArgs& a, bool fill, hipStream_t st) {
     }
 }
 template <int NV>
-void launch_walk(const WalkArgs& a, bool fill, bool direct, hipStream_t st) {
-    if (direct) launch_walk_d<NV, true>(a, fill, st);
-    else launch_walk_d<NV, false>(a, fill, st);
+void launch_walk(const WalkArgs& a, bool fill, bool direct, bool pairs, hipStream_t st) {
+    if (direct) launch_walk_d<NV, true>(a, fill, pairs, st);
+    else launch_walk_d<NV, false>(a, fill, pairs, st);
 }
 template <int NV>
 void launch_range(const RangeArgs& a, bool fill, hipStream_t st) {
@@ -30,8 +30,8 @@ void launch_range(const RangeArgs& a, bool fill, hipStream_t st) {
     if (fill) k_range_deps<NV, true><<<g, 256, 0, st>>>(a);
     else k_range_deps<NV, false><<<g, 256, 0, st>>>(a);
 }
-void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, hipStream_t st) {
-    NV_DISPATCH(nv, launch_walk, a, fill, direct, st);
+void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, bool pairs, hipStream_t st) {
+    NV_DISPATCH(nv, launch_walk, a, fill, direct, pairs, st);
 }
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st) {
     NV_DISPATCH(nv, launch_range, a, fill, st);

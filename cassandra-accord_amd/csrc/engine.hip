@@ -388,7 +388,9 @@ static int load_working(ad_handle* h) {
     CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
     CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
     CK(dalloc(h, S_UIDX, &h->nh, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
-    CK(dalloc(h, S_CNT, &h->cnt, (size_t)nvc * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
+    CK(dalloc(h, S_CNT, &h->cnt8, (size_t)ncb_of(nvc) * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
+    CK(dalloc(h, S_CNTX, &h->cntx, (size_t)nvc * P)); CK(dalloc(h, S_INL, &h->inl, (size_t)nvc * P * WALK_INL));
+    CK(dalloc(h, S_DFR, &h->dfr, n));
     CK(dalloc(h, S_NK, &h->nk, (size_t)nvc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nvc * n + n));
     CK(dalloc(h, S_VN, &h->vn, n)); CK(dalloc(h, S_VOFF, &h->voff, n + 1));
     CK(dalloc(h, S_LVL, &h->lvl, n + 1)); CK(dalloc(h, S_ORDER, &h->order, n + 1));

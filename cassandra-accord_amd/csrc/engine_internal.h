@@ -86,7 +86,9 @@ struct ad_handle {
     uint8_t* e_meta = nullptr;
     uint64_t *e_exec1 = nullptr, *pm_w = nullptr, *pm_c = nullptr;
     int32_t *seg_start = nullptr, *ud_prev = nullptr;
-    uint32_t *cnt = nullptr, *dst = nullptr, *nk = nullptr, *ne = nullptr;
+    uint8_t *cnt8 = nullptr, *dfr = nullptr;             // per (pair, class) byte counts; per txn deferred flag
+    uint32_t *cntx = nullptr, *inl = nullptr;            // saturated counts; the walk's inline ids
+    uint32_t *dst = nullptr, *nk = nullptr, *ne = nullptr;
     // virtual items (large txns)
     size_t V = 0;
     uint32_t *vn = nullptr, *voff = nullptr, *vi_txn = nullptr, *vi_pos = nullptr, *vi_u = nullptr;
@@ -247,6 +249,7 @@ enum Slot : size_t {
     S_RIDX = S_RCEND, S_NONEROWS, S_LROWS, S_UMEDC, S_UMED,
     S_GLCT, S_GLCM, S_GLCE, S_GLCP, S_GLLW, S_GLEC, S_GLEO, S_GLXC, S_GLXO, S_GLCONS, S_GLE, S_GLIN,
     S_GLSRC, S_GLDST, S_GLSRC2, S_GLDST2, S_GLDEG, S_GLREM, S_GLXOFF, S_GLFL, S_GLFRONT, S_GLKEY, S_CFKU,
+    S_CNTX, S_INL, S_DFR,
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 192
@@ -339,10 +342,11 @@ int csr_sizes(ad_handle* h, const Csr& c, ad_csr_sizes* s);
 int fetch_rows(ad_handle* h, const Csr& c, int kw, size_t lo, size_t hi, ad_csr_sizes* s, ad_csr_out* out);
 int fetch_empty(ad_handle* h, ad_csr_out* out);
 // deps_walk.hip: count / fill walks of the key entries and virtual items, and the RangeDeps join
-void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, hipStream_t st);
+void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, bool pairs, hipStream_t st);
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st);
 // deps_layout.hip: per-txn offsets / layout / unions of the computed key classes
-void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* overflow);
+void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy);
+void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_large_sums_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_large_layout_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_union_nv(int nv, const UnionArgs& ua, bool direct, hipStream_t st);

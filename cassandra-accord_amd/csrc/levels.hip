@@ -178,7 +178,7 @@ int levels_solve_edges(ad_handle* h, const uint64_t* d_edges, size_t m, size_t N
     CK(ensure_scratch(h, std::max(h->scratch_cap, (size_t)(3 * (radix_hist_len(m1) + 128) + 64 * 1024) * 4)));
     HIPCHK(h, hipMemsetAsync(indeg, 0, N1 * 4, st));
     HIPCHK(h, hipMemsetAsync(L, 0, (N + 1) * 4, st));
-    HIPCHK(h, hipMemsetAsync(fl, 0, 4 * 64 + 64, st));
+    HIPCHK(h, hipMemsetAsync(fl, 0, (4 * 64 + 64) * 4, st));
     uint32_t* bad = fl + 4 * 64;             // [0] bad edge; [1] always zero (the first wavefront's gate)
     if (m) k_edges_split<<<ceil_div((long)m, 256), 256, 0, st>>>(m, d_edges, src, dst, indeg, (uint32_t)N, bad);
     uint32_t hb = 0;

@@ -776,6 +776,8 @@ int ad_shard_order(ad_handle* h, uint32_t* level_out, uint32_t* order_out) {
     if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
     uint32_t *ord, *tmp;
     CK(dalloc(h, S_ORDER, &ord, std::max(n, H) + 1));
+    // the one-exchange path solves levels without a local level pass: the order's sort buffers are sized here
+    if (!ls_reserve_order(h->ls, H, st)) return set_err(h, AD_ERR_NOMEM, "ad_shard_order: out of device memory");
     CK(dalloc(h, S_MSCR, &tmp, 2 * H + 2));
     levels_order_rows(h, H, h->home_rows, ord);
     k_home_gid<<<ceil_div((long)H, 256), 256, 0, st>>>(H, ord, h->home_gid, tmp);           // order -> global ids

@@ -21,7 +21,7 @@ enum KernelId : int {
 inline const char* kernel_name(int k) {
     static const char* names[K_COUNT] = {
         "k_minmax", "k_pack", "k_radix_hist", "k_radix_scatter", "scan_radix", "k_gather_entries", "scan_elide",
-        "k_deps_walk<count>", "k_txn_counts", "scan_offsets", "k_txn_layout", "k_deps_walk<fill>", "k_txn_union",
+        "k_deps_walk<count>", "k_txn_counts", "scan_offsets", "k_txn_finish", "k_deps_walk<fill>", "k_txn_union",
         "k_merge<count>", "k_merge<write>", "chain_prep", "scan_chain", "order_sort", "k_range_deps", "vitems",
         "k_union_lds", "level_edges", "kahn_levels", "k_merge_heavy<count>", "k_merge_heavy<write>",
         "max_conflicts", "merge_offsets", "csr_offsets", "block_levels", "recover"};

@@ -1,7 +1,14 @@
-set -eo pipefail
-mkdir -p gpurun_out/r03d
+set -o pipefail
+D=gpurun_out/${TAG:-r03e}
+mkdir -p $D
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_stream.py tests/test_gpu_cfk_state.py tests/test_gpu_history.py tests/test_gpu_accept.py tests/test_gpu_parity.py tests/test_gpu_sharding.py > gpurun_out/r03d/tests.log 2>&1
-echo tests ok
-timeout -k 10 300 python3 -u bench.py --steps 10 --cpu-sample 0 --breakdown > gpurun_out/r03d/bench.json 2> gpurun_out/r03d/bench.err
+rc=0
+timeout -k 10 1000 python3 -u -m pytest --maxfail=15 -v --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests} > $D/tests.log 2>&1 || rc=$?
+echo "tests rc=$rc"
+# 1 = some tests failed (the GPU is fine); anything else (timeout, abort, fault) ends the call here
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || exit $?
+echo smoke ok
+timeout -k 10 300 python3 -u bench.py --steps 10 --cpu-sample 0 --breakdown > $D/bench.json 2> $D/bench.err || exit $?
 echo bench ok
+exit $rc

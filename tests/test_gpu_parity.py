@@ -76,7 +76,7 @@ def test_pull_levels_forced_abort(engine_factory, name, bump):
     if name == "C2":
         b = workload.config("C2", n=60000, seed=31)
     else:
-        b = workload.generate(30000, keys_per_txn=4, keyspace=20000 if name == "bumps" else 3000, slow_frac=0.3,
+        b = workload.generate(30000, keys_per_txn=4, keyspace=20000 if name == "bumps" else 8000, slow_frac=0.3,
                               bump_max=bump, seed=bump + 3)
     eng = engine_factory()
     check(engine_factory, b, fixpoint=4, eng=eng)
