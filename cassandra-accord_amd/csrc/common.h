@@ -114,4 +114,17 @@ __device__ inline void wave_set_flag(bool event, uint32_t* flag) {
     if (__ballot(event) && __lane_id() == 0 && *(volatile uint32_t*)flag == 0u) *(volatile uint32_t*)flag = 1u;
 }
 
+// Appends `v` for every lane with `event` to list[*count ...]: one atomic per wave (rare events: deferred txns,
+// overflowing pairs), slots in lane order.
+__device__ inline void wave_append(bool event, uint32_t v, uint32_t* list, uint32_t* count) {
+    const uint64_t m = __ballot(event);
+    if (!m) return;
+    const int lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (event) list[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
 }  // namespace ad

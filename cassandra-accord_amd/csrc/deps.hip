@@ -145,6 +145,15 @@ int stage_deps(ad_handle* h) {
     wa.gid = (h->sharded || h->hist_active) ? h->gid : nullptr;
     wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt8 = h->cnt8; wa.cntx = h->cntx; wa.inl = h->inl; wa.dfr = h->dfr; wa.dst = h->dst;
+    wa.key_off = h->key_off;
+    uint32_t* heavy = h->totd + MAX_TOTALS - 1;          // heavy-merge hint (read with the totals)
+    uint32_t* items_count = heavy - 1;                    // the fill walk's items (count walk)
+    uint32_t* dtx_count = heavy - 2;                      // deferred small txns (offsets scan)
+    uint32_t *items = nullptr, *dtx = nullptr;
+    CK(dalloc(h, S_OVI, &items, std::max<size_t>(P, 1)));
+    CK(dalloc(h, S_DTX, &dtx, std::max<size_t>(n, 1)));
+    wa.items_out = items; wa.items_count = items_count;
+    HIPCHK(h, hipMemsetAsync(dtx_count, 0, 12, st));     // [deferred txns, items, heavy-merge hint]
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
     wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
     wa.qpos = qpos; wa.ex1 = h->ex1; wa.bound_max = h->bound_max ? 1 : 0;
@@ -155,16 +164,13 @@ int stage_deps(ad_handle* h) {
     ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
-    uint32_t* heavy = h->totd + MAX_TOTALS - 1;          // heavy-merge hint (read with the totals)
-    uint32_t* any_dfr = heavy - 1;                        // some small txn deferred to the fill walk + union
     if (n > 0 && h->V > 0) {
         KScope ks(K_VITEMS);
         launch_large_sums_nv(nv, ta, direct, st);
     }
     if (n > 0) {
-        HIPCHK(h, hipMemsetAsync(any_dfr, 0, 8, st));          // [deferred, heavy-merge hint]
         KScope ks(K_SCAN_OFFSETS, n);
-        launch_offsets_nv(h, nv, direct, cls, heavy);
+        launch_offsets_nv(h, nv, direct, cls, heavy, dtx, dtx_count);
     } else {
         for (int k = 0; k < nc; ++k) csr_offsets(h, h->deps[cls[k]], h->nk, h->ne);
     }
@@ -193,14 +199,16 @@ int stage_deps(ad_handle* h) {
     }
     const int ncol = tt.count;
     tt.src[tt.count++] = heavy;
-    tt.src[tt.count++] = any_dfr;
+    tt.src[tt.count++] = items_count;
+    tt.src[tt.count++] = dtx_count;
     std::vector<uint32_t> got(tt.count, 0);
     CK(read_totals_params(h, tt, got.data()));
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
     // k_txn_finish completes every small txn whose pairs kept all their ids inline; only the deferred ones need
     // the fill walk and the union (none on most C2 batches)
-    const bool deferred = n > 0 && got[ncol + 1] != 0;
-    h->times.deps_path = deferred ? 2u : 1u;
+    const uint32_t nitems = n > 0 ? got[ncol + 1] : 0, ndtx = n > 0 ? got[ncol + 2] : 0;
+    h->times.deferred_txns = ndtx;
+    h->times.fill_items = nitems;
     h->merge_heavy = n == 0 || got[ncol] != 0 || h->n_large > 0 || Q > 0;
     CK(check_params(h));
     h->deps_entries = 0;
@@ -223,17 +231,17 @@ int stage_deps(ad_handle* h) {
     ta.inl = h->inl; ta.dfr = h->dfr;
     if (n > 0) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
-    wa.only_dfr = 1;
-    launch_walk_nv(nv, wa, true, direct, deferred, st);
+    wa.items = items; wa.nitems = nitems;
+    launch_walk_nv(nv, wa, true, direct, nitems > 0, st);
     if (Q > 0 && n > 0) launch_range_nv(nv, ra, true, st);
     UnionArgs ua{};
-    ua.n = n; ua.nvc = nc; ua.meta = h->meta; ua.dfr = h->dfr;
+    ua.n = n; ua.nvc = nc; ua.meta = h->meta; ua.rows = dtx; ua.nrows = ndtx;
     for (int vc = 0; vc < nc; ++vc) {
         Csr& c = h->deps[cls[vc]];
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    if (n > 0 && deferred) { KScope ks(K_TXN_UNION, n); launch_union_nv(nv, ua, direct, st); }
+    if (ndtx > 0) { KScope ks(K_TXN_UNION, ndtx); launch_union_nv(nv, ua, direct, st); }
     // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
         KScope ks(K_UNION_LDS);

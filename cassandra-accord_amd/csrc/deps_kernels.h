@@ -352,9 +352,13 @@ struct WalkArgs {
     uint8_t* cnt8;            // real pairs, AoS by pair: [p * NCB + k] count of class k, 255 = see cntx
     uint32_t* cntx;           // [p * NC + k] exact count where cnt8 saturated (>= 255)
     uint32_t* inl;            // [(p * NC + k) * WALK_INL + q]: the first WALK_INL ids the walk emits (descending)
-    uint8_t* dfr;             // [txn] 1: a pair of the txn emits more than WALK_INL ids in some class, or the offsets
-                              // scan could not finish the txn (fill walk + union needed); count walk / scan write it
-    int only_dfr;             // fill walk: only the entries of deferred txns (0: every entry)
+    uint8_t* dfr;             // [txn] 1: a pair of the txn emits more than WALK_INL ids in some class, or the txn has
+                              // more than 4 keys with entries (fill walk + k_txn_union); count walk / scan write it
+    const uint32_t* key_off;  // per txn (a txn with more than 4 keys: every pair with entries goes to the fill walk)
+    uint32_t* items_out;      // count walk: the sorted positions the fill walk visits, *items_count of them
+    uint32_t* items_count;
+    const uint32_t* items;    // fill walk: that list, nitems long
+    size_t nitems;
     const uint32_t* dst;      // real pairs, AoS by pair: absolute k2t slot of the last entry (fill)
     int32_t* k2t[NVC_MAX];    // per-vc keysToTxnIds (fill)
     // virtual items (large txns): item x queries key segment u = vi_u[x] ([useg[u], ...)) before position vi_pos[x]
@@ -471,13 +475,12 @@ template <int NV, bool FILL, bool DIRECT>
 static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     constexpr int NC = DIRECT ? 2 * NV : NV;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= (a.qpos ? a.P : a.P - a.prm->n_keys_u)) return;
-    const size_t s = a.qpos ? x : (size_t)a.nh[x];
+    if (x >= (FILL ? a.nitems : (a.qpos ? a.P : a.P - a.prm->n_keys_u))) return;
+    const size_t s = FILL ? (size_t)a.items[x] : (a.qpos ? x : (size_t)a.nh[x]);
     const int seg0 = a.seg_start[s];
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
     const uint32_t qk = meta_kind(mi);
-    if (FILL && a.only_dfr && !a.dfr[i]) return;      // finished by the offsets scan from the inline ids
     // the pair's counts / slots live AoS by pair index (the per-txn kernels read them contiguously)
     const size_t p = a.sval[s];
     const size_t pb = p * NC;
@@ -527,6 +530,13 @@ static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
 #pragma unroll
         for (int q = 0; q < NCB / 4; ++q) d[q] = w[q];
         if (over) a.dfr[i] = 1;
+        // the fill walk's items: pairs that overflowed their inline ids, and every pair with entries of a txn
+        // with more than 4 keys (k_txn_finish lays those out from dst)
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) any |= c[k] > 0;
+        const bool wide = query && a.key_off[i + 1] - a.key_off[i] > 4u;
+        wave_append(over || (wide && any), (uint32_t)s, a.items_out, a.items_count);
     }
 }
 
@@ -672,7 +682,8 @@ struct OffsetsOp {
     uint32_t* o_ent_off[NVC];
     uint32_t* o_k2t_off[NVC];
     uint8_t* dfr;                 // [txn] deferred to the fill walk + union (set by the walk, or here)
-    uint32_t* any_dfr;            // some deferred txn has entries
+    uint32_t* dtx;                // the deferred txns (k_txn_union's list), *dtx_count of them
+    uint32_t* dtx_count;
     const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
     const uint32_t* lsum_e;
     uint32_t* heavy;              // set when some txn's CSRs total more than MERGE_HEAVY keys + entries
@@ -725,10 +736,12 @@ struct OffsetsOp {
         }
         // small txns k_txn_finish cannot finish from the inline ids: a pair overflowed them (the walk set
         // dfr), or more than 4 keys carry entries
-        if (meta[t] & META_LARGE) return;
-        bool d = dfr[t] != 0;
-        if (!d && ents > 0 && key_off[t + 1] - key_off[t] > 4) { dfr[t] = 1; d = true; }
-        if (d && *(volatile uint32_t*)any_dfr == 0u) *(volatile uint32_t*)any_dfr = 1u;
+        bool d = false;
+        if (!(meta[t] & META_LARGE)) {
+            d = dfr[t] != 0;
+            if (!d && ents > 0 && key_off[t + 1] - key_off[t] > 4) { dfr[t] = 1; d = true; }
+        }
+        wave_append(d, (uint32_t)t, dtx, dtx_count);      // k_txn_union's rows
     }
 };
 
@@ -753,103 +766,126 @@ __device__ inline void sort16(uint64_t* v) {
     }
 }
 
-// Per small txn, after the CSRs are sized: the KeyDeps layout of every computed class (keys in ascending order,
-// keysToTxnIds header), then, unless the txn is deferred, the per-key lists from the count walk's inline ids
-// (emitted descending, laid out ascending) and the TxnId union with every entry remapped to its index
-// (RelationMultiMap.AbstractBuilder's finishKey/build, utils/RelationMultiMap.java:201-260) -- the fill walk and
-// k_txn_union then run only for the deferred txns (dst: their pairs' last k2t slots).  One thread per txn;
-// the classes in a runtime loop, the <= 4 pairs and <= WALK_INL ids per pair at compile-time indices, so the
-// union of up to 16 (TxnId, slot) pairs is one register sorting network.
+// Per (small txn, class), after the CSRs are sized: the KeyDeps layout (keys in ascending order, keysToTxnIds
+// header); the per-key lists from the count walk's inline ids (emitted descending, laid out ascending); and,
+// unless the txn is deferred, the TxnId union with every entry remapped to its index (RelationMultiMap.
+// AbstractBuilder's finishKey/build, utils/RelationMultiMap.java:201-260).  A pair the count walk put on its
+// item list (some class emitted more than WALK_INL ids, or the txn has more than 4 keys) gets its last k2t slot
+// in dst instead, for walk<fill> over that list; deferred txns are then unioned by k_txn_union over the scan's
+// txn list.  Grid (txns, classes): every load of a thread is issued before its first store (offsets, counts,
+// keys, then the inline ids), so a thread waits for three memory round trips; the <= 4 pairs x WALK_INL ids are
+// at compile-time indices and the union of up to 16 (TxnId, slot) pairs is one register sorting network.
 template <int NVC>
 static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
     if (t >= a.n) return;
-    if (a.meta[t] & META_LARGE) return;            // k_large_layout
+    const uint32_t kb = a.out_key_off[c][t], ke = a.out_key_off[c][t + 1];
     const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
+    const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
+    const bool large = (a.meta[t] & META_LARGE) != 0;
     const bool defer = a.dfr[t] != 0;
+    if (large) return;                              // k_large_layout
+    const uint32_t nk = ke - kb;
+    if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; return; }
     constexpr int NCB = ncb_of(NVC);
-    if (e - b > 4) {                                // deferred whenever it has entries (OffsetsOp::store)
-#pragma unroll 1
-        for (int c = 0; c < NVC; ++c) {
-            const uint32_t kb = a.out_key_off[c][t], nk = a.out_key_off[c][t + 1] - kb;
-            if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; continue; }
-            const uint32_t mb = a.out_k2t_off[c][t];
-            uint32_t run = nk, kk = 0;
-            for (uint32_t x = b; x < e; ++x) {
-                const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, x, c);
-                if (cc == 0) continue;
-                a.out_keys[c][kb + kk] = a.keys[x];
-                a.dst[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
-                run += cc;
-                a.out_k2t[c][mb + kk] = (int32_t)run;
-                ++kk;
-            }
+    int32_t* k2t = a.out_k2t[c];
+    if (e - b > 4) {                                // every pair with entries is on the walk's item list
+        uint32_t run = nk, kk = 0;
+        for (uint32_t x = b; x < e; ++x) {
+            const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, x, c);
+            if (cc == 0) continue;
+            a.out_keys[c][kb + kk] = a.keys[x];
+            a.dst[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
+            run += cc;
+            k2t[mb + kk] = (int32_t)run;
+            ++kk;
         }
         return;
     }
+    uint32_t cc[4];
+    bool walked[4];                                 // the pair is on the fill walk's list (some class overflowed)
     uint64_t kx[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) kx[j] = b + j < e ? a.keys[b + j] : 0ull;
-#pragma unroll 1
-    for (int c = 0; c < NVC; ++c) {
-        const uint32_t kb = a.out_key_off[c][t], nk = a.out_key_off[c][t + 1] - kb;
-        if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; continue; }
-        const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
-        uint32_t cc[4];
+    for (int j = 0; j < 4; ++j) {
+        uint32_t v[NVC];
+        if (b + j < e) pair_counts<NVC>(a.cnt8, a.cntx, b + j, v);
+        else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cc[j] = b + j < e ? pair_count(a.cnt8, a.cntx, NCB, NVC, b + j, c) : 0u;
-        uint32_t run = nk, kk = 0, rb[4];
+            for (int k = 0; k < NVC; ++k) v[k] = 0u;
+        }
+        bool w = false;
+#pragma unroll
+        for (int k = 0; k < NVC; ++k) w |= v[k] > (uint32_t)WALK_INL;
+        walked[j] = w;
+        cc[j] = v[0];
+#pragma unroll
+        for (int k = 1; k < NVC; ++k) cc[j] = k == c ? v[k] : cc[j];
+        kx[j] = b + j < e ? a.keys[b + j] : 0ull;
+    }
+    uint32_t id[4][WALK_INL];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
+#pragma unroll
+        for (int q = 0; q < WALK_INL; ++q) id[j][q] = (!walked[j] && (uint32_t)q < cc[j]) ? src[q] : 0u;
+    }
+    uint32_t run = nk, kk = 0, rb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        rb[j] = run;
+        if (cc[j] == 0) continue;
+        a.out_keys[c][kb + kk] = kx[j];
+        if (walked[j]) a.dst[(size_t)(b + j) * NVC + c] = mb + run + cc[j] - 1;
+        run += cc[j];
+        k2t[mb + kk] = (int32_t)run;
+        ++kk;
+    }
+    if (defer) {                                    // raw TxnIds of the inline lists; k_txn_union remaps
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            rb[j] = run;
-            if (cc[j] == 0) continue;
-            a.out_keys[c][kb + kk] = kx[j];
-            if (defer) a.dst[(size_t)(b + j) * NVC + c] = mb + run + cc[j] - 1;
-            run += cc[j];
-            a.out_k2t[c][mb + kk] = (int32_t)run;
-            ++kk;
-        }
-        if (defer) continue;
-        int32_t* k2t = a.out_k2t[c];
-        uint32_t* tx = a.out_txns[c] + ob;
-        if (nk == 1) {                              // one key: its list is the union, indices 0..cc-1
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (cc[j] == 0) continue;
-                const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
-#pragma unroll
-                for (int q = 0; q < WALK_INL; ++q) {
-                    if ((uint32_t)q < cc[j]) {
-                        const uint32_t pos = cc[j] - 1 - (uint32_t)q;
-                        tx[pos] = src[q];
-                        k2t[mb + rb[j] + pos] = (int32_t)pos;
-                    }
-                }
-                a.out_tcnt[c][t] = cc[j];
-            }
-            continue;
-        }
-        // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index
-        uint64_t v[16];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
+            if (walked[j]) continue;
 #pragma unroll
             for (int q = 0; q < WALK_INL; ++q)
-                v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)src[q] << 32) | (uint64_t)(mb + rb[j] + cc[j] - 1 - (uint32_t)q) : ~0ull;
+                if ((uint32_t)q < cc[j]) k2t[mb + rb[j] + cc[j] - 1 - (uint32_t)q] = (int32_t)id[j][q];
         }
-        sort16(v);
-        uint32_t u = 0, prev = 0xFFFFFFFFu;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (v[r] != ~0ull) {
-                const uint32_t id = (uint32_t)(v[r] >> 32);
-                if (id != prev) { tx[u++] = id; prev = id; }
-                k2t[(uint32_t)v[r]] = (int32_t)(u - 1);
-            }
-        }
-        a.out_tcnt[c][t] = u;
+        return;
     }
+    uint32_t* tx = a.out_txns[c] + ob;
+    if (nk == 1) {                                  // one key: its list is the union, indices 0..cc-1
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (cc[j] == 0) continue;
+#pragma unroll
+            for (int q = 0; q < WALK_INL; ++q) {
+                if ((uint32_t)q < cc[j]) {
+                    const uint32_t pos = cc[j] - 1 - (uint32_t)q;
+                    tx[pos] = id[j][q];
+                    k2t[mb + rb[j] + pos] = (int32_t)pos;
+                }
+            }
+            a.out_tcnt[c][t] = cc[j];
+        }
+        return;
+    }
+    // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index
+    uint64_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < WALK_INL; ++q)
+            v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)id[j][q] << 32) | (uint64_t)(mb + rb[j] + cc[j] - 1 - (uint32_t)q) : ~0ull;
+    sort16(v);
+    uint32_t u = 0, prev = 0xFFFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (v[r] != ~0ull) {
+            const uint32_t x = (uint32_t)(v[r] >> 32);
+            if (x != prev) { tx[u++] = x; prev = x; }
+            k2t[(uint32_t)v[r]] = (int32_t)(u - 1);
+        }
+    }
+    a.out_tcnt[c][t] = u;
 }
 static_assert(WALK_INL == 4, "k_txn_finish's sorting network holds 4 pairs x 4 ids");
 
@@ -918,16 +954,16 @@ struct UnionArgs {
     int32_t* k2t[NVC_MAX];
     uint32_t* txns[NVC_MAX];
     uint32_t* tcnt[NVC_MAX];
-    const uint8_t* dfr;           // nullable: every small txn; else only the deferred ones
+    const uint32_t* rows;         // the deferred txns (OffsetsOp's list), nrows of them
+    size_t nrows;
 };
 
 // Small txns: register K-way merge of the per-key lists (large txns: k_union_lds).
 template <int NVC>
 static __global__ __launch_bounds__(256) void k_txn_union(UnionArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    if (a.meta[t] & META_LARGE) return;
-    if (a.dfr && !a.dfr[t]) return;          // finished by the offsets scan
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= a.nrows) return;
+    const size_t t = a.rows[x];              // the other small txns were finished by k_txn_finish
     // every CSR's key range up front: the loads issue together instead of behind each CSR's stores
     uint32_t kb[NVC], ke[NVC];
 #pragma unroll

@@ -6,10 +6,10 @@
 // the scan also marks the small txns k_txn_finish cannot finish from the walk's inline ids.  Computed class k
 // is CSR cls[k] (every class, or the keyDeps class of each view when the batch has no directKeyDeps).
 template <int NC>
-void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* heavy) {
+void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count) {
     OffsetsOp<NC> op{};
     op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt8 = h->cnt8; op.cntx = h->cntx;
-    op.dfr = h->dfr; op.any_dfr = heavy - 1;
+    op.dfr = h->dfr; op.dtx = dtx; op.dtx_count = dtx_count;
     op.lsum_k = h->nk; op.lsum_e = h->ne; op.heavy = heavy;
     for (int k = 0; k < NC; ++k) {
         const int c = cls[k];
@@ -18,14 +18,15 @@ void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* heavy) {
     scan_any(h, op, h->n);
 }
 template <int NV>
-void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy) {
-    if (direct) launch_offsets_nc<2 * NV>(h, cls, heavy);
-    else launch_offsets_nc<NV>(h, cls, heavy);
+void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count) {
+    if (direct) launch_offsets_nc<2 * NV>(h, cls, heavy, dtx, dtx_count);
+    else launch_offsets_nc<NV>(h, cls, heavy, dtx, dtx_count);
 }
 template <int NV>
 void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
-    if (direct) k_txn_finish<2 * NV><<<ceil_div((long)ta.n, 256), 256, 0, st>>>(ta);
-    else k_txn_finish<NV><<<ceil_div((long)ta.n, 256), 256, 0, st>>>(ta);
+    const dim3 g((unsigned)ceil_div((long)ta.n, 256), direct ? 2 * NV : NV);
+    if (direct) k_txn_finish<2 * NV><<<g, 256, 0, st>>>(ta);
+    else k_txn_finish<NV><<<g, 256, 0, st>>>(ta);
 }
 
 template <int NV>
@@ -43,12 +44,12 @@ void launch_large_layout(const TxnArgs& ta, bool direct, hipStream_t st) {
 
 template <int NV>
 void launch_union(const UnionArgs& ua, bool direct, hipStream_t st) {
-    if (direct) k_txn_union<2 * NV><<<ceil_div((long)ua.n, 256), 256, 0, st>>>(ua);
-    else k_txn_union<NV><<<ceil_div((long)ua.n, 256), 256, 0, st>>>(ua);
+    if (direct) k_txn_union<2 * NV><<<ceil_div((long)ua.nrows, 256), 256, 0, st>>>(ua);
+    else k_txn_union<NV><<<ceil_div((long)ua.nrows, 256), 256, 0, st>>>(ua);
 }
 
-void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy) {
-    NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy);
+void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count) {
+    NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy, dtx, dtx_count);
 }
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_finish, ta, direct, st); }
 void launch_large_sums_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_large_sums, ta, direct, st); }

@@ -6,7 +6,7 @@
 template <int NV, bool DIRECT>
 void launch_walk_d(const WalkArgs& a, bool fill, bool pairs, hipStream_t st) {
     if (a.P > 0 && pairs) {
-        const int g = ceil_div((long)a.P, 256);
+        const int g = ceil_div((long)(fill ? a.nitems : a.P), 256);
         KScope ks(fill ? K_WALK_FILL : K_WALK_COUNT, a.P);
         if (fill) k_deps_walk<NV, true, DIRECT><<<g, 256, 0, st>>>(a);
         else k_deps_walk<NV, false, DIRECT><<<g, 256, 0, st>>>(a);

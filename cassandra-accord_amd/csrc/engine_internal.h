@@ -249,7 +249,7 @@ enum Slot : size_t {
     S_RIDX = S_RCEND, S_NONEROWS, S_LROWS, S_UMEDC, S_UMED,
     S_GLCT, S_GLCM, S_GLCE, S_GLCP, S_GLLW, S_GLEC, S_GLEO, S_GLXC, S_GLXO, S_GLCONS, S_GLE, S_GLIN,
     S_GLSRC, S_GLDST, S_GLSRC2, S_GLDST2, S_GLDEG, S_GLREM, S_GLXOFF, S_GLFL, S_GLFRONT, S_GLKEY, S_CFKU,
-    S_CNTX, S_INL, S_DFR,
+    S_CNTX, S_INL, S_DFR, S_OVI, S_DTX,
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 192
@@ -345,7 +345,7 @@ int fetch_empty(ad_handle* h, ad_csr_out* out);
 void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, bool pairs, hipStream_t st);
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st);
 // deps_layout.hip: per-txn offsets / layout / unions of the computed key classes
-void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy);
+void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count);
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_large_sums_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_large_layout_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);

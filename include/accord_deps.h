@@ -294,9 +294,10 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
                                     /* R when the batch has no directKeyDeps (no key sync points)   */
     uint32_t level_path;            /* the pull levels' outcome: 0 not tried, 1 pulled, 2 a far    */
                                     /* predecessor (> 65536 rows ahead) -> Kahn, 3 aborted -> Kahn   */
-    uint32_t deps_path;             /* 1: small txns finished by the offsets scan from the walk's     */
-                                    /* inline ids (fill walk + union only for deferred txns);        */
-                                    /* 2: layout after sizing (every txn through fill walk + union)   */
+    uint32_t deferred_txns;         /* small txns the walk's inline ids could not finish: unioned by  */
+                                    /* k_txn_union (the rest by k_txn_finish)                         */
+    uint32_t fill_items;            /* (txn, key) entries the fill walk re-walks (overflowed pairs,    */
+                                    /* pairs of txns with more than 4 keys)                           */
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
