@@ -6,6 +6,7 @@
 // lsb & 0x1E, node signed) whenever MB+HB+4+NB <= 64 (checked per batch; AD_ERR_UNSUPPORTED otherwise).
 // Equality of ts64 is Timestamp.equals (IDENTITY_LSB = hlc bits | 0x1E, Timestamp.java:41,244-249).
 #pragma once
+#include <initializer_list>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -112,6 +113,43 @@ inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 // a lane first reads the flag and only stores if it is still clear; every writer stores the same value.
 __device__ inline void wave_set_flag(bool event, uint32_t* flag) {
     if (__ballot(event) && __lane_id() == 0 && *(volatile uint32_t*)flag == 0u) *(volatile uint32_t*)flag = 1u;
+}
+
+// Several buffer fills in one launch (each hipMemsetAsync is a dispatch of its own: ~16 per C2 step cost
+// ~80 us of mostly launch time).  Segments are 4-byte aligned, their byte value replicated into words.
+constexpr int FILL_SEGS = 8;
+struct FillList {
+    uint32_t* p[FILL_SEGS];
+    uint64_t end[FILL_SEGS];     // inclusive prefix of the segments' word counts
+    uint32_t v[FILL_SEGS];
+    int n;
+};
+static __global__ __launch_bounds__(256) void k_fill_multi(FillList f) {
+    const uint64_t total = f.n ? f.end[f.n - 1] : 0;
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (uint64_t)gridDim.x * blockDim.x) {
+        int k = 0;
+#pragma unroll
+        for (int q = 0; q < FILL_SEGS - 1; ++q) k += (q < f.n - 1 && x >= f.end[q]) ? 1 : 0;
+        const uint64_t b = k ? f.end[k - 1] : 0;
+        f.p[k][x - b] = f.v[k];
+    }
+}
+
+// One launch for several fills (k_fill_multi): {pointer, bytes, byte value}; 4-byte aligned pointers and sizes
+// (else that segment falls back to hipMemsetAsync).
+struct FillSeg { void* p; size_t bytes; uint8_t v; };
+inline void fill_multi(hipStream_t st, std::initializer_list<FillSeg> segs) {
+    FillList f{};
+    uint64_t acc = 0;
+    for (const FillSeg& g : segs) {
+        if (!g.p || g.bytes == 0) continue;
+        if (((uintptr_t)g.p & 3) || (g.bytes & 3) || f.n == FILL_SEGS) { hipMemsetAsync(g.p, g.v, g.bytes, st); continue; }
+        acc += g.bytes / 4;
+        f.p[f.n] = (uint32_t*)g.p; f.end[f.n] = acc; f.v[f.n] = 0x01010101u * g.v; ++f.n;
+    }
+    if (!f.n) return;
+    const uint64_t blocks = (acc + 255) / 256 < 4096 ? (acc + 255) / 256 : 4096;
+    k_fill_multi<<<(unsigned)blocks, 256, 0, st>>>(f);
 }
 
 // Appends `v` for every lane with `event` to list[*count ...]: one atomic per wave (rare events: deferred txns,

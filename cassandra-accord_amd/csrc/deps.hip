@@ -83,6 +83,14 @@ static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64
     qpos[i] = (uint32_t)lo;
 }
 
+int side_stream(ad_handle* h) {
+    if (h->sst) return AD_OK;
+    HIPCHK(h, hipStreamCreateWithFlags(&h->sst, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    return AD_OK;
+}
+
 int stage_deps(ad_handle* h) {
     StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
@@ -153,12 +161,12 @@ int stage_deps(ad_handle* h) {
     CK(dalloc(h, S_OVI, &items, std::max<size_t>(P, 1)));
     CK(dalloc(h, S_DTX, &dtx, std::max<size_t>(n, 1)));
     wa.items_out = items; wa.items_count = items_count;
-    HIPCHK(h, hipMemsetAsync(dtx_count, 0, 12, st));     // [deferred txns, items, heavy-merge hint]
+
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
     wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
     wa.qpos = qpos; wa.ex1 = h->ex1; wa.bound_max = h->bound_max ? 1 : 0;
-    if (P > 0) HIPCHK(h, hipMemsetAsync(h->cnt8, 0, (size_t)ncb_of(nc) * P, st));   // segment heads keep zero counts
-    if (n > 0) HIPCHK(h, hipMemsetAsync(h->dfr, 0, n, st));
+    // [deferred txns, items, heavy-merge hint]; the pairs' counts (segment heads keep zero); deferred flags
+    fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
     launch_walk_nv(nv, wa, false, direct, true, st);
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
@@ -229,11 +237,6 @@ int stage_deps(ad_handle* h) {
     }
     // ---- fill
     ta.inl = h->inl; ta.dfr = h->dfr;
-    if (n > 0) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
-    if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
-    wa.items = items; wa.nitems = nitems;
-    launch_walk_nv(nv, wa, true, direct, nitems > 0, st);
-    if (Q > 0 && n > 0) launch_range_nv(nv, ra, true, st);
     UnionArgs ua{};
     ua.n = n; ua.nvc = nc; ua.meta = h->meta; ua.rows = dtx; ua.nrows = ndtx;
     for (int vc = 0; vc < nc; ++vc) {
@@ -241,7 +244,28 @@ int stage_deps(ad_handle* h) {
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    if (ndtx > 0) { KScope ks(K_TXN_UNION, ndtx); launch_union_nv(nv, ua, direct, st); }
+    // The deferred small txns (their layout, the fill walk of the listed pairs, their union: a chain of small
+    // latency-bound launches, ~30 us on C2 for 3 txns) run on a side stream, overlapping k_txn_finish over the
+    // others; joined at the end of the stage.
+    const bool side = ndtx > 0 || nitems > 0;
+    if (side) {
+        CK(side_stream(h));
+        HIPCHK(h, hipEventRecord(h->ev_fork, st));
+        HIPCHK(h, hipStreamWaitEvent(h->sst, h->ev_fork, 0));
+        TxnArgs td = ta;
+        td.rows = dtx; td.nrows = ndtx;
+        if (ndtx > 0) launch_finish_nv(nv, td, direct, h->sst);
+        WalkArgs wp = wa;
+        wp.V = 0; wp.items = items; wp.nitems = nitems;
+        if (nitems > 0) launch_walk_nv(nv, wp, true, direct, true, h->sst);
+        if (ndtx > 0) launch_union_nv(nv, ua, direct, h->sst);
+        HIPCHK(h, hipEventRecord(h->ev_join, h->sst));
+    }
+    ta.rows = nullptr; ta.nrows = n;
+    if (n > 0) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
+    if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
+    if (h->V > 0) launch_walk_nv(nv, wa, true, direct, false, st);           // the virtual items' fill walk
+    if (Q > 0 && n > 0) launch_range_nv(nv, ra, true, st);
     // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
         KScope ks(K_UNION_LDS);
@@ -288,6 +312,7 @@ int stage_deps(ad_handle* h) {
         }
         CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
     }
+    if (side) HIPCHK(h, hipStreamWaitEvent(st, h->ev_join, 0));
     // Virtual-item work arrays are dead once the CSRs are filled; they stay allocated for the next batch
     // (re-allocating C4's ~90 GB of them every batch cost more than the walks) unless the merge runs out of
     // HBM, when release_dead gives them back (STAGE_MERGE).

@@ -72,13 +72,6 @@ struct Params {                // device-side batch statistics (filled by k_minm
 enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
                   ERR_RANGEBITS = 32, ERR_CAP = 64 };
 
-static __global__ void k_params_init(Params* p) {
-    p->msb_min = ~0ull; p->msb_max = 0; p->hlc_min = ~0ull; p->hlc_max = 0;
-    p->key_min = ~0ull; p->key_max = 0; p->rs_min = ~0ull; p->re_max = 0; p->rw_max = 0;
-    p->node_min_b = ~0u; p->node_max_b = 0; p->max_keys = 0; p->err = 0;
-    p->n_large = 0; p->n_keys_u = 0; p->n_vitems = 0; p->n_special = 0; p->pad_ = 0;
-}
-
 __device__ inline unsigned long long wmin64(unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { unsigned long long u = __shfl_xor(v, o); v = u < v ? u : v; }
@@ -172,23 +165,25 @@ static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const uns
         const int k = threadIdx.x;
         unsigned long long v = k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
                                          : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
+        // the only writer of these fields (no separate initialisation launch)
         switch (k) {
-            case 0: atomicMin(&out->msb_min, ~v); break;
-            case 1: atomicMax(&out->msb_max, v); break;
-            case 2: atomicMin(&out->hlc_min, ~v); break;
-            case 3: atomicMax(&out->hlc_max, v); break;
-            case 4: atomicMin(&out->node_min_b, (unsigned)~v); break;
-            case 5: atomicMax(&out->node_max_b, (unsigned)v); break;
-            case 6: atomicMin(&out->key_min, ~v); break;
-            case 7: atomicMax(&out->key_max, v); break;
-            case 8: atomicMax(&out->max_keys, (unsigned)v); break;
-            case 9: atomicMin(&out->rs_min, ~v); break;
-            case 10: atomicMax(&out->re_max, v); break;
-            case 11: atomicMax(&out->rw_max, v); break;
-            case 12: if (v) atomicAdd(&out->n_large, (unsigned)v); break;
-            case 13: if (v) atomicAdd(&out->n_special, (unsigned)v); break;
+            case 0: out->msb_min = ~v; break;
+            case 1: out->msb_max = v; break;
+            case 2: out->hlc_min = ~v; break;
+            case 3: out->hlc_max = v; break;
+            case 4: out->node_min_b = (unsigned)~v; break;
+            case 5: out->node_max_b = (unsigned)v; break;
+            case 6: out->key_min = ~v; break;
+            case 7: out->key_max = v; break;
+            case 8: out->max_keys = (unsigned)v; break;
+            case 9: out->rs_min = ~v; break;
+            case 10: out->re_max = v; break;
+            case 11: out->rw_max = v; break;
+            case 12: out->n_large = (unsigned)v; break;
+            case 13: out->n_special = (unsigned)v; break;
         }
     }
+    if (threadIdx.x == 0) { out->err = 0; out->n_keys_u = 0; out->n_vitems = 0; out->pad_ = 0; }
 }
 
 // Packs timestamps, builds per-txn meta, the sort input and validates footprints.  One thread per txn.
@@ -587,6 +582,8 @@ struct TxnArgs {
     uint32_t* out_tcnt[NVC_MAX];
     const uint32_t* inl;          // the count walk's inline ids [(p * nvc + vc) * WALK_INL + q], descending
     const uint8_t* dfr;           // [txn] deferred to the fill walk + k_txn_union
+    const uint32_t* rows;         // k_txn_finish: nullable = every txn except the deferred ones; else these rows
+    size_t nrows;
     uint32_t* dst;                // AoS by pair [p * nvc + vc]
     Params* prm;
     // large txns (virtual items, in (txn, key) order): items [voff[t], voff[t+1])
@@ -777,9 +774,11 @@ __device__ inline void sort16(uint64_t* v) {
 // at compile-time indices and the union of up to 16 (TxnId, slot) pairs is one register sorting network.
 template <int NVC>
 static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int c = blockIdx.y;
-    if (t >= a.n) return;
+    if (x >= a.nrows) return;
+    const size_t t = a.rows ? a.rows[x] : x;      // rows: the deferred txns (side stream); else every txn
+    if (!a.rows && a.dfr[t]) return;
     const uint32_t kb = a.out_key_off[c][t], ke = a.out_key_off[c][t + 1];
     const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
     const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];

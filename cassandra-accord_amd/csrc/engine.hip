@@ -199,7 +199,6 @@ int check_params(ad_handle* h) {
 int stage_prepare(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     hipStream_t st = h->st;
-    k_params_init<<<1, 1, 0, st>>>(h->prm);
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
         KScope ks(K_MINMAX, n);
@@ -452,6 +451,9 @@ void ad_close(ad_handle* h) {
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->st) hipStreamSynchronize(h->st);
     if (h->cst) { hipStreamSynchronize(h->cst); hipStreamDestroy(h->cst); }
+    if (h->sst) { hipStreamSynchronize(h->sst); hipStreamDestroy(h->sst); }
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
+    if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->cev) hipEventDestroy(h->cev);
     if (h->sev) hipEventDestroy(h->sev);
     if (h->pub_host) hipHostFree(h->pub_host);
@@ -1131,7 +1133,7 @@ int ad_run_pipeline(ad_handle* h) {
     CK(stage_levels(h, true));
     HIPCHK(h, hipEventRecord(h->ev[5], st));
     HIPCHK(h, hipEventSynchronize(h->ev[5]));
-    if (h->order_pending && h->order_bad) {      // optimistic order failed its check: general path, timed in
+    if (order_failed(h)) {                       // optimistic order failed its check: general path, timed in
         CK(finish_order(h));
         HIPCHK(h, hipEventRecord(h->ev[5], st));
         HIPCHK(h, hipEventSynchronize(h->ev[5]));

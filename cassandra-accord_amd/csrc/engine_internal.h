@@ -46,6 +46,8 @@ struct ad_handle {
     int device = 0;
     ad_config cfg{};
     hipStream_t st = nullptr;
+    hipStream_t sst = nullptr;           // side stream (deps: deferred small txns), forked / joined by events
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     std::vector<DBuf> bufs;
     // loaded batch
@@ -61,8 +63,7 @@ struct ad_handle {
     Params hprm{};
     uint32_t* totd = nullptr;          // device: gathered CSR totals (read_totals_params)
     int level_mode = AD_LEVELS_AUTO;
-    bool order_pending = false;          // optimistic order issued; order_bad valid after a stream sync
-    uint32_t order_bad = 0;
+    bool order_pending = false;          // optimistic order issued; its check (pub_host[1]) valid after a stream sync
     // CSRs whose offsets are known to be all zero (an empty class: directKeyDeps without sync points,
     // RangeDeps without range txns), per CSR block: valid while the buffer, n and the allocation
     // generation are unchanged, so steady-state batches skip re-zeroing them
@@ -263,6 +264,7 @@ static_assert(CSR_SRANGE0 + MAXV <= CSR_BLOCKS_MAX, "zero-offset cache covers ev
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
 
+
 inline int bits_of(uint64_t x) { return x == 0 ? 0 : 64 - __builtin_clzll(x); }
 
 int ensure_scratch(ad_handle* h, size_t bytes);
@@ -328,9 +330,11 @@ int stage_prepare(ad_handle* h);
 int stage_sort(ad_handle* h);
 RadixScratch radix_scratch(ad_handle* h, size_t n);
 int stage_deps(ad_handle* h);
+int side_stream(ad_handle* h);
 int stage_merge(ad_handle* h);
 int stage_levels(ad_handle* h, bool want_order);
 int finish_order(ad_handle* h);
+bool order_failed(const ad_handle* h);
 // K unions computed together; out[k] = Deps.merge over in[k][0..np) per output txn (merge.hip)
 int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* out_block, const int* kw,
                 const Csr* const (*in)[MAXV], const int32_t* const (*rows)[MAXV], int np, uint64_t* entries);

@@ -943,23 +943,21 @@ static __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint3
     }
 }
 // max of the per-workgroup maxima (one workgroup); strips LV_FINAL from the levels afterwards
-static __global__ __launch_bounds__(1024) void k_level_pull_max(uint32_t nb, const uint32_t* __restrict__ bmax, uint32_t* out) {
-    __shared__ uint32_t wm[1024 / WAVE];
-    uint32_t m = 0;
-    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) m = bmax[i] > m ? bmax[i] : m;
-#pragma unroll
-    for (int o = WAVE / 2; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(m, o); m = y > m ? y : m; }
-    if (__lane_id() == 0) wm[threadIdx.x / WAVE] = m;
+// Clears the FINAL bits and folds the greatest level into *maxl: per block one check-then-atomicMax (the level
+// is reached by the first blocks, so later blocks mostly only read it; no contended atomic on one address).
+static __global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L, uint32_t* maxl) {
+    __shared__ uint32_t wm[256 / WAVE];
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t v = 0;
+    if (t < n) { v = L[t] & ~LV_FINAL; L[t] = v; }
+    v = wave_max(v);
+    if (__lane_id() == 0) wm[threadIdx.x / WAVE] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t x = 0;
-        for (int w = 0; w < 1024 / WAVE; ++w) x = wm[w] > x ? wm[w] : x;
-        *out = x;
+        uint32_t x = wm[0];
+        for (int w = 1; w < 256 / WAVE; ++w) x = wm[w] > x ? wm[w] : x;
+        if (x > *(volatile uint32_t*)maxl) atomicMax(maxl, x);
     }
-}
-static __global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n) L[t] &= ~LV_FINAL;
 }
 
 // Deep graphs (C3: the hot key's ~10^5 Writes make ~10^5 levels, a handful of txns each): one launch per
@@ -1275,7 +1273,8 @@ struct LevelInputs {
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
     int force_blocks;                    // pure key-chain batches: executeAt blocks even for short chains (tests)
-    uint32_t* order_verify;              // optimistic order: host word receiving the fast-path failure flag
+    uint32_t* order_verify;              // optimistic order: host-mapped word (device address) receiving the fast-path
+                                         // failure flag; null: the order syncs on its own check
     bool* order_pending;                 // set when the caller must check *order_verify after its sync
 };
 
@@ -1332,7 +1331,8 @@ static __global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uin
 }
 // flags[0] = max level, flags[1] |= 1 unless okey ascends and every slot is filled
 static __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ oidx,
-                                                    const uint32_t* __restrict__ olvl, uint32_t* __restrict__ flags) {
+                                                    const uint32_t* __restrict__ olvl, uint32_t* __restrict__ flags,
+                                                    uint32_t* fail_out) {
     uint32_t v = 0;
     bool bad = false;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
@@ -1351,6 +1351,7 @@ static __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint6
         for (int k = 1; k < 256 / WAVE; ++k) { mx = mx > red[k] ? mx : red[k]; b |= rb[k]; }
         atomicMax(&flags[0], mx);
         if (b) atomicOr(&flags[1], 1u);
+        if (b && fail_out) *(volatile uint32_t*)fail_out = 1u;    // host-mapped: read after the caller's sync
     }
 }
 // level of each txn in `perm` order (dst) + max level (fallback path).  Grid-stride over a bounded grid:
@@ -1378,11 +1379,12 @@ static __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, cons
 }
 
 // Returns true when the order was produced optimistically (known_maxl >= 0: the level count is known,
-// so no host sync is needed here): the fast path's verification flag is then copied to *verify_host and
-// the caller, after its own stream sync, reruns order_rows with known_maxl = -1 if it is set.
+// so no host sync is needed here): the fast path's verification failure is then stored by k_rank_check into
+// *verify_dev (a host-mapped word the caller zeroed; a device-to-pageable copy here would stall the stream for
+// a host round trip), and the caller, after its own stream sync, reruns order_rows with known_maxl = -1 if set.
 inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
                        uint32_t exec_bits, uint32_t* order_out, hipStream_t st, int known_maxl = -1,
-                       uint32_t* verify_host = nullptr) {
+                       uint32_t* verify_dev = nullptr) {
     KScope ks(K_ORDER, m);
     RadixScratch rs;
     const size_t hl = radix_hist_len(m);
@@ -1393,15 +1395,13 @@ inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     uint32_t *k = ls.sk0, *v = ls.sv0, *ko = ls.sk1, *vo = ls.sv1;
     uint32_t* of = ls.flags + 8;                              // [0] max level, [1] fast path failed
     const int gg = std::min(g, ORDER_GRID);
-    const bool optimistic = known_maxl >= 0 && verify_host != nullptr;
+    const bool optimistic = known_maxl >= 0 && verify_dev != nullptr;
     uint32_t fl[2] = {0, 0};
     // fast path: windowed inversion ranks + verification
-    hipMemsetAsync(of, 0, 8, st);
-    hipMemsetAsync(v, 0xFF, m * 4, st);                       // WR_EMPTY: detects rank collisions
+    fill_multi(st, {{of, 8, 0}, {v, m * 4, 0xFF}});           // flags; WR_EMPTY: detects rank collisions
     k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1);
-    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, of);
+    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, of, optimistic ? verify_dev : nullptr);
     if (optimistic) {
-        hipMemcpyAsync(verify_host, of + 1, 4, hipMemcpyDeviceToHost, st);
         fl[0] = (uint32_t)known_maxl;
     } else {
         hipMemcpyAsync(fl, of, 8, hipMemcpyDeviceToHost, st);
@@ -1581,9 +1581,15 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     }
 
     ls.pull_path = 0;
-    hipMemsetAsync(ls.flags, 0, 64, st);
-    if (n > 0) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
-    if (!in.keep_levels) hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
+    {
+        // flags; levels (unless given); the pull path's predecessor runs (zero: none) for pure key batches
+        const bool pull_try = in.kahn_ok && !in.keep_levels && P > 0 && !ls.pull_off && in.n_large == 0 && in.n_special == 0 &&
+                              !(in.merged_direct && in.merged_direct->ncap > 0) && !(in.merged_range && in.merged_range->ncap > 0);
+        fill_multi(st, {{ls.flags, 128, 0}, {in.keep_levels ? nullptr : in.lvl, std::max<size_t>(n, 1) * 4, 0},
+                        {pull_try ? ls.succ : nullptr, P * 8, 0}});
+        // local-only txns are key-domain specials (n_special): a pull batch has none
+        if (n > 0 && !pull_try) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
+    }
     *iters = 0;
     {
         // ---- chain order, segment table, pair -> segment, long-segment positions, (c) constraints
@@ -1654,15 +1660,13 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             {
                 KScope ks(K_KAHN, P);
                 const int gn = ceil_div((long)n, 256);
-                hipMemsetAsync(ls.succ, 0, P * 8, st);                    // predecessor runs (zero: none)
-                hipMemsetAsync(ls.flags + 16, 0, 12, st);                 // [16] abort, [17] max level, [18] far pred
+                // predecessor runs zeroed above; ls.flags [16] abort, [17] max level, [18] far pred (zeroed above)
                 k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
                                                   ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1,
                                                   ls.flags + 18);
                 k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
                                                  ls.sk1, ls.pull_force_abort ? 1 : 0);
-                k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
-                k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
+                k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl, ls.flags + 17);
                 if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 3, res)) {
                     err = "exec levels: device error";
                     return AD_ERR_DEVICE;

@@ -54,11 +54,14 @@ int stage_levels(ad_handle* h, bool want_order) {
     h->ls.bl_rounds = 0;
     h->ls.bl_used = false;
     h->order_pending = false;
-    h->order_bad = 0;
-    li.order_verify = &h->order_bad;
+    set_level_pub(h);
+    li.order_verify = nullptr;
+    if (h->pub_host) {                       // the optimistic order's failure flag: a host-mapped word
+        __atomic_store_n(h->pub_host + 1, 0u, __ATOMIC_RELEASE);
+        li.order_verify = h->pub_dev + 1;
+    }
     li.order_pending = &h->order_pending;
     int iters = 0;
-    set_level_pub(h);
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
     if (rc != AD_OK) return rc;
     h->level_iters = (uint32_t)iters;
@@ -71,10 +74,14 @@ int stage_levels(ad_handle* h, bool want_order) {
 
 // After a stream sync: if the optimistic execution order failed its verification, redo it on the
 // general path (radix sort by executeAt) and wait for it.
+bool order_failed(const ad_handle* h) {
+    return h->order_pending && h->pub_host && __atomic_load_n(h->pub_host + 1, __ATOMIC_ACQUIRE) != 0u;
+}
 int finish_order(ad_handle* h) {
     if (!h->order_pending) return AD_OK;
+    const bool bad = order_failed(h);
     h->order_pending = false;
-    if (!h->order_bad) return AD_OK;
+    if (!bad) return AD_OK;
     order_rows(h->ls, h->n, nullptr, h->ex1, h->lvl, h->pack.total_bits, h->order, h->st);
     HIPCHK(h, hipStreamSynchronize(h->st));
     return AD_OK;
