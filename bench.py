@@ -123,25 +123,45 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(sample_n, cfg="C2", reps=5):
+def cpu_share():
+    """Host threads this job may use: the CPU affinity set, capped by the cgroup CPU quota (cpu.max) and by
+    OMP_NUM_THREADS when the lease sets it (the GPU box gives one GPU's job a 16-CPU share of a larger host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = "affinity"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            c = max(1, int(int(q) // int(per)))
+            if c < n:
+                n, src = c, "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < n:
+        n, src = int(omp), "OMP_NUM_THREADS"
+    return n, src
+
+
+def cpu_baseline(sample_n, cfg="C2", reps=3):
     """The oracle (oracle/, the CPU restatement of the reference algorithms) on a bounded sample of the same
     workload on this host, SURVEY §8d / BASELINE.md §2: one warm-up, then the median of `reps` runs, with 1
-    thread and with T threads (T in {1, nproc}, capped at the box's 16-core share; the deps stage runs one
-    single-threaded store per key-range shard as InMemoryCommandStore.SingleThread, combined by
-    PreAccept.reduce; merge and levels stay serial).  The sample is the first `sample_n` txns of the step's own
-    generator (seeded identically): per-txn work is uniform along a C2/C3 batch, so the rate extrapolates to
-    the full batch.  Test infrastructure: timed here as the reported baseline only."""
+    thread and with T threads (T = the job's CPU share, cpu_share()).  Threads answer contiguous TxnId ranges
+    over one shared CFK index (every PreAccept query only reads it; each thread keeps its own pruning state) and
+    merge contiguous txn ranges; the execution levels are one serial executeAt-order sweep (the release DP is a
+    sequential dependency).  The sample is the first `sample_n` txns of the step's own generator (seeded
+    identically): per-txn work is uniform along a C2/C3 batch, so the rate extrapolates to the full batch
+    (checked once against the full batch: `bench.py --cpu-full`).  Test infrastructure: timed here as the
+    reported baseline only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     b = workload.config(cfg, n=sample_n)
     name = cfg
     cfg = abi.make_config(WINDOW, REPLICAS, DROP_P, workload.SEEDS[name])
     flags = O.FLAG_PRUNE | O.FLAG_MERGE | O.FLAG_LEVELS
-    nproc = os.cpu_count() or 1
-    # the threaded restatement shards key txns only (range txns span stores: single-threaded oracle)
-    tset = {1} if b.get("range_off") is not None else {1, max(1, min(16, nproc))}
+    T, src = cpu_share()
     runs = {}
-    for threads in sorted(tset):
+    for threads in sorted({1, T}):
         O.OracleResult(b, cfg, flags, threads=threads).stats()          # warm-up
         ts = []
         for _ in range(reps):
@@ -149,19 +169,31 @@ def cpu_baseline(sample_n, cfg="C2", reps=5):
             ts.append((s["t_deps"] + s["t_merge"] + s["t_levels"], s))
         ts.sort(key=lambda x: x[0])
         runs[threads] = ts[len(ts) // 2]
-    T = max(runs)
     t, s = runs[T]
-    t1 = runs[1][0]
-    return {"value": sample_n / t, "unit": "txn/s", "cores": T, "kind": "port",
-            "single_thread_value": sample_n / t1, "nproc": nproc, "cpu_model": cpu_model(), "median_of": reps,
-            "warmup": 1,
+    t1, s1 = runs[1]
+    return {"value": sample_n / t, "unit": "txn/s", "cores": T, "cores_source": src, "kind": "port",
+            "single_thread_value": sample_n / t1, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "median_of": reps, "warmup": 1,
             "sample": "%s generator, first %d txns of the same seeded batch (seed %#x; the rate extrapolates to the "
                       "full batch), PreAccept deps x%d views + Deps.merge + exec levels, oracle with CFK pruning "
                       "(restatement, not the Java reference: byId is built up front and levels are one sweep); "
-                      "median of %d after 1 warm-up: %d threads %.2f s (deps %.2f, merge %.2f, levels %.2f), "
-                      "1 thread %.2f s"
-                      % (name, sample_n, workload.SEEDS[name], REPLICAS, reps, T, t, s["t_deps"], s["t_merge"],
-                         s["t_levels"], t1)}
+                      "%d threads over TxnId ranges (deps, merge; levels serial), median of %d after 1 warm-up: "
+                      "%.2f s (deps %.2f, merge %.2f, levels %.2f); 1 thread %.2f s (deps %.2f, merge %.2f, levels %.2f)"
+                      % (name, sample_n, workload.SEEDS[name], REPLICAS, T, reps, t, s["t_deps"], s["t_merge"],
+                         s["t_levels"], t1, s1["t_deps"], s1["t_merge"], s1["t_levels"])}
+
+
+def cpu_full(cfg="C2"):
+    """One run of the T-thread oracle over the FULL batch of `cfg` (validates the sample extrapolation)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    b = workload.config(cfg)
+    c = abi.make_config(WINDOW, REPLICAS, DROP_P, workload.SEEDS[cfg])
+    T, src = cpu_share()
+    s = O.OracleResult(b, c, O.FLAG_PRUNE | O.FLAG_MERGE | O.FLAG_LEVELS, threads=T).stats()
+    t = s["t_deps"] + s["t_merge"] + s["t_levels"]
+    return {"config": cfg, "n": b["n"], "threads": T, "cores_source": src, "seconds": t, "value": b["n"] / t,
+            "t_deps": s["t_deps"], "t_merge": s["t_merge"], "t_levels": s["t_levels"]}
 
 
 def end_to_end(eng, batch, steps):
@@ -413,6 +445,8 @@ def main():
                          "or C4 (mixed key + range txns, 4M); the JSON line names it in config.workload")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="txns in the CPU-baseline sample (default 262144; C4: 16384; 0 = skip)")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="also time the T-thread oracle once over the FULL batch (validates the sample's extrapolation)")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel breakdown to stderr")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the end-to-end (H2D + pipeline + D2H through the C-ABI) side measurement")
@@ -498,10 +532,12 @@ def main():
         "end_to_end": e2e,
         "cpu_baseline": None,
     }
-    sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 17)
+    sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 18)
     if rank == 0 and world == 1 and sample > 0:
         out["cpu_baseline"] = cpu_baseline(sample, cfgname)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if args.cpu_full and rank == 0:
+        out["cpu_full_batch"] = cpu_full(cfgname)
     eng.close()
     print(json.dumps(out), flush=True)
 

@@ -36,6 +36,7 @@
 #include <map>
 #include <stdexcept>
 #include <string>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -298,11 +299,18 @@ struct Config {
 struct Cfk {
     uint64_t key;
     std::vector<uint32_t> byId;
-    // baseline pruning state (Pruning.java:164-233): a prefix of byId that can never again be
-    // emitted (committed, executeAt below the running maxCommittedWriteBefore) is dropped.
+};
+// baseline pruning state of one CFK (Pruning.java:164-233): a prefix of byId that can never again be emitted
+// (committed, executeAt below the running maxCommittedWriteBefore) is dropped.  Kept apart from the CFK so
+// threads answering disjoint TxnId ranges share one immutable byId index, each with its own pruning state.
+struct CfkPrune {
     size_t prunedBefore = 0;
     bool hasPrunedMaxWrite = false;
     Ts prunedMaxWrite{0, 0, 0};
+};
+struct CfkIndex {
+    std::vector<Cfk> cfks;              // sorted by key
+    std::vector<uint32_t> rangeTxns;    // ranks of range-domain txns (rangeCommands registry)
 };
 
 struct Oracle {
@@ -311,19 +319,26 @@ struct Oracle {
     bool prune;
     bool accept;                        // bound = executeAt (Accept / GetDeps) instead of TxnId (PreAccept)
     bool bound_max = false;             // bound = Timestamp.MAX (GetEphemeralReadDeps.java:76)
-    std::vector<Cfk> cfks;              // sorted by key
-    std::vector<uint32_t> rangeTxns;    // ranks of range-domain txns (rangeCommands registry)
+    std::shared_ptr<const CfkIndex> index;
+    const std::vector<Cfk>& cfks;
+    const std::vector<uint32_t>& rangeTxns;
+    std::vector<CfkPrune> pst;          // per CFK (this Oracle's queries only)
 
-    Oracle(const Batch& b, const Config& c, bool prune_, bool accept_ = false)
-        : B(b), cfg(c), prune(prune_ && !accept_), accept(accept_) {
+    static std::shared_ptr<const CfkIndex> build_index(const Batch& B) {
+        auto ix = std::make_shared<CfkIndex>();
         std::map<uint64_t, std::vector<uint32_t>> m;
         for (uint32_t i = 0; i < B.n; ++i) {
-            if (domain_of(B.tx[i]) == AD_DOMAIN_RANGE) { rangeTxns.push_back(i); continue; }
+            if (domain_of(B.tx[i]) == AD_DOMAIN_RANGE) { ix->rangeTxns.push_back(i); continue; }
             if (!manages(B.tx[i])) continue;   // EphemeralRead etc: never registered in CFK
             for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) m[B.keys[p]].push_back(i);
         }
-        for (auto& e : m) { Cfk c2; c2.key = e.first; c2.byId = std::move(e.second); cfks.push_back(std::move(c2)); }
+        for (auto& e : m) { Cfk c2; c2.key = e.first; c2.byId = std::move(e.second); ix->cfks.push_back(std::move(c2)); }
+        return ix;
     }
+    Oracle(const Batch& b, const Config& c, bool prune_, bool accept_ = false, std::shared_ptr<const CfkIndex> shared = nullptr)
+        : B(b), cfg(c), prune(prune_ && !accept_), accept(accept_), index(shared ? shared : build_index(b)),
+          cfks(index->cfks), rangeTxns(index->rangeTxns), pst(index->cfks.size()) {}
+    CfkPrune& prune_of(const Cfk& c) { return pst[&c - cfks.data()]; }
 
     // rows -> global arrival ranks (a batch that carries earlier batches' kept rows first; nullptr = identity)
     const uint32_t* gid = nullptr;
@@ -354,7 +369,8 @@ struct Oracle {
     // CommandsForKey.mapReduceActive(startedBefore = bound, testKind = kind_i.witnesses()) — CommandsForKey.java:925-983;
     // PreAccept.calculatePartialDeps' fn leaves out the txn itself (:258-260: p1 = txnId when executeAt != txnId)
     template <class F>
-    void map_reduce_active(Cfk& cfk, uint32_t i, uint32_t view, F&& emit) {
+    void map_reduce_active(const Cfk& cfk, uint32_t i, uint32_t view, F&& emit) {
+        CfkPrune& ps = prune_of(cfk);
         const Ts& bound = bound_of(i);
         const uint32_t qp = query_pos(i);
         const int qkind = kind_of(B.tx[i]);
@@ -363,9 +379,9 @@ struct Oracle {
         // maxCommittedWriteBefore (:930-943): the greatest executeAt of a committed Write in
         // committedByExecuteAt with executeAt < startedBefore.  committedByExecuteAt holds the byId
         // entries (all have TxnId < bound here) whose status >= COMMITTED and != INVALID.
-        bool hasM = cfk.hasPrunedMaxWrite;
-        Ts M = cfk.prunedMaxWrite;
-        for (size_t x = cfk.prunedBefore; x < end; ++x) {
+        bool hasM = ps.hasPrunedMaxWrite;
+        Ts M = ps.prunedMaxWrite;
+        for (size_t x = ps.prunedBefore; x < end; ++x) {
             uint32_t j = cfk.byId[x];
             if (j == i) continue;
             if (!in_committed_by_execute_at(seen_status_q(qp, j))) continue;
@@ -373,7 +389,7 @@ struct Oracle {
             if (ts_cmp(B.ex[j], bound) >= 0) continue;
             if (!hasM || ts_cmp(B.ex[j], M) > 0) { M = B.ex[j]; hasM = true; }
         }
-        for (size_t x = cfk.prunedBefore; x < end; ++x) {                       // :945-965
+        for (size_t x = ps.prunedBefore; x < end; ++x) {                        // :945-965
             uint32_t j = cfk.byId[x];
             if (j == i) continue;
             const Ts& txn = B.tx[j];
@@ -395,7 +411,7 @@ struct Oracle {
             // Pruning.maybePrune restated for the steady state: later queries have a larger bound and
             // a larger-or-equal M, so committed entries (seen committed by every later query) with
             // executeAt < M, before any non-prunable entry, are never emitted again.
-            size_t x = cfk.prunedBefore;
+            size_t x = ps.prunedBefore;
             while (x < end) {
                 uint32_t j = cfk.byId[x];
                 if (in_window(i + 1, j)) break;                 // still in flight for the next query
@@ -404,15 +420,15 @@ struct Oracle {
                 bool skip = st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID;
                 if (!skip && !(committed && ts_cmp(B.ex[j], M) < 0 && witnesses(AD_KIND_WRITE, kind_of(B.tx[j])))) break;
                 if (committed && kind_of(B.tx[j]) == AD_KIND_WRITE && ts_cmp(B.ex[j], bound) < 0) {
-                    if (!cfk.hasPrunedMaxWrite || ts_cmp(B.ex[j], cfk.prunedMaxWrite) > 0) { cfk.prunedMaxWrite = B.ex[j]; cfk.hasPrunedMaxWrite = true; }
+                    if (!ps.hasPrunedMaxWrite || ts_cmp(B.ex[j], ps.prunedMaxWrite) > 0) { ps.prunedMaxWrite = B.ex[j]; ps.hasPrunedMaxWrite = true; }
                 }
                 ++x;
             }
-            cfk.prunedBefore = x;
+            ps.prunedBefore = x;
         }
     }
 
-    Cfk* find_cfk(uint64_t key) {
+    const Cfk* find_cfk(uint64_t key) const {
         auto it = std::lower_bound(cfks.begin(), cfks.end(), key, [](const Cfk& c, uint64_t k) { return c.key < k; });
         return it != cfks.end() && it->key == key ? &*it : nullptr;
     }
@@ -431,7 +447,7 @@ struct Oracle {
         if (domain_of(me) == AD_DOMAIN_KEY) {
             std::vector<uint64_t> ks(B.keys.begin() + B.key_off[i], B.keys.begin() + B.key_off[i + 1]);
             std::sort(ks.begin(), ks.end());                     // Keys are sorted
-            for (uint64_t k : ks) { Cfk* c = find_cfk(k); if (c) map_reduce_active(*c, i, view, emit_key); }
+            for (uint64_t k : ks) { const Cfk* c = find_cfk(k); if (c) map_reduce_active(*c, i, view, emit_key); }
         } else {
             for (uint32_t q = B.range_off[i]; q < B.range_off[i + 1]; ++q) {
                 const RangeK& r = B.ranges[q];
@@ -495,7 +511,7 @@ struct Oracle {
         const bool key_dom = domain_of(B.tx[i]) == AD_DOMAIN_KEY;
         if (key_dom) {
             for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
-                Cfk* c = find_cfk(B.keys[p]);
+                const Cfk* c = find_cfk(B.keys[p]);
                 if (c) cfk_prefix(*c);
             }
         } else {
@@ -586,12 +602,22 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
     std::sort(byExec.begin(), byExec.end(), [&](uint32_t a, uint32_t b) { return ts_cmp(B.ex[a], B.ex[b]) < 0; });
     std::vector<int64_t> level(n, -1);
     struct Chain { std::vector<Ts> exec; std::vector<int64_t> pmAll; int64_t maxAll = -1, maxW = -1; };
-    std::map<uint64_t, Chain> chains;
+    // keys as dense ids (sorted distinct keys): chains and byId in flat vectors instead of ordered maps
+    std::vector<uint64_t> uk(B.keys.begin(), B.keys.end());
+    std::sort(uk.begin(), uk.end());
+    uk.erase(std::unique(uk.begin(), uk.end()), uk.end());
+    auto kid_of = [&](uint64_t k) -> int64_t {
+        auto it = std::lower_bound(uk.begin(), uk.end(), k);
+        return it != uk.end() && *it == k ? (int64_t)(it - uk.begin()) : -1;
+    };
+    std::vector<uint32_t> pkid(B.keys.size());
+    for (size_t p = 0; p < B.keys.size(); ++p) pkid[p] = (uint32_t)kid_of(B.keys[p]);
+    std::vector<Chain> chains(uk.size());
     // per key: the managed-execution txns in TxnId (= batch) order (CommandsForKey.byId restricted to them)
-    std::map<uint64_t, std::vector<uint32_t>> byId;
+    std::vector<std::vector<uint32_t>> byId(uk.size());
     for (uint32_t t = 0; t < n; ++t)
         if (manages_execution(B.tx[t]))
-            for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) byId[B.keys[p]].push_back(t);
+            for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) byId[pkid[p]].push_back(t);
     auto resolve = [&](uint32_t t) {
         int64_t lv = -1;
         const Ts& me = B.tx[t];
@@ -613,9 +639,8 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
         if (manages_execution(me)) {
             bool w = kind == AD_KIND_WRITE;
             for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
-                auto it = chains.find(B.keys[p]);
-                if (it == chains.end()) continue;
-                lv = std::max(lv, w ? it->second.maxAll : it->second.maxW);
+                const Chain& c = chains[pkid[p]];             // an empty chain: maxAll = maxW = -1
+                lv = std::max(lv, w ? c.maxAll : c.maxW);
             }
         } else {
             // unmanaged: per key of keyDeps, bound = max executeAt of its qualifying deps (+ byId between them)
@@ -632,15 +657,13 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
                     fold(dep);
                     first = std::min(first, dep); last = std::max(last, dep);
                 }
-                auto bit = byId.find(kd.keys[ki]);
-                if (sync_point && first != UINT32_MAX && bit != byId.end()) {
-                    const std::vector<uint32_t>& ids = bit->second;
+                const int64_t kk = kid_of(kd.keys[ki]);
+                if (sync_point && first != UINT32_MAX && kk >= 0) {
+                    const std::vector<uint32_t>& ids = byId[kk];
                     for (auto q = std::lower_bound(ids.begin(), ids.end(), first); q != ids.end() && *q <= last; ++q) fold(*q);
                 }
-                if (!has) continue;
-                auto it = chains.find(kd.keys[ki]);
-                if (it == chains.end()) continue;
-                Chain& c = it->second;
+                if (!has || kk < 0) continue;
+                Chain& c = chains[kk];
                 size_t pos = std::upper_bound(c.exec.begin(), c.exec.end(), bnd, [](const Ts& a, const Ts& b) { return ts_cmp(a, b) < 0; }) - c.exec.begin();
                 if (pos > 0) lv = std::max(lv, c.pmAll[pos - 1]);
             }
@@ -649,7 +672,7 @@ static std::vector<uint32_t> exec_levels(const Batch& B, const std::vector<TxnDe
         if (manages_execution(me)) {
             bool w = kind == AD_KIND_WRITE;
             for (uint32_t p = B.key_off[t]; p < B.key_off[t + 1]; ++p) {
-                Chain& c = chains[B.keys[p]];
+                Chain& c = chains[pkid[p]];
                 c.maxAll = std::max(c.maxAll, level[t]);
                 if (w) c.maxW = std::max(c.maxW, level[t]);
                 c.exec.push_back(myExec);
@@ -730,8 +753,26 @@ static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uin
                 o.gid = gid;
                 for (uint32_t i = 0; i < n; ++i) all[v][i] = o.preaccept(i, v);
             }
+        } else if (!(flags & 64)) {
+            // T threads over contiguous TxnId ranges of the batch, one shared immutable CFK index: every query
+            // only reads it (each thread keeps its own pruning state; a range's first query on a key scans the
+            // key's whole prefix once, then pruning keeps it short), so the answers equal the serial run's
+            auto ix = Oracle::build_index(B);
+            std::vector<std::thread> pool;
+            for (uint32_t s = 0; s < threads; ++s) {
+                pool.emplace_back([&, s]() {
+                    const uint32_t i0 = (uint32_t)((uint64_t)n * s / threads), i1 = (uint32_t)((uint64_t)n * (s + 1) / threads);
+                    for (uint32_t v = 0; v < R; ++v) {
+                        Oracle o(B, cfg, (flags & 1) && !gid, (flags & 40) != 0, ix);
+                        o.bound_max = (flags & 32) != 0;
+                        o.gid = gid;
+                        for (uint32_t i = i0; i < i1; ++i) all[v][i] = o.preaccept(i, v);
+                    }
+                });
+            }
+            for (auto& th : pool) th.join();
         } else {
-            if (flags & 40) throw std::invalid_argument("threaded oracle: executeAt / MAX-bound deps unsupported");
+            if (flags & 40) throw std::invalid_argument("key-sharded oracle: executeAt / MAX-bound deps unsupported");
             // Shard the key space into `threads` contiguous ranges of the batch's distinct keys
             // (ShardDistributor.EvenSplit, local/ShardDistributor.java:32-80), one single-threaded
             // store per shard; each store answers the part of every query that falls in its range;
@@ -790,17 +831,28 @@ static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uin
         std::vector<TxnDeps> merged;
         if (flags & 6) {
             auto t2 = std::chrono::steady_clock::now();
-            // Deps.merge(list) = per class LinearMerger over the replies in order (Deps.java:281-286)
+            // Deps.merge(list) = per class LinearMerger over the replies in order (Deps.java:281-286); txns are
+            // independent: T threads over contiguous ranges
             merged.resize(n);
-            for (uint32_t i = 0; i < n; ++i) {
-                TxnDeps acc;
-                for (uint32_t v = 0; v < R; ++v) {
-                    if (view_mask && !view_mask[(size_t)v * n + i]) continue;
-                    acc.key = linear_union(acc.key, all[v][i].key);
-                    acc.direct = linear_union(acc.direct, all[v][i].direct);
-                    acc.range = linear_union(acc.range, all[v][i].range);
+            auto merge_range = [&](uint32_t i0, uint32_t i1) {
+                for (uint32_t i = i0; i < i1; ++i) {
+                    TxnDeps acc;
+                    for (uint32_t v = 0; v < R; ++v) {
+                        if (view_mask && !view_mask[(size_t)v * n + i]) continue;
+                        acc.key = linear_union(acc.key, all[v][i].key);
+                        acc.direct = linear_union(acc.direct, all[v][i].direct);
+                        acc.range = linear_union(acc.range, all[v][i].range);
+                    }
+                    merged[i] = std::move(acc);
                 }
-                merged[i] = std::move(acc);
+            };
+            if (threads <= 1) {
+                merge_range(0, n);
+            } else {
+                std::vector<std::thread> pool;
+                for (uint32_t s = 0; s < threads; ++s)
+                    pool.emplace_back(merge_range, (uint32_t)((uint64_t)n * s / threads), (uint32_t)((uint64_t)n * (s + 1) / threads));
+                for (auto& th : pool) th.join();
             }
             auto t3 = std::chrono::steady_clock::now();
             res->t_merge = std::chrono::duration<double>(t3 - t2).count();

@@ -71,6 +71,7 @@ def lib():
 FLAG_PRUNE, FLAG_MERGE, FLAG_LEVELS, FLAG_ACCEPT = 1, 2, 4, 8
 FLAG_DONE = 16     # levels over a CFK history batch: APPLIED / INVALID txns are done (AD_LEVEL_DONE)
 FLAG_BOUND_MAX = 32  # deps with bound Timestamp.MAX (GetEphemeralReadDeps), answered after every arrival
+FLAG_KEY_SHARDS = 64  # threads > 1: key-range-sharded stores + PreAccept.reduce (default: TxnId ranges, shared index)
 
 
 class OracleResult:

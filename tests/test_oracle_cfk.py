@@ -234,7 +234,7 @@ def test_threaded_oracle_equals_single_store():
         b["keys"][ko[t]:ko[t + 1]] = np.sort(row)
     cfg = abi.make_config(32, 3, 0.1, 7)
     one = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS, threads=1)
-    four = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS, threads=4)
+    four = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS | O.FLAG_KEY_SHARDS, threads=4)
     for v in range(3):
         for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
             assert one.deps(v, c).equal(four.deps(v, c))

@@ -55,4 +55,14 @@ def test_threaded_pruned_equals_serial():
     b = workload.config("C2", n=40000)
     cfg = abi.make_config(32, 3, 0.1, workload.SEEDS["C2"])
     flags = O.FLAG_MERGE | O.FLAG_LEVELS | O.FLAG_PRUNE
-    _same(O.OracleResult(b, cfg, flags, threads=4), O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS), 3)
+    _same(O.OracleResult(b, cfg, flags | O.FLAG_KEY_SHARDS, threads=4), O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS), 3)
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C4"])
+def test_txn_range_threads_equal_serial(name):
+    # the CPU baseline's threading: T threads over TxnId ranges sharing one CFK index, each with its own pruning
+    # state (C4: range txns too); deps of every view and class, merged Deps and levels equal the serial oracle's
+    b = workload.config(name, n=20000 if name != "C4" else 6000)
+    cfg = abi.make_config(32, 3, 0.1, workload.SEEDS[name])
+    flags = O.FLAG_MERGE | O.FLAG_LEVELS | O.FLAG_PRUNE
+    _same(O.OracleResult(b, cfg, flags, threads=7), O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS), 3)
