@@ -83,14 +83,6 @@ static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64
     qpos[i] = (uint32_t)lo;
 }
 
-int side_stream(ad_handle* h) {
-    if (h->sst) return AD_OK;
-    HIPCHK(h, hipStreamCreateWithFlags(&h->sst, hipStreamNonBlocking));
-    HIPCHK(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    HIPCHK(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-    return AD_OK;
-}
-
 int stage_deps(ad_handle* h) {
     StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
@@ -154,6 +146,7 @@ int stage_deps(ad_handle* h) {
     wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt8 = h->cnt8; wa.cntx = h->cntx; wa.inl = h->inl; wa.dfr = h->dfr; wa.dst = h->dst;
     wa.key_off = h->key_off;
+    CK(dalloc(h, S_POSOF, &wa.posof, std::max<size_t>(P, 1)));
     uint32_t* heavy = h->totd + MAX_TOTALS - 1;          // heavy-merge hint (read with the totals)
     uint32_t* items_count = heavy - 1;                    // the fill walk's items (count walk)
     uint32_t* dtx_count = heavy - 2;                      // deferred small txns (offsets scan)
@@ -244,27 +237,15 @@ int stage_deps(ad_handle* h) {
         ua.key_off[vc] = c.key_off; ua.k2t_off[vc] = c.k2t_off; ua.ent_off[vc] = c.ent_off; ua.k2t[vc] = c.k2t;
         ua.txns[vc] = c.txns; ua.tcnt[vc] = c.tcnt;
     }
-    // The deferred small txns (their layout, the fill walk of the listed pairs, their union: a chain of small
-    // latency-bound launches, ~30 us on C2 for 3 txns) run on a side stream, overlapping k_txn_finish over the
-    // others; joined at the end of the stage.
-    const bool side = ndtx > 0 || nitems > 0;
-    if (side) {
-        CK(side_stream(h));
-        HIPCHK(h, hipEventRecord(h->ev_fork, st));
-        HIPCHK(h, hipStreamWaitEvent(h->sst, h->ev_fork, 0));
-        TxnArgs td = ta;
-        td.rows = dtx; td.nrows = ndtx;
-        if (ndtx > 0) launch_finish_nv(nv, td, direct, h->sst);
-        WalkArgs wp = wa;
-        wp.V = 0; wp.items = items; wp.nitems = nitems;
-        if (nitems > 0) launch_walk_nv(nv, wp, true, direct, true, h->sst);
-        if (ndtx > 0) launch_union_nv(nv, ua, direct, h->sst);
-        HIPCHK(h, hipEventRecord(h->ev_join, h->sst));
-    }
-    ta.rows = nullptr; ta.nrows = n;
+    // small txns: k_txn_finish (re-walking in place the pairs that overflowed their inline ids); txns with more
+    // than 4 keys (deferred) get their layout there and their lists from the fill walk of their pairs + k_txn_union
+    ta.nrows = n;
+    ta.w = wa;
     if (n > 0) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
-    if (h->V > 0) launch_walk_nv(nv, wa, true, direct, false, st);           // the virtual items' fill walk
+    wa.items = items; wa.nitems = nitems;
+    launch_walk_nv(nv, wa, true, direct, nitems > 0, st);
+    if (ndtx > 0) { KScope ks(K_TXN_UNION, ndtx); launch_union_nv(nv, ua, direct, st); }
     if (Q > 0 && n > 0) launch_range_nv(nv, ra, true, st);
     // large txns' key CSRs and every RangeDeps CSR: LDS sort union (overflowing CSRs queued for a big pass)
     if (n > 0 && (h->n_large > 0 || Q > 0)) {
@@ -312,7 +293,6 @@ int stage_deps(ad_handle* h) {
         }
         CK(union_overflow(h, la, ovf_count, ovf, Q > 0));
     }
-    if (side) HIPCHK(h, hipStreamWaitEvent(st, h->ev_join, 0));
     // Virtual-item work arrays are dead once the CSRs are filled; they stay allocated for the next batch
     // (re-allocating C4's ~90 GB of them every batch cost more than the walks) unless the merge runs out of
     // HBM, when release_dead gives them back (STAGE_MERGE).

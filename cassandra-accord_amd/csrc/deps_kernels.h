@@ -347,9 +347,10 @@ struct WalkArgs {
     uint8_t* cnt8;            // real pairs, AoS by pair: [p * NCB + k] count of class k, 255 = see cntx
     uint32_t* cntx;           // [p * NC + k] exact count where cnt8 saturated (>= 255)
     uint32_t* inl;            // [(p * NC + k) * WALK_INL + q]: the first WALK_INL ids the walk emits (descending)
-    uint8_t* dfr;             // [txn] 1: a pair of the txn emits more than WALK_INL ids in some class, or the txn has
-                              // more than 4 keys with entries (fill walk + k_txn_union); count walk / scan write it
+    uint8_t* dfr;             // [txn] 1: the txn has more than 4 keys with entries (fill walk + k_txn_union; the
+                              // offsets scan writes it)
     const uint32_t* key_off;  // per txn (a txn with more than 4 keys: every pair with entries goes to the fill walk)
+    uint32_t* posof;          // [pair] sorted position, written for the pairs that overflowed their inline ids
     uint32_t* items_out;      // count walk: the sorted positions the fill walk visits, *items_count of them
     uint32_t* items_count;
     const uint32_t* items;    // fill walk: that list, nitems long
@@ -466,16 +467,37 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t gq, ui
 template <int NV, bool DIRECT>
 __device__ inline int walk_class(int v, bool direct) { return DIRECT ? 2 * v + (direct ? 1 : 0) : v; }
 
+// The query of the key entry at sorted position s (txn i, meta mi): CommandsForKey.mapReduceActive over its key's
+// entries below the bound, every replica view (walk_query).  Small key-domain query txns only (large ones are
+// virtual items; the other kinds query nothing).
+template <int NV, class Emit>
+__device__ inline void walk_entry(const WalkArgs& a, size_t s, uint32_t i, uint32_t mi, Emit&& emit) {
+    const uint32_t qk = meta_kind(mi);
+    if (!(meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE))) return;
+    const int seg0 = a.seg_start[s];
+    if (a.qpos) {
+        // first entry of the segment at or past the bound: ranks ascend inside a segment
+        const uint32_t qi = a.qpos[i];
+        size_t lo = s + 1, hi = a.P;
+        while (lo < hi) {
+            const size_t m = (lo + hi) >> 1;
+            if (a.seg_start[m] == seg0 && a.e_txn[m] < qi) lo = m + 1; else hi = m;
+        }
+        walk_query<NV>(a, i, a.gid ? a.gid[i] : qi, a.bound1(i), qk, (int)lo, seg0, emit);
+    } else {
+        const uint32_t gi = a.gid ? a.gid[i] : i;
+        walk_query<NV>(a, i, gi, a.tx_ts[i] + 1, qk, (int)s, seg0, emit);
+    }
+}
+
 template <int NV, bool FILL, bool DIRECT>
 static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
     constexpr int NC = DIRECT ? 2 * NV : NV;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= (FILL ? a.nitems : (a.qpos ? a.P : a.P - a.prm->n_keys_u))) return;
     const size_t s = FILL ? (size_t)a.items[x] : (a.qpos ? x : (size_t)a.nh[x]);
-    const int seg0 = a.seg_start[s];
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
-    const uint32_t qk = meta_kind(mi);
     // the pair's counts / slots live AoS by pair index (the per-txn kernels read them contiguously)
     const size_t p = a.sval[s];
     const size_t pb = p * NC;
@@ -492,23 +514,7 @@ static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
             c[k]++;
         }
     };
-    // small key-domain query txns only (large ones are virtual items)
-    const bool query = meta_domain(mi) == AD_DOMAIN_KEY && qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && !(mi & META_LARGE);
-    if (query) {
-        if (a.qpos) {
-            // first entry of the segment at or past the bound: ranks ascend inside a segment
-            const uint32_t qi = a.qpos[i];
-            size_t lo = s + 1, hi = a.P;
-            while (lo < hi) {
-                const size_t m = (lo + hi) >> 1;
-                if (a.seg_start[m] == seg0 && a.e_txn[m] < qi) lo = m + 1; else hi = m;
-            }
-            walk_query<NV>(a, i, a.gid ? a.gid[i] : qi, a.bound1(i), qk, (int)lo, seg0, emit);
-        } else {
-            const uint32_t gi = a.gid ? a.gid[i] : i;
-            walk_query<NV>(a, i, gi, a.tx_ts[i] + 1, qk, (int)s, seg0, emit);
-        }
-    }
+    walk_entry<NV>(a, s, i, mi, emit);
     if (!FILL) {
         constexpr int NCB = ncb_of(NC);
         uint32_t w[NCB / 4];
@@ -524,14 +530,15 @@ static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
         uint32_t* d = reinterpret_cast<uint32_t*>(a.cnt8 + p * NCB);
 #pragma unroll
         for (int q = 0; q < NCB / 4; ++q) d[q] = w[q];
-        if (over) a.dfr[i] = 1;
-        // the fill walk's items: pairs that overflowed their inline ids, and every pair with entries of a txn
-        // with more than 4 keys (k_txn_finish lays those out from dst)
         bool any = false;
 #pragma unroll
         for (int k = 0; k < NC; ++k) any |= c[k] > 0;
-        const bool wide = query && a.key_off[i + 1] - a.key_off[i] > 4u;
-        wave_append(over || (wide && any), (uint32_t)s, a.items_out, a.items_count);
+        const bool wide = a.key_off[i + 1] - a.key_off[i] > 4u;
+        // a pair of a <= 4-key txn that overflowed its inline ids: k_txn_finish re-walks it from here
+        if (over && !wide) a.posof[p] = (uint32_t)s;
+        // the fill walk's items: every pair with entries of a txn with more than 4 keys (deferred to walk<fill>
+        // + k_txn_union; k_txn_finish lays them out)
+        wave_append(wide && any, (uint32_t)s, a.items_out, a.items_count);
     }
 }
 
@@ -582,8 +589,8 @@ struct TxnArgs {
     uint32_t* out_tcnt[NVC_MAX];
     const uint32_t* inl;          // the count walk's inline ids [(p * nvc + vc) * WALK_INL + q], descending
     const uint8_t* dfr;           // [txn] deferred to the fill walk + k_txn_union
-    const uint32_t* rows;         // k_txn_finish: nullable = every txn except the deferred ones; else these rows
-    size_t nrows;
+    size_t nrows;                 // k_txn_finish: txns
+    WalkArgs w;                   // k_txn_finish re-walks the pairs that overflowed their inline ids (w.posof)
     uint32_t* dst;                // AoS by pair [p * nvc + vc]
     Params* prm;
     // large txns (virtual items, in (txn, key) order): items [voff[t], voff[t+1])
@@ -763,129 +770,6 @@ __device__ inline void sort16(uint64_t* v) {
     }
 }
 
-// Per (small txn, class), after the CSRs are sized: the KeyDeps layout (keys in ascending order, keysToTxnIds
-// header); the per-key lists from the count walk's inline ids (emitted descending, laid out ascending); and,
-// unless the txn is deferred, the TxnId union with every entry remapped to its index (RelationMultiMap.
-// AbstractBuilder's finishKey/build, utils/RelationMultiMap.java:201-260).  A pair the count walk put on its
-// item list (some class emitted more than WALK_INL ids, or the txn has more than 4 keys) gets its last k2t slot
-// in dst instead, for walk<fill> over that list; deferred txns are then unioned by k_txn_union over the scan's
-// txn list.  Grid (txns, classes): every load of a thread is issued before its first store (offsets, counts,
-// keys, then the inline ids), so a thread waits for three memory round trips; the <= 4 pairs x WALK_INL ids are
-// at compile-time indices and the union of up to 16 (TxnId, slot) pairs is one register sorting network.
-template <int NVC>
-static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
-    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
-    if (x >= a.nrows) return;
-    const size_t t = a.rows ? a.rows[x] : x;      // rows: the deferred txns (side stream); else every txn
-    if (!a.rows && a.dfr[t]) return;
-    const uint32_t kb = a.out_key_off[c][t], ke = a.out_key_off[c][t + 1];
-    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
-    const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
-    const bool large = (a.meta[t] & META_LARGE) != 0;
-    const bool defer = a.dfr[t] != 0;
-    if (large) return;                              // k_large_layout
-    const uint32_t nk = ke - kb;
-    if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; return; }
-    constexpr int NCB = ncb_of(NVC);
-    int32_t* k2t = a.out_k2t[c];
-    if (e - b > 4) {                                // every pair with entries is on the walk's item list
-        uint32_t run = nk, kk = 0;
-        for (uint32_t x = b; x < e; ++x) {
-            const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, x, c);
-            if (cc == 0) continue;
-            a.out_keys[c][kb + kk] = a.keys[x];
-            a.dst[(size_t)x * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
-            run += cc;
-            k2t[mb + kk] = (int32_t)run;
-            ++kk;
-        }
-        return;
-    }
-    uint32_t cc[4];
-    bool walked[4];                                 // the pair is on the fill walk's list (some class overflowed)
-    uint64_t kx[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t v[NVC];
-        if (b + j < e) pair_counts<NVC>(a.cnt8, a.cntx, b + j, v);
-        else {
-#pragma unroll
-            for (int k = 0; k < NVC; ++k) v[k] = 0u;
-        }
-        bool w = false;
-#pragma unroll
-        for (int k = 0; k < NVC; ++k) w |= v[k] > (uint32_t)WALK_INL;
-        walked[j] = w;
-        cc[j] = v[0];
-#pragma unroll
-        for (int k = 1; k < NVC; ++k) cc[j] = k == c ? v[k] : cc[j];
-        kx[j] = b + j < e ? a.keys[b + j] : 0ull;
-    }
-    uint32_t id[4][WALK_INL];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
-#pragma unroll
-        for (int q = 0; q < WALK_INL; ++q) id[j][q] = (!walked[j] && (uint32_t)q < cc[j]) ? src[q] : 0u;
-    }
-    uint32_t run = nk, kk = 0, rb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        rb[j] = run;
-        if (cc[j] == 0) continue;
-        a.out_keys[c][kb + kk] = kx[j];
-        if (walked[j]) a.dst[(size_t)(b + j) * NVC + c] = mb + run + cc[j] - 1;
-        run += cc[j];
-        k2t[mb + kk] = (int32_t)run;
-        ++kk;
-    }
-    if (defer) {                                    // raw TxnIds of the inline lists; k_txn_union remaps
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (walked[j]) continue;
-#pragma unroll
-            for (int q = 0; q < WALK_INL; ++q)
-                if ((uint32_t)q < cc[j]) k2t[mb + rb[j] + cc[j] - 1 - (uint32_t)q] = (int32_t)id[j][q];
-        }
-        return;
-    }
-    uint32_t* tx = a.out_txns[c] + ob;
-    if (nk == 1) {                                  // one key: its list is the union, indices 0..cc-1
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (cc[j] == 0) continue;
-#pragma unroll
-            for (int q = 0; q < WALK_INL; ++q) {
-                if ((uint32_t)q < cc[j]) {
-                    const uint32_t pos = cc[j] - 1 - (uint32_t)q;
-                    tx[pos] = id[j][q];
-                    k2t[mb + rb[j] + pos] = (int32_t)pos;
-                }
-            }
-            a.out_tcnt[c][t] = cc[j];
-        }
-        return;
-    }
-    // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index
-    uint64_t v[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < WALK_INL; ++q)
-            v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)id[j][q] << 32) | (uint64_t)(mb + rb[j] + cc[j] - 1 - (uint32_t)q) : ~0ull;
-    sort16(v);
-    uint32_t u = 0, prev = 0xFFFFFFFFu;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        if (v[r] != ~0ull) {
-            const uint32_t x = (uint32_t)(v[r] >> 32);
-            if (x != prev) { tx[u++] = x; prev = x; }
-            k2t[(uint32_t)v[r]] = (int32_t)(u - 1);
-        }
-    }
-    a.out_tcnt[c][t] = u;
-}
 static_assert(WALK_INL == 4, "k_txn_finish's sorting network holds 4 pairs x 4 ids");
 
 // Union of up to KMAX sorted lists living in k2t[lo[k] .. hi[k]) -> out (unique, ascending); then
@@ -943,6 +827,129 @@ __device__ inline uint32_t union_small(int32_t* __restrict__ k2t, uint32_t mb, u
     return union_lists<KM>(k2t, lo, hi, (int)nk, out);
 }
 
+// Per (small txn, class), after the CSRs are sized: the KeyDeps layout (keys in ascending order, keysToTxnIds
+// header), the per-key lists and the TxnId union with every entry remapped to its index (RelationMultiMap.
+// AbstractBuilder's finishKey/build, utils/RelationMultiMap.java:201-260).  Lists come from the count walk's
+// inline ids (emitted descending, laid out ascending); when every list of the class fits them, the union of up to
+// 4 pairs x WALK_INL (TxnId, slot) pairs is one register sorting network.  A pair whose class overflowed them is
+// re-walked here (walk_entry from the position the count walk left in posof, this class only) and the class's
+// lists are then unioned from memory (union_small) -- rare (C2: a few txns per batch), and inside this kernel its
+// latency hides behind the other threads instead of forming a serial chain of small launches.  Txns with more
+// than 4 keys (deferred: dfr) only get their layout and the fill walk's dst slots; walk<fill> + k_txn_union
+// finish them.  Grid (txns, classes): the offsets, counts and keys are loaded before the ids and the first store.
+template <int NV, bool DIRECT>
+static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
+    constexpr int NVC = DIRECT ? 2 * NV : NV;
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (x >= a.nrows) return;
+    const size_t t = x;
+    const uint32_t kb = a.out_key_off[c][t], ke = a.out_key_off[c][t + 1];
+    const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
+    const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
+    const uint32_t mt = a.meta[t];
+    const bool defer = a.dfr[t] != 0;
+    if (mt & META_LARGE) return;                    // k_large_layout
+    const uint32_t nk = ke - kb;
+    if (nk == 0) { if (!defer) a.out_tcnt[c][t] = 0; return; }
+    constexpr int NCB = ncb_of(NVC);
+    int32_t* k2t = a.out_k2t[c];
+    if (e - b > 4) {                                // deferred: every pair with entries is on the fill walk's list
+        uint32_t run = nk, kk = 0;
+        for (uint32_t y = b; y < e; ++y) {
+            const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, y, c);
+            if (cc == 0) continue;
+            a.out_keys[c][kb + kk] = a.keys[y];
+            a.dst[(size_t)y * NVC + c] = mb + run + cc - 1;      // the fill walk emits descending from here
+            run += cc;
+            k2t[mb + kk] = (int32_t)run;
+            ++kk;
+        }
+        return;
+    }
+    uint32_t cc[4];
+    uint64_t kx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cc[j] = b + j < e ? pair_count(a.cnt8, a.cntx, NCB, NVC, b + j, c) : 0u;
+        kx[j] = b + j < e ? a.keys[b + j] : 0ull;
+    }
+    bool ovf = false;                               // some list of this class overflowed its inline ids
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ovf |= cc[j] > (uint32_t)WALK_INL;
+    uint32_t id[4][WALK_INL];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t* src = a.inl + ((size_t)(b + j) * NVC + c) * WALK_INL;
+#pragma unroll
+        for (int q = 0; q < WALK_INL; ++q) id[j][q] = (uint32_t)q < cc[j] && cc[j] <= (uint32_t)WALK_INL ? src[q] : 0u;
+    }
+    uint32_t run = nk, kk = 0, rb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        rb[j] = run;
+        if (cc[j] == 0) continue;
+        a.out_keys[c][kb + kk] = kx[j];
+        run += cc[j];
+        k2t[mb + kk] = (int32_t)run;
+        ++kk;
+    }
+    uint32_t* tx = a.out_txns[c] + ob;
+    if (ovf) {
+        // the lists in memory (raw TxnIds, ascending): inline ids, and the overflowed pairs re-walked for this class
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (cc[j] == 0) continue;
+            if (cc[j] <= (uint32_t)WALK_INL) {
+#pragma unroll
+                for (int q = 0; q < WALK_INL; ++q)
+                    if ((uint32_t)q < cc[j]) k2t[mb + rb[j] + cc[j] - 1 - (uint32_t)q] = (int32_t)id[j][q];
+            } else {
+                const size_t sp = a.w.posof[b + j];
+                uint32_t slot = mb + rb[j] + cc[j] - 1;
+                walk_entry<NV>(a.w, sp, (uint32_t)t, mt, [&](int v, bool direct, uint32_t dj) {
+                    if (walk_class<NV, DIRECT>(v, direct) == c) k2t[slot--] = (int32_t)dj;
+                });
+            }
+        }
+        a.out_tcnt[c][t] = union_small<4>(k2t, mb, nk, tx);
+        return;
+    }
+    if (nk == 1) {                                  // one key: its list is the union, indices 0..cc-1
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (cc[j] == 0) continue;
+#pragma unroll
+            for (int q = 0; q < WALK_INL; ++q) {
+                if ((uint32_t)q < cc[j]) {
+                    const uint32_t pos = cc[j] - 1 - (uint32_t)q;
+                    tx[pos] = id[j][q];
+                    k2t[mb + rb[j] + pos] = (int32_t)pos;
+                }
+            }
+            a.out_tcnt[c][t] = cc[j];
+        }
+        return;
+    }
+    // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index
+    uint64_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < WALK_INL; ++q)
+            v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)id[j][q] << 32) | (uint64_t)(mb + rb[j] + cc[j] - 1 - (uint32_t)q) : ~0ull;
+    sort16(v);
+    uint32_t u = 0, prev = 0xFFFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (v[r] != ~0ull) {
+            const uint32_t y = (uint32_t)(v[r] >> 32);
+            if (y != prev) { tx[u++] = y; prev = y; }
+            k2t[(uint32_t)v[r]] = (int32_t)(u - 1);
+        }
+    }
+    a.out_tcnt[c][t] = u;
+}
 struct UnionArgs {
     size_t n;
     int nvc;

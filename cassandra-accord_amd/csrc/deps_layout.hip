@@ -25,8 +25,8 @@ void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy, 
 template <int NV>
 void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
     const dim3 g((unsigned)ceil_div((long)ta.nrows, 256), direct ? 2 * NV : NV);
-    if (direct) k_txn_finish<2 * NV><<<g, 256, 0, st>>>(ta);
-    else k_txn_finish<NV><<<g, 256, 0, st>>>(ta);
+    if (direct) k_txn_finish<NV, true><<<g, 256, 0, st>>>(ta);
+    else k_txn_finish<NV, false><<<g, 256, 0, st>>>(ta);
 }
 
 template <int NV>

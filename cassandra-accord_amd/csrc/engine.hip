@@ -451,9 +451,6 @@ void ad_close(ad_handle* h) {
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->st) hipStreamSynchronize(h->st);
     if (h->cst) { hipStreamSynchronize(h->cst); hipStreamDestroy(h->cst); }
-    if (h->sst) { hipStreamSynchronize(h->sst); hipStreamDestroy(h->sst); }
-    if (h->ev_fork) hipEventDestroy(h->ev_fork);
-    if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->cev) hipEventDestroy(h->cev);
     if (h->sev) hipEventDestroy(h->sev);
     if (h->pub_host) hipHostFree(h->pub_host);

@@ -46,8 +46,6 @@ struct ad_handle {
     int device = 0;
     ad_config cfg{};
     hipStream_t st = nullptr;
-    hipStream_t sst = nullptr;           // side stream (deps: deferred small txns), forked / joined by events
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     std::vector<DBuf> bufs;
     // loaded batch
@@ -250,7 +248,7 @@ enum Slot : size_t {
     S_RIDX = S_RCEND, S_NONEROWS, S_LROWS, S_UMEDC, S_UMED,
     S_GLCT, S_GLCM, S_GLCE, S_GLCP, S_GLLW, S_GLEC, S_GLEO, S_GLXC, S_GLXO, S_GLCONS, S_GLE, S_GLIN,
     S_GLSRC, S_GLDST, S_GLSRC2, S_GLDST2, S_GLDEG, S_GLREM, S_GLXOFF, S_GLFL, S_GLFRONT, S_GLKEY, S_CFKU,
-    S_CNTX, S_INL, S_DFR, S_OVI, S_DTX,
+    S_CNTX, S_INL, S_DFR, S_OVI, S_DTX, S_POSOF,
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 192
@@ -330,7 +328,6 @@ int stage_prepare(ad_handle* h);
 int stage_sort(ad_handle* h);
 RadixScratch radix_scratch(ad_handle* h, size_t n);
 int stage_deps(ad_handle* h);
-int side_stream(ad_handle* h);
 int stage_merge(ad_handle* h);
 int stage_levels(ad_handle* h, bool want_order);
 int finish_order(ad_handle* h);

@@ -943,21 +943,23 @@ static __global__ __launch_bounds__(256) void k_level_pull(size_t n, const uint3
     }
 }
 // max of the per-workgroup maxima (one workgroup); strips LV_FINAL from the levels afterwards
-// Clears the FINAL bits and folds the greatest level into *maxl: per block one check-then-atomicMax (the level
-// is reached by the first blocks, so later blocks mostly only read it; no contended atomic on one address).
-static __global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L, uint32_t* maxl) {
-    __shared__ uint32_t wm[256 / WAVE];
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t v = 0;
-    if (t < n) { v = L[t] & ~LV_FINAL; L[t] = v; }
-    v = wave_max(v);
-    if (__lane_id() == 0) wm[threadIdx.x / WAVE] = v;
+// the greatest level from k_level_pull's per-block maxima (one workgroup); then the FINAL bits cleared
+static __global__ __launch_bounds__(1024) void k_level_pull_max(uint32_t nb, const uint32_t* __restrict__ bmax, uint32_t* out) {
+    __shared__ uint32_t wm[1024 / WAVE];
+    uint32_t m = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) m = bmax[i] > m ? bmax[i] : m;
+    m = wave_max(m);
+    if (__lane_id() == 0) wm[threadIdx.x / WAVE] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t x = wm[0];
-        for (int w = 1; w < 256 / WAVE; ++w) x = wm[w] > x ? wm[w] : x;
-        if (x > *(volatile uint32_t*)maxl) atomicMax(maxl, x);
+        uint32_t x = 0;
+        for (int w = 0; w < 1024 / WAVE; ++w) x = wm[w] > x ? wm[w] : x;
+        *out = x;
     }
+}
+static __global__ __launch_bounds__(256) void k_level_strip(size_t n, uint32_t* __restrict__ L) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) L[t] &= ~LV_FINAL;
 }
 
 // Deep graphs (C3: the hot key's ~10^5 Writes make ~10^5 levels, a handful of txns each): one launch per
@@ -1666,7 +1668,8 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                                                   ls.flags + 18);
                 k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
                                                  ls.sk1, ls.pull_force_abort ? 1 : 0);
-                k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl, ls.flags + 17);
+                k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
+                k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
                 if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 3, res)) {
                     err = "exec levels: device error";
                     return AD_ERR_DEVICE;
