@@ -224,6 +224,7 @@ class ShardStore:
         L.ad_shard_import_host.argtypes = [vp, C.c_void_p, C.c_uint32, u64p]
         L.ad_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ad_comm_init.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
+        L.ad_comm_destroy.argtypes = [vp]
         L.ad_shard_alltoall.argtypes = [vp, u64p]
         L.ad_shard_merge.argtypes = [vp, C.POINTER(abi.AdCsrSizes), C.POINTER(C.c_size_t)]
         L.ad_shard_fetch.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut), C.POINTER(C.c_uint32)]
@@ -304,6 +305,9 @@ class ShardStore:
     def comm_init(self, world, rank, uid):
         u = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
         self._check(self.L.ad_comm_init(self.eng.h, world, rank, u), "ad_comm_init")
+
+    def comm_destroy(self):
+        self._check(self.L.ad_comm_destroy(self.eng.h), "ad_comm_destroy")
 
 
     def merge(self):
@@ -528,6 +532,8 @@ class RcclTransport(GlooTransport):
         except engine.AccordDepsError as e:
             err = e
         if not self.all_ok(err is None):
+            if err is None:            # this rank's init succeeded, a peer's did not: drop the communicator
+                store.comm_destroy()
             raise RcclUnavailable("ncclCommInitRank failed on some rank%s" % (": %s" % err if err else ""))
 
     def all_ok(self, ok):

@@ -72,15 +72,38 @@ int union_overflow(ad_handle* h, LdsUnionArgs la, uint32_t* ovf_count, uint2* ov
 
 // Accept / GetDeps bound: per txn the number of batch TxnIds below its executeAt (TxnIds and executeAts share
 // one packed order; tx_ts ascends with the batch).
+// An executeAt below its TxnId is no valid Accept / GetDeps bound (executeAt >= TxnId, Timestamp order): flagged
+// (ERR_EXECBELOW -> AD_ERR_ARGUMENT) instead of answered from a wrong position.
 static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64_t* __restrict__ tx_ts, const uint64_t* __restrict__ ex1,
-                                                   uint32_t* __restrict__ qpos, int bound_max) {
+                                                   uint32_t* __restrict__ qpos, int bound_max, Params* prm) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (bound_max) { qpos[i] = (uint32_t)n; return; }   // Timestamp.MAX: every TxnId is below it
-    const uint64_t e = ex1[i] - 1;
-    size_t lo = i, hi = n;              // executeAt >= TxnId
-    while (lo < hi) { const size_t m = (lo + hi) >> 1; if (tx_ts[m] < e) lo = m + 1; else hi = m; }
-    qpos[i] = (uint32_t)lo;
+    bool bad = false;
+    if (i < n) {
+        if (bound_max) {
+            qpos[i] = (uint32_t)n;                          // Timestamp.MAX: every TxnId is below it
+        } else {
+            const uint64_t e1 = ex1[i];
+            bad = e1 == 0 || e1 - 1 < tx_ts[i];
+            const uint64_t e = e1 ? e1 - 1 : 0;
+            size_t lo = bad ? 0 : i, hi = n;                 // executeAt >= TxnId: the search starts at i
+            while (lo < hi) { const size_t m = (lo + hi) >> 1; if (tx_ts[m] < e) lo = m + 1; else hi = m; }
+            qpos[i] = (uint32_t)lo;
+        }
+    }
+    if (__ballot(bad) && __lane_id() == 0) atomicOr(&prm->err, (unsigned)ERR_EXECBELOW);
+}
+
+// Fills in the lone entries the deps stage's gather skipped (k_gather_entries<true>): called before anything
+// that reads every sorted entry (execution levels other than the pull pass, MaxConflicts, recovery, CFK retain,
+// sharded level passes).
+int complete_entries(ad_handle* h) {
+    if (!h->entries_partial) return AD_OK;
+    h->entries_partial = false;
+    const size_t P = h->P;
+    if (P) k_complete_singletons<<<ceil_div((long)P, 256), 256, 0, h->st>>>(P, h->sval, h->prec, h->skey, h->e_txn, h->e_meta,
+                                                                          h->e_exec1, h->ud_prev, h->pm_w, h->pm_c);
+    HIPCHK(h, hipGetLastError());
+    return AD_OK;
 }
 
 int stage_deps(ad_handle* h) {
@@ -102,7 +125,15 @@ int stage_deps(ad_handle* h) {
     for (int k = 0; k < nc; ++k) dirty_csr(h, cls[k]);
     for (int v = 0; v < nv; ++v) dirty_csr(h, CSR_RANGE0 + v);
     if (P > 0) {
-        { KScope ks(K_GATHER, P); k_gather_entries<<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->e_txn, h->e_meta, h->e_exec1); }
+        // lone entries skipped when nothing of this stage reads them (PreAccept bound: the executeAt-bound walks
+        // visit every entry; large / range txns query every key in their ranges)
+        const bool skip = !h->accept && h->n_large == 0 && Q == 0 && h->key_bits <= 32;
+        h->entries_partial = skip;
+        KScope ks(K_GATHER, P);
+        if (skip) k_gather_entries<true><<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->skey, h->e_txn, h->e_meta, h->e_exec1);
+        else k_gather_entries<false><<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->skey, h->e_txn, h->e_meta, h->e_exec1);
+    }
+    if (P > 0) {
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
                     h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm,
                     h->key_bits > 32 ? h->keys : nullptr, h->sval};
@@ -113,7 +144,7 @@ int stage_deps(ad_handle* h) {
     const uint32_t* qpos = nullptr;
     if (h->accept) {
         CK(dalloc(h, S_QPOS, &h->qpos, std::max<size_t>(n, 1)));
-        if (n) k_query_pos<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->tx_ts, h->ex1, h->qpos, h->bound_max ? 1 : 0);
+        if (n) k_query_pos<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->tx_ts, h->ex1, h->qpos, h->bound_max ? 1 : 0, h->prm);
         qpos = h->qpos;
     }
     // ---- virtual items of large txns

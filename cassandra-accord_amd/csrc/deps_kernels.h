@@ -70,7 +70,7 @@ struct Params {                // device-side batch statistics (filled by k_minm
                                                  // ephemeral reads, local-only): unmanaged execution
 };
 enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
-                  ERR_RANGEBITS = 32, ERR_CAP = 64 };
+                  ERR_RANGEBITS = 32, ERR_CAP = 64, ERR_EXECBELOW = 128 };
 
 __device__ inline unsigned long long wmin64(unsigned long long v) {
 #pragma unroll
@@ -235,16 +235,47 @@ static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64
 
 // Sorted entry SoA: one random 16-byte record read per entry (the pair's txn, meta and executeAt were
 // packed per pair by k_pack in pair order, i.e. coalesced), instead of three dependent random loads.
+// SKIP (batches of small key txns, 32-bit key spread, PreAccept bound): an entry alone in its key segment has no
+// entry before or after it, so no query of this batch reads it (the walks and the pull levels only visit
+// multi-entry segments); it gets a placeholder without the random read (C2: ~80% of entries), and
+// k_complete_singletons fills it in before anything that reads every entry (complete_entries).
+__device__ inline bool lone_entry(size_t s, size_t P, const uint32_t* __restrict__ skey) {
+    const uint32_t k = skey[s];
+    return (s == 0 || skey[s - 1] != k) && (s + 1 == P || skey[s + 1] != k);
+}
+template <bool SKIP>
 static __global__ __launch_bounds__(256) void k_gather_entries(size_t P, const uint32_t* __restrict__ sval,
-                                                        const PairRec* __restrict__ prec,
+                                                        const PairRec* __restrict__ prec, const uint32_t* __restrict__ skey,
                                                         uint32_t* __restrict__ e_txn, uint8_t* __restrict__ e_meta,
                                                         uint64_t* __restrict__ e_exec1) {
     size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P) return;
+    if (SKIP && lone_entry(s, P, skey)) {
+        e_txn[s] = 0; e_meta[s] = 0; e_exec1[s] = 0;
+        return;
+    }
     const PairRec r = prec[sval[s]];
     e_txn[s] = r.txn;
     e_meta[s] = (uint8_t)r.meta;
     e_exec1[s] = r.ex1;
+}
+// The lone entries k_gather_entries<true> skipped: their record, and the elision scan's state at them (a segment
+// head with nothing before it: ElideOp::load of the entry itself; seg_start is already theirs).
+static __global__ __launch_bounds__(256) void k_complete_singletons(size_t P, const uint32_t* __restrict__ sval,
+                                                             const PairRec* __restrict__ prec, const uint32_t* __restrict__ skey,
+                                                             uint32_t* __restrict__ e_txn, uint8_t* __restrict__ e_meta,
+                                                             uint64_t* __restrict__ e_exec1, int32_t* __restrict__ ud_prev,
+                                                             uint64_t* __restrict__ pm_w, uint64_t* __restrict__ pm_c) {
+    size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P || !lone_entry(s, P, skey)) return;
+    const PairRec r = prec[sval[s]];
+    e_txn[s] = r.txn;
+    e_meta[s] = (uint8_t)r.meta;
+    e_exec1[s] = r.ex1;
+    const uint32_t cat = category(r.meta);
+    ud_prev[s] = cat == CAT_ALWAYS ? (int32_t)s : -1;
+    pm_c[s] = cat == CAT_ELIDABLE ? r.ex1 : 0ull;
+    pm_w[s] = (cat == CAT_ELIDABLE && meta_kind(r.meta) == AD_KIND_WRITE) ? r.ex1 : 0ull;
 }
 
 // Segmented prefix state of CommandsForKey.mapReduceActive over the (key, TxnId)-sorted entries.

@@ -190,6 +190,7 @@ int check_params(ad_handle* h) {
     if (e & ERR_KEYORDER) return set_err(h, AD_ERR_ARGUMENT, "a txn's keys must be strictly ascending (Keys), and range txns carry no keys");
     if (e & ERR_RANGEORDER) return set_err(h, AD_ERR_ARGUMENT, "a txn's ranges must be sorted, disjoint, start < end (Ranges), and key txns carry no ranges");
     if (e & ERR_CAP) return set_err(h, AD_ERR_UNSUPPORTED, "more than 8192 dependency entries in one txn's CSR (LDS union capacity)");
+    if (e & ERR_EXECBELOW) return set_err(h, AD_ERR_ARGUMENT, "ad_accept_deps: an executeAt below its TxnId is no Accept / GetDeps bound");
     return AD_OK;
 }
 
@@ -653,6 +654,7 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
+    CK(complete_entries(h));
     const size_t n = h->n, P = h->P;
     const int nv = (int)h->cfg.replicas;
     hipStream_t st = h->st;
@@ -825,6 +827,7 @@ int ad_recover(ad_handle* h, const uint32_t* rows, size_t nq, size_t* entries) {
         if (rows[q] >= h->n) return set_err(h, AD_ERR_ARGUMENT, "ad_recover: row " + std::to_string(rows[q]) + " out of range");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
+    CK(complete_entries(h));
     hipStream_t st = h->st;
     h->rc_ready = false;
     uint32_t *drows = nullptr, *cnt = nullptr, *off = nullptr;

@@ -146,6 +146,7 @@ struct ad_handle {
     bool mc_ready = false;           // the MaxConflicts scan of the current batch is on the device (export)
     const uint8_t* mc_fast = nullptr;  // [replicas * n] fast-path flags of the last ad_max_conflicts(_ts)
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
+    bool entries_partial = false;    // the deps stage skipped the lone entries' gather (complete_entries)
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
     bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
@@ -328,6 +329,7 @@ int stage_prepare(ad_handle* h);
 int stage_sort(ad_handle* h);
 RadixScratch radix_scratch(ad_handle* h, size_t n);
 int stage_deps(ad_handle* h);
+int complete_entries(ad_handle* h);
 int stage_merge(ad_handle* h);
 int stage_levels(ad_handle* h, bool want_order);
 int finish_order(ad_handle* h);

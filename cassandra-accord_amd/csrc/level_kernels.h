@@ -1275,6 +1275,8 @@ struct LevelInputs {
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
     int force_blocks;                    // pure key-chain batches: executeAt blocks even for short chains (tests)
+    int (*complete)(void*);              // nullable: fills in every sorted entry before a path other than the pull pass
+    void* complete_ctx;
     uint32_t* order_verify;              // optimistic order: host-mapped word (device address) receiving the fast-path
                                          // failure flag; null: the order syncs on its own check
     bool* order_pending;                 // set when the caller must check *order_verify after its sync
@@ -1674,6 +1676,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     err = "exec levels: device error";
                     return AD_ERR_DEVICE;
                 }
+            }
+            if ((lng || res[0] || res[2]) && in.complete && in.complete(in.complete_ctx) != AD_OK) {
+                err = "exec levels: device error";
+                return AD_ERR_DEVICE;
             }
             if (lng) return block_path();                                  // deep key chains: executeAt blocks
             ls.pull_path = res[2] ? 2 : (res[0] ? 3 : 1);                   // 1 pulled, 2 far predecessors, 3 aborted

@@ -62,6 +62,13 @@ int stage_levels(ad_handle* h, bool want_order) {
     }
     li.order_pending = &h->order_pending;
     int iters = 0;
+    // only the pull pass reads nothing but multi-entry key segments; every other level path reads every entry
+    const bool pull_first = li.kahn_ok && !li.force_blocks && h->P > 0 && !h->ls.pull_off && h->n_large == 0 &&
+                            h->n_special == 0 && h->merged[AD_CLASS_DIRECT_KEY].ncap == 0 &&
+                            !(h->merged_has_range && h->merged[AD_CLASS_RANGE].ncap > 0);
+    if (!pull_first) CK(complete_entries(h));
+    li.complete = [](void* x) { return complete_entries((ad_handle*)x); };
+    li.complete_ctx = h;
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
     if (rc != AD_OK) return rc;
     h->level_iters = (uint32_t)iters;
@@ -100,6 +107,7 @@ void levels_order_rows(ad_handle* h, size_t m, const uint32_t* rows, uint32_t* o
 // one-exchange sharded levels (global_levels.h)
 // ---------------------------------------------------------------------------------------------------
 int levels_export_edges(ad_handle* h, size_t* m_out, bool global_ranks, bool done_aware) {
+    CK(complete_entries(h));
     const size_t n = h->n, P = h->P;
     hipStream_t st = h->st;
     const uint32_t* gid = global_ranks ? h->gid : nullptr;

@@ -16,6 +16,7 @@ int ad_cfk_retain(ad_handle* h, size_t* retained) {
     if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_retain: key batches only (no range txns)");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
+    CK(complete_entries(h));
     hipStream_t st = h->st;
     const size_t n = h->n, P = h->P;
     const uint32_t* gid = h->hist_active ? h->gid : nullptr;
@@ -424,6 +425,19 @@ int ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id_
     return AD_OK;
 }
 
+// Tears the handle's communicator down (ncclCommAbort: the peers may have failed their init, so no collective
+// teardown); the handle can then take another ad_comm_init or stay on a host transport.
+int ad_comm_destroy(ad_handle* h) {
+    if (!h) return AD_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    if (h->comm) {
+        hipStreamSynchronize(h->st);
+        ncclCommAbort(h->comm);
+        h->comm = nullptr;
+    }
+    return AD_OK;
+}
+
 // RCCL all-to-all of the per-destination blobs over xGMI (grouped point-to-point send/recv; the recv
 // sizes come from the peers' export sizes, exchanged by the caller).
 int ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world] */) {
@@ -574,6 +588,7 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     g_tracer = &h->tracer;
     if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_levels_round: sharded deps first");
     hipSetDevice(h->device);
+    CK(complete_entries(h));
     hipStream_t st = h->st;
     const size_t n = h->n;
     // Unmanaged txns (range txns, key-domain sync points / ephemeral reads) and the key txns depending on range

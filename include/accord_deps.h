@@ -417,6 +417,9 @@ int  ad_shard_import_host(ad_handle* h, const void* src /* blobs in source order
                           const uint64_t* sizes /* [world] */);
 int  ad_comm_unique_id(uint8_t* out /* [128] */);
 int  ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id /* [128] */);
+/* Aborts and releases the handle's communicator (a partial init across ranks: the ranks whose init succeeded
+ * drop theirs before falling back to a host transport).  No-op without one. */
+int  ad_comm_destroy(ad_handle* h);
 int  ad_shard_alltoall(ad_handle* h, const uint64_t* recv_sizes /* [world]: peers' bytes[this store] */);
 int  ad_shard_merge(ad_handle* h, ad_csr_sizes* sizes /* [(replicas+1)*3]; view == replicas: merged */, size_t* n_home);
 int  ad_shard_fetch(ad_handle* h, uint32_t view, uint32_t cls, ad_csr_out* out, uint32_t* home_gid /* [n_home] or NULL */);

@@ -45,6 +45,8 @@ CASES = {
     "hot_keys": (lambda: workload.generate(2000, keys_per_txn=2, keyspace=5, slow_frac=0.5, bump_max=300, seed=11),
                  (4, 2, 0.3, 11), True),
     "mixed_kinds": (lambda: mixed_kinds(1500, 12), (8, 3, 0.2, 12), False),
+    # all five kinds with their execution levels / order frozen too (sync points' byId fold, awaitsOnlyDeps)
+    "mixed_kinds_levels": (lambda: mixed_kinds(1500, 13), (8, 3, 0.2, 13), True),
     # the reference's own seeded RangeDepsTest inputs (tests/refgen.py; tests/test_oracle_rangedeps.py checks the
     # oracle on them against RangeDepsTest.Validate's model): testRandom's first recorded seed and the first
     # nemesis layout of testNemesisRanges' recorded seed, as engine batches of range Writes + Validate's queries

@@ -118,3 +118,17 @@ def test_ephemeral_read_deps_bound_max(engine_factory, case):
     for i in range(0, b["n"], 97):
         later += int((got.txn(i)[1] > i).sum())
     assert later > 0
+
+
+def test_accept_rejects_executeat_below_txnid(engine_factory):
+    # an executeAt below its TxnId is no Accept / GetDeps bound (the arrival search assumes
+    # executeAt >= TxnId); the batch is refused with IllegalArgumentException, and PreAccept on it still works
+    from accord_amd import engine
+    b = workload.config("C2", n=5000)
+    b["exec_lsb"] = b["exec_lsb"].copy()
+    b["exec_lsb"][1234] = b["txn_lsb"][1234] - np.uint64(7 << 16)
+    eng = engine_factory()
+    eng.load(b)
+    with pytest.raises(engine.IllegalArgumentException):
+        eng.accept_deps()
+    eng.preaccept_deps()
