@@ -69,7 +69,8 @@ class AdStageTimes(C.Structure):
                 ("level_iterations", C.c_uint32), ("walk_items", C.c_uint32),
                 ("level_blocks", C.c_uint32), ("level_rounds", C.c_uint32),
                 ("key_classes", C.c_uint32), ("level_path", C.c_uint32),
-                ("deferred_txns", C.c_uint32), ("fill_items", C.c_uint32)]
+                ("deferred_txns", C.c_uint32), ("fill_items", C.c_uint32),
+                ("deps_speculative", C.c_uint32)]
 
 
 def ptr(a, ctype):

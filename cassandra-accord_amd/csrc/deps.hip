@@ -233,8 +233,43 @@ int stage_deps(ad_handle* h) {
     tt.src[tt.count++] = heavy;
     tt.src[tt.count++] = items_count;
     tt.src[tt.count++] = dtx_count;
+    // Speculative finish (small key batches whose key-class buffers from an earlier batch exist): k_txn_finish is
+    // enqueued BEFORE the host reads the totals, into those buffers, behind k_cap_check's guard (a CSR total beyond
+    // its buffer's capacity makes every thread exit).  The host reads the totals while the finish runs and re-runs
+    // it after sizing only if the guard fired: no host round trip between the offsets scan and the finish.
+    uint32_t* spec_bad = heavy - 3;
+    bool spec = n > 0 && h->V == 0 && Q == 0;
+    CapCheck capc{};
+    for (int k = 0; k < nc && spec; ++k) {
+        const int c = cls[k];
+        const size_t base = S_CSR0 + 10 * (size_t)c;
+        const size_t ck = csr_cap(h, c, 4, 8), cm = csr_cap(h, c, 5, 4), ct = csr_cap(h, c, 6, 4);
+        if (!ck || !cm || !ct) { spec = false; break; }
+        Csr& x = h->deps[c];
+        const uint32_t* tots[3] = {x.key_off + n, x.k2t_off + n, x.ent_off + n};
+        const size_t caps[3] = {ck, cm, ct};
+        for (int q = 0; q < 3; ++q) { capc.tot[capc.m] = tots[q]; capc.cap[capc.m++] = (uint32_t)std::min<size_t>(caps[q], 0xFFFFFFFFu); }
+        ta.out_key_off[k] = x.key_off; ta.out_k2t_off[k] = x.k2t_off; ta.out_ent_off[k] = x.ent_off; ta.out_tcnt[k] = x.tcnt;
+        ta.out_keys[k] = (uint64_t*)h->bufs[base + 4].p; ta.out_k2t[k] = (int32_t*)h->bufs[base + 5].p;
+        ta.out_txns[k] = (uint32_t*)h->bufs[base + 6].p;
+    }
+    ta.inl = h->inl; ta.dfr = h->dfr; ta.nrows = n;
+    if (spec) {
+        capc.bad = spec_bad;
+        k_cap_check<<<1, 64, 0, st>>>(capc);
+        tt.src[tt.count++] = spec_bad;
+    }
     std::vector<uint32_t> got(tt.count, 0);
-    CK(read_totals_params(h, tt, got.data()));
+    uint32_t seq = 0;
+    CK(publish_totals(h, tt, got.data(), &seq));       // the read-back first, then the speculative finish
+    if (spec) {
+        ta.w = wa;
+        ta.spec_bad = spec_bad;
+        KScope ks(K_TXN_LAYOUT, n);
+        launch_finish_nv(nv, ta, direct, st);
+        ta.spec_bad = nullptr;
+    }
+    CK(wait_totals(h, seq, tt.count, got.data()));
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
     // k_txn_finish completes every small txn whose pairs kept all their ids inline; only the deferred ones need
     // the fill walk and the union (none on most C2 batches)
@@ -270,9 +305,11 @@ int stage_deps(ad_handle* h) {
     }
     // small txns: k_txn_finish (re-walking in place the pairs that overflowed their inline ids); txns with more
     // than 4 keys (deferred) get their layout there and their lists from the fill walk of their pairs + k_txn_union
-    ta.nrows = n;
+    // (unless the speculative launch above already did it)
+    const bool spec_ok = spec && got[ncol + 3] == 0;
+    h->times.deps_speculative = spec ? (spec_ok ? 1u : 2u) : 0u;
     ta.w = wa;
-    if (n > 0) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
+    if (n > 0 && !spec_ok) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
     wa.items = items; wa.nitems = nitems;
     launch_walk_nv(nv, wa, true, direct, nitems > 0, st);

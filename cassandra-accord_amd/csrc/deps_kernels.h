@@ -621,6 +621,7 @@ struct TxnArgs {
     const uint32_t* inl;          // the count walk's inline ids [(p * nvc + vc) * WALK_INL + q], descending
     const uint8_t* dfr;           // [txn] deferred to the fill walk + k_txn_union
     size_t nrows;                 // k_txn_finish: txns
+    const uint32_t* spec_bad;     // k_txn_finish launched before the sizes reached the host: exit when set
     WalkArgs w;                   // k_txn_finish re-walks the pairs that overflowed their inline ids (w.posof)
     uint32_t* dst;                // AoS by pair [p * nvc + vc]
     Params* prm;
@@ -868,13 +869,30 @@ __device__ inline uint32_t union_small(int32_t* __restrict__ k2t, uint32_t mb, u
 // latency hides behind the other threads instead of forming a serial chain of small launches.  Txns with more
 // than 4 keys (deferred: dfr) only get their layout and the fill walk's dst slots; walk<fill> + k_txn_union
 // finish them.  Grid (txns, classes): the offsets, counts and keys are loaded before the ids and the first store.
+// The speculative k_txn_finish's guard: some CSR total exceeds the capacity of the buffer it was launched into.
+struct CapCheck {
+    const uint32_t* tot[3 * NVC_MAX];
+    uint32_t cap[3 * NVC_MAX];
+    int m;
+    uint32_t* bad;
+};
+static __global__ __launch_bounds__(64) void k_cap_check(CapCheck a) {
+    const int l = threadIdx.x;
+    const bool over = l < a.m && *a.tot[l] > a.cap[l];
+    const uint64_t m = __ballot(over);
+    if (l == 0) *a.bad = m ? 1u : 0u;
+}
+
 template <int NV, bool DIRECT>
 static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     constexpr int NVC = DIRECT ? 2 * NV : NV;
+    if (a.spec_bad && *a.spec_bad) return;          // speculative launch into too-small buffers: re-run after sizing
+    // class-minor lanes: the NVC threads of one txn are neighbours, so their shared per-txn loads (key_off, meta,
+    // counts, keys) fall on the same lines within a wave instead of being fetched once per class pass
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
-    if (x >= a.nrows) return;
-    const size_t t = x;
+    if (x >= a.nrows * NVC) return;
+    const size_t t = x / NVC;
+    const int c = (int)(x - t * NVC);
     const uint32_t kb = a.out_key_off[c][t], ke = a.out_key_off[c][t + 1];
     const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
     const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];

@@ -24,7 +24,7 @@ void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy, 
 }
 template <int NV>
 void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
-    const dim3 g((unsigned)ceil_div((long)ta.nrows, 256), direct ? 2 * NV : NV);
+    const unsigned g = (unsigned)ceil_div((long)ta.nrows * (direct ? 2 * NV : NV), 256);
     if (direct) k_txn_finish<NV, true><<<g, 256, 0, st>>>(ta);
     else k_txn_finish<NV, false><<<g, 256, 0, st>>>(ta);
 }

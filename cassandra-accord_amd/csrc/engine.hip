@@ -134,19 +134,29 @@ static int pub_ready(ad_handle* h) {
     h->pub_dev = (uint32_t*)d;
     return AD_OK;
 }
-int read_totals_params(ad_handle* h, const TotTable& t, uint32_t* host) {
-    if (pub_ready(h) != AD_OK) {        // no mapped memory: copy + stream sync
+// Two halves so work can be enqueued between the publish and the wait (the speculative finish / merge write):
+// publish_totals enqueues the read-back, wait_totals spins on it.
+int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* seq_out) {
+    if (pub_ready(h) != AD_OK) {        // no mapped memory: copy (the wait is a stream sync)
         if (t.count > 0) {
             k_collect_totals<<<1, MAX_TOTALS, 0, h->st>>>(t, h->totd);
             HIPCHK(h, hipMemcpyAsync(host, h->totd, (size_t)t.count * 4, hipMemcpyDeviceToHost, h->st));
         }
         HIPCHK(h, hipMemcpyAsync(&h->hprm, h->prm, sizeof(Params), hipMemcpyDeviceToHost, h->st));
-        HIPCHK(h, hipStreamSynchronize(h->st));
+        *seq_out = 0;
         return AD_OK;
     }
     const uint32_t seq = ++h->pub_seq;
     k_publish<<<1, 128, 0, h->st>>>(t, h->prm, h->pub_dev, seq);
     HIPCHK(h, hipGetLastError());
+    *seq_out = seq;
+    return AD_OK;
+}
+int wait_totals(ad_handle* h, uint32_t seq, int count, uint32_t* host) {
+    if (seq == 0) {
+        HIPCHK(h, hipStreamSynchronize(h->st));
+        return AD_OK;
+    }
     volatile uint32_t* flag = h->pub_host;
     uint64_t spins = 0;
     const auto t0 = std::chrono::steady_clock::now();
@@ -165,9 +175,14 @@ int read_totals_params(ad_handle* h, const TotTable& t, uint32_t* host) {
             }
         }
     }
-    if (t.count > 0) std::memcpy(host, h->pub_host + PUB_TOT, (size_t)t.count * 4);
+    if (count > 0) std::memcpy(host, h->pub_host + PUB_TOT, (size_t)count * 4);
     std::memcpy(&h->hprm, h->pub_host + PUB_PRM, sizeof(Params));
     return AD_OK;
+}
+int read_totals_params(ad_handle* h, const TotTable& t, uint32_t* host) {
+    uint32_t seq = 0;
+    CK(publish_totals(h, t, host, &seq));
+    return wait_totals(h, seq, t.count, host);
 }
 // the level stage's flag read-backs share the handle's mapped buffer (the totals region)
 void set_level_pub(ad_handle* h) {

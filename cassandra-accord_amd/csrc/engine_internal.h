@@ -298,6 +298,8 @@ struct TotTable { const uint32_t* src[MAX_TOTALS]; int count; };
 void csr_offsets(ad_handle* h, Csr& c, const uint32_t* nk, const uint32_t* ne);
 // The [n] totals of several device offset arrays and the batch Params -> host (engine.hip: k_publish)
 int read_totals_params(ad_handle* h, const TotTable& t, uint32_t* host);
+int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* seq_out);
+int wait_totals(ad_handle* h, uint32_t seq, int count, uint32_t* host);
 void set_level_pub(ad_handle* h);
 int read_params(ad_handle* h);
 int check_params(ad_handle* h);

@@ -25,6 +25,7 @@
 //      the critical path (C2: ~9).
 //   5. order: LSD radix sorts by executeAt (64-bit, two 32-bit halves) then stably by level.
 #pragma once
+#include <functional>
 #include <chrono>
 #include <cstring>
 
@@ -1151,15 +1152,18 @@ struct Publisher {
     int off = 0, cap = 0;               // the words this user may write: [off, off + cap)
 };
 // a[0..na) -> ha, b[0..nb) -> hb, waiting on the mapped buffer (else a copy + stream sync)
+// between (nullable): work enqueued after the read-back and before the host waits for it (speculation)
 inline bool publish_read(const Publisher& p, hipStream_t st, const uint32_t* a, int na, uint32_t* ha,
-                         const uint32_t* b, int nb, uint32_t* hb) {
+                         const uint32_t* b, int nb, uint32_t* hb, const std::function<void()>* between = nullptr) {
     if (!p.host || na + nb > p.cap || na > 128 || nb > 128) {
         if (na && hipMemcpyAsync(ha, a, (size_t)na * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
         if (nb && hipMemcpyAsync(hb, b, (size_t)nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+        if (between) (*between)();
         return hipStreamSynchronize(st) == hipSuccess;
     }
     const uint32_t seq = ++*p.seq;
     k_publish2<<<1, 128, 0, st>>>(a, na, b, nb, p.dev, p.off, seq);
+    if (between) (*between)();
     uint64_t spins = 0;
     const auto t0 = std::chrono::steady_clock::now();
     while (__atomic_load_n(p.host, __ATOMIC_ACQUIRE) != seq) {
@@ -1336,7 +1340,7 @@ static __global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uin
 // flags[0] = max level, flags[1] |= 1 unless okey ascends and every slot is filled
 static __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ oidx,
                                                     const uint32_t* __restrict__ olvl, uint32_t* __restrict__ flags,
-                                                    uint32_t* fail_out) {
+                                                    uint32_t* fail_out, uint32_t max_level) {
     uint32_t v = 0;
     bool bad = false;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
@@ -1354,6 +1358,7 @@ static __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint6
         uint32_t mx = red[0], b = rb[0];
         for (int k = 1; k < 256 / WAVE; ++k) { mx = mx > red[k] ? mx : red[k]; b |= rb[k]; }
         atomicMax(&flags[0], mx);
+        if (mx > max_level) b = 1;                                 // the optimistic level pass was too narrow
         if (b) atomicOr(&flags[1], 1u);
         if (b && fail_out) *(volatile uint32_t*)fail_out = 1u;    // host-mapped: read after the caller's sync
     }
@@ -1404,7 +1409,8 @@ inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     // fast path: windowed inversion ranks + verification
     fill_multi(st, {{of, 8, 0}, {v, m * 4, 0xFF}});           // flags; WR_EMPTY: detects rank collisions
     k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1);
-    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, of, optimistic ? verify_dev : nullptr);
+    k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, of, optimistic ? verify_dev : nullptr,
+                                     optimistic ? (uint32_t)known_maxl : 0xFFFFFFFFu);
     if (optimistic) {
         fl[0] = (uint32_t)known_maxl;
     } else {
@@ -1662,6 +1668,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             ls.chains_ready = false;
             uint32_t lng = 0, res[3] = {0, 0, 0};
             {
+                {
                 KScope ks(K_KAHN, P);
                 const int gn = ceil_div((long)n, 256);
                 // predecessor runs zeroed above; ls.flags [16] abort, [17] max level, [18] far pred (zeroed above)
@@ -1672,9 +1679,24 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                                                  ls.sk1, ls.pull_force_abort ? 1 : 0);
                 k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
                 k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
-                if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 3, res)) {
+                }
+                // the order of the pulled levels, enqueued before the host waits on the pull's flags: one 8-bit
+                // level pass (levels up to 255; k_rank_check flags a deeper batch, then finish_order redoes it)
+                bool spec_order = false;
+                const std::function<void()> spec = [&]() {
+                    if (want_order && n > 0 && in.order_verify) {
+                        *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, 255, in.order_verify);
+                        spec_order = true;
+                    }
+                };
+                if (!publish_read(ls.pub, st, ls.flags + 7, 1, &lng, ls.flags + 16, 3, res, &spec)) {
                     err = "exec levels: device error";
                     return AD_ERR_DEVICE;
+                }
+                if (spec_order && !lng && !res[0] && !res[2]) {
+                    ls.pull_path = 1;
+                    *iters = (int)res[1] + 1;
+                    return AD_OK;
                 }
             }
             if ((lng || res[0] || res[2]) && in.complete && in.complete(in.complete_ctx) != AD_OK) {

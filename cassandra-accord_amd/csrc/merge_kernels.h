@@ -17,6 +17,7 @@ namespace ad {
 struct MergeArgs {
     size_t n;
     int nv;
+    const uint32_t* spec_bad;    // write pass launched before the merged sizes reached the host: exit when set
     const uint32_t* key_off[MAXV];
     const uint64_t* keys[MAXV];
     const uint32_t* k2t_off[MAXV];
@@ -60,6 +61,7 @@ template <int NV, bool WRITE, int KW>
 static __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n) return;
+    if (WRITE && a.spec_bad && *a.spec_bad) return;   // speculative write into too-small buffers: re-run after sizing
     constexpr uint32_t INF = 0xFFFFFFFFu;
     // ---- 1. union of TxnId rank lists
     // input row of output txn t in each part (shard merge: a global txn's row in each source, -1 = absent)
@@ -228,6 +230,7 @@ template <int NV, bool WRITE, int KW>
 static __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
     constexpr uint32_t INF = 0xFFFFFFFFu;
     __shared__ uint32_t sU[WRITE ? MH_LDS : 1];
+    if (WRITE && a.spec_bad && *a.spec_bad) return;
     const uint32_t H = *a.hcount;
     for (uint32_t hi = blockIdx.x; hi < H; hi += gridDim.x) {
         const uint32_t t = a.hlist[hi];

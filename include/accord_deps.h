@@ -296,8 +296,10 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
                                     /* predecessor (> 65536 rows ahead) -> Kahn, 3 aborted -> Kahn   */
     uint32_t deferred_txns;         /* small txns the walk's inline ids could not finish: unioned by  */
                                     /* k_txn_union (the rest by k_txn_finish)                         */
-    uint32_t fill_items;            /* (txn, key) entries the fill walk re-walks (overflowed pairs,    */
-                                    /* pairs of txns with more than 4 keys)                           */
+    uint32_t fill_items;            /* (txn, key) entries the fill walk re-walks (pairs of txns with   */
+                                    /* more than 4 keys)                                              */
+    uint32_t deps_speculative;      /* k_txn_finish launched before the CSR sizes reached the host:    */
+                                    /* 0 no, 1 yes and the buffers fit, 2 yes but re-run after sizing  */
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
