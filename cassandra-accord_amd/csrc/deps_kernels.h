@@ -919,10 +919,9 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     uint32_t cc[4];
     uint64_t kx[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        cc[j] = b + j < e ? pair_count(a.cnt8, a.cntx, NCB, NVC, b + j, c) : 0u;
-        kx[j] = b + j < e ? a.keys[b + j] : 0ull;
-    }
+    for (int j = 0; j < 4; ++j) cc[j] = b + j < e ? pair_count(a.cnt8, a.cntx, NCB, NVC, b + j, c) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kx[j] = cc[j] > 0 ? a.keys[b + j] : 0ull;     // only the keys with entries
     bool ovf = false;                               // some list of this class overflowed its inline ids
 #pragma unroll
     for (int j = 0; j < 4; ++j) ovf |= cc[j] > (uint32_t)WALK_INL;

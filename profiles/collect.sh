@@ -25,7 +25,10 @@ echo "fetch done"
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
     python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 > "$OUT/write.log" 2>&1
 echo "write done"
-# 4. the other BASELINE configs on one GPU (secondary lines: C3 Zipf deep chains, C4 4M mixed key + range)
+# 4. the CPU baseline's extrapolation check: the T-thread oracle once over the full C2 batch
+timeout -k 10 600 python3 -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 --no-e2e --cpu-full > "$OUT/cpu_full.json" 2> "$OUT/cpu_full.err"
+echo "cpu full done"
+# 5. the other BASELINE configs on one GPU (secondary lines: C3 Zipf deep chains, C4 4M mixed key + range)
 timeout -k 10 300 python3 -u "$ROOT/bench.py" --config C3 --steps 5 --warmup 2 --breakdown > "$OUT/c3.json" 2> "$OUT/c3.err"
 echo "c3 done"
 timeout -k 10 400 python3 -u "$ROOT/bench.py" --config C4 --steps 2 --warmup 1 --breakdown > "$OUT/c4.json" 2> "$OUT/c4.err"
