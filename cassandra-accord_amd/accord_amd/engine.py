@@ -101,7 +101,7 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
-            "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_alltoall", "ad_shard_merge",
+            "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
             "ad_shard_levels_allreduce", "ad_shard_order", "ad_shard_set_holders", "ad_shard_levels_deltas",
             "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows", "ad_cfk_update",

@@ -225,6 +225,7 @@ class ShardStore:
         L.ad_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ad_comm_init.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
         L.ad_comm_destroy.argtypes = [vp]
+        L.ad_shard_query_positions.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.ad_shard_alltoall.argtypes = [vp, u64p]
         L.ad_shard_merge.argtypes = [vp, C.POINTER(abi.AdCsrSizes), C.POINTER(C.c_size_t)]
         L.ad_shard_fetch.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrOut), C.POINTER(C.c_uint32)]
@@ -267,6 +268,16 @@ class ShardStore:
             self.holders = np.ascontiguousarray(holders, np.uint8)
             self._check(self.L.ad_shard_set_holders(self.eng.h, self.holders.ctypes.data_as(C.POINTER(C.c_uint8))),
                         "ad_shard_set_holders")
+
+    def accept(self, gq=None, bound_max=False):
+        """Accept / GetDeps deps of the slice (bound = executeAt; gq = the global arrival positions of the local
+        rows' executeAts, query_positions), or GetEphemeralReadDeps (bound = Timestamp.MAX)."""
+        if bound_max:
+            self.eng.ephemeral_read_deps()
+            return
+        g = np.ascontiguousarray(gq, np.uint32)
+        self._check(self.L.ad_shard_query_positions(self.eng.h, _u32p(g)), "ad_shard_query_positions")
+        self.eng.accept_deps()
 
     def preaccept(self):
         self._check(self.L.ad_preaccept_deps(self.eng.h, None), "ad_preaccept_deps")
@@ -411,6 +422,17 @@ class ShardStore:
         od = np.zeros(max(self.n_home, 1), np.uint32)
         self._check(self.L.ad_shard_order(self.eng.h, _u32p(lv), _u32p(od)), "ad_shard_order")
         return lv[:self.n_home], od[:self.n_home]
+
+
+def query_positions(batch):
+    """Per txn of the global batch, the number of its TxnIds below the txn's executeAt under Timestamp.compareTo
+    (Timestamp.java:208-217): where an Accept / GetDeps query with bound executeAt is answered."""
+    def key(msb, lsb, node):
+        return (int(msb), int(lsb) >> 16, int(lsb) & 0x1E, int(node))
+    import bisect
+    tx = [key(batch["txn_msb"][i], batch["txn_lsb"][i], batch["txn_node"][i]) for i in range(batch["n"])]
+    return np.array([bisect.bisect_left(tx, key(batch["exec_msb"][i], batch["exec_lsb"][i], batch["exec_node"][i]))
+                     for i in range(batch["n"])], np.uint32)
 
 
 def unique_id():
@@ -613,9 +635,14 @@ class LocalTransport:
     """Several stores in one process (tests): the same protocol with in-process exchange."""
 
     @staticmethod
-    def run(stores, max_rounds=1 << 16, levels="gather"):
+    def run(stores, max_rounds=1 << 16, levels="gather", deps="preaccept", gq=None):
+        """deps: "preaccept", "accept" (gq: the global query positions, query_positions) or "ephemeral";
+        levels None: stop after the home merge."""
         for s in stores:
-            s.preaccept()
+            if deps == "preaccept":
+                s.preaccept()
+            else:
+                s.accept(None if gq is None else gq[s.gid], bound_max=deps == "ephemeral")
         sizes = [s.export() for s in stores]
         bufs = [s.send_buffer() for s in stores]
         offs = [np.concatenate([[0], np.cumsum(z)]).astype(np.int64) for z in sizes]
@@ -624,6 +651,8 @@ class LocalTransport:
             s.import_host(np.concatenate(parts) if parts else np.zeros(0, np.uint8),
                           np.array([sizes[k][d] for k in range(len(stores))], np.uint64))
             s.merge()
+        if levels is None:
+            return 0
         if levels == "gather":
             edges = np.concatenate([s.level_edges() for s in stores])
             for s in stores:

@@ -189,6 +189,7 @@ int stage_deps(ad_handle* h) {
     wa.V = h->V; wa.vi_txn = h->vi_txn; wa.vi_pos = h->vi_pos; wa.vi_u = h->vi_u; wa.useg = h->useg;
     wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
     wa.qpos = qpos; wa.ex1 = h->ex1; wa.bound_max = h->bound_max ? 1 : 0;
+    wa.gqpos = (h->accept && h->sharded) ? h->gqpos : nullptr;
     // [deferred txns, items, heavy-merge hint]; the pairs' counts (segment heads keep zero); deferred flags
     fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
     launch_walk_nv(nv, wa, false, direct, true, st);
@@ -214,6 +215,7 @@ int stage_deps(ad_handle* h) {
     ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
     ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
     ra.qpos = qpos;
+    ra.gqpos = wa.gqpos;
     ra.gid = wa.gid;
     if (Q > 0 && n > 0) {
         launch_range_nv(nv, ra, false, st);

@@ -399,6 +399,8 @@ struct WalkArgs {
     // executeAt-bound queries (Accept / GetDeps; nullable = PreAccept, bound TxnId): per txn the arrival position
     // of its bound, q = #{j : TxnId_j < executeAt_i}; ex1 = executeAt + 1
     const uint32_t* qpos;
+    const uint32_t* gqpos;    // sharded stores: the bound's GLOBAL arrival position per local row (window placement;
+                              // qpos stays the local position for the segment search); nullable = qpos
     const uint64_t* ex1;
     int bound_max;            // GetEphemeralReadDeps: bound Timestamp.MAX (qpos = n; no executeAt bound)
     __device__ uint64_t bound1(uint32_t i) const { return bound_max ? ~0ull : ex1[i]; }
@@ -514,7 +516,7 @@ __device__ inline void walk_entry(const WalkArgs& a, size_t s, uint32_t i, uint3
             const size_t m = (lo + hi) >> 1;
             if (a.seg_start[m] == seg0 && a.e_txn[m] < qi) lo = m + 1; else hi = m;
         }
-        walk_query<NV>(a, i, a.gid ? a.gid[i] : qi, a.bound1(i), qk, (int)lo, seg0, emit);
+        walk_query<NV>(a, i, a.gqpos ? a.gqpos[i] : qi, a.bound1(i), qk, (int)lo, seg0, emit);
     } else {
         const uint32_t gi = a.gid ? a.gid[i] : i;
         walk_query<NV>(a, i, gi, a.tx_ts[i] + 1, qk, (int)s, seg0, emit);
@@ -592,7 +594,7 @@ static __global__ __launch_bounds__(256) void k_vitem_walk(WalkArgs a) {
         else c[vc]++;
     };
     if (qk <= AD_KIND_EXCLUSIVE_SYNC_POINT) {
-        const uint32_t gq = a.qpos ? a.qpos[i] : (a.gid ? a.gid[i] : i);
+        const uint32_t gq = a.qpos ? (a.gqpos ? a.gqpos[i] : a.qpos[i]) : (a.gid ? a.gid[i] : i);
         walk_query<NV>(a, i, gq, a.qpos ? a.bound1(i) : a.tx_ts[i] + 1, qk, (int)a.vi_pos[x], (int)a.useg[a.vi_u[x]], emit);
     }
     if (!FILL) {

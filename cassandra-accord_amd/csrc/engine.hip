@@ -551,6 +551,7 @@ int ad_load_batch(ad_handle* h, const ad_batch* b) {
     CK(load_working(h));
     HIPCHK(h, hipStreamSynchronize(st));
     h->loaded = true;
+    h->gq_ready = false;
     return AD_OK;
 }
 
@@ -607,6 +608,7 @@ int ad_load_batch_commit(ad_handle* h) {
     h->hist_rows = 0;
     CK(load_working(h));
     h->loaded = true;
+    h->gq_ready = false;
     return AD_OK;
 }
 
@@ -627,7 +629,16 @@ static int run_deps(ad_handle* h, ad_csr_sizes* sizes, bool accept, bool bound_m
     if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
-    if (accept && h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_accept_deps: sharded stores answer PreAccept deps only");
+    if (accept && h->sharded) {
+        // the window sits at the bound's global arrival position (ad_shard_query_positions); Timestamp.MAX: after
+        // every arrival of the global batch
+        CK(dalloc(h, S_GQPOS, &h->gqpos, std::max<size_t>(h->n, 1)));
+        if (bound_max) {
+            if (h->n) HIPCHK(h, hipMemsetD32Async(h->gqpos, (int)h->n_global, h->n, h->st));
+        } else if (!h->gq_ready) {
+            return set_err(h, AD_ERR_STATE, "ad_accept_deps on a sharded store: ad_shard_query_positions first");
+        }
+    }
     if (accept && h->hist_active) return set_err(h, AD_ERR_UNSUPPORTED, "ad_accept_deps: not over a CFK history batch");
     hipSetDevice(h->device);
     h->accept = accept;
@@ -837,7 +848,6 @@ int ad_recover(ad_handle* h, const uint32_t* rows, size_t nq, size_t* entries) {
     if (!h || (nq && !rows)) return AD_ERR_ARGUMENT;
     if (!h->have_deps || !h->have_merged)
         return set_err(h, AD_ERR_STATE, "ad_recover needs the batch's deps and merged Deps (ad_merge_deps / _fast / ad_merge_host)");
-    if (h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_recover: not in sharded mode");
     for (size_t q = 0; q < nq; ++q)
         if (rows[q] >= h->n) return set_err(h, AD_ERR_ARGUMENT, "ad_recover: row " + std::to_string(rows[q]) + " out of range");
     hipSetDevice(h->device);

@@ -164,6 +164,8 @@ struct ad_handle {
     bool hist_active = false;        // the loaded batch's rows [0, hist_rows) are history; gid = global ranks
     size_t hist_rows = 0;
     uint32_t* qpos = nullptr;        // [n] arrival position of each txn's executeAt (accept bound)
+    uint32_t* gqpos = nullptr;       // sharded stores: [n] the GLOBAL arrival position of each row's executeAt
+    bool gq_ready = false;           // ad_shard_query_positions ran for the loaded batch
     // BeginRecovery queries (recovery_kernels.h): outputs of the last ad_recover
     size_t rc_nq = 0;
     bool rc_ready = false;
@@ -249,7 +251,7 @@ enum Slot : size_t {
     S_RIDX = S_RCEND, S_NONEROWS, S_LROWS, S_UMEDC, S_UMED,
     S_GLCT, S_GLCM, S_GLCE, S_GLCP, S_GLLW, S_GLEC, S_GLEO, S_GLXC, S_GLXO, S_GLCONS, S_GLE, S_GLIN,
     S_GLSRC, S_GLDST, S_GLSRC2, S_GLDST2, S_GLDEG, S_GLREM, S_GLXOFF, S_GLFL, S_GLFRONT, S_GLKEY, S_CFKU,
-    S_CNTX, S_INL, S_DFR, S_OVI, S_DTX, S_POSOF,
+    S_CNTX, S_INL, S_DFR, S_OVI, S_DTX, S_POSOF, S_GQPOS,
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 192

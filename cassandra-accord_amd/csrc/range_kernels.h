@@ -89,6 +89,7 @@ struct RangeArgs {
     uint64_t* keys_v[MAXV];      // (start, end) interleaved
     int32_t* k2t_v[MAXV];
     const uint32_t* qpos;        // executeAt-bound queries: per txn the bound's arrival position (nullable)
+    const uint32_t* gqpos;       // sharded stores: the bound's global arrival position (window; nullable = qpos)
     const uint32_t* gid;         // sharded stores: local row -> global arrival rank (window, drops; nullable)
 };
 
@@ -124,7 +125,7 @@ static __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
     const uint32_t qi = a.qpos ? a.qpos[i] : i;
     // window and drop decisions use global arrival ranks (shard-invariant); emitted ids stay local rows
     const uint32_t gi = a.gid ? a.gid[i] : i;
-    const uint32_t gq = a.qpos ? qi : gi;
+    const uint32_t gq = a.qpos ? (a.gqpos ? a.gqpos[i] : qi) : gi;
     const uint32_t lo_w = a.window == 0 ? gq : (gq > a.window ? gq - a.window : 0u);
     uint32_t ecount[NV], kcount[NV];
     uint64_t cs[NV], ce[NV];

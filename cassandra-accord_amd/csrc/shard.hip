@@ -803,6 +803,22 @@ int ad_shard_order(ad_handle* h, uint32_t* level_out, uint32_t* order_out) {
     return AD_OK;
 }
 
+// Accept / GetDeps on a sharded store: per local row, the number of TxnIds of the GLOBAL batch below the row's
+// executeAt (the arrival position the query is answered at; the store holds only its slice, so the caller that
+// has the whole batch supplies it).  Valid until the next load.
+int ad_shard_query_positions(ad_handle* h, const uint32_t* gq) {
+    if (!h || (!gq && h->n)) return AD_ERR_ARGUMENT;
+    if (!h->sharded) return set_err(h, AD_ERR_STATE, "ad_shard_query_positions: ad_shard_setup first");
+    hipSetDevice(h->device);
+    for (size_t i = 0; i < h->n; ++i)
+        if (gq[i] > h->n_global) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_query_positions: position beyond the global batch");
+    CK(dalloc(h, S_GQPOS, &h->gqpos, std::max<size_t>(h->n, 1)));
+    if (h->n) HIPCHK(h, hipMemcpyAsync(h->gqpos, gq, h->n * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->gq_ready = true;
+    return AD_OK;
+}
+
 // ---- one-exchange levels (global_levels.h, levels.hip)
 int ad_shard_level_edges(ad_handle* h, size_t* m, uint64_t* out) {
     if (!h || !m) return AD_ERR_ARGUMENT;

@@ -418,6 +418,14 @@ int  ad_shard_send_to_host(ad_handle* h, void* dst /* [sum bytes]: blobs in dest
 int  ad_shard_import_host(ad_handle* h, const void* src /* blobs in source order */, uint32_t world,
                           const uint64_t* sizes /* [world] */);
 int  ad_comm_unique_id(uint8_t* out /* [128] */);
+/* Accept / GetDeps (ad_accept_deps) on a sharded store: gq[n] = per local row, the number of TxnIds of the GLOBAL
+ * batch below the row's executeAt (the arrival position its executeAt-bound query is answered at; the store holds
+ * only its slice).  Messages/Accept.java:113-116 run per store through CommandStores.mapReduce
+ * (local/CommandStores.java:576-593).  Required before ad_accept_deps on a sharded handle (not for
+ * ad_ephemeral_read_deps: Timestamp.MAX is after every arrival); valid until the next load.  ad_recover works on
+ * sharded stores as on any store: each answers from its own slice and its own replicas' merged Deps (the
+ * reference's per-store PartialDeps; messages/BeginRecovery.java:118). */
+int  ad_shard_query_positions(ad_handle* h, const uint32_t* gq);
 int  ad_comm_init(ad_handle* h, uint32_t world, uint32_t rank, const uint8_t* id /* [128] */);
 /* Aborts and releases the handle's communicator (a partial init across ranks: the ranks whose init succeeded
  * drop theirs before falling back to a host transport).  No-op without one. */

@@ -464,3 +464,81 @@ def test_c5_full_shape_8_stores(engine_factory):
     finally:
         for st in stores:
             st.close()
+
+
+@pytest.mark.parametrize("deps,shards,range_frac", [("accept", 2, 0.0), ("accept", 3, 0.1), ("ephemeral", 3, 0.1),
+                                                    ("accept", 4, 0.05)])
+def test_sharded_accept_equals_presplit_unsharded(engine_factory, deps, shards, range_frac):
+    # Accept / GetDeps (bound executeAt, answered at the bound's GLOBAL arrival position: ad_shard_query_positions)
+    # and GetEphemeralReadDeps (bound Timestamp.MAX) on every store, then the home merge: each home txn's per-view
+    # and merged Deps equal the unsharded engine's on the presplit batch (Accept.java:113-116 per store through
+    # CommandStores.mapReduce, CommandStores.java:576-593)
+    w, r, p, s = 32, 3, 0.1, 0xACC0D1
+    ks = 400_000
+    b = workload.generate(20000, 4, ks, "uniform", range_frac=range_frac, range_width_max=1 << 12, slow_frac=0.3,
+                          bump_max=200, seed=60 + shards)
+    bounds = sharding.even_bounds(0, ks, shards)
+    eng = engine_factory(window=w, replicas=r, drop_p=p, seed=s)
+    eng.load(sharding.presplit(b, bounds))
+    if deps == "ephemeral":
+        eng.ephemeral_read_deps()
+    else:
+        eng.accept_deps()
+    classes = range(3) if range_frac else (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)
+    views = [{c: eng.fetch_deps(v, c) for c in classes} for v in range(r)]
+    eng.merge()
+    merged = {c: eng.fetch_merged(c) for c in classes}
+    hs = sharding.home_stores(b, bounds)
+    gq = sharding.query_positions(b)
+    stores = []
+    try:
+        for k in range(shards):
+            local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+            st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
+            stores.append(st)
+            st.load(local, gid, hs[gid], b["n"], k, shards)
+        assert sharding.LocalTransport.run(stores, levels=None, deps=deps, gq=gq) == 0
+        seen = np.zeros(b["n"], bool)
+        for st in stores:
+            for v in range(r + 1):
+                for c in classes:
+                    got, hg = st.fetch(v, c)
+                    want = merged[c] if v == r else views[v][c]
+                    assert blob._rows_of(want, hg).equal(got), "store view %d class %d differs" % (v, c)
+            _, hg = st.fetch(r, abi.CLASS_KEY)
+            assert not seen[hg].any()
+            seen[hg] = True
+    finally:
+        for st in stores:
+            st.close()
+
+
+def test_sharded_store_recovery(engine_factory):
+    # BeginRecovery's store queries on sharded stores (BeginRecovery.java:118 through CommandStores.mapReduce): every
+    # store answers from its own slice and its own replicas' merged Deps (the store's PartialDeps) — the oracle on
+    # that slice with those Deps, for the store's recovering rows
+    import oracle as O
+    from test_gpu_recovery import _same
+    from test_oracle_recovery import _mixed
+    shards, w, r, p, s = 3, 16, 2, 0.2, 9
+    b = _mixed(3000, 300, 0.1, 21)
+    bounds = sharding.even_bounds(0, 300, shards)
+    hs = sharding.home_stores(b, bounds)
+    gq = sharding.query_positions(b)
+    total = 0
+    for k in range(shards):
+        local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
+        st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
+        try:
+            st.load(local, gid, hs[gid], b["n"], k, shards)
+            st.accept(gq[gid])
+            st.eng.merge()
+            merged = [st.eng.fetch_merged(c) for c in range(3)]
+            rows = [i for i in range(local["n"]) if local["status"][i] < abi.ST_COMMITTED][:400]
+            rows += [i for i in range(local["n"]) if local["status"][i] >= abi.ST_COMMITTED][:20]
+            got = st.eng.recover(rows)
+            _same(got, O.recover(local, merged, rows), rows)
+            total += sum(len(got[0][x][c][2]) for x in range(2) for c in range(3))
+        finally:
+            st.close()
+    assert total > 0
