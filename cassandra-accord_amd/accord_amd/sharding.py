@@ -635,28 +635,46 @@ class LocalTransport:
     """Several stores in one process (tests): the same protocol with in-process exchange."""
 
     @staticmethod
-    def run(stores, max_rounds=1 << 16, levels="gather", deps="preaccept", gq=None):
+    def run(stores, max_rounds=1 << 16, levels="gather", deps="preaccept", gq=None, timings=None):
         """deps: "preaccept", "accept" (gq: the global query positions, query_positions) or "ephemeral";
-        levels None: stop after the home merge."""
+        levels None: stop after the home merge.  timings (dict): seconds per phase, summed over the stores (the
+        stores run one after another in this process: each phase's sum is what S GPUs would spend in parallel,
+        times S)."""
+        import time
+        t = [time.perf_counter()]
+
+        def lap(name):
+            now = time.perf_counter()
+            if timings is not None:
+                timings[name] = timings.get(name, 0.0) + now - t[0]
+            t[0] = now
         for s in stores:
             if deps == "preaccept":
                 s.preaccept()
             else:
                 s.accept(None if gq is None else gq[s.gid], bound_max=deps == "ephemeral")
+        lap("deps")
         sizes = [s.export() for s in stores]
         bufs = [s.send_buffer() for s in stores]
+        lap("export")
         offs = [np.concatenate([[0], np.cumsum(z)]).astype(np.int64) for z in sizes]
         for d, s in enumerate(stores):
             parts = [bufs[k][offs[k][d]:offs[k][d + 1]] for k in range(len(stores))]
             s.import_host(np.concatenate(parts) if parts else np.zeros(0, np.uint8),
                           np.array([sizes[k][d] for k in range(len(stores))], np.uint64))
+            lap("exchange")
             s.merge()
+            lap("home_merge")
         if levels is None:
             return 0
         if levels == "gather":
             edges = np.concatenate([s.level_edges() for s in stores])
+            lap("level_edges")
+            if timings is not None:
+                timings["level_edges_count"] = int(len(edges))
             for s in stores:
                 s.depth = s.levels_solve(edges)
+            lap("level_solve")
             return 1
         changed = [s.levels_round(True) for s in stores]
         rounds = 1

@@ -4,6 +4,8 @@ unsharded engine bit for bit: KeyDeps are shard-invariant, and window/drop decis
 Levels: levels="gather" (the default: every store's constraint edges gathered once and solved,
 ad_shard_level_edges / ad_shard_levels_solve / ad_shard_levels_gather) and levels="rounds" (the per-round
 delta / dense exchange, rounds = graph depth)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -454,13 +456,24 @@ def test_c5_full_shape_8_stores(engine_factory):
     stores, _, _ = _make_stores(b, 8, w, r, p, s, 10_000_000, delta=False)
     try:
         timings = {}
-        assert sharding.LocalTransport.run(stores) == 1
+        assert sharding.LocalTransport.run(stores, timings=timings) == 1
+        t2 = time.perf_counter()
+        for st in stores:
+            st.order()
+        timings["order"] = time.perf_counter() - t2
         t2 = time.perf_counter()
         assert all(st.depth == lv.max() + 1 for st in stores)
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all(), "every txn has exactly one home store"
-        print("C5 16M x 8 stores: unsharded %.1f s, 8-store protocol %.1f s, check %.1f s"
-              % (t1 - t0, t2 - t1, time.perf_counter() - t2))
+        rec = {"txns": int(b["n"]), "stores": 8, "unsharded_s": t1 - t0, "protocol_s": t2 - t1,
+               "check_s": time.perf_counter() - t2, "phases_s_summed_over_stores": timings,
+               "local_txns_per_store": [int(st.gid.size) for st in stores], "depth": int(lv.max() + 1)}
+        print("C5 16M x 8 stores:", rec)
+        out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+        if os.path.isdir(out):
+            import json
+            with open(os.path.join(out, "c5_8_stores.json"), "w") as f:
+                json.dump(rec, f)
     finally:
         for st in stores:
             st.close()
