@@ -81,6 +81,8 @@ def lib():
         L.ad_merge_deps_fast.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_max_conflicts_ts.argtypes = [vp, vp, vp, vp, vp]
         L.ad_max_conflicts_export.argtypes = [vp, C.POINTER(C.c_size_t), vp, vp, vp, vp]
+        L.ad_max_conflicts_carry_ranges.argtypes = [vp, C.c_size_t, vp, vp, vp, vp, vp]
+        L.ad_max_conflicts_export_ranges.argtypes = [vp, C.POINTER(C.c_size_t), vp, vp, vp, vp, vp]
         L.ad_recover.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.ad_fetch_recovery.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.ad_fetch_recovery_flags.argtypes = [vp, vp]
@@ -97,7 +99,8 @@ def lib():
 
 
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
-            "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_merge_deps_fast",
+            "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
+            "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
             "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
@@ -410,6 +413,24 @@ class DepsEngine:
                                                   nd.ctypes.data), "ad_max_conflicts_export")
         c = m.value
         return k[:c], ms[:c], ls[:c], nd[:c]
+
+    def max_conflicts_carry_ranges(self, table):
+        """The range part of the store's MaxConflicts map: (starts, ends, msb, lsb, node), sorted disjoint (s, e]."""
+        a = tuple(np.ascontiguousarray(x, dt) for x, dt in zip(table, (np.uint64,) * 4 + (np.int32,)))
+        self._carry_ranges = a
+        self._check(lib().ad_max_conflicts_carry_ranges(self.h, len(a[0]), *(x.ctypes.data for x in a)),
+                    "ad_max_conflicts_carry_ranges")
+
+    def max_conflicts_export_ranges(self):
+        """The intervals of the MaxConflicts map after this batch: (starts, ends, msb, lsb, node)."""
+        m = C.c_size_t()
+        self._check(lib().ad_max_conflicts_export_ranges(self.h, C.byref(m), None, None, None, None, None),
+                    "ad_max_conflicts_export_ranges")
+        k = max(m.value, 1)
+        out = tuple(np.zeros(k, np.uint64) for _ in range(4)) + (np.zeros(k, np.int32),)
+        self._check(lib().ad_max_conflicts_export_ranges(self.h, C.byref(m), *(x.ctypes.data for x in out)),
+                    "ad_max_conflicts_export_ranges")
+        return tuple(x[:m.value] for x in out)
 
     def run_pipeline(self):
         self._check(lib().ad_run_pipeline(self.h), "ad_run_pipeline")

@@ -292,11 +292,48 @@ __device__ inline int ts3_cmp(const Ts3& a, const Ts3& b) {          // Timestam
     if (af != bf) return af < bf ? -1 : 1;
     return a.node < b.node ? -1 : (a.node > b.node ? 1 : 0);
 }
+// The range part of the carried map (round 3): sorted disjoint intervals (s, e] with a Timestamp each.  A key k
+// is the interval (k - 1, k] (Range.EndInclusive over the order-preserving u64 keys), so the point table and the
+// interval table together are the reference's ReducingRangeMap (MaxConflicts extends ReducingRangeMap<Timestamp>,
+// local/MaxConflicts.java:32-59): get(keys or ranges) folds max over every point and interval the footprint meets;
+// update(footprint, executeAt) merges a piece per key / range (ReducingIntervalMap.merge with Timestamp::max).
+struct McIntervals {
+    size_t m;
+    const uint64_t *s, *e, *cm, *cl;
+    const int32_t* cn;
+};
+// Timestamp::max; of two that compare equal the larger raw lsb (a total order: the fold is order-independent)
+__device__ inline void ts3_fold(const Ts3& c, Ts3& best, bool& has) {
+    const int d = has ? ts3_cmp(c, best) : 1;
+    if (d > 0 || (d == 0 && c.lsb > best.lsb)) { best = c; has = true; }
+}
+// a range txn the store records in MaxConflicts: globally visible kind, not TRANSITIVELY_KNOWN / INVALID
+__device__ inline bool mc_range_recorded(uint32_t m) {
+    const uint32_t k = meta_kind(m), st = meta_status(m);
+    return (k == AD_KIND_READ || k == AD_KIND_WRITE || k == AD_KIND_SYNC_POINT || k == AD_KIND_EXCLUSIVE_SYNC_POINT) &&
+           st != AD_ST_TRANSITIVELY_KNOWN && st != AD_ST_INVALID;
+}
+// the interval containing key k (s < k <= e): the first interval with e >= k
+__device__ inline void mci_stab(const McIntervals& r, uint64_t k, Ts3& best, bool& has) {
+    size_t lo = 0, hi = r.m;
+    while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (r.e[mid] < k) lo = mid + 1; else hi = mid; }
+    if (lo < r.m && r.s[lo] < k) ts3_fold(Ts3{r.cm[lo], r.cl[lo], r.cn[lo]}, best, has);
+}
+// every interval meeting (qs, qe]: from the first with e > qs while s < qe
+__device__ inline void mci_span(const McIntervals& r, uint64_t qs, uint64_t qe, Ts3& best, bool& has) {
+    size_t lo = 0, hi = r.m;
+    while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (r.e[mid] <= qs) lo = mid + 1; else hi = mid; }
+    for (size_t x = lo; x < r.m && r.s[x] < qe; ++x) ts3_fold(Ts3{r.cm[x], r.cl[x], r.cn[x]}, best, has);
+}
+
 struct McCarryArgs {
     size_t n;
     int nv;
     const uint32_t* key_off;
     const uint64_t* keys;
+    const uint32_t* range_off;               // range txns' footprints (nullable: a key batch)
+    const uint64_t *rs, *re;
+    McIntervals iv;                          // the carried intervals
     const uint64_t *tm, *tl, *em, *el;       // batch TxnId / executeAt
     const int32_t *tn, *en;
     const uint32_t* local_rank;              // [v * n + t]
@@ -312,13 +349,23 @@ static __global__ __launch_bounds__(256) void k_mc_carry(McCarryArgs a) {
     if (t >= a.n) return;
     Ts3 cb{0, 0, 0};
     bool has = false;
-    for (uint32_t p = a.key_off[t]; p < a.key_off[t + 1] && a.m; ++p) {
+    for (uint32_t p = a.key_off[t]; p < a.key_off[t + 1]; ++p) {
         const uint64_t k = a.keys[p];
-        size_t lo = 0, hi = a.m;
-        while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (a.ck[mid] < k) lo = mid + 1; else hi = mid; }
-        if (lo < a.m && a.ck[lo] == k) {
-            const Ts3 c{a.cm[lo], a.cl[lo], a.cn[lo]};
-            if (!has || ts3_cmp(c, cb) > 0) { cb = c; has = true; }
+        if (a.m) {
+            size_t lo = 0, hi = a.m;
+            while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (a.ck[mid] < k) lo = mid + 1; else hi = mid; }
+            if (lo < a.m && a.ck[lo] == k) ts3_fold(Ts3{a.cm[lo], a.cl[lo], a.cn[lo]}, cb, has);
+        }
+        if (a.iv.m) mci_stab(a.iv, k, cb, has);
+    }
+    if (a.range_off) {
+        // a range footprint: every carried point inside (qs, qe] and every carried interval meeting it
+        for (uint32_t q = a.range_off[t]; q < a.range_off[t + 1]; ++q) {
+            const uint64_t qs = a.rs[q], qe = a.re[q];
+            size_t lo = 0, hi = a.m;
+            while (lo < hi) { const size_t mid = (lo + hi) >> 1; if (a.ck[mid] <= qs) lo = mid + 1; else hi = mid; }
+            for (size_t x = lo; x < a.m && a.ck[x] <= qe; ++x) ts3_fold(Ts3{a.cm[x], a.cl[x], a.cn[x]}, cb, has);
+            if (a.iv.m) mci_span(a.iv, qs, qe, cb, has);
         }
     }
     const Ts3 me{a.tm[t], a.tl[t], a.tn[t]};
@@ -385,6 +432,109 @@ static __global__ __launch_bounds__(256) void k_mc_export_gather(uint32_t count,
     if (k >= count) return;
     const uint32_t i = slot[k];
     ok[k] = sk[i]; om[k] = sm[i]; ol[k] = sl[i]; on[k] = sn[i];
+}
+
+// ---- export of the interval part: the piecewise max of the carried intervals and the batch's range txns ------
+// Breakpoints X = every interval endpoint (carried and batch), sorted and unique; the elementary segments
+// (X[g], X[g+1]] each take the max of the carried interval and the batch range entries (recorded owners: status not
+// TRANSITIVELY_KNOWN / INVALID, as the key scan) that contain X[g+1]; runs of equal values are merged into one
+// interval and empty segments dropped (ReducingIntervalMap's normal form).
+static __global__ __launch_bounds__(256) void k_mci_points(size_t m, const uint64_t* __restrict__ cs, const uint64_t* __restrict__ ce,
+                                                    size_t Q, const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
+                                                    uint64_t base, uint64_t* __restrict__ x, uint32_t* __restrict__ lo32,
+                                                    uint32_t* __restrict__ idx) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t N = 2 * (m + Q);
+    if (i >= N) return;
+    const size_t j = i >> 1;
+    const uint64_t v = j < m ? ((i & 1) ? ce[j] : cs[j]) : ((i & 1) ? re[j - m] : rs[j - m]);
+    x[i] = v;
+    lo32[i] = (uint32_t)(v - base);
+    idx[i] = (uint32_t)i;
+}
+// second LSD pass over a spread beyond 32 bits: the high halves of the points in their current order
+static __global__ __launch_bounds__(256) void k_mci_hi(size_t N, const uint64_t* __restrict__ x, const uint32_t* __restrict__ idx,
+                                                uint64_t base, uint32_t* __restrict__ hi32) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) hi32[i] = (uint32_t)((x[idx[i]] - base) >> 32);
+}
+// unique flags of the sorted points
+static __global__ __launch_bounds__(256) void k_mci_unique(size_t N, const uint64_t* __restrict__ x, const uint32_t* __restrict__ idx,
+                                                    uint8_t* __restrict__ first) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) first[i] = (i == 0 || x[idx[i]] != x[idx[i - 1]]) ? 1 : 0;
+}
+static __global__ __launch_bounds__(256) void k_mci_gather_points(uint32_t S, const uint32_t* __restrict__ rows, const uint64_t* __restrict__ x,
+                                                           const uint32_t* __restrict__ idx, uint64_t* __restrict__ xu) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < S) xu[k] = x[idx[rows[k]]];
+}
+struct MciSegArgs {
+    uint32_t S;                              // unique breakpoints; segments g = 0 .. S-2
+    const uint64_t* xu;
+    McIntervals iv;
+    size_t Q;                                // batch range entries sorted by (start, end, owner) + their index
+    const uint64_t *es, *ee;
+    const uint32_t* eown;
+    RangeIndex ix;
+    const uint8_t* meta;                     // owners' meta (recorded?) and raw executeAt
+    const uint64_t *em, *el;
+    const int32_t* en;
+    uint64_t *vm, *vl;                       // [S] segment values (vm = vl = 0, vn = 0 and has = 0: none)
+    int32_t* vn;
+    uint8_t* has;
+};
+// one wave per segment: the carried interval and the batch entries containing y = X[g + 1]
+static __global__ __launch_bounds__(256) void k_mci_segments(MciSegArgs a) {
+    const size_t g = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (g + 1 >= a.S) return;
+    const int lane = __lane_id();
+    const uint64_t y = a.xu[g + 1];
+    Ts3 best{0, 0, 0};
+    bool any = false;
+    if (a.Q) {
+        ri_walk(a.ix, a.es, (uint32_t)a.Q, true, a.xu, nullptr, nullptr, (uint32_t)(g + 1), (uint32_t)(g + 2),
+                [&](uint32_t clo, uint32_t chi) {
+            const uint32_t x = clo + (uint32_t)lane;
+            if (x < chi && a.es[x] < y && a.ee[x] >= y) {
+                const uint32_t j = a.eown[x];
+                if (mc_range_recorded(a.meta[j])) ts3_fold(Ts3{a.em[j], a.el[j], a.en[j]}, best, any);
+            }
+        });
+        // the wave's max
+#pragma unroll
+        for (int o = WAVE / 2; o > 0; o >>= 1) {
+            const Ts3 c{__shfl_xor(best.msb, o), __shfl_xor(best.lsb, o), __shfl_xor(best.node, o)};
+            const bool ca = __shfl_xor((int)any, o) != 0;
+            if (ca) ts3_fold(c, best, any);
+        }
+    }
+    if (lane != 0) return;
+    if (a.iv.m) mci_stab(a.iv, y, best, any);
+    a.vm[g] = any ? best.msb : 0ull;
+    a.vl[g] = any ? best.lsb : 0ull;
+    a.vn[g] = any ? best.node : 0;
+    a.has[g] = any ? 1 : 0;
+}
+// piece starts / ends: a segment with a value whose neighbour has no value or another one
+static __global__ __launch_bounds__(256) void k_mci_pieces(uint32_t nseg, const uint64_t* __restrict__ vm, const uint64_t* __restrict__ vl,
+                                                    const int32_t* __restrict__ vn, const uint8_t* __restrict__ has,
+                                                    uint8_t* __restrict__ start, uint8_t* __restrict__ end) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    auto same = [&](uint32_t a, uint32_t b) { return has[a] && has[b] && vm[a] == vm[b] && vl[a] == vl[b] && vn[a] == vn[b]; };
+    start[g] = (has[g] && !(g > 0 && same(g - 1, g))) ? 1 : 0;
+    end[g] = (has[g] && !(g + 1 < nseg && same(g, g + 1))) ? 1 : 0;
+}
+static __global__ __launch_bounds__(256) void k_mci_emit(uint32_t cnt, const uint32_t* __restrict__ starts, const uint32_t* __restrict__ ends,
+                                                  const uint64_t* __restrict__ xu, const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ vl, const int32_t* __restrict__ vn,
+                                                  uint64_t* __restrict__ os, uint64_t* __restrict__ oe, uint64_t* __restrict__ om,
+                                                  uint64_t* __restrict__ ol, int32_t* __restrict__ on) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cnt) return;
+    const uint32_t g0 = starts[k], g1 = ends[k];
+    os[k] = xu[g0]; oe[k] = xu[g1 + 1]; om[k] = vm[g0]; ol[k] = vl[g0]; on[k] = vn[g0];
 }
 
 }  // namespace ad

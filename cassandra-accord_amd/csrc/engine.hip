@@ -765,9 +765,34 @@ int ad_max_conflicts_carry(ad_handle* h, size_t m, const uint64_t* keys, const u
     return AD_OK;
 }
 
+int ad_max_conflicts_carry_ranges(ad_handle* h, size_t m, const uint64_t* starts, const uint64_t* ends, const uint64_t* msb,
+                                  const uint64_t* lsb, const int32_t* node) {
+    if (!h || (m && (!starts || !ends || !msb || !lsb || !node))) return AD_ERR_ARGUMENT;
+    for (size_t i = 0; i < m; ++i) {
+        if (!(starts[i] < ends[i])) return set_err(h, AD_ERR_ARGUMENT, "carried MaxConflicts intervals need start < end");
+        if (i && starts[i] < ends[i - 1])
+            return set_err(h, AD_ERR_ARGUMENT, "carried MaxConflicts intervals must be sorted and disjoint");
+    }
+    hipSetDevice(h->device);
+    const size_t c = std::max<size_t>(m, 1);
+    CK(dalloc(h, S_MCIS, &h->mci_s, c)); CK(dalloc(h, S_MCIE, &h->mci_e, c)); CK(dalloc(h, S_MCIM, &h->mci_cm, c));
+    CK(dalloc(h, S_MCIL, &h->mci_cl, c)); CK(dalloc(h, S_MCIN, &h->mci_cn, c));
+    if (m) {
+        HIPCHK(h, hipMemcpyAsync(h->mci_s, starts, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mci_e, ends, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mci_cm, msb, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mci_cl, lsb, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->mci_cn, node, m * 4, hipMemcpyHostToDevice, h->st));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->mci_m = m;
+    h->mci_lo = m ? starts[0] : 0;
+    h->mci_hi = m ? ends[m - 1] : 0;
+    return AD_OK;
+}
+
 int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast) {
     if (!h) return AD_ERR_ARGUMENT;
-    if (h->Q > 0) return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts_ts: the carried MaxConflicts map is per key (key batches)");
     uint32_t *rank = nullptr, *local = nullptr;
     uint8_t* fst = nullptr;
     CK(run_max_conflicts(h, &rank, &fst, &local));
@@ -782,7 +807,12 @@ int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* nod
         McCarryArgs c{};
         c.n = n; c.nv = (int)nv; c.key_off = h->key_off; c.keys = h->keys;
         c.tm = h->tm; c.tl = h->tl; c.tn = h->tn; c.em = h->em; c.el = h->el; c.en = h->en;
-        c.local_rank = local; c.m = h->mc_m; c.ck = h->mc_ck; c.cm = h->mc_cm; c.cl = h->mc_cl; c.cn = h->mc_cn;
+        // the batch row holding each answer: the range fold updates `local` only on sharded / history batches
+        const bool gid = h->sharded || h->hist_active;
+        c.local_rank = (gid || h->Q == 0) ? local : rank;
+        if (h->Q > 0) { c.range_off = h->range_off; c.rs = h->range_s; c.re = h->range_e; }
+        c.iv = McIntervals{h->mci_m, h->mci_s, h->mci_e, h->mci_cm, h->mci_cl, h->mci_cn};
+        c.m = h->mc_m; c.ck = h->mc_ck; c.cm = h->mc_cm; c.cl = h->mc_cl; c.cn = h->mc_cn;
         c.om = om; c.ol = ol; c.on = on; c.fast = of;
         KScope ks(K_MAX_CONFLICTS);
         k_mc_carry<<<ceil_div((long)n, 256), 256, 0, st>>>(c);
@@ -801,7 +831,6 @@ int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* nod
 int ad_max_conflicts_export(ad_handle* h, size_t* m_out, uint64_t* keys, uint64_t* msb, uint64_t* lsb, int32_t* node) {
     if (!h || !m_out) return AD_ERR_ARGUMENT;
     if (!h->mc_ready) return set_err(h, AD_ERR_STATE, "ad_max_conflicts_export: run ad_max_conflicts(_ts) on this batch first");
-    if (h->Q > 0) return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts_export: the carried MaxConflicts map is per key (key batches)");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
     const uint32_t U = h->P ? h->hprm.n_keys_u : 0;
@@ -838,6 +867,90 @@ int ad_max_conflicts_export(ad_handle* h, size_t* m_out, uint64_t* keys, uint64_
         if (node) HIPCHK(h, hipMemcpyAsync(node, on_, count * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(h, hipStreamSynchronize(st));
+    return AD_OK;
+}
+
+// The interval part of the map after the batch (conflict_kernels.h k_mci_*): breakpoints of the carried intervals and
+// the batch's range entries, LSD-sorted and made unique; per elementary segment the max of what contains it; runs
+// of one value compacted into pieces.  Two calls as ad_max_conflicts_export (starts == NULL: *m only).
+int ad_max_conflicts_export_ranges(ad_handle* h, size_t* m_out, uint64_t* starts, uint64_t* ends, uint64_t* msb,
+                                   uint64_t* lsb, int32_t* node) {
+    if (!h || !m_out) return AD_ERR_ARGUMENT;
+    if (!h->mc_ready) return set_err(h, AD_ERR_STATE, "ad_max_conflicts_export_ranges: run ad_max_conflicts(_ts) on this batch first");
+    hipSetDevice(h->device);
+    g_tracer = &h->tracer;
+    hipStream_t st = h->st;
+    const size_t mi = h->mci_m, Q = h->Q, N = 2 * (mi + Q);
+    *m_out = 0;
+    if (N == 0) return AD_OK;
+    if (N >= (1ull << 31)) return set_err(h, AD_ERR_UNSUPPORTED, "ad_max_conflicts_export_ranges: too many intervals");
+    // breakpoint spread: carried [mci_lo, mci_hi], batch [rbase, rbase + 2^range_bits)
+    uint64_t lo = ~0ull, hi = 0;
+    if (mi) { lo = std::min<uint64_t>(lo, h->mci_lo); hi = std::max<uint64_t>(hi, h->mci_hi); }
+    if (Q) {
+        lo = std::min<uint64_t>(lo, h->rbase);
+        const uint64_t span = h->range_bits >= 64 ? ~0ull : ((1ull << h->range_bits) - 1);
+        hi = std::max<uint64_t>(hi, h->rbase + std::min<uint64_t>(span, ~0ull - h->rbase));
+    }
+    int bits = 0;
+    for (uint64_t d = hi - lo; d; d >>= 1) ++bits;
+    const size_t c = N + 16;
+    uint64_t *x, *xu, *vm, *vl, *os, *oe, *om, *ol;
+    uint32_t *k0, *v0, *k1, *v1, *rows, *ps, *pe;
+    int32_t *vn, *on;
+    uint8_t *fl, *has, *fs, *fe;
+    CK(dalloc(h, S_MXX, &x, c)); CK(dalloc(h, S_MXK0, &k0, c)); CK(dalloc(h, S_MXV0, &v0, c)); CK(dalloc(h, S_MXK1, &k1, c));
+    CK(dalloc(h, S_MXV1, &v1, c)); CK(dalloc(h, S_MXF, &fl, c)); CK(dalloc(h, S_MXR, &rows, c + 1)); CK(dalloc(h, S_MXU, &xu, c));
+    CK(dalloc(h, S_MXVM, &vm, c)); CK(dalloc(h, S_MXVL, &vl, c)); CK(dalloc(h, S_MXVN, &vn, c)); CK(dalloc(h, S_MXH, &has, c));
+    CK(dalloc(h, S_MXFS, &fs, c)); CK(dalloc(h, S_MXFE, &fe, c)); CK(dalloc(h, S_MXPS, &ps, c + 1)); CK(dalloc(h, S_MXPE, &pe, c + 1));
+    CK(dalloc(h, S_MXOS, &os, c)); CK(dalloc(h, S_MXOE, &oe, c)); CK(dalloc(h, S_MXOM, &om, c)); CK(dalloc(h, S_MXOL, &ol, c));
+    CK(dalloc(h, S_MXON, &on, c));
+    CK(ensure_scratch(h, std::max(h->scratch_cap, std::max((size_t)(3 * (radix_hist_len(N) + 128) + 64 * 1024) * 4,
+                                                           device_scan_scratch<CompactFlagOp>(N)))));
+    const int gN = ceil_div((long)N, 256);
+    uint32_t S = 0, cnt = 0;
+    {
+        KScope ks(K_MAX_CONFLICTS, N);
+        k_mci_points<<<gN, 256, 0, st>>>(mi, h->mci_s, h->mci_e, Q, h->es, h->ee, lo, x, k0, v0);
+        uint32_t *k = k0, *v = v0, *ko = k1, *vo = v1;
+        if (radix_sort_pairs(k, v, ko, vo, N, std::min(bits, 32), radix_scratch(h, N), st)) { std::swap(k, ko); std::swap(v, vo); }
+        if (bits > 32) {
+            k_mci_hi<<<gN, 256, 0, st>>>(N, x, v, lo, k);
+            if (radix_sort_pairs(k, v, ko, vo, N, bits - 32, radix_scratch(h, N), st)) { std::swap(k, ko); std::swap(v, vo); }
+        }
+        k_mci_unique<<<gN, 256, 0, st>>>(N, x, v, fl);
+        device_scan(CompactFlagOp{fl, rows, rows + c, N}, N, (uint32_t*)h->scratch, st);
+        HIPCHK(h, hipMemcpyAsync(&S, rows + c, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        if (S >= 2) {
+            const uint32_t nseg = S - 1;
+            k_mci_gather_points<<<ceil_div((long)S, 256), 256, 0, st>>>(S, rows, x, v, xu);
+            MciSegArgs a{};
+            a.S = S; a.xu = xu;
+            a.iv = McIntervals{mi, h->mci_s, h->mci_e, h->mci_cm, h->mci_cl, h->mci_cn};
+            a.Q = Q; a.es = h->es; a.ee = h->ee; a.eown = h->eown; a.ix = h->ix; a.meta = h->meta;
+            a.em = h->em; a.el = h->el; a.en = h->en;
+            a.vm = vm; a.vl = vl; a.vn = vn; a.has = has;
+            k_mci_segments<<<ceil_div((long)nseg * WAVE, 256), 256, 0, st>>>(a);
+            k_mci_pieces<<<ceil_div((long)nseg, 256), 256, 0, st>>>(nseg, vm, vl, vn, has, fs, fe);
+            device_scan(CompactFlagOp{fs, ps, ps + c, nseg}, nseg, (uint32_t*)h->scratch, st);
+            device_scan(CompactFlagOp{fe, pe, pe + c, nseg}, nseg, (uint32_t*)h->scratch, st);
+            HIPCHK(h, hipMemcpyAsync(&cnt, ps + c, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(h, hipStreamSynchronize(st));
+            if (cnt) k_mci_emit<<<ceil_div((long)cnt, 256), 256, 0, st>>>(cnt, ps, pe, xu, vm, vl, vn, os, oe, om, ol, on);
+        }
+    }
+    HIPCHK(h, hipGetLastError());
+    *m_out = cnt;
+    if (starts && cnt) {
+        HIPCHK(h, hipMemcpyAsync(starts, os, cnt * 8, hipMemcpyDeviceToHost, st));
+        if (ends) HIPCHK(h, hipMemcpyAsync(ends, oe, cnt * 8, hipMemcpyDeviceToHost, st));
+        if (msb) HIPCHK(h, hipMemcpyAsync(msb, om, cnt * 8, hipMemcpyDeviceToHost, st));
+        if (lsb) HIPCHK(h, hipMemcpyAsync(lsb, ol, cnt * 8, hipMemcpyDeviceToHost, st));
+        if (node) HIPCHK(h, hipMemcpyAsync(node, on, cnt * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    h->tracer.resolve();
     return AD_OK;
 }
 

@@ -143,6 +143,10 @@ struct ad_handle {
     size_t mc_m = 0;
     uint64_t *mc_ck = nullptr, *mc_cm = nullptr, *mc_cl = nullptr;
     int32_t* mc_cn = nullptr;
+    size_t mci_m = 0;                // ... and its intervals (s, e] from range txns (ad_max_conflicts_carry_ranges)
+    uint64_t *mci_s = nullptr, *mci_e = nullptr, *mci_cm = nullptr, *mci_cl = nullptr;
+    int32_t* mci_cn = nullptr;
+    uint64_t mci_lo = 0, mci_hi = 0;  // smallest start / greatest end
     bool mc_ready = false;           // the MaxConflicts scan of the current batch is on the device (export)
     const uint8_t* mc_fast = nullptr;  // [replicas * n] fast-path flags of the last ad_max_conflicts(_ts)
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
@@ -252,9 +256,12 @@ enum Slot : size_t {
     S_GLCT, S_GLCM, S_GLCE, S_GLCP, S_GLLW, S_GLEC, S_GLEO, S_GLXC, S_GLXO, S_GLCONS, S_GLE, S_GLIN,
     S_GLSRC, S_GLDST, S_GLSRC2, S_GLDST2, S_GLDEG, S_GLREM, S_GLXOFF, S_GLFL, S_GLFRONT, S_GLKEY, S_CFKU,
     S_CNTX, S_INL, S_DFR, S_OVI, S_DTX, S_POSOF, S_GQPOS,
+    S_MCIS, S_MCIE, S_MCIM, S_MCIL, S_MCIN,                     // carried MaxConflicts intervals
+    S_MXX, S_MXK0, S_MXV0, S_MXK1, S_MXV1, S_MXF, S_MXR, S_MXU, S_MXVM, S_MXVL, S_MXVN, S_MXH, S_MXFS, S_MXFE,
+    S_MXPS, S_MXPE, S_MXOS, S_MXOE, S_MXOM, S_MXOL, S_MXON,    // their export
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
-    S_CSR0 = 192
+    S_CSR0 = 256
 };
 static_assert(S_NUM_FIXED <= S_CSR0, "fixed device slots overlap the CSR slot blocks");
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),

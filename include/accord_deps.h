@@ -264,13 +264,26 @@ int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8
  *   ad_max_conflicts_export  the table after this batch: the carry merged with every key's greatest recorded
  *                            executeAt in the batch (final statuses; TRANSITIVELY_KNOWN / INVALID unrecorded).
  *                            Two calls: keys == NULL returns *m only.  Needs ad_max_conflicts(_ts) on the batch.
+ *   ad_max_conflicts_carry_ranges   the range part of the carried map (MaxConflicts is a ReducingRangeMap,
+ *                            local/MaxConflicts.java:32-59): sorted disjoint intervals (start, end] (start < end,
+ *                            end <= next start) with a Timestamp each; m = 0 clears it.  A key k is the interval
+ *                            (k - 1, k], so the key table and the intervals together are the whole map: _ts folds
+ *                            every carried key and interval the txn's keys or ranges meet (range txns included)
+ *   ad_max_conflicts_export_ranges  the intervals after this batch: the carried intervals merged with every range
+ *                            the batch's recorded range txns cover (MaxConflicts.update = merge(this, create(ranges,
+ *                            executeAt)), Timestamp::max), as the normal form — maximal pieces of one value.  Two calls
+ *                            as _export (starts == NULL: *m only).  Key txns update the key table, range txns the
+ *                            intervals; Timestamps that compare equal keep the larger raw lsb.
  * A txn that PreAccepts in a later batch than a larger-TxnId txn (arrival order != TxnId order,
- * PreAcceptTest.multiKeyTimestampUpdate) sees it through the carry.  The carried table is per key: key batches only
- * (AD_ERR_UNSUPPORTED for _ts / _export when the batch has range txns). */
+ * PreAcceptTest.multiKeyTimestampUpdate) sees it through the carry. */
 int  ad_max_conflicts_carry(ad_handle* h, size_t m, const uint64_t* keys, const uint64_t* msb, const uint64_t* lsb,
                             const int32_t* node);
+int  ad_max_conflicts_carry_ranges(ad_handle* h, size_t m, const uint64_t* starts, const uint64_t* ends,
+                                   const uint64_t* msb, const uint64_t* lsb, const int32_t* node);
 int  ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast);
 int  ad_max_conflicts_export(ad_handle* h, size_t* m, uint64_t* keys, uint64_t* msb, uint64_t* lsb, int32_t* node);
+int  ad_max_conflicts_export_ranges(ad_handle* h, size_t* m, uint64_t* starts, uint64_t* ends, uint64_t* msb,
+                                    uint64_t* lsb, int32_t* node);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Device-resident pipeline (benchmark / service loop): stage 1 + 2 + 3 with no host copies of */

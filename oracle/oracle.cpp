@@ -33,6 +33,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <iterator>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -903,9 +904,13 @@ int oracle_max_conflicts(const ad_batch* b, const ad_config* c, uint32_t* max_ra
     }
 }
 
-/* MaxConflicts carried across batches (ad_max_conflicts_carry / _ts / _export): the carry table is the store's
- * MaxConflicts map from earlier batches (local/MaxConflicts.java:32-96); maxConflicts.get(keys) of a batch txn
- * is the greatest of the carried values on its keys and the batch answer above (Timestamp::max). */
+/* MaxConflicts carried across batches (ad_max_conflicts_carry / _ts / _export): the carry is the store's
+ * MaxConflicts map from earlier batches (local/MaxConflicts.java:32-96), held as two tables — points (a key k is
+ * the interval (k - 1, k]) and sorted disjoint intervals (s, e] from range txns — that together are the
+ * reference's ReducingRangeMap<Timestamp>.  maxConflicts.get(keysOrRanges) of a batch txn is the greatest of the
+ * carried values its footprint meets (foldl Timestamp::max, :46-54) and the batch answer above.  Among carried
+ * values that compare equal the larger raw lsb is kept (a deterministic tie rule; the reference's Timestamp::max
+ * keeps whichever its merge order meets first). */
 static bool carry_lookup(size_t m, const uint64_t* ck, const uint64_t* cm, const uint64_t* cl, const int32_t* cn,
                          uint64_t k, Ts* out) {
     const uint64_t* it = std::lower_bound(ck, ck + m, k);
@@ -914,12 +919,17 @@ static bool carry_lookup(size_t m, const uint64_t* ck, const uint64_t* cm, const
     *out = Ts{cm[x], cl[x], cn[x]};
     return true;
 }
+static inline void carry_fold(const Ts& t, Ts& cb, bool& has) {
+    const int c = has ? ts_cmp(t, cb) : 1;
+    if (c > 0 || (c == 0 && t.lsb > cb.lsb)) { cb = t; has = true; }
+}
 
-int oracle_max_conflicts_ts(const ad_batch* b, const ad_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
-                            const uint64_t* cl, const int32_t* cn, uint64_t* om, uint64_t* ol, int32_t* on, uint8_t* fast) {
+int oracle_max_conflicts_ts_ranges(const ad_batch* b, const ad_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
+                                   const uint64_t* cl, const int32_t* cn, size_t mi, const uint64_t* is, const uint64_t* ie,
+                                   const uint64_t* im, const uint64_t* il, const int32_t* in, uint64_t* om, uint64_t* ol,
+                                   int32_t* on, uint8_t* fast) {
     try {
         Batch B(b);
-        if (B.range_off[B.n] > 0) return AD_ERR_UNSUPPORTED;
         Config cfg;
         cfg.window = c->window; cfg.replicas = c->replicas ? c->replicas : 1; cfg.seed = c->seed;
         cfg.drop_thresh = ad_drop_threshold(c->drop_p);
@@ -928,9 +938,19 @@ int oracle_max_conflicts_ts(const ad_batch* b, const ad_config* c, size_t m, con
         for (uint32_t i = 0; i < n; ++i) {
             bool has = false;
             Ts cb{0, 0, 0};
-            for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
-                Ts t;
-                if (carry_lookup(m, ck, cm, cl, cn, B.keys[p], &t) && (!has || ts_cmp(t, cb) > 0)) { cb = t; has = true; }
+            auto meet = [&](uint64_t qs, uint64_t qe) {         // every carried point / interval meeting (qs, qe]
+                for (size_t x = 0; x < m; ++x) if (qs < ck[x] && ck[x] <= qe) carry_fold(Ts{cm[x], cl[x], cn[x]}, cb, has);
+                for (size_t x = 0; x < mi; ++x) if (is[x] < qe && ie[x] > qs) carry_fold(Ts{im[x], il[x], in[x]}, cb, has);
+            };
+            if (domain_of(B.tx[i]) == AD_DOMAIN_KEY) {
+                for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p) {
+                    const uint64_t k = B.keys[p];
+                    Ts t;
+                    if (carry_lookup(m, ck, cm, cl, cn, k, &t)) carry_fold(t, cb, has);
+                    for (size_t x = 0; x < mi; ++x) if (is[x] < k && k <= ie[x]) carry_fold(Ts{im[x], il[x], in[x]}, cb, has);
+                }
+            } else {
+                for (uint32_t q = B.range_off[i]; q < B.range_off[i + 1]; ++q) meet(B.ranges[q].s, B.ranges[q].e);
             }
             for (uint32_t v = 0; v < cfg.replicas; ++v) {
                 const uint32_t r = o.max_conflict(i, v);
@@ -948,6 +968,44 @@ int oracle_max_conflicts_ts(const ad_batch* b, const ad_config* c, size_t m, con
     }
 }
 
+int oracle_max_conflicts_ts(const ad_batch* b, const ad_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
+                            const uint64_t* cl, const int32_t* cn, uint64_t* om, uint64_t* ol, int32_t* on, uint8_t* fast) {
+    return oracle_max_conflicts_ts_ranges(b, c, m, ck, cm, cl, cn, 0, nullptr, nullptr, nullptr, nullptr, nullptr, om, ol,
+                                          on, fast);
+}
+
+/* The interval part of the map after the batch: ReducingIntervalMap as boundaries + a value (or none) per gap,
+ * updated txn by txn in TxnId order with every range of each range txn the store records (globally visible, not
+ * TRANSITIVELY_KNOWN / INVALID): MaxConflicts.update = merge(this, create(ranges, executeAt)) (:56-59), merge =
+ * ReducingIntervalMap.merge with Timestamp::max; adjacent gaps of one value coalesce (the builder's normal form).
+ * Output: the valued pieces (s, e] in order.  out == NULL: size only. */
+struct IntervalMap {
+    std::vector<uint64_t> b;            // boundaries, ascending; gap x = (b[x], b[x + 1]]
+    std::vector<int> has;               // [b.size() - 1]
+    std::vector<Ts> v;
+    void merge_range(uint64_t s, uint64_t e, const Ts& t) {
+        if (!(s < e)) return;
+        std::vector<uint64_t> nb;
+        std::merge(b.begin(), b.end(), &s, &s + 1, std::back_inserter(nb));
+        std::vector<uint64_t> tmp;
+        std::merge(nb.begin(), nb.end(), &e, &e + 1, std::back_inserter(tmp));
+        tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+        std::vector<int> nh(tmp.size() ? tmp.size() - 1 : 0, 0);
+        std::vector<Ts> nv(nh.size(), Ts{0, 0, 0});
+        size_t x = 0;                    // the old gap holding the new gap g
+        for (size_t g = 0; g + 1 < tmp.size(); ++g) {
+            const uint64_t y = tmp[g + 1];
+            while (x + 1 < b.size() && b[x + 1] < y) ++x;
+            bool h = false;
+            Ts cur{0, 0, 0};
+            if (x + 1 < b.size() && b[x] < y && y <= b[x + 1] && has[x]) { h = true; cur = v[x]; }
+            if (s < y && y <= e) carry_fold(t, cur, h);
+            nh[g] = h ? 1 : 0;
+            nv[g] = cur;
+        }
+        b.swap(tmp); has.swap(nh); v.swap(nv);
+    }
+};
 /* The MaxConflicts table after the batch: carry merged with, per key, the greatest executeAt of the batch txns
  * the store recorded there (globally visible, not TRANSITIVELY_KNOWN / INVALID).  out == NULL: size only. */
 int oracle_max_conflicts_export(const ad_batch* b, size_t m, const uint64_t* ck, const uint64_t* cm, const uint64_t* cl,
@@ -968,6 +1026,39 @@ int oracle_max_conflicts_export(const ad_batch* b, size_t m, const uint64_t* ck,
         if (!ok) return AD_OK;
         size_t x = 0;
         for (auto& e : t) { ok[x] = e.first; om[x] = e.second.msb; ol[x] = e.second.lsb; on[x] = e.second.node; ++x; }
+        return AD_OK;
+    } catch (const std::exception&) {
+        return AD_ERR_ARGUMENT;
+    }
+}
+
+int oracle_max_conflicts_export_ranges(const ad_batch* b, size_t mi, const uint64_t* is, const uint64_t* ie, const uint64_t* im,
+                                       const uint64_t* il, const int32_t* in, size_t* count, uint64_t* os, uint64_t* oe,
+                                       uint64_t* om, uint64_t* ol, int32_t* on) {
+    try {
+        Batch B(b);
+        IntervalMap map;
+        for (size_t x = 0; x < mi; ++x) map.merge_range(is[x], ie[x], Ts{im[x], il[x], in[x]});
+        for (uint32_t i = 0; i < (uint32_t)B.n; ++i) {
+            if (domain_of(B.tx[i]) != AD_DOMAIN_RANGE || !globally_visible(kind_of(B.tx[i]))) continue;
+            if (B.st[i] == AD_ST_TRANSITIVELY_KNOWN || B.st[i] == AD_ST_INVALID) continue;
+            for (uint32_t q = B.range_off[i]; q < B.range_off[i + 1]; ++q) map.merge_range(B.ranges[q].s, B.ranges[q].e, B.ex[i]);
+        }
+        std::vector<size_t> st, en;     // valued runs of one raw value
+        for (size_t g = 0; g < map.has.size(); ++g) {
+            if (!map.has[g]) continue;
+            const Ts& t = map.v[g];
+            const bool same = g > 0 && map.has[g - 1] && map.v[g - 1].msb == t.msb && map.v[g - 1].lsb == t.lsb &&
+                              map.v[g - 1].node == t.node;
+            if (same) en.back() = g;
+            else { st.push_back(g); en.push_back(g); }
+        }
+        *count = st.size();
+        if (!os) return AD_OK;
+        for (size_t k = 0; k < st.size(); ++k) {
+            const Ts& t = map.v[st[k]];
+            os[k] = map.b[st[k]]; oe[k] = map.b[en[k] + 1]; om[k] = t.msb; ol[k] = t.lsb; on[k] = t.node;
+        }
         return AD_OK;
     } catch (const std::exception&) {
         return AD_ERR_ARGUMENT;

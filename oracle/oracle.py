@@ -48,6 +48,10 @@ def lib():
                                               vp, vp, vp, vp]
         L.oracle_max_conflicts_export.argtypes = [C.POINTER(abi.AdBatch), C.c_size_t, vp, vp, vp, vp, C.POINTER(C.c_size_t),
                                                   vp, vp, vp, vp]
+        L.oracle_max_conflicts_ts_ranges.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_size_t, vp, vp, vp,
+                                                     vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_max_conflicts_export_ranges.argtypes = [C.POINTER(abi.AdBatch), C.c_size_t, vp, vp, vp, vp, vp,
+                                                         C.POINTER(C.c_size_t), vp, vp, vp, vp, vp]
         L.oracle_build.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_size_t,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]
@@ -155,18 +159,29 @@ def _carry(table):
     return tuple(np.ascontiguousarray(a, dt) for a, dt in zip(table, (np.uint64, np.uint64, np.uint64, np.int32)))
 
 
-def max_conflicts_ts(batch, cfg, carry=None):
-    """maxConflicts.get(keys) over a carried MaxConflicts table + the batch, as timestamps:
-    (msb [R, n], lsb [R, n], node [R, n], fast [R, n])."""
+EMPTY_CARRY_RANGES = (np.zeros(0, np.uint64),) * 4 + (np.zeros(0, np.int32),)
+
+
+def _carry_ranges(table):
+    table = EMPTY_CARRY_RANGES if table is None else table
+    return tuple(np.ascontiguousarray(a, dt) for a, dt in zip(table, (np.uint64,) * 4 + (np.int32,)))
+
+
+def max_conflicts_ts(batch, cfg, carry=None, carry_ranges=None):
+    """maxConflicts.get(keys or ranges) over a carried MaxConflicts map (key table + interval table) + the batch, as
+    timestamps: (msb [R, n], lsb [R, n], node [R, n], fast [R, n])."""
     b = abi.make_batch(batch)
     n, R = batch["n"], cfg.replicas
     ck, cm, cl, cn = _carry(carry)
+    rs, re_, rm, rl, rn = _carry_ranges(carry_ranges)
     om = np.zeros((R, max(n, 1)), np.uint64)
     ol = np.zeros((R, max(n, 1)), np.uint64)
     on = np.zeros((R, max(n, 1)), np.int32)
     fa = np.zeros((R, max(n, 1)), np.uint8)
-    rc = lib().oracle_max_conflicts_ts(C.byref(b), C.byref(cfg), len(ck), ck.ctypes.data, cm.ctypes.data, cl.ctypes.data,
-                                       cn.ctypes.data, om.ctypes.data, ol.ctypes.data, on.ctypes.data, fa.ctypes.data)
+    rc = lib().oracle_max_conflicts_ts_ranges(C.byref(b), C.byref(cfg), len(ck), ck.ctypes.data, cm.ctypes.data,
+                                              cl.ctypes.data, cn.ctypes.data, len(rs), rs.ctypes.data, re_.ctypes.data,
+                                              rm.ctypes.data, rl.ctypes.data, rn.ctypes.data, om.ctypes.data,
+                                              ol.ctypes.data, on.ctypes.data, fa.ctypes.data)
     if rc != abi.AD_OK:
         raise ValueError("oracle_max_conflicts_ts rc=%d" % rc)
     return om[:, :n].copy(), ol[:, :n].copy(), on[:, :n].copy(), fa[:, :n].copy()
@@ -185,6 +200,21 @@ def max_conflicts_export(batch, carry=None):
            np.zeros(max(m.value, 1), np.int32))
     lib().oracle_max_conflicts_export(C.byref(b), len(ck), ck.ctypes.data, cm.ctypes.data, cl.ctypes.data, cn.ctypes.data,
                                       C.byref(m), *(a.ctypes.data for a in out))
+    return tuple(a[:m.value].copy() for a in out)
+
+
+def max_conflicts_export_ranges(batch, carry_ranges=None):
+    """The interval part of the MaxConflicts map after the batch: (starts, ends, msb, lsb, node), pieces (s, e]."""
+    b = abi.make_batch(batch)
+    rs, re_, rm, rl, rn = _carry_ranges(carry_ranges)
+    args = (len(rs), rs.ctypes.data, re_.ctypes.data, rm.ctypes.data, rl.ctypes.data, rn.ctypes.data)
+    m = C.c_size_t()
+    rc = lib().oracle_max_conflicts_export_ranges(C.byref(b), *args, C.byref(m), None, None, None, None, None)
+    if rc != abi.AD_OK:
+        raise ValueError("oracle_max_conflicts_export_ranges rc=%d" % rc)
+    k = max(m.value, 1)
+    out = (np.zeros(k, np.uint64),) + tuple(np.zeros(k, np.uint64) for _ in range(3)) + (np.zeros(k, np.int32),)
+    lib().oracle_max_conflicts_export_ranges(C.byref(b), *args, C.byref(m), *(a.ctypes.data for a in out))
     return tuple(a[:m.value].copy() for a in out)
 
 

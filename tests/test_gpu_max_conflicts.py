@@ -81,17 +81,23 @@ def test_after_merge_and_levels(engine_factory):
     assert np.array_equal(r0, r1) and np.array_equal(f0, f1)
 
 
-def test_call_order_and_range_carry_rejected(engine_factory):
+def test_call_order_and_carry_validation(engine_factory):
     eng = engine_factory()
     b = workload.generate(2000, range_frac=0.1, seed=3)
     eng.load(b)
     with pytest.raises(engine.IllegalStateException):
         eng.max_conflicts()                            # before ad_preaccept_deps
     eng.preaccept_deps()
+    with pytest.raises(engine.IllegalStateException):
+        eng.max_conflicts_export_ranges()              # before ad_max_conflicts(_ts)
     eng.max_conflicts()
-    with pytest.raises(engine.AccordDepsError) as e:
-        eng.max_conflicts_ts()                         # the carried map is per key
-    assert e.value.rc == abi.AD_ERR_UNSUPPORTED
+    eng.max_conflicts_ts()                             # range txns: the carried map covers ranges too
+    one = np.ones(2, np.uint64)
+    for s_, e_ in (([5, 3], [6, 9]), ([1, 4], [5, 8]), ([4, 9], [4, 12])):   # unsorted, overlapping, empty
+        with pytest.raises(engine.AccordDepsError) as e:
+            eng.max_conflicts_carry_ranges((np.array(s_, np.uint64), np.array(e_, np.uint64), one, one,
+                                            np.ones(2, np.int32)))
+        assert e.value.rc == abi.AD_ERR_ARGUMENT
 
 
 @pytest.mark.parametrize("n,keyspace,rf,width,window,replicas,drop", [(3000, 3000, 0.2, 200, 16, 3, 0.2),
@@ -205,3 +211,79 @@ def test_gpu_fast_path_merge(engine_factory, name, window, drop):
     eng.merge()
     full = O.OracleResult(b, abi.make_config(window, R, drop, 0x51DE), O.FLAG_MERGE)
     assert eng.fetch_merged(abi.CLASS_KEY).equal(full.merged(abi.CLASS_KEY))
+
+
+# ---- the carried map's range part: intervals (s, e] from range txns (ad_max_conflicts_carry_ranges / _export_ranges)
+def _store_chain(engine_factory, batches, cfg_args, carry_k=None, carry_r=None):
+    eng = engine_factory(window=cfg_args[0], replicas=cfg_args[1], drop_p=cfg_args[2], seed=cfg_args[3])
+    out = []
+    for b in batches:
+        eng.load(b)
+        eng.preaccept_deps()
+        eng.max_conflicts_carry(O.EMPTY_CARRY if carry_k is None else carry_k)
+        eng.max_conflicts_carry_ranges(O.EMPTY_CARRY_RANGES if carry_r is None else carry_r)
+        ts = tuple(a.copy() for a in eng.max_conflicts_ts())
+        carry_k = tuple(a.copy() for a in eng.max_conflicts_export())
+        carry_r = tuple(a.copy() for a in eng.max_conflicts_export_ranges())
+        out.append((ts, carry_k, carry_r))
+    return out
+
+
+def _mixed_batch(n, keyspace, width, seed, hlc_start):
+    rng = np.random.default_rng(seed)
+    kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT,
+                        abi.KIND_EXCLUSIVE_SYNC_POINT], p=[0.35, 0.35, 0.1, 0.1, 0.1], size=n)
+    status = rng.integers(0, 8, size=n).astype(np.uint8)
+    return workload.generate(n, keys_per_txn=3, keyspace=keyspace, range_frac=0.2, range_width_max=width, seed=seed,
+                             slow_frac=0.3, bump_max=400, kinds=kinds, status=status, hlc_start=hlc_start)
+
+
+@pytest.mark.parametrize("n,keyspace,width,window,replicas,drop", [(3000, 2000, 100, 16, 3, 0.2),
+                                                                   (6000, 50000, 3000, 32, 2, 0.1),
+                                                                   (2000, 1 << 44, 1 << 38, 0, 1, 0.0)])
+def test_gpu_range_carry_chain_equals_oracle(engine_factory, n, keyspace, width, window, replicas, drop):
+    # four batches of one store with key AND range txns: every batch's maxConflicts timestamps / fast flags and
+    # both tables after it equal the oracle's (the last case spreads the breakpoints beyond 32 bits: two LSD passes)
+    batches = [_mixed_batch(n, keyspace, width, 300 + k, 1_000_000 + 80_000 * k) for k in range(4)]
+    cfg_args = (window, replicas, drop, 0xCAFE)
+    got = _store_chain(engine_factory, batches, cfg_args)
+    cfg = abi.make_config(*cfg_args)
+    ck = cr = None
+    for k, (b, (ts, gk, gr)) in enumerate(zip(batches, got)):
+        want = O.max_conflicts_ts(b, cfg, ck, cr)
+        for x, y, name in zip(ts, want, ("msb", "lsb", "node", "fast")):
+            bad = np.nonzero((x != y).any(axis=0))[0]
+            assert len(bad) == 0, "batch %d %s differs at txns %s" % (k, name, bad[:8])
+        ck = O.max_conflicts_export(b, ck)
+        cr = O.max_conflicts_export_ranges(b, cr)
+        assert all(np.array_equal(x, y) for x, y in zip(gk, ck)), "batch %d key table" % k
+        assert len(gr[0]) == len(cr[0]), "batch %d: %d pieces vs oracle %d" % (k, len(gr[0]), len(cr[0]))
+        assert all(np.array_equal(x, y) for x, y in zip(gr, cr)), "batch %d intervals" % k
+    assert cr[0].size > 0 and ck[0].size > 0
+    is_range = (batches[-1]["txn_lsb"] & np.uint64(1)).astype(bool)
+    assert (got[-1][0][3][:, is_range] == 0).any()     # range txns pushed off the fast path by the carry
+
+
+def test_gpu_range_carry_seeded_and_empty(engine_factory):
+    # a host-seeded interval table (no range txns in the batch) passes through the export unchanged but normalised;
+    # a batch of key txns stabs it; an empty map exports nothing
+    rng = np.random.default_rng(9)
+    cuts = np.unique(rng.integers(0, 5000, size=400)).astype(np.uint64)
+    s_, e_ = cuts[0:-1:2], cuts[1::2]
+    k = min(len(s_), len(e_))
+    s_, e_ = s_[:k], e_[:k]
+    h = (1_000_000 + rng.integers(0, 3, size=k)).astype(np.uint64)     # few values: equal neighbours coalesce
+    msb = np.full(k, 1 << 16, np.uint64)
+    lsb = (h << np.uint64(16)) | np.uint64(abi.KIND_WRITE << 1 | 1)
+    node = np.ones(k, np.int32)
+    carry_r = (s_, e_, msb, lsb, node)
+    b = workload.generate(3000, keys_per_txn=2, keyspace=5000, seed=10, hlc_start=900_000)
+    got = _store_chain(engine_factory, [b], (0, 1, 0.0, 1), None, carry_r)
+    cfg = abi.make_config(0, 1, 0.0, 1)
+    want = O.max_conflicts_ts(b, cfg, None, carry_r)
+    assert all(np.array_equal(x, y) for x, y in zip(got[0][0], want))
+    assert (got[0][0][3] == 0).any()
+    wr = O.max_conflicts_export_ranges(b, carry_r)
+    assert all(np.array_equal(x, y) for x, y in zip(got[0][2], wr))
+    empty = _store_chain(engine_factory, [b], (0, 1, 0.0, 1))
+    assert empty[0][2][0].size == 0

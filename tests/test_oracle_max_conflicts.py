@@ -183,3 +183,139 @@ def test_reduce_witnessed_across_stores():
         got_rank, got_fast, _ = sharding.reduce_witnessed(b, parts)
         assert np.array_equal(got_rank, want_rank) and np.array_equal(got_fast, want_fast)
     assert want_fast.min() == 0
+
+
+# ---- the carried map's range part (ad_max_conflicts_carry_ranges / _export_ranges) -------------------------------
+def _order(msb, lsb, node):
+    """Timestamp.compareTo key (Timestamp.java:208-217), then raw lsb: the tie rule of the carried map."""
+    return (int(msb), int(lsb) >> 16, int(lsb) & 0x1E, int(node), int(lsb))
+
+
+def _recorded_ranges(b):
+    """(start, end, ts) of every range the batch's recorded range txns cover (globally visible kinds, status not
+    TRANSITIVELY_KNOWN / INVALID)."""
+    out = []
+    if b["range_off"] is None:
+        return out
+    for i in range(b["n"]):
+        lsb = int(b["txn_lsb"][i])
+        kind, dom, st = (lsb >> 1) & 0xF, lsb & 1, int(b["status"][i])
+        if dom != 1 or kind not in (R, W, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT):
+            continue
+        if st in (abi.ST_TRANSITIVELY_KNOWN, abi.ST_INVALID):
+            continue
+        ts = (int(b["exec_msb"][i]), int(b["exec_lsb"][i]), int(b["exec_node"][i]))
+        for q in range(int(b["range_off"][i]), int(b["range_off"][i + 1])):
+            out.append((int(b["range_start"][q]), int(b["range_end"][q]), ts))
+    return out
+
+
+def _sweep_export(b, carry_ranges):
+    """Independent restatement of the interval export: every breakpoint, the max over what contains each elementary
+    gap, maximal runs of one value (the oracle merges txn by txn instead)."""
+    pieces = [(int(s), int(e), (int(m), int(l), int(n))) for s, e, m, l, n in zip(*carry_ranges)]
+    pieces += _recorded_ranges(b)
+    xs = sorted({p for s, e, _ in pieces for p in (s, e)})
+    vals = []
+    for g in range(len(xs) - 1):
+        y = xs[g + 1]
+        best = None
+        for s, e, t in pieces:
+            if s < y <= e and (best is None or _order(*t) > _order(*best)):
+                best = t
+        vals.append(best)
+    out = []
+    for g, v in enumerate(vals):
+        if v is None:
+            continue
+        if out and out[-1][1] == xs[g] and out[-1][2] == v:
+            out[-1] = (out[-1][0], xs[g + 1], v)
+        else:
+            out.append((xs[g], xs[g + 1], v))
+    return out
+
+
+def _random_carry_ranges(rng, keyspace, hlc, count):
+    cuts = np.unique(rng.integers(0, keyspace, size=2 * count))
+    s, e = cuts[0:-1:2], cuts[1::2]
+    k = min(len(s), len(e))
+    s, e = s[:k].astype(np.uint64), e[:k].astype(np.uint64)
+    epoch = np.ones(k, np.uint64)
+    h = hlc + rng.integers(0, 400, size=k)
+    msb = (epoch << np.uint64(16)) | (np.asarray(h, np.uint64) >> np.uint64(48))
+    lsb = (np.asarray(h, np.uint64) << np.uint64(16)) | (np.uint64(abi.KIND_WRITE << 1) | np.uint64(1))
+    node = rng.integers(1, 9, size=k).astype(np.int32)
+    return s, e, msb, lsb, node
+
+
+def _range_batch(seed, n=400, keyspace=600):
+    rng = np.random.default_rng(seed)
+    kinds = rng.choice([R, W, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT],
+                       p=[0.35, 0.35, 0.1, 0.1, 0.1], size=n)
+    status = rng.integers(0, 8, size=n).astype(np.uint8)
+    return workload.generate(n, keys_per_txn=2, keyspace=keyspace, range_frac=0.3, range_width_max=80, seed=seed,
+                             slow_frac=0.3, bump_max=300, kinds=kinds, status=status)
+
+
+def test_export_ranges_equals_sweep():
+    for seed in (11, 12, 13):
+        b = _range_batch(seed)
+        rng = np.random.default_rng(seed)
+        carry = _random_carry_ranges(rng, 600, 1_000_000, 40) if seed != 11 else O.EMPTY_CARRY_RANGES
+        got = O.max_conflicts_export_ranges(b, carry)
+        want = _sweep_export(b, carry)
+        assert [(int(s), int(e), (int(m), int(l), int(n))) for s, e, m, l, n in zip(*got)] == want
+        assert len(want) > 10
+        # normal form: sorted, disjoint, no two touching pieces of one value
+        assert all(got[1][k] <= got[0][k + 1] for k in range(len(want) - 1))
+
+
+def test_ts_folds_carried_points_and_intervals():
+    for seed in (21, 22):
+        b = _range_batch(seed)
+        rng = np.random.default_rng(seed)
+        carry_r = _random_carry_ranges(rng, 600, 1_000_500, 30)
+        keys = np.unique(rng.integers(0, 600, size=80)).astype(np.uint64)
+        kh = 1_000_000 + rng.integers(0, 900, size=len(keys))
+        kmsb = (np.uint64(1) << np.uint64(16)) | (kh.astype(np.uint64) >> np.uint64(48))
+        klsb = kh.astype(np.uint64) << np.uint64(16) | np.uint64(abi.KIND_WRITE << 1)
+        carry_k = (keys, kmsb, klsb, rng.integers(1, 9, size=len(keys)).astype(np.int32))
+        cfg = abi.make_config(8, 2, 0.2, 0xF00 + seed)
+        om, ol, on, fast = O.max_conflicts_ts(b, cfg, carry_k, carry_r)
+        rank, _ = O.max_conflicts(b, cfg)
+        is_range = (b["txn_lsb"] & np.uint64(1)).astype(bool)
+        for i in range(b["n"]):
+            best = None
+            def fold(t):
+                nonlocal best
+                if best is None or _order(*t) > _order(*best):
+                    best = t
+            if not is_range[i]:
+                for p in range(int(b["key_off"][i]), int(b["key_off"][i + 1])):
+                    k = int(b["keys"][p])
+                    for x in range(len(keys)):
+                        if int(keys[x]) == k:
+                            fold((int(carry_k[1][x]), int(carry_k[2][x]), int(carry_k[3][x])))
+                    for s, e, m, l, n in zip(*carry_r):
+                        if int(s) < k <= int(e):
+                            fold((int(m), int(l), int(n)))
+            else:
+                for q in range(int(b["range_off"][i]), int(b["range_off"][i + 1])):
+                    qs, qe = int(b["range_start"][q]), int(b["range_end"][q])
+                    for x in range(len(keys)):
+                        if qs < int(keys[x]) <= qe:
+                            fold((int(carry_k[1][x]), int(carry_k[2][x]), int(carry_k[3][x])))
+                    for s, e, m, l, n in zip(*carry_r):
+                        if int(s) < qe and int(e) > qs:
+                            fold((int(m), int(l), int(n)))
+            for v in range(2):
+                t = best
+                r = int(rank[v, i])
+                if r != NONE:
+                    bt = (int(b["exec_msb"][r]), int(b["exec_lsb"][r]), int(b["exec_node"][r]))
+                    if t is None or _order(*bt)[:4] > _order(*t)[:4]:
+                        t = bt
+                assert (int(om[v, i]), int(ol[v, i]), int(on[v, i])) == (t if t is not None else (0, 0, 0)), (v, i)
+                me = (int(b["txn_msb"][i]), int(b["txn_lsb"][i]), int(b["txn_node"][i]))
+                assert int(fast[v, i]) == int(t is None or _order(*me)[:4] >= _order(*t)[:4])
+        assert fast.min() == 0 and fast.max() == 1
