@@ -1132,6 +1132,178 @@ static __global__ __launch_bounds__(256) void k_xedges(XEdgeArgs a) {
     if (!FILL && local) atomicAdd(&a.indeg[t], local);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// One-pass levels for mixed key + range batches (C4): every txn pulls its level from its sources — (a) its
+// key-chain predecessor runs (the chain build in pred mode), (b)/(c) the same sources k_xedges turns into Kahn
+// edges — instead of the sources pushing ~10^9 releases through the wavefronts (C4: 1.74·10^9 (b)/(c) edges, one
+// returning atomic each, plus 5,650 grid-wide wavefront launches).  Every source of T has a strictly smaller
+// executeAt (no ExclusiveSyncPoint / EphemeralRead in the batch: those await deps of any executeAt), so the txns
+// are taken in executeAt order (k_window_rank's permutation): a grid of co-resident waves (sized from the
+// occupancy) walks the ranks, wave w taking ranks w, w + W, w + 2W, ...; each txn is pulled by the whole wave,
+// its lanes striding over the source lists MP_ILP loads at a time and waiting on sources not yet final.  By
+// induction on the rank the lowest unfinished txn's wave is at it and every source it waits on is final, so
+// nothing deadlocks, and the waiting is bounded to the resident window instead of the whole batch (the earlier
+// per-txn pull of mixed batches kept ~10^6 lanes polling; 64-txn chunks per wave serialised their txns).
+// The (c) sources are listed per txn beforehand (k_csrc).  A wait longer than ~1 s raises *abort; every wave
+// then leaves and the caller runs the Kahn path.
+struct MixPullArgs {
+    size_t n;
+    const uint32_t* perm;                // executeAt rank -> txn
+    const uint32_t* key_off;
+    const uint2* pred;                   // (a) predecessor runs per pair (PRED_TXN: one txn in .x)
+    const uint32_t* c_txn;
+    const uint8_t* c_meta;
+    EdgeArgs e;                          // (b) merged direct / range deps; (c) merged KeyDeps + cons_pos
+    int do_b, do_c;
+    const unsigned long long* coff;      // (c) sources as a list per txn (k_csrc): cs[coff[t] .. coff[t + 1])
+    const uint32_t* cs;
+    uint32_t* L;                         // levels | LV_FINAL
+    uint32_t* abort_flag;
+    uint32_t* maxlvl;
+};
+constexpr int MP_GRID = 2048;         // co-resident workgroups at most (8 per CU)
+// the (c) sources of unmanaged t this lane owns (its share of t's merged KeyDeps keys): per key with a
+// constraint position p, the Reads after the last Write at or before p and that Write (k_xedges' rule)
+template <class F>
+__device__ inline void mp_c_walk(const MixPullArgs& a, uint32_t t, uint32_t lane, F&& f) {
+    const EdgeArgs& e = a.e;
+    for (uint32_t x = e.mk_key_off[t] + lane; x < e.mk_key_off[t + 1]; x += WAVE) {
+        const int32_t p = e.cons_pos[x];
+        if (p < 0) continue;
+        const int32_t s0 = e.seg_start[p];
+        for (int32_t q = p;; --q) {
+            const uint32_t mq = a.c_meta[q];
+            if (manages_execution(mq)) {
+                f(e.c_txn[q]);
+                if (meta_kind(mq) == AD_KIND_WRITE) break;
+            }
+            if (q == s0) break;
+        }
+    }
+}
+// (c) source lists, one wave per txn (lanes stride its keys): count pass -> cnt[t]; fill pass (offsets scanned)
+// -> each lane writes its sources after the lanes before it.  No atomics: a txn writes its own run.
+template <bool FILL>
+static __global__ __launch_bounds__(256) void k_csrc(MixPullArgs a, unsigned long long* __restrict__ cnt, uint32_t* __restrict__ cs) {
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (t >= a.n) return;
+    const uint32_t lane = (uint32_t)__lane_id();
+    if (manages_execution(a.e.meta[t])) {
+        if (!FILL && lane == 0) cnt[t] = 0;
+        return;
+    }
+    uint32_t c = 0;
+    mp_c_walk(a, (uint32_t)t, lane, [&](uint32_t) { ++c; });
+    if (!FILL) {
+        c = wave_sum(c);
+        if (lane == 0) cnt[t] = c;
+        return;
+    }
+    uint32_t inc = c;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += y;
+    }
+    unsigned long long w = a.coff[t] + (inc - c);
+    mp_c_walk(a, (uint32_t)t, lane, [&](uint32_t src) { cs[w++] = src; });
+}
+__device__ inline uint32_t mp_load(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// wait until L[s] is final (or the pull is abandoned: *ab); returns it
+__device__ inline uint32_t mp_wait(const MixPullArgs& a, uint32_t s, uint32_t v, bool& ab) {
+    uint32_t spins = 0;
+    const uint64_t w0 = wall_clock64();
+    while (!(v & LV_FINAL)) {
+        if ((++spins & 63u) == 0u && (wall_clock64() - w0 > PULL_CAP_TICKS || mp_load(a.abort_flag) != 0u)) {
+            ab = true;
+            return LV_FINAL;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        v = mp_load(&a.L[s]);
+    }
+    return v;
+}
+// a heavy txn's share of one source list ids[b, e) (lane-strided), MP_ILP ids at a time: the id loads, (b) the
+// executeAt filter, the level loads, then the waits — a few memory round trips per MP_ILP * 64 sources
+constexpr int MP_ILP = 8;
+template <bool FILTER, class I>
+__device__ inline void mp_wait_list(const MixPullArgs& a, const uint32_t* __restrict__ ids, I b, I e, uint32_t lane, uint64_t my,
+                                    uint32_t& m, bool& ab) {
+    for (I x = b + lane; x < e && !ab; x += (I)WAVE * MP_ILP) {
+        uint32_t sv[MP_ILP], lv[MP_ILP];
+        bool use[MP_ILP];
+#pragma unroll
+        for (int u = 0; u < MP_ILP; ++u) { const I y = x + (I)u * WAVE; use[u] = y < e; sv[u] = use[u] ? ids[y] : 0u; }
+        if (FILTER) {
+#pragma unroll
+            for (int u = 0; u < MP_ILP; ++u) use[u] = use[u] && a.e.ex1[sv[u]] < my;
+        }
+#pragma unroll
+        for (int u = 0; u < MP_ILP; ++u) lv[u] = use[u] ? mp_load(&a.L[sv[u]]) : LV_FINAL;
+#pragma unroll
+        for (int u = 0; u < MP_ILP; ++u) {
+            if (!use[u]) continue;
+            const uint32_t v = (lv[u] & LV_FINAL) ? lv[u] : mp_wait(a, sv[u], lv[u], ab);
+            const uint32_t l = (v & ~LV_FINAL) + 1u;
+            m = l > m ? l : m;
+        }
+    }
+}
+static __global__ __launch_bounds__(256) void k_level_pull_mixed(MixPullArgs a) {
+    const uint32_t lane = (uint32_t)__lane_id();
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const size_t W = (size_t)gridDim.x * blockDim.x / WAVE;
+    uint32_t wmax = 0;
+    for (size_t r = w; r < a.n; r += W) {
+        const uint32_t t = a.perm[r];
+        uint32_t m = 0;
+        bool ab = false;
+        // (a) predecessor runs (a handful): lane-strided over the pairs
+        for (uint32_t p = a.key_off[t] + lane; p < a.key_off[t + 1] && !ab; p += WAVE) {
+            const uint2 pr = a.pred[p];
+            const bool one = (pr.y & PRED_TXN) != 0u;
+            const uint32_t len = pr.y & ~PRED_TXN;
+            for (uint32_t x = 0; x < len && !ab; ++x) {
+                const uint32_t src = one ? pr.x : a.c_txn[pr.x + x];
+                const uint32_t v = mp_wait(a, src, mp_load(&a.L[src]), ab);
+                const uint32_t l = (v & ~LV_FINAL) + 1u;
+                m = l > m ? l : m;
+            }
+        }
+        if (a.do_b) {
+            const uint64_t my = a.e.ex1[t];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                if (a.e.txns[c]) {
+                    const uint32_t b0 = a.e.ent_off[c][t];
+                    mp_wait_list<true, uint32_t>(a, a.e.txns[c], b0, b0 + a.e.tcnt[c][t], lane, my, m, ab);
+                }
+        }
+        if (a.do_c) mp_wait_list<false, unsigned long long>(a, a.cs, a.coff[t], a.coff[t + 1], lane, 0ull, m, ab);
+        if (__ballot(ab)) {
+            if (lane == 0) __hip_atomic_store(a.abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        m = wave_max(m);
+        if (lane == 0) __hip_atomic_store(&a.L[t], m | LV_FINAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wmax = m > wmax ? m : wmax;
+    }
+    if (lane == 0 && wmax) atomicMax(a.maxlvl, wmax);
+}
+// kinds a mixed pull cannot take: ExclusiveSyncPoint / EphemeralRead (their deps need not precede them in executeAt)
+static __global__ __launch_bounds__(256) void k_mix_kinds(size_t n, const uint8_t* __restrict__ meta, uint32_t* __restrict__ flag) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    wave_set_flag(t < n && awaits_only_deps(meta[t]), flag);
+}
+// the executeAt permutation from k_window_rank: every slot filled and the keys ascending, else *bad
+static __global__ __launch_bounds__(256) void k_perm_check(size_t n, const uint64_t* __restrict__ key, const uint32_t* __restrict__ perm,
+                                                    uint32_t* __restrict__ bad) {
+    bool b = false;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        if (perm[i] == 0xFFFFFFFFu || (i + 1 < n && key[i] > key[i + 1])) b = true;
+    wave_set_flag(b, bad);
+}
+
 // Small device results to the host without a stream sync (the engine's host-mapped coherent buffer, see
 // engine.hip read_totals_params): copy a[0..na) and b[0..nb) to pub[off..], fence, bump pub[0] = seq.
 static __global__ __launch_bounds__(128) void k_publish2(const uint32_t* __restrict__ a, int na, const uint32_t* __restrict__ b, int nb,
@@ -1186,6 +1358,8 @@ struct LevelState {
     size_t capP = 0, capN = 0, capK = 0;
     Publisher pub;                      // set by the engine: flag read-backs without a stream sync
     bool pull_off = false;              // AD_LEVELS_KAHN: skip the one-pass pull levels
+    bool mixpull_off = false;           // AD_LEVELS_NO_MIXPULL: mixed batches straight to the Kahn wavefronts
+    int mixpull_path = 0;               // last mixed pull: 0 none, 1 pulled, 2 long chain, 3 kinds, 4 rank miss, 5 aborted
     bool pull_force_abort = false;      // AD_LEVELS_PULL_ABORT (tests): every pull lane aborts, Kahn recomputes
     int pull_path = 0;                  // last pull attempt: 0 none, 1 pulled, 2 far predecessors -> Kahn, 3 aborted -> Kahn
     int kb_hint = 0;                    // wavefronts in the first Kahn launch batch (previous depth + 1)
@@ -1591,6 +1765,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     }
 
     ls.pull_path = 0;
+    ls.mixpull_path = 0;
     {
         // flags; levels (unless given); the pull path's predecessor runs (zero: none) for pure key batches
         const bool pull_try = in.kahn_ok && !in.keep_levels && P > 0 && !ls.pull_off && in.n_large == 0 && in.n_special == 0 &&
@@ -1716,6 +1891,95 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             }
             hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);     // aborted / far: the wavefronts below
         }
+        // ---- one-pass pull levels for mixed key + range batches (k_level_pull_mixed): executeAt order,
+        // persistent waves; kinds whose deps may follow them in executeAt, a long chain or a rank miss (a far
+        // slow-path bump) skip it, an abort falls through to the Kahn wavefronts
+        if (in.kahn_ok && !in.keep_levels && P > 0 && in.n_special == 0 && (has_b || has_c) && !ls.pull_off && !ls.mixpull_off) {
+            ls.chains_ready = false;
+            uint32_t fl[32] = {0};
+            const int gn1 = ceil_div((long)n, 256);
+            {
+                KScope ks(K_KAHN, P);
+                k_mix_kinds<<<gn1, 256, 0, st>>>(n, in.meta, ls.flags + 20);
+                hipMemsetAsync(ls.succ, 0, P * 8, st);
+                if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
+                k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0, 1);
+                hipMemsetAsync(ls.sv1, 0xFF, n * 4, st);
+                k_window_rank<<<ceil_div((long)n, WR_N), WR_T, 0, st>>>(n, in.ex1, nullptr, in.lvl, ls.key64, ls.sv1, ls.sk1, ls.flags + 21);
+                k_perm_check<<<std::min(gn1, 2048), 256, 0, st>>>(n, ls.key64, ls.sv1, ls.flags + 21);
+            }
+            if (hipMemcpyAsync(fl, ls.flags, sizeof(fl), hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+                err = "exec levels: device error";
+                return AD_ERR_DEVICE;
+            }
+            if (fl[5]) {
+                err = "exec levels: local-only txns are not part of the batch execution order";
+                return AD_ERR_UNSUPPORTED;
+            }
+            ls.mixpull_path = fl[7] ? 2 : (fl[20] ? 3 : (fl[21] ? 4 : 0));
+            if (!fl[7] && !fl[20] && !fl[21]) {
+                uint32_t res[2] = {0, 0};
+                {
+                    KScope ks(K_KAHN, P);
+                    MixPullArgs ma{};
+                    ma.n = n; ma.perm = ls.sv1; ma.key_off = in.key_off; ma.pred = ls.succ; ma.c_txn = ls.c_txn; ma.c_meta = ls.c_meta;
+                    ma.e = ea; ma.do_b = has_b ? 1 : 0; ma.do_c = has_c ? 1 : 0; ma.L = in.lvl;
+                    ma.abort_flag = ls.flags + 23; ma.maxlvl = ls.flags + 24;
+                    if (has_c) {
+                        // (c) sources per txn: count, offsets, fill (one sync for the total)
+                        if (ls.capX < n + 1 || !ls.xcnt) {
+                            const size_t c = n + 1;
+                            if (!grow((void**)&ls.xcnt, c * 8) || !grow((void**)&ls.xoff, c * 8) || !grow((void**)&ls.xcur, c * 8)) goto oom;
+                            ls.capX = c;
+                        }
+                        k_unmanaged_prep<<<ceil_div((long)n * WAVE, 256), 256, 0, st>>>(ea);
+                        const int gw = ceil_div((long)n * WAVE, 256);
+                        k_csrc<false><<<gw, 256, 0, st>>>(ma, ls.xcnt, nullptr);
+                        device_scan(SumOp<unsigned long long>{ls.xcnt, ls.xoff, n}, n, (unsigned long long*)ls.agg, st);
+                        unsigned long long ctot = 0;
+                        if (hipMemcpyAsync(&ctot, ls.xoff + n, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                            hipStreamSynchronize(st) != hipSuccess) {
+                            err = "exec levels: device error";
+                            return AD_ERR_DEVICE;
+                        }
+                        if (ls.xs_cap < ctot || !ls.xs) {
+                            const size_t c = std::max<size_t>(ctot + ctot / 8, 1);
+                            if (!grow((void**)&ls.xs, c * 4)) goto oom;
+                            ls.xs_cap = c;
+                        }
+                        ma.coff = ls.xoff;
+                        ma.cs = ls.xs;
+                        k_csrc<true><<<gw, 256, 0, st>>>(ma, nullptr, ls.xs);
+                    }
+                    // every wave must be resident at once (rank-strided waits): the occupancy bound, with margin
+                    int occ = 0, dev = 0, cus = 0;
+                    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_level_pull_mixed, 256, 0) != hipSuccess || occ < 1) occ = 1;
+                    hipGetDevice(&dev);
+                    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
+                    const int grid = std::max(1, std::min({gn1, MP_GRID, occ * cus * 3 / 4}));
+                    k_level_pull_mixed<<<grid, 256, 0, st>>>(ma);
+                    k_level_strip<<<gn1, 256, 0, st>>>(n, in.lvl);
+                }
+                if (hipMemcpyAsync(res, ls.flags + 23, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+                    err = "exec levels: device error";
+                    return AD_ERR_DEVICE;
+                }
+                if (!res[0]) {
+                    ls.mixpull_path = 1;
+                    const int lv = (int)res[1] + 1;
+                    *iters = lv;
+                    if (want_order && n > 0 && in.order_verify)
+                        *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, lv - 1, in.order_verify);
+                    else if (want_order && n > 0)
+                        order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st);
+                    return AD_OK;
+                }
+                ls.mixpull_path = 5;                                               // aborted
+                hipMemsetAsync(in.lvl, 0, std::max<size_t>(n, 1) * 4, st);
+            }
+            hipMemsetAsync(ls.flags + 7, 0, 4, st);
+        }
         if (in.kahn_ok && !in.keep_levels && P > 0 && in.n_special == 0) {
             ls.chains_ready = false;
             int lv = 0;
@@ -1788,6 +2052,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                         err = "exec levels: device error";
                         return AD_ERR_DEVICE;
                     }
+                    if (getenv("AD_DEBUG_LEVELS")) fprintf(stderr, "kahn xedges: %llu edges over %zu txns\n", etot, n);
                     {
                         if (ls.xs_cap < etot || !ls.xs) {
                             const size_t c = std::max<size_t>(etot + etot / 8, 1);

@@ -74,7 +74,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     h->level_iters = (uint32_t)iters;
     h->times.level_rounds = h->ls.bl_rounds;
     h->times.level_blocks = h->ls.bl_used ? h->ls.bl.nblocks : 0;
-    h->times.level_path = (uint32_t)h->ls.pull_path;
+    h->times.level_path = h->ls.mixpull_path ? 10u + (uint32_t)h->ls.mixpull_path : (uint32_t)h->ls.pull_path;
     h->have_levels = true;
     return AD_OK;
 }

@@ -306,7 +306,10 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
     uint32_t key_classes;           /* key-footprint CSRs the deps stage computed per batch: 2R, or */
                                     /* R when the batch has no directKeyDeps (no key sync points)   */
     uint32_t level_path;            /* the pull levels' outcome: 0 not tried, 1 pulled, 2 a far    */
-                                    /* predecessor (> 65536 rows ahead) -> Kahn, 3 aborted -> Kahn   */
+                                    /* predecessor (> 65536 rows ahead) -> Kahn, 3 aborted -> Kahn;  */
+                                    /* mixed key + range batches 10 + (1 pulled in executeAt order,  */
+                                    /* 2 long chain, 3 ExclusiveSyncPoint / EphemeralRead present, 4 */
+                                    /* executeAt rank miss, 5 aborted) -> else the Kahn wavefronts   */
     uint32_t deferred_txns;         /* small txns the walk's inline ids could not finish: unioned by  */
                                     /* k_txn_union (the rest by k_txn_finish)                         */
     uint32_t fill_items;            /* (txn, key) entries the fill walk re-walks (pairs of txns with   */

@@ -172,6 +172,9 @@ def test_gpu_preaccept_kat_multi_key(engine_factory):
     clock.now = Wt.from_values(1, 100, 0, 1)
     w = Wt.preaccept_witnessed_at(Wt.from_values(1, 50, abi.KIND_WRITE << 1, 3), (int(m2[0, 0]), int(l2[0, 0]), int(n2[0, 0])), clock)
     assert (Wt.epoch(w), Wt.hlc(w), w[2]) == (1, 110, 1)
+    # PreAcceptOk.equals -> Timestamp.equals (Timestamp.java:244-249): the identity flags (kind, domain) included
+    assert Wt.equals(w, Wt.from_values(1, 110, abi.KIND_WRITE << 1, 1))
+    assert not Wt.equals(w, Wt.from_values(1, 110, 0, 1))
 
 
 @pytest.mark.parametrize("keyspace,window,replicas,drop", [(40, 0, 1, 0.0), (300, 16, 3, 0.2), (5000, 32, 2, 0.1)])

@@ -320,6 +320,42 @@ def test_c4_scaled(engine_factory):
     check(engine_factory, b)
 
 
+@pytest.mark.parametrize("n,keyspace,rf,width,slow,bump", [(40000, 400_000, 0.1, 1 << 13, 0.1, 16),
+                                                            (30000, 20000, 0.2, 300, 0.3, 16),
+                                                            (30000, 20000, 0.2, 300, 0.3, 200),
+                                                            (20000, 3000, 0.05, 50, 0.5, 2000)])
+def test_mixed_pull_levels(engine_factory, n, keyspace, rf, width, slow, bump):
+    # mixed key + range batches take the executeAt-ordered pull (k_level_pull_mixed, level_path 11) unless a
+    # slow-path bump moves an executeAt beyond the rank window (then 14 -> Kahn); either way the oracle's levels
+    # and order, and the Kahn wavefronts (AD_LEVELS_KAHN) on the same batch agree
+    kinds = np.where(np.random.default_rng(n).random(n) < 0.5, abi.KIND_WRITE, abi.KIND_READ)
+    b = workload.generate(n, 4, keyspace, "uniform", range_frac=rf, range_width_max=width, slow_frac=slow,
+                          bump_max=bump, kinds=kinds, seed=n + keyspace)
+    eng = engine_factory()
+    check(engine_factory, b, eng=eng)
+    path = eng.last_times()["level_path"]
+    assert path in (11, 14), path
+    if bump <= 16:                                            # within k_window_rank's +-64 rows
+        assert path == 11
+    lv, order, _ = eng.exec_levels()
+    lv, order = lv.copy(), order.copy()
+    eng.set_level_mode(3)                                     # AD_LEVELS_KAHN
+    lk, ok, _ = eng.exec_levels()
+    assert np.array_equal(lv, lk) and np.array_equal(order, ok)
+    assert lv.max() > 10
+
+
+def test_mixed_pull_skips_awaits_only_deps(engine_factory):
+    # an ExclusiveSyncPoint / EphemeralRead may depend on a larger executeAt: the mixed pull is skipped (13)
+    rng = np.random.default_rng(77)
+    n = 6000
+    kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ], size=n, p=[0.45, 0.45, 0.1])
+    b = workload.generate(n, 3, 5000, "uniform", range_frac=0.1, range_width_max=100, kinds=kinds, seed=77)
+    eng = engine_factory(window=16)
+    check(engine_factory, b, eng=eng, window=16)
+    assert eng.last_times()["level_path"] in (0, 13)
+
+
 def test_merge_host_equals_oracle_merge(engine_factory):
     # Deps.merge of replies supplied by the host (the coordinator's network replies): feed the oracle's
     # per-view replies in, compare with the oracle's LinearMerger result
