@@ -249,6 +249,52 @@ static __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
             if (tc[v] > tc[pv]) pv = v;
             if (nk[v] > nk[pk]) pk = v;
         }
+        // replies identical in every view (the usual case for long lists: they differ only where a view dropped an
+        // in-flight dependency, and a txn's in-window deps are few): the union is any one of them — a streaming
+        // compare of the views, then a copy of view 0 with its own offsets (the merged TxnId list is the same list,
+        // so the per-key entries' TxnId indices carry over unchanged)
+        {
+            bool same = rv[0] >= 0;
+#pragma unroll
+            for (int v = 1; v < NV; ++v) same = same && rv[v] >= 0 && tc[v] == tc[0] && nk[v] == nk[0];
+            const uint32_t klen = nk[0] ? (uint32_t)a.k2t[0][mb[0] + nk[0] - 1] : 0u;   // header + entries
+#pragma unroll
+            for (int v = 1; v < NV; ++v) same = same && (nk[v] ? (uint32_t)a.k2t[v][mb[v] + nk[v] - 1] : 0u) == klen;
+            if (same) {
+                bool diff = false;
+                for (uint32_t i = threadIdx.x; i < tc[0] && !diff; i += MH_T) {
+                    const uint32_t x = a.txns[0][tb[0] + i];
+#pragma unroll
+                    for (int v = 1; v < NV; ++v) diff |= a.txns[v][tb[v] + i] != x;
+                }
+                for (uint32_t i = threadIdx.x; i < KW * nk[0] && !diff; i += MH_T) {
+                    const uint64_t x = a.keys[0][(size_t)KW * kb[0] + i];
+#pragma unroll
+                    for (int v = 1; v < NV; ++v) diff |= a.keys[v][(size_t)KW * kb[v] + i] != x;
+                }
+                for (uint32_t i = threadIdx.x; i < klen && !diff; i += MH_T) {
+                    const int32_t x = a.k2t[0][mb[0] + i];
+#pragma unroll
+                    for (int v = 1; v < NV; ++v) diff |= a.k2t[v][mb[v] + i] != x;
+                }
+                same = !__syncthreads_or(diff ? 1 : 0);
+            }
+            if (same) {
+                if (!WRITE) {
+                    if (threadIdx.x == 0) { a.mk[t] = nk[0]; a.me[t] = klen - nk[0]; a.mu[t] = tc[0]; }
+                } else {
+                    uint32_t* ot = a.o_txns + a.o_ent_off[t];
+                    for (uint32_t i = threadIdx.x; i < tc[0]; i += MH_T) ot[i] = a.txns[0][tb[0] + i];
+                    uint64_t* okk = a.o_keys + (size_t)KW * a.o_key_off[t];
+                    for (uint32_t i = threadIdx.x; i < KW * nk[0]; i += MH_T) okk[i] = a.keys[0][(size_t)KW * kb[0] + i];
+                    int32_t* ok2 = a.o_k2t + a.o_k2t_off[t];
+                    for (uint32_t i = threadIdx.x; i < klen; i += MH_T) ok2[i] = a.k2t[0][mb[0] + i];
+                    if (threadIdx.x == 0) a.o_tcnt[t] = tc[0];
+                }
+                __syncthreads();
+                continue;
+            }
+        }
         // chunk size: spread the larger of the two lists over the whole workgroup (a key Write's ~10^2-10^3 RangeDeps
         // used to keep 19 of 256 threads busy with fixed 32-item chunks), at least MCH_MIN items per chunk
         const uint32_t big = tc[pv] > nk[pk] ? tc[pv] : nk[pk];
