@@ -341,7 +341,7 @@ int stage_deps(ad_handle* h) {
             CK(dalloc(h, S_LROWS, &lrows, n + 64));
             device_scan(LargeRowsOp{h->meta, lrows, lrows + n, n}, n, (uint32_t*)h->scratch, st);
             la.rows = lrows; la.rows_total = lrows + n;
-            k_union_lds<<<dim3((unsigned)h->n_large, (unsigned)nc), UB, 0, st>>>(la);
+            k_union_lds_views<<<dim3((unsigned)h->n_large, (unsigned)(direct ? 2 : 1)), UB, 0, st>>>(la, nv);
             la.rows = nullptr; la.rows_total = nullptr;
         }
         if (Q > 0) {
@@ -358,7 +358,7 @@ int stage_deps(ad_handle* h) {
             CK(dalloc(h, S_UMED, &med, (size_t)n * nv + 1));
             HIPCHK(h, hipMemsetAsync(med_count, 0, 4, st));
             la.med_count = med_count; la.med = med;
-            k_union_lds_small<<<dim3((unsigned)n, (unsigned)nv), US_T, 0, st>>>(la);
+            k_union_lds_small<<<(unsigned)n, US_T, 0, st>>>(la);
             k_union_lds_list<<<8192, UB, 0, st>>>(la);
         }
         CK(union_overflow(h, la, ovf_count, ovf, Q > 0));

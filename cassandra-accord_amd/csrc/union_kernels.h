@@ -198,7 +198,7 @@ struct LdsUnionArgs {
 // Union of one (txn, CSR): sort the txn's per-key TxnId ranks in buf (n2 >= ne), unique them into the
 // CSR's TxnId table, then remap every entry to its index (RelationMultiMap.java:201-260).
 template <int NT>
-__device__ inline void union_body(uint32_t* buf, uint32_t* wsum, int32_t* body, uint32_t ne, uint32_t* out, uint32_t* tcnt) {
+__device__ inline uint32_t union_body(uint32_t* buf, uint32_t* wsum, int32_t* body, uint32_t ne, uint32_t* out, uint32_t* tcnt) {
     uint32_t n2 = 1;
     while (n2 < ne) n2 <<= 1;
     for (uint32_t x = threadIdx.x; x < n2; x += NT) buf[x] = x < ne ? (uint32_t)body[x] : 0xFFFFFFFFu;
@@ -227,6 +227,57 @@ __device__ inline void union_body(uint32_t* buf, uint32_t* wsum, int32_t* body, 
         body[x] = (int32_t)lo;
     }
     if (threadIdx.x == 0) *tcnt = total;
+    return total;
+}
+
+// The union of one txn's CSR in several replica views (csr[v], v < nvw) at once.  The views' per-key lists differ
+// only where a view dropped an in-flight dependency (rare for a given txn), and identical bodies have identical
+// unions and remaps: the first view whose list fits `cap` is sorted, every view with an equal body (a streaming
+// compare) receives a copy of its unique TxnId list (still in buf) and remapped body, the rest are sorted on
+// their own.  Lists above cap go to too_big(v, csr).  Returns after a final barrier.
+template <int NT, class TooBig>
+__device__ inline void union_views(const LdsUnionArgs& a, uint32_t t, const int* csr, int nvw, uint32_t* buf, uint32_t* wsum,
+                                   uint32_t cap, TooBig&& too_big) {
+    uint32_t ne[MAXV], mb[MAXV], nk[MAXV];
+    int r = -1;
+    for (int v = 0; v < nvw; ++v) {
+        const int c = csr[v];
+        nk[v] = a.key_off[c][t + 1] - a.key_off[c][t];
+        mb[v] = a.k2t_off[c][t];
+        ne[v] = nk[v] ? a.k2t_off[c][t + 1] - mb[v] - nk[v] : 0u;
+        if (nk[v] == 0) { if (threadIdx.x == 0) a.tcnt[c][t] = 0; continue; }
+        if (ne[v] > cap) { if (threadIdx.x == 0) too_big(v, c); continue; }
+        if (r < 0) r = v;
+    }
+    if (r < 0) return;
+    const int cr = csr[r];
+    int32_t* body_r = a.k2t[cr] + mb[r] + nk[r];
+    uint32_t same = 0;
+    for (int v = r + 1; v < nvw; ++v) {
+        if (nk[v] == 0 || ne[v] > cap || ne[v] != ne[r]) continue;
+        const int32_t* body_v = a.k2t[csr[v]] + mb[v] + nk[v];
+        bool diff = false;
+        for (uint32_t x = threadIdx.x; x < ne[r] && !diff; x += NT) diff = body_v[x] != body_r[x];
+        if (!__syncthreads_or(diff ? 1 : 0)) same |= 1u << v;
+    }
+    const uint32_t tot = union_body<NT>(buf, wsum, body_r, ne[r], a.txns[cr] + a.ent_off[cr][t], &a.tcnt[cr][t]);
+    // the copies first (buf still holds the reference's unique list), then the views that differ
+    for (int v = r + 1; v < nvw; ++v) {
+        if (!(same >> v & 1u)) continue;
+        const int c = csr[v];
+        int32_t* body_v = a.k2t[c] + mb[v] + nk[v];
+        uint32_t* out = a.txns[c] + a.ent_off[c][t];
+        for (uint32_t x = threadIdx.x; x < tot; x += NT) out[x] = buf[x];
+        for (uint32_t x = threadIdx.x; x < ne[v]; x += NT) body_v[x] = body_r[x];   // this thread's own remaps
+        if (threadIdx.x == 0) a.tcnt[c][t] = tot;
+    }
+    for (int v = r + 1; v < nvw; ++v) {
+        const int c = csr[v];
+        if (nk[v] == 0 || ne[v] > cap || (same >> v & 1u)) continue;
+        __syncthreads();
+        union_body<NT>(buf, wsum, a.k2t[c] + mb[v] + nk[v], ne[v], a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
+    }
+    __syncthreads();
 }
 
 // the rows of the large txns (the key-CSR launch only has work there: C4's 4M-row grid x 6 CSRs launched
@@ -274,52 +325,57 @@ static __global__ __launch_bounds__(UB) void k_union_lds(LdsUnionArgs a) {
     union_body<UB>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
 }
 
+// grid (#large rows, classes per view): one workgroup per (large txn, class) unions every view's CSR of the class
+// (csr = 2v + class), sharing the sort between identical views
+static __global__ __launch_bounds__(UB) void k_union_lds_views(LdsUnionArgs a, int nvw) {
+    if (blockIdx.x >= *a.rows_total) return;
+    const uint32_t t = a.rows[blockIdx.x];
+    __shared__ uint32_t buf[UNION_CAP];
+    __shared__ uint32_t wsum[UB / WAVE];
+    int cs[MAXV];
+    for (int v = 0; v < nvw; ++v) cs[v] = 2 * v + (int)blockIdx.y;
+    union_views<UB>(a, t, cs, nvw, buf, wsum, (uint32_t)UNION_CAP, [&](int, int c) {
+        const uint32_t k = atomicAdd(a.ovf_count, 1u);
+        if (k < a.ovf_cap) a.ovf[k] = make_uint2(t, (uint32_t)c);
+        else atomicOr(&a.prm->err, ERR_CAP);
+        a.tcnt[c][t] = 0;
+    });
+}
+
 // RangeDeps of every txn (C4: ~10^7 (txn, view) lists of a few hundred entries): one 64-thread workgroup with a
 // 2 KiB LDS buffer per (txn, CSR).  The 256-thread kernel's 32 KiB buffer held a CU to 5 workgroups, i.e. 5
 // unions in flight per CU, each a chain of ~40 barrier-separated bitonic stages; single-wave workgroups fit 32
 // per CU and their barriers are cheap.  Lists above UNION_SMALL go to the medium queue (k_union_lds_list).
 constexpr int UNION_SMALL = 512, US_T = 64;
+// One workgroup per txn unions every view's RangeDeps CSR (union_views: identical views share one sort); the views
+// whose lists exceed UNION_SMALL are queued together as (txn, view mask) for k_union_lds_list.
 static __global__ __launch_bounds__(US_T) void k_union_lds_small(LdsUnionArgs a) {
     const size_t t = blockIdx.x;
-    const int c = a.csr_base + (int)blockIdx.y;
     if (t >= a.n) return;
     __shared__ uint32_t buf[UNION_SMALL];
     __shared__ uint32_t wsum[1];
-    const uint32_t nk = a.key_off[c][t + 1] - a.key_off[c][t];
-    if (nk == 0) {
-        if (threadIdx.x == 0) a.tcnt[c][t] = 0;
-        return;
-    }
-    const uint32_t mb = a.k2t_off[c][t];
-    const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
-    if (ne > (uint32_t)UNION_SMALL) {
-        if (threadIdx.x == 0) a.med[atomicAdd(a.med_count, 1u)] = make_uint2((uint32_t)t, (uint32_t)c);
-        return;
-    }
-    union_body<US_T>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
+    int cs[MAXV];
+    for (int v = 0; v < a.ncsr; ++v) cs[v] = a.csr_base + v;
+    uint32_t big = 0;
+    union_views<US_T>(a, (uint32_t)t, cs, a.ncsr, buf, wsum, (uint32_t)UNION_SMALL, [&](int v, int) { big |= 1u << v; });
+    if (threadIdx.x == 0 && big) a.med[atomicAdd(a.med_count, 1u)] = make_uint2((uint32_t)t, big);
 }
-// the medium queue: grid-stride over the device-side count, one 256-thread workgroup per item (LDS up to
-// UNION_CAP; above it the overflow queue as in k_union_lds)
+// the medium queue: grid-stride over the device-side count, one 256-thread workgroup per (txn, view mask) (LDS up
+// to UNION_CAP; above it the overflow queue as in k_union_lds)
 static __global__ __launch_bounds__(UB) void k_union_lds_list(LdsUnionArgs a) {
     __shared__ uint32_t buf[UNION_CAP];
     __shared__ uint32_t wsum[UB / WAVE];
     const uint32_t count = *a.med_count;
     for (uint32_t it = blockIdx.x; it < count; it += gridDim.x) {
-        const uint32_t t = a.med[it].x, c = a.med[it].y;
-        const uint32_t nk = a.key_off[c][t + 1] - a.key_off[c][t];
-        const uint32_t mb = a.k2t_off[c][t];
-        const uint32_t ne = a.k2t_off[c][t + 1] - mb - nk;
-        if (ne > (uint32_t)UNION_CAP) {
-            if (threadIdx.x == 0) {
-                const uint32_t k = atomicAdd(a.ovf_count, 1u);
-                if (k < a.ovf_cap) a.ovf[k] = make_uint2(t, c);
-                else atomicOr(&a.prm->err, ERR_CAP);
-                a.tcnt[c][t] = 0;
-            }
-            continue;
-        }
-        union_body<UB>(buf, wsum, a.k2t[c] + mb + nk, ne, a.txns[c] + a.ent_off[c][t], &a.tcnt[c][t]);
-        __syncthreads();
+        const uint32_t t = a.med[it].x, mask = a.med[it].y;
+        int cs[MAXV], nvw = 0;
+        for (int v = 0; v < a.ncsr; ++v) if (mask >> v & 1u) cs[nvw++] = a.csr_base + v;
+        union_views<UB>(a, t, cs, nvw, buf, wsum, (uint32_t)UNION_CAP, [&](int, int c) {
+            const uint32_t k = atomicAdd(a.ovf_count, 1u);
+            if (k < a.ovf_cap) a.ovf[k] = make_uint2(t, (uint32_t)c);
+            else atomicOr(&a.prm->err, ERR_CAP);
+            a.tcnt[c][t] = 0;
+        });
     }
 }
 
