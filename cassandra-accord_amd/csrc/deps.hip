@@ -166,7 +166,7 @@ int stage_deps(ad_handle* h) {
         CK(dalloc(h, S_VTXN, &h->vi_txn, V)); CK(dalloc(h, S_VPOS, &h->vi_pos, V)); CK(dalloc(h, S_VSEG, &h->vi_u, V));
         CK(dalloc(h, S_VCNT, &h->vcnt, (size_t)V * nc));
         va.vi_txn = h->vi_txn; va.vi_pos = h->vi_pos; va.vi_u = h->vi_u;
-        if (V > 0) k_vitems<true><<<ceil_div((long)n, 256), 256, 0, st>>>(va);
+        if (V > 0) k_vitems_fill<<<ceil_div((long)n * WAVE, 256), 256, 0, st>>>(va);
     }
     // ---- walk (count)
     WalkArgs wa{};

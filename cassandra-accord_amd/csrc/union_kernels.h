@@ -113,6 +113,45 @@ static __global__ __launch_bounds__(256) void k_vitems(VItemArgs a) {
     if (!FILL) a.vn[t] = c;
 }
 
+// Fill pass, one wave per large txn: the lanes stride over its items (a range txn's ~10^3-10^4 CFK keys were one
+// thread's serial chain of binary searches: C4's fill pass was 130 ms of tail latency)
+static __global__ __launch_bounds__(256) void k_vitems_fill(VItemArgs a) {
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (t >= a.n) return;
+    const uint32_t m = a.meta[t];
+    if (!(m & META_LARGE)) return;
+    const uint32_t lane = (uint32_t)__lane_id();
+    const uint32_t U = a.prm->n_keys_u;
+    const uint32_t x0 = a.voff[t];
+    if (meta_domain(m) == AD_DOMAIN_KEY) {
+        const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
+        for (uint32_t p = b + lane; p < e; p += WAVE) {
+            const uint64_t k = a.keys[p];
+            const uint32_t u = lb_u64(a.ukey, 0, U, k);
+            const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+            const uint32_t s = a.qpos ? lb_u32(a.e_txn, s0, s1, a.qpos[t]) : ub_u32(a.e_txn, s0, s1, (uint32_t)t) - 1;
+            const uint32_t x = x0 + (p - b);
+            a.vi_txn[x] = (uint32_t)t;
+            a.vi_pos[x] = s;
+            a.vi_u[x] = u;
+        }
+        return;
+    }
+    uint32_t x = x0;
+    for (uint32_t q = a.range_off[t]; q < a.range_off[t + 1]; ++q) {
+        uint32_t lo, hi;
+        keys_in_range(a, U, a.rs[q], a.re[q], lo, hi);
+        for (uint32_t u = lo + lane; u < hi; u += WAVE) {
+            const uint32_t s0 = a.useg[u], s1 = a.useg[u + 1];
+            const uint32_t y = x + (u - lo);
+            a.vi_txn[y] = (uint32_t)t;
+            a.vi_pos[y] = a.qpos ? lb_u32(a.e_txn, s0, s1, a.qpos[t]) : ub_u32(a.e_txn, s0, s1, (uint32_t)t);
+            a.vi_u[y] = u;
+        }
+        x += hi - lo;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Block-level helpers (256 threads)
 // ---------------------------------------------------------------------------------------------------
