@@ -1160,6 +1160,7 @@ struct MixPullArgs {
     uint32_t* L;                         // levels | LV_FINAL
     uint32_t* abort_flag;
     uint32_t* maxlvl;
+    int force_abort;                     // tests (AD_LEVELS_PULL_ABORT): every wave aborts at once, Kahn recomputes
 };
 constexpr int MP_GRID = 2048;         // co-resident workgroups at most (8 per CU)
 // the (c) sources of unmanaged t this lane owns (its share of t's merged KeyDeps keys): per key with a
@@ -1254,6 +1255,10 @@ static __global__ __launch_bounds__(256) void k_level_pull_mixed(MixPullArgs a) 
     const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     const size_t W = (size_t)gridDim.x * blockDim.x / WAVE;
     uint32_t wmax = 0;
+    if (a.force_abort) {
+        if (lane == 0) __hip_atomic_store(a.abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     for (size_t r = w; r < a.n; r += W) {
         const uint32_t t = a.perm[r];
         uint32_t m = 0;
@@ -1925,7 +1930,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                     MixPullArgs ma{};
                     ma.n = n; ma.perm = ls.sv1; ma.key_off = in.key_off; ma.pred = ls.succ; ma.c_txn = ls.c_txn; ma.c_meta = ls.c_meta;
                     ma.e = ea; ma.do_b = has_b ? 1 : 0; ma.do_c = has_c ? 1 : 0; ma.L = in.lvl;
-                    ma.abort_flag = ls.flags + 23; ma.maxlvl = ls.flags + 24;
+                    ma.abort_flag = ls.flags + 23; ma.maxlvl = ls.flags + 24; ma.force_abort = ls.pull_force_abort ? 1 : 0;
                     if (has_c) {
                         // (c) sources per txn: count, offsets, fill (one sync for the total)
                         if (ls.capX < n + 1 || !ls.xcnt) {

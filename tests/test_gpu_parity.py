@@ -345,6 +345,16 @@ def test_mixed_pull_levels(engine_factory, n, keyspace, rf, width, slow, bump):
     assert lv.max() > 10
 
 
+def test_mixed_pull_forced_abort(engine_factory):
+    # AD_LEVELS_PULL_ABORT: the mixed pull aborts at once (level_path 15) and the Kahn wavefronts recompute the
+    # batch from scratch (pred-mode runs, flags and levels reset): still the oracle's levels and order
+    b = workload.generate(20000, 4, 200_000, "uniform", range_frac=0.1, range_width_max=1 << 12, seed=91)
+    eng = engine_factory()
+    eng.set_level_mode(4)                                     # AD_LEVELS_PULL_ABORT
+    check(engine_factory, b, eng=eng)
+    assert eng.last_times()["level_path"] == 15
+
+
 def test_mixed_pull_skips_awaits_only_deps(engine_factory):
     # an ExclusiveSyncPoint / EphemeralRead may depend on a larger executeAt: the mixed pull is skipped (13)
     rng = np.random.default_rng(77)
