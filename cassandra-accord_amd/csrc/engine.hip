@@ -1252,6 +1252,17 @@ int ad_fetch_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out) {
     return AD_OK;
 }
 
+// The pipeline's final wait: poll the event instead of hipEventSynchronize's blocking wait (its wake-up was most
+// of the ~37 us the GPU sat idle between consecutive batches)
+static int spin_event(ad_handle* h, hipEvent_t e) {
+    for (uint64_t k = 0;; ++k) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return AD_OK;
+        if (q != hipErrorNotReady) { HIPCHK(h, q); }
+        if (k > (1u << 22)) { HIPCHK(h, hipEventSynchronize(e)); return AD_OK; }   // a long batch: block instead
+    }
+}
+
 int ad_run_pipeline(ad_handle* h) {
     if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
@@ -1270,7 +1281,7 @@ int ad_run_pipeline(ad_handle* h) {
     HIPCHK(h, hipEventRecord(h->ev[4], st));
     CK(stage_levels(h, true));
     HIPCHK(h, hipEventRecord(h->ev[5], st));
-    HIPCHK(h, hipEventSynchronize(h->ev[5]));
+    CK(spin_event(h, h->ev[5]));
     if (order_failed(h)) {                       // optimistic order failed its check: general path, timed in
         CK(finish_order(h));
         HIPCHK(h, hipEventRecord(h->ev[5], st));
