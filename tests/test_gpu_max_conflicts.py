@@ -168,8 +168,10 @@ def test_gpu_preaccept_kat_multi_key(engine_factory):
     (m1, l1, n1, f1, c1), (m2, l2, n2, f2, c2) = _engine_store(engine_factory, [first, second], 0, 1, 0.0, 1)
     assert f1[0, 0] == 1 and f2[0, 0] == 0
     assert (int(m2[0, 0]), int(l2[0, 0]), int(n2[0, 0])) == Wt.from_values(1, 100, abi.KIND_WRITE << 1, 2)
-    clock = Wt.NodeClock(1, 1, 110)
-    clock.now = Wt.from_values(1, 100, 0, 1)
+    # the node clock as PreAcceptTest builds it (test_oracle_preaccept_kats.test_multi_key_timestamp_update): Node.now
+    # made at epoch 0, the HLC 10 ahead, so nowAtLeast takes the max conflict's bits, flags included
+    clock = Wt.NodeClock(1, 1, 100, now_epoch=0)
+    clock.clock += 10
     w = Wt.preaccept_witnessed_at(Wt.from_values(1, 50, abi.KIND_WRITE << 1, 3), (int(m2[0, 0]), int(l2[0, 0]), int(n2[0, 0])), clock)
     assert (Wt.epoch(w), Wt.hlc(w), w[2]) == (1, 110, 1)
     # PreAcceptOk.equals -> Timestamp.equals (Timestamp.java:244-249): the identity flags (kind, domain) included
