@@ -212,7 +212,7 @@ int stage_deps(ad_handle* h) {
     // ---- RangeDeps (count)
     RangeArgs ra{};
     ra.n = n; ra.Q = Q; ra.key_off = h->key_off; ra.keys = h->keys; ra.range_off = h->range_off; ra.rs = h->range_s;
-    ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix;
+    ra.re = h->range_e; ra.meta = h->meta; ra.es = h->es; ra.ee = h->ee; ra.eown = h->eown; ra.ix = h->ix; ra.prm = h->prm;
     ra.window = h->cfg.window; ra.thresh = wa.thresh; ra.seed = h->cfg.seed; ra.rnk = h->rnk; ra.rne = h->rne;
     ra.qpos = qpos;
     ra.gqpos = wa.gqpos;

@@ -66,8 +66,9 @@ struct Params {                // device-side batch statistics (filled by k_minm
     unsigned int max_keys, err;                  // err bits below
     unsigned int n_large, n_keys_u;              // large txns; distinct keys (after sort)
     unsigned long long n_vitems;                 // virtual items
-    unsigned int n_special, pad_;                // key-domain txns that are not Read/Write (sync points,
+    unsigned int n_special;                      // key-domain txns that are not Read/Write (sync points,
                                                  // ephemeral reads, local-only): unmanaged execution
+    unsigned int range_kinds;                    // bit k: the batch holds a range-domain txn of kind k
 };
 enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
                   ERR_RANGEBITS = 32, ERR_CAP = 64, ERR_EXECBELOW = 128 };
@@ -91,11 +92,12 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
                                                 const uint32_t* __restrict__ key_off, const uint64_t* __restrict__ keys,
                                                 size_t P, const uint64_t* __restrict__ rs, const uint64_t* __restrict__ re,
                                                 size_t Q, unsigned long long* __restrict__ partial) {
-    constexpr int NF = 14, NSUM = 12;
+    constexpr int NF = 15, NSUM = 12, NOR = 14;
     // fields: 0 msb_min 1 msb_max 2 hlc_min 3 hlc_max 4 node_min 5 node_max 6 key_min 7 key_max 8 max_keys
     //         9 rs_min 10 re_max 11 rw_max ; *_min are stored complemented so every field is a max
-    //         12 large txns, 13 special key-domain txns (sums, fields >= NSUM)
-    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    //         12 large txns, 13 special key-domain txns (sums, fields NSUM .. NOR-1)
+    //         14 kinds of the range-domain txns (a bit mask: OR, fields >= NOR)
+    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         unsigned long long a = tm[i], b = em[i], ha = tl[i] >> 16, hb = el[i] >> 16;
@@ -108,6 +110,7 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
         f[12] += ((tl[i] & 1) == AD_DOMAIN_RANGE || kc > (unsigned)KMAX) ? 1ull : 0ull;
         const unsigned kind = (unsigned)((tl[i] >> 1) & 7);
         f[13] += ((tl[i] & 1) == AD_DOMAIN_KEY && kind != AD_KIND_READ && kind != AD_KIND_WRITE) ? 1ull : 0ull;
+        f[14] |= (tl[i] & 1) == AD_DOMAIN_RANGE ? 1ull << kind : 0ull;
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
         unsigned long long k = keys[i];
@@ -128,13 +131,14 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
     for (int k = NSUM; k < NF; ++k) {
         unsigned long long v = f[k];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        for (int o = 32; o > 0; o >>= 1) { const unsigned long long u = __shfl_xor(v, o); v = k >= NOR ? (v | u) : v + u; }
         if (__lane_id() == 0) red[w][k] = v;
     }
     __syncthreads();
     if (threadIdx.x < NF) {
         const int k = threadIdx.x;
-        unsigned long long v = k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
+        unsigned long long v = k >= NOR ? (red[0][k] | red[1][k] | red[2][k] | red[3][k])
+                             : k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
                                          : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
         partial[(size_t)blockIdx.x * NF + k] = v;
     }
@@ -142,18 +146,20 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
 
 // second level of k_minmax: one block folds the per-block partials into Params (no contended atomics)
 static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out) {
-    constexpr int NF = 14, NSUM = 12;
+    constexpr int NF = 15, NSUM = 12, NOR = 14;
     __shared__ unsigned long long red[4][NF];
-    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = threadIdx.x; b < nblk; b += blockDim.x)
         for (int k = 0; k < NF; ++k) {
             const unsigned long long v = partial[(size_t)b * NF + k];
-            f[k] = k >= NSUM ? f[k] + v : max(f[k], v);
+            f[k] = k >= NOR ? (f[k] | v) : k >= NSUM ? f[k] + v : max(f[k], v);
         }
     const int w = threadIdx.x / WAVE;
     for (int k = 0; k < NF; ++k) {
         unsigned long long v = f[k];
-        if (k >= NSUM) {
+        if (k >= NOR) {
+            for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+        } else if (k >= NSUM) {
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         } else {
             v = wmax64(v);
@@ -163,7 +169,8 @@ static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const uns
     __syncthreads();
     if (threadIdx.x < NF) {
         const int k = threadIdx.x;
-        unsigned long long v = k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
+        unsigned long long v = k >= NOR ? (red[0][k] | red[1][k] | red[2][k] | red[3][k])
+                             : k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
                                          : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
         // the only writer of these fields (no separate initialisation launch)
         switch (k) {
@@ -181,9 +188,10 @@ static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const uns
             case 11: out->rw_max = v; break;
             case 12: out->n_large = (unsigned)v; break;
             case 13: out->n_special = (unsigned)v; break;
+            case 14: out->range_kinds = (unsigned)v; break;
         }
     }
-    if (threadIdx.x == 0) { out->err = 0; out->n_keys_u = 0; out->n_vitems = 0; out->pad_ = 0; }
+    if (threadIdx.x == 0) { out->err = 0; out->n_keys_u = 0; out->n_vitems = 0; }
 }
 
 // Packs timestamps, builds per-txn meta, the sort input and validates footprints.  One thread per txn.

@@ -80,6 +80,7 @@ struct RangeArgs {
     const uint64_t* ee;
     const uint32_t* eown;
     RangeIndex ix;               // max-end tree over the sorted entries (range_index.h)
+    const Params* prm;           // range_kinds: a query whose kind witnesses none of them walks nothing (nullable)
     uint32_t window, thresh;
     uint64_t seed;
     uint32_t* rnk;               // [v * n + t]  distinct ranges (count pass)
@@ -140,7 +141,10 @@ static __global__ __launch_bounds__(256) void k_range_deps(RangeArgs a) {
             mb[v] = a.k2t_off_v[v][i];
         }
     }
-    const bool query = qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && fe > fb && a.Q > 0;
+    uint32_t wk = 0;                                   // the range kinds this query's kind witnesses
+#pragma unroll
+    for (uint32_t k = 0; k <= AD_KIND_EXCLUSIVE_SYNC_POINT; ++k) wk |= witnesses(qk, k) ? 1u << k : 0u;
+    const bool query = qk <= AD_KIND_EXCLUSIVE_SYNC_POINT && fe > fb && a.Q > 0 && (!a.prm || (wk & a.prm->range_kinds));
     if (query) {
         // the index walk visits, in entry order, the chunks that can hold a hit; the predicate is exact
         ri_walk(a.ix, a.es, (uint32_t)a.Q, key_dom, a.keys, a.rs, a.re, fb, fe, [&](uint32_t clo, uint32_t chi) {
