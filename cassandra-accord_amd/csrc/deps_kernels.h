@@ -684,27 +684,35 @@ static __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
     if (t >= a.n || !(a.meta[t] & META_LARGE)) return;
     const uint32_t b = a.voff[t], e = a.voff[t + 1];
     const uint64_t below = (1ull << __lane_id()) - 1ull;
-#pragma unroll 1
+    // every class in one pass over the items: the item's key is loaded once, its NVC counts are adjacent
+    uint32_t kb[NVC], mb[NVC], run[NVC], kk[NVC];
+#pragma unroll
     for (int c = 0; c < NVC; ++c) {
-        const uint32_t kb = a.out_key_off[c][t];
-        const uint32_t nk = a.out_key_off[c][t + 1] - kb;
-        if (nk == 0) continue;
-        const uint32_t mb = a.out_k2t_off[c][t];
-        uint32_t run = nk, kk = 0;
-        for (uint32_t x0 = b; x0 < e; x0 += WAVE) {
-            const uint32_t x = x0 + __lane_id();
-            const uint32_t v = x < e ? a.vcnt[(size_t)x * NVC + c] : 0u;
-            const uint32_t incl = wave_incl_sum(v);
-            const uint64_t nz = __ballot(v > 0);
-            if (v > 0) {
-                const uint32_t r = kk + (uint32_t)__popcll(nz & below);
-                const uint32_t before = run + incl - v;
-                a.out_keys[c][kb + r] = a.ukey[a.vi_u[x]];
-                a.vdst[(size_t)x * NVC + c] = mb + before + v - 1;
-                a.out_k2t[c][mb + r] = (int32_t)(before + v);
+        kb[c] = a.out_key_off[c][t];
+        run[c] = a.out_key_off[c][t + 1] - kb[c];            // the header: entries start after the keys
+        mb[c] = a.out_k2t_off[c][t];
+        kk[c] = 0;
+    }
+    for (uint32_t x0 = b; x0 < e; x0 += WAVE) {
+        const uint32_t x = x0 + __lane_id();
+        uint32_t v[NVC];
+        bool any = false;
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) { v[c] = x < e ? a.vcnt[(size_t)x * NVC + c] : 0u; any |= v[c] > 0; }
+        const uint64_t key = any ? a.ukey[a.vi_u[x]] : 0ull;
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) {
+            const uint32_t incl = wave_incl_sum(v[c]);
+            const uint64_t nz = __ballot(v[c] > 0);
+            if (v[c] > 0) {
+                const uint32_t r = kk[c] + (uint32_t)__popcll(nz & below);
+                const uint32_t before = run[c] + incl - v[c];
+                a.out_keys[c][kb[c] + r] = key;
+                a.vdst[(size_t)x * NVC + c] = mb[c] + before + v[c] - 1;
+                a.out_k2t[c][mb[c] + r] = (int32_t)(before + v[c]);
             }
-            run += __builtin_amdgcn_readlane(incl, WAVE - 1);
-            kk += (uint32_t)__popcll(nz);
+            run[c] += __builtin_amdgcn_readlane(incl, WAVE - 1);
+            kk[c] += (uint32_t)__popcll(nz);
         }
     }
 }
