@@ -319,3 +319,28 @@ def test_ts_folds_carried_points_and_intervals():
                 me = (int(b["txn_msb"][i]), int(b["txn_lsb"][i]), int(b["txn_node"][i]))
                 assert int(fast[v, i]) == int(t is None or _order(*me)[:4] >= _order(*t)[:4])
         assert fast.min() == 0 and fast.max() == 1
+
+
+def test_export_ranges_chain_is_one_merge():
+    # carrying the interval map through two batches equals one merge of everything they and the carry recorded
+    # (ReducingIntervalMap.merge with Timestamp::max is associative and commutative)
+    b1, b2 = _range_batch(31), _range_batch(32)
+    rng = np.random.default_rng(33)
+    carry = _random_carry_ranges(rng, 600, 1_000_000, 25)
+    chained = O.max_conflicts_export_ranges(b2, O.max_conflicts_export_ranges(b1, carry))
+    pieces = [(int(s), int(e), (int(m), int(l), int(n))) for s, e, m, l, n in zip(*carry)]
+    pieces += _recorded_ranges(b1) + _recorded_ranges(b2)
+    xs = sorted({p for s, e, _ in pieces for p in (s, e)})
+    want = []
+    for g in range(len(xs) - 1):
+        best = None
+        for s, e, t in pieces:
+            if s < xs[g + 1] <= e and (best is None or _order(*t) > _order(*best)):
+                best = t
+        if best is None:
+            continue
+        if want and want[-1][1] == xs[g] and want[-1][2] == best:
+            want[-1] = (want[-1][0], xs[g + 1], best)
+        else:
+            want.append((xs[g], xs[g + 1], best))
+    assert [(int(s), int(e), (int(m), int(l), int(n))) for s, e, m, l, n in zip(*chained)] == want
