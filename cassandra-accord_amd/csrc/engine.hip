@@ -215,7 +215,7 @@ int check_params(ad_handle* h) {
 int stage_prepare(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     hipStream_t st = h->st;
-    const int g = (int)std::min<size_t>(4096, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));   // enough loads in flight to stream
+    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
         KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
