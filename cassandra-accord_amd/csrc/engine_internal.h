@@ -259,6 +259,7 @@ enum Slot : size_t {
     S_MCIS, S_MCIE, S_MCIM, S_MCIL, S_MCIN,                     // carried MaxConflicts intervals
     S_MXX, S_MXK0, S_MXV0, S_MXK1, S_MXV1, S_MXF, S_MXR, S_MXU, S_MXVM, S_MXVL, S_MXVN, S_MXH, S_MXFS, S_MXFE,
     S_MXPS, S_MXPE, S_MXOS, S_MXOE, S_MXOM, S_MXOL, S_MXON,    // their export
+    S_MHS,                                                      // heavy merge: identical-replies flags
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 256

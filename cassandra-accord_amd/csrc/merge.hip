@@ -24,6 +24,8 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
     uint32_t* hl;                                   // heavy-txn lists [K * n] + counters [K]
     CK(dalloc(h, S_MHL, &hl, (size_t)K * n + 64));
     uint32_t* hc = hl + (size_t)K * n;
+    uint8_t* hs;                                    // heavy txns' identical-replies flags [K * n]
+    CK(dalloc(h, S_MHS, &hs, (size_t)K * n + 64));
     if (n > 0) HIPCHK(h, hipMemsetAsync(hc, 0, (size_t)K * 4, st));
     std::vector<MergeArgs> ma(K);
     for (int k = 0; k < K; ++k) {
@@ -39,7 +41,7 @@ int merge_multi(ad_handle* h, size_t n, int K, Csr* const* out, const size_t* ou
             a.row[v] = rows ? rows[k][v] : nullptr;
         }
         a.mk = mk + (size_t)k * n; a.me = me + (size_t)k * n; a.mu = mu + (size_t)k * n;
-        if (h->merge_heavy) { a.hlist = hl + (size_t)k * n; a.hcount = hc + k; }
+        if (h->merge_heavy) { a.hlist = hl + (size_t)k * n; a.hcount = hc + k; a.hsame = hs + (size_t)k * n; }
         if (n > 0) merge_launch(a, np, false, kw[k], st);
     }
     if (n > 0) {

@@ -37,6 +37,7 @@ struct MergeArgs {
     // heavy txns (long lists: range txns' KeyDeps, key txns' RangeDeps) go to k_merge_heavy
     uint32_t* hcount;            // [1] appended by the count pass
     uint32_t* hlist;             // [n]
+    uint8_t* hsame;              // [n] heavy txn whose replies are identical in every view (count pass -> write pass)
 };
 
 // A txn whose replies hold more than MERGE_HEAVY TxnIds + keys in total is merged by one workgroup
@@ -260,7 +261,9 @@ static __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
             const uint32_t klen = nk[0] ? (uint32_t)a.k2t[0][mb[0] + nk[0] - 1] : 0u;   // header + entries
 #pragma unroll
             for (int v = 1; v < NV; ++v) same = same && (nk[v] ? (uint32_t)a.k2t[v][mb[v] + nk[v] - 1] : 0u) == klen;
-            if (same) {
+            if (same && WRITE && a.hsame) {
+                same = a.hsame[t] != 0;                      // the count pass compared the views
+            } else if (same) {
                 bool diff = false;
                 for (uint32_t i = threadIdx.x; i < tc[0] && !diff; i += MH_T) {
                     const uint32_t x = a.txns[0][tb[0] + i];
@@ -278,6 +281,7 @@ static __global__ __launch_bounds__(MH_T) void k_merge_heavy(MergeArgs a) {
                     for (int v = 1; v < NV; ++v) diff |= a.k2t[v][mb[v] + i] != x;
                 }
                 same = !__syncthreads_or(diff ? 1 : 0);
+                if (!WRITE && a.hsame && threadIdx.x == 0) a.hsame[t] = same ? 1 : 0;
             }
             if (same) {
                 if (!WRITE) {
