@@ -364,6 +364,7 @@ static __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
     const uint32_t mb = a.mk_k2t_off[t];
     const uint32_t tb = a.mk_ent_off[t];
     const uint64_t my = a.ex1[t];
+    uint32_t ulo = 0;                                      // this lane's previous key's position in ukey
     for (uint32_t ki = __lane_id(); ki < nk; ki += WAVE) {
         int32_t pos = -1;
         if (unmanaged) {
@@ -375,7 +376,19 @@ static __global__ __launch_bounds__(256) void k_unmanaged_prep(EdgeArgs a) {
                 if ((any_exec || e < my) && e > bnd) bnd = e;
             }
             const uint64_t key = a.mk_keys[kb + ki];
-            const uint32_t u = from < to ? lb_u64(a.ukey, 0, a.U, key) : a.U;
+            uint32_t u = a.U;
+            if (from < to) {
+                // the txn's keys ascend and sit among ukey's: gallop from the lane's previous key (a range txn's
+                // keys are nearly consecutive in ukey, 64 apart per lane) instead of a full binary search
+                uint32_t lo = ulo, hi = a.U, step = WAVE;
+                while (true) {
+                    const uint32_t p = lo + step;
+                    if (p >= a.U) break;
+                    if (a.ukey[p] < key) { lo = p + 1; step <<= 1; } else { hi = p + 1; break; }
+                }
+                u = lb_u64(a.ukey, lo, hi, key);
+                ulo = u;
+            }
             const bool found = u < a.U && a.ukey[u] == key;
             if (sync && found) {
                 // per-key lists are ascending: first and last dependency (batch ranks = TxnId order)
