@@ -279,9 +279,12 @@ def roofline_of(eng, dom, n, P, st, large=False, pmc=True):
 
 
 ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profiles/*_pmc.json keys)
+    # exact symbols as rocprofv3 prints them (template arguments included); rocprof_match() also accepts a
+    # bare base name ("ad::k_txn_finish") for any instantiation, so a new template argument cannot silently
+    # drop the traffic figure again (round 3 mapped k_txn_finish to "<3>" while rocprof recorded "<3, false>")
     "k_deps_walk<fill>": "ad::k_deps_walk<3, true, false>", "k_deps_walk<count>": "ad::k_deps_walk<3, false, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
-    "k_gather_entries": "ad::k_gather_entries", "k_txn_finish": "ad::k_txn_finish<3>",
+    "k_gather_entries": "ad::k_gather_entries<true>", "k_txn_finish": "ad::k_txn_finish<3, false>",
     "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<3>",
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
@@ -313,10 +316,14 @@ def pmc_traffic(kernel):
     ks = doc.get("kernels", {})
 
     def entries(name):
-        for k, e in ks.items():
-            nm, grid = k.rsplit(" grid=", 1)
-            if nm == name and "FETCH_SIZE_KB_mean" in e and "WRITE_SIZE_KB_mean" in e:
-                yield int(grid), e
+        got = [(k.rsplit(" grid=", 1), e) for k, e in ks.items() if "FETCH_SIZE_KB_mean" in e and "WRITE_SIZE_KB_mean" in e]
+        exact = [(int(g), e) for (nm, g), e in got if nm == name]
+        if exact or "<" in name:
+            yield from exact
+            return
+        for (nm, g), e in got:                # bare base name: every instantiation of that kernel
+            if nm.split("<", 1)[0] == name:
+                yield int(g), e
 
     def bytes_of(e):
         return (e["FETCH_SIZE_KB_mean"] / cal + e["WRITE_SIZE_KB_mean"]) * 1024.0
@@ -333,6 +340,19 @@ def pmc_traffic(kernel):
             tot += bytes_of(e) * e["dispatches"]
             seen = True
     return (tot / steps, os.path.relpath(files[-1], ROOT)) if seen else (None, None)
+
+
+LEVEL_PATH_ABORTED = {3: "pull levels", 15: "executeAt-ordered mixed pull levels"}
+
+
+def warn_level_fallback(st):
+    """The persistent pull-level kernels give up after ~1 s without progress (e.g. CUs taken by other work on the
+    device) and the Kahn wavefronts recompute the batch: the levels stay exact but slow.  Say so instead of letting
+    the fallback show only as a slower level stage (ad_stage_times.level_path)."""
+    what = LEVEL_PATH_ABORTED.get(st.get("level_path"))
+    if what:
+        print("warning: the %s aborted (level_path %d); this step's levels ran on the Kahn fallback"
+              % (what, st["level_path"]), file=sys.stderr)
 
 
 def print_breakdown(brk, st):
@@ -489,6 +509,7 @@ def main():
     t1 = time.perf_counter()
     dt = t1 - t0
     st = eng.last_times()
+    warn_level_fallback(st)
     roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc=cfgname == "C2")
     mc = None
     if Q == 0:
@@ -527,7 +548,7 @@ def main():
                      "frac": pipe_gbs / HBM_PEAK_GBS,
                      "stage_ms": {k: st[k] for k in ("prepare", "sort", "deps", "merge", "levels", "total")},
                      "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
-                     "level_iterations": st["level_iterations"]},
+                     "level_iterations": st["level_iterations"], "level_path": st["level_path"]},
         "max_conflicts": mc,
         "end_to_end": e2e,
         "cpu_baseline": None,

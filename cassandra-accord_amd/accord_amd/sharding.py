@@ -480,20 +480,26 @@ class GlooTransport:
         store.import_host(recv.numpy(), rsz)
 
     def gather_levels(self, store):
-        """One-exchange levels: all-gather every store's constraint edges (padded to the largest count), then
-        the store solves their union.  Returns the level count."""
+        """One-exchange levels: every store's constraint edges reach every store, then the store solves their
+        union.  Returns the level count.  The edges travel as one broadcast per source store into its slice of
+        one exactly sized buffer (no padding to the largest store: skewed stores would otherwise hold world x
+        the largest edge list)."""
         edges = store.level_edges()
         cnt = self.torch.tensor([edges.size], dtype=self.torch.int64)
-        counts = [self.torch.zeros(1, dtype=self.torch.int64) for _ in range(self.dist.get_world_size())]
+        world, me = self.dist.get_world_size(), self.dist.get_rank()
+        counts = [self.torch.zeros(1, dtype=self.torch.int64) for _ in range(world)]
         self.dist.all_gather(counts, cnt)
         counts = [int(c.item()) for c in counts]
-        top = max(max(counts), 1)
-        mine = self.torch.zeros(top, dtype=self.torch.int64)
-        mine[:edges.size] = self.torch.from_numpy(edges.view(np.int64).copy())
-        parts = [self.torch.zeros(top, dtype=self.torch.int64) for _ in counts]
-        self.dist.all_gather(parts, mine)
-        allv = np.concatenate([p.numpy()[:c] for p, c in zip(parts, counts)]).view(np.uint64)
-        return store.levels_solve(allv)
+        allv = self.torch.empty(sum(counts), dtype=self.torch.int64)
+        off = 0
+        for r, c in enumerate(counts):
+            part = allv.narrow(0, off, c)
+            if r == me:
+                part.copy_(self.torch.from_numpy(edges.view(np.int64)))
+            if c:
+                self.dist.broadcast(part, src=r)
+            off += c
+        return store.levels_solve(allv.numpy().view(np.uint64))
 
     def allreduce_levels(self, store, changed):
         """Delta mode: all-to-all of the raised levels of shared txns; dense mode: all-reduce(max) of the level

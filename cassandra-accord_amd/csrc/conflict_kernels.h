@@ -302,7 +302,12 @@ struct McIntervals {
     const uint64_t *s, *e, *cm, *cl;
     const int32_t* cn;
 };
-// Timestamp::max; of two that compare equal the larger raw lsb (a total order: the fold is order-independent)
+// Timestamp::max; of two that compare equal the larger raw lsb (a total order: the fold is order-independent).
+// Deliberate divergence, documented in DESIGN.md §7: the reference keeps the folded value on a tie in get
+// (foldl(.., Timestamp::max, ..) = max(value, acc)) and the existing map's value in merge, i.e. the survivor of a
+// tie depends on the fold order.  compareTo-equal timestamps of DIFFERENT txns cannot occur (compareTo covers the
+// identity bits epoch, hlc, kind flags, node: Timestamp.java:208-217), so a tie is one txn's timestamp seen twice
+// and only bits outside compareTo (domain bit 0, REJECTED 0x8000) can differ — those this rule may pick otherwise.
 __device__ inline void ts3_fold(const Ts3& c, Ts3& best, bool& has) {
     const int d = has ? ts3_cmp(c, best) : 1;
     if (d > 0 || (d == 0 && c.lsb > best.lsb)) { best = c; has = true; }

@@ -594,8 +594,9 @@ int ad_load_batch_commit(ad_handle* h) {
     if (!h->stage_pending) return set_err(h, AD_ERR_STATE, "ad_load_batch_commit: no staged batch (ad_load_batch_async)");
     hipSetDevice(h->device);
     HIPCHK(h, hipEventSynchronize(h->cev));          // the host batch may be reused once this returns
+    // checked before the staged batch is consumed: after ad_cfk_reset the caller can commit it again
+    if (h->hist_valid) return set_err(h, AD_ERR_UNSUPPORTED, "ad_load_batch_commit: CFK history was retained after the async load (ad_cfk_reset, or ad_load_batch)");
     h->stage_pending = false;
-    if (h->hist_valid) return set_err(h, AD_ERR_UNSUPPORTED, "ad_load_batch_commit: CFK history was retained after the async load (ad_load_batch)");
     for (int k = 0; k < 12; ++k) std::swap(h->bufs[IN_SLOTS[k]], h->bufs[S_STG0 + k]);
     bind_inputs(h);
     h->n = h->stg_n; h->P = h->stg_p; h->Q = h->stg_q;

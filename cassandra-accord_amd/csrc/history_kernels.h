@@ -173,8 +173,14 @@ static __global__ __launch_bounds__(256) void k_cfk_update_apply(CfkUpdate a) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.m) return;
     const uint32_t r = a.row[i];
-    a.hst[r] = a.ust[i];
-    if (a.um) { a.hem[r] = a.um[i]; a.hel[r] = a.ul[i]; a.hen[r] = a.un[i]; }
+    const uint32_t from = a.hst[r], to = a.ust[i];
+    a.hst[r] = to;
+    // executeAt is written only where the move decides it: not for PREACCEPTED / INVALID (no executeAt,
+    // CommandsForKey.InternalStatus.hasExecuteAtOrDeps), and not once it is fixed (COMMITTED / STABLE: the check
+    // proved the given one compares equal; the stored raw bits, flags included, stay)
+    const bool fixed = from == AD_ST_COMMITTED || from == AD_ST_STABLE;
+    const bool decided = to == AD_ST_ACCEPTED || to == AD_ST_COMMITTED || to == AD_ST_STABLE || to == AD_ST_APPLIED;
+    if (a.um && decided && !fixed) { a.hem[r] = a.um[i]; a.hel[r] = a.ul[i]; a.hen[r] = a.un[i]; }
 }
 
 }  // namespace ad

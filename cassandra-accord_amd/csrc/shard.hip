@@ -14,6 +14,7 @@ int ad_cfk_retain(ad_handle* h, size_t* retained) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_cfk_retain: run ad_preaccept_deps on the batch first");
     if (h->sharded) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_retain: not in sharded mode");
     if (h->Q) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_retain: key batches only (no range txns)");
+    if (h->stage_pending) return set_err(h, AD_ERR_STATE, "ad_cfk_retain: a batch is staged (ad_load_batch_commit it first)");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     CK(complete_entries(h));
