@@ -14,6 +14,7 @@ AD_ERR_UNSORTED = -3
 AD_ERR_UNSUPPORTED = -4
 AD_ERR_DEVICE = -5
 AD_ERR_NOMEM = -6
+FAST_REJECTED = 2                 # ad_max_conflicts fast flag: the replica rejects (AD_FAST_REJECTED)
 AD_RANK_NONE = 0xFFFFFFFF   # ad_max_conflicts: Timestamp.NONE
 AD_LEVEL_DONE = 0xFFFFFFFF  # ad_exec_levels over a CFK history batch: an APPLIED / INVALID row
 

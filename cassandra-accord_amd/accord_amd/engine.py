@@ -62,6 +62,9 @@ def lib():
         L.ad_fetch_merged.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut)]
         L.ad_fetch_rows.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, C.POINTER(abi.AdCsrSizes),
                                     C.POINTER(abi.AdCsrOut)]
+        L.ad_fetch_inverse.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
+        L.ad_preaccept_expiry.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ad_run_pipeline.argtypes = [vp]
@@ -101,7 +104,7 @@ def lib():
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
@@ -324,6 +327,21 @@ class DepsEngine:
         self._check(lib().ad_fetch_rows(self.h, view, cls, lo, hi, C.byref(s), C.byref(o)), "ad_fetch_rows")
         return out
 
+    def fetch_inverse(self, view, cls, lo=0, hi=None):
+        """KeyDeps.txnIdsToKeys / RangeDeps.txnIdsToRanges (RelationMultiMap.invert) of rows [lo, hi) of view
+        `view`'s class `cls` (view == replicas: the merged Deps), computed on the device: (off [m + 1], inv) with
+        row i's inverse at inv[off[i]:off[i + 1]] = nTxnIds end offsets (based at nTxnIds), then per TxnId index
+        its ascending key (range) indices."""
+        hi = self.n if hi is None else hi
+        tot = C.c_size_t()
+        off = np.zeros(hi - lo + 1, np.uint32)
+        self._check(lib().ad_fetch_inverse(self.h, view, cls, lo, hi, C.byref(tot),
+                                           off.ctypes.data_as(C.POINTER(C.c_uint32)), None), "ad_fetch_inverse")
+        inv = np.zeros(max(tot.value, 1), np.int32)
+        self._check(lib().ad_fetch_inverse(self.h, view, cls, lo, hi, C.byref(tot), None,
+                                           inv.ctypes.data_as(C.POINTER(C.c_int32))), "ad_fetch_inverse")
+        return off, inv[:tot.value]
+
     def merge(self):
         sizes = (abi.AdCsrSizes * abi.NUM_CLASSES)()
         self._check(lib().ad_merge_deps(self.h, sizes), "ad_merge_deps")
@@ -388,6 +406,18 @@ class DepsEngine:
         self._carry = (k, m, l, nd)
         self._check(lib().ad_max_conflicts_carry(self.h, len(k), k.ctypes.data, m.ctypes.data, l.ctypes.data,
                                                  nd.ctypes.data), "ad_max_conflicts_carry")
+
+    NO_TIMEOUT = 0xFFFFFFFFFFFFFFFF
+
+    def preaccept_expiry(self, now=0, timeout=NO_TIMEOUT, reject_before=None):
+        """CommandStore.preaccept's expiry state for the following max_conflicts(_ts) calls (ad_preaccept_expiry): the
+        clock's now (hlc), preAcceptTimeout (NO_TIMEOUT: none) and rejectBefore (witness.RejectBefore.table() arrays,
+        or None).  Fast flags then read 1 fast path, 0 slow path, abi.FAST_REJECTED rejected (uniqueNow(TxnId)
+        .asRejected()); ExclusiveSyncPoints answer their TxnId."""
+        t = reject_before if reject_before is not None else (np.zeros(0, np.uint64),) * 4 + (np.zeros(0, np.int32),)
+        s, e, m, l, nd = (np.ascontiguousarray(a, dt) for a, dt in zip(t, (np.uint64,) * 4 + (np.int32,)))
+        self._check(lib().ad_preaccept_expiry(self.h, now, timeout, len(s), s.ctypes.data, e.ctypes.data, m.ctypes.data,
+                                              l.ctypes.data, nd.ctypes.data), "ad_preaccept_expiry")
 
     def max_conflicts_ts(self):
         """maxConflicts.get(keys) per view and txn over the carry and the batch as raw timestamps:

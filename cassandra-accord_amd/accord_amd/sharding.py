@@ -197,7 +197,10 @@ def reduce_witnessed(batch, parts):
         for v in range(R):
             best[v, gid] = np.maximum(best[v, gid], p[v])
             ep[v, gid] = np.maximum(ep[v, gid], e[v])
-            fast[v, gid] &= f[v]
+            # fast only if every store answered TxnId; rejected (AD_FAST_REJECTED) if any store rejected it: mergeMax
+            # keeps the REJECTED flag (Timestamp.mergeFlags, PreAccept.reduce :141-156)
+            cur = fast[v, gid]
+            fast[v, gid] = np.where((cur == 2) | (f[v] == 2), 2, cur & f[v])
     out = np.full((R, n), abi.AD_RANK_NONE, np.uint32)
     has = best >= 0
     out[has] = order[best[has]].astype(np.uint32)

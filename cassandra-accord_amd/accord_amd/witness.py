@@ -7,8 +7,14 @@ clock read and a comparison, restated here from the reference:
 * ``NodeClock.unique_now``          Node.uniqueNow / uniqueNow(atLeast) / nowAtLeast, local/Node.java:335-375
 * ``preaccept_witnessed_at``        CommandStore.preaccept, local/CommandStore.java:322-347: TxnId on the fast
                                     path (TxnId >= maxConflict and the txn's epoch is current), else
-                                    time.uniqueNow(maxConflict).  The expiry / rejectBefore test and the
-                                    ExclusiveSyncPoint branch (:326-333) are not modelled.
+                                    time.uniqueNow(maxConflict).
+* ``preaccept``                     the whole of CommandStore.preaccept (:322-347): the expiry test
+                                    (preAcceptTimeout, :326) and the rejectBefore fold (:327-328) ->
+                                    uniqueNow(TxnId).asRejected(); ExclusiveSyncPoint -> markExclusiveSyncPoint +
+                                    TxnId (:333-337); else the fast-path test above.  The device applies the same
+                                    rules to its fast flags (ad_preaccept_expiry; AD_FAST_REJECTED).
+* ``RejectBefore``                  CommandStore.rejectBefore, the ReducingRangeMap<Timestamp> markExclusiveSyncPoint
+                                    builds (:300-306), as sorted disjoint (start, end] intervals.
 
 Timestamps are (msb, lsb, node) int triples (Accord's raw bits, as the C-ABI passes them).
 """
@@ -95,3 +101,79 @@ def preaccept_witnessed_at(txn_id, max_conflict, clock, permit_fast_path=True):
     if permit_fast_path and compare(txn_id, mc) >= 0 and epoch(txn_id) >= clock.topology_epoch:
         return txn_id
     return clock.unique_now(mc)
+
+
+REJECTED_FLAG = 0x8000                 # Timestamp.REJECTED_FLAG (:32)
+KIND_SYNC_POINT, KIND_EXCLUSIVE_SYNC_POINT = 3, 4
+
+
+def as_rejected(t):
+    """Timestamp.asRejected (:144-147)."""
+    return (t[0], t[1] | REJECTED_FLAG, t[2])
+
+
+def kind(t):
+    return (t[1] >> 1) & 7
+
+
+class RejectBefore:
+    """CommandStore.rejectBefore: ReducingRangeMap<Timestamp> of the greatest ExclusiveSyncPoint TxnId marked over
+    each range (markExclusiveSyncPoint, CommandStore.java:300-306: ReducingRangeMap.add(.., Timestamp::max)), held as
+    sorted disjoint intervals (s, e] -> Timestamp in normal form (adjacent equal values coalesced).  A key k is the
+    interval (k - 1, k]."""
+
+    def __init__(self):
+        self.iv = []                   # [(s, e, ts)]
+
+    def add(self, ranges, ts):
+        pts = sorted({p for s, e, _ in self.iv for p in (s, e)} | {p for s, e in ranges for p in (s, e)})
+        out = []
+        for a, b in zip(pts, pts[1:]):
+            best = None
+            for s, e, t in self.iv:
+                if s <= a and b <= e:
+                    best = t
+            if any(s <= a and b <= e for s, e in ranges) and (best is None or compare(ts, best) > 0):
+                best = ts
+            if best is None:
+                continue
+            if out and out[-1][1] == a and out[-1][2] == best:
+                out[-1] = (out[-1][0], b, best)
+            else:
+                out.append((a, b, best))
+        self.iv = out
+
+    def rejects(self, txn_id, keys=(), ranges=()):
+        """rejectBefore.foldl(keys, rejectIfBefore.compareTo(test) > 0 ? null : test, txnId, isNull) == null."""
+        for s, e, t in self.iv:
+            if any(s < k <= e for k in keys) or any(s < qe and e > qs for qs, qe in ranges):
+                if compare(t, txn_id) > 0:
+                    return True
+        return False
+
+    def table(self):
+        """(starts, ends, msb, lsb, node) arrays for ad_preaccept_expiry / the oracle."""
+        import numpy as np
+        iv = self.iv
+        return (np.array([x[0] for x in iv], np.uint64), np.array([x[1] for x in iv], np.uint64),
+                np.array([x[2][0] for x in iv], np.uint64), np.array([x[2][1] for x in iv], np.uint64),
+                np.array([x[2][2] for x in iv], np.int32))
+
+
+def preaccept(txn_id, max_conflict, clock, keys=(), ranges=(), reject_before=None, pre_accept_timeout=None,
+              permit_fast_path=True):
+    """CommandStore.preaccept (local/CommandStore.java:322-347) given maxConflicts.get(keys or ranges): the witnessedAt
+    the replica answers.  keys / ranges: the txn's footprint sliced to the store (ranges as (start, end] pairs);
+    reject_before: the store's RejectBefore (marked here when txn_id is an ExclusiveSyncPoint, as the reference does);
+    pre_accept_timeout: Agent.preAcceptTimeout in hlc units (None: no timeout test)."""
+    expired = (pre_accept_timeout is not None and clock.clock - hlc(txn_id) >= pre_accept_timeout
+               and kind(txn_id) not in (KIND_SYNC_POINT, KIND_EXCLUSIVE_SYNC_POINT))
+    if reject_before is not None and not expired:
+        expired = reject_before.rejects(txn_id, keys, ranges)
+    if expired:
+        return as_rejected(clock.unique_now(txn_id))
+    if kind(txn_id) == KIND_EXCLUSIVE_SYNC_POINT:
+        if reject_before is not None:
+            reject_before.add(list(ranges) + [(k - 1, k) for k in keys], txn_id)
+        return txn_id
+    return preaccept_witnessed_at(txn_id, max_conflict, clock, permit_fast_path)

@@ -389,6 +389,48 @@ static __global__ __launch_bounds__(256) void k_mc_carry(McCarryArgs a) {
         a.fast[o] = (!any || ts3_cmp(me, best) >= 0) ? 1 : 0;               // TxnId.compareTo(max) >= 0
     }
 }
+// The rest of CommandStore.preaccept (local/CommandStore.java:322-347) around maxConflicts.get, as a pass over the
+// fast flags either max-conflicts path left ([v * n + t]; the same store state answers every view):
+//   isExpired = now - TxnId.hlc >= preAcceptTimeout && !kind.isSyncPoint          (:326)
+//            || rejectBefore.foldl(keys, rejectIfBefore > TxnId -> reject)         (:327-328)
+//   expired  -> time.uniqueNow(TxnId).asRejected(): fast = AD_FAST_REJECTED          (:330-331)
+//   ExclusiveSyncPoint -> TxnId unconditionally (markExclusiveSyncPoint): fast = 1   (:333-337)
+// rejectBefore is a ReducingRangeMap<Timestamp> (the greatest ExclusiveSyncPoint TxnId marked over each range,
+// markExclusiveSyncPoint :300-306), carried as sorted disjoint intervals (s, e]; a key stabs (k - 1, k].
+struct PreacceptRules {
+    size_t n;
+    int nv;
+    const uint32_t* key_off;
+    const uint64_t* keys;
+    const uint32_t* range_off;               // nullable: a key batch
+    const uint64_t *rs, *re;
+    const uint64_t *tm, *tl;
+    McIntervals rb;                          // rejectBefore
+    int clock;                               // the timeout test applies
+    uint64_t now_hlc, timeout;
+    uint8_t* fast;
+};
+static __global__ __launch_bounds__(256) void k_preaccept_rules(PreacceptRules a) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint64_t msb = a.tm[t], lsb = a.tl[t];
+    const uint32_t kind = (uint32_t)(lsb >> 1) & 7u;
+    const bool sync_point = kind == AD_KIND_SYNC_POINT || kind == AD_KIND_EXCLUSIVE_SYNC_POINT;
+    const uint64_t hlc = ((msb & 0x7FFFull) << 48) | (lsb >> 16);
+    bool expired = a.clock && !sync_point && (int64_t)(a.now_hlc - hlc) >= (int64_t)a.timeout;
+    if (!expired && a.rb.m) {
+        Ts3 rb{0, 0, 0};
+        bool has = false;
+        for (uint32_t p = a.key_off[t]; p < a.key_off[t + 1]; ++p) mci_stab(a.rb, a.keys[p], rb, has);
+        if (a.range_off)
+            for (uint32_t q = a.range_off[t]; q < a.range_off[t + 1]; ++q) mci_span(a.rb, a.rs[q], a.re[q], rb, has);
+        // any rejectIfBefore > TxnId rejects: the max over the footprint decides
+        expired = has && ts3_cmp(rb, Ts3{msb, lsb, 0}) > 0;
+    }
+    if (!expired && kind != AD_KIND_EXCLUSIVE_SYNC_POINT) return;
+    for (int v = 0; v < a.nv; ++v) a.fast[(size_t)v * a.n + t] = expired ? AD_FAST_REJECTED : 1;
+}
+
 // Export: the union of the carry table and the batch's per-key maxima (the recorded-entry prefix max at each
 // key segment's end), merged by key ranks into slots with gaps (a key in both lands on one slot), then
 // compacted.  slot[i] of a batch key = i + #carry keys below it; of a carry key = j + #batch keys below it.

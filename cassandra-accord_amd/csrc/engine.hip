@@ -677,6 +677,20 @@ int fetch_empty(ad_handle* h, ad_csr_out* out) {
 
 // CommandStore.preaccept's maxConflicts.get(keys) per view (conflict_kernels.h), over the sorted entries the
 // deps stage left on the device: leaves max_rank / fast (and the batch-local rank) in their slots.
+// CommandStore.preaccept around maxConflicts.get (conflict_kernels.h k_preaccept_rules): ExclusiveSyncPoints answer
+// their TxnId, expired txns (timeout / rejectBefore) are rejected
+static void apply_preaccept_rules(ad_handle* h, uint8_t* fast) {
+    if (!h->n) return;
+    PreacceptRules r{};
+    r.n = h->n; r.nv = (int)h->cfg.replicas; r.key_off = h->key_off; r.keys = h->keys;
+    if (h->Q > 0) { r.range_off = h->range_off; r.rs = h->range_s; r.re = h->range_e; }
+    r.tm = h->tm; r.tl = h->tl;
+    r.rb = McIntervals{h->rb_m, h->rb_s, h->rb_e, h->rb_cm, h->rb_cl, h->rb_cn};
+    r.clock = h->rb_clock; r.now_hlc = h->rb_now; r.timeout = h->rb_timeout;
+    r.fast = fast;
+    k_preaccept_rules<<<ceil_div((long)h->n, 256), 256, 0, h->st>>>(r);
+}
+
 static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_out, uint32_t** local_out) {
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "no deps computed");
     hipSetDevice(h->device);
@@ -725,6 +739,7 @@ static int run_max_conflicts(ad_handle* h, uint32_t** rank_out, uint8_t** fast_o
                 k_mc_globalize<<<ceil_div((long)(n * nv), 256), 256, 0, st>>>(n * nv, local, a.gid, rank);
         }
     }
+    apply_preaccept_rules(h, fst);
     HIPCHK(h, hipGetLastError());
     h->mc_ready = true;
     h->mc_fast = fst;
@@ -792,6 +807,32 @@ int ad_max_conflicts_carry_ranges(ad_handle* h, size_t m, const uint64_t* starts
     return AD_OK;
 }
 
+int ad_preaccept_expiry(ad_handle* h, uint64_t now_hlc, uint64_t pre_accept_timeout, size_t m, const uint64_t* starts,
+                        const uint64_t* ends, const uint64_t* msb, const uint64_t* lsb, const int32_t* node) {
+    if (!h || (m && (!starts || !ends || !msb || !lsb || !node))) return AD_ERR_ARGUMENT;
+    for (size_t i = 0; i < m; ++i) {
+        if (!(starts[i] < ends[i])) return set_err(h, AD_ERR_ARGUMENT, "rejectBefore intervals need start < end");
+        if (i && starts[i] < ends[i - 1]) return set_err(h, AD_ERR_ARGUMENT, "rejectBefore intervals must be sorted and disjoint");
+    }
+    hipSetDevice(h->device);
+    const size_t c = std::max<size_t>(m, 1);
+    CK(dalloc(h, S_RBS, &h->rb_s, c)); CK(dalloc(h, S_RBE, &h->rb_e, c)); CK(dalloc(h, S_RBM, &h->rb_cm, c));
+    CK(dalloc(h, S_RBL, &h->rb_cl, c)); CK(dalloc(h, S_RBN, &h->rb_cn, c));
+    if (m) {
+        HIPCHK(h, hipMemcpyAsync(h->rb_s, starts, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->rb_e, ends, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->rb_cm, msb, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->rb_cl, lsb, m * 8, hipMemcpyHostToDevice, h->st));
+        HIPCHK(h, hipMemcpyAsync(h->rb_cn, node, m * 4, hipMemcpyHostToDevice, h->st));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    h->rb_m = m;
+    h->rb_clock = pre_accept_timeout != AD_NO_TIMEOUT;
+    h->rb_now = now_hlc;
+    h->rb_timeout = pre_accept_timeout;
+    return AD_OK;
+}
+
 int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* node, uint8_t* fast) {
     if (!h) return AD_ERR_ARGUMENT;
     uint32_t *rank = nullptr, *local = nullptr;
@@ -817,6 +858,7 @@ int ad_max_conflicts_ts(ad_handle* h, uint64_t* msb, uint64_t* lsb, int32_t* nod
         c.om = om; c.ol = ol; c.on = on; c.fast = of;
         KScope ks(K_MAX_CONFLICTS);
         k_mc_carry<<<ceil_div((long)n, 256), 256, 0, st>>>(c);
+        apply_preaccept_rules(h, of);
         HIPCHK(h, hipGetLastError());
         h->mc_fast = of;
         if (msb) HIPCHK(h, hipMemcpyAsync(msb, om, n * nv * 8, hipMemcpyDeviceToHost, st));
@@ -1075,7 +1117,7 @@ int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
 
 static __global__ void k_fast_rows(size_t n, int nv, const uint8_t* __restrict__ fast, int32_t* __restrict__ rows) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x < n * (size_t)nv) rows[x] = fast[x] ? (int32_t)(x % n) : -1;
+    if (x < n * (size_t)nv) rows[x] = fast[x] == 1 ? (int32_t)(x % n) : -1;     // not AD_FAST_REJECTED
 }
 
 // The coordinator's fast-path merge (CoordinateTransaction.onPreAccepted :75): per txn, only the replies whose

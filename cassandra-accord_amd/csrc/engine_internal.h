@@ -24,6 +24,7 @@
 #include "conflict_kernels.h"
 #include "level_kernels.h"
 #include "history_kernels.h"
+#include "invert_kernels.h"
 #include "recovery_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
@@ -147,6 +148,12 @@ struct ad_handle {
     uint64_t *mci_s = nullptr, *mci_e = nullptr, *mci_cm = nullptr, *mci_cl = nullptr;
     int32_t* mci_cn = nullptr;
     uint64_t mci_lo = 0, mci_hi = 0;  // smallest start / greatest end
+    // the rest of CommandStore.preaccept (ad_preaccept_expiry): rejectBefore intervals + the clock's timeout test
+    size_t rb_m = 0;
+    uint64_t *rb_s = nullptr, *rb_e = nullptr, *rb_cm = nullptr, *rb_cl = nullptr;
+    int32_t* rb_cn = nullptr;
+    int rb_clock = 0;
+    uint64_t rb_now = 0, rb_timeout = 0;
     bool mc_ready = false;           // the MaxConflicts scan of the current batch is on the device (export)
     const uint8_t* mc_fast = nullptr;  // [replicas * n] fast-path flags of the last ad_max_conflicts(_ts)
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
@@ -260,6 +267,8 @@ enum Slot : size_t {
     S_MXX, S_MXK0, S_MXV0, S_MXK1, S_MXV1, S_MXF, S_MXR, S_MXU, S_MXVM, S_MXVL, S_MXVN, S_MXH, S_MXFS, S_MXFE,
     S_MXPS, S_MXPE, S_MXOS, S_MXOE, S_MXOM, S_MXOL, S_MXON,    // their export
     S_MHS,                                                      // heavy merge: identical-replies flags
+    S_IVC, S_IVK0, S_IVV0, S_IVK1, S_IVV1, S_IVOUT,             // ad_fetch_inverse (invert_kernels.h)
+    S_RBS, S_RBE, S_RBM, S_RBL, S_RBN,                          // rejectBefore intervals (ad_preaccept_expiry)
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 256

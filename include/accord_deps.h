@@ -23,6 +23,9 @@
  *       Deps.merge(List, Function)                  primitives/Deps.java:281-286
  *       KeyDeps.merge / RelationMultiMap.LinearMerger  primitives/KeyDeps.java:115-135, utils/RelationMultiMap.java:284-406
  *       RelationMultiMap.linearUnion                utils/RelationMultiMap.java:562-816
+ *   ad_fetch_inverse
+ *       KeyDeps.txnIdsToKeys / RangeDeps.txnIdsToRanges  primitives/KeyDeps.java:362-367, RangeDeps.java:576-582
+ *       RelationMultiMap.invert                     utils/RelationMultiMap.java:907-938
  *   ad_exec_levels
  *       Commands.initialiseWaitingOn/updateWaitingOn/maybeExecute  local/Commands.java:617-775
  *       CommandsForKey.notifyManaged                local/cfk/CommandsForKey.java:1208-1289
@@ -220,6 +223,16 @@ int  ad_merge_deps_fast(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */
  * txn window by txn window, as the replies of KeyDeps/RangeDeps.SerializerSupport.create are consumed. */
 int  ad_fetch_rows(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t hi, ad_csr_sizes* sizes, ad_csr_out* out);
 
+/* The txn -> keys inverse of rows [lo, hi) of view `view`'s class `cls` (view == replicas: the merged Deps), built on
+ * the device: KeyDeps.txnIdsToKeys (primitives/KeyDeps.java:362-367) / RangeDeps.txnIdsToRanges
+ * (primitives/RangeDeps.java:576-582), i.e. RelationMultiMap.invert (utils/RelationMultiMap.java:907-938) of each row's
+ * keysToTxnIds.  Row i's inverse is inv[off[i] .. off[i+1]): nTxnIds end offsets (the first based at nTxnIds), then
+ * per TxnId index its key (range) indices ascending — the int[] the reference caches in txnIdsToKeys.  *total = the
+ * window's ints; off / inv may be NULL (two calls: sizes, then the data).  AD_ERR_UNSUPPORTED when the window holds
+ * 2^31 ints or more (page smaller windows, as with ad_fetch_rows). */
+int  ad_fetch_inverse(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t hi, size_t* total,
+                      uint32_t* off /* [hi-lo+1] */, int32_t* inv /* [*total] */);
+
 /* Stage 2' — Deps.merge of caller-supplied replies (host CSR, same batch).  parts[r*AD_NUM_CLASSES+c]. */
 typedef struct ad_csr_in {
     const uint32_t* key_off; const uint64_t* keys; const uint32_t* k2t_off; const int32_t* k2t;
@@ -253,6 +266,22 @@ int  ad_exec_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out, uint
 /* ad_exec_levels over a batch carrying CFK history: the level of a row already APPLIED or INVALID (done) */
 #define AD_LEVEL_DONE 0xFFFFFFFFu
 int  ad_max_conflicts(ad_handle* h, uint32_t* max_rank /* [replicas*n] */, uint8_t* fast /* [replicas*n] */);
+
+/* The rest of CommandStore.preaccept (local/CommandStore.java:322-347) around maxConflicts.get; it shapes the fast
+ * flags of ad_max_conflicts and ad_max_conflicts_ts (the same store state answers every view):
+ *   isExpired = now - TxnId.hlc >= preAcceptTimeout && !kind.isSyncPoint()                         (:326)
+ *            || rejectBefore.foldl(keys, rejectIfBefore > TxnId -> reject)                            (:327-328)
+ *     -> the replica answers time.uniqueNow(TxnId).asRejected(): fast = AD_FAST_REJECTED               (:330-331)
+ *   an ExclusiveSyncPoint that is not expired answers its TxnId whatever maxConflict is: fast = 1      (:333-337)
+ * ad_preaccept_expiry sets that state for the following calls: the node clock's now (hlc units) and
+ * Agent.preAcceptTimeout (AD_NO_TIMEOUT: no timeout test; the handle's default), and rejectBefore — the
+ * ReducingRangeMap<Timestamp> markExclusiveSyncPoint builds (:300-306: Timestamp::max of the ExclusiveSyncPoint TxnIds
+ * marked over each range) — as sorted disjoint intervals (start, end] with a Timestamp each (a key k stabs
+ * (k - 1, k]); m = 0 clears it.  The host merges each batch's ExclusiveSyncPoints into it (witness.RejectBefore). */
+#define AD_FAST_REJECTED 2
+#define AD_NO_TIMEOUT 0xFFFFFFFFFFFFFFFFull
+int  ad_preaccept_expiry(ad_handle* h, uint64_t now_hlc, uint64_t pre_accept_timeout, size_t m, const uint64_t* starts,
+                         const uint64_t* ends, const uint64_t* msb, const uint64_t* lsb, const int32_t* node);
 
 /* Stage 1b across batches — the store's MaxConflicts map outlives a batch (local/MaxConflicts.java:32-96,
  * CommandStore.updateMaxConflicts :282-291).  The host carries it between batches as a table sorted by key:

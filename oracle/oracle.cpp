@@ -881,6 +881,58 @@ static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uin
 
 const char* oracle_error(const oracle_result* r) { return r->error.empty() ? nullptr : r->error.c_str(); }
 
+/* The rest of CommandStore.preaccept (local/CommandStore.java:322-347) around the maxConflicts test, restated
+ * literally; the state is set by oracle_set_preaccept_expiry (test infrastructure: one global store state):
+ *   boolean isExpired = time.now() - txnId.hlc() >= preAcceptTimeout && !txnId.kind().isSyncPoint();        :326
+ *   if (rejectBefore != null && !isExpired)
+ *       isExpired = null == rejectBefore.foldl(keys, (rejectIfBefore, test) -> rejectIfBefore.compareTo(test) > 0
+ *                                                                                ? null : test, txnId, Objects::isNull);
+ *   if (isExpired) return time.uniqueNow(txnId).asRejected();           -> fast = AD_FAST_REJECTED (2)     :330-331
+ *   if (txnId.kind() == ExclusiveSyncPoint) { markExclusiveSyncPoint(..); return txnId; }   -> fast = 1    :333-337
+ * rejectBefore is a ReducingRangeMap<Timestamp>: intervals (s, e]; a key k meets (s < k <= e), a range (qs, qe]
+ * meets s < qe && e > qs. */
+static struct {
+    bool clock = false;
+    uint64_t now = 0, timeout = 0;
+    std::vector<uint64_t> s, e, msb, lsb;
+    std::vector<int32_t> node;
+} g_expiry;
+
+int oracle_set_preaccept_expiry(uint64_t now, uint64_t timeout, size_t m, const uint64_t* s, const uint64_t* e,
+                                const uint64_t* msb, const uint64_t* lsb, const int32_t* node) {
+    g_expiry.clock = timeout != AD_NO_TIMEOUT;
+    g_expiry.now = now; g_expiry.timeout = timeout;
+    g_expiry.s.assign(s, s + m); g_expiry.e.assign(e, e + m);
+    g_expiry.msb.assign(msb, msb + m); g_expiry.lsb.assign(lsb, lsb + m); g_expiry.node.assign(node, node + m);
+    return AD_OK;
+}
+
+static void preaccept_rules(const Batch& B, uint32_t i, uint32_t replicas, uint8_t* fast) {
+    const Ts& t = B.tx[i];
+    const uint32_t kind = kind_of(t);
+    const uint64_t hlc = ((t.msb & 0x7FFFull) << 48) | (t.lsb >> 16);
+    const bool sync_point = kind == AD_KIND_SYNC_POINT || kind == AD_KIND_EXCLUSIVE_SYNC_POINT;
+    bool expired = g_expiry.clock && (int64_t)(g_expiry.now - hlc) >= (int64_t)g_expiry.timeout && !sync_point;
+    if (!expired && !g_expiry.s.empty()) {
+        bool rejected = false;                 // the foldl turned null: some rejectIfBefore > txnId
+        auto test = [&](size_t x) {
+            if (ts_cmp(Ts{g_expiry.msb[x], g_expiry.lsb[x], g_expiry.node[x]}, t) > 0) rejected = true;
+        };
+        for (size_t x = 0; x < g_expiry.s.size() && !rejected; ++x) {
+            if (domain_of(t) == AD_DOMAIN_KEY) {
+                for (uint32_t p = B.key_off[i]; p < B.key_off[i + 1]; ++p)
+                    if (g_expiry.s[x] < B.keys[p] && B.keys[p] <= g_expiry.e[x]) { test(x); break; }
+            } else {
+                for (uint32_t q = B.range_off[i]; q < B.range_off[i + 1]; ++q)
+                    if (g_expiry.s[x] < B.ranges[q].e && g_expiry.e[x] > B.ranges[q].s) { test(x); break; }
+            }
+        }
+        expired = rejected;
+    }
+    if (!expired && kind != AD_KIND_EXCLUSIVE_SYNC_POINT) return;
+    for (uint32_t v = 0; v < replicas; ++v) fast[(size_t)v * B.n + i] = expired ? AD_FAST_REJECTED : 1;
+}
+
 /* witnessedAt proposal per view (CommandStore.preaccept, local/CommandStore.java:322-347): max_rank[v*n+i] =
  * Oracle::max_conflict (key and range footprints), fast[v*n+i] = TxnId_i >= that executeAt (or none) — the
  * fast-path test :343.  -1 on invalid input. */
@@ -898,6 +950,7 @@ int oracle_max_conflicts(const ad_batch* b, const ad_config* c, uint32_t* max_ra
                 max_rank[(size_t)v * n + i] = m;
                 fast[(size_t)v * n + i] = (m == UINT32_MAX || ts_cmp(B.tx[i], B.ex[m]) >= 0) ? 1 : 0;
             }
+        for (uint32_t i = 0; i < n; ++i) preaccept_rules(B, i, cfg.replicas, fast);
         return AD_OK;
     } catch (const std::exception&) {
         return AD_ERR_ARGUMENT;
@@ -961,6 +1014,7 @@ int oracle_max_conflicts_ts_ranges(const ad_batch* b, const ad_config* c, size_t
                 om[x] = any ? best.msb : 0; ol[x] = any ? best.lsb : 0; on[x] = any ? best.node : 0;
                 fast[x] = (!any || ts_cmp(B.tx[i], best) >= 0) ? 1 : 0;
             }
+            preaccept_rules(B, i, cfg.replicas, fast);
         }
         return AD_OK;
     } catch (const std::exception&) {
@@ -1139,6 +1193,34 @@ int oracle_union(const uint64_t* lk, size_t nlk, const uint32_t* lv, size_t nlv,
     std::copy(o.keys.begin(), o.keys.end(), ok); *nok = o.keys.size();
     std::copy(o.vals.begin(), o.vals.end(), ov); *nov = o.vals.size();
     std::copy(o.k2t.begin(), o.k2t.end(), om); *nom = o.k2t.size();
+    return AD_OK;
+}
+
+/* RelationMultiMap.invert — utils/RelationMultiMap.java:907-938, as KeyDeps.txnIdsToKeys (primitives/KeyDeps.java
+ * :362-367) and RangeDeps.txnIdsToRanges (primitives/RangeDeps.java:576-582) call it: src = keysToTxnIds
+ * (srcKeyCount end offsets, then value indices), trg = trgKeyCount end offsets (base trgKeyCount), then per value
+ * index its key indices ascending.  trg must hold trgKeyCount + srcLength - srcKeyCount ints. */
+int oracle_invert(const int32_t* src, size_t src_len, size_t src_keys, size_t trg_keys, int32_t* trg) {
+    if (src_len < src_keys) return AD_ERR_ARGUMENT;
+    const size_t len = trg_keys + src_len - src_keys;
+    std::fill(trg, trg + len, 0);
+    if (len == 0) return AD_OK;
+    // first pass: count per value
+    for (size_t i = src_keys; i < src_len; ++i) {
+        if (src[i] < 0 || (size_t)src[i] >= trg_keys) return AD_ERR_ARGUMENT;
+        trg[src[i]]++;
+    }
+    // into offsets (base trgKeyCount), then shifted forward one so trg[v] is v's start
+    trg[0] += (int32_t)trg_keys;
+    for (size_t i = 1; i < trg_keys; ++i) trg[i] += trg[i - 1];
+    for (size_t i = trg_keys; i-- > 1;) trg[i] = trg[i - 1];
+    trg[0] = (int32_t)trg_keys;
+    // place each key at its value's cursor (the cursor ends as the value's end offset)
+    size_t k = 0;
+    for (size_t i = src_keys; i < src_len; ++i) {
+        while (k < src_keys && i == (size_t)src[k]) ++k;
+        trg[trg[src[i]]++] = (int32_t)k;
+    }
     return AD_OK;
 }
 

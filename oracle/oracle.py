@@ -59,6 +59,8 @@ def lib():
         L.oracle_union.argtypes = [u64p, C.c_size_t, u32p, C.c_size_t, i32p, C.c_size_t,
                                    u64p, C.c_size_t, u32p, C.c_size_t, i32p, C.c_size_t,
                                    u64p, szp, u32p, szp, i32p, szp]
+        L.oracle_set_preaccept_expiry.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
+        L.oracle_invert.argtypes = [i32p, C.c_size_t, C.c_size_t, C.c_size_t, i32p]
         L.oracle_recover.restype = C.c_void_p
         L.oracle_recover.argtypes = [C.POINTER(abi.AdBatch), C.c_void_p, C.c_void_p, C.c_size_t]
         L.oracle_recovery_error.restype = C.c_char_p
@@ -167,6 +169,18 @@ def _carry_ranges(table):
     return tuple(np.ascontiguousarray(a, dt) for a, dt in zip(table, (np.uint64,) * 4 + (np.int32,)))
 
 
+NO_TIMEOUT = 0xFFFFFFFFFFFFFFFF
+
+
+def set_preaccept_expiry(now=0, timeout=NO_TIMEOUT, reject_before=None):
+    """The store state of CommandStore.preaccept's expiry test (oracle.cpp preaccept_rules) for the following
+    max_conflicts / max_conflicts_ts calls: the clock's now (hlc), preAcceptTimeout (NO_TIMEOUT: no timeout test) and
+    rejectBefore as (starts, ends, msb, lsb, node) intervals (s, e] (None: empty)."""
+    s, e, m, l, nd = _carry_ranges(reject_before)
+    lib().oracle_set_preaccept_expiry(now, timeout, len(s), s.ctypes.data, e.ctypes.data, m.ctypes.data, l.ctypes.data,
+                                      nd.ctypes.data)
+
+
 def max_conflicts_ts(batch, cfg, carry=None, carry_ranges=None):
     """maxConflicts.get(keys or ranges) over a carried MaxConflicts map (key table + interval table) + the batch, as
     timestamps: (msb [R, n], lsb [R, n], node [R, n], fast [R, n])."""
@@ -255,6 +269,17 @@ def union_relation(left, right):
                        _p(rk, C.c_uint64), len(rk), _p(rv, C.c_uint32), len(rv), _p(rm, C.c_int32), len(rm),
                        _p(ok, C.c_uint64), C.byref(nk), _p(ov, C.c_uint32), C.byref(nv), _p(om, C.c_int32), C.byref(nm))
     return ok[:nk.value].copy(), ov[:nv.value].copy(), om[:nm.value].copy()
+
+
+def invert(k2t, n_keys, n_vals):
+    """RelationMultiMap.invert (oracle.cpp oracle_invert): keysToTxnIds of n_keys keys over n_vals TxnIds ->
+    txnIdsToKeys (KeyDeps.txnIdsToKeys / RangeDeps.txnIdsToRanges)."""
+    src = np.ascontiguousarray(k2t, np.int32)
+    out = np.zeros(max(n_vals + len(src) - n_keys, 1), np.int32)
+    rc = lib().oracle_invert(_p(src, C.c_int32), len(src), n_keys, n_vals, _p(out, C.c_int32))
+    if rc != abi.AD_OK:
+        raise ValueError("invert rejected input (rc=%d)" % rc)
+    return out[:n_vals + len(src) - n_keys].copy()
 
 
 EMPTY_RELATION = (np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int32))

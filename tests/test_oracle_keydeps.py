@@ -128,3 +128,49 @@ def test_builder_duplicate_values_deduplicated():
     keys, vals, k2t = O.build_relation(np.array([9, 9, 9, 3], np.uint64), np.array([4, 2, 4, 1], np.uint32))
     assert list(keys) == [3, 9] and list(vals) == [1, 2, 4]
     assert list(k2t) == [3, 5, 0, 1, 2]
+
+
+def check_inverse(rel, canonical, rank):
+    """KeyDepsTest.testSimpleEquality's inverse check (:443-450): participatingKeys(txnId) == invertCanonical()
+    for every TxnId, where participatingKeys reads txnIdsToKeys = RelationMultiMap.invert(keysToTxnIds)
+    (KeyDeps.java:318-330, :362-367; RelationMultiMap.java:907-938)."""
+    keys, vals, k2t = rel
+    inv = O.invert(k2t, len(keys), len(vals))
+    nt = len(vals)
+    assert len(inv) == nt + len(k2t) - len(keys)
+    inverted = {}
+    for k, s in canonical.items():
+        for t in s:
+            inverted.setdefault(rank[t], []).append(k)
+    assert sorted(inverted) == [int(v) for v in vals]
+    start = nt
+    for ti, v in enumerate(vals):
+        end = int(inv[ti])
+        assert [int(keys[x]) for x in inv[start:end]] == sorted(inverted[int(v)])
+        start = end
+    assert start == len(inv)
+
+
+def test_invert_matches_invert_canonical():
+    """txnIdsToKeys over the KeyDepsTest.main seeds (testMerge inputs, built and merged)."""
+    for seed in range(200):
+        deps = refgen.testmerge_inputs(seed)
+        rank = ranks_of(deps)
+        merged = O.EMPTY_RELATION
+        for d in deps:
+            if not d.canonical:
+                continue
+            rel = build(d.add_order(), rank)
+            check_inverse(rel, d.canonical, rank)
+            merged = O.union_relation(merged, rel)
+        check_inverse(merged, union_canonical(deps), rank)
+
+
+def test_invert_edge_cases():
+    assert len(O.invert(np.zeros(0, np.int32), 0, 0)) == 0
+    # one key, three txns
+    assert list(O.invert(np.array([4, 0, 1, 2], np.int32), 1, 3)) == [4, 5, 6, 0, 0, 0]
+    # two keys sharing txn 1; the reference layout is nKeys end offsets then indices
+    assert list(O.invert(np.array([4, 5, 0, 1, 1], np.int32), 2, 2)) == [3, 5, 0, 0, 1]
+    # a TxnId without keys (legal for SerializerSupport input) gets an empty run
+    assert list(O.invert(np.array([3, 0, 2], np.int32), 1, 3)) == [4, 4, 5, 0, 0]

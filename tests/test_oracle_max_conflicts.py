@@ -317,7 +317,8 @@ def test_ts_folds_carried_points_and_intervals():
                         t = bt
                 assert (int(om[v, i]), int(ol[v, i]), int(on[v, i])) == (t if t is not None else (0, 0, 0)), (v, i)
                 me = (int(b["txn_msb"][i]), int(b["txn_lsb"][i]), int(b["txn_node"][i]))
-                assert int(fast[v, i]) == int(t is None or _order(*me)[:4] >= _order(*t)[:4])
+                esp = (int(b["txn_lsb"][i]) >> 1) & 7 == abi.KIND_EXCLUSIVE_SYNC_POINT   # CommandStore.java:333-337
+                assert int(fast[v, i]) == int(esp or t is None or _order(*me)[:4] >= _order(*t)[:4])
         assert fast.min() == 0 and fast.max() == 1
 
 
