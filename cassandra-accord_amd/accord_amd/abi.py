@@ -43,6 +43,34 @@ class AdBatch(C.Structure):
                 ("range_off", _u32p), ("range_start", _u64p), ("range_end", _u64p)]
 
 
+class AdCfkState(C.Structure):
+    """ad_cfk_state: CFK states (byId TxnInfos per key) for ad_cfk_notify."""
+    _fields_ = [("keys", C.c_size_t), ("rows", C.c_size_t), ("row_off", _u32p),
+                ("txn_msb", _u64p), ("txn_lsb", _u64p), ("txn_node", _i32p),
+                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p),
+                ("status", _u8p), ("miss_off", _u32p), ("missing", _u32p)]
+
+
+CFK_STATE_FIELDS = (("row_off", np.uint32), ("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),
+                    ("exec_msb", np.uint64), ("exec_lsb", np.uint64), ("exec_node", np.int32), ("status", np.uint8),
+                    ("miss_off", np.uint32), ("missing", np.uint32))
+
+
+def make_cfk_state(st):
+    """Dict of arrays (CFK_STATE_FIELDS) -> (AdCfkState, keep-alive list)."""
+    keep = {}
+    for f, dt in CFK_STATE_FIELDS:
+        keep[f] = np.ascontiguousarray(st[f], dt)
+    s = AdCfkState()
+    s.keys = len(keep["row_off"]) - 1
+    s.rows = len(keep["status"])
+    for f, dt in CFK_STATE_FIELDS:
+        a = keep[f]
+        ct = {np.uint32: _u32p, np.uint64: _u64p, np.int32: _i32p, np.uint8: _u8p}[dt]
+        setattr(s, f, a.ctypes.data_as(ct))
+    return s, keep
+
+
 class AdConfig(C.Structure):
     _fields_ = [("window", C.c_uint32), ("replicas", C.c_uint32), ("drop_p", C.c_float),
                 ("pad_", C.c_uint32), ("seed", C.c_uint64)]

@@ -64,6 +64,7 @@ def lib():
                                     C.POINTER(abi.AdCsrOut)]
         L.ad_fetch_inverse.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t),
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
+        L.ad_cfk_notify.argtypes = [vp, C.POINTER(abi.AdCfkState), C.POINTER(C.c_uint8)]
         L.ad_preaccept_expiry.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
@@ -104,7 +105,7 @@ def lib():
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
@@ -286,6 +287,15 @@ class DepsEngine:
         rej = np.zeros(max(nq, 1), np.uint8)
         self._check(lib().ad_fetch_recovery_flags(self.h, rej.ctypes.data), "ad_fetch_recovery_flags")
         return out, rej[:nq]
+
+    def cfk_notify(self, state):
+        """CommandsForKey.notifyManaged's release rule (ad_cfk_notify) over CFK states: `state` is a dict of the
+        abi.CFK_STATE_FIELDS arrays (per key its byId TxnInfos: TxnId, InternalStatus, executeAt, missing as row
+        indices).  Returns not_waiting [rows] uint8."""
+        s, keep = abi.make_cfk_state(state)
+        out = np.zeros(max(s.rows, 1), np.uint8)
+        self._check(lib().ad_cfk_notify(self.h, C.byref(s), out.ctypes.data_as(C.POINTER(C.c_uint8))), "ad_cfk_notify")
+        return out[:s.rows]
 
     def cfk_update(self, gid, status, exec_msb=None, exec_lsb=None, exec_node=None):
         """Status transitions of kept rows between batches (after cfk_retain, before the next load): gid[m]

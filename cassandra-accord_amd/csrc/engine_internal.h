@@ -25,6 +25,7 @@
 #include "level_kernels.h"
 #include "history_kernels.h"
 #include "invert_kernels.h"
+#include "notify_kernels.h"
 #include "recovery_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
@@ -269,6 +270,7 @@ enum Slot : size_t {
     S_MHS,                                                      // heavy merge: identical-replies flags
     S_IVC, S_IVK0, S_IVV0, S_IVK1, S_IVV1, S_IVOUT,             // ad_fetch_inverse (invert_kernels.h)
     S_RBS, S_RBE, S_RBM, S_RBL, S_RBN,                          // rejectBefore intervals (ad_preaccept_expiry)
+    S_NF0, S_NF_END = S_NF0 + 14,                               // ad_cfk_notify inputs / scratch / outputs
     S_STG0, S_STG_END = S_STG0 + 12,
     S_NUM_FIXED,
     S_CSR0 = 256

@@ -427,6 +427,35 @@ int  ad_cfk_update(ad_handle* h, size_t m, const uint32_t* gid, const uint8_t* s
                    const uint64_t* exec_lsb, const int32_t* exec_node);
 int  ad_cfk_rows(ad_handle* h, size_t* hist_rows /* out */, uint32_t* gid /* [n] global rank per row, or NULL */);
 
+/* CommandsForKey's execution release rule over CFK states as a store holds them (the reference's serialized form,
+ * CommandsForKey.SerializerSupport.create(Key, TxnInfo[], Unmanaged[], prunedBefore), local/cfk/CommandsForKey.java
+ * :226-232): per key, its byId TxnInfos — TxnId, InternalStatus, executeAt, missing().  Replaces
+ * CommandsForKey.notifyManaged (:1208-1289) run over all of committedByExecuteAt with every kind admitted:
+ * not_waiting[row] = 1 for each STABLE key Read / Write the rule lets go (NotifySink.notWaiting on this key) — it
+ * lies after the last applied Write and at or before the first unapplied Write (executeAt order), and the undecided
+ * (status < COMMITTED) Reads / Writes with a lower TxnId than its executeAt that it conflicts with, plus the
+ * unapplied committed Reads ahead of it when it is a Write, number exactly its missing entries from minUndecided on
+ * (:1237-1280): a Stable txn whose dependency set holds an undecided lower TxnId waits for it to be decided.
+ * Undecided rows (status < ACCEPTED) need no executeAt (the fields are not read).  Each key is computed
+ * independently (one workgroup per key); pruning state (prunedBefore, loadingPruned) is not taken: the states must
+ * not be waiting on pruned TxnIds.  AD_ERR_UNSORTED if a key's TxnIds are not strictly ascending, AD_ERR_ARGUMENT
+ * for a missing index outside its key. */
+typedef struct ad_cfk_state {
+    size_t keys;                    /* CFK states                                                */
+    size_t rows;                    /* TxnInfo rows over all keys                                */
+    const uint32_t* row_off;        /* [keys+1] rows of key k: [row_off[k], row_off[k+1]), byId (TxnId) order */
+    const uint64_t* txn_msb;        /* [rows] TxnId                                              */
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint64_t* exec_msb;       /* [rows] executeAt (ACCEPTED .. APPLIED rows)               */
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const uint8_t*  status;         /* [rows] InternalStatus (AD_ST_*)                           */
+    const uint32_t* miss_off;       /* [rows+1] TxnInfo.missing() CSR                            */
+    const uint32_t* missing;        /* row indices within the key (0 = its first row), ascending */
+} ad_cfk_state;
+int  ad_cfk_notify(ad_handle* h, const ad_cfk_state* s, uint8_t* not_waiting /* [rows] */);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU key-range sharding (one handle = one CommandStore = one GPU).                     */
 /*                                                                                             */

@@ -1,25 +1,32 @@
 """Shared helpers for the CommandsForKey state-evolution tests.
 
-TRANSITIONS restates CommandsForKeyTest.Canon's transition table (accord-core/src/test/java/accord/local/cfk/
-CommandsForKeyTest.java:235-246) over CommandsForKey.InternalStatus (CommandsForKey.java:493-611): SaveStatus
-NotDefined is TRANSITIVELY_KNOWN here, PreAccepted / AcceptedInvalidate(WithDefinition) are PREACCEPTED
-(PREACCEPTED_OR_ACCEPTED_INVALIDATE), Accepted(WithDefinition) ACCEPTED, then COMMITTED, STABLE, APPLIED,
-INVALID.  `brute_levels` is an independent restatement of the release rule the Canon invariants check
-(:175-222): a txn is ready once every txn on its keys that executes before it and that it witnesses has applied
-(Read/Write chains; applied / invalidated txns are done and wait for nothing)."""
+The transition table is CommandsForKeyTest.Canon.TRANSITIONS exactly, over SaveStatus (accord-core/src/test/java/
+accord/local/cfk/CommandsForKeyTest.java:235-246, restated in cfk_canon.TRANSITIONS): a row's SaveStatus moves, and
+the CommandsForKey sees InternalStatus.from(SaveStatus) (CommandsForKey.java:504-528): PreAccepted and
+AcceptedInvalidateWithDefinition are PREACCEPTED, Accepted(WithDefinition) ACCEPTED, then COMMITTED, STABLE, APPLIED,
+INVALID; NotDefined and AcceptedInvalidate (no definition) have none, so the CFK does not change on them.  An
+AcceptedInvalidate(WithDefinition) row can only become Invalidated (:240-241).  `brute_levels` is an independent
+restatement of the release rule the Canon invariants check (:175-222): a txn is ready once every txn on its keys that
+executes before it and that it witnesses has applied (Read/Write chains; applied / invalidated txns are done and wait
+for nothing)."""
 import numpy as np
 
+import cfk_canon as K
 from accord_amd import abi
 
 TK, PA, AC, CM, SB, AP, IV = (abi.ST_TRANSITIVELY_KNOWN, abi.ST_PREACCEPTED, abi.ST_ACCEPTED, abi.ST_COMMITTED,
                               abi.ST_STABLE, abi.ST_APPLIED, abi.ST_INVALID)
-TRANSITIONS = {
-    TK: (PA, PA, AC, CM, SB, IV),      # NotDefined -> PreAccepted, AcceptedInvalidate(+Def), Accepted, Committed, Stable, Invalidated
-    PA: (PA, AC, CM, SB, IV),          # PreAccepted -> AcceptedInvalidateWithDefinition, AcceptedWithDefinition, ...
-    AC: (CM, SB, IV),
-    CM: (SB,),
-    SB: (AP,),
-}
+TRANSITIONS = K.TRANSITIONS                 # SaveStatus -> its successors (:235-246)
+INTERNAL = K._INTERNAL                      # SaveStatus -> InternalStatus (None: the CFK does not change)
+SAVE_OF = {TK: K.NOT_DEFINED, PA: K.PRE_ACCEPTED, AC: K.ACCEPTED_SS, CM: K.COMMITTED_SS, SB: K.STABLE_SS,
+           AP: K.APPLIED_SS, IV: K.INVALIDATED}
+
+
+def save_statuses(status):
+    """A SaveStatus for each InternalStatus (the unambiguous representative: PREACCEPTED -> PreAccepted)."""
+    return np.array([SAVE_OF[int(s)] for s in status], np.int64)
+
+
 DONE = (AP, IV)
 
 
@@ -76,23 +83,31 @@ def ready_invariant(b, lvl):
                     assert b["status"][d] in DONE, "txn %d released before %d (executes earlier, witnessed) applied" % (t, d)
 
 
-def transitions(rng, status, ready, p_move=0.35, p_apply=0.6, p_invalid=0.02):
-    """One round of Canon-style updates over rows with the given current statuses: every non-terminal row moves
-    with probability p_move to a random successor of TRANSITIONS (INVALID only with probability p_invalid);
-    STABLE rows apply only when `ready` (released at level 0), with probability p_apply.  Returns (rows, new)."""
+def transitions(rng, status, ready, save, p_move=0.35, p_apply=0.6, p_invalid=0.02):
+    """One round of Canon-style updates: every row moves with probability p_move along TRANSITIONS from its SaveStatus
+    save[r] (Invalidated only with probability p_invalid); STABLE rows apply only when `ready` (released at level 0),
+    with probability p_apply.  save is updated in place; returns (rows, new InternalStatus) of the rows whose
+    InternalStatus changes (the CommandsForKey updates: a move to NotDefined / AcceptedInvalidate, or between the
+    two PREACCEPTED SaveStatuses, changes nothing there)."""
     rows, new = [], []
-    for r, s in enumerate(status):
-        s = int(s)
-        if s == SB:
+    for r in range(len(status)):
+        ss = int(save[r])
+        if ss == K.STABLE_SS:
             if ready[r] and rng.random() < p_apply:
+                save[r] = K.APPLIED_SS
                 rows.append(r)
                 new.append(AP)
             continue
-        if s not in TRANSITIONS or rng.random() >= p_move:
+        if ss not in TRANSITIONS or ss == K.STABLE_SS or rng.random() >= p_move:
             continue
-        choices = [x for x in TRANSITIONS[s] if x != IV or rng.random() < p_invalid]
+        # Invalidated is rare unless it is the only successor (AcceptedInvalidate(WithDefinition), :240-241)
+        choices = [x for x in TRANSITIONS[ss] if x != K.INVALIDATED or len(TRANSITIONS[ss]) == 1 or rng.random() < p_invalid]
         if not choices:
             continue
-        rows.append(r)
-        new.append(int(rng.choice(choices)))
+        nss = int(choices[rng.integers(len(choices))])
+        save[r] = nss
+        ni = INTERNAL.get(nss)
+        if ni is not None and ni != int(status[r]):
+            rows.append(r)
+            new.append(ni)
     return np.array(rows, np.int64), np.array(new, np.uint8)

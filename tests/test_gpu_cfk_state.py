@@ -10,7 +10,7 @@ import pytest
 
 import oracle as O
 from accord_amd import abi, engine, workload
-from cfk_state import AP, CM, IV, PA, SB, TRANSITIONS, brute_levels, ready_invariant, transitions
+from cfk_state import AP, CM, IV, PA, SB, TRANSITIONS, brute_levels, ready_invariant, save_statuses, transitions
 from test_oracle_history import _mapped, _take, keep_rows
 
 pytestmark = pytest.mark.gpu
@@ -29,6 +29,7 @@ def test_cfk_state_stream(engine_factory, n_b, nb, keyspace, replicas):
     cfg = abi.make_config(0, replicas, 0.0, 0x5EED)       # snapshot queries: the statuses are current
     eng = engine_factory(window=0, replicas=replicas, drop_p=0.0, seed=0x5EED)
     pruned_total = 0
+    save = save_statuses(stream["status"])
     for k in range(n_b):
         seen = (k + 1) * nb
         rows = np.arange(k * nb, seen)
@@ -65,7 +66,7 @@ def test_cfk_state_stream(engine_factory, n_b, nb, keyspace, replicas):
         keep = keep_rows(_take(upto, gid.astype(np.int64)), gid, 0)
         assert eng.cfk_retain() == len(keep)
         keep_gids = gid[keep]
-        rows_upd, new = transitions(rng, upto["status"], [x == 0 for x in lvl])
+        rows_upd, new = transitions(rng, upto["status"], [x == 0 for x in lvl], save[:seen])
         held = np.zeros(seen, bool)
         held[keep_gids] = True
         assert not np.isin(upto["status"][~held], [PA, abi.ST_ACCEPTED, CM, SB]).any(), "a pruned row still had to execute"

@@ -7,7 +7,7 @@ import pytest
 
 import oracle as O
 from accord_amd import abi, workload
-from cfk_state import DONE, PA, SB, brute_levels, ready_invariant, transitions
+from cfk_state import DONE, PA, SB, brute_levels, ready_invariant, save_statuses, transitions
 
 
 def _levels(b, flags=O.FLAG_MERGE | O.FLAG_LEVELS | O.FLAG_DONE):
@@ -46,12 +46,13 @@ def test_canon_stream_ready_invariant():
     n = 600
     b = workload.generate(n, keys_per_txn=2, keyspace=25, status=np.full(n, PA, np.uint8), slow_frac=0.3, bump_max=30, seed=7)
     applied = 0
+    save = save_statuses(b["status"])
     for step in range(60):
         lv, _ = _levels(b)
         lvl = [None if x == abi.AD_LEVEL_DONE else int(x) for x in lv]
         assert lvl == brute_levels(b)
         ready_invariant(b, lvl)
-        rows, new = transitions(rng, b["status"], [x == 0 for x in lvl])
+        rows, new = transitions(rng, b["status"], [x == 0 for x in lvl], save)
         applied += int((new == abi.ST_APPLIED).sum())
         b["status"][rows] = new
     assert applied > 150 and (np.isin(b["status"], DONE)).mean() > 0.2
