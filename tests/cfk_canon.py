@@ -825,7 +825,7 @@ class Run:
         canon = Canon(rnd, self.domains)
         cfk = CFK(self.domains)
         self.canon, self.cfk = canon, cfk
-        self.snapshots = []                           # (event index, rows, cumulative managed notified set)
+        self.snapshots = []                           # (event, rows, notified-and-STABLE set, full-scan release set)
         self.events = 0
         self.notified = set()
         self.full_scan_mismatches = []
@@ -881,7 +881,7 @@ class Run:
                     self.full_scan_mismatches.append((self.events, sorted(got - want), sorted(want - got)))
             if snapshot_every and (fresh or self.events % snapshot_every == 0):
                 self.snapshots.append((self.events, self.rows(), frozenset(
-                    t for t in self.notified if cfk.info[t].status == STABLE)))
+                    t for t in self.notified if cfk.info[t].status == STABLE), frozenset(full_scan_ready(cfk))))
 
     def rows(self):
         """The CFK as the C-ABI takes it (CommandsForKey.SerializerSupport.create, :226-232): byId TxnInfos —

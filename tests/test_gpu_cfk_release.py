@@ -21,14 +21,15 @@ SEEDS = list(range(20))
 
 
 def _check_states(eng, snapshots, domains):
-    st = K.pack_states([rows for _, rows, _ in snapshots])
+    st = K.pack_states([rows for _, rows, _, _ in snapshots])
     got = eng.cfk_notify(st)
     off = st["row_off"]
     released = 0
-    for k, (ev, rows, want) in enumerate(snapshots):
+    for k, (ev, rows, want, full) in enumerate(snapshots):
         g = got[off[k]:off[k + 1]]
         dev = {rows[i][0] for i in np.nonzero(g)[0]}
         assert dev == set(want), "event %d: device %s, reference %s" % (ev, sorted(dev - set(want))[:4], sorted(set(want) - dev)[:4])
+        assert dev == set(full), "event %d: device vs the full-scan restatement" % ev
         released += len(dev)
         # Canon notWaiting invariant (:208-211) on the device's release
         for t in dev:
