@@ -6,13 +6,16 @@ One step = one pass of the hot path over one device-resident batch:
   Deps.merge of the 3 replies, and execution levels/order over the merged graph.
 
 N = 1 (BASELINE.json configs[1], C2): one 1M-txn batch (4 keys/txn, uniform over 10M keys) on one GPU,
-  ad_run_pipeline().
-N > 1 (configs[4], C5 shape, weak scaling): a global batch of N x 1M txns over N x 10M keys, key-range
-  sharded across the N GPUs (one process and CommandStore per GPU, ShardDistributor.EvenSplit).  Most txns
-  span several stores, so each step is the full cross-shard protocol (accord_amd.sharding.run_store):
-  local deps on the store's slice, export, all-gather of the per-store fragments over RCCL/xGMI, merge of
-  the fragments of the store's home txns (PreAccept.reduce) and across replica views (Deps.merge), and the
-  distributed level fixpoint (rounds of local chain relaxation + RCCL all-reduce(max)), then the order.
+  ad_run_pipeline().  The line also carries `scaling_reference`: C5's generator at 2,097,152 txns on one unsharded
+  store, the per-GPU baseline of the N > 1 series below.
+N > 1 (configs[4], C5, weak scaling): a global batch of N x 2,097,152 txns of C5's generator (4 uniform keys over
+  10^7 keys; N = 8 is C5 itself, 16,777,216 txns), key-range sharded across the N GPUs (one process and
+  CommandStore per GPU, ShardDistributor.EvenSplit).  Most txns span several stores, so each step is the full
+  cross-shard protocol (accord_amd.sharding.run_store): local deps on the store's slice, export, all-to-all of the
+  per-destination fragments over RCCL/xGMI, merge of the fragments of the store's home txns (PreAccept.reduce) and
+  across replica views (Deps.merge), then the execution levels by the protocol sharding.choose_levels picks:
+  distributed delta rounds (each store relaxes only its own key chains; only raised levels of txns another store
+  holds travel) for shallow graphs like C5's, or one exchange of every store's constraint edges for deep ones.
 
 Timing: W untimed warmup steps; then barrier + device sync, K timed steps, device sync + barrier,
 max over ranks.  The HIP work runs on the engine's own stream; every step ends synchronised on it, so
@@ -378,12 +381,15 @@ class stdout_to_stderr:
         return False
 
 
+C5_PER_GPU = 1 << 21            # C5: 16,777,216 txns over 8 GPUs
+
+
 def main_sharded(args, rank, world, local, dist):
     """N > 1: the C5 cross-shard protocol (see module docstring)."""
     from accord_amd import sharding
     n_total = args.n * world
-    batch = workload.generate(n_total, 4, KEYSPACE * world, "uniform", seed=workload.SEEDS["C5"])
-    bounds = sharding.even_bounds(0, KEYSPACE * world, world)
+    batch = workload.generate(n_total, 4, KEYSPACE, "uniform", seed=workload.SEEDS["C5"])
+    bounds = sharding.even_bounds(0, KEYSPACE, world)
     lb, gid, home = sharding.slice_for_shard(batch, bounds[rank], bounds[rank + 1])
     hs = sharding.home_stores(batch, bounds)[gid]
     holders = sharding.holder_masks(batch, bounds)[gid]
@@ -431,17 +437,20 @@ def main_sharded(args, rank, world, local, dist):
     dt = float(t.item())
     roof = roofline_of(store.eng, dom, n_loc, P_loc, store.eng.last_times(), pmc=False)
     store.eng.set_trace(0)
+    protocol = ("delta rounds (each store relaxes its own key chains; raised levels of shared txns travel)"
+                if rounds <= sharding.AUTO_ROUND_CAP else "one exchange of every store's constraint edges")
     out = {
         "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
         "value": n_total * args.steps / dt, "unit": "txn/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C5 generator, BASELINE configs[4] shape)",
-        "config": {"workload": "C5: %d txns x 4 keys uniform over %dM keys, key-range sharded over %d GPUs "
-                               "(cross-shard deps all-to-all to the home store, distributed level rounds); R=%d views, W=%d, drop %.1f"
-                               % (n_total, 10 * world, world, REPLICAS, WINDOW, DROP_P),
+        "config": {"workload": "C5 generator: %d txns (%d per GPU) x 4 keys uniform over 10M keys, key-range sharded "
+                               "over %d GPUs (cross-shard deps all-to-all to the home store, levels by %s); R=%d views, "
+                               "W=%d, drop %.1f" % (n_total, args.n, world, world, protocol, REPLICAS, WINDOW, DROP_P),
                    "txns_total": n_total, "txns_per_gpu": args.n, "local_txns_rank0": n_loc, "local_pairs_rank0": P_loc,
-                   "keys_per_txn": 4, "keyspace": KEYSPACE * world, "replicas": REPLICAS, "window": WINDOW,
+                   "keys_per_txn": 4, "keyspace": KEYSPACE, "replicas": REPLICAS, "window": WINDOW,
                    "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds,
+                   "level_protocol": protocol,
                    "level_exchange_bytes_rank0": 8 * store.pairs_sent,
                    "level_exchange_bytes_dense": 4 * (n_total + 1) * rounds,
                    "phase_ms_rank0": {k: round(v * 1e3 / args.steps, 3) for k, v in phases.items()}},
@@ -477,7 +486,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        args.n = args.n or (1 << 20)
+        args.n = args.n or C5_PER_GPU
         import torch.distributed as tdist
         with stdout_to_stderr():          # gloo's connection notices
             tdist.init_process_group("gloo")

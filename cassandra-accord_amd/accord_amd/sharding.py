@@ -591,10 +591,18 @@ class LevelsNotConverged(RuntimeError):
     final and must not be reported (every store raises it in the same round: the flag is all-reduced)."""
 
 
-def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="gather"):
-    """The per-store protocol after load(): returns the number of level exchanges (1 with levels="gather",
-    the default; the round count with levels="rounds", the per-round delta / dense exchange, which raises
-    LevelsNotConverged if the rounds reach max_rounds while levels are still changing).
+AUTO_ROUND_CAP = 128
+
+
+def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="auto", round_cap=AUTO_ROUND_CAP):
+    """The per-store protocol after load(): returns the number of level exchanges.
+    levels="rounds": the per-round delta (holders set) / dense exchange, each store relaxing only its own key chains;
+      raises LevelsNotConverged if the rounds reach max_rounds while levels are still changing.
+    levels="gather": one exchange of every store's constraint edges, every store solving their union (returns 1).
+    levels="auto" (default): delta rounds while they converge within round_cap rounds — per-store work and exchange
+      volume independent of the store count, rounds ~ the graph's depth (C5: tens) — else, every store agreeing (the
+      round flag is global), the one-exchange gather for the deep graph (C3-like hot keys: ~10^5 levels); without
+      holder masks the gather.  Returns round_cap + 1 when it fell back.
     timings (dict, optional) accumulates wall seconds per phase (each phase ends synchronised)."""
     import time
     clock = time.perf_counter
@@ -612,11 +620,28 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="gather
     lap("exchange")
     store.merge()
     lap("merge")
+    if levels == "auto":
+        if store.delta:
+            return run_levels_auto(store, transport, round_cap, lap)
+        levels = "gather"
     if levels == "gather":
         store.depth = transport.gather_levels(store)
         lap("levels")
         return 1
     return run_levels(store, transport, max_rounds, lap)
+
+
+def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
+    """levels="auto" of run_store: the delta rounds, or — when they have not converged after round_cap rounds (every
+    store sees the same global round flag, so all switch together) — the one-exchange gather, which recomputes the
+    levels from every store's constraint edges.  Returns the rounds, or round_cap + 1 after the fallback."""
+    lap = lap or (lambda name: None)
+    try:
+        return run_levels(store, transport, round_cap, lap)
+    except LevelsNotConverged:
+        store.depth = transport.gather_levels(store)
+        lap("levels_gather")
+        return round_cap + 1
 
 
 def run_levels(store, transport, max_rounds=1 << 16, lap=None):
@@ -676,6 +701,15 @@ class LocalTransport:
             lap("home_merge")
         if levels is None:
             return 0
+        if levels == "auto":
+            if all(s.delta for s in stores):
+                try:
+                    r = LocalTransport._rounds(stores, AUTO_ROUND_CAP)
+                    lap("level_rounds")
+                    return r
+                except LevelsNotConverged:
+                    lap("level_rounds")
+            levels = "gather"
         if levels == "gather":
             edges = np.concatenate([s.level_edges() for s in stores])
             lap("level_edges")
@@ -685,6 +719,12 @@ class LocalTransport:
                 s.depth = s.levels_solve(edges)
             lap("level_solve")
             return 1
+        r = LocalTransport._rounds(stores, max_rounds)
+        lap("level_rounds")
+        return r
+
+    @staticmethod
+    def _rounds(stores, max_rounds):
         changed = [s.levels_round(True) for s in stores]
         rounds = 1
         while True:

@@ -206,3 +206,57 @@ def test_holder_masks():
          "keys": np.array([1, 9, 5, 2, 8], np.uint64)}
     m = sharding.holder_masks(b, sharding.even_bounds(0, 10, 2))
     assert m.tolist() == [3, 0, 2, 3]
+
+
+class HostAutoStore(HostLevelStore):
+    """Both level interfaces (rounds and edges) over one store, as the engine's ShardStore has them."""
+
+    def __init__(self, local, gid, holders, n_global, rank, world, glob):
+        super().__init__(local, gid, holders, n_global, rank, world)
+        self.n_global, self.glob = n_global, glob
+        self._edges = HostEdgeStore(local, gid, n_global, glob)
+
+    def level_edges(self):
+        return self._edges.level_edges()
+
+    def levels_solve(self, edges):
+        depth = self._edges.levels_solve(edges)
+        self.G = self._edges.G.astype(np.uint64)
+        return depth
+
+
+def _auto_worker(rank, world, port, n, dist_kind, cap):
+    sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from accord_amd import abi, sharding, workload
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ks = 3000 if dist_kind == "zipf" else 200_000
+        b = workload.generate(n, 3, ks, dist_kind, seed=13)
+        bounds = sharding.even_bounds(0, ks, world)
+        masks = sharding.holder_masks(b, bounds)
+        local, gid, _ = sharding.slice_for_shard(b, bounds[rank], bounds[rank + 1])
+        store = HostAutoStore(local, gid, masks[gid], n, rank, world, b)
+        rounds = sharding.run_levels_auto(store, sharding.GlooTransport(dist), round_cap=cap)
+        want, _ = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_LEVELS).levels()
+        assert np.array_equal(store.G[gid].astype(np.uint32), want[gid]), "rank %d: levels differ" % rank
+        if dist_kind == "zipf":
+            assert rounds == cap + 1, "a deep graph falls back to the one-exchange gather"
+        else:
+            assert rounds <= cap, "a shallow graph converges in delta rounds"
+    finally:
+        dist.destroy_process_group()
+
+
+def test_auto_levels_rounds_over_gloo():
+    # C5-like uniform keys: the delta rounds converge, no edge exchange
+    mp.spawn(_auto_worker, args=(2, _free_port(), 3000, "uniform", 64), nprocs=2, join=True)
+
+
+def test_auto_levels_fall_back_to_gather_over_gloo():
+    # Zipf hot keys with a small round cap: every rank switches to the gather together, levels still exact
+    mp.spawn(_auto_worker, args=(2, _free_port(), 2500, "zipf", 3), nprocs=2, join=True)
