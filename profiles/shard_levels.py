@@ -13,7 +13,7 @@ from accord_amd import sharding, workload  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 per = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
-protos = sys.argv[3:] or ["gather", "rounds"]
+protos = sys.argv[3:] or ["gather", "rounds", "auto"]
 w, r, p, seed = 32, 3, 0.1, workload.SEEDS["C5"]
 b = workload.generate(S * per, 4, 10_000_000, "uniform", seed=seed)
 bounds = sharding.even_bounds(0, 10_000_000, S)
