@@ -384,6 +384,26 @@ class stdout_to_stderr:
 C5_PER_GPU = 1 << 21            # C5: 16,777,216 txns over 8 GPUs
 
 
+def scaling_reference(eng, args):
+    """N = 1 side measurement (outside the timed region of `value`): the per-GPU baseline of the N > 1 series —
+    C5's generator at C5_PER_GPU txns, the same draw a 1-rank C5 run would make, on ONE unsharded store
+    (ad_run_pipeline; no cross-shard protocol).  N x this rate is what perfect weak scaling of the sharded runs
+    would reach."""
+    batch = workload.generate(C5_PER_GPU, 4, KEYSPACE, "uniform", seed=workload.SEEDS["C5"])
+    eng.load(batch)
+    for _ in range(max(args.warmup, 1)):
+        eng.run_pipeline()
+    steps = max(1, min(args.steps, 5))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.run_pipeline()
+    dt = (time.perf_counter() - t0) / steps
+    st = eng.last_times()
+    return {"workload": "C5 generator: %d txns x 4 keys uniform over 10M keys, one CommandStore (no sharding)"
+                        % C5_PER_GPU, "txns": C5_PER_GPU, "steps": steps, "ms_per_step": dt * 1e3,
+            "value": C5_PER_GPU / dt, "unit": "txn/s", "level_path": st["level_path"]}
+
+
 def main_sharded(args, rank, world, local, dist):
     """N > 1: the C5 cross-shard protocol (see module docstring)."""
     from accord_amd import sharding
@@ -480,6 +500,8 @@ def main():
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the end-to-end (H2D + pipeline + D2H through the C-ABI) side measurement")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl", help="N>1 exchange: RCCL over xGMI or host/gloo")
+    ap.add_argument("--no-scaling-ref", dest="scaling_ref", action="store_false",
+                    help="N=1 C2: skip the scaling_reference side measurement (C5's per-GPU batch, one store)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -568,6 +590,8 @@ def main():
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if args.cpu_full and rank == 0:
         out["cpu_full_batch"] = cpu_full(cfgname)
+    if cfgname == "C2" and args.scaling_ref:
+        out["scaling_reference"] = scaling_reference(eng, args)
     eng.close()
     print(json.dumps(out), flush=True)
 

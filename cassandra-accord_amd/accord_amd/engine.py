@@ -489,14 +489,15 @@ class DepsEngine:
         self._check(lib().ad_last_times(self.h, C.byref(t)), "ad_last_times")
         return {f: getattr(t, f) for f, _ in abi.AdStageTimes._fields_}
 
-    LEVELS_AUTO, LEVELS_FIXPOINT, LEVELS_BLOCKS, LEVELS_KAHN, LEVELS_PULL_ABORT = 0, 1, 2, 3, 4
+    LEVELS_AUTO, LEVELS_FIXPOINT, LEVELS_BLOCKS, LEVELS_KAHN, LEVELS_PULL_ABORT, LEVELS_BLOCKS_WIDE = 0, 1, 2, 3, 4, 5
 
     def set_level_mode(self, mode):
         """LEVELS_AUTO (default; False): one-pass pull levels for short key chains, executeAt blocks for deep
         key-only batches, Kahn with explicit edges for mixed batches; LEVELS_FIXPOINT (True): always the chain
         fixpoint; LEVELS_BLOCKS: executeAt blocks for every key-only batch; LEVELS_KAHN: the Kahn wavefront
         instead of the pull levels; LEVELS_PULL_ABORT (tests): the pull levels abort at once and the Kahn
-        wavefronts recompute the batch (the abort path of AUTO)."""
+        wavefronts recompute the batch (the abort path of AUTO); LEVELS_BLOCKS_WIDE (tests): LEVELS_BLOCKS with the
+        64-bit scan words the block walk uses for batches of more than 2^20 txns."""
         mode = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
         self._check(lib().ad_set_level_mode(self.h, mode), "ad_set_level_mode")
 

@@ -9,21 +9,25 @@
 // into consecutive executeAt blocks whose only inputs from the past are the per-key states (y_k, w_k) the
 // earlier blocks leave (the "carry").  Inside a block:
 //   * the entries are grouped by key (key-major, executeAt-minor: a contiguous run of each key's chain);
-//   * along one key the DP step is a max-plus affine map of (y, w) — Read: y' = max(y, w+1, a), w' = w;
-//     Write: y' = w' = max(y+1, a), a = the txn's level from its other keys — and maps compose, so ONE
-//     block-wide scan resolves every key run of the block at once, whatever its depth;
+//   * along one key the DP runs in write epochs (a Write and the Reads after it): a Write's level is
+//     max(previous Write's level + 1 (+1 more if the epoch had Reads), its own bound a, 1 + the epoch's
+//     greatest Read bound), a Read's max(a, previous Write's level + 1) -- a max-plus recurrence that unrolls
+//     into two max scans of one packed word per entry (below), so ONE pair of wave scans resolves every key
+//     run of the block at once, whatever its depth;
 //   * txns couple key runs (a = max over the txn's entries), so the scan repeats until no txn's level
-//     rises (a Jacobi fixpoint inside the block: ~6 rounds for C3's 256-txn blocks, because only the
+//     rises (a Jacobi fixpoint inside the block: ~6.4 rounds for C3's ~250-txn blocks, because only the
 //     block's few hot keys couple).
 // One workgroup walks the blocks in executeAt order (the carry is a sequential dependency); each block's
-// state lives in LDS.  Cost = blocks x rounds x one 1024-entry LDS scan, instead of depth x one global
-// wavefront (C3: ~2.7*10^4 scans vs ~1.6*10^5 wavefronts).
+// state lives in LDS.  Cost = blocks x rounds x two one-word wave scans, instead of depth x one global
+// wavefront (C3: ~2.7*10^4 rounds vs ~1.6*10^5 wavefronts).  (Round 3 scanned 2x2 max-plus maps of six ints:
+// ~2,400 cycles a round, 72 % of the walk.)
 //
 // Preparation (all parallel, once per batch): chain order by (key, executeAt) (k_chain_rank), executeAt rank
 // of every txn (order_rows with zero levels), block of every txn from the prefix of its entry counts
 // (blocks hold <= BL_CAP entries and <= BL_CAP txns), a stable radix sort of the chain positions by block,
-// and one 8-byte record per entry: carry slot (the key's segment head), txn index inside the block, Write /
-// first-of-key-in-block / last-of-key-in-block bits.
+// one 8-byte record per entry: carry slot (the key's segment head), txn index inside the block, Write /
+// first-of-key-in-block / last-of-key-in-block bits; then per block the compacted multi-entry runs with their
+// static epoch / run ids and write-step prefix (k_bl_compact).
 #pragma once
 
 namespace ad {
@@ -31,31 +35,7 @@ namespace ad {
 constexpr int BL_T = 256;                    // one wave per SIMD
 constexpr int BL_EPT = 4;                    // entries per thread
 constexpr int BL_CAP = BL_T * BL_EPT;        // entries (and txns) per block
-constexpr int BL_NEG = -(1 << 28);
 constexpr uint32_t BL_TL = (1u << 11) - 1;     // txn-in-block index bits of a record's high word
-
-// y' = max(y + a00, w + a01, c0), w' = max(y + a10, w + a11, c1)
-struct BlMap {
-    int a00, a01, a10, a11, c0, c1;
-};
-__device__ inline int bl_clamp(int x) { return x < BL_NEG ? BL_NEG : x; }
-__device__ inline BlMap bl_identity() { return BlMap{0, BL_NEG, BL_NEG, 0, BL_NEG, BL_NEG}; }
-// g o f (f earlier, g later); entries clamp at BL_NEG so repeated composition never overflows
-__device__ inline BlMap bl_compose(const BlMap& f, const BlMap& g) {
-    BlMap h;
-    h.a00 = bl_clamp(max(f.a00 + g.a00, f.a10 + g.a01));
-    h.a01 = bl_clamp(max(f.a01 + g.a00, f.a11 + g.a01));
-    h.a10 = bl_clamp(max(f.a00 + g.a10, f.a10 + g.a11));
-    h.a11 = bl_clamp(max(f.a01 + g.a10, f.a11 + g.a11));
-    h.c0 = bl_clamp(max(max(f.c0 + g.a00, f.c1 + g.a01), g.c0));
-    h.c1 = bl_clamp(max(max(f.c0 + g.a10, f.c1 + g.a11), g.c1));
-    return h;
-}
-struct BlOp {                                 // adaptor for the DPP wave scan (scan.h)
-    using S = BlMap;
-    __device__ S identity() const { return bl_identity(); }
-    __device__ S combine(const S& f, const S& g) const { return bl_compose(f, g); }
-};
 
 // executeAt rank of every txn (order[k] = txn at rank k)
 static __global__ __launch_bounds__(256) void k_bl_erank(size_t n, const uint32_t* __restrict__ order, uint32_t* __restrict__ erank) {
@@ -154,123 +134,215 @@ static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint3
     wave_set_flag(b_, bad);
 }
 
-// Rounds over the block's multi-entry key runs, compacted (in block order) into mfl / mcar, by ONE wave with
-// E entries per lane: no barrier and no cross-wave step per round.  Every txn's singleton entries were
-// folded into lv by the prefill, so only these entries can raise a level.  The round body is branch-free
-// (absent entries are identity maps whose raises go to per-lane sink slots past BL_CAP).  On return mout[k] holds the
-// carry-out of every LAST entry k (state after it, from the final levels).  Returns the rounds.
-template <int E>
-__device__ inline uint32_t bl_wave_rounds(int nm, const uint32_t* __restrict__ mfl, const int2* __restrict__ mcar, int* lv,
-                                          const uint8_t* nl, int2* mout) {
+// ---- the multi-entry key runs of a block, compacted once per block (all blocks in parallel) ----
+// Along one key run the Read/Write rule splits into write epochs: a Write W_{k+1} closes epoch k (W_k and the
+// Reads after it), and its level is X_{k+1} = max(X_k + d_k, b_k) with d_k = 1 + [epoch k has Reads] and
+// b_k = max(a(W_{k+1}), 1 + the greatest a of epoch k's Reads); a Read of epoch k gets max(a, X_k + 1).  The
+// carry (y0, w0) of the run's head is epoch 0 (X_0 = w0, y0 taken as one more Read value of epoch 0).  With D
+// the prefix sum of d over the block's Writes this unrolls to X(p) = D(p) + max over the run's epochs so far of
+// z, z = b - D(W) (and w0 - D before the head): two max scans of one packed word per entry (segment id in the
+// high bits, so a plain unsigned max restarts at every epoch / run) instead of a scan of 2x2 max-plus maps.
+// d, D, the epoch and run ids are static per block: k_bl_compact computes them before the walk.
+// crec (uint4 per multi-entry run entry, at boff[b] + c for the c-th one of block b, block slot order):
+//   x  txn slot in block (11) | Write << 11 | HEAD << 12 | LAST << 13 | G << 14 | SRC << 15 (2) | D << 17 (12)
+//   y  epoch id (11) | run id << 11 (11) | block slot << 22 (10)          (ids count from 1 inside the block)
+//   z  carry slot (the key's segment head)      w  LDS ring index of the head's carry source (SRC 1)
+constexpr int BC_DS = 17;
+struct BlPackSum {                            // rn (11) | ep << 11 (11) | d << 22 (12) | cnt << 34 (11)
+    using S = unsigned long long;
+    __device__ S identity() const { return 0ull; }
+    __device__ S combine(S a, S b) const { return a + b; }
+};
+static __global__ __launch_bounds__(BL_T) void k_bl_compact(uint32_t B, const uint32_t* __restrict__ boff, const uint64_t* __restrict__ rec,
+                                                     uint4* __restrict__ crec, uint32_t* __restrict__ mt) {
+    __shared__ unsigned long long sred[BL_T / WAVE];
+    const uint32_t b = blockIdx.x;
+    if (b >= B) return;
+    const uint32_t j0 = boff[b], j1 = boff[b + 1];
+    const int tid = threadIdx.x;
+    uint32_t fl[BL_EPT];
+    unsigned long long v[BL_EPT], tot = 0;
+#pragma unroll
+    for (int e = 0; e < BL_EPT; ++e) {
+        const uint32_t j = j0 + (uint32_t)(tid * BL_EPT + e);
+        fl[e] = BL_NONE;
+        v[e] = 0;
+        if (j >= j1) continue;
+        const uint32_t f = (uint32_t)(rec[j] >> 32);
+        const bool head = f & (1u << BL_SH_HEAD), last = f & (1u << BL_SH_LAST), w = f & (1u << BL_SH_W);
+        if (head && last) continue;                                  // a singleton run: not compacted
+        fl[e] = f;
+        uint32_t d = 0;
+        if (w) d = head ? 1u : (((uint32_t)(rec[j - 1] >> 32) & (1u << BL_SH_W)) ? 1u : 2u);
+        v[e] = (unsigned long long)(head ? 1u : 0u) | ((unsigned long long)((w || head) ? 1u : 0u) << 11) |
+               ((unsigned long long)d << 22) | (1ull << 34);
+        tot += v[e];
+    }
+    unsigned long long total;
+    unsigned long long run = block_exclusive_scan<BlPackSum, BL_T>(BlPackSum{}, tot, sred, &total);
+#pragma unroll
+    for (int e = 0; e < BL_EPT; ++e) {
+        if (fl[e] == BL_NONE) continue;
+        run += v[e];
+        const uint32_t rn = (uint32_t)(run & 0x7FFu), ep = (uint32_t)((run >> 11) & 0x7FFu);
+        const uint32_t ds = (uint32_t)((run >> 22) & 0xFFFu), c = (uint32_t)(run >> 34) - 1u;
+        const uint32_t j = j0 + (uint32_t)(tid * BL_EPT + e);
+        const uint32_t key = (uint32_t)rec[j];
+        crec[j0 + c] = make_uint4((fl[e] & 0x1FFFFu) | (ds << BC_DS), ep | (rn << 11) | ((j - j0) << 22), key,
+                                  fl[e] >> BL_SH_RING);
+    }
+    if (tid == 0) mt[b] = (uint32_t)(total >> 34);
+}
+
+// Packed scan words: segment id in the high bits, value + BZ_BIAS in the low bits (u32: values < 2^20, i.e.
+// batches of <= 2^20 txns; u64 otherwise).  The word 0 is below every real entry's (ids count from 1).
+constexpr int BZ_BIAS = 1 << 12;
+template <class PK> __device__ constexpr int bz_sh() { return sizeof(PK) == 4 ? 21 : 32; }
+template <class PK> __device__ inline PK bz_pack(uint32_t seg, int v) {
+    return ((PK)seg << bz_sh<PK>()) | (PK)(uint32_t)(v + BZ_BIAS);
+}
+template <class PK> __device__ inline int bz_val(PK p) {
+    return (int)(uint32_t)(p & (((PK)1 << bz_sh<PK>()) - 1)) - BZ_BIAS;
+}
+template <class PK>
+struct BzMax {
+    using S = PK;
+    __device__ S identity() const { return (PK)0; }
+    __device__ S combine(S a, S b) const { return a > b ? a : b; }
+};
+
+// Jacobi rounds over the block's compacted multi-entry runs by ONE wave, E consecutive entries per lane: per
+// round the two packed max scans above give every entry's level candidate x; x > a raises the txn (LDS
+// atomicMax).  Until no txn with a non-LAST entry rises (nl).  Absent entries (beyond nm) read and raise the
+// lane's sink slot past BL_CAP.  Then the carry-out of every LAST entry -- y' = max(y0, the levels of the
+// run's txns), w' = max(w0, the levels of its Writes) -- into the ring (and global memory for G).  Returns
+// the rounds.
+template <int E, class PK>
+__device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const int2* __restrict__ hc, int* lv,
+                                     const uint8_t* nl, int2* ring, int rb, int2* carry, uint32_t* stuck) {
     const int lane = __lane_id();
-    uint32_t slot[E];
-    bool valid[E], head[E], wr[E], last[E];
-    int yc[E], wc[E], py[E], pw[E], a[E];
+    uint32_t slot[E], ds[E], ep[E], rn[E];
+    bool wr[E], hd[E], lst[E];
+    int y0[E], w0[E], a[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int k = lane * E + e;
-        valid[e] = k < nm;
-        const uint32_t fe = valid[e] ? mfl[k] : 0u;
-        const int2 c = valid[e] ? mcar[k] : make_int2(-1, -1);
-        slot[e] = valid[e] ? (fe & BL_TL) : (uint32_t)(BL_CAP + lane);     // absent: the lane's own sink
-        head[e] = fe & (1u << BL_SH_HEAD);
-        wr[e] = fe & (1u << BL_SH_W);
-        last[e] = valid[e] && (fe & (1u << BL_SH_LAST));
-        yc[e] = c.x; wc[e] = c.y;
-        py[e] = pw[e] = -1;
+        const bool v = k < nm;
+        const uint4 c = v ? cr[k] : make_uint4(0u, 0u, 0u, 0u);
+        slot[e] = v ? (c.x & BL_TL) : (uint32_t)(BL_CAP + lane);
+        wr[e] = (c.x >> BL_SH_W) & 1u;
+        hd[e] = (c.x >> BL_SH_HEAD) & 1u;
+        lst[e] = (c.x >> BL_SH_LAST) & 1u;
+        ds[e] = c.x >> BC_DS;
+        ep[e] = c.y & 0x7FFu;
+        rn[e] = (c.y >> 11) & 0x7FFu;
+        const int2 h = hd[e] ? hc[k] : make_int2(-1, -1);
+        y0[e] = h.x; w0[e] = h.y;
     }
-    const BlOp op{};
+    const BzMax<PK> op{};
     uint32_t it = 0;
     while (true) {
 #pragma unroll
         for (int e = 0; e < E; ++e) a[e] = lv[slot[e]];
-        // the lane's aggregate, field by field (a struct select would go through scratch memory)
-        int g00 = 0, g01 = BL_NEG, g10 = BL_NEG, g11 = 0, gc0 = BL_NEG, gc1 = BL_NEG;
+        // scan 1: Read values by epoch (a Write opens its epoch with the bare segment word)
+        PK r1 = 0, pre1[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            // head -> constant; Write: y' = w' = max(y + 1, a); Read: y' = max(y, w + 1, a), w' = w
-            const bool W = wr[e], H = head[e], V = valid[e];
-            const int hx = W ? max(yc[e] + 1, a[e]) : max(wc[e] + 1, a[e]);
-            const int c0w = max(gc0 + 1, a[e]);
-            int n00 = W ? g00 + 1 : max(g00, g10 + 1);
-            int n01 = W ? g01 + 1 : max(g01, g11 + 1);
-            int n10 = W ? g00 + 1 : g10;
-            int n11 = W ? g01 + 1 : g11;
-            int nc0 = W ? c0w : max(max(gc0, gc1 + 1), a[e]);
-            int nc1 = W ? c0w : gc1;
-            n00 = H ? BL_NEG : n00;
-            n01 = H ? BL_NEG : n01;
-            n10 = H ? BL_NEG : n10;
-            n11 = H ? BL_NEG : n11;
-            nc0 = H ? max(yc[e], hx) : nc0;
-            nc1 = H ? (W ? hx : wc[e]) : nc1;
-            g00 = V ? n00 : g00; g01 = V ? n01 : g01; g10 = V ? n10 : g10;
-            g11 = V ? n11 : g11; gc0 = V ? nc0 : gc0; gc1 = V ? nc1 : gc1;
+            pre1[e] = r1;
+            const PK rv = wr[e] ? bz_pack<PK>(ep[e], -BZ_BIAS) : bz_pack<PK>(ep[e], hd[e] ? max(a[e], y0[e]) : a[e]);
+            r1 = r1 > rv ? r1 : rv;
         }
-        BlMap agg;
-        agg.a00 = g00; agg.a01 = g01; agg.a10 = g10; agg.a11 = g11; agg.c0 = gc0; agg.c1 = gc1;
-        agg.a00 = bl_clamp(agg.a00); agg.a01 = bl_clamp(agg.a01); agg.a10 = bl_clamp(agg.a10); agg.a11 = bl_clamp(agg.a11);
-        const BlMap inc = wave_incl_scan(op, agg);
-        const BlMap pre = wave_shift_up1(op, inc);
-        int y = max(pre.a00 - 1, max(pre.a01 - 1, pre.c0));
-        int w = max(pre.a10 - 1, max(pre.a11 - 1, pre.c1));
+        const PK in1 = wave_shift_up1(op, wave_incl_scan(op, r1));
+        // scan 2: z by run
+        PK r2 = 0, inc2[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const PK prev = in1 > pre1[e] ? in1 : pre1[e];         // the previous epoch's greatest Read value
+            const int d = (int)ds[e];
+            const int b = hd[e] ? max(a[e], y0[e] + 1) : max(a[e], bz_val<PK>(prev) + 1);
+            const int z = hd[e] ? (wr[e] ? max(w0[e] - d + 1, b - d) : w0[e] - d) : b - d;
+            const PK zv = (wr[e] || hd[e]) ? bz_pack<PK>(rn[e], z) : (PK)0;
+            r2 = r2 > zv ? r2 : zv;
+            inc2[e] = r2;
+        }
+        const PK in2 = wave_shift_up1(op, wave_incl_scan(op, r2));
         bool up = false;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            y = head[e] ? yc[e] : y;
-            w = head[e] ? wc[e] : w;
-            py[e] = y; pw[e] = w;
-            const int x = wr[e] ? max(y + 1, a[e]) : max(w + 1, a[e]);
-            if (x > a[e]) {                              // rare after the first round: the branch is skipped
+            const PK zm = in2 > inc2[e] ? in2 : inc2[e];
+            const int X = (int)ds[e] + bz_val<PK>(zm);
+            const int x = wr[e] ? X : max(a[e], X + 1);
+            if (x > a[e]) {                                  // rare after the first rounds
                 atomicMax(&lv[slot[e]], x);
                 up |= nl[slot[e]] != 0;
             }
-            y = max(y, x);
-            w = wr[e] ? x : w;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this round's raises before the next reads
         ++it;
         if (!__ballot(up)) break;
+        // each round finalises at least the lowest unfinished txn of the block: more rounds than txns + 1 is
+        // a broken invariant; stop (the host reports it) instead of spinning
+        if (it > (uint32_t)BL_CAP + 1) { *stuck = 1u; break; }
     }
+    // carry-out of the runs
+    PK ry = 0, rw = 0, iy[E], iw[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        if (!last[e]) continue;
         const int x = lv[slot[e]];
-        mout[lane * E + e] = make_int2(max(py[e], x), wr[e] ? x : pw[e]);
+        const int vy = hd[e] ? max(x, y0[e]) : x;
+        const int vw = wr[e] ? (hd[e] ? max(x, w0[e]) : x) : (hd[e] ? w0[e] : -BZ_BIAS);
+        const PK py = bz_pack<PK>(rn[e], vy), pw = bz_pack<PK>(rn[e], vw);
+        ry = ry > py ? ry : py;
+        rw = rw > pw ? rw : pw;
+        iy[e] = ry; iw[e] = rw;
+    }
+    const PK iny = wave_shift_up1(op, wave_incl_scan(op, ry));
+    const PK inw = wave_shift_up1(op, wave_incl_scan(op, rw));
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int k = lane * E + e;
+        if (k >= nm || !lst[e]) continue;
+        const uint4 c = cr[k];
+        const PK my = iny > iy[e] ? iny : iy[e], mw = inw > iw[e] ? inw : iw[e];
+        const int2 o = make_int2(bz_val<PK>(my), bz_val<PK>(mw));
+        ring[rb + (int)(c.y >> 22)] = o;
+        if ((c.x >> BL_SH_G) & 1u) {
+            int* g = reinterpret_cast<int*>(&carry[c.z]);
+            __hip_atomic_store(g, o.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(g + 1, o.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
     return it;
 }
 
-struct BlIntSum {
-    using S = int;
-    __device__ S identity() const { return 0; }
-    __device__ S combine(S a, S b) const { return a + b; }
-};
-
 // The sequential walk over the blocks (one workgroup; see the file header).  Per block:
-//   setup (all waves)  carry-in of the key runs that start here (LDS ring of the last three blocks'
-//                      carry-outs, else global memory), prefill of every txn's level with its heads' carry
-//                      bounds (a singleton run is then final), compaction of the multi-entry runs in block
-//                      order;
-//   rounds (wave 0)    bl_wave_rounds until no txn with a non-final entry rises; meanwhile waves 1-3 stage
-//                      the NEXT block's records, global carry-ins and order slice into LDS, so no global
-//                      load latency sits on the sequential path;
-//   out (all waves)    carry-out of every run (ring; global memory for keys whose next run is >= 3 blocks
-//                      away) and the levels.
+//   setup (all waves)  singleton runs (a key's only entry in the block): carry-in from the LDS ring of the last
+//                      three blocks' carry-outs or global memory, prefill of the txn's level with that bound (a
+//                      singleton is then final); wave 0 loads its compacted multi-entry run entries and their
+//                      heads' carry-ins and prefills those bounds;
+//   rounds (wave 0)    bl_rounds, whose end writes the multi-entry runs' carry-outs; meanwhile waves 1-3 stage
+//                      the NEXT block's records, compacted entries, global carry-ins and order slice into LDS, so
+//                      no global load latency sits on the sequential path;
+//   out (all waves)    carry-out of the singleton runs (ring; global memory for keys whose next run is >= 3
+//                      blocks away) and the levels.
 // Global carries are written and read by this one workgroup (one CU): workgroup-scope ordering suffices.  A
-// block's global stores are released (fence) at the end of the NEXT block, before that block's own stores,
-// and read no earlier than the staging during the block after that.
-// stats[0] = greatest level + 1, stats[1] = rounds, stats[2..3] = clock64 in rounds, stats[4..5] = total.
+// block's global stores are released (fence) at the end of the NEXT block, and read no earlier than the
+// staging during the block after that.
+// stats[0] = greatest level + 1, stats[1] = rounds, stats[2..3] = clock64 in rounds, stats[4..5] = total,
+// stats[6] = a block's rounds did not converge.
 __device__ inline void bl_stage(uint32_t b, uint32_t B, int t, int nthr, const uint32_t* __restrict__ boff,
-                                const uint32_t* __restrict__ tb, const uint64_t* __restrict__ rec, const int2* carry,
-                                const uint32_t* __restrict__ order, uint64_t* srec, int2* scar, uint32_t* sord, uint32_t* sbnd) {
+                                const uint32_t* __restrict__ tb, const uint64_t* __restrict__ rec, const uint4* __restrict__ crec,
+                                const uint32_t* __restrict__ mt, const int2* carry, const uint32_t* __restrict__ order,
+                                uint64_t* srec, int2* scar, uint32_t* sord, uint4* scr, int2* shc, uint32_t* sbnd) {
     if (b >= B) return;
-    const uint32_t j0 = boff[b], j1 = boff[b + 1], t0 = tb[b], t1 = tb[b + 1];
+    const uint32_t j0 = boff[b], j1 = boff[b + 1], t0 = tb[b], t1 = tb[b + 1], m = mt[b];
     for (int x = t; x < BL_CAP; x += nthr) {
         const uint32_t j = j0 + (uint32_t)x;
         const uint64_t r = j < j1 ? rec[j] : ~0ull;
         int2 c = make_int2(-1, -1);
-        if (r != ~0ull && (((uint32_t)(r >> 32) >> BL_SH_SRC) & 3u) == 2u) {
+        const uint32_t f = (uint32_t)(r >> 32);
+        // singleton heads' global carry-ins (the multi-entry runs' heads are staged with their compacted entries)
+        if (r != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) && ((f >> BL_SH_SRC) & 3u) == 2u) {
             const int* g = reinterpret_cast<const int*>(&carry[(uint32_t)r]);
             c.x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             c.y = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -278,34 +350,52 @@ __device__ inline void bl_stage(uint32_t b, uint32_t B, int t, int nthr, const u
         srec[x] = r;
         scar[x] = c;
         sord[x] = (uint32_t)x < t1 - t0 ? order[t0 + x] : 0u;
+        if ((uint32_t)x < m) {
+            const uint4 q = crec[j0 + x];
+            int2 h = make_int2(-1, -1);
+            if ((q.x >> BL_SH_HEAD) & 1u) {
+                const uint32_t src = (q.x >> BL_SH_SRC) & 3u;
+                if (src == 2u) {
+                    const int* g = reinterpret_cast<const int*>(&carry[q.z]);
+                    h.x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    h.y = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else if (src == 1u) {
+                    h.x = -2; h.y = (int)q.w;              // resolved from the ring at setup (ring index)
+                }
+            }
+            scr[x] = q;
+            shc[x] = h;
+        }
     }
-    if (t == 0) { sbnd[0] = j0; sbnd[1] = j1; sbnd[2] = t0; sbnd[3] = t1; }
+    if (t == 0) { sbnd[0] = j0; sbnd[1] = j1; sbnd[2] = t0; sbnd[3] = t1; sbnd[4] = m; }
 }
 
+template <class PK>
 static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const uint32_t* __restrict__ boff, const uint32_t* __restrict__ tb,
-                                                       const uint64_t* __restrict__ rec, int2* carry,
+                                                       const uint64_t* __restrict__ rec, const uint4* __restrict__ crec,
+                                                       const uint32_t* __restrict__ mt, int2* carry,
                                                        const uint32_t* __restrict__ order, uint32_t* __restrict__ L,
                                                        uint32_t* __restrict__ stats) {
     __shared__ int lvb[2][BL_CAP + WAVE];      // levels of the block's txns (txn-in-block index), by block parity;
                                                // [BL_CAP + lane]: sinks of the rounds' absent entries
     __shared__ uint8_t nlb[2][BL_CAP + WAVE];     // txn has an entry that is not its key's last in the block
     __shared__ int2 ring[3 * BL_CAP];          // carry-out of every slot of the last three blocks
-    __shared__ uint32_t mfl[BL_CAP];           // compacted multi-entry runs: record flags
-    __shared__ int2 mcar[BL_CAP];              //   carry-in (heads)
-    __shared__ int2 mout[BL_CAP];              //   carry-out (LAST entries)
-    __shared__ uint64_t srec[BL_CAP];          // staged next block: records, global carry-ins, order slice
+    __shared__ uint4 scrb[2][BL_CAP];          // compacted multi-entry run entries (by block parity: the next
+    __shared__ int2 shcb[2][BL_CAP];           //   block's are staged while this one's rounds run), their heads'
+                                               //   carry-ins (-2: from the ring); staged next block:
+    __shared__ uint64_t srec[BL_CAP];          //   records, singleton global carry-ins, order slice
     __shared__ int2 scar[BL_CAP];
     __shared__ uint32_t sord[BL_CAP];
-    __shared__ uint32_t sbnd[4];
-    __shared__ int sred[BL_T / WAVE];
-    __shared__ uint32_t srounds;
+    __shared__ uint32_t sbnd[5];
+    __shared__ uint32_t sstuck;
     const int tid = threadIdx.x, lane = __lane_id();
+    if (tid == 0) sstuck = 0u;
     const uint64_t tstart = clock64();
     uint64_t tround = 0;
     for (int x = tid; x < BL_CAP + WAVE; x += BL_T) { lvb[0][x] = lvb[1][x] = 0; nlb[0][x] = nlb[1][x] = 0; }
     int maxl = -1;
     uint32_t rounds = 0;
-    bl_stage(0, B, tid, BL_T, boff, tb, rec, carry, order, srec, scar, sord, sbnd);
+    bl_stage(0, B, tid, BL_T, boff, tb, rec, crec, mt, carry, order, srec, scar, sord, scrb[0], shcb[0], sbnd);
     uint32_t pfl[BL_EPT];
 #pragma unroll
     for (int e = 0; e < BL_EPT; ++e) pfl[e] = BL_NONE;
@@ -314,7 +404,11 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         const int pb = b & 1;
         int* lv = lvb[pb];
         uint8_t* nl = nlb[pb];
+        uint4* scr = scrb[pb];
+        int2* shc = shcb[pb];
         const uint32_t nt = sbnd[3] - sbnd[2];
+        const int nm = (int)sbnd[4];
+        const int rb = (int)(b % 3) * BL_CAP;
         uint32_t fl[BL_EPT], key[BL_EPT], ord[BL_EPT];
         int yc[BL_EPT], wc[BL_EPT];
 #pragma unroll
@@ -326,17 +420,16 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
             yc[e] = c.x; wc[e] = c.y;
             ord[e] = sord[tid + e * BL_T];
         }
-        // ---- setup: clear the previous block's slots (other parity), carry-in, prefill, compaction
+        // ---- setup: clear the previous block's slots (other parity); singleton carry-in + prefill; nl
 #pragma unroll
         for (int e = 0; e < BL_EPT; ++e)
             if (pfl[e] != BL_NONE) { lvb[pb ^ 1][pfl[e] & BL_TL] = 0; nlb[pb ^ 1][pfl[e] & BL_TL] = 0; }
-        int mcount = 0;
 #pragma unroll
         for (int e = 0; e < BL_EPT; ++e) {
             const uint32_t f = fl[e];
             if (f == BL_NONE) continue;
             const bool head = f & (1u << BL_SH_HEAD), last = f & (1u << BL_SH_LAST);
-            if (head) {
+            if (head && last) {
                 const uint32_t src = (f >> BL_SH_SRC) & 3u;
                 if (src == 0u) { yc[e] = -1; wc[e] = -1; }
                 else if (src == 1u) { const int2 c = ring[f >> BL_SH_RING]; yc[e] = c.x; wc[e] = c.y; }
@@ -344,71 +437,59 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
                 if (lb > 0) atomicMax(&lv[f & BL_TL], lb);
             }
             if (!last) nl[f & BL_TL] = 1;
-            mcount += (head && last) ? 0 : 1;
         }
-        int mtotal;
-        const int mbase = block_exclusive_scan<BlIntSum, BL_T>(BlIntSum{}, mcount, sred, &mtotal);
-        {
-            int k = mbase;
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                const uint32_t f = fl[e];
-                if (f == BL_NONE || ((f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)))) continue;
-                mfl[k] = f;
-                mcar[k] = make_int2(yc[e], wc[e]);
-                ++k;
+        // wave 0: the multi-entry runs' heads: carry-in (ring sources resolved here) and prefill
+        if (tid < WAVE) {
+            for (int k = lane; k < nm; k += WAVE) {
+                const uint4 q = scr[k];
+                if (!((q.x >> BL_SH_HEAD) & 1u)) continue;
+                int2 h = shc[k];
+                if ((q.x >> BL_SH_SRC & 3u) == 0u) h = make_int2(-1, -1);
+                else if (h.x == -2) h = ring[h.y];
+                shc[k] = h;
+                const int lb = ((q.x >> BL_SH_W) & 1u) ? h.x + 1 : h.y + 1;
+                if (lb > 0) atomicMax(&lv[q.x & BL_TL], lb);
             }
         }
         __syncthreads();
         // ---- rounds (wave 0) | staging of the next block (waves 1-3)
         if (tid < WAVE) {
-            if (mtotal > 0) {
+            if (nm > 0) {
                 const uint64_t t0 = clock64();
                 uint32_t r;
-                const int epl = (mtotal + WAVE - 1) / WAVE;        // entries per lane
-                if (epl <= 2) r = bl_wave_rounds<2>(mtotal, mfl, mcar, lv, nl, mout);
-                else if (epl <= 3) r = bl_wave_rounds<3>(mtotal, mfl, mcar, lv, nl, mout);
-                else if (epl <= 4) r = bl_wave_rounds<4>(mtotal, mfl, mcar, lv, nl, mout);
-                else if (epl <= 5) r = bl_wave_rounds<5>(mtotal, mfl, mcar, lv, nl, mout);
-                else if (epl <= 6) r = bl_wave_rounds<6>(mtotal, mfl, mcar, lv, nl, mout);
-                else if (epl <= 8) r = bl_wave_rounds<8>(mtotal, mfl, mcar, lv, nl, mout);
-                else if (epl <= 12) r = bl_wave_rounds<12>(mtotal, mfl, mcar, lv, nl, mout);
-                else r = bl_wave_rounds<16>(mtotal, mfl, mcar, lv, nl, mout);
+                const int epl = (nm + WAVE - 1) / WAVE;        // entries per lane
+                if (epl <= 2) r = bl_rounds<2, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 3) r = bl_rounds<3, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 4) r = bl_rounds<4, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 5) r = bl_rounds<5, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 6) r = bl_rounds<6, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 8) r = bl_rounds<8, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 12) r = bl_rounds<12, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
+                else r = bl_rounds<16, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
                 tround += clock64() - t0;
                 rounds += r;
             }
         } else {
-            bl_stage(b + 1, B, tid - WAVE, BL_T - WAVE, boff, tb, rec, carry, order, srec, scar, sord, sbnd);
+            bl_stage(b + 1, B, tid - WAVE, BL_T - WAVE, boff, tb, rec, crec, mt, carry, order, srec, scar, sord, scrb[pb ^ 1],
+                     shcb[pb ^ 1], sbnd);
         }
         __syncthreads();
-        // ---- out: carry-out of every run's LAST entry, levels.  The fence first releases the previous
-        // block's global carries (issued a block ago) before this block's are issued.
+        // ---- out: carry-out of the singleton runs, levels.  The fence first releases the previous block's
+        // global carries (issued a block ago) before this block's are issued.
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        const int rb = (int)(b % 3) * BL_CAP;
-        {
-            int k = mbase;
 #pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                const uint32_t f = fl[e];
-                if (f == BL_NONE) continue;
-                const bool head = f & (1u << BL_SH_HEAD), last = f & (1u << BL_SH_LAST);
-                const bool multi = !(head && last);
-                if (last) {
-                    int2 c;
-                    if (multi) {
-                        c = mout[k];
-                    } else {
-                        const int x = lv[f & BL_TL];
-                        c = make_int2(max(yc[e], x), (f & (1u << BL_SH_W)) ? x : wc[e]);
-                    }
-                    ring[rb + tid * BL_EPT + e] = c;
-                    if (f & (1u << BL_SH_G)) {
-                        int* g = reinterpret_cast<int*>(&carry[key[e]]);
-                        __hip_atomic_store(g, c.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_store(g + 1, c.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
+        for (int e = 0; e < BL_EPT; ++e) {
+            const uint32_t f = fl[e];
+            if (f == BL_NONE) continue;
+            if ((f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST))) {
+                const int x = lv[f & BL_TL];
+                const int2 c = make_int2(max(yc[e], x), (f & (1u << BL_SH_W)) ? x : wc[e]);
+                ring[rb + tid * BL_EPT + e] = c;
+                if (f & (1u << BL_SH_G)) {
+                    int* g = reinterpret_cast<int*>(&carry[key[e]]);
+                    __hip_atomic_store(g, c.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(g + 1, c.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                if (multi) ++k;
             }
         }
 #pragma unroll
@@ -423,6 +504,7 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
 #pragma unroll
         for (int e = 0; e < BL_EPT; ++e) pfl[e] = fl[e];
         __syncthreads();
+        if (sstuck) break;
     }
     maxl = wave_max(maxl);
     if (lane == 0) atomicMax(&stats[0], (uint32_t)(maxl + 1));
@@ -431,20 +513,22 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         const uint64_t tot = clock64() - tstart;
         stats[2] = (uint32_t)tround; stats[3] = (uint32_t)(tround >> 32);
         stats[4] = (uint32_t)tot; stats[5] = (uint32_t)(tot >> 32);
+        stats[6] = sstuck;
     }
 }
 
 struct BlockBufs {                             // grow-only, owned by LevelState
     uint64_t* rec = nullptr;                   // [P]
     uint32_t *epre = nullptr, *erank = nullptr, *bk = nullptr, *bv = nullptr, *bk2 = nullptr, *bv2 = nullptr;
-    uint32_t *tb = nullptr, *boff = nullptr, *stats = nullptr, *rs = nullptr;
+    uint32_t *tb = nullptr, *boff = nullptr, *stats = nullptr, *rs = nullptr, *mt = nullptr;
     int2* carry = nullptr;
+    uint4* crec = nullptr;                     // [P] compacted multi-entry run entries (k_bl_compact)
     size_t capP = 0, capN = 0, capB = 0, rs_cap = 0;
     uint32_t nblocks = 0;                      // blocks of the last run
 };
 
 inline void free_block_bufs(BlockBufs& b) {
-    void* ps[] = {b.rec, b.epre, b.erank, b.bk, b.bv, b.bk2, b.bv2, b.tb, b.boff, b.stats, b.rs, b.carry};
+    void* ps[] = {b.rec, b.epre, b.erank, b.bk, b.bv, b.bk2, b.bv2, b.tb, b.boff, b.stats, b.rs, b.carry, b.crec, b.mt};
     for (void* p : ps) if (p) hipFree(p);
     b = BlockBufs{};
 }

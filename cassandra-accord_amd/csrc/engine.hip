@@ -1359,7 +1359,7 @@ const char* ad_kernel_name(int kid) { return kernel_name(kid); }
 
 int ad_set_level_mode(ad_handle* h, int mode) {
     if (!h || (mode != AD_LEVELS_AUTO && mode != AD_LEVELS_FIXPOINT && mode != AD_LEVELS_BLOCKS && mode != AD_LEVELS_KAHN &&
-               mode != AD_LEVELS_PULL_ABORT))
+               mode != AD_LEVELS_PULL_ABORT && mode != AD_LEVELS_BLOCKS_WIDE))
         return AD_ERR_ARGUMENT;
     h->level_mode = mode;
     return AD_OK;

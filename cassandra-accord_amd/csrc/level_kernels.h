@@ -1471,6 +1471,7 @@ struct LevelInputs {
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
     int force_blocks;                    // pure key-chain batches: executeAt blocks even for short chains (tests)
+    int wide_words;                      // block path: 64-bit scan words even for batches of <= 2^20 txns (tests)
     int (*complete)(void*);              // nullable: fills in every sorted entry before a path other than the pull pass
     void* complete_ctx;
     uint32_t* order_verify;              // optimistic order: host-mapped word (device address) receiving the fast-path
@@ -1647,7 +1648,8 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
     if (bb.capP < P || !bb.rec) {
         const size_t c = std::max<size_t>(P, 1);
         if (!grow((void**)&bb.rec, c * 8) || !grow((void**)&bb.bk, c * 4) || !grow((void**)&bb.bv, c * 4) ||
-            !grow((void**)&bb.bk2, c * 4) || !grow((void**)&bb.bv2, c * 4) || !grow((void**)&bb.carry, c * 8))
+            !grow((void**)&bb.bk2, c * 4) || !grow((void**)&bb.bv2, c * 4) || !grow((void**)&bb.carry, c * 8) ||
+            !grow((void**)&bb.crec, c * 16))
             goto oom;
         bb.capP = c;
     }
@@ -1658,7 +1660,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
     }
     if (bb.capB < Bmax + 1 || !bb.tb) {
         const size_t c = Bmax + 1;
-        if (!grow((void**)&bb.tb, c * 4) || !grow((void**)&bb.boff, c * 4)) goto oom;
+        if (!grow((void**)&bb.tb, c * 4) || !grow((void**)&bb.boff, c * 4) || !grow((void**)&bb.mt, c * 4)) goto oom;
         bb.capB = c;
     }
     if (!bb.stats && !grow((void**)&bb.stats, 64)) goto oom;
@@ -1713,16 +1715,24 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         k_bl_inverse<<<gP, 256, 0, st>>>(P, sv, inv);
         k_bl_records<<<gP, 256, 0, st>>>(P, sk, sv, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.epre, bcap, bb.tb,
                                          bb.boff, bb.rec, bb.stats + 3);
-        // 4. the walk
+        k_bl_compact<<<nb, BL_T, 0, st>>>(nb, bb.boff, bb.rec, bb.crec, bb.mt);
+        // 4. the walk (packed scan words: 32-bit while every level fits 20 bits)
         hipMemsetAsync(bb.carry, 0xFF, P * 8, st);
-        k_level_blocks<<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.carry, in.order, in.lvl, bb.stats);
-        uint32_t s4[4] = {0, 0, 0, 0};
-        if (hipMemcpyAsync(s4, bb.stats, 16, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        if (n <= (1u << 20) && !in.wide_words)
+            k_level_blocks<uint32_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.carry, in.order, in.lvl, bb.stats);
+        else
+            k_level_blocks<uint64_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.carry, in.order, in.lvl, bb.stats);
+        uint32_t s4[7] = {0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyAsync(s4, bb.stats, 28, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
             err = "exec levels: device error";
             return AD_ERR_DEVICE;
         }
         if (s4[3]) {
             err = "exec levels: block layout invariant violated (txn index beyond the block)";
+            return AD_ERR_STATE;
+        }
+        if (s4[6]) {
+            err = "exec levels: a block's rounds did not converge";
             return AD_ERR_STATE;
         }
         *depth = (int)s4[0];

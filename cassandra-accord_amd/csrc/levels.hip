@@ -48,7 +48,8 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.n_special = h->n_special;
     li.exec_bits = h->pack.total_bits;
     li.kahn_ok = h->level_mode != AD_LEVELS_FIXPOINT ? 1 : 0;
-    li.force_blocks = h->level_mode == AD_LEVELS_BLOCKS ? 1 : 0;
+    li.force_blocks = (h->level_mode == AD_LEVELS_BLOCKS || h->level_mode == AD_LEVELS_BLOCKS_WIDE) ? 1 : 0;
+    li.wide_words = h->level_mode == AD_LEVELS_BLOCKS_WIDE ? 1 : 0;
     h->ls.pull_off = h->level_mode == AD_LEVELS_KAHN;
     h->ls.pull_force_abort = h->level_mode == AD_LEVELS_PULL_ABORT;
     h->ls.bl_rounds = 0;

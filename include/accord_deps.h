@@ -351,8 +351,8 @@ int  ad_last_times(ad_handle* h, ad_stage_times* out);
 /* Execution-level algorithm (all give identical levels; the choice only affects speed):
  * AD_LEVELS_AUTO (default): batches with only key Read/Write txns (no direct/range deps, no range txns) use
  * one-pass pull levels (each txn publishes 1 + its predecessors' maximum once they are final, one launch)
- * while every key chain is short, and executeAt blocks (block_levels.h: one LDS max-plus scan fixpoint per
- * block, walked in executeAt order) when some chain is long (deep graphs: Zipf hot keys); mixed batches use
+ * while every key chain is short, and executeAt blocks (block_levels.h: a Jacobi fixpoint of write-epoch max
+ * scans per block, walked in executeAt order) when some chain is long (deep graphs: Zipf hot keys); mixed batches use
  * the Kahn wavefront (each txn visited once, when released) with explicit (b)/(c) edges.
  * AD_LEVELS_FIXPOINT always uses the chain fixpoint; AD_LEVELS_BLOCKS uses the executeAt blocks for every
  * key-only batch; AD_LEVELS_KAHN uses the Kahn wavefront instead of the pull levels (tests cross-check the
@@ -362,6 +362,7 @@ int  ad_last_times(ad_handle* h, ad_stage_times* out);
 #define AD_LEVELS_BLOCKS 2
 #define AD_LEVELS_KAHN 3
 #define AD_LEVELS_PULL_ABORT 4      /* tests: the pull levels abort at once, the Kahn wavefronts recompute the batch */
+#define AD_LEVELS_BLOCKS_WIDE 5     /* tests: AD_LEVELS_BLOCKS with the 64-bit scan words batches of > 2^20 txns use */
 int  ad_set_level_mode(ad_handle* h, int mode);
 
 /* Per-kernel HIP-event timing (trace mode).  mask bit k enables kernel id k (0 <= k < ad_kernel_count()); the

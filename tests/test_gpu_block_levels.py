@@ -56,6 +56,14 @@ def test_blocks_configs(engine_factory, name, n):
     check_levels(engine_factory, workload.config(name, n=n))
 
 
+@pytest.mark.parametrize("name,n", [("C3", 200000), ("C3", 20000)])
+def test_blocks_wide_scan_words(engine_factory, name, n):
+    # the 64-bit packed scan words batches of more than 2^20 txns use (LEVELS_BLOCKS_WIDE forces them here)
+    check_levels(engine_factory, workload.config(name, n=n), mode=engine.DepsEngine.LEVELS_BLOCKS_WIDE)
+    check_levels(engine_factory, workload.generate(4000, keys_per_txn=4, keyspace=40, seed=7),
+                 mode=engine.DepsEngine.LEVELS_BLOCKS_WIDE)
+
+
 @pytest.mark.parametrize("keyspace,n", [(300, 5000), (40, 3000), (4000, 20000), (3, 2000)])
 def test_blocks_dense_keyspaces(engine_factory, keyspace, n):
     # very deep graphs: every block is one or a few long key runs coupled by every txn
