@@ -91,7 +91,7 @@ def test_refusals(engine_factory):
     unsorted = K.pack_states([[(b, K.KEY, K.PREACC, b, []), (a, K.KEY, K.PREACC, a, [])]])
     with pytest.raises(engine.AccordDepsError) as e:
         eng.cfk_notify(unsorted)
-    assert e.value.args[0] == abi.AD_ERR_UNSORTED
+    assert e.value.rc == abi.AD_ERR_UNSORTED
     bad = K.pack_states([[(a, K.KEY, K.PREACC, a, []), (b, K.KEY, K.STABLE, K.ts_from_values(1, 30, 1), [5])]])
     with pytest.raises(engine.IllegalArgumentException):
         eng.cfk_notify(bad)
