@@ -13,9 +13,10 @@ N > 1 (configs[4], C5, weak scaling): a global batch of N x 2,097,152 txns of C5
   CommandStore per GPU, ShardDistributor.EvenSplit).  Most txns span several stores, so each step is the full
   cross-shard protocol (accord_amd.sharding.run_store): local deps on the store's slice, export, all-to-all of the
   per-destination fragments over RCCL/xGMI, merge of the fragments of the store's home txns (PreAccept.reduce) and
-  across replica views (Deps.merge), then the execution levels by the protocol sharding.choose_levels picks:
-  distributed delta rounds (each store relaxes only its own key chains; only raised levels of txns another store
-  holds travel) for shallow graphs like C5's, or one exchange of every store's constraint edges for deep ones.
+  across replica views (Deps.merge), then the execution levels by sharding.run_store's "auto" protocol:
+  distributed Kahn waves for shallow graphs like C5's (each store walks only its own constraint edges; a txn
+  costs one READY and one RELEASE message per holder), or one exchange of every store's constraint edges for deep
+  ones.
 
 Timing: W untimed warmup steps; then barrier + device sync, K timed steps, device sync + barrier,
 max over ranks.  The HIP work runs on the engine's own stream; every step ends synchronised on it, so
@@ -40,7 +41,7 @@ WINDOW, REPLICAS, DROP_P = 32, 3, 0.1
 KEYSPACE = 10_000_000
 
 
-def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
+def alg_bytes(kernel, calls, units, n, P, R, st, large=False, steps=1):
     """Algorithmic HBM bytes moved by all traced launches of `kernel` (DESIGN.md §3 lists the per-unit
     figures): the minimum bytes the kernel must read + write for the elements it processed.  `units` is the
     sum of elements over the launches (pairs, txns, sort items or output rows, recorded per launch by the
@@ -48,7 +49,9 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
     Every kernel the C2 / C3 pipelines trace has a model, so the roofline kernel is the one with the most
     time.  With large txns (range txns, C4) the run's entry count D also holds the entries of the
     virtual-item walks and the LDS unions, so the D-based models of k_txn_union / k_deps_walk<fill> /
-    k_merge would overcount: those return None there (not candidates)."""
+    k_merge would overcount: those return None there (not candidates), and the large-txn regions (vitems,
+    k_range_deps, k_union_lds) get per-step models from the step's counts instead, times `steps` (the pipeline
+    steps the launches span)."""
     D = st["deps_entries"]           # emitted dependency entries over all views/classes
     M = st["merged_entries"]         # entries of the merged Deps
     W = st["walk_items"]             # entries the deps walks visit
@@ -89,8 +92,20 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False):
         # window rank (12 B in, 16 B out), check (16 B), one level radix pass (4 + 16 B), order out (4 B)
         "order_sort": units * 68,
     }
-    if large and kernel in ("k_txn_union", "k_deps_walk<fill>", "k_merge<count>", "k_merge<write>"):
-        return None
+    if large:
+        # large-txn regions (C4), lower bounds from the step's counts: V virtual items, Dr RangeDeps entries.
+        # vitems: each item record (12 B: txn, insert position, key index) + its C count / slot words written by
+        # the item pass, read + written by the count walk, read by the fill walk (the entries it visits are not
+        # counted); k_range_deps: every RangeDeps entry visited by the count and the fill pass (21 B: start, end,
+        # owner, meta, executeAt) and written once (4 B); k_union_lds: 12 B per unioned entry (read the per-key id,
+        # write the keysToTxnIds index and the TxnId), priced on every entry of the step (the small txns'
+        # share, unioned in registers by k_txn_finish, is < 2 % on C4).
+        V, Dr = st.get("vitems", 0), st.get("range_entries", 0)
+        per["vitems"] = steps * V * 3 * (12 + 4 * C)
+        per["k_range_deps"] = steps * Dr * (2 * 21 + 4)
+        per["k_union_lds"] = steps * 12 * D
+        if kernel in ("k_txn_union", "k_deps_walk<fill>", "k_merge<count>", "k_merge<write>"):
+            return None
     return per.get(kernel)
 
 
@@ -268,11 +283,11 @@ def trace_roofline(eng, run_step, n, P, large=False):
     return dom, brk, st
 
 
-def roofline_of(eng, dom, n, P, st, large=False, pmc=True):
+def roofline_of(eng, dom, n, P, st, large=False, pmc=True, steps=1):
     """achieved = the dominant kernel's algorithmic bytes over its launches in the timed region / its summed
     HIP-event time (events on the engine stream, bracketing only this kernel)."""
     calls, ms, units = eng.kernel_stats()[dom]
-    ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st, large)
+    ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st, large, steps)
     achieved = ab / (ms * 1e-3) / 1e9
     # the committed PMC passes (profiles/collect.sh) run the default C2 bench: other configs report no traffic
     traffic, src = pmc_traffic(dom) if pmc else (None, None)
@@ -457,8 +472,9 @@ def main_sharded(args, rank, world, local, dist):
     dt = float(t.item())
     roof = roofline_of(store.eng, dom, n_loc, P_loc, store.eng.last_times(), pmc=False)
     store.eng.set_trace(0)
-    protocol = ("delta rounds (each store relaxes its own key chains; raised levels of shared txns travel)"
-                if rounds <= sharding.AUTO_ROUND_CAP else "one exchange of every store's constraint edges")
+    protocol = ("distributed Kahn waves (each store walks only its own constraint edges; per txn one READY and one "
+                "RELEASE message per holder)" if rounds <= sharding.AUTO_ROUND_CAP
+                else "one exchange of every store's constraint edges")
     out = {
         "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
         "value": n_total * args.steps / dt, "unit": "txn/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -471,8 +487,7 @@ def main_sharded(args, rank, world, local, dist):
                    "keys_per_txn": 4, "keyspace": KEYSPACE, "replicas": REPLICAS, "window": WINDOW,
                    "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds,
                    "level_protocol": protocol,
-                   "level_exchange_bytes_rank0": 8 * store.pairs_sent,
-                   "level_exchange_bytes_dense": 4 * (n_total + 1) * rounds,
+                   "level_exchange_bytes_rank0": getattr(store, "kahn_bytes", 8 * store.pairs_sent),
                    "phase_ms_rank0": {k: round(v * 1e3 / args.steps, 3) for k, v in phases.items()}},
         "roofline": roof,
         "cpu_baseline": None,
@@ -541,7 +556,7 @@ def main():
     dt = t1 - t0
     st = eng.last_times()
     warn_level_fallback(st)
-    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc=cfgname == "C2")
+    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc=cfgname == "C2", steps=args.steps)
     mc = None
     if Q == 0:
         # side measurement, outside the timed region: the witnessedAt proposal (ad_max_conflicts) on the same

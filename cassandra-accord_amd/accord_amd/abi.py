@@ -99,7 +99,8 @@ class AdStageTimes(C.Structure):
                 ("level_blocks", C.c_uint32), ("level_rounds", C.c_uint32),
                 ("key_classes", C.c_uint32), ("level_path", C.c_uint32),
                 ("deferred_txns", C.c_uint32), ("fill_items", C.c_uint32),
-                ("deps_speculative", C.c_uint32)]
+                ("deps_speculative", C.c_uint32),
+                ("vitems", C.c_uint64), ("range_entries", C.c_uint64)]
 
 
 def ptr(a, ctype):

@@ -244,6 +244,13 @@ class ShardStore:
         L.ad_shard_level_edges.argtypes = [vp, C.POINTER(C.c_size_t), u64p]
         L.ad_shard_levels_solve.argtypes = [vp, u64p, C.c_size_t, C.POINTER(C.c_uint32)]
         L.ad_shard_levels_gather.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.ad_shard_kahn_begin.argtypes = [vp]
+        L.ad_shard_kahn_outbox.argtypes = [vp, C.POINTER(C.c_uint32), u64p]
+        L.ad_shard_kahn_inbox.argtypes = [vp, u64p, C.c_size_t]
+        L.ad_shard_kahn_exchange.argtypes = [vp, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.ad_shard_kahn_decide.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.ad_shard_kahn_apply.argtypes = [vp, C.c_uint32, C.POINTER(C.c_uint64)]
+        L.ad_shard_kahn_sent.argtypes = [vp, C.POINTER(C.c_uint64)]
         self.delta = False
         self.pairs_sent = 0
 
@@ -420,6 +427,48 @@ class ShardStore:
         self._check(self.L.ad_shard_levels_gather(self.eng.h, C.byref(d)), "ad_shard_levels_gather")
         return d.value
 
+    # ---- distributed Kahn waves (levels="kahn"; ad_shard_kahn_*)
+    def kahn_begin(self):
+        """The store's local constraint graph and wave 0's READY messages (needs holder masks)."""
+        self._check(self.L.ad_shard_kahn_begin(self.eng.h), "ad_shard_kahn_begin")
+
+    def kahn_outbox(self):
+        """The current phase's messages per destination: (counts[world], messages in destination order)."""
+        cnt = np.zeros(self.world, np.uint32)
+        self._check(self.L.ad_shard_kahn_outbox(self.eng.h, _u32p(cnt), None), "ad_shard_kahn_outbox")
+        msgs = np.zeros(max(int(cnt.sum()), 1), np.uint64)
+        self._check(self.L.ad_shard_kahn_outbox(self.eng.h, _u32p(cnt), msgs.ctypes.data_as(C.POINTER(C.c_uint64))),
+                    "ad_shard_kahn_outbox")
+        return cnt, msgs[:int(cnt.sum())]
+
+    def kahn_inbox(self, msgs):
+        m = np.ascontiguousarray(msgs, np.uint64)
+        self._check(self.L.ad_shard_kahn_inbox(self.eng.h, m.ctypes.data_as(C.POINTER(C.c_uint64)) if m.size else None,
+                                               m.size), "ad_shard_kahn_inbox")
+
+    def kahn_exchange(self, status):
+        """RCCL: the outbox to the peers, theirs into the inbox; returns whether some store's status was set."""
+        a = C.c_uint32()
+        self._check(self.L.ad_shard_kahn_exchange(self.eng.h, 1 if status else 0, C.byref(a)), "ad_shard_kahn_exchange")
+        return bool(a.value)
+
+    def kahn_decide(self):
+        """Home store: READYs counted, complete txns released (RELEASE outbox); returns whether it released any."""
+        r = C.c_uint32()
+        self._check(self.L.ad_shard_kahn_decide(self.eng.h, C.byref(r)), "ad_shard_kahn_decide")
+        return bool(r.value)
+
+    def kahn_apply(self, level):
+        """Every holder: RELEASEs get `level`, successors' READYs fill the outbox; returns the rows still unreleased."""
+        u = C.c_uint64()
+        self._check(self.L.ad_shard_kahn_apply(self.eng.h, level, C.byref(u)), "ad_shard_kahn_apply")
+        return u.value
+
+    def kahn_sent(self):
+        s_ = C.c_uint64()
+        self._check(self.L.ad_shard_kahn_sent(self.eng.h, C.byref(s_)), "ad_shard_kahn_sent")
+        return s_.value
+
     def order(self):
         lv = np.zeros(max(self.n_home, 1), np.uint32)
         od = np.zeros(max(self.n_home, 1), np.uint32)
@@ -523,6 +572,18 @@ class GlooTransport:
         return self.any(changed)
 
 
+    def kahn_exchange(self, store, status):
+        """One Kahn phase: every store's outbox to its destinations (all-to-all), the received messages into the
+        inbox; returns whether some store's status was set (the wave released something)."""
+        cnt, msgs = store.kahn_outbox()
+        rcnt = self.recv_sizes(cnt.astype(np.uint64))
+        recv = self.torch.zeros(int(rcnt.sum()), dtype=self.torch.int64)
+        self.dist.all_to_all_single(recv, self.torch.from_numpy(msgs.view(np.int64).copy()),
+                                    output_split_sizes=[int(x) for x in rcnt], input_split_sizes=[int(x) for x in cnt])
+        store.kahn_inbox(recv.numpy().view(np.uint64))
+        return self.any(status)
+
+
 class RcclUnavailable(RuntimeError):
     """RCCL cannot be used by this group (decided identically on every rank, before any collective RCCL call)."""
 
@@ -585,6 +646,9 @@ class RcclTransport(GlooTransport):
             return store.levels_exchange()   # counts all-gather + pair send/recv, all over RCCL
         return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
+    def kahn_exchange(self, store, status):
+        return store.kahn_exchange(status)   # counts + status all-gather, grouped send/recv, all over RCCL
+
 
 class LevelsNotConverged(RuntimeError):
     """The distributed level rounds hit their cap while some store still raised a level: the levels are not
@@ -595,14 +659,16 @@ AUTO_ROUND_CAP = 128
 
 
 def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="auto", round_cap=AUTO_ROUND_CAP):
-    """The per-store protocol after load(): returns the number of level exchanges.
+    """The per-store protocol after load(): returns the number of level exchanges (waves / rounds).
+    levels="kahn": distributed Kahn waves (run_levels_kahn; holder masks needed): per txn one READY and one RELEASE
+      message per holder over the whole batch, each store touching only its own constraint edges.
     levels="rounds": the per-round delta (holders set) / dense exchange, each store relaxing only its own key chains;
       raises LevelsNotConverged if the rounds reach max_rounds while levels are still changing.
     levels="gather": one exchange of every store's constraint edges, every store solving their union (returns 1).
-    levels="auto" (default): delta rounds while they converge within round_cap rounds — per-store work and exchange
-      volume independent of the store count, rounds ~ the graph's depth (C5: tens) — else, every store agreeing (the
-      round flag is global), the one-exchange gather for the deep graph (C3-like hot keys: ~10^5 levels); without
-      holder masks the gather.  Returns round_cap + 1 when it fell back.
+    levels="auto" (default): the Kahn waves while the graph is shallow (at most round_cap waves: C5 takes ~60),
+      else -- every store sees the same global release flag, so all switch together -- the one-exchange gather for
+      deep graphs (C3-like hot keys: ~10^5 levels, one wave each); without holder masks the gather.  Returns
+      round_cap + 1 when it fell back.
     timings (dict, optional) accumulates wall seconds per phase (each phase ends synchronised)."""
     import time
     clock = time.perf_counter
@@ -628,20 +694,50 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="auto",
         store.depth = transport.gather_levels(store)
         lap("levels")
         return 1
+    if levels == "kahn":
+        return run_levels_kahn(store, transport, None, lap)
     return run_levels(store, transport, max_rounds, lap)
 
 
 def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
-    """levels="auto" of run_store: the delta rounds, or — when they have not converged after round_cap rounds (every
-    store sees the same global round flag, so all switch together) — the one-exchange gather, which recomputes the
-    levels from every store's constraint edges.  Returns the rounds, or round_cap + 1 after the fallback."""
+    """levels="auto" of run_store: the Kahn waves, or -- when the graph is deeper than round_cap waves (every store
+    sees the same global release flag, so all switch together) -- the one-exchange gather, which recomputes the
+    levels from every store's constraint edges.  Returns the waves, or round_cap + 1 after the fallback."""
     lap = lap or (lambda name: None)
     try:
-        return run_levels(store, transport, round_cap, lap)
+        return run_levels_kahn(store, transport, round_cap, lap)
     except LevelsNotConverged:
         store.depth = transport.gather_levels(store)
         lap("levels_gather")
         return round_cap + 1
+
+
+def run_levels_kahn(store, transport, wave_cap=None, lap=None):
+    """Distributed Kahn waves (ad_shard_kahn_*, csrc/kahn_shard_kernels.h): wave l moves the READYs of the rows whose
+    local predecessors are all released to their home stores, the home stores release the txns every holder
+    reported (level l) and send RELEASE to the holders, which record the level and free their successors.  Stops
+    after the first wave that released nothing anywhere; raises LevelsNotConverged past wave_cap waves (all stores
+    together).  Sets store.depth and store.kahn_bytes (8 B per message sent to another store); returns the waves."""
+    lap = lap or (lambda name: None)
+    store.kahn_begin()
+    lap("levels_local")
+    level = 0
+    while True:
+        transport.kahn_exchange(store, False)              # READYs -> home stores
+        rel = store.kahn_decide()
+        any_rel = transport.kahn_exchange(store, rel)      # RELEASEs -> holders; status: this store released some
+        unreleased = store.kahn_apply(level)
+        if not any_rel:
+            break
+        level += 1
+        if wave_cap is not None and level >= wave_cap:
+            raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
+    lap("levels_waves")
+    if unreleased:
+        raise engine.AccordDepsError(abi.AD_ERR_ARGUMENT, "Kahn waves: %d rows never released (a cycle)" % unreleased)
+    store.depth = level
+    store.kahn_bytes = 8 * store.kahn_sent()
+    return level + 1
 
 
 def run_levels(store, transport, max_rounds=1 << 16, lap=None):
@@ -701,14 +797,20 @@ class LocalTransport:
             lap("home_merge")
         if levels is None:
             return 0
+        fell_back = False
+        if levels == "kahn":
+            r = LocalTransport._kahn(stores, None)
+            lap("level_waves")
+            return r
         if levels == "auto":
             if all(s.delta for s in stores):
                 try:
-                    r = LocalTransport._rounds(stores, AUTO_ROUND_CAP)
-                    lap("level_rounds")
+                    r = LocalTransport._kahn(stores, AUTO_ROUND_CAP)
+                    lap("level_waves")
                     return r
                 except LevelsNotConverged:
-                    lap("level_rounds")
+                    lap("level_waves")
+            fell_back = True
             levels = "gather"
         if levels == "gather":
             edges = np.concatenate([s.level_edges() for s in stores])
@@ -718,10 +820,41 @@ class LocalTransport:
             for s in stores:
                 s.depth = s.levels_solve(edges)
             lap("level_solve")
-            return 1
+            return AUTO_ROUND_CAP + 1 if fell_back else 1     # as run_levels_auto reports the fallback
         r = LocalTransport._rounds(stores, max_rounds)
         lap("level_rounds")
         return r
+
+    @staticmethod
+    def _kahn(stores, wave_cap):
+        """run_levels_kahn for stores in one process: each phase's outboxes routed to the inboxes."""
+        def route():
+            out = [s.kahn_outbox() for s in stores]
+            for d, s in enumerate(stores):
+                parts = []
+                for cnt, msgs in out:
+                    o = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
+                    parts.append(msgs[o[d]:o[d + 1]])
+                s.kahn_inbox(np.concatenate(parts) if parts else np.zeros(0, np.uint64))
+        for s in stores:
+            s.kahn_begin()
+        level = 0
+        while True:
+            route()
+            rel = [s.kahn_decide() for s in stores]
+            route()
+            unreleased = [s.kahn_apply(level) for s in stores]
+            if not any(rel):
+                break
+            level += 1
+            if wave_cap is not None and level >= wave_cap:
+                raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
+        if any(unreleased):
+            raise engine.AccordDepsError(abi.AD_ERR_ARGUMENT, "Kahn waves: rows never released (a cycle)")
+        for s in stores:
+            s.depth = level
+            s.kahn_bytes = 8 * s.kahn_sent()
+        return level + 1
 
     @staticmethod
     def _rounds(stores, max_rounds):

@@ -222,7 +222,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
                                      const uint8_t* nl, int2* ring, int rb, int2* carry, uint32_t* stuck) {
     const int lane = __lane_id();
     uint32_t slot[E], ds[E], ep[E], rn[E];
-    bool wr[E], hd[E], lst[E];
+    bool wr[E], hd[E], lst[E], nle[E];
     int y0[E], w0[E], a[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -238,6 +238,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
         rn[e] = (c.y >> 11) & 0x7FFu;
         const int2 h = hd[e] ? hc[k] : make_int2(-1, -1);
         y0[e] = h.x; w0[e] = h.y;
+        nle[e] = nl[slot[e]] != 0;                       // static for the block: read once, not per round
     }
     const BzMax<PK> op{};
     uint32_t it = 0;
@@ -272,10 +273,9 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
             const PK zm = in2 > inc2[e] ? in2 : inc2[e];
             const int X = (int)ds[e] + bz_val<PK>(zm);
             const int x = wr[e] ? X : max(a[e], X + 1);
-            if (x > a[e]) {                                  // rare after the first rounds
-                atomicMax(&lv[slot[e]], x);
-                up |= nl[slot[e]] != 0;
-            }
+            const bool r = x > a[e];
+            if (r) atomicMax(&lv[slot[e]], x);               // rare after the first rounds
+            up |= r && nle[e];
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this round's raises before the next reads
         ++it;
@@ -329,43 +329,57 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
 // block's global stores are released (fence) at the end of the NEXT block, and read no earlier than the
 // staging during the block after that.
 // stats[0] = greatest level + 1, stats[1] = rounds, stats[2..3] = clock64 in rounds, stats[4..5] = total,
-// stats[6] = a block's rounds did not converge.
+// stats[6] = a block's rounds did not converge, stats[7..9] = clock64 / 256 in setup, waiting for the staging
+// waves after the rounds, and out (thread 0).
+// The loads are issued for all of a thread's slots before any is used (records, compacted entries and order slice
+// first, then the dependent global carry-ins), so the staging costs two memory round trips instead of two per slot
+// (it ran 2,900 cycles per C3 block past the rounds when each slot waited for its own loads).
+constexpr int BL_SI = (BL_CAP + (BL_T - WAVE) - 1) / (BL_T - WAVE);   // slots per staging thread (3 waves)
+__device__ inline int2 bl_carry_load(const int2* carry, uint32_t slot) {
+    const int* g = reinterpret_cast<const int*>(&carry[slot]);
+    return make_int2(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                     __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
 __device__ inline void bl_stage(uint32_t b, uint32_t B, int t, int nthr, const uint32_t* __restrict__ boff,
                                 const uint32_t* __restrict__ tb, const uint64_t* __restrict__ rec, const uint4* __restrict__ crec,
                                 const uint32_t* __restrict__ mt, const int2* carry, const uint32_t* __restrict__ order,
                                 uint64_t* srec, int2* scar, uint32_t* sord, uint4* scr, int2* shc, uint32_t* sbnd) {
     if (b >= B) return;
     const uint32_t j0 = boff[b], j1 = boff[b + 1], t0 = tb[b], t1 = tb[b + 1], m = mt[b];
-    for (int x = t; x < BL_CAP; x += nthr) {
-        const uint32_t j = j0 + (uint32_t)x;
-        const uint64_t r = j < j1 ? rec[j] : ~0ull;
-        int2 c = make_int2(-1, -1);
-        const uint32_t f = (uint32_t)(r >> 32);
+    uint64_t r[BL_SI];
+    uint4 q[BL_SI];
+    uint32_t o[BL_SI];
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const uint32_t x = (uint32_t)(t + i * nthr);
+        r[i] = (x < (uint32_t)BL_CAP && j0 + x < j1) ? rec[j0 + x] : ~0ull;
+        o[i] = x < t1 - t0 ? order[t0 + x] : 0u;
+        q[i] = x < m ? crec[j0 + x] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    int2 c[BL_SI], h[BL_SI];
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const uint32_t x = (uint32_t)(t + i * nthr);
+        c[i] = make_int2(-1, -1);
+        h[i] = make_int2(-1, -1);
+        const uint32_t f = (uint32_t)(r[i] >> 32);
         // singleton heads' global carry-ins (the multi-entry runs' heads are staged with their compacted entries)
-        if (r != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) && ((f >> BL_SH_SRC) & 3u) == 2u) {
-            const int* g = reinterpret_cast<const int*>(&carry[(uint32_t)r]);
-            c.x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            c.y = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (r[i] != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) && ((f >> BL_SH_SRC) & 3u) == 2u)
+            c[i] = bl_carry_load(carry, (uint32_t)r[i]);
+        if (x < m && ((q[i].x >> BL_SH_HEAD) & 1u)) {
+            const uint32_t src = (q[i].x >> BL_SH_SRC) & 3u;
+            if (src == 2u) h[i] = bl_carry_load(carry, q[i].z);
+            else if (src == 1u) h[i] = make_int2(-2, (int)q[i].w);   // resolved from the ring at setup (ring index)
         }
-        srec[x] = r;
-        scar[x] = c;
-        sord[x] = (uint32_t)x < t1 - t0 ? order[t0 + x] : 0u;
-        if ((uint32_t)x < m) {
-            const uint4 q = crec[j0 + x];
-            int2 h = make_int2(-1, -1);
-            if ((q.x >> BL_SH_HEAD) & 1u) {
-                const uint32_t src = (q.x >> BL_SH_SRC) & 3u;
-                if (src == 2u) {
-                    const int* g = reinterpret_cast<const int*>(&carry[q.z]);
-                    h.x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    h.y = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else if (src == 1u) {
-                    h.x = -2; h.y = (int)q.w;              // resolved from the ring at setup (ring index)
-                }
-            }
-            scr[x] = q;
-            shc[x] = h;
-        }
+    }
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const uint32_t x = (uint32_t)(t + i * nthr);
+        if (x >= (uint32_t)BL_CAP) continue;
+        srec[x] = r[i];
+        scar[x] = c[i];
+        sord[x] = o[i];
+        if (x < m) { scr[x] = q[i]; shc[x] = h[i]; }
     }
     if (t == 0) { sbnd[0] = j0; sbnd[1] = j1; sbnd[2] = t0; sbnd[3] = t1; sbnd[4] = m; }
 }
@@ -400,7 +414,9 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
 #pragma unroll
     for (int e = 0; e < BL_EPT; ++e) pfl[e] = BL_NONE;
     __syncthreads();
+    uint64_t tsetup = 0, twait = 0, tout = 0;          // clock64 per phase (thread 0), AD_DEBUG_LEVELS
     for (uint32_t b = 0; b < B; ++b) {
+        const uint64_t tb0 = clock64();
         const int pb = b & 1;
         int* lv = lvb[pb];
         uint8_t* nl = nlb[pb];
@@ -438,20 +454,21 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
             }
             if (!last) nl[f & BL_TL] = 1;
         }
-        // wave 0: the multi-entry runs' heads: carry-in (ring sources resolved here) and prefill
-        if (tid < WAVE) {
-            for (int k = lane; k < nm; k += WAVE) {
-                const uint4 q = scr[k];
-                if (!((q.x >> BL_SH_HEAD) & 1u)) continue;
-                int2 h = shc[k];
-                if ((q.x >> BL_SH_SRC & 3u) == 0u) h = make_int2(-1, -1);
-                else if (h.x == -2) h = ring[h.y];
-                shc[k] = h;
-                const int lb = ((q.x >> BL_SH_W) & 1u) ? h.x + 1 : h.y + 1;
-                if (lb > 0) atomicMax(&lv[q.x & BL_TL], lb);
-            }
+        // the multi-entry runs' heads (all waves): carry-in (ring sources resolved here) and prefill
+        for (int k = tid; k < nm; k += BL_T) {
+            const uint4 q = scr[k];
+            if (!((q.x >> BL_SH_HEAD) & 1u)) continue;
+            int2 h = shc[k];
+            if ((q.x >> BL_SH_SRC & 3u) == 0u) h = make_int2(-1, -1);
+            else if (h.x == -2) h = ring[h.y];
+            shc[k] = h;
+            const int lb = ((q.x >> BL_SH_W) & 1u) ? h.x + 1 : h.y + 1;
+            if (lb > 0) atomicMax(&lv[q.x & BL_TL], lb);
         }
         __syncthreads();
+        const uint64_t tb1 = clock64();
+        tsetup += tb1 - tb0;
+        uint64_t tb2 = tb1;
         // ---- rounds (wave 0) | staging of the next block (waves 1-3)
         if (tid < WAVE) {
             if (nm > 0) {
@@ -466,7 +483,8 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
                 else if (epl <= 8) r = bl_rounds<8, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
                 else if (epl <= 12) r = bl_rounds<12, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
                 else r = bl_rounds<16, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                tround += clock64() - t0;
+                tb2 = clock64();
+                tround += tb2 - t0;
                 rounds += r;
             }
         } else {
@@ -474,6 +492,8 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
                      shcb[pb ^ 1], sbnd);
         }
         __syncthreads();
+        const uint64_t tb3 = clock64();
+        twait += tb3 - tb2;
         // ---- out: carry-out of the singleton runs, levels.  The fence first releases the previous block's
         // global carries (issued a block ago) before this block's are issued.
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -504,6 +524,7 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
 #pragma unroll
         for (int e = 0; e < BL_EPT; ++e) pfl[e] = fl[e];
         __syncthreads();
+        tout += clock64() - tb3;
         if (sstuck) break;
     }
     maxl = wave_max(maxl);
@@ -514,6 +535,7 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         stats[2] = (uint32_t)tround; stats[3] = (uint32_t)(tround >> 32);
         stats[4] = (uint32_t)tot; stats[5] = (uint32_t)(tot >> 32);
         stats[6] = sstuck;
+        stats[7] = (uint32_t)(tsetup >> 8); stats[8] = (uint32_t)(twait >> 8); stats[9] = (uint32_t)(tout >> 8);
     }
 }
 

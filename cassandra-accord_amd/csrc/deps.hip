@@ -281,10 +281,13 @@ int stage_deps(ad_handle* h) {
     h->merge_heavy = n == 0 || got[ncol] != 0 || h->n_large > 0 || Q > 0;
     CK(check_params(h));
     h->deps_entries = 0;
+    h->times.range_entries = 0;
+    h->times.vitems = h->V;
     for (int c = 0; c < ncsr; ++c) {
         Csr& x = csr_at(c);
         x.nkeys = tot[3 * c]; x.nk2t = tot[3 * c + 1]; x.ncap = tot[3 * c + 2];
         h->deps_entries += x.ncap;
+        if (c >= nc) h->times.range_entries += x.ncap;
         if (c < nc) {
             CK(alloc_csr_data(h, cls[c], x, 1));
             ta.out_key_off[c] = x.key_off; ta.out_k2t_off[c] = x.k2t_off; ta.out_keys[c] = x.keys; ta.out_k2t[c] = x.k2t;

@@ -141,6 +141,16 @@ struct ad_handle {
     uint32_t *dbase_dev = nullptr, *dcnt_dev = nullptr;
     uint64_t* dout = nullptr;
     std::vector<uint32_t> dbase, dcnt;   // [world + 1] region starts; [world] last round's pair counts
+    // distributed Kahn levels (ad_shard_kahn_*, kahn_shard_kernels.h)
+    std::vector<uint8_t> home_host, holders_host;   // local row -> home store / holder mask (host copies)
+    std::vector<uint32_t> ks_base;   // [2 * (MAX_STORES + 1)]: READY then RELEASE region starts per destination
+    uint32_t *ks_base_dev = nullptr, *ks_cnt_dev = nullptr, *ks_rem = nullptr, *ks_rcnt = nullptr, *ks_flag = nullptr;
+    uint32_t* ks_xs = nullptr;
+    uint64_t *ks_out = nullptr, *ks_in = nullptr, *ks_xoff = nullptr;
+    size_t ks_in_m = 0, ks_unreleased = 0;
+    uint64_t ks_sent = 0;            // messages this batch sent to other stores
+    int ks_phase = -1;               // the outbox holds 0: READY, 1: RELEASE messages
+    bool ks_levels = false;          // lvl holds this batch's levels from the Kahn waves (ad_shard_order reads them)
     // MaxConflicts carried from earlier batches (ad_max_conflicts_carry): sorted keys + timestamps on the device
     size_t mc_m = 0;
     uint64_t *mc_ck = nullptr, *mc_cm = nullptr, *mc_cl = nullptr;
@@ -272,6 +282,8 @@ enum Slot : size_t {
     S_RBS, S_RBE, S_RBM, S_RBL, S_RBN,                          // rejectBefore intervals (ad_preaccept_expiry)
     S_NF0, S_NF_END = S_NF0 + 14,                               // ad_cfk_notify inputs / scratch / outputs
     S_STG0, S_STG_END = S_STG0 + 12,
+    S_KSSRC, S_KSDST, S_KSSRC2, S_KSDST2, S_KSREM, S_KSXOFF, S_KSRCNT, S_KSFL, S_KSBASE, S_KSCNT, S_KSOUT,
+    S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
     S_NUM_FIXED,
     S_CSR0 = 256
 };

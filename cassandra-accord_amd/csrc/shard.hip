@@ -184,6 +184,10 @@ int ad_shard_setup(ad_handle* h, const uint32_t* gid, const uint8_t* home_store,
     }
     std::vector<uint8_t> home(n);
     for (size_t i = 0; i < n; ++i) home[i] = home_store[i] == self ? 1 : 0;
+    h->home_host.assign(home_store, home_store + n);
+    h->holders_host.clear();
+    h->ks_levels = false;
+    h->ks_phase = -1;
     CK(dalloc(h, S_GID, &h->gid, n)); CK(dalloc(h, S_HOME, &h->home, n)); CK(dalloc(h, S_HSTORE, &h->hstore, n));
     if (n) {
         HIPCHK(h, hipMemcpyAsync(h->gid, gid, n * 4, hipMemcpyHostToDevice, h->st));
@@ -599,6 +603,7 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     // deps restricted to its keys), computed once per batch.
     const bool mixed = h->Q > 0 || h->n_special > 0 || h->n_large > 0;
     if (first && mixed) CK(stage_merge(h));
+    h->ks_levels = false;
     CK(dalloc(h, S_G, &h->G, h->n_global + 1));
     uint32_t* flag = nullptr;
     CK(dalloc(h, S_NE, &flag, 16));
@@ -664,6 +669,7 @@ int ad_shard_set_holders(ad_handle* h, const uint8_t* holders) {
     CK(dalloc(h, S_DOUT, &h->dout, std::max<size_t>(h->dbase[W], 1)));
     if (n) HIPCHK(h, hipMemcpyAsync(h->holders, holders, n, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, hipMemcpyAsync(h->dbase_dev, h->dbase.data(), (W + 1) * 4, hipMemcpyHostToDevice, h->st));
+    h->holders_host.assign(holders, holders + n);
     HIPCHK(h, hipStreamSynchronize(h->st));
     h->dcnt.assign(W, 0);
     return AD_OK;
@@ -783,13 +789,15 @@ int ad_shard_levels_allreduce(ad_handle* h, uint32_t* any_changed) {
 
 // Home txns' levels and execution order (by (level, executeAt)), as global ranks; on the device.
 int ad_shard_order(ad_handle* h, uint32_t* level_out, uint32_t* order_out) {
-    if (!h || !h->G || h->sdeps.empty()) return set_err(h, AD_ERR_STATE, "ad_shard_order: levels rounds + ad_shard_merge first");
+    if (!h || (!h->G && !h->ks_levels) || h->sdeps.empty())
+        return set_err(h, AD_ERR_STATE, "ad_shard_order: levels (rounds, gather or Kahn waves) + ad_shard_merge first");
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     hipStream_t st = h->st;
     const size_t H = h->H, n = h->n;
     if (H == 0) return AD_OK;
-    if (n) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
+    // the Kahn waves leave the levels in lvl already; the other protocols in the global array G
+    if (n && !h->ks_levels) k_levels_gather<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->G, h->lvl);
     uint32_t *ord, *tmp;
     CK(dalloc(h, S_ORDER, &ord, std::max(n, H) + 1));
     // the one-exchange path solves levels without a local level pass: the order's sort buffers are sized here
@@ -852,6 +860,7 @@ int ad_shard_levels_solve(ad_handle* h, const uint64_t* edges, size_t m, uint32_
     CK(dalloc(h, S_GLIN, &buf, std::max<size_t>(m, 1)));
     if (m) HIPCHK(h, hipMemcpyAsync(buf, edges, m * 8, hipMemcpyHostToDevice, h->st));
     CK(dalloc(h, S_G, &h->G, h->n_global + 1));
+    h->ks_levels = false;
     return levels_solve_edges(h, buf, m, h->n_global, h->G, depth);
 }
 
@@ -895,6 +904,7 @@ int ad_shard_levels_gather(ad_handle* h, uint32_t* depth) {
     if (first != ncclSuccess) return set_err(h, AD_ERR_DEVICE, what + ": " + ncclGetErrorString(first));
     if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclGroupEnd (level edges): ") + ncclGetErrorString(r));
     CK(dalloc(h, S_G, &h->G, h->n_global + 1));
+    h->ks_levels = false;
     return levels_solve_edges(h, all, off[W], h->n_global, h->G, depth);
 }
 

@@ -1,0 +1,246 @@
+// shard_kahn.hip — execution levels of a key-range sharded batch by distributed Kahn wavefronts
+// (kahn_shard_kernels.h has the protocol).  Per wave the host moves two message sets between the stores: READYs
+// (to the txn's home store) and RELEASEs (from the home store to every holder).  RCCL moves them device to device
+// (ad_shard_kahn_exchange: per-destination counts + a status word all-gathered, then grouped send/recv); host
+// transports use ad_shard_kahn_outbox / ad_shard_kahn_inbox.
+#include "engine_internal.h"
+#include "global_levels.h"
+#include "kahn_shard_kernels.h"
+
+#include <algorithm>
+
+using namespace ad;
+
+namespace {
+
+uint32_t* ks_base(ad_handle* h, int phase) { return h->ks_base_dev + (size_t)phase * (MAX_STORES + 1); }
+
+int ks_bad(ad_handle* h, const char* what) {
+    uint32_t bad = 0;
+    HIPCHK(h, hipMemcpyAsync(&bad, h->ks_flag + 2, 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    if (bad) return set_err(h, AD_ERR_ARGUMENT, what);
+    return AD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// The store's local constraint graph (its key chains' transitive reduction plus its (b)/(c) edges, local rows:
+// the same edges ad_shard_level_edges exports), its successor lists, and wave 0's READY messages.
+int ad_shard_kahn_begin(ad_handle* h) {
+    if (!h) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (!h->sharded || !h->have_deps) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_begin: sharded deps first");
+    if (!h->holders || h->holders_host.size() != h->n)
+        return set_err(h, AD_ERR_STATE, "ad_shard_kahn_begin: ad_shard_set_holders first (the RELEASE fan-out)");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const size_t n = h->n;
+    const uint32_t W = h->world;
+    const bool mixed = h->Q > 0 || h->n_special > 0 || h->n_large > 0;
+    if (mixed && !h->have_merged) {
+        CK(stage_merge(h));
+        h->merged_has_range = h->Q > 0;
+    }
+    size_t m = 0;
+    CK(levels_export_edges(h, &m, false, false));
+    const size_t m1 = std::max<size_t>(m, 1), n1 = std::max<size_t>(n, 1);
+    uint32_t *src, *dst, *src2, *dst2;
+    CK(dalloc(h, S_KSSRC, &src, m1)); CK(dalloc(h, S_KSDST, &dst, m1));
+    CK(dalloc(h, S_KSSRC2, &src2, m1)); CK(dalloc(h, S_KSDST2, &dst2, m1));
+    CK(dalloc(h, S_KSREM, &h->ks_rem, n1)); CK(dalloc(h, S_KSXOFF, &h->ks_xoff, n + 1));
+    CK(dalloc(h, S_KSRCNT, &h->ks_rcnt, n1)); CK(dalloc(h, S_KSFL, &h->ks_flag, 16));
+    CK(dalloc(h, S_KSBASE, &h->ks_base_dev, 2 * (MAX_STORES + 1))); CK(dalloc(h, S_KSCNT, &h->ks_cnt_dev, MAX_STORES + 1));
+    // outbox regions: READY to d <= local rows homed at d; RELEASE to d <= home rows d also holds
+    std::vector<uint64_t> rc(W, 0), lc(W, 0);
+    for (size_t i = 0; i < n; ++i) {
+        rc[h->home_host[i]]++;
+        if (h->home_host[i] == h->self)
+            for (uint32_t d = 0; d < W; ++d) lc[d] += (h->holders_host[i] >> d) & 1u;
+    }
+    h->ks_base.assign(2 * (MAX_STORES + 1), 0);
+    for (uint32_t d = 0; d < W; ++d) {
+        h->ks_base[d + 1] = h->ks_base[d] + (uint32_t)rc[d];
+        h->ks_base[MAX_STORES + 1 + d + 1] = h->ks_base[MAX_STORES + 1 + d] + (uint32_t)lc[d];
+    }
+    const size_t cap = std::max<size_t>(std::max(h->ks_base[W], h->ks_base[MAX_STORES + 1 + W]), 1);
+    CK(dalloc(h, S_KSOUT, &h->ks_out, cap));
+    HIPCHK(h, hipMemcpyAsync(h->ks_base_dev, h->ks_base.data(), 2 * (MAX_STORES + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemsetAsync(h->ks_rem, 0, n1 * 4, st));
+    HIPCHK(h, hipMemsetAsync(h->ks_flag, 0, 64, st));
+    CK(ensure_scratch(h, std::max(h->scratch_cap, (size_t)(3 * (radix_hist_len(m1) + 128) + 64 * 1024) * 4)));
+    // in-degrees (remaining local predecessors) and the successor lists by source
+    if (m) k_edges_split<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->gl_edges, src, dst, h->ks_rem, (uint32_t)n, h->ks_flag + 2);
+    h->ks_xs = dst;
+    if (m) {
+        const int bits = std::max(1, bits_of(n - 1));
+        if (radix_sort_pairs(src, dst, src2, dst2, m, bits, radix_scratch(h, m), st)) { std::swap(src, src2); h->ks_xs = dst2; }
+        k_xoff_bounds<<<ceil_div((long)n + 1, 256), 256, 0, st>>>(m, src, (uint32_t)n, h->ks_xoff);
+    } else {
+        HIPCHK(h, hipMemsetAsync(h->ks_xoff, 0, (n + 1) * 8, st));
+    }
+    HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
+    if (n) k_ks_init<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->hstore, h->ks_rem, h->lvl, h->ks_rcnt,
+                                                             ks_base(h, 0), h->ks_cnt_dev, h->ks_out);
+    HIPCHK(h, hipGetLastError());
+    CK(ks_bad(h, "ad_shard_kahn_begin: a level edge out of range or a self edge"));
+    h->ks_phase = 0;
+    h->ks_unreleased = n;
+    h->ks_sent = 0;
+    h->ks_in_m = 0;
+    h->ks_levels = true;
+    h->level_iters = 0;
+    return AD_OK;
+}
+
+// Host transports: the outbox of the current phase, per destination (counts[world]) and, if msgs is given, the
+// messages in destination order (counts' sum of them).
+int ad_shard_kahn_outbox(ad_handle* h, uint32_t* counts, uint64_t* msgs) {
+    if (!h || !counts) return AD_ERR_ARGUMENT;
+    if (h->ks_phase < 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_outbox: ad_shard_kahn_begin first");
+    hipSetDevice(h->device);
+    const uint32_t W = h->world;
+    HIPCHK(h, hipMemcpyAsync(counts, h->ks_cnt_dev, W * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    if (msgs) {
+        const uint32_t* b = h->ks_base.data() + (size_t)h->ks_phase * (MAX_STORES + 1);
+        size_t at = 0;
+        for (uint32_t d = 0; d < W; ++d) {
+            if (counts[d]) HIPCHK(h, hipMemcpyAsync(msgs + at, h->ks_out + b[d], (size_t)counts[d] * 8, hipMemcpyDeviceToHost, h->st));
+            at += counts[d];
+            if (d != h->self) h->ks_sent += counts[d];
+        }
+        HIPCHK(h, hipStreamSynchronize(h->st));
+    }
+    return AD_OK;
+}
+
+// Host transports: the messages this store received (every source's region for it, any order).
+int ad_shard_kahn_inbox(ad_handle* h, const uint64_t* msgs, size_t m) {
+    if (!h || (m && !msgs)) return AD_ERR_ARGUMENT;
+    if (h->ks_phase < 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_inbox: ad_shard_kahn_begin first");
+    hipSetDevice(h->device);
+    for (size_t i = 0; i < m; ++i)
+        if ((msgs[i] >> 32) != 0 || msgs[i] >= h->n_global) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_inbox: global rank out of range");
+    CK(dalloc(h, S_KSIN, &h->ks_in, std::max<size_t>(m, 1)));
+    if (m) HIPCHK(h, hipMemcpyAsync(h->ks_in, msgs, m * 8, hipMemcpyHostToDevice, h->st));
+    h->ks_in_m = m;
+    return AD_OK;
+}
+
+// RCCL: the per-destination counts plus this store's status word all-gathered (a world x (world + 1) matrix), then
+// the regions by grouped point-to-point send/recv into the inbox (this store's own region by a device copy).
+// *any_status: some store's status word was nonzero.
+int ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status) {
+    if (!h || !any_status) return AD_ERR_ARGUMENT;
+    if (!h->comm || h->ks_phase < 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_exchange: ad_comm_init + ad_shard_kahn_begin first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const uint32_t W = h->world, self = h->self;
+    uint32_t* mat = nullptr;
+    CK(dalloc(h, S_KSMAT, &mat, (size_t)MAX_STORES * (MAX_STORES + 1)));
+    HIPCHK(h, hipMemcpyAsync(h->ks_cnt_dev + W, &status, 4, hipMemcpyHostToDevice, st));
+    ncclResult_t r = ncclAllGather(h->ks_cnt_dev, mat, W + 1, ncclUint32, h->comm, st);
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllGather (Kahn counts): ") + ncclGetErrorString(r));
+    std::vector<uint32_t> M((size_t)W * (W + 1));
+    HIPCHK(h, hipMemcpyAsync(M.data(), mat, M.size() * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    uint64_t recv_total = 0;
+    uint32_t any = 0;
+    for (uint32_t s = 0; s < W; ++s) {
+        recv_total += M[(size_t)s * (W + 1) + self];
+        any |= M[(size_t)s * (W + 1) + W];
+    }
+    *any_status = any ? 1u : 0u;
+    CK(dalloc(h, S_KSIN, &h->ks_in, std::max<uint64_t>(recv_total, 1)));
+    const uint32_t* b = h->ks_base.data() + (size_t)h->ks_phase * (MAX_STORES + 1);
+    if (ncclGroupStart() != ncclSuccess) return set_err(h, AD_ERR_DEVICE, "ncclGroupStart");
+    ncclResult_t first = ncclSuccess;
+    std::string what;
+    size_t ro = 0;
+    for (uint32_t p = 0; p < W && first == ncclSuccess; ++p) {
+        const uint32_t sn = M[(size_t)self * (W + 1) + p], rn = M[(size_t)p * (W + 1) + self];
+        if (p == self) {
+            if (sn) HIPCHK(h, hipMemcpyAsync(h->ks_in + ro, h->ks_out + b[p], (size_t)sn * 8, hipMemcpyDeviceToDevice, st));
+        } else {
+            if (sn) {
+                ncclResult_t e = ncclSend(h->ks_out + b[p], (size_t)sn * 8, ncclUint8, (int)p, h->comm, st);
+                if (e != ncclSuccess) { first = e; what = "ncclSend (Kahn) to " + std::to_string(p); }
+                h->ks_sent += sn;
+            }
+            if (first == ncclSuccess && rn) {
+                ncclResult_t e = ncclRecv(h->ks_in + ro, (size_t)rn * 8, ncclUint8, (int)p, h->comm, st);
+                if (e != ncclSuccess) { first = e; what = "ncclRecv (Kahn) from " + std::to_string(p); }
+            }
+        }
+        ro += rn;
+    }
+    r = ncclGroupEnd();
+    if (first != ncclSuccess) return set_err(h, AD_ERR_DEVICE, what + ": " + ncclGetErrorString(first));
+    if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclGroupEnd (Kahn): ") + ncclGetErrorString(r));
+    h->ks_in_m = recv_total;
+    return AD_OK;
+}
+
+// Home store: the received READYs counted; txns every holder reported are released (this wave) and their
+// RELEASEs fill the outbox.  *released: this store released some txn.
+int ad_shard_kahn_decide(ad_handle* h, uint32_t* released) {
+    if (!h || !released) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (h->ks_phase != 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_decide: exchange the READY outbox first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
+    HIPCHK(h, hipMemsetAsync(h->ks_flag, 0, 4, st));
+    const size_t m = h->ks_in_m;
+    if (m) k_ks_decide<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, h->gid, h->home, h->holders, h->ks_rcnt,
+                                                               ks_base(h, 1), h->ks_cnt_dev, h->ks_out, h->ks_flag,
+                                                               h->ks_flag + 2);
+    HIPCHK(h, hipGetLastError());
+    uint32_t f[3] = {0, 0, 0};
+    HIPCHK(h, hipMemcpyAsync(f, h->ks_flag, 12, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_decide: a READY for a txn this store does not home");
+    *released = f[0] ? 1u : 0u;
+    h->ks_phase = 1;
+    h->ks_in_m = 0;
+    return AD_OK;
+}
+
+// Every holder: the received RELEASEs get level `level`; their local successors' remaining in-degrees drop and
+// the rows reaching zero fill the outbox with the next wave's READYs.  *unreleased: local rows still without a level.
+int ad_shard_kahn_apply(ad_handle* h, uint32_t level, uint64_t* unreleased) {
+    if (!h || !unreleased) return AD_ERR_ARGUMENT;
+    g_tracer = &h->tracer;
+    if (h->ks_phase != 1) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_apply: ad_shard_kahn_decide + the RELEASE exchange first");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
+    HIPCHK(h, hipMemsetAsync(h->ks_flag + 1, 0, 4, st));
+    const size_t m = h->ks_in_m;
+    if (m) k_ks_apply<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, level, h->gid, h->hstore, h->ks_xoff, h->ks_xs,
+                                                              h->ks_rem, h->lvl, ks_base(h, 0), h->ks_cnt_dev, h->ks_out,
+                                                              h->ks_flag, h->ks_flag + 2);
+    HIPCHK(h, hipGetLastError());
+    uint32_t f[3] = {0, 0, 0};
+    HIPCHK(h, hipMemcpyAsync(f, h->ks_flag, 12, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_apply: a RELEASE for a txn this store does not hold, or twice");
+    h->ks_unreleased -= std::min<size_t>(h->ks_unreleased, f[1]);
+    if (m) h->level_iters = level + 1;
+    *unreleased = h->ks_unreleased;
+    h->ks_phase = 0;
+    h->ks_in_m = 0;
+    return AD_OK;
+}
+
+// Messages this batch's waves sent to other stores (8 bytes each).
+int ad_shard_kahn_sent(ad_handle* h, uint64_t* sent) {
+    if (!h || !sent) return AD_ERR_ARGUMENT;
+    *sent = h->ks_sent;
+    return AD_OK;
+}
+
+}  // extern "C"

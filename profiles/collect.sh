@@ -3,7 +3,8 @@
 #   /usr/local/graft/bin/gpurun --timeout 900 -- 'bash profiles/collect.sh r01_v2'
 # 1. the default bench line (C2, with the CPU baseline leg) + its per-kernel HIP-event breakdown;
 # 2. rocprofv3 --kernel-trace --stats of a short bench run (kernel durations to cross-check `roofline`);
-# 3. two separate PMC passes (FETCH_SIZE, WRITE_SIZE — they do not fit one pass on gfx950);
+# 3. two separate PMC passes (FETCH_SIZE, WRITE_SIZE — they do not fit one pass on gfx950), and the same two
+#    for C3 at the end;
 # then, back in the build container (gpurun merges gpurun_out/ back):
 #   python3 profiles/summarize.py gpurun_out/TAG TAG      -> profiles/TAG_*
 # Every GPU step has its own time limit and the steps are chained (set -e): a failure ends the script.
@@ -33,3 +34,10 @@ timeout -k 10 300 python3 -u "$ROOT/bench.py" --config C3 --steps 5 --warmup 2 -
 echo "c3 done"
 timeout -k 10 400 python3 -u "$ROOT/bench.py" --config C4 --steps 2 --warmup 1 --breakdown > "$OUT/c4.json" 2> "$OUT/c4.err"
 echo "c4 done"
+# 6. C3's PMC passes (the block level walk dominates it), separate counters as above
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c3fetch" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --config C3 --steps 1 --warmup 1 --cpu-sample 0 --no-e2e > "$OUT/c3fetch.log" 2>&1
+echo "c3 fetch done"
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c3write" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --config C3 --steps 1 --warmup 1 --cpu-sample 0 --no-e2e > "$OUT/c3write.log" 2>&1
+echo "c3 write done"

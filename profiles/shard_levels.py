@@ -24,7 +24,7 @@ for proto in protos:
     for k in range(S):
         local, gid, _ = sharding.slice_for_shard(b, bounds[k], bounds[k + 1])
         st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=seed)
-        st.load(local, gid, hs[gid], b["n"], k, S, holders=masks[gid] if proto == "rounds" else None)
+        st.load(local, gid, hs[gid], b["n"], k, S, holders=masks[gid] if proto in ("rounds", "kahn", "auto") else None)
         stores.append(st)
     for rep in range(2):                                   # the first is a warm-up
         tm = {}
@@ -34,7 +34,7 @@ for proto in protos:
     rec = {"proto": proto, "stores": S, "txns": int(b["n"]), "rounds": rounds, "wall_s": dt,
            "phases_s_summed": {k: round(v, 4) for k, v in tm.items()},
            "local_txns": [int(st.gid.size) for st in stores],
-           "pairs_sent": [int(getattr(st, "pairs_sent", 0)) for st in stores], "depth": int(getattr(stores[0], "depth", 0) or 0)}
+           "pairs_sent": [int(getattr(st, "pairs_sent", 0)) for st in stores], "kahn_bytes": [int(getattr(st, "kahn_bytes", 0)) for st in stores], "depth": int(getattr(stores[0], "depth", 0) or 0)}
     print(json.dumps(rec), flush=True)
     for st in stores:
         st.close()

@@ -2,6 +2,8 @@
 """Condense one collect.sh run into committed summaries (profiles/TAG_*):
   TAG_bench.json          the bench line;           TAG_breakdown.txt  its HIP-event per-kernel breakdown
   TAG_kernel_stats.csv    rocprofv3 --stats summary (all kernels of the short bench run)
+  TAG_c3_pmc.json         the same for the C3 line (block level walk); TAG_c3_bench.json / TAG_c4_bench.json /
+                          TAG_cpu_full.json   the secondary lines
   TAG_pmc.json            per kernel (rocprof name + grid): mean FETCH_SIZE / WRITE_SIZE per dispatch (KB as
                           rocprofv3 reports them) and dispatch counts, plus the 4-byte streaming-read calibration
                           measured on k_radix_hist (reads exactly units*4 key bytes, coalesced 4 B/lane).
@@ -81,6 +83,24 @@ def main():
            "calibration_4B_stream_read": cal, "kernels": res}
     with open(dst("pmc.json"), "w") as f:
         json.dump(doc, f, indent=1)
+    # C3's passes (collect.sh step 6): per kernel as above
+    f3, w3 = pmc(os.path.join(out, "c3fetch"), "FETCH_SIZE"), pmc(os.path.join(out, "c3write"), "WRITE_SIZE")
+    if f3 or w3:
+        r3 = {}
+        for k in sorted(set(f3) | set(w3)):
+            e = {}
+            if k in f3:
+                e["FETCH_SIZE_KB_mean"], e["dispatches"] = f3[k]
+            if k in w3:
+                e["WRITE_SIZE_KB_mean"] = w3[k][0]
+                e.setdefault("dispatches", w3[k][1])
+            r3[k] = e
+        with open(dst("c3_pmc.json"), "w") as f:
+            json.dump({"note": doc["note"] + " C3 (1M Zipf txns), bench.py --config C3 --steps 1 --warmup 1.",
+                       "kernels": r3}, f, indent=1)
+    for name in ("c3.json", "c4.json", "cpu_full.json"):
+        if os.path.exists(os.path.join(out, name)):
+            shutil.copy(os.path.join(out, name), dst(name.replace(".json", "_bench.json") if name != "cpu_full.json" else name))
     print("wrote", [os.path.basename(p) for p in glob.glob(os.path.join(HERE, tag + "_*"))])
 
 

@@ -33,7 +33,8 @@ def same_txn(got, h, want, g):
 @pytest.mark.parametrize("name,shards,levels,delta", [("C2", 2, "gather", False), ("C2", 4, "gather", True),
                                                        ("C3", 3, "gather", False), ("C2", 2, "rounds", True),
                                                        ("C3", 3, "rounds", True), ("C3", 3, "rounds", False),
-                                                       ("C2", 4, "rounds", False)])
+                                                       ("C2", 4, "rounds", False), ("C2", 2, "kahn", True),
+                                                       ("C3", 3, "kahn", True), ("C2", 4, "kahn", True)])
 def test_sharded_equals_unsharded(engine_factory, name, shards, levels, delta):
     # levels="rounds" + delta: level rounds exchange only raised levels of shared txns (ad_shard_set_holders);
     # rounds without delta: the dense all-reduce of the whole level array; "gather": one edge exchange
@@ -52,7 +53,9 @@ def test_sharded_equals_unsharded(engine_factory, name, shards, levels, delta):
             stores.append(st)
             st.load(local, gid, hs[gid], b["n"], k, shards, holders=masks[gid] if delta else None)
         rounds = sharding.LocalTransport.run(stores, levels=levels)
-        assert rounds >= 1 and (levels == "rounds" or rounds == 1)
+        assert rounds >= 1 and (levels != "gather" or rounds == 1)
+        if levels == "kahn":
+            assert rounds == int(lv.max()) + 2 and all(st.depth == lv.max() + 1 for st in stores)
         seen = np.zeros(b["n"], bool)
         pos = {int(t): i for i, t in enumerate(order)}
         for st in stores:
@@ -221,7 +224,8 @@ def test_host_fragments_import(engine_factory):
             st.close()
 
 
-@pytest.mark.parametrize("levels,delta", [("gather", False), ("rounds", True), ("rounds", False)])
+@pytest.mark.parametrize("levels,delta", [("gather", False), ("rounds", True), ("rounds", False), ("kahn", True),
+                                          ("auto", True)])
 def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta):
     # the RCCL transport end to end on the one GPU: a world = 1 communicator (ad_comm_init), the grouped
     # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and the levels — gather: ncclAllGather of the
@@ -239,7 +243,9 @@ def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta):
         tr = sharding.RcclTransport(dist, stores[0], 0, 1)
         assert tr.name == "rccl"
         rounds = sharding.run_store(stores[0], tr, levels=levels)
-        assert rounds >= 1 and (levels == "rounds" or rounds == 1)
+        assert rounds >= 1 and (levels != "gather" or rounds == 1)
+        if levels in ("kahn", "auto"):      # ad_shard_kahn_exchange: counts + status all-gather, self copy
+            assert rounds == int(lv.max()) + 2
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all()
         # a second communicator on the same handle is refused (no leak of the first)
@@ -297,7 +303,8 @@ def unsharded3(engine_factory, b, w, r, p, s):
 
 @pytest.mark.parametrize("shards,levels,delta,special", [(2, "gather", True, False), (3, "gather", True, True),
                                                           (4, "gather", False, True), (4, "rounds", True, False),
-                                                          (3, "rounds", False, False)])
+                                                          (3, "rounds", False, False), (3, "kahn", True, True),
+                                                          (4, "kahn", True, False)])
 def test_sharded_range_txns_equal_presplit_unsharded(engine_factory, shards, levels, delta, special):
     # range txns sliced at the store bounds; the stores together must equal the unsharded engine on
     # the batch whose ranges are cut at the same bounds (sharding.presplit; the CPU test
@@ -445,29 +452,37 @@ def test_sharded_c3_full_size_8_stores(engine_factory):
 
 def test_c5_full_shape_8_stores(engine_factory):
     # BASELINE C5 at its shape, in one process: 16,777,216 txns (4 uniform keys over 10^7) over 8 key-range stores
-    # through LocalTransport (export, exchange, home merge, one level-edge exchange, order), against the unsharded
-    # engine on the same batch: every view and the merged Deps of every home txn of every store, levels and order
+    # through LocalTransport (export, exchange, home merge, the levels by the default "auto" protocol -- Kahn waves,
+    # each store walking only its own constraint edges -- and order), against the unsharded engine on the same batch:
+    # every view and the merged Deps of every home txn of every store, levels and order.  Records the level-exchange
+    # bytes each store sends (8 B per READY / RELEASE message to another store): the one-exchange gather shipped
+    # every store's constraint edges to every GPU (62.1 M edges, 497 MB received per store in round 3).
     import time
     w, r, p, s = 32, 3, 0.1, workload.SEEDS["C5"]
     t0 = time.perf_counter()
     b = workload.config("C5")
     views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
     t1 = time.perf_counter()
-    stores, _, _ = _make_stores(b, 8, w, r, p, s, 10_000_000, delta=False)
+    stores, _, _ = _make_stores(b, 8, w, r, p, s, 10_000_000, delta=True)
     try:
         timings = {}
-        assert sharding.LocalTransport.run(stores, timings=timings) == 1
+        rounds = sharding.LocalTransport.run(stores, levels="auto", timings=timings)
+        assert rounds <= sharding.AUTO_ROUND_CAP, "C5 is shallow: the Kahn waves finish"
+        level_bytes = [int(st.kahn_bytes) for st in stores]
+        # per txn one READY and one RELEASE per other holder: ~77 MB per store, vs the gather's 497 MB of edges
+        # on every store and the delta rounds' ~534 MB per store (every raise of every shared level)
+        assert max(level_bytes) < 128 << 20, level_bytes
         t2 = time.perf_counter()
         for st in stores:
             st.order()
         timings["order"] = time.perf_counter() - t2
         t2 = time.perf_counter()
-        assert all(st.depth == lv.max() + 1 for st in stores)
-        seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
+        seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])     # levels included
         assert seen[np.diff(b["key_off"]) > 0].all(), "every txn has exactly one home store"
         rec = {"txns": int(b["n"]), "stores": 8, "unsharded_s": t1 - t0, "protocol_s": t2 - t1,
                "check_s": time.perf_counter() - t2, "phases_s_summed_over_stores": timings,
-               "local_txns_per_store": [int(st.gid.size) for st in stores], "depth": int(lv.max() + 1)}
+               "local_txns_per_store": [int(st.gid.size) for st in stores], "depth": int(lv.max() + 1),
+               "level_protocol": "Kahn waves", "level_waves": rounds, "level_bytes_sent_per_store": level_bytes}
         print("C5 16M x 8 stores:", rec)
         out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
         if os.path.isdir(out):

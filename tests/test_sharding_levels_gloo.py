@@ -208,13 +208,79 @@ def test_holder_masks():
     assert m.tolist() == [3, 0, 2, 3]
 
 
-class HostAutoStore(HostLevelStore):
-    """Both level interfaces (rounds and edges) over one store, as the engine's ShardStore has them."""
+class HostKahnStore:
+    """Host model of ad_shard_kahn_begin / _decide / _apply (csrc/kahn_shard_kernels.h) for pure key batches of
+    Reads and Writes: the store's own constraint edges (HostEdgeStore.level_edges, the engine's
+    levels_export_edges) over its local rows, READY to the home store when a row's last local predecessor was
+    released, RELEASE from the home store to every holder once all holders reported."""
 
-    def __init__(self, local, gid, holders, n_global, rank, world, glob):
-        super().__init__(local, gid, holders, n_global, rank, world)
-        self.n_global, self.glob = n_global, glob
+    delta = True
+
+    def __init__(self, local, gid, holders, home, n_global, rank, world, glob):
+        self.gid, self.holders, self.home = gid, holders.astype(np.int64), home
+        self.rank, self.world, self.n_global = rank, world, n_global
         self._edges = HostEdgeStore(local, gid, n_global, glob)
+        self.row = {int(g): i for i, g in enumerate(gid)}
+        self.G = np.zeros(n_global, np.uint64)
+
+    def kahn_begin(self):
+        n = len(self.gid)
+        e = self._edges.level_edges()
+        self.succ = [[] for _ in range(n)]
+        self.rem = np.zeros(n, np.int64)
+        for x in e:
+            s_, d_ = self.row[int(x) >> 32], self.row[int(x) & 0xFFFFFFFF]
+            self.succ[s_].append(d_)
+            self.rem[d_] += 1
+        self.rcnt = np.zeros(n, np.int64)
+        self.lvl = np.full(n, -1, np.int64)
+        self.sent = 0
+        self.out = {d: [] for d in range(self.world)}
+        for i in np.nonzero(self.rem == 0)[0]:
+            self.out[int(self.home[i])].append(int(self.gid[i]))
+
+    def kahn_outbox(self):
+        cnt = np.array([len(self.out[d]) for d in range(self.world)], np.uint32)
+        self.sent += int(cnt.sum()) - int(cnt[self.rank])
+        msgs = np.array([g for d in range(self.world) for g in self.out[d]], np.uint64)
+        return cnt, msgs
+
+    def kahn_inbox(self, msgs):
+        self.inbox = [int(g) for g in msgs]
+
+    def kahn_decide(self):
+        self.out = {d: [] for d in range(self.world)}
+        rel = False
+        for g in self.inbox:
+            r = self.row[g]
+            assert int(self.home[r]) == self.rank, "READY only to the home store"
+            self.rcnt[r] += 1
+            if self.rcnt[r] == bin(int(self.holders[r])).count("1"):
+                for d in range(self.world):
+                    if (self.holders[r] >> d) & 1:
+                        self.out[d].append(g)
+                rel = True
+        return rel
+
+    def kahn_apply(self, level):
+        self.out = {d: [] for d in range(self.world)}
+        for g in self.inbox:
+            r = self.row[g]
+            assert self.lvl[r] < 0, "one RELEASE per txn"
+            self.lvl[r] = level
+            self.G[g] = level
+            for s_ in self.succ[r]:
+                self.rem[s_] -= 1
+                if self.rem[s_] == 0:
+                    self.out[int(self.home[s_])].append(int(self.gid[s_]))
+        return int((self.lvl < 0).sum())
+
+    def kahn_sent(self):
+        return self.sent
+
+
+class HostAutoStore(HostKahnStore):
+    """Both level interfaces (Kahn waves and edges) over one store, as the engine's ShardStore has them."""
 
     def level_edges(self):
         return self._edges.level_edges()
@@ -223,6 +289,44 @@ class HostAutoStore(HostLevelStore):
         depth = self._edges.levels_solve(edges)
         self.G = self._edges.G.astype(np.uint64)
         return depth
+
+
+def _kahn_worker(rank, world, port, n, dist_kind):
+    sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import torch
+    from accord_amd import abi, sharding, workload
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ks = 3000 if dist_kind == "zipf" else 200_000
+        b = workload.generate(n, 3, ks, dist_kind, seed=14)
+        bounds = sharding.even_bounds(0, ks, world)
+        masks = sharding.holder_masks(b, bounds)
+        hs = sharding.home_stores(b, bounds)
+        local, gid, _ = sharding.slice_for_shard(b, bounds[rank], bounds[rank + 1])
+        store = HostKahnStore(local, gid, masks[gid], hs[gid], n, rank, world, b)
+        waves = sharding.run_levels_kahn(store, sharding.GlooTransport(dist))
+        want, _ = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_LEVELS).levels()
+        assert np.array_equal(store.lvl.astype(np.uint32), want[gid]), "rank %d: levels differ" % rank
+        assert store.depth == int(want.max()) + 1 and waves == store.depth + 1
+        # per txn at most one READY and one RELEASE per holder cross the wire (never per round)
+        others = ((masks[gid].astype(np.int64) & ~(1 << rank)) != 0).sum()
+        bound = torch.tensor([store.kahn_sent(), 2 * int(sum(bin(int(m)).count("1") - 1 for m in masks[gid]))],
+                             dtype=torch.int64)
+        assert bound[0] <= bound[1] and (others == 0 or bound[0] > 0), bound
+        assert store.kahn_bytes == 8 * store.kahn_sent()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_kahn_level_waves_over_gloo():
+    # uniform keys (C5-like, shallow) and Zipf hot keys (deep chains crossing both stores)
+    mp.spawn(_kahn_worker, args=(2, _free_port(), 3000, "uniform"), nprocs=2, join=True)
+    mp.spawn(_kahn_worker, args=(2, _free_port(), 2000, "zipf"), nprocs=2, join=True)
 
 
 def _auto_worker(rank, world, port, n, dist_kind, cap):
@@ -240,20 +344,20 @@ def _auto_worker(rank, world, port, n, dist_kind, cap):
         bounds = sharding.even_bounds(0, ks, world)
         masks = sharding.holder_masks(b, bounds)
         local, gid, _ = sharding.slice_for_shard(b, bounds[rank], bounds[rank + 1])
-        store = HostAutoStore(local, gid, masks[gid], n, rank, world, b)
+        store = HostAutoStore(local, gid, masks[gid], sharding.home_stores(b, bounds)[gid], n, rank, world, b)
         rounds = sharding.run_levels_auto(store, sharding.GlooTransport(dist), round_cap=cap)
         want, _ = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_LEVELS).levels()
         assert np.array_equal(store.G[gid].astype(np.uint32), want[gid]), "rank %d: levels differ" % rank
         if dist_kind == "zipf":
             assert rounds == cap + 1, "a deep graph falls back to the one-exchange gather"
         else:
-            assert rounds <= cap, "a shallow graph converges in delta rounds"
+            assert rounds <= cap, "a shallow graph finishes in Kahn waves"
     finally:
         dist.destroy_process_group()
 
 
 def test_auto_levels_rounds_over_gloo():
-    # C5-like uniform keys: the delta rounds converge, no edge exchange
+    # C5-like uniform keys: the Kahn waves finish, no edge exchange
     mp.spawn(_auto_worker, args=(2, _free_port(), 3000, "uniform", 64), nprocs=2, join=True)
 
 
