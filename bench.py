@@ -244,24 +244,42 @@ def end_to_end(eng, batch, steps):
         t0 = time.perf_counter()
         eng.fetch_merged_all(outs)
         t_d2h = time.perf_counter() - t0
-        # the stream: upload of the next batch overlapped with this batch's pipeline
+        # the stream: upload of the next batch overlapped with this batch's pipeline; every call's wall time is
+        # recorded (host_ms) so a slow run names the call that was slow (round 3 saw 2.8 vs 5.8 ms on the same code
+        # and could not say which part moved)
         k = 0
         eng.load_async(pb[k & 1])
-        t0 = time.perf_counter()
+        ph = {"commit": 0.0, "upload_issue": 0.0, "pipeline": 0.0, "fetch_merged": 0.0, "fetch_levels": 0.0}
+        per_step, dev_ms = [], 0.0
+        clock = time.perf_counter
+        t0 = clock()
         for _ in range(steps):
+            a = clock()
             eng.load_commit()
+            b_ = clock()
             k += 1
             eng.load_async(pb[k & 1])
+            c = clock()
             eng.run_pipeline()
+            d = clock()
+            dev_ms += eng.last_times()["total"]
             eng.fetch_merged_all(outs)
+            e = clock()
             eng.fetch_levels(lvo)
-        dt = (time.perf_counter() - t0) / steps
+            f = clock()
+            for key, v in (("commit", b_ - a), ("upload_issue", c - b_), ("pipeline", d - c), ("fetch_merged", e - d),
+                           ("fetch_levels", f - e)):
+                ph[key] += v
+            per_step.append((f - a) * 1e3)
+        dt = (clock() - t0) / steps
         eng.load_commit()
     finally:
         arena.close()
     return {"ms_per_step": dt * 1e3, "value": n / dt, "unit": "txn/s", "h2d_bytes": h2d, "d2h_bytes": d2h,
             "steps": steps, "h2d_GBps": h2d / t_h2d / 1e9, "d2h_GBps": (d2h - 8 * n) / t_d2h / 1e9,
             "h2d_ms": t_h2d * 1e3, "d2h_ms": t_d2h * 1e3,
+            "host_ms_per_step": {k_: round(v * 1e3 / steps, 3) for k_, v in ph.items()},
+            "pipeline_device_ms": dev_ms / steps, "step_ms": [round(x, 3) for x in per_step],
             "what": "pinned host buffers; ad_load_batch_async(batch k+1) || ad_run_pipeline(batch k), "
                     "ad_fetch_merged_all (3 classes, one call) + ad_fetch_levels, ad_load_batch_commit"}
 
@@ -571,7 +589,7 @@ def main():
         mc = {"bound": "hbm", "avg_ms": ms / calls, "launches": calls, "alg_bytes": ab, "achieved_GBps": gbs,
               "frac": gbs / HBM_PEAK_GBS}
     eng.set_trace(0)
-    e2e = end_to_end(eng, batch, max(1, min(args.steps, 3))) if args.e2e and Q == 0 else None
+    e2e = end_to_end(eng, batch, max(1, min(args.steps, 5))) if args.e2e and Q == 0 else None
     ms_per_step = dt * 1e3 / args.steps
     value = n * args.steps / dt
     pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st, Q) / (dt / args.steps) / 1e9

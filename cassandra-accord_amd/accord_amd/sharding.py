@@ -712,10 +712,20 @@ def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
         return round_cap + 1
 
 
+def kahn_coord(g, holders):
+    """The store that coordinates txn g in the Kahn waves (csrc/kahn_shard_kernels.h ks_coord): the
+    (g mod holders)-th set bit of its holder mask."""
+    k, m = int(g) % bin(int(holders)).count("1"), int(holders)
+    for _ in range(k):
+        m &= m - 1
+    return (m & -m).bit_length() - 1
+
+
 def run_levels_kahn(store, transport, wave_cap=None, lap=None):
     """Distributed Kahn waves (ad_shard_kahn_*, csrc/kahn_shard_kernels.h): wave l moves the READYs of the rows whose
-    local predecessors are all released to their home stores, the home stores release the txns every holder
-    reported (level l) and send RELEASE to the holders, which record the level and free their successors.  Stops
+    local predecessors are all released to their coordinators (kahn_coord: one holder per txn, spread evenly), the
+    coordinators release the txns every holder reported (level l) and send RELEASE to the holders, which record
+    the level and free their successors.  Stops
     after the first wave that released nothing anywhere; raises LevelsNotConverged past wave_cap waves (all stores
     together).  Sets store.depth and store.kahn_bytes (8 B per message sent to another store); returns the waves."""
     lap = lap or (lambda name: None)
@@ -723,7 +733,7 @@ def run_levels_kahn(store, transport, wave_cap=None, lap=None):
     lap("levels_local")
     level = 0
     while True:
-        transport.kahn_exchange(store, False)              # READYs -> home stores
+        transport.kahn_exchange(store, False)              # READYs -> coordinators
         rel = store.kahn_decide()
         any_rel = transport.kahn_exchange(store, rel)      # RELEASEs -> holders; status: this store released some
         unreleased = store.kahn_apply(level)

@@ -315,36 +315,43 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
     return it;
 }
 
-// The sequential walk over the blocks (one workgroup; see the file header).  Per block:
-//   setup (all waves)  singleton runs (a key's only entry in the block): carry-in from the LDS ring of the last
-//                      three blocks' carry-outs or global memory, prefill of the txn's level with that bound (a
-//                      singleton is then final); wave 0 loads its compacted multi-entry run entries and their
-//                      heads' carry-ins and prefills those bounds;
-//   rounds (wave 0)    bl_rounds, whose end writes the multi-entry runs' carry-outs; meanwhile waves 1-3 stage
-//                      the NEXT block's records, compacted entries, global carry-ins and order slice into LDS, so
-//                      no global load latency sits on the sequential path;
-//   out (all waves)    carry-out of the singleton runs (ring; global memory for keys whose next run is >= 3
-//                      blocks away) and the levels.
-// Global carries are written and read by this one workgroup (one CU): workgroup-scope ordering suffices.  A
-// block's global stores are released (fence) at the end of the NEXT block, and read no earlier than the
-// staging during the block after that.
+// The sequential walk over the blocks (one workgroup; see the file header), pipelined so that only the rounds and
+// two short LDS phases sit on the sequential path.  Wave 0 runs the rounds (W0); waves 1-3 are the workers.  Per
+// block b:
+//   R_b   W0: rounds(b), then the carry-outs of b's multi-entry runs (ring; global memory for keys whose next run is
+//         >= 3 blocks away).  Workers, meanwhile: load block b + 1 (records, compacted entries, order slice, then the
+//         dependent global carry-ins, all issued before any is used) and prefill its txn levels from every head
+//         whose carry does not come from the ring (a singleton run is then final), flag its non-last entries.
+//   P1_b  workers: the carry-outs of b's singleton runs (ring, global) and b's levels into L.
+//   P2_b  all: clear the level buffer block b + 2 will use; block b + 1's heads whose carry comes from the ring
+//         (their key's previous run ended in block b or b - 1) resolve it and prefill.
+// Levels / flags live in three buffers by b % 3; staged block data in two by b % 2.  Global carries are written and
+// read by this one workgroup (one CU): workgroup-scope ordering suffices; every thread releases (fence) its earlier
+// global carry stores at the start of each R phase (W0's were issued at the end of the previous rounds, the
+// workers' in the previous P1: both complete by then in practice, so the fence costs W0 nothing), and a key's
+// global carry is read by the staging of a block at least three blocks later, after that fence and two barriers.
 // stats[0] = greatest level + 1, stats[1] = rounds, stats[2..3] = clock64 in rounds, stats[4..5] = total,
-// stats[6] = a block's rounds did not converge, stats[7..9] = clock64 / 256 in setup, waiting for the staging
-// waves after the rounds, and out (thread 0).
-// The loads are issued for all of a thread's slots before any is used (records, compacted entries and order slice
-// first, then the dependent global carry-ins), so the staging costs two memory round trips instead of two per slot
-// (it ran 2,900 cycles per C3 block past the rounds when each slot waited for its own loads).
-constexpr int BL_SI = (BL_CAP + (BL_T - WAVE) - 1) / (BL_T - WAVE);   // slots per staging thread (3 waves)
+// stats[6] = a block's rounds did not converge, stats[7..9] = clock64 / 256 waiting for the workers after the
+// rounds, in P1 and in P2 (thread 0).
+constexpr int BL_SI = (BL_CAP + (BL_T - WAVE) - 1) / (BL_T - WAVE);   // slots per worker thread (3 waves)
 __device__ inline int2 bl_carry_load(const int2* carry, uint32_t slot) {
     const int* g = reinterpret_cast<const int*>(&carry[slot]);
     return make_int2(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
                      __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-__device__ inline void bl_stage(uint32_t b, uint32_t B, int t, int nthr, const uint32_t* __restrict__ boff,
-                                const uint32_t* __restrict__ tb, const uint64_t* __restrict__ rec, const uint4* __restrict__ crec,
-                                const uint32_t* __restrict__ mt, const int2* carry, const uint32_t* __restrict__ order,
-                                uint64_t* srec, int2* scar, uint32_t* sord, uint4* scr, int2* shc, uint32_t* sbnd) {
-    if (b >= B) return;
+struct BlStage {                               // one block's staged data in LDS (two of these, by block parity)
+    uint64_t rec[BL_CAP];                      // slot records (~0: none)
+    int2 car[BL_CAP];                          // singleton runs' carry-in (src 1: resolved in P2)
+    uint32_t ord[BL_CAP];                      // txn of each txn slot
+    uint4 cr[BL_CAP];                          // compacted multi-entry run entries
+    int2 hc[BL_CAP];                           // their heads' carry-in (-2: from the ring, resolved in P2)
+    uint32_t bnd[5];                           // j0, j1, t0, t1, compacted entries
+};
+// Load block b into `s` and prefill its levels (lv / nl: its buffers) from every head whose carry is known now.
+__device__ inline void bl_stage_prefill(uint32_t b, int t, int nthr, const uint32_t* __restrict__ boff,
+                                        const uint32_t* __restrict__ tb, const uint64_t* __restrict__ rec,
+                                        const uint4* __restrict__ crec, const uint32_t* __restrict__ mt, const int2* carry,
+                                        const uint32_t* __restrict__ order, BlStage& s, int* lv, uint8_t* nl) {
     const uint32_t j0 = boff[b], j1 = boff[b + 1], t0 = tb[b], t1 = tb[b + 1], m = mt[b];
     uint64_t r[BL_SI];
     uint4 q[BL_SI];
@@ -363,25 +370,40 @@ __device__ inline void bl_stage(uint32_t b, uint32_t B, int t, int nthr, const u
         c[i] = make_int2(-1, -1);
         h[i] = make_int2(-1, -1);
         const uint32_t f = (uint32_t)(r[i] >> 32);
-        // singleton heads' global carry-ins (the multi-entry runs' heads are staged with their compacted entries)
         if (r[i] != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) && ((f >> BL_SH_SRC) & 3u) == 2u)
             c[i] = bl_carry_load(carry, (uint32_t)r[i]);
         if (x < m && ((q[i].x >> BL_SH_HEAD) & 1u)) {
             const uint32_t src = (q[i].x >> BL_SH_SRC) & 3u;
             if (src == 2u) h[i] = bl_carry_load(carry, q[i].z);
-            else if (src == 1u) h[i] = make_int2(-2, (int)q[i].w);   // resolved from the ring at setup (ring index)
+            else if (src == 1u) h[i] = make_int2(-2, (int)q[i].w);
         }
     }
 #pragma unroll
     for (int i = 0; i < BL_SI; ++i) {
         const uint32_t x = (uint32_t)(t + i * nthr);
         if (x >= (uint32_t)BL_CAP) continue;
-        srec[x] = r[i];
-        scar[x] = c[i];
-        sord[x] = o[i];
-        if (x < m) { scr[x] = q[i]; shc[x] = h[i]; }
+        s.rec[x] = r[i];
+        s.car[x] = c[i];
+        s.ord[x] = o[i];
+        const uint32_t f = (uint32_t)(r[i] >> 32);
+        if (r[i] != ~0ull) {
+            const bool head = f & (1u << BL_SH_HEAD), last = f & (1u << BL_SH_LAST);
+            if (head && last && ((f >> BL_SH_SRC) & 3u) != 1u) {
+                const int lb = (f & (1u << BL_SH_W)) ? c[i].x + 1 : c[i].y + 1;
+                if (lb > 0) atomicMax(&lv[f & BL_TL], lb);
+            }
+            if (!last) nl[f & BL_TL] = 1;
+        }
+        if (x < m) {
+            s.cr[x] = q[i];
+            s.hc[x] = h[i];
+            if (((q[i].x >> BL_SH_HEAD) & 1u) && h[i].x != -2) {
+                const int lb = ((q[i].x >> BL_SH_W) & 1u) ? h[i].x + 1 : h[i].y + 1;
+                if (lb > 0) atomicMax(&lv[q[i].x & BL_TL], lb);
+            }
+        }
     }
-    if (t == 0) { sbnd[0] = j0; sbnd[1] = j1; sbnd[2] = t0; sbnd[3] = t1; sbnd[4] = m; }
+    if (t == 0) { s.bnd[0] = j0; s.bnd[1] = j1; s.bnd[2] = t0; s.bnd[3] = t1; s.bnd[4] = m; }
 }
 
 template <class PK>
@@ -390,141 +412,121 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
                                                        const uint32_t* __restrict__ mt, int2* carry,
                                                        const uint32_t* __restrict__ order, uint32_t* __restrict__ L,
                                                        uint32_t* __restrict__ stats) {
-    __shared__ int lvb[2][BL_CAP + WAVE];      // levels of the block's txns (txn-in-block index), by block parity;
+    __shared__ int lvb[3][BL_CAP + WAVE];      // levels of a block's txns (txn-in-block index), by block % 3;
                                                // [BL_CAP + lane]: sinks of the rounds' absent entries
-    __shared__ uint8_t nlb[2][BL_CAP + WAVE];     // txn has an entry that is not its key's last in the block
+    __shared__ uint8_t nlb[3][BL_CAP + WAVE];     // txn has an entry that is not its key's last in the block
     __shared__ int2 ring[3 * BL_CAP];          // carry-out of every slot of the last three blocks
-    __shared__ uint4 scrb[2][BL_CAP];          // compacted multi-entry run entries (by block parity: the next
-    __shared__ int2 shcb[2][BL_CAP];           //   block's are staged while this one's rounds run), their heads'
-                                               //   carry-ins (-2: from the ring); staged next block:
-    __shared__ uint64_t srec[BL_CAP];          //   records, singleton global carry-ins, order slice
-    __shared__ int2 scar[BL_CAP];
-    __shared__ uint32_t sord[BL_CAP];
-    __shared__ uint32_t sbnd[5];
+    __shared__ BlStage stg[2];
     __shared__ uint32_t sstuck;
     const int tid = threadIdx.x, lane = __lane_id();
     if (tid == 0) sstuck = 0u;
     const uint64_t tstart = clock64();
-    uint64_t tround = 0;
-    for (int x = tid; x < BL_CAP + WAVE; x += BL_T) { lvb[0][x] = lvb[1][x] = 0; nlb[0][x] = nlb[1][x] = 0; }
+    uint64_t tround = 0, twait = 0, tp1 = 0, tp2 = 0;
+    for (int x = tid; x < BL_CAP + WAVE; x += BL_T) {
+        lvb[0][x] = lvb[1][x] = lvb[2][x] = 0;
+        nlb[0][x] = nlb[1][x] = nlb[2][x] = 0;
+    }
+    __syncthreads();
     int maxl = -1;
     uint32_t rounds = 0;
-    bl_stage(0, B, tid, BL_T, boff, tb, rec, crec, mt, carry, order, srec, scar, sord, scrb[0], shcb[0], sbnd);
-    uint32_t pfl[BL_EPT];
-#pragma unroll
-    for (int e = 0; e < BL_EPT; ++e) pfl[e] = BL_NONE;
+    if (B > 0) bl_stage_prefill(0, tid, BL_T, boff, tb, rec, crec, mt, carry, order, stg[0], lvb[0], nlb[0]);   // no ring sources
     __syncthreads();
-    uint64_t tsetup = 0, twait = 0, tout = 0;          // clock64 per phase (thread 0), AD_DEBUG_LEVELS
     for (uint32_t b = 0; b < B; ++b) {
-        const uint64_t tb0 = clock64();
-        const int pb = b & 1;
-        int* lv = lvb[pb];
-        uint8_t* nl = nlb[pb];
-        uint4* scr = scrb[pb];
-        int2* shc = shcb[pb];
-        const uint32_t nt = sbnd[3] - sbnd[2];
-        const int nm = (int)sbnd[4];
+        BlStage& S = stg[b & 1];
+        int* lv = lvb[b % 3];
+        uint8_t* nl = nlb[b % 3];
+        const int nm = (int)S.bnd[4];
+        const uint32_t nt = S.bnd[3] - S.bnd[2];
         const int rb = (int)(b % 3) * BL_CAP;
-        uint32_t fl[BL_EPT], key[BL_EPT], ord[BL_EPT];
-        int yc[BL_EPT], wc[BL_EPT];
-#pragma unroll
-        for (int e = 0; e < BL_EPT; ++e) {
-            const uint64_t r = srec[tid * BL_EPT + e];
-            key[e] = (uint32_t)r;
-            fl[e] = r == ~0ull ? BL_NONE : (uint32_t)(r >> 32);
-            const int2 c = scar[tid * BL_EPT + e];
-            yc[e] = c.x; wc[e] = c.y;
-            ord[e] = sord[tid + e * BL_T];
-        }
-        // ---- setup: clear the previous block's slots (other parity); singleton carry-in + prefill; nl
-#pragma unroll
-        for (int e = 0; e < BL_EPT; ++e)
-            if (pfl[e] != BL_NONE) { lvb[pb ^ 1][pfl[e] & BL_TL] = 0; nlb[pb ^ 1][pfl[e] & BL_TL] = 0; }
-#pragma unroll
-        for (int e = 0; e < BL_EPT; ++e) {
-            const uint32_t f = fl[e];
-            if (f == BL_NONE) continue;
-            const bool head = f & (1u << BL_SH_HEAD), last = f & (1u << BL_SH_LAST);
-            if (head && last) {
-                const uint32_t src = (f >> BL_SH_SRC) & 3u;
-                if (src == 0u) { yc[e] = -1; wc[e] = -1; }
-                else if (src == 1u) { const int2 c = ring[f >> BL_SH_RING]; yc[e] = c.x; wc[e] = c.y; }
-                const int lb = (f & (1u << BL_SH_W)) ? yc[e] + 1 : wc[e] + 1;
-                if (lb > 0) atomicMax(&lv[f & BL_TL], lb);
-            }
-            if (!last) nl[f & BL_TL] = 1;
-        }
-        // the multi-entry runs' heads (all waves): carry-in (ring sources resolved here) and prefill
-        for (int k = tid; k < nm; k += BL_T) {
-            const uint4 q = scr[k];
-            if (!((q.x >> BL_SH_HEAD) & 1u)) continue;
-            int2 h = shc[k];
-            if ((q.x >> BL_SH_SRC & 3u) == 0u) h = make_int2(-1, -1);
-            else if (h.x == -2) h = ring[h.y];
-            shc[k] = h;
-            const int lb = ((q.x >> BL_SH_W) & 1u) ? h.x + 1 : h.y + 1;
-            if (lb > 0) atomicMax(&lv[q.x & BL_TL], lb);
-        }
-        __syncthreads();
-        const uint64_t tb1 = clock64();
-        tsetup += tb1 - tb0;
-        uint64_t tb2 = tb1;
-        // ---- rounds (wave 0) | staging of the next block (waves 1-3)
+        // ---- R_b: rounds (wave 0) | next block's load + prefill (workers).  The fence releases this thread's
+        // global carry stores of block b - 1 (issued two phases ago, so normally complete: no wait on W0's path)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        uint64_t tr1 = clock64();
         if (tid < WAVE) {
             if (nm > 0) {
                 const uint64_t t0 = clock64();
                 uint32_t r;
                 const int epl = (nm + WAVE - 1) / WAVE;        // entries per lane
-                if (epl <= 2) r = bl_rounds<2, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 3) r = bl_rounds<3, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 4) r = bl_rounds<4, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 5) r = bl_rounds<5, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 6) r = bl_rounds<6, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 8) r = bl_rounds<8, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 12) r = bl_rounds<12, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                else r = bl_rounds<16, PK>(nm, scr, shc, lv, nl, ring, rb, carry, &sstuck);
-                tb2 = clock64();
-                tround += tb2 - t0;
+                if (epl <= 2) r = bl_rounds<2, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 3) r = bl_rounds<3, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 4) r = bl_rounds<4, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 5) r = bl_rounds<5, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 6) r = bl_rounds<6, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 8) r = bl_rounds<8, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else if (epl <= 12) r = bl_rounds<12, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                else r = bl_rounds<16, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
+                tr1 = clock64();
+                tround += tr1 - t0;
                 rounds += r;
             }
-        } else {
-            bl_stage(b + 1, B, tid - WAVE, BL_T - WAVE, boff, tb, rec, crec, mt, carry, order, srec, scar, sord, scrb[pb ^ 1],
-                     shcb[pb ^ 1], sbnd);
+        } else if (b + 1 < B) {
+            bl_stage_prefill(b + 1, tid - WAVE, BL_T - WAVE, boff, tb, rec, crec, mt, carry, order, stg[(b + 1) & 1],
+                             lvb[(b + 1) % 3], nlb[(b + 1) % 3]);
         }
         __syncthreads();
-        const uint64_t tb3 = clock64();
-        twait += tb3 - tb2;
-        // ---- out: carry-out of the singleton runs, levels.  The fence first releases the previous block's
-        // global carries (issued a block ago) before this block's are issued.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#pragma unroll
-        for (int e = 0; e < BL_EPT; ++e) {
-            const uint32_t f = fl[e];
-            if (f == BL_NONE) continue;
+        const uint64_t tq1 = clock64();
+        twait += tq1 - tr1;
+        // ---- P1_b (workers): singleton runs' carry-outs, b's levels (W0 issues no global stores here: a store's
+        // completion would sit on its path at the next fence)
+        for (int x = tid - WAVE; x >= 0 && x < BL_CAP; x += BL_T - WAVE) {
+            const uint64_t rr = S.rec[x];
+            if (rr == ~0ull) continue;
+            const uint32_t f = (uint32_t)(rr >> 32);
             if ((f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST))) {
-                const int x = lv[f & BL_TL];
-                const int2 c = make_int2(max(yc[e], x), (f & (1u << BL_SH_W)) ? x : wc[e]);
-                ring[rb + tid * BL_EPT + e] = c;
+                const int2 ci = S.car[x];
+                const int l = lv[f & BL_TL];
+                const int2 c = make_int2(max(ci.x, l), (f & (1u << BL_SH_W)) ? l : ci.y);
+                ring[rb + x] = c;
                 if (f & (1u << BL_SH_G)) {
-                    int* g = reinterpret_cast<int*>(&carry[key[e]]);
+                    int* g = reinterpret_cast<int*>(&carry[(uint32_t)rr]);
                     __hip_atomic_store(g, c.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(g + 1, c.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
+        for (int x = tid - WAVE; x >= 0 && (uint32_t)x < nt; x += BL_T - WAVE) {
+            const int l = lv[x];
+            L[S.ord[x]] = (uint32_t)l;
+            maxl = max(maxl, l);
+        }
+        __syncthreads();
+        const uint64_t tq2 = clock64();
+        tp1 += tq2 - tq1;
+        // ---- P2_b: clear the buffers of block b + 2 (last used by b - 1); b + 1's ring-sourced heads
+        {
+            int* lc = lvb[(b + 2) % 3];
+            uint8_t* nc = nlb[(b + 2) % 3];
+            for (int x = tid; x < BL_CAP + WAVE; x += BL_T) { lc[x] = 0; nc[x] = 0; }
+        }
+        if (b + 1 < B) {
+            BlStage& N = stg[(b + 1) & 1];
+            int* lvn = lvb[(b + 1) % 3];
 #pragma unroll
-        for (int e = 0; e < BL_EPT; ++e) {
-            const uint32_t x = (uint32_t)(tid + e * BL_T);
-            if (x < nt) {
-                const int l = lv[x];
-                L[ord[e]] = (uint32_t)l;
-                maxl = max(maxl, l);
+            for (int e = 0; e < BL_EPT; ++e) {
+                const int x = tid * BL_EPT + e;
+                const uint64_t rr = N.rec[x];
+                if (rr == ~0ull) continue;
+                const uint32_t f = (uint32_t)(rr >> 32);
+                if ((f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) && ((f >> BL_SH_SRC) & 3u) == 1u) {
+                    const int2 c = ring[f >> BL_SH_RING];
+                    N.car[x] = c;
+                    const int lb = (f & (1u << BL_SH_W)) ? c.x + 1 : c.y + 1;
+                    if (lb > 0) atomicMax(&lvn[f & BL_TL], lb);
+                }
+            }
+            const int mn = (int)N.bnd[4];
+            for (int k = tid; k < mn; k += BL_T) {
+                const int2 h = N.hc[k];
+                if (h.x != -2) continue;
+                const uint4 q = N.cr[k];
+                const int2 c = ring[h.y];
+                N.hc[k] = c;
+                const int lb = ((q.x >> BL_SH_W) & 1u) ? c.x + 1 : c.y + 1;
+                if (lb > 0) atomicMax(&lvn[q.x & BL_TL], lb);
             }
         }
-#pragma unroll
-        for (int e = 0; e < BL_EPT; ++e) pfl[e] = fl[e];
         __syncthreads();
-        tout += clock64() - tb3;
+        tp2 += clock64() - tq2;
         if (sstuck) break;
     }
     maxl = wave_max(maxl);
@@ -535,7 +537,7 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         stats[2] = (uint32_t)tround; stats[3] = (uint32_t)(tround >> 32);
         stats[4] = (uint32_t)tot; stats[5] = (uint32_t)(tot >> 32);
         stats[6] = sstuck;
-        stats[7] = (uint32_t)(tsetup >> 8); stats[8] = (uint32_t)(twait >> 8); stats[9] = (uint32_t)(tout >> 8);
+        stats[7] = (uint32_t)(twait >> 8); stats[8] = (uint32_t)(tp1 >> 8); stats[9] = (uint32_t)(tp2 >> 8);
     }
 }
 

@@ -1,6 +1,6 @@
 // shard_kahn.hip — execution levels of a key-range sharded batch by distributed Kahn wavefronts
 // (kahn_shard_kernels.h has the protocol).  Per wave the host moves two message sets between the stores: READYs
-// (to the txn's home store) and RELEASEs (from the home store to every holder).  RCCL moves them device to device
+// (to the txn's coordinator, one of its holders) and RELEASEs (from the coordinator to every holder).  RCCL moves them device to device
 // (ad_shard_kahn_exchange: per-destination counts + a status word all-gathered, then grouped send/recv); host
 // transports use ad_shard_kahn_outbox / ad_shard_kahn_inbox.
 #include "engine_internal.h"
@@ -53,11 +53,15 @@ int ad_shard_kahn_begin(ad_handle* h) {
     CK(dalloc(h, S_KSREM, &h->ks_rem, n1)); CK(dalloc(h, S_KSXOFF, &h->ks_xoff, n + 1));
     CK(dalloc(h, S_KSRCNT, &h->ks_rcnt, n1)); CK(dalloc(h, S_KSFL, &h->ks_flag, 16));
     CK(dalloc(h, S_KSBASE, &h->ks_base_dev, 2 * (MAX_STORES + 1))); CK(dalloc(h, S_KSCNT, &h->ks_cnt_dev, MAX_STORES + 1));
-    // outbox regions: READY to d <= local rows homed at d; RELEASE to d <= home rows d also holds
+    // outbox regions: READY to d <= local rows d coordinates; RELEASE to d <= rows this store coordinates that d holds
+    std::vector<uint32_t> gids(n);
+    if (n) HIPCHK(h, hipMemcpyAsync(gids.data(), h->gid, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
     std::vector<uint64_t> rc(W, 0), lc(W, 0);
     for (size_t i = 0; i < n; ++i) {
-        rc[h->home_host[i]]++;
-        if (h->home_host[i] == h->self)
+        const uint32_t c = ks_coord(gids[i], h->holders_host[i]);
+        rc[c]++;
+        if (c == h->self)
             for (uint32_t d = 0; d < W; ++d) lc[d] += (h->holders_host[i] >> d) & 1u;
     }
     h->ks_base.assign(2 * (MAX_STORES + 1), 0);
@@ -82,7 +86,7 @@ int ad_shard_kahn_begin(ad_handle* h) {
         HIPCHK(h, hipMemsetAsync(h->ks_xoff, 0, (n + 1) * 8, st));
     }
     HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
-    if (n) k_ks_init<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->hstore, h->ks_rem, h->lvl, h->ks_rcnt,
+    if (n) k_ks_init<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->holders, h->ks_rem, h->lvl, h->ks_rcnt,
                                                              ks_base(h, 0), h->ks_cnt_dev, h->ks_out);
     HIPCHK(h, hipGetLastError());
     CK(ks_bad(h, "ad_shard_kahn_begin: a level edge out of range or a self edge"));
@@ -184,7 +188,7 @@ int ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status) 
     return AD_OK;
 }
 
-// Home store: the received READYs counted; txns every holder reported are released (this wave) and their
+// Coordinator: the received READYs counted; txns every holder reported are released (this wave) and their
 // RELEASEs fill the outbox.  *released: this store released some txn.
 int ad_shard_kahn_decide(ad_handle* h, uint32_t* released) {
     if (!h || !released) return AD_ERR_ARGUMENT;
@@ -195,14 +199,14 @@ int ad_shard_kahn_decide(ad_handle* h, uint32_t* released) {
     HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->ks_flag, 0, 4, st));
     const size_t m = h->ks_in_m;
-    if (m) k_ks_decide<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, h->gid, h->home, h->holders, h->ks_rcnt,
+    if (m) k_ks_decide<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, h->gid, h->self, h->holders, h->ks_rcnt,
                                                                ks_base(h, 1), h->ks_cnt_dev, h->ks_out, h->ks_flag,
                                                                h->ks_flag + 2);
     HIPCHK(h, hipGetLastError());
     uint32_t f[3] = {0, 0, 0};
     HIPCHK(h, hipMemcpyAsync(f, h->ks_flag, 12, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
-    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_decide: a READY for a txn this store does not home");
+    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_decide: a READY for a txn this store does not coordinate");
     *released = f[0] ? 1u : 0u;
     h->ks_phase = 1;
     h->ks_in_m = 0;
@@ -220,7 +224,7 @@ int ad_shard_kahn_apply(ad_handle* h, uint32_t level, uint64_t* unreleased) {
     HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->ks_flag + 1, 0, 4, st));
     const size_t m = h->ks_in_m;
-    if (m) k_ks_apply<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, level, h->gid, h->hstore, h->ks_xoff, h->ks_xs,
+    if (m) k_ks_apply<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, level, h->gid, h->holders, h->ks_xoff, h->ks_xs,
                                                               h->ks_rem, h->lvl, ks_base(h, 0), h->ks_cnt_dev, h->ks_out,
                                                               h->ks_flag, h->ks_flag + 2);
     HIPCHK(h, hipGetLastError());

@@ -9,7 +9,8 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 rc=0
-timeout -k 10 ${TEST_LIMIT:-900} python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${@:-tests} \
+[ $# -gt 0 ] || set -- tests
+timeout -k 10 ${TEST_LIMIT:-900} python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$@" \
     > "$OUT/tests.log" 2>&1 || rc=$?
 echo "tests rc=$rc"; tail -3 "$OUT/tests.log"
 [ $rc -le 1 ] || exit $rc

@@ -211,13 +211,16 @@ def test_holder_masks():
 class HostKahnStore:
     """Host model of ad_shard_kahn_begin / _decide / _apply (csrc/kahn_shard_kernels.h) for pure key batches of
     Reads and Writes: the store's own constraint edges (HostEdgeStore.level_edges, the engine's
-    levels_export_edges) over its local rows, READY to the home store when a row's last local predecessor was
-    released, RELEASE from the home store to every holder once all holders reported."""
+    levels_export_edges) over its local rows, READY to the txn's coordinator (sharding.kahn_coord) when a row's last
+    local predecessor was released, RELEASE from the coordinator to every holder once all holders reported."""
 
     delta = True
 
     def __init__(self, local, gid, holders, home, n_global, rank, world, glob):
-        self.gid, self.holders, self.home = gid, holders.astype(np.int64), home
+        sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+        from accord_amd import sharding
+        self.gid, self.holders = gid, holders.astype(np.int64)
+        self.home = np.array([sharding.kahn_coord(g, m) for g, m in zip(gid, holders)], np.int64)   # coordinators
         self.rank, self.world, self.n_global = rank, world, n_global
         self._edges = HostEdgeStore(local, gid, n_global, glob)
         self.row = {int(g): i for i, g in enumerate(gid)}
@@ -253,7 +256,7 @@ class HostKahnStore:
         rel = False
         for g in self.inbox:
             r = self.row[g]
-            assert int(self.home[r]) == self.rank, "READY only to the home store"
+            assert int(self.home[r]) == self.rank, "READY only to the txn's coordinator"
             self.rcnt[r] += 1
             if self.rcnt[r] == bin(int(self.holders[r])).count("1"):
                 for d in range(self.world):
