@@ -194,6 +194,17 @@ static __global__ __launch_bounds__(BL_T) void k_bl_compact(uint32_t B, const ui
     if (tid == 0) mt[b] = (uint32_t)(total >> 34);
 }
 
+// a key's global carry (y, w) moves as one 8-byte word: one memory transaction per carry instead of two
+__device__ inline int2 bl_carry_load(const int2* carry, uint32_t slot) {
+    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&carry[slot]), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+}
+__device__ inline void bl_carry_store(int2* carry, uint32_t slot, int2 c) {
+    const uint64_t v = (uint64_t)(uint32_t)c.x | ((uint64_t)(uint32_t)c.y << 32);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(&carry[slot]), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Packed scan words: segment id in the high bits, value + BZ_BIAS in the low bits (u32: values < 2^20, i.e.
 // batches of <= 2^20 txns; u64 otherwise).  The word 0 is below every real entry's (ids count from 1).
 constexpr int BZ_BIAS = 1 << 12;
@@ -306,11 +317,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
         const PK my = iny > iy[e] ? iny : iy[e], mw = inw > iw[e] ? inw : iw[e];
         const int2 o = make_int2(bz_val<PK>(my), bz_val<PK>(mw));
         ring[rb + (int)(c.y >> 22)] = o;
-        if ((c.x >> BL_SH_G) & 1u) {
-            int* g = reinterpret_cast<int*>(&carry[c.z]);
-            __hip_atomic_store(g, o.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(g + 1, o.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        if ((c.x >> BL_SH_G) & 1u) bl_carry_store(carry, c.z, o);
     }
     return it;
 }
@@ -334,11 +341,11 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
 // stats[6] = a block's rounds did not converge, stats[7..9] = clock64 / 256 waiting for the workers after the
 // rounds, in P1 and in P2 (thread 0).
 constexpr int BL_SI = (BL_CAP + (BL_T - WAVE) - 1) / (BL_T - WAVE);   // slots per worker thread (3 waves)
-__device__ inline int2 bl_carry_load(const int2* carry, uint32_t slot) {
-    const int* g = reinterpret_cast<const int*>(&carry[slot]);
-    return make_int2(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
-                     __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for the wave's outstanding global stores
+// (s_waitcnt vmcnt(0)), which put every block's level and carry stores (~1-2 us to complete) on the sequential
+// path: 23 M of the walk's 78 M clocks on C3.  Global carries get their own release fence (top of each R phase).
+__device__ inline void bl_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 struct BlStage {                               // one block's staged data in LDS (two of these, by block parity)
     uint64_t rec[BL_CAP];                      // slot records (~0: none)
     int2 car[BL_CAP];                          // singleton runs' carry-in (src 1: resolved in P2)
@@ -421,7 +428,7 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
     const int tid = threadIdx.x, lane = __lane_id();
     if (tid == 0) sstuck = 0u;
     const uint64_t tstart = clock64();
-    uint64_t tround = 0, twait = 0, tp1 = 0, tp2 = 0;
+    uint64_t tround = 0, twait = 0, tp1 = 0, tp2 = 0, tp2w = 0, tp1w = 0;
     for (int x = tid; x < BL_CAP + WAVE; x += BL_T) {
         lvb[0][x] = lvb[1][x] = lvb[2][x] = 0;
         nlb[0][x] = nlb[1][x] = nlb[2][x] = 0;
@@ -463,36 +470,53 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
             bl_stage_prefill(b + 1, tid - WAVE, BL_T - WAVE, boff, tb, rec, crec, mt, carry, order, stg[(b + 1) & 1],
                              lvb[(b + 1) % 3], nlb[(b + 1) % 3]);
         }
-        __syncthreads();
+        bl_barrier();
         const uint64_t tq1 = clock64();
         twait += tq1 - tr1;
+        const uint64_t tw0 = clock64();
         // ---- P1_b (workers): singleton runs' carry-outs, b's levels (W0 issues no global stores here: a store's
-        // completion would sit on its path at the next fence)
-        for (int x = tid - WAVE; x >= 0 && x < BL_CAP; x += BL_T - WAVE) {
-            const uint64_t rr = S.rec[x];
-            if (rr == ~0ull) continue;
-            const uint32_t f = (uint32_t)(rr >> 32);
-            if ((f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST))) {
-                const int2 ci = S.car[x];
-                const int l = lv[f & BL_TL];
-                const int2 c = make_int2(max(ci.x, l), (f & (1u << BL_SH_W)) ? l : ci.y);
-                ring[rb + x] = c;
-                if (f & (1u << BL_SH_G)) {
-                    int* g = reinterpret_cast<int*>(&carry[(uint32_t)rr]);
-                    __hip_atomic_store(g, c.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_store(g + 1, c.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // completion would sit on its path at the next fence).  Every LDS load of a thread's slots is issued before
+        // any is used (one round trip per dependent step, not per slot).
+        if (tid >= WAVE) {
+            const int t = tid - WAVE;
+            uint64_t rr[BL_SI];
+            uint32_t od[BL_SI];
+            int2 ci[BL_SI];
+            int ls[BL_SI], lo[BL_SI];
+#pragma unroll
+            for (int i = 0; i < BL_SI; ++i) {
+                const int x = t + i * (BL_T - WAVE);
+                rr[i] = x < BL_CAP ? S.rec[x] : ~0ull;
+                ci[i] = x < BL_CAP ? S.car[x] : make_int2(-1, -1);
+                od[i] = (uint32_t)x < nt ? S.ord[x] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < BL_SI; ++i) {
+                const int x = t + i * (BL_T - WAVE);
+                ls[i] = rr[i] != ~0ull ? lv[(uint32_t)(rr[i] >> 32) & BL_TL] : 0;
+                lo[i] = (uint32_t)x < nt ? lv[x] : -1;
+            }
+#pragma unroll
+            for (int i = 0; i < BL_SI; ++i) {
+                const int x = t + i * (BL_T - WAVE);
+                const uint32_t f = (uint32_t)(rr[i] >> 32);
+                if (rr[i] != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST))) {
+                    const int2 c = make_int2(max(ci[i].x, ls[i]), (f & (1u << BL_SH_W)) ? ls[i] : ci[i].y);
+                    ring[rb + x] = c;
+                    if (f & (1u << BL_SH_G)) bl_carry_store(carry, (uint32_t)rr[i], c);
+                }
+                if ((uint32_t)x < nt) {
+                    L[od[i]] = (uint32_t)lo[i];
+                    maxl = max(maxl, lo[i]);
                 }
             }
         }
-        for (int x = tid - WAVE; x >= 0 && (uint32_t)x < nt; x += BL_T - WAVE) {
-            const int l = lv[x];
-            L[S.ord[x]] = (uint32_t)l;
-            maxl = max(maxl, l);
-        }
-        __syncthreads();
+        tp1w += clock64() - tw0;
+        bl_barrier();
         const uint64_t tq2 = clock64();
         tp1 += tq2 - tq1;
-        // ---- P2_b: clear the buffers of block b + 2 (last used by b - 1); b + 1's ring-sourced heads
+        // ---- P2_b: clear the buffers of block b + 2 (last used by b - 1); b + 1's ring-sourced heads (loads
+        // first, as in P1)
         {
             int* lc = lvb[(b + 2) % 3];
             uint8_t* nc = nlb[(b + 2) % 3];
@@ -501,31 +525,51 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         if (b + 1 < B) {
             BlStage& N = stg[(b + 1) & 1];
             int* lvn = lvb[(b + 1) % 3];
+            uint64_t rr[BL_EPT];
+            int2 rc[BL_EPT];
+#pragma unroll
+            for (int e = 0; e < BL_EPT; ++e) rr[e] = N.rec[tid * BL_EPT + e];
 #pragma unroll
             for (int e = 0; e < BL_EPT; ++e) {
-                const int x = tid * BL_EPT + e;
-                const uint64_t rr = N.rec[x];
-                if (rr == ~0ull) continue;
-                const uint32_t f = (uint32_t)(rr >> 32);
-                if ((f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) && ((f >> BL_SH_SRC) & 3u) == 1u) {
-                    const int2 c = ring[f >> BL_SH_RING];
-                    N.car[x] = c;
-                    const int lb = (f & (1u << BL_SH_W)) ? c.x + 1 : c.y + 1;
-                    if (lb > 0) atomicMax(&lvn[f & BL_TL], lb);
-                }
+                const uint32_t f = (uint32_t)(rr[e] >> 32);
+                const bool want = rr[e] != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) &&
+                                  ((f >> BL_SH_SRC) & 3u) == 1u;
+                rc[e] = want ? ring[f >> BL_SH_RING] : make_int2(-3, -3);
+            }
+#pragma unroll
+            for (int e = 0; e < BL_EPT; ++e) {
+                if (rc[e].x == -3) continue;
+                const uint32_t f = (uint32_t)(rr[e] >> 32);
+                N.car[tid * BL_EPT + e] = rc[e];
+                const int lb = (f & (1u << BL_SH_W)) ? rc[e].x + 1 : rc[e].y + 1;
+                if (lb > 0) atomicMax(&lvn[f & BL_TL], lb);
             }
             const int mn = (int)N.bnd[4];
-            for (int k = tid; k < mn; k += BL_T) {
-                const int2 h = N.hc[k];
-                if (h.x != -2) continue;
-                const uint4 q = N.cr[k];
-                const int2 c = ring[h.y];
-                N.hc[k] = c;
-                const int lb = ((q.x >> BL_SH_W) & 1u) ? c.x + 1 : c.y + 1;
-                if (lb > 0) atomicMax(&lvn[q.x & BL_TL], lb);
+            int2 hh[BL_EPT];
+#pragma unroll
+            for (int e = 0; e < BL_EPT; ++e) {
+                const int k = tid + e * BL_T;
+                hh[e] = k < mn ? N.hc[k] : make_int2(-1, -1);
+            }
+            uint32_t qx[BL_EPT];
+#pragma unroll
+            for (int e = 0; e < BL_EPT; ++e) {
+                const int k = tid + e * BL_T;
+                qx[e] = hh[e].x == -2 ? N.cr[k].x : 0u;
+                hh[e] = hh[e].x == -2 ? ring[hh[e].y] : make_int2(-3, -3);
+            }
+#pragma unroll
+            for (int e = 0; e < BL_EPT; ++e) {
+                if (hh[e].x == -3) continue;
+                const int k = tid + e * BL_T;
+                N.hc[k] = hh[e];
+                const int lb = ((qx[e] >> BL_SH_W) & 1u) ? hh[e].x + 1 : hh[e].y + 1;
+                if (lb > 0) atomicMax(&lvn[qx[e] & BL_TL], lb);
             }
         }
-        __syncthreads();
+        const uint64_t tq3 = clock64();
+        tp2w += tq3 - tq2;
+        bl_barrier();
         tp2 += clock64() - tq2;
         if (sstuck) break;
     }
@@ -538,7 +582,9 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         stats[4] = (uint32_t)tot; stats[5] = (uint32_t)(tot >> 32);
         stats[6] = sstuck;
         stats[7] = (uint32_t)(twait >> 8); stats[8] = (uint32_t)(tp1 >> 8); stats[9] = (uint32_t)(tp2 >> 8);
+        stats[10] = (uint32_t)(tp2w >> 8);
     }
+    if (tid == WAVE) { stats[11] = (uint32_t)(tp1w >> 8); stats[12] = (uint32_t)(tp2w >> 8); }
 }
 
 struct BlockBufs {                             // grow-only, owned by LevelState

@@ -161,6 +161,36 @@ def test_snapshot_window_zero(engine_factory):
     check(engine_factory, workload.config("C3", n=5000, seed=3), window=0)
 
 
+def test_undecided_execute_at_is_not_read(engine_factory):
+    # the boundary needs no executeAt for a txn that is not committed (the reference's TxnInfo has none before
+    # COMMITTED): with W = 0 (the plain snapshot a CommandStore holds) the deps of every view and the merged Deps
+    # are the same whether undecided rows carry their eventual executeAt or just their TxnId
+    rng = np.random.default_rng(21)
+    n = 8000
+    kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_SYNC_POINT, abi.KIND_EXCLUSIVE_SYNC_POINT],
+                       size=n, p=[0.4, 0.4, 0.1, 0.1])
+    status = rng.choice([abi.ST_APPLIED, abi.ST_STABLE, abi.ST_COMMITTED, abi.ST_PREACCEPTED, abi.ST_ACCEPTED,
+                         abi.ST_INVALID, abi.ST_TRANSITIVELY_KNOWN, abi.ST_HISTORICAL], size=n,
+                        p=[0.3, 0.1, 0.1, 0.2, 0.1, 0.1, 0.05, 0.05]).astype(np.uint8)
+    a = workload.generate(n, keys_per_txn=3, keyspace=300, kinds=kinds, status=status, slow_frac=0.5, seed=22)
+    b = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+    undecided = ~np.isin(status, [abi.ST_COMMITTED, abi.ST_STABLE, abi.ST_APPLIED])
+    for f, g in (("exec_msb", "txn_msb"), ("exec_lsb", "txn_lsb"), ("exec_node", "txn_node")):
+        b[f][undecided] = a[g][undecided]
+    assert undecided.sum() > 1000 and not np.array_equal(a["exec_lsb"], b["exec_lsb"])
+    got = []
+    for batch in (a, b):
+        eng = engine_factory(window=0, replicas=2, drop_p=0.0, seed=1)
+        eng.load(batch)
+        eng.preaccept_deps()
+        eng.merge()
+        got.append([eng.fetch_deps(v, c) for v in range(2) for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)] +
+                   [eng.fetch_merged(c) for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY)])
+    for x, y in zip(*got):
+        assert x.equal(y)
+    check(engine_factory, b, window=0, replicas=2, drop_p=0.0, levels=False)     # and the oracle agrees
+
+
 def test_hot_single_key_and_big_bumps(engine_factory):
     # every txn on one of 3 keys; slow path bumps far beyond the window's hlc span exercise the exact
     # maxCommittedWriteBefore fallback (executeAt of an applied write >= the query's TxnId)
