@@ -33,7 +33,10 @@
 namespace ad {
 
 constexpr int BL_T = 256;                    // one wave per SIMD
-constexpr int BL_EPT = 4;                    // entries per thread
+#ifndef AD_BL_EPT
+#define AD_BL_EPT 4
+#endif
+constexpr int BL_EPT = AD_BL_EPT;            // entries per thread
 constexpr int BL_CAP = BL_T * BL_EPT;        // entries (and txns) per block
 constexpr uint32_t BL_TL = (1u << 11) - 1;     // txn-in-block index bits of a record's high word
 
@@ -92,7 +95,9 @@ static __global__ __launch_bounds__(256) void k_bl_bounds(uint32_t B, size_t n, 
 //   bits 47-48  HEAD's carry source: 0 none (the key's first entry: (-1, -1)), 1 the LDS ring (the key's
 //               previous run ended 1 or 2 blocks earlier), 2 global memory (earlier)
 //   bits 49-60  LDS ring index of that previous run's last entry ((block % 3) * BL_CAP + slot in its block)
-constexpr int BL_SH_W = 11, BL_SH_HEAD = 12, BL_SH_LAST = 13, BL_SH_G = 14, BL_SH_SRC = 15, BL_SH_RING = 17;
+//   bit  61     LAST entry whose key continues 1 or 2 blocks later (its carry goes to the LDS ring only)
+constexpr int BL_SH_W = 11, BL_SH_HEAD = 12, BL_SH_LAST = 13, BL_SH_G = 14, BL_SH_SRC = 15, BL_SH_RING = 17,
+              BL_SH_R = 29;
 constexpr uint32_t BL_NONE = 0xFFFFFFFFu;
 __device__ inline uint32_t bl_block_of(uint32_t q, const uint32_t* c_txn, const uint32_t* erank, const uint32_t* epre, uint32_t bcap) {
     return epre[erank[c_txn[q]]] / bcap;
@@ -118,8 +123,8 @@ static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint3
         b_ = tl > BL_TL || j - boff[b] >= (uint32_t)BL_CAP;
         uint64_t fl = (uint64_t)(tl & BL_TL) | ((uint64_t)(meta_kind(c_meta[q]) == AD_KIND_WRITE) << BL_SH_W) |
                       ((uint64_t)head << BL_SH_HEAD) | ((uint64_t)last << BL_SH_LAST);
-        if (last && q + 1 < P && (uint32_t)seg_start[q + 1] == key && bl_block_of(q + 1, c_txn, erank, epre, bcap) >= b + 3)
-            fl |= 1ull << BL_SH_G;
+        if (last && q + 1 < P && (uint32_t)seg_start[q + 1] == key)
+            fl |= 1ull << (bl_block_of(q + 1, c_txn, erank, epre, bcap) >= b + 3 ? BL_SH_G : BL_SH_R);
         if (head && q != key) {                                   // the key's previous run
             const uint32_t pb = bl_block_of(q - 1, c_txn, erank, epre, bcap);
             if (b - pb <= 2) {
@@ -189,11 +194,14 @@ static __global__ __launch_bounds__(BL_T) void k_bl_compact(uint32_t B, const ui
         const uint32_t j = j0 + (uint32_t)(tid * BL_EPT + e);
         const uint32_t key = (uint32_t)rec[j];
         crec[j0 + c] = make_uint4((fl[e] & 0x1FFFFu) | (ds << BC_DS), ep | (rn << 11) | ((j - j0) << 22), key,
-                                  fl[e] >> BL_SH_RING);
+                                  (fl[e] >> BL_SH_RING) & 0xFFFu);
     }
     if (tid == 0) mt[b] = (uint32_t)(total >> 34);
 }
 
+// w ? a : b on values (a ternary over the members of an int2 held in a register array was compiled into a pointer
+// select and a scratch round trip per slot)
+__device__ inline int bl_sel(bool w, int a, int b) { return b + ((a - b) & -(int)w); }
 // a key's global carry (y, w) moves as one 8-byte word: one memory transaction per carry instead of two
 __device__ inline int2 bl_carry_load(const int2* carry, uint32_t slot) {
     const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&carry[slot]), __ATOMIC_RELAXED,
@@ -225,16 +233,17 @@ struct BzMax {
 // Jacobi rounds over the block's compacted multi-entry runs by ONE wave, E consecutive entries per lane: per
 // round the two packed max scans above give every entry's level candidate x; x > a raises the txn (LDS
 // atomicMax).  Until no txn with a non-LAST entry rises (nl).  Absent entries (beyond nm) read and raise the
-// lane's sink slot past BL_CAP.  Then the carry-out of every LAST entry -- y' = max(y0, the levels of the
-// run's txns), w' = max(w0, the levels of its Writes) -- into the ring (and global memory for G).  Returns
-// the rounds.
+// lane's sink slot past BL_CAP.  A head whose carry comes from the ring (-2, ring index) reads it first (this
+// wave wrote it one or two blocks earlier).  Then the carry-out of every LAST entry -- y' = max(y0, the levels
+// of the run's txns), w' = max(w0, the levels of its Writes) -- into the ring.  Returns the rounds.
 template <int E, class PK>
 __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const int2* __restrict__ hc, int* lv,
-                                     const uint8_t* nl, int2* ring, int rb, int2* carry, uint32_t* stuck) {
+                                     const uint8_t* nl, int2* ring, int rb, uint32_t* stuck) {
     const int lane = __lane_id();
     uint32_t slot[E], ds[E], ep[E], rn[E];
     bool wr[E], hd[E], lst[E], nle[E];
     int y0[E], w0[E], a[E];
+    int2 h[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int k = lane * E + e;
@@ -247,10 +256,18 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
         ds[e] = c.x >> BC_DS;
         ep[e] = c.y & 0x7FFu;
         rn[e] = (c.y >> 11) & 0x7FFu;
-        const int2 h = hd[e] ? hc[k] : make_int2(-1, -1);
-        y0[e] = h.x; w0[e] = h.y;
+        h[e] = hd[e] ? hc[k] : make_int2(-1, -1);
         nle[e] = nl[slot[e]] != 0;                       // static for the block: read once, not per round
     }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (h[e].x != -2) continue;
+        h[e] = ring[h[e].y];
+        const int lb = bl_sel(wr[e], h[e].x, h[e].y) + 1;
+        if (lb > 0) atomicMax(&lv[slot[e]], lb);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) { y0[e] = h[e].x; w0[e] = h[e].y; }
     const BzMax<PK> op{};
     uint32_t it = 0;
     while (true) {
@@ -313,52 +330,59 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
     for (int e = 0; e < E; ++e) {
         const int k = lane * E + e;
         if (k >= nm || !lst[e]) continue;
-        const uint4 c = cr[k];
         const PK my = iny > iy[e] ? iny : iy[e], mw = inw > iw[e] ? inw : iw[e];
-        const int2 o = make_int2(bz_val<PK>(my), bz_val<PK>(mw));
-        ring[rb + (int)(c.y >> 22)] = o;
-        if ((c.x >> BL_SH_G) & 1u) bl_carry_store(carry, c.z, o);
+        ring[rb + (int)(cr[k].y >> 22)] = make_int2(bz_val<PK>(my), bz_val<PK>(mw));
     }
     return it;
 }
 
-// The sequential walk over the blocks (one workgroup; see the file header), pipelined so that only the rounds and
-// two short LDS phases sit on the sequential path.  Wave 0 runs the rounds (W0); waves 1-3 are the workers.  Per
-// block b:
-//   R_b   W0: rounds(b), then the carry-outs of b's multi-entry runs (ring; global memory for keys whose next run is
-//         >= 3 blocks away).  Workers, meanwhile: load block b + 1 (records, compacted entries, order slice, then the
-//         dependent global carry-ins, all issued before any is used) and prefill its txn levels from every head
-//         whose carry does not come from the ring (a singleton run is then final), flag its non-last entries.
-//   P1_b  workers: the carry-outs of b's singleton runs (ring, global) and b's levels into L.
-//   P2_b  all: clear the level buffer block b + 2 will use; block b + 1's heads whose carry comes from the ring
-//         (their key's previous run ended in block b or b - 1) resolve it and prefill.
-// Levels / flags live in three buffers by b % 3; staged block data in two by b % 2.  Global carries are written and
-// read by this one workgroup (one CU): workgroup-scope ordering suffices; every thread releases (fence) its earlier
-// global carry stores at the start of each R phase (W0's were issued at the end of the previous rounds, the
-// workers' in the previous P1: both complete by then in practice, so the fence costs W0 nothing), and a key's
-// global carry is read by the staging of a block at least three blocks later, after that fence and two barriers.
+// The sequential walk over the blocks (one workgroup; see the file header).  Only wave 0 (W0) is on the
+// sequential path, and it touches LDS only; waves 1-3 (the workers) do all global memory traffic one block
+// ahead / one block behind.  Per block b, ONE phase R_b:
+//   W0       the singleton runs of b whose carry comes from the ring (list la: their key's previous run ended
+//            one or two blocks earlier) -> carry-in, txn lower bound; the rounds of b's multi-entry runs and
+//            their carry-outs into the ring; the carry-outs of b's singleton runs whose key continues one or two
+//            blocks later (list lb) into the ring.
+//   workers  block b - 1's levels into L and its carry-outs for keys continuing >= 3 blocks later into global
+//            memory (the "G" carries); clear the buffers block b + 2 will use; load block b + 1 (records,
+//            compacted entries, order slice, then the dependent global carry-ins, all issued before any is
+//            used), prefill its txn levels from every head whose carry is known (a singleton run is then
+//            final), flag its non-last entries, and build its la / lb lists; release their global stores.
+// Levels / flags / bounds / list counts live in four buffers by b % 4 (W0's b, the workers' b - 1, b + 1 and the
+// cleared b + 2); staged block data in two by b % 2: a worker reads block b - 1's slot x and then overwrites it
+// with block b + 1's, and the two use the same slot -> thread mapping, so no barrier is needed between them.
+// A G carry stored while block b - 1 is retired (R_b) is read by the staging of block >= b + 2 (R_{b+1} or
+// later), after the workers' release fence and the barrier that ends R_b.
 // stats[0] = greatest level + 1, stats[1] = rounds, stats[2..3] = clock64 in rounds, stats[4..5] = total,
-// stats[6] = a block's rounds did not converge, stats[7..9] = clock64 / 256 waiting for the workers after the
-// rounds, in P1 and in P2 (thread 0).
+// stats[6] = a block's rounds did not converge, stats[7] = clock64 / 256 W0 waited for the workers,
+// stats[8] = W0's list work, stats[9] = the workers' work (thread WAVE).
 constexpr int BL_SI = (BL_CAP + (BL_T - WAVE) - 1) / (BL_T - WAVE);   // slots per worker thread (3 waves)
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for the wave's outstanding global stores
-// (s_waitcnt vmcnt(0)), which put every block's level and carry stores (~1-2 us to complete) on the sequential
-// path: 23 M of the walk's 78 M clocks on C3.  Global carries get their own release fence (top of each R phase).
+// (s_waitcnt vmcnt(0)); the workers release their global stores themselves (end of their phase).
 __device__ inline void bl_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+struct BlSum32 {
+    using S = uint32_t;
+    __device__ S identity() const { return 0u; }
+    __device__ S combine(S a, S b) const { return a + b; }
+};
 struct BlStage {                               // one block's staged data in LDS (two of these, by block parity)
     uint64_t rec[BL_CAP];                      // slot records (~0: none)
-    int2 car[BL_CAP];                          // singleton runs' carry-in (src 1: resolved in P2)
+    int2 car[BL_CAP];                          // singleton runs' carry-in (ring-sourced ones: written by W0)
     uint32_t ord[BL_CAP];                      // txn of each txn slot
     uint4 cr[BL_CAP];                          // compacted multi-entry run entries
-    int2 hc[BL_CAP];                           // their heads' carry-in (-2: from the ring, resolved in P2)
-    uint32_t bnd[5];                           // j0, j1, t0, t1, compacted entries
+    int2 hc[BL_CAP];                           // their heads' carry-in ((-2, ring index): W0 reads the ring)
+    uint64_t la[BL_CAP];                       // ring-sourced singleton runs: ring | W << 12 | txn << 13 | slot << 32
+    uint32_t lb[BL_CAP];                       // ring-continuing singleton runs: slot | txn << 10 | W << 21
 };
+struct BlBounds { uint32_t j0, j1, t0, t1, m, cnt; };   // cnt: la entries | lb entries << 16
+
 // Load block b into `s` and prefill its levels (lv / nl: its buffers) from every head whose carry is known now.
+// Called by whole waves (the list appends are wave-aggregated).
 __device__ inline void bl_stage_prefill(uint32_t b, int t, int nthr, const uint32_t* __restrict__ boff,
                                         const uint32_t* __restrict__ tb, const uint64_t* __restrict__ rec,
                                         const uint4* __restrict__ crec, const uint32_t* __restrict__ mt, const int2* carry,
-                                        const uint32_t* __restrict__ order, BlStage& s, int* lv, uint8_t* nl) {
+                                        const uint32_t* __restrict__ order, BlStage& s, BlBounds& bd, int* lv, uint8_t* nl) {
     const uint32_t j0 = boff[b], j1 = boff[b + 1], t0 = tb[b], t1 = tb[b + 1], m = mt[b];
     uint64_t r[BL_SI];
     uint4 q[BL_SI];
@@ -385,9 +409,12 @@ __device__ inline void bl_stage_prefill(uint32_t b, int t, int nthr, const uint3
             else if (src == 1u) h[i] = make_int2(-2, (int)q[i].w);
         }
     }
+    uint32_t cnt = 0;
+    bool ia[BL_SI], ib[BL_SI];
 #pragma unroll
     for (int i = 0; i < BL_SI; ++i) {
         const uint32_t x = (uint32_t)(t + i * nthr);
+        ia[i] = ib[i] = false;
         if (x >= (uint32_t)BL_CAP) continue;
         s.rec[x] = r[i];
         s.car[x] = c[i];
@@ -395,22 +422,89 @@ __device__ inline void bl_stage_prefill(uint32_t b, int t, int nthr, const uint3
         const uint32_t f = (uint32_t)(r[i] >> 32);
         if (r[i] != ~0ull) {
             const bool head = f & (1u << BL_SH_HEAD), last = f & (1u << BL_SH_LAST);
-            if (head && last && ((f >> BL_SH_SRC) & 3u) != 1u) {
-                const int lb = (f & (1u << BL_SH_W)) ? c[i].x + 1 : c[i].y + 1;
-                if (lb > 0) atomicMax(&lv[f & BL_TL], lb);
+            if (head && last) {
+                if (((f >> BL_SH_SRC) & 3u) != 1u) {
+                    const int lb = bl_sel(f & (1u << BL_SH_W), c[i].x, c[i].y) + 1;
+                    if (lb > 0) atomicMax(&lv[f & BL_TL], lb);
+                } else {
+                    ia[i] = true;
+                }
+                ib[i] = (f >> BL_SH_R) & 1u;
             }
             if (!last) nl[f & BL_TL] = 1;
         }
+        cnt += (ia[i] ? 1u : 0u) + (ib[i] ? 1u << 16 : 0u);
         if (x < m) {
             s.cr[x] = q[i];
             s.hc[x] = h[i];
             if (((q[i].x >> BL_SH_HEAD) & 1u) && h[i].x != -2) {
-                const int lb = ((q[i].x >> BL_SH_W) & 1u) ? h[i].x + 1 : h[i].y + 1;
+                const int lb = bl_sel((q[i].x >> BL_SH_W) & 1u, h[i].x, h[i].y) + 1;
                 if (lb > 0) atomicMax(&lv[q[i].x & BL_TL], lb);
             }
         }
     }
-    if (t == 0) { s.bnd[0] = j0; s.bnd[1] = j1; s.bnd[2] = t0; s.bnd[3] = t1; s.bnd[4] = m; }
+    // wave-aggregated list append: one LDS atomic per wave for both lists
+    const uint32_t inc = wave_incl_scan(BlSum32{}, cnt);
+    uint32_t base = 0;
+    if (__lane_id() == WAVE - 1) base = atomicAdd(&bd.cnt, inc);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, WAVE - 1) + inc - cnt;
+    uint32_t pa = base & 0xFFFFu, pb = base >> 16;
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const uint32_t x = (uint32_t)(t + i * nthr);
+        const uint32_t f = (uint32_t)(r[i] >> 32);
+        const uint32_t tl = f & BL_TL, w = (f >> BL_SH_W) & 1u;
+        if (ia[i]) s.la[pa++] = (uint64_t)(((f >> BL_SH_RING) & 0xFFFu) | (w << 12) | (tl << 13)) | ((uint64_t)x << 32);
+        if (ib[i]) s.lb[pb++] = x | (tl << 10) | (w << 21);
+    }
+    if (t == 0) { bd.j0 = j0; bd.j1 = j1; bd.t0 = t0; bd.t1 = t1; bd.m = m; }
+}
+
+// Retire block b (workers, the same slot -> thread mapping as bl_stage_prefill): its levels into L and the
+// carries of keys continuing >= 3 blocks later into global memory (a singleton run's from its carry-in and its
+// txn's level; a multi-entry run's from the ring, where W0 left it).  Returns the greatest level seen.
+__device__ inline int bl_retire(int t, int nthr, const BlStage& s, const BlBounds& bd, const int* lv, const int2* ring,
+                                int rb, int2* carry, uint32_t* __restrict__ L) {
+    const uint32_t nt = bd.t1 - bd.t0;
+    uint64_t rr[BL_SI];
+    uint32_t od[BL_SI];
+    int2 ci[BL_SI];
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const int x = t + i * nthr;
+        rr[i] = x < BL_CAP ? s.rec[x] : ~0ull;
+        ci[i] = x < BL_CAP ? s.car[x] : make_int2(-1, -1);
+        od[i] = (uint32_t)x < nt ? s.ord[x] : 0u;
+    }
+    int ls[BL_SI], lo[BL_SI];
+    int2 rg[BL_SI];
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const int x = t + i * nthr;
+        const uint32_t f = (uint32_t)(rr[i] >> 32);
+        const bool g = rr[i] != ~0ull && (f & (1u << BL_SH_G));
+        const bool single = (f & (1u << BL_SH_HEAD)) != 0;     // a G entry is LAST: HEAD too = singleton run
+        ls[i] = g && single ? lv[f & BL_TL] : 0;
+        rg[i] = g && !single ? ring[rb + x] : make_int2(0, 0);
+        lo[i] = (uint32_t)x < nt ? lv[x] : -1;
+    }
+    int maxl = -1;
+#pragma unroll
+    for (int i = 0; i < BL_SI; ++i) {
+        const int x = t + i * nthr;
+        const uint32_t f = (uint32_t)(rr[i] >> 32);
+        if (rr[i] != ~0ull && (f & (1u << BL_SH_G))) {
+            const int2 c = (f & (1u << BL_SH_HEAD))
+                               ? make_int2(max(ci[i].x, ls[i]), bl_sel(f & (1u << BL_SH_W), ls[i], ci[i].y))
+                               : rg[i];
+            bl_carry_store(carry, (uint32_t)rr[i], c);
+        }
+        if ((uint32_t)x < nt) {
+            L[od[i]] = (uint32_t)lo[i];
+            maxl = max(maxl, lo[i]);
+        }
+    }
+    return maxl;
 }
 
 template <class PK>
@@ -419,159 +513,100 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
                                                        const uint32_t* __restrict__ mt, int2* carry,
                                                        const uint32_t* __restrict__ order, uint32_t* __restrict__ L,
                                                        uint32_t* __restrict__ stats) {
-    __shared__ int lvb[3][BL_CAP + WAVE];      // levels of a block's txns (txn-in-block index), by block % 3;
-                                               // [BL_CAP + lane]: sinks of the rounds' absent entries
-    __shared__ uint8_t nlb[3][BL_CAP + WAVE];     // txn has an entry that is not its key's last in the block
-    __shared__ int2 ring[3 * BL_CAP];          // carry-out of every slot of the last three blocks
+    __shared__ __align__(16) int lvb[4][BL_CAP + WAVE];     // levels of a block's txns (txn-in-block index), by
+                                                            // block % 4; [BL_CAP + lane]: the rounds' sinks
+    __shared__ __align__(16) uint8_t nlb[4][BL_CAP + WAVE];  // txn has an entry that is not its key's last
+    __shared__ int2 ring[3 * BL_CAP];          // carry-out of the slots of the last three blocks (by block % 3)
     __shared__ BlStage stg[2];
+    __shared__ BlBounds bnd[4];
     __shared__ uint32_t sstuck;
+    static_assert((BL_CAP + WAVE) % 16 == 0, "buffers are cleared 16 bytes at a time");
     const int tid = threadIdx.x, lane = __lane_id();
     if (tid == 0) sstuck = 0u;
+    if (tid < 4) bnd[tid].cnt = 0u;
     const uint64_t tstart = clock64();
-    uint64_t tround = 0, twait = 0, tp1 = 0, tp2 = 0, tp2w = 0, tp1w = 0;
+    uint64_t tround = 0, twait = 0, tlist = 0, twork = 0;
     for (int x = tid; x < BL_CAP + WAVE; x += BL_T) {
-        lvb[0][x] = lvb[1][x] = lvb[2][x] = 0;
-        nlb[0][x] = nlb[1][x] = nlb[2][x] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { lvb[k][x] = 0; nlb[k][x] = 0; }
     }
     __syncthreads();
     int maxl = -1;
     uint32_t rounds = 0;
-    if (B > 0) bl_stage_prefill(0, tid, BL_T, boff, tb, rec, crec, mt, carry, order, stg[0], lvb[0], nlb[0]);   // no ring sources
+    if (B > 0) bl_stage_prefill(0, tid, BL_T, boff, tb, rec, crec, mt, carry, order, stg[0], bnd[0], lvb[0], nlb[0]);
     __syncthreads();
     for (uint32_t b = 0; b < B; ++b) {
-        BlStage& S = stg[b & 1];
-        int* lv = lvb[b % 3];
-        uint8_t* nl = nlb[b % 3];
-        const int nm = (int)S.bnd[4];
-        const uint32_t nt = S.bnd[3] - S.bnd[2];
-        const int rb = (int)(b % 3) * BL_CAP;
-        // ---- R_b: rounds (wave 0) | next block's load + prefill (workers).  The fence releases this thread's
-        // global carry stores of block b - 1 (issued two phases ago, so normally complete: no wait on W0's path)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        uint64_t tr1 = clock64();
+        const uint64_t tb0 = clock64();
         if (tid < WAVE) {
+            BlStage& S = stg[b & 1];
+            int* lv = lvb[b & 3];
+            const int rb = (int)(b % 3) * BL_CAP;
+            const uint32_t cnt = bnd[b & 3].cnt, na = cnt & 0xFFFFu, nbl = cnt >> 16;
+            const int nm = (int)bnd[b & 3].m;
+            // ring-sourced singleton runs: carry-in and txn lower bound
+            for (uint32_t k = lane; k < na; k += WAVE) {
+                const uint64_t e = S.la[k];
+                const int2 c = ring[(uint32_t)e & 0xFFFu];
+                S.car[(uint32_t)(e >> 32)] = c;
+                const int lb = bl_sel(((uint32_t)e >> 12) & 1u, c.x, c.y) + 1;
+                if (lb > 0) atomicMax(&lv[((uint32_t)e >> 13) & BL_TL], lb);
+            }
+            const uint64_t t1 = clock64();
             if (nm > 0) {
-                const uint64_t t0 = clock64();
+                uint8_t* nl = nlb[b & 3];
                 uint32_t r;
                 const int epl = (nm + WAVE - 1) / WAVE;        // entries per lane
-                if (epl <= 2) r = bl_rounds<2, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 3) r = bl_rounds<3, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 4) r = bl_rounds<4, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 5) r = bl_rounds<5, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 6) r = bl_rounds<6, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 8) r = bl_rounds<8, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else if (epl <= 12) r = bl_rounds<12, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                else r = bl_rounds<16, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, carry, &sstuck);
-                tr1 = clock64();
-                tround += tr1 - t0;
+                if (epl <= 2) r = bl_rounds<2, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else if (epl <= 3) r = bl_rounds<3, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else if (epl <= 4) r = bl_rounds<4, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else if (epl <= 5) r = bl_rounds<5, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else if (epl <= 6) r = bl_rounds<6, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else if (epl <= 8) r = bl_rounds<8, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else if (epl <= 12) r = bl_rounds<12, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
+                else r = bl_rounds<16, PK>(nm, S.cr, S.hc, lv, nl, ring, rb, &sstuck);
                 rounds += r;
             }
-        } else if (b + 1 < B) {
-            bl_stage_prefill(b + 1, tid - WAVE, BL_T - WAVE, boff, tb, rec, crec, mt, carry, order, stg[(b + 1) & 1],
-                             lvb[(b + 1) % 3], nlb[(b + 1) % 3]);
+            const uint64_t t2 = clock64();
+            tround += t2 - t1;
+            // ring-continuing singleton runs: carry-out (the txn's level is final now)
+            for (uint32_t k = lane; k < nbl; k += WAVE) {
+                const uint32_t e = S.lb[k];
+                const uint32_t x = e & 0x3FFu;
+                const int2 ci = S.car[x];
+                const int l = lv[(e >> 10) & BL_TL];
+                ring[rb + (int)x] = make_int2(max(ci.x, l), bl_sel((e >> 21) & 1u, l, ci.y));
+            }
+            const uint64_t t3 = clock64();
+            tlist += (t1 - tb0) + (t3 - t2);
+            bl_barrier();
+            twait += clock64() - t3;
+        } else {
+            const int t = tid - WAVE, nthr = BL_T - WAVE;
+            if (b > 0) {
+                const uint32_t p = b - 1;
+                maxl = max(maxl, bl_retire(t, nthr, stg[p & 1], bnd[p & 3], lvb[p & 3], ring, (int)(p % 3) * BL_CAP,
+                                           carry, L));
+            }
+            {   // clear the buffers of block b + 2 (last used by block b - 2, retired in the previous phase)
+                int4* lc = reinterpret_cast<int4*>(lvb[(b + 2) & 3]);
+                int4* nc = reinterpret_cast<int4*>(nlb[(b + 2) & 3]);
+                for (int x = t; x < (BL_CAP + WAVE) / 4; x += nthr) lc[x] = make_int4(0, 0, 0, 0);
+                for (int x = t; x < (BL_CAP + WAVE) / 16; x += nthr) nc[x] = make_int4(0, 0, 0, 0);
+                if (t == 0) bnd[(b + 2) & 3].cnt = 0u;
+            }
+            if (b + 1 < B)
+                bl_stage_prefill(b + 1, t, nthr, boff, tb, rec, crec, mt, carry, order, stg[(b + 1) & 1],
+                                 bnd[(b + 1) & 3], lvb[(b + 1) & 3], nlb[(b + 1) & 3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");    // the retired block's G carries
+            twork += clock64() - tb0;
+            bl_barrier();
         }
-        bl_barrier();
-        const uint64_t tq1 = clock64();
-        twait += tq1 - tr1;
-        const uint64_t tw0 = clock64();
-        // ---- P1_b (workers): singleton runs' carry-outs, b's levels (W0 issues no global stores here: a store's
-        // completion would sit on its path at the next fence).  Every LDS load of a thread's slots is issued before
-        // any is used (one round trip per dependent step, not per slot).
-        if (tid >= WAVE) {
-            const int t = tid - WAVE;
-            uint64_t rr[BL_SI];
-            uint32_t od[BL_SI];
-            int2 ci[BL_SI];
-            int ls[BL_SI], lo[BL_SI];
-#pragma unroll
-            for (int i = 0; i < BL_SI; ++i) {
-                const int x = t + i * (BL_T - WAVE);
-                rr[i] = x < BL_CAP ? S.rec[x] : ~0ull;
-                ci[i] = x < BL_CAP ? S.car[x] : make_int2(-1, -1);
-                od[i] = (uint32_t)x < nt ? S.ord[x] : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < BL_SI; ++i) {
-                const int x = t + i * (BL_T - WAVE);
-                ls[i] = rr[i] != ~0ull ? lv[(uint32_t)(rr[i] >> 32) & BL_TL] : 0;
-                lo[i] = (uint32_t)x < nt ? lv[x] : -1;
-            }
-#pragma unroll
-            for (int i = 0; i < BL_SI; ++i) {
-                const int x = t + i * (BL_T - WAVE);
-                const uint32_t f = (uint32_t)(rr[i] >> 32);
-                if (rr[i] != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST))) {
-                    const int2 c = make_int2(max(ci[i].x, ls[i]), (f & (1u << BL_SH_W)) ? ls[i] : ci[i].y);
-                    ring[rb + x] = c;
-                    if (f & (1u << BL_SH_G)) bl_carry_store(carry, (uint32_t)rr[i], c);
-                }
-                if ((uint32_t)x < nt) {
-                    L[od[i]] = (uint32_t)lo[i];
-                    maxl = max(maxl, lo[i]);
-                }
-            }
-        }
-        tp1w += clock64() - tw0;
-        bl_barrier();
-        const uint64_t tq2 = clock64();
-        tp1 += tq2 - tq1;
-        // ---- P2_b: clear the buffers of block b + 2 (last used by b - 1); b + 1's ring-sourced heads (loads
-        // first, as in P1)
-        {
-            int* lc = lvb[(b + 2) % 3];
-            uint8_t* nc = nlb[(b + 2) % 3];
-            for (int x = tid; x < BL_CAP + WAVE; x += BL_T) { lc[x] = 0; nc[x] = 0; }
-        }
-        if (b + 1 < B) {
-            BlStage& N = stg[(b + 1) & 1];
-            int* lvn = lvb[(b + 1) % 3];
-            uint64_t rr[BL_EPT];
-            int2 rc[BL_EPT];
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) rr[e] = N.rec[tid * BL_EPT + e];
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                const uint32_t f = (uint32_t)(rr[e] >> 32);
-                const bool want = rr[e] != ~0ull && (f & (1u << BL_SH_HEAD)) && (f & (1u << BL_SH_LAST)) &&
-                                  ((f >> BL_SH_SRC) & 3u) == 1u;
-                rc[e] = want ? ring[f >> BL_SH_RING] : make_int2(-3, -3);
-            }
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                if (rc[e].x == -3) continue;
-                const uint32_t f = (uint32_t)(rr[e] >> 32);
-                N.car[tid * BL_EPT + e] = rc[e];
-                const int lb = (f & (1u << BL_SH_W)) ? rc[e].x + 1 : rc[e].y + 1;
-                if (lb > 0) atomicMax(&lvn[f & BL_TL], lb);
-            }
-            const int mn = (int)N.bnd[4];
-            int2 hh[BL_EPT];
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                const int k = tid + e * BL_T;
-                hh[e] = k < mn ? N.hc[k] : make_int2(-1, -1);
-            }
-            uint32_t qx[BL_EPT];
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                const int k = tid + e * BL_T;
-                qx[e] = hh[e].x == -2 ? N.cr[k].x : 0u;
-                hh[e] = hh[e].x == -2 ? ring[hh[e].y] : make_int2(-3, -3);
-            }
-#pragma unroll
-            for (int e = 0; e < BL_EPT; ++e) {
-                if (hh[e].x == -3) continue;
-                const int k = tid + e * BL_T;
-                N.hc[k] = hh[e];
-                const int lb = ((qx[e] >> BL_SH_W) & 1u) ? hh[e].x + 1 : hh[e].y + 1;
-                if (lb > 0) atomicMax(&lvn[qx[e] & BL_TL], lb);
-            }
-        }
-        const uint64_t tq3 = clock64();
-        tp2w += tq3 - tq2;
-        bl_barrier();
-        tp2 += clock64() - tq2;
         if (sstuck) break;
+    }
+    if (tid >= WAVE && B > 0 && !sstuck) {
+        const uint32_t p = B - 1;
+        maxl = max(maxl, bl_retire(tid - WAVE, BL_T - WAVE, stg[p & 1], bnd[p & 3], lvb[p & 3], ring,
+                                   (int)(p % 3) * BL_CAP, carry, L));
     }
     maxl = wave_max(maxl);
     if (lane == 0) atomicMax(&stats[0], (uint32_t)(maxl + 1));
@@ -581,10 +616,9 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
         stats[2] = (uint32_t)tround; stats[3] = (uint32_t)(tround >> 32);
         stats[4] = (uint32_t)tot; stats[5] = (uint32_t)(tot >> 32);
         stats[6] = sstuck;
-        stats[7] = (uint32_t)(twait >> 8); stats[8] = (uint32_t)(tp1 >> 8); stats[9] = (uint32_t)(tp2 >> 8);
-        stats[10] = (uint32_t)(tp2w >> 8);
+        stats[7] = (uint32_t)(twait >> 8); stats[8] = (uint32_t)(tlist >> 8);
     }
-    if (tid == WAVE) { stats[11] = (uint32_t)(tp1w >> 8); stats[12] = (uint32_t)(tp2w >> 8); }
+    if (tid == WAVE) stats[9] = (uint32_t)(twork >> 8);
 }
 
 struct BlockBufs {                             // grow-only, owned by LevelState

@@ -1738,13 +1738,12 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         *depth = (int)s4[0];
         if (rounds_out) *rounds_out = s4[1];
         if (getenv("AD_DEBUG_LEVELS")) {
-            uint32_t s6[13];
-            hipMemcpy(s6, bb.stats, 52, hipMemcpyDeviceToHost);
+            uint32_t s6[10];
+            hipMemcpy(s6, bb.stats, 40, hipMemcpyDeviceToHost);
             const double tr = (double)((uint64_t)s6[3] << 32 | s6[2]), tt = (double)((uint64_t)s6[5] << 32 | s6[4]);
-            fprintf(stderr, "block levels: %u blocks, %u rounds, depth %u; clock64 rounds %.0f (%.1f%%) of %.0f; worker wait %.0f, "
-                            "P1 %.0f, P2 %.0f (W0 work %.0f; worker work P1 %.0f, P2 %.0f)\n", nb, s6[1], s6[0], tr,
-                    100.0 * tr / (tt > 0 ? tt : 1), tt, 256.0 * s6[7], 256.0 * s6[8], 256.0 * s6[9], 256.0 * s6[10],
-                    256.0 * s6[11], 256.0 * s6[12]);
+            fprintf(stderr, "block levels: %u blocks, %u rounds, depth %u; clock64 rounds %.0f (%.1f%%) of %.0f; W0 waited %.0f, "
+                            "W0 lists %.0f; workers' phase work %.0f\n", nb, s6[1], s6[0], tr,
+                    100.0 * tr / (tt > 0 ? tt : 1), tt, 256.0 * s6[7], 256.0 * s6[8], 256.0 * s6[9]);
         }
     }
     return AD_OK;
