@@ -1649,7 +1649,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         const size_t c = std::max<size_t>(P, 1);
         if (!grow((void**)&bb.rec, c * 8) || !grow((void**)&bb.bk, c * 4) || !grow((void**)&bb.bv, c * 4) ||
             !grow((void**)&bb.bk2, c * 4) || !grow((void**)&bb.bv2, c * 4) || !grow((void**)&bb.carry, c * 8) ||
-            !grow((void**)&bb.crec, c * 16))
+            !grow((void**)&bb.crec, c * 16) || !grow((void**)&bb.la, c * 8) || !grow((void**)&bb.lb, c * 4))
             goto oom;
         bb.capP = c;
     }
@@ -1660,7 +1660,9 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
     }
     if (bb.capB < Bmax + 1 || !bb.tb) {
         const size_t c = Bmax + 1;
-        if (!grow((void**)&bb.tb, c * 4) || !grow((void**)&bb.boff, c * 4) || !grow((void**)&bb.mt, c * 4)) goto oom;
+        if (!grow((void**)&bb.tb, c * 4) || !grow((void**)&bb.boff, c * 4) || !grow((void**)&bb.mt, c * 4) ||
+            !grow((void**)&bb.lcnt, c * 4))
+            goto oom;
         bb.capB = c;
     }
     if (!bb.stats && !grow((void**)&bb.stats, 64)) goto oom;
@@ -1715,13 +1717,17 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         k_bl_inverse<<<gP, 256, 0, st>>>(P, sv, inv);
         k_bl_records<<<gP, 256, 0, st>>>(P, sk, sv, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.epre, bcap, bb.tb,
                                          bb.boff, bb.rec, bb.stats + 3);
-        k_bl_compact<<<nb, BL_T, 0, st>>>(nb, bb.boff, bb.rec, bb.crec, bb.mt);
+        k_bl_compact<<<nb, BL_T, 0, st>>>(nb, bb.boff, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt);
         // 4. the walk (packed scan words: 32-bit while every level fits 20 bits)
-        hipMemsetAsync(bb.carry, 0xFF, P * 8, st);
+        // (no carry initialisation: a head reads a global carry only from a producer flagged to store it)
+        uint32_t* Lr = bb.erank;                   // free after the records: the levels by executeAt rank
         if (n <= (1u << 20) && !in.wide_words)
-            k_level_blocks<uint32_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.carry, in.order, in.lvl, bb.stats);
+            k_level_blocks<uint32_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
+                                                              bb.stats);
         else
-            k_level_blocks<uint64_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.carry, in.order, in.lvl, bb.stats);
+            k_level_blocks<uint64_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
+                                                              bb.stats);
+        k_bl_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.order, Lr, in.lvl);
         uint32_t s4[7] = {0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyAsync(s4, bb.stats, 28, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
             err = "exec levels: device error";
@@ -1738,12 +1744,14 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         *depth = (int)s4[0];
         if (rounds_out) *rounds_out = s4[1];
         if (getenv("AD_DEBUG_LEVELS")) {
-            uint32_t s6[10];
-            hipMemcpy(s6, bb.stats, 40, hipMemcpyDeviceToHost);
+            uint32_t s6[16];
+            hipMemcpy(s6, bb.stats, 64, hipMemcpyDeviceToHost);
             const double tr = (double)((uint64_t)s6[3] << 32 | s6[2]), tt = (double)((uint64_t)s6[5] << 32 | s6[4]);
             fprintf(stderr, "block levels: %u blocks, %u rounds, depth %u; clock64 rounds %.0f (%.1f%%) of %.0f; W0 waited %.0f, "
-                            "W0 lists %.0f; workers' phase work %.0f\n", nb, s6[1], s6[0], tr,
-                    100.0 * tr / (tt > 0 ? tt : 1), tt, 256.0 * s6[7], 256.0 * s6[8], 256.0 * s6[9]);
+                            "W0 lists %.0f; workers' phase work %.0f (retire %.0f, clear %.0f, stage %.0f); rounds' init %.0f, "
+                            "carry-out %.0f; entries per lane %.2f\n", nb, s6[1],
+                    s6[0], tr, 100.0 * tr / (tt > 0 ? tt : 1), tt, 256.0 * s6[7], 256.0 * s6[8], 256.0 * s6[9],
+                    256.0 * s6[10], 256.0 * s6[11], 256.0 * s6[12], 256.0 * s6[13], 256.0 * s6[14], (double)s6[15] / nb);
         }
     }
     return AD_OK;
