@@ -368,10 +368,10 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
             const PK zm = bz_max(in2, inc2[e]);
             const int x = max((int)(uint32_t)(zm & M) + c7[e], a[e] + ka[e]);
             const bool r = x > a[e];
-            if (r) atomicMax(&lv[slot[e]], x);               // rare after the first rounds
+            atomicMax(&lv[slot[e]], x);                      // unconditional: no exec-mask dance (x <= a: no-op)
             up |= r && nle[e];
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this round's raises before the next reads
+        // (no wait for the raises: a wave's LDS operations complete in order, so the next round's reads see them)
         ++it;
         if (!__ballot(up)) break;
         // each round finalises at least the lowest unfinished txn of the block: more rounds than txns + 1 is
