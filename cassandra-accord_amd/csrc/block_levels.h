@@ -427,7 +427,14 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
 // stats[6] = a block's rounds did not converge, stats[7] = clock64 / 256 W0 waited for the workers,
 // stats[8] = W0's list work, stats[9] = the workers' work (thread WAVE), stats[10..12] = its retire, clear and
 // staging parts.
-constexpr int BL_SI = (BL_CAP + (BL_T - WAVE) - 1) / (BL_T - WAVE);   // slots per worker thread (3 waves)
+// The walk's workgroup: 256 threads (W0 + 3 worker waves, one per SIMD) or 512 (W0's SIMD partner, wave 4, idles
+// so that W0 keeps its SIMD's issue slots; 6 worker waves, two per SIMD, hide each other's latencies).
+#ifndef AD_BL_WT
+#define AD_BL_WT 256
+#endif
+constexpr int BL_WT = AD_BL_WT;
+constexpr int BL_NW = BL_WT == 512 ? BL_WT - 2 * WAVE : BL_WT - WAVE;   // worker threads
+constexpr int BL_SI = (BL_CAP + BL_NW - 1) / BL_NW;                       // slots per worker thread
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for the wave's outstanding global stores
 // (s_waitcnt vmcnt(0)); the workers release their global stores themselves (end of their phase).
 __device__ inline void bl_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -583,7 +590,7 @@ __device__ inline int bl_retire(int t, int nthr, const BlStage& s, const BlBound
 }
 
 template <class PK>
-static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const uint32_t* __restrict__ boff, const uint32_t* __restrict__ tb,
+static __global__ __launch_bounds__(BL_WT) void k_level_blocks(uint32_t B, const uint32_t* __restrict__ boff, const uint32_t* __restrict__ tb,
                                                        const uint64_t* __restrict__ rec, const uint4* __restrict__ crec,
                                                        const uint32_t* __restrict__ mt, const uint64_t* __restrict__ la,
                                                        const uint32_t* __restrict__ lb, const uint32_t* __restrict__ lcnt,
@@ -601,7 +608,7 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
     if (tid == 0) sstuck = 0u;
     const uint64_t tstart = clock64();
     uint64_t tround = 0, twait = 0, tlist = 0, twork = 0, tret = 0, tclr = 0, tstg = 0, tph[2] = {0, 0}, sepl = 0;
-    for (int x = tid; x < BL_CAP + WAVE; x += BL_T) {
+    for (int x = tid; x < BL_CAP + WAVE; x += BL_WT) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) lvb[k][x] = 0;
     }
@@ -611,9 +618,9 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
     if (B > 0) {                               // block 0: staged by every thread
         BlPre p0;
         uint64_t vc[BL_SI], vh[BL_SI];
-        bl_load_static(bl_load_bounds(0, boff, tb, mt, lcnt), tid, BL_T, rec, crec, la, lb, p0);
-        bl_load_carries(tid, BL_T, p0, carry, vc, vh);
-        bl_stage_write(tid, BL_T, p0, vc, vh, stg[0], bnd[0], lvb[0]);
+        bl_load_static(bl_load_bounds(0, boff, tb, mt, lcnt), tid, BL_WT, rec, crec, la, lb, p0);
+        bl_load_carries(tid, BL_WT, p0, carry, vc, vh);
+        bl_stage_write(tid, BL_WT, p0, vc, vh, stg[0], bnd[0], lvb[0]);
     }
     __syncthreads();
     // Each role runs its own loop (one barrier per block in both), so the workers' registers carried across
@@ -665,8 +672,14 @@ static __global__ __launch_bounds__(BL_T) void k_level_blocks(uint32_t B, const 
             twait += clock64() - t3;
             if (sstuck) break;
         }
+    } else if (BL_WT == 512 && tid / WAVE == 4) {
+        for (uint32_t b = 0; b < B; ++b) {     // W0's SIMD partner: barriers only
+            bl_barrier();
+            if (sstuck) break;
+        }
     } else {
-        const int t = tid - WAVE, nthr = BL_T - WAVE;
+        const int w = tid / WAVE;
+        const int t = (BL_WT == 512 && w > 4 ? tid - 2 * WAVE : tid - WAVE), nthr = BL_NW;
         BlPre cur, nxt;                        // static inputs of blocks b + 1 and b + 2
         BlBnd bn{};                            // bounds of block b + 2
         if (B > 1) bl_load_static(bl_load_bounds(1, boff, tb, mt, lcnt), t, nthr, rec, crec, la, lb, cur);

@@ -1722,10 +1722,10 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         // (no carry initialisation: a head reads a global carry only from a producer flagged to store it)
         uint32_t* Lr = bb.erank;                   // free after the records: the levels by executeAt rank
         if (n <= (1u << 20) && !in.wide_words)
-            k_level_blocks<uint32_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
+            k_level_blocks<uint32_t><<<1, BL_WT, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
                                                               bb.stats);
         else
-            k_level_blocks<uint64_t><<<1, BL_T, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
+            k_level_blocks<uint64_t><<<1, BL_WT, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
                                                               bb.stats);
         k_bl_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.order, Lr, in.lvl);
         uint32_t s4[7] = {0, 0, 0, 0, 0, 0, 0};
