@@ -430,7 +430,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
 // The walk's workgroup: 256 threads (W0 + 3 worker waves, one per SIMD) or 512 (W0's SIMD partner, wave 4, idles
 // so that W0 keeps its SIMD's issue slots; 6 worker waves, two per SIMD, hide each other's latencies).
 #ifndef AD_BL_WT
-#define AD_BL_WT 256
+#define AD_BL_WT 512
 #endif
 constexpr int BL_WT = AD_BL_WT;
 constexpr int BL_NW = BL_WT == 512 ? BL_WT - 2 * WAVE : BL_WT - WAVE;   // worker threads
