@@ -242,6 +242,16 @@ __device__ inline void bl_carry_store(int2* carry, uint32_t slot, int2 c) {
     __hip_atomic_store(reinterpret_cast<uint64_t*>(&carry[slot]), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Phase clocks of the walk (AD_DEBUG_LEVELS prints them) only in AD_BL_TIMERS builds: a clock read waits for the
+// wave's outstanding LDS operations, which the timed code would otherwise overlap.
+__device__ inline uint64_t bl_clk() {
+#ifdef AD_BL_TIMERS
+    return clock64();
+#else
+    return 0;
+#endif
+}
+
 // Packed scan words: segment id in the high bits, value + BZ_BIAS in the low bits (u32: values < 2^20, i.e.
 // batches of <= 2^20 txns; u64 otherwise).  The word 0 is below every real entry's (ids count from 1).
 constexpr int BZ_BIAS = 1 << 12;
@@ -269,7 +279,7 @@ struct BzMax {
 template <int E, class PK>
 __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const int2* __restrict__ hc, int* lv,
                                      int2* ring, int rb, uint32_t* stuck, uint64_t* tph) {
-    const uint64_t tq0 = clock64();
+    const uint64_t tq0 = bl_clk();
     const int lane = __lane_id();
     uint32_t slot[E], ds[E], ep[E], rn[E], bs[E];
     bool wr[E], hd[E], lst[E], nle[E];
@@ -339,7 +349,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
     }
     const BzMax<PK> op{};
     uint32_t it = 0;
-    const uint64_t tq1 = clock64();
+    const uint64_t tq1 = bl_clk();
     tph[0] += tq1 - tq0;
     while (true) {
 #pragma unroll
@@ -378,7 +388,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
         // a broken invariant; stop (the host reports it) instead of spinning
         if (it > (uint32_t)BL_CAP + 1) { *stuck = 1u; break; }
     }
-    const uint64_t tq2 = clock64();
+    const uint64_t tq2 = bl_clk();
     // carry-out of the runs
     PK ry = 0, rw = 0, iy[E], iw[E];
 #pragma unroll
@@ -400,7 +410,7 @@ __device__ inline uint32_t bl_rounds(int nm, const uint4* __restrict__ cr, const
         const PK my = iny > iy[e] ? iny : iy[e], mw = inw > iw[e] ? inw : iw[e];
         ring[rb + (int)bs[e]] = make_int2(bz_val<PK>(my), bz_val<PK>(mw));
     }
-    tph[1] += clock64() - tq2;
+    tph[1] += bl_clk() - tq2;
     return it;
 }
 
@@ -627,7 +637,7 @@ static __global__ __launch_bounds__(BL_WT) void k_level_blocks(uint32_t B, const
     // blocks do not add to wave 0's register pressure in the rounds.
     if (tid < WAVE) {
         for (uint32_t b = 0; b < B; ++b) {
-            const uint64_t tb0 = clock64();
+            const uint64_t tb0 = bl_clk();
             BlStage& S = stg[b & 1];
             int* lv = lvb[b & 3];
             const int rb = (int)(b % 3) * BL_CAP;
@@ -641,7 +651,7 @@ static __global__ __launch_bounds__(BL_WT) void k_level_blocks(uint32_t B, const
                 const int lb = bl_sel(((uint32_t)e >> 12) & 1u, c.x, c.y) + 1;
                 if (lb > 0) atomicMax(&lv[((uint32_t)e >> 13) & BL_TL], lb);
             }
-            const uint64_t t1 = clock64();
+            const uint64_t t1 = bl_clk();
             if (nm > 0) {
                 uint32_t r;
                 const int epl = (nm + WAVE - 1) / WAVE;        // entries per lane
@@ -656,7 +666,7 @@ static __global__ __launch_bounds__(BL_WT) void k_level_blocks(uint32_t B, const
                 else r = bl_rounds<16, PK>(nm, S.cr, S.hc, lv, ring, rb, &sstuck, tph);
                 rounds += r;
             }
-            const uint64_t t2 = clock64();
+            const uint64_t t2 = bl_clk();
             tround += t2 - t1;
             // ring-continuing singleton runs: carry-out (the txn's level is final now)
             for (uint32_t k = lane; k < nbl; k += WAVE) {
@@ -666,10 +676,10 @@ static __global__ __launch_bounds__(BL_WT) void k_level_blocks(uint32_t B, const
                 const int l = lv[(e >> 10) & BL_TL];
                 ring[rb + (int)x] = make_int2(max(ci.x, l), bl_sel((e >> 21) & 1u, l, ci.y));
             }
-            const uint64_t t3 = clock64();
+            const uint64_t t3 = bl_clk();
             tlist += (t1 - tb0) + (t3 - t2);
             bl_barrier();
-            twait += clock64() - t3;
+            twait += bl_clk() - t3;
             if (sstuck) break;
         }
     } else if (BL_WT == 512 && tid / WAVE == 4) {
@@ -685,28 +695,28 @@ static __global__ __launch_bounds__(BL_WT) void k_level_blocks(uint32_t B, const
         if (B > 1) bl_load_static(bl_load_bounds(1, boff, tb, mt, lcnt), t, nthr, rec, crec, la, lb, cur);
         if (B > 2) bn = bl_load_bounds(2, boff, tb, mt, lcnt);
         for (uint32_t b = 0; b < B; ++b) {
-            const uint64_t tb0 = clock64();
+            const uint64_t tb0 = bl_clk();
             // issue first: block b + 1's global carry-ins and block b + 2's static loads; retire block b - 1 and
             // clear block b + 2's buffers while they are in flight
             uint64_t vc[BL_SI], vh[BL_SI];
             if (b + 1 < B) bl_load_carries(t, nthr, cur, carry, vc, vh);
             if (b + 2 < B) bl_load_static(bn, t, nthr, rec, crec, la, lb, nxt);
             if (b + 3 < B) bn = bl_load_bounds(b + 3, boff, tb, mt, lcnt);
-            const uint64_t tw1 = clock64();
+            const uint64_t tw1 = bl_clk();
             if (b > 0) {
                 const uint32_t p = b - 1;
                 maxl = max(maxl, bl_retire(t, nthr, stg[p & 1], bnd[p & 3], lvb[p & 3], ring, (int)(p % 3) * BL_CAP,
                                            carry, Lr));
             }
-            const uint64_t tw2 = clock64();
+            const uint64_t tw2 = bl_clk();
             {   // the buffers of block b + 2 (last used by block b - 2, retired in the previous phase)
                 int4* lc = reinterpret_cast<int4*>(lvb[(b + 2) & 3]);
                 for (int x = t; x < (BL_CAP + WAVE) / 4; x += nthr) lc[x] = make_int4(0, 0, 0, 0);
             }
-            const uint64_t tw3 = clock64();
+            const uint64_t tw3 = bl_clk();
             if (b + 1 < B) bl_stage_write(t, nthr, cur, vc, vh, stg[(b + 1) & 1], bnd[(b + 1) & 3], lvb[(b + 1) & 3]);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");    // the retired block's G carries
-            const uint64_t tw4 = clock64();
+            const uint64_t tw4 = bl_clk();
             twork += tw4 - tb0;
             tret += tw2 - tw1;
             tclr += tw3 - tw2;
