@@ -307,8 +307,9 @@ def roofline_of(eng, dom, n, P, st, large=False, pmc=True, steps=1):
     calls, ms, units = eng.kernel_stats()[dom]
     ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st, large, steps)
     achieved = ab / (ms * 1e-3) / 1e9
-    # the committed PMC passes (profiles/collect.sh) run the default C2 bench: other configs report no traffic
-    traffic, src = pmc_traffic(dom) if pmc else (None, None)
+    # the committed PMC passes (profiles/collect.sh) run the default C2 bench and C3 (pmc="c3"); C4 and the
+    # sharded lines report no traffic
+    traffic, src = pmc_traffic(dom, "c3" if pmc == "c3" else "") if pmc else (None, None)
     return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "alg_bytes_per_launch": ab / calls, "avg_launch_ms": ms / calls, "launches": calls}
@@ -330,10 +331,13 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<3>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<3>, 1024, 4>",
                      "ad::k_scan_apply<ad::OffsetsOp<3>, 256, 4>"),
     "order_sort": ("ad::k_window_rank", "ad::k_rank_check"),
+    # C3's executeAt-block level region (its block sort's radix kernels are shared names and not attributed)
+    "block_levels": ("ad::k_bl_erank", "ad::k_bl_chain_block", "ad::k_bl_bounds", "ad::k_bl_inverse",
+                     "ad::k_bl_records", "ad::k_bl_compact", "ad::k_level_blocks", "ad::k_bl_scatter"),
 }
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, tag=""):
     """HBM-side bytes per launch (per pipeline step for a composite region) of `kernel` from the newest committed
     PMC summary (profiles/*_pmc.json, written by profiles/collect.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3
     passes of this bench).  For a single kernel the largest-grid dispatch is the batch-sized one; a composite
@@ -343,6 +347,8 @@ def pmc_traffic(kernel):
     streams" also holds at 4 B/lane); random accesses are not calibrated.  None if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    files = [f for f in files if f.endswith("_%s_pmc.json" % tag)] if tag else \
+        [f for f in files if os.path.basename(f).count("_") == 2]          # rNN_vK_pmc.json: the C2 passes
     want = ROCPROF_NAME.get(kernel)
     if not files or not want:
         return None, None
@@ -574,7 +580,8 @@ def main():
     dt = t1 - t0
     st = eng.last_times()
     warn_level_fallback(st)
-    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc=cfgname == "C2", steps=args.steps)
+    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc={"C2": True, "C3": "c3"}.get(cfgname, False),
+                       steps=args.steps)
     mc = None
     if Q == 0:
         # side measurement, outside the timed region: the witnessedAt proposal (ad_max_conflicts) on the same
