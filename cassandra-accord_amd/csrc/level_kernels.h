@@ -702,6 +702,18 @@ __device__ inline void kahn_release_run(const uint32_t* __restrict__ ids, I b, I
     }
 }
 // ---------------------------------------------------------------------------------------------------
+// any key segment longer than SHORT_SEG: the chain build's long-chain test alone (no chain is built)
+static __global__ __launch_bounds__(256) void k_any_long_seg(size_t P, const int32_t* __restrict__ seg_start,
+                                                     uint32_t* __restrict__ any_long) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool lng = false;
+    if (j < P) {
+        const int32_t h = seg_start[j];
+        lng = h >= 0 && j - (size_t)h >= SHORT_SEG;
+    }
+    wave_set_flag(lng, any_long);
+}
+
 // Kahn chain build for batches with long chains (C3's Zipf hot keys: ~10^5 entries on one key), all
 // positions in parallel instead of one thread per segment:
 //   1. k_chain_rank: executeAt order inside each key segment by windowed inversion ranks (entries arrive in
@@ -1410,6 +1422,7 @@ struct LevelState {
     BlockBufs bl;                        // deep key-chain batches: executeAt blocks (block_levels.h)
     uint32_t bl_rounds = 0;              // block scan rounds of the last block-path run
     bool bl_used = false;                // the last run_levels took the block path
+    bool long_hint = false;              // the previous batch had long key chains: test for them up front
 };
 
 // The buffers order_rows needs for m rows (run_levels sizes them too; callers ordering rows without a
@@ -1868,6 +1881,25 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
             }
             return block_path();
         }
+        // a handle whose previous batch had long chains (C3's stream) tests for them with one light kernel and
+        // goes straight to the block path, instead of a pull pass that would find them and be discarded
+        if (ls.long_hint && pure && !in.keep_levels && P > 0 && in.kahn_ok && !ls.pull_off) {
+            k_any_long_seg<<<ceil_div((long)P, 256), 256, 0, st>>>(P, in.seg_start, ls.flags + 7);
+            if (hipMemcpyAsync(host, ls.flags, 32, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+                err = "exec levels: device error";
+                return AD_ERR_DEVICE;
+            }
+            if (host[7] && !host[5]) {
+                hipMemsetAsync(ls.flags + 7, 0, 4, st);
+                if (in.complete && in.complete(in.complete_ctx) != AD_OK) {   // the block path reads every entry
+                    err = "exec levels: device error";
+                    return AD_ERR_DEVICE;
+                }
+                return block_path();
+            }
+            if (host[7]) hipMemsetAsync(ls.flags + 7, 0, 4, st);
+            ls.long_hint = false;
+        }
         // ---- Kahn wavefront (short-chain key batches): chain build + wavefronts with no decision sync;
         // the first batch's readback also carries the kinds / long-chain flags, and a long chain found by
         // the build sends the batch to the fixpoint below
@@ -1915,7 +1947,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 err = "exec levels: device error";
                 return AD_ERR_DEVICE;
             }
-            if (lng) return block_path();                                  // deep key chains: executeAt blocks
+            if (lng) {                                                     // deep key chains: executeAt blocks
+                ls.long_hint = true;
+                return block_path();
+            }
             ls.pull_path = res[2] ? 2 : (res[0] ? 3 : 1);                   // 1 pulled, 2 far predecessors, 3 aborted
             if (!res[0] && !res[2]) {
                 const int lv = (int)res[1] + 1;

@@ -119,6 +119,23 @@ def test_blocks_pipeline_repeat(engine_factory):
         assert eng.last_times()["level_blocks"] > 0
 
 
+def test_long_chain_hint_alternating_batches(engine_factory):
+    # AUTO on one handle: after a deep batch the next batch is first tested for long chains (one light kernel)
+    # and goes straight to the block path; a short-chain batch after it must fall back to the pull path
+    eng = engine_factory(window=32, replicas=3, drop_p=0.1, seed=0xACC0D2)
+    eng.set_level_mode(engine.DepsEngine.LEVELS_AUTO)
+    cfg = abi.make_config(32, 3, 0.1, 0xACC0D2)
+    for name, n, blocks in (("C3", 60000, True), ("C3", 60000, True), ("C2", 50000, False), ("C2", 50000, False),
+                            ("C3", 90000, True)):
+        b = workload.config(name, n=n)
+        eng.load(b)
+        eng.run_pipeline()
+        lv, order = eng.fetch_levels()
+        rlv, rorder = O.OracleResult(b, cfg, O.FLAG_MERGE | O.FLAG_LEVELS).levels()
+        assert np.array_equal(lv, rlv) and np.array_equal(order, rorder), (name, n)
+        assert (eng.last_times()["level_blocks"] > 0) == blocks, (name, n)
+
+
 def test_blocks_mode_with_sync_points_takes_relaxation(engine_factory):
     # the block path covers pure Read/Write key batches only: with sync points a forced BLOCKS run resolves the
     # unmanaged waits on the relaxation path (its iteration count is not the depth) and still equals the oracle
