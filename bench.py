@@ -241,19 +241,26 @@ def end_to_end(eng, batch, steps):
         eng.load_commit()
         t_h2d = time.perf_counter() - t0
         eng.run_pipeline()
+        eng.fetch_merged_all(outs)               # (the first page-out into fresh pinned pages runs cold)
         t0 = time.perf_counter()
         eng.fetch_merged_all(outs)
         t_d2h = time.perf_counter() - t0
         # the stream: upload of the next batch overlapped with this batch's pipeline; every call's wall time is
         # recorded (host_ms) so a slow run names the call that was slow (round 3 saw 2.8 vs 5.8 ms on the same code
         # and could not say which part moved)
+        # two untimed stream steps first: the first page-outs into fresh pinned pages run at about half the
+        # steady rate (r04_v2: steps of 6.1, 5.6, then 3.65 ms), which made the mean swing with the step count
         k = 0
         eng.load_async(pb[k & 1])
         ph = {"commit": 0.0, "upload_issue": 0.0, "pipeline": 0.0, "fetch_merged": 0.0, "fetch_levels": 0.0}
-        per_step, dev_ms = [], 0.0
+        per_step, cold, dev_ms = [], [], 0.0
         clock = time.perf_counter
-        t0 = clock()
-        for _ in range(steps):
+        warm = 2
+        for i in range(warm + steps):
+            if i == warm:
+                t0 = clock()
+                ph = dict.fromkeys(ph, 0.0)
+                dev_ms = 0.0
             a = clock()
             eng.load_commit()
             b_ = clock()
@@ -270,7 +277,7 @@ def end_to_end(eng, batch, steps):
             for key, v in (("commit", b_ - a), ("upload_issue", c - b_), ("pipeline", d - c), ("fetch_merged", e - d),
                            ("fetch_levels", f - e)):
                 ph[key] += v
-            per_step.append((f - a) * 1e3)
+            (per_step if i >= warm else cold).append((f - a) * 1e3)
         dt = (clock() - t0) / steps
         eng.load_commit()
     finally:
@@ -280,6 +287,7 @@ def end_to_end(eng, batch, steps):
             "h2d_ms": t_h2d * 1e3, "d2h_ms": t_d2h * 1e3,
             "host_ms_per_step": {k_: round(v * 1e3 / steps, 3) for k_, v in ph.items()},
             "pipeline_device_ms": dev_ms / steps, "step_ms": [round(x, 3) for x in per_step],
+            "cold_step_ms": [round(x, 3) for x in cold],
             "what": "pinned host buffers; ad_load_batch_async(batch k+1) || ad_run_pipeline(batch k), "
                     "ad_fetch_merged_all (3 classes, one call) + ad_fetch_levels, ad_load_batch_commit"}
 
