@@ -514,7 +514,7 @@ def main_sharded(args, rank, world, local, dist):
         "dtype": "u32/u64 (integer)", "data": "synthetic (seeded C5 generator, BASELINE configs[4] shape)",
         "config": {"workload": "C5 generator: %d txns (%d per GPU) x 4 keys uniform over 10M keys, key-range sharded "
                                "over %d GPUs (cross-shard deps all-to-all to the home store, levels by %s); R=%d views, "
-                               "W=%d, drop %.1f" % (n_total, args.n, world, world, protocol, REPLICAS, WINDOW, DROP_P),
+                               "W=%d, drop %.1f" % (n_total, args.n, world, protocol, REPLICAS, WINDOW, DROP_P),
                    "txns_total": n_total, "txns_per_gpu": args.n, "local_txns_rank0": n_loc, "local_pairs_rank0": P_loc,
                    "keys_per_txn": 4, "keyspace": KEYSPACE, "replicas": REPLICAS, "window": WINDOW,
                    "parallelism": "key-range shards x%d" % world, "transport": tr.name, "level_rounds": rounds,
@@ -527,6 +527,62 @@ def main_sharded(args, rank, world, local, dist):
     store.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_contract(args):
+    """The --gpus / WORLD_SIZE contract, settled before anything touches a GPU.
+    * A launcher (torch.distributed.run) set WORLD_SIZE: it must equal --gpus, else exit 2 (a mismatch would
+      measure another world than the one the line names).
+    * No launcher and --gpus N > 1: start N fresh child processes of this script, one per rank (RANK, LOCAL_RANK,
+      WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), relay rank 0's stdout (the JSON line; the
+      other ranks' stdout goes to stderr) and return the first non-zero exit code, else 0.  A rank that fails ends
+      the others (their exact PIDs), so no rank waits for ever at a barrier.  The per-store fan-out this models is
+      CommandStores.mapReduce (accord-core/src/main/java/accord/local/CommandStores.java:576-593).
+    Returns None when this process is itself the rank to run."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print("bench.py: WORLD_SIZE=%s but --gpus %d; refusing to measure a different world" % (env_world, args.gpus),
+                  file=sys.stderr)
+            return 2
+        return None
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if args.gpus == 1:
+        return None
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
 
 
 def main():
@@ -549,11 +605,22 @@ def main():
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl", help="N>1 exchange: RCCL over xGMI or host/gloo")
     ap.add_argument("--no-scaling-ref", dest="scaling_ref", action="store_false",
                     help="N=1 C2: skip the scaling_reference side measurement (C5's per-GPU batch, one store)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)   # tests: report the rank env, no GPU
     args = ap.parse_args()
 
+    launched = launch_contract(args)
+    if launched is not None:
+        sys.exit(launched)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        if rank == 0 or world == 1:
+            print(json.dumps({"rank": rank, "world": world, "local": local, "gpus": args.gpus,
+                              "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))}))
+        else:
+            print("rank %d of %d (local %d)" % (rank, world, local), file=sys.stderr)
+        return
     if world > 1:
         args.n = args.n or C5_PER_GPU
         import torch.distributed as tdist
@@ -630,6 +697,9 @@ def main():
                      "level_iterations": st["level_iterations"], "level_path": st["level_path"]},
         "max_conflicts": mc,
         "end_to_end": e2e,
+        "value_scope": ("device-resident: the batch is uploaded (ad_load_batch) before the timed region and the "
+                        "results stay in HBM; end_to_end.value is the PCIe-inclusive rate SURVEY §8(d) describes "
+                        "(upload of the next batch overlapped, merged Deps + levels paged out)"),
         "cpu_baseline": None,
     }
     sample = args.cpu_sample if args.cpu_sample is not None else (1 << 14 if cfgname == "C4" else 1 << 18)

@@ -572,16 +572,17 @@ class GlooTransport:
         return self.any(changed)
 
 
-    def kahn_exchange(self, store, status):
+    def kahn_exchange(self, store, status, want_status=True):
         """One Kahn phase: every store's outbox to its destinations (all-to-all), the received messages into the
-        inbox; returns whether some store's status was set (the wave released something)."""
+        inbox; returns whether some store's status was set (the wave released something).  want_status=False (the
+        READY phase) skips that all-reduce and returns False."""
         cnt, msgs = store.kahn_outbox()
         rcnt = self.recv_sizes(cnt.astype(np.uint64))
         recv = self.torch.zeros(int(rcnt.sum()), dtype=self.torch.int64)
         self.dist.all_to_all_single(recv, self.torch.from_numpy(msgs.view(np.int64).copy()),
                                     output_split_sizes=[int(x) for x in rcnt], input_split_sizes=[int(x) for x in cnt])
         store.kahn_inbox(recv.numpy().view(np.uint64))
-        return self.any(status)
+        return self.any(status) if want_status else False
 
 
 class RcclUnavailable(RuntimeError):
@@ -646,7 +647,7 @@ class RcclTransport(GlooTransport):
             return store.levels_exchange()   # counts all-gather + pair send/recv, all over RCCL
         return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
-    def kahn_exchange(self, store, status):
+    def kahn_exchange(self, store, status, want_status=True):
         return store.kahn_exchange(status)   # counts + status all-gather, grouped send/recv, all over RCCL
 
 
@@ -704,6 +705,12 @@ def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
     sees the same global release flag, so all switch together) -- the one-exchange gather, which recomputes the
     levels from every store's constraint edges.  Returns the waves, or round_cap + 1 after the fallback."""
     lap = lap or (lambda name: None)
+    # the previous batch's depth on this store (every store agrees: one all-reduce per batch): a deep graph goes
+    # straight to the gather instead of spending round_cap waves to find out again (ADVICE r04)
+    if transport.any(getattr(store, "depth", 0) > round_cap):
+        store.depth = transport.gather_levels(store)
+        lap("levels_gather")
+        return round_cap + 1
     try:
         return run_levels_kahn(store, transport, round_cap, lap)
     except LevelsNotConverged:
@@ -733,7 +740,7 @@ def run_levels_kahn(store, transport, wave_cap=None, lap=None):
     lap("levels_local")
     level = 0
     while True:
-        transport.kahn_exchange(store, False)              # READYs -> coordinators
+        transport.kahn_exchange(store, False, want_status=False)   # READYs -> coordinators (no status needed)
         rel = store.kahn_decide()
         any_rel = transport.kahn_exchange(store, rel)      # RELEASEs -> holders; status: this store released some
         unreleased = store.kahn_apply(level)

@@ -100,6 +100,11 @@ static __global__ __launch_bounds__(256) void k_bl_bounds(uint32_t B, size_t n, 
 constexpr int BL_SH_W = 11, BL_SH_HEAD = 12, BL_SH_LAST = 13, BL_SH_G = 14, BL_SH_SRC = 15, BL_SH_RING = 17,
               BL_SH_R = 29;
 constexpr uint32_t BL_NONE = 0xFFFFFFFFu;
+static_assert(BL_CAP - 1 <= (int)BL_TL, "txn-in-block index must fit the record's 11-bit field");
+static_assert(3 * BL_CAP <= (1 << 12), "LDS ring index ((block % 3) * BL_CAP + slot) must fit 12 bits");
+// stats words: [0..15] the walk's (k_level_blocks, below), [16] k_bl_records' layout-violation flag
+constexpr int BL_STAT_RECORDS_BAD = 16;
+constexpr size_t BL_STATS_BYTES = 4 * (BL_STAT_RECORDS_BAD + 4);
 __device__ inline uint32_t bl_block_of(uint32_t q, const uint32_t* c_txn, const uint32_t* erank, const uint32_t* epre, uint32_t bcap) {
     return epre[erank[c_txn[q]]] / bcap;
 }

@@ -12,6 +12,9 @@ int ad_cfk_notify(ad_handle* h, const ad_cfk_state* s, uint8_t* not_waiting) {
         if (s->row_off[k + 1] < s->row_off[k]) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_notify: row_off must be non-decreasing");
     const size_t nm = n ? s->miss_off[n] : 0;
     if (n && s->miss_off[0] != 0) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_notify: miss_off must start at 0");
+    for (size_t i = 0; i < n; ++i)          // every row's missing run inside [0, miss_off[n]]: no read past the array
+        if (s->miss_off[i + 1] < s->miss_off[i] || s->miss_off[i + 1] > nm)
+            return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_notify: miss_off must be non-decreasing and end at the missing count");
     if (nm && !s->missing) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_notify: missing entries without an array");
     if (K == 0) return AD_OK;
     hipSetDevice(h->device);

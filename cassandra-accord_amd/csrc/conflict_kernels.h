@@ -405,6 +405,7 @@ struct PreacceptRules {
     const uint32_t* range_off;               // nullable: a key batch
     const uint64_t *rs, *re;
     const uint64_t *tm, *tl;
+    const int32_t* tn;                       // TxnId node: compareTo's last tiebreak (Timestamp.java:208-217)
     McIntervals rb;                          // rejectBefore
     int clock;                               // the timeout test applies
     uint64_t now_hlc, timeout;
@@ -425,7 +426,7 @@ static __global__ __launch_bounds__(256) void k_preaccept_rules(PreacceptRules a
         if (a.range_off)
             for (uint32_t q = a.range_off[t]; q < a.range_off[t + 1]; ++q) mci_span(a.rb, a.rs[q], a.re[q], rb, has);
         // any rejectIfBefore > TxnId rejects: the max over the footprint decides
-        expired = has && ts3_cmp(rb, Ts3{msb, lsb, 0}) > 0;
+        expired = has && ts3_cmp(rb, Ts3{msb, lsb, a.tn[t]}) > 0;   // the real TxnId (CommandStore.java:328)
     }
     if (!expired && kind != AD_KIND_EXCLUSIVE_SYNC_POINT) return;
     for (int v = 0; v < a.nv; ++v) a.fast[(size_t)v * a.n + t] = expired ? AD_FAST_REJECTED : 1;

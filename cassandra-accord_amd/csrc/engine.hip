@@ -684,7 +684,7 @@ static void apply_preaccept_rules(ad_handle* h, uint8_t* fast) {
     PreacceptRules r{};
     r.n = h->n; r.nv = (int)h->cfg.replicas; r.key_off = h->key_off; r.keys = h->keys;
     if (h->Q > 0) { r.range_off = h->range_off; r.rs = h->range_s; r.re = h->range_e; }
-    r.tm = h->tm; r.tl = h->tl;
+    r.tm = h->tm; r.tl = h->tl; r.tn = h->tn;
     r.rb = McIntervals{h->rb_m, h->rb_s, h->rb_e, h->rb_cm, h->rb_cl, h->rb_cn};
     r.clock = h->rb_clock; r.now_hlc = h->rb_now; r.timeout = h->rb_timeout;
     r.fast = fast;

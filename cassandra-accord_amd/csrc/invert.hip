@@ -38,13 +38,18 @@ int ad_fetch_inverse(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_
     k_inv_counts<<<ceil_div((long)m, 256), 256, 0, st>>>(a);
     scan_offsets(h, a.nt, tb, m);      // exclusive: [m + 1]
     scan_offsets(h, a.ne, eb, m);
-    std::vector<uint32_t> htb(m + 1), heb(m + 1);
+    std::vector<uint32_t> hcnt(2 * m), htb(m + 1), heb(m + 1);
+    HIPCHK(h, hipMemcpyAsync(hcnt.data(), cnt, 2 * m * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipMemcpyAsync(htb.data(), tb, (m + 1) * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipMemcpyAsync(heb.data(), eb, (m + 1) * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
-    const size_t NT = htb[m], E = heb[m];
-    if (NT + E >= (size_t)1 << 31)
+    // the totals in 64 bits from the per-row counts: the u32 prefix sums above wrap past 2^32
+    uint64_t NT64 = 0, E64 = 0;
+    for (size_t i = 0; i < m; ++i) { NT64 += hcnt[i]; E64 += hcnt[m + i]; }
+    if (NT64 + E64 >= (uint64_t)1 << 31)
         return set_err(h, AD_ERR_UNSUPPORTED, "ad_fetch_inverse: the window's inverse exceeds 2^31 ints (page a smaller row window)");
+    const size_t NT = htb[m], E = heb[m];
+    if (NT != NT64 || E != E64) return set_err(h, AD_ERR_DEVICE, "ad_fetch_inverse: device prefix sums disagree with the counts");
     *total = NT + E;
     if (off) for (size_t i = 0; i <= m; ++i) off[i] = htb[i] + heb[i];
     if (!inv) return AD_OK;

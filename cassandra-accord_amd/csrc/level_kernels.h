@@ -1678,7 +1678,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
             goto oom;
         bb.capB = c;
     }
-    if (!bb.stats && !grow((void**)&bb.stats, 64)) goto oom;
+    if (!bb.stats && !grow((void**)&bb.stats, BL_STATS_BYTES)) goto oom;
     {
         const size_t rneed = (3 * (radix_hist_len(std::max<size_t>(P, 1)) + 128) + 64 * 1024) * 4;
         if (bb.rs_cap < rneed) { if (!grow((void**)&bb.rs, rneed)) goto oom; bb.rs_cap = rneed; }
@@ -1690,7 +1690,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         const int gP = ceil_div((long)P, 256), gn = ceil_div((long)n, 256);
         // 1. chain order (key, executeAt): windowed inversion ranks, else the serial per-key insertion
         hipMemsetAsync(ls.c_pair, 0xFF, P * 4, st);
-        hipMemsetAsync(bb.stats, 0, 64, st);
+        hipMemsetAsync(bb.stats, 0, BL_STATS_BYTES, st);
         k_chain_rank<<<ceil_div((long)P, CR_N), CR_T, 0, st>>>(P, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval,
                                                                ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
         k_chain_check<<<std::min(gP, 2048), 256, 0, st>>>(P, in.seg_start, ls.c_exec1, ls.c_pair, bb.stats + 2);
@@ -1729,7 +1729,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         uint32_t* inv = sk == bb.bk ? bb.bk2 : bb.bk;         // the sort's free ping-pong buffer
         k_bl_inverse<<<gP, 256, 0, st>>>(P, sv, inv);
         k_bl_records<<<gP, 256, 0, st>>>(P, sk, sv, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.epre, bcap, bb.tb,
-                                         bb.boff, bb.rec, bb.stats + 3);
+                                         bb.boff, bb.rec, bb.stats + BL_STAT_RECORDS_BAD);
         k_bl_compact<<<nb, BL_T, 0, st>>>(nb, bb.boff, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt);
         // 4. the walk (packed scan words: 32-bit while every level fits 20 bits)
         // (no carry initialisation: a head reads a global carry only from a producer flagged to store it)
@@ -1741,12 +1741,12 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
             k_level_blocks<uint64_t><<<1, BL_WT, 0, st>>>(nb, bb.boff, bb.tb, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt, bb.carry, Lr,
                                                               bb.stats);
         k_bl_scatter<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.order, Lr, in.lvl);
-        uint32_t s4[7] = {0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpyAsync(s4, bb.stats, 28, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        uint32_t s4[BL_STATS_BYTES / 4] = {};
+        if (hipMemcpyAsync(s4, bb.stats, BL_STATS_BYTES, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
             err = "exec levels: device error";
             return AD_ERR_DEVICE;
         }
-        if (s4[3]) {
+        if (s4[BL_STAT_RECORDS_BAD]) {
             err = "exec levels: block layout invariant violated (txn index beyond the block)";
             return AD_ERR_STATE;
         }

@@ -140,3 +140,55 @@ def test_gpu_preaccept_rules_equal_oracle(engine_factory, timeout):
     _, plain = eng.max_conflicts()
     esp = (b["txn_lsb"] >> np.uint64(1)) & np.uint64(7) == abi.KIND_EXCLUSIVE_SYNC_POINT
     assert (plain != abi.FAST_REJECTED).all() and (plain[:, esp] == 1).all()
+
+
+def _tie_case(seed=11):
+    """rejectBefore entries equal to a txn's own TxnId (not rejected: `rejectIfBefore > txnId` is false on a tie,
+    CommandStore.java:328) and the same msb / hlc / flags from a lower and a higher node (only the higher one
+    rejects: node is compareTo's last tiebreak, Timestamp.java:208-217).  One key per txn over a wide keyspace,
+    so each mark stabs only the txn it was made for."""
+    b = workload.generate(400, keys_per_txn=1, keyspace=1 << 40, seed=seed)
+    rb = Wt.RejectBefore()
+    want = {}
+    for j, i in enumerate(range(5, 400, 7)):
+        k = int(b["keys"][b["key_off"][i]])
+        t = (int(b["txn_msb"][i]), int(b["txn_lsb"][i]), int(b["txn_node"][i]))
+        d = (0, -1, 1)[j % 3] if t[2] > 1 else (0, 1)[j % 2]
+        rb.add([(k - 1, k)], (t[0], t[1], t[2] + d))
+        want[i] = d > 0
+    return b, rb, want
+
+
+def test_reject_before_ties_on_the_real_txn_id():
+    b, rb, want = _tie_case()
+    cfg = abi.make_config(0, 1, 0.0, 0xE9)
+    try:
+        O.set_preaccept_expiry(0, O.NO_TIMEOUT, rb.table())
+        _, fast = O.max_conflicts(b, cfg)
+    finally:
+        O.set_preaccept_expiry()
+    for i, rej in want.items():
+        t = (int(b["txn_msb"][i]), int(b["txn_lsb"][i]), int(b["txn_node"][i]))
+        k = int(b["keys"][b["key_off"][i]])
+        assert rb.rejects(t, [k], []) == rej
+        assert (fast[0, i] == abi.FAST_REJECTED) == rej, i
+    assert any(want.values()) and not all(want.values())
+
+
+@pytest.mark.gpu
+def test_gpu_reject_before_ties_on_the_real_txn_id(engine_factory):
+    b, rb, want = _tie_case()
+    cfg = abi.make_config(0, 1, 0.0, 0xE9)
+    eng = engine_factory(window=0, replicas=1, drop_p=0.0, seed=0xE9)
+    eng.load(b)
+    eng.preaccept_deps()
+    eng.preaccept_expiry(0, eng.NO_TIMEOUT, rb.table())
+    _, d_fast = eng.max_conflicts()
+    try:
+        O.set_preaccept_expiry(0, O.NO_TIMEOUT, rb.table())
+        _, w_fast = O.max_conflicts(b, cfg)
+    finally:
+        O.set_preaccept_expiry()
+    assert np.array_equal(d_fast, w_fast)
+    for i, rej in want.items():
+        assert (d_fast[0, i] == abi.FAST_REJECTED) == rej, i

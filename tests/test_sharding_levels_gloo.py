@@ -355,6 +355,15 @@ def _auto_worker(rank, world, port, n, dist_kind, cap):
             assert rounds == cap + 1, "a deep graph falls back to the one-exchange gather"
         else:
             assert rounds <= cap, "a shallow graph finishes in Kahn waves"
+        # the next batch on the same store: the previous depth decides up front (a deep one skips the waves)
+        begun = []
+        store.kahn_begin = lambda f=store.kahn_begin: (begun.append(1), f())[1]
+        again = sharding.run_levels_auto(store, sharding.GlooTransport(dist), round_cap=cap)
+        assert np.array_equal(store.G[gid].astype(np.uint32), want[gid])
+        if dist_kind == "zipf":
+            assert again == cap + 1 and not begun, "deep again: straight to the gather"
+        else:
+            assert again <= cap and begun
     finally:
         dist.destroy_process_group()
 
