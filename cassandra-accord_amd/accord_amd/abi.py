@@ -51,6 +51,30 @@ class AdCfkState(C.Structure):
                 ("status", _u8p), ("miss_off", _u32p), ("missing", _u32p)]
 
 
+class AdCfkEvents(C.Structure):
+    """ad_cfk_events: CommandsForKey.update events for the resident store (ad_cfk_store_apply), grouped by key."""
+    _fields_ = [("m", C.c_size_t), ("ev_off", _u32p), ("txn_msb", _u64p), ("txn_lsb", _u64p), ("txn_node", _i32p),
+                ("status", _u8p), ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p),
+                ("deps_off", _u32p), ("deps_msb", _u64p), ("deps_lsb", _u64p), ("deps_node", _i32p)]
+
+
+CFK_EVENT_FIELDS = (("ev_off", np.uint32), ("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),
+                    ("status", np.uint8), ("exec_msb", np.uint64), ("exec_lsb", np.uint64), ("exec_node", np.int32),
+                    ("deps_off", np.uint32), ("deps_msb", np.uint64), ("deps_lsb", np.uint64), ("deps_node", np.int32))
+
+
+def make_cfk_events(ev):
+    """Dict of arrays (CFK_EVENT_FIELDS) -> (AdCfkEvents, keep-alive dict)."""
+    keep = {f: np.ascontiguousarray(ev[f], dt) for f, dt in CFK_EVENT_FIELDS}
+    s = AdCfkEvents()
+    s.m = len(keep["status"])
+    for f, dt in CFK_EVENT_FIELDS:
+        a = keep[f]
+        ct = {np.uint32: _u32p, np.uint64: _u64p, np.int32: _i32p, np.uint8: _u8p}[dt]
+        setattr(s, f, a.ctypes.data_as(ct) if a.size else None)
+    return s, keep
+
+
 CFK_STATE_FIELDS = (("row_off", np.uint32), ("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),
                     ("exec_msb", np.uint64), ("exec_lsb", np.uint64), ("exec_node", np.int32), ("status", np.uint8),
                     ("miss_off", np.uint32), ("missing", np.uint32))

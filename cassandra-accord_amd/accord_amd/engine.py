@@ -65,6 +65,10 @@ def lib():
         L.ad_fetch_inverse.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t),
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
         L.ad_cfk_notify.argtypes = [vp, C.POINTER(abi.AdCfkState), C.POINTER(C.c_uint8)]
+        L.ad_cfk_store_open.argtypes = [vp, C.c_uint32, C.c_uint32]
+        L.ad_cfk_store_apply.argtypes = [vp, C.POINTER(abi.AdCfkEvents)]
+        L.ad_cfk_store_notify.argtypes = [vp, vp, vp]
+        L.ad_cfk_store_fetch.argtypes = [vp, C.c_uint32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 9
         L.ad_preaccept_expiry.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
@@ -105,7 +109,7 @@ def lib():
 EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
@@ -298,6 +302,44 @@ class DepsEngine:
         out = np.zeros(max(s.rows, 1), np.uint8)
         self._check(lib().ad_cfk_notify(self.h, C.byref(s), out.ctypes.data_as(C.POINTER(C.c_uint8))), "ad_cfk_notify")
         return out[:s.rows]
+
+    # ---- device-resident CommandsForKey states (ad_cfk_store_*) -------------------------------------------------
+    def cfk_store_open(self, keys, capacity):
+        """K resident CFKs of up to `capacity` rows each (rounded up to a multiple of 64, at most 8192)."""
+        self._check(lib().ad_cfk_store_open(self.h, keys, capacity), "ad_cfk_store_open")
+        self._cs_keys, self._cs_cap = keys, (capacity + 63) // 64 * 64
+
+    def cfk_store_apply(self, events):
+        """CommandsForKey.update events (a dict of abi.CFK_EVENT_FIELDS arrays, grouped by key through ev_off)."""
+        s, keep = abi.make_cfk_events(events)
+        self._check(lib().ad_cfk_store_apply(self.h, C.byref(s)), "ad_cfk_store_apply")
+
+    def cfk_store_notify(self):
+        """notifyManaged's release rule over the resident rows: (rows [K], not_waiting [K, capacity] uint8)."""
+        rows = np.zeros(self._cs_keys, np.uint32)
+        out = np.zeros((self._cs_keys, self._cs_cap), np.uint8)
+        self._check(lib().ad_cfk_store_notify(self.h, rows.ctypes.data, out.ctypes.data), "ad_cfk_store_notify")
+        return rows, out
+
+    def cfk_store_fetch(self, key):
+        """One key's resident rows: dict of txn_msb/lsb/node, exec_msb/lsb/node, status, miss_off, missing (byId row
+        indices)."""
+        n, tot = C.c_size_t(), C.c_size_t()
+        nulls = [None] * 9
+        self._check(lib().ad_cfk_store_fetch(self.h, key, C.byref(n), C.byref(tot), *nulls), "ad_cfk_store_fetch")
+        r = n.value
+        out = {"txn_msb": np.zeros(max(r, 1), np.uint64), "txn_lsb": np.zeros(max(r, 1), np.uint64),
+               "txn_node": np.zeros(max(r, 1), np.int32), "exec_msb": np.zeros(max(r, 1), np.uint64),
+               "exec_lsb": np.zeros(max(r, 1), np.uint64), "exec_node": np.zeros(max(r, 1), np.int32),
+               "status": np.zeros(max(r, 1), np.uint8), "miss_off": np.zeros(r + 1, np.uint32),
+               "missing": np.zeros(max(tot.value, 1), np.uint32)}
+        order = ("txn_msb", "txn_lsb", "txn_node", "exec_msb", "exec_lsb", "exec_node", "status", "miss_off", "missing")
+        self._check(lib().ad_cfk_store_fetch(self.h, key, C.byref(n), C.byref(tot), *(out[f].ctypes.data for f in order)),
+                    "ad_cfk_store_fetch")
+        for f in order:
+            if f != "miss_off":
+                out[f] = out[f][:r if f != "missing" else tot.value]
+        return out
 
     def cfk_update(self, gid, status, exec_msb=None, exec_lsb=None, exec_node=None):
         """Status transitions of kept rows between batches (after cfk_retain, before the next load): gid[m]

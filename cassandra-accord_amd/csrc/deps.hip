@@ -124,16 +124,21 @@ int stage_deps(ad_handle* h) {
     for (int v = 0; v < nv; ++v) CK(alloc_csr(h, CSR_RANGE0 + v, h->rdeps[v], n));
     for (int k = 0; k < nc; ++k) dirty_csr(h, cls[k]);
     for (int v = 0; v < nv; ++v) dirty_csr(h, CSR_RANGE0 + v);
-    if (P > 0) {
-        // lone entries skipped when nothing of this stage reads them (PreAccept bound: the executeAt-bound walks
-        // visit every entry; large / range txns query every key in their ranges)
-        const bool skip = !h->accept && h->n_large == 0 && Q == 0 && h->key_bits <= 32;
+    // lone entries skipped when nothing of this stage reads them (PreAccept bound: the executeAt-bound walks
+    // visit every entry; large / range txns query every key in their ranges)
+    const bool skip = P > 0 && !h->accept && h->n_large == 0 && Q == 0 && h->key_bits <= 32;
+    // the same batches, unless a key segment outgrew a tile: gather + elision state + count walk in one kernel
+    // (seg_fuse_kernels.h); its overflow flag comes back with the totals, and an overflowing batch re-runs here on
+    // the three-kernel path
+    const bool fuse = skip && !h->seg_long;
+    uint32_t* fuse_over = h->totd + MAX_TOTALS - 5;
+    if (P > 0 && !fuse) {
         h->entries_partial = skip;
         KScope ks(K_GATHER, P);
         if (skip) k_gather_entries<true><<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->skey, h->e_txn, h->e_meta, h->e_exec1);
         else k_gather_entries<false><<<ceil_div((long)P, 256), 256, 0, st>>>(P, h->sval, h->prec, h->skey, h->e_txn, h->e_meta, h->e_exec1);
     }
-    if (P > 0) {
+    if (P > 0 && !fuse) {
         ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
                     h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm,
                     h->key_bits > 32 ? h->keys : nullptr, h->sval};
@@ -190,9 +195,27 @@ int stage_deps(ad_handle* h) {
     wa.vcnt = h->vcnt; wa.vdst = h->vcnt;
     wa.qpos = qpos; wa.ex1 = h->ex1; wa.bound_max = h->bound_max ? 1 : 0;
     wa.gqpos = (h->accept && h->sharded) ? h->gqpos : nullptr;
-    // [deferred txns, items, heavy-merge hint]; the pairs' counts (segment heads keep zero); deferred flags
-    fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
-    launch_walk_nv(nv, wa, false, direct, true, st);
+    // [overflow flag, deferred txns, items, heavy-merge hint]; the pairs' counts (segment heads keep zero);
+    // deferred flags
+    if (fuse) {
+        h->entries_partial = true;
+        fill_multi(st, {{fuse_over, 4, 0}, {dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
+        const size_t ntiles = (P + SF_TILE - 1) / SF_TILE;
+        SegFuseArgs f{};
+        f.P = P; f.ntiles = ntiles; f.skey = h->skey; f.prec = h->prec; f.overflow = fuse_over;
+        CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 2 * ntiles));
+        f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
+        f.pm_w = h->pm_w; f.pm_c = h->pm_c;
+        { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
+        {
+            KScope ks(K_SEG_KEYS, P);
+            k_seg_tile_scan<<<1, 1024, 0, st>>>(ntiles, P, f.tile_cnt, h->useg, h->prm);
+            k_seg_keys<<<(unsigned)ntiles, SF_T, 0, st>>>(f.tile_lo, f.tile_cnt, h->skey, h->hprm.key_min, h->ukey, h->useg, h->nh);
+        }
+    } else {
+        fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
+        launch_walk_nv(nv, wa, false, direct, true, st);
+    }
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
@@ -235,6 +258,8 @@ int stage_deps(ad_handle* h) {
     tt.src[tt.count++] = heavy;
     tt.src[tt.count++] = items_count;
     tt.src[tt.count++] = dtx_count;
+    const int col_over = tt.count;
+    tt.src[tt.count++] = fuse_over;
     // Speculative finish (small key batches whose key-class buffers from an earlier batch exist): k_txn_finish is
     // enqueued BEFORE the host reads the totals, into those buffers, behind k_cap_check's guard (a CSR total beyond
     // its buffer's capacity makes every thread exit).  The host reads the totals while the finish runs and re-runs
@@ -272,6 +297,13 @@ int stage_deps(ad_handle* h) {
         ta.spec_bad = nullptr;
     }
     CK(wait_totals(h, seq, tt.count, got.data()));
+    if (fuse && got[col_over] != 0) {
+        // a key segment too long for a k_seg_fuse tile: this batch takes the three-kernel path (the speculative
+        // finish, if any, exited or is redone there)
+        HIPCHK(h, hipStreamSynchronize(st));
+        h->seg_long = true;
+        return stage_deps(h);
+    }
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
     // k_txn_finish completes every small txn whose pairs kept all their ids inline; only the deferred ones need
     // the fill walk and the union (none on most C2 batches)
@@ -311,7 +343,7 @@ int stage_deps(ad_handle* h) {
     // small txns: k_txn_finish (re-walking in place the pairs that overflowed their inline ids); txns with more
     // than 4 keys (deferred) get their layout there and their lists from the fill walk of their pairs + k_txn_union
     // (unless the speculative launch above already did it)
-    const bool spec_ok = spec && got[ncol + 3] == 0;
+    const bool spec_ok = spec && got[col_over + 1] == 0;
     h->times.deps_speculative = spec ? (spec_ok ? 1u : 2u) : 0u;
     ta.w = wa;
     if (n > 0 && !spec_ok) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }

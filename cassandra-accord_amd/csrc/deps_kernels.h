@@ -532,11 +532,21 @@ __device__ inline void walk_entry(const WalkArgs& a, size_t s, uint32_t i, uint3
 }
 
 template <int NV, bool FILL, bool DIRECT>
+__device__ inline void walk_pair_entry(const WalkArgs& a, size_t s);
+
+template <int NV, bool FILL, bool DIRECT>
 static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
-    constexpr int NC = DIRECT ? 2 * NV : NV;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= (FILL ? a.nitems : (a.qpos ? a.P : a.P - a.prm->n_keys_u))) return;
     const size_t s = FILL ? (size_t)a.items[x] : (a.qpos ? x : (size_t)a.nh[x]);
+    walk_pair_entry<NV, FILL, DIRECT>(a, s);
+}
+
+// One sorted entry's query (count: counts, inline ids, overflow position, fill items; fill: the entries into their
+// slots).  The entry state arrays of `a` may point into LDS (k_seg_fuse: shifted so that [s] lands in the tile).
+template <int NV, bool FILL, bool DIRECT>
+__device__ inline void walk_pair_entry(const WalkArgs& a, size_t s) {
+    constexpr int NC = DIRECT ? 2 * NV : NV;
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
     // the pair's counts / slots live AoS by pair index (the per-txn kernels read them contiguously)

@@ -36,3 +36,13 @@ void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, bool pair
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st) {
     NV_DISPATCH(nv, launch_range, a, fill, st);
 }
+
+// k_seg_fuse (seg_fuse_kernels.h): gather + elision state + count walk per tile of key segments
+template <int NV>
+void launch_seg_fuse(const SegFuseArgs& f, const WalkArgs& w, bool direct, hipStream_t st) {
+    if (direct) k_seg_fuse<NV, true><<<(unsigned)f.ntiles, SF_T, 0, st>>>(f, w);
+    else k_seg_fuse<NV, false><<<(unsigned)f.ntiles, SF_T, 0, st>>>(f, w);
+}
+void launch_seg_fuse_nv(int nv, const SegFuseArgs& f, const WalkArgs& w, bool direct, hipStream_t st) {
+    NV_DISPATCH(nv, launch_seg_fuse, f, w, direct, st);
+}

@@ -394,8 +394,11 @@ void launch_mc_ranges(const McRangeArgs& a, hipStream_t st) {
 // The working buffers of a loaded batch of h->n rows, h->P pairs, h->Q ranges (grow-only slots).
 static int load_working(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
+    h->seg_long = false;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     CK(dalloc(h, S_PRM, &h->prm, 1)); CK(dalloc(h, S_TOT, &h->totd, MAX_TOTALS));
+    // a batch merged from host replies (ad_merge_host) never runs stage_prepare: its Params must read clean
+    HIPCHK(h, hipMemsetAsync(h->prm, 0, sizeof(Params), h->st));
     CK(dalloc(h, S_TXTS, &h->tx_ts, n)); CK(dalloc(h, S_EX1, &h->ex1, n)); CK(dalloc(h, S_META, &h->meta, n));
     CK(dalloc(h, S_PTXN, &h->prec, P));
     CK(dalloc(h, S_KA, &h->ka, P)); CK(dalloc(h, S_VA, &h->va, P)); CK(dalloc(h, S_KB, &h->kb, P)); CK(dalloc(h, S_VB, &h->vb, P));

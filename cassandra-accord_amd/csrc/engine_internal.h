@@ -26,6 +26,8 @@
 #include "history_kernels.h"
 #include "invert_kernels.h"
 #include "notify_kernels.h"
+#include "cfk_store_kernels.h"
+#include "seg_fuse_kernels.h"
 #include "recovery_kernels.h"
 #include "merge_kernels.h"
 #include "radix_sort.h"
@@ -169,6 +171,7 @@ struct ad_handle {
     const uint8_t* mc_fast = nullptr;  // [replicas * n] fast-path flags of the last ad_max_conflicts(_ts)
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     bool entries_partial = false;    // the deps stage skipped the lone entries' gather (complete_entries)
+    bool seg_long = false;           // the loaded batch has a key segment too long for k_seg_fuse's tiles
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
     bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
@@ -195,6 +198,15 @@ struct ad_handle {
     uint8_t* rc_rej = nullptr;
     uint64_t* rc_keys[RC_OUT] = {};
     uint32_t* rc_txn[RC_OUT] = {};
+    // device-resident CommandsForKey states (cfk_store_kernels.h, ad_cfk_store_*): K keys x cap byId rows
+    struct CfkStore {
+        uint32_t K = 0, cap = 0, words = 0;
+        uint32_t* cnt = nullptr;
+        uint64_t *tm = nullptr, *tl = nullptr, *em = nullptr, *el = nullptr, *bits = nullptr;
+        int32_t *tn = nullptr, *en = nullptr;
+        uint8_t *st = nullptr, *out = nullptr;
+        uint32_t *slot = nullptr, *pre = nullptr, *flags = nullptr;
+    } cs;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -284,8 +296,11 @@ enum Slot : size_t {
     S_STG0, S_STG_END = S_STG0 + 12,
     S_KSSRC, S_KSDST, S_KSSRC2, S_KSDST2, S_KSREM, S_KSXOFF, S_KSRCNT, S_KSFL, S_KSBASE, S_KSCNT, S_KSOUT,
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
+    S_CS0, S_CS_END = S_CS0 + 14,                               // resident CFK store (ad_cfk_store_*)
+    S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
+    S_SFLO, S_SFCNT,                                            // k_seg_fuse tiles
     S_NUM_FIXED,
-    S_CSR0 = 256
+    S_CSR0 = 320
 };
 static_assert(S_NUM_FIXED <= S_CSR0, "fixed device slots overlap the CSR slot blocks");
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
@@ -381,6 +396,7 @@ int fetch_rows(ad_handle* h, const Csr& c, int kw, size_t lo, size_t hi, ad_csr_
 int fetch_empty(ad_handle* h, ad_csr_out* out);
 // deps_walk.hip: count / fill walks of the key entries and virtual items, and the RangeDeps join
 void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, bool pairs, hipStream_t st);
+void launch_seg_fuse_nv(int nv, const SegFuseArgs& f, const WalkArgs& w, bool direct, hipStream_t st);
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st);
 // deps_layout.hip: per-txn offsets / layout / unions of the computed key classes
 void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count);

@@ -34,7 +34,14 @@ struct NotifyArgs {
     uint8_t* out;                            // [rows] 1: notWaiting on this key
     uint32_t* bad_order;                     // TxnIds not strictly ascending within a key
     uint32_t* bad_miss;                      // a missing index outside its key / not below its txn's bound
+    // device-resident store (cfk_store_kernels.h; row_off == nullptr): key k's rows are [k * cap, k * cap + cnt[k]),
+    // missing() as a bitmap over the key's slots (bits[(k * cap + slot) * words ...]) instead of the CSR
+    const uint32_t* cnt;
+    uint32_t cap, words;
+    const uint32_t* slot;
+    const uint64_t* bits;
 };
+constexpr uint32_t NF_MAX_WORDS = 128;       // the bitmap reader: at most 8192 rows per key
 
 __device__ inline bool nf_rw(uint64_t lsb) {             // managesExecution: key-domain Read / Write
     const uint32_t k = (uint32_t)(lsb >> 1) & 7u;
@@ -70,7 +77,9 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
     const size_t key = blockIdx.x;
     if (key >= a.K) return;
     const int tid = threadIdx.x;
-    const uint32_t lo = a.row_off[key], hi = a.row_off[key + 1], L = hi - lo;
+    const uint32_t lo = a.row_off ? a.row_off[key] : (uint32_t)key * a.cap;
+    const uint32_t hi = a.row_off ? a.row_off[key + 1] : lo + a.cnt[key], L = hi - lo;
+    __shared__ uint64_t s_mask[NF_MAX_WORDS];
     // pass 1: maxAW, order check, minUndecided
     Ts3 maw{0, 0, 0};
     bool has_maw = false, bad = false, bad_m = false;
@@ -147,6 +156,17 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
     }
     rstar = s_c[0];
     __syncthreads();
+    // bitmap reader: the slots whose missing bit counts -- Read / Write rows at or after minUndecided
+    if (a.bits) {
+        for (uint32_t w = tid; w < a.words; w += NF_T) s_mask[w] = 0ull;
+        __syncthreads();
+        for (uint32_t r = tid; r < L; r += NF_T)
+            if (r >= (minund == L ? 0u : minund) && nf_rw(a.tl[lo + r])) {
+                const uint32_t sl = a.slot[lo + r];
+                atomicOr((unsigned long long*)&s_mask[sl >> 6], 1ull << (sl & 63));
+            }
+        __syncthreads();
+    }
     // pass 4: per STABLE Read / Write row, the release test
     for (uint32_t r = tid; r < L; r += NF_T) {
         const size_t x = lo + r;
@@ -154,7 +174,8 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
         const uint8_t s = a.st[x];
         const uint64_t lsb = a.tl[x];
         // missing indices must lie in the segment
-        for (uint32_t m = a.miss_off[x]; m < a.miss_off[x + 1]; ++m) if (a.miss[m] >= L) bad_m = true;
+        if (!a.bits)
+            for (uint32_t m = a.miss_off[x]; m < a.miss_off[x + 1]; ++m) if (a.miss[m] >= L) bad_m = true;
         if (s == AD_ST_STABLE && nf_rw(lsb)) {
             const Ts3 e{a.em[x], a.el[x], a.en[x]};
             const bool eligible = (!has_maw || ts3_cmp(e, maw) > 0) && (!has_ws || ts3_cmp(e, ws) <= 0);
@@ -169,9 +190,14 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
                 const uint32_t und_rw = blo < L ? a.pre[(lo + blo) * 2 + 1] : carry_rw;
                 const uint32_t expect = nf_write(lsb) ? rstar + und_rw : und_w;
                 uint32_t mc = 0;
-                for (uint32_t m = a.miss_off[x]; m < a.miss_off[x + 1]; ++m) {
-                    const uint32_t j = a.miss[m];
-                    if (j < L && j >= (minund == L ? 0u : minund) && nf_rw(a.tl[lo + j])) ++mc;   // minUndecided null: from 0
+                if (a.bits) {
+                    const uint64_t* row = a.bits + ((size_t)lo + a.slot[x]) * a.words;
+                    for (uint32_t w = 0; w < a.words; ++w) mc += (uint32_t)__popcll(row[w] & s_mask[w]);
+                } else {
+                    for (uint32_t m = a.miss_off[x]; m < a.miss_off[x + 1]; ++m) {
+                        const uint32_t j = a.miss[m];
+                        if (j < L && j >= (minund == L ? 0u : minund) && nf_rw(a.tl[lo + j])) ++mc;   // minUndecided null: from 0
+                    }
                 }
                 rel = expect == mc ? 1 : 0;
             }

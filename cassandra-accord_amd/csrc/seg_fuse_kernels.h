@@ -1,0 +1,214 @@
+// seg_fuse_kernels.h — the deps stage's front for PreAccept batches of small key txns (C2), one kernel instead of
+// three: the sorted entries' gather, CommandsForKey.mapReduceActive's per-key elision state (the ElideOp scan) and
+// the count walk, per tile of whole key segments in LDS.
+//
+// The elision state is a SEGMENTED prefix (it restarts at every key: CommandsForKey.java:925-983 reads one key's
+// byId), so a tile that starts and ends on key-segment boundaries needs nothing from its neighbours: each tile of
+// SF_TILE nominal sorted positions moves its start and end forward to the next segment head (one 64-lane ballot
+// per step), loads its keys, gathers the records of the entries in multi-entry segments (an entry alone in its
+// segment is read by no query of the batch: complete_entries fills it in for the stages that read every entry),
+// resolves each segment's state serially in LDS (a C2 segment holds ~1.5 entries), writes the state arrays the
+// later stages read (seg_start for every entry; txn, meta, executeAt + 1, last always-emitted entry and the two
+// prefix maxima for the multi-entry segments), and runs every non-head entry's query against the LDS copy.
+// Replaces k_gather_entries<true> + the three ElideOp scan launches + k_deps_walk<count>, whose reads of the
+// per-entry arrays were spread over every sorted position (C2: 767,867 queries among 4,194,304 entries; the walk
+// fetched 9.5x its byte model).  The distinct keys, segment starts and the dense non-head list (ElideOp's store)
+// follow from the per-tile head counts: k_seg_tile_scan (one workgroup) + k_seg_keys.
+// A tile longer than SF_CAP (a key segment of more than ~500 entries: Zipf hot keys) raises *overflow and the
+// host runs the three-kernel path instead (the handle then remembers the batch had long segments).
+#pragma once
+#include "deps_kernels.h"
+
+namespace ad {
+
+constexpr int SF_T = 256;
+constexpr int SF_TILE = 1024;                  // nominal sorted positions per tile
+constexpr int SF_CAP = 1536;                   // LDS entries per tile: the tile + its last segment's tail
+
+struct SegFuseArgs {
+    size_t P, ntiles;
+    const uint32_t* skey;                      // sorted (key - key_min), 32-bit spreads
+    const PairRec* prec;
+    uint32_t* tile_lo;                         // [ntiles + 1] each tile's first sorted position
+    uint32_t* tile_cnt;                        // [2 * ntiles]: heads, non-heads
+    uint32_t* overflow;
+    uint32_t *e_txn;                           // global entry state (written)
+    uint8_t* e_meta;
+    uint64_t* e_exec1;
+    int32_t *seg_start, *ud_prev;
+    uint64_t *pm_w, *pm_c;
+};
+
+constexpr uint32_t SF_NONE = 0xFFFFFFFFu;
+// first segment head at or after x (x == P: P), searched by one wave 64 positions at a time; SF_NONE if none within
+// SF_CAP positions
+__device__ inline uint32_t sf_next_head(const uint32_t* __restrict__ skey, size_t P, size_t x) {
+    const int lane = __lane_id();
+    for (uint32_t d = 0; d < (uint32_t)SF_CAP + 64; d += WAVE) {
+        const size_t y = x + d + lane;
+        const bool h = y >= P || y == 0 || skey[y] != skey[y - 1];
+        const uint64_t m = __ballot(h);
+        if (m) return (uint32_t)(x + d + (__ffsll((unsigned long long)m) - 1));
+    }
+    return SF_NONE;
+}
+
+template <int NV, bool DIRECT>
+static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArgs w) {
+    __shared__ uint32_t s_key[SF_CAP + 1];
+    __shared__ uint32_t s_txn[SF_CAP];
+    __shared__ uint8_t s_meta[SF_CAP];
+    __shared__ uint64_t s_ex1[SF_CAP];
+    __shared__ int32_t s_ss[SF_CAP];
+    __shared__ int32_t s_ud[SF_CAP];
+    __shared__ uint64_t s_pw[SF_CAP];
+    __shared__ uint64_t s_pc[SF_CAP];
+    __shared__ uint32_t s_bounds[2];
+    __shared__ uint32_t s_cnt[2];
+    const size_t b = blockIdx.x;
+    const int tid = threadIdx.x, wv = tid / WAVE;
+    const size_t P = f.P;
+    if (wv < 2) {
+        const size_t x = (b + wv) * (size_t)SF_TILE;
+        const uint32_t hd = x >= P ? (uint32_t)P : sf_next_head(f.skey, P, x);
+        if (__lane_id() == 0) s_bounds[wv] = hd;
+    }
+    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
+    __syncthreads();
+    if (s_bounds[0] == SF_NONE || s_bounds[1] == SF_NONE || s_bounds[1] - min(s_bounds[0], s_bounds[1]) > (uint32_t)SF_CAP) {
+        // a key segment too long for one tile: the host takes the three-kernel path
+        if (tid == 0) *f.overflow = 1u;
+        return;
+    }
+    const uint32_t lo = s_bounds[0];
+    const uint32_t hi = max(s_bounds[1], lo);
+    if (tid == 0) {
+        f.tile_lo[b] = lo;
+        if (b + 1 == f.ntiles) f.tile_lo[f.ntiles] = (uint32_t)P;
+    }
+    const uint32_t L = hi - lo;
+    // keys (+ the next tile's first key: a head, or P)
+    for (uint32_t i = tid; i < L; i += SF_T) s_key[i] = f.skey[lo + i];
+    __syncthreads();
+    // heads / lone flags; gather the records of multi-entry segments
+    uint32_t heads = 0, nonheads = 0;
+    for (uint32_t i = tid; i < L; i += SF_T) {
+        const bool head = i == 0 || s_key[i] != s_key[i - 1];
+        const bool last = i + 1 == L || s_key[i + 1] != s_key[i];
+        heads += head ? 1u : 0u;
+        nonheads += head ? 0u : 1u;
+        if (!(head && last)) {
+            const PairRec r = f.prec[w.sval[lo + i]];
+            s_txn[i] = r.txn; s_meta[i] = (uint8_t)r.meta; s_ex1[i] = r.ex1;
+            f.e_txn[lo + i] = r.txn; f.e_meta[lo + i] = (uint8_t)r.meta; f.e_exec1[lo + i] = r.ex1;
+        }
+    }
+    atomicAdd(&s_cnt[0], heads);
+    atomicAdd(&s_cnt[1], nonheads);
+    __syncthreads();
+    // per segment (its head's thread): the elision scan state, serially (ElideOp::combine restarted at the head)
+    for (uint32_t i = tid; i < L; i += SF_T) {
+        if (!(i == 0 || s_key[i] != s_key[i - 1])) continue;
+        const int32_t hs = (int32_t)(lo + i);
+        uint32_t e = i + 1;
+        while (e < L && s_key[e] == s_key[i]) ++e;
+        if (e == i + 1) {                                     // lone: only its segment start (the rest: complete_entries)
+            f.seg_start[lo + i] = hs;
+            continue;
+        }
+        int32_t ud = -1;
+        uint64_t pw = 0, pc = 0;
+        for (uint32_t q = i; q < e; ++q) {
+            const uint32_t m = s_meta[q];
+            const uint32_t cat = category(m);
+            const uint64_t x1 = s_ex1[q];
+            if (cat == CAT_ALWAYS) ud = (int32_t)(lo + q);
+            if (cat == CAT_ELIDABLE) {
+                pc = x1 > pc ? x1 : pc;
+                if (meta_kind(m) == AD_KIND_WRITE) pw = x1 > pw ? x1 : pw;
+            }
+            s_ss[q] = hs; s_ud[q] = ud; s_pw[q] = pw; s_pc[q] = pc;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < L; i += SF_T) {
+        const bool head = i == 0 || s_key[i] != s_key[i - 1];
+        const bool last = i + 1 == L || s_key[i + 1] != s_key[i];
+        if (head && last) continue;
+        f.seg_start[lo + i] = s_ss[i]; f.ud_prev[lo + i] = s_ud[i]; f.pm_w[lo + i] = s_pw[i]; f.pm_c[lo + i] = s_pc[i];
+    }
+    if (tid == 0) { f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1]; }
+    // the queries of the non-head entries, against the LDS copy (sorted position s -> s - lo)
+    WalkArgs a = w;
+    a.e_txn = s_txn - lo; a.e_meta = s_meta - lo; a.e_exec1 = s_ex1 - lo; a.seg_start = s_ss - lo; a.ud_prev = s_ud - lo;
+    a.pm_w = s_pw - lo; a.pm_c = s_pc - lo;
+    for (uint32_t i0 = 0; i0 < L; i0 += SF_T) {
+        const uint32_t i = i0 + tid;
+        const bool q = i < L && i > 0 && s_key[i] == s_key[i - 1];
+        if (q) walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + i);
+    }
+}
+
+// Exclusive prefix of the tiles' head / non-head counts (one workgroup); n_keys_u = the heads, useg[U] = P.
+static __global__ __launch_bounds__(1024) void k_seg_tile_scan(size_t ntiles, size_t P, uint32_t* __restrict__ tile_cnt,
+                                                               uint32_t* __restrict__ useg, Params* prm) {
+    __shared__ uint32_t s_h[1024], s_n[1024];
+    uint32_t carry_h = 0, carry_n = 0;
+    for (size_t base = 0; base < ntiles; base += 1024) {
+        const size_t t = base + threadIdx.x;
+        const uint32_t h = t < ntiles ? tile_cnt[2 * t] : 0u, nn = t < ntiles ? tile_cnt[2 * t + 1] : 0u;
+        s_h[threadIdx.x] = h; s_n[threadIdx.x] = nn;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint32_t yh = threadIdx.x >= (unsigned)o ? s_h[threadIdx.x - o] : 0u;
+            const uint32_t yn = threadIdx.x >= (unsigned)o ? s_n[threadIdx.x - o] : 0u;
+            __syncthreads();
+            s_h[threadIdx.x] += yh; s_n[threadIdx.x] += yn;
+            __syncthreads();
+        }
+        if (t < ntiles) { tile_cnt[2 * t] = carry_h + s_h[threadIdx.x] - h; tile_cnt[2 * t + 1] = carry_n + s_n[threadIdx.x] - nn; }
+        carry_h += s_h[1023]; carry_n += s_n[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        useg[carry_h] = (uint32_t)P;
+        prm->n_keys_u = carry_h;
+    }
+}
+
+// ElideOp's store, per tile: the distinct keys (ukey, useg) and the dense list of non-head entries (nh), in order.
+static __global__ __launch_bounds__(SF_T) void k_seg_keys(const uint32_t* __restrict__ tile_lo, const uint32_t* __restrict__ tile_cnt,
+                                                          const uint32_t* __restrict__ skey, uint64_t key_min,
+                                                          uint64_t* __restrict__ ukey, uint32_t* __restrict__ useg,
+                                                          uint32_t* __restrict__ nh) {
+    __shared__ uint32_t s_w[SF_T / WAVE][2];
+    const size_t b = blockIdx.x;
+    const uint32_t lo = tile_lo[b], hi = tile_lo[b + 1];
+    uint32_t ch = tile_cnt[2 * b], cn = tile_cnt[2 * b + 1];
+    const int tid = threadIdx.x, lane = __lane_id(), wv = tid / WAVE;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t base = lo; base < hi; base += SF_T) {
+        const uint32_t s = base + tid;
+        const bool in = s < hi;
+        const bool head = in && (s == 0 || skey[s] != skey[s - 1]);
+        const bool non = in && !head;
+        const uint64_t mh = __ballot(head), mn = __ballot(non);
+        if (lane == 0) { s_w[wv][0] = (uint32_t)__popcll(mh); s_w[wv][1] = (uint32_t)__popcll(mn); }
+        __syncthreads();
+        uint32_t ph = ch, pn = cn, th = 0, tn = 0;
+        for (int k = 0; k < SF_T / WAVE; ++k) {
+            if (k < wv) { ph += s_w[k][0]; pn += s_w[k][1]; }
+            th += s_w[k][0]; tn += s_w[k][1];
+        }
+        if (head) {
+            const uint32_t u = ph + (uint32_t)__popcll(mh & below);
+            ukey[u] = (uint64_t)skey[s] + key_min;
+            useg[u] = s;
+        }
+        if (non) nh[pn + (uint32_t)__popcll(mn & below)] = s;
+        ch += th; cn += tn;
+        __syncthreads();
+    }
+}
+
+}  // namespace ad

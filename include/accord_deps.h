@@ -459,6 +459,45 @@ typedef struct ad_cfk_state {
 } ad_cfk_state;
 int  ad_cfk_notify(ad_handle* h, const ad_cfk_state* s, uint8_t* not_waiting /* [rows] */);
 
+/* Device-resident CommandsForKey states.  The handle keeps `keys` CFKs of up to `capacity` TxnInfo rows
+ * each in HBM -- byId rows (TxnId, InternalStatus, executeAt) and their missing() sets -- and applies the host's
+ * stream of CommandsForKey.update calls to them on the device:
+ *   CommandsForKey.update / Updating.insertOrUpdate   local/cfk/CommandsForKey.java:987-1057, Updating.java:99-358
+ *   (missing() maintained as the reference does: a row with deps misses every undecided txn below its depsKnownBefore
+ *   it witnesses and its deps lack; deps unknown to the CFK become TRANSITIVELY_KNOWN rows, :178-227; a newly known
+ *   undecided txn joins, a txn that commits or is invalidated leaves, every other row's missing set --
+ *   Utils.addToMissingArrays / removeFromMissingArrays, Utils.java:70-172)
+ *   Updating.updateUnmanaged's insertAdditionsOnly (:452-514): an event with status TRANSITIVELY_KNOWN
+ * Ballots are zero: an event whose InternalStatus does not rise above the row's is ignored.  Events are grouped by key
+ * (ev_off[key] .. ev_off[key + 1]) and applied in order per key, keys in parallel (one workgroup each).
+ * ad_cfk_store_notify then runs CommandsForKey.notifyManaged's release rule (as ad_cfk_notify) over the resident
+ * rows -- nothing is uploaded -- and ad_cfk_store_fetch reads one key back in ad_cfk_state's layout (missing() as byId
+ * row indices).  capacity <= 8192 (rounded up to a multiple of 64); AD_ERR_UNSUPPORTED when a key outgrows it.
+ * Not pruned (Pruning.java:164-233 runs on the batch rows, ad_cfk_retain).                                           */
+typedef struct ad_cfk_events {
+    size_t m;                       /* events                                                          */
+    const uint32_t* ev_off;         /* [keys + 1] events of key k: [ev_off[k], ev_off[k + 1])          */
+    const uint64_t* txn_msb;        /* [m] the command's TxnId (lsb: flags with kind and domain)       */
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint8_t*  status;         /* [m] its InternalStatus after the update (AD_ST_*)              */
+    const uint64_t* exec_msb;       /* [m] executeAt (statuses ACCEPTED .. APPLIED)                   */
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const uint32_t* deps_off;       /* [m + 1] the command's deps at this key (statuses with deps)     */
+    const uint64_t* deps_msb;       /*         TxnIds strictly ascending                              */
+    const uint64_t* deps_lsb;
+    const int32_t*  deps_node;
+} ad_cfk_events;
+int  ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity);
+int  ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev);
+int  ad_cfk_store_notify(ad_handle* h, uint32_t* rows /* [keys] */, uint8_t* not_waiting /* [keys * capacity] */);
+/* one key's rows: *rows (and *missing total); arrays may be NULL (two calls); miss_off[rows + 1], missing = byId row
+ * indices within the key, ascending per row */
+int  ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missing_total, uint64_t* txn_msb,
+                        uint64_t* txn_lsb, int32_t* txn_node, uint64_t* exec_msb, uint64_t* exec_lsb, int32_t* exec_node,
+                        uint8_t* status, uint32_t* miss_off, uint32_t* missing);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU key-range sharding (one handle = one CommandStore = one GPU).                     */
 /*                                                                                             */

@@ -531,6 +531,7 @@ class CFK:
         self.ids = []
         self.info = {}
         self.unmanageds = []                          # sorted (pending, waitingUntil, txnId)
+        self.log = None                               # list: the CommandsForKey.update calls as device events
 
     def copy(self):
         c = CFK(self.domains)
@@ -585,6 +586,8 @@ class CFK:
         if new is None:
             return False, None, None
         t = cmd.txn
+        if self.log is not None:                      # (txnId, InternalStatus, executeAt, deps) as ad_cfk_store_apply takes it
+            self.log.append((t, new, cmd.execute_at if has_deps(new) else t, tuple(cmd.deps) if has_deps(new) else ()))
         cur = self.info.get(t)
         if cur is not None and new <= cur.status:      # ballots ZERO: only a higher InternalStatus updates
             return False, None, None
@@ -763,6 +766,8 @@ class CFK:
             if not ready_to_apply:
                 for a in missing:                     # insertAdditionsOnly (:452-514)
                     self._insert(Info(a, TK, a))
+                    if self.log is not None:
+                        self.log.append((a, TK, a, ()))
                 for a in missing:
                     self._add_missing_everywhere(a)
                 rec = (APPLY_P, executes_at, wt) if waiting_to_apply else (COMMIT_P, tx[-1], wt)
@@ -812,8 +817,9 @@ class Run:
     """One seed of the restated harness.  events: per update, (txnId, SaveStatus) and the managed notifications it
     caused; snapshots: the CFK after events chosen by `snapshot_every` (and every event with a notification)."""
 
-    def __init__(self, seed, min_count, snapshot_every=0, check_full_scan=False, count_gating=False):
+    def __init__(self, seed, min_count, snapshot_every=0, check_full_scan=False, count_gating=False, log=False):
         self.seed = seed
+        self.event_log = [] if log else None          # per harness event: the CFK update calls it made (CFK.log)
         rnd = Rnd(seed)
         self.run_task_chance = max(0.01, float(rnd.next_float()))
         import numpy as np
@@ -824,6 +830,8 @@ class Run:
         self.domains = {}
         canon = Canon(rnd, self.domains)
         cfk = CFK(self.domains)
+        if log:
+            cfk.log = []
         self.canon, self.cfk = canon, cfk
         self.snapshots = []                           # (event, rows, notified-and-STABLE set, full-scan release set)
         self.events = 0
@@ -870,6 +878,9 @@ class Run:
                 # harness or the release rule reads, and is not modelled)
                 cfk.update_unmanaged(nxt, canon.not_waiting, True)
             self.events += 1
+            if log:
+                self.event_log.append(list(cfk.log))
+                cfk.log.clear()
             fresh = [t for t, _ in canon.notified[before:] if canon.manages_execution(t)]
             self.notified.update(fresh)
             if count_gating and gating_cases(cfk):
