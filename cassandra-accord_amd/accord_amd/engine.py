@@ -119,8 +119,8 @@ EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_
             "ad_recover", "ad_fetch_recovery", "ad_fetch_recovery_flags", "ad_shard_level_edges", "ad_shard_levels_solve",
             "ad_shard_levels_gather", "ad_ephemeral_read_deps", "ad_load_batch_async", "ad_load_batch_commit",
             "ad_host_alloc", "ad_host_free", "ad_merged_sizes", "ad_fetch_merged_all", "ad_shard_kahn_begin",
-            "ad_shard_kahn_outbox", "ad_shard_kahn_inbox", "ad_shard_kahn_exchange", "ad_shard_kahn_decide",
-            "ad_shard_kahn_apply", "ad_shard_kahn_sent")
+            "ad_shard_kahn_outbox", "ad_shard_kahn_inbox", "ad_shard_kahn_exchange", "ad_shard_kahn_step",
+            "ad_shard_kahn_finish", "ad_shard_kahn_sent")
 
 
 class PinnedArena:

@@ -248,8 +248,8 @@ class ShardStore:
         L.ad_shard_kahn_outbox.argtypes = [vp, C.POINTER(C.c_uint32), u64p]
         L.ad_shard_kahn_inbox.argtypes = [vp, u64p, C.c_size_t]
         L.ad_shard_kahn_exchange.argtypes = [vp, C.c_uint32, C.POINTER(C.c_uint32)]
-        L.ad_shard_kahn_decide.argtypes = [vp, C.POINTER(C.c_uint32)]
-        L.ad_shard_kahn_apply.argtypes = [vp, C.c_uint32, C.POINTER(C.c_uint64)]
+        L.ad_shard_kahn_step.argtypes = [vp, C.c_uint32]
+        L.ad_shard_kahn_finish.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.ad_shard_kahn_sent.argtypes = [vp, C.POINTER(C.c_uint64)]
         self.delta = False
         self.pairs_sent = 0
@@ -446,22 +446,21 @@ class ShardStore:
         self._check(self.L.ad_shard_kahn_inbox(self.eng.h, m.ctypes.data_as(C.POINTER(C.c_uint64)) if m.size else None,
                                                m.size), "ad_shard_kahn_inbox")
 
-    def kahn_exchange(self, status):
-        """RCCL: the outbox to the peers, theirs into the inbox; returns whether some store's status was set."""
+    def kahn_exchange(self):
+        """RCCL: the outbox to the holders, theirs into the inbox; returns whether any store sent anything."""
         a = C.c_uint32()
-        self._check(self.L.ad_shard_kahn_exchange(self.eng.h, 1 if status else 0, C.byref(a)), "ad_shard_kahn_exchange")
+        self._check(self.L.ad_shard_kahn_exchange(self.eng.h, 0, C.byref(a)), "ad_shard_kahn_exchange")
         return bool(a.value)
 
-    def kahn_decide(self):
-        """Home store: READYs counted, complete txns released (RELEASE outbox); returns whether it released any."""
-        r = C.c_uint32()
-        self._check(self.L.ad_shard_kahn_decide(self.eng.h, C.byref(r)), "ad_shard_kahn_decide")
-        return bool(r.value)
+    def kahn_step(self, level):
+        """One wave on the device: READYs counted, rows every holder reported released at `level`, their successors'
+        READYs into the outbox (no host wait)."""
+        self._check(self.L.ad_shard_kahn_step(self.eng.h, level), "ad_shard_kahn_step")
 
-    def kahn_apply(self, level):
-        """Every holder: RELEASEs get `level`, successors' READYs fill the outbox; returns the rows still unreleased."""
+    def kahn_finish(self):
+        """After the last wave: the local rows never released (a cycle if any)."""
         u = C.c_uint64()
-        self._check(self.L.ad_shard_kahn_apply(self.eng.h, level, C.byref(u)), "ad_shard_kahn_apply")
+        self._check(self.L.ad_shard_kahn_finish(self.eng.h, C.byref(u)), "ad_shard_kahn_finish")
         return u.value
 
     def kahn_sent(self):
@@ -572,17 +571,19 @@ class GlooTransport:
         return self.any(changed)
 
 
-    def kahn_exchange(self, store, status, want_status=True):
-        """One Kahn phase: every store's outbox to its destinations (all-to-all), the received messages into the
-        inbox; returns whether some store's status was set (the wave released something).  want_status=False (the
-        READY phase) skips that all-reduce and returns False."""
+    def kahn_exchange(self, store):
+        """One Kahn wave's exchange: every store's outbox to its destinations (all-to-all), the received READYs into the
+        inbox; returns whether any store sent anything (the counts all-to-all already tells every store what it gets;
+        one all-reduce of the sent totals ends the waves on every store together)."""
         cnt, msgs = store.kahn_outbox()
+        if not self.any(int(cnt.sum()) > 0):
+            return False
         rcnt = self.recv_sizes(cnt.astype(np.uint64))
         recv = self.torch.zeros(int(rcnt.sum()), dtype=self.torch.int64)
         self.dist.all_to_all_single(recv, self.torch.from_numpy(msgs.view(np.int64).copy()),
                                     output_split_sizes=[int(x) for x in rcnt], input_split_sizes=[int(x) for x in cnt])
         store.kahn_inbox(recv.numpy().view(np.uint64))
-        return self.any(status) if want_status else False
+        return True
 
 
 class RcclUnavailable(RuntimeError):
@@ -647,8 +648,8 @@ class RcclTransport(GlooTransport):
             return store.levels_exchange()   # counts all-gather + pair send/recv, all over RCCL
         return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
-    def kahn_exchange(self, store, status, want_status=True):
-        return store.kahn_exchange(status)   # counts + status all-gather, grouped send/recv, all over RCCL
+    def kahn_exchange(self, store):
+        return store.kahn_exchange()         # counts all-gather (the wave's one host sync), grouped send/recv over RCCL
 
 
 class LevelsNotConverged(RuntimeError):
@@ -719,36 +720,24 @@ def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
         return round_cap + 1
 
 
-def kahn_coord(g, holders):
-    """The store that coordinates txn g in the Kahn waves (csrc/kahn_shard_kernels.h ks_coord): the
-    (g mod holders)-th set bit of its holder mask."""
-    k, m = int(g) % bin(int(holders)).count("1"), int(holders)
-    for _ in range(k):
-        m &= m - 1
-    return (m & -m).bit_length() - 1
-
-
 def run_levels_kahn(store, transport, wave_cap=None, lap=None):
-    """Distributed Kahn waves (ad_shard_kahn_*, csrc/kahn_shard_kernels.h): wave l moves the READYs of the rows whose
-    local predecessors are all released to their coordinators (kahn_coord: one holder per txn, spread evenly), the
-    coordinators release the txns every holder reported (level l) and send RELEASE to the holders, which record
-    the level and free their successors.  Stops
-    after the first wave that released nothing anywhere; raises LevelsNotConverged past wave_cap waves (all stores
-    together).  Sets store.depth and store.kahn_bytes (8 B per message sent to another store); returns the waves."""
+    """Distributed Kahn waves (ad_shard_kahn_*, csrc/kahn_shard_kernels.h), one exchange per wave: the READYs of the rows
+    whose local predecessors are all released go to every holder of their txn; every holder releases (at this wave)
+    the txns all their holders reported and frees their successors, whose READYs form the next wave.  Stops at the first
+    exchange in which no store sent anything; raises LevelsNotConverged past wave_cap waves (all stores together).  Sets
+    store.depth and store.kahn_bytes (8 B per message sent to another store); returns the waves + 1 (the final, empty
+    exchange)."""
     lap = lap or (lambda name: None)
     store.kahn_begin()
     lap("levels_local")
     level = 0
-    while True:
-        transport.kahn_exchange(store, False, want_status=False)   # READYs -> coordinators (no status needed)
-        rel = store.kahn_decide()
-        any_rel = transport.kahn_exchange(store, rel)      # RELEASEs -> holders; status: this store released some
-        unreleased = store.kahn_apply(level)
-        if not any_rel:
-            break
+    while transport.kahn_exchange(store):
+        store.kahn_step(level)
         level += 1
         if wave_cap is not None and level >= wave_cap:
+            store.kahn_finish()
             raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
+    unreleased = store.kahn_finish()
     lap("levels_waves")
     if unreleased:
         raise engine.AccordDepsError(abi.AD_ERR_ARGUMENT, "Kahn waves: %d rows never released (a cycle)" % unreleased)
@@ -844,29 +833,30 @@ class LocalTransport:
 
     @staticmethod
     def _kahn(stores, wave_cap):
-        """run_levels_kahn for stores in one process: each phase's outboxes routed to the inboxes."""
+        """run_levels_kahn for stores in one process: each wave's outboxes routed to the inboxes."""
         def route():
             out = [s.kahn_outbox() for s in stores]
+            if not any(int(cnt.sum()) for cnt, _ in out):
+                return False
             for d, s in enumerate(stores):
                 parts = []
                 for cnt, msgs in out:
                     o = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
                     parts.append(msgs[o[d]:o[d + 1]])
                 s.kahn_inbox(np.concatenate(parts) if parts else np.zeros(0, np.uint64))
+            return True
         for s in stores:
             s.kahn_begin()
         level = 0
-        while True:
-            route()
-            rel = [s.kahn_decide() for s in stores]
-            route()
-            unreleased = [s.kahn_apply(level) for s in stores]
-            if not any(rel):
-                break
+        while route():
+            for s in stores:
+                s.kahn_step(level)
             level += 1
             if wave_cap is not None and level >= wave_cap:
+                for s in stores:
+                    s.kahn_finish()
                 raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
-        if any(unreleased):
+        if any(s.kahn_finish() for s in stores):
             raise engine.AccordDepsError(abi.AD_ERR_ARGUMENT, "Kahn waves: rows never released (a cycle)")
         for s in stores:
             s.depth = level

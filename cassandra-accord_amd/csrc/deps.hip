@@ -131,7 +131,7 @@ int stage_deps(ad_handle* h) {
     // (seg_fuse_kernels.h); its overflow flag comes back with the totals, and an overflowing batch re-runs here on
     // the three-kernel path
     const bool fuse = skip && !h->seg_long;
-    uint32_t* fuse_over = h->totd + MAX_TOTALS - 5;
+    uint32_t* fuse_over = h->totd + MAX_TOTALS - 6;      // (MAX_TOTALS - 5: the merge's speculation guard)
     if (P > 0 && !fuse) {
         h->entries_partial = skip;
         KScope ks(K_GATHER, P);
@@ -209,8 +209,9 @@ int stage_deps(ad_handle* h) {
         { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
         {
             KScope ks(K_SEG_KEYS, P);
-            k_seg_tile_scan<<<1, 1024, 0, st>>>(ntiles, P, f.tile_cnt, h->useg, h->prm);
-            k_seg_keys<<<(unsigned)ntiles, SF_T, 0, st>>>(f.tile_lo, f.tile_cnt, h->skey, h->hprm.key_min, h->ukey, h->useg, h->nh);
+            k_seg_tile_scan<<<1, 1024, 0, st>>>(ntiles, P, f.tile_cnt, h->useg, h->prm, fuse_over);
+            k_seg_keys<<<(unsigned)ntiles, SF_T, 0, st>>>(f.tile_lo, f.tile_cnt, h->skey, h->hprm.key_min, h->ukey, h->useg, h->nh,
+                                                          fuse_over);
         }
     } else {
         fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
@@ -220,7 +221,9 @@ int stage_deps(ad_handle* h) {
     ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
-    if (n > 0 && h->V > 0) {
+    // every large txn's per-CSR totals, also when no range meets a CFK key (V = 0: a batch of range txns only); the
+    // offsets scan reads them for every large txn
+    if (n > 0 && h->n_large > 0) {
         KScope ks(K_VITEMS);
         launch_large_sums_nv(nv, ta, direct, st);
     }

@@ -151,7 +151,7 @@ struct ad_handle {
     uint64_t *ks_out = nullptr, *ks_in = nullptr, *ks_xoff = nullptr;
     size_t ks_in_m = 0, ks_unreleased = 0;
     uint64_t ks_sent = 0;            // messages this batch sent to other stores
-    int ks_phase = -1;               // the outbox holds 0: READY, 1: RELEASE messages
+    int ks_phase = -1;               // 0 after ad_shard_kahn_begin: the outbox holds the next wave's READYs
     bool ks_levels = false;          // lvl holds this batch's levels from the Kahn waves (ad_shard_order reads them)
     // MaxConflicts carried from earlier batches (ad_max_conflicts_carry): sorted keys + timestamps on the device
     size_t mc_m = 0;

@@ -1,37 +1,28 @@
 // kahn_shard_kernels.h — execution levels of a key-range sharded batch as distributed Kahn wavefronts
-// (SURVEY §8e, round 4).
+// (round 4, one exchange per wave since round 5).
 //
 // Every execution constraint is local to one store (global_levels.h): an (a) key-chain edge lives with the key's
 // store, a (b) direct / range dependency edge and a (c) unmanaged chain bound with a store whose slice both ends
-// touch.  So a txn's level is 1 + the greatest level of its predecessors over the stores that hold it, and it can
-// be released at level l once EVERY holder has released all of its local predecessors by level l - 1.  Per wave
-// (level) l, each store
-//   1. sends READY(txn) to the txn's coordinator (one of its holders, ks_coord) for every local row whose last
-//      local predecessor was released at level l - 1 (level 0: the rows without local predecessors);
-//   2. coordinators count READYs; a txn whose count reaches its holder count is released at level l, and
-//      RELEASE(txn) goes to every holder (itself included);
-//   3. every store applies the RELEASEs: the row's level is l, its local successors' remaining in-degrees drop, and
-//      those reaching zero are step 1 of wave l + 1.
-// Waves stop when one released nothing.  Each txn costs (holders) READY + (holders) RELEASE messages in total, once
-// per batch -- not once per round as the delta exchange's raised levels, nor every store's edges on every store as
-// the one-exchange gather -- and each store touches only its own edges.  Messages are u64 (global rank in the low
-// word); regions per destination are sized by what can be sent there at most (a row is ready once; a coordinated
-// txn released once), so appends never overflow.
+// touch.  So a txn's level is 1 + the greatest level of its predecessors over the stores that hold it: it is
+// released at wave l once EVERY holder has released all of its local predecessors by wave l - 1.  Per wave l:
+//   1. exchange: every store's READY(txn) messages reach the txn's holders (the store itself included: its own
+//      region is a device copy);
+//   2. every holder counts the READYs of its rows; a row whose count reaches its txn's holder count is released at
+//      level l -- on every holder in the same wave, since every holder receives the same READYs -- its local
+//      successors' remaining in-degrees drop, and those reaching zero send READY to all of their txn's holders
+//      (wave l + 1's messages).
+// Waves stop at the first exchange that moves nothing anywhere (every store sees the same count matrix).  One
+// exchange and one host synchronisation (the count all-gather that sizes the receives) per wave; the round-4 protocol
+// sent READY to one coordinating holder and RELEASE back (two exchanges and four host round trips per wave).  A txn
+// costs holders x holders READYs over the batch (holders x (holders - 1) over the network).  Messages are u64 (global
+// rank in the low word); the region for destination d holds at most one READY per local row d also holds, so appends
+// never overflow.
 #pragma once
 #include "shard_kernels.h"
 
 namespace ad {
 
 constexpr uint32_t KS_UNRELEASED = 0xFFFFFFFFu;
-
-// The store that counts a txn's READYs and sends its RELEASEs: one of its holders, picked by global rank (the
-// (g mod holders)-th set bit of the holder mask), so the coordination spreads evenly over the stores.  (The txn's
-// home store -- its first key's -- would coordinate ~41 % of C5's txns on store 0 at N = 8.)
-__host__ __device__ inline uint32_t ks_coord(uint32_t g, uint32_t holders) {
-    uint32_t k = g % (uint32_t)__builtin_popcount(holders), m = holders;
-    for (; k > 0; --k) m &= m - 1u;
-    return (uint32_t)__builtin_ctz(m);
-}
 
 // One message per lane to the region of `dest` (wave-aggregated append; every lane of the wave must call it).
 __device__ inline void ks_append(bool want, uint32_t dest, uint64_t msg, const uint32_t* __restrict__ base,
@@ -57,6 +48,13 @@ __device__ inline size_t ks_row(const uint32_t* __restrict__ gid, size_t n, uint
     return (lo < n && gid[lo] == g) ? lo : n;
 }
 
+// READY(g) of row r to every holder of its txn (this store included), one wave-aggregated append per destination
+__device__ inline void ks_ready_all(bool want, uint32_t holders, uint64_t msg, const uint32_t* __restrict__ base,
+                                    uint32_t* __restrict__ cnt, uint64_t* __restrict__ out) {
+#pragma unroll
+    for (int d = 0; d < MAX_STORES; ++d) ks_append(want && ((holders >> d) & 1u), (uint32_t)d, msg, base, cnt, out);
+}
+
 // Wave 0: every row starts unreleased; rows without local predecessors are ready.
 static __global__ __launch_bounds__(256) void k_ks_init(size_t n, const uint32_t* __restrict__ gid, const uint8_t* __restrict__ holders,
                                                  const uint32_t* __restrict__ rem, uint32_t* __restrict__ lvl,
@@ -64,53 +62,26 @@ static __global__ __launch_bounds__(256) void k_ks_init(size_t n, const uint32_t
                                                  uint32_t* __restrict__ cnt, uint64_t* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool want = false;
-    uint32_t dest = 0;
+    uint32_t hm = 0;
     uint64_t msg = 0;
     if (i < n) {
         lvl[i] = KS_UNRELEASED;
         rcnt[i] = 0;
-        if (rem[i] == 0) { want = true; dest = ks_coord(gid[i], holders[i]); msg = gid[i]; }
+        if (rem[i] == 0) { want = true; hm = holders[i]; msg = gid[i]; }
     }
-    ks_append(want, dest, msg, base, cnt, out);
+    ks_ready_all(want, hm, msg, base, cnt, out);
 }
 
-// Coordinator: READYs in; a txn whose count reaches its holder count is released at `level` -> RELEASE to every
-// holder.  bad[0]: a message for a row this store does not coordinate; flag[0]: released something.
-static __global__ __launch_bounds__(256) void k_ks_decide(size_t m, const uint64_t* __restrict__ in, size_t n,
-                                                   const uint32_t* __restrict__ gid, uint32_t self,
-                                                   const uint8_t* __restrict__ holders, uint32_t* __restrict__ rcnt,
-                                                   const uint32_t* __restrict__ base, uint32_t* __restrict__ cnt,
-                                                   uint64_t* __restrict__ out, uint32_t* __restrict__ flag,
-                                                   uint32_t* __restrict__ bad) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t mask = 0;
-    uint64_t msg = 0;
-    bool b = false;
-    if (i < m) {
-        const uint32_t g = (uint32_t)in[i];
-        const size_t r = ks_row(gid, n, g);
-        if (r >= n || ks_coord(g, holders[r]) != self) {
-            b = true;
-        } else {
-            const uint32_t hm = holders[r];
-            if (atomicAdd(&rcnt[r], 1u) + 1u == (uint32_t)__popc(hm)) { mask = hm; msg = g; }
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < MAX_STORES; ++d) ks_append((mask >> d) & 1u, (uint32_t)d, msg, base, cnt, out);
-    wave_set_flag(mask != 0, flag);
-    wave_set_flag(b, bad);
-}
-
-// Every holder: RELEASEs in -> the row's level, then its local successors' remaining in-degrees; rows reaching
-// zero send READY to their coordinator (the next wave).  flag[1] += rows released here.
-static __global__ __launch_bounds__(256) void k_ks_apply(size_t m, const uint64_t* __restrict__ in, size_t n, uint32_t level,
-                                                  const uint32_t* __restrict__ gid, const uint8_t* __restrict__ holders,
-                                                  const uint64_t* __restrict__ xoff, const uint32_t* __restrict__ xs,
-                                                  uint32_t* __restrict__ rem, uint32_t* __restrict__ lvl,
-                                                  const uint32_t* __restrict__ base, uint32_t* __restrict__ cnt,
-                                                  uint64_t* __restrict__ out, uint32_t* __restrict__ flag,
-                                                  uint32_t* __restrict__ bad) {
+// One wave: the READYs received in; a row whose count reaches its holder count is released at `level`, its local
+// successors' remaining in-degrees drop, and the rows reaching zero send READY to every holder (the next wave).
+// flag[1] += rows released; bad[0]: a READY for a row this store does not hold, or for a released row.
+static __global__ __launch_bounds__(256) void k_ks_step(size_t m, const uint64_t* __restrict__ in, size_t n, uint32_t level,
+                                                 const uint32_t* __restrict__ gid, const uint8_t* __restrict__ holders,
+                                                 const uint64_t* __restrict__ xoff, const uint32_t* __restrict__ xs,
+                                                 uint32_t* __restrict__ rem, uint32_t* __restrict__ lvl,
+                                                 uint32_t* __restrict__ rcnt, const uint32_t* __restrict__ base,
+                                                 uint32_t* __restrict__ cnt, uint64_t* __restrict__ out,
+                                                 uint32_t* __restrict__ flag, uint32_t* __restrict__ bad) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t beg = 0, end = 0;
     bool b = false, got = false;
@@ -118,7 +89,7 @@ static __global__ __launch_bounds__(256) void k_ks_apply(size_t m, const uint64_
         const size_t r = ks_row(gid, n, (uint32_t)in[i]);
         if (r >= n || lvl[r] != KS_UNRELEASED) {
             b = true;
-        } else {
+        } else if (atomicAdd(&rcnt[r], 1u) + 1u == (uint32_t)__popc(holders[r])) {
             lvl[r] = level;
             beg = xoff[r]; end = xoff[r + 1];
             got = true;
@@ -130,13 +101,13 @@ static __global__ __launch_bounds__(256) void k_ks_apply(size_t m, const uint64_
         const bool has = beg + k < end;
         if (!__ballot(has)) break;
         bool want = false;
-        uint32_t dest = 0;
+        uint32_t hm = 0;
         uint64_t msg = 0;
         if (has) {
             const uint32_t s = xs[beg + k];
-            if (atomicSub(&rem[s], 1u) == 1u) { want = true; dest = ks_coord(gid[s], holders[s]); msg = gid[s]; }
+            if (atomicSub(&rem[s], 1u) == 1u) { want = true; hm = holders[s]; msg = gid[s]; }
         }
-        ks_append(want, dest, msg, base, cnt, out);
+        ks_ready_all(want, hm, msg, base, cnt, out);
     }
     wave_set_flag(b, bad);
 }

@@ -150,9 +150,13 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
 }
 
 // Exclusive prefix of the tiles' head / non-head counts (one workgroup); n_keys_u = the heads, useg[U] = P.
+// Both run before the host has read k_seg_fuse's overflow flag: after an overflow (some tiles never wrote their bounds
+// or counts) they do nothing, and the host re-runs the batch on the three-kernel path.
 static __global__ __launch_bounds__(1024) void k_seg_tile_scan(size_t ntiles, size_t P, uint32_t* __restrict__ tile_cnt,
-                                                               uint32_t* __restrict__ useg, Params* prm) {
+                                                               uint32_t* __restrict__ useg, Params* prm,
+                                                               const uint32_t* __restrict__ overflow) {
     __shared__ uint32_t s_h[1024], s_n[1024];
+    if (*(const volatile uint32_t*)overflow) return;
     uint32_t carry_h = 0, carry_n = 0;
     for (size_t base = 0; base < ntiles; base += 1024) {
         const size_t t = base + threadIdx.x;
@@ -180,8 +184,9 @@ static __global__ __launch_bounds__(1024) void k_seg_tile_scan(size_t ntiles, si
 static __global__ __launch_bounds__(SF_T) void k_seg_keys(const uint32_t* __restrict__ tile_lo, const uint32_t* __restrict__ tile_cnt,
                                                           const uint32_t* __restrict__ skey, uint64_t key_min,
                                                           uint64_t* __restrict__ ukey, uint32_t* __restrict__ useg,
-                                                          uint32_t* __restrict__ nh) {
+                                                          uint32_t* __restrict__ nh, const uint32_t* __restrict__ overflow) {
     __shared__ uint32_t s_w[SF_T / WAVE][2];
+    if (*(const volatile uint32_t*)overflow) return;
     const size_t b = blockIdx.x;
     const uint32_t lo = tile_lo[b], hi = tile_lo[b + 1];
     uint32_t ch = tile_cnt[2 * b], cn = tile_cnt[2 * b + 1];

@@ -1,8 +1,9 @@
 // shard_kahn.hip — execution levels of a key-range sharded batch by distributed Kahn wavefronts
-// (kahn_shard_kernels.h has the protocol).  Per wave the host moves two message sets between the stores: READYs
-// (to the txn's coordinator, one of its holders) and RELEASEs (from the coordinator to every holder).  RCCL moves them device to device
-// (ad_shard_kahn_exchange: per-destination counts + a status word all-gathered, then grouped send/recv); host
-// transports use ad_shard_kahn_outbox / ad_shard_kahn_inbox.
+// (kahn_shard_kernels.h has the protocol).  Per wave the host moves one message set between the stores: every
+// store's READYs to the txns' holders.  RCCL moves them device to device (ad_shard_kahn_exchange: the per-destination
+// counts all-gathered -- the wave's one host synchronisation -- then grouped send/recv); host transports use
+// ad_shard_kahn_outbox / ad_shard_kahn_inbox.  ad_shard_kahn_step then runs the wave on the device without waiting for
+// it; ad_shard_kahn_finish reads the error flags and the released count once, after the last wave.
 #include "engine_internal.h"
 #include "global_levels.h"
 #include "kahn_shard_kernels.h"
@@ -13,7 +14,7 @@ using namespace ad;
 
 namespace {
 
-uint32_t* ks_base(ad_handle* h, int phase) { return h->ks_base_dev + (size_t)phase * (MAX_STORES + 1); }
+uint32_t* ks_base(ad_handle* h) { return h->ks_base_dev; }
 
 int ks_bad(ad_handle* h, const char* what) {
     uint32_t bad = 0;
@@ -53,23 +54,13 @@ int ad_shard_kahn_begin(ad_handle* h) {
     CK(dalloc(h, S_KSREM, &h->ks_rem, n1)); CK(dalloc(h, S_KSXOFF, &h->ks_xoff, n + 1));
     CK(dalloc(h, S_KSRCNT, &h->ks_rcnt, n1)); CK(dalloc(h, S_KSFL, &h->ks_flag, 16));
     CK(dalloc(h, S_KSBASE, &h->ks_base_dev, 2 * (MAX_STORES + 1))); CK(dalloc(h, S_KSCNT, &h->ks_cnt_dev, MAX_STORES + 1));
-    // outbox regions: READY to d <= local rows d coordinates; RELEASE to d <= rows this store coordinates that d holds
-    std::vector<uint32_t> gids(n);
-    if (n) HIPCHK(h, hipMemcpyAsync(gids.data(), h->gid, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(h, hipStreamSynchronize(st));
-    std::vector<uint64_t> rc(W, 0), lc(W, 0);
-    for (size_t i = 0; i < n; ++i) {
-        const uint32_t c = ks_coord(gids[i], h->holders_host[i]);
-        rc[c]++;
-        if (c == h->self)
-            for (uint32_t d = 0; d < W; ++d) lc[d] += (h->holders_host[i] >> d) & 1u;
-    }
+    // outbox regions: READY to d <= the local rows whose txn d holds (each row is ready once)
+    std::vector<uint64_t> lc(W, 0);
+    for (size_t i = 0; i < n; ++i)
+        for (uint32_t d = 0; d < W; ++d) lc[d] += (h->holders_host[i] >> d) & 1u;
     h->ks_base.assign(2 * (MAX_STORES + 1), 0);
-    for (uint32_t d = 0; d < W; ++d) {
-        h->ks_base[d + 1] = h->ks_base[d] + (uint32_t)rc[d];
-        h->ks_base[MAX_STORES + 1 + d + 1] = h->ks_base[MAX_STORES + 1 + d] + (uint32_t)lc[d];
-    }
-    const size_t cap = std::max<size_t>(std::max(h->ks_base[W], h->ks_base[MAX_STORES + 1 + W]), 1);
+    for (uint32_t d = 0; d < W; ++d) h->ks_base[d + 1] = h->ks_base[d] + (uint32_t)lc[d];
+    const size_t cap = std::max<size_t>(h->ks_base[W], 1);
     CK(dalloc(h, S_KSOUT, &h->ks_out, cap));
     HIPCHK(h, hipMemcpyAsync(h->ks_base_dev, h->ks_base.data(), 2 * (MAX_STORES + 1) * 4, hipMemcpyHostToDevice, st));
     HIPCHK(h, hipMemsetAsync(h->ks_rem, 0, n1 * 4, st));
@@ -87,7 +78,7 @@ int ad_shard_kahn_begin(ad_handle* h) {
     }
     HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
     if (n) k_ks_init<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->gid, h->holders, h->ks_rem, h->lvl, h->ks_rcnt,
-                                                             ks_base(h, 0), h->ks_cnt_dev, h->ks_out);
+                                                             ks_base(h), h->ks_cnt_dev, h->ks_out);
     HIPCHK(h, hipGetLastError());
     CK(ks_bad(h, "ad_shard_kahn_begin: a level edge out of range or a self edge"));
     h->ks_phase = 0;
@@ -109,7 +100,7 @@ int ad_shard_kahn_outbox(ad_handle* h, uint32_t* counts, uint64_t* msgs) {
     HIPCHK(h, hipMemcpyAsync(counts, h->ks_cnt_dev, W * 4, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     if (msgs) {
-        const uint32_t* b = h->ks_base.data() + (size_t)h->ks_phase * (MAX_STORES + 1);
+        const uint32_t* b = h->ks_base.data();
         size_t at = 0;
         for (uint32_t d = 0; d < W; ++d) {
             if (counts[d]) HIPCHK(h, hipMemcpyAsync(msgs + at, h->ks_out + b[d], (size_t)counts[d] * 8, hipMemcpyDeviceToHost, h->st));
@@ -134,9 +125,9 @@ int ad_shard_kahn_inbox(ad_handle* h, const uint64_t* msgs, size_t m) {
     return AD_OK;
 }
 
-// RCCL: the per-destination counts plus this store's status word all-gathered (a world x (world + 1) matrix), then
-// the regions by grouped point-to-point send/recv into the inbox (this store's own region by a device copy).
-// *any_status: some store's status word was nonzero.
+// RCCL: the per-destination counts all-gathered (a world x (world + 1) matrix; the last column is unused), the wave's
+// one host synchronisation, then the regions by grouped point-to-point send/recv into the inbox (this store's own region
+// by a device copy).  *any_status: some store sent something (else the waves are over; `status` is ignored).
 int ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status) {
     if (!h || !any_status) return AD_ERR_ARGUMENT;
     if (!h->comm || h->ks_phase < 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_exchange: ad_comm_init + ad_shard_kahn_begin first");
@@ -145,21 +136,20 @@ int ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status) 
     const uint32_t W = h->world, self = h->self;
     uint32_t* mat = nullptr;
     CK(dalloc(h, S_KSMAT, &mat, (size_t)MAX_STORES * (MAX_STORES + 1)));
-    HIPCHK(h, hipMemcpyAsync(h->ks_cnt_dev + W, &status, 4, hipMemcpyHostToDevice, st));
+    (void)status;
     ncclResult_t r = ncclAllGather(h->ks_cnt_dev, mat, W + 1, ncclUint32, h->comm, st);
     if (r != ncclSuccess) return set_err(h, AD_ERR_DEVICE, std::string("ncclAllGather (Kahn counts): ") + ncclGetErrorString(r));
     std::vector<uint32_t> M((size_t)W * (W + 1));
     HIPCHK(h, hipMemcpyAsync(M.data(), mat, M.size() * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
-    uint64_t recv_total = 0;
-    uint32_t any = 0;
+    uint64_t recv_total = 0, sent_any = 0;
     for (uint32_t s = 0; s < W; ++s) {
         recv_total += M[(size_t)s * (W + 1) + self];
-        any |= M[(size_t)s * (W + 1) + W];
+        for (uint32_t d = 0; d < W; ++d) sent_any += M[(size_t)s * (W + 1) + d];
     }
-    *any_status = any ? 1u : 0u;
+    *any_status = sent_any ? 1u : 0u;
     CK(dalloc(h, S_KSIN, &h->ks_in, std::max<uint64_t>(recv_total, 1)));
-    const uint32_t* b = h->ks_base.data() + (size_t)h->ks_phase * (MAX_STORES + 1);
+    const uint32_t* b = h->ks_base.data();
     if (ncclGroupStart() != ncclSuccess) return set_err(h, AD_ERR_DEVICE, "ncclGroupStart");
     ncclResult_t first = ncclSuccess;
     std::string what;
@@ -188,55 +178,35 @@ int ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status) 
     return AD_OK;
 }
 
-// Coordinator: the received READYs counted; txns every holder reported are released (this wave) and their
-// RELEASEs fill the outbox.  *released: this store released some txn.
-int ad_shard_kahn_decide(ad_handle* h, uint32_t* released) {
-    if (!h || !released) return AD_ERR_ARGUMENT;
+// One wave on the device (no host synchronisation): the received READYs counted, rows every holder reported released
+// at `level`, their successors' READYs into the (cleared) outbox for the next exchange.
+int ad_shard_kahn_step(ad_handle* h, uint32_t level) {
+    if (!h) return AD_ERR_ARGUMENT;
     g_tracer = &h->tracer;
-    if (h->ks_phase != 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_decide: exchange the READY outbox first");
+    if (h->ks_phase != 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_step: ad_shard_kahn_begin first");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
     HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
-    HIPCHK(h, hipMemsetAsync(h->ks_flag, 0, 4, st));
     const size_t m = h->ks_in_m;
-    if (m) k_ks_decide<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, h->gid, h->self, h->holders, h->ks_rcnt,
-                                                               ks_base(h, 1), h->ks_cnt_dev, h->ks_out, h->ks_flag,
-                                                               h->ks_flag + 2);
+    if (m) k_ks_step<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, level, h->gid, h->holders, h->ks_xoff, h->ks_xs,
+                                                             h->ks_rem, h->lvl, h->ks_rcnt, ks_base(h), h->ks_cnt_dev, h->ks_out,
+                                                             h->ks_flag, h->ks_flag + 2);
     HIPCHK(h, hipGetLastError());
-    uint32_t f[3] = {0, 0, 0};
-    HIPCHK(h, hipMemcpyAsync(f, h->ks_flag, 12, hipMemcpyDeviceToHost, st));
-    HIPCHK(h, hipStreamSynchronize(st));
-    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_decide: a READY for a txn this store does not coordinate");
-    *released = f[0] ? 1u : 0u;
-    h->ks_phase = 1;
+    if (m) h->level_iters = level + 1;
     h->ks_in_m = 0;
     return AD_OK;
 }
 
-// Every holder: the received RELEASEs get level `level`; their local successors' remaining in-degrees drop and
-// the rows reaching zero fill the outbox with the next wave's READYs.  *unreleased: local rows still without a level.
-int ad_shard_kahn_apply(ad_handle* h, uint32_t level, uint64_t* unreleased) {
+// After the last wave: the error flag and the rows still unreleased (a cycle if any).
+int ad_shard_kahn_finish(ad_handle* h, uint64_t* unreleased) {
     if (!h || !unreleased) return AD_ERR_ARGUMENT;
-    g_tracer = &h->tracer;
-    if (h->ks_phase != 1) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_apply: ad_shard_kahn_decide + the RELEASE exchange first");
+    if (h->ks_phase != 0) return set_err(h, AD_ERR_STATE, "ad_shard_kahn_finish: ad_shard_kahn_begin first");
     hipSetDevice(h->device);
-    hipStream_t st = h->st;
-    HIPCHK(h, hipMemsetAsync(h->ks_cnt_dev, 0, (MAX_STORES + 1) * 4, st));
-    HIPCHK(h, hipMemsetAsync(h->ks_flag + 1, 0, 4, st));
-    const size_t m = h->ks_in_m;
-    if (m) k_ks_apply<<<ceil_div((long)m, 256), 256, 0, st>>>(m, h->ks_in, h->n, level, h->gid, h->holders, h->ks_xoff, h->ks_xs,
-                                                              h->ks_rem, h->lvl, ks_base(h, 0), h->ks_cnt_dev, h->ks_out,
-                                                              h->ks_flag, h->ks_flag + 2);
-    HIPCHK(h, hipGetLastError());
     uint32_t f[3] = {0, 0, 0};
-    HIPCHK(h, hipMemcpyAsync(f, h->ks_flag, 12, hipMemcpyDeviceToHost, st));
-    HIPCHK(h, hipStreamSynchronize(st));
-    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn_apply: a RELEASE for a txn this store does not hold, or twice");
-    h->ks_unreleased -= std::min<size_t>(h->ks_unreleased, f[1]);
-    if (m) h->level_iters = level + 1;
-    *unreleased = h->ks_unreleased;
-    h->ks_phase = 0;
-    h->ks_in_m = 0;
+    HIPCHK(h, hipMemcpyAsync(f, h->ks_flag, 12, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    if (f[2]) return set_err(h, AD_ERR_ARGUMENT, "ad_shard_kahn: a READY for a txn this store does not hold, or already released");
+    *unreleased = h->n - std::min<size_t>(h->n, f[1]);
     return AD_OK;
 }
 

@@ -578,25 +578,26 @@ int  ad_shard_order(ad_handle* h, uint32_t* level_out /* [n_home] */, uint32_t* 
 int  ad_shard_level_edges(ad_handle* h, size_t* m, uint64_t* out);
 int  ad_shard_levels_solve(ad_handle* h, const uint64_t* edges, size_t m, uint32_t* depth);
 int  ad_shard_levels_gather(ad_handle* h, uint32_t* depth);
-/* Distributed Kahn wavefronts (round 4; the default for shallow graphs): a txn is released at wave l once every
- * store holding it has released all of its local predecessors by wave l - 1 (every constraint is local to one
- * store, see above).  Per wave: each store sends READY(txn) to the txn's home store for its rows whose last local
- * predecessor was released; the home store releases the txns all holders reported and sends RELEASE(txn) to every
- * holder; the holders record the level and decrement their successors.  Each txn costs one READY and one RELEASE
- * per holder over the whole batch (8 bytes each), and each store touches only its own constraint edges.
+/* Distributed Kahn wavefronts (the default for shallow graphs): a txn is released at wave l once every store holding
+ * it has released all of its local predecessors by wave l - 1 (every constraint is local to one store, see above).
+ * Per wave ONE exchange: each store sends READY(txn) to every holder of the txn (itself included) for its rows whose
+ * last local predecessor was released; every holder counts them and releases the txns all holders reported, at the
+ * same wave on every holder, then decrements their local successors.  A txn costs holders x holders READYs over the
+ * batch (8 bytes each; the store's own by a device copy), and each store touches only its own constraint edges.
  * Replaces the CommandsForKey.notifyManaged cascade across CommandStores (local/cfk/CommandsForKey.java:1208-1289,
  * local/CommandStores.java:576-593) with the batch's waves.
  *   ad_shard_set_holders, then ad_shard_kahn_begin (the local graph + wave 0's READYs); per wave l = 0, 1, ...:
- *   exchange (READYs) -> ad_shard_kahn_decide -> exchange (RELEASEs; status = *released) ->
- *   ad_shard_kahn_apply(l); stop after the wave in which no store released anything (levels = l), then
- *   ad_shard_order.  Exchange over RCCL: ad_shard_kahn_exchange (status word OR-reduced into *any_status); over a
- *   host transport: ad_shard_kahn_outbox (per-destination counts and messages) -> peers -> ad_shard_kahn_inbox. */
+ *   exchange (the READYs; stop when no store sent anything: levels = l) -> ad_shard_kahn_step(l) (device only, no host
+ *   wait); after the last wave ad_shard_kahn_finish (*unreleased: rows never released, i.e. a cycle), then
+ *   ad_shard_order.  Exchange over RCCL: ad_shard_kahn_exchange (the per-destination counts all-gathered: the wave's
+ *   one host synchronisation; *any_status = some store sent something; `status` is ignored); over a host transport:
+ *   ad_shard_kahn_outbox (per-destination counts and messages) -> peers -> ad_shard_kahn_inbox. */
 int  ad_shard_kahn_begin(ad_handle* h);
 int  ad_shard_kahn_outbox(ad_handle* h, uint32_t* counts /* [world] */, uint64_t* msgs /* or NULL: counts only */);
 int  ad_shard_kahn_inbox(ad_handle* h, const uint64_t* msgs, size_t m);
 int  ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status);
-int  ad_shard_kahn_decide(ad_handle* h, uint32_t* released);
-int  ad_shard_kahn_apply(ad_handle* h, uint32_t level, uint64_t* unreleased);
+int  ad_shard_kahn_step(ad_handle* h, uint32_t level);
+int  ad_shard_kahn_finish(ad_handle* h, uint64_t* unreleased);
 int  ad_shard_kahn_sent(ad_handle* h, uint64_t* sent);
 
 #ifdef __cplusplus

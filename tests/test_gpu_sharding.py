@@ -244,7 +244,7 @@ def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta):
         assert tr.name == "rccl"
         rounds = sharding.run_store(stores[0], tr, levels=levels)
         assert rounds >= 1 and (levels != "gather" or rounds == 1)
-        if levels in ("kahn", "auto"):      # ad_shard_kahn_exchange: counts + status all-gather, self copy
+        if levels in ("kahn", "auto"):      # ad_shard_kahn_exchange: counts all-gather, self copy
             assert rounds == int(lv.max()) + 2
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all()
@@ -469,9 +469,10 @@ def test_c5_full_shape_8_stores(engine_factory):
         rounds = sharding.LocalTransport.run(stores, levels="auto", timings=timings)
         assert rounds <= sharding.AUTO_ROUND_CAP, "C5 is shallow: the Kahn waves finish"
         level_bytes = [int(st.kahn_bytes) for st in stores]
-        # per txn one READY and one RELEASE per other holder: ~77 MB per store, vs the gather's 497 MB of edges
-        # on every store and the delta rounds' ~534 MB per store (every raise of every shared level)
-        assert max(level_bytes) < 128 << 20, level_bytes
+        # per txn one READY from each holder to each other holder over the batch (one exchange per wave): ~129 MB per
+        # store (E[h(h-1)] = 8.07 messages per txn at 8 stores; round 4's READY-to-coordinator + RELEASE sent ~77 MB in
+        # twice the exchanges), vs the gather's 497 MB of edges on every store and the delta rounds' ~534 MB per store
+        assert max(level_bytes) < 160 << 20, level_bytes
         t2 = time.perf_counter()
         for st in stores:
             st.order()

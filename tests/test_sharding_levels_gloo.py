@@ -209,22 +209,24 @@ def test_holder_masks():
 
 
 class HostKahnStore:
-    """Host model of ad_shard_kahn_begin / _decide / _apply (csrc/kahn_shard_kernels.h) for pure key batches of
-    Reads and Writes: the store's own constraint edges (HostEdgeStore.level_edges, the engine's
-    levels_export_edges) over its local rows, READY to the txn's coordinator (sharding.kahn_coord) when a row's last
-    local predecessor was released, RELEASE from the coordinator to every holder once all holders reported."""
+    """Host model of ad_shard_kahn_begin / _step / _finish (csrc/kahn_shard_kernels.h) for pure key batches of Reads and
+    Writes: the store's own constraint edges (HostEdgeStore.level_edges, the engine's levels_export_edges) over its local
+    rows; a row whose last local predecessor was released sends READY to every holder of its txn (itself included); a
+    row released once all of its txn's holders reported it, at that wave on every holder."""
 
     delta = True
 
     def __init__(self, local, gid, holders, home, n_global, rank, world, glob):
-        sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
-        from accord_amd import sharding
         self.gid, self.holders = gid, holders.astype(np.int64)
-        self.home = np.array([sharding.kahn_coord(g, m) for g, m in zip(gid, holders)], np.int64)   # coordinators
         self.rank, self.world, self.n_global = rank, world, n_global
         self._edges = HostEdgeStore(local, gid, n_global, glob)
         self.row = {int(g): i for i, g in enumerate(gid)}
         self.G = np.zeros(n_global, np.uint64)
+
+    def _ready(self, i):
+        for d in range(self.world):
+            if (self.holders[i] >> d) & 1:
+                self.out[d].append(int(self.gid[i]))
 
     def kahn_begin(self):
         n = len(self.gid)
@@ -240,7 +242,7 @@ class HostKahnStore:
         self.sent = 0
         self.out = {d: [] for d in range(self.world)}
         for i in np.nonzero(self.rem == 0)[0]:
-            self.out[int(self.home[i])].append(int(self.gid[i]))
+            self._ready(i)
 
     def kahn_outbox(self):
         cnt = np.array([len(self.out[d]) for d in range(self.world)], np.uint32)
@@ -251,31 +253,22 @@ class HostKahnStore:
     def kahn_inbox(self, msgs):
         self.inbox = [int(g) for g in msgs]
 
-    def kahn_decide(self):
+    def kahn_step(self, level):
         self.out = {d: [] for d in range(self.world)}
-        rel = False
         for g in self.inbox:
             r = self.row[g]
-            assert int(self.home[r]) == self.rank, "READY only to the txn's coordinator"
+            assert self.lvl[r] < 0, "no READY for a released txn"
             self.rcnt[r] += 1
             if self.rcnt[r] == bin(int(self.holders[r])).count("1"):
-                for d in range(self.world):
-                    if (self.holders[r] >> d) & 1:
-                        self.out[d].append(g)
-                rel = True
-        return rel
+                self.lvl[r] = level
+                self.G[g] = level
+                for s_ in self.succ[r]:
+                    self.rem[s_] -= 1
+                    if self.rem[s_] == 0:
+                        self._ready(s_)
+        self.inbox = []
 
-    def kahn_apply(self, level):
-        self.out = {d: [] for d in range(self.world)}
-        for g in self.inbox:
-            r = self.row[g]
-            assert self.lvl[r] < 0, "one RELEASE per txn"
-            self.lvl[r] = level
-            self.G[g] = level
-            for s_ in self.succ[r]:
-                self.rem[s_] -= 1
-                if self.rem[s_] == 0:
-                    self.out[int(self.home[s_])].append(int(self.gid[s_]))
+    def kahn_finish(self):
         return int((self.lvl < 0).sum())
 
     def kahn_sent(self):
@@ -316,11 +309,11 @@ def _kahn_worker(rank, world, port, n, dist_kind):
         want, _ = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_LEVELS).levels()
         assert np.array_equal(store.lvl.astype(np.uint32), want[gid]), "rank %d: levels differ" % rank
         assert store.depth == int(want.max()) + 1 and waves == store.depth + 1
-        # per txn at most one READY and one RELEASE per holder cross the wire (never per round)
+        # per local row exactly one READY to each other holder crosses the wire over the batch (never per round)
         others = ((masks[gid].astype(np.int64) & ~(1 << rank)) != 0).sum()
-        bound = torch.tensor([store.kahn_sent(), 2 * int(sum(bin(int(m)).count("1") - 1 for m in masks[gid]))],
+        bound = torch.tensor([store.kahn_sent(), int(sum(bin(int(m)).count("1") - 1 for m in masks[gid]))],
                              dtype=torch.int64)
-        assert bound[0] <= bound[1] and (others == 0 or bound[0] > 0), bound
+        assert bound[0] == bound[1] and (others == 0 or bound[0] > 0), bound
         assert store.kahn_bytes == 8 * store.kahn_sent()
     finally:
         dist.destroy_process_group()
