@@ -323,9 +323,9 @@ def roofline_of(eng, dom, n, P, st, large=False, pmc=True, steps=1):
     calls, ms, units = eng.kernel_stats()[dom]
     ab = alg_bytes(dom, calls, units, n, P, REPLICAS, st, large, steps)
     achieved = ab / (ms * 1e-3) / 1e9
-    # the committed PMC passes (profiles/collect.sh) run the default C2 bench and C3 (pmc="c3"); C4 and the
+    # the committed PMC passes (profiles/collect.sh) run the default C2 bench, C3 (pmc="c3") and C4 (pmc="c4"); the
     # sharded lines report no traffic
-    traffic, src = pmc_traffic(dom, "c3" if pmc == "c3" else "") if pmc else (None, None)
+    traffic, src = pmc_traffic(dom, pmc if pmc in ("c3", "c4") else "") if pmc else (None, None)
     return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "alg_bytes_per_launch": ab / calls, "avg_launch_ms": ms / calls, "launches": calls}
@@ -348,6 +348,10 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<3>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<3>, 1024, 4>",
                      "ad::k_scan_apply<ad::OffsetsOp<3>, 256, 4>"),
     "order_sort": ("ad::k_window_rank", "ad::k_rank_check"),
+    # C4's virtual-item region (bare base names: every instantiation)
+    "vitems": ("ad::k_vitems", "ad::k_vitems_fill", "ad::k_vitem_walk", "ad::k_large_sums", "ad::k_large_layout"),
+    "k_range_deps": ("ad::k_range_deps",), "k_union_lds": ("ad::k_union_lds_views", "ad::k_union_lds_small",
+                                                             "ad::k_union_lds_list", "ad::k_union_big"),
     # C3's executeAt-block level region (its block sort's radix kernels are shared names and not attributed)
     "block_levels": ("ad::k_bl_erank", "ad::k_bl_chain_block", "ad::k_bl_bounds", "ad::k_bl_inverse",
                      "ad::k_bl_records", "ad::k_bl_compact", "ad::k_level_blocks", "ad::k_bl_scatter"),
@@ -664,7 +668,7 @@ def main():
     dt = t1 - t0
     st = eng.last_times()
     warn_level_fallback(st)
-    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc={"C2": True, "C3": "c3"}.get(cfgname, False),
+    roof = roofline_of(eng, dom, n, P, st, large=Q > 0, pmc={"C2": True, "C3": "c3", "C4": "c4"}.get(cfgname, False),
                        steps=args.steps)
     mc = None
     if Q == 0:

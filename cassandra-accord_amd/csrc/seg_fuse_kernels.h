@@ -22,8 +22,9 @@
 namespace ad {
 
 constexpr int SF_T = 256;
-constexpr int SF_TILE = 1024;                  // nominal sorted positions per tile
-constexpr int SF_CAP = 1536;                   // LDS entries per tile: the tile + its last segment's tail
+constexpr int SF_TILE = 512;                   // nominal sorted positions per tile
+constexpr int SF_CAP = 768;                    // LDS entries per tile: the tile + its last segment's tail (~34 KB of LDS:
+                                               // four workgroups per CU)
 
 struct SegFuseArgs {
     size_t P, ntiles;
@@ -53,6 +54,18 @@ __device__ inline uint32_t sf_next_head(const uint32_t* __restrict__ skey, size_
     return SF_NONE;
 }
 
+// wave-aggregated append of v to an LDS list (order inside the list is immaterial to its users)
+__device__ inline void sf_list_append(bool want, uint16_t v, uint16_t* list, uint32_t* count) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (want) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
 template <int NV, bool DIRECT>
 static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArgs w) {
     __shared__ uint32_t s_key[SF_CAP + 1];
@@ -63,8 +76,10 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     __shared__ int32_t s_ud[SF_CAP];
     __shared__ uint64_t s_pw[SF_CAP];
     __shared__ uint64_t s_pc[SF_CAP];
+    __shared__ uint16_t s_glist[SF_CAP];
+    __shared__ uint16_t s_qlist[SF_CAP];
     __shared__ uint32_t s_bounds[2];
-    __shared__ uint32_t s_cnt[2];
+    __shared__ uint32_t s_cnt[4];
     const size_t b = blockIdx.x;
     const int tid = threadIdx.x, wv = tid / WAVE;
     const size_t P = f.P;
@@ -73,7 +88,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         const uint32_t hd = x >= P ? (uint32_t)P : sf_next_head(f.skey, P, x);
         if (__lane_id() == 0) s_bounds[wv] = hd;
     }
-    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
+    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; s_cnt[2] = 0; s_cnt[3] = 0; }
     __syncthreads();
     if (s_bounds[0] == SF_NONE || s_bounds[1] == SF_NONE || s_bounds[1] - min(s_bounds[0], s_bounds[1]) > (uint32_t)SF_CAP) {
         // a key segment too long for one tile: the host takes the three-kernel path
@@ -87,38 +102,41 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         if (b + 1 == f.ntiles) f.tile_lo[f.ntiles] = (uint32_t)P;
     }
     const uint32_t L = hi - lo;
-    // keys (+ the next tile's first key: a head, or P)
     for (uint32_t i = tid; i < L; i += SF_T) s_key[i] = f.skey[lo + i];
     __syncthreads();
-    // heads / lone flags; gather the records of multi-entry segments
+    // flags per entry; the multi-entry segments' entries (gathered) and the non-head entries (queried) listed densely
+    // in LDS, so the random gathers and the query walks run on full waves (~34 % / ~18 % of a C2 tile's entries)
     uint32_t heads = 0, nonheads = 0;
-    for (uint32_t i = tid; i < L; i += SF_T) {
-        const bool head = i == 0 || s_key[i] != s_key[i - 1];
-        const bool last = i + 1 == L || s_key[i + 1] != s_key[i];
+    for (uint32_t i0 = 0; i0 < L; i0 += SF_T) {
+        const uint32_t i = i0 + tid;
+        const bool in = i < L;
+        const bool head = in && (i == 0 || s_key[i] != s_key[i - 1]);
+        const bool last = in && (i + 1 == L || s_key[i + 1] != s_key[i]);
         heads += head ? 1u : 0u;
-        nonheads += head ? 0u : 1u;
-        if (!(head && last)) {
-            const PairRec r = f.prec[w.sval[lo + i]];
-            s_txn[i] = r.txn; s_meta[i] = (uint8_t)r.meta; s_ex1[i] = r.ex1;
-            f.e_txn[lo + i] = r.txn; f.e_meta[lo + i] = (uint8_t)r.meta; f.e_exec1[lo + i] = r.ex1;
-        }
+        nonheads += (in && !head) ? 1u : 0u;
+        if (head && last) f.seg_start[lo + i] = (int32_t)(lo + i);     // lone: its segment start (rest: complete_entries)
+        sf_list_append(in && !(head && last), (uint16_t)i, s_glist, &s_cnt[2]);
+        sf_list_append(in && !head, (uint16_t)i, s_qlist, &s_cnt[3]);
     }
     atomicAdd(&s_cnt[0], heads);
     atomicAdd(&s_cnt[1], nonheads);
     __syncthreads();
-    // per segment (its head's thread): the elision scan state, serially (ElideOp::combine restarted at the head)
+    const uint32_t ng = s_cnt[2], nq = s_cnt[3];
+    for (uint32_t x = tid; x < ng; x += SF_T) {
+        const uint32_t i = s_glist[x];
+        const PairRec r = f.prec[w.sval[lo + i]];
+        s_txn[i] = r.txn; s_meta[i] = (uint8_t)r.meta; s_ex1[i] = r.ex1;
+        f.e_txn[lo + i] = r.txn; f.e_meta[lo + i] = (uint8_t)r.meta; f.e_exec1[lo + i] = r.ex1;
+    }
+    __syncthreads();
+    // per multi-entry segment (its head's thread): the elision scan state, serially (ElideOp::combine restarted at the
+    // head)
     for (uint32_t i = tid; i < L; i += SF_T) {
-        if (!(i == 0 || s_key[i] != s_key[i - 1])) continue;
+        if (!(i == 0 || s_key[i] != s_key[i - 1]) || i + 1 == L || s_key[i + 1] != s_key[i]) continue;
         const int32_t hs = (int32_t)(lo + i);
-        uint32_t e = i + 1;
-        while (e < L && s_key[e] == s_key[i]) ++e;
-        if (e == i + 1) {                                     // lone: only its segment start (the rest: complete_entries)
-            f.seg_start[lo + i] = hs;
-            continue;
-        }
         int32_t ud = -1;
         uint64_t pw = 0, pc = 0;
-        for (uint32_t q = i; q < e; ++q) {
+        for (uint32_t q = i; q < L && s_key[q] == s_key[i]; ++q) {
             const uint32_t m = s_meta[q];
             const uint32_t cat = category(m);
             const uint64_t x1 = s_ex1[q];
@@ -131,10 +149,8 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < L; i += SF_T) {
-        const bool head = i == 0 || s_key[i] != s_key[i - 1];
-        const bool last = i + 1 == L || s_key[i + 1] != s_key[i];
-        if (head && last) continue;
+    for (uint32_t x = tid; x < ng; x += SF_T) {
+        const uint32_t i = s_glist[x];
         f.seg_start[lo + i] = s_ss[i]; f.ud_prev[lo + i] = s_ud[i]; f.pm_w[lo + i] = s_pw[i]; f.pm_c[lo + i] = s_pc[i];
     }
     if (tid == 0) { f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1]; }
@@ -142,11 +158,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     WalkArgs a = w;
     a.e_txn = s_txn - lo; a.e_meta = s_meta - lo; a.e_exec1 = s_ex1 - lo; a.seg_start = s_ss - lo; a.ud_prev = s_ud - lo;
     a.pm_w = s_pw - lo; a.pm_c = s_pc - lo;
-    for (uint32_t i0 = 0; i0 < L; i0 += SF_T) {
-        const uint32_t i = i0 + tid;
-        const bool q = i < L && i > 0 && s_key[i] == s_key[i - 1];
-        if (q) walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + i);
-    }
+    for (uint32_t x = tid; x < nq; x += SF_T) walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + s_qlist[x]);
 }
 
 // Exclusive prefix of the tiles' head / non-head counts (one workgroup); n_keys_u = the heads, useg[U] = P.

@@ -4,7 +4,7 @@
 # 1. the default bench line (C2, with the CPU baseline leg) + its per-kernel HIP-event breakdown;
 # 2. rocprofv3 --kernel-trace --stats of a short bench run (kernel durations to cross-check `roofline`);
 # 3. two separate PMC passes (FETCH_SIZE, WRITE_SIZE — they do not fit one pass on gfx950), and the same two
-#    for C3 at the end;
+#    for C3 and for C4 at the end;
 # then, back in the build container (gpurun merges gpurun_out/ back):
 #   python3 profiles/summarize.py gpurun_out/TAG TAG      -> profiles/TAG_*
 # Every GPU step has its own time limit and the steps are chained (set -e): a failure ends the script.
@@ -43,3 +43,10 @@ echo "c3 fetch done"
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c3write" -o run --output-format csv -- \
     python3 "$ROOT/bench.py" --config C3 --steps 1 --warmup 1 --cpu-sample 0 --no-e2e > "$OUT/c3write.log" 2>&1
 echo "c3 write done"
+# 7. C4's PMC passes (the virtual-item region dominates it)
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c4fetch" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --config C4 --steps 1 --warmup 1 --cpu-sample 0 --no-e2e > "$OUT/c4fetch.log" 2>&1
+echo "c4 fetch done"
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c4write" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --config C4 --steps 1 --warmup 1 --cpu-sample 0 --no-e2e > "$OUT/c4write.log" 2>&1
+echo "c4 write done"

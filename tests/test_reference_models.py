@@ -303,8 +303,10 @@ def test_gpu_deps_self_with_contains_max(engine_factory):
     """DepsTest.test's checks on the device's own Deps (C4-like mix: all three classes populated): with(self) ==
     self (validateSelfWith: Deps.merge of a reply with itself, ad_merge_host), contains (validateContains: every
     class's TxnIds are in the merged txnIds), maxTxnId == the max over the three classes (validateMaxTxnId)."""
+    kinds = np.random.default_rng(31).choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_SYNC_POINT,
+                                              abi.KIND_EXCLUSIVE_SYNC_POINT], p=[0.42, 0.42, 0.08, 0.08], size=6000)
     b = workload.generate(6000, keys_per_txn=3, keyspace=20_000, range_frac=0.1, range_width_max=300, seed=31,
-                          kinds=None)
+                          kinds=kinds)             # key-domain sync points (witnessed by ExclusiveSyncPoints): directKeyDeps
     eng = engine_factory(window=8, replicas=1, drop_p=0.0, seed=2)
     eng.load(b)
     eng.preaccept_deps()
