@@ -72,12 +72,12 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False, steps=1):
         "k_deps_walk<fill>": calls * (W * (46 + 4 * C) + 4 * D),  # C end slots in, the entries out
         # the fused tile kernel (gather + elision state + count walk, seg_fuse_kernels.h), a lower bound: every
         # sorted key read and segment start written (8 B/pair); per query entry (at least the W non-head entries are
-        # gathered) its pair index + 16-byte record read and its state written (txn, meta, executeAt + 1, last
+        # gathered) its pair index + 16-byte record read, its position appended to nh, its state written (txn, meta, executeAt + 1, last
         # always-emitted, two prefix maxima: 33 B), its C count bytes and tx_ts read (8 B); 4 B per emitted id
-        "k_seg_fuse": calls * (P * 8 + W * (4 + 16 + 33 + 8 + C) + 4 * D),
-        # ElideOp's store from the tile counts: keys re-read (4 B/pair), U = P - W distinct keys (8 + 4 B) and the
-        # W non-head positions (4 B) written
-        "seg_keys": calls * (P * 4 + (P - W) * 12 + W * 4),
+        "k_seg_fuse": calls * (P * 8 + W * (8 + 16 + 33 + 8 + C) + 4 * D),
+        # the distinct keys from the tile counts (only for the stages that read every key; not in the C2 pipeline):
+        # keys re-read (4 B/pair), U = P - W keys and segment starts written (12 B)
+        "seg_keys": calls * (P * 4 + (P - W) * 12),
         # per txn: key_off, 4 offsets in + tcnt out per class; per pair key + count bytes; per entry the inline id
         # in, k2t entry + TxnId out
         "k_txn_finish": units * (8 + 20 * C) + calls * (P * (8 + ncb) + 12 * D),
@@ -339,7 +339,7 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
     "k_gather_entries": "ad::k_gather_entries<true>", "k_txn_finish": "ad::k_txn_finish<3, false>",
     "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<3>",
-    "k_seg_fuse": "ad::k_seg_fuse<3, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_keys"),
+    "k_seg_fuse": "ad::k_seg_fuse<3, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_ukeys"),
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
     # are shared fill/copy kernels and are not attributed)

@@ -96,6 +96,18 @@ def make_cfk_state(st):
 
 
 class AdConfig(C.Structure):
+    """ad_config: the store's replica views."""
+    _fields_ = [("replicas", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class AdReplicaModel(C.Structure):
+    """ad_replica_model: the benchmark's in-flight window / replica drop model (generator setting)."""
+    _fields_ = [("window", C.c_uint32), ("drop_p", C.c_float), ("seed", C.c_uint64)]
+
+
+class ModelConfig(C.Structure):
+    """One query model (replicas + window / drop_p / seed): the oracle's oracle_config; the engine splits it
+    into ad_config + ad_replica_model."""
     _fields_ = [("window", C.c_uint32), ("replicas", C.c_uint32), ("drop_p", C.c_float),
                 ("pad_", C.c_uint32), ("seed", C.c_uint64)]
 
@@ -164,7 +176,7 @@ def make_batch(b):
 
 
 def make_config(window=32, replicas=3, drop_p=0.1, seed=0xACC0D1):
-    return AdConfig(window, replicas, drop_p, 0, seed)
+    return ModelConfig(window, replicas, drop_p, 0, seed)
 
 
 class Csr:

@@ -44,6 +44,7 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.ad_open.argtypes = [C.c_int, C.POINTER(abi.AdConfig), C.POINTER(vp)]
+        L.ad_set_replica_model.argtypes = [vp, C.POINTER(abi.AdReplicaModel)]
         L.ad_close.argtypes = [vp]
         L.ad_close.restype = None
         L.ad_last_error.argtypes = [vp]
@@ -106,7 +107,7 @@ def lib():
     return _LIB
 
 
-EXPORTED = ("ad_open", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
+EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
             "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
@@ -166,15 +167,19 @@ class DepsEngine:
     """One CommandStore shard on one GPU (an ad_handle)."""
 
     def __init__(self, device=0, window=32, replicas=3, drop_p=0.1, seed=0xACC0D1):
+        """replicas -> ad_config; window / drop_p / seed -> ad_set_replica_model (the benchmark's replica model:
+        window=0, drop_p=0 is the plain snapshot a live store queries).  self.cfg holds all four for the oracle."""
         self.cfg = abi.make_config(window, replicas, drop_p, seed)
         self.replicas = replicas
         self.device = device
         h = C.c_void_p()
-        rc = lib().ad_open(device, C.byref(self.cfg), C.byref(h))
+        rc = lib().ad_open(device, C.byref(abi.AdConfig(replicas, 0)), C.byref(h))
         if rc != abi.AD_OK:
             raise AccordDepsError(rc, "ad_open(device=%d) failed" % device)
         self.h = h
         self.n = 0
+        self._check(lib().ad_set_replica_model(h, C.byref(abi.AdReplicaModel(window, drop_p, seed))),
+                    "ad_set_replica_model")
 
     def close(self):
         if getattr(self, "h", None):

@@ -97,6 +97,16 @@ static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64
 // that reads every sorted entry (execution levels other than the pull pass, MaxConflicts, recovery, CFK retain,
 // sharded level passes).
 int complete_entries(ad_handle* h) {
+    if (h->keys_partial) {               // k_seg_fuse's batches: the distinct keys and segment starts, from its tiles
+        h->keys_partial = false;
+        const size_t nt = h->sf_ntiles;
+        KScope ks(K_SEG_KEYS, h->P);
+        if (nt) k_seg_tile_scan<<<1, 1024, 0, h->st>>>(nt, h->P, (uint32_t*)h->bufs[S_SFCNT].p, h->useg);
+        if (nt) k_seg_ukeys<<<(unsigned)nt, SF_T, 0, h->st>>>(nt, (const uint32_t*)h->bufs[S_SFLO].p,
+                                                             (const uint32_t*)h->bufs[S_SFCNT].p, h->skey, h->hprm.key_min,
+                                                             h->ukey, h->useg);
+        HIPCHK(h, hipGetLastError());
+    }
     if (!h->entries_partial) return AD_OK;
     h->entries_partial = false;
     const size_t P = h->P;
@@ -131,6 +141,7 @@ int stage_deps(ad_handle* h) {
     // (seg_fuse_kernels.h); its overflow flag comes back with the totals, and an overflowing batch re-runs here on
     // the three-kernel path
     const bool fuse = skip && !h->seg_long;
+    h->keys_partial = false;
     uint32_t* fuse_over = h->totd + MAX_TOTALS - 6;      // (MAX_TOTALS - 5: the merge's speculation guard)
     if (P > 0 && !fuse) {
         h->entries_partial = skip;
@@ -199,21 +210,22 @@ int stage_deps(ad_handle* h) {
     // deferred flags
     if (fuse) {
         h->entries_partial = true;
-        fill_multi(st, {{fuse_over, 4, 0}, {dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
         const size_t ntiles = (P + SF_TILE - 1) / SF_TILE;
         SegFuseArgs f{};
         f.P = P; f.ntiles = ntiles; f.skey = h->skey; f.prec = h->prec; f.overflow = fuse_over;
-        CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 2 * ntiles));
+        CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 4 * ntiles + SF_PARTS));
+        f.hpart = f.tile_cnt + 4 * ntiles;
+        fill_multi(st, {{fuse_over, 4, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0},
+                        {h->dfr, n, 0}});
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;
         { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
-        {
-            KScope ks(K_SEG_KEYS, P);
-            k_seg_tile_scan<<<1, 1024, 0, st>>>(ntiles, P, f.tile_cnt, h->useg, h->prm, fuse_over);
-            k_seg_keys<<<(unsigned)ntiles, SF_T, 0, st>>>(f.tile_lo, f.tile_cnt, h->skey, h->hprm.key_min, h->ukey, h->useg, h->nh,
-                                                          fuse_over);
-        }
+        k_seg_heads<<<1, SF_PARTS, 0, st>>>(f.hpart, h->prm, fuse_over);
+        h->nh_valid = false;               // no dense non-head list: the level chain build runs over every position
+        h->keys_partial = true;            // ukey / useg on demand (complete_entries)
+        h->sf_ntiles = ntiles;
     } else {
+        h->nh_valid = true;
         fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
         launch_walk_nv(nv, wa, false, direct, true, st);
     }

@@ -395,6 +395,7 @@ void launch_mc_ranges(const McRangeArgs& a, hipStream_t st) {
 static int load_working(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     h->seg_long = false;
+    h->keys_partial = false;
     const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
     CK(dalloc(h, S_PRM, &h->prm, 1)); CK(dalloc(h, S_TOT, &h->totd, MAX_TOTALS));
     // a batch merged from host replies (ad_merge_host) never runs stage_prepare: its Params must read clean
@@ -453,7 +454,7 @@ int ad_open(int device, const ad_config* cfg, ad_handle** out) {
     if (device < 0 || device >= count) return AD_ERR_ARGUMENT;
     ad_handle* h = new ad_handle();
     h->device = device;
-    h->cfg = *cfg;
+    h->cfg.replicas = cfg->replicas;                  // window 0, no drops: the snapshot (ad_set_replica_model)
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return AD_ERR_DEVICE;
@@ -461,6 +462,15 @@ int ad_open(int device, const ad_config* cfg, ad_handle** out) {
     for (auto& e : h->ev) hipEventCreate(&e);
     h->tracer.st = h->st;
     *out = h;
+    return AD_OK;
+}
+
+int ad_set_replica_model(ad_handle* h, const ad_replica_model* m) {
+    if (!h || !m) return AD_ERR_ARGUMENT;
+    if (!(m->drop_p >= 0.0f && m->drop_p <= 1.0f)) return set_err(h, AD_ERR_ARGUMENT, "drop_p outside [0, 1]");
+    h->cfg.window = m->window;
+    h->cfg.drop_p = m->drop_p;
+    h->cfg.seed = m->seed;
     return AD_OK;
 }
 

@@ -46,9 +46,17 @@ using Csr = ad::DevCsr;
 
 constexpr size_t CSR_BLOCKS_MAX = 96;
 
+// The handle's query model: replicas from ad_config; window / drop_p / seed from ad_replica_model (0: the snapshot)
+struct ModelCfg {
+    uint32_t window = 0;
+    uint32_t replicas = 1;
+    float drop_p = 0.0f;
+    uint64_t seed = 0;
+};
+
 struct ad_handle {
     int device = 0;
-    ad_config cfg{};
+    ModelCfg cfg{};                  // replicas (ad_config) + the replica model (ad_replica_model)
     hipStream_t st = nullptr;
     std::string err;
     std::vector<DBuf> bufs;
@@ -172,6 +180,9 @@ struct ad_handle {
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     bool entries_partial = false;    // the deps stage skipped the lone entries' gather (complete_entries)
     bool seg_long = false;           // the loaded batch has a key segment too long for k_seg_fuse's tiles
+    bool nh_valid = false;           // nh holds the batch's non-head entries (not after k_seg_fuse)
+    bool keys_partial = false;       // k_seg_fuse left ukey / useg to complete_entries (from its tiles)
+    size_t sf_ntiles = 0;
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;
     bool merge_heavy = true;         // Deps.merge may meet heavy txns (false: the deps stage saw none)
@@ -298,7 +309,7 @@ enum Slot : size_t {
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
     S_CS0, S_CS_END = S_CS0 + 14,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
-    S_SFLO, S_SFCNT,                                            // k_seg_fuse tiles
+    S_SFLO, S_SFCNT,                                     // k_seg_fuse tiles
     S_NUM_FIXED,
     S_CSR0 = 320
 };

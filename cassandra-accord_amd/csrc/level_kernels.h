@@ -592,7 +592,8 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
 // predecessors (indeg) and a backward pass gives its successor run (succ[pair]).  Single-entry segments
 // have no edges and are skipped; a segment longer than SHORT_SEG raises *any_long and the caller falls
 // back to the fixpoint (whose chain preparation handles long chains).
-// One thread per non-head entry (ElideOp's dense list); the second entry of each segment builds it.
+// One thread per non-head entry (ElideOp's dense list; nh == null: one per sorted position, the batches whose deps
+// stage ran k_seg_fuse, which builds no list); the second entry of each segment builds it.
 static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
                                                      const int32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
@@ -604,7 +605,7 @@ static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint
                                                      uint32_t* __restrict__ any_far = nullptr) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool lng = false, far = false;
-    const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
+    const size_t s2 = nh ? (x < P - prm->n_keys_u ? (size_t)nh[x] : 0) : (x + 1 < P ? x + 1 : 0);
     const size_t s = s2 - 1;
     if (s2 > 0 && seg_start[s2] == (int32_t)s) {
         size_t end = s + 2;

@@ -6,8 +6,10 @@
 // (64-bit masks: the CDNA wavefront is 64 lanes), the in-round rank is popcount(mask & lanes-below),
 // and per-wave digit counters live in LDS.  Pass structure:
 //   k_radix_hist    : per-tile digit histogram (LDS, per-wave privatised) -> hist[digit][tile]
-//   device_scan     : exclusive sum over hist (digit-major) -> global digit offsets per tile
-//   k_radix_scatter : recompute ranks, scatter keys/values to their final slots
+//   k_radix_rowscan : one workgroup per digit: exclusive sum along its row -> offs[digit][tile], tot[digit]
+//   k_radix_scatter : the digit bases from tot (a 256-entry block scan per tile), recompute ranks, scatter
+//                     keys/values to their final slots
+// (the row scan is one launch where a digit-major scan of the whole histogram was three)
 // Replaces the per-key Arrays.sort in RelationMultiMap.AbstractBuilder.finishKey/build
 // (utils/RelationMultiMap.java:158-169, 208-216, 230-243) by one batch-wide stable key sort.
 #pragma once
@@ -53,6 +55,38 @@ __device__ inline uint64_t match_digit(uint32_t d, bool valid) {
     return m;
 }
 
+// Exclusive sum of each digit's per-tile counts (one workgroup per digit, rows of ntiles) and the digit's total.
+static __global__ __launch_bounds__(1024) void k_radix_rowscan(const uint32_t* __restrict__ hist, int ntiles,
+                                                               uint32_t* __restrict__ offs, uint32_t* __restrict__ tot) {
+    __shared__ uint32_t wsum[1024 / WAVE];
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
+    uint32_t* orow = offs + (size_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (int base = 0; base < ntiles; base += 1024) {
+        const int t = base + threadIdx.x;
+        const uint32_t x = t < ntiles ? row[t] : 0u;
+        uint32_t incl = x;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == WAVE - 1) wsum[w] = incl;
+        __syncthreads();
+        uint32_t pre = 0, all = 0;
+#pragma unroll
+        for (int k = 0; k < 1024 / WAVE; ++k) {
+            pre += k < w ? wsum[k] : 0u;
+            all += wsum[k];
+        }
+        if (t < ntiles) orow[t] = carry + pre + incl - x;
+        carry += all;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
 // LDS-staged scatter: every item's position inside the tile sorted by digit is computed from the
 // per-wave ballot ranks, the tile's (key, value) pairs are written to LDS in that order, and then read
 // back sequentially: consecutive threads write consecutive global slots of one digit's run, so the global
@@ -60,10 +94,11 @@ __device__ inline uint64_t match_digit(uint32_t d, bool valid) {
 static __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             size_t n, int shift, int ntiles,
-                                                            const uint32_t* __restrict__ offs) {
+                                                            const uint32_t* __restrict__ offs,
+                                                            const uint32_t* __restrict__ dtot) {
     __shared__ uint32_t cnt[RS_WAVES][256];
     __shared__ uint32_t gbase[256];          // global slot of the tile's first item of digit d, minus its tile slot
-    __shared__ uint32_t wsum[RS_WAVES];
+    __shared__ uint32_t wsum[RS_WAVES], wtot[RS_WAVES];
     __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
     const int w = threadIdx.x / WAVE;
     const int lane = threadIdx.x % WAVE;
@@ -99,17 +134,21 @@ static __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_
 #pragma unroll
         for (int x = 0; x < RS_WAVES; ++x) tot += cnt[x][d];
         uint32_t incl = tot;
+        const uint32_t dt = dtot[d];            // the digit's total over all tiles
+        uint32_t dincl = dt;
 #pragma unroll
         for (int o = 1; o < WAVE; o <<= 1) {
             uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
+            uint32_t z = __shfl_up(dincl, o);
+            if (lane >= o) { incl += y; dincl += z; }
         }
-        if (lane == WAVE - 1) wsum[w] = incl;
+        if (lane == WAVE - 1) { wsum[w] = incl; wtot[w] = dincl; }
         __syncthreads();
-        uint32_t pre = 0;
-        for (int x = 0; x < w; ++x) pre += wsum[x];
+        uint32_t pre = 0, dpre = 0;
+        for (int x = 0; x < w; ++x) { pre += wsum[x]; dpre += wtot[x]; }
         uint32_t run = pre + incl - tot;          // tile slot of digit d's first item
-        gbase[d] = offs[(size_t)d * ntiles + blockIdx.x] - run;
+        // global slot of digit d's first item in this tile: the digits below d, then the tiles before this one
+        gbase[d] = (dpre + dincl - dt) + offs[(size_t)d * ntiles + blockIdx.x] - run;
 #pragma unroll
         for (int x = 0; x < RS_WAVES; ++x) {
             uint32_t c = cnt[x][d];
@@ -142,7 +181,7 @@ static __global__ __launch_bounds__(RS_BLOCK) void k_radix_scatter(const uint32_
 struct RadixScratch {
     uint32_t* hist;     // [256 * ntiles + 1]
     uint32_t* offs;     // [256 * ntiles + 1]
-    uint32_t* agg;      // scan aggregates
+    uint32_t* agg;      // scratch: [256] per-digit totals
 };
 
 inline size_t radix_hist_len(size_t n) { return (size_t)256 * ceil_div((long)n, RS_TILE) + 1; }
@@ -161,8 +200,8 @@ inline bool radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t*
         uint32_t* ko = flip ? k0 : k1;
         uint32_t* vo = flip ? v0 : v1;
         { KScope ks(K_RADIX_HIST, n); k_radix_hist<<<ntiles, RS_BLOCK, 0, st>>>(ki, n, shift, ntiles, s.hist); }
-        { KScope ks(K_SCAN_RADIX, hl); device_scan(SumOp<uint32_t>{s.hist, s.offs, hl}, hl, s.agg, st); }
-        { KScope ks(K_RADIX_SCATTER, n); k_radix_scatter<<<ntiles, RS_BLOCK, 0, st>>>(ki, vi, ko, vo, n, shift, ntiles, s.offs); }
+        { KScope ks(K_SCAN_RADIX, hl); k_radix_rowscan<<<256, 1024, 0, st>>>(s.hist, ntiles, s.offs, s.agg); }
+        { KScope ks(K_RADIX_SCATTER, n); k_radix_scatter<<<ntiles, RS_BLOCK, 0, st>>>(ki, vi, ko, vo, n, shift, ntiles, s.offs, s.agg); }
         flip = !flip;
     }
     return flip;

@@ -12,26 +12,29 @@
 // prefix maxima for the multi-entry segments), and runs every non-head entry's query against the LDS copy.
 // Replaces k_gather_entries<true> + the three ElideOp scan launches + k_deps_walk<count>, whose reads of the
 // per-entry arrays were spread over every sorted position (C2: 767,867 queries among 4,194,304 entries; the walk
-// fetched 9.5x its byte model).  The distinct keys, segment starts and the dense non-head list (ElideOp's store)
-// follow from the per-tile head counts: k_seg_tile_scan (one workgroup) + k_seg_keys.
-// A tile longer than SF_CAP (a key segment of more than ~500 entries: Zipf hot keys) raises *overflow and the
-// host runs the three-kernel path instead (the handle then remembers the batch had long segments).
+// fetched 9.5x its byte model).  ElideOp's store: the tiles' head counts go to 256 partial sums (one atomic per tile,
+// spread over 256 words: a single counter serialised 16K tiles' atomics, +65 us) that k_seg_heads adds into n_keys_u;
+// no dense non-head list is built (its one user, the level chain build, then runs over every sorted position); the
+// distinct keys and segment starts only on demand (k_seg_tile_scan + k_seg_ukeys, from complete_entries).
+// A tile longer than SF_CAP (a key segment of more than ~SF_CAP - SF_TILE entries: Zipf hot keys) raises *overflow and
+// the host runs the three-kernel path instead (the handle then remembers the batch had long segments).
 #pragma once
 #include "deps_kernels.h"
 
 namespace ad {
 
 constexpr int SF_T = 256;
-constexpr int SF_TILE = 512;                   // nominal sorted positions per tile
-constexpr int SF_CAP = 768;                    // LDS entries per tile: the tile + its last segment's tail (~34 KB of LDS:
-                                               // four workgroups per CU)
+constexpr int SF_TILE = 256;                   // nominal sorted positions per tile
+constexpr int SF_CAP = 384;                    // LDS entries per tile: the tile + its last segment's tail (~17 KB of LDS:
+                                               // eight workgroups per CU)
 
 struct SegFuseArgs {
     size_t P, ntiles;
     const uint32_t* skey;                      // sorted (key - key_min), 32-bit spreads
     const PairRec* prec;
     uint32_t* tile_lo;                         // [ntiles + 1] each tile's first sorted position
-    uint32_t* tile_cnt;                        // [2 * ntiles]: heads, non-heads
+    uint32_t* tile_cnt;                        // [4 * ntiles]: heads, non-heads; then their exclusive offsets
+    uint32_t* hpart;                           // [SF_PARTS] head-count partial sums (zeroed)
     uint32_t* overflow;
     uint32_t *e_txn;                           // global entry state (written)
     uint8_t* e_meta;
@@ -40,6 +43,7 @@ struct SegFuseArgs {
     uint64_t *pm_w, *pm_c;
 };
 
+constexpr int SF_PARTS = 256;
 constexpr uint32_t SF_NONE = 0xFFFFFFFFu;
 // first segment head at or after x (x == P: P), searched by one wave 64 positions at a time; SF_NONE if none within
 // SF_CAP positions
@@ -153,7 +157,10 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         const uint32_t i = s_glist[x];
         f.seg_start[lo + i] = s_ss[i]; f.ud_prev[lo + i] = s_ud[i]; f.pm_w[lo + i] = s_pw[i]; f.pm_c[lo + i] = s_pc[i];
     }
-    if (tid == 0) { f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1]; }
+    if (tid == 0) {
+        f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1];
+        if (s_cnt[0]) atomicAdd(&f.hpart[b % SF_PARTS], s_cnt[0]);
+    }
     // the queries of the non-head entries, against the LDS copy (sorted position s -> s - lo)
     WalkArgs a = w;
     a.e_txn = s_txn - lo; a.e_meta = s_meta - lo; a.e_exec1 = s_ex1 - lo; a.seg_start = s_ss - lo; a.ud_prev = s_ud - lo;
@@ -161,14 +168,28 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     for (uint32_t x = tid; x < nq; x += SF_T) walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + s_qlist[x]);
 }
 
-// Exclusive prefix of the tiles' head / non-head counts (one workgroup); n_keys_u = the heads, useg[U] = P.
-// Both run before the host has read k_seg_fuse's overflow flag: after an overflow (some tiles never wrote their bounds
-// or counts) they do nothing, and the host re-runs the batch on the three-kernel path.
-static __global__ __launch_bounds__(1024) void k_seg_tile_scan(size_t ntiles, size_t P, uint32_t* __restrict__ tile_cnt,
-                                                               uint32_t* __restrict__ useg, Params* prm,
-                                                               const uint32_t* __restrict__ overflow) {
-    __shared__ uint32_t s_h[1024], s_n[1024];
+// n_keys_u = the tiles' heads (after k_seg_fuse; nothing after an overflow: the host re-runs the batch)
+static __global__ __launch_bounds__(SF_PARTS) void k_seg_heads(const uint32_t* __restrict__ hpart, Params* prm,
+                                                              const uint32_t* __restrict__ overflow) {
+    __shared__ uint32_t s_w[SF_PARTS / WAVE];
     if (*(const volatile uint32_t*)overflow) return;
+    uint32_t v = hpart[threadIdx.x];
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (__lane_id() == 0) s_w[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < SF_PARTS / WAVE; ++k) t += s_w[k];
+        prm->n_keys_u = t;
+    }
+}
+
+// Exclusive prefix of the tiles' head / non-head counts (one workgroup); useg[U] = P (U = the heads, = n_keys_u).
+// Runs on demand (complete_entries), after the host saw no overflow.
+static __global__ __launch_bounds__(1024) void k_seg_tile_scan(size_t ntiles, size_t P, uint32_t* __restrict__ tile_cnt,
+                                                               uint32_t* __restrict__ useg) {
+    __shared__ uint32_t s_h[1024], s_n[1024];
     uint32_t carry_h = 0, carry_n = 0;
     for (size_t base = 0; base < ntiles; base += 1024) {
         const size_t t = base + threadIdx.x;
@@ -182,48 +203,45 @@ static __global__ __launch_bounds__(1024) void k_seg_tile_scan(size_t ntiles, si
             s_h[threadIdx.x] += yh; s_n[threadIdx.x] += yn;
             __syncthreads();
         }
-        if (t < ntiles) { tile_cnt[2 * t] = carry_h + s_h[threadIdx.x] - h; tile_cnt[2 * t + 1] = carry_n + s_n[threadIdx.x] - nn; }
+        if (t < ntiles) {
+            tile_cnt[2 * ntiles + 2 * t] = carry_h + s_h[threadIdx.x] - h;
+            tile_cnt[2 * ntiles + 2 * t + 1] = carry_n + s_n[threadIdx.x] - nn;
+        }
         carry_h += s_h[1023]; carry_n += s_n[1023];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        useg[carry_h] = (uint32_t)P;
-        prm->n_keys_u = carry_h;
-    }
+    if (threadIdx.x == 0) useg[carry_h] = (uint32_t)P;
 }
 
-// ElideOp's store, per tile: the distinct keys (ukey, useg) and the dense list of non-head entries (nh), in order.
-static __global__ __launch_bounds__(SF_T) void k_seg_keys(const uint32_t* __restrict__ tile_lo, const uint32_t* __restrict__ tile_cnt,
-                                                          const uint32_t* __restrict__ skey, uint64_t key_min,
-                                                          uint64_t* __restrict__ ukey, uint32_t* __restrict__ useg,
-                                                          uint32_t* __restrict__ nh, const uint32_t* __restrict__ overflow) {
-    __shared__ uint32_t s_w[SF_T / WAVE][2];
-    if (*(const volatile uint32_t*)overflow) return;
+// On demand (complete_entries: only the stages that read every key need it, not the C2 pipeline): the distinct
+// keys (ukey) and their segment starts (useg), in order.
+static __global__ __launch_bounds__(SF_T) void k_seg_ukeys(size_t ntiles, const uint32_t* __restrict__ tile_lo,
+                                                           const uint32_t* __restrict__ tile_cnt,
+                                                           const uint32_t* __restrict__ skey, uint64_t key_min,
+                                                           uint64_t* __restrict__ ukey, uint32_t* __restrict__ useg) {
+    __shared__ uint32_t s_w[SF_T / WAVE];
     const size_t b = blockIdx.x;
     const uint32_t lo = tile_lo[b], hi = tile_lo[b + 1];
-    uint32_t ch = tile_cnt[2 * b], cn = tile_cnt[2 * b + 1];
+    uint32_t ch = tile_cnt[2 * ntiles + 2 * b];
     const int tid = threadIdx.x, lane = __lane_id(), wv = tid / WAVE;
     const uint64_t below = (1ull << lane) - 1ull;
     for (uint32_t base = lo; base < hi; base += SF_T) {
         const uint32_t s = base + tid;
-        const bool in = s < hi;
-        const bool head = in && (s == 0 || skey[s] != skey[s - 1]);
-        const bool non = in && !head;
-        const uint64_t mh = __ballot(head), mn = __ballot(non);
-        if (lane == 0) { s_w[wv][0] = (uint32_t)__popcll(mh); s_w[wv][1] = (uint32_t)__popcll(mn); }
+        const bool head = s < hi && (s == 0 || skey[s] != skey[s - 1]);
+        const uint64_t mh = __ballot(head);
+        if (lane == 0) s_w[wv] = (uint32_t)__popcll(mh);
         __syncthreads();
-        uint32_t ph = ch, pn = cn, th = 0, tn = 0;
+        uint32_t ph = ch, th = 0;
         for (int k = 0; k < SF_T / WAVE; ++k) {
-            if (k < wv) { ph += s_w[k][0]; pn += s_w[k][1]; }
-            th += s_w[k][0]; tn += s_w[k][1];
+            if (k < wv) ph += s_w[k];
+            th += s_w[k];
         }
         if (head) {
             const uint32_t u = ph + (uint32_t)__popcll(mh & below);
             ukey[u] = (uint64_t)skey[s] + key_min;
             useg[u] = s;
         }
-        if (non) nh[pn + (uint32_t)__popcll(mn & below)] = s;
-        ch += th; cn += tn;
+        ch += th;
         __syncthreads();
     }
 }

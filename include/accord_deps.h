@@ -92,7 +92,8 @@ typedef struct ad_batch {
     const uint64_t* exec_msb;       /* [n] final (committed) executeAt                        */
     const uint64_t* exec_lsb;       /* [n]                                                    */
     const int32_t*  exec_node;      /* [n]                                                    */
-    const uint8_t*  status;         /* [n] InternalStatus a txn has once outside the in-flight window */
+    const uint8_t*  status;         /* [n] the row's InternalStatus (under a replica model with    */
+                                    /*     window W > 0: its status once outside the window)      */
     const uint32_t* key_off;        /* [n+1] key footprint CSR                                */
     const uint64_t* keys;           /* [key_off[n]] order-preserving key encoding (Key.compareTo) */
     const uint32_t* range_off;      /* [n+1] range footprint CSR (NULL when no range txns)    */
@@ -100,18 +101,26 @@ typedef struct ad_batch {
     const uint64_t* range_end;      /* [range_off[n]]                                         */
 } ad_batch;
 
-/* Status model for one batch query: when txn i (rank order) is PreAccepted, every
- * txn j < i with j >= i - window is still in flight (PREACCEPTED_OR_ACCEPTED_INVALIDATE); every
- * j < i - window has its given final status.  window = 0 is the plain snapshot query.
- * A replica view r in [0, replicas) additionally has not yet witnessed each in-flight j with
- * probability drop_p, decided by ad_drop_hash(seed, r, i, j) (the same function the oracle uses). */
+/* Store configuration: the number of replica views a handle answers for (the coordinator's R PreAccept
+ * replies, CoordinatePreAccept / PreAccept.reduce).  A live GpuCommandStore opens with replicas = 1 and
+ * reads every row's status as given (the W = 0 snapshot of SafeCommandStore.mapReduceActive,
+ * local/SafeCommandStore.java:292). */
 typedef struct ad_config {
-    uint32_t window;                /* W (BASELINE: 32)                                        */
     uint32_t replicas;              /* R replica views to build (1..8)                          */
-    float    drop_p;                /* per in-flight dependency drop probability per view       */
-    uint32_t pad_;
-    uint64_t seed;                  /* drop hash seed                                          */
+    uint32_t reserved_;             /* 0                                                        */
 } ad_config;
+
+/* The benchmark's replica model — a workload generator setting, not store state: when txn i
+ * (rank order) is PreAccepted, every txn j < i with j >= i - window is still in flight
+ * (PREACCEPTED_OR_ACCEPTED_INVALIDATE); every j < i - window has its given status.  A replica view r in
+ * [0, replicas) additionally has not yet witnessed each in-flight j with probability drop_p, decided by
+ * ad_drop_hash(seed, r, i, j) (the same function the oracle uses).  A handle starts with window = 0 and
+ * drop_p = 0 (the plain snapshot); ad_set_replica_model changes it for the following stage calls. */
+typedef struct ad_replica_model {
+    uint32_t window;                /* W (BASELINE: 32)                                        */
+    float    drop_p;                /* per in-flight dependency drop probability per view       */
+    uint64_t seed;                  /* drop hash seed                                          */
+} ad_replica_model;
 
 /* ------------------------------------------------------------------------------------------ */
 /* Batched PartialDeps output.  For class c of view v, per txn i:                               */
@@ -161,6 +170,8 @@ static inline uint32_t ad_drop_threshold(float p) {
 /* Lifecycle                                                                                   */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_open(int device, const ad_config* cfg, ad_handle** out);
+/* Benchmark / test generators only (see ad_replica_model): a live store never calls it. */
+int  ad_set_replica_model(ad_handle* h, const ad_replica_model* model);
 void ad_close(ad_handle* h);
 const char* ad_last_error(const ad_handle* h);
 int  ad_device_count(void);

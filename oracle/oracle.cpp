@@ -28,6 +28,14 @@
  * is Java and cannot be compiled or run in this image (no JVM), see DESIGN.md §Oracle.
  */
 #include "../include/accord_deps.h"
+/* The query model the tests hand the oracle in one struct: ad_config's replicas + ad_replica_model's window,
+ * drop_p and seed (the engine takes them through ad_open and ad_set_replica_model). */
+typedef struct oracle_config {
+    uint32_t window, replicas;
+    float drop_p;
+    uint32_t pad_;
+    uint64_t seed;
+} oracle_config;
 
 #include <algorithm>
 #include <chrono>
@@ -713,28 +721,28 @@ extern "C" {
  * GetDeps; no pruning), bit4 = levels with APPLIED / INVALID txns done (CFK history batches), bit5 = bound
  * Timestamp.MAX (GetEphemeralReadDeps); threads: key-range shards
  * for the deps stage (InMemoryCommandStore.SingleThread per shard + PreAccept.reduce). */
-oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+oracle_result* oracle_run_masked(const ad_batch* b, const oracle_config* c, uint32_t flags, uint32_t threads,
                                  const uint8_t* view_mask);
-oracle_result* oracle_run(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads) {
+oracle_result* oracle_run(const ad_batch* b, const oracle_config* c, uint32_t flags, uint32_t threads) {
     return oracle_run_masked(b, c, flags, threads, nullptr);
 }
 
 /* As oracle_run; view_mask (nullable, [replicas * n]) selects, per txn, the replies the merge folds: the
  * coordinator's fast-path merge takes only the replies whose witnessedAt == TxnId
  * (CoordinateTransaction.onPreAccepted, coordinate/CoordinateTransaction.java:71-101, :75). */
-static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+static oracle_result* oracle_run_impl(const ad_batch* b, const oracle_config* c, uint32_t flags, uint32_t threads,
                                       const uint8_t* view_mask, const uint32_t* gid);
-oracle_result* oracle_run_masked(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+oracle_result* oracle_run_masked(const ad_batch* b, const oracle_config* c, uint32_t flags, uint32_t threads,
                                  const uint8_t* view_mask) {
     return oracle_run_impl(b, c, flags, threads, view_mask, nullptr);
 }
 /* As oracle_run over a batch whose rows carry global arrival ranks gid[n] (the engine's CFK history layout:
  * kept rows of earlier batches, then the new txns); window and drop decisions use gid.  Single-threaded,
  * PreAccept bound. */
-oracle_result* oracle_run_gid(const ad_batch* b, const ad_config* c, uint32_t flags, const uint32_t* gid) {
+oracle_result* oracle_run_gid(const ad_batch* b, const oracle_config* c, uint32_t flags, const uint32_t* gid) {
     return oracle_run_impl(b, c, flags & ~8u, 1, nullptr, gid);
 }
-static oracle_result* oracle_run_impl(const ad_batch* b, const ad_config* c, uint32_t flags, uint32_t threads,
+static oracle_result* oracle_run_impl(const ad_batch* b, const oracle_config* c, uint32_t flags, uint32_t threads,
                                       const uint8_t* view_mask, const uint32_t* gid) {
     oracle_result* res = new oracle_result();
     try {
@@ -936,7 +944,7 @@ static void preaccept_rules(const Batch& B, uint32_t i, uint32_t replicas, uint8
 /* witnessedAt proposal per view (CommandStore.preaccept, local/CommandStore.java:322-347): max_rank[v*n+i] =
  * Oracle::max_conflict (key and range footprints), fast[v*n+i] = TxnId_i >= that executeAt (or none) — the
  * fast-path test :343.  -1 on invalid input. */
-int oracle_max_conflicts(const ad_batch* b, const ad_config* c, uint32_t* max_rank, uint8_t* fast) {
+int oracle_max_conflicts(const ad_batch* b, const oracle_config* c, uint32_t* max_rank, uint8_t* fast) {
     try {
         Batch B(b);
         Config cfg;
@@ -977,7 +985,7 @@ static inline void carry_fold(const Ts& t, Ts& cb, bool& has) {
     if (c > 0 || (c == 0 && t.lsb > cb.lsb)) { cb = t; has = true; }
 }
 
-int oracle_max_conflicts_ts_ranges(const ad_batch* b, const ad_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
+int oracle_max_conflicts_ts_ranges(const ad_batch* b, const oracle_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
                                    const uint64_t* cl, const int32_t* cn, size_t mi, const uint64_t* is, const uint64_t* ie,
                                    const uint64_t* im, const uint64_t* il, const int32_t* in, uint64_t* om, uint64_t* ol,
                                    int32_t* on, uint8_t* fast) {
@@ -1022,7 +1030,7 @@ int oracle_max_conflicts_ts_ranges(const ad_batch* b, const ad_config* c, size_t
     }
 }
 
-int oracle_max_conflicts_ts(const ad_batch* b, const ad_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
+int oracle_max_conflicts_ts(const ad_batch* b, const oracle_config* c, size_t m, const uint64_t* ck, const uint64_t* cm,
                             const uint64_t* cl, const int32_t* cn, uint64_t* om, uint64_t* ol, int32_t* on, uint8_t* fast) {
     return oracle_max_conflicts_ts_ranges(b, c, m, ck, cm, cl, cn, 0, nullptr, nullptr, nullptr, nullptr, nullptr, om, ol,
                                           on, fast);

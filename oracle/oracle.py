@@ -29,11 +29,11 @@ def lib():
             build()
         L = C.CDLL(path)
         L.oracle_run.restype = C.c_void_p
-        L.oracle_run.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_uint32]
+        L.oracle_run.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.ModelConfig), C.c_uint32, C.c_uint32]
         L.oracle_run_masked.restype = C.c_void_p
-        L.oracle_run_masked.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_uint32, C.c_void_p]
+        L.oracle_run_masked.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.ModelConfig), C.c_uint32, C.c_uint32, C.c_void_p]
         L.oracle_run_gid.restype = C.c_void_p
-        L.oracle_run_gid.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_uint32, C.c_void_p]
+        L.oracle_run_gid.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.ModelConfig), C.c_uint32, C.c_void_p]
         L.oracle_error.restype = C.c_char_p
         L.oracle_error.argtypes = [C.c_void_p]
         L.oracle_sizes.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(abi.AdCsrSizes)]
@@ -41,14 +41,14 @@ def lib():
         L.oracle_levels.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
         L.oracle_free.argtypes = [C.c_void_p]
-        L.oracle_max_conflicts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.POINTER(C.c_uint32),
+        L.oracle_max_conflicts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.ModelConfig), C.POINTER(C.c_uint32),
                                            C.POINTER(C.c_uint8)]
         vp = C.c_void_p
-        L.oracle_max_conflicts_ts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_size_t, vp, vp, vp, vp,
+        L.oracle_max_conflicts_ts.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.ModelConfig), C.c_size_t, vp, vp, vp, vp,
                                               vp, vp, vp, vp]
         L.oracle_max_conflicts_export.argtypes = [C.POINTER(abi.AdBatch), C.c_size_t, vp, vp, vp, vp, C.POINTER(C.c_size_t),
                                                   vp, vp, vp, vp]
-        L.oracle_max_conflicts_ts_ranges.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.AdConfig), C.c_size_t, vp, vp, vp,
+        L.oracle_max_conflicts_ts_ranges.argtypes = [C.POINTER(abi.AdBatch), C.POINTER(abi.ModelConfig), C.c_size_t, vp, vp, vp,
                                                      vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_max_conflicts_export_ranges.argtypes = [C.POINTER(abi.AdBatch), C.c_size_t, vp, vp, vp, vp, vp,
                                                          C.POINTER(C.c_size_t), vp, vp, vp, vp, vp]

@@ -89,7 +89,7 @@ int main() {
         HostBatch b = make(g, 300 + g() % 900, round % 2 ? 60 : 5000, ranges, mixed, 1000000 + 20000ull * round);
         ad_batch bv = b.view();
         if (!ranges) bv.range_off = nullptr;
-        ad_config cfg{(uint32_t)(round % 3 ? 8 : 0), 3, round % 2 ? 0.2f : 0.0f, 0, (uint64_t)round};
+        oracle_config cfg{(uint32_t)(round % 3 ? 8 : 0), 3, round % 2 ? 0.2f : 0.0f, 0, (uint64_t)round};
         for (uint32_t threads : {1u, 3u}) {
             if (threads > 1 && ranges) continue;
             const uint32_t flags = (mixed ? 0u : 4u) | 2u | (threads > 1 ? 1u : 0u);

@@ -350,3 +350,107 @@ def rangedeps_expected(canonical, queries):
             ends.append(len(ks) + len(idx))
         out.append((ks, tx, ends + idx))
     return out
+
+
+# ---------------------------------------------------------------------------------------------------------
+# ReducingRangeMapTest.testRandomAdds (test/utils/ReducingRangeMapTest.java:166-232, RandomMap :234-292,
+# RandomWithCanonical.validate :385-470) — the additions and the probes its validate() draws, in stream order
+# ---------------------------------------------------------------------------------------------------------
+INT_MIN_J, INT_MAX_J = -(1 << 31), (1 << 31) - 1
+
+
+def next_double(r):
+    """java.util.Random.nextDouble(): ((long) next(26) << 27) + next(27)) * 2^-53."""
+    return ((r.next(26) << 27) + r.next(27)) * (1.0 / (1 << 53))
+
+
+def _jint_of_double(x):
+    """(int) of a double: truncation toward zero, saturating at the int range."""
+    return max(INT_MIN_J, min(INT_MAX_J, int(x)))
+
+
+def rrm_rk(r):
+    """ReducingRangeMapTest.rk(Random) (:62-69)."""
+    k = r.nextInt()
+    if r.nextBoolean():
+        k = _i32(-k)
+    if k == INT_MAX_J:
+        k -= 1
+    if k == INT_MIN_J:
+        k += 1
+    return k
+
+
+def rrm_add_one(r, max_range_count, max_coverage, min_chance):
+    """RandomMap.addOneRandom (:251-275) -> (StartInclusive ranges [s, e) after Ranges.of, hlc of ts(b))."""
+    count = 1 if max_range_count == 1 else 1 + r.nextInt(max_range_count - 1)
+    b = r.nextInt(INT_MAX_J)
+    cov = float(_f32(max_coverage))
+    chance = _f32(min_chance)
+    ranges = []
+    for _ in range(count):
+        length = _jint_of_double(2 * next_double(r) * cov * INT_MAX_J)
+        if length == 0:
+            length = 1
+        if next_float(r) <= chance:
+            if r.nextBoolean():
+                ranges.append((INT_MIN_J + 1, INT_MIN_J + 1 + length))
+            else:
+                ranges.append((INT_MAX_J - length - 1, INT_MAX_J - 1))
+        else:
+            start = r.nextInt(INT_MAX_J - length - 1)       # ValueError when the bound is <= 0, as Java throws
+            ranges.append((start, start + length))
+    return ranges_of(ranges), b
+
+
+def rrm_validate_probes(r, canonical_keys):
+    """The points and foldl queries RandomWithCanonical.validate (:385-470) draws: (points, [(keys, ranges)]).
+    points = decr/self/incr of every canonical key (int arithmetic wraps, as IntKey.Routing's does) then 1000
+    rk(random); each foldl query is RoutingKeys.of(1 + nextInt(20) random keys) and the Ranges built from them
+    (:409-428; [MIN_VALUE, k) / [k, MAX_VALUE) ends use MINIMUM_EXCL / MAXIMUM_EXCL)."""
+    points = []
+    for k in canonical_keys:
+        points += [_i32(k - 1), k, _i32(k + 1)]
+    for _ in range(1000):
+        points.append(rrm_rk(r))
+    folds = []
+    for _ in range(100):
+        count = 1 + r.nextInt(20)
+        keys = sorted(set(rrm_rk(r) for _ in range(count)))
+        rs, i = [], 0
+        if len(keys) % 2 == 1 and r.nextBoolean():
+            rs.append((INT_MIN_J, keys[0]))
+            i = 1
+        while i + 1 < len(keys):
+            rs.append((keys[i], keys[i + 1]))
+            i += 2
+        if i < len(keys):
+            rs.append((keys[i], INT_MAX_J))
+        folds.append((keys, ranges_of(rs)))
+    return points, folds
+
+
+def rrm_canonical_keys(additions):
+    """The keys of RandomWithCanonical.canonical after the additions (:374-379): MIN_VALUE, MAX_VALUE and every
+    range's start and end."""
+    ks = {INT_MIN_J, INT_MAX_J}
+    for ranges, _ in additions:
+        for s, e in ranges:
+            ks.add(s)
+            ks.add(e)
+    return sorted(ks)
+
+
+def rrm_random_adds(seed, merges, additions, max_ranges, max_coverage, min_chance):
+    """ReducingRangeMapTest.testRandomAdds(seed, ...) (:210-232): per merged map its additions [(ranges, b)] and the
+    probes its validate drew; the merge choices (random.nextBoolean per merge, :300-302); the probes of the final
+    validate over the merged map.  Returns (maps: [(additions, probes)], final_probes)."""
+    r = JavaRandom(seed)
+    maps = []
+    for _ in range(merges):
+        adds = [rrm_add_one(r, max_ranges, max_coverage, min_chance) for _ in range(additions)]
+        maps.append((adds, rrm_validate_probes(r, rrm_canonical_keys(adds))))
+    for _ in maps:
+        r.nextBoolean()                           # ReducingRangeMap.merge or mergeIntervals: the same map
+    allad = [a for adds, _ in maps for a in adds]
+    return maps, rrm_validate_probes(r, rrm_canonical_keys(allad))

@@ -58,5 +58,7 @@ def test_open_without_device_fails_loudly():
     with pytest.raises(engine.AccordDepsError):
         engine.DepsEngine(device=0)
     h = C.c_void_p()
-    cfg = abi.make_config()
+    cfg = abi.AdConfig(3, 0)
     assert engine.lib().ad_open(0, C.byref(cfg), C.byref(h)) == abi.AD_ERR_DEVICE
+    assert engine.lib().ad_open(0, C.byref(abi.AdConfig(0, 0)), C.byref(h)) == abi.AD_ERR_ARGUMENT
+    assert engine.lib().ad_set_replica_model(None, C.byref(abi.AdReplicaModel(32, 0.1, 1))) == abi.AD_ERR_ARGUMENT

@@ -389,3 +389,163 @@ def test_gpu_ts3_fold_tie_kat(engine_factory):
         w = O.max_conflicts_ts(b, abi.make_config(0, 1, 0.0, 1), carry=carry, carry_ranges=iv)
         for x, y in zip((m, l, nd, fast), w):
             assert np.array_equal(x, y)
+
+
+# ---- ReducingRangeMapTest.testRandomAdds (test/utils/ReducingRangeMapTest.java:166-232): the MaxConflicts range carry
+# The test's additions (RandomMap.addOneRandom: 1-2 StartInclusive ranges [s, e) per addition, one Timestamp
+# ts(b) = (epoch 1, hlc b, flags 0, node 1) each), its three maps merged with Timestamp::max, and the probes its
+# validate() draws (decr/self/incr of every canonical key, 1000 random keys, 100 foldl key sets and their Ranges) are
+# regenerated from the seed (refgen.rrm_random_adds).  Expected values come from the map's definition -- a point's
+# value is the max over the added ranges containing it (Range.StartInclusive.contains: s <= p < e), a range query's
+# the max over the added ranges it intersects -- not from the test's canonical TreeMap: that one keys each interval
+# by its lower bound but reads it with ceilingEntry (:312-315), and the test swallows AssertionFailedError (:225-228),
+# so its own expectation is not a usable oracle.
+# Mapping: each addition is a recorded range Write (TxnId epoch 0, executeAt ts(b)) of one batch, [s, e) the
+# interval (u(s) - 1, u(e) - 1] with u(x) = x + 2^31 + 1 (a key k stabs (k - 1, k]); a map is that batch's
+# max_conflicts_export_ranges, the merge is the carry (MaxConflicts.update = merge(this, ...), Timestamp::max).  A probe
+# is a txn of a second batch (status INVALID, so it records nothing) answered by max_conflicts_ts over the map alone.
+RRM_OFF = (1 << 31) + 1
+RRM_CASES = [(8532037884171168001, 3, 1, 3, 0.1, 0.1)] + [
+    (seed, 3, adds, 3, cov, chance) for adds in (1, 10, 100) for cov in (0.01, 0.1, 0.5) for chance in (0.01, 0.1)
+    for seed in (0x5EED0000 + 7 * adds + int(cov * 1000) + int(chance * 100), 0x0ACC0FFEE + adds)]
+
+
+def _rrm_u(x):
+    return x + RRM_OFF
+
+
+def _rrm_ts(b):
+    return (1 << 15, b << 16, 1)
+
+
+def _rrm_batch(txns, epoch):
+    """txns: [(kind, status, keys list, ranges [(a, b)) list, executeAt hlc or None)] -> a batch dict."""
+    n = len(txns)
+    tm, tl, tn, em, el, en, st, ko, ks, ro, rs, re_ = [], [], [], [], [], [], [], [0], [], [0], [], []
+    for i, (kind, status, keys, ranges, ex) in enumerate(txns):
+        flags = (kind << 1) | (1 if ranges else 0)
+        m, l, nd = R.txn_id(epoch, i + 1, flags, 1)
+        tm.append(m); tl.append(l); tn.append(nd)
+        e = _rrm_ts(ex) if ex is not None else (m, l, nd)
+        em.append(e[0]); el.append(e[1]); en.append(e[2])
+        st.append(status)
+        ks += [_rrm_u(k) for k in keys]
+        ko.append(len(ks))
+        for a, b in ranges:
+            rs.append(_rrm_u(a) - 1); re_.append(_rrm_u(b) - 1)
+        ro.append(len(rs))
+    u64 = lambda v: np.array(v, np.uint64)  # noqa: E731
+    return {"n": n, "txn_msb": u64(tm), "txn_lsb": u64(tl), "txn_node": np.array(tn, np.int32), "exec_msb": u64(em),
+            "exec_lsb": u64(el), "exec_node": np.array(en, np.int32), "status": np.array(st, np.uint8),
+            "key_off": np.array(ko, np.uint32), "keys": u64(ks), "range_off": np.array(ro, np.uint32) if rs else None,
+            "range_start": u64(rs) if rs else None, "range_end": u64(re_) if rs else None}
+
+
+def _rrm_adds_batch(adds):
+    return _rrm_batch([(abi.KIND_WRITE, abi.ST_APPLIED, [], ranges, b) for ranges, b in adds], 0)
+
+
+def _rrm_probe_batch(probes):
+    points, folds = probes
+    txns = [(abi.KIND_READ, abi.ST_INVALID, [p], [], None) for p in points]
+    for keys, ranges in folds:
+        txns.append((abi.KIND_READ, abi.ST_INVALID, keys, [], None))
+        txns.append((abi.KIND_READ, abi.ST_INVALID, [], ranges, None))
+    return _rrm_batch(txns, 2)
+
+
+def _rrm_expected(adds, probes):
+    """Per probe txn the map's answer: (msb, lsb, node) of the max ts(b), or Timestamp.NONE (0, 0, 0)."""
+    rs = [(s, e, b) for ranges, b in adds for s, e in ranges]
+
+    def point(p):
+        return max((b for s, e, b in rs if s <= p < e), default=None)
+
+    def span(a, c):
+        return max((b for s, e, b in rs if s < c and a < e), default=None)
+    points, folds = probes
+    vals = [point(p) for p in points]
+    for keys, ranges in folds:
+        vals.append(max((v for v in (point(k) for k in keys) if v is not None), default=None))
+        vals.append(max((v for v in (span(a, c) for a, c in ranges) if v is not None), default=None))
+    out = np.array([_rrm_ts(v) if v is not None else (0, 0, 0) for v in vals], np.int64)
+    return out[:, 0].astype(np.uint64), out[:, 1].astype(np.uint64), out[:, 2].astype(np.int32)
+
+
+def _rrm_normal_form(adds):
+    """The map as maximal pieces of one value, in the export's coordinates: (starts, ends, msb, lsb, node)."""
+    rs = [(s, e, b) for ranges, b in adds for s, e in ranges]
+    cuts = sorted({x for s, e, _ in rs for x in (s, e)})
+    pieces = []
+    for x, y in zip(cuts, cuts[1:]):
+        v = max((b for s, e, b in rs if s <= x and y <= e), default=None)
+        if v is None:
+            continue
+        if pieces and pieces[-1][1] == x and pieces[-1][2] == v:
+            pieces[-1][1] = y
+        else:
+            pieces.append([x, y, v])
+    u64 = lambda v: np.array(v, np.uint64)  # noqa: E731
+    return (u64([_rrm_u(x) - 1 for x, _, _ in pieces]), u64([_rrm_u(y) - 1 for _, y, _ in pieces]),
+            u64([1 << 15] * len(pieces)), u64([v << 16 for _, _, v in pieces]), np.ones(len(pieces), np.int32))
+
+
+def _rrm_case(case):
+    try:
+        return R.rrm_random_adds(*case)
+    except ValueError:                      # nextInt(MAX_VALUE - length - 1) with a bound <= 0: the Java test throws
+        return None
+
+
+def _rrm_check(export_ranges, answer, case):
+    """export_ranges(batch, carry) -> the map; answer(batch, carry) -> (msb, lsb, node) arrays [n]."""
+    got = _rrm_case(case)
+    if got is None:
+        return False
+    maps, final = got
+    carry = None
+    for adds, probes in maps:
+        own = export_ranges(_rrm_adds_batch(adds), None)
+        want = _rrm_normal_form(adds)
+        assert all(np.array_equal(x, y) for x, y in zip(own, want)), "%s: map pieces" % (case,)
+        for x, y, name in zip(answer(_rrm_probe_batch(probes), own), _rrm_expected(adds, probes), ("msb", "lsb", "node")):
+            bad = np.nonzero(x != y)[0]
+            assert len(bad) == 0, "%s: validate %s differs at probes %s" % (case, name, bad[:8])
+        carry = export_ranges(_rrm_adds_batch(adds), carry)
+    alladds = [a for adds, _ in maps for a in adds]
+    assert all(np.array_equal(x, y) for x, y in zip(carry, _rrm_normal_form(alladds))), "%s: merged pieces" % (case,)
+    for x, y in zip(answer(_rrm_probe_batch(final), carry), _rrm_expected(alladds, final)):
+        assert np.array_equal(x, y), "%s: final validate" % (case,)
+    return True
+
+
+def test_oracle_reducing_range_map_random_adds():
+    cfg = abi.make_config(0, 1, 0.0, 1)
+
+    def answer(b, carry):
+        m, l, nd, _ = O.max_conflicts_ts(b, cfg, None, carry)
+        return m[0], l[0], nd[0]
+    done = sum(_rrm_check(O.max_conflicts_export_ranges, answer, c) for c in RRM_CASES)
+    assert done >= len(RRM_CASES) - 3
+
+
+@pytest.mark.gpu
+def test_gpu_reducing_range_map_random_adds(engine_factory):
+    eng = engine_factory(window=0, replicas=1, drop_p=0.0, seed=1)
+
+    def run(b, carry):
+        eng.load(b)
+        eng.preaccept_deps()
+        eng.max_conflicts_carry(O.EMPTY_CARRY)
+        eng.max_conflicts_carry_ranges(O.EMPTY_CARRY_RANGES if carry is None else carry)
+        return eng.max_conflicts_ts()
+
+    def export_ranges(b, carry):
+        run(b, carry)
+        return tuple(a.copy() for a in eng.max_conflicts_export_ranges())
+
+    def answer(b, carry):
+        m, l, nd, _ = run(b, carry)
+        return m[0].copy(), l[0].copy(), nd[0].copy()
+    done = sum(_rrm_check(export_ranges, answer, c) for c in RRM_CASES[::2])
+    assert done >= len(RRM_CASES[::2]) - 2
