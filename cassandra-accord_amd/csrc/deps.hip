@@ -119,13 +119,25 @@ int complete_entries(ad_handle* h) {
 int stage_deps(ad_handle* h) {
     StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
-    const int nv = (int)h->cfg.replicas, nvc = 2 * nv;
+    // The union view (ad_run_pipeline): Deps.merge of the R replies is the union of their (key, TxnId) relations
+    // (RelationMultiMap.LinearMerger folds them with linearUnion per key), and the R views walk the same segments
+    // and differ only in the in-flight entries a view dropped.  So the walk emits a view R = "kept by some view"
+    // alongside the R replies, and k_txn_finish lays it out as one more class: the merged Deps come out of the deps
+    // stage and stage_merge runs no merge kernel.  Key-only PreAccept batches of one store (no range txns, no
+    // virtual items: their joins are per real view).
+    const bool want_u = h->want_union;
+    h->want_union = false;                                // one stage call (the overflow re-run below re-arms it)
+    const bool uni = want_u && Q == 0 && !h->accept && !h->sharded && !h->hist_active && h->n_large == 0 &&
+                     (int)h->cfg.replicas + 1 <= MAXV;
+    h->deps_union = uni;
+    const int nv = (int)h->cfg.replicas + (uni ? 1 : 0), nvc = 2 * nv;
     hipStream_t st = h->st;
     // directKeyDeps entries come only from key-domain sync points (CommandsForKey.managesExecution is false
     // for them, Deps.java:80-106); without any in the batch every directKeyDeps CSR is empty, so only the R
     // keyDeps classes are computed (computed class k = CSR cls[k]) and the direct CSRs are zero offsets.
     const bool direct = h->n_special > 0;
     const int nc = direct ? nvc : nv;
+    const int nc_real = direct ? 2 * (int)h->cfg.replicas : (int)h->cfg.replicas;   // classes of the R replies
     int cls[NVC_MAX];
     for (int k = 0; k < nc; ++k) cls[k] = direct ? k : 2 * k;
     h->deps_direct = direct;
@@ -189,6 +201,7 @@ int stage_deps(ad_handle* h) {
     wa.e_txn = h->e_txn; wa.e_meta = h->e_meta; wa.e_exec1 = h->e_exec1; wa.seg_start = h->seg_start;
     wa.ud_prev = h->ud_prev; wa.pm_w = h->pm_w; wa.pm_c = h->pm_c; wa.tx_ts = h->tx_ts; wa.meta = h->meta; wa.P = P;
     wa.window = h->cfg.window; wa.thresh = ad_drop_threshold(h->cfg.drop_p); wa.seed = h->cfg.seed;
+    wa.union_last = uni ? 1 : 0;
     wa.gid = (h->sharded || h->hist_active) ? h->gid : nullptr;
     wa.nh = h->nh; wa.prm = h->prm;
     wa.sval = h->sval; wa.cnt8 = h->cnt8; wa.cntx = h->cntx; wa.inl = h->inl; wa.dfr = h->dfr; wa.dst = h->dst;
@@ -197,6 +210,7 @@ int stage_deps(ad_handle* h) {
     uint32_t* heavy = h->totd + MAX_TOTALS - 1;          // heavy-merge hint (read with the totals)
     uint32_t* items_count = heavy - 1;                    // the fill walk's items (count walk)
     uint32_t* dtx_count = heavy - 2;                      // deferred small txns (offsets scan)
+    uint32_t* fovf_count = h->totd + MAX_TOTALS - 7;      // k_txn_finish's overflowed (txn, class) rows
     uint32_t *items = nullptr, *dtx = nullptr;
     CK(dalloc(h, S_OVI, &items, std::max<size_t>(P, 1)));
     CK(dalloc(h, S_DTX, &dtx, std::max<size_t>(n, 1)));
@@ -215,7 +229,7 @@ int stage_deps(ad_handle* h) {
         f.P = P; f.ntiles = ntiles; f.skey = h->skey; f.prec = h->prec; f.overflow = fuse_over;
         CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 4 * ntiles + SF_PARTS));
         f.hpart = f.tile_cnt + 4 * ntiles;
-        fill_multi(st, {{fuse_over, 4, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0},
+        fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0},
                         {h->dfr, n, 0}});
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;
@@ -226,13 +240,15 @@ int stage_deps(ad_handle* h) {
         h->sf_ntiles = ntiles;
     } else {
         h->nh_valid = true;
-        fill_multi(st, {{dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
+        fill_multi(st, {{fovf_count, 4, 0}, {dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
         launch_walk_nv(nv, wa, false, direct, true, st);
     }
     TxnArgs ta{};
     ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
+    CK(dalloc(h, S_FOVF, &ta.ovf_rows, std::max<size_t>(n * (size_t)nc, 1)));
+    ta.ovf_count = fovf_count;
     // every large txn's per-CSR totals, also when no range meets a CFK key (V = 0: a batch of range txns only); the
     // offsets scan reads them for every large txn
     if (n > 0 && h->n_large > 0) {
@@ -317,6 +333,7 @@ int stage_deps(ad_handle* h) {
         // finish, if any, exited or is redone there)
         HIPCHK(h, hipStreamSynchronize(st));
         h->seg_long = true;
+        h->want_union = want_u;
         return stage_deps(h);
     }
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
@@ -333,7 +350,8 @@ int stage_deps(ad_handle* h) {
     for (int c = 0; c < ncsr; ++c) {
         Csr& x = csr_at(c);
         x.nkeys = tot[3 * c]; x.nk2t = tot[3 * c + 1]; x.ncap = tot[3 * c + 2];
-        h->deps_entries += x.ncap;
+        // the replies' entries (the union view's are the merged Deps': merged_entries)
+        if (!(uni && c >= nc_real && c < nc)) h->deps_entries += x.ncap;
         if (c >= nc) h->times.range_entries += x.ncap;
         if (c < nc) {
             CK(alloc_csr_data(h, cls[c], x, 1));

@@ -382,6 +382,7 @@ struct WalkArgs {
     uint32_t window;
     uint32_t thresh;
     uint64_t seed;
+    int union_last;           // view NV - 1 is the union of the others (deps.hip stage_deps: the merged Deps)
     const uint32_t* sval;     // sorted position -> pair index p
     uint8_t* cnt8;            // real pairs, AoS by pair: [p * NCB + k] count of class k, 255 = see cntx
     uint32_t* cntx;           // [p * NC + k] exact count where cnt8 saturated (>= 255)
@@ -445,9 +446,18 @@ __device__ inline void walk_query(const WalkArgs& a, uint32_t i, uint32_t gq, ui
         const uint32_t mj = a.e_meta[q];
         if (!manages(mj) || !witnesses(qk, meta_kind(mj))) continue;
         const bool direct = !manages_execution(mj);
+        if (a.union_last) {
+            // the union view: j is in the merged Deps iff some reply kept it
+            bool kept = false;
 #pragma unroll
-        for (int v = 0; v < NV; ++v)
-            if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh)) emit(v, direct, j);
+            for (int v = 0; v + 1 < NV; ++v)
+                if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh)) { emit(v, direct, j); kept = true; }
+            if (kept) emit(NV - 1, direct, j);
+        } else {
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (!(a.thresh && drop_hash(a.seed, (uint32_t)v, gi, gj) < a.thresh)) emit(v, direct, j);
+        }
     }
     // 2. the committed prefix [seg0, p]: mapReduceActive with transitive-dependency elision.
     const int p = q;
@@ -651,6 +661,8 @@ struct TxnArgs {
     uint32_t* vdst;               // [x * nvc + vc] (aliases vcnt: each slot is read, then rewritten, once)
     const uint32_t* vi_u;         // item -> distinct-key index (its key = ukey[u])
     const uint64_t* ukey;
+    uint32_t* ovf_rows;           // k_txn_finish -> k_txn_finish_ovf: (txn * nvc + class) rows whose lists overflowed
+    uint32_t* ovf_count;          //   their inline ids (zeroed before the finish)
 };
 
 // Large txns (virtual items: range-domain txns, >16-key txns), one wave per txn: per-CSR key and entry
@@ -810,7 +822,8 @@ struct OffsetsOp {
 };
 
 // Sorts 16 keys ascending in registers (bitonic network, compile-time indices only).
-__device__ inline void sort16(uint64_t* v) {
+template <class T>
+__device__ inline void sort16(T* v) {
 #pragma unroll
     for (int k = 2; k <= 16; k <<= 1) {
 #pragma unroll
@@ -819,7 +832,7 @@ __device__ inline void sort16(uint64_t* v) {
             for (int i = 0; i < 16; ++i) {
                 const int l = i ^ j;
                 if (l > i) {
-                    const uint64_t x = v[i], y = v[l];
+                    const T x = v[i], y = v[l];
                     const bool up = (i & k) == 0;
                     const bool sw = up ? x > y : x < y;
                     v[i] = sw ? y : x;
@@ -911,7 +924,8 @@ static __global__ __launch_bounds__(64) void k_cap_check(CapCheck a) {
     if (l == 0) *a.bad = m ? 1u : 0u;
 }
 
-template <int NV, bool DIRECT>
+// WIDE: batches of 2^28 txns or more (the 32-bit sort words hold TxnId << 4)
+template <int NV, bool DIRECT, bool WIDE>
 static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     constexpr int NVC = DIRECT ? 2 * NV : NV;
     if (a.spec_bad && *a.spec_bad) return;          // speculative launch into too-small buffers: re-run after sizing
@@ -972,23 +986,10 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     }
     uint32_t* tx = a.out_txns[c] + ob;
     if (ovf) {
-        // the lists in memory (raw TxnIds, ascending): inline ids, and the overflowed pairs re-walked for this class
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (cc[j] == 0) continue;
-            if (cc[j] <= (uint32_t)WALK_INL) {
-#pragma unroll
-                for (int q = 0; q < WALK_INL; ++q)
-                    if ((uint32_t)q < cc[j]) k2t[mb + rb[j] + cc[j] - 1 - (uint32_t)q] = (int32_t)id[j][q];
-            } else {
-                const size_t sp = a.w.posof[b + j];
-                uint32_t slot = mb + rb[j] + cc[j] - 1;
-                walk_entry<NV>(a.w, sp, (uint32_t)t, mt, [&](int v, bool direct, uint32_t dj) {
-                    if (walk_class<NV, DIRECT>(v, direct) == c) k2t[slot--] = (int32_t)dj;
-                });
-            }
-        }
-        a.out_tcnt[c][t] = union_small<4>(k2t, mb, nk, tx);
+        // some list of this class overflowed its inline ids: k_txn_finish_ovf lays the lists out from memory (a
+        // re-walk of the overflowed pairs); kept out of this kernel, whose registers it would raise from 60 to 81
+        // (8 -> 5 waves per SIMD)
+        wave_append(true, (uint32_t)(t * NVC + c), a.ovf_rows, a.ovf_count);
         return;
     }
     if (nk == 1) {                                  // one key: its list is the union, indices 0..cc-1
@@ -1007,13 +1008,39 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
         }
         return;
     }
-    // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index
+    // several keys: (TxnId, k2t slot) pairs sorted in registers, equal TxnIds folded into one index.  Batches below
+    // 2^28 txns sort 32-bit words (TxnId << 4 | pair * 4 + id): half the registers of (TxnId, slot) u64 pairs
+    // (82 -> fewer VGPRs: more waves per SIMD for this latency-bound kernel)
+    uint32_t sb[4];                                 // k2t slot of pair j's id 0 (ids run downwards from it)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sb[j] = mb + rb[j] + cc[j] - 1;
+    if (!WIDE) {
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < WALK_INL; ++q)
+                v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? (id[j][q] << 4) | (uint32_t)(j * WALK_INL + q) : ~0u;
+        sort16(v);
+        uint32_t u = 0, prev = 0xFFFFFFFFu;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (v[r] != ~0u) {
+                const uint32_t y = v[r] >> 4, jq = v[r] & 15u, j = jq >> 2;
+                const uint32_t base = j == 0 ? sb[0] : j == 1 ? sb[1] : j == 2 ? sb[2] : sb[3];
+                if (y != prev) { tx[u++] = y; prev = y; }
+                k2t[base - (jq & 3u)] = (int32_t)(u - 1);
+            }
+        }
+        a.out_tcnt[c][t] = u;
+        return;
+    }
     uint64_t v[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int q = 0; q < WALK_INL; ++q)
-            v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)id[j][q] << 32) | (uint64_t)(mb + rb[j] + cc[j] - 1 - (uint32_t)q) : ~0ull;
+            v[j * WALK_INL + q] = (uint32_t)q < cc[j] ? ((uint64_t)id[j][q] << 32) | (uint64_t)(sb[j] - (uint32_t)q) : ~0ull;
     sort16(v);
     uint32_t u = 0, prev = 0xFFFFFFFFu;
 #pragma unroll
@@ -1026,6 +1053,43 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     }
     a.out_tcnt[c][t] = u;
 }
+// The (txn, class) rows k_txn_finish listed: the per-key lists in memory (raw TxnIds, ascending) from the inline ids
+// and, for the overflowed pairs, a re-walk of that pair for this class (walk_entry from posof), then the union
+// (union_small).  Rare (C2: a few txns); grid-stride over the device-side count.
+template <int NV, bool DIRECT>
+static __global__ __launch_bounds__(256) void k_txn_finish_ovf(TxnArgs a) {
+    constexpr int NVC = DIRECT ? 2 * NV : NV;
+    constexpr int NCB = ncb_of(NVC);
+    if (a.spec_bad && *a.spec_bad) return;
+    const uint32_t cnt = *(const volatile uint32_t*)a.ovf_count;
+    for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < cnt; x += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t r = a.ovf_rows[x];
+        const size_t t = r / NVC;
+        const int c = (int)(r - t * NVC);
+        const uint32_t nk = a.out_key_off[c][t + 1] - a.out_key_off[c][t];
+        const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
+        const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
+        const uint32_t mt = a.meta[t];
+        int32_t* k2t = a.out_k2t[c];
+        uint32_t run = nk;
+        for (uint32_t y = b; y < e; ++y) {                   // <= 4 pairs (k_txn_finish's small txns)
+            const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, y, c);
+            if (cc == 0) continue;
+            if (cc <= (uint32_t)WALK_INL) {
+                const uint32_t* src = a.inl + ((size_t)y * NVC + c) * WALK_INL;
+                for (uint32_t q = 0; q < cc; ++q) k2t[mb + run + cc - 1 - q] = (int32_t)src[q];
+            } else {
+                uint32_t slot = mb + run + cc - 1;
+                walk_entry<NV>(a.w, (size_t)a.w.posof[y], (uint32_t)t, mt, [&](int v, bool direct, uint32_t dj) {
+                    if (walk_class<NV, DIRECT>(v, direct) == c) k2t[slot--] = (int32_t)dj;
+                });
+            }
+            run += cc;
+        }
+        a.out_tcnt[c][t] = union_small<4>(k2t, mb, nk, a.out_txns[c] + ob);
+    }
+}
+
 struct UnionArgs {
     size_t n;
     int nvc;

@@ -25,8 +25,17 @@ void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy, 
 template <int NV>
 void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
     const unsigned g = (unsigned)ceil_div((long)ta.nrows * (direct ? 2 * NV : NV), 256);
-    if (direct) k_txn_finish<NV, true><<<g, 256, 0, st>>>(ta);
-    else k_txn_finish<NV, false><<<g, 256, 0, st>>>(ta);
+    const bool wide = ta.n >= (1u << 28) - 1;       // ids beyond the 32-bit sort words (TxnId << 4)
+    if (direct) {
+        if (wide) k_txn_finish<NV, true, true><<<g, 256, 0, st>>>(ta);
+        else k_txn_finish<NV, true, false><<<g, 256, 0, st>>>(ta);
+    } else {
+        if (wide) k_txn_finish<NV, false, true><<<g, 256, 0, st>>>(ta);
+        else k_txn_finish<NV, false, false><<<g, 256, 0, st>>>(ta);
+    }
+    const unsigned go = std::min(g, 16384u);             // the overflowed rows (a device-side count)
+    if (direct) k_txn_finish_ovf<NV, true><<<go, 256, 0, st>>>(ta);
+    else k_txn_finish_ovf<NV, false><<<go, 256, 0, st>>>(ta);
 }
 
 template <int NV>

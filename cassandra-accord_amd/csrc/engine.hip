@@ -407,10 +407,12 @@ static int load_working(ad_handle* h) {
     CK(dalloc(h, S_EEXEC, &h->e_exec1, P)); CK(dalloc(h, S_PMW, &h->pm_w, P)); CK(dalloc(h, S_PMC, &h->pm_c, P));
     CK(dalloc(h, S_SEG, &h->seg_start, P)); CK(dalloc(h, S_UD, &h->ud_prev, P));
     CK(dalloc(h, S_UIDX, &h->nh, P)); CK(dalloc(h, S_UKEY, &h->ukey, P)); CK(dalloc(h, S_USEG, &h->useg, P + 1));
-    CK(dalloc(h, S_CNT, &h->cnt8, (size_t)ncb_of(nvc) * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nvc * P));
-    CK(dalloc(h, S_CNTX, &h->cntx, (size_t)nvc * P)); CK(dalloc(h, S_INL, &h->inl, (size_t)nvc * P * WALK_INL));
+    // per-pair / per-txn class words: the R replies' classes plus the union view's (ad_run_pipeline, stage_deps)
+    const int nwc = 2 * std::min(nv + 1, MAXV);
+    CK(dalloc(h, S_CNT, &h->cnt8, (size_t)ncb_of(nwc) * P)); CK(dalloc(h, S_DST, &h->dst, (size_t)nwc * P));
+    CK(dalloc(h, S_CNTX, &h->cntx, (size_t)nwc * P)); CK(dalloc(h, S_INL, &h->inl, (size_t)nwc * P * WALK_INL));
     CK(dalloc(h, S_DFR, &h->dfr, n));
-    CK(dalloc(h, S_NK, &h->nk, (size_t)nvc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nvc * n + n));
+    CK(dalloc(h, S_NK, &h->nk, (size_t)nwc * n + n)); CK(dalloc(h, S_NE, &h->ne, (size_t)nwc * n + n));
     CK(dalloc(h, S_VN, &h->vn, n)); CK(dalloc(h, S_VOFF, &h->voff, n + 1));
     CK(dalloc(h, S_LVL, &h->lvl, n + 1)); CK(dalloc(h, S_ORDER, &h->order, n + 1));
     CK(dalloc(h, S_ROWN, &h->rowner, Q)); CK(dalloc(h, S_RK0, &h->rk0, Q)); CK(dalloc(h, S_RV0, &h->rv0, Q));
@@ -1178,10 +1180,20 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
 
 // The merged Deps of every class in one call: Deps.merge's outputs carry exact per-txn TxnId offsets
 // (MultiOffsetsOp), so every array goes straight from HBM into the caller's buffers (pinned: DMA) with one stream
-// sync and no host-side compaction.  out[c] sized by ad_merged_sizes.
+// sync and no host-side compaction.  out[c] sized by ad_merged_sizes.  Merged Deps built as the deps stage's union
+// view (ad_run_pipeline) hold per-txn capacity regions like the replies: those go through fetch_csr's compaction.
 int ad_merged_sizes(ad_handle* h, ad_csr_sizes* sizes /* [3] */) {
     if (!h || !sizes) return AD_ERR_ARGUMENT;
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
+    if (!h->merged_exact) {
+        hipSetDevice(h->device);
+        for (int c = 0; c < 3; ++c) {
+            if (c == AD_CLASS_RANGE && !h->merged_has_range) { sizes[c] = ad_csr_sizes{h->n, 0, 0, 0, 0}; continue; }
+            CK(csr_sizes(h, h->merged[c], &sizes[c]));
+            sizes[c].txn_cap = sizes[c].txns;             // the compacted lists fetched below
+        }
+        return AD_OK;
+    }
     for (int c = 0; c < 3; ++c) {
         const Csr& m = h->merged[c];
         const bool empty = c == AD_CLASS_RANGE && !h->merged_has_range;
@@ -1194,6 +1206,10 @@ int ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [3] */) {
     if (!h || !out) return AD_ERR_ARGUMENT;
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     hipSetDevice(h->device);
+    if (!h->merged_exact) {
+        for (int c = 0; c < 3; ++c) CK(ad_fetch_merged(h, (uint32_t)c, &out[c]));
+        return AD_OK;
+    }
     hipStream_t st = h->st;
     const size_t n = h->n;
     for (int c = 0; c < 3; ++c) {
@@ -1330,6 +1346,7 @@ int ad_run_pipeline(ad_handle* h) {
     HIPCHK(h, hipEventRecord(h->ev[1], st));
     CK(stage_sort(h));
     HIPCHK(h, hipEventRecord(h->ev[2], st));
+    h->want_union = true;                        // the merged Deps as the deps stage's union view (stage_deps)
     CK(stage_deps(h));
     HIPCHK(h, hipEventRecord(h->ev[3], st));
     CK(stage_merge(h));

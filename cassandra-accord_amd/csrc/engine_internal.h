@@ -180,6 +180,9 @@ struct ad_handle {
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     bool entries_partial = false;    // the deps stage skipped the lone entries' gather (complete_entries)
     bool seg_long = false;           // the loaded batch has a key segment too long for k_seg_fuse's tiles
+    bool want_union = false;         // ad_run_pipeline: the deps stage also builds the union view (the merged Deps)
+    bool deps_union = false;         // the last deps stage did: deps[2R], deps[2R + 1] are the merged key classes
+    bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
     bool nh_valid = false;           // nh holds the batch's non-head entries (not after k_seg_fuse)
     bool keys_partial = false;       // k_seg_fuse left ukey / useg to complete_entries (from its tiles)
     size_t sf_ntiles = 0;
@@ -309,7 +312,7 @@ enum Slot : size_t {
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
     S_CS0, S_CS_END = S_CS0 + 14,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
-    S_SFLO, S_SFCNT,                                     // k_seg_fuse tiles
+    S_SFLO, S_SFCNT, S_FOVF,                                     // k_seg_fuse tiles
     S_NUM_FIXED,
     S_CSR0 = 320
 };

@@ -592,20 +592,14 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
 // predecessors (indeg) and a backward pass gives its successor run (succ[pair]).  Single-entry segments
 // have no edges and are skipped; a segment longer than SHORT_SEG raises *any_long and the caller falls
 // back to the fixpoint (whose chain preparation handles long chains).
-// One thread per non-head entry (ElideOp's dense list; nh == null: one per sorted position, the batches whose deps
-// stage ran k_seg_fuse, which builds no list); the second entry of each segment builds it.
-static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
-                                                     const int32_t* __restrict__ seg_start,
-                                                     const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
-                                                     const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
-                                                     uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
-                                                     uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
-                                                     uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
-                                                     uint32_t* __restrict__ any_long, int full, int pred_mode = 0,
-                                                     uint32_t* __restrict__ any_far = nullptr) {
-    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool lng = false, far = false;
-    const size_t s2 = nh ? (x < P - prm->n_keys_u ? (size_t)nh[x] : 0) : (x + 1 < P ? x + 1 : 0);
+// The chain of the key segment whose second entry is s2 (s2 = 0 or not a second entry: nothing).
+__device__ inline void chain_build_seg(size_t P, size_t s2, const int32_t* __restrict__ seg_start,
+                                       const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                       const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                       uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                       uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
+                                       uint32_t* __restrict__ indeg, uint2* __restrict__ succ, int full, int pred_mode,
+                                       bool& lng, bool& far) {
     const size_t s = s2 - 1;
     if (s2 > 0 && seg_start[s2] == (int32_t)s) {
         size_t end = s + 2;
@@ -666,6 +660,52 @@ static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint
                 succ[c_pair[q]] = sc;
             }
         }
+    }
+}
+
+// One thread per non-head entry (ElideOp's dense list); the second entry of each segment builds it.  nh == null (the
+// batches whose deps stage ran k_seg_fuse, which builds no list): each workgroup covers CB_SPAN sorted positions and
+// first compacts its segments' second entries into LDS, so the builders run on full waves (one thread per position
+// left ~85 % of the lanes of this latency-bound kernel idle: 41 -> 115 us on C2)
+constexpr int CB_SPAN = 1024;
+static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
+                                                     const int32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                                     const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                                     uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                                     uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
+                                                     uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
+                                                     uint32_t* __restrict__ any_long, int full, int pred_mode = 0,
+                                                     uint32_t* __restrict__ any_far = nullptr) {
+    bool lng = false, far = false;
+    if (nh) {
+        const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
+        chain_build_seg(P, s2, seg_start, e_txn, e_meta, e_exec1, sval, c_txn, c_meta, c_exec1, c_pair, indeg, succ, full,
+                        pred_mode, lng, far);
+    } else {
+        __shared__ uint32_t q[CB_SPAN];
+        __shared__ uint32_t qn;
+        if (threadIdx.x == 0) qn = 0;
+        __syncthreads();
+        const size_t base = (size_t)blockIdx.x * CB_SPAN;
+        const int lane = __lane_id();
+        for (int k = 0; k < CB_SPAN / 256; ++k) {
+            const size_t s2 = base + (size_t)k * 256 + threadIdx.x + 1;
+            const bool want = s2 < P && seg_start[s2] == (int32_t)(s2 - 1);
+            const uint64_t m = __ballot(want);
+            if (!m) continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t b0 = 0;
+            if (lane == leader) b0 = atomicAdd(&qn, (uint32_t)__popcll(m));
+            b0 = __shfl(b0, leader);
+            if (want) q[b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)s2;
+        }
+        __syncthreads();
+        const uint32_t nq = qn;
+        for (uint32_t k = threadIdx.x; k < nq; k += blockDim.x)
+            chain_build_seg(P, q[k], seg_start, e_txn, e_meta, e_exec1, sval, c_txn, c_meta, c_exec1, c_pair, indeg, succ,
+                            full, pred_mode, lng, far);
     }
     wave_set_flag(lng, any_long);
     if (any_far) wave_set_flag(far, any_far);
@@ -1570,6 +1610,52 @@ static __global__ __launch_bounds__(256) void k_rank_check(size_t m, const uint6
         if (b && fail_out) *(volatile uint32_t*)fail_out = 1u;    // host-mapped: read after the caller's sync
     }
 }
+// The optimistic order's check fused into the level pass's digit histogram (levels <= 255: one 8-bit digit): per
+// RS_TILE tile of the executeAt-rank-ordered rows, the level histogram k_radix_hist writes, and k_rank_check's
+// verification (every slot filled, executeAt ascending, no level above the assumed depth) on the same reads.
+static __global__ __launch_bounds__(RS_BLOCK) void k_rank_check_hist(size_t m, const uint64_t* __restrict__ okey,
+                                                                     const uint32_t* __restrict__ oidx,
+                                                                     const uint32_t* __restrict__ olvl, int ntiles,
+                                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ flags,
+                                                                     uint32_t* fail_out, uint32_t max_level) {
+    __shared__ uint32_t h[RS_WAVES][256];
+    __shared__ uint32_t red[RS_WAVES], rb[RS_WAVES];
+    const int w = threadIdx.x / WAVE;
+    for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_BLOCK) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+    uint32_t v = 0;
+    bool bad = false;
+#pragma unroll 4
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        const size_t i = base + (size_t)k * RS_BLOCK + threadIdx.x;
+        if (i < m) {
+            const uint32_t x = olvl[i];
+            atomicAdd(&h[w][x & 0xFF], 1u);
+            v = x > v ? x : v;
+            if (oidx[i] == WR_EMPTY || (i + 1 < m && okey[i] > okey[i + 1])) bad = true;
+        }
+    }
+    v = wave_max(v);
+    const bool wbad = __ballot(bad) != 0;
+    if (__lane_id() == 0) { red[w] = v; rb[w] = wbad ? 1u : 0u; }
+    __syncthreads();
+    for (int d = threadIdx.x; d < 256; d += RS_BLOCK) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int x = 0; x < RS_WAVES; ++x) c += h[x][d];
+        hist[(size_t)d * ntiles + blockIdx.x] = c;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t mx = red[0], b = rb[0];
+        for (int k = 1; k < RS_WAVES; ++k) { mx = mx > red[k] ? mx : red[k]; b |= rb[k]; }
+        atomicMax(&flags[0], mx);
+        if (mx > max_level) b = 1;
+        if (b) atomicOr(&flags[1], 1u);
+        if (b && fail_out) *(volatile uint32_t*)fail_out = 1u;    // host-mapped: read after the caller's sync
+    }
+}
+
 // level of each txn in `perm` order (dst) + max level (fallback path).  Grid-stride over a bounded grid:
 // one atomic per block.
 constexpr int ORDER_GRID = 1024;
@@ -1616,6 +1702,15 @@ inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     // fast path: windowed inversion ranks + verification
     fill_multi(st, {{of, 8, 0}, {v, m * 4, 0xFF}});           // flags; WR_EMPTY: detects rank collisions
     k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1);
+    if (optimistic && known_maxl > 0 && known_maxl <= 255) {
+        // one stable pass by level whose histogram kernel is also the check, written straight into order_out
+        const int ntiles = ceil_div((long)m, RS_TILE);
+        k_rank_check_hist<<<ntiles, RS_BLOCK, 0, st>>>(m, ls.key64, v, k, ntiles, rs.hist, of, verify_dev,
+                                                       (uint32_t)known_maxl);
+        k_radix_rowscan<<<256, 1024, 0, st>>>(rs.hist, ntiles, rs.offs, rs.agg);
+        k_radix_scatter<<<ntiles, RS_BLOCK, 0, st>>>(k, v, ko, order_out, m, 0, ntiles, rs.offs, rs.agg);
+        return true;
+    }
     k_rank_check<<<gg, 256, 0, st>>>(m, ls.key64, v, k, of, optimistic ? verify_dev : nullptr,
                                      optimistic ? (uint32_t)known_maxl : 0xFFFFFFFFu);
     if (optimistic) {
@@ -1830,6 +1925,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
     {
         // ---- chain order, segment table, pair -> segment, long-segment positions, (c) constraints
         const int gP = ceil_div((long)std::max<size_t>(P, 1), 256);
+        const int gCB = ceil_div((long)std::max<size_t>(P, 1), CB_SPAN);     // k_chain_build without nh
         const bool has_b = (in.merged_direct && in.merged_direct->ncap > 0) || (in.merged_range && in.merged_range->ncap > 0);
         const bool has_c = (in.n_large > 0 || in.n_special > 0) && nkm > 0 && P > 0;
         PushCtx push{};
@@ -1917,7 +2013,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 KScope ks(K_KAHN, P);
                 const int gn = ceil_div((long)n, 256);
                 // predecessor runs zeroed above; ls.flags [16] abort, [17] max level, [18] far pred (zeroed above)
-                k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                k_chain_build<<<in.nh ? gP : gCB, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
                                                   ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1,
                                                   ls.flags + 18);
                 k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
@@ -1976,7 +2072,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 k_mix_kinds<<<gn1, 256, 0, st>>>(n, in.meta, ls.flags + 20);
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
                 if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-                k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                k_chain_build<<<in.nh ? gP : gCB, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
                                                   ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0, 1);
                 hipMemsetAsync(ls.sv1, 0xFF, n * 4, st);
                 k_window_rank<<<ceil_div((long)n, WR_N), WR_T, 0, st>>>(n, in.ex1, nullptr, in.lvl, ls.key64, ls.sv1, ls.sk1, ls.flags + 21);
@@ -2065,7 +2161,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
                 // (c) searches every chain in executeAt order, singletons included
                 if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-                k_chain_build<<<gP, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
+                k_chain_build<<<in.nh ? gP : gCB, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
                                                   ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0);
                 // long chains found by the build (flags[7]): rebuild every chain with the parallel kernels
                 bool long_done = false;

@@ -151,6 +151,7 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
         ++K;
     }
     CK(merge_multi(h, n, K, out, blocks, kw, in, view_rows ? rows : nullptr, np, &h->merged_entries));
+    h->merged_exact = true;
     h->have_merged = true;
     return AD_OK;
 }
@@ -159,6 +160,19 @@ int stage_merge(ad_handle* h) {
     StageScope sc(h, STAGE_MERGE);
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps before ad_preaccept_deps");
     const int nv = (int)h->cfg.replicas;
+    if (h->deps_union) {
+        // the deps stage built the union view (stage_deps): the merged key classes are its CSRs, the range class
+        // is empty (no range txns in such a batch)
+        const size_t n = h->n;
+        h->merged[AD_CLASS_KEY] = h->deps[2 * nv];
+        h->merged[AD_CLASS_DIRECT_KEY] = h->deps[2 * nv + 1];
+        CK(zero_csr(h, CSR_MERGED0 + AD_CLASS_RANGE, h->merged[AD_CLASS_RANGE], n));
+        h->merged_entries = 0;
+        for (int c = 0; c < 2; ++c) h->merged_entries += h->merged[c].nk2t - h->merged[c].nkeys;
+        h->merged_exact = false;
+        h->have_merged = true;
+        return AD_OK;
+    }
     const Csr* parts[3][MAXV] = {};
     for (int v = 0; v < nv; ++v) {
         parts[0][v] = &h->deps[2 * v];

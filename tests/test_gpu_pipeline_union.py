@@ -1,0 +1,65 @@
+"""ad_run_pipeline's merged Deps as the deps stage's union view (deps.hip stage_deps, merge.hip stage_merge): the
+replies, the merged Deps (per class, ad_fetch_merged and ad_fetch_merged_all) and the levels equal the oracle's
+Deps.merge (RelationMultiMap.LinearMerger, utils/RelationMultiMap.java:284-406) on batches that take every branch
+of the deps stage: the fused tile kernel, the three-kernel path (hot keys), direct classes (sync points), txns with
+more than four keys (fill walk + k_txn_union), inline-id overflow re-walks, 1 and 7 replica views."""
+import numpy as np
+import pytest
+
+import oracle as O
+from accord_amd import abi, workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixed(n, seed):
+    rng = np.random.default_rng(seed)
+    kinds = rng.choice([abi.KIND_READ, abi.KIND_WRITE, abi.KIND_EPHEMERAL_READ, abi.KIND_SYNC_POINT,
+                        abi.KIND_EXCLUSIVE_SYNC_POINT], p=[0.4, 0.4, 0.1, 0.05, 0.05], size=n)
+    status = rng.integers(0, 8, size=n).astype(np.uint8)
+    return workload.generate(n, keys_per_txn=3, keyspace=5000, seed=seed, kinds=kinds, status=status)
+
+
+CASES = {
+    "c2": (lambda: workload.config("C2", n=50000, seed=9), (32, 3, 0.1)),
+    "mixed_direct": (lambda: _mixed(20000, 4), (16, 3, 0.2)),
+    "hot_keys": (lambda: workload.generate(20000, keys_per_txn=2, keyspace=50, seed=5), (32, 3, 0.1)),
+    "wide": (lambda: workload.generate(10000, keys_per_txn=6, keyspace=20000, seed=6), (32, 3, 0.1)),
+    "one_view": (lambda: workload.config("C2", n=30000, seed=7), (0, 1, 0.0)),
+    "seven_views": (lambda: workload.generate(20000, keys_per_txn=4, keyspace=30000, seed=8), (64, 7, 0.3)),
+    "c3": (lambda: workload.config("C3", n=20000, seed=10), (32, 3, 0.1)),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_pipeline_union_equals_oracle(engine_factory, name):
+    make, (w, r, d) = CASES[name]
+    b = make()
+    eng = engine_factory(window=w, replicas=r, drop_p=d, seed=0x5EED)
+    eng.load(b)
+    eng.run_pipeline()
+    ref = O.OracleResult(b, abi.make_config(w, r, d, 0x5EED), O.FLAG_MERGE | O.FLAG_LEVELS)
+    for v in range(r):
+        for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
+            got, want = eng.fetch_rows(v, c, 0, b["n"]), ref.deps(v, c)
+            assert got.equal(want), "%s view %d class %d differs at txn %s" % (name, v, c, got.first_difference(want))
+    merged = [eng.fetch_rows(r, c, 0, b["n"]) for c in range(abi.NUM_CLASSES)]   # view == replicas: the merged Deps
+    for c in range(abi.NUM_CLASSES):
+        want = ref.merged(c)
+        assert merged[c].equal(want), "%s merged class %d differs at txn %s" % (name, c, merged[c].first_difference(want))
+    allm = eng.fetch_merged_all()
+    for c in range(abi.NUM_CLASSES):
+        assert allm[c].equal(merged[c]), "%s: ad_fetch_merged_all class %d" % (name, c)
+    s = eng.merged_sizes()
+    for c in range(abi.NUM_CLASSES):
+        assert s[c].txns == s[c].txn_cap == len(merged[c].txns)
+    lv, order = eng.fetch_levels()
+    rlv, rorder = ref.levels()
+    assert np.array_equal(lv, rlv) and np.array_equal(order, rorder)
+    # the staged calls after the pipeline: ad_merge_deps on the pipeline's deps, then a plain preaccept + merge
+    eng.merge()
+    assert all(eng.fetch_merged(c).equal(merged[c]) for c in range(abi.NUM_CLASSES))
+    eng.preaccept_deps()
+    eng.merge()
+    assert all(eng.fetch_merged(c).equal(merged[c]) for c in range(abi.NUM_CLASSES))
+    assert eng.merged_sizes()[abi.CLASS_KEY].txns == s[abi.CLASS_KEY].txns
