@@ -337,17 +337,18 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     # drop the traffic figure again (round 3 mapped k_txn_finish to "<3>" while rocprof recorded "<3, false>")
     "k_deps_walk<fill>": "ad::k_deps_walk<3, true, false>", "k_deps_walk<count>": "ad::k_deps_walk<3, false, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
-    "k_gather_entries": "ad::k_gather_entries<true>", "k_txn_finish": "ad::k_txn_finish<3, false>",
+    "k_gather_entries": "ad::k_gather_entries<true>", "k_txn_finish": "ad::k_txn_finish<4, false, false>",
     "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<3>",
-    "k_seg_fuse": "ad::k_seg_fuse<3, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_ukeys"),
+    "k_seg_fuse": "ad::k_seg_fuse<4, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_ukeys"),
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
     # are shared fill/copy kernels and are not attributed)
     "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_step", "ad::k_chain_rank", "ad::k_chain_check",
                     "ad::k_chain_links", "ad::k_frontier_collect", "ad::k_kahn_small"),
-    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<3>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<3>, 1024, 4>",
-                     "ad::k_scan_apply<ad::OffsetsOp<3>, 256, 4>"),
-    "order_sort": ("ad::k_window_rank", "ad::k_rank_check"),
+    # (C2's pipeline computes 4 key classes: the 3 replies + the union view that is the merged Deps)
+    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<4>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<4>, 1024, 4>",
+                     "ad::k_scan_apply<ad::OffsetsOp<4>, 256, 4>"),
+    "order_sort": ("ad::k_window_rank", "ad::k_rank_check", "ad::k_rank_check_hist"),
     # C4's virtual-item region (bare base names: every instantiation)
     "vitems": ("ad::k_vitems", "ad::k_vitems_fill", "ad::k_vitem_walk", "ad::k_large_sums", "ad::k_large_layout"),
     "k_range_deps": ("ad::k_range_deps",), "k_union_lds": ("ad::k_union_lds_views", "ad::k_union_lds_small",

@@ -93,6 +93,24 @@ static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64
     if (__ballot(bad) && __lane_id() == 0) atomicOr(&prm->err, (unsigned)ERR_EXECBELOW);
 }
 
+int side_fork(ad_handle* h) {
+    if (!h->xst) {
+        HIPCHK(h, hipStreamCreateWithFlags(&h->xst, hipStreamNonBlocking));
+        HIPCHK(h, hipEventCreateWithFlags(&h->xev0, hipEventDisableTiming));
+        HIPCHK(h, hipEventCreateWithFlags(&h->xev1, hipEventDisableTiming));
+    }
+    HIPCHK(h, hipEventRecord(h->xev0, h->st));
+    HIPCHK(h, hipStreamWaitEvent(h->xst, h->xev0, 0));
+    h->xjoin = true;
+    return AD_OK;
+}
+void side_join(ad_handle* h) {
+    if (!h->xjoin) return;
+    hipEventRecord(h->xev1, h->xst);
+    hipStreamWaitEvent(h->st, h->xev1, 0);
+    h->xjoin = false;
+}
+
 // Fills in the lone entries the deps stage's gather skipped (k_gather_entries<true>): called before anything
 // that reads every sorted entry (execution levels other than the pull pass, MaxConflicts, recovery, CFK retain,
 // sharded level passes).
@@ -116,6 +134,16 @@ int complete_entries(ad_handle* h) {
     return AD_OK;
 }
 
+// The key-class CSRs a deps stage computes: R replies (+ the union view, see stage_deps), keyDeps only or keyDeps
+// + directKeyDeps; stage_prepare asks too (k_pack clears that many count bytes per pair).
+int deps_class_plan(const ad_handle* h, bool want_union, bool* uni_out) {
+    const bool uni = want_union && h->Q == 0 && !h->accept && !h->sharded && !h->hist_active && h->n_large == 0 &&
+                     (int)h->cfg.replicas + 1 <= MAXV;
+    if (uni_out) *uni_out = uni;
+    const int nv = (int)h->cfg.replicas + (uni ? 1 : 0);
+    return h->n_special > 0 ? 2 * nv : nv;
+}
+
 int stage_deps(ad_handle* h) {
     StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
@@ -127,8 +155,8 @@ int stage_deps(ad_handle* h) {
     // virtual items: their joins are per real view).
     const bool want_u = h->want_union;
     h->want_union = false;                                // one stage call (the overflow re-run below re-arms it)
-    const bool uni = want_u && Q == 0 && !h->accept && !h->sharded && !h->hist_active && h->n_large == 0 &&
-                     (int)h->cfg.replicas + 1 <= MAXV;
+    bool uni = false;
+    deps_class_plan(h, want_u, &uni);
     h->deps_union = uni;
     const int nv = (int)h->cfg.replicas + (uni ? 1 : 0), nvc = 2 * nv;
     hipStream_t st = h->st;
@@ -229,8 +257,10 @@ int stage_deps(ad_handle* h) {
         f.P = P; f.ntiles = ntiles; f.skey = h->skey; f.prec = h->prec; f.overflow = fuse_over;
         CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 4 * ntiles + SF_PARTS));
         f.hpart = f.tile_cnt + 4 * ntiles;
-        fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0},
-                        {h->dfr, n, 0}});
+        const bool packed = h->cnt8_cleared == ncb_of(nc);   // k_pack cleared the count bytes and deferred flags
+        h->cnt8_cleared = 0;
+        fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0},
+                        {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0}, {packed ? nullptr : h->dfr, n, 0}});
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;
         { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
@@ -240,7 +270,10 @@ int stage_deps(ad_handle* h) {
         h->sf_ntiles = ntiles;
     } else {
         h->nh_valid = true;
-        fill_multi(st, {{fovf_count, 4, 0}, {dtx_count, 12, 0}, {h->cnt8, (size_t)ncb_of(nc) * P, 0}, {h->dfr, n, 0}});
+        const bool packed = h->cnt8_cleared == ncb_of(nc);
+        h->cnt8_cleared = 0;
+        fill_multi(st, {{fovf_count, 4, 0}, {dtx_count, 12, 0}, {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0},
+                        {packed ? nullptr : h->dfr, n, 0}});
         launch_walk_nv(nv, wa, false, direct, true, st);
     }
     TxnArgs ta{};
@@ -325,12 +358,15 @@ int stage_deps(ad_handle* h) {
         ta.spec_bad = spec_bad;
         KScope ks(K_TXN_LAYOUT, n);
         launch_finish_nv(nv, ta, direct, st);
+        CK(side_fork(h));
+        launch_finish_ovf_nv(nv, ta, direct, h->xst);
         ta.spec_bad = nullptr;
     }
     CK(wait_totals(h, seq, tt.count, got.data()));
     if (fuse && got[col_over] != 0) {
         // a key segment too long for a k_seg_fuse tile: this batch takes the three-kernel path (the speculative
         // finish, if any, exited or is redone there)
+        side_join(h);                                    // the speculative finish's side-stream rows
         HIPCHK(h, hipStreamSynchronize(st));
         h->seg_long = true;
         h->want_union = want_u;
@@ -379,7 +415,12 @@ int stage_deps(ad_handle* h) {
     const bool spec_ok = spec && got[col_over + 1] == 0;
     h->times.deps_speculative = spec ? (spec_ok ? 1u : 2u) : 0u;
     ta.w = wa;
-    if (n > 0 && !spec_ok) { KScope ks(K_TXN_LAYOUT, n); launch_finish_nv(nv, ta, direct, st); }
+    if (n > 0 && !spec_ok) {
+        KScope ks(K_TXN_LAYOUT, n);
+        launch_finish_nv(nv, ta, direct, st);
+        CK(side_fork(h));
+        launch_finish_ovf_nv(nv, ta, direct, h->xst);
+    }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
     wa.items = items; wa.nitems = nitems;
     launch_walk_nv(nv, wa, true, direct, nitems > 0, st);
@@ -434,6 +475,7 @@ int stage_deps(ad_handle* h) {
     // Virtual-item work arrays are dead once the CSRs are filled; they stay allocated for the next batch
     // (re-allocating C4's ~90 GB of them every batch cost more than the walks) unless the merge runs out of
     // HBM, when release_dead gives them back (STAGE_MERGE).
+    if (!h->xdefer) side_join(h);
     h->have_deps = true;
     h->ls.chains_ready = false;
     h->times.deps_entries = h->deps_entries;

@@ -33,9 +33,8 @@ void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
         if (wide) k_txn_finish<NV, false, true><<<g, 256, 0, st>>>(ta);
         else k_txn_finish<NV, false, false><<<g, 256, 0, st>>>(ta);
     }
-    const unsigned go = std::min(g, 16384u);             // the overflowed rows (a device-side count)
-    if (direct) k_txn_finish_ovf<NV, true><<<go, 256, 0, st>>>(ta);
-    else k_txn_finish_ovf<NV, false><<<go, 256, 0, st>>>(ta);
+    // the overflowed rows (a device-side count: rare, so a small grid — 16K idle workgroups cost 27 us)
+
 }
 
 template <int NV>
@@ -61,6 +60,15 @@ void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32
     NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy, dtx, dtx_count);
 }
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_finish, ta, direct, st); }
+// The overflowed rows (a device-side count: rare, so a small grid; each row is a chain of dependent loads — ~27 us
+// of latency for a handful of rows on C2 — which is why it runs on the side stream)
+template <int NV>
+void launch_finish_ovf(const TxnArgs& ta, bool direct, hipStream_t st) {
+    const unsigned g = (unsigned)std::min<long>(ceil_div((long)ta.nrows * (direct ? 2 * NV : NV), 256), 256);
+    if (direct) k_txn_finish_ovf<NV, true><<<g, 256, 0, st>>>(ta);
+    else k_txn_finish_ovf<NV, false><<<g, 256, 0, st>>>(ta);
+}
+void launch_finish_ovf_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_finish_ovf, ta, direct, st); }
 void launch_large_sums_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_large_sums, ta, direct, st); }
 void launch_large_layout_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_large_layout, ta, direct, st); }
 void launch_union_nv(int nv, const UnionArgs& ua, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_union, ua, direct, st); }

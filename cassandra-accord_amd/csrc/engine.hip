@@ -240,10 +240,15 @@ int stage_prepare(ad_handle* h) {
     h->rbase = Q ? p.rs_min : 0;
     h->wmax = Q ? p.rw_max : 0;
     h->range_bits = Q ? bits_of(p.re_max - p.rs_min) : 0;    // > 32: each endpoint sorted in two 32-bit halves
+    // the deps stage's count bytes (ncb per pair) and deferred flags are cleared here, in pair / txn order, instead of
+    // by a fill launch of their own
+    const int ncb = ncb_of(deps_class_plan(h, h->want_union, nullptr));
+    h->cnt8_cleared = ncb;
     KScope ks(K_PACK, n);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
-                                                    h->range_e, h->tx_ts, h->ex1, h->meta, h->prec, h->ka, h->va, h->prm);
+                                                    h->range_e, h->tx_ts, h->ex1, h->meta, h->prec, h->ka, h->va, h->prm,
+                                                    (uint32_t*)h->cnt8, ncb / 4, h->dfr);
     return AD_OK;
 }
 
@@ -482,6 +487,9 @@ void ad_close(ad_handle* h) {
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->st) hipStreamSynchronize(h->st);
     if (h->cst) { hipStreamSynchronize(h->cst); hipStreamDestroy(h->cst); }
+    if (h->xst) { hipStreamSynchronize(h->xst); hipStreamDestroy(h->xst); }
+    if (h->xev0) hipEventDestroy(h->xev0);
+    if (h->xev1) hipEventDestroy(h->xev1);
     if (h->cev) hipEventDestroy(h->cev);
     if (h->sev) hipEventDestroy(h->sev);
     if (h->pub_host) hipHostFree(h->pub_host);
@@ -1342,17 +1350,24 @@ int ad_run_pipeline(ad_handle* h) {
     hipSetDevice(h->device);
     hipStream_t st = h->st;
     HIPCHK(h, hipEventRecord(h->ev[0], st));
+    h->want_union = true;                        // the merged Deps as the deps stage's union view (stage_deps)
     CK(stage_prepare(h));
     HIPCHK(h, hipEventRecord(h->ev[1], st));
     CK(stage_sort(h));
     HIPCHK(h, hipEventRecord(h->ev[2], st));
-    h->want_union = true;                        // the merged Deps as the deps stage's union view (stage_deps)
-    CK(stage_deps(h));
+    h->xdefer = true;                            // k_txn_finish_ovf's side stream joins where its rows are read
+    const int rc_deps = stage_deps(h);
+    h->xdefer = false;
+    CK(rc_deps);
     HIPCHK(h, hipEventRecord(h->ev[3], st));
-    CK(stage_merge(h));
-    h->merged_has_range = h->Q > 0;
-    HIPCHK(h, hipEventRecord(h->ev[4], st));
-    CK(stage_levels(h, true));
+    int rc = stage_merge(h);
+    if (rc == AD_OK) {
+        h->merged_has_range = h->Q > 0;
+        HIPCHK(h, hipEventRecord(h->ev[4], st));
+        rc = stage_levels(h, true);
+    }
+    side_join(h);                                // also on an error: nothing may read the CSRs before the side rows
+    CK(rc);
     HIPCHK(h, hipEventRecord(h->ev[5], st));
     CK(spin_event(h, h->ev[5]));
     if (order_failed(h)) {                       // optimistic order failed its check: general path, timed in

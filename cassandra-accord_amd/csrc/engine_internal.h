@@ -180,6 +180,7 @@ struct ad_handle {
     bool have_deps = false, have_merged = false, have_levels = false, merged_has_range = false;
     bool entries_partial = false;    // the deps stage skipped the lone entries' gather (complete_entries)
     bool seg_long = false;           // the loaded batch has a key segment too long for k_seg_fuse's tiles
+    int cnt8_cleared = 0;            // count bytes per pair k_pack cleared for the next deps stage (0: none)
     bool want_union = false;         // ad_run_pipeline: the deps stage also builds the union view (the merged Deps)
     bool deps_union = false;         // the last deps stage did: deps[2R], deps[2R + 1] are the merged key classes
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
@@ -193,6 +194,10 @@ struct ad_handle {
     bool bound_max = false;          // ... with bound = Timestamp.MAX (ad_ephemeral_read_deps)
     // ad_load_batch_async: the next batch's inputs on a copy stream into the staging slots
     hipStream_t cst = nullptr;
+    hipStream_t xst = nullptr;       // side stream: k_txn_finish_ovf's latency-bound rows, overlapped with later stages
+    hipEvent_t xev0 = nullptr, xev1 = nullptr;
+    bool xjoin = false;              // work queued on xst that the main stream has not waited for
+    bool xdefer = false;             // ad_run_pipeline: stage_deps leaves the join to the stages that read its CSRs
     hipEvent_t cev = nullptr, sev = nullptr;
     bool stage_pending = false;
     size_t stg_n = 0, stg_p = 0, stg_q = 0;
@@ -394,6 +399,7 @@ int stage_sort(ad_handle* h);
 RadixScratch radix_scratch(ad_handle* h, size_t n);
 int stage_deps(ad_handle* h);
 int complete_entries(ad_handle* h);
+int deps_class_plan(const ad_handle* h, bool want_union, bool* uni_out);
 int stage_merge(ad_handle* h);
 int stage_levels(ad_handle* h, bool want_order);
 int finish_order(ad_handle* h);
@@ -415,6 +421,10 @@ void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st);
 // deps_layout.hip: per-txn offsets / layout / unions of the computed key classes
 void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count);
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
+void launch_finish_ovf_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
+// k_txn_finish_ovf on the side stream xst (forked after the finish; joined before anything reads the deps CSRs)
+int side_fork(ad_handle* h);
+void side_join(ad_handle* h);
 void launch_large_sums_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_large_layout_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_union_nv(int nv, const UnionArgs& ua, bool direct, hipStream_t st);

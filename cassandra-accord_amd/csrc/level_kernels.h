@@ -667,7 +667,7 @@ __device__ inline void chain_build_seg(size_t P, size_t s2, const int32_t* __res
 // batches whose deps stage ran k_seg_fuse, which builds no list): each workgroup covers CB_SPAN sorted positions and
 // first compacts its segments' second entries into LDS, so the builders run on full waves (one thread per position
 // left ~85 % of the lanes of this latency-bound kernel idle: 41 -> 115 us on C2)
-constexpr int CB_SPAN = 1024;
+constexpr int CB_SPAN = 1536;             // ~230 builders per workgroup of 256 on C2
 static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint32_t* __restrict__ nh, const Params* __restrict__ prm,
                                                      const int32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,

@@ -67,7 +67,10 @@ int stage_levels(ad_handle* h, bool want_order) {
     const bool pull_first = li.kahn_ok && !li.force_blocks && h->P > 0 && !h->ls.pull_off && h->n_large == 0 &&
                             h->n_special == 0 && h->merged[AD_CLASS_DIRECT_KEY].ncap == 0 &&
                             !(h->merged_has_range && h->merged[AD_CLASS_RANGE].ncap > 0);
-    if (!pull_first) CK(complete_entries(h));
+    if (!pull_first) {
+        side_join(h);                                     // the other level paths read the merged Deps
+        CK(complete_entries(h));
+    }
     li.complete = [](void* x) { return complete_entries((ad_handle*)x); };
     li.complete_ctx = h;
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);

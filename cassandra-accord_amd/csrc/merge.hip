@@ -173,6 +173,7 @@ int stage_merge(ad_handle* h) {
         h->have_merged = true;
         return AD_OK;
     }
+    side_join(h);                                       // the merge reads every reply's CSRs
     const Csr* parts[3][MAXV] = {};
     for (int v = 0; v < nv; ++v) {
         parts[0][v] = &h->deps[2 * v];

@@ -75,6 +75,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     __shared__ uint32_t s_key[SF_CAP + 1];
     __shared__ uint32_t s_txn[SF_CAP];
     __shared__ uint8_t s_meta[SF_CAP];
+    __shared__ uint8_t s_eq[SF_CAP];             // the entry's executeAt == TxnId (PREC_EXEQ)
     __shared__ uint64_t s_ex1[SF_CAP];
     __shared__ int32_t s_ss[SF_CAP];
     __shared__ int32_t s_ud[SF_CAP];
@@ -126,10 +127,14 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     atomicAdd(&s_cnt[1], nonheads);
     __syncthreads();
     const uint32_t ng = s_cnt[2], nq = s_cnt[3];
-    for (uint32_t x = tid; x < ng; x += SF_T) {
+    // list slots dealt round-robin over the waves (slot = lane * waves + wave): a tile's ~90 gathers / ~47 queries
+    // then keep every wave busy with a quarter of them instead of one wave walking all of them (its chain of
+    // dependent loads set the tile's time while the others sat finished, holding the workgroup's LDS)
+    const uint32_t rr = (uint32_t)(__lane_id() * (SF_T / WAVE) + wv);
+    for (uint32_t x = rr; x < ng; x += SF_T) {
         const uint32_t i = s_glist[x];
         const PairRec r = f.prec[w.sval[lo + i]];
-        s_txn[i] = r.txn; s_meta[i] = (uint8_t)r.meta; s_ex1[i] = r.ex1;
+        s_txn[i] = r.txn; s_meta[i] = (uint8_t)r.meta; s_ex1[i] = r.ex1; s_eq[i] = (r.meta & PREC_EXEQ) ? 1 : 0;
         f.e_txn[lo + i] = r.txn; f.e_meta[lo + i] = (uint8_t)r.meta; f.e_exec1[lo + i] = r.ex1;
     }
     __syncthreads();
@@ -153,7 +158,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         }
     }
     __syncthreads();
-    for (uint32_t x = tid; x < ng; x += SF_T) {
+    for (uint32_t x = rr; x < ng; x += SF_T) {
         const uint32_t i = s_glist[x];
         f.seg_start[lo + i] = s_ss[i]; f.ud_prev[lo + i] = s_ud[i]; f.pm_w[lo + i] = s_pw[i]; f.pm_c[lo + i] = s_pc[i];
     }
@@ -165,7 +170,11 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     WalkArgs a = w;
     a.e_txn = s_txn - lo; a.e_meta = s_meta - lo; a.e_exec1 = s_ex1 - lo; a.seg_start = s_ss - lo; a.ud_prev = s_ud - lo;
     a.pm_w = s_pw - lo; a.pm_c = s_pc - lo;
-    for (uint32_t x = tid; x < nq; x += SF_T) walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + s_qlist[x]);
+    // (the PreAccept bound TxnId + 1 from the record when executeAt == TxnId: no random tx_ts read for ~90 % of them)
+    for (uint32_t x = rr; x < nq; x += SF_T) {
+        const uint32_t q = s_qlist[x];
+        walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + q, s_eq[q] ? s_ex1[q] : 0ull);
+    }
 }
 
 // n_keys_u = the tiles' heads (after k_seg_fuse; nothing after an overflow: the host re-runs the batch)
