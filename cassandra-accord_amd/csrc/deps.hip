@@ -181,6 +181,7 @@ int stage_deps(ad_handle* h) {
     // (seg_fuse_kernels.h); its overflow flag comes back with the totals, and an overflowing batch re-runs here on
     // the three-kernel path
     const bool fuse = skip && !h->seg_long;
+    const uint32_t* fuse_hpart = nullptr;
     h->keys_partial = false;
     uint32_t* fuse_over = h->totd + MAX_TOTALS - 6;      // (MAX_TOTALS - 5: the merge's speculation guard)
     if (P > 0 && !fuse) {
@@ -264,7 +265,7 @@ int stage_deps(ad_handle* h) {
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;
         { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
-        k_seg_heads<<<1, SF_PARTS, 0, st>>>(f.hpart, h->prm, fuse_over);
+        fuse_hpart = f.hpart;              // n_keys_u: summed by the deps publish (PubExtra)
         h->nh_valid = false;               // no dense non-head list: the level chain build runs over every position
         h->keys_partial = true;            // ukey / useg on demand (complete_entries)
         h->sf_ntiles = ntiles;
@@ -345,14 +346,19 @@ int stage_deps(ad_handle* h) {
         ta.out_txns[k] = (uint32_t*)h->bufs[base + 6].p;
     }
     ta.inl = h->inl; ta.dfr = h->dfr; ta.nrows = n;
+    // the publish also evaluates the speculative finish's capacity guard (k_cap_check's rule) and sums the fused
+    // kernel's head counts into n_keys_u (k_seg_heads): one launch
+    PubExtra pex{};
     if (spec) {
         capc.bad = spec_bad;
-        k_cap_check<<<1, 64, 0, st>>>(capc);
+        pex.cap = capc;
         tt.src[tt.count++] = spec_bad;
     }
+    pex.hpart = fuse_hpart; pex.nparts = SF_PARTS; pex.prm = h->prm;
     std::vector<uint32_t> got(tt.count, 0);
     uint32_t seq = 0;
-    CK(publish_totals(h, tt, got.data(), &seq));       // the read-back first, then the speculative finish
+    host_mark(h, "deps publish");
+    CK(publish_totals(h, tt, got.data(), &seq, &pex));  // the read-back first, then the speculative finish
     if (spec) {
         ta.w = wa;
         ta.spec_bad = spec_bad;
@@ -363,6 +369,7 @@ int stage_deps(ad_handle* h) {
         ta.spec_bad = nullptr;
     }
     CK(wait_totals(h, seq, tt.count, got.data()));
+    host_mark(h, "deps waited");
     if (fuse && got[col_over] != 0) {
         // a key segment too long for a k_seg_fuse tile: this batch takes the three-kernel path (the speculative
         // finish, if any, exited or is redone there)
@@ -400,6 +407,7 @@ int stage_deps(ad_handle* h) {
             ra.key_off_v[v] = x.key_off; ra.k2t_off_v[v] = x.k2t_off; ra.keys_v[v] = x.keys; ra.k2t_v[v] = x.k2t;
         }
     }
+    host_mark(h, "deps alloc");
     // ---- fill
     ta.inl = h->inl; ta.dfr = h->dfr;
     UnionArgs ua{};
@@ -475,6 +483,7 @@ int stage_deps(ad_handle* h) {
     // Virtual-item work arrays are dead once the CSRs are filled; they stay allocated for the next batch
     // (re-allocating C4's ~90 GB of them every batch cost more than the walks) unless the merge runs out of
     // HBM, when release_dead gives them back (STAGE_MERGE).
+    host_mark(h, "deps deps_end");
     if (!h->xdefer) side_join(h);
     h->have_deps = true;
     h->ls.chains_ready = false;

@@ -146,7 +146,10 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
 }
 
 // second level of k_minmax: one block folds the per-block partials into Params (no contended atomics)
-static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out) {
+// pub_flag != null: also publishes the Params to the host-mapped words (pub_prm) and releases seq into *pub_flag, as
+// k_publish would in a launch of its own (engine.hip publish_totals)
+static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out,
+                                                       uint32_t* pub_flag = nullptr, uint32_t* pub_prm = nullptr, uint32_t seq = 0) {
     constexpr int NF = 15, NSUM = 12, NOR = 14;
     __shared__ unsigned long long red[4][NF];
     unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -193,6 +196,16 @@ static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const uns
         }
     }
     if (threadIdx.x == 0) { out->err = 0; out->n_keys_u = 0; out->n_vitems = 0; }
+    if (pub_flag) {
+        __syncthreads();
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(out);
+        for (int x = threadIdx.x; x < (int)(sizeof(Params) / 4); x += blockDim.x) pub_prm[x] = pw[x];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(pub_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // Packs timestamps, builds per-txn meta, the sort input and validates footprints.  A wave owns 64 consecutive txns:
@@ -950,6 +963,14 @@ struct CapCheck {
     uint32_t cap[3 * NVC_MAX];
     int m;
     uint32_t* bad;
+};
+// What a publish does before it copies the totals (engine.hip k_publish): the speculative finish's capacity guard
+// (k_cap_check's rule) and k_seg_fuse's head count (k_seg_heads' sum into n_keys_u) — one launch instead of three
+struct PubExtra {
+    CapCheck cap;                 // cap.bad == null: none
+    const uint32_t* hpart;        // null: none
+    int nparts;
+    Params* prm;
 };
 static __global__ __launch_bounds__(64) void k_cap_check(CapCheck a) {
     const int l = threadIdx.x;

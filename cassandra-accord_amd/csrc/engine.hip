@@ -105,8 +105,24 @@ static __global__ void k_collect_totals(TotTable t, uint32_t* out) {
     const int i = threadIdx.x;
     if (i < t.count) out[i] = *t.src[i];
 }
-static __global__ __launch_bounds__(128) void k_publish(TotTable t, const Params* __restrict__ prm, uint32_t* pub, uint32_t seq) {
+static __global__ __launch_bounds__(128) void k_publish(TotTable t, const Params* __restrict__ prm, uint32_t* pub, uint32_t seq,
+                                                        PubExtra ex) {
     const int i = threadIdx.x;
+    if (ex.cap.bad || ex.hpart) {
+        if (ex.cap.bad && i < WAVE) {
+            const bool over = i < ex.cap.m && *ex.cap.tot[i] > ex.cap.cap[i];
+            const uint64_t m = __ballot(over);
+            if (i == 0) *ex.cap.bad = m ? 1u : 0u;
+        }
+        if (ex.hpart && i >= WAVE && i < 2 * WAVE) {
+            uint32_t v = 0;
+            for (int x = i - WAVE; x < ex.nparts; x += WAVE) v += ex.hpart[x];
+#pragma unroll
+            for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if (i == WAVE) ex.prm->n_keys_u = v;
+        }
+        __syncthreads();
+    }
     if (i < t.count) pub[PUB_TOT + i] = *t.src[i];
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(prm);
     for (int w = i; w < (int)(sizeof(Params) / 4); w += blockDim.x) pub[PUB_PRM + w] = pw[w];
@@ -136,8 +152,10 @@ static int pub_ready(ad_handle* h) {
 }
 // Two halves so work can be enqueued between the publish and the wait (the speculative finish / merge write):
 // publish_totals enqueues the read-back, wait_totals spins on it.
-int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* seq_out) {
+int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* seq_out, const PubExtra* ex) {
     if (pub_ready(h) != AD_OK) {        // no mapped memory: copy (the wait is a stream sync)
+        if (ex && ex->cap.bad) k_cap_check<<<1, 64, 0, h->st>>>(ex->cap);
+        if (ex && ex->hpart) k_seg_heads<<<1, SF_PARTS, 0, h->st>>>(ex->hpart, ex->prm, nullptr);
         if (t.count > 0) {
             k_collect_totals<<<1, MAX_TOTALS, 0, h->st>>>(t, h->totd);
             HIPCHK(h, hipMemcpyAsync(host, h->totd, (size_t)t.count * 4, hipMemcpyDeviceToHost, h->st));
@@ -147,7 +165,7 @@ int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* se
         return AD_OK;
     }
     const uint32_t seq = ++h->pub_seq;
-    k_publish<<<1, 128, 0, h->st>>>(t, h->prm, h->pub_dev, seq);
+    k_publish<<<1, 128, 0, h->st>>>(t, h->prm, h->pub_dev, seq, ex ? *ex : PubExtra{});
     HIPCHK(h, hipGetLastError());
     *seq_out = seq;
     return AD_OK;
@@ -220,9 +238,16 @@ int stage_prepare(ad_handle* h) {
         KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
         k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_s, h->range_e, Q, partial);
-        k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm);
+        if (pub_ready(h) == AD_OK) {
+            // the reduce publishes the Params itself: no k_publish launch between it and the host's read
+            const uint32_t seq = ++h->pub_seq;
+            k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm, h->pub_dev, h->pub_dev + PUB_PRM, seq);
+            CK(wait_totals(h, seq, 0, nullptr));
+        } else {
+            k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm);
+            CK(read_params(h));
+        }
     }
-    CK(read_params(h));
     const Params& p = h->hprm;
     if (n == 0) return AD_OK;
     int MB = bits_of(p.msb_max - p.msb_min), HB = bits_of(p.hlc_max - p.hlc_min), NB = bits_of((uint64_t)(p.node_max_b - p.node_min_b));
@@ -1349,23 +1374,30 @@ int ad_run_pipeline(ad_handle* h) {
     if (!h->loaded) return set_err(h, AD_ERR_STATE, "no batch loaded");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
+    h->ht.clear();
+    host_mark(h, "start");
     HIPCHK(h, hipEventRecord(h->ev[0], st));
     h->want_union = true;                        // the merged Deps as the deps stage's union view (stage_deps)
     CK(stage_prepare(h));
+    host_mark(h, "prepare returned");
     HIPCHK(h, hipEventRecord(h->ev[1], st));
     CK(stage_sort(h));
     HIPCHK(h, hipEventRecord(h->ev[2], st));
+    host_mark(h, "sort enqueued");
     h->xdefer = true;                            // k_txn_finish_ovf's side stream joins where its rows are read
     const int rc_deps = stage_deps(h);
     h->xdefer = false;
     CK(rc_deps);
     HIPCHK(h, hipEventRecord(h->ev[3], st));
+    host_mark(h, "deps returned");
     int rc = stage_merge(h);
+    host_mark(h, "merge returned");
     if (rc == AD_OK) {
         h->merged_has_range = h->Q > 0;
         HIPCHK(h, hipEventRecord(h->ev[4], st));
         rc = stage_levels(h, true);
     }
+    host_mark(h, "levels returned");
     side_join(h);                                // also on an error: nothing may read the CSRs before the side rows
     CK(rc);
     HIPCHK(h, hipEventRecord(h->ev[5], st));
@@ -1389,6 +1421,14 @@ int ad_run_pipeline(ad_handle* h) {
     h->times.level_edges = h->P;
     h->times.walk_items = (uint32_t)(h->P - (h->P ? h->hprm.n_keys_u : 0));
     h->tracer.resolve();
+    host_mark(h, "end");
+    if (h->host_timers == 1 && h->ht.size() > 1) {
+        std::string line = "host_timers";
+        for (size_t i = 1; i < h->ht.size(); ++i)
+            line += std::string(" | ") + h->ht[i].first + " " +
+                    std::to_string(std::chrono::duration<double, std::micro>(h->ht[i].second - h->ht[0].second).count());
+        fprintf(stderr, "%s\n", line.c_str());
+    }
     return AD_OK;
 }
 

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -59,6 +60,10 @@ struct ad_handle {
     ModelCfg cfg{};                  // replicas (ad_config) + the replica model (ad_replica_model)
     hipStream_t st = nullptr;
     std::string err;
+    // AD_HOST_TIMERS=1: host-side timestamps at marked points of ad_run_pipeline, printed to stderr per call
+    // (where the host, not the device, sets the pace: the launch gaps in the kernel trace)
+    int host_timers = -1;
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> ht;
     std::vector<DBuf> bufs;
     // loaded batch
     size_t n = 0, P = 0, Q = 0;
@@ -365,7 +370,7 @@ struct TotTable { const uint32_t* src[MAX_TOTALS]; int count; };
 void csr_offsets(ad_handle* h, Csr& c, const uint32_t* nk, const uint32_t* ne);
 // The [n] totals of several device offset arrays and the batch Params -> host (engine.hip: k_publish)
 int read_totals_params(ad_handle* h, const TotTable& t, uint32_t* host);
-int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* seq_out);
+int publish_totals(ad_handle* h, const TotTable& t, uint32_t* host, uint32_t* seq_out, const PubExtra* ex = nullptr);
 int wait_totals(ad_handle* h, uint32_t seq, int count, uint32_t* host);
 void set_level_pub(ad_handle* h);
 int read_params(ad_handle* h);
@@ -385,6 +390,11 @@ int check_params(ad_handle* h);
 
 // Capacity (elements) of CSR block `block`'s data buffers as currently allocated (0 if none).
 size_t csr_cap(ad_handle* h, size_t block, int which, size_t elem);
+
+inline void host_mark(ad_handle* h, const char* what) {
+    if (h->host_timers < 0) { const char* e = getenv("AD_HOST_TIMERS"); h->host_timers = (e && *e == '1') ? 1 : 0; }
+    if (h->host_timers) h->ht.emplace_back(what, std::chrono::steady_clock::now());
+}
 
 struct StageScope {
     ad_handle* h;

@@ -1684,9 +1684,10 @@ static __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, cons
 // so no host sync is needed here): the fast path's verification failure is then stored by k_rank_check into
 // *verify_dev (a host-mapped word the caller zeroed; a device-to-pageable copy here would stall the stream for
 // a host round trip), and the caller, after its own stream sync, reruns order_rows with known_maxl = -1 if set.
+// prefilled: the caller's earlier fill already cleared ls.flags[8..9] and set ls.sv0 to the sentinel (the pull path)
 inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
                        uint32_t exec_bits, uint32_t* order_out, hipStream_t st, int known_maxl = -1,
-                       uint32_t* verify_dev = nullptr) {
+                       uint32_t* verify_dev = nullptr, bool prefilled = false) {
     KScope ks(K_ORDER, m);
     RadixScratch rs;
     const size_t hl = radix_hist_len(m);
@@ -1700,7 +1701,7 @@ inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     const bool optimistic = known_maxl >= 0 && verify_dev != nullptr;
     uint32_t fl[2] = {0, 0};
     // fast path: windowed inversion ranks + verification
-    fill_multi(st, {{of, 8, 0}, {v, m * 4, 0xFF}});           // flags; WR_EMPTY: detects rank collisions
+    if (!prefilled) fill_multi(st, {{of, 8, 0}, {v, m * 4, 0xFF}});   // flags; WR_EMPTY: detects rank collisions
     k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1);
     if (optimistic && known_maxl > 0 && known_maxl <= 255) {
         // one stable pass by level whose histogram kernel is also the check, written straight into order_out
@@ -1916,8 +1917,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // flags; levels (unless given); the pull path's predecessor runs (zero: none) for pure key batches
         const bool pull_try = in.kahn_ok && !in.keep_levels && P > 0 && !ls.pull_off && in.n_large == 0 && in.n_special == 0 &&
                               !(in.merged_direct && in.merged_direct->ncap > 0) && !(in.merged_range && in.merged_range->ncap > 0);
+        // (and the pull path's order: its collision sentinel, order_rows prefilled)
         fill_multi(st, {{ls.flags, 128, 0}, {in.keep_levels ? nullptr : in.lvl, std::max<size_t>(n, 1) * 4, 0},
-                        {pull_try ? ls.succ : nullptr, P * 8, 0}});
+                        {pull_try ? ls.succ : nullptr, P * 8, 0}, {pull_try ? ls.sv0 : nullptr, n * 4, 0xFF}});
         // local-only txns are key-domain specials (n_special): a pull batch has none
         if (n > 0 && !pull_try) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
     }
@@ -2026,7 +2028,8 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 bool spec_order = false;
                 const std::function<void()> spec = [&]() {
                     if (want_order && n > 0 && in.order_verify) {
-                        *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, 255, in.order_verify);
+                        *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, 255, in.order_verify,
+                                                       true);
                         spec_order = true;
                     }
                 };

@@ -73,6 +73,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     }
     li.complete = [](void* x) { return complete_entries((ad_handle*)x); };
     li.complete_ctx = h;
+    host_mark(h, "levels enqueue");
     int rc = run_levels(h->ls, li, want_order, h->st, &iters, h->err);
     if (rc != AD_OK) return rc;
     h->level_iters = (uint32_t)iters;
