@@ -66,13 +66,16 @@ struct BlCntOp {
 };
 // block of every chain position (blocks cut the entry prefix every bcap; a txn belongs to the block its
 // first entry falls in, so a block holds < bcap + max keys per txn entries)
+// (blk: the same block per chain position, kept for k_bl_records past the sort's ping-pong)
 static __global__ __launch_bounds__(256) void k_bl_chain_block(size_t P, const uint32_t* __restrict__ c_txn, const uint32_t* __restrict__ erank,
                                                         const uint32_t* __restrict__ epre, uint32_t bcap, uint32_t* __restrict__ bk,
-                                                        uint32_t* __restrict__ bv) {
+                                                        uint32_t* __restrict__ bv, uint32_t* __restrict__ blk) {
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P) return;
-    bk[q] = epre[erank[c_txn[q]]] / bcap;
+    const uint32_t b = epre[erank[c_txn[q]]] / bcap;
+    bk[q] = b;
     bv[q] = (uint32_t)q;
+    blk[q] = b;
 }
 // tb[b] = first executeAt rank of block b, boff[b] = first slot of block b (b = 0..B)
 static __global__ __launch_bounds__(256) void k_bl_bounds(uint32_t B, size_t n, size_t P, const uint32_t* __restrict__ epre, uint32_t bcap,
@@ -112,35 +115,45 @@ static __global__ __launch_bounds__(256) void k_bl_inverse(size_t P, const uint3
     const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < P) inv[sv[j]] = (uint32_t)j;
 }
-static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-                                                    const uint32_t* __restrict__ inv, const uint32_t* __restrict__ c_txn,
-                                                    const uint8_t* __restrict__ c_meta, const int32_t* __restrict__ seg_start,
-                                                    const uint32_t* __restrict__ erank, const uint32_t* __restrict__ epre, uint32_t bcap,
+// One thread per CHAIN position q (coalesced reads of the chain arrays and of q's neighbours), its record stored at
+// its block-sorted slot inv[q].  Along a key's chain the blocks never decrease (blocks are executeAt ranges) and the
+// block sort is stable, so the entry before q in its block is q - 1 exactly when blk[q - 1] == blk[q] and q is not
+// its key's first position (else q heads its key's run in the block); symmetrically for the last entry.  Walking the
+// block-sorted slots instead made ~10 dependent random reads per entry (seg_start / c_txn / erank / epre of q and of
+// both neighbours): 1.36 GB fetched per C3 launch for 4M entries.
+static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint32_t* __restrict__ blk, const uint32_t* __restrict__ inv,
+                                                    const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
+                                                    const int32_t* __restrict__ seg_start, const uint32_t* __restrict__ erank,
                                                     const uint32_t* __restrict__ tb, const uint32_t* __restrict__ boff,
                                                     uint64_t* __restrict__ rec, uint32_t* __restrict__ bad) {
-    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool b_ = false;
-    if (j < P) {
-        const uint32_t b = sk[j], q = sv[j];
+    if (q < P) {
+        const uint32_t b = blk[q];
         const uint32_t key = (uint32_t)seg_start[q];
-        const bool head = j == 0 || sk[j - 1] != b || (uint32_t)seg_start[sv[j - 1]] != key;
-        const bool last = j + 1 == P || sk[j + 1] != b || (uint32_t)seg_start[sv[j + 1]] != key;
+        const uint32_t j = inv[q];
+        const bool first_of_key = q == key;
+        const bool next_same_key = q + 1 < P && (uint32_t)seg_start[q + 1] == key;
+        const uint32_t bprev = first_of_key ? 0u : blk[q - 1];
+        const uint32_t bnext = next_same_key ? blk[q + 1] : 0u;
+        const bool head = first_of_key || bprev != b;
+        const bool last = !next_same_key || bnext != b;
         const uint32_t tl = erank[c_txn[q]] - tb[b];
         b_ = tl > BL_TL || j - boff[b] >= (uint32_t)BL_CAP;
         uint64_t fl = (uint64_t)(tl & BL_TL) | ((uint64_t)(meta_kind(c_meta[q]) == AD_KIND_WRITE) << BL_SH_W) |
                       ((uint64_t)head << BL_SH_HEAD) | ((uint64_t)last << BL_SH_LAST);
-        if (last && q + 1 < P && (uint32_t)seg_start[q + 1] == key)
-            fl |= 1ull << (bl_block_of(q + 1, c_txn, erank, epre, bcap) >= b + 3 ? BL_SH_G : BL_SH_R);
-        if (head && q != key) {                                   // the key's previous run
-            const uint32_t pb = bl_block_of(q - 1, c_txn, erank, epre, bcap);
-            if (b - pb <= 2) {
-                const uint32_t ps = inv[q - 1] - boff[pb];
-                fl |= (1ull << BL_SH_SRC) | ((uint64_t)((pb % 3) * BL_CAP + ps) << BL_SH_RING);
+        if (last && next_same_key) fl |= 1ull << (bnext >= b + 3 ? BL_SH_G : BL_SH_R);
+        uint32_t lo = 0;
+        if (head && !first_of_key) {                                // the key's previous run
+            if (b - bprev <= 2) {
+                const uint32_t ps = inv[q - 1] - boff[bprev];
+                fl |= (1ull << BL_SH_SRC) | ((uint64_t)((bprev % 3) * BL_CAP + ps) << BL_SH_RING);
             } else {
                 fl |= 2ull << BL_SH_SRC;
+                lo = inv[q - 1];
             }
         }
-        rec[j] = (uint64_t)(((fl >> BL_SH_SRC) & 3u) == 2u ? inv[q - 1] : 0u) | (fl << 32);
+        rec[j] = (uint64_t)lo | (fl << 32);
     }
     wave_set_flag(b_, bad);
 }

@@ -1813,7 +1813,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         }
         const uint32_t nb = etot / bcap + 1;
         bb.nblocks = nb;
-        k_bl_chain_block<<<gP, 256, 0, st>>>(P, ls.c_txn, bb.erank, bb.epre, bcap, bb.bk, bb.bv);
+        k_bl_chain_block<<<gP, 256, 0, st>>>(P, ls.c_txn, bb.erank, bb.epre, bcap, bb.bk, bb.bv, bb.lb);   // lb: free until compact
         RadixScratch rs;
         const size_t hl = radix_hist_len(P);
         rs.hist = bb.rs;
@@ -1825,8 +1825,8 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         k_bl_bounds<<<ceil_div((long)nb + 1, 256), 256, 0, st>>>(nb, n, P, bb.epre, bcap, sk, bb.tb, bb.boff);
         uint32_t* inv = sk == bb.bk ? bb.bk2 : bb.bk;         // the sort's free ping-pong buffer
         k_bl_inverse<<<gP, 256, 0, st>>>(P, sv, inv);
-        k_bl_records<<<gP, 256, 0, st>>>(P, sk, sv, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.epre, bcap, bb.tb,
-                                         bb.boff, bb.rec, bb.stats + BL_STAT_RECORDS_BAD);
+        k_bl_records<<<gP, 256, 0, st>>>(P, bb.lb, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.tb, bb.boff, bb.rec,
+                                         bb.stats + BL_STAT_RECORDS_BAD);
         k_bl_compact<<<nb, BL_T, 0, st>>>(nb, bb.boff, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt);
         // 4. the walk (packed scan words: 32-bit while every level fits 20 bits)
         // (no carry initialisation: a head reads a global carry only from a producer flagged to store it)
