@@ -55,8 +55,10 @@ class AdCfkEvents(C.Structure):
     """ad_cfk_events: CommandsForKey.update events for the resident store (ad_cfk_store_apply), grouped by key."""
     _fields_ = [("m", C.c_size_t), ("ev_off", _u32p), ("txn_msb", _u64p), ("txn_lsb", _u64p), ("txn_node", _i32p),
                 ("status", _u8p), ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p),
-                ("deps_off", _u32p), ("deps_msb", _u64p), ("deps_lsb", _u64p), ("deps_node", _i32p)]
+                ("deps_off", _u32p), ("deps_msb", _u64p), ("deps_lsb", _u64p), ("deps_node", _i32p), ("op", _u8p)]
 
+
+CFK_OP_UPDATE, CFK_OP_LOAD, CFK_OP_PRUNE, CFK_OP_LOADING = 0, 1, 2, 3      # AD_CFK_OP_*
 
 CFK_EVENT_FIELDS = (("ev_off", np.uint32), ("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),
                     ("status", np.uint8), ("exec_msb", np.uint64), ("exec_lsb", np.uint64), ("exec_node", np.int32),
@@ -72,6 +74,9 @@ def make_cfk_events(ev):
         a = keep[f]
         ct = {np.uint32: _u32p, np.uint64: _u64p, np.int32: _i32p, np.uint8: _u8p}[dt]
         setattr(s, f, a.ctypes.data_as(ct) if a.size else None)
+    if ev.get("op") is not None:                     # optional: AD_CFK_OP_* per event (NULL: every event an UPDATE)
+        keep["op"] = np.ascontiguousarray(ev["op"], np.uint8)
+        s.op = keep["op"].ctypes.data_as(_u8p) if keep["op"].size else None
     return s, keep
 
 

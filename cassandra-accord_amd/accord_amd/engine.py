@@ -70,6 +70,7 @@ def lib():
         L.ad_cfk_store_apply.argtypes = [vp, C.POINTER(abi.AdCfkEvents)]
         L.ad_cfk_store_notify.argtypes = [vp, vp, vp]
         L.ad_cfk_store_fetch.argtypes = [vp, C.c_uint32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 9
+        L.ad_cfk_store_pruning.argtypes = [vp, C.c_uint32, vp, vp, vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 5
         L.ad_preaccept_expiry.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
@@ -110,7 +111,7 @@ def lib():
 EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
@@ -344,6 +345,26 @@ class DepsEngine:
         for f in order:
             if f != "miss_off":
                 out[f] = out[f][:r if f != "missing" else tot.value]
+        return out
+
+    def cfk_store_pruning(self, key):
+        """One key's prunedBefore (msb, lsb, node) and loadingPruned table: dict of pruned_before, lp_msb/lsb/node,
+        lp_off, lp_rows (the witnesses that are rows, byId row indices)."""
+        n, tot = C.c_size_t(), C.c_size_t()
+        self._check(lib().ad_cfk_store_pruning(self.h, key, None, None, None, C.byref(n), C.byref(tot), *([None] * 5)),
+                    "ad_cfk_store_pruning")
+        L = n.value
+        pm, pl, pn = C.c_uint64(), C.c_uint64(), C.c_int32()
+        out = {"lp_msb": np.zeros(max(L, 1), np.uint64), "lp_lsb": np.zeros(max(L, 1), np.uint64),
+               "lp_node": np.zeros(max(L, 1), np.int32), "lp_off": np.zeros(L + 1, np.uint32),
+               "lp_rows": np.zeros(max(tot.value, 1), np.uint32)}
+        self._check(lib().ad_cfk_store_pruning(self.h, key, C.byref(pm), C.byref(pl), C.byref(pn), C.byref(n), C.byref(tot),
+                                               *(out[f].ctypes.data for f in ("lp_msb", "lp_lsb", "lp_node", "lp_off",
+                                                                             "lp_rows"))), "ad_cfk_store_pruning")
+        for f in ("lp_msb", "lp_lsb", "lp_node"):
+            out[f] = out[f][:L]
+        out["lp_rows"] = out["lp_rows"][:tot.value]
+        out["pruned_before"] = (pm.value, pl.value, pn.value)
         return out
 
     def cfk_update(self, gid, status, exec_msb=None, exec_lsb=None, exec_node=None):

@@ -17,6 +17,14 @@ int ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity) {
     CK(dalloc(h, S_CS0 + 6, &c.en, rows)); CK(dalloc(h, S_CS0 + 7, &c.st, rows)); CK(dalloc(h, S_CS0 + 8, &c.slot, rows));
     CK(dalloc(h, S_CS0 + 9, &c.bits, rows * c.words)); CK(dalloc(h, S_CS0 + 10, &c.out, rows));
     CK(dalloc(h, S_CS0 + 11, &c.pre, 2 * rows)); CK(dalloc(h, S_CS0 + 12, &c.flags, 4));
+    CK(dalloc(h, S_CS0 + 13, &c.pbm, c.K)); CK(dalloc(h, S_CS0 + 14, &c.pbl, c.K)); CK(dalloc(h, S_CS0 + 15, &c.pbn, c.K));
+    CK(dalloc(h, S_CS0 + 16, &c.lp_cnt, c.K)); CK(dalloc(h, S_CS0 + 17, &c.lpm, rows));
+    CK(dalloc(h, S_CS0 + 18, &c.lpl, rows)); CK(dalloc(h, S_CS0 + 19, &c.lpn, rows));
+    CK(dalloc(h, S_CS0 + 20, &c.lp_bits, rows * c.words));
+    HIPCHK(h, hipMemsetAsync(c.pbm, 0, (size_t)c.K * 8, h->st));
+    HIPCHK(h, hipMemsetAsync(c.pbl, 0, (size_t)c.K * 8, h->st));
+    HIPCHK(h, hipMemsetAsync(c.pbn, 0, (size_t)c.K * 4, h->st));
+    HIPCHK(h, hipMemsetAsync(c.lp_cnt, 0, (size_t)c.K * 4, h->st));
     HIPCHK(h, hipMemsetAsync(c.cnt, 0, (size_t)c.K * 4, h->st));
     HIPCHK(h, hipMemsetAsync(c.flags, 0, 16, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
@@ -40,6 +48,14 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
         return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: an event array is missing");
     for (size_t e = 0; e < m; ++e)
         if (ev->status[e] > AD_ST_INVALID) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: status out of range");
+    if (ev->op)
+        for (size_t e = 0; e < m; ++e) {
+            if (ev->op[e] > AD_CFK_OP_LOADING) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: op out of range");
+            if (ev->op[e] == AD_CFK_OP_PRUNE && ev->exec_node[e] < 0)
+                return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: a PRUNE event's interval (exec_node) is negative");
+            if (ev->op[e] == AD_CFK_OP_LOADING && ev->deps_off[e + 1] - ev->deps_off[e] > 1)
+                return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: a LOADING event names at most one witness");
+        }
     const size_t nd = ev->deps_off[m];
     if (nd && (!ev->deps_msb || !ev->deps_lsb || !ev->deps_node))
         return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: deps without arrays");
@@ -54,6 +70,11 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     CK(dalloc(h, S_CSE0 + 3, &etn, m)); CK(dalloc(h, S_CSE0 + 4, &est, m)); CK(dalloc(h, S_CSE0 + 5, &eem, m));
     CK(dalloc(h, S_CSE0 + 6, &eel, m)); CK(dalloc(h, S_CSE0 + 7, &een, m)); CK(dalloc(h, S_CSE0 + 8, &doff, m + 1));
     CK(dalloc(h, S_CSE0 + 9, &dtm, dn)); CK(dalloc(h, S_CSE0 + 10, &dtl, dn)); CK(dalloc(h, S_CSE0 + 11, &dtn, dn));
+    uint8_t* eop = nullptr;
+    if (ev->op) {
+        CK(dalloc(h, S_CSE0 + 12, &eop, m));
+        HIPCHK(h, hipMemcpyAsync(eop, ev->op, m, hipMemcpyHostToDevice, st));
+    }
     HIPCHK(h, hipMemcpyAsync(eo, ev->ev_off, (c.K + 1) * 4, hipMemcpyHostToDevice, st));
     HIPCHK(h, hipMemcpyAsync(etm, ev->txn_msb, m * 8, hipMemcpyHostToDevice, st));
     HIPCHK(h, hipMemcpyAsync(etl, ev->txn_lsb, m * 8, hipMemcpyHostToDevice, st));
@@ -74,6 +95,8 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     a.ev_off = eo; a.etm = etm; a.etl = etl; a.etn = etn; a.est = est; a.eem = eem; a.eel = eel; a.een = een;
     a.dep_off = doff; a.dtm = dtm; a.dtl = dtl; a.dtn = dtn;
     a.overflow = c.flags; a.bad = c.flags + 1;
+    a.pbm = c.pbm; a.pbl = c.pbl; a.pbn = c.pbn; a.lp_cnt = c.lp_cnt; a.lpm = c.lpm; a.lpl = c.lpl; a.lpn = c.lpn;
+    a.lp_bits = c.lp_bits; a.eop = eop;
     k_cfk_apply<<<c.K, CS_T, 0, st>>>(a);
     HIPCHK(h, hipGetLastError());
     uint32_t f[2] = {0, 0};
@@ -95,6 +118,7 @@ int ad_cfk_store_notify(ad_handle* h, uint32_t* rows, uint8_t* not_waiting) {
     a.K = c.K; a.row_off = nullptr; a.cnt = c.cnt; a.cap = c.cap; a.words = c.words; a.slot = c.slot; a.bits = c.bits;
     a.tm = c.tm; a.tl = c.tl; a.tn = c.tn; a.em = c.em; a.el = c.el; a.en = c.en; a.st = c.st;
     a.pre = c.pre; a.out = c.out; a.bad_order = c.flags + 2; a.bad_miss = c.flags + 3;
+    a.lp_cnt = c.lp_cnt; a.lpm = c.lpm; a.lpl = c.lpl; a.lpn = c.lpn; a.lp_bits = c.lp_bits;
     k_cfk_notify<<<c.K, NF_T, 0, st>>>(a);
     HIPCHK(h, hipGetLastError());
     if (rows) HIPCHK(h, hipMemcpyAsync(rows, c.cnt, (size_t)c.K * 4, hipMemcpyDeviceToHost, st));
@@ -158,5 +182,64 @@ int ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missing
     if (miss_off) miss_off[n] = (uint32_t)tot;
     *rows = n;
     if (missing_total) *missing_total = tot;
+    return AD_OK;
+}
+
+int ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint64_t* pruned_lsb, int32_t* pruned_node,
+                         size_t* loading, size_t* witness_total, uint64_t* lp_msb, uint64_t* lp_lsb, int32_t* lp_node,
+                         uint32_t* lp_off, uint32_t* lp_rows) {
+    if (!h || !loading) return AD_ERR_ARGUMENT;
+    auto& c = h->cs;
+    if (!c.K) return set_err(h, AD_ERR_STATE, "ad_cfk_store_pruning before ad_cfk_store_open");
+    if (key >= c.K) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_pruning: key out of range");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    uint32_t L = 0, n = 0;
+    uint64_t pm = 0, pl = 0;
+    int32_t pn = 0;
+    HIPCHK(h, hipMemcpyAsync(&L, c.lp_cnt + key, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(&n, c.cnt + key, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(&pm, c.pbm + key, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(&pl, c.pbl + key, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(&pn, c.pbn + key, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (pruned_msb) *pruned_msb = pm;
+    if (pruned_lsb) *pruned_lsb = pl;
+    if (pruned_node) *pruned_node = pn;
+    const size_t base = (size_t)key * c.cap;
+    std::vector<uint32_t> slot(n);
+    std::vector<uint64_t> bits((size_t)L * c.words);
+    if (n) HIPCHK(h, hipMemcpyAsync(slot.data(), c.slot + base, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    if (L) {
+        HIPCHK(h, hipMemcpyAsync(bits.data(), c.lp_bits + base * c.words, (size_t)L * c.words * 8, hipMemcpyDeviceToHost, st));
+        if (lp_msb) HIPCHK(h, hipMemcpyAsync(lp_msb, c.lpm + base, (size_t)L * 8, hipMemcpyDeviceToHost, st));
+        if (lp_lsb) HIPCHK(h, hipMemcpyAsync(lp_lsb, c.lpl + base, (size_t)L * 8, hipMemcpyDeviceToHost, st));
+        if (lp_node) HIPCHK(h, hipMemcpyAsync(lp_node, c.lpn + base, (size_t)L * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    std::vector<uint32_t> row_of(c.cap, 0xFFFFFFFFu);
+    for (uint32_t r = 0; r < n; ++r) {
+        if (slot[r] >= n) return set_err(h, AD_ERR_DEVICE, "ad_cfk_store_pruning: slot out of range");
+        row_of[slot[r]] = r;
+    }
+    size_t tot = 0;
+    std::vector<uint32_t> tmp;
+    for (uint32_t j = 0; j < L; ++j) {
+        tmp.clear();
+        const uint64_t* b = bits.data() + (size_t)j * c.words;
+        for (uint32_t w = 0; w < c.words; ++w)
+            for (uint64_t x = b[w]; x; x &= x - 1) {
+                const uint32_t s = w * 64 + (uint32_t)__builtin_ctzll(x);
+                if (s >= n) return set_err(h, AD_ERR_DEVICE, "ad_cfk_store_pruning: a witness bit beyond the rows");
+                tmp.push_back(row_of[s]);
+            }
+        std::sort(tmp.begin(), tmp.end());
+        if (lp_off) lp_off[j] = (uint32_t)tot;
+        if (lp_rows) std::copy(tmp.begin(), tmp.end(), lp_rows + tot);
+        tot += tmp.size();
+    }
+    if (lp_off) lp_off[L] = (uint32_t)tot;
+    *loading = L;
+    if (witness_total) *witness_total = tot;
     return AD_OK;
 }

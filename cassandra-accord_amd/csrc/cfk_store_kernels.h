@@ -14,6 +14,12 @@
 // built in LDS by the workgroup in one pass over the key's rows.
 // Events of one key are applied in order by its workgroup (the reference's per-key sequence of updates); keys run in
 // parallel.  The release rule then runs over these rows (k_cfk_notify with the bitmap reader, notify_kernels.h).
+// Pruning (local/cfk/Pruning.java): per key prunedBefore's TxnId and the loadingPruned table -- per entry a TxnId and its
+// witnessedBy as a bitmap over slots (a witness that is not a row of the key is never read: isWaitingOnPruned asks about
+// rows, addToMissingArrays skips rows).  A PRUNE event runs maybePrune / pruneBefore in the workgroup: the candidate
+// prune point from order statistics over the committed rows (no committedByExecuteAt array is kept), pruneBefore's
+// sequential byId scan with the merged missing() set in LDS, then the rows, their slots and every bitmap are compacted
+// (a removed row is Applied or invalidated, so no missing() bit names it).
 #pragma once
 #include "notify_kernels.h"
 
@@ -40,7 +46,20 @@ struct CfkStoreArgs {
     const int32_t* dtn;
     uint32_t* overflow;                       // a key ran out of rows
     uint32_t* bad;                            // an event's deps not strictly ascending
+    // pruning state
+    uint64_t *pbm, *pbl;                      // [K] prunedBefore's TxnId (TxnId.NONE: zeros)
+    int32_t* pbn;
+    uint32_t* lp_cnt;                         // [K] loadingPruned entries
+    uint64_t *lpm, *lpl;                      // [K * cap] their TxnIds
+    int32_t* lpn;
+    uint64_t* lp_bits;                        // [(K * cap) * words] their witnesses
+    const uint8_t* eop;                       // [m] event op (CS_OP_*; nullptr: every event an UPDATE)
 };
+// event ops (ad_cfk_events.op)
+constexpr uint32_t CS_OP_UPDATE = 0;         // CommandsForKey.update (or insertAdditionsOnly: status TRANSITIVELY_KNOWN)
+constexpr uint32_t CS_OP_LOAD = 1;           // CommandsForKey.updatePruned of a loaded pruned command
+constexpr uint32_t CS_OP_PRUNE = 2;          // maybePrune(exec_node = pruneInterval, exec_msb = minHlcDelta)
+constexpr uint32_t CS_OP_LOADING = 3;        // txn joins loadingPruned, witnessed by the event's deps
 
 __device__ inline bool cs_has_deps(uint32_t s) {            // InternalStatus.hasExecuteAtOrDeps
     return s == AD_ST_ACCEPTED || s == AD_ST_COMMITTED || s == AD_ST_STABLE || s == AD_ST_APPLIED;
@@ -90,14 +109,16 @@ __device__ inline uint32_t cs_find(const CfkStoreArgs& a, size_t base, uint32_t 
 }
 
 // Utils.addToMissingArrays (:97-172): txn `t` (slot ts) joins the missing set of every row that has deps, witnesses
-// it and whose depsKnownBefore is above it -- except t itself and `skip` (the command being updated).
+// it and whose depsKnownBefore is above it -- except t itself, `skip` (the command being updated) and the slots set in
+// `dont` (a loaded pruned TxnId's witnessedBy, Updating.java:351).
 __device__ inline void cs_add_missing(const CfkStoreArgs& a, size_t base, uint32_t n, const Ts3& t, uint32_t ts,
-                                      uint32_t skip_slot) {
+                                      uint32_t skip_slot, const uint64_t* dont = nullptr) {
     const uint32_t kt = cs_kind(t.lsb);
     for (uint32_t r = threadIdx.x; r < n; r += CS_T) {
         const size_t x = base + r;
         const uint32_t s = a.slot[x];
         if (s == ts || s == skip_slot || !cs_has_deps(a.st[x]) || !witnesses(cs_kind(a.tl[x]), kt)) continue;
+        if (dont && ((dont[s >> 6] >> (s & 63)) & 1ull)) continue;
         if (ts3_cmp(cs_dkb(a, x), t) > 0) {
             uint64_t* w = a.bits + ((size_t)(base + s)) * a.words + (ts >> 6);
             *w |= 1ull << (ts & 63);
@@ -128,6 +149,236 @@ __device__ inline uint32_t cs_insert(const CfkStoreArgs& a, size_t base, uint32_
     return s;
 }
 
+// ---- loadingPruned (Pruning.LoadingPruned, Pruning.java:50-114) ----------------------------------------------------
+// the entry of TxnId t in key's table, or -1 (TxnIds are unique in the table)
+__device__ inline int cs_lp_find(const CfkStoreArgs& a, uint32_t key, uint32_t L, const Ts3& t, int* s_j) {
+    if (threadIdx.x == 0) *s_j = -1;
+    __syncthreads();
+    const size_t lb = (size_t)key * a.cap;
+    for (uint32_t j = threadIdx.x; j < L; j += CS_T)
+        if (ts3_cmp(Ts3{a.lpm[lb + j], a.lpl[lb + j], a.lpn[lb + j]}, t) == 0) *s_j = (int)j;
+    __syncthreads();
+    const int j = *s_j;
+    __syncthreads();
+    return j;
+}
+// Pruning.loadPruned: t joins the table (or is found there) and slot `w` (if any) joins its witnesses; false: full
+__device__ inline bool cs_lp_add(const CfkStoreArgs& a, uint32_t key, uint32_t& L, const Ts3& t, uint32_t w, int* s_j) {
+    const size_t lb = (size_t)key * a.cap;
+    int j = cs_lp_find(a, key, L, t, s_j);
+    if (j < 0) {
+        if (L >= a.cap) return false;
+        j = (int)L++;
+        for (uint32_t q = threadIdx.x; q < a.words; q += CS_T) a.lp_bits[(lb + j) * a.words + q] = 0ull;
+        if (threadIdx.x == 0) { a.lpm[lb + j] = t.msb; a.lpl[lb + j] = t.lsb; a.lpn[lb + j] = t.node; }
+        __syncthreads();
+    }
+    if (w != 0xFFFFFFFFu && threadIdx.x == 0) a.lp_bits[(lb + j) * a.words + (w >> 6)] |= 1ull << (w & 63);
+    __syncthreads();
+    return true;
+}
+// Pruning.removeLoadingPruned: entry j leaves (the last entry takes its place)
+__device__ inline void cs_lp_remove(const CfkStoreArgs& a, uint32_t key, uint32_t& L, int j) {
+    const size_t lb = (size_t)key * a.cap;
+    const uint32_t last = L - 1;
+    if ((uint32_t)j != last) {
+        for (uint32_t q = threadIdx.x; q < a.words; q += CS_T)
+            a.lp_bits[(lb + j) * a.words + q] = a.lp_bits[(lb + last) * a.words + q];
+        if (threadIdx.x == 0) { a.lpm[lb + j] = a.lpm[lb + last]; a.lpl[lb + j] = a.lpl[lb + last]; a.lpn[lb + j] = a.lpn[lb + last]; }
+    }
+    --L;
+    __syncthreads();
+}
+
+// ---- maybePrune / pruneBefore (Pruning.java:164-331) --------------------------------------------------------------
+struct CsPruneLds {
+    Ts3 v[CS_T];
+    int h[CS_T];
+    uint32_t c[CS_T];
+    uint64_t merged[CS_MAX_WORDS];            // pruneBefore's mergedMissing (slot bitmap)
+    uint64_t gone[CS_MAX_WORDS];              // removed rows (byId index bitmap)
+    uint64_t dead[CS_MAX_WORDS];              // their slots
+    uint32_t gpc[CS_MAX_WORDS], dpc[CS_MAX_WORDS];   // exclusive prefix popcounts of gone / dead per word
+    uint64_t stage[CS_T / 64][CS_MAX_WORDS];  // one remapped bitmap row per wave
+    uint32_t idx;
+};
+__device__ inline uint64_t cs_hlc(const Ts3& t) { return ((t.msb & 0x7FFFull) << 48) | (t.lsb >> 16); }
+__device__ inline uint32_t cs_block_sum(uint32_t v, uint32_t* s_c) {
+    const int tid = threadIdx.x;
+    s_c[tid] = v;
+    __syncthreads();
+    for (int o = CS_T / 2; o > 0; o >>= 1) {
+        if (tid < o) s_c[tid] += s_c[tid + o];
+        __syncthreads();
+    }
+    const uint32_t r = s_c[0];
+    __syncthreads();
+    return r;
+}
+// bits below position i that are set in bitmap b (with its exclusive per-word prefix counts pc)
+__device__ inline uint32_t cs_rank(const uint64_t* b, const uint32_t* pc, uint32_t i) {
+    const uint64_t low = (i & 63) ? (b[i >> 6] & ((1ull << (i & 63)) - 1ull)) : 0ull;
+    return pc[i >> 6] + (uint32_t)__popcll(low);
+}
+// old slot row `src` of a bitmap -> its columns compacted (dead columns dropped) into stage (words), one wave
+__device__ inline void cs_remap_row(const CfkStoreArgs& a, const uint64_t* src, uint64_t* stage, const CsPruneLds& s,
+                                    int lane) {
+    for (uint32_t q = lane; q < a.words; q += 64) stage[q] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t q = lane; q < a.words; q += 64) {
+        uint64_t x = src[q] & ~s.dead[q];
+        while (x) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(x);
+            x &= x - 1;
+            const uint32_t o = q * 64 + b, ns = o - cs_rank(s.dead, s.dpc, o);
+            atomicOr((unsigned long long*)&stage[ns >> 6], 1ull << (ns & 63));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_t base, uint32_t& n, uint32_t L,
+                                      uint32_t interval, int64_t min_hlc_delta, CsPruneLds& s) {
+    const int tid = threadIdx.x;
+    // maxAppliedWriteByExecuteAt: the Applied Write executing last, and its index in committedByExecuteAt
+    Ts3 maw{0, 0, 0};
+    bool has = false;
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (a.st[x] == AD_ST_APPLIED && cs_kind(a.tl[x]) == AD_KIND_WRITE) {
+            const Ts3 e{a.em[x], a.el[x], a.en[x]};
+            if (!has || ts3_cmp(e, maw) > 0) { maw = e; has = true; }
+        }
+    }
+    nf_block_fold<true>(maw, has, s.v, s.h);
+    if (!has) return;
+    uint32_t below = 0;
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (cs_decided(a.st[x]) && ts3_cmp(Ts3{a.em[x], a.el[x], a.en[x]}, maw) < 0) ++below;
+    }
+    if (cs_block_sum(below, s.c) < interval) return;
+    // the prune point: the Applied Write executing last among those before maxAppliedWrite within minHlcDelta of it
+    const int64_t lim = (int64_t)cs_hlc(maw) - min_hlc_delta;
+    Ts3 pex{0, 0, 0};
+    bool hp = false;
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (a.st[x] == AD_ST_APPLIED && cs_kind(a.tl[x]) == AD_KIND_WRITE) {
+            const Ts3 e{a.em[x], a.el[x], a.en[x]};
+            if (ts3_cmp(e, maw) < 0 && (int64_t)cs_hlc(e) <= lim && (!hp || ts3_cmp(e, pex) > 0)) { pex = e; hp = true; }
+        }
+    }
+    nf_block_fold<true>(pex, hp, s.v, s.h);
+    if (!hp) return;
+    if (tid == 0) s.idx = n;
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (a.st[x] == AD_ST_APPLIED && cs_kind(a.tl[x]) == AD_KIND_WRITE &&
+            ts3_cmp(Ts3{a.em[x], a.el[x], a.en[x]}, pex) == 0) atomicMin(&s.idx, r);
+    }
+    __syncthreads();
+    const uint32_t p = s.idx;                                     // byId position of the new prunedBefore
+    __syncthreads();
+    if (p >= n) return;
+    const Ts3 pt{a.tm[base + p], a.tl[base + p], a.tn[base + p]};
+    if (ts3_cmp(pt, Ts3{a.pbm[key], a.pbl[key], a.pbn[key]}) <= 0 || p == 0) return;
+    // pruneBefore's byId scan below p
+    const uint64_t* pbits = a.bits + (base + a.slot[base + p]) * a.words;
+    for (uint32_t q = tid; q < a.words; q += CS_T) { s.merged[q] = pbits[q]; s.gone[q] = 0ull; s.dead[q] = 0ull; }
+    __syncthreads();
+    bool any = false;
+    for (uint32_t r = 0; r < p; ++r) {
+        const size_t x = base + r;
+        const uint32_t st = a.st[x];
+        bool rm = false;
+        if (st == AD_ST_INVALID) {
+            rm = true;
+        } else if (st == AD_ST_APPLIED) {
+            const Ts3 e{a.em[x], a.el[x], a.en[x]};
+            if (ts3_cmp(e, pex) < 0) {
+                const uint64_t* b = a.bits + (base + a.slot[x]) * a.words;
+                bool extra = false;
+                for (uint32_t q = tid; q < a.words; q += CS_T) extra |= (b[q] & ~s.merged[q]) != 0ull;
+                extra = __syncthreads_or(extra);
+                if (!extra) rm = true;
+                else if (ts3_cmp(e, Ts3{a.tm[x], a.tl[x], a.tn[x]}) == 0)
+                    for (uint32_t q = tid; q < a.words; q += CS_T) s.merged[q] |= b[q];
+            }
+        }
+        if (rm) {
+            any = true;
+            if (tid == 0) {
+                const uint32_t sl = a.slot[x];
+                s.gone[r >> 6] |= 1ull << (r & 63);
+                s.dead[sl >> 6] |= 1ull << (sl & 63);
+            }
+        }
+        __syncthreads();
+    }
+    if (!any) return;                                             // pos == retainCount: nothing changes
+    if (tid == 0) {
+        a.pbm[key] = pt.msb; a.pbl[key] = pt.lsb; a.pbn[key] = pt.node;
+        uint32_t g = 0, d = 0;
+        for (uint32_t q = 0; q < a.words; ++q) {
+            s.gpc[q] = g; s.dpc[q] = d;
+            g += (uint32_t)__popcll(s.gone[q]); d += (uint32_t)__popcll(s.dead[q]);
+        }
+        s.idx = g;
+    }
+    __syncthreads();
+    const uint32_t removed = s.idx;
+    // rows: kept rows move down to their rank among the kept (chunks in ascending order: a row is read before any
+    // write can reach its position), their slots renumbered to the rank among the kept slots
+    for (uint32_t r0 = 0; r0 < n; r0 += CS_T) {
+        const uint32_t r = r0 + tid;
+        const bool keep = r < n && !((s.gone[r >> 6] >> (r & 63)) & 1ull);
+        uint64_t vtm = 0, vtl = 0, vem = 0, vel = 0;
+        int32_t vtn = 0, ven = 0;
+        uint8_t vst = 0;
+        uint32_t vsl = 0, to = 0;
+        if (keep) {
+            const size_t x = base + r;
+            vtm = a.tm[x]; vtl = a.tl[x]; vtn = a.tn[x]; vem = a.em[x]; vel = a.el[x]; ven = a.en[x]; vst = a.st[x];
+            vsl = a.slot[x];
+            vsl -= cs_rank(s.dead, s.dpc, vsl);
+            to = r - cs_rank(s.gone, s.gpc, r);
+        }
+        __syncthreads();
+        if (keep) {
+            const size_t y = base + to;
+            a.tm[y] = vtm; a.tl[y] = vtl; a.tn[y] = vtn; a.em[y] = vem; a.el[y] = vel; a.en[y] = ven; a.st[y] = vst;
+            a.slot[y] = vsl;
+        }
+        __syncthreads();
+    }
+    // missing() bitmaps: each kept slot's row moves to its new slot with its columns compacted (one wave per slot,
+    // CS_T / 64 slots per step, every read of a step before its writes)
+    const int wv = tid >> 6, lane = tid & 63;
+    for (uint32_t s0 = 0; s0 < n; s0 += CS_T / 64) {
+        const uint32_t sl = s0 + wv;
+        const bool keep = sl < n && !((s.dead[sl >> 6] >> (sl & 63)) & 1ull);
+        if (keep) cs_remap_row(a, a.bits + (base + sl) * a.words, s.stage[wv], s, lane);
+        __syncthreads();
+        if (keep) {
+            uint64_t* dst = a.bits + (base + sl - cs_rank(s.dead, s.dpc, sl)) * a.words;
+            for (uint32_t q = lane; q < a.words; q += 64) dst[q] = s.stage[wv][q];
+        }
+        __syncthreads();
+    }
+    // loadingPruned witnesses: pruned rows leave, the others renumbered
+    const size_t lb = (size_t)key * a.cap;
+    for (uint32_t j0 = 0; j0 < L; j0 += CS_T / 64) {
+        const uint32_t j = j0 + wv;
+        if (j < L) cs_remap_row(a, a.lp_bits + (lb + j) * a.words, s.stage[wv], s, lane);
+        __syncthreads();
+        if (j < L) for (uint32_t q = lane; q < a.words; q += 64) a.lp_bits[(lb + j) * a.words + q] = s.stage[wv][q];
+        __syncthreads();
+    }
+    n -= removed;
+}
+
 // CommandsForKey.update for a stream of commands (ballots all zero: a command updates its TxnInfo only when its
 // InternalStatus rises, as in CommandsForKeyTest), Updating.insertOrUpdate's cases (Updating.java:99-358):
 //   statuses with deps (ACCEPTED .. APPLIED): the row's missing set is rebuilt from the command's deps (every
@@ -138,21 +389,74 @@ __device__ inline uint32_t cs_insert(const CfkStoreArgs& a, size_t base, uint32_
 //   statuses without deps: a new row joins the others' missing sets unless INVALID; an undecided row invalidated
 //     leaves them.
 // A TRANSITIVELY_KNOWN event is the insertAdditionsOnly path of Updating.updateUnmanaged (:452-514).
+// Pruning: deps below prunedBefore that the rows lack join loadingPruned instead of the rows (removePrunedAdditions,
+// Utils.java:229-244); a LOAD event, or an update of a TxnId in loadingPruned, is CommandsForKey.update's wasPruned path
+// (:1015-1024: no missing(), the TxnId joins the other rows' missing() except its witnesses'); PRUNE / LOADING events
+// as CS_OP_* says.
 static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
     __shared__ uint64_t s_miss[CS_MAX_WORDS];
     __shared__ uint32_t s_add[CS_T];          // this event's additions (slots), CS_T at a time
     __shared__ uint32_t s_nadd;
+    __shared__ uint32_t s_pr[CS_T];           // this event's pruned additions (dep indices)
+    __shared__ uint32_t s_npr;
+    __shared__ int s_j;
+    __shared__ CsPruneLds s_prune;
     const uint32_t key = blockIdx.x;
     if (key >= a.K) return;
     const size_t base = (size_t)key * a.cap;
     uint32_t n = a.cnt[key];
+    uint32_t L = a.lp_cnt[key];
     for (uint32_t e = a.ev_off[key]; e < a.ev_off[key + 1]; ++e) {
         const Ts3 t{a.etm[e], a.etl[e], a.etn[e]};
+        const uint32_t op = a.eop ? a.eop[e] : CS_OP_UPDATE;
+        if (op == CS_OP_PRUNE) {
+            cs_maybe_prune(a, key, base, n, L, (uint32_t)a.een[e], (int64_t)a.eem[e], s_prune);
+            __syncthreads();
+            continue;
+        }
+        if (op == CS_OP_LOADING) {
+            uint32_t w = 0xFFFFFFFFu;
+            if (a.dep_off[e + 1] > a.dep_off[e]) {
+                const uint32_t j = a.dep_off[e];
+                bool f;
+                const uint32_t q = cs_find(a, base, n, Ts3{a.dtm[j], a.dtl[j], a.dtn[j]}, f);
+                if (f) w = a.slot[base + q];
+            }
+            if (!cs_lp_add(a, key, L, t, w, &s_j)) { if (threadIdx.x == 0) *a.overflow = 1u; break; }
+            continue;
+        }
         const uint32_t ns = a.est[e];
         bool found;
         const uint32_t p = cs_find(a, base, n, t, found);
         const uint32_t cur = found ? a.st[base + p] : 0xFFu;
         if (found && ns <= cur) continue;                            // not a higher InternalStatus: no change
+        const int jl = cs_lp_find(a, key, L, t, &s_j);
+        if (op == CS_OP_LOAD || jl >= 0) {
+            // TxnInfo.create: executeAt (statuses with one), no missing(); the loadingPruned entry's witnesses skip it
+            const Ts3 ex{a.eem[e], a.eel[e], a.een[e]};
+            for (uint32_t w = threadIdx.x; w < a.words; w += CS_T)
+                s_miss[w] = jl >= 0 ? a.lp_bits[((size_t)key * a.cap + jl) * a.words + w] : 0ull;
+            __syncthreads();
+            if (jl >= 0) cs_lp_remove(a, key, L, jl);
+            uint32_t ts;
+            if (!found) {
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; break; }
+                ts = cs_insert(a, base, n, p, t, ns, ex);
+            } else {
+                ts = a.slot[base + p];
+                if (threadIdx.x == 0) {
+                    const size_t x = base + p;
+                    a.st[x] = (uint8_t)ns; a.em[x] = ex.msb; a.el[x] = ex.lsb; a.en[x] = ex.node;
+                }
+                for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + ts)) * a.words + w] = 0ull;
+                __syncthreads();
+            }
+            if (cs_decided(ns) && !(found && cs_decided(cur))) cs_remove_missing(a, base, n, ts);
+            else if (found && cur < AD_ST_COMMITTED && ns == AD_ST_INVALID) cs_remove_missing(a, base, n, ts);
+            else if (!found && ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu, s_miss);
+            __syncthreads();
+            continue;
+        }
         const uint32_t d0 = a.dep_off[e], d1 = a.dep_off[e + 1];
         if (cs_has_deps(ns)) {
             const Ts3 ex{a.eem[e], a.eel[e], a.een[e]};
@@ -177,9 +481,10 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 atomicOr((unsigned long long*)&s_miss[s >> 6], 1ull << (s & 63));
             }
             __syncthreads();
-            // deps unknown to the CFK: TRANSITIVELY_KNOWN rows, in deps order
-            if (threadIdx.x == 0) s_nadd = 0;
+            // deps unknown to the CFK: TRANSITIVELY_KNOWN rows, in deps order (below prunedBefore: loadingPruned)
+            if (threadIdx.x == 0) { s_nadd = 0; s_npr = 0; }
             __syncthreads();
+            const Ts3 pb{a.pbm[key], a.pbl[key], a.pbn[key]};
             for (uint32_t j = d0; j < d1; ++j) {
                 const Ts3 d{a.dtm[j], a.dtl[j], a.dtn[j]};
                 if (j > d0 && ts3_cmp(Ts3{a.dtm[j - 1], a.dtl[j - 1], a.dtn[j - 1]}, d) >= 0) {
@@ -189,7 +494,14 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 bool f;
                 const uint32_t q = cs_find(a, base, n, d, f);
                 if (f) continue;
-                if (n >= a.cap || s_nadd >= (uint32_t)CS_T) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; return; }
+                if (ts3_cmp(d, pb) < 0) {
+                    if (s_npr >= (uint32_t)CS_T) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
+                    __syncthreads();
+                    if (threadIdx.x == 0) s_pr[s_npr++] = j;
+                    __syncthreads();
+                    continue;
+                }
+                if (n >= a.cap || s_nadd >= (uint32_t)CS_T) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
                 const uint32_t s = cs_insert(a, base, n, q, d, AD_ST_TRANSITIVELY_KNOWN, d);
                 if (threadIdx.x == 0) s_add[s_nadd++] = s;
                 __syncthreads();
@@ -198,7 +510,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             bool fnow;
             const uint32_t p2 = cs_find(a, base, n, t, fnow);           // t's position after the additions
             if (!fnow) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
                 ts = cs_insert(a, base, n, p2, t, ns, ex);
             } else {
                 ts = a.slot[base + p2];
@@ -209,6 +521,15 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             }
             for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + ts)) * a.words + w] = s_miss[w];
             __syncthreads();
+            const uint32_t npr = s_npr;
+            for (uint32_t k = 0; k < npr; ++k) {
+                const uint32_t j = s_pr[k];
+                if (!cs_lp_add(a, key, L, Ts3{a.dtm[j], a.dtl[j], a.dtn[j]}, ts, &s_j)) {
+                    if (threadIdx.x == 0) *a.overflow = 1u;
+                    a.cnt[key] = n; a.lp_cnt[key] = L;
+                    return;
+                }
+            }
             const uint32_t nadd = s_nadd;
             for (uint32_t k = 0; k < nadd; ++k) {
                 const uint32_t s = s_add[k];
@@ -226,7 +547,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             if (found && cur < AD_ST_COMMITTED && ns >= AD_ST_COMMITTED) cs_remove_missing(a, base, n, ts);
         } else {
             if (!found) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
                 const uint32_t ts = cs_insert(a, base, n, p, t, ns, t);
                 if (ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             } else {
@@ -242,7 +563,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) a.cnt[key] = n;
+    if (threadIdx.x == 0) { a.cnt[key] = n; a.lp_cnt[key] = L; }
 }
 
 }  // namespace ad

@@ -258,6 +258,8 @@ int stage_deps(ad_handle* h) {
         f.P = P; f.ntiles = ntiles; f.skey = h->skey; f.prec = h->prec; f.overflow = fuse_over;
         CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 4 * ntiles + SF_PARTS));
         f.hpart = f.tile_cnt + 4 * ntiles;
+        CK(dalloc(h, S_SFSEC, &f.sec, ntiles * (size_t)SF_SEC + ntiles));
+        f.sec_cnt = f.sec + ntiles * (size_t)SF_SEC;
         const bool packed = h->cnt8_cleared == ncb_of(nc);   // k_pack cleared the count bytes and deferred flags
         h->cnt8_cleared = 0;
         fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0},

@@ -230,6 +230,9 @@ struct ad_handle {
         int32_t *tn = nullptr, *en = nullptr;
         uint8_t *st = nullptr, *out = nullptr;
         uint32_t *slot = nullptr, *pre = nullptr, *flags = nullptr;
+        uint64_t *pbm = nullptr, *pbl = nullptr, *lpm = nullptr, *lpl = nullptr, *lp_bits = nullptr;  // pruning
+        int32_t *pbn = nullptr, *lpn = nullptr;
+        uint32_t* lp_cnt = nullptr;
     } cs;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
@@ -320,9 +323,9 @@ enum Slot : size_t {
     S_STG0, S_STG_END = S_STG0 + 12,
     S_KSSRC, S_KSDST, S_KSSRC2, S_KSDST2, S_KSREM, S_KSXOFF, S_KSRCNT, S_KSFL, S_KSBASE, S_KSCNT, S_KSOUT,
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
-    S_CS0, S_CS_END = S_CS0 + 14,                               // resident CFK store (ad_cfk_store_*)
+    S_CS0, S_CS_END = S_CS0 + 22,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
-    S_SFLO, S_SFCNT, S_FOVF,                                     // k_seg_fuse tiles
+    S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles
     S_NUM_FIXED,
     S_CSR0 = 320
 };

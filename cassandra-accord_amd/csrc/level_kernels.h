@@ -676,9 +676,21 @@ static __global__ __launch_bounds__(256) void k_chain_build(size_t P, const uint
                                                      uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
                                                      uint32_t* __restrict__ indeg, uint2* __restrict__ succ,
                                                      uint32_t* __restrict__ any_long, int full, int pred_mode = 0,
-                                                     uint32_t* __restrict__ any_far = nullptr) {
+                                                     uint32_t* __restrict__ any_far = nullptr,
+                                                     const uint32_t* __restrict__ sec = nullptr,
+                                                     const uint32_t* __restrict__ sec_cnt = nullptr, int sec_cap = 0,
+                                                     uint32_t sec_tiles = 0) {
     bool lng = false, far = false;
-    if (nh) {
+    if (sec) {
+        // k_seg_fuse's per-tile lists of the segments' second entries: one wave per tile
+        const uint32_t tile = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+        if (tile < sec_tiles) {
+            const uint32_t c = sec_cnt[tile];
+            for (uint32_t x = __lane_id(); x < c; x += WAVE)
+                chain_build_seg(P, sec[(size_t)tile * sec_cap + x], seg_start, e_txn, e_meta, e_exec1, sval, c_txn, c_meta,
+                                c_exec1, c_pair, indeg, succ, full, pred_mode, lng, far);
+        }
+    } else if (nh) {
         const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
         const size_t s2 = x < P - prm->n_keys_u ? (size_t)nh[x] : 0;
         chain_build_seg(P, s2, seg_start, e_txn, e_meta, e_exec1, sval, c_txn, c_meta, c_exec1, c_pair, indeg, succ, full,
@@ -1507,6 +1519,10 @@ struct LevelInputs {
     const int32_t* seg_start;
     const uint32_t* sval;                // sorted position -> pair
     const uint32_t* nh;                  // non-head entries (ElideOp), P - prm->n_keys_u of them
+    const uint32_t* sec = nullptr;       // or k_seg_fuse's per-tile second-entry lists (sec_cap per tile, sec_cnt each)
+    const uint32_t* sec_cnt = nullptr;
+    int sec_cap = 0;
+    uint32_t sec_tiles = 0;
     const Params* prm;
     const uint32_t* key_off;
     const uint8_t* meta;
@@ -1928,6 +1944,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         // ---- chain order, segment table, pair -> segment, long-segment positions, (c) constraints
         const int gP = ceil_div((long)std::max<size_t>(P, 1), 256);
         const int gCB = ceil_div((long)std::max<size_t>(P, 1), CB_SPAN);     // k_chain_build without nh
+        const int cb_grid = in.sec ? (int)ceil_div((long)std::max<uint32_t>(in.sec_tiles, 1), 4) : in.nh ? gP : gCB;
         const bool has_b = (in.merged_direct && in.merged_direct->ncap > 0) || (in.merged_range && in.merged_range->ncap > 0);
         const bool has_c = (in.n_large > 0 || in.n_special > 0) && nkm > 0 && P > 0;
         PushCtx push{};
@@ -2015,9 +2032,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 KScope ks(K_KAHN, P);
                 const int gn = ceil_div((long)n, 256);
                 // predecessor runs zeroed above; ls.flags [16] abort, [17] max level, [18] far pred (zeroed above)
-                k_chain_build<<<in.nh ? gP : gCB, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                k_chain_build<<<cb_grid, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
                                                   ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1,
-                                                  ls.flags + 18);
+                                                  ls.flags + 18, in.sec, in.sec_cnt, in.sec_cap, in.sec_tiles);
                 k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
                                                  ls.sk1, ls.pull_force_abort ? 1 : 0);
                 k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
@@ -2075,8 +2092,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 k_mix_kinds<<<gn1, 256, 0, st>>>(n, in.meta, ls.flags + 20);
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
                 if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-                k_chain_build<<<in.nh ? gP : gCB, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
-                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0, 1);
+                k_chain_build<<<cb_grid, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0, 1,
+                                                  nullptr, in.sec, in.sec_cnt, in.sec_cap, in.sec_tiles);
                 hipMemsetAsync(ls.sv1, 0xFF, n * 4, st);
                 k_window_rank<<<ceil_div((long)n, WR_N), WR_T, 0, st>>>(n, in.ex1, nullptr, in.lvl, ls.key64, ls.sv1, ls.sk1, ls.flags + 21);
                 k_perm_check<<<std::min(gn1, 2048), 256, 0, st>>>(n, ls.key64, ls.sv1, ls.flags + 21);
@@ -2164,8 +2182,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 hipMemsetAsync(ls.succ, 0, P * 8, st);
                 // (c) searches every chain in executeAt order, singletons included
                 if (has_c) k_chain_copy<<<gP, 256, 0, st>>>(P, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta, ls.c_exec1, ls.c_pair);
-                k_chain_build<<<in.nh ? gP : gCB, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
-                                                  ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0);
+                k_chain_build<<<cb_grid, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn, ls.c_meta,
+                                                  ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, has_c ? 1 : 0, 0,
+                                                  nullptr, in.sec, in.sec_cnt, in.sec_cap, in.sec_tiles);
                 // long chains found by the build (flags[7]): rebuild every chain with the parallel kernels
                 bool long_done = false;
                 auto long_build = [&]() -> bool {

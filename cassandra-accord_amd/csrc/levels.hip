@@ -38,7 +38,11 @@ int stage_levels(ad_handle* h, bool want_order) {
     if (h->hist_active) return levels_history(h, want_order);
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
-    li.seg_start = h->seg_start; li.sval = h->sval; li.nh = h->nh_valid ? h->nh : nullptr; li.prm = h->prm; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
+    li.seg_start = h->seg_start; li.sval = h->sval; li.nh = h->nh_valid ? h->nh : nullptr;
+    if (!h->nh_valid && h->sf_ntiles) {               // k_seg_fuse's per-tile second-entry lists
+        li.sec = (const uint32_t*)h->bufs[S_SFSEC].p; li.sec_cap = SF_SEC; li.sec_tiles = (uint32_t)h->sf_ntiles;
+        li.sec_cnt = li.sec + h->sf_ntiles * (size_t)SF_SEC;
+    } li.prm = h->prm; li.key_off = h->key_off; li.meta = h->meta; li.ex1 = h->ex1;
     li.lvl = h->lvl; li.order = h->order;
     li.merged_key = &h->merged[AD_CLASS_KEY];
     li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];

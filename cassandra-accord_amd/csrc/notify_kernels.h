@@ -40,6 +40,12 @@ struct NotifyArgs {
     uint32_t cap, words;
     const uint32_t* slot;
     const uint64_t* bits;
+    // the store's loadingPruned tables (nullptr: none): a STABLE txn that witnessed a pruned Read / Write TxnId below its
+    // executeAt that is still loading is not released (Pruning.isWaitingOnPruned, Pruning.java:119-135; :1222)
+    const uint32_t* lp_cnt;
+    const uint64_t *lpm, *lpl;
+    const int32_t* lpn;
+    const uint64_t* lp_bits;
 };
 constexpr uint32_t NF_MAX_WORDS = 128;       // the bitmap reader: at most 8192 rows per key
 
@@ -200,6 +206,13 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
                     }
                 }
                 rel = expect == mc ? 1 : 0;
+                if (rel && a.lp_cnt) {
+                    const size_t lb = key * a.cap;
+                    const uint32_t sl = a.slot[x];
+                    for (uint32_t j = 0; j < a.lp_cnt[key]; ++j)
+                        if (nf_rw(a.lpl[lb + j]) && ts3_cmp(Ts3{a.lpm[lb + j], a.lpl[lb + j], a.lpn[lb + j]}, e) < 0 &&
+                            ((a.lp_bits[(lb + j) * a.words + (sl >> 6)] >> (sl & 63)) & 1ull)) { rel = 0; break; }
+                }
             }
         }
         a.out[x] = rel;

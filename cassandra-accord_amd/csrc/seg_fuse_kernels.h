@@ -35,6 +35,8 @@ struct SegFuseArgs {
     uint32_t* tile_lo;                         // [ntiles + 1] each tile's first sorted position
     uint32_t* tile_cnt;                        // [4 * ntiles]: heads, non-heads; then their exclusive offsets
     uint32_t* hpart;                           // [SF_PARTS] head-count partial sums (zeroed)
+    uint32_t* sec;                             // [ntiles * SF_SEC]: each tile's multi-entry segments' second entries
+    uint32_t* sec_cnt;                         // [ntiles]            (the level chain build's threads)
     uint32_t* overflow;
     uint32_t *e_txn;                           // global entry state (written)
     uint8_t* e_meta;
@@ -44,6 +46,7 @@ struct SegFuseArgs {
 };
 
 constexpr int SF_PARTS = 256;
+constexpr int SF_SEC = SF_CAP / 2;             // second entries per tile: at most one per two entries
 constexpr uint32_t SF_NONE = 0xFFFFFFFFu;
 // first segment head at or after x (x == P: P), searched by one wave 64 positions at a time; SF_NONE if none within
 // SF_CAP positions
@@ -83,8 +86,9 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     __shared__ uint64_t s_pc[SF_CAP];
     __shared__ uint16_t s_glist[SF_CAP];
     __shared__ uint16_t s_qlist[SF_CAP];
+    __shared__ uint16_t s_slist[SF_SEC];
     __shared__ uint32_t s_bounds[2];
-    __shared__ uint32_t s_cnt[4];
+    __shared__ uint32_t s_cnt[5];
     const size_t b = blockIdx.x;
     const int tid = threadIdx.x, wv = tid / WAVE;
     const size_t P = f.P;
@@ -93,7 +97,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         const uint32_t hd = x >= P ? (uint32_t)P : sf_next_head(f.skey, P, x);
         if (__lane_id() == 0) s_bounds[wv] = hd;
     }
-    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; s_cnt[2] = 0; s_cnt[3] = 0; }
+    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; s_cnt[2] = 0; s_cnt[3] = 0; s_cnt[4] = 0; }
     __syncthreads();
     if (s_bounds[0] == SF_NONE || s_bounds[1] == SF_NONE || s_bounds[1] - min(s_bounds[0], s_bounds[1]) > (uint32_t)SF_CAP) {
         // a key segment too long for one tile: the host takes the three-kernel path
@@ -122,6 +126,9 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         if (head && last) f.seg_start[lo + i] = (int32_t)(lo + i);     // lone: its segment start (rest: complete_entries)
         sf_list_append(in && !(head && last), (uint16_t)i, s_glist, &s_cnt[2]);
         sf_list_append(in && !head, (uint16_t)i, s_qlist, &s_cnt[3]);
+        // the second entry of a segment (its predecessor is the head)
+        const bool second = in && !head && (i == 1 || s_key[i - 2] != s_key[i - 1]);
+        sf_list_append(second, (uint16_t)i, s_slist, &s_cnt[4]);
     }
     atomicAdd(&s_cnt[0], heads);
     atomicAdd(&s_cnt[1], nonheads);
@@ -164,7 +171,9 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     if (tid == 0) {
         f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1];
         if (s_cnt[0]) atomicAdd(&f.hpart[b % SF_PARTS], s_cnt[0]);
+        f.sec_cnt[b] = s_cnt[4];
     }
+    for (uint32_t x = tid; x < s_cnt[4]; x += SF_T) f.sec[b * (size_t)SF_SEC + x] = lo + s_slist[x];
     // the queries of the non-head entries, against the LDS copy (sorted position s -> s - lo)
     WalkArgs a = w;
     a.e_txn = s_txn - lo; a.e_meta = s_meta - lo; a.e_exec1 = s_ex1 - lo; a.seg_start = s_ss - lo; a.ud_prev = s_ud - lo;

@@ -484,7 +484,21 @@ int  ad_cfk_notify(ad_handle* h, const ad_cfk_state* s, uint8_t* not_waiting /* 
  * ad_cfk_store_notify then runs CommandsForKey.notifyManaged's release rule (as ad_cfk_notify) over the resident
  * rows -- nothing is uploaded -- and ad_cfk_store_fetch reads one key back in ad_cfk_state's layout (missing() as byId
  * row indices).  capacity <= 8192 (rounded up to a multiple of 64); AD_ERR_UNSUPPORTED when a key outgrows it.
- * Not pruned (Pruning.java:164-233 runs on the batch rows, ad_cfk_retain).                                           */
+ * Pruning (local/cfk/Pruning.java) on the resident rows, by event op (op == NULL: every event AD_CFK_OP_UPDATE):
+ *   AD_CFK_OP_UPDATE   CommandsForKey.update; deps below the key's prunedBefore that it lacks join its loadingPruned
+ *                      table witnessed by the command (Utils.removePrunedAdditions :229-244, Updating.java:111-117)
+ *                      instead of becoming rows; a TxnId in loadingPruned takes the LOAD path (:1015-1016)
+ *   AD_CFK_OP_LOAD     CommandsForKey.updatePruned (:998-1005): the loaded command's row (no missing(); the TxnId joins
+ *                      the other rows' missing() except its loadingPruned witnesses'; the entry leaves the table)
+ *   AD_CFK_OP_PRUNE    CommandsForKey.maybePrune(pruneInterval = exec_node, minHlcDelta = exec_msb) (Pruning.java:164-331)
+ *   AD_CFK_OP_LOADING  txn joins loadingPruned witnessed by its one dep, if any (an unmanaged's pruned deps,
+ *                      Updating.java:806-815)
+ * ad_cfk_store_notify holds a STABLE txn whose loadingPruned witness entry precedes its executeAt (isWaitingOnPruned,
+ * Pruning.java:119-135); ad_cfk_store_pruning reads prunedBefore and the table back.                                 */
+#define AD_CFK_OP_UPDATE  0
+#define AD_CFK_OP_LOAD    1
+#define AD_CFK_OP_PRUNE   2
+#define AD_CFK_OP_LOADING 3
 typedef struct ad_cfk_events {
     size_t m;                       /* events                                                          */
     const uint32_t* ev_off;         /* [keys + 1] events of key k: [ev_off[k], ev_off[k + 1])          */
@@ -499,6 +513,7 @@ typedef struct ad_cfk_events {
     const uint64_t* deps_msb;       /*         TxnIds strictly ascending                              */
     const uint64_t* deps_lsb;
     const int32_t*  deps_node;
+    const uint8_t*  op;             /* [m] AD_CFK_OP_* per event, or NULL                              */
 } ad_cfk_events;
 int  ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity);
 int  ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev);
@@ -508,6 +523,11 @@ int  ad_cfk_store_notify(ad_handle* h, uint32_t* rows /* [keys] */, uint8_t* not
 int  ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missing_total, uint64_t* txn_msb,
                         uint64_t* txn_lsb, int32_t* txn_node, uint64_t* exec_msb, uint64_t* exec_lsb, int32_t* exec_node,
                         uint8_t* status, uint32_t* miss_off, uint32_t* missing);
+/* one key's prunedBefore (TxnId.NONE: zeros) and loadingPruned table: *loading entries (and *witness_total); arrays may
+ * be NULL (two calls); lp_off[loading + 1], lp_rows = the witnesses that are rows, as byId row indices ascending    */
+int  ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint64_t* pruned_lsb, int32_t* pruned_node,
+                          size_t* loading, size_t* witness_total, uint64_t* lp_msb, uint64_t* lp_lsb, int32_t* lp_node,
+                          uint32_t* lp_off, uint32_t* lp_rows);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU key-range sharding (one handle = one CommandStore = one GPU).                     */

@@ -10,11 +10,13 @@
 # Every GPU step has its own time limit and the steps are chained (set -e): a failure ends the script.
 set -eo pipefail
 TAG=${1:?tag}
+PART=${2:-all}          # c2: steps 1-4 only; c34: steps 5-7 only (two gpurun calls stay inside the call limit)
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
+if [ "$PART" != "c34" ]; then
 timeout -k 10 420 python3 -u "$ROOT/bench.py" --breakdown > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench done"
 # (--no-e2e: the end-to-end side measurement overlaps PCIe uploads with pipelines, whose kernels then run slower
@@ -31,6 +33,8 @@ echo "write done"
 # 4. the CPU baseline's extrapolation check: the T-thread oracle once over the full C2 batch
 timeout -k 10 600 python3 -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 --no-e2e --cpu-full > "$OUT/cpu_full.json" 2> "$OUT/cpu_full.err"
 echo "cpu full done"
+fi
+[ "$PART" = "c2" ] && exit 0
 # 5. the other BASELINE configs on one GPU (secondary lines: C3 Zipf deep chains, C4 4M mixed key + range)
 timeout -k 10 300 python3 -u "$ROOT/bench.py" --config C3 --steps 5 --warmup 2 --breakdown > "$OUT/c3.json" 2> "$OUT/c3.err"
 echo "c3 done"

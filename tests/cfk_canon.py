@@ -18,17 +18,31 @@ literally, RNG call for RNG call, over a restatement of the CommandsForKey state
                                       Utils.findCommit / findFirstApply / findApply :363-393
 * WaitingOn                           local/Command.java:1225-1560 (key bit + direct range / key TxnId bits)
 
+* Pruning (Run(prune=True), the reference's test(seed)): CommandsForKey.maybePrune / pruneBefore
+                                      (local/cfk/Pruning.java:164-331) on rnd.decide(pruneChance) and after a loaded
+                                      Applied command (SafeCommandsForKey.update :66-83); prunedBefore; loadingPruned
+                                      (Pruning.LoadingPruned :50-114: pruned additions of an update, Updating.java:111-117,
+                                      and pruned deps of an unmanaged, :803-815); the test's task queue
+                                      (TestCommandStore.queue / runOneTask, CommandsForKeyTest.java:917-953) holding
+                                      PostProcess.LoadPruned loads (-> CommandsForKey.updatePruned :998-1005) and
+                                      Updating.updateUnmanagedAsync (:690-700) for unmanageds below prunedBefore;
+                                      isWaitingOnPruned in notifyManaged (:1222), isAnyPredecessorWaitingOnPruned for
+                                      sync points (Updating.java:796), loadingPruned's first TxnId bounding the commit
+                                      notifications (PostProcess.java:171).
 Deliberate limits, stated where they act:
-* Pruning is not applied: test(seed) still draws pruneChance, pruneHlcDelta, pruneInterval and every
-  rnd.decide(pruneChance), but maybePrune (Pruning.java:164-233) is not run, so no TxnId is ever below prunedBefore,
-  loadingPruned stays empty and the task queue stays empty (every queued task in the reference comes from pruned
-  TxnIds: PostProcess.LoadPruned, Updating.updateUnmanagedAsync).  A seed whose Java run prunes diverges from it after
-  that point.  Pruning of the device state is exercised by ad_cfk_retain's tests.
+* Run(prune=False) (the default, kept for the earlier tests) draws every rnd.decide(pruneChance) but never prunes, so no
+  TxnId is ever below prunedBefore and the task queue stays empty.
+* Order inside one harness step: CommandsForKeyUpdate.postProcess runs notifyManaged on the PRE-prune CFK and the
+  notifier chain on the current (post-prune) one.  The restatement prunes after notifyManaged: pruning removes only
+  Applied rows executing before the new prunedBefore (at or below maxAppliedWriteByExecuteAt) and invalidated rows, none
+  of which notifyManaged reads (it starts after maxAppliedWrite, counts undecided rows, and reads missing() sets, which
+  hold no committed TxnId), so its notifications are the same either way.
 * Ballots are all ZERO (as in Canon), so the ballot-ordered CFK updates reduce to "the InternalStatus must rise".
 No JVM exists here, so the stream cannot be compared with a Java run: parity of the stream itself is unpinned; what is
 pinned is that the restated harness satisfies the reference's own invariants (:175-180, :208-218) on every seed run.
 """
 import bisect
+import collections
 
 import numpy as np
 
@@ -520,10 +534,12 @@ class Info:
 
 
 COMMIT_P, APPLY_P = 0, 1                              # Unmanaged.Pending
+# ops of the device event log (CFK.log entries (txnId, InternalStatus, executeAt, deps[, op[, interval, hlcDelta]]))
+OP_UPDATE, OP_LOAD, OP_PRUNE, OP_LOADING = 0, 1, 2, 3
 
 
 class CFK:
-    """One key's CommandsForKey (no pruning): byId Infos, unmanageds; the derived committedByExecuteAt,
+    """One key's CommandsForKey: byId Infos, unmanageds, prunedBefore, loadingPruned; the derived committedByExecuteAt,
     minUndecidedById and maxAppliedWriteByExecuteAt are recomputed from byId as the constructor does (:642-681)."""
 
     def __init__(self, domains):
@@ -532,13 +548,34 @@ class CFK:
         self.info = {}
         self.unmanageds = []                          # sorted (pending, waitingUntil, txnId)
         self.log = None                               # list: the CommandsForKey.update calls as device events
+        self.pruned_before = NONE                     # prunedBefore's TxnId (NO_INFO: TxnId.NONE)
+        self.loading = {}                             # loadingPruned: TxnId -> witnessedBy (sorted tuple)
+        self.last_load = ()                           # the TxnIds the last update / updateUnmanaged asked to load
+        self.prunes = 0                               # pruneBefore calls that removed rows
 
     def copy(self):
         c = CFK(self.domains)
         c.ids = list(self.ids)
         c.info = {t: Info(i.txn, i.status, i.execute_at, set(i.missing), i.deps) for t, i in self.info.items()}
         c.unmanageds = list(self.unmanageds)
+        c.pruned_before, c.loading = self.pruned_before, dict(self.loading)
         return c
+
+    def manages(self, t):                             # CommandsForKey.manages :185-188
+        return self.domains[t] == KEY and kind_of(t) in ANY_GLOBALLY_VISIBLE
+
+    def _load_pruned(self, ids, witness):             # Pruning.loadPruned :79-94 (witnessedBy merged by linearUnion)
+        for d in ids:
+            w = set(self.loading.get(d, ()))
+            if witness is not None:
+                w.add(witness)
+            self.loading[d] = tuple(sorted(w))
+
+    def waiting_on_pruned(self, waiting, execute_at):  # Pruning.isWaitingOnPruned :119-135
+        return any(lid < execute_at and self.me(lid) and waiting in w for lid, w in self.loading.items())
+
+    def any_predecessor_waiting_on_pruned(self, waiting):   # Pruning.isAnyPredecessorWaitingOnPruned :140-157
+        return any(lid < waiting and self.me(lid) and w and waiting >= w[0] for lid, w in self.loading.items())
 
     def me(self, t):
         return self.domains[t] == KEY and kind_of(t) in (READ, WRITE)
@@ -566,12 +603,13 @@ class CFK:
         bisect.insort(self.ids, info.txn)
         self.info[info.txn] = info
 
-    def _add_missing_everywhere(self, a, skip=None):
+    def _add_missing_everywhere(self, a, skip=None, do_not_insert=()):
         """a (uncommitted, newly known) joins the missing array of every txn with deps that witnesses it and whose
-        depsKnownBefore is above it (Utils.addToMissingArrays :97-172, Updating.insertOrUpdateWithAdditions :385-450)."""
+        depsKnownBefore is above it (Utils.addToMissingArrays :97-172, Updating.insertOrUpdateWithAdditions :385-450),
+        except the members of do_not_insert (a loaded pruned TxnId's witnessedBy, Updating.java:351)."""
         ka = kind_of(a)
         for u in self.info.values():
-            if u.txn == a or u.txn == skip or not has_deps(u.status):
+            if u.txn == a or u.txn == skip or not has_deps(u.status) or u.txn in do_not_insert:
                 continue
             if witnesses(kind_of(u.txn), ka) and u.deps_known_before() > a:
                 u.missing.add(a)
@@ -580,18 +618,46 @@ class CFK:
         for u in self.info.values():
             u.missing.discard(a)
 
-    def update(self, cmd):
-        """CommandsForKey.update (:987-1057) for a managed command -> (changed, curInfo, newInfo, notifier txns)."""
+    def update(self, cmd, was_pruned=False):
+        """CommandsForKey.update (:987-1057) for a managed command, or updatePruned (:998-1005) for a loaded pruned one
+        -> (changed, curInfo status, newInfo); self.last_load = the pruned additions to load (LoadPruned)."""
+        self.last_load = ()
         new = _INTERNAL.get(cmd.ss)
-        if new is None:
-            return False, None, None
         t = cmd.txn
+        if was_pruned:
+            if new is None:
+                new = TK
+            if not self.manages(t):
+                new = TK if new < COMMITTED else INVALID
+        elif new is None:
+            return False, None, None
+        loading_for = self.loading.get(t)             # loadingPrunedFor(loadingPruned, txnId, null)
+        was_pruned = was_pruned or loading_for is not None
         if self.log is not None:                      # (txnId, InternalStatus, executeAt, deps) as ad_cfk_store_apply takes it
-            self.log.append((t, new, cmd.execute_at if has_deps(new) else t, tuple(cmd.deps) if has_deps(new) else ()))
+            if was_pruned:
+                self.log.append((t, new, cmd.execute_at if has_deps(new) else t, (), OP_LOAD))
+            else:
+                self.log.append((t, new, cmd.execute_at if has_deps(new) else t, tuple(cmd.deps) if has_deps(new) else ()))
         cur = self.info.get(t)
         if cur is not None and new <= cur.status:      # ballots ZERO: only a higher InternalStatus updates
             return False, None, None
         cur_status = cur.status if cur is not None else None
+        if was_pruned:                                # TxnInfo.create: no missing(), no additions (:1024, :1053)
+            ex = cmd.execute_at if has_deps(new) else t
+            if loading_for is not None:               # insertOrUpdate :295
+                del self.loading[t]
+            if cur is None:
+                self._insert(Info(t, new, ex))
+            else:
+                cur.status, cur.execute_at, cur.missing, cur.deps = new, ex, set(), None
+            was_committed = cur_status is not None and cur_status in (COMMITTED, STABLE, APPLIED)
+            if new in (COMMITTED, STABLE, APPLIED) and not was_committed:          # :340-343
+                self._remove_missing_everywhere(t)
+            elif cur is not None and cur_status < COMMITTED and new == INVALID:
+                self._remove_missing_everywhere(t)
+            elif cur is None and new != INVALID:
+                self._add_missing_everywhere(t, do_not_insert=loading_for or ())
+            return True, cur_status, self.info[t]
         if has_deps(new):
             ex = cmd.execute_at
             deps = cmd.deps
@@ -606,6 +672,11 @@ class CFK:
                 if iu.status < COMMITTED and witnesses(kt, kind_of(u)) and u not in dep_set:
                     missing.add(u)
             additions = [d for d in deps if d not in self.info]
+            pruned = [d for d in additions if d < self.pruned_before]       # Utils.removePrunedAdditions :229-244
+            if pruned:
+                additions = [d for d in additions if d >= self.pruned_before]
+                self._load_pruned(pruned, t)
+                self.last_load = tuple(pruned)
             for a in additions:                       # TRANSITIVELY_KNOWN additions (:178-227)
                 self._insert(Info(a, TK, a))
             if cur is None:
@@ -631,11 +702,62 @@ class CFK:
             new_info = self.info[t]
         return True, cur_status, new_info
 
+    # -- Pruning.maybePrune / pruneBefore (Pruning.java:164-331)
+    def maybe_prune(self, prune_interval, min_hlc_delta):
+        if self.log is not None:
+            self.log.append((NONE, 0, NONE, (), OP_PRUNE, prune_interval, min_hlc_delta))
+        committed = self.committed()
+        i = self.max_applied_write(committed)
+        if i < prune_interval:                        # maxAppliedWriteByExecuteAt < pruneInterval (-1 when none)
+            return False
+        max_prune_hlc = committed[i].execute_at[1] - min_hlc_delta
+        i -= 1
+        while i >= 0:
+            x = committed[i]
+            if kind_of(x.txn) == WRITE and x.execute_at[1] <= max_prune_hlc and x.status == APPLIED:
+                break
+            i -= 1
+        if i < 0:
+            return False
+        npb = committed[i]
+        if npb.txn <= self.pruned_before:
+            return False
+        pos = bisect.bisect_left(self.ids, npb.txn)   # insertPos
+        if pos == 0:
+            return False
+        return self._prune_before(npb, pos)
+
+    def _prune_before(self, npb, pos):
+        """Removes the Applied rows before npb (in TxnId and executeAt) whose missing() the later retained rows cover, and
+        the invalidated rows before it (:199-297); prunedBefore = npb."""
+        merged = set(npb.missing)
+        remove = []
+        for k in range(pos):
+            x = self.info[self.ids[k]]
+            if x.status == INVALID:
+                remove.append(x.txn)
+            elif x.status == APPLIED and x.execute_at < npb.execute_at:
+                if not x.missing or x.missing <= merged:
+                    remove.append(x.txn)
+                elif x.execute_at == x.txn:
+                    merged |= x.missing
+        if not remove:                                # pos == retainCount: unchanged (prunedBefore not advanced)
+            return False
+        gone = set(remove)
+        self.ids = [t for t in self.ids if t not in gone]
+        for t in remove:
+            del self.info[t]
+        self.pruned_before = npb.txn
+        self.prunes += 1
+        return True
+
     # -- notifyUnmanaged (PostProcess.java:143-244)
     def notify_unmanaged(self, cur_status, new_info):
         commit_notify, apply_notify = [], []
         mu = self.min_undecided()
         bound = self.ids[mu] if mu >= 0 else MAX
+        if self.loading:                              # PostProcess.java:171
+            bound = min(bound, min(self.loading))
         end = 0
         while end < len(self.unmanageds) and self.unmanageds[end][0] == COMMIT_P and bound > self.unmanageds[end][1]:
             end += 1
@@ -704,7 +826,7 @@ class CFK:
             if txn.status == APPLIED or not self.me(txn.txn):
                 continue
             kind = kind_of(txn.txn)
-            if kind in kinds or i == any_at:
+            if (kind in kinds or i == any_at) and not self.waiting_on_pruned(txn.txn, txn.execute_at):
                 if txn.status == STABLE:
                     if undecided_index < len(self.ids):
                         nxt = bisect.bisect_left(self.ids, txn.execute_at, undecided_index)
@@ -723,6 +845,7 @@ class CFK:
 
     # -- updateUnmanaged (Updating.java:715-849)
     def update_unmanaged(self, cmd, sink, register, add_list=None):
+        self.last_load = ()
         if cmd.has_been(S_TRUNCATED):
             return
         wt, wex = cmd.txn, cmd.execute_at
@@ -762,8 +885,19 @@ class CFK:
                     missing.append(tx[i])
                     i += 1
                 else:
-                    raise AssertionError("unmanaged dependency %s unknown to the CFK without pruning" % (tx[i],))
+                    assert tx[i] < self.pruned_before, "unmanaged dependency %s unknown to the CFK" % (tx[i],)
+                    i += 1
+            if wk in (SYNC, ESP) and self.any_predecessor_waiting_on_pruned(wt):      # :796-797
+                ready_to_apply = waiting_to_apply = False
             if not ready_to_apply:
+                pruned = [a for a in missing if a < self.pruned_before]            # :806-815
+                if pruned:
+                    missing = missing[len(pruned):]
+                    self._load_pruned(pruned, wt)
+                    if self.log is not None:
+                        for a in pruned:
+                            self.log.append((a, 0, a, (wt,), OP_LOADING))
+                    self.last_load = tuple(pruned)
                 for a in missing:                     # insertAdditionsOnly (:452-514)
                     self._insert(Info(a, TK, a))
                     if self.log is not None:
@@ -817,7 +951,8 @@ class Run:
     """One seed of the restated harness.  events: per update, (txnId, SaveStatus) and the managed notifications it
     caused; snapshots: the CFK after events chosen by `snapshot_every` (and every event with a notification)."""
 
-    def __init__(self, seed, min_count, snapshot_every=0, check_full_scan=False, count_gating=False, log=False):
+    def __init__(self, seed, min_count, snapshot_every=0, check_full_scan=False, count_gating=False, log=False,
+                 prune=False):
         self.seed = seed
         self.event_log = [] if log else None          # per harness event: the CFK update calls it made (CFK.log)
         rnd = Rnd(seed)
@@ -838,7 +973,27 @@ class Run:
         self.notified = set()
         self.full_scan_mismatches = []
         self.gated_events = 0                         # events after which some STABLE txn is held by an undecided dep
-        queue = []                                     # always empty without pruning
+        queue = collections.deque()                   # TestCommandStore.queue: ('load' | 'unmanaged', TxnId)
+        self.tasks_run = 0
+        self.loads = 0
+        sink = canon.not_waiting
+
+        def run_one_task():                           # TestCommandStore.runOneTask (:932-939)
+            if not queue:
+                return
+            self.tasks_run += 1
+            what, t = queue.popleft()
+            cmd = canon.by_id.get(t)
+            if what == 'load':                        # PostProcess.LoadPruned.load -> SafeCommandsForKey.updatePruned
+                changed, cur_status, new_info = cfk.update(cmd, was_pruned=True)
+                if not changed:                       # updateCfk == prevCfk: nothing to post-process
+                    return
+                self.loads += 1
+                self._post_update(cfk, canon, queue, cur_status, new_info, cmd, True, sink,
+                                  prune_now=cmd.has_been(S_APPLIED))
+            else:                                     # Updating.updateUnmanagedAsync (:690-700)
+                cfk.update_unmanaged(cmd, sink, False)
+
         c = 0
         while not canon.is_done():
             c += 1
@@ -846,37 +1001,24 @@ class Run:
                 canon.close()
             rtc = np.float32(self.run_task_chance)
             if rnd.decide(rtc - rtc / np.float32(1 + len(queue))):
-                pass                                   # runOneTask: the queue is empty
+                run_one_task()
             up = canon.update(len(queue) > 0)
             if up is None:
+                run_one_task()
                 continue
             prev, nxt = up
             before = len(canon.notified)
             if canon.manages(nxt.txn):
                 changed, cur_status, new_info = cfk.update(nxt)
-                commit_n, apply_n = ([], []) if not changed else cfk.notify_unmanaged(cur_status, new_info)
-                rnd.decide(np.float32(self.prune_chance))     # maybePrune not applied (module docstring)
-                # result.postProcess: the CFK's own notifyManaged, then the notifier chain (NotifyNotWaiting of the
-                # APPLY-released unmanageds, then NotifyUnmanagedOfCommit)
-                if changed:
-                    cfk.post_process(cur_status, nxt, canon.not_waiting)
-                elif nxt.txn in cfk.info:                     # an unchanged CFK still post-processes the command
-                    cfk.post_process(cfk.info[nxt.txn].status, nxt, canon.not_waiting)
-                for u in apply_n:
-                    canon.not_waiting(u)
-                if commit_n:
-                    adds = []
-                    for u in commit_n:
-                        cfk.update_unmanaged(canon.by_id.get(u), canon.not_waiting, False, adds)
-                    for rec in sorted(adds):
-                        k = bisect.bisect_left(cfk.unmanageds, rec)
-                        if k == len(cfk.unmanageds) or cfk.unmanageds[k] != rec:
-                            cfk.unmanageds.insert(k, rec)
+                do_prune = rnd.decide(np.float32(self.prune_chance)) and prune
+                self._post_update(cfk, canon, queue, cur_status, new_info, nxt, changed, sink, prune_now=do_prune)
             if not canon.manages_execution(nxt.txn) and nxt.has_been(S_STABLE) and not nxt.has_been(S_TRUNCATED):
                 # registerUnmanaged(safeStore, new TestSafeCommand(.., update.next)): the command as updated (the
                 # WaitingOn executeAtLeast bump for awaitsOnlyDeps kinds, Updating.java:806-815, changes nothing the
-                # harness or the release rule reads, and is not modelled)
-                cfk.update_unmanaged(nxt, canon.not_waiting, True)
+                # harness or the release rule reads, and is not modelled); its pruned deps are queued loads
+                cfk.update_unmanaged(nxt, sink, True)
+                for t in cfk.last_load:
+                    queue.append(('load', t))
             self.events += 1
             if log:
                 self.event_log.append(list(cfk.log))
@@ -892,7 +1034,38 @@ class Run:
                     self.full_scan_mismatches.append((self.events, sorted(got - want), sorted(want - got)))
             if snapshot_every and (fresh or self.events % snapshot_every == 0):
                 self.snapshots.append((self.events, self.rows(), frozenset(
-                    t for t in self.notified if cfk.info[t].status == STABLE), frozenset(full_scan_ready(cfk))))
+                    t for t in self.notified if cfk.info.get(t) is not None and cfk.info[t].status == STABLE),
+                    frozenset(full_scan_ready(cfk))))
+        self.queue_left = len(queue)
+
+    def _post_update(self, cfk, canon, queue, cur_status, new_info, cmd, changed, sink, prune_now):
+        """CommandsForKeyUpdate.postProcess after CommandsForKey.update / updatePruned (+ maybePrune):
+        notifyUnmanaged's lists (computed by the update), notifyManaged, LoadPruned, NotifyNotWaiting,
+        NotifyUnmanagedOfCommit (PostProcess.java:60-244)."""
+        load = cfk.last_load
+        commit_n, apply_n = ([], []) if not changed else cfk.notify_unmanaged(cur_status, new_info)
+        # the CFK's own notifyManaged (on the pre-prune CFK: see the module docstring)
+        if changed:
+            cfk.post_process(cur_status, cmd, sink)
+        elif cmd.txn in cfk.info:                     # an unchanged CFK still post-processes the command
+            cfk.post_process(cfk.info[cmd.txn].status, cmd, sink)
+        if prune_now:
+            cfk.maybe_prune(self.prune_interval, self.prune_hlc_delta)
+        for t in load:                                # LoadPruned: every TxnId is below prunedBefore -> queued
+            queue.append(('load', t))
+        for u in apply_n:
+            sink(u)
+        if commit_n:
+            adds = []
+            for u in commit_n:
+                if u < cfk.pruned_before:             # ifLoadedAndInitialised == null -> updateUnmanagedAsync
+                    queue.append(('unmanaged', u))
+                else:
+                    cfk.update_unmanaged(canon.by_id.get(u), sink, False, adds)
+            for rec in sorted(adds):
+                k = bisect.bisect_left(cfk.unmanageds, rec)
+                if k == len(cfk.unmanageds) or cfk.unmanageds[k] != rec:
+                    cfk.unmanageds.insert(k, rec)
 
     def rows(self):
         """The CFK as the C-ABI takes it (CommandsForKey.SerializerSupport.create, :226-232): byId TxnInfos —
