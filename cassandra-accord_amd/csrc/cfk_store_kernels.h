@@ -397,8 +397,6 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
     __shared__ uint64_t s_miss[CS_MAX_WORDS];
     __shared__ uint32_t s_add[CS_T];          // this event's additions (slots), CS_T at a time
     __shared__ uint32_t s_nadd;
-    __shared__ uint32_t s_pr[CS_T];           // this event's pruned additions (dep indices)
-    __shared__ uint32_t s_npr;
     __shared__ int s_j;
     __shared__ CsPruneLds s_prune;
     const uint32_t key = blockIdx.x;
@@ -482,7 +480,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             }
             __syncthreads();
             // deps unknown to the CFK: TRANSITIVELY_KNOWN rows, in deps order (below prunedBefore: loadingPruned)
-            if (threadIdx.x == 0) { s_nadd = 0; s_npr = 0; }
+            if (threadIdx.x == 0) s_nadd = 0;
             __syncthreads();
             const Ts3 pb{a.pbm[key], a.pbl[key], a.pbn[key]};
             for (uint32_t j = d0; j < d1; ++j) {
@@ -494,13 +492,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 bool f;
                 const uint32_t q = cs_find(a, base, n, d, f);
                 if (f) continue;
-                if (ts3_cmp(d, pb) < 0) {
-                    if (s_npr >= (uint32_t)CS_T) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
-                    __syncthreads();
-                    if (threadIdx.x == 0) s_pr[s_npr++] = j;
-                    __syncthreads();
-                    continue;
-                }
+                if (ts3_cmp(d, pb) < 0) continue;                      // a pruned addition: loadingPruned, below
                 if (n >= a.cap || s_nadd >= (uint32_t)CS_T) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
                 const uint32_t s = cs_insert(a, base, n, q, d, AD_ST_TRANSITIVELY_KNOWN, d);
                 if (threadIdx.x == 0) s_add[s_nadd++] = s;
@@ -521,10 +513,14 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             }
             for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + ts)) * a.words + w] = s_miss[w];
             __syncthreads();
-            const uint32_t npr = s_npr;
-            for (uint32_t k = 0; k < npr; ++k) {
-                const uint32_t j = s_pr[k];
-                if (!cs_lp_add(a, key, L, Ts3{a.dtm[j], a.dtl[j], a.dtn[j]}, ts, &s_j)) {
+            // pruned additions (deps below prunedBefore that are not rows): loadingPruned, witnessed by this command
+            for (uint32_t j = d0; j < d1; ++j) {
+                const Ts3 d{a.dtm[j], a.dtl[j], a.dtn[j]};
+                if (ts3_cmp(d, pb) >= 0) break;                       // deps ascend
+                bool f;
+                cs_find(a, base, n, d, f);
+                if (f) continue;
+                if (!cs_lp_add(a, key, L, d, ts, &s_j)) {
                     if (threadIdx.x == 0) *a.overflow = 1u;
                     a.cnt[key] = n; a.lp_cnt[key] = L;
                     return;

@@ -975,6 +975,7 @@ class Run:
         self.gated_events = 0                         # events after which some STABLE txn is held by an undecided dep
         queue = collections.deque()                   # TestCommandStore.queue: ('load' | 'unmanaged', TxnId)
         self.tasks_run = 0
+        self.max_rows = 0
         self.loads = 0
         sink = canon.not_waiting
 
@@ -1020,6 +1021,7 @@ class Run:
                 for t in cfk.last_load:
                     queue.append(('load', t))
             self.events += 1
+            self.max_rows = max(self.max_rows, len(cfk.ids))
             if log:
                 self.event_log.append(list(cfk.log))
                 cfk.log.clear()

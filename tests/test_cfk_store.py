@@ -112,7 +112,7 @@ def test_gpu_store_follows_the_harness(engine_factory, chunk, prune):
     seeds = (PRUNE_SEEDS if prune else SEEDS)[chunk * 10:(chunk + 1) * 10]
     runs = [K.Run(seed, 1000, snapshot_every=25, log=True, prune=prune) for seed in seeds]
     eng = engine_factory(window=0, replicas=1, drop_p=0.0, seed=1)
-    cap = max(len(r.cfk.ids) for r in runs) + 64
+    cap = max(r.max_rows for r in runs) + 64
     eng.cfk_store_open(len(runs), cap)
     snaps = [{ev: (rows, want, full) for ev, rows, want, full in r.snapshots} for r in runs]
     steps = max(len(r.event_log) for r in runs)
