@@ -148,10 +148,11 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
 // second level of k_minmax: one block folds the per-block partials into Params (no contended atomics)
 // pub_flag != null: also publishes the Params to the host-mapped words (pub_prm) and releases seq into *pub_flag, as
 // k_publish would in a launch of its own (engine.hip publish_totals)
-static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out,
+constexpr int MM_FINAL_T = 256;
+static __global__ __launch_bounds__(MM_FINAL_T) void k_minmax_final(int nblk, const unsigned long long* __restrict__ partial, Params* out,
                                                        uint32_t* pub_flag = nullptr, uint32_t* pub_prm = nullptr, uint32_t seq = 0) {
-    constexpr int NF = 15, NSUM = 12, NOR = 14;
-    __shared__ unsigned long long red[4][NF];
+    constexpr int NF = 15, NSUM = 12, NOR = 14, NW = MM_FINAL_T / WAVE;
+    __shared__ unsigned long long red[NW][NF];
     unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = threadIdx.x; b < nblk; b += blockDim.x)
         for (int k = 0; k < NF; ++k) {
@@ -173,9 +174,8 @@ static __global__ __launch_bounds__(256) void k_minmax_final(int nblk, const uns
     __syncthreads();
     if (threadIdx.x < NF) {
         const int k = threadIdx.x;
-        unsigned long long v = k >= NOR ? (red[0][k] | red[1][k] | red[2][k] | red[3][k])
-                             : k >= NSUM ? red[0][k] + red[1][k] + red[2][k] + red[3][k]
-                                         : max(max(red[0][k], red[1][k]), max(red[2][k], red[3][k]));
+        unsigned long long v = red[0][k];
+        for (int x = 1; x < NW; ++x) v = k >= NOR ? (v | red[x][k]) : k >= NSUM ? v + red[x][k] : max(v, red[x][k]);
         // the only writer of these fields (no separate initialisation launch)
         switch (k) {
             case 0: out->msb_min = ~v; break;

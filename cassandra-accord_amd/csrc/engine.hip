@@ -1202,13 +1202,73 @@ int ad_merge_deps_fast(ad_handle* h, ad_csr_sizes* sizes) {
     return AD_OK;
 }
 
+// Union-view merged Deps (capacity regions + per-txn unique counts) compacted ON THE DEVICE into exact per-txn
+// TxnId lists, once per batch, so the fetch is straight DMA into the caller's (pinned) buffers as for exact merges:
+// one exclusive scan of the counts and one copy pass per class, then one small read of the totals.
+static __global__ void k_compact_rows(size_t n, const uint32_t* __restrict__ ent_off, const uint32_t* __restrict__ tcnt,
+                                      const uint32_t* __restrict__ xoff, const uint32_t* __restrict__ txns,
+                                      uint32_t* __restrict__ out) {
+    // one wave per 64 txns, lanes over one txn's entries at a time (rows are short: coalesced within a row)
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int lane = threadIdx.x % WAVE;
+    const size_t t0 = w * WAVE;
+    for (size_t t = t0; t < t0 + WAVE && t < n; ++t) {
+        const uint32_t c = tcnt[t], src = ent_off[t], dst = xoff[t];
+        for (uint32_t j = lane; j < c; j += WAVE) out[dst + j] = txns[src + j];
+    }
+}
+static int merged_compact(ad_handle* h) {
+    if (h->merged_exact || h->merged_compacted) return AD_OK;
+    const size_t n = h->n;
+    hipStream_t st = h->st;
+    uint32_t* totals = nullptr;
+    CK(dalloc(h, S_MXS, &totals, 4));
+    CK(ensure_scratch(h, device_scan_scratch<SumOp<uint32_t>>(n)));
+    for (int c = 0; c < 3; ++c) {
+        h->mx_tot[c] = 0;
+        const Csr& m = h->merged[c];
+        if (c == AD_CLASS_RANGE && !h->merged_has_range) continue;
+        CK(dalloc(h, S_MXO0 + c, &h->mx_off[c], n + 1));
+        CK(dalloc(h, S_MXT0 + c, &h->mx_txns[c], std::max<size_t>(m.ncap, 1)));
+        if (n == 0 || m.ncap == 0) {
+            HIPCHK(h, hipMemsetAsync(h->mx_off[c], 0, (n + 1) * 4, st));
+        } else {
+            SumOp<uint32_t> op{m.tcnt, h->mx_off[c], n};
+            device_scan(op, n, (uint32_t*)h->scratch, st);
+            k_compact_rows<<<ceil_div((long)ceil_div((long)n, WAVE) * WAVE, 256), 256, 0, st>>>(
+                n, m.ent_off, m.tcnt, h->mx_off[c], m.txns, h->mx_txns[c]);
+        }
+        HIPCHK(h, hipMemcpyAsync(totals + c, h->mx_off[c] + n, 4, hipMemcpyDeviceToDevice, st));
+    }
+    uint32_t tot[3] = {0, 0, 0};
+    HIPCHK(h, hipMemcpyAsync(tot, totals, 12, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    for (int c = 0; c < 3; ++c)
+        if (!(c == AD_CLASS_RANGE && !h->merged_has_range)) h->mx_tot[c] = tot[c];
+    h->merged_compacted = true;
+    return AD_OK;
+}
+
 int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
     if (!h || !out) return AD_ERR_ARGUMENT;
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     if (cls >= AD_NUM_CLASSES) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
-    if (cls == AD_CLASS_RANGE) return h->merged_has_range ? fetch_csr(h, h->merged[2], 2, out) : fetch_empty(h, out);
-    return fetch_csr(h, h->merged[cls], 1, out);
+    if (cls == AD_CLASS_RANGE && !h->merged_has_range) return fetch_empty(h, out);
+    if (h->merged_exact) return fetch_csr(h, h->merged[cls], cls == AD_CLASS_RANGE ? 2 : 1, out);
+    CK(merged_compact(h));               // union view: the device-compacted lists, straight DMA
+    const Csr& m = h->merged[cls];
+    const size_t n = h->n;
+    const int kw = cls == AD_CLASS_RANGE ? 2 : 1;
+    hipStream_t st = h->st;
+    HIPCHK(h, hipMemcpyAsync(out->key_off, m.key_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(out->k2t_off, m.k2t_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(out->txn_off, h->mx_off[cls], (n + 1) * 4, hipMemcpyDeviceToHost, st));
+    if (m.nkeys) HIPCHK(h, hipMemcpyAsync(out->keys, m.keys, m.nkeys * 8 * kw, hipMemcpyDeviceToHost, st));
+    if (m.nk2t) HIPCHK(h, hipMemcpyAsync(out->k2t, m.k2t, m.nk2t * 4, hipMemcpyDeviceToHost, st));
+    if (h->mx_tot[cls]) HIPCHK(h, hipMemcpyAsync(out->txns, h->mx_txns[cls], h->mx_tot[cls] * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    return AD_OK;
 }
 
 // The merged Deps of every class in one call: Deps.merge's outputs carry exact per-txn TxnId offsets
@@ -1220,10 +1280,11 @@ int ad_merged_sizes(ad_handle* h, ad_csr_sizes* sizes /* [3] */) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     if (!h->merged_exact) {
         hipSetDevice(h->device);
+        CK(merged_compact(h));
         for (int c = 0; c < 3; ++c) {
+            const Csr& m = h->merged[c];
             if (c == AD_CLASS_RANGE && !h->merged_has_range) { sizes[c] = ad_csr_sizes{h->n, 0, 0, 0, 0}; continue; }
-            CK(csr_sizes(h, h->merged[c], &sizes[c]));
-            sizes[c].txn_cap = sizes[c].txns;             // the compacted lists fetched below
+            sizes[c] = ad_csr_sizes{h->n, m.nkeys, m.nk2t, h->mx_tot[c], h->mx_tot[c]};   // the compacted lists
         }
         return AD_OK;
     }
@@ -1239,10 +1300,7 @@ int ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [3] */) {
     if (!h || !out) return AD_ERR_ARGUMENT;
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     hipSetDevice(h->device);
-    if (!h->merged_exact) {
-        for (int c = 0; c < 3; ++c) CK(ad_fetch_merged(h, (uint32_t)c, &out[c]));
-        return AD_OK;
-    }
+    CK(merged_compact(h));
     hipStream_t st = h->st;
     const size_t n = h->n;
     for (int c = 0; c < 3; ++c) {
@@ -1253,12 +1311,15 @@ int ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [3] */) {
             continue;
         }
         const int kw = c == AD_CLASS_RANGE ? 2 : 1;
+        const uint32_t* toff = h->merged_exact ? m.ent_off : h->mx_off[c];
+        const uint32_t* tx = h->merged_exact ? m.txns : h->mx_txns[c];
+        const size_t nt = h->merged_exact ? m.ncap : h->mx_tot[c];
         HIPCHK(h, hipMemcpyAsync(o.key_off, m.key_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipMemcpyAsync(o.k2t_off, m.k2t_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(o.txn_off, m.ent_off, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(o.txn_off, toff, (n + 1) * 4, hipMemcpyDeviceToHost, st));
         if (m.nkeys) HIPCHK(h, hipMemcpyAsync(o.keys, m.keys, m.nkeys * 8 * kw, hipMemcpyDeviceToHost, st));
         if (m.nk2t) HIPCHK(h, hipMemcpyAsync(o.k2t, m.k2t, m.nk2t * 4, hipMemcpyDeviceToHost, st));
-        if (m.ncap) HIPCHK(h, hipMemcpyAsync(o.txns, m.txns, m.ncap * 4, hipMemcpyDeviceToHost, st));
+        if (nt) HIPCHK(h, hipMemcpyAsync(o.txns, tx, nt * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(h, hipStreamSynchronize(st));
     return AD_OK;

@@ -189,6 +189,10 @@ struct ad_handle {
     bool want_union = false;         // ad_run_pipeline: the deps stage also builds the union view (the merged Deps)
     bool deps_union = false;         // the last deps stage did: deps[2R], deps[2R + 1] are the merged key classes
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
+    bool merged_compacted = false;   // !merged_exact: the exact offsets / lists below are built (merged_compact)
+    uint32_t* mx_off[3] = {};        //   per class: exact TxnId offsets [n + 1]
+    uint32_t* mx_txns[3] = {};       //   and the compacted TxnId lists
+    size_t mx_tot[3] = {};
     bool nh_valid = false;           // nh holds the batch's non-head entries (not after k_seg_fuse)
     bool keys_partial = false;       // k_seg_fuse left ukey / useg to complete_entries (from its tiles)
     size_t sf_ntiles = 0;
@@ -326,6 +330,7 @@ enum Slot : size_t {
     S_CS0, S_CS_END = S_CS0 + 22,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
     S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles
+    S_MXO0, S_MXO_END = S_MXO0 + 3, S_MXT0, S_MXT_END = S_MXT0 + 3, S_MXS,  // union-view merged Deps compacted for fetch
     S_NUM_FIXED,
     S_CSR0 = 320
 };

@@ -170,6 +170,7 @@ int stage_merge(ad_handle* h) {
         h->merged_entries = 0;
         for (int c = 0; c < 2; ++c) h->merged_entries += h->merged[c].nk2t - h->merged[c].nkeys;
         h->merged_exact = false;
+        h->merged_compacted = false;
         h->have_merged = true;
         return AD_OK;
     }
