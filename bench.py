@@ -70,11 +70,13 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False, steps=1):
         # (count: one byte per class out, the first WALK_INL emitted ids per class kept inline: 4 B per entry)
         "k_deps_walk<count>": calls * (W * (46 + C) + 4 * D),
         "k_deps_walk<fill>": calls * (W * (46 + 4 * C) + 4 * D),  # C end slots in, the entries out
-        # the fused tile kernel (gather + elision state + count walk, seg_fuse_kernels.h), a lower bound: every
-        # sorted key read and segment start written (8 B/pair); per query entry (at least the W non-head entries are
-        # gathered) its pair index + 16-byte record read, its position appended to nh, its state written (txn, meta, executeAt + 1, last
-        # always-emitted, two prefix maxima: 33 B), its C count bytes and tx_ts read (8 B); 4 B per emitted id
-        "k_seg_fuse": calls * (P * 8 + W * (8 + 16 + 33 + 8 + C) + 4 * D),
+        # the fused tile kernel (gather + elision state + count walk, seg_fuse_kernels.h): every sorted key read and a
+        # lone entry's segment start written (8 B/pair); per entry of a multi-entry key segment (G = walk_items + the
+        # segments: the heads are the first queries' predecessors) its pair index + 16-byte record read and its state
+        # written (txn, meta, executeAt + 1: 13 B; segment start, last always-emitted, two prefix maxima: 24 B); per
+        # query (W) its C count bytes written and its txn's PreAccept bound read (8 B); 4 B per emitted id.  (Until round
+        # 5 the model priced W gathers only: the G - W head gathers were missing, ~37 MB of C2's 132 MB.)
+        "k_seg_fuse": calls * (P * 8 + (st.get("gather_items") or W) * (4 + 16 + 13 + 24) + W * (C + 8) + 4 * D),
         # the distinct keys from the tile counts (only for the stages that read every key; not in the C2 pipeline):
         # keys re-read (4 B/pair), U = P - W keys and segment starts written (12 B)
         "seg_keys": calls * (P * 4 + (P - W) * 12),

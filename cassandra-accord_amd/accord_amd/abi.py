@@ -141,7 +141,8 @@ class AdStageTimes(C.Structure):
                 ("key_classes", C.c_uint32), ("level_path", C.c_uint32),
                 ("deferred_txns", C.c_uint32), ("fill_items", C.c_uint32),
                 ("deps_speculative", C.c_uint32),
-                ("vitems", C.c_uint64), ("range_entries", C.c_uint64)]
+                ("vitems", C.c_uint64), ("range_entries", C.c_uint64),
+                ("gather_items", C.c_uint32), ("reserved_", C.c_uint32)]
 
 
 def ptr(a, ctype):

@@ -256,13 +256,13 @@ int stage_deps(ad_handle* h) {
         const size_t ntiles = (P + SF_TILE - 1) / SF_TILE;
         SegFuseArgs f{};
         f.P = P; f.ntiles = ntiles; f.skey = h->skey; f.prec = h->prec; f.overflow = fuse_over;
-        CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 4 * ntiles + SF_PARTS));
+        CK(dalloc(h, S_SFLO, &f.tile_lo, ntiles + 1)); CK(dalloc(h, S_SFCNT, &f.tile_cnt, 4 * ntiles + 2 * SF_PARTS));
         f.hpart = f.tile_cnt + 4 * ntiles;
         CK(dalloc(h, S_SFSEC, &f.sec, ntiles * (size_t)SF_SEC + ntiles));
         f.sec_cnt = f.sec + ntiles * (size_t)SF_SEC;
         const bool packed = h->cnt8_cleared == ncb_of(nc);   // k_pack cleared the count bytes and deferred flags
         h->cnt8_cleared = 0;
-        fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, SF_PARTS * 4, 0},
+        fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, 2 * SF_PARTS * 4, 0},
                         {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0}, {packed ? nullptr : h->dfr, n, 0}});
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;

@@ -70,6 +70,7 @@ struct Params {                // device-side batch statistics (filled by k_minm
     unsigned int n_special;                      // key-domain txns that are not Read/Write (sync points,
                                                  // ephemeral reads, local-only): unmanaged execution
     unsigned int range_kinds;                    // bit k: the batch holds a range-domain txn of kind k
+    unsigned int n_multi;                        // key segments with more than one entry (k_seg_fuse batches)
 };
 enum : unsigned { ERR_UNSORTED = 1, ERR_KEYS = 2, ERR_DUPKEY = 4, ERR_KEYORDER = 8, ERR_RANGEORDER = 16,
                   ERR_RANGEBITS = 32, ERR_CAP = 64, ERR_EXECBELOW = 128 };
@@ -195,7 +196,7 @@ static __global__ __launch_bounds__(MM_FINAL_T) void k_minmax_final(int nblk, co
             case 14: out->range_kinds = (unsigned)v; break;
         }
     }
-    if (threadIdx.x == 0) { out->err = 0; out->n_keys_u = 0; out->n_vitems = 0; }
+    if (threadIdx.x == 0) { out->err = 0; out->n_keys_u = 0; out->n_vitems = 0; out->n_multi = 0; }
     if (pub_flag) {
         __syncthreads();
         const uint32_t* pw = reinterpret_cast<const uint32_t*>(out);

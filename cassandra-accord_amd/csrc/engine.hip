@@ -116,10 +116,11 @@ static __global__ __launch_bounds__(128) void k_publish(TotTable t, const Params
         }
         if (ex.hpart && i >= WAVE && i < 2 * WAVE) {
             uint32_t v = 0;
-            for (int x = i - WAVE; x < ex.nparts; x += WAVE) v += ex.hpart[x];
+            uint32_t u = 0;
+            for (int x = i - WAVE; x < ex.nparts; x += WAVE) { v += ex.hpart[x]; u += ex.hpart[ex.nparts + x]; }
 #pragma unroll
-            for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            if (i == WAVE) ex.prm->n_keys_u = v;
+            for (int o = WAVE / 2; o > 0; o >>= 1) { v += __shfl_xor(v, o); u += __shfl_xor(u, o); }
+            if (i == WAVE) { ex.prm->n_keys_u = v; ex.prm->n_multi = u; }   // heads; multi-entry segments
         }
         __syncthreads();
     }
@@ -1481,6 +1482,7 @@ int ad_run_pipeline(ad_handle* h) {
     h->times.level_iterations = h->level_iters;
     h->times.level_edges = h->P;
     h->times.walk_items = (uint32_t)(h->P - (h->P ? h->hprm.n_keys_u : 0));
+    h->times.gather_items = (!h->nh_valid && h->sf_ntiles && h->P) ? h->times.walk_items + h->hprm.n_multi : 0u;
     h->tracer.resolve();
     host_mark(h, "end");
     if (h->host_timers == 1 && h->ht.size() > 1) {

@@ -34,7 +34,7 @@ struct SegFuseArgs {
     const PairRec* prec;
     uint32_t* tile_lo;                         // [ntiles + 1] each tile's first sorted position
     uint32_t* tile_cnt;                        // [4 * ntiles]: heads, non-heads; then their exclusive offsets
-    uint32_t* hpart;                           // [SF_PARTS] head-count partial sums (zeroed)
+    uint32_t* hpart;                           // [2 * SF_PARTS] head-count, then multi-entry-segment partial sums (zeroed)
     uint32_t* sec;                             // [ntiles * SF_SEC]: each tile's multi-entry segments' second entries
     uint32_t* sec_cnt;                         // [ntiles]            (the level chain build's threads)
     uint32_t* overflow;
@@ -171,6 +171,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     if (tid == 0) {
         f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1];
         if (s_cnt[0]) atomicAdd(&f.hpart[b % SF_PARTS], s_cnt[0]);
+        if (s_cnt[4]) atomicAdd(&f.hpart[SF_PARTS + b % SF_PARTS], s_cnt[4]);    // multi-entry segments
         f.sec_cnt[b] = s_cnt[4];
     }
     for (uint32_t x = tid; x < s_cnt[4]; x += SF_T) f.sec[b * (size_t)SF_SEC + x] = lo + s_slist[x];
@@ -188,17 +189,18 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
 // n_keys_u = the tiles' heads (after k_seg_fuse; nothing after an overflow: the host re-runs the batch)
 static __global__ __launch_bounds__(SF_PARTS) void k_seg_heads(const uint32_t* __restrict__ hpart, Params* prm,
                                                               const uint32_t* __restrict__ overflow) {
-    __shared__ uint32_t s_w[SF_PARTS / WAVE];
+    __shared__ uint32_t s_w[SF_PARTS / WAVE], s_m[SF_PARTS / WAVE];
     if (overflow && *(const volatile uint32_t*)overflow) return;
-    uint32_t v = hpart[threadIdx.x];
+    uint32_t v = hpart[threadIdx.x], u = hpart[SF_PARTS + threadIdx.x];
 #pragma unroll
-    for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (__lane_id() == 0) s_w[threadIdx.x / WAVE] = v;
+    for (int o = WAVE / 2; o > 0; o >>= 1) { v += __shfl_xor(v, o); u += __shfl_xor(u, o); }
+    if (__lane_id() == 0) { s_w[threadIdx.x / WAVE] = v; s_m[threadIdx.x / WAVE] = u; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int k = 0; k < SF_PARTS / WAVE; ++k) t += s_w[k];
+        uint32_t t = 0, m = 0;
+        for (int k = 0; k < SF_PARTS / WAVE; ++k) { t += s_w[k]; m += s_m[k]; }
         prm->n_keys_u = t;
+        prm->n_multi = m;
     }
 }
 

@@ -358,6 +358,10 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
                                     /* 0 no, 1 yes and the buffers fit, 2 yes but re-run after sizing  */
     uint64_t vitems;                /* virtual query items of large txns (one per (txn, CFK key))      */
     uint64_t range_entries;         /* RangeDeps entries over all views (part of deps_entries)         */
+    uint32_t gather_items;          /* entries in key segments of more than one entry: the records the */
+                                    /* fused tile kernel (k_seg_fuse) gathers (walk_items + segments);  */
+                                    /* 0 when the batch took the three-kernel path                      */
+    uint32_t reserved_;
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 

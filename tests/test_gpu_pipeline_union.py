@@ -63,3 +63,19 @@ def test_pipeline_union_equals_oracle(engine_factory, name):
     eng.merge()
     assert all(eng.fetch_merged(c).equal(merged[c]) for c in range(abi.NUM_CLASSES))
     assert eng.merged_sizes()[abi.CLASS_KEY].txns == s[abi.CLASS_KEY].txns
+
+
+@pytest.mark.parametrize("name", ["c2", "one_view"])
+def test_gather_items_counts_multi_entry_segments(engine_factory, name):
+    """ad_stage_times.gather_items (k_seg_fuse's gathered records, the byte model's G) == the entries whose key holds
+    more than one entry of the batch; walk_items == those entries minus one per such key."""
+    make, (w, r, d) = CASES[name]
+    b = make()
+    eng = engine_factory(window=w, replicas=r, drop_p=d, seed=0x5EED)
+    eng.load(b)
+    eng.run_pipeline()
+    st = eng.last_times()
+    _, cnt = np.unique(np.asarray(b["keys"]), return_counts=True)
+    multi = cnt[cnt > 1]
+    assert st["gather_items"] == int(multi.sum())
+    assert st["walk_items"] == int(multi.sum()) - len(multi)
