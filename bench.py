@@ -356,7 +356,7 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     "k_range_deps": ("ad::k_range_deps",), "k_union_lds": ("ad::k_union_lds_views", "ad::k_union_lds_small",
                                                              "ad::k_union_lds_list", "ad::k_union_big"),
     # C3's executeAt-block level region (its block sort's radix kernels are shared names and not attributed)
-    "block_levels": ("ad::k_bl_erank", "ad::k_bl_chain_block", "ad::k_bl_bounds", "ad::k_bl_inverse",
+    "block_levels": ("ad::k_bl_erank", "ad::k_bl_tbounds", "ad::k_bl_chain_block", "ad::k_bl_chain_block_tb", "ad::k_bl_bounds", "ad::k_bl_inverse",
                      "ad::k_bl_records", "ad::k_bl_compact", "ad::k_level_blocks", "ad::k_bl_scatter"),
 }
 

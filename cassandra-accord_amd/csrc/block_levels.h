@@ -77,6 +77,40 @@ static __global__ __launch_bounds__(256) void k_bl_chain_block(size_t P, const u
     bv[q] = (uint32_t)q;
     blk[q] = b;
 }
+// The blocks' first executeAt ranks alone (tb of k_bl_bounds, before the block sort): tb[b] = first rank whose entry
+// prefix reaches b * bcap, b = 0..B
+static __global__ __launch_bounds__(256) void k_bl_tbounds(uint32_t B, size_t n, const uint32_t* __restrict__ epre, uint32_t bcap,
+                                                    uint32_t* __restrict__ tb) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > B) return;
+    const uint64_t want = (uint64_t)b * bcap;
+    size_t lo = 0, hi = n;
+    while (lo < hi) { const size_t m = (lo + hi) >> 1; if (epre[m] < want) lo = m + 1; else hi = m; }
+    tb[b] = (uint32_t)lo;
+}
+// k_bl_chain_block with the block found from the txn's executeAt rank among the blocks' first ranks (tb, in LDS)
+// instead of a second random read (epre[rank]), and the txn's index inside its block kept per chain position (tl:
+// k_bl_records reads it in chain order instead of gathering erank again).  One random read per entry (erank of its
+// txn) where there were three.
+constexpr int BL_TB_LDS = 8192;               // blocks + 1 held in LDS (32 KB)
+static __global__ __launch_bounds__(256) void k_bl_chain_block_tb(size_t P, uint32_t B, const uint32_t* __restrict__ c_txn,
+                                                           const uint32_t* __restrict__ erank, const uint32_t* __restrict__ tb,
+                                                           uint32_t* __restrict__ bk, uint32_t* __restrict__ bv,
+                                                           uint32_t* __restrict__ blk, uint32_t* __restrict__ tl) {
+    __shared__ uint32_t s_tb[BL_TB_LDS];
+    for (uint32_t x = threadIdx.x; x <= B; x += blockDim.x) s_tb[x] = tb[x];
+    __syncthreads();
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < P; q += stride) {
+        const uint32_t r = erank[c_txn[q]];
+        uint32_t lo = 0, hi = B;                    // the last block whose first rank is <= r
+        while (lo < hi) { const uint32_t m = (lo + hi + 1) >> 1; if (s_tb[m] <= r) lo = m; else hi = m - 1; }
+        bk[q] = lo;
+        bv[q] = (uint32_t)q;
+        blk[q] = lo;
+        tl[q] = r - s_tb[lo];
+    }
+}
 // tb[b] = first executeAt rank of block b, boff[b] = first slot of block b (b = 0..B)
 static __global__ __launch_bounds__(256) void k_bl_bounds(uint32_t B, size_t n, size_t P, const uint32_t* __restrict__ epre, uint32_t bcap,
                                                    const uint32_t* __restrict__ sk, uint32_t* __restrict__ tb, uint32_t* __restrict__ boff) {
@@ -121,11 +155,13 @@ static __global__ __launch_bounds__(256) void k_bl_inverse(size_t P, const uint3
 // its key's first position (else q heads its key's run in the block); symmetrically for the last entry.  Walking the
 // block-sorted slots instead made ~10 dependent random reads per entry (seg_start / c_txn / erank / epre of q and of
 // both neighbours): 1.36 GB fetched per C3 launch for 4M entries.
+// (tlq != nullptr: the txn-in-block index per chain position from k_bl_chain_block_tb; else erank[c_txn[q]] - tb[b])
 static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint32_t* __restrict__ blk, const uint32_t* __restrict__ inv,
                                                     const uint32_t* __restrict__ c_txn, const uint8_t* __restrict__ c_meta,
                                                     const int32_t* __restrict__ seg_start, const uint32_t* __restrict__ erank,
                                                     const uint32_t* __restrict__ tb, const uint32_t* __restrict__ boff,
-                                                    uint64_t* __restrict__ rec, uint32_t* __restrict__ bad) {
+                                                    uint64_t* __restrict__ rec, uint32_t* __restrict__ bad,
+                                                    const uint32_t* __restrict__ tlq = nullptr) {
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool b_ = false;
     if (q < P) {
@@ -138,7 +174,7 @@ static __global__ __launch_bounds__(256) void k_bl_records(size_t P, const uint3
         const uint32_t bnext = next_same_key ? blk[q + 1] : 0u;
         const bool head = first_of_key || bprev != b;
         const bool last = !next_same_key || bnext != b;
-        const uint32_t tl = erank[c_txn[q]] - tb[b];
+        const uint32_t tl = tlq ? tlq[q] : erank[c_txn[q]] - tb[b];
         b_ = tl > BL_TL || j - boff[b] >= (uint32_t)BL_CAP;
         uint64_t fl = (uint64_t)(tl & BL_TL) | ((uint64_t)(meta_kind(c_meta[q]) == AD_KIND_WRITE) << BL_SH_W) |
                       ((uint64_t)head << BL_SH_HEAD) | ((uint64_t)last << BL_SH_LAST);
@@ -777,6 +813,7 @@ struct BlockBufs {                             // grow-only, owned by LevelState
     uint64_t* rec = nullptr;                   // [P]
     uint32_t *epre = nullptr, *erank = nullptr, *bk = nullptr, *bv = nullptr, *bk2 = nullptr, *bv2 = nullptr;
     uint32_t *tb = nullptr, *boff = nullptr, *stats = nullptr, *rs = nullptr, *mt = nullptr, *lcnt = nullptr;
+    uint32_t* tl = nullptr;                    // [P] txn-in-block index per chain position (k_bl_chain_block_tb)
     uint64_t* la = nullptr;                    // [P] per block: ring-sourced singleton runs (k_bl_compact)
     uint32_t* lb = nullptr;                    // [P] per block: ring-continuing singleton runs
     int2* carry = nullptr;
@@ -787,7 +824,7 @@ struct BlockBufs {                             // grow-only, owned by LevelState
 
 inline void free_block_bufs(BlockBufs& b) {
     void* ps[] = {b.rec, b.epre, b.erank, b.bk, b.bv, b.bk2, b.bv2, b.tb, b.boff, b.stats, b.rs, b.carry, b.crec, b.mt,
-                  b.lcnt, b.la, b.lb};
+                  b.lcnt, b.la, b.lb, b.tl};
     for (void* p : ps) if (p) hipFree(p);
     b = BlockBufs{};
 }

@@ -1771,11 +1771,12 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
     const uint32_t bcap = BL_CAP - 16;         // n_large == 0: at most 16 keys per txn
     const size_t B = P / bcap + 2;             // upper bound on blocks (the entry prefix counts key-less txns too)
     const size_t Bmax = (P + n) / bcap + 2;
-    if (bb.capP < P || !bb.rec) {
+    if (bb.capP < P || !bb.rec || !bb.tl) {
         const size_t c = std::max<size_t>(P, 1);
         if (!grow((void**)&bb.rec, c * 8) || !grow((void**)&bb.bk, c * 4) || !grow((void**)&bb.bv, c * 4) ||
             !grow((void**)&bb.bk2, c * 4) || !grow((void**)&bb.bv2, c * 4) || !grow((void**)&bb.carry, c * 8) ||
-            !grow((void**)&bb.crec, c * 16) || !grow((void**)&bb.la, c * 8) || !grow((void**)&bb.lb, c * 4))
+            !grow((void**)&bb.crec, c * 16) || !grow((void**)&bb.la, c * 8) || !grow((void**)&bb.lb, c * 4) ||
+            !grow((void**)&bb.tl, c * 4))
             goto oom;
         bb.capP = c;
     }
@@ -1829,7 +1830,14 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         }
         const uint32_t nb = etot / bcap + 1;
         bb.nblocks = nb;
-        k_bl_chain_block<<<gP, 256, 0, st>>>(P, ls.c_txn, bb.erank, bb.epre, bcap, bb.bk, bb.bv, bb.lb);   // lb: free until compact
+        const uint32_t* tlq = nullptr;           // lb: free until compact
+        if (nb + 1 <= (uint32_t)BL_TB_LDS) {
+            k_bl_tbounds<<<ceil_div((long)nb + 1, 256), 256, 0, st>>>(nb, n, bb.epre, bcap, bb.tb);
+            k_bl_chain_block_tb<<<std::min(gP, 2048), 256, 0, st>>>(P, nb, ls.c_txn, bb.erank, bb.tb, bb.bk, bb.bv, bb.lb, bb.tl);
+            tlq = bb.tl;
+        } else {
+            k_bl_chain_block<<<gP, 256, 0, st>>>(P, ls.c_txn, bb.erank, bb.epre, bcap, bb.bk, bb.bv, bb.lb);
+        }
         RadixScratch rs;
         const size_t hl = radix_hist_len(P);
         rs.hist = bb.rs;
@@ -1842,7 +1850,7 @@ inline int run_block_levels(LevelState& ls, BlockBufs& bb, const LevelInputs& in
         uint32_t* inv = sk == bb.bk ? bb.bk2 : bb.bk;         // the sort's free ping-pong buffer
         k_bl_inverse<<<gP, 256, 0, st>>>(P, sv, inv);
         k_bl_records<<<gP, 256, 0, st>>>(P, bb.lb, inv, ls.c_txn, ls.c_meta, in.seg_start, bb.erank, bb.tb, bb.boff, bb.rec,
-                                         bb.stats + BL_STAT_RECORDS_BAD);
+                                         bb.stats + BL_STAT_RECORDS_BAD, tlq);
         k_bl_compact<<<nb, BL_T, 0, st>>>(nb, bb.boff, bb.rec, bb.crec, bb.mt, bb.la, bb.lb, bb.lcnt);
         // 4. the walk (packed scan words: 32-bit while every level fits 20 bits)
         // (no carry initialisation: a head reads a global carry only from a producer flagged to store it)
