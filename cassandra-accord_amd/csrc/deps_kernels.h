@@ -214,6 +214,15 @@ static __global__ __launch_bounds__(MM_FINAL_T) void k_minmax_final(int nblk, co
 // shuffle search over the lanes' key offsets), so the per-pair stores (record, sort key / value, the deps stage's
 // count words) are coalesced runs.  One thread writing its own txn's 4 pairs left each store instruction a 64-byte
 // stride across the wave: 2.2x the written bytes at the memory side and ~70 % of the wave cycles issue-stalled.
+// Device-side plan (PackPlan.dprm != null): the packing parameters, the key base and the count words per pair from
+// the Params k_minmax_final wrote, as stage_prepare derives them on the host -- so k_pack is enqueued right behind the
+// reduce and the host reads the Params while it runs (the host's wait no longer sits between the two kernels).
+struct PackPlan {
+    const Params* dprm;                        // null: pk / key_min / ncw as given
+    int nv_small, nv_large;                    // views when the batch has no / some large txns (the union view)
+    int has_keys;
+};
+__device__ inline int dbits_of(uint64_t x) { return x == 0 ? 0 : 64 - __clzll((long long)x); }
 static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_min,
                                               const uint64_t* __restrict__ tm, const uint64_t* __restrict__ tl,
                                               const int32_t* __restrict__ tn, const uint64_t* __restrict__ em,
@@ -224,9 +233,25 @@ static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64
                                               uint64_t* __restrict__ tx_ts, uint64_t* __restrict__ ex1,
                                               uint8_t* __restrict__ meta, PairRec* __restrict__ prec,
                                               uint32_t* __restrict__ skey, uint32_t* __restrict__ sval, Params* prm,
-                                              uint32_t* __restrict__ cnt_words, int ncw, uint8_t* __restrict__ dfr) {
+                                              uint32_t* __restrict__ cnt_words, int ncw, uint8_t* __restrict__ dfr,
+                                              PackPlan plan = PackPlan{nullptr, 0, 0, 0}) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = __lane_id();
+    if (plan.dprm) {
+        const Params& p = *plan.dprm;
+        const int MB = dbits_of(p.msb_max - p.msb_min), HB = dbits_of(p.hlc_max - p.hlc_min);
+        const int NB = dbits_of((uint64_t)(p.node_max_b - p.node_min_b));
+        pk.msb_min = p.msb_min;
+        pk.hlc_min = p.hlc_min;
+        pk.node_min = (int64_t)(int32_t)(p.node_min_b ^ 0x80000000u);
+        pk.sh_flags = (uint32_t)NB;
+        pk.sh_hlc = (uint32_t)(NB + 4);
+        pk.sh_msb = (uint32_t)(NB + 4 + HB);
+        pk.total_bits = (uint32_t)(NB + 4 + HB + MB);   // > 63: the host refuses the batch after its read
+        key_min = plan.has_keys ? p.key_min : 0ull;
+        const int nv = p.n_large == 0 ? plan.nv_small : plan.nv_large;
+        ncw = ncb_of(p.n_special > 0 ? 2 * nv : nv) / 4;
+    }
     const size_t t0 = i - (size_t)lane;                 // the wave's first txn
     if (t0 >= n) return;                                // whole wave past the batch (waves stay converged below)
     const bool live = i < n;

@@ -234,15 +234,32 @@ int check_params(ad_handle* h) {
 int stage_prepare(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     hipStream_t st = h->st;
+    h->pack_enqueued = false;
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
         KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
         k_minmax<<<g, 256, 0, st>>>(n, h->tm, h->tl, h->tn, h->em, h->el, h->en, h->key_off, h->keys, P, h->range_s, h->range_e, Q, partial);
         if (pub_ready(h) == AD_OK) {
-            // the reduce publishes the Params itself: no k_publish launch between it and the host's read
+            // the reduce publishes the Params itself: no k_publish launch between it and the host's read; k_pack
+            // follows at once and derives its parameters from the device Params (PackPlan), the host reads them
+            // while it runs
             const uint32_t seq = ++h->pub_seq;
             k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm, h->pub_dev, h->pub_dev + PUB_PRM, seq);
+            if (n > 0) {
+                bool uni_small = false;
+                const uint32_t nl = h->n_large;
+                h->n_large = 0;                                  // the plan as if no large txn: the union view's rule
+                deps_class_plan(h, h->want_union, &uni_small);
+                h->n_large = nl;
+                PackPlan plan{h->prm, (int)h->cfg.replicas + (uni_small ? 1 : 0), (int)h->cfg.replicas, P ? 1 : 0};
+                KScope ks(K_PACK, n);
+                k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, TsPack{}, 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
+                                                                h->status, h->key_off, h->keys, Q ? h->range_off : nullptr,
+                                                                h->range_s, h->range_e, h->tx_ts, h->ex1, h->meta, h->prec,
+                                                                h->ka, h->va, h->prm, (uint32_t*)h->cnt8, 0, h->dfr, plan);
+                h->pack_enqueued = true;
+            }
             CK(wait_totals(h, seq, 0, nullptr));
         } else {
             k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm);
@@ -270,6 +287,10 @@ int stage_prepare(ad_handle* h) {
     // by a fill launch of their own
     const int ncb = ncb_of(deps_class_plan(h, h->want_union, nullptr));
     h->cnt8_cleared = ncb;
+    if (h->pack_enqueued) {                      // k_pack already runs on the device Params (the same plan)
+        h->pack_enqueued = false;
+        return AD_OK;
+    }
     KScope ks(K_PACK, n);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
