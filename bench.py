@@ -328,6 +328,10 @@ def roofline_of(eng, dom, n, P, st, large=False, pmc=True, steps=1):
     # the committed PMC passes (profiles/collect.sh) run the default C2 bench, C3 (pmc="c3") and C4 (pmc="c4"); the
     # sharded lines report no traffic
     traffic, src = pmc_traffic(dom, pmc if pmc in ("c3", "c4") else "") if pmc else (None, None)
+    if traffic is not None and not isinstance(ROCPROF_NAME.get(dom), str) and calls > steps:
+        # a composite region's PMC bytes are per pipeline step; the line's figures are per region launch (C4's vitems
+        # region runs several launches per step)
+        traffic = traffic * steps / calls
     return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "alg_bytes_per_launch": ab / calls, "avg_launch_ms": ms / calls, "launches": calls}
