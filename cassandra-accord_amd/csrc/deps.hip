@@ -262,8 +262,11 @@ int stage_deps(ad_handle* h) {
         f.sec_cnt = f.sec + ntiles * (size_t)SF_SEC;
         const bool packed = h->cnt8_cleared == ncb_of(nc);   // k_pack cleared the count bytes and deferred flags
         h->cnt8_cleared = 0;
-        fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, 2 * SF_PARTS * 4, 0},
-                        {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0}, {packed ? nullptr : h->dfr, n, 0}});
+        const bool small = h->small_cleared;                  // ... and the small counters (pack_clear_list)
+        h->small_cleared = false;
+        if (!(packed && small))
+            fill_multi(st, {{fovf_count, 8, 0}, {dtx_count, 12, 0}, {f.hpart, 2 * SF_PARTS * 4, 0},
+                            {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0}, {packed ? nullptr : h->dfr, n, 0}});
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;
         { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
@@ -275,6 +278,7 @@ int stage_deps(ad_handle* h) {
         h->nh_valid = true;
         const bool packed = h->cnt8_cleared == ncb_of(nc);
         h->cnt8_cleared = 0;
+        h->small_cleared = false;
         fill_multi(st, {{fovf_count, 4, 0}, {dtx_count, 12, 0}, {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0},
                         {packed ? nullptr : h->dfr, n, 0}});
         launch_walk_nv(nv, wa, false, direct, true, st);

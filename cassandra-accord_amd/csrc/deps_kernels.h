@@ -221,6 +221,8 @@ struct PackPlan {
     const Params* dprm;                        // null: pk / key_min / ncw as given
     int nv_small, nv_large;                    // views when the batch has no / some large txns (the union view)
     int has_keys;
+    uint32_t* clr[3];                          // small counters the deps stage needs zeroed (block 0 clears them:
+    int clr_words[3];                          // no fill launch between the sort and k_seg_fuse)
 };
 __device__ inline int dbits_of(uint64_t x) { return x == 0 ? 0 : 64 - __clzll((long long)x); }
 static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_min,
@@ -234,9 +236,12 @@ static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64
                                               uint8_t* __restrict__ meta, PairRec* __restrict__ prec,
                                               uint32_t* __restrict__ skey, uint32_t* __restrict__ sval, Params* prm,
                                               uint32_t* __restrict__ cnt_words, int ncw, uint8_t* __restrict__ dfr,
-                                              PackPlan plan = PackPlan{nullptr, 0, 0, 0}) {
+                                              PackPlan plan = PackPlan{}) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = __lane_id();
+    if (blockIdx.x == 0)
+        for (int c = 0; c < 3; ++c)
+            for (int x = threadIdx.x; x < plan.clr_words[c]; x += blockDim.x) plan.clr[c][x] = 0u;
     if (plan.dprm) {
         const Params& p = *plan.dprm;
         const int MB = dbits_of(p.msb_max - p.msb_min), HB = dbits_of(p.hlc_max - p.hlc_min);

@@ -231,10 +231,25 @@ int check_params(ad_handle* h) {
 // ---------------------------------------------------------------------------------------------------
 // prepare + sort
 // ---------------------------------------------------------------------------------------------------
+// The deps stage's small counters (totals words: k_txn_finish's overflow rows + the fused kernel's overflow flag, the
+// deferred txns / fill items / heavy hint) and k_seg_fuse's partial sums, zeroed by k_pack's first block: the deps
+// stage then needs no fill launch before k_seg_fuse (deps.hip reads small_cleared).
+static int pack_clear_list(ad_handle* h, PackPlan& plan) {
+    const size_t ntiles = (h->P + SF_TILE - 1) / SF_TILE;
+    uint32_t* tile_cnt = nullptr;
+    CK(dalloc(h, S_SFCNT, &tile_cnt, 4 * ntiles + 2 * SF_PARTS));
+    plan.clr[0] = h->totd + MAX_TOTALS - 7; plan.clr_words[0] = 2;
+    plan.clr[1] = h->totd + MAX_TOTALS - 3; plan.clr_words[1] = 3;
+    plan.clr[2] = tile_cnt + 4 * ntiles;    plan.clr_words[2] = 2 * SF_PARTS;
+    h->small_cleared = true;
+    return AD_OK;
+}
+
 int stage_prepare(ad_handle* h) {
     const size_t n = h->n, P = h->P, Q = h->Q;
     hipStream_t st = h->st;
     h->pack_enqueued = false;
+    h->small_cleared = false;
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
         KScope ks(K_MINMAX, n);
@@ -252,7 +267,8 @@ int stage_prepare(ad_handle* h) {
                 h->n_large = 0;                                  // the plan as if no large txn: the union view's rule
                 deps_class_plan(h, h->want_union, &uni_small);
                 h->n_large = nl;
-                PackPlan plan{h->prm, (int)h->cfg.replicas + (uni_small ? 1 : 0), (int)h->cfg.replicas, P ? 1 : 0};
+                PackPlan plan{h->prm, (int)h->cfg.replicas + (uni_small ? 1 : 0), (int)h->cfg.replicas, P ? 1 : 0, {}, {}};
+                CK(pack_clear_list(h, plan));
                 KScope ks(K_PACK, n);
                 k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, TsPack{}, 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                                 h->status, h->key_off, h->keys, Q ? h->range_off : nullptr,
@@ -291,11 +307,13 @@ int stage_prepare(ad_handle* h) {
         h->pack_enqueued = false;
         return AD_OK;
     }
+    PackPlan plan{};
+    CK(pack_clear_list(h, plan));
     KScope ks(K_PACK, n);
     k_pack<<<ceil_div((long)n, 256), 256, 0, st>>>(n, h->pack, P ? p.key_min : 0, h->tm, h->tl, h->tn, h->em, h->el, h->en,
                                                     h->status, h->key_off, h->keys, Q ? h->range_off : nullptr, h->range_s,
                                                     h->range_e, h->tx_ts, h->ex1, h->meta, h->prec, h->ka, h->va, h->prm,
-                                                    (uint32_t*)h->cnt8, ncb / 4, h->dfr);
+                                                    (uint32_t*)h->cnt8, ncb / 4, h->dfr, plan);
     return AD_OK;
 }
 

@@ -189,6 +189,7 @@ struct ad_handle {
     bool want_union = false;         // ad_run_pipeline: the deps stage also builds the union view (the merged Deps)
     bool deps_union = false;         // the last deps stage did: deps[2R], deps[2R + 1] are the merged key classes
     bool pack_enqueued = false;      // stage_prepare: k_pack launched on the device Params (PackPlan)
+    bool small_cleared = false;      // k_pack zeroed the deps stage's small counters (pack_clear_list)
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
     bool merged_compacted = false;   // !merged_exact: the exact offsets / lists below are built (merged_compact)
     uint32_t* mx_off[3] = {};        //   per class: exact TxnId offsets [n + 1]
