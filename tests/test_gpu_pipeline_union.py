@@ -79,3 +79,21 @@ def test_gather_items_counts_multi_entry_segments(engine_factory, name):
     multi = cnt[cnt > 1]
     assert st["gather_items"] == int(multi.sum())
     assert st["walk_items"] == int(multi.sum()) - len(multi)
+
+
+def test_speculative_key_sort_across_key_spreads(engine_factory):
+    """stage_prepare sorts the keys right behind k_pack with the previous batch's key spread, before reading this
+    batch's Params: a wider spread (more 8-bit passes) must redo the sort, a narrower one keeps it (an extra pass
+    over an all-zero digit).  One handle, batches of 10-, 24-, 10- and 17-bit key spreads, each == the oracle."""
+    eng = engine_factory(window=16, replicas=3, drop_p=0.1, seed=0x5EED)
+    for i, keyspace in enumerate((1000, 10_000_000, 1000, 100_000)):
+        b = workload.generate(20000, keys_per_txn=3, keyspace=keyspace, seed=40 + i)
+        eng.load(b)
+        eng.run_pipeline()
+        ref = O.OracleResult(b, abi.make_config(16, 3, 0.1, 0x5EED), O.FLAG_MERGE | O.FLAG_LEVELS)
+        for c in (abi.CLASS_KEY, abi.CLASS_DIRECT_KEY):
+            got = eng.fetch_rows(3, c, 0, b["n"])
+            assert got.equal(ref.merged(c)), "batch %d (keyspace %d) merged class %d" % (i, keyspace, c)
+        lv, order = eng.fetch_levels()
+        rlv, rorder = ref.levels()
+        assert np.array_equal(lv, rlv) and np.array_equal(order, rorder), "batch %d levels" % i
