@@ -269,12 +269,22 @@ int stage_deps(ad_handle* h) {
                             {packed ? nullptr : h->cnt8, (size_t)ncb_of(nc) * P, 0}, {packed ? nullptr : h->dfr, n, 0}});
         f.e_txn = h->e_txn; f.e_meta = h->e_meta; f.e_exec1 = h->e_exec1; f.seg_start = h->seg_start; f.ud_prev = h->ud_prev;
         f.pm_w = h->pm_w; f.pm_c = h->pm_c;
+        // the pull pass's chains from the tile's LDS copy (k_pack zeroed succ and the level flags): key Read/Write
+        // batches only (no sync points: the pull pass's own condition)
+        if (h->chains_pending && !direct && h->n_large == 0 && h->n_special == 0) {
+            f.c_txn = h->ls.c_txn; f.c_meta = h->ls.c_meta; f.c_exec1 = h->ls.c_exec1; f.c_pair = h->ls.c_pair;
+            f.succ = h->ls.succ; f.any_long = h->ls.flags + 7; f.any_far = h->ls.flags + 18;
+            h->chains_prebuilt = true;
+        }
+        h->chains_pending = false;
         { KScope ks(K_SEG_FUSE, P); launch_seg_fuse_nv(nv, f, wa, direct, st); }
         fuse_hpart = f.hpart;              // n_keys_u: summed by the deps publish (PubExtra)
         h->nh_valid = false;               // no dense non-head list: the level chain build runs over every position
         h->keys_partial = true;            // ukey / useg on demand (complete_entries)
         h->sf_ntiles = ntiles;
     } else {
+        h->chains_pending = false;
+        h->chains_prebuilt = false;
         h->nh_valid = true;
         const bool packed = h->cnt8_cleared == ncb_of(nc);
         h->cnt8_cleared = 0;

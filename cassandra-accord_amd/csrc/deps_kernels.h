@@ -221,8 +221,10 @@ struct PackPlan {
     const Params* dprm;                        // null: pk / key_min / ncw as given
     int nv_small, nv_large;                    // views when the batch has no / some large txns (the union view)
     int has_keys;
-    uint32_t* clr[3];                          // small counters the deps stage needs zeroed (block 0 clears them:
-    int clr_words[3];                          // no fill launch between the sort and k_seg_fuse)
+    uint32_t* clr[4];                          // small counters the deps stage needs zeroed (block 0 clears them:
+    int clr_words[4];                          // no fill launch between the sort and k_seg_fuse)
+    uint2* succ;                               // per pair: the pull pass's predecessor words, zeroed (k_seg_fuse builds
+                                               // the chains in ad_run_pipeline: LevelInputs.chains_prebuilt)
 };
 __device__ inline int dbits_of(uint64_t x) { return x == 0 ? 0 : 64 - __clzll((long long)x); }
 static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64_t key_min,
@@ -240,7 +242,7 @@ static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = __lane_id();
     if (blockIdx.x == 0)
-        for (int c = 0; c < 3; ++c)
+        for (int c = 0; c < 4; ++c)
             for (int x = threadIdx.x; x < plan.clr_words[c]; x += blockDim.x) plan.clr[c][x] = 0u;
     if (plan.dprm) {
         const Params& p = *plan.dprm;
@@ -312,6 +314,7 @@ static __global__ __launch_bounds__(256) void k_pack(size_t n, TsPack pk, uint64
             skey[p] = (uint32_t)(k - key_min);
             sval[p] = p;
             for (int w = 0; w < ncw; ++w) cnt_words[(size_t)p * ncw + w] = 0u;     // the deps stage's count bytes
+            if (plan.succ) plan.succ[p] = make_uint2(0u, 0u);
         }
     }
     if (err) atomicOr(&prm->err, err);

@@ -242,6 +242,17 @@ static int pack_clear_list(ad_handle* h, PackPlan& plan) {
     plan.clr[1] = h->totd + MAX_TOTALS - 3; plan.clr_words[1] = 3;
     plan.clr[2] = tile_cnt + 4 * ntiles;    plan.clr_words[2] = 2 * SF_PARTS;
     h->small_cleared = true;
+    // ad_run_pipeline on a key-only batch whose levels will try the pull pass first: its succ words and flags zeroed
+    // here too, so k_seg_fuse can build the chains (stage_deps decides; run_levels then skips k_chain_build)
+    const bool pull = h->want_union && h->P > 0 && h->Q == 0 && !h->ls.long_hint && !h->no_fused_chains &&
+                      h->level_mode != AD_LEVELS_FIXPOINT && h->level_mode != AD_LEVELS_BLOCKS &&
+                      h->level_mode != AD_LEVELS_BLOCKS_WIDE && h->level_mode != AD_LEVELS_KAHN && !h->hist_active;
+    if (pull) {
+        if (!ls_reserve_chains(h->ls, h->P, h->st)) return set_err(h, AD_ERR_NOMEM, "exec levels: out of device memory");
+        plan.clr[3] = h->ls.flags; plan.clr_words[3] = 32;
+        plan.succ = h->ls.succ;
+        h->chains_pending = true;
+    }
     return AD_OK;
 }
 
@@ -250,6 +261,8 @@ int stage_prepare(ad_handle* h) {
     hipStream_t st = h->st;
     h->pack_enqueued = false;
     h->small_cleared = false;
+    h->chains_pending = false;
+    h->chains_prebuilt = false;
     const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
         KScope ks(K_MINMAX, n);

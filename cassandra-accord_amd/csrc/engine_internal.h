@@ -190,6 +190,9 @@ struct ad_handle {
     bool deps_union = false;         // the last deps stage did: deps[2R], deps[2R + 1] are the merged key classes
     bool pack_enqueued = false;      // stage_prepare: k_pack launched on the device Params (PackPlan)
     bool small_cleared = false;      // k_pack zeroed the deps stage's small counters (pack_clear_list)
+    bool chains_pending = false;     // k_pack zeroed the pull pass's succ words and flags (ad_run_pipeline)
+    bool chains_prebuilt = false;    // k_seg_fuse built the pull pass's chains (LevelInputs.chains_prebuilt)
+    bool no_fused_chains = getenv("AD_NO_FUSED_CHAINS") != nullptr;   // A/B switch
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
     bool merged_compacted = false;   // !merged_exact: the exact offsets / lists below are built (merged_compact)
     uint32_t* mx_off[3] = {};        //   per class: exact TxnId offsets [n + 1]

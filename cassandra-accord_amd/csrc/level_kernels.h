@@ -592,18 +592,16 @@ __device__ inline void chain_build_regs(size_t s, int len, const uint32_t* __res
 // predecessors (indeg) and a backward pass gives its successor run (succ[pair]).  Single-entry segments
 // have no edges and are skipped; a segment longer than SHORT_SEG raises *any_long and the caller falls
 // back to the fixpoint (whose chain preparation handles long chains).
-// The chain of the key segment whose second entry is s2 (s2 = 0 or not a second entry: nothing).
-__device__ inline void chain_build_seg(size_t P, size_t s2, const int32_t* __restrict__ seg_start,
-                                       const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
-                                       const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
-                                       uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
-                                       uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
-                                       uint32_t* __restrict__ indeg, uint2* __restrict__ succ, int full, int pred_mode,
-                                       bool& lng, bool& far) {
-    const size_t s = s2 - 1;
-    if (s2 > 0 && seg_start[s2] == (int32_t)s) {
-        size_t end = s + 2;
-        while (end < P && seg_start[end] == (int32_t)s && end - s <= SHORT_SEG) ++end;
+// The chain of the key segment [s, end) (sorted positions; e_* may point into LDS: k_seg_fuse builds the chains of
+// its tile's segments from its LDS copy).
+__device__ inline void chain_build_range(size_t s, size_t end,
+                                         const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                         const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                         uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                         uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
+                                         uint32_t* __restrict__ indeg, uint2* __restrict__ succ, int full, int pred_mode,
+                                         bool& lng, bool& far) {
+    {
         if (end - s > SHORT_SEG) {
             lng = true;
         } else if (end - s <= CB_REG) {
@@ -660,6 +658,22 @@ __device__ inline void chain_build_seg(size_t P, size_t s2, const int32_t* __res
                 succ[c_pair[q]] = sc;
             }
         }
+    }
+}
+// The chain of the key segment whose second entry is s2 (s2 = 0 or not a second entry: nothing).
+__device__ inline void chain_build_seg(size_t P, size_t s2, const int32_t* __restrict__ seg_start,
+                                       const uint32_t* __restrict__ e_txn, const uint8_t* __restrict__ e_meta,
+                                       const uint64_t* __restrict__ e_exec1, const uint32_t* __restrict__ sval,
+                                       uint32_t* __restrict__ c_txn, uint8_t* __restrict__ c_meta,
+                                       uint64_t* __restrict__ c_exec1, uint32_t* __restrict__ c_pair,
+                                       uint32_t* __restrict__ indeg, uint2* __restrict__ succ, int full, int pred_mode,
+                                       bool& lng, bool& far) {
+    const size_t s = s2 - 1;
+    if (s2 > 0 && seg_start[s2] == (int32_t)s) {
+        size_t end = s + 2;
+        while (end < P && seg_start[end] == (int32_t)s && end - s <= SHORT_SEG) ++end;
+        chain_build_range(s, end, e_txn, e_meta, e_exec1, sval, c_txn, c_meta, c_exec1, c_pair, indeg, succ, full,
+                          pred_mode, lng, far);
     }
 }
 
@@ -1480,6 +1494,25 @@ struct LevelState {
 
 // The buffers order_rows needs for m rows (run_levels sizes them too; callers ordering rows without a
 // run_levels pass on the handle reserve them here).
+// The chain buffers of the pull pass (capP group) and the flags, before the deps stage: k_seg_fuse builds the pull
+// pass's chains from its LDS copy in ad_run_pipeline (LevelInputs.chains_prebuilt); run_levels finds them reserved.
+inline bool ls_reserve_chains(LevelState& ls, size_t P, hipStream_t st) {
+    auto grow = [&](void** p, size_t bytes) -> bool {
+        if (*p) { hipStreamSynchronize(st); hipFree(*p); *p = nullptr; }
+        return hipMalloc(p, bytes) == hipSuccess;
+    };
+    if (ls.capP < P || !ls.c_txn) {
+        const size_t c = std::max<size_t>(P, 1);
+        if (!grow((void**)&ls.c_txn, c * 4) || !grow((void**)&ls.c_meta, c) || !grow((void**)&ls.c_exec1, c * 8) ||
+            !grow((void**)&ls.pm_all, c * 4) || !grow((void**)&ls.c_pair, c * 4) || !grow((void**)&ls.succ, c * 8) ||
+            !grow((void**)&ls.pair_seg, c * 4) || !grow((void**)&ls.seg_len, c * 4) || !grow((void**)&ls.stamp, c * 4) ||
+            !grow((void**)&ls.heads, c * 4) || !grow((void**)&ls.long_pos, c * 4))
+            return false;
+        ls.capP = c;
+    }
+    if (!ls.flags && !grow((void**)&ls.flags, 256)) return false;
+    return true;
+}
 inline bool ls_reserve_order(LevelState& ls, size_t m, hipStream_t st) {
     auto grow = [&](void** p, size_t bytes) -> bool {
         if (*p) { hipStreamSynchronize(st); hipFree(*p); *p = nullptr; }
@@ -1540,6 +1573,8 @@ struct LevelInputs {
     uint32_t exec_bits;
     int keep_levels;                     // sharded rounds: start from the given levels, reuse the chains
     int kahn_ok;                         // single-store batch: the Kahn wavefront may replace the fixpoint
+    int chains_prebuilt = 0;             // k_seg_fuse built the pull pass's chains (succ, c_txn, flags 7 / 18) and k_pack
+                                         // zeroed succ and the flags before it: the pull pass skips k_chain_build
     int force_blocks;                    // pure key-chain batches: executeAt blocks even for short chains (tests)
     int wide_words;                      // block path: 64-bit scan words even for batches of <= 2^20 txns (tests)
     int (*complete)(void*);              // nullable: fills in every sorted entry before a path other than the pull pass
@@ -1942,8 +1977,9 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
         const bool pull_try = in.kahn_ok && !in.keep_levels && P > 0 && !ls.pull_off && in.n_large == 0 && in.n_special == 0 &&
                               !(in.merged_direct && in.merged_direct->ncap > 0) && !(in.merged_range && in.merged_range->ncap > 0);
         // (and the pull path's order: its collision sentinel, order_rows prefilled)
-        fill_multi(st, {{ls.flags, 128, 0}, {in.keep_levels ? nullptr : in.lvl, std::max<size_t>(n, 1) * 4, 0},
-                        {pull_try ? ls.succ : nullptr, P * 8, 0}, {pull_try ? ls.sv0 : nullptr, n * 4, 0xFF}});
+        const bool pre = in.chains_prebuilt && pull_try;
+        fill_multi(st, {{pre ? nullptr : ls.flags, 128, 0}, {in.keep_levels ? nullptr : in.lvl, std::max<size_t>(n, 1) * 4, 0},
+                        {pull_try && !pre ? ls.succ : nullptr, P * 8, 0}, {pull_try ? ls.sv0 : nullptr, n * 4, 0xFF}});
         // local-only txns are key-domain specials (n_special): a pull batch has none
         if (n > 0 && !pull_try) k_level_kinds<<<ceil_div((long)n, 256), 256, 0, st>>>(n, in.meta, ls.flags + 5);
     }
@@ -2040,9 +2076,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 KScope ks(K_KAHN, P);
                 const int gn = ceil_div((long)n, 256);
                 // predecessor runs zeroed above; ls.flags [16] abort, [17] max level, [18] far pred (zeroed above)
-                k_chain_build<<<cb_grid, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
-                                                  ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1,
-                                                  ls.flags + 18, in.sec, in.sec_cnt, in.sec_cap, in.sec_tiles);
+                if (!in.chains_prebuilt)
+                    k_chain_build<<<cb_grid, 256, 0, st>>>(P, in.nh, in.prm, in.seg_start, in.e_txn, in.e_meta, in.e_exec1, in.sval, ls.c_txn,
+                                                      ls.c_meta, ls.c_exec1, ls.c_pair, ls.indeg, ls.succ, ls.flags + 7, 0, 1,
+                                                      ls.flags + 18, in.sec, in.sec_cnt, in.sec_cap, in.sec_tiles);
                 k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
                                                  ls.sk1, ls.pull_force_abort ? 1 : 0);
                 k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);

@@ -52,6 +52,8 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.n_special = h->n_special;
     li.exec_bits = h->pack.total_bits;
     li.kahn_ok = h->level_mode != AD_LEVELS_FIXPOINT ? 1 : 0;
+    li.chains_prebuilt = h->chains_prebuilt ? 1 : 0;        // k_seg_fuse built them (ad_run_pipeline)
+    h->chains_prebuilt = false;
     li.force_blocks = (h->level_mode == AD_LEVELS_BLOCKS || h->level_mode == AD_LEVELS_BLOCKS_WIDE) ? 1 : 0;
     li.wide_words = h->level_mode == AD_LEVELS_BLOCKS_WIDE ? 1 : 0;
     h->ls.pull_off = h->level_mode == AD_LEVELS_KAHN;

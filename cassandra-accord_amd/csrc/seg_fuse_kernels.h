@@ -20,6 +20,7 @@
 // the host runs the three-kernel path instead (the handle then remembers the batch had long segments).
 #pragma once
 #include "deps_kernels.h"
+#include "level_kernels.h"
 
 namespace ad {
 
@@ -43,6 +44,14 @@ struct SegFuseArgs {
     uint64_t* e_exec1;
     int32_t *seg_start, *ud_prev;
     uint64_t *pm_w, *pm_c;
+    // the pull pass's key chains (ad_run_pipeline; c_txn == null: the level stage builds them): each multi-entry
+    // segment's chain from the LDS copy (chain_build_range in pred mode) -- replaces the level stage's k_chain_build
+    uint32_t* c_txn;
+    uint8_t* c_meta;
+    uint64_t* c_exec1;
+    uint32_t* c_pair;
+    uint2* succ;
+    uint32_t *any_long, *any_far;
 };
 
 constexpr int SF_PARTS = 256;
@@ -183,6 +192,18 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     for (uint32_t x = rr; x < nq; x += SF_T) {
         const uint32_t q = s_qlist[x];
         walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + q, s_eq[q] ? s_ex1[q] : 0ull);
+    }
+    if (f.c_txn) {
+        bool lng = false, far = false;
+        for (uint32_t x = tid; x < s_cnt[4]; x += SF_T) {
+            const uint32_t i = s_slist[x], s0 = i - 1;            // the segment's second entry and its head
+            uint32_t e = i + 1;
+            while (e < L && s_key[e] == s_key[s0]) ++e;
+            chain_build_range((size_t)lo + s0, (size_t)lo + e, s_txn - lo, s_meta - lo, s_ex1 - lo, w.sval, f.c_txn,
+                              f.c_meta, f.c_exec1, f.c_pair, nullptr, f.succ, 0, 1, lng, far);
+        }
+        wave_set_flag(lng, f.any_long);
+        wave_set_flag(far, f.any_far);
     }
 }
 
