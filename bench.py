@@ -76,7 +76,10 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False, steps=1):
         # written (txn, meta, executeAt + 1: 13 B; segment start, last always-emitted, two prefix maxima: 24 B); per
         # query (W) its C count bytes written and its txn's PreAccept bound read (8 B); 4 B per emitted id.  (Until round
         # 5 the model priced W gathers only: the G - W head gathers were missing, ~37 MB of C2's 132 MB.)
-        "k_seg_fuse": calls * (P * 8 + (st.get("gather_items") or W) * (4 + 16 + 13 + 24) + W * (C + 8) + 4 * D),
+        # + in ad_run_pipeline (chains_fused) the pull pass's chains: c_txn per gathered entry (4 B) and a predecessor
+        # word per non-head entry (8 B)
+        "k_seg_fuse": calls * (P * 8 + (st.get("gather_items") or W) * (4 + 16 + 13 + 24) + W * (C + 8) + 4 * D +
+                               ((st.get("gather_items") or W) * 4 + W * 8 if st.get("chains_fused") else 0)),
         # the distinct keys from the tile counts (only for the stages that read every key; not in the C2 pipeline):
         # keys re-read (4 B/pair), U = P - W keys and segment starts written (12 B)
         "seg_keys": calls * (P * 4 + (P - W) * 12),

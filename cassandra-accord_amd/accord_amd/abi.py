@@ -142,7 +142,7 @@ class AdStageTimes(C.Structure):
                 ("deferred_txns", C.c_uint32), ("fill_items", C.c_uint32),
                 ("deps_speculative", C.c_uint32),
                 ("vitems", C.c_uint64), ("range_entries", C.c_uint64),
-                ("gather_items", C.c_uint32), ("reserved_", C.c_uint32)]
+                ("gather_items", C.c_uint32), ("chains_fused", C.c_uint32)]
 
 
 def ptr(a, ctype):

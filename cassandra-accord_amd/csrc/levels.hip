@@ -53,6 +53,7 @@ int stage_levels(ad_handle* h, bool want_order) {
     li.exec_bits = h->pack.total_bits;
     li.kahn_ok = h->level_mode != AD_LEVELS_FIXPOINT ? 1 : 0;
     li.chains_prebuilt = h->chains_prebuilt ? 1 : 0;        // k_seg_fuse built them (ad_run_pipeline)
+    h->times.chains_fused = (uint32_t)li.chains_prebuilt;
     h->chains_prebuilt = false;
     li.force_blocks = (h->level_mode == AD_LEVELS_BLOCKS || h->level_mode == AD_LEVELS_BLOCKS_WIDE) ? 1 : 0;
     li.wide_words = h->level_mode == AD_LEVELS_BLOCKS_WIDE ? 1 : 0;

@@ -361,7 +361,7 @@ typedef struct ad_stage_times {     /* milliseconds of the last ad_run_pipeline,
     uint32_t gather_items;          /* entries in key segments of more than one entry: the records the */
                                     /* fused tile kernel (k_seg_fuse) gathers (walk_items + segments);  */
                                     /* 0 when the batch took the three-kernel path                      */
-    uint32_t reserved_;
+    uint32_t chains_fused;          /* 1: k_seg_fuse built the pull pass's key chains (no k_chain_build) */
 } ad_stage_times;
 int  ad_last_times(ad_handle* h, ad_stage_times* out);
 
