@@ -101,6 +101,7 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
     //         14 kinds of the range-domain txns (a bit mask: OR, fields >= NOR)
     unsigned long long f[NF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const size_t stride = (size_t)gridDim.x * blockDim.x;
+#pragma unroll 2
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         unsigned long long a = tm[i], b = em[i], ha = tl[i] >> 16, hb = el[i] >> 16;
         unsigned long long na = (unsigned)tn[i] ^ 0x80000000u, nb = (unsigned)en[i] ^ 0x80000000u;
@@ -114,8 +115,16 @@ static __global__ __launch_bounds__(256) void k_minmax(size_t n, const uint64_t*
         f[13] += ((tl[i] & 1) == AD_DOMAIN_KEY && kind != AD_KIND_READ && kind != AD_KIND_WRITE) ? 1ull : 0ull;
         f[14] |= (tl[i] & 1) == AD_DOMAIN_RANGE ? 1ull << kind : 0ull;
     }
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
-        unsigned long long k = keys[i];
+    // keys as 16-byte pairs (the buffer is a device allocation: 16-byte aligned), four pairs in flight per thread
+    const size_t P2 = P >> 1;
+    const ulonglong2* __restrict__ kp = reinterpret_cast<const ulonglong2*>(keys);
+#pragma unroll 4
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < P2; i += stride) {
+        const ulonglong2 k = kp[i];
+        f[6] = max(f[6], ~min(k.x, k.y)); f[7] = max(f[7], max(k.x, k.y));
+    }
+    if ((P & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long k = keys[P - 1];
         f[6] = max(f[6], ~k); f[7] = max(f[7], k);
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < Q; i += stride) {

@@ -263,7 +263,7 @@ int stage_prepare(ad_handle* h) {
     h->small_cleared = false;
     h->chains_pending = false;
     h->chains_prebuilt = false;
-    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
+    const int g = (int)std::min<size_t>(2048, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));  // 2048 x 15 partials fit the 1 MB scratch floor
     {
         KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
