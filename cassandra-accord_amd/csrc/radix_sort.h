@@ -30,10 +30,26 @@ static __global__ __launch_bounds__(RS_BLOCK) void k_radix_hist(const uint32_t* 
     for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_BLOCK) (&h[0][0])[i] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * RS_TILE;
+    if (base + RS_TILE <= n && ((uintptr_t)keys & 15) == 0) {
+        // a full tile: the histogram is order-free, so each thread takes four 16-byte loads (all issued before
+        // the first LDS atomic) instead of sixteen 4-byte ones
+        const uint4* __restrict__ kv = reinterpret_cast<const uint4*>(keys + base);
+        uint4 q[RS_ITEMS / 4];
+#pragma unroll
+        for (int k = 0; k < RS_ITEMS / 4; ++k) q[k] = kv[k * RS_BLOCK + threadIdx.x];   // coalesced
+#pragma unroll
+        for (int k = 0; k < RS_ITEMS / 4; ++k) {
+            atomicAdd(&h[w][(q[k].x >> shift) & 0xFF], 1u);
+            atomicAdd(&h[w][(q[k].y >> shift) & 0xFF], 1u);
+            atomicAdd(&h[w][(q[k].z >> shift) & 0xFF], 1u);
+            atomicAdd(&h[w][(q[k].w >> shift) & 0xFF], 1u);
+        }
+    } else {
 #pragma unroll 4
-    for (int k = 0; k < RS_ITEMS; ++k) {
-        size_t i = base + (size_t)k * RS_BLOCK + threadIdx.x;   // coalesced
-        if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 0xFF], 1u);
+        for (int k = 0; k < RS_ITEMS; ++k) {
+            size_t i = base + (size_t)k * RS_BLOCK + threadIdx.x;   // coalesced
+            if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 0xFF], 1u);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < 256; d += RS_BLOCK) {
