@@ -263,7 +263,7 @@ int stage_prepare(ad_handle* h) {
     h->small_cleared = false;
     h->chains_pending = false;
     h->chains_prebuilt = false;
-    const int g = (int)std::min<size_t>(2048, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));  // 2048 x 15 partials fit the 1 MB scratch floor
+    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));  // 1024 partials: k_minmax_final is a one-workgroup, latency-bound fold
     {
         KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
@@ -273,7 +273,7 @@ int stage_prepare(ad_handle* h) {
             // follows at once and derives its parameters from the device Params (PackPlan), the host reads them
             // while it runs
             const uint32_t seq = ++h->pub_seq;
-            k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm, h->pub_dev, h->pub_dev + PUB_PRM, seq);
+            k_minmax_final<<<1, MM_FINAL_T, 0, st>>>(g, partial, h->prm, h->pub_dev, h->pub_dev + PUB_PRM, seq);
             if (n > 0) {
                 bool uni_small = false;
                 const uint32_t nl = h->n_large;
@@ -291,7 +291,7 @@ int stage_prepare(ad_handle* h) {
             }
             CK(wait_totals(h, seq, 0, nullptr));
         } else {
-            k_minmax_final<<<1, 256, 0, st>>>(g, partial, h->prm);
+            k_minmax_final<<<1, MM_FINAL_T, 0, st>>>(g, partial, h->prm);
             CK(read_params(h));
         }
     }
