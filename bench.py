@@ -97,6 +97,10 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False, steps=1):
         # write pass also writes the merged rows (16 B/txn + 8 B/entry)
         "k_merge<count>": units * 16 * R + 8 * D,
         "k_merge<write>": units * (16 * R + 16) + 8 * D + 8 * M,
+        # the one-pass merge into capacity regions (k_merge_cap): per txn every reply's key_off / k2t_off / ent_off /
+        # tcnt (16 B per reply), the replies' lists (TxnId + keysToTxnIds word: 8 B per reply entry), the capacity
+        # offsets + exact counts out (24 B) and the merged lists (8 B per merged entry)
+        "k_merge_cap": units * (16 * R + 24) + 8 * D + 8 * M,
         # the level stage priced as SURVEY §8(d) B_level: per pair its u64 entry (8 B), per predecessor edge
         # (the walk items: entries with an earlier entry of their key) 8 B, per txn in-degree + level (8 B);
         # the same figure for the Kahn region and for the executeAt-block path
@@ -174,7 +178,7 @@ def cpu_share():
     return n, src
 
 
-def cpu_baseline(sample_n, cfg="C2", reps=3):
+def cpu_baseline(sample_n, cfg="C2", reps=5):
     """The oracle (oracle/, the CPU restatement of the reference algorithms) on a bounded sample of the same
     workload on this host, SURVEY §8d / BASELINE.md §2: one warm-up, then the median of `reps` runs, with 1
     thread and with T threads (T = the job's CPU share, cpu_share()).  Threads answer contiguous TxnId ranges
@@ -305,6 +309,26 @@ def end_to_end(eng, batch, steps):
                     "ad_fetch_merged_all (3 classes, one call) + ad_fetch_levels, ad_load_batch_commit"}
 
 
+def union_view_side(eng, n, steps=5):
+    """Side figure, outside the timed region: the same pipeline with ad_set_pipeline_union — the merged Deps built
+    as the deps stage's union view instead of k_merge_cap over the replies.  Only a generator that holds every view's
+    inputs can take that shortcut (a coordinator receiving replies cannot), so it is never `value`."""
+    eng.set_pipeline_union(True)
+    try:
+        eng.run_pipeline()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.run_pipeline()
+        dt = time.perf_counter() - t0
+        st = eng.last_times()
+    finally:
+        eng.set_pipeline_union(False)
+    eng.run_pipeline()
+    return {"ms_per_step": dt * 1e3 / steps, "txn_per_s": n * steps / dt, "merge_stage_ms": st["merge"],
+            "deps_stage_ms": st["deps"], "steps": steps,
+            "what": "generator-only shortcut (merged Deps = union view of the deps stage), not a Deps.merge of replies"}
+
+
 def trace_roofline(eng, run_step, n, P, large=False):
     """Untimed all-kernels breakdown pass -> the dominant kernel among those with an algorithmic byte
     model.  Returns (dominant kernel, breakdown, last times)."""
@@ -346,17 +370,18 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     # drop the traffic figure again (round 3 mapped k_txn_finish to "<3>" while rocprof recorded "<3, false>")
     "k_deps_walk<fill>": "ad::k_deps_walk<3, true, false>", "k_deps_walk<count>": "ad::k_deps_walk<3, false, false>",
     "k_radix_scatter": "ad::k_radix_scatter", "k_radix_hist": "ad::k_radix_hist",
-    "k_gather_entries": "ad::k_gather_entries<true>", "k_txn_finish": "ad::k_txn_finish<4, false, false>",
+    "k_gather_entries": "ad::k_gather_entries<true>", "k_txn_finish": "ad::k_txn_finish<3, false, false>",
     "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<3>",
-    "k_seg_fuse": "ad::k_seg_fuse<4, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_ukeys"),
+    "k_seg_fuse": "ad::k_seg_fuse<3, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_ukeys"),
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
+    "k_merge_cap": "ad::k_merge_cap<3>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
     # are shared fill/copy kernels and are not attributed)
     "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_step", "ad::k_chain_rank", "ad::k_chain_check",
                     "ad::k_chain_links", "ad::k_frontier_collect", "ad::k_kahn_small"),
-    # (C2's pipeline computes 4 key classes: the 3 replies + the union view that is the merged Deps)
-    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<4>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<4>, 1024, 4>",
-                     "ad::k_scan_apply<ad::OffsetsOp<4>, 256, 4>"),
+    # (C2's pipeline computes 3 key classes: the 3 replies; with ad_set_pipeline_union 4)
+    "scan_offsets": ("ad::k_scan_reduce<ad::OffsetsOp<3>, 256, 4>", "ad::k_scan_aggregates<ad::OffsetsOp<3>, 1024, 4>",
+                     "ad::k_scan_apply<ad::OffsetsOp<3>, 256, 4>"),
     "order_sort": ("ad::k_window_rank", "ad::k_rank_check", "ad::k_rank_check_hist"),
     # C4's virtual-item region (bare base names: every instantiation)
     "vitems": ("ad::k_vitems", "ad::k_vitems_fill", "ad::k_vitem_walk", "ad::k_large_sums", "ad::k_large_layout"),
@@ -694,6 +719,7 @@ def main():
         mc = {"bound": "hbm", "avg_ms": ms / calls, "launches": calls, "alg_bytes": ab, "achieved_GBps": gbs,
               "frac": gbs / HBM_PEAK_GBS}
     eng.set_trace(0)
+    union_view = union_view_side(eng, n) if Q == 0 else None
     e2e = end_to_end(eng, batch, max(1, min(args.steps, 5))) if args.e2e and Q == 0 else None
     ms_per_step = dt * 1e3 / args.steps
     value = n * args.steps / dt
@@ -719,6 +745,7 @@ def main():
                      "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
                      "level_iterations": st["level_iterations"], "level_path": st["level_path"]},
         "max_conflicts": mc,
+        "union_view": union_view,
         "end_to_end": e2e,
         "value_scope": ("device-resident: the batch is uploaded (ad_load_batch) before the timed region and the "
                         "results stay in HBM; end_to_end.value is the PCIe-inclusive rate SURVEY §8(d) describes "

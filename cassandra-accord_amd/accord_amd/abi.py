@@ -58,6 +58,12 @@ class AdCfkEvents(C.Structure):
                 ("deps_off", _u32p), ("deps_msb", _u64p), ("deps_lsb", _u64p), ("deps_node", _i32p), ("op", _u8p)]
 
 
+class AdCfkQueries(C.Structure):
+    """ad_cfk_queries: mapReduceActive queries against the resident store (ad_cfk_store_query)."""
+    _fields_ = [("nq", C.c_size_t), ("key_off", _u32p), ("keys", _u32p), ("txn_msb", _u64p), ("txn_lsb", _u64p),
+                ("txn_node", _i32p), ("bound_msb", _u64p), ("bound_lsb", _u64p), ("bound_node", _i32p)]
+
+
 CFK_OP_UPDATE, CFK_OP_LOAD, CFK_OP_PRUNE, CFK_OP_LOADING = 0, 1, 2, 3      # AD_CFK_OP_*
 
 CFK_EVENT_FIELDS = (("ev_off", np.uint32), ("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),

@@ -71,6 +71,8 @@ def lib():
         L.ad_cfk_store_notify.argtypes = [vp, vp, vp]
         L.ad_cfk_store_fetch.argtypes = [vp, C.c_uint32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 9
         L.ad_cfk_store_pruning.argtypes = [vp, C.c_uint32, vp, vp, vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 5
+        L.ad_cfk_store_query.argtypes = [vp, C.POINTER(abi.AdCfkQueries), C.POINTER(abi.AdCsrSizes)]
+        L.ad_cfk_store_query_fetch.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut), vp, vp, vp]
         L.ad_preaccept_expiry.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
         L.ad_exec_levels.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
@@ -80,6 +82,7 @@ def lib():
         L.ad_last_times.argtypes = [vp, C.POINTER(abi.AdStageTimes)]
         L.ad_set_trace.argtypes = [vp, C.c_uint64]
         L.ad_set_level_mode.argtypes = [vp, C.c_int]
+        L.ad_set_pipeline_union.argtypes = [vp, C.c_int]
         L.ad_kernel_count.restype = C.c_int
         L.ad_kernel_name.argtypes = [C.c_int]
         L.ad_kernel_name.restype = C.c_char_p
@@ -111,8 +114,8 @@ def lib():
 EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
-            "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_cfk_store_query", "ad_cfk_store_query_fetch", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_pipeline_union", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
             "ad_shard_fetch", "ad_shard_levels_round", "ad_shard_levels_get", "ad_shard_levels_set",
@@ -313,7 +316,7 @@ class DepsEngine:
     def cfk_store_open(self, keys, capacity):
         """K resident CFKs of up to `capacity` rows each (rounded up to a multiple of 64, at most 8192)."""
         self._check(lib().ad_cfk_store_open(self.h, keys, capacity), "ad_cfk_store_open")
-        self._cs_keys, self._cs_cap = keys, (capacity + 63) // 64 * 64
+        self._cs_keys, self._cs_cap = keys, capacity          # not_waiting rows at the caller's capacity
 
     def cfk_store_apply(self, events):
         """CommandsForKey.update events (a dict of abi.CFK_EVENT_FIELDS arrays, grouped by key through ev_off)."""
@@ -365,6 +368,40 @@ class DepsEngine:
             out[f] = out[f][:L]
         out["lp_rows"] = out["lp_rows"][:tot.value]
         out["pruned_before"] = (pm.value, pl.value, pn.value)
+        return out
+
+    def cfk_store_query(self, key_off, keys, txn, bound):
+        """CommandsForKey.mapReduceActive over the resident rows for queries (ad_cfk_store_query): key_off [nq + 1] /
+        keys (store key indices, ascending per query); txn and bound: (msb, lsb, node) arrays [nq] (the querying TxnId and
+        startedBefore).  Returns [keyDeps, directKeyDeps], each a dict of key_off, keys, k2t_off, k2t, txn_off and the
+        TxnIds as txn_msb / txn_lsb / txn_node."""
+        ko = np.ascontiguousarray(key_off, np.uint32)
+        ks = np.ascontiguousarray(keys, np.uint32)
+        arr = [np.ascontiguousarray(x, dt) for x, dt in zip((*txn, *bound), (np.uint64, np.uint64, np.int32) * 2)]
+        q = abi.AdCfkQueries()
+        q.nq = len(ko) - 1
+        q.key_off = ko.ctypes.data_as(abi._u32p); q.keys = ks.ctypes.data_as(abi._u32p)
+        for f, x in zip(("txn_msb", "txn_lsb", "txn_node", "bound_msb", "bound_lsb", "bound_node"), arr):
+            setattr(q, f, x.ctypes.data_as(abi._i32p if x.dtype == np.int32 else abi._u64p))
+        sizes = (abi.AdCsrSizes * 2)()
+        self._check(lib().ad_cfk_store_query(self.h, C.byref(q), sizes), "ad_cfk_store_query")
+        out = []
+        for cls in range(2):
+            sz = sizes[cls]
+            d = {"key_off": np.zeros(q.nq + 1, np.uint32), "keys": np.zeros(max(sz.keys, 1), np.uint64),
+                 "k2t_off": np.zeros(q.nq + 1, np.uint32), "k2t": np.zeros(max(sz.k2t, 1), np.int32),
+                 "txn_off": np.zeros(q.nq + 1, np.uint32), "txn_msb": np.zeros(max(sz.txns, 1), np.uint64),
+                 "txn_lsb": np.zeros(max(sz.txns, 1), np.uint64), "txn_node": np.zeros(max(sz.txns, 1), np.int32)}
+            o = abi.AdCsrOut()
+            o.key_off = d["key_off"].ctypes.data_as(abi._u32p); o.keys = d["keys"].ctypes.data_as(abi._u64p)
+            o.k2t_off = d["k2t_off"].ctypes.data_as(abi._u32p); o.k2t = d["k2t"].ctypes.data_as(abi._i32p)
+            o.txn_off = d["txn_off"].ctypes.data_as(abi._u32p); o.txns = None
+            self._check(lib().ad_cfk_store_query_fetch(self.h, cls, C.byref(o), d["txn_msb"].ctypes.data,
+                                                       d["txn_lsb"].ctypes.data, d["txn_node"].ctypes.data),
+                        "ad_cfk_store_query_fetch")
+            for f, nf in (("keys", sz.keys), ("k2t", sz.k2t), ("txn_msb", sz.txns), ("txn_lsb", sz.txns), ("txn_node", sz.txns)):
+                d[f] = d[f][:nf]
+            out.append(d)
         return out
 
     def cfk_update(self, gid, status, exec_msb=None, exec_lsb=None, exec_node=None):
@@ -570,6 +607,11 @@ class DepsEngine:
         64-bit scan words the block walk uses for batches of more than 2^20 txns."""
         mode = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
         self._check(lib().ad_set_level_mode(self.h, mode), "ad_set_level_mode")
+
+    def set_pipeline_union(self, on):
+        """True: run_pipeline builds the merged Deps as the deps stage's union view (a generator-only shortcut, a
+        side figure); False (default): k_merge_cap merges the R replies' CSRs (Deps.merge)."""
+        self._check(lib().ad_set_pipeline_union(self.h, 1 if on else 0), "ad_set_pipeline_union")
 
     def set_trace(self, mask):
         """Enable HIP-event timing of the kernels whose id bit is set (see kernel_ids())."""

@@ -1,6 +1,15 @@
 // cfk_store.hip — ad_cfk_store_*: device-resident CommandsForKey states driven by CommandsForKey.update events
 // (cfk_store_kernels.h), with CommandsForKey.notifyManaged's release rule over the resident rows (notify_kernels.h).
 #include "engine_internal.h"
+#include "cfk_query_kernels.h"
+
+// Timestamp.compareTo on the host (Timestamp.java:208-217; the device's ts3_cmp)
+static int host_ts_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64_t bl, int32_t bn) {
+    if (am != bm) return am < bm ? -1 : 1;
+    if ((al >> 16) != (bl >> 16)) return (al >> 16) < (bl >> 16) ? -1 : 1;
+    if ((al & 0x1E) != (bl & 0x1E)) return (al & 0x1E) < (bl & 0x1E) ? -1 : 1;
+    return an < bn ? -1 : (an > bn ? 1 : 0);
+}
 
 int ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity) {
     if (!h) return AD_ERR_ARGUMENT;
@@ -9,6 +18,7 @@ int ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity) {
     hipSetDevice(h->device);
     auto& c = h->cs;
     c.K = keys;
+    c.ucap = capacity;
     c.cap = (capacity + 63) & ~63u;
     c.words = c.cap / 64;
     const size_t rows = (size_t)c.K * c.cap;
@@ -59,6 +69,14 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     const size_t nd = ev->deps_off[m];
     if (nd && (!ev->deps_msb || !ev->deps_lsb || !ev->deps_node))
         return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: deps without arrays");
+    // every event's deps strictly ascending (a Deps' TxnIds), checked before anything reaches the device: the kernel
+    // would otherwise have half-applied the key's events when it met them (the store stays as it was on an error)
+    for (size_t e = 0; e < m; ++e)
+        for (uint32_t j = ev->deps_off[e] + 1; j < ev->deps_off[e + 1]; ++j)
+            if (host_ts_cmp(ev->deps_msb[j - 1], ev->deps_lsb[j - 1], ev->deps_node[j - 1], ev->deps_msb[j], ev->deps_lsb[j],
+                            ev->deps_node[j]) >= 0)
+                return set_err(h, AD_ERR_UNSORTED, "ad_cfk_store_apply: event " + std::to_string(e) +
+                                                       "'s deps are not strictly ascending");
     hipSetDevice(h->device);
     hipStream_t st = h->st;
     uint32_t *eo, *doff;
@@ -97,13 +115,16 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     a.overflow = c.flags; a.bad = c.flags + 1;
     a.pbm = c.pbm; a.pbl = c.pbl; a.pbn = c.pbn; a.lp_cnt = c.lp_cnt; a.lpm = c.lpm; a.lpl = c.lpl; a.lpn = c.lpn;
     a.lp_bits = c.lp_bits; a.eop = eop;
+    HIPCHK(h, hipMemsetAsync(c.flags, 0, 8, st));          // this call's overflow / order flags
     k_cfk_apply<<<c.K, CS_T, 0, st>>>(a);
     HIPCHK(h, hipGetLastError());
     uint32_t f[2] = {0, 0};
     HIPCHK(h, hipMemcpyAsync(f, c.flags, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     if (f[1]) return set_err(h, AD_ERR_UNSORTED, "ad_cfk_store_apply: an event's deps are not strictly ascending");
-    if (f[0]) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_store_apply: a key outgrew the store's capacity");
+    // (the key that ran out is left as far as its last complete event: reopen the store, or fetch it and replay)
+    if (f[0]) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_store_apply: a key outgrew the store's capacity (rows or "
+                                                    "loadingPruned entries); the key keeps its state up to the event before");
     return AD_OK;
 }
 
@@ -122,7 +143,9 @@ int ad_cfk_store_notify(ad_handle* h, uint32_t* rows, uint8_t* not_waiting) {
     k_cfk_notify<<<c.K, NF_T, 0, st>>>(a);
     HIPCHK(h, hipGetLastError());
     if (rows) HIPCHK(h, hipMemcpyAsync(rows, c.cnt, (size_t)c.K * 4, hipMemcpyDeviceToHost, st));
-    if (not_waiting) HIPCHK(h, hipMemcpyAsync(not_waiting, c.out, (size_t)c.K * c.cap, hipMemcpyDeviceToHost, st));
+    // not_waiting is [keys * capacity] at the caller's (unrounded) capacity: a 2D copy out of the 64-row-aligned rows
+    if (not_waiting)
+        HIPCHK(h, hipMemcpy2DAsync(not_waiting, c.ucap, c.out, c.cap, c.ucap, c.K, hipMemcpyDeviceToHost, st));
     uint32_t f[2] = {0, 0};
     HIPCHK(h, hipMemcpyAsync(f, c.flags + 2, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
@@ -241,5 +264,151 @@ int ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint6
     if (lp_off) lp_off[L] = (uint32_t)tot;
     *loading = L;
     if (witness_total) *witness_total = tot;
+    return AD_OK;
+}
+
+// ---- mapReduceActive over the resident rows (cfk_query_kernels.h) ---------------------------------------------------
+int ad_cfk_store_query(ad_handle* h, const ad_cfk_queries* q, ad_csr_sizes* sizes) {
+    if (!h || !q) return AD_ERR_ARGUMENT;
+    auto& c = h->cs;
+    if (!c.K) return set_err(h, AD_ERR_STATE, "ad_cfk_store_query before ad_cfk_store_open");
+    const size_t nq = q->nq;
+    if (nq && (!q->key_off || !q->txn_msb || !q->txn_lsb || !q->txn_node || !q->bound_msb || !q->bound_lsb || !q->bound_node))
+        return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_query: an array is missing");
+    if (nq && q->key_off[0] != 0) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_query: key_off must start at 0");
+    const size_t items = nq ? q->key_off[nq] : 0;
+    if (items && !q->keys) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_query: keys missing");
+    std::vector<uint32_t> iq(items);
+    for (size_t x = 0; x < nq; ++x) {
+        if (q->key_off[x + 1] < q->key_off[x]) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_query: key_off not monotone");
+        for (uint32_t j = q->key_off[x]; j < q->key_off[x + 1]; ++j) {
+            if (q->keys[j] >= c.K) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_query: key out of range");
+            if (j > q->key_off[x] && q->keys[j] <= q->keys[j - 1])
+                return set_err(h, AD_ERR_UNSORTED, "ad_cfk_store_query: a query's keys are not strictly ascending");
+            iq[j] = (uint32_t)x;
+        }
+    }
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    auto& r = h->csq;
+    r.nq = nq; r.items = items;
+    const size_t nq1 = std::max<size_t>(nq, 1), it1 = std::max<size_t>(items, 1);
+    CfkQueryArgs a{};
+    a.s.K = c.K; a.s.cap = c.cap; a.s.words = c.words; a.s.cnt = c.cnt;
+    a.s.tm = c.tm; a.s.tl = c.tl; a.s.tn = c.tn; a.s.em = c.em; a.s.el = c.el; a.s.en = c.en; a.s.st = c.st;
+    a.s.pbm = c.pbm; a.s.pbl = c.pbl; a.s.pbn = c.pbn;
+    a.nq = (uint32_t)nq; a.items = (uint32_t)items;
+    uint32_t *qoff, *qkey, *diq, *icnt, *ioff, *qeoff, *icur;
+    uint64_t *qtm, *qtl, *qbm, *qbl;
+    int32_t *qtn, *qbn;
+    CK(dalloc(h, S_CSQ0 + 0, &qoff, nq + 1)); CK(dalloc(h, S_CSQ0 + 1, &qkey, it1)); CK(dalloc(h, S_CSQ0 + 2, &diq, it1));
+    CK(dalloc(h, S_CSQ0 + 3, &qtm, nq1)); CK(dalloc(h, S_CSQ0 + 4, &qtl, nq1)); CK(dalloc(h, S_CSQ0 + 5, &qtn, nq1));
+    CK(dalloc(h, S_CSQ0 + 6, &qbm, nq1)); CK(dalloc(h, S_CSQ0 + 7, &qbl, nq1)); CK(dalloc(h, S_CSQ0 + 8, &qbn, nq1));
+    CK(dalloc(h, S_CSQ0 + 9, &icnt, 2 * it1)); CK(dalloc(h, S_CSQ0 + 10, &ioff, 2 * it1));
+    CK(dalloc(h, S_CSQ0 + 11, &qeoff, 2 * (nq + 1))); CK(dalloc(h, S_CSQ0 + 12, &icur, 2 * it1));
+    if (nq) {
+        HIPCHK(h, hipMemcpyAsync(qoff, q->key_off, (nq + 1) * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(qtm, q->txn_msb, nq * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(qtl, q->txn_lsb, nq * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(qtn, q->txn_node, nq * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(qbm, q->bound_msb, nq * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(qbl, q->bound_lsb, nq * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(qbn, q->bound_node, nq * 4, hipMemcpyHostToDevice, st));
+    }
+    if (items) {
+        HIPCHK(h, hipMemcpyAsync(qkey, q->keys, items * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(diq, iq.data(), items * 4, hipMemcpyHostToDevice, st));
+    }
+    a.qoff = qoff; a.qkey = qkey; a.iq = diq; a.qtm = qtm; a.qtl = qtl; a.qtn = qtn; a.qbm = qbm; a.qbl = qbl; a.qbn = qbn;
+    a.icnt = icnt; a.ioff = ioff; a.qeoff = qeoff; a.icur = icur;
+    // count pass -> per (item, class) offsets and per-query entry bases (host: this is the store's query API, not the
+    // batch pipeline), then fill and union
+    std::vector<uint32_t> cnt(2 * items), off(2 * items), qe(2 * (nq + 1), 0);
+    if (items) {
+        k_csq_items<false><<<ceil_div((long)items * WAVE, 256), 256, 0, st>>>(a);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(cnt.data(), icnt, items * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    uint64_t tot[2] = {0, 0};
+    for (size_t x = 0; x < nq; ++x) {
+        for (int cl = 0; cl < 2; ++cl) qe[cl * (nq + 1) + x] = (uint32_t)tot[cl];
+        for (uint32_t j = q->key_off[x]; j < q->key_off[x + 1]; ++j)
+            for (int cl = 0; cl < 2; ++cl) { off[2 * j + cl] = (uint32_t)tot[cl]; tot[cl] += cnt[2 * j + cl]; }
+    }
+    for (int cl = 0; cl < 2; ++cl) qe[cl * (nq + 1) + nq] = (uint32_t)tot[cl];
+    if (tot[0] + items > 0xFFFFFFFFull || tot[1] + items > 0xFFFFFFFFull)
+        return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_store_query: more than 2^32 entries");
+    if (items) HIPCHK(h, hipMemcpyAsync(ioff, off.data(), items * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(qeoff, qe.data(), qe.size() * 4, hipMemcpyHostToDevice, st));
+    for (int cl = 0; cl < 2; ++cl) {
+        const size_t e1 = std::max<size_t>(tot[cl], 1);
+        CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 0, &a.lm[cl], e1)); CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 1, &a.ll[cl], e1));
+        CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 2, &a.ln[cl], e1)); CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 3, &a.okeys[cl], it1));
+        CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 4, &a.ok2t[cl], items + tot[cl] + 1));
+        CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 5, &a.otm[cl], e1)); CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 6, &a.otl[cl], e1));
+        CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 7, &a.otn[cl], e1));
+        CK(dalloc(h, S_CSQ0 + 13 + 10 * cl + 8, &a.okc[cl], 3 * nq1));
+        a.oen[cl] = a.okc[cl] + nq1; a.otc[cl] = a.okc[cl] + 2 * nq1;
+        r.lists[cl] = tot[cl];
+        r.okeys[cl] = a.okeys[cl]; r.ok2t[cl] = a.ok2t[cl]; r.otm[cl] = a.otm[cl]; r.otl[cl] = a.otl[cl]; r.otn[cl] = a.otn[cl];
+        r.okc[cl] = a.okc[cl]; r.oen[cl] = a.oen[cl]; r.otc[cl] = a.otc[cl];
+    }
+    r.qe = qe;
+    r.qoff.assign(q->key_off, q->key_off + nq + 1);
+    if (items) k_csq_items<true><<<ceil_div((long)items * WAVE, 256), 256, 0, st>>>(a);
+    if (nq) k_csq_union<<<ceil_div((long)nq * 2, 256), 256, 0, st>>>(a);
+    HIPCHK(h, hipGetLastError());
+    std::vector<uint32_t> counts[2];
+    for (int cl = 0; cl < 2; ++cl) {
+        counts[cl].resize(3 * nq1);
+        if (nq) HIPCHK(h, hipMemcpyAsync(counts[cl].data(), a.okc[cl], 3 * nq1 * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    for (int cl = 0; cl < 2; ++cl) {
+        r.kc[cl].assign(counts[cl].begin(), counts[cl].begin() + nq);
+        r.en[cl].assign(counts[cl].begin() + nq1, counts[cl].begin() + nq1 + nq);
+        r.tc[cl].assign(counts[cl].begin() + 2 * nq1, counts[cl].begin() + 2 * nq1 + nq);
+        size_t k = 0, m = 0, t = 0;
+        for (size_t x = 0; x < nq; ++x) { k += r.kc[cl][x]; m += r.kc[cl][x] + r.en[cl][x]; t += r.tc[cl][x]; }
+        if (sizes) sizes[cl] = ad_csr_sizes{nq, k, m, t, t};
+    }
+    r.ready = true;
+    return AD_OK;
+}
+
+int ad_cfk_store_query_fetch(ad_handle* h, uint32_t cls, ad_csr_out* out, uint64_t* txn_msb, uint64_t* txn_lsb, int32_t* txn_node) {
+    if (!h || !out || cls > 1) return AD_ERR_ARGUMENT;
+    auto& r = h->csq;
+    if (!r.ready) return set_err(h, AD_ERR_STATE, "ad_cfk_store_query_fetch before ad_cfk_store_query");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    const size_t nq = r.nq, items = r.items, e = r.lists[cls];
+    std::vector<uint64_t> keys(std::max<size_t>(items, 1)), tm(std::max<size_t>(e, 1)), tl(std::max<size_t>(e, 1));
+    std::vector<int32_t> k2t(items + e + 1), tn(std::max<size_t>(e, 1));
+    if (items) HIPCHK(h, hipMemcpyAsync(keys.data(), r.okeys[cls], items * 8, hipMemcpyDeviceToHost, st));
+    if (items + e) HIPCHK(h, hipMemcpyAsync(k2t.data(), r.ok2t[cls], (items + e) * 4, hipMemcpyDeviceToHost, st));
+    if (e) {
+        HIPCHK(h, hipMemcpyAsync(tm.data(), r.otm[cls], e * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(tl.data(), r.otl[cls], e * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(tn.data(), r.otn[cls], e * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    size_t ko = 0, mo = 0, to = 0;
+    out->key_off[0] = 0; out->k2t_off[0] = 0; out->txn_off[0] = 0;
+    for (size_t x = 0; x < nq; ++x) {
+        const uint32_t i0 = r.qoff[x], eb = r.qe[cls * (nq + 1) + x];
+        const uint32_t nk = r.kc[cls][x], nm = nk + r.en[cls][x], nt = r.tc[cls][x];
+        for (uint32_t j = 0; j < nk; ++j) out->keys[ko + j] = keys[i0 + j];
+        for (uint32_t j = 0; j < nm; ++j) out->k2t[mo + j] = k2t[i0 + eb + j];
+        for (uint32_t j = 0; j < nt; ++j) {
+            if (txn_msb) txn_msb[to + j] = tm[eb + j];
+            if (txn_lsb) txn_lsb[to + j] = tl[eb + j];
+            if (txn_node) txn_node[to + j] = tn[eb + j];
+            if (out->txns) out->txns[to + j] = (uint32_t)(to + j);
+        }
+        ko += nk; mo += nm; to += nt;
+        out->key_off[x + 1] = (uint32_t)ko; out->k2t_off[x + 1] = (uint32_t)mo; out->txn_off[x + 1] = (uint32_t)to;
+    }
     return AD_OK;
 }

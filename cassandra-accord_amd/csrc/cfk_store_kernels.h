@@ -479,9 +479,28 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 atomicOr((unsigned long long*)&s_miss[s >> 6], 1ull << (s & 63));
             }
             __syncthreads();
-            // deps unknown to the CFK: TRANSITIVELY_KNOWN rows, in deps order (below prunedBefore: loadingPruned)
+            // deps unknown to the CFK: TRANSITIVELY_KNOWN rows, in deps order (below prunedBefore: loadingPruned).
+            // Their missing() joins are applied in chunks of CS_T additions (s_add): a join touches the rows that
+            // witness the addition other than the command's own, whose missing() is s_miss (written below)
             if (threadIdx.x == 0) s_nadd = 0;
             __syncthreads();
+            const uint32_t cmd_slot = found ? a.slot[base + p] : 0xFFFFFFFFu;
+            auto flush_adds = [&](uint32_t skip) {
+                const uint32_t nadd = s_nadd;
+                for (uint32_t k = 0; k < nadd; ++k) {
+                    const uint32_t s = s_add[k];
+                    // the addition's TxnId: find its row through the slot (rows shifted since): a scan for the slot
+                    __shared__ uint32_t s_row;
+                    for (uint32_t r = threadIdx.x; r < n; r += CS_T) if (a.slot[base + r] == s) s_row = r;
+                    __syncthreads();
+                    const size_t x = base + s_row;
+                    const Ts3 ad{a.tm[x], a.tl[x], a.tn[x]};
+                    cs_add_missing(a, base, n, ad, s, skip);
+                }
+                __syncthreads();
+                if (threadIdx.x == 0) s_nadd = 0;
+                __syncthreads();
+            };
             const Ts3 pb{a.pbm[key], a.pbl[key], a.pbn[key]};
             for (uint32_t j = d0; j < d1; ++j) {
                 const Ts3 d{a.dtm[j], a.dtl[j], a.dtn[j]};
@@ -493,7 +512,8 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 const uint32_t q = cs_find(a, base, n, d, f);
                 if (f) continue;
                 if (ts3_cmp(d, pb) < 0) continue;                      // a pruned addition: loadingPruned, below
-                if (n >= a.cap || s_nadd >= (uint32_t)CS_T) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
+                if (s_nadd >= (uint32_t)CS_T) flush_adds(cmd_slot);
                 const uint32_t s = cs_insert(a, base, n, q, d, AD_ST_TRANSITIVELY_KNOWN, d);
                 if (threadIdx.x == 0) s_add[s_nadd++] = s;
                 __syncthreads();
@@ -526,19 +546,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                     return;
                 }
             }
-            const uint32_t nadd = s_nadd;
-            for (uint32_t k = 0; k < nadd; ++k) {
-                const uint32_t s = s_add[k];
-                bool f2;
-                // the addition's TxnId: find its row through the slot (rows shifted since): a scan for the slot
-                __shared__ uint32_t s_row;
-                for (uint32_t r = threadIdx.x; r < n; r += CS_T) if (a.slot[base + r] == s) s_row = r;
-                __syncthreads();
-                const size_t x = base + s_row;
-                const Ts3 ad{a.tm[x], a.tl[x], a.tn[x]};
-                (void)f2;
-                cs_add_missing(a, base, n, ad, s, ts);
-            }
+            flush_adds(ts);
             if (!found && ns < AD_ST_COMMITTED) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             if (found && cur < AD_ST_COMMITTED && ns >= AD_ST_COMMITTED) cs_remove_missing(a, base, n, ts);
         } else {

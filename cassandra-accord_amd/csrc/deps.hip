@@ -144,7 +144,16 @@ int deps_class_plan(const ad_handle* h, bool want_union, bool* uni_out) {
     return h->n_special > 0 ? 2 * nv : nv;
 }
 
+static int stage_deps_impl(ad_handle* h);
+// On an error after the finish's side stream forked, nothing may reuse the buffers k_txn_finish_ovf still reads or
+// writes: join it on every error return.
 int stage_deps(ad_handle* h) {
+    const int rc = stage_deps_impl(h);
+    if (rc != AD_OK) side_join(h);
+    return rc;
+}
+
+static int stage_deps_impl(ad_handle* h) {
     StageScope sc(h, STAGE_DEPS);
     const size_t n = h->n, P = h->P, Q = h->Q;
     // The union view (ad_run_pipeline): Deps.merge of the R replies is the union of their (key, TxnId) relations
@@ -307,7 +316,7 @@ int stage_deps(ad_handle* h) {
     }
     if (n > 0) {
         KScope ks(K_SCAN_OFFSETS, n);
-        launch_offsets_nv(h, nv, direct, cls, heavy, dtx, dtx_count);
+        launch_offsets_nv(h, nv, direct, cls, heavy, dtx, dtx_count, ta.ovf_rows, fovf_count);
     } else {
         for (int k = 0; k < nc; ++k) csr_offsets(h, h->deps[cls[k]], h->nk, h->ne);
     }
@@ -378,10 +387,11 @@ int stage_deps(ad_handle* h) {
     if (spec) {
         ta.w = wa;
         ta.spec_bad = spec_bad;
-        KScope ks(K_TXN_LAYOUT, n);
-        launch_finish_nv(nv, ta, direct, st);
+        // the overflowed rows (listed by the offsets scan) on the side stream, beside the finish
         CK(side_fork(h));
         launch_finish_ovf_nv(nv, ta, direct, h->xst);
+        KScope ks(K_TXN_LAYOUT, n);
+        launch_finish_nv(nv, ta, direct, st);
         ta.spec_bad = nullptr;
     }
     CK(wait_totals(h, seq, tt.count, got.data()));
@@ -393,7 +403,7 @@ int stage_deps(ad_handle* h) {
         HIPCHK(h, hipStreamSynchronize(st));
         h->seg_long = true;
         h->want_union = want_u;
-        return stage_deps(h);
+        return stage_deps_impl(h);
     }
     std::copy(got.begin(), got.begin() + ncol, tot.begin());
     // k_txn_finish completes every small txn whose pairs kept all their ids inline; only the deferred ones need
@@ -440,10 +450,11 @@ int stage_deps(ad_handle* h) {
     h->times.deps_speculative = spec ? (spec_ok ? 1u : 2u) : 0u;
     ta.w = wa;
     if (n > 0 && !spec_ok) {
-        KScope ks(K_TXN_LAYOUT, n);
-        launch_finish_nv(nv, ta, direct, st);
+        side_join(h);                                    // a speculative side launch exited on the guard
         CK(side_fork(h));
         launch_finish_ovf_nv(nv, ta, direct, h->xst);
+        KScope ks(K_TXN_LAYOUT, n);
+        launch_finish_nv(nv, ta, direct, st);
     }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
     wa.items = items; wa.nitems = nitems;

@@ -853,6 +853,8 @@ struct OffsetsOp {
     const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
     const uint32_t* lsum_e;
     uint32_t* heavy;              // set when some txn's CSRs total more than MERGE_HEAVY keys + entries
+    uint32_t* ovf_rows;           // (txn * NVC + class) rows k_txn_finish_ovf lays out (a pair's list overflowed the
+    uint32_t* ovf_count;          //   walk's inline ids): listed here so that kernel can run beside k_txn_finish
 
     __device__ S identity() const {
         S s;
@@ -908,6 +910,20 @@ struct OffsetsOp {
             if (!d && ents > 0 && key_off[t + 1] - key_off[t] > 4) { dfr[t] = 1; d = true; }
         }
         wave_append(d, (uint32_t)t, dtx, dtx_count);      // k_txn_union's rows
+        // k_txn_finish's small txns (<= 4 pairs) with a class whose list overflowed the inline ids (that kernel's own
+        // test, on the pair counts the load just read)
+        uint32_t ovf = 0;
+        if (!(meta[t] & META_LARGE) && key_off[t + 1] - key_off[t] <= 4) {
+            for (uint32_t x = key_off[t]; x < key_off[t + 1]; ++x) {
+                uint32_t v[NVC];
+                pair_counts<NVC>(cnt8, cntx, x, v);
+#pragma unroll
+                for (int c = 0; c < NVC; ++c) ovf |= (v[c] > (uint32_t)WALK_INL ? 1u : 0u) << c;
+            }
+        }
+        if (__ballot(ovf != 0))
+#pragma unroll
+            for (int c = 0; c < NVC; ++c) wave_append((ovf >> c) & 1u, (uint32_t)(t * NVC + c), ovf_rows, ovf_count);
     }
 };
 
@@ -1072,6 +1088,10 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
 #pragma unroll
         for (int q = 0; q < WALK_INL; ++q) id[j][q] = (uint32_t)q < cc[j] && cc[j] <= (uint32_t)WALK_INL ? src[q] : 0u;
     }
+    // some list of this class overflowed its inline ids: k_txn_finish_ovf lays the class out from memory (a re-walk
+    // of the overflowed pairs; the offsets scan listed the row, and that kernel runs beside this one); kept out of
+    // this kernel, whose registers it would raise from 60 to 81 (8 -> 5 waves per SIMD)
+    if (ovf) return;
     uint32_t run = nk, kk = 0, rb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1083,13 +1103,6 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
         ++kk;
     }
     uint32_t* tx = a.out_txns[c] + ob;
-    if (ovf) {
-        // some list of this class overflowed its inline ids: k_txn_finish_ovf lays the lists out from memory (a
-        // re-walk of the overflowed pairs); kept out of this kernel, whose registers it would raise from 60 to 81
-        // (8 -> 5 waves per SIMD)
-        wave_append(true, (uint32_t)(t * NVC + c), a.ovf_rows, a.ovf_count);
-        return;
-    }
     if (nk == 1) {                                  // one key: its list is the union, indices 0..cc-1
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1164,15 +1177,18 @@ static __global__ __launch_bounds__(256) void k_txn_finish_ovf(TxnArgs a) {
         const uint32_t r = a.ovf_rows[x];
         const size_t t = r / NVC;
         const int c = (int)(r - t * NVC);
-        const uint32_t nk = a.out_key_off[c][t + 1] - a.out_key_off[c][t];
+        const uint32_t kb = a.out_key_off[c][t], nk = a.out_key_off[c][t + 1] - kb;
         const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
         const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
         const uint32_t mt = a.meta[t];
         int32_t* k2t = a.out_k2t[c];
-        uint32_t run = nk;
+        uint32_t run = nk, kk = 0;
         for (uint32_t y = b; y < e; ++y) {                   // <= 4 pairs (k_txn_finish's small txns)
             const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, y, c);
             if (cc == 0) continue;
+            a.out_keys[c][kb + kk] = a.keys[y];               // the key and its keysToTxnIds end (header)
+            k2t[mb + kk] = (int32_t)(run + cc);
+            ++kk;
             if (cc <= (uint32_t)WALK_INL) {
                 const uint32_t* src = a.inl + ((size_t)y * NVC + c) * WALK_INL;
                 for (uint32_t q = 0; q < cc; ++q) k2t[mb + run + cc - 1 - q] = (int32_t)src[q];

@@ -1110,6 +1110,7 @@ int ad_recover(ad_handle* h, const uint32_t* rows, size_t nq, size_t* entries) {
     hipSetDevice(h->device);
     g_tracer = &h->tracer;
     CK(complete_entries(h));
+    CK(merged_ready(h));
     hipStream_t st = h->st;
     h->rc_ready = false;
     uint32_t *drows = nullptr, *cnt = nullptr, *off = nullptr;
@@ -1208,6 +1209,7 @@ int ad_merge_deps(ad_handle* h, ad_csr_sizes* sizes) {
     CK(stage_merge(h));
     h->merged_has_range = h->Q > 0;
     if (sizes) {
+        CK(merged_ready(h));
         CK(csr_sizes(h, h->merged[0], &sizes[0]));
         CK(csr_sizes(h, h->merged[1], &sizes[1]));
         if (h->Q) CK(csr_sizes(h, h->merged[2], &sizes[2]));
@@ -1308,6 +1310,7 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
     if (cls >= AD_NUM_CLASSES) return AD_ERR_ARGUMENT;
     hipSetDevice(h->device);
     if (cls == AD_CLASS_RANGE && !h->merged_has_range) return fetch_empty(h, out);
+    CK(merged_ready(h));
     if (h->merged_exact) return fetch_csr(h, h->merged[cls], cls == AD_CLASS_RANGE ? 2 : 1, out);
     CK(merged_compact(h));               // union view: the device-compacted lists, straight DMA
     const Csr& m = h->merged[cls];
@@ -1331,6 +1334,8 @@ int ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out) {
 int ad_merged_sizes(ad_handle* h, ad_csr_sizes* sizes /* [3] */) {
     if (!h || !sizes) return AD_ERR_ARGUMENT;
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
+    hipSetDevice(h->device);
+    CK(merged_ready(h));
     if (!h->merged_exact) {
         hipSetDevice(h->device);
         CK(merged_compact(h));
@@ -1353,6 +1358,7 @@ int ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [3] */) {
     if (!h || !out) return AD_ERR_ARGUMENT;
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
     hipSetDevice(h->device);
+    CK(merged_ready(h));
     CK(merged_compact(h));
     hipStream_t st = h->st;
     const size_t n = h->n;
@@ -1386,6 +1392,7 @@ int ad_fetch_rows(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_t h
     const Csr* c;
     if (view == h->cfg.replicas) {
         if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_fetch_rows of the merged Deps before ad_merge_deps");
+        CK(merged_ready(h));
         c = &h->merged[cls];
     } else {
         if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_fetch_rows before ad_preaccept_deps");
@@ -1491,7 +1498,9 @@ int ad_run_pipeline(ad_handle* h) {
     h->ht.clear();
     host_mark(h, "start");
     HIPCHK(h, hipEventRecord(h->ev[0], st));
-    h->want_union = true;                        // the merged Deps as the deps stage's union view (stage_deps)
+    // the merged Deps: k_merge_cap over the R replies (stage_merge); ad_set_pipeline_union(h, 1) instead builds them
+    // as the deps stage's union view, a shortcut only a generator that holds every view's inputs can take
+    h->want_union = h->pipeline_union;
     CK(stage_prepare(h));
     host_mark(h, "prepare returned");
     HIPCHK(h, hipEventRecord(h->ev[1], st));
@@ -1499,9 +1508,9 @@ int ad_run_pipeline(ad_handle* h) {
     HIPCHK(h, hipEventRecord(h->ev[2], st));
     host_mark(h, "sort enqueued");
     h->xdefer = true;                            // k_txn_finish_ovf's side stream joins where its rows are read
-    const int rc_deps = stage_deps(h);
+    const int rc_deps = stage_deps(h);            // (joins the side stream itself on an error)
     h->xdefer = false;
-    CK(rc_deps);
+    if (rc_deps != AD_OK) { side_join(h); return rc_deps; }
     HIPCHK(h, hipEventRecord(h->ev[3], st));
     host_mark(h, "deps returned");
     int rc = stage_merge(h);
@@ -1549,6 +1558,11 @@ int ad_run_pipeline(ad_handle* h) {
 
 int ad_last_times(ad_handle* h, ad_stage_times* out) {
     if (!h || !out) return AD_ERR_ARGUMENT;
+    if (h->mcap_entries_pending) {
+        hipSetDevice(h->device);
+        CK(merged_entries_resolve(h));
+        h->times.merged_entries = h->merged_entries;
+    }
     *out = h->times;
     return AD_OK;
 }
@@ -1562,6 +1576,12 @@ int ad_set_level_mode(ad_handle* h, int mode) {
                mode != AD_LEVELS_PULL_ABORT && mode != AD_LEVELS_BLOCKS_WIDE))
         return AD_ERR_ARGUMENT;
     h->level_mode = mode;
+    return AD_OK;
+}
+
+int ad_set_pipeline_union(ad_handle* h, int on) {
+    if (!h) return AD_ERR_ARGUMENT;
+    h->pipeline_union = on != 0;
     return AD_OK;
 }
 

@@ -195,6 +195,12 @@ struct ad_handle {
     bool no_fused_chains = getenv("AD_NO_FUSED_CHAINS") != nullptr;   // A/B switch
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
     bool merged_compacted = false;   // !merged_exact: the exact offsets / lists below are built (merged_compact)
+    bool pipeline_union = false;     // ad_set_pipeline_union: ad_run_pipeline takes the union view (a generator shortcut)
+    bool merged_cap = false;         // merged key classes in k_merge_cap's capacity layout (merged_ready compacts them)
+    bool mcap_direct = false;        //   ... the directKeyDeps class too
+    uint32_t *mcap_kcnt[2] = {}, *mcap_ment[2] = {}, *mcap_part[2] = {};
+    unsigned mcap_blocks = 0;
+    bool mcap_entries_pending = false;   // merged_entries = the sum of mcap_part (read lazily)
     uint32_t* mx_off[3] = {};        //   per class: exact TxnId offsets [n + 1]
     uint32_t* mx_txns[3] = {};       //   and the compacted TxnId lists
     size_t mx_tot[3] = {};
@@ -234,6 +240,7 @@ struct ad_handle {
     // device-resident CommandsForKey states (cfk_store_kernels.h, ad_cfk_store_*): K keys x cap byId rows
     struct CfkStore {
         uint32_t K = 0, cap = 0, words = 0;
+        uint32_t ucap = 0;           // the caller's capacity (cap: rounded up to whole 64-slot words)
         uint32_t* cnt = nullptr;
         uint64_t *tm = nullptr, *tl = nullptr, *em = nullptr, *el = nullptr, *bits = nullptr;
         int32_t *tn = nullptr, *en = nullptr;
@@ -243,6 +250,17 @@ struct ad_handle {
         int32_t *pbn = nullptr, *lpn = nullptr;
         uint32_t* lp_cnt = nullptr;
     } cs;
+    // the last ad_cfk_store_query (cfk_query_kernels.h): capacity-laid outputs per class + exact counts on the host
+    struct CfkQueryOut {
+        bool ready = false;
+        size_t nq = 0, items = 0, lists[2] = {0, 0};
+        uint64_t* okeys[2] = {};
+        int32_t* ok2t[2] = {};
+        uint64_t *otm[2] = {}, *otl[2] = {};
+        int32_t* otn[2] = {};
+        uint32_t *okc[2] = {}, *oen[2] = {}, *otc[2] = {};
+        std::vector<uint32_t> qoff, qe, kc[2], en[2], tc[2];
+    } csq;
     // levels
     uint32_t *lvl = nullptr, *order = nullptr;
     uint32_t level_iters = 0;
@@ -336,15 +354,19 @@ enum Slot : size_t {
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
     S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles
     S_MXO0, S_MXO_END = S_MXO0 + 3, S_MXT0, S_MXT_END = S_MXT0 + 3, S_MXS,  // union-view merged Deps compacted for fetch
+    S_MCK0, S_MCK1, S_MCE0, S_MCE1, S_MCP0, S_MCP1,                          // k_merge_cap: kcnt, ment, block parts
+    S_MCL, S_MCLS0, S_MCLS1,                                                  //   pass-2 list counters, lists
+    S_CSQ0, S_CSQ_END = S_CSQ0 + 34,                                           // ad_cfk_store_query
     S_NUM_FIXED,
-    S_CSR0 = 320
+    S_CSR0 = 400
 };
 static_assert(S_NUM_FIXED <= S_CSR0, "fixed device slots overlap the CSR slot blocks");
 // CSR slot blocks (10 slots each): key-class CSRs [0, NVC_MAX), range CSRs [NVC_MAX, NVC_MAX + MAXV),
 // merged [NVC_MAX + MAXV, +3)
 constexpr size_t CSR_RANGE0 = NVC_MAX, CSR_MERGED0 = NVC_MAX + MAXV, CSR_HOST0 = CSR_MERGED0 + 3;
 constexpr size_t CSR_SHARD0 = CSR_HOST0 + 3 * MAXV, CSR_SMERGED0 = CSR_SHARD0 + NVC_MAX, CSR_SRANGE0 = CSR_SMERGED0 + 3;
-static_assert(CSR_SRANGE0 + MAXV <= CSR_BLOCKS_MAX, "zero-offset cache covers every CSR block");
+constexpr size_t CSR_MCAP0 = CSR_SRANGE0 + MAXV;          // k_merge_cap's capacity-laid merged key classes (2)
+static_assert(CSR_MCAP0 + 2 <= CSR_BLOCKS_MAX, "zero-offset cache covers every CSR block");
 
 #define CK(x) do { int rc_ = (x); if (rc_ != AD_OK) return rc_; } while (0)
 
@@ -424,6 +446,11 @@ int stage_deps(ad_handle* h);
 int complete_entries(ad_handle* h);
 int deps_class_plan(const ad_handle* h, bool want_union, bool* uni_out);
 int stage_merge(ad_handle* h);
+// k_merge_cap's capacity-laid merged classes -> the exact CSRs in h->merged (no-op otherwise); every reader of
+// h->merged's keys / lists calls it first
+int merged_ready(ad_handle* h);
+// the merged entries of the last merge (k_merge_cap: its per-workgroup sums, read here)
+int merged_entries_resolve(ad_handle* h);
 int stage_levels(ad_handle* h, bool want_order);
 int finish_order(ad_handle* h);
 bool order_failed(const ad_handle* h);
@@ -442,7 +469,8 @@ void launch_walk_nv(int nv, const WalkArgs& a, bool fill, bool direct, bool pair
 void launch_seg_fuse_nv(int nv, const SegFuseArgs& f, const WalkArgs& w, bool direct, hipStream_t st);
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st);
 // deps_layout.hip: per-txn offsets / layout / unions of the computed key classes
-void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count);
+void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count,
+                       uint32_t* ovf_rows, uint32_t* ovf_count);
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_finish_ovf_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 // k_txn_finish_ovf on the side stream xst (forked after the finish; joined before anything reads the deps CSRs)

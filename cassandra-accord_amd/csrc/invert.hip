@@ -10,6 +10,7 @@ int ad_fetch_inverse(ad_handle* h, uint32_t view, uint32_t cls, size_t lo, size_
     const Csr* c;
     if (view == h->cfg.replicas) {
         if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_fetch_inverse of the merged Deps before ad_merge_deps");
+        CK(merged_ready(h));
         c = &h->merged[cls];
     } else {
         if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_fetch_inverse before ad_preaccept_deps");

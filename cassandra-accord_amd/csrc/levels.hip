@@ -76,6 +76,7 @@ int stage_levels(ad_handle* h, bool want_order) {
                             !(h->merged_has_range && h->merged[AD_CLASS_RANGE].ncap > 0);
     if (!pull_first) {
         side_join(h);                                     // the other level paths read the merged Deps
+        CK(merged_ready(h));
         CK(complete_entries(h));
     }
     li.complete = [](void* x) { return complete_entries((ad_handle*)x); };
@@ -120,6 +121,7 @@ void levels_order_rows(ad_handle* h, size_t m, const uint32_t* rows, uint32_t* o
 // ---------------------------------------------------------------------------------------------------
 int levels_export_edges(ad_handle* h, size_t* m_out, bool global_ranks, bool done_aware) {
     CK(complete_entries(h));
+    CK(merged_ready(h));
     const size_t n = h->n, P = h->P;
     hipStream_t st = h->st;
     const uint32_t* gid = global_ranks ? h->gid : nullptr;

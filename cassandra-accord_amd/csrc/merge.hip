@@ -4,6 +4,8 @@
 // ---------------------------------------------------------------------------------------------------
 // merge
 // ---------------------------------------------------------------------------------------------------
+static bool getenv_flag(const char* name) { const char* e = getenv(name); return e && *e && *e != '0'; }
+
 template <int K>
 void launch_multi_offsets(ad_handle* h, size_t n, const uint32_t* mk, const uint32_t* me, const uint32_t* mu, Csr* const* out) {
     MultiOffsetsOp<K> op{};
@@ -131,6 +133,8 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
                 bool has_direct) {
     const size_t n = h->n;
     h->merged_entries = 0;
+    h->merged_cap = false;
+    h->mcap_entries_pending = false;
     Csr* out[3];
     size_t blocks[3];
     int kw[3];
@@ -156,10 +160,137 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
     return AD_OK;
 }
 
+// Deps.merge of the R replies' key classes in one k_merge_cap launch per class (merge_kernels.h): the merged
+// CSRs in capacity layout, no host round trip.  Batches whose deps stage saw no heavy txn, no range and no
+// virtual items (their classes go through merge_parts).
+constexpr unsigned MCAP_G2 = 1024;                  // pass 2's grid (grid-stride over the listed txns)
+template <int NV>
+static void launch_merge_cap(const MergeCapArgs& a, unsigned g, hipStream_t st) {
+    k_merge_cap<NV><<<g, 256, 0, st>>>(a);
+    k_merge_cap_list<NV><<<std::min(g, MCAP_G2), 256, 0, st>>>(a);
+}
+
+static int merge_cap(ad_handle* h) {
+    const size_t n = h->n;
+    const int nv = (int)h->cfg.replicas;
+    hipStream_t st = h->st;
+    const bool direct = h->deps_direct;
+    CK(zero_csr(h, CSR_MERGED0 + AD_CLASS_RANGE, h->merged[AD_CLASS_RANGE], n));
+    if (!direct) CK(zero_csr(h, CSR_MERGED0 + AD_CLASS_DIRECT_KEY, h->merged[AD_CLASS_DIRECT_KEY], n));
+    const unsigned g = (unsigned)ceil_div((long)n, 256);
+    h->mcap_blocks = g + std::min(g, MCAP_G2);
+    uint32_t* lc = nullptr;                             // [class][2]: list count, finished pass-2 workgroups
+    if (!h->bufs.empty() && h->bufs.size() > S_MCL && h->bufs[S_MCL].p) lc = (uint32_t*)h->bufs[S_MCL].p;
+    if (!lc) {
+        CK(dalloc(h, S_MCL, &lc, 4));
+        HIPCHK(h, hipMemsetAsync(lc, 0, 16, st));          // then kept at zero by pass 2's last workgroup
+    }
+    for (int c = 0; c < (direct ? 2 : 1); ++c) {
+        Csr m{};
+        const size_t block = CSR_MCAP0 + c;
+        CK(alloc_csr(h, block, m, n));
+        dirty_csr(h, block);
+        MergeCapArgs a{};
+        a.n = n;
+        for (int v = 0; v < nv; ++v) {
+            const Csr& x = h->deps[2 * v + c];
+            m.nkeys += x.nkeys; m.nk2t += x.nk2t; m.ncap += x.ncap;
+            a.key_off[v] = x.key_off; a.keys[v] = x.keys; a.k2t_off[v] = x.k2t_off; a.k2t[v] = x.k2t;
+            a.ent_off[v] = x.ent_off; a.txns[v] = x.txns; a.tcnt[v] = x.tcnt;
+        }
+        CK(alloc_csr_data(h, block, m, 1));
+        CK(dalloc(h, S_MCK0 + c, &h->mcap_kcnt[c], std::max<size_t>(n, 1)));
+        CK(dalloc(h, S_MCE0 + c, &h->mcap_ment[c], std::max<size_t>(n, 1)));
+        CK(dalloc(h, S_MCP0 + c, &h->mcap_part[c], std::max<size_t>(h->mcap_blocks, 1)));
+        CK(dalloc(h, S_MCLS0 + c, &a.list, std::max<size_t>(n, 1)));
+        a.list_count = lc + 2 * c; a.list_done = lc + 2 * c + 1;
+        a.part2 = g;
+        a.o_key_off = m.key_off; a.o_k2t_off = m.k2t_off; a.o_ent_off = m.ent_off;
+        a.o_kcnt = h->mcap_kcnt[c]; a.o_ment = h->mcap_ment[c]; a.o_tcnt = m.tcnt;
+        a.o_keys = m.keys; a.o_k2t = m.k2t; a.o_txns = m.txns; a.part = h->mcap_part[c];
+        if (n) {
+            KScope ks(K_MERGE_CAP, n);
+            NV_DISPATCH(nv, launch_merge_cap, a, g, st);
+        } else {
+            HIPCHK(h, hipMemsetAsync(m.key_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(m.ent_off, 0, 4, st));
+        }
+        h->merged[c] = m;                                    // capacity sizes until merged_ready
+    }
+    h->mcap_direct = direct;
+    h->merged_cap = true;
+    h->merged_exact = true;
+    h->merged_compacted = false;
+    h->mcap_entries_pending = true;
+    h->merged_entries = 0;
+    h->have_merged = true;
+    return AD_OK;
+}
+
+int merged_entries_resolve(ad_handle* h) {
+    if (!h->mcap_entries_pending) return AD_OK;
+    h->mcap_entries_pending = false;
+    uint64_t tot = 0;
+    if (h->merged_cap) {
+        std::vector<uint32_t> p(h->mcap_blocks);
+        for (int c = 0; c < (h->mcap_direct ? 2 : 1) && h->mcap_blocks; ++c) {
+            HIPCHK(h, hipMemcpyAsync(p.data(), h->mcap_part[c], p.size() * 4, hipMemcpyDeviceToHost, h->st));
+            HIPCHK(h, hipStreamSynchronize(h->st));
+            for (uint32_t x : p) tot += x;
+        }
+        h->merged_entries = tot;
+        h->times.merged_entries = tot;
+    }
+    return AD_OK;
+}
+
+int merged_ready(ad_handle* h) {
+    if (!h->merged_cap) return AD_OK;
+    CK(merged_entries_resolve(h));
+    const size_t n = h->n;
+    hipStream_t st = h->st;
+    CK(ensure_scratch(h, device_scan_scratch<MultiOffsetsOp<1>>(std::max<size_t>(n, 1))));
+    for (int c = 0; c < (h->mcap_direct ? 2 : 1); ++c) {
+        const Csr cap = h->merged[c];
+        Csr x{};
+        const size_t block = CSR_MERGED0 + c;
+        CK(alloc_csr(h, block, x, n));
+        dirty_csr(h, block);
+        if (n) {
+            MultiOffsetsOp<1> op{};
+            op.n = n; op.mk = h->mcap_kcnt[c]; op.me = h->mcap_ment[c]; op.mu = cap.tcnt;
+            op.key_off[0] = x.key_off; op.ent_off[0] = x.ent_off; op.k2t_off[0] = x.k2t_off;
+            scan_any(h, op, n);
+        } else {
+            HIPCHK(h, hipMemsetAsync(x.key_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(x.k2t_off, 0, 4, st));
+            HIPCHK(h, hipMemsetAsync(x.ent_off, 0, 4, st));
+        }
+        uint32_t tot[3] = {0, 0, 0};
+        HIPCHK(h, hipMemcpyAsync(&tot[0], x.key_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[1], x.k2t_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(&tot[2], x.ent_off + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        x.nkeys = tot[0]; x.nk2t = tot[1]; x.ncap = tot[2];
+        CK(alloc_csr_data(h, block, x, 1));
+        if (n)
+            k_merge_compact<<<ceil_div((long)n, 256), 256, 0, st>>>(n, cap.key_off, cap.k2t_off, cap.ent_off, h->mcap_kcnt[c],
+                                                                    h->mcap_ment[c], cap.tcnt, cap.keys, cap.k2t, cap.txns,
+                                                                    x.key_off, x.k2t_off, x.ent_off, x.keys, x.k2t, x.txns, x.tcnt);
+        HIPCHK(h, hipGetLastError());
+        h->merged[c] = x;
+    }
+    h->merged_cap = false;
+    return AD_OK;
+}
+
 int stage_merge(ad_handle* h) {
     StageScope sc(h, STAGE_MERGE);
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_merge_deps before ad_preaccept_deps");
     const int nv = (int)h->cfg.replicas;
+    h->merged_cap = false;
+    h->mcap_entries_pending = false;
     if (h->deps_union) {
         // the deps stage built the union view (stage_deps): the merged key classes are its CSRs, the range class
         // is empty (no range txns in such a batch)
@@ -175,6 +306,10 @@ int stage_merge(ad_handle* h) {
         return AD_OK;
     }
     side_join(h);                                       // the merge reads every reply's CSRs
+    if (!h->merge_heavy && h->Q == 0 && h->n_large == 0 && !getenv_flag("AD_NO_MERGE_CAP")) {
+        h->merged_has_range = false;
+        return merge_cap(h);
+    }
     const Csr* parts[3][MAXV] = {};
     for (int v = 0; v < nv; ++v) {
         parts[0][v] = &h->deps[2 * v];

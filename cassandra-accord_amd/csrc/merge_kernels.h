@@ -526,6 +526,426 @@ inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t 
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Deps.merge of the R replies in ONE pass (k_merge_cap; key classes of batches without heavy txns).
+//
+// The count pass, the offsets scan and the host's read of the merged totals that k_merge needs before its write
+// pass are all avoidable: a union is never larger than the sum of its parts, so each output txn gets a CAPACITY
+// region whose offsets are the element-wise sum of the replies' own offset arrays (prefix sums add up), and the
+// merged keys / keysToTxnIds block / TxnIds are written into it with their exact counts beside it (kcnt, ment,
+// tcnt).  merged_ready() compacts that into the exact CSR when something needs it (fetch, levels over merged
+// deps, recovery, inverse); nothing on a key batch's pipeline does.
+//
+// Per txn one thread.  Small replies (the C2 / C3 case: <= 8 TxnIds, <= 4 keys, <= 12 keysToTxnIds words per
+// view) are merged in registers with every load issued up front (offsets, then all list words at once: two
+// dependent memory round trips instead of one per merge step):
+//   - TxnId union: an id is OWNED by the first view that lists it; its merged position is the number of owned
+//     ids below it (compares only, no data-dependent register indexing);
+//   - keys: the same ownership / rank on the keys;
+//   - per merged key the set of merged TxnId positions is a bitmask: each view's per-key index list (the
+//     keysToTxnIds entries between two header ends) becomes a mask over its own ids, remapped through the ranks
+//     (remapToSuperset, SortedArrays.java:1249-1275) and OR-ed into the merged key's mask (the per-key
+//     linearUnion, RelationMultiMap.java:562-816); set bits in ascending order are the sorted index list.
+// Larger replies take the serial R-way merge-path loops of k_merge (key union counted first: the header precedes
+// the entries).  Merged entries per workgroup go to part[] (the host sums them lazily).
+// ---------------------------------------------------------------------------------------------------
+struct MergeCapArgs {
+    size_t n;
+    const uint32_t* key_off[MAXV];
+    const uint64_t* keys[MAXV];
+    const uint32_t* k2t_off[MAXV];
+    const int32_t* k2t[MAXV];
+    const uint32_t* ent_off[MAXV];
+    const uint32_t* txns[MAXV];
+    const uint32_t* tcnt[MAXV];
+    uint32_t *o_key_off, *o_k2t_off, *o_ent_off;    // [n + 1] capacity offsets (sums of the replies')
+    uint32_t *o_kcnt, *o_ment, *o_tcnt;             // [n] merged keys / keysToTxnIds entries / TxnIds
+    uint64_t* o_keys;
+    int32_t* o_k2t;
+    uint32_t* o_txns;
+    uint32_t* part;                                 // merged entries per workgroup: pass 1's, then pass 2's at part2
+    uint32_t part2;
+    uint32_t* list;                                 // [n] txns pass 1 leaves to pass 2
+    uint32_t* list_count;                           // zero before pass 1; pass 2's last workgroup clears it
+    uint32_t* list_done;                            // pass 2's finished workgroups (cleared with it)
+};
+constexpr int MC_T = 8, MC_K = 4, MC_S = 12;
+
+// Serial merge of one txn's replies into its capacity region (any sizes).
+template <int NV>
+__device__ inline void merge_cap_serial(const MergeCapArgs& a, const uint32_t* kb, const uint32_t* nk, const uint32_t* mb,
+                                        const uint32_t* tb, const uint32_t* tc, uint32_t okb, uint32_t omb, uint32_t otb,
+                                        uint32_t& okc, uint32_t& oent, uint32_t& otc) {
+    constexpr uint32_t INF = 0xFFFFFFFFu;
+    uint32_t cur[NV], head[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) { cur[v] = tb[v]; head[v] = tc[v] ? a.txns[v][cur[v]] : INF; }
+    uint32_t* out = a.o_txns + otb;
+    uint32_t mu = 0;
+    while (true) {
+        uint32_t mn = INF;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) mn = head[v] < mn ? head[v] : mn;
+        if (mn == INF) break;
+        out[mu++] = mn;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (head[v] == mn) { ++cur[v]; head[v] = cur[v] < tb[v] + tc[v] ? a.txns[v][cur[v]] : INF; }
+    }
+    // merged key count first: the keysToTxnIds header (one end offset per key) precedes the entries
+    uint32_t kc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) kc[v] = kb[v];
+    uint32_t mk = 0;
+    while (true) {
+        bool any = false;
+        uint64_t kmin = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (kc[v] < kb[v] + nk[v]) { const uint64_t k = a.keys[v][kc[v]]; if (!any || k < kmin) { kmin = k; any = true; } }
+        if (!any) break;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) if (kc[v] < kb[v] + nk[v] && a.keys[v][kc[v]] == kmin) ++kc[v];
+        ++mk;
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) kc[v] = kb[v];
+    uint32_t ep = omb + mk, j = 0;
+    while (true) {
+        bool any = false;
+        uint64_t kmin = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (kc[v] < kb[v] + nk[v]) { const uint64_t k = a.keys[v][kc[v]]; if (!any || k < kmin) { kmin = k; any = true; } }
+        if (!any) break;
+        uint32_t lc[NV], le[NV], lh[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            lc[v] = 0; le[v] = 0; lh[v] = INF;
+            if (kc[v] < kb[v] + nk[v] && a.keys[v][kc[v]] == kmin) {
+                const uint32_t ki = kc[v] - kb[v];
+                lc[v] = mb[v] + (ki == 0 ? nk[v] : (uint32_t)a.k2t[v][mb[v] + ki - 1]);
+                le[v] = mb[v] + (uint32_t)a.k2t[v][mb[v] + ki];
+                lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF;
+                ++kc[v];
+            }
+        }
+        uint32_t x = 0;
+        while (true) {
+            uint32_t mn = INF;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) mn = lh[v] < mn ? lh[v] : mn;
+            if (mn == INF) break;
+            while (out[x] < mn) ++x;
+            a.o_k2t[ep++] = (int32_t)x;
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (lh[v] == mn) { ++lc[v]; lh[v] = lc[v] < le[v] ? a.txns[v][tb[v] + (uint32_t)a.k2t[v][lc[v]]] : INF; }
+        }
+        a.o_keys[okb + j] = kmin;
+        a.o_k2t[omb + j] = (int32_t)(ep - omb);
+        ++j;
+    }
+    okc = mk; oent = ep - omb - mk; otc = mu;
+}
+
+// Register merge of small replies (NV <= 4); false when the merged keys exceed MC_K (then nothing was written).
+template <int NV>
+__device__ inline bool merge_cap_small(const MergeCapArgs& a, const uint32_t* kb, const uint32_t* nk, const uint32_t* mb,
+                                       const uint32_t* ms, const uint32_t* tb, const uint32_t* tc, uint32_t okb, uint32_t omb,
+                                       uint32_t otb, uint32_t& okc, uint32_t& oent, uint32_t& otc) {
+    constexpr uint32_t INF = 0xFFFFFFFFu;
+    uint32_t T[NV][MC_T];
+    uint64_t K[NV][MC_K];
+    int32_t S[NV][MC_S];
+    // every load unconditional, at an index clamped into the reply's own list (a conditional load merged with a
+    // constant at a branch join makes the compiler wait for each load before the next: one latency per slot); a reply
+    // without deps reads element 0 (every buffer holds at least 256 bytes)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const bool h = tc[v] != 0;
+#pragma unroll
+        for (int s = 0; s < MC_T; ++s) {
+            const uint32_t x = a.txns[v][h ? tb[v] + min((uint32_t)s, tc[v] - 1) : 0u];
+            T[v][s] = (uint32_t)s < tc[v] ? x : INF;
+        }
+#pragma unroll
+        for (int i = 0; i < MC_K; ++i) {
+            const uint64_t x = a.keys[v][h ? kb[v] + min((uint32_t)i, nk[v] - 1) : 0u];
+            K[v][i] = (uint32_t)i < nk[v] ? x : 0ull;
+        }
+#pragma unroll
+        for (int s = 0; s < MC_S; ++s) {
+            const int32_t x = a.k2t[v][h ? mb[v] + min((uint32_t)s, ms[v] - 1) : 0u];
+            S[v][s] = (uint32_t)s < ms[v] ? x : 0;
+        }
+    }
+    // keys: ownership (first view listing the key) and merged positions
+    uint32_t kown[NV], nkm = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        kown[v] = 0;
+#pragma unroll
+        for (int i = 0; i < MC_K; ++i) {
+            bool o = (uint32_t)i < nk[v];
+#pragma unroll
+            for (int w = 0; w < v; ++w)
+#pragma unroll
+                for (int i2 = 0; i2 < MC_K; ++i2) o = o && !((uint32_t)i2 < nk[w] && K[w][i2] == K[v][i]);
+            kown[v] |= (o ? 1u : 0u) << i;
+        }
+        nkm += (uint32_t)__popc(kown[v]);
+    }
+    if (nkm > (uint32_t)MC_K) return false;
+    // per view: its per-key index lists as masks, key i in bits [8i, 8i + 8) (entry slots s >= nk: key = #ends <= s)
+    uint32_t m[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        m[v] = 0;
+#pragma unroll
+        for (int s = 0; s < MC_S; ++s) {
+            if ((uint32_t)s >= nk[v] && (uint32_t)s < ms[v]) {
+                uint32_t ki = 0;
+#pragma unroll
+                for (int j = 0; j < MC_K; ++j) ki += ((uint32_t)j < nk[v] && S[v][j] <= s) ? 1u : 0u;
+                m[v] |= 1u << (8 * ki + (uint32_t)S[v][s]);
+            }
+        }
+    }
+    // TxnIds: ownership, merged positions, the owned ids written at their positions
+    uint32_t own[NV], nu = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        own[v] = 0;
+#pragma unroll
+        for (int s = 0; s < MC_T; ++s) {
+            bool o = (uint32_t)s < tc[v];
+#pragma unroll
+            for (int w = 0; w < v; ++w)
+#pragma unroll
+                for (int s2 = 0; s2 < MC_T; ++s2) o = o && T[w][s2] != T[v][s];
+            own[v] |= (o ? 1u : 0u) << s;
+        }
+        nu += (uint32_t)__popc(own[v]);
+    }
+    uint32_t R[NV][MC_T];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int s = 0; s < MC_T; ++s) {
+            uint32_t r = 0;
+#pragma unroll
+            for (int w = 0; w < NV; ++w)
+#pragma unroll
+                for (int s2 = 0; s2 < MC_T; ++s2) r += ((own[w] >> s2 & 1u) && T[w][s2] < T[v][s]) ? 1u : 0u;
+            R[v][s] = r;
+            if (own[v] >> s & 1u) a.o_txns[otb + r] = T[v][s];
+        }
+    // per merged key: the mask of merged TxnId positions
+    uint32_t M[MC_K];
+#pragma unroll
+    for (int j = 0; j < MC_K; ++j) M[j] = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int i = 0; i < MC_K; ++i) {
+            if ((uint32_t)i >= nk[v]) continue;
+            uint32_t kr = 0;
+#pragma unroll
+            for (int w = 0; w < NV; ++w)
+#pragma unroll
+                for (int i2 = 0; i2 < MC_K; ++i2) kr += ((kown[w] >> i2 & 1u) && K[w][i2] < K[v][i]) ? 1u : 0u;
+            uint32_t B = 0;
+#pragma unroll
+            for (int e = 0; e < MC_T; ++e) B |= ((m[v] >> (8 * i + e)) & 1u) << R[v][e];
+#pragma unroll
+            for (int j = 0; j < MC_K; ++j) M[j] |= kr == (uint32_t)j ? B : 0u;
+            if (kown[v] >> i & 1u) a.o_keys[okb + kr] = K[v][i];
+        }
+    uint32_t run = nkm;
+#pragma unroll
+    for (int j = 0; j < MC_K; ++j) {
+        if ((uint32_t)j >= nkm) break;
+        uint32_t x = M[j];
+        while (x) { a.o_k2t[omb + run++] = __ffs(x) - 1; x &= x - 1; }
+        a.o_k2t[omb + j] = (int32_t)run;
+    }
+    okc = nkm; oent = run - nkm; otc = nu;
+    return true;
+}
+
+// Block sum of one value per thread (256 threads) -> out (thread 0)
+__device__ inline void merge_cap_block_sum(uint32_t v, uint32_t* out) {
+    __shared__ uint32_t sh[256 / WAVE];
+#pragma unroll
+    for (int d = WAVE / 2; d > 0; d >>= 1) v += __shfl_xor(v, d);
+    if (__lane_id() == 0) sh[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < 256 / WAVE; ++w) s += sh[w];
+        *out = s;
+    }
+}
+
+// Pass 1, one thread per txn: the capacity offsets, and every txn whose replies need no merging — none has deps, or
+// the replies that have any are identical (they differ only where a view dropped an in-flight dependency: C2's
+// usual case) — settled by a copy.  The others go to a list (wave-aggregated append) for pass 2, where they are dense
+// (a full register merge in pass 1 ran every wave through it: nearly every wave holds one such txn).
+template <int NV>
+static __global__ __launch_bounds__(256) void k_merge_cap(MergeCapArgs a) {
+    constexpr uint32_t INF = 0xFFFFFFFFu;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t ent = 0;
+    bool defer = false;
+    if (t < a.n) {
+        uint32_t kb[NV], nk[NV], mb[NV], ms[NV], tb[NV], tc[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            kb[v] = a.key_off[v][t]; nk[v] = a.key_off[v][t + 1] - kb[v];
+            mb[v] = a.k2t_off[v][t]; ms[v] = a.k2t_off[v][t + 1] - mb[v];
+            tb[v] = a.ent_off[v][t]; tc[v] = a.tcnt[v][t];
+        }
+        uint32_t okb = 0, omb = 0, otb = 0, any = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) { okb += kb[v]; omb += mb[v]; otb += tb[v]; any |= tc[v]; }
+        a.o_key_off[t] = okb; a.o_k2t_off[t] = omb; a.o_ent_off[t] = otb;
+        if (t + 1 == a.n) {
+            uint32_t ek = 0, em = 0, et = 0;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) { ek += kb[v] + nk[v]; em += mb[v] + ms[v]; et += a.ent_off[v][a.n]; }
+            a.o_key_off[a.n] = ek; a.o_k2t_off[a.n] = em; a.o_ent_off[a.n] = et;
+        }
+        uint32_t okc = 0, oent = 0, otc = 0;
+        if (any) {
+            // the first reply with deps (f) and whether every reply with deps has its shape and fits the registers
+            uint32_t fkb = 0, fnk = 0, fmb = 0, fms = 0, ftb = 0, ftc = 0;
+            bool got = false;
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (!got && tc[v]) { fkb = kb[v]; fnk = nk[v]; fmb = mb[v]; fms = ms[v]; ftb = tb[v]; ftc = tc[v]; got = true; }
+            bool same = ftc <= (uint32_t)MC_T && fnk <= (uint32_t)MC_K && fms <= (uint32_t)MC_S;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) same = same && (tc[v] == 0 || (tc[v] == ftc && nk[v] == fnk && ms[v] == fms));
+            if (same) {
+                uint32_t T[MC_T];
+                uint64_t K[MC_K];
+                int32_t S[MC_S];
+                // f's lists, then every other reply with deps compared word for word (all loads issued together)
+                const uint32_t* ft = nullptr;
+                const uint64_t* fk = nullptr;
+                const int32_t* fm = nullptr;
+                bool gf = false;
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    if (!gf && tc[v]) { ft = a.txns[v]; fk = a.keys[v]; fm = a.k2t[v]; gf = true; }
+                // unconditional loads at clamped indices (see merge_cap_small): f has deps, so ftc, fnk >= 1, fms >= 2
+#pragma unroll
+                for (int s = 0; s < MC_T; ++s) { const uint32_t x = ft[ftb + min((uint32_t)s, ftc - 1)]; T[s] = (uint32_t)s < ftc ? x : INF; }
+#pragma unroll
+                for (int i = 0; i < MC_K; ++i) { const uint64_t x = fk[fkb + min((uint32_t)i, fnk - 1)]; K[i] = (uint32_t)i < fnk ? x : 0ull; }
+#pragma unroll
+                for (int s = 0; s < MC_S; ++s) { const int32_t x = fm[fmb + min((uint32_t)s, fms - 1)]; S[s] = (uint32_t)s < fms ? x : 0; }
+                // every other reply with deps, word for word: the differences OR-ed under masks (arithmetic, not a
+                // short-circuit test: a branch around each compare would sink each load into it)
+                uint32_t diff = 0;
+                uint64_t diffk = 0;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    const bool h = tc[v] != 0;
+                    const uint32_t hm = h ? ~0u : 0u;
+#pragma unroll
+                    for (int s = 0; s < MC_T; ++s) {
+                        const uint32_t x = a.txns[v][h ? tb[v] + min((uint32_t)s, ftc - 1) : 0u];
+                        diff |= (x ^ T[s]) & ((uint32_t)s < ftc ? hm : 0u);
+                    }
+#pragma unroll
+                    for (int i = 0; i < MC_K; ++i) {
+                        const uint64_t x = a.keys[v][h ? kb[v] + min((uint32_t)i, fnk - 1) : 0u];
+                        diffk |= (x ^ K[i]) & ((uint32_t)i < fnk && h ? ~0ull : 0ull);
+                    }
+#pragma unroll
+                    for (int s = 0; s < MC_S; ++s) {
+                        const uint32_t x = (uint32_t)a.k2t[v][h ? mb[v] + min((uint32_t)s, fms - 1) : 0u];
+                        diff |= (x ^ (uint32_t)S[s]) & ((uint32_t)s < fms ? hm : 0u);
+                    }
+                }
+                same = diff == 0 && diffk == 0;
+                if (same) {
+#pragma unroll
+                    for (int s = 0; s < MC_T; ++s) if ((uint32_t)s < ftc) a.o_txns[otb + s] = T[s];
+#pragma unroll
+                    for (int i = 0; i < MC_K; ++i) if ((uint32_t)i < fnk) a.o_keys[okb + i] = K[i];
+#pragma unroll
+                    for (int s = 0; s < MC_S; ++s) if ((uint32_t)s < fms) a.o_k2t[omb + s] = S[s];
+                    okc = fnk; oent = fms - fnk; otc = ftc;
+                }
+            }
+            defer = !same;
+        }
+        if (!defer) { a.o_kcnt[t] = okc; a.o_ment[t] = oent; a.o_tcnt[t] = otc; }
+        ent = oent;
+    }
+    wave_append(defer, (uint32_t)t, a.list, a.list_count);
+    merge_cap_block_sum(ent, a.part + blockIdx.x);
+}
+
+// Pass 2: the listed txns, dense — the register merge for small replies (NV <= 4), else the serial loops.  The last
+// workgroup to finish clears the list count for the next merge.
+template <int NV>
+static __global__ __launch_bounds__(256) void k_merge_cap_list(MergeCapArgs a) {
+    const uint32_t L = *(const volatile uint32_t*)a.list_count;
+    uint32_t ent = 0;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < L; x += gridDim.x * blockDim.x) {
+        const size_t t = a.list[x];
+        uint32_t kb[NV], nk[NV], mb[NV], ms[NV], tb[NV], tc[NV];
+        bool small = NV <= 4;
+        uint32_t okb = 0, omb = 0, otb = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            kb[v] = a.key_off[v][t]; nk[v] = a.key_off[v][t + 1] - kb[v];
+            mb[v] = a.k2t_off[v][t]; ms[v] = a.k2t_off[v][t + 1] - mb[v];
+            tb[v] = a.ent_off[v][t]; tc[v] = a.tcnt[v][t];
+            okb += kb[v]; omb += mb[v]; otb += tb[v];
+            small = small && tc[v] <= (uint32_t)MC_T && nk[v] <= (uint32_t)MC_K && ms[v] <= (uint32_t)MC_S;
+        }
+        uint32_t okc = 0, oent = 0, otc = 0;
+        bool done = false;
+        if constexpr (NV <= 4) {
+            if (small) done = merge_cap_small<NV>(a, kb, nk, mb, ms, tb, tc, okb, omb, otb, okc, oent, otc);
+        }
+        if (!done) merge_cap_serial<NV>(a, kb, nk, mb, tb, tc, okb, omb, otb, okc, oent, otc);
+        a.o_kcnt[t] = okc; a.o_ment[t] = oent; a.o_tcnt[t] = otc;
+        ent += oent;
+    }
+    merge_cap_block_sum(ent, a.part + a.part2 + blockIdx.x);
+    __shared__ uint32_t s_last;
+    __threadfence();
+    if (threadIdx.x == 0) s_last = atomicAdd(a.list_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0 && s_last) { *(volatile uint32_t*)a.list_count = 0u; *(volatile uint32_t*)a.list_done = 0u; }
+}
+
+// The exact CSR of a capacity-laid merge (merged_ready): exact offsets come from MultiOffsetsOp over (kcnt, ment,
+// tcnt); then each txn's keys, keysToTxnIds block and TxnIds move down (one thread per txn: outside the pipeline).
+static __global__ __launch_bounds__(256) void k_merge_compact(size_t n, const uint32_t* __restrict__ ckoff, const uint32_t* __restrict__ cmoff,
+                                                              const uint32_t* __restrict__ ctoff, const uint32_t* __restrict__ kcnt,
+                                                              const uint32_t* __restrict__ ment, const uint32_t* __restrict__ tcnt,
+                                                              const uint64_t* __restrict__ ckeys, const int32_t* __restrict__ ck2t,
+                                                              const uint32_t* __restrict__ ctxns, const uint32_t* __restrict__ xkoff,
+                                                              const uint32_t* __restrict__ xmoff, const uint32_t* __restrict__ xtoff,
+                                                              uint64_t* __restrict__ xkeys, int32_t* __restrict__ xk2t,
+                                                              uint32_t* __restrict__ xtxns, uint32_t* __restrict__ xtcnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t nk = kcnt[t], nm = nk + ment[t], nt = tcnt[t];
+    for (uint32_t i = 0; i < nk; ++i) xkeys[xkoff[t] + i] = ckeys[ckoff[t] + i];
+    for (uint32_t i = 0; i < nm; ++i) xk2t[xmoff[t] + i] = ck2t[cmoff[t] + i];
+    for (uint32_t i = 0; i < nt; ++i) xtxns[xtoff[t] + i] = ctxns[ctoff[t] + i];
+    xtcnt[t] = nt;
+}
+
 inline void merge_launch(const MergeArgs& a, int nv, bool write, int kw, hipStream_t st) {
     switch (nv) {
         case 1: merge_launch_nv<1>(a, write, kw, st); break;

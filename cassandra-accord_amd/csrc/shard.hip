@@ -620,6 +620,7 @@ int ad_shard_levels_round(ad_handle* h, int first, uint32_t* changed) {
     li.ukey = h->ukey; li.useg = h->useg; li.U = h->P ? h->hprm.n_keys_u : 0;
     if (mixed) {
         if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_shard_levels_round: first round missing");
+        CK(merged_ready(h));
         li.merged_key = &h->merged[AD_CLASS_KEY];
         li.merged_direct = &h->merged[AD_CLASS_DIRECT_KEY];
         li.merged_range = &h->merged[AD_CLASS_RANGE];

@@ -15,7 +15,7 @@ namespace ad {
 enum KernelId : int {
     K_MINMAX, K_PACK, K_RADIX_HIST, K_RADIX_SCATTER, K_SCAN_RADIX, K_GATHER, K_SCAN_ELIDE, K_WALK_COUNT,
     K_TXN_COUNTS, K_SCAN_OFFSETS, K_TXN_LAYOUT, K_WALK_FILL, K_TXN_UNION, K_MERGE_COUNT, K_MERGE_WRITE,
-    K_CHAIN_PREP, K_SCAN_CHAIN, K_ORDER, K_RANGE, K_VITEMS, K_UNION_LDS, K_LEVEL_EDGES, K_KAHN, K_MERGE_HEAVY_COUNT, K_MERGE_HEAVY_WRITE, K_MAX_CONFLICTS, K_MERGE_OFFSETS, K_CSR_OFFSETS, K_BLOCK_LEVELS, K_RECOVER, K_SEG_FUSE, K_SEG_KEYS, K_COUNT
+    K_CHAIN_PREP, K_SCAN_CHAIN, K_ORDER, K_RANGE, K_VITEMS, K_UNION_LDS, K_LEVEL_EDGES, K_KAHN, K_MERGE_HEAVY_COUNT, K_MERGE_HEAVY_WRITE, K_MAX_CONFLICTS, K_MERGE_OFFSETS, K_CSR_OFFSETS, K_BLOCK_LEVELS, K_RECOVER, K_SEG_FUSE, K_SEG_KEYS, K_MERGE_CAP, K_COUNT
 };
 
 inline const char* kernel_name(int k) {
@@ -24,7 +24,7 @@ inline const char* kernel_name(int k) {
         "k_deps_walk<count>", "k_txn_counts", "scan_offsets", "k_txn_finish", "k_deps_walk<fill>", "k_txn_union",
         "k_merge<count>", "k_merge<write>", "chain_prep", "scan_chain", "order_sort", "k_range_deps", "vitems",
         "k_union_lds", "level_edges", "kahn_levels", "k_merge_heavy<count>", "k_merge_heavy<write>",
-        "max_conflicts", "merge_offsets", "csr_offsets", "block_levels", "recover", "k_seg_fuse", "seg_keys"};
+        "max_conflicts", "merge_offsets", "csr_offsets", "block_levels", "recover", "k_seg_fuse", "seg_keys", "k_merge_cap"};
     return (k >= 0 && k < K_COUNT) ? names[k] : "?";
 }
 

@@ -330,6 +330,10 @@ int  ad_max_conflicts_export_ranges(ad_handle* h, size_t* m, uint64_t* starts, u
 /* outputs.  Kernel timing: HIP events on the handle's stream.                                 */
 /* ------------------------------------------------------------------------------------------ */
 int  ad_run_pipeline(ad_handle* h);
+/* on != 0: ad_run_pipeline builds the merged Deps as the deps stage's "union view" (an entry kept by any replica
+ * view) instead of merging the R replies (k_merge_cap, the default).  A shortcut only a generator holding every
+ * view's inputs can take — a coordinator receiving replies from other nodes cannot; kept as a side figure. */
+int  ad_set_pipeline_union(ad_handle* h, int on);
 /* Levels and execution order left on the device by the last ad_run_pipeline / ad_exec_levels (no
  * recomputation).  Either pointer may be NULL.  AD_ERR_STATE if none were computed for this batch. */
 int  ad_fetch_levels(ad_handle* h, uint32_t* level_out, uint32_t* order_out);
@@ -532,6 +536,31 @@ int  ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missin
 int  ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint64_t* pruned_lsb, int32_t* pruned_node,
                           size_t* loading, size_t* witness_total, uint64_t* lp_msb, uint64_t* lp_lsb, int32_t* lp_node,
                           uint32_t* lp_off, uint32_t* lp_rows);
+/* CommandsForKey.mapReduceActive over the resident rows (local/cfk/CommandsForKey.java:925-983), as
+ * PreAccept.calculatePartialDeps (messages/PreAccept.java:245-267) asks it, for a batch of queries: query q's txn on its
+ * store keys with bound startedBefore (PreAccept / ExclusiveSyncPoint: its TxnId; Accept / GetDeps: its executeAt, the txn
+ * itself then left out), kinds = the txn's Kind.witnesses(); elision against the last committed Write executing before
+ * the bound; when startedBefore <= the key's prunedBefore, the earliest committed Write executing at or after it (the
+ * future dependency standing in for pruned txns, :967-980).  Per query its PartialDeps' keyDeps (Read / Write deps) and
+ * directKeyDeps (sync points) in Deps.Builder's canonical CSR (Deps.java:80-106): keys = store key indices ascending,
+ * unique TxnIds ascending, keysToTxnIds.  sizes[2]: keyDeps, directKeyDeps (n = queries).  Errors as ad_cfk_store_apply;
+ * AD_ERR_UNSORTED when a query's keys are not strictly ascending. */
+typedef struct ad_cfk_queries {
+    size_t nq;
+    const uint32_t* key_off;        /* [nq + 1] query q's keys: [key_off[q], key_off[q + 1])           */
+    const uint32_t* keys;           /* store key indices, strictly ascending per query                 */
+    const uint64_t* txn_msb;        /* [nq] the querying txn's TxnId (kind from lsb)                   */
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint64_t* bound_msb;      /* [nq] startedBefore                                              */
+    const uint64_t* bound_lsb;
+    const int32_t*  bound_node;
+} ad_cfk_queries;
+int  ad_cfk_store_query(ad_handle* h, const ad_cfk_queries* q, ad_csr_sizes* sizes /* [2] */);
+/* one class of the last ad_cfk_store_query: out->key_off / keys / k2t_off / k2t / txn_off sized by its sizes (out->txns, if
+ * not NULL, gets 0..txns-1); the TxnIds themselves into txn_msb / txn_lsb / txn_node [txns] */
+int  ad_cfk_store_query_fetch(ad_handle* h, uint32_t cls, ad_csr_out* out, uint64_t* txn_msb, uint64_t* txn_lsb,
+                              int32_t* txn_node);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU key-range sharding (one handle = one CommandStore = one GPU).                     */

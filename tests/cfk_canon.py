@@ -702,6 +702,37 @@ class CFK:
             new_info = self.info[t]
         return True, cur_status, new_info
 
+    # -- CommandsForKey.mapReduceActive (:925-983), as PreAccept.calculatePartialDeps asks it (PreAccept.java:245-267)
+    def map_reduce_active(self, started_before, kinds, exclude=None):
+        """The TxnIds mapReduceActive hands the builder for a query with bound `started_before` witnessing `kinds`,
+        minus `exclude` (calculatePartialDeps' own TxnId when the bound is its executeAt), ascending and unique (the
+        Deps.Builder's sorted set)."""
+        end = bisect.bisect_left(self.ids, started_before)            # insertPos :1373-1378
+        committed = self.committed()                                  # committedByExecuteAt :660-667
+        maw = self.max_applied_write(committed)
+        i = bisect.bisect_left([c.execute_at for c in committed], started_before) - 1   # :930-941 (last < bound)
+        while i >= 0 and kind_of(committed[i].txn) != WRITE:
+            i -= 1
+        mcwb = committed[i].execute_at if i >= 0 else None
+        out = set()
+        for t in self.ids[:end]:                                      # :945-965
+            if kind_of(t) not in kinds:
+                continue
+            inf = self.info[t]
+            if inf.status in (COMMITTED, STABLE, APPLIED):
+                if mcwb is not None and inf.execute_at < mcwb and kind_of(t) in (READ, WRITE):
+                    continue                                          # ELIDE_TRANSITIVE_DEPENDENCIES, Write.witnesses
+            elif inf.status in (TK, INVALID):
+                continue
+            out.add(t)
+        if started_before <= self.pruned_before and maw >= 0:          # :967-980
+            j = bisect.bisect_left([c.execute_at for c in committed[:maw]], started_before)
+            while kind_of(committed[j].txn) != WRITE:
+                j += 1
+            out.add(committed[j].txn)
+        out.discard(exclude)
+        return sorted(out)
+
     # -- Pruning.maybePrune / pruneBefore (Pruning.java:164-331)
     def maybe_prune(self, prune_interval, min_hlc_delta):
         if self.log is not None:
@@ -946,14 +977,55 @@ def full_scan_ready(cfk):
     return out
 
 
+def canon_view(canon):
+    """Canon's committedByExecuteAt as the release invariants read it: (executeAt, txnId, SaveStatus order, domain,
+    still waiting on the key) per committed command, executeAt ascending."""
+    out = []
+    for ex in canon.committed_by_execute_at.head(MAX):
+        c = canon.committed_by_execute_at.get(ex)
+        w = c.waiting_on
+        out.append((ex, c.txn, SS_ORDER[c.ss], canon.domains[c.txn], bool(w is not None and w.key)))
+    return out
+
+
+def release_invariant_violations(view, released):
+    """The reference's execution-order invariants, applied to a release set (txns let go at this state): for each
+    released T, (:175-180 / :208-212) every committed command executing before T that T witnesses (key domain) has
+    Applied (ExclusiveSyncPoints / EphemeralReads await only their deps); (:214-218) no Stable command executing after T
+    that witnesses T (and awaits more than its deps) has been let go — neither earlier (its key bit cleared) nor in
+    the same set.  Returns the violations."""
+    rel = set(released)
+    by_txn = {t: (ex, so, dom, waiting) for ex, t, so, dom, waiting in view}
+    bad = []
+    for t in rel:
+        if t not in by_txn:
+            bad.append(("not committed", t))
+            continue
+        tex = by_txn[t][0]
+        pk = kind_of(t)
+        for ex, c, so, dom, waiting in view:
+            if ex < tex:
+                if pk not in (ESP, EPH) and dom != RANGE and witnesses(pk, kind_of(c)) and so < SS_ORDER[APPLIED_SS]:
+                    bad.append(("unapplied predecessor", t, c))
+            elif ex > tex and by_txn[t][2] == KEY:
+                if kind_of(c) in (ESP, EPH) or not witnesses(kind_of(c), pk) or so < SS_ORDER[STABLE_SS]:
+                    continue
+                if not waiting or c in rel:
+                    bad.append(("successor released first", t, c))
+    return bad
+
+
 # ---- CommandsForKeyTest.test(seed, minCount) (:590-646) --------------------------------------------------------------
 class Run:
     """One seed of the restated harness.  events: per update, (txnId, SaveStatus) and the managed notifications it
     caused; snapshots: the CFK after events chosen by `snapshot_every` (and every event with a notification)."""
 
     def __init__(self, seed, min_count, snapshot_every=0, check_full_scan=False, count_gating=False, log=False,
-                 prune=False):
+                 prune=False, keep_states_every=0, snapshot_lag=False):
         self.seed = seed
+        self.states = {}                              # event -> CFK copy (keep_states_every: mapReduceActive probes)
+        self.canon_views = {}                         # snapshot event -> canon_view(canon) (release invariants)
+        self.lag_events = 0
         self.event_log = [] if log else None          # per harness event: the CFK update calls it made (CFK.log)
         rnd = Rnd(seed)
         self.run_task_chance = max(0.01, float(rnd.next_float()))
@@ -1034,7 +1106,15 @@ class Run:
                 got = set(full_scan_ready(cfk))
                 if got != want:
                     self.full_scan_mismatches.append((self.events, sorted(got - want), sorted(want - got)))
-            if snapshot_every and (fresh or self.events % snapshot_every == 0):
+            if keep_states_every and self.events % keep_states_every == 0:
+                self.states[self.events] = cfk.copy()
+            lagging = False
+            if snapshot_lag:                          # also every state where the notifications lag the full scan
+                want = {t for t in self.notified if cfk.info.get(t) is not None and cfk.info[t].status == STABLE}
+                lagging = set(full_scan_ready(cfk)) != want
+                self.lag_events += lagging
+            if snapshot_every and (fresh or lagging or self.events % snapshot_every == 0):
+                self.canon_views[self.events] = canon_view(canon)
                 self.snapshots.append((self.events, self.rows(), frozenset(
                     t for t in self.notified if cfk.info.get(t) is not None and cfk.info[t].status == STABLE),
                     frozenset(full_scan_ready(cfk))))

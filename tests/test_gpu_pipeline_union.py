@@ -1,8 +1,10 @@
-"""ad_run_pipeline's merged Deps as the deps stage's union view (deps.hip stage_deps, merge.hip stage_merge): the
-replies, the merged Deps (per class, ad_fetch_merged and ad_fetch_merged_all) and the levels equal the oracle's
-Deps.merge (RelationMultiMap.LinearMerger, utils/RelationMultiMap.java:284-406) on batches that take every branch
-of the deps stage: the fused tile kernel, the three-kernel path (hot keys), direct classes (sync points), txns with
-more than four keys (fill walk + k_txn_union), inline-id overflow re-walks, 1 and 7 replica views."""
+"""ad_run_pipeline's merged Deps — by default k_merge_cap over the R replies' CSRs (merge.hip merge_cap: one pass into
+capacity regions, compacted by merged_ready for the fetch), or, with ad_set_pipeline_union, the deps stage's union
+view (deps.hip stage_deps): the replies, the merged Deps (per class, ad_fetch_merged and ad_fetch_merged_all) and the
+levels equal the oracle's Deps.merge (RelationMultiMap.LinearMerger, utils/RelationMultiMap.java:284-406) on batches
+that take every branch of the deps stage: the fused tile kernel, the three-kernel path (hot keys), direct classes
+(sync points), txns with more than four keys (fill walk + k_txn_union), inline-id overflow re-walks, 1, 2, 4 and 7
+replica views (k_merge_cap's register path for <= 4 views, its serial loops above and for long lists)."""
 import numpy as np
 import pytest
 
@@ -28,14 +30,18 @@ CASES = {
     "one_view": (lambda: workload.config("C2", n=30000, seed=7), (0, 1, 0.0)),
     "seven_views": (lambda: workload.generate(20000, keys_per_txn=4, keyspace=30000, seed=8), (64, 7, 0.3)),
     "c3": (lambda: workload.config("C3", n=20000, seed=10), (32, 3, 0.1)),
+    "two_views": (lambda: workload.config("C2", n=30000, seed=11), (48, 2, 0.3)),
+    "four_views": (lambda: workload.generate(20000, keys_per_txn=4, keyspace=3000, seed=12), (40, 4, 0.25)),
 }
 
 
+@pytest.mark.parametrize("union", [False, True], ids=["merge", "union_view"])
 @pytest.mark.parametrize("name", list(CASES))
-def test_pipeline_union_equals_oracle(engine_factory, name):
+def test_pipeline_union_equals_oracle(engine_factory, name, union):
     make, (w, r, d) = CASES[name]
     b = make()
     eng = engine_factory(window=w, replicas=r, drop_p=d, seed=0x5EED)
+    eng.set_pipeline_union(union)
     eng.load(b)
     eng.run_pipeline()
     ref = O.OracleResult(b, abi.make_config(w, r, d, 0x5EED), O.FLAG_MERGE | O.FLAG_LEVELS)
@@ -53,6 +59,9 @@ def test_pipeline_union_equals_oracle(engine_factory, name):
     s = eng.merged_sizes()
     for c in range(abi.NUM_CLASSES):
         assert s[c].txns == s[c].txn_cap == len(merged[c].txns)
+    if not union:      # the merged entries k_merge_cap counted (per-workgroup sums) == the merged Deps' entries
+        want_e = sum(len(merged[c].k2t) - len(merged[c].keys) for c in range(abi.NUM_CLASSES))
+        assert eng.last_times()["merged_entries"] == want_e
     lv, order = eng.fetch_levels()
     rlv, rorder = ref.levels()
     assert np.array_equal(lv, rlv) and np.array_equal(order, rorder)
