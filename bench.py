@@ -97,10 +97,10 @@ def alg_bytes(kernel, calls, units, n, P, R, st, large=False, steps=1):
         # write pass also writes the merged rows (16 B/txn + 8 B/entry)
         "k_merge<count>": units * 16 * R + 8 * D,
         "k_merge<write>": units * (16 * R + 16) + 8 * D + 8 * M,
-        # the one-pass merge into capacity regions (k_merge_cap): per txn every reply's key_off / k2t_off / ent_off /
-        # tcnt (16 B per reply), the replies' lists (TxnId + keysToTxnIds word: 8 B per reply entry), the capacity
-        # offsets + exact counts out (24 B) and the merged lists (8 B per merged entry)
-        "k_merge_cap": units * (16 * R + 24) + 8 * D + 8 * M,
+        # Deps.merge of the replies as references (k_merge_ref; the txns whose replies differ merged in the pass): per txn
+        # every reply's key_off / k2t_off / ent_off / tcnt (16 B per reply) and the reference out (1 B); every reply entry
+        # compared once (TxnId + keysToTxnIds word: 8 B); the few merged rows are not counted
+        "k_merge_ref": units * (16 * R + 1) + 8 * D,
         # the level stage priced as SURVEY §8(d) B_level: per pair its u64 entry (8 B), per predecessor edge
         # (the walk items: entries with an earlier entry of their key) 8 B, per txn in-degree + level (8 B);
         # the same figure for the Kahn region and for the executeAt-block path
@@ -311,7 +311,7 @@ def end_to_end(eng, batch, steps):
 
 def union_view_side(eng, n, steps=5):
     """Side figure, outside the timed region: the same pipeline with ad_set_pipeline_union — the merged Deps built
-    as the deps stage's union view instead of k_merge_cap over the replies.  Only a generator that holds every view's
+    as the deps stage's union view instead of k_merge_ref over the replies.  Only a generator that holds every view's
     inputs can take that shortcut (a coordinator receiving replies cannot), so it is never `value`."""
     eng.set_pipeline_union(True)
     try:
@@ -374,7 +374,7 @@ ROCPROF_NAME = {                # tracer name -> rocprof kernel symbol(s) (profi
     "k_minmax": "ad::k_minmax", "k_pack": "ad::k_pack", "k_txn_union": "ad::k_txn_union<3>",
     "k_seg_fuse": "ad::k_seg_fuse<3, false>", "seg_keys": ("ad::k_seg_tile_scan", "ad::k_seg_ukeys"),
     "k_merge<count>": "ad::k_merge<3, false, 1>", "k_merge<write>": "ad::k_merge<3, true, 1>",
-    "k_merge_cap": "ad::k_merge_cap<3>",
+    "k_merge_ref": "ad::k_merge_ref<3>",
     # composite regions: every member kernel's dispatches of one pipeline step (the region's memsets and copies
     # are shared fill/copy kernels and are not attributed)
     "kahn_levels": ("ad::k_chain_build", "ad::k_kahn_step", "ad::k_chain_rank", "ad::k_chain_check",

@@ -64,7 +64,7 @@ class AdCfkQueries(C.Structure):
                 ("txn_node", _i32p), ("bound_msb", _u64p), ("bound_lsb", _u64p), ("bound_node", _i32p)]
 
 
-CFK_OP_UPDATE, CFK_OP_LOAD, CFK_OP_PRUNE, CFK_OP_LOADING = 0, 1, 2, 3      # AD_CFK_OP_*
+CFK_OP_UPDATE, CFK_OP_LOAD, CFK_OP_PRUNE, CFK_OP_LOADING, CFK_OP_UNMANAGED, CFK_OP_UNMANAGED_RECHECK = 0, 1, 2, 3, 4, 5  # AD_CFK_OP_*
 
 CFK_EVENT_FIELDS = (("ev_off", np.uint32), ("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),
                     ("status", np.uint8), ("exec_msb", np.uint64), ("exec_lsb", np.uint64), ("exec_node", np.int32),

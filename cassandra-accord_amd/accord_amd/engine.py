@@ -72,6 +72,8 @@ def lib():
         L.ad_cfk_store_fetch.argtypes = [vp, C.c_uint32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 9
         L.ad_cfk_store_pruning.argtypes = [vp, C.c_uint32, vp, vp, vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 5
         L.ad_cfk_store_query.argtypes = [vp, C.POINTER(abi.AdCfkQueries), C.POINTER(abi.AdCsrSizes)]
+        L.ad_cfk_store_unmanaged.argtypes = [vp, C.c_uint32, C.POINTER(C.c_size_t)] + [vp] * 7
+        L.ad_cfk_store_notified.argtypes = [vp, vp, C.POINTER(C.c_size_t)] + [vp] * 5
         L.ad_cfk_store_query_fetch.argtypes = [vp, C.c_uint32, C.POINTER(abi.AdCsrOut), vp, vp, vp]
         L.ad_preaccept_expiry.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_size_t, vp, vp, vp, vp, vp]
         L.ad_merge_host.argtypes = [vp, C.POINTER(abi.AdCsrIn), C.c_uint32, C.POINTER(abi.AdCsrSizes)]
@@ -114,7 +116,7 @@ def lib():
 EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_cfk_store_query", "ad_cfk_store_query_fetch", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_cfk_store_query", "ad_cfk_store_query_fetch", "ad_cfk_store_unmanaged", "ad_cfk_store_notified", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_pipeline_union", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
@@ -370,6 +372,34 @@ class DepsEngine:
         out["pruned_before"] = (pm.value, pl.value, pn.value)
         return out
 
+    def cfk_store_unmanaged(self, key):
+        """One key's unmanaged registry (Unmanaged.compareTo order): list of (pending, waitingUntil (msb, lsb, node),
+        TxnId (msb, lsb, node))."""
+        n = C.c_size_t()
+        self._check(lib().ad_cfk_store_unmanaged(self.h, key, C.byref(n), *([None] * 7)), "ad_cfk_store_unmanaged")
+        m = n.value
+        arr = [np.zeros(max(m, 1), dt) for dt in (np.uint8, np.uint64, np.uint64, np.int32, np.uint64, np.uint64, np.int32)]
+        self._check(lib().ad_cfk_store_unmanaged(self.h, key, C.byref(n), *(x.ctypes.data for x in arr)), "ad_cfk_store_unmanaged")
+        return [(int(arr[0][i]), (int(arr[1][i]), int(arr[2][i]), int(arr[3][i])), (int(arr[4][i]), int(arr[5][i]), int(arr[6][i])))
+                for i in range(m)]
+
+    def cfk_store_notified(self):
+        """The last cfk_store_apply's unmanaged notifications: per key a list of (event index within the key's events
+        of the call, tag, TxnId (msb, lsb, node)); tag 0 commit, 1 applied, 2 ready at (re)registration."""
+        cnt = np.zeros(self._cs_keys, np.uint32)
+        tot = C.c_size_t()
+        self._check(lib().ad_cfk_store_notified(self.h, cnt.ctypes.data, C.byref(tot), *([None] * 5)), "ad_cfk_store_notified")
+        m = tot.value
+        arr = [np.zeros(max(m, 1), dt) for dt in (np.uint32, np.uint8, np.uint64, np.uint64, np.int32)]
+        self._check(lib().ad_cfk_store_notified(self.h, cnt.ctypes.data, C.byref(tot), *(x.ctypes.data for x in arr)),
+                    "ad_cfk_store_notified")
+        out, o = [], 0
+        for k in range(self._cs_keys):
+            out.append([(int(arr[0][i]), int(arr[1][i]), (int(arr[2][i]), int(arr[3][i]), int(arr[4][i])))
+                        for i in range(o, o + int(cnt[k]))])
+            o += int(cnt[k])
+        return out
+
     def cfk_store_query(self, key_off, keys, txn, bound):
         """CommandsForKey.mapReduceActive over the resident rows for queries (ad_cfk_store_query): key_off [nq + 1] /
         keys (store key indices, ascending per query); txn and bound: (msb, lsb, node) arrays [nq] (the querying TxnId and
@@ -610,7 +640,7 @@ class DepsEngine:
 
     def set_pipeline_union(self, on):
         """True: run_pipeline builds the merged Deps as the deps stage's union view (a generator-only shortcut, a
-        side figure); False (default): k_merge_cap merges the R replies' CSRs (Deps.merge)."""
+        side figure); False (default): k_merge_ref merges the R replies' CSRs (Deps.merge)."""
         self._check(lib().ad_set_pipeline_union(self.h, 1 if on else 0), "ad_set_pipeline_union")
 
     def set_trace(self, mask):

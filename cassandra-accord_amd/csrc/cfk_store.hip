@@ -31,6 +31,14 @@ int ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity) {
     CK(dalloc(h, S_CS0 + 16, &c.lp_cnt, c.K)); CK(dalloc(h, S_CS0 + 17, &c.lpm, rows));
     CK(dalloc(h, S_CS0 + 18, &c.lpl, rows)); CK(dalloc(h, S_CS0 + 19, &c.lpn, rows));
     CK(dalloc(h, S_CS0 + 20, &c.lp_bits, rows * c.words));
+    CK(dalloc(h, S_CSU0 + 0, &c.lp_xm, rows)); CK(dalloc(h, S_CSU0 + 1, &c.lp_xl, rows)); CK(dalloc(h, S_CSU0 + 2, &c.lp_xn, rows));
+    CK(dalloc(h, S_CSU0 + 3, &c.lp_xh, rows)); CK(dalloc(h, S_CSU0 + 4, &c.um_cnt, c.K)); CK(dalloc(h, S_CSU0 + 5, &c.um_p, rows));
+    CK(dalloc(h, S_CSU0 + 6, &c.um_wm, rows)); CK(dalloc(h, S_CSU0 + 7, &c.um_wl, rows)); CK(dalloc(h, S_CSU0 + 8, &c.um_wn, rows));
+    CK(dalloc(h, S_CSU0 + 9, &c.um_tm, rows)); CK(dalloc(h, S_CSU0 + 10, &c.um_tl, rows)); CK(dalloc(h, S_CSU0 + 11, &c.um_tn, rows));
+    CK(dalloc(h, S_CSU0 + 12, &c.nt_cnt, c.K));
+    HIPCHK(h, hipMemsetAsync(c.um_cnt, 0, (size_t)c.K * 4, h->st));
+    HIPCHK(h, hipMemsetAsync(c.nt_cnt, 0, (size_t)c.K * 4, h->st));
+    c.nt_total = 0;
     HIPCHK(h, hipMemsetAsync(c.pbm, 0, (size_t)c.K * 8, h->st));
     HIPCHK(h, hipMemsetAsync(c.pbl, 0, (size_t)c.K * 8, h->st));
     HIPCHK(h, hipMemsetAsync(c.pbn, 0, (size_t)c.K * 4, h->st));
@@ -53,14 +61,21 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
         if (ev->ev_off[k + 1] < ev->ev_off[k]) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: ev_off not monotone");
     for (size_t e = 0; e < m; ++e)
         if (ev->deps_off[e + 1] < ev->deps_off[e]) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: deps_off not monotone");
-    if (m == 0) return AD_OK;
+    if (m == 0) {
+        hipSetDevice(h->device);
+        HIPCHK(h, hipMemsetAsync(c.nt_cnt, 0, (size_t)c.K * 4, h->st));   // this call notified nothing
+        c.ev_off_host.assign(ev->ev_off, ev->ev_off + c.K + 1);
+        c.nt_base_host.assign(c.K + 1, 0);
+        HIPCHK(h, hipStreamSynchronize(h->st));
+        return AD_OK;
+    }
     if (!ev->txn_msb || !ev->txn_lsb || !ev->txn_node || !ev->status || !ev->exec_msb || !ev->exec_lsb || !ev->exec_node)
         return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: an event array is missing");
     for (size_t e = 0; e < m; ++e)
         if (ev->status[e] > AD_ST_INVALID) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: status out of range");
     if (ev->op)
         for (size_t e = 0; e < m; ++e) {
-            if (ev->op[e] > AD_CFK_OP_LOADING) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: op out of range");
+            if (ev->op[e] > AD_CFK_OP_UNMANAGED_RECHECK) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: op out of range");
             if (ev->op[e] == AD_CFK_OP_PRUNE && ev->exec_node[e] < 0)
                 return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_apply: a PRUNE event's interval (exec_node) is negative");
             if (ev->op[e] == AD_CFK_OP_LOADING && ev->deps_off[e + 1] - ev->deps_off[e] > 1)
@@ -115,6 +130,23 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     a.overflow = c.flags; a.bad = c.flags + 1;
     a.pbm = c.pbm; a.pbl = c.pbl; a.pbn = c.pbn; a.lp_cnt = c.lp_cnt; a.lpm = c.lpm; a.lpl = c.lpl; a.lpn = c.lpn;
     a.lp_bits = c.lp_bits; a.eop = eop;
+    a.lp_xm = c.lp_xm; a.lp_xl = c.lp_xl; a.lp_xn = c.lp_xn; a.lp_xh = c.lp_xh;
+    a.um_cnt = c.um_cnt; a.um_p = c.um_p; a.um_wm = c.um_wm; a.um_wl = c.um_wl; a.um_wn = c.um_wn;
+    a.um_tm = c.um_tm; a.um_tl = c.um_tl; a.um_tn = c.um_tn;
+    // notifications: per key a region of (its events + the registry's capacity) entries
+    {
+        std::vector<uint32_t> nb(c.K + 1, 0);
+        for (uint32_t k = 0; k < c.K; ++k) nb[k + 1] = nb[k] + (ev->ev_off[k + 1] - ev->ev_off[k]) + c.cap;
+        c.nt_base_host = nb;
+        const size_t tot = std::max<size_t>(nb[c.K], 1);
+        CK(dalloc(h, S_CSU0 + 13, &c.nt_base, c.K + 1)); CK(dalloc(h, S_CSU0 + 14, &c.nt_ev, tot));
+        CK(dalloc(h, S_CSU0 + 15, &c.nt_tag, tot)); CK(dalloc(h, S_CSU0 + 16, &c.nt_tm, tot));
+        CK(dalloc(h, S_CSU0 + 17, &c.nt_tl, tot)); CK(dalloc(h, S_CSU0 + 18, &c.nt_tn, tot));
+        HIPCHK(h, hipMemcpyAsync(c.nt_base, nb.data(), (c.K + 1) * 4, hipMemcpyHostToDevice, st));
+        c.ev_off_host.assign(ev->ev_off, ev->ev_off + c.K + 1);
+    }
+    a.nt_base = c.nt_base; a.nt_cnt = c.nt_cnt; a.nt_ev = c.nt_ev; a.nt_tag = c.nt_tag;
+    a.nt_tm = c.nt_tm; a.nt_tl = c.nt_tl; a.nt_tn = c.nt_tn;
     HIPCHK(h, hipMemsetAsync(c.flags, 0, 8, st));          // this call's overflow / order flags
     k_cfk_apply<<<c.K, CS_T, 0, st>>>(a);
     HIPCHK(h, hipGetLastError());
@@ -409,6 +441,71 @@ int ad_cfk_store_query_fetch(ad_handle* h, uint32_t cls, ad_csr_out* out, uint64
         }
         ko += nk; mo += nm; to += nt;
         out->key_off[x + 1] = (uint32_t)ko; out->k2t_off[x + 1] = (uint32_t)mo; out->txn_off[x + 1] = (uint32_t)to;
+    }
+    return AD_OK;
+}
+
+// ---- the unmanaged registry and the last apply's unmanaged notifications -----------------------------------------
+int ad_cfk_store_unmanaged(ad_handle* h, uint32_t key, size_t* count, uint8_t* pending, uint64_t* wait_msb,
+                           uint64_t* wait_lsb, int32_t* wait_node, uint64_t* txn_msb, uint64_t* txn_lsb, int32_t* txn_node) {
+    if (!h || !count) return AD_ERR_ARGUMENT;
+    auto& c = h->cs;
+    if (!c.K) return set_err(h, AD_ERR_STATE, "ad_cfk_store_unmanaged before ad_cfk_store_open");
+    if (key >= c.K) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_unmanaged: key out of range");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    uint32_t U = 0;
+    HIPCHK(h, hipMemcpyAsync(&U, c.um_cnt + key, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    *count = U;
+    const size_t b = (size_t)key * c.cap;
+    if (U) {
+        if (pending) HIPCHK(h, hipMemcpyAsync(pending, c.um_p + b, U, hipMemcpyDeviceToHost, st));
+        if (wait_msb) HIPCHK(h, hipMemcpyAsync(wait_msb, c.um_wm + b, U * 8, hipMemcpyDeviceToHost, st));
+        if (wait_lsb) HIPCHK(h, hipMemcpyAsync(wait_lsb, c.um_wl + b, U * 8, hipMemcpyDeviceToHost, st));
+        if (wait_node) HIPCHK(h, hipMemcpyAsync(wait_node, c.um_wn + b, U * 4, hipMemcpyDeviceToHost, st));
+        if (txn_msb) HIPCHK(h, hipMemcpyAsync(txn_msb, c.um_tm + b, U * 8, hipMemcpyDeviceToHost, st));
+        if (txn_lsb) HIPCHK(h, hipMemcpyAsync(txn_lsb, c.um_tl + b, U * 8, hipMemcpyDeviceToHost, st));
+        if (txn_node) HIPCHK(h, hipMemcpyAsync(txn_node, c.um_tn + b, U * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    return AD_OK;
+}
+
+int ad_cfk_store_notified(ad_handle* h, uint32_t* counts, size_t* total, uint32_t* event, uint8_t* tag, uint64_t* txn_msb,
+                          uint64_t* txn_lsb, int32_t* txn_node) {
+    if (!h || !total) return AD_ERR_ARGUMENT;
+    auto& c = h->cs;
+    if (!c.K) return set_err(h, AD_ERR_STATE, "ad_cfk_store_notified before ad_cfk_store_open");
+    hipSetDevice(h->device);
+    hipStream_t st = h->st;
+    std::vector<uint32_t> cnt(c.K);
+    HIPCHK(h, hipMemcpyAsync(cnt.data(), c.nt_cnt, (size_t)c.K * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    size_t tot = 0;
+    for (uint32_t k = 0; k < c.K; ++k) { if (counts) counts[k] = cnt[k]; tot += cnt[k]; }
+    *total = tot;
+    if (!event && !tag && !txn_msb && !txn_lsb && !txn_node) return AD_OK;
+    size_t o = 0;
+    for (uint32_t k = 0; k < c.K && tot; ++k) {
+        if (!cnt[k]) continue;
+        const size_t b = c.nt_base_host[k];
+        if (event) {
+            HIPCHK(h, hipMemcpyAsync(event + o, c.nt_ev + b, cnt[k] * 4, hipMemcpyDeviceToHost, st));
+        }
+        if (tag) HIPCHK(h, hipMemcpyAsync(tag + o, c.nt_tag + b, cnt[k], hipMemcpyDeviceToHost, st));
+        if (txn_msb) HIPCHK(h, hipMemcpyAsync(txn_msb + o, c.nt_tm + b, cnt[k] * 8, hipMemcpyDeviceToHost, st));
+        if (txn_lsb) HIPCHK(h, hipMemcpyAsync(txn_lsb + o, c.nt_tl + b, cnt[k] * 8, hipMemcpyDeviceToHost, st));
+        if (txn_node) HIPCHK(h, hipMemcpyAsync(txn_node + o, c.nt_tn + b, cnt[k] * 4, hipMemcpyDeviceToHost, st));
+        o += cnt[k];
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (event) {                                 // event indices relative to the key's events of the call
+        o = 0;
+        for (uint32_t k = 0; k < c.K; ++k) {
+            for (uint32_t i = 0; i < cnt[k]; ++i) event[o + i] -= c.ev_off_host[k];
+            o += cnt[k];
+        }
     }
     return AD_OK;
 }

@@ -53,13 +53,32 @@ struct CfkStoreArgs {
     uint64_t *lpm, *lpl;                      // [K * cap] their TxnIds
     int32_t* lpn;
     uint64_t* lp_bits;                        // [(K * cap) * words] their witnesses
+    uint64_t *lp_xm, *lp_xl;                  // [K * cap] each entry's least witness TxnId, rows or not
+    int32_t* lp_xn;                           //   (isAnyPredecessorWaitingOnPruned reads witnessedBy's first)
+    uint8_t* lp_xh;
     const uint8_t* eop;                       // [m] event op (CS_OP_*; nullptr: every event an UPDATE)
+    // unmanaged registry (CommandsForKey.unmanageds, sorted by Unmanaged.compareTo: pending, waitingUntil, txnId)
+    uint32_t* um_cnt;                         // [K]
+    uint8_t* um_p;                            // [K * cap] COMMIT (0) / APPLY (1)
+    uint64_t *um_wm, *um_wl, *um_tm, *um_tl;
+    int32_t *um_wn, *um_tn;
+    // this call's unmanaged notifications, key k's at nt_base[k]: (event, tag, TxnId) in order; tag 0 =
+    // NotifyUnmanagedOfCommit, 1 = NotifyNotWaiting (applied), 2 = registerUnmanaged / updateUnmanaged found it ready
+    const uint32_t* nt_base;
+    uint32_t* nt_cnt;                         // [K]
+    uint32_t* nt_ev;
+    uint8_t* nt_tag;
+    uint64_t *nt_tm, *nt_tl;
+    int32_t* nt_tn;
 };
 // event ops (ad_cfk_events.op)
 constexpr uint32_t CS_OP_UPDATE = 0;         // CommandsForKey.update (or insertAdditionsOnly: status TRANSITIVELY_KNOWN)
 constexpr uint32_t CS_OP_LOAD = 1;           // CommandsForKey.updatePruned of a loaded pruned command
 constexpr uint32_t CS_OP_PRUNE = 2;          // maybePrune(exec_node = pruneInterval, exec_msb = minHlcDelta)
 constexpr uint32_t CS_OP_LOADING = 3;        // txn joins loadingPruned, witnessed by the event's deps
+constexpr uint32_t CS_OP_UNMANAGED = 4;      // registerUnmanaged: Updating.updateUnmanaged(register = true)
+constexpr uint32_t CS_OP_UNMANAGED_RECHECK = 5;   // updateUnmanaged(register = false): a notified commit re-checked
+constexpr uint32_t UM_COMMIT = 0, UM_APPLY = 1;
 
 __device__ inline bool cs_has_deps(uint32_t s) {            // InternalStatus.hasExecuteAtOrDeps
     return s == AD_ST_ACCEPTED || s == AD_ST_COMMITTED || s == AD_ST_STABLE || s == AD_ST_APPLIED;
@@ -162,18 +181,26 @@ __device__ inline int cs_lp_find(const CfkStoreArgs& a, uint32_t key, uint32_t L
     __syncthreads();
     return j;
 }
-// Pruning.loadPruned: t joins the table (or is found there) and slot `w` (if any) joins its witnesses; false: full
-__device__ inline bool cs_lp_add(const CfkStoreArgs& a, uint32_t key, uint32_t& L, const Ts3& t, uint32_t w, int* s_j) {
+// Pruning.loadPruned: t joins the table (or is found there) and slot `w` (if any) joins its witnesses, the witness
+// TxnId `wt` (if has_wt; a row or not) its least witness; false: full
+__device__ inline bool cs_lp_add(const CfkStoreArgs& a, uint32_t key, uint32_t& L, const Ts3& t, uint32_t w, int* s_j,
+                                 const Ts3& wt = Ts3{0, 0, 0}, bool has_wt = false) {
     const size_t lb = (size_t)key * a.cap;
     int j = cs_lp_find(a, key, L, t, s_j);
     if (j < 0) {
         if (L >= a.cap) return false;
         j = (int)L++;
         for (uint32_t q = threadIdx.x; q < a.words; q += CS_T) a.lp_bits[(lb + j) * a.words + q] = 0ull;
-        if (threadIdx.x == 0) { a.lpm[lb + j] = t.msb; a.lpl[lb + j] = t.lsb; a.lpn[lb + j] = t.node; }
+        if (threadIdx.x == 0) { a.lpm[lb + j] = t.msb; a.lpl[lb + j] = t.lsb; a.lpn[lb + j] = t.node; a.lp_xh[lb + j] = 0; }
         __syncthreads();
     }
     if (w != 0xFFFFFFFFu && threadIdx.x == 0) a.lp_bits[(lb + j) * a.words + (w >> 6)] |= 1ull << (w & 63);
+    if (has_wt && threadIdx.x == 0) {
+        const size_t x = lb + j;
+        if (!a.lp_xh[x] || ts3_cmp(wt, Ts3{a.lp_xm[x], a.lp_xl[x], a.lp_xn[x]}) < 0) {
+            a.lp_xm[x] = wt.msb; a.lp_xl[x] = wt.lsb; a.lp_xn[x] = wt.node; a.lp_xh[x] = 1;
+        }
+    }
     __syncthreads();
     return true;
 }
@@ -184,7 +211,11 @@ __device__ inline void cs_lp_remove(const CfkStoreArgs& a, uint32_t key, uint32_
     if ((uint32_t)j != last) {
         for (uint32_t q = threadIdx.x; q < a.words; q += CS_T)
             a.lp_bits[(lb + j) * a.words + q] = a.lp_bits[(lb + last) * a.words + q];
-        if (threadIdx.x == 0) { a.lpm[lb + j] = a.lpm[lb + last]; a.lpl[lb + j] = a.lpl[lb + last]; a.lpn[lb + j] = a.lpn[lb + last]; }
+        if (threadIdx.x == 0) {
+            a.lpm[lb + j] = a.lpm[lb + last]; a.lpl[lb + j] = a.lpl[lb + last]; a.lpn[lb + j] = a.lpn[lb + last];
+            a.lp_xm[lb + j] = a.lp_xm[lb + last]; a.lp_xl[lb + j] = a.lp_xl[lb + last]; a.lp_xn[lb + j] = a.lp_xn[lb + last];
+            a.lp_xh[lb + j] = a.lp_xh[lb + last];
+        }
     }
     --L;
     __syncthreads();
@@ -379,6 +410,201 @@ __device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_
     n -= removed;
 }
 
+// ---- unmanaged txns (CommandsForKey.unmanageds; Updating.updateUnmanaged :715-849, PostProcess.notifyUnmanaged :164-246)
+__device__ inline bool cs_me(uint64_t lsb) {                   // CommandsForKey.managesExecution: key-domain Read / Write
+    const uint32_t k = cs_kind(lsb);
+    return (lsb & 1ull) == 0 && (k == AD_KIND_READ || k == AD_KIND_WRITE);
+}
+// Unmanaged.compareTo: pending, then waitingUntil, then txnId
+__device__ inline int cs_um_cmp(uint32_t p1, const Ts3& w1, const Ts3& t1, uint32_t p2, const Ts3& w2, const Ts3& t2) {
+    if (p1 != p2) return p1 < p2 ? -1 : 1;
+    const int c = ts3_cmp(w1, w2);
+    return c != 0 ? c : ts3_cmp(t1, t2);
+}
+__device__ inline Ts3 cs_um_w(const CfkStoreArgs& a, size_t x) { return Ts3{a.um_wm[x], a.um_wl[x], a.um_wn[x]}; }
+__device__ inline Ts3 cs_um_t(const CfkStoreArgs& a, size_t x) { return Ts3{a.um_tm[x], a.um_tl[x], a.um_tn[x]}; }
+// (thread 0) one notification of this call
+__device__ inline void cs_um_emit(const CfkStoreArgs& a, uint32_t key, uint32_t e, uint32_t tag, const Ts3& t) {
+    const uint32_t o = a.nt_base[key] + a.nt_cnt[key]++;
+    a.nt_ev[o] = e; a.nt_tag[o] = (uint8_t)tag; a.nt_tm[o] = t.msb; a.nt_tl[o] = t.lsb; a.nt_tn[o] = t.node;
+}
+// (thread 0) entries [s, e) leave the registry
+__device__ inline void cs_um_remove(const CfkStoreArgs& a, size_t ub, uint32_t& U, uint32_t s, uint32_t e) {
+    const uint32_t d = e - s;
+    for (uint32_t i = e; i < U; ++i) {
+        const size_t x = ub + i, y = ub + i - d;
+        a.um_p[y] = a.um_p[x]; a.um_wm[y] = a.um_wm[x]; a.um_wl[y] = a.um_wl[x]; a.um_wn[y] = a.um_wn[x];
+        a.um_tm[y] = a.um_tm[x]; a.um_tl[y] = a.um_tl[x]; a.um_tn[y] = a.um_tn[x];
+    }
+    U -= d;
+}
+// (thread 0) (p, w, t) joins the sorted registry unless present (linearUnion of the sorted arrays); false: full
+__device__ inline bool cs_um_insert(const CfkStoreArgs& a, size_t ub, uint32_t cap, uint32_t& U, uint32_t p, const Ts3& w,
+                                    const Ts3& t) {
+    uint32_t lo = 0, hi = U;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (cs_um_cmp(a.um_p[ub + m], cs_um_w(a, ub + m), cs_um_t(a, ub + m), p, w, t) < 0) lo = m + 1; else hi = m;
+    }
+    if (lo < U && cs_um_cmp(a.um_p[ub + lo], cs_um_w(a, ub + lo), cs_um_t(a, ub + lo), p, w, t) == 0) return true;
+    if (U >= cap) return false;
+    for (uint32_t i = U; i > lo; --i) {
+        const size_t x = ub + i - 1, y = ub + i;
+        a.um_p[y] = a.um_p[x]; a.um_wm[y] = a.um_wm[x]; a.um_wl[y] = a.um_wl[x]; a.um_wn[y] = a.um_wn[x];
+        a.um_tm[y] = a.um_tm[x]; a.um_tl[y] = a.um_tl[x]; a.um_tn[y] = a.um_tn[x];
+    }
+    const size_t x = ub + lo;
+    a.um_p[x] = (uint8_t)p; a.um_wm[x] = w.msb; a.um_wl[x] = w.lsb; a.um_wn[x] = w.node;
+    a.um_tm[x] = t.msb; a.um_tl[x] = t.lsb; a.um_tn[x] = t.node;
+    ++U;
+    return true;
+}
+
+// PostProcess.notifyUnmanaged after an update that changed the key (new InternalStatus ns, executeAt ex): the unmanageds
+// waiting for every managed txn below minUndecided (and below the first loadingPruned TxnId) to commit are notified
+// (findCommit, exclusive bound); when the update applied something, the ones waiting for the contiguous applied prefix
+// to reach their waitingUntil (maxContiguousManagedApplied, findFirstApply / findApply, inclusive).
+__device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t base, uint32_t n, uint32_t L, uint32_t ns,
+                                    const Ts3& ex, uint32_t e, CsPruneLds& s, uint32_t* s_U) {
+    const int tid = threadIdx.x;
+    const size_t ub = (size_t)key * a.cap, lb = ub;
+    Ts3 b{0, 0, 0};
+    bool hb = false;
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (a.st[x] < AD_ST_COMMITTED && cs_me(a.tl[x])) {
+            const Ts3 u{a.tm[x], a.tl[x], a.tn[x]};
+            if (!hb || ts3_cmp(u, b) < 0) { b = u; hb = true; }
+        }
+    }
+    for (uint32_t j = tid; j < L; j += CS_T) {
+        const Ts3 u{a.lpm[lb + j], a.lpl[lb + j], a.lpn[lb + j]};
+        if (!hb || ts3_cmp(u, b) < 0) { b = u; hb = true; }
+    }
+    nf_block_fold<false>(b, hb, s.v, s.h);
+    if (tid == 0) {
+        uint32_t U = *s_U, end = 0;
+        while (end < U && a.um_p[ub + end] == UM_COMMIT && (!hb || ts3_cmp(b, cs_um_w(a, ub + end)) > 0)) ++end;
+        for (uint32_t i = 0; i < end; ++i) cs_um_emit(a, key, e, 0, cs_um_t(a, ub + i));
+        if (end) cs_um_remove(a, ub, U, 0, end);
+        *s_U = U;
+    }
+    __syncthreads();
+    if (ns < AD_ST_APPLIED) return;
+    // maxContiguousManagedApplied (CommandsForKey.java:1419-1436): the last committed txn by executeAt before the first
+    // committed, unapplied Read / Write executing after maxAppliedWrite
+    Ts3 maw{0, 0, 0}, bl{0, 0, 0}, mca{0, 0, 0};
+    bool hm = false, hbl = false, hmca = false;
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (a.st[x] == AD_ST_APPLIED && cs_kind(a.tl[x]) == AD_KIND_WRITE) {
+            const Ts3 u{a.em[x], a.el[x], a.en[x]};
+            if (!hm || ts3_cmp(u, maw) > 0) { maw = u; hm = true; }
+        }
+    }
+    nf_block_fold<true>(maw, hm, s.v, s.h);
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        const uint32_t st = a.st[x];
+        if (cs_decided(st) && st != AD_ST_APPLIED && cs_me(a.tl[x])) {
+            const Ts3 u{a.em[x], a.el[x], a.en[x]};
+            if ((!hm || ts3_cmp(u, maw) > 0) && (!hbl || ts3_cmp(u, bl) < 0)) { bl = u; hbl = true; }
+        }
+    }
+    nf_block_fold<false>(bl, hbl, s.v, s.h);
+    for (uint32_t r = tid; r < n; r += CS_T) {
+        const size_t x = base + r;
+        if (cs_decided(a.st[x])) {
+            const Ts3 u{a.em[x], a.el[x], a.en[x]};
+            if ((!hbl || ts3_cmp(u, bl) < 0) && (!hmca || ts3_cmp(u, mca) > 0)) { mca = u; hmca = true; }
+        }
+    }
+    nf_block_fold<true>(mca, hmca, s.v, s.h);
+    if (hmca && ts3_cmp(mca, ex) < 0) hmca = false;
+    if (hmca && tid == 0) {
+        uint32_t U = *s_U, st = 0;
+        while (st < U && a.um_p[ub + st] == UM_COMMIT) ++st;
+        uint32_t end = st;
+        while (end < U && ts3_cmp(mca, cs_um_w(a, ub + end)) >= 0) ++end;
+        for (uint32_t i = st; i < end; ++i) cs_um_emit(a, key, e, 1, cs_um_t(a, ub + i));
+        if (end != st) cs_um_remove(a, ub, U, st, end);
+        *s_U = U;
+    }
+    __syncthreads();
+}
+
+// Updating.updateUnmanaged (:715-849) for unmanaged txn t (kind from its TxnId, executeAt wex) whose deps at this key are
+// the Read / Write TxnIds dep[d0, d1): readyToApply / waitingToApply / executesAt over the rows it depends on (and, for
+// sync points, the managed rows between its first and last dependency); register (registerUnmanaged): a dependency the
+// key does not know holds it back (its TRANSITIVELY_KNOWN row or its loadingPruned entry is an earlier event of the
+// stream); not ready -> (APPLY, executesAt) or (COMMIT, the last dependency) joins the registry, else it is notified.
+// false: the registry is full.
+__device__ inline bool cs_um_update(const CfkStoreArgs& a, uint32_t key, size_t base, uint32_t n, uint32_t L, const Ts3& t,
+                                    const Ts3& wex, uint32_t d0, uint32_t d1, bool reg, uint32_t e, CsPruneLds& s,
+                                    uint32_t* s_U) {
+    const int tid = threadIdx.x;
+    if (d0 == d1) {
+        if (tid == 0) cs_um_emit(a, key, e, 2, t);
+        __syncthreads();
+        return true;
+    }
+    const uint32_t wk = cs_kind(t.lsb);
+    const bool sync = wk == AD_KIND_SYNC_POINT || wk == AD_KIND_EXCLUSIVE_SYNC_POINT;
+    bool ready = true, waiting = true, hx = false;
+    Ts3 xm{0, 0, 0};
+    auto consider = [&](size_t x) {
+        const uint32_t st = a.st[x];
+        if (st < AD_ST_COMMITTED) { ready = waiting = false; return; }
+        if (st == AD_ST_INVALID) return;
+        const Ts3 u{a.em[x], a.el[x], a.en[x]};
+        if (ts3_cmp(u, wex) < 0 || wk == AD_KIND_EPHEMERAL_READ ||
+            (wk == AD_KIND_EXCLUSIVE_SYNC_POINT && ts3_cmp(Ts3{a.tm[x], a.tl[x], a.tn[x]}, t) < 0)) {
+            ready = ready && st == AD_ST_APPLIED;
+            if (!hx || ts3_cmp(u, xm) > 0) { xm = u; hx = true; }
+        }
+    };
+    for (uint32_t j = d0 + tid; j < d1; j += CS_T) {
+        bool f;
+        const uint32_t q = cs_find(a, base, n, Ts3{a.dtm[j], a.dtl[j], a.dtn[j]}, f);
+        if (f) consider(base + q);
+        else if (reg) ready = waiting = false;
+    }
+    if (sync) {                                                   // the managed rows between the deps (:760-777)
+        bool f0, f1;
+        const uint32_t lo = cs_find(a, base, n, Ts3{a.dtm[d0], a.dtl[d0], a.dtn[d0]}, f0);
+        uint32_t hi = cs_find(a, base, n, Ts3{a.dtm[d1 - 1], a.dtl[d1 - 1], a.dtn[d1 - 1]}, f1);
+        hi += f1 ? 1u : 0u;
+        for (uint32_t r = lo + tid; r < hi; r += CS_T)
+            if (cs_me(a.tl[base + r])) consider(base + r);
+        // Pruning.isAnyPredecessorWaitingOnPruned (:140-157): a loading managed TxnId below t witnessed at or before t
+        const size_t lb = (size_t)key * a.cap;
+        bool anyp = false;
+        for (uint32_t j = tid; j < L; j += CS_T) {
+            const size_t x = lb + j;
+            anyp |= ts3_cmp(Ts3{a.lpm[x], a.lpl[x], a.lpn[x]}, t) < 0 && cs_me(a.lpl[x]) && a.lp_xh[x] &&
+                    ts3_cmp(t, Ts3{a.lp_xm[x], a.lp_xl[x], a.lp_xn[x]}) >= 0;
+        }
+        if (anyp) ready = waiting = false;
+    }
+    ready = __syncthreads_and(ready ? 1 : 0) != 0;
+    waiting = __syncthreads_and(waiting ? 1 : 0) != 0;
+    nf_block_fold<true>(xm, hx, s.v, s.h);
+    bool ok = true;
+    if (tid == 0) {
+        const size_t ub = (size_t)key * a.cap;
+        uint32_t U = *s_U;
+        if (ready) cs_um_emit(a, key, e, 2, t);
+        else if (waiting) ok = cs_um_insert(a, ub, a.cap, U, UM_APPLY, xm, t);
+        else ok = cs_um_insert(a, ub, a.cap, U, UM_COMMIT, Ts3{a.dtm[d1 - 1], a.dtl[d1 - 1], a.dtn[d1 - 1]}, t);
+        *s_U = U;
+        s.idx = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    ok = s.idx != 0;
+    __syncthreads();
+    return ok;
+}
+
 // CommandsForKey.update for a stream of commands (ballots all zero: a command updates its TxnInfo only when its
 // InternalStatus rises, as in CommandsForKeyTest), Updating.insertOrUpdate's cases (Updating.java:99-358):
 //   statuses with deps (ACCEPTED .. APPLIED): the row's missing set is rebuilt from the command's deps (every
@@ -399,11 +625,14 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
     __shared__ uint32_t s_nadd;
     __shared__ int s_j;
     __shared__ CsPruneLds s_prune;
+    __shared__ uint32_t s_U;
     const uint32_t key = blockIdx.x;
     if (key >= a.K) return;
     const size_t base = (size_t)key * a.cap;
     uint32_t n = a.cnt[key];
     uint32_t L = a.lp_cnt[key];
+    if (threadIdx.x == 0) { s_U = a.um_cnt[key]; a.nt_cnt[key] = 0; }
+    __syncthreads();
     for (uint32_t e = a.ev_off[key]; e < a.ev_off[key + 1]; ++e) {
         const Ts3 t{a.etm[e], a.etl[e], a.etn[e]};
         const uint32_t op = a.eop ? a.eop[e] : CS_OP_UPDATE;
@@ -414,13 +643,24 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
         }
         if (op == CS_OP_LOADING) {
             uint32_t w = 0xFFFFFFFFu;
-            if (a.dep_off[e + 1] > a.dep_off[e]) {
+            Ts3 wt{0, 0, 0};
+            const bool hw = a.dep_off[e + 1] > a.dep_off[e];
+            if (hw) {
                 const uint32_t j = a.dep_off[e];
+                wt = Ts3{a.dtm[j], a.dtl[j], a.dtn[j]};
                 bool f;
-                const uint32_t q = cs_find(a, base, n, Ts3{a.dtm[j], a.dtl[j], a.dtn[j]}, f);
+                const uint32_t q = cs_find(a, base, n, wt, f);
                 if (f) w = a.slot[base + q];
             }
-            if (!cs_lp_add(a, key, L, t, w, &s_j)) { if (threadIdx.x == 0) *a.overflow = 1u; break; }
+            if (!cs_lp_add(a, key, L, t, w, &s_j, wt, hw)) { if (threadIdx.x == 0) *a.overflow = 1u; break; }
+            continue;
+        }
+        if (op == CS_OP_UNMANAGED || op == CS_OP_UNMANAGED_RECHECK) {
+            if (!cs_um_update(a, key, base, n, L, t, Ts3{a.eem[e], a.eel[e], a.een[e]}, a.dep_off[e], a.dep_off[e + 1],
+                              op == CS_OP_UNMANAGED, e, s_prune, &s_U)) {
+                if (threadIdx.x == 0) *a.overflow = 1u;
+                break;
+            }
             continue;
         }
         const uint32_t ns = a.est[e];
@@ -453,6 +693,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             else if (found && cur < AD_ST_COMMITTED && ns == AD_ST_INVALID) cs_remove_missing(a, base, n, ts);
             else if (!found && ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu, s_miss);
             __syncthreads();
+            cs_um_notify(a, key, base, n, L, ns, ex, e, s_prune, &s_U);
             continue;
         }
         const uint32_t d0 = a.dep_off[e], d1 = a.dep_off[e + 1];
@@ -512,7 +753,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 const uint32_t q = cs_find(a, base, n, d, f);
                 if (f) continue;
                 if (ts3_cmp(d, pb) < 0) continue;                      // a pruned addition: loadingPruned, below
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; return; }
                 if (s_nadd >= (uint32_t)CS_T) flush_adds(cmd_slot);
                 const uint32_t s = cs_insert(a, base, n, q, d, AD_ST_TRANSITIVELY_KNOWN, d);
                 if (threadIdx.x == 0) s_add[s_nadd++] = s;
@@ -522,7 +763,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             bool fnow;
             const uint32_t p2 = cs_find(a, base, n, t, fnow);           // t's position after the additions
             if (!fnow) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; return; }
                 ts = cs_insert(a, base, n, p2, t, ns, ex);
             } else {
                 ts = a.slot[base + p2];
@@ -540,8 +781,8 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 bool f;
                 cs_find(a, base, n, d, f);
                 if (f) continue;
-                if (!cs_lp_add(a, key, L, d, ts, &s_j)) {
-                    if (threadIdx.x == 0) *a.overflow = 1u;
+                if (!cs_lp_add(a, key, L, d, ts, &s_j, t, true)) {
+                    if (threadIdx.x == 0) { *a.overflow = 1u; a.um_cnt[key] = s_U; }
                     a.cnt[key] = n; a.lp_cnt[key] = L;
                     return;
                 }
@@ -549,9 +790,11 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             flush_adds(ts);
             if (!found && ns < AD_ST_COMMITTED) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             if (found && cur < AD_ST_COMMITTED && ns >= AD_ST_COMMITTED) cs_remove_missing(a, base, n, ts);
+            __syncthreads();
+            cs_um_notify(a, key, base, n, L, ns, ex, e, s_prune, &s_U);
         } else {
             if (!found) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; return; }
                 const uint32_t ts = cs_insert(a, base, n, p, t, ns, t);
                 if (ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             } else {
@@ -564,10 +807,12 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 __syncthreads();
                 if (cur < AD_ST_COMMITTED && ns == AD_ST_INVALID) cs_remove_missing(a, base, n, ts);
             }
+            __syncthreads();
+            cs_um_notify(a, key, base, n, L, ns, t, e, s_prune, &s_U);
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { a.cnt[key] = n; a.lp_cnt[key] = L; }
+    if (threadIdx.x == 0) { a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; }
 }
 
 }  // namespace ad

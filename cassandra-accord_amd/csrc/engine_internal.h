@@ -196,10 +196,12 @@ struct ad_handle {
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
     bool merged_compacted = false;   // !merged_exact: the exact offsets / lists below are built (merged_compact)
     bool pipeline_union = false;     // ad_set_pipeline_union: ad_run_pipeline takes the union view (a generator shortcut)
-    bool merged_cap = false;         // merged key classes in k_merge_cap's capacity layout (merged_ready compacts them)
+    bool merged_cap = false;         // merged key classes as k_merge_ref's references + merged rows (merged_ready compacts)
     bool mcap_direct = false;        //   ... the directKeyDeps class too
-    uint32_t *mcap_kcnt[2] = {}, *mcap_ment[2] = {}, *mcap_part[2] = {};
+    MergeCapArgs mcap_args[2] = {};  //   the last merge's references / merged-row region per class (merged_ready)
+    uint32_t* mcap_part[2] = {};
     unsigned mcap_blocks = 0;
+    int mcap_phase = 0;              //   which of the two counter sets this call uses
     bool mcap_entries_pending = false;   // merged_entries = the sum of mcap_part (read lazily)
     uint32_t* mx_off[3] = {};        //   per class: exact TxnId offsets [n + 1]
     uint32_t* mx_txns[3] = {};       //   and the compacted TxnId lists
@@ -249,6 +251,19 @@ struct ad_handle {
         uint64_t *pbm = nullptr, *pbl = nullptr, *lpm = nullptr, *lpl = nullptr, *lp_bits = nullptr;  // pruning
         int32_t *pbn = nullptr, *lpn = nullptr;
         uint32_t* lp_cnt = nullptr;
+        uint64_t *lp_xm = nullptr, *lp_xl = nullptr;                 // loadingPruned least witness TxnIds
+        int32_t* lp_xn = nullptr;
+        uint8_t* lp_xh = nullptr;
+        uint32_t* um_cnt = nullptr;                                  // unmanaged registry
+        uint8_t* um_p = nullptr;
+        uint64_t *um_wm = nullptr, *um_wl = nullptr, *um_tm = nullptr, *um_tl = nullptr;
+        int32_t *um_wn = nullptr, *um_tn = nullptr;
+        uint32_t *nt_base = nullptr, *nt_cnt = nullptr, *nt_ev = nullptr;   // the last apply's notifications
+        uint8_t* nt_tag = nullptr;
+        uint64_t *nt_tm = nullptr, *nt_tl = nullptr;
+        int32_t* nt_tn = nullptr;
+        size_t nt_total = 0;
+        std::vector<uint32_t> nt_base_host, ev_off_host;
     } cs;
     // the last ad_cfk_store_query (cfk_query_kernels.h): capacity-laid outputs per class + exact counts on the host
     struct CfkQueryOut {
@@ -357,6 +372,7 @@ enum Slot : size_t {
     S_MCK0, S_MCK1, S_MCE0, S_MCE1, S_MCP0, S_MCP1,                          // k_merge_cap: kcnt, ment, block parts
     S_MCL, S_MCLS0, S_MCLS1,                                                  //   pass-2 list counters, lists
     S_CSQ0, S_CSQ_END = S_CSQ0 + 34,                                           // ad_cfk_store_query
+    S_CSU0, S_CSU_END = S_CSU0 + 20,                                           // the store's unmanaged registry
     S_NUM_FIXED,
     S_CSR0 = 400
 };

@@ -160,14 +160,19 @@ int merge_parts(ad_handle* h, const Csr* const parts[3][MAXV], int np, bool has_
     return AD_OK;
 }
 
-// Deps.merge of the R replies' key classes in one k_merge_cap launch per class (merge_kernels.h): the merged
-// CSRs in capacity layout, no host round trip.  Batches whose deps stage saw no heavy txn, no range and no
-// virtual items (their classes go through merge_parts).
-constexpr unsigned MCAP_G2 = 1024;                  // pass 2's grid (grid-stride over the listed txns)
+// Deps.merge of the R replies' key classes (merge_kernels.h: k_merge_ref, one thread per txn; the txns whose replies
+// differ merged in the same pass): the merged rows as references to a reply plus a region of merged rows, one launch,
+// no host round trip.  Batches whose deps stage saw no heavy txn, no range and no virtual items (the rest go through merge_parts).
 template <int NV>
-static void launch_merge_cap(const MergeCapArgs& a, unsigned g, hipStream_t st) {
-    k_merge_cap<NV><<<g, 256, 0, st>>>(a);
-    k_merge_cap_list<NV><<<std::min(g, MCAP_G2), 256, 0, st>>>(a);
+static void launch_merge_cap(const MergeCapArgs& a, unsigned g, hipStream_t st) { k_merge_ref<NV><<<g, 256, 0, st>>>(a); }
+template <int NV>
+static void launch_merge_ready_counts(const MergeCapArgs& a, uint32_t* k, uint32_t* m, uint32_t* t, hipStream_t st) {
+    k_merge_ready_counts<NV><<<ceil_div((long)a.n, 256), 256, 0, st>>>(a, k, m, t);
+}
+template <int NV>
+static void launch_merge_ready_copy(const MergeCapArgs& a, const Csr& x, const uint32_t* k, const uint32_t* m,
+                                    const uint32_t* t, hipStream_t st) {
+    k_merge_ready_copy<NV><<<ceil_div((long)a.n, 256), 256, 0, st>>>(a, x.key_off, x.k2t_off, x.ent_off, k, m, t, x.keys, x.k2t, x.txns);
 }
 
 static int merge_cap(ad_handle* h) {
@@ -178,19 +183,21 @@ static int merge_cap(ad_handle* h) {
     CK(zero_csr(h, CSR_MERGED0 + AD_CLASS_RANGE, h->merged[AD_CLASS_RANGE], n));
     if (!direct) CK(zero_csr(h, CSR_MERGED0 + AD_CLASS_DIRECT_KEY, h->merged[AD_CLASS_DIRECT_KEY], n));
     const unsigned g = (unsigned)ceil_div((long)n, 256);
-    h->mcap_blocks = g + std::min(g, MCAP_G2);
-    uint32_t* lc = nullptr;                             // [class][2]: list count, finished pass-2 workgroups
-    if (!h->bufs.empty() && h->bufs.size() > S_MCL && h->bufs[S_MCL].p) lc = (uint32_t*)h->bufs[S_MCL].p;
-    if (!lc) {
-        CK(dalloc(h, S_MCL, &lc, 4));
-        HIPCHK(h, hipMemsetAsync(lc, 0, 16, st));          // then kept at zero by pass 2's last workgroup
-    }
+    h->mcap_blocks = g;
+    // per class two sets of 4 counters (merged txns, region keys / words / ids): this call's and the next's (zeroed by
+    // this call), alternating
+    uint32_t* ctr = nullptr;
+    const bool fresh = h->bufs.size() <= S_MCL || !h->bufs[S_MCL].p;
+    CK(dalloc(h, S_MCL, &ctr, 16));
+    if (fresh) HIPCHK(h, hipMemsetAsync(ctr, 0, 64, st));
+    const int ph = h->mcap_phase;
+    h->mcap_phase ^= 1;
+    const size_t n1 = std::max<size_t>(n, 1);
     for (int c = 0; c < (direct ? 2 : 1); ++c) {
         Csr m{};
         const size_t block = CSR_MCAP0 + c;
-        CK(alloc_csr(h, block, m, n));
-        dirty_csr(h, block);
-        MergeCapArgs a{};
+        MergeCapArgs& a = h->mcap_args[c];
+        a = MergeCapArgs{};
         a.n = n;
         for (int v = 0; v < nv; ++v) {
             const Csr& x = h->deps[2 * v + c];
@@ -198,31 +205,28 @@ static int merge_cap(ad_handle* h) {
             a.key_off[v] = x.key_off; a.keys[v] = x.keys; a.k2t_off[v] = x.k2t_off; a.k2t[v] = x.k2t;
             a.ent_off[v] = x.ent_off; a.txns[v] = x.txns; a.tcnt[v] = x.tcnt;
         }
-        CK(alloc_csr_data(h, block, m, 1));
-        CK(dalloc(h, S_MCK0 + c, &h->mcap_kcnt[c], std::max<size_t>(n, 1)));
-        CK(dalloc(h, S_MCE0 + c, &h->mcap_ment[c], std::max<size_t>(n, 1)));
+        CK(alloc_csr_data(h, block, m, 1));                  // the merged-row region: the replies' totals
+        uint32_t* lst = nullptr;
+        CK(dalloc(h, S_MCLS0 + c, &lst, 8 * n1));            // list, lidx, six per-list arrays
+        CK(dalloc(h, S_MCK0 + c, &a.src, n1));
         CK(dalloc(h, S_MCP0 + c, &h->mcap_part[c], std::max<size_t>(h->mcap_blocks, 1)));
-        CK(dalloc(h, S_MCLS0 + c, &a.list, std::max<size_t>(n, 1)));
-        a.list_count = lc + 2 * c; a.list_done = lc + 2 * c + 1;
-        a.part2 = g;
-        a.o_key_off = m.key_off; a.o_k2t_off = m.k2t_off; a.o_ent_off = m.ent_off;
-        a.o_kcnt = h->mcap_kcnt[c]; a.o_ment = h->mcap_ment[c]; a.o_tcnt = m.tcnt;
-        a.o_keys = m.keys; a.o_k2t = m.k2t; a.o_txns = m.txns; a.part = h->mcap_part[c];
+        a.list = lst; a.lidx = lst + n1;
+        a.l_koff = lst + 2 * n1; a.l_moff = lst + 3 * n1; a.l_toff = lst + 4 * n1;
+        a.l_kcnt = lst + 5 * n1; a.l_ment = lst + 6 * n1; a.l_tcnt = lst + 7 * n1;
+        a.cnt = ctr + 8 * c + 4 * ph; a.cnt_next = ctr + 8 * c + 4 * (ph ^ 1);
+        a.o_keys = m.keys; a.o_k2t = m.k2t; a.o_txns = m.txns;
+        a.part = h->mcap_part[c]; a.part2 = g;
         if (n) {
             KScope ks(K_MERGE_CAP, n);
             NV_DISPATCH(nv, launch_merge_cap, a, g, st);
-        } else {
-            HIPCHK(h, hipMemsetAsync(m.key_off, 0, 4, st));
-            HIPCHK(h, hipMemsetAsync(m.k2t_off, 0, 4, st));
-            HIPCHK(h, hipMemsetAsync(m.ent_off, 0, 4, st));
         }
-        h->merged[c] = m;                                    // capacity sizes until merged_ready
+        h->merged[c] = m;                                    // the region's sizes (ncap > 0 iff any reply has deps)
     }
     h->mcap_direct = direct;
     h->merged_cap = true;
     h->merged_exact = true;
     h->merged_compacted = false;
-    h->mcap_entries_pending = true;
+    h->mcap_entries_pending = n > 0;
     h->merged_entries = 0;
     h->have_merged = true;
     return AD_OK;
@@ -249,19 +253,25 @@ int merged_ready(ad_handle* h) {
     if (!h->merged_cap) return AD_OK;
     CK(merged_entries_resolve(h));
     const size_t n = h->n;
+    const int nv = (int)h->cfg.replicas;
     hipStream_t st = h->st;
     CK(ensure_scratch(h, device_scan_scratch<MultiOffsetsOp<1>>(std::max<size_t>(n, 1))));
+    uint32_t* cnts = nullptr;
+    CK(dalloc(h, S_MCE0, &cnts, 3 * std::max<size_t>(n, 1)));
     for (int c = 0; c < (h->mcap_direct ? 2 : 1); ++c) {
-        const Csr cap = h->merged[c];
+        const MergeCapArgs& a = h->mcap_args[c];
         Csr x{};
         const size_t block = CSR_MERGED0 + c;
         CK(alloc_csr(h, block, x, n));
         dirty_csr(h, block);
+        uint32_t *kc = cnts, *me = cnts + std::max<size_t>(n, 1), *tc = cnts + 2 * std::max<size_t>(n, 1);
         if (n) {
+            NV_DISPATCH(nv, launch_merge_ready_counts, a, kc, me, tc, st);
             MultiOffsetsOp<1> op{};
-            op.n = n; op.mk = h->mcap_kcnt[c]; op.me = h->mcap_ment[c]; op.mu = cap.tcnt;
+            op.n = n; op.mk = kc; op.me = me; op.mu = tc;
             op.key_off[0] = x.key_off; op.ent_off[0] = x.ent_off; op.k2t_off[0] = x.k2t_off;
             scan_any(h, op, n);
+            HIPCHK(h, hipMemcpyAsync(x.tcnt, tc, n * 4, hipMemcpyDeviceToDevice, st));
         } else {
             HIPCHK(h, hipMemsetAsync(x.key_off, 0, 4, st));
             HIPCHK(h, hipMemsetAsync(x.k2t_off, 0, 4, st));
@@ -274,10 +284,7 @@ int merged_ready(ad_handle* h) {
         HIPCHK(h, hipStreamSynchronize(st));
         x.nkeys = tot[0]; x.nk2t = tot[1]; x.ncap = tot[2];
         CK(alloc_csr_data(h, block, x, 1));
-        if (n)
-            k_merge_compact<<<ceil_div((long)n, 256), 256, 0, st>>>(n, cap.key_off, cap.k2t_off, cap.ent_off, h->mcap_kcnt[c],
-                                                                    h->mcap_ment[c], cap.tcnt, cap.keys, cap.k2t, cap.txns,
-                                                                    x.key_off, x.k2t_off, x.ent_off, x.keys, x.k2t, x.txns, x.tcnt);
+        if (n) NV_DISPATCH(nv, launch_merge_ready_copy, a, x, kc, me, tc, st);
         HIPCHK(h, hipGetLastError());
         h->merged[c] = x;
     }

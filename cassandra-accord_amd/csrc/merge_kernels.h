@@ -527,28 +527,29 @@ inline void merge_launch_nv(const MergeArgs& a, bool write, int kw, hipStream_t 
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Deps.merge of the R replies in ONE pass (k_merge_cap; key classes of batches without heavy txns).
+// Deps.merge of the R replies in one pass without a count pass, offsets scan or host round trip (k_merge_ref; key
+// classes of batches whose deps stage saw no heavy txn).
 //
-// The count pass, the offsets scan and the host's read of the merged totals that k_merge needs before its write
-// pass are all avoidable: a union is never larger than the sum of its parts, so each output txn gets a CAPACITY
-// region whose offsets are the element-wise sum of the replies' own offset arrays (prefix sums add up), and the
-// merged keys / keysToTxnIds block / TxnIds are written into it with their exact counts beside it (kcnt, ment,
-// tcnt).  merged_ready() compacts that into the exact CSR when something needs it (fetch, levels over merged
-// deps, recovery, inverse); nothing on a key batch's pipeline does.
-//
-// Per txn one thread.  Small replies (the C2 / C3 case: <= 8 TxnIds, <= 4 keys, <= 12 keysToTxnIds words per
-// view) are merged in registers with every load issued up front (offsets, then all list words at once: two
-// dependent memory round trips instead of one per merge step):
+// LinearMerger / linearUnion return an input unchanged when it already is the union (RelationMultiMap.java:583-589:
+// "one side is a superset").  Replies differ only where a replica dropped an in-flight dependency, so for nearly every
+// txn (C2: all but ~12 of 1M) the replies that have deps are identical: k_merge_ref, one thread per txn, compares them
+// word for word and records the txn's merged row as a REFERENCE to that reply's row (src[t] = its view; MC_EMPTY when
+// no reply has deps).  Every other txn is merged by its own thread right after (such txns are rare: a wave that holds one
+// runs the merge, the others do not) — in registers for small replies (<= 8 TxnIds, <= 4 keys, <= 12 keysToTxnIds words
+// per view):
 //   - TxnId union: an id is OWNED by the first view that lists it; its merged position is the number of owned
 //     ids below it (compares only, no data-dependent register indexing);
 //   - keys: the same ownership / rank on the keys;
 //   - per merged key the set of merged TxnId positions is a bitmask: each view's per-key index list (the
 //     keysToTxnIds entries between two header ends) becomes a mask over its own ids, remapped through the ranks
 //     (remapToSuperset, SortedArrays.java:1249-1275) and OR-ed into the merged key's mask (the per-key
-//     linearUnion, RelationMultiMap.java:562-816); set bits in ascending order are the sorted index list.
-// Larger replies take the serial R-way merge-path loops of k_merge (key union counted first: the header precedes
-// the entries).  Merged entries per workgroup go to part[] (the host sums them lazily).
+//     linearUnion, RelationMultiMap.java:562-816); set bits in ascending order are the sorted index list;
+// else with k_merge's serial R-way merge-path loops — into a region whose space each wave claims with one atomic per
+// counter, the txn's place recorded in the list arrays (lidx[t] -> l_*).  merged_ready() turns references + merged rows into the exact CSR when something reads it (fetch, levels over
+// merged deps, recovery, inverse); a key batch's pipeline reads nothing of it.  Merged entries per workgroup go to
+// part[] (the host sums them lazily).
 // ---------------------------------------------------------------------------------------------------
+constexpr uint8_t MC_EMPTY = 0xFE, MC_LIST = 0xFF;
 struct MergeCapArgs {
     size_t n;
     const uint32_t* key_off[MAXV];
@@ -558,16 +559,18 @@ struct MergeCapArgs {
     const uint32_t* ent_off[MAXV];
     const uint32_t* txns[MAXV];
     const uint32_t* tcnt[MAXV];
-    uint32_t *o_key_off, *o_k2t_off, *o_ent_off;    // [n + 1] capacity offsets (sums of the replies')
-    uint32_t *o_kcnt, *o_ment, *o_tcnt;             // [n] merged keys / keysToTxnIds entries / TxnIds
-    uint64_t* o_keys;
+    uint8_t* src;                                   // [n] the reply the merged row equals, MC_EMPTY or MC_LIST
+    uint32_t* lidx;                                 // [n] a merged txn's index in the list arrays
+    uint32_t* list;                                 // (unused)
+    uint32_t* cnt;                                  // this call's counters: [0] merged txns, [1..3] region keys / words / ids
+    uint32_t* cnt_next;                             // the next call's (this call zeroes them)
+    uint32_t *l_koff, *l_moff, *l_toff;             // [list] a merged row's place in the region
+    uint32_t *l_kcnt, *l_ment, *l_tcnt;             // [list] its keys / keysToTxnIds entries / TxnIds
+    uint64_t* o_keys;                               // the region (capacity: the replies' totals summed)
     int32_t* o_k2t;
     uint32_t* o_txns;
-    uint32_t* part;                                 // merged entries per workgroup: pass 1's, then pass 2's at part2
+    uint32_t* part;                                 // [gridDim.x] merged entries per workgroup
     uint32_t part2;
-    uint32_t* list;                                 // [n] txns pass 1 leaves to pass 2
-    uint32_t* list_count;                           // zero before pass 1; pass 2's last workgroup clears it
-    uint32_t* list_done;                            // pass 2's finished workgroups (cleared with it)
 };
 constexpr int MC_T = 8, MC_K = 4, MC_S = 12;
 
@@ -789,12 +792,9 @@ __device__ inline void merge_cap_block_sum(uint32_t v, uint32_t* out) {
     }
 }
 
-// Pass 1, one thread per txn: the capacity offsets, and every txn whose replies need no merging — none has deps, or
-// the replies that have any are identical (they differ only where a view dropped an in-flight dependency: C2's
-// usual case) — settled by a copy.  The others go to a list (wave-aggregated append) for pass 2, where they are dense
-// (a full register merge in pass 1 ran every wave through it: nearly every wave holds one such txn).
+// (at most 128 VGPRs — 4 waves per SIMD for the compare pass; the rare inline merge may spill)
 template <int NV>
-static __global__ __launch_bounds__(256) void k_merge_cap(MergeCapArgs a) {
+static __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_ref(MergeCapArgs a) {
     constexpr uint32_t INF = 0xFFFFFFFFu;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t ent = 0;
@@ -807,53 +807,43 @@ static __global__ __launch_bounds__(256) void k_merge_cap(MergeCapArgs a) {
             mb[v] = a.k2t_off[v][t]; ms[v] = a.k2t_off[v][t + 1] - mb[v];
             tb[v] = a.ent_off[v][t]; tc[v] = a.tcnt[v][t];
         }
-        uint32_t okb = 0, omb = 0, otb = 0, any = 0;
+        uint32_t any = 0;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) { okb += kb[v]; omb += mb[v]; otb += tb[v]; any |= tc[v]; }
-        a.o_key_off[t] = okb; a.o_k2t_off[t] = omb; a.o_ent_off[t] = otb;
-        if (t + 1 == a.n) {
-            uint32_t ek = 0, em = 0, et = 0;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) { ek += kb[v] + nk[v]; em += mb[v] + ms[v]; et += a.ent_off[v][a.n]; }
-            a.o_key_off[a.n] = ek; a.o_k2t_off[a.n] = em; a.o_ent_off[a.n] = et;
-        }
-        uint32_t okc = 0, oent = 0, otc = 0;
+        for (int v = 0; v < NV; ++v) any |= tc[v];
+        uint8_t src = MC_EMPTY;
         if (any) {
-            // the first reply with deps (f) and whether every reply with deps has its shape and fits the registers
+            // the first reply with deps (f); every other reply with deps must have its shape (and fit the registers)
             uint32_t fkb = 0, fnk = 0, fmb = 0, fms = 0, ftb = 0, ftc = 0;
-            bool got = false;
+            int fi = NV;
 #pragma unroll
-            for (int v = 0; v < NV; ++v)
-                if (!got && tc[v]) { fkb = kb[v]; fnk = nk[v]; fmb = mb[v]; fms = ms[v]; ftb = tb[v]; ftc = tc[v]; got = true; }
+            for (int v = NV - 1; v >= 0; --v)
+                if (tc[v]) { fkb = kb[v]; fnk = nk[v]; fmb = mb[v]; fms = ms[v]; ftb = tb[v]; ftc = tc[v]; fi = v; }
             bool same = ftc <= (uint32_t)MC_T && fnk <= (uint32_t)MC_K && fms <= (uint32_t)MC_S;
 #pragma unroll
             for (int v = 0; v < NV; ++v) same = same && (tc[v] == 0 || (tc[v] == ftc && nk[v] == fnk && ms[v] == fms));
             if (same) {
+                const uint32_t* ft = a.txns[0];
+                const uint64_t* fk = a.keys[0];
+                const int32_t* fm = a.k2t[0];
+#pragma unroll
+                for (int v = 1; v < NV; ++v) if (fi == v) { ft = a.txns[v]; fk = a.keys[v]; fm = a.k2t[v]; }
+                // every load unconditional, at an index clamped into the list (f has deps: ftc, fnk >= 1, fms >= 2); the
+                // differences OR-ed under masks — arithmetic, not short-circuit tests: a branch around a compare sinks its
+                // load into it, one memory latency per slot
                 uint32_t T[MC_T];
                 uint64_t K[MC_K];
-                int32_t S[MC_S];
-                // f's lists, then every other reply with deps compared word for word (all loads issued together)
-                const uint32_t* ft = nullptr;
-                const uint64_t* fk = nullptr;
-                const int32_t* fm = nullptr;
-                bool gf = false;
+                uint32_t S[MC_S];
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
-                    if (!gf && tc[v]) { ft = a.txns[v]; fk = a.keys[v]; fm = a.k2t[v]; gf = true; }
-                // unconditional loads at clamped indices (see merge_cap_small): f has deps, so ftc, fnk >= 1, fms >= 2
+                for (int s = 0; s < MC_T; ++s) T[s] = ft[ftb + min((uint32_t)s, ftc - 1)];
 #pragma unroll
-                for (int s = 0; s < MC_T; ++s) { const uint32_t x = ft[ftb + min((uint32_t)s, ftc - 1)]; T[s] = (uint32_t)s < ftc ? x : INF; }
+                for (int i = 0; i < MC_K; ++i) K[i] = fk[fkb + min((uint32_t)i, fnk - 1)];
 #pragma unroll
-                for (int i = 0; i < MC_K; ++i) { const uint64_t x = fk[fkb + min((uint32_t)i, fnk - 1)]; K[i] = (uint32_t)i < fnk ? x : 0ull; }
-#pragma unroll
-                for (int s = 0; s < MC_S; ++s) { const int32_t x = fm[fmb + min((uint32_t)s, fms - 1)]; S[s] = (uint32_t)s < fms ? x : 0; }
-                // every other reply with deps, word for word: the differences OR-ed under masks (arithmetic, not a
-                // short-circuit test: a branch around each compare would sink each load into it)
+                for (int s = 0; s < MC_S; ++s) S[s] = (uint32_t)fm[fmb + min((uint32_t)s, fms - 1)];
                 uint32_t diff = 0;
                 uint64_t diffk = 0;
 #pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const bool h = tc[v] != 0;
+                for (int v = 1; v < NV; ++v) {                   // views after f (those before it have no deps)
+                    const bool h = tc[v] != 0 && v > fi;
                     const uint32_t hm = h ? ~0u : 0u;
 #pragma unroll
                     for (int s = 0; s < MC_T; ++s) {
@@ -868,82 +858,113 @@ static __global__ __launch_bounds__(256) void k_merge_cap(MergeCapArgs a) {
 #pragma unroll
                     for (int s = 0; s < MC_S; ++s) {
                         const uint32_t x = (uint32_t)a.k2t[v][h ? mb[v] + min((uint32_t)s, fms - 1) : 0u];
-                        diff |= (x ^ (uint32_t)S[s]) & ((uint32_t)s < fms ? hm : 0u);
+                        diff |= (x ^ S[s]) & ((uint32_t)s < fms ? hm : 0u);
                     }
                 }
                 same = diff == 0 && diffk == 0;
-                if (same) {
-#pragma unroll
-                    for (int s = 0; s < MC_T; ++s) if ((uint32_t)s < ftc) a.o_txns[otb + s] = T[s];
-#pragma unroll
-                    for (int i = 0; i < MC_K; ++i) if ((uint32_t)i < fnk) a.o_keys[okb + i] = K[i];
-#pragma unroll
-                    for (int s = 0; s < MC_S; ++s) if ((uint32_t)s < fms) a.o_k2t[omb + s] = S[s];
-                    okc = fnk; oent = fms - fnk; otc = ftc;
-                }
+                (void)INF;
             }
-            defer = !same;
+            if (same) { src = (uint8_t)fi; ent = fms - fnk; }
+            else { src = MC_LIST; defer = true; }
         }
-        if (!defer) { a.o_kcnt[t] = okc; a.o_ment[t] = oent; a.o_tcnt[t] = otc; }
-        ent = oent;
+        a.src[t] = src;
     }
-    wave_append(defer, (uint32_t)t, a.list, a.list_count);
+    // txns whose replies differ (C2: ~12 of 1M) are merged right here: a listed txn's wave claims the region space of
+    // its listed lanes (the replies' sizes summed) with one atomic per counter, then each such lane merges its txn
+    if (__ballot(defer)) {
+        const size_t tt = defer ? t : 0;
+        uint32_t kb[NV], nk[NV], mb[NV], ms[NV], tb[NV], tc[NV];
+        bool small = NV <= 4;
+        uint32_t ck = 0, cm = 0, ct = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            kb[v] = a.key_off[v][tt]; nk[v] = a.key_off[v][tt + 1] - kb[v];
+            mb[v] = a.k2t_off[v][tt]; ms[v] = a.k2t_off[v][tt + 1] - mb[v];
+            tb[v] = a.ent_off[v][tt]; tc[v] = a.tcnt[v][tt];
+            if (!defer) { nk[v] = ms[v] = tc[v] = 0; }
+            ck += nk[v]; cm += ms[v]; ct += tc[v];
+            small = small && tc[v] <= (uint32_t)MC_T && nk[v] <= (uint32_t)MC_K && ms[v] <= (uint32_t)MC_S;
+        }
+        uint32_t sk = ck, sm = cm, st = ct;
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+            const uint32_t yk = __shfl_up(sk, d), ym = __shfl_up(sm, d), yt = __shfl_up(st, d);
+            if ((int)__lane_id() >= d) { sk += yk; sm += ym; st += yt; }
+        }
+        const uint64_t lm = __ballot(defer);
+        uint32_t bk = 0, bm = 0, bt = 0, bl = 0;
+        if (__lane_id() == WAVE - 1) {
+            bk = atomicAdd(a.cnt + 1, sk); bm = atomicAdd(a.cnt + 2, sm); bt = atomicAdd(a.cnt + 3, st);
+            bl = atomicAdd(a.cnt, (uint32_t)__popcll(lm));
+        }
+        bk = __shfl(bk, WAVE - 1); bm = __shfl(bm, WAVE - 1); bt = __shfl(bt, WAVE - 1); bl = __shfl(bl, WAVE - 1);
+        if (defer) {
+            const uint32_t x = bl + (uint32_t)__popcll(lm & ((1ull << __lane_id()) - 1ull));
+            const uint32_t okb = bk + sk - ck, omb = bm + sm - cm, otb = bt + st - ct;
+            uint32_t okc = 0, oent = 0, otc = 0;
+            bool done = false;
+            if constexpr (NV <= 4) {
+                if (small) done = merge_cap_small<NV>(a, kb, nk, mb, ms, tb, tc, okb, omb, otb, okc, oent, otc);
+            }
+            if (!done) merge_cap_serial<NV>(a, kb, nk, mb, tb, tc, okb, omb, otb, okc, oent, otc);
+            a.l_koff[x] = okb; a.l_moff[x] = omb; a.l_toff[x] = otb;
+            a.l_kcnt[x] = okc; a.l_ment[x] = oent; a.l_tcnt[x] = otc;
+            a.lidx[t] = x;
+            ent = oent;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 4) a.cnt_next[threadIdx.x] = 0u;    // the next call's counters
     merge_cap_block_sum(ent, a.part + blockIdx.x);
 }
 
-// Pass 2: the listed txns, dense — the register merge for small replies (NV <= 4), else the serial loops.  The last
-// workgroup to finish clears the list count for the next merge.
+// merged_ready: per txn the merged row's counts (from the reply it references, or its merged row), then (after an
+// exclusive scan, MultiOffsetsOp) the copy into the exact CSR — outside the pipeline.
 template <int NV>
-static __global__ __launch_bounds__(256) void k_merge_cap_list(MergeCapArgs a) {
-    const uint32_t L = *(const volatile uint32_t*)a.list_count;
-    uint32_t ent = 0;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < L; x += gridDim.x * blockDim.x) {
-        const size_t t = a.list[x];
-        uint32_t kb[NV], nk[NV], mb[NV], ms[NV], tb[NV], tc[NV];
-        bool small = NV <= 4;
-        uint32_t okb = 0, omb = 0, otb = 0;
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            kb[v] = a.key_off[v][t]; nk[v] = a.key_off[v][t + 1] - kb[v];
-            mb[v] = a.k2t_off[v][t]; ms[v] = a.k2t_off[v][t + 1] - mb[v];
-            tb[v] = a.ent_off[v][t]; tc[v] = a.tcnt[v][t];
-            okb += kb[v]; omb += mb[v]; otb += tb[v];
-            small = small && tc[v] <= (uint32_t)MC_T && nk[v] <= (uint32_t)MC_K && ms[v] <= (uint32_t)MC_S;
-        }
-        uint32_t okc = 0, oent = 0, otc = 0;
-        bool done = false;
-        if constexpr (NV <= 4) {
-            if (small) done = merge_cap_small<NV>(a, kb, nk, mb, ms, tb, tc, okb, omb, otb, okc, oent, otc);
-        }
-        if (!done) merge_cap_serial<NV>(a, kb, nk, mb, tb, tc, okb, omb, otb, okc, oent, otc);
-        a.o_kcnt[t] = okc; a.o_ment[t] = oent; a.o_tcnt[t] = otc;
-        ent += oent;
-    }
-    merge_cap_block_sum(ent, a.part + a.part2 + blockIdx.x);
-    __shared__ uint32_t s_last;
-    __threadfence();
-    if (threadIdx.x == 0) s_last = atomicAdd(a.list_done, 1u) == gridDim.x - 1 ? 1u : 0u;
-    __syncthreads();
-    if (threadIdx.x == 0 && s_last) { *(volatile uint32_t*)a.list_count = 0u; *(volatile uint32_t*)a.list_done = 0u; }
-}
-
-// The exact CSR of a capacity-laid merge (merged_ready): exact offsets come from MultiOffsetsOp over (kcnt, ment,
-// tcnt); then each txn's keys, keysToTxnIds block and TxnIds move down (one thread per txn: outside the pipeline).
-static __global__ __launch_bounds__(256) void k_merge_compact(size_t n, const uint32_t* __restrict__ ckoff, const uint32_t* __restrict__ cmoff,
-                                                              const uint32_t* __restrict__ ctoff, const uint32_t* __restrict__ kcnt,
-                                                              const uint32_t* __restrict__ ment, const uint32_t* __restrict__ tcnt,
-                                                              const uint64_t* __restrict__ ckeys, const int32_t* __restrict__ ck2t,
-                                                              const uint32_t* __restrict__ ctxns, const uint32_t* __restrict__ xkoff,
-                                                              const uint32_t* __restrict__ xmoff, const uint32_t* __restrict__ xtoff,
-                                                              uint64_t* __restrict__ xkeys, int32_t* __restrict__ xk2t,
-                                                              uint32_t* __restrict__ xtxns, uint32_t* __restrict__ xtcnt) {
+static __global__ __launch_bounds__(256) void k_merge_ready_counts(MergeCapArgs a, uint32_t* kcnt, uint32_t* ment, uint32_t* tcnt) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+    if (t >= a.n) return;
+    const uint8_t s = a.src[t];
+    uint32_t k = 0, m = 0, c = 0;
+    if (s == MC_LIST) {
+        const uint32_t x = a.lidx[t];
+        k = a.l_kcnt[x]; m = a.l_ment[x]; c = a.l_tcnt[x];
+    } else if (s != MC_EMPTY) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (v == s) {
+                k = a.key_off[v][t + 1] - a.key_off[v][t];
+                m = a.k2t_off[v][t + 1] - a.k2t_off[v][t] - k;
+                c = a.tcnt[v][t];
+            }
+    }
+    kcnt[t] = k; ment[t] = m; tcnt[t] = c;
+}
+template <int NV>
+static __global__ __launch_bounds__(256) void k_merge_ready_copy(MergeCapArgs a, const uint32_t* __restrict__ xkoff,
+                                                                  const uint32_t* __restrict__ xmoff, const uint32_t* __restrict__ xtoff,
+                                                                  const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ ment,
+                                                                  const uint32_t* __restrict__ tcnt, uint64_t* __restrict__ xkeys,
+                                                                  int32_t* __restrict__ xk2t, uint32_t* __restrict__ xtxns) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint8_t s = a.src[t];
+    if (s == MC_EMPTY) return;
+    const uint64_t* keys = a.o_keys;
+    const int32_t* k2t = a.o_k2t;
+    const uint32_t* txns = a.o_txns;
+    uint32_t kb = 0, mb = 0, tb = 0;
+    if (s == MC_LIST) {
+        const uint32_t x = a.lidx[t];
+        kb = a.l_koff[x]; mb = a.l_moff[x]; tb = a.l_toff[x];
+    } else {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (v == s) { keys = a.keys[v]; k2t = a.k2t[v]; txns = a.txns[v]; kb = a.key_off[v][t]; mb = a.k2t_off[v][t]; tb = a.ent_off[v][t]; }
+    }
     const uint32_t nk = kcnt[t], nm = nk + ment[t], nt = tcnt[t];
-    for (uint32_t i = 0; i < nk; ++i) xkeys[xkoff[t] + i] = ckeys[ckoff[t] + i];
-    for (uint32_t i = 0; i < nm; ++i) xk2t[xmoff[t] + i] = ck2t[cmoff[t] + i];
-    for (uint32_t i = 0; i < nt; ++i) xtxns[xtoff[t] + i] = ctxns[ctoff[t] + i];
-    xtcnt[t] = nt;
+    for (uint32_t i = 0; i < nk; ++i) xkeys[xkoff[t] + i] = keys[kb + i];
+    for (uint32_t i = 0; i < nm; ++i) xk2t[xmoff[t] + i] = k2t[mb + i];
+    for (uint32_t i = 0; i < nt; ++i) xtxns[xtoff[t] + i] = txns[tb + i];
 }
 
 inline void merge_launch(const MergeArgs& a, int nv, bool write, int kw, hipStream_t st) {

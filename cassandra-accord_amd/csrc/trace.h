@@ -24,7 +24,7 @@ inline const char* kernel_name(int k) {
         "k_deps_walk<count>", "k_txn_counts", "scan_offsets", "k_txn_finish", "k_deps_walk<fill>", "k_txn_union",
         "k_merge<count>", "k_merge<write>", "chain_prep", "scan_chain", "order_sort", "k_range_deps", "vitems",
         "k_union_lds", "level_edges", "kahn_levels", "k_merge_heavy<count>", "k_merge_heavy<write>",
-        "max_conflicts", "merge_offsets", "csr_offsets", "block_levels", "recover", "k_seg_fuse", "seg_keys", "k_merge_cap"};
+        "max_conflicts", "merge_offsets", "csr_offsets", "block_levels", "recover", "k_seg_fuse", "seg_keys", "k_merge_ref"};
     return (k >= 0 && k < K_COUNT) ? names[k] : "?";
 }
 

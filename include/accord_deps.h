@@ -501,12 +501,24 @@ int  ad_cfk_notify(ad_handle* h, const ad_cfk_state* s, uint8_t* not_waiting /* 
  *   AD_CFK_OP_PRUNE    CommandsForKey.maybePrune(pruneInterval = exec_node, minHlcDelta = exec_msb) (Pruning.java:164-331)
  *   AD_CFK_OP_LOADING  txn joins loadingPruned witnessed by its one dep, if any (an unmanaged's pruned deps,
  *                      Updating.java:806-815)
+ *   AD_CFK_OP_UNMANAGED         registerUnmanaged (Updating.updateUnmanaged :715-849, register = true) of unmanaged txn
+ *                               txn (a range txn, sync point or ephemeral read; exec = its executeAt) whose Read / Write
+ *                               deps at this key are the event's deps: readyToApply -> notified (tag 2), else joins the
+ *                               key's unmanaged registry as (APPLY, executesAt) or (COMMIT, its last dep).  The TRANSITIVELY_
+ *                               KNOWN rows / LOADING entries of deps the key does not know are the events before it.
+ *   AD_CFK_OP_UNMANAGED_RECHECK updateUnmanaged(register = false): an unmanaged notified of commit, re-checked
+ * Every UPDATE / LOAD that changes a row then runs PostProcess.notifyUnmanaged (:164-246) over the registry: entries waiting
+ * for commits below minUndecided (and the first loadingPruned TxnId) are notified (tag 0) and leave it, and after an apply
+ * those whose waitingUntil the contiguous applied prefix reached (tag 1).  ad_cfk_store_notified returns the last apply's
+ * notifications, ad_cfk_store_unmanaged a key's registry.
  * ad_cfk_store_notify holds a STABLE txn whose loadingPruned witness entry precedes its executeAt (isWaitingOnPruned,
  * Pruning.java:119-135); ad_cfk_store_pruning reads prunedBefore and the table back.                                 */
 #define AD_CFK_OP_UPDATE  0
 #define AD_CFK_OP_LOAD    1
 #define AD_CFK_OP_PRUNE   2
 #define AD_CFK_OP_LOADING 3
+#define AD_CFK_OP_UNMANAGED 4
+#define AD_CFK_OP_UNMANAGED_RECHECK 5
 typedef struct ad_cfk_events {
     size_t m;                       /* events                                                          */
     const uint32_t* ev_off;         /* [keys + 1] events of key k: [ev_off[k], ev_off[k + 1])          */
@@ -536,6 +548,15 @@ int  ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missin
 int  ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint64_t* pruned_lsb, int32_t* pruned_node,
                           size_t* loading, size_t* witness_total, uint64_t* lp_msb, uint64_t* lp_lsb, int32_t* lp_node,
                           uint32_t* lp_off, uint32_t* lp_rows);
+/* one key's unmanaged registry in Unmanaged.compareTo order: *count entries of (pending: 0 COMMIT / 1 APPLY, waitingUntil,
+ * TxnId); arrays may be NULL (two calls) */
+int  ad_cfk_store_unmanaged(ad_handle* h, uint32_t key, size_t* count, uint8_t* pending, uint64_t* wait_msb,
+                            uint64_t* wait_lsb, int32_t* wait_node, uint64_t* txn_msb, uint64_t* txn_lsb, int32_t* txn_node);
+/* the last ad_cfk_store_apply's unmanaged notifications, per key in order (counts[keys]), keys concatenated: event = the
+ * index among that key's events of the call, tag 0 commit (NotifyUnmanagedOfCommit), 1 applied (NotifyNotWaiting),
+ * 2 ready at its (re)registration; arrays may be NULL (two calls) */
+int  ad_cfk_store_notified(ad_handle* h, uint32_t* counts, size_t* total, uint32_t* event, uint8_t* tag, uint64_t* txn_msb,
+                           uint64_t* txn_lsb, int32_t* txn_node);
 /* CommandsForKey.mapReduceActive over the resident rows (local/cfk/CommandsForKey.java:925-983), as
  * PreAccept.calculatePartialDeps (messages/PreAccept.java:245-267) asks it, for a batch of queries: query q's txn on its
  * store keys with bound startedBefore (PreAccept / ExclusiveSyncPoint: its TxnId; Accept / GetDeps: its executeAt, the txn

@@ -535,7 +535,7 @@ class Info:
 
 COMMIT_P, APPLY_P = 0, 1                              # Unmanaged.Pending
 # ops of the device event log (CFK.log entries (txnId, InternalStatus, executeAt, deps[, op[, interval, hlcDelta]]))
-OP_UPDATE, OP_LOAD, OP_PRUNE, OP_LOADING = 0, 1, 2, 3
+OP_UPDATE, OP_LOAD, OP_PRUNE, OP_LOADING, OP_UNMANAGED, OP_UNMANAGED_RECHECK = 0, 1, 2, 3, 4, 5
 
 
 class CFK:
@@ -548,6 +548,8 @@ class CFK:
         self.info = {}
         self.unmanageds = []                          # sorted (pending, waitingUntil, txnId)
         self.log = None                               # list: the CommandsForKey.update calls as device events
+        self.notes = None                             # with log: the unmanaged notifications, (tag, TxnId) in order —
+                                                      # 0 notifyUnmanaged commit, 1 notifyUnmanaged applied, 2 ready
         self.pruned_before = NONE                     # prunedBefore's TxnId (NO_INFO: TxnId.NONE)
         self.loading = {}                             # loadingPruned: TxnId -> witnessedBy (sorted tuple)
         self.last_load = ()                           # the TxnIds the last update / updateUnmanaged asked to load
@@ -795,6 +797,8 @@ class CFK:
         if end > 0:
             commit_notify = [u[2] for u in self.unmanageds[:end]]
             self.unmanageds = self.unmanageds[end:]
+            if self.notes is not None:
+                self.notes.extend((0, u) for u in commit_notify)
         if new_info.status >= APPLIED:
             committed = self.committed()
             k = self.max_applied_write(committed) + 1
@@ -813,6 +817,8 @@ class CFK:
                 if start != e:
                     apply_notify = [u[2] for u in self.unmanageds[start:e]]
                     self.unmanageds = self.unmanageds[:start] + self.unmanageds[e:]
+                    if self.notes is not None:
+                        self.notes.extend((1, u) for u in apply_notify)
         assert not (new_info.status == INVALID and cur_status is not None and cur_status in (COMMITTED, STABLE, APPLIED))
         return commit_notify, apply_notify
 
@@ -935,6 +941,8 @@ class CFK:
                         self.log.append((a, TK, a, ()))
                 for a in missing:
                     self._add_missing_everywhere(a)
+                if self.log is not None:              # the registration itself (the device evaluates it after the above)
+                    self.log.append((wt, 0, wex, tuple(tx), OP_UNMANAGED if register else OP_UNMANAGED_RECHECK))
                 rec = (APPLY_P, executes_at, wt) if waiting_to_apply else (COMMIT_P, tx[-1], wt)
                 if add_list is not None:
                     add_list.append(rec)
@@ -943,6 +951,9 @@ class CFK:
                 if k == len(self.unmanageds) or self.unmanageds[k] != rec:
                     self.unmanageds.insert(k, rec)
                 return
+        if self.log is not None:
+            self.log.append((wt, 0, wex, tuple(tx), OP_UNMANAGED if register else OP_UNMANAGED_RECHECK))
+            self.notes.append((2, wt))
         sink(wt)
 
 
@@ -1027,6 +1038,7 @@ class Run:
         self.canon_views = {}                         # snapshot event -> canon_view(canon) (release invariants)
         self.lag_events = 0
         self.event_log = [] if log else None          # per harness event: the CFK update calls it made (CFK.log)
+        self.note_log = [] if log else None           # per harness event: its unmanaged notifications (CFK.notes)
         rnd = Rnd(seed)
         self.run_task_chance = max(0.01, float(rnd.next_float()))
         import numpy as np
@@ -1039,6 +1051,7 @@ class Run:
         cfk = CFK(self.domains)
         if log:
             cfk.log = []
+            cfk.notes = []
         self.canon, self.cfk = canon, cfk
         self.snapshots = []                           # (event, rows, notified-and-STABLE set, full-scan release set)
         self.events = 0
@@ -1097,6 +1110,8 @@ class Run:
             if log:
                 self.event_log.append(list(cfk.log))
                 cfk.log.clear()
+                self.note_log.append(list(cfk.notes))
+                cfk.notes.clear()
             fresh = [t for t, _ in canon.notified[before:] if canon.manages_execution(t)]
             self.notified.update(fresh)
             if count_gating and gating_cases(cfk):

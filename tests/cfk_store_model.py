@@ -92,6 +92,8 @@ class StoreModel:
         if op == K.OP_PRUNE:
             self.maybe_prune(ev[5], ev[6])
             return
+        if op in (K.OP_UNMANAGED, K.OP_UNMANAGED_RECHECK):   # the registry is not modelled here (no row changes)
+            return
         if op == K.OP_LOADING:
             w = 0
             for d in deps:

@@ -317,3 +317,63 @@ def test_gpu_store_queries_follow_map_reduce_active(engine_factory, chunk):
             fut += any(future_dep_fires(states[k], b) for k in ks)
     assert nq > 1000 and multi > 50 and entries > 1000
     assert fut > 20                                       # the prunedBefore branch was taken
+
+
+# ---- unmanaged txns on the device (AD_CFK_OP_UNMANAGED*, notifyUnmanaged) -------------------------------------------------
+def _pack_step(runs, e):
+    per_key = [r.event_log[e - 1] if e <= len(r.event_log) else [] for r in runs]
+    ev = [M.pack_events([evs], r.domains) for evs, r in zip(per_key, runs)]
+    merged = {f: np.concatenate([x[f] for x in ev]) if f not in ("ev_off", "deps_off") else None for f in ev[0]}
+    off, doff = [0], [0]
+    for x in ev:
+        off.append(off[-1] + len(x["status"]))
+        doff.extend((x["deps_off"][1:] + doff[-1]).tolist())
+    merged["ev_off"] = np.array(off, np.uint32)
+    merged["deps_off"] = np.array(doff, np.uint32)
+    return merged
+
+
+def test_harness_logs_unmanaged_registrations():
+    """CPU: the harness's event log carries every registerUnmanaged / updateUnmanaged call (AD_CFK_OP_UNMANAGED*), and its
+    notifications (commit, applied, ready) occur, with and without pruning."""
+    for prune in (False, True):
+        reg = notes = 0
+        tags = set()
+        for seed in (1, 4, 7):
+            r = K.Run(seed, 1000, log=True, prune=prune)
+            reg += sum(1 for evs in r.event_log for ev in evs if len(ev) > 4 and ev[4] in (K.OP_UNMANAGED, K.OP_UNMANAGED_RECHECK))
+            notes += sum(len(x) for x in r.note_log)
+            tags |= {t for x in r.note_log for t, _ in x}
+        assert reg > 100 and notes > 100 and tags == {0, 1, 2}, (prune, reg, notes, tags)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prune", [False, True])
+def test_gpu_store_unmanaged_follow_the_harness(engine_factory, prune):
+    """20 Canon seeds as 20 keys, lockstep: after every harness step the device's unmanaged notifications (in order, per key)
+    == the restated notifyUnmanaged / updateUnmanaged's (PostProcess.java:164-246, Updating.java:715-849), and every 25
+    steps the device's unmanaged registry == the restated CFK's unmanageds."""
+    seeds = PRUNE_SEEDS if prune else SEEDS
+    runs = [K.Run(seed, 1000, log=True, prune=prune, keep_states_every=25) for seed in seeds]
+    eng = engine_factory(window=0, replicas=1, drop_p=0.0, seed=1)
+    eng.cfk_store_open(len(runs), max(r.max_rows for r in runs) + 64)
+    steps = max(len(r.event_log) for r in runs)
+    seen, regs, tags = 0, 0, {0: 0, 1: 0, 2: 0}
+    for e in range(1, steps + 1):
+        eng.cfk_store_apply(_pack_step(runs, e))
+        got = eng.cfk_store_notified()
+        for k, r in enumerate(runs):
+            want = [(t, K.ts_bits(u, r.domains[u])) for t, u in (r.note_log[e - 1] if e <= len(r.note_log) else [])]
+            assert [(t, u) for _ev, t, u in got[k]] == want, "seed %d step %d" % (seeds[k], e)
+            seen += len(want)
+            for t, _ in want:
+                tags[t] += 1
+            st = r.states.get(e)
+            if st is not None:
+                reg = eng.cfk_store_unmanaged(k)
+                assert reg == [(p, K.ts_bits(w), K.ts_bits(u, r.domains[u])) for p, w, u in st.unmanageds], \
+                    "seed %d step %d: registry" % (seeds[k], e)
+                regs += len(reg)
+    assert seen > 500 and regs > 100 and min(tags.values()) > 20, (seen, regs, tags)
+    _record("store_unmanaged_%s" % ("prune" if prune else "plain"), {"notifications": seen, "by_tag": tags,
+                                                                      "registry_entries_checked": regs})

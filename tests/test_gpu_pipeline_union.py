@@ -1,10 +1,10 @@
-"""ad_run_pipeline's merged Deps — by default k_merge_cap over the R replies' CSRs (merge.hip merge_cap: one pass into
-capacity regions, compacted by merged_ready for the fetch), or, with ad_set_pipeline_union, the deps stage's union
+"""ad_run_pipeline's merged Deps — by default k_merge_ref over the R replies' CSRs (merge.hip merge_cap: references to an
+identical reply, the other txns merged in the same pass, compacted by merged_ready for the fetch), or, with ad_set_pipeline_union, the deps stage's union
 view (deps.hip stage_deps): the replies, the merged Deps (per class, ad_fetch_merged and ad_fetch_merged_all) and the
 levels equal the oracle's Deps.merge (RelationMultiMap.LinearMerger, utils/RelationMultiMap.java:284-406) on batches
 that take every branch of the deps stage: the fused tile kernel, the three-kernel path (hot keys), direct classes
 (sync points), txns with more than four keys (fill walk + k_txn_union), inline-id overflow re-walks, 1, 2, 4 and 7
-replica views (k_merge_cap's register path for <= 4 views, its serial loops above and for long lists)."""
+replica views (k_merge_ref's register path for <= 4 views, its serial loops above and for long lists)."""
 import numpy as np
 import pytest
 
@@ -59,7 +59,7 @@ def test_pipeline_union_equals_oracle(engine_factory, name, union):
     s = eng.merged_sizes()
     for c in range(abi.NUM_CLASSES):
         assert s[c].txns == s[c].txn_cap == len(merged[c].txns)
-    if not union:      # the merged entries k_merge_cap counted (per-workgroup sums) == the merged Deps' entries
+    if not union:      # the merged entries k_merge_ref counted (per-workgroup sums) == the merged Deps' entries
         want_e = sum(len(merged[c].k2t) - len(merged[c].keys) for c in range(abi.NUM_CLASSES))
         assert eng.last_times()["merged_entries"] == want_e
     lv, order = eng.fetch_levels()
