@@ -499,6 +499,21 @@ def scaling_reference(eng, args):
             "value": C5_PER_GPU / dt, "unit": "txn/s", "level_path": st["level_path"]}
 
 
+def pick_transport(name, dist, store, rank, world):
+    """The N > 1 exchange: RCCL over xGMI when asked for and every rank can use it, else the host (gloo) transport —
+    decided on every rank together (sharding.RcclTransport raises RcclUnavailable on all ranks at once, e.g. ranks
+    sharing one GPU, no unique id on rank 0, or a failed ncclCommInitRank anywhere), so no rank is left inside a
+    collective the others never enter.  config.transport names the outcome."""
+    from accord_amd import sharding
+    if name == "rccl":
+        try:
+            with stdout_to_stderr():      # RCCL's version banner
+                return sharding.RcclTransport(dist, store, rank, world)
+        except sharding.RcclUnavailable as e:
+            print("rank %d: RCCL unavailable (%s); using the host transport" % (rank, e), file=sys.stderr)
+    return sharding.GlooTransport(dist)
+
+
 def main_sharded(args, rank, world, local, dist):
     """N > 1: the C5 cross-shard protocol (see module docstring)."""
     from accord_amd import sharding
@@ -512,15 +527,7 @@ def main_sharded(args, rank, world, local, dist):
     device = local % max(1, engine.device_count())
     store = sharding.ShardStore(device, window=WINDOW, replicas=REPLICAS, drop_p=DROP_P, seed=workload.SEEDS["C5"])
     store.load(lb, gid, hs, n_total, rank, world, holders=holders)     # delta level exchange
-    tr = None
-    if args.transport == "rccl":
-        try:
-            with stdout_to_stderr():      # RCCL's version banner
-                tr = sharding.RcclTransport(dist, store, rank, world)
-        except sharding.RcclUnavailable as e:   # decided on every rank together (e.g. ranks sharing one GPU)
-            print("rank %d: RCCL unavailable (%s); using the host transport" % (rank, e), file=sys.stderr)
-    if tr is None:
-        tr = sharding.GlooTransport(dist)
+    tr = pick_transport(args.transport, dist, store, rank, world)
 
     phases = {}
 

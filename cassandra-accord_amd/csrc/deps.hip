@@ -115,6 +115,22 @@ void side_join(ad_handle* h) {
 // that reads every sorted entry (execution levels other than the pull pass, MaxConflicts, recovery, CFK retain,
 // sharded level passes).
 int complete_entries(ad_handle* h) {
+    if (h->state_partial) {              // k_seg_fuse wrote no entry state: the gather + ElideOp scan rebuild all of it
+        h->state_partial = h->keys_partial = h->entries_partial = false;
+        const size_t P = h->P;
+        if (P) {
+            KScope ks(K_GATHER, P);
+            k_gather_entries<false><<<ceil_div((long)P, 256), 256, 0, h->st>>>(P, h->sval, h->prec, h->skey, h->e_txn,
+                                                                              h->e_meta, h->e_exec1);
+            ElideOp eop{h->skey, h->e_meta, h->e_exec1, h->seg_start, h->ud_prev, h->pm_w, h->pm_c,
+                        h->nh, h->ukey, h->useg, h->hprm.key_min, P, h->prm,
+                        h->key_bits > 32 ? h->keys : nullptr, h->sval};
+            scan_any(h, eop, P);
+            h->nh_valid = true;
+        }
+        HIPCHK(h, hipGetLastError());
+        return AD_OK;
+    }
     if (h->keys_partial) {               // k_seg_fuse's batches: the distinct keys and segment starts, from its tiles
         h->keys_partial = false;
         const size_t nt = h->sf_ntiles;
@@ -192,6 +208,7 @@ static int stage_deps_impl(ad_handle* h) {
     const bool fuse = skip && !h->seg_long;
     const uint32_t* fuse_hpart = nullptr;
     h->keys_partial = false;
+    h->state_partial = false;
     uint32_t* fuse_over = h->totd + MAX_TOTALS - 6;      // (MAX_TOTALS - 5: the merge's speculation guard)
     if (P > 0 && !fuse) {
         h->entries_partial = skip;
@@ -290,6 +307,7 @@ static int stage_deps_impl(ad_handle* h) {
         fuse_hpart = f.hpart;              // n_keys_u: summed by the deps publish (PubExtra)
         h->nh_valid = false;               // no dense non-head list: the level chain build runs over every position
         h->keys_partial = true;            // ukey / useg on demand (complete_entries)
+        h->state_partial = true;           // the entry state too (k_seg_fuse writes it for re-walked segments only)
         h->sf_ntiles = ntiles;
     } else {
         h->chains_pending = false;

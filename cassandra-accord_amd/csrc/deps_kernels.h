@@ -632,7 +632,7 @@ __device__ inline void walk_entry(const WalkArgs& a, size_t s, uint32_t i, uint3
 }
 
 template <int NV, bool FILL, bool DIRECT>
-__device__ inline void walk_pair_entry(const WalkArgs& a, size_t s, uint64_t b1 = 0);
+__device__ inline bool walk_pair_entry(const WalkArgs& a, size_t s, uint64_t b1 = 0);
 
 template <int NV, bool FILL, bool DIRECT>
 static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
@@ -644,8 +644,10 @@ static __global__ __launch_bounds__(256) void k_deps_walk(WalkArgs a) {
 
 // One sorted entry's query (count: counts, inline ids, overflow position, fill items; fill: the entries into their
 // slots).  The entry state arrays of `a` may point into LDS (k_seg_fuse: shifted so that [s] lands in the tile).
+// Count mode returns whether a later kernel re-walks this entry from the global entry state (an overflowed list,
+// k_txn_finish_ovf; a wide txn's pair, the fill walk).
 template <int NV, bool FILL, bool DIRECT>
-__device__ inline void walk_pair_entry(const WalkArgs& a, size_t s, uint64_t b1) {
+__device__ inline bool walk_pair_entry(const WalkArgs& a, size_t s, uint64_t b1) {
     constexpr int NC = DIRECT ? 2 * NV : NV;
     const uint32_t i = a.e_txn[s];
     const uint32_t mi = a.e_meta[s];
@@ -690,7 +692,9 @@ __device__ inline void walk_pair_entry(const WalkArgs& a, size_t s, uint64_t b1)
         // the fill walk's items: every pair with entries of a txn with more than 4 keys (deferred to walk<fill>
         // + k_txn_union; k_txn_finish lays them out)
         wave_append(wide && any, (uint32_t)s, a.items_out, a.items_count);
+        return (over && !wide) || (wide && any);
     }
+    return false;
 }
 
 // Virtual items (large txns), one thread per item; counts/slots AoS [x * NC + vc].

@@ -244,7 +244,7 @@ static int pack_clear_list(ad_handle* h, PackPlan& plan) {
     h->small_cleared = true;
     // ad_run_pipeline on a key-only batch whose levels will try the pull pass first: its succ words and flags zeroed
     // here too, so k_seg_fuse can build the chains (stage_deps decides; run_levels then skips k_chain_build)
-    const bool pull = h->want_union && h->P > 0 && h->Q == 0 && !h->ls.long_hint && !h->no_fused_chains &&
+    const bool pull = h->in_pipeline && h->P > 0 && h->Q == 0 && !h->ls.long_hint && !h->no_fused_chains &&
                       h->level_mode != AD_LEVELS_FIXPOINT && h->level_mode != AD_LEVELS_BLOCKS &&
                       h->level_mode != AD_LEVELS_BLOCKS_WIDE && h->level_mode != AD_LEVELS_KAHN && !h->hist_active;
     if (pull) {
@@ -1501,7 +1501,10 @@ int ad_run_pipeline(ad_handle* h) {
     // the merged Deps: k_merge_cap over the R replies (stage_merge); ad_set_pipeline_union(h, 1) instead builds them
     // as the deps stage's union view, a shortcut only a generator that holds every view's inputs can take
     h->want_union = h->pipeline_union;
-    CK(stage_prepare(h));
+    h->in_pipeline = true;                       // stage_prepare: k_seg_fuse may build the pull pass's chains
+    const int rc_prep = stage_prepare(h);
+    h->in_pipeline = false;
+    CK(rc_prep);
     host_mark(h, "prepare returned");
     HIPCHK(h, hipEventRecord(h->ev[1], st));
     CK(stage_sort(h));

@@ -195,6 +195,7 @@ struct ad_handle {
     bool no_fused_chains = getenv("AD_NO_FUSED_CHAINS") != nullptr;   // A/B switch
     bool merged_exact = true;        // merged TxnId lists exact (k_merge); false: capacity regions + tcnt (union view)
     bool merged_compacted = false;   // !merged_exact: the exact offsets / lists below are built (merged_compact)
+    bool in_pipeline = false;        // ad_run_pipeline's stage_prepare is running
     bool pipeline_union = false;     // ad_set_pipeline_union: ad_run_pipeline takes the union view (a generator shortcut)
     bool merged_cap = false;         // merged key classes as k_merge_ref's references + merged rows (merged_ready compacts)
     bool mcap_direct = false;        //   ... the directKeyDeps class too
@@ -208,6 +209,7 @@ struct ad_handle {
     size_t mx_tot[3] = {};
     bool nh_valid = false;           // nh holds the batch's non-head entries (not after k_seg_fuse)
     bool keys_partial = false;       // k_seg_fuse left ukey / useg to complete_entries (from its tiles)
+    bool state_partial = false;      // ... and the entry state (complete_entries: gather + ElideOp scan)
     size_t sf_ntiles = 0;
     int stage = 0;                   // STAGE_* while a stage allocates (what an allocation failure may evict)
     bool evicting = false;

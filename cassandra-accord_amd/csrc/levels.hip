@@ -36,6 +36,9 @@ int stage_levels(ad_handle* h, bool want_order) {
     if (!h->have_merged) return set_err(h, AD_ERR_STATE, "ad_exec_levels before ad_merge_deps");
     if (!h->have_deps) return set_err(h, AD_ERR_STATE, "ad_exec_levels needs ad_preaccept_deps on this batch (its key chains)");
     if (h->hist_active) return levels_history(h, want_order);
+    // k_seg_fuse left the entry state to complete_entries: the pull pass's own chain build reads it (the chains
+    // k_seg_fuse prebuilt in ad_run_pipeline do not)
+    if (h->state_partial && !h->chains_prebuilt) CK(complete_entries(h));
     LevelInputs li{};
     li.n = h->n; li.P = h->P; li.e_txn = h->e_txn; li.e_meta = h->e_meta; li.e_exec1 = h->e_exec1;
     li.seg_start = h->seg_start; li.sval = h->sval; li.nh = h->nh_valid ? h->nh : nullptr;

@@ -7,9 +7,10 @@
 // SF_TILE nominal sorted positions moves its start and end forward to the next segment head (one 64-lane ballot
 // per step), loads its keys, gathers the records of the entries in multi-entry segments (an entry alone in its
 // segment is read by no query of the batch: complete_entries fills it in for the stages that read every entry),
-// resolves each segment's state serially in LDS (a C2 segment holds ~1.5 entries), writes the state arrays the
-// later stages read (seg_start for every entry; txn, meta, executeAt + 1, last always-emitted entry and the two
-// prefix maxima for the multi-entry segments), and runs every non-head entry's query against the LDS copy.
+// resolves each segment's state serially in LDS (a C2 segment holds ~1.5 entries), runs every non-head entry's query
+// against the LDS copy, and writes the global entry state (txn, meta, executeAt + 1, segment start, last always-emitted
+// entry, the two prefix maxima) only for the segments a later kernel re-walks (complete_entries rebuilds it for the
+// stages that read every entry).
 // Replaces k_gather_entries<true> + the three ElideOp scan launches + k_deps_walk<count>, whose reads of the
 // per-entry arrays were spread over every sorted position (C2: 767,867 queries among 4,194,304 entries; the walk
 // fetched 9.5x its byte model).  ElideOp's store: the tiles' head counts go to 256 partial sums (one atomic per tile,
@@ -96,6 +97,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     __shared__ uint16_t s_glist[SF_CAP];
     __shared__ uint16_t s_qlist[SF_CAP];
     __shared__ uint16_t s_slist[SF_SEC];
+    __shared__ uint8_t s_need[SF_CAP];           // by segment head: some query of the segment is re-walked later
     __shared__ uint32_t s_bounds[2];
     __shared__ uint32_t s_cnt[5];
     const size_t b = blockIdx.x;
@@ -132,7 +134,7 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         const bool last = in && (i + 1 == L || s_key[i + 1] != s_key[i]);
         heads += head ? 1u : 0u;
         nonheads += (in && !head) ? 1u : 0u;
-        if (head && last) f.seg_start[lo + i] = (int32_t)(lo + i);     // lone: its segment start (rest: complete_entries)
+        if (in) s_need[i] = 0;
         sf_list_append(in && !(head && last), (uint16_t)i, s_glist, &s_cnt[2]);
         sf_list_append(in && !head, (uint16_t)i, s_qlist, &s_cnt[3]);
         // the second entry of a segment (its predecessor is the head)
@@ -150,7 +152,6 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         const uint32_t i = s_glist[x];
         const PairRec r = f.prec[w.sval[lo + i]];
         s_txn[i] = r.txn; s_meta[i] = (uint8_t)r.meta; s_ex1[i] = r.ex1; s_eq[i] = (r.meta & PREC_EXEQ) ? 1 : 0;
-        f.e_txn[lo + i] = r.txn; f.e_meta[lo + i] = (uint8_t)r.meta; f.e_exec1[lo + i] = r.ex1;
     }
     __syncthreads();
     // per multi-entry segment (its head's thread): the elision scan state, serially (ElideOp::combine restarted at the
@@ -173,10 +174,6 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
         }
     }
     __syncthreads();
-    for (uint32_t x = rr; x < ng; x += SF_T) {
-        const uint32_t i = s_glist[x];
-        f.seg_start[lo + i] = s_ss[i]; f.ud_prev[lo + i] = s_ud[i]; f.pm_w[lo + i] = s_pw[i]; f.pm_c[lo + i] = s_pc[i];
-    }
     if (tid == 0) {
         f.tile_cnt[2 * b] = s_cnt[0]; f.tile_cnt[2 * b + 1] = s_cnt[1];
         if (s_cnt[0]) atomicAdd(&f.hpart[b % SF_PARTS], s_cnt[0]);
@@ -191,7 +188,19 @@ static __global__ __launch_bounds__(SF_T) void k_seg_fuse(SegFuseArgs f, WalkArg
     // (the PreAccept bound TxnId + 1 from the record when executeAt == TxnId: no random tx_ts read for ~90 % of them)
     for (uint32_t x = rr; x < nq; x += SF_T) {
         const uint32_t q = s_qlist[x];
-        walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + q, s_eq[q] ? s_ex1[q] : 0ull);
+        if (walk_pair_entry<NV, false, DIRECT>(a, (size_t)lo + q, s_eq[q] ? s_ex1[q] : 0ull)) s_need[s_ss[q] - (int32_t)lo] = 1;
+    }
+    __syncthreads();
+    // The global entry state (gathered record + elision state) only for the segments a later kernel re-walks from it
+    // (overflowed lists: k_txn_finish_ovf; wide txns: the fill walk) — C2: a few segments per batch.  Every other
+    // stage that reads the entries (levels other than the pull pass, MaxConflicts, recovery, CFK retain, sharded
+    // levels) calls complete_entries first, which rebuilds the whole state with the gather + ElideOp scan (the
+    // scattered state writes were ~60 % of this kernel's HBM write traffic).
+    for (uint32_t x = rr; x < ng; x += SF_T) {
+        const uint32_t i = s_glist[x];
+        if (!s_need[s_ss[i] - (int32_t)lo]) continue;
+        f.e_txn[lo + i] = s_txn[i]; f.e_meta[lo + i] = s_meta[i]; f.e_exec1[lo + i] = s_ex1[i];
+        f.seg_start[lo + i] = s_ss[i]; f.ud_prev[lo + i] = s_ud[i]; f.pm_w[lo + i] = s_pw[i]; f.pm_c[lo + i] = s_pc[i];
     }
     if (f.c_txn) {
         bool lng = false, far = false;

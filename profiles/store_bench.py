@@ -5,8 +5,9 @@ event stream: events/s, with the hottest key's serial chain named.
 Stream (seeded, synthetic): BASELINE configs[2]'s generator — 1,048,576 txns x 4 keys, Zipf(0.99) over 10^7 keys,
 50 % Reads / Writes — replayed as the CommandsForKey.update calls a replica makes (CommandsForKey.java:987-1057): txn i
 is PreAccepted at step i, Committed and Stable (executeAt = TxnId, deps = the earlier txns on the key within the
-in-flight window W that it witnesses, Kind.witnesses) at step i + W, Applied at step i + 2W; after every Apply a
-maybePrune(4, 0) event on the key (Pruning.java:164-233) keeps each key's rows near its in-flight set.  Every
+in-flight window W that it witnesses, Kind.witnesses — on the Commit update) at step i + W, Applied at step i + 2W;
+after every Apply a maybePrune(4, 0) event on the key (Pruning.java:164-233) keeps each key's rows near its in-flight
+set.  Every
 (txn, key) pair is one event per transition on its key: ~21 M events over ~1.1 M keys.  Events go to the store in
 calls of `--batch` txns' steps, grouped by key; keys are applied in parallel (one workgroup each) and each key's
 events in order — the hottest key (~200 k pairs, ~1 M events) is a serial chain, as it is in the reference (one
@@ -85,7 +86,10 @@ def pack_call(b, kidx, ptxn, dep, key_off, s0, s1, window, K):
            # executeAt = TxnId (fast path); a PRUNE event: interval 4 in exec_node, minHlcDelta 0 in exec_msb
            "exec_msb": np.where(prune, 0, tm[t]).astype(np.uint64), "exec_lsb": np.where(prune, 0, tl[t]).astype(np.uint64),
            "exec_node": np.where(prune, 4, tn[t]).astype(np.int32)}
-    with_deps = (tr >= 1) & (tr <= 3)
+    # deps on the Commit; the Stable / Apply updates carry none: by then every witnessed txn below the command is decided
+    # (committed at its own step + W), so the rebuilt missing() is empty either way, and re-sending deps that pruning
+    # already removed would only queue loads of them (LoadPruned) this stream does not model
+    with_deps = tr == 1
     d = np.where(with_deps[:, None], dep[pair], -1)
     cnt = (d >= 0).sum(1)
     doff = np.zeros(m + 1, np.uint32)
