@@ -148,11 +148,31 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     a.nt_base = c.nt_base; a.nt_cnt = c.nt_cnt; a.nt_ev = c.nt_ev; a.nt_tag = c.nt_tag;
     a.nt_tm = c.nt_tm; a.nt_tl = c.nt_tl; a.nt_tn = c.nt_tn;
     HIPCHK(h, hipMemsetAsync(c.flags, 0, 8, st));          // this call's overflow / order flags
-    k_cfk_apply<<<c.K, CS_T, 0, st>>>(a);
+    const char* tmr = getenv("AD_CS_TIMERS");
+    uint64_t* dbg = nullptr;
+    if (tmr && tmr[0] == '1') {
+        HIPCHK(h, hipMalloc(&dbg, 8 * 128));
+        HIPCHK(h, hipMemsetAsync(dbg, 0, 8 * 128, st));
+    }
+    a.dbg = dbg;
+    // rows in LDS while the key's events apply when they fit (AD_CFK_STORE_HBM=1: the HBM-resident kernel, for tests)
+    const char* hbm = getenv("AD_CFK_STORE_HBM");
+    if (c.cap <= CS_LDS_CAP && !(hbm && hbm[0] == '1')) k_cfk_apply<true><<<c.K, CS_T, 0, st>>>(a);
+    else k_cfk_apply<false><<<c.K, CS_T, 0, st>>>(a);
     HIPCHK(h, hipGetLastError());
     uint32_t f[2] = {0, 0};
     HIPCHK(h, hipMemcpyAsync(f, c.flags, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
+    if (dbg) {                                   // per key % 8 group: op class (cycles, events)
+        uint64_t d[128];
+        HIPCHK(h, hipMemcpy(d, dbg, sizeof d, hipMemcpyDeviceToHost));
+        hipFree(dbg);
+        for (int g = 0; g < 8; ++g) {
+            fprintf(stderr, "cs_timers g%d", g);
+            for (int k = 0; k < 8; ++k) fprintf(stderr, " %d:%llu/%llu", k, (unsigned long long)d[16 * g + 2 * k], (unsigned long long)d[16 * g + 2 * k + 1]);
+            fprintf(stderr, "\n");
+        }
+    }
     if (f[1]) return set_err(h, AD_ERR_UNSORTED, "ad_cfk_store_apply: an event's deps are not strictly ascending");
     // (the key that ran out is left as far as its last complete event: reopen the store, or fetch it and replay)
     if (f[0]) return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_store_apply: a key outgrew the store's capacity (rows or "

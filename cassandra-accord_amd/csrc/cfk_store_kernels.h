@@ -25,7 +25,10 @@
 
 namespace ad {
 
-constexpr int CS_T = 256;
+// One wave per key: the per-event folds (maxAppliedWrite, minUndecided, the prune point, ...) are wave reductions with
+// no workgroup barrier (a 256-thread fold was ~10 barriers; an event ran ~4 of them: ~9.4 us per event on the hottest
+// key's serial chain with the rows already in LDS)
+constexpr int CS_T = 64;
 constexpr uint32_t CS_MAX_WORDS = NF_MAX_WORDS; // capacity <= 8192 rows per key
 
 struct CfkStoreArgs {
@@ -70,6 +73,7 @@ struct CfkStoreArgs {
     uint8_t* nt_tag;
     uint64_t *nt_tm, *nt_tl;
     int32_t* nt_tn;
+    uint64_t* dbg;                            // AD_CS_TIMERS=1: per op class clock64 sums and counts (else nullptr)
 };
 // event ops (ad_cfk_events.op)
 constexpr uint32_t CS_OP_UPDATE = 0;         // CommandsForKey.update (or insertAdditionsOnly: status TRANSITIVELY_KNOWN)
@@ -171,6 +175,7 @@ __device__ inline uint32_t cs_insert(const CfkStoreArgs& a, size_t base, uint32_
 // ---- loadingPruned (Pruning.LoadingPruned, Pruning.java:50-114) ----------------------------------------------------
 // the entry of TxnId t in key's table, or -1 (TxnIds are unique in the table)
 __device__ inline int cs_lp_find(const CfkStoreArgs& a, uint32_t key, uint32_t L, const Ts3& t, int* s_j) {
+    if (L == 0) return -1;                                        // (uniform: L is the workgroup's count)
     if (threadIdx.x == 0) *s_j = -1;
     __syncthreads();
     const size_t lb = (size_t)key * a.cap;
@@ -234,17 +239,23 @@ struct CsPruneLds {
     uint32_t idx;
 };
 __device__ inline uint64_t cs_hlc(const Ts3& t) { return ((t.msb & 0x7FFFull) << 48) | (t.lsb >> 16); }
-__device__ inline uint32_t cs_block_sum(uint32_t v, uint32_t* s_c) {
-    const int tid = threadIdx.x;
-    s_c[tid] = v;
-    __syncthreads();
-    for (int o = CS_T / 2; o > 0; o >>= 1) {
-        if (tid < o) s_c[tid] += s_c[tid + o];
-        __syncthreads();
+__device__ inline uint32_t cs_block_sum(uint32_t v, uint32_t*) {
+    static_assert(CS_T == 64, "one wave per key");
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+// the block's greatest (MAX) / least TxnId-ordered value among the lanes that have one (every lane gets it)
+template <bool MAX>
+__device__ inline void cs_fold(Ts3& v, bool& has) {
+    static_assert(CS_T == 64, "one wave per key");
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t mh = (uint32_t)__shfl_xor((int)(uint32_t)(v.msb >> 32), o), ml = (uint32_t)__shfl_xor((int)(uint32_t)v.msb, o);
+        const uint32_t lh = (uint32_t)__shfl_xor((int)(uint32_t)(v.lsb >> 32), o), ll = (uint32_t)__shfl_xor((int)(uint32_t)v.lsb, o);
+        const int nd = __shfl_xor(v.node, o);
+        const bool hu = __shfl_xor(has ? 1 : 0, o) != 0;
+        const Ts3 u{((uint64_t)mh << 32) | ml, ((uint64_t)lh << 32) | ll, nd};
+        if (hu && (!has || (MAX ? ts3_cmp(u, v) > 0 : ts3_cmp(u, v) < 0))) { v = u; has = true; }
     }
-    const uint32_t r = s_c[0];
-    __syncthreads();
-    return r;
 }
 // bits below position i that are set in bitmap b (with its exclusive per-word prefix counts pc)
 __device__ inline uint32_t cs_rank(const uint64_t* b, const uint32_t* pc, uint32_t i) {
@@ -281,7 +292,7 @@ __device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_
             if (!has || ts3_cmp(e, maw) > 0) { maw = e; has = true; }
         }
     }
-    nf_block_fold<true>(maw, has, s.v, s.h);
+    cs_fold<true>(maw, has);
     if (!has) return;
     uint32_t below = 0;
     for (uint32_t r = tid; r < n; r += CS_T) {
@@ -300,7 +311,7 @@ __device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_
             if (ts3_cmp(e, maw) < 0 && (int64_t)cs_hlc(e) <= lim && (!hp || ts3_cmp(e, pex) > 0)) { pex = e; hp = true; }
         }
     }
-    nf_block_fold<true>(pex, hp, s.v, s.h);
+    cs_fold<true>(pex, hp);
     if (!hp) return;
     if (tid == 0) s.idx = n;
     __syncthreads();
@@ -467,6 +478,7 @@ __device__ inline bool cs_um_insert(const CfkStoreArgs& a, size_t ub, uint32_t c
 __device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t base, uint32_t n, uint32_t L, uint32_t ns,
                                     const Ts3& ex, uint32_t e, CsPruneLds& s, uint32_t* s_U) {
     const int tid = threadIdx.x;
+    if (*s_U == 0) return;                                        // no unmanaged txn waits on this key
     const size_t ub = (size_t)key * a.cap, lb = ub;
     Ts3 b{0, 0, 0};
     bool hb = false;
@@ -481,7 +493,7 @@ __device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t 
         const Ts3 u{a.lpm[lb + j], a.lpl[lb + j], a.lpn[lb + j]};
         if (!hb || ts3_cmp(u, b) < 0) { b = u; hb = true; }
     }
-    nf_block_fold<false>(b, hb, s.v, s.h);
+    cs_fold<false>(b, hb);
     if (tid == 0) {
         uint32_t U = *s_U, end = 0;
         while (end < U && a.um_p[ub + end] == UM_COMMIT && (!hb || ts3_cmp(b, cs_um_w(a, ub + end)) > 0)) ++end;
@@ -502,7 +514,7 @@ __device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t 
             if (!hm || ts3_cmp(u, maw) > 0) { maw = u; hm = true; }
         }
     }
-    nf_block_fold<true>(maw, hm, s.v, s.h);
+    cs_fold<true>(maw, hm);
     for (uint32_t r = tid; r < n; r += CS_T) {
         const size_t x = base + r;
         const uint32_t st = a.st[x];
@@ -511,7 +523,7 @@ __device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t 
             if ((!hm || ts3_cmp(u, maw) > 0) && (!hbl || ts3_cmp(u, bl) < 0)) { bl = u; hbl = true; }
         }
     }
-    nf_block_fold<false>(bl, hbl, s.v, s.h);
+    cs_fold<false>(bl, hbl);
     for (uint32_t r = tid; r < n; r += CS_T) {
         const size_t x = base + r;
         if (cs_decided(a.st[x])) {
@@ -519,7 +531,7 @@ __device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t 
             if ((!hbl || ts3_cmp(u, bl) < 0) && (!hmca || ts3_cmp(u, mca) > 0)) { mca = u; hmca = true; }
         }
     }
-    nf_block_fold<true>(mca, hmca, s.v, s.h);
+    cs_fold<true>(mca, hmca);
     if (hmca && ts3_cmp(mca, ex) < 0) hmca = false;
     if (hmca && tid == 0) {
         uint32_t U = *s_U, st = 0;
@@ -588,7 +600,7 @@ __device__ inline bool cs_um_update(const CfkStoreArgs& a, uint32_t key, size_t 
     }
     ready = __syncthreads_and(ready ? 1 : 0) != 0;
     waiting = __syncthreads_and(waiting ? 1 : 0) != 0;
-    nf_block_fold<true>(xm, hx, s.v, s.h);
+    cs_fold<true>(xm, hx);
     bool ok = true;
     if (tid == 0) {
         const size_t ub = (size_t)key * a.cap;
@@ -619,23 +631,48 @@ __device__ inline bool cs_um_update(const CfkStoreArgs& a, uint32_t key, size_t 
 // Utils.java:229-244); a LOAD event, or an update of a TxnId in loadingPruned, is CommandsForKey.update's wasPruned path
 // (:1015-1024: no missing(), the TxnId joins the other rows' missing() except its witnesses'); PRUNE / LOADING events
 // as CS_OP_* says.
-static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
-    __shared__ uint64_t s_miss[CS_MAX_WORDS];
-    __shared__ uint32_t s_add[CS_T];          // this event's additions (slots), CS_T at a time
-    __shared__ uint32_t s_nadd;
-    __shared__ int s_j;
-    __shared__ CsPruneLds s_prune;
-    __shared__ uint32_t s_U;
-    const uint32_t key = blockIdx.x;
-    if (key >= a.K) return;
-    const size_t base = (size_t)key * a.cap;
-    uint32_t n = a.cnt[key];
-    uint32_t L = a.lp_cnt[key];
-    if (threadIdx.x == 0) { s_U = a.um_cnt[key]; a.nt_cnt[key] = 0; }
-    __syncthreads();
-    for (uint32_t e = a.ev_off[key]; e < a.ev_off[key + 1]; ++e) {
+constexpr uint32_t CS_EV_CHUNK = 128, CS_DEP_CHUNK = 512;
+struct CsEvChunk {                            // a chunk of the key's events and their deps (k_cfk_apply)
+    uint64_t tm[CS_EV_CHUNK], tl[CS_EV_CHUNK], xm[CS_EV_CHUNK], xl[CS_EV_CHUNK];
+    int32_t tn[CS_EV_CHUNK], xn[CS_EV_CHUNK];
+    uint8_t st[CS_EV_CHUNK], op[CS_EV_CHUNK];
+    uint32_t doff[CS_EV_CHUNK + 1];
+    uint64_t dm[CS_DEP_CHUNK], dl[CS_DEP_CHUNK];
+    int32_t dn[CS_DEP_CHUNK];
+    uint32_t m;
+};
+struct CsApplyLds {
+    CsEvChunk ev;
+    uint64_t miss[CS_MAX_WORDS];
+    uint32_t add[CS_T];                       // this event's additions (slots), CS_T at a time
+    uint32_t nadd, row, U;
+    int j;
+    uint64_t t0;
+    uint32_t tcls;
+    CsPruneLds prune;
+};
+// The key's events in order (a = the rows' view: HBM, or the LDS copy with base 0).  Returns early when the key runs
+// out of rows or loadingPruned / registry entries (overflow flag set); n, L and s.U are the key's counts either way.
+__device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkStoreArgs& a, uint32_t key, size_t base, uint32_t& n, uint32_t& L,
+                                       CsApplyLds& sh, uint32_t e_lo, uint32_t e_hi, uint32_t e_id0) {
+    uint64_t* s_miss = sh.miss;
+    uint32_t* s_add = sh.add;
+    uint32_t& s_nadd = sh.nadd;
+    int& s_j = sh.j;
+    CsPruneLds& s_prune = sh.prune;
+    uint32_t& s_U = sh.U;
+    for (uint32_t e = e_lo; e < e_hi; ++e) {
         const Ts3 t{a.etm[e], a.etl[e], a.etn[e]};
         const uint32_t op = a.eop ? a.eop[e] : CS_OP_UPDATE;
+        if (a.dbg && threadIdx.x == 0) {                          // the previous event's cycles, by its class
+            const uint64_t now = clock64();
+            if (sh.tcls < 8) {
+                atomicAdd((unsigned long long*)&a.dbg[2 * (key % 8) * 8 + 2 * sh.tcls], (unsigned long long)(now - sh.t0));
+                atomicAdd((unsigned long long*)&a.dbg[2 * (key % 8) * 8 + 2 * sh.tcls + 1], 1ull);
+            }
+            sh.t0 = now;
+            sh.tcls = op == CS_OP_UPDATE ? (a.dep_off[e + 1] > a.dep_off[e] ? 0u : (cs_has_deps(a.est[e]) ? 1u : 2u)) : 2u + op;
+        }
         if (op == CS_OP_PRUNE) {
             cs_maybe_prune(a, key, base, n, L, (uint32_t)a.een[e], (int64_t)a.eem[e], s_prune);
             __syncthreads();
@@ -652,14 +689,14 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 const uint32_t q = cs_find(a, base, n, wt, f);
                 if (f) w = a.slot[base + q];
             }
-            if (!cs_lp_add(a, key, L, t, w, &s_j, wt, hw)) { if (threadIdx.x == 0) *a.overflow = 1u; break; }
+            if (!cs_lp_add(a, key, L, t, w, &s_j, wt, hw)) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
             continue;
         }
         if (op == CS_OP_UNMANAGED || op == CS_OP_UNMANAGED_RECHECK) {
             if (!cs_um_update(a, key, base, n, L, t, Ts3{a.eem[e], a.eel[e], a.een[e]}, a.dep_off[e], a.dep_off[e + 1],
-                              op == CS_OP_UNMANAGED, e, s_prune, &s_U)) {
+                              op == CS_OP_UNMANAGED, e + e_id0, s_prune, &s_U)) {
                 if (threadIdx.x == 0) *a.overflow = 1u;
-                break;
+                return false;
             }
             continue;
         }
@@ -678,7 +715,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             if (jl >= 0) cs_lp_remove(a, key, L, jl);
             uint32_t ts;
             if (!found) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; break; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
                 ts = cs_insert(a, base, n, p, t, ns, ex);
             } else {
                 ts = a.slot[base + p];
@@ -693,7 +730,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             else if (found && cur < AD_ST_COMMITTED && ns == AD_ST_INVALID) cs_remove_missing(a, base, n, ts);
             else if (!found && ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu, s_miss);
             __syncthreads();
-            cs_um_notify(a, key, base, n, L, ns, ex, e, s_prune, &s_U);
+            cs_um_notify(a, key, base, n, L, ns, ex, e + e_id0, s_prune, &s_U);
             continue;
         }
         const uint32_t d0 = a.dep_off[e], d1 = a.dep_off[e + 1];
@@ -731,10 +768,9 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 for (uint32_t k = 0; k < nadd; ++k) {
                     const uint32_t s = s_add[k];
                     // the addition's TxnId: find its row through the slot (rows shifted since): a scan for the slot
-                    __shared__ uint32_t s_row;
-                    for (uint32_t r = threadIdx.x; r < n; r += CS_T) if (a.slot[base + r] == s) s_row = r;
+                    for (uint32_t r = threadIdx.x; r < n; r += CS_T) if (a.slot[base + r] == s) sh.row = r;
                     __syncthreads();
-                    const size_t x = base + s_row;
+                    const size_t x = base + sh.row;
                     const Ts3 ad{a.tm[x], a.tl[x], a.tn[x]};
                     cs_add_missing(a, base, n, ad, s, skip);
                 }
@@ -753,7 +789,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 const uint32_t q = cs_find(a, base, n, d, f);
                 if (f) continue;
                 if (ts3_cmp(d, pb) < 0) continue;                      // a pruned addition: loadingPruned, below
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
                 if (s_nadd >= (uint32_t)CS_T) flush_adds(cmd_slot);
                 const uint32_t s = cs_insert(a, base, n, q, d, AD_ST_TRANSITIVELY_KNOWN, d);
                 if (threadIdx.x == 0) s_add[s_nadd++] = s;
@@ -763,7 +799,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             bool fnow;
             const uint32_t p2 = cs_find(a, base, n, t, fnow);           // t's position after the additions
             if (!fnow) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
                 ts = cs_insert(a, base, n, p2, t, ns, ex);
             } else {
                 ts = a.slot[base + p2];
@@ -782,19 +818,18 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 cs_find(a, base, n, d, f);
                 if (f) continue;
                 if (!cs_lp_add(a, key, L, d, ts, &s_j, t, true)) {
-                    if (threadIdx.x == 0) { *a.overflow = 1u; a.um_cnt[key] = s_U; }
-                    a.cnt[key] = n; a.lp_cnt[key] = L;
-                    return;
+                    if (threadIdx.x == 0) *a.overflow = 1u;
+                    return false;
                 }
             }
             flush_adds(ts);
             if (!found && ns < AD_ST_COMMITTED) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             if (found && cur < AD_ST_COMMITTED && ns >= AD_ST_COMMITTED) cs_remove_missing(a, base, n, ts);
             __syncthreads();
-            cs_um_notify(a, key, base, n, L, ns, ex, e, s_prune, &s_U);
+            cs_um_notify(a, key, base, n, L, ns, ex, e + e_id0, s_prune, &s_U);
         } else {
             if (!found) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; return; }
+                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
                 const uint32_t ts = cs_insert(a, base, n, p, t, ns, t);
                 if (ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             } else {
@@ -808,11 +843,99 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
                 if (cur < AD_ST_COMMITTED && ns == AD_ST_INVALID) cs_remove_missing(a, base, n, ts);
             }
             __syncthreads();
-            cs_um_notify(a, key, base, n, L, ns, t, e, s_prune, &s_U);
+            cs_um_notify(a, key, base, n, L, ns, t, e + e_id0, s_prune, &s_U);
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = s_U; }
+    return true;
+}
+
+// One workgroup per key with events.  LDS: the key's rows and missing() bitmaps (capacity <= CS_LDS_CAP) are copied
+// into LDS, the events applied there and the result written back once — every row read of an event (the byId
+// searches, the missing() rebuild, the notify folds) is then an LDS access instead of an HBM round trip (~10 dependent
+// ones per event: ~10 us per event on the hottest key's serial chain).  loadingPruned and the unmanaged registry
+// (empty for most keys) stay in HBM.
+constexpr uint32_t CS_LDS_CAP = 256;
+template <bool LDS>
+static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
+    __shared__ CsApplyLds sh;
+    constexpr uint32_t RC = LDS ? CS_LDS_CAP : 1u, BW = LDS ? CS_LDS_CAP * (CS_LDS_CAP / 64) : 1u;
+    __shared__ uint64_t r_tm[RC], r_tl[RC], r_em[RC], r_el[RC], r_bits[BW];
+    __shared__ int32_t r_tn[RC], r_en[RC];
+    __shared__ uint32_t r_slot[RC];
+    __shared__ uint8_t r_st[RC];
+    const uint32_t key = blockIdx.x;
+    if (key >= a.K) return;
+    if (threadIdx.x == 0) a.nt_cnt[key] = 0;
+    if (a.ev_off[key] == a.ev_off[key + 1]) return;              // no events: the key is unchanged
+    const size_t gbase = (size_t)key * a.cap;
+    uint32_t n = a.cnt[key];
+    uint32_t L = a.lp_cnt[key];
+    if (threadIdx.x == 0) { sh.U = a.um_cnt[key]; sh.tcls = 8; sh.t0 = 0; }
+    CfkStoreArgs v = a;
+    size_t base = gbase;
+    if (LDS) {
+        for (uint32_t r = threadIdx.x; r < n; r += CS_T) {
+            const size_t x = gbase + r;
+            r_tm[r] = a.tm[x]; r_tl[r] = a.tl[x]; r_tn[r] = a.tn[x]; r_em[r] = a.em[x]; r_el[r] = a.el[x];
+            r_en[r] = a.en[x]; r_st[r] = a.st[x]; r_slot[r] = a.slot[x];
+        }
+        for (uint32_t i = threadIdx.x; i < n * a.words; i += CS_T) r_bits[i] = a.bits[gbase * a.words + i];
+        v.tm = r_tm; v.tl = r_tl; v.tn = r_tn; v.em = r_em; v.el = r_el; v.en = r_en; v.st = r_st; v.slot = r_slot;
+        v.bits = r_bits;
+        base = 0;
+    }
+    __syncthreads();
+    // the events in chunks of <= CS_EV_CHUNK whose deps fit CS_DEP_CHUNK, staged in LDS by one parallel load each (the
+    // events' fields, then their deps): per event no dependent HBM read is left on the key's serial path (the deps'
+    // searches and the additions scan read one dependency after another).  An event with more deps than a chunk holds
+    // runs alone from HBM.
+    for (uint32_t e = a.ev_off[key], end = a.ev_off[key + 1]; e < end;) {
+        const uint32_t lim = min(end - e, CS_EV_CHUNK);
+        for (uint32_t i = threadIdx.x; i <= lim; i += CS_T) sh.ev.doff[i] = a.dep_off[e + i];
+        if (threadIdx.x == 0) sh.ev.m = 0;
+        __syncthreads();
+        const uint32_t d0 = sh.ev.doff[0];
+        for (uint32_t i = threadIdx.x + 1; i <= lim; i += CS_T)
+            if (sh.ev.doff[i] - d0 <= CS_DEP_CHUNK) atomicMax(&sh.ev.m, i);
+        __syncthreads();
+        const uint32_t m = sh.ev.m, nd = m ? sh.ev.doff[m] - d0 : 0u;
+        bool ok;
+        if (m == 0) {                                             // one event with more deps than a chunk
+            ok = cs_apply_events(v, key, base, n, L, sh, e, e + 1, 0);
+            e += 1;
+        } else {
+            for (uint32_t i = threadIdx.x; i < m; i += CS_T) {
+                const uint32_t x = e + i;
+                sh.ev.tm[i] = a.etm[x]; sh.ev.tl[i] = a.etl[x]; sh.ev.tn[i] = a.etn[x]; sh.ev.st[i] = a.est[x];
+                sh.ev.xm[i] = a.eem[x]; sh.ev.xl[i] = a.eel[x]; sh.ev.xn[i] = a.een[x];
+                sh.ev.op[i] = a.eop ? a.eop[x] : (uint8_t)CS_OP_UPDATE;
+            }
+            for (uint32_t j = threadIdx.x; j < nd; j += CS_T) {
+                sh.ev.dm[j] = a.dtm[d0 + j]; sh.ev.dl[j] = a.dtl[d0 + j]; sh.ev.dn[j] = a.dtn[d0 + j];
+            }
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i <= m; i += CS_T) sh.ev.doff[i] -= d0;
+            __syncthreads();
+            CfkStoreArgs w = v;
+            w.etm = sh.ev.tm; w.etl = sh.ev.tl; w.etn = sh.ev.tn; w.est = sh.ev.st; w.eem = sh.ev.xm; w.eel = sh.ev.xl;
+            w.een = sh.ev.xn; w.eop = sh.ev.op; w.dep_off = sh.ev.doff; w.dtm = sh.ev.dm; w.dtl = sh.ev.dl; w.dtn = sh.ev.dn;
+            ok = cs_apply_events(w, key, base, n, L, sh, 0, m, e);
+            e += m;
+        }
+        __syncthreads();
+        if (!ok) break;
+    }
+    __syncthreads();
+    if (LDS) {                                                    // slots are dense: [0, n) rows, [0, n) bitmaps
+        for (uint32_t r = threadIdx.x; r < n; r += CS_T) {
+            const size_t x = gbase + r;
+            a.tm[x] = r_tm[r]; a.tl[x] = r_tl[r]; a.tn[x] = r_tn[r]; a.em[x] = r_em[r]; a.el[x] = r_el[r];
+            a.en[x] = r_en[r]; a.st[x] = r_st[r]; a.slot[x] = r_slot[r];
+        }
+        for (uint32_t i = threadIdx.x; i < n * a.words; i += CS_T) a.bits[gbase * a.words + i] = r_bits[i];
+    }
+    if (threadIdx.x == 0) { a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = sh.U; }
 }
 
 }  // namespace ad

@@ -30,8 +30,8 @@ echo "fetch done"
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
     python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --no-e2e --no-scaling-ref > "$OUT/write.log" 2>&1
 echo "write done"
-# 4. the CPU baseline's extrapolation check: the T-thread oracle once over the full C2 batch
-timeout -k 10 600 python3 -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 --no-e2e --cpu-full > "$OUT/cpu_full.json" 2> "$OUT/cpu_full.err"
+# 4. the CPU baseline's extrapolation check: the T-thread oracle once over the full C2 batch (NO_CPU_FULL=1 skips it)
+[ -n "${NO_CPU_FULL:-}" ] || timeout -k 10 600 python3 -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 --no-e2e --cpu-full > "$OUT/cpu_full.json" 2> "$OUT/cpu_full.err"
 echo "cpu full done"
 fi
 [ "$PART" = "c2" ] && exit 0

@@ -133,12 +133,18 @@ def _bits_rows(rows, domains):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk,prune", [(0, False), (1, False), (0, True), (1, True)])
-def test_gpu_store_follows_the_harness(engine_factory, chunk, prune):
+# (1000 events: ~850 rows per key, the HBM-resident apply kernel; 240 events: <= 256 rows, the LDS-resident one)
+@pytest.mark.parametrize("chunk,prune,events", [(0, False, 1000), (1, False, 1000), (0, True, 1000), (1, True, 1000),
+                                                (0, False, 240), (0, True, 240)])
+def test_gpu_store_follows_the_harness(engine_factory, chunk, prune, events):
     seeds = (PRUNE_SEEDS if prune else SEEDS)[chunk * 10:(chunk + 1) * 10]
-    runs = [K.Run(seed, 1000, snapshot_every=25, log=True, prune=prune, snapshot_lag=prune) for seed in seeds]
+    runs = [K.Run(seed, events, snapshot_every=25 if events >= 1000 else 8, log=True, prune=prune, snapshot_lag=prune)
+            for seed in seeds]
     eng = engine_factory(window=0, replicas=1, drop_p=0.0, seed=1)
     cap = max(r.max_rows for r in runs) + 64
+    if events < 1000:
+        assert max(r.max_rows for r in runs) <= 256
+        cap = 256
     extras = 0
     eng.cfk_store_open(len(runs), cap)
     snaps = [{ev: (rows, want, full) for ev, rows, want, full in r.snapshots} for r in runs]
