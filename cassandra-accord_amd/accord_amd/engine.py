@@ -127,7 +127,7 @@ EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_
             "ad_shard_levels_gather", "ad_ephemeral_read_deps", "ad_load_batch_async", "ad_load_batch_commit",
             "ad_host_alloc", "ad_host_free", "ad_merged_sizes", "ad_fetch_merged_all", "ad_shard_kahn_begin",
             "ad_shard_kahn_outbox", "ad_shard_kahn_inbox", "ad_shard_kahn_exchange", "ad_shard_kahn_step",
-            "ad_shard_kahn_finish", "ad_shard_kahn_sent")
+            "ad_shard_kahn_finish", "ad_shard_kahn_sent", "ad_shard_kahn_run", "ad_shard_kahn_depth")
 
 
 class PinnedArena:

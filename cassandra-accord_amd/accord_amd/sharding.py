@@ -251,6 +251,8 @@ class ShardStore:
         L.ad_shard_kahn_step.argtypes = [vp, C.c_uint32]
         L.ad_shard_kahn_finish.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.ad_shard_kahn_sent.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.ad_shard_kahn_run.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.ad_shard_kahn_depth.argtypes = [vp, C.POINTER(C.c_uint32)]
         self.delta = False
         self.pairs_sent = 0
 
@@ -463,6 +465,23 @@ class ShardStore:
         self._check(self.L.ad_shard_kahn_finish(self.eng.h, C.byref(u)), "ad_shard_kahn_finish")
         return u.value
 
+    def kahn_run(self, slot=0, check_every=4, lag=2, wave_cap=1 << 16):
+        """RCCL: the whole wave loop with fixed exchange slots and no host synchronisation between waves (every
+        check_every waves an all-reduce of the READYs still queued, read lag checks later); returns the waves run.
+        Raises LevelsNotConverged past wave_cap waves (every store together)."""
+        w = C.c_uint32()
+        rc = self.L.ad_shard_kahn_run(self.eng.h, slot, check_every, lag, wave_cap, C.byref(w))
+        if rc == abi.AD_ERR_UNSUPPORTED:
+            raise LevelsNotConverged("Kahn waves still releasing after %d waves" % w.value)
+        self._check(rc, "ad_shard_kahn_run")
+        return w.value
+
+    def kahn_depth(self):
+        """After the waves: the greatest level + 1 (the levels ride in the READYs)."""
+        d = C.c_uint32()
+        self._check(self.L.ad_shard_kahn_depth(self.eng.h, C.byref(d)), "ad_shard_kahn_depth")
+        return d.value
+
     def kahn_sent(self):
         s_ = C.c_uint64()
         self._check(self.L.ad_shard_kahn_sent(self.eng.h, C.byref(s_)), "ad_shard_kahn_sent")
@@ -502,10 +521,14 @@ class GlooTransport:
 
     name = "host(gloo)"
 
-    def __init__(self, dist):
+    def __init__(self, dist, kahn_slot=None):
         self.dist = dist
         import torch
         self.torch = torch
+        # Kahn waves: at most kahn_slot READYs per destination and wave (the rest wait in a per-destination backlog,
+        # as in ad_shard_kahn_run's fixed slots; None: every queued READY each wave)
+        self.kahn_slot = kahn_slot
+        self._backlog = None
 
     def max_u64(self, x):
         t = self.torch.tensor([x], dtype=self.torch.int64)
@@ -574,9 +597,23 @@ class GlooTransport:
     def kahn_exchange(self, store):
         """One Kahn wave's exchange: every store's outbox to its destinations (all-to-all), the received READYs into the
         inbox; returns whether any store sent anything (the counts all-to-all already tells every store what it gets;
-        one all-reduce of the sent totals ends the waves on every store together)."""
+        one all-reduce of the sent totals ends the waves on every store together).  With kahn_slot, at most that many
+        READYs per destination leave per wave, the rest the next waves (levels ride in the READYs)."""
         cnt, msgs = store.kahn_outbox()
+        if self.kahn_slot is not None:
+            world = len(cnt)
+            if self._backlog is None or len(self._backlog) != world:
+                self._backlog = [np.zeros(0, np.uint64) for _ in range(world)]
+            o = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
+            send = []
+            for d in range(world):
+                q = np.concatenate([self._backlog[d], msgs[o[d]:o[d + 1]]])
+                send.append(q[:self.kahn_slot])
+                self._backlog[d] = q[self.kahn_slot:]
+            cnt = np.array([len(x) for x in send], np.uint32)
+            msgs = np.concatenate(send) if send else np.zeros(0, np.uint64)
         if not self.any(int(cnt.sum()) > 0):
+            self._backlog = None
             return False
         rcnt = self.recv_sizes(cnt.astype(np.uint64))
         recv = self.torch.zeros(int(rcnt.sum()), dtype=self.torch.int64)
@@ -648,8 +685,16 @@ class RcclTransport(GlooTransport):
             return store.levels_exchange()   # counts all-gather + pair send/recv, all over RCCL
         return store.levels_allreduce()      # the round flags ride in the same RCCL all-reduce
 
+    # Kahn waves: ad_shard_kahn_run (fixed slots, no host synchronisation between waves) unless kahn_run_loop is False
+    kahn_run_loop = True
+    kahn_slot, kahn_check_every, kahn_lag = 0, 4, 2
+
+    def kahn_run(self, store, wave_cap=None):
+        return store.kahn_run(self.kahn_slot or 0, self.kahn_check_every, self.kahn_lag,
+                              wave_cap if wave_cap is not None else 1 << 16)
+
     def kahn_exchange(self, store):
-        return store.kahn_exchange()         # counts all-gather (the wave's one host sync), grouped send/recv over RCCL
+        return store.kahn_exchange()         # counts all-gather (one host sync per wave), grouped send/recv over RCCL
 
 
 class LevelsNotConverged(RuntimeError):
@@ -721,29 +766,40 @@ def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
 
 
 def run_levels_kahn(store, transport, wave_cap=None, lap=None):
-    """Distributed Kahn waves (ad_shard_kahn_*, csrc/kahn_shard_kernels.h), one exchange per wave: the READYs of the rows
-    whose local predecessors are all released go to every holder of their txn; every holder releases (at this wave)
-    the txns all their holders reported and frees their successors, whose READYs form the next wave.  Stops at the first
-    exchange in which no store sent anything; raises LevelsNotConverged past wave_cap waves (all stores together).  Sets
-    store.depth and store.kahn_bytes (8 B per message sent to another store); returns the waves + 1 (the final, empty
-    exchange)."""
+    """Distributed Kahn waves (ad_shard_kahn_*, csrc/kahn_shard_kernels.h): the READYs of the rows whose local
+    predecessors are all released go to every holder of their txn with a level bound; every holder releases the txns all
+    their holders reported (at the greatest bound) and frees their successors, whose READYs form the next wave.  Over
+    RCCL the store runs the whole loop itself (ad_shard_kahn_run: fixed slots, no host synchronisation between waves);
+    otherwise one exchange per wave until an exchange in which no store sent anything.  Raises LevelsNotConverged past
+    wave_cap waves (all stores together).  Sets store.depth and store.kahn_bytes (8 B per message sent to another
+    store); returns the exchanges (waves + 1 for the per-wave loop: the final, empty exchange)."""
     lap = lap or (lambda name: None)
     store.kahn_begin()
     lap("levels_local")
-    level = 0
-    while transport.kahn_exchange(store):
-        store.kahn_step(level)
-        level += 1
-        if wave_cap is not None and level >= wave_cap:
+    if getattr(transport, "kahn_run_loop", False):
+        try:
+            waves = transport.kahn_run(store, wave_cap)
+        except LevelsNotConverged:
             store.kahn_finish()
-            raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
+            raise
+        exchanges = waves
+    else:
+        level = 0
+        while transport.kahn_exchange(store):
+            store.kahn_step(level)
+            level += 1
+            if wave_cap is not None and level >= wave_cap:
+                store.kahn_finish()
+                raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
+        exchanges = level + 1
     unreleased = store.kahn_finish()
     lap("levels_waves")
     if unreleased:
         raise engine.AccordDepsError(abi.AD_ERR_ARGUMENT, "Kahn waves: %d rows never released (a cycle)" % unreleased)
-    store.depth = level
+    # the batch's depth: the greatest level over every store (one all-reduce per batch)
+    store.depth = transport.max_u64(store.kahn_depth()) if hasattr(store, "kahn_depth") else exchanges - 1
     store.kahn_bytes = 8 * store.kahn_sent()
-    return level + 1
+    return exchanges
 
 
 def run_levels(store, transport, max_rounds=1 << 16, lap=None):
@@ -771,8 +827,9 @@ class LocalTransport:
     """Several stores in one process (tests): the same protocol with in-process exchange."""
 
     @staticmethod
-    def run(stores, max_rounds=1 << 16, levels="gather", deps="preaccept", gq=None, timings=None):
+    def run(stores, max_rounds=1 << 16, levels="gather", deps="preaccept", gq=None, timings=None, kahn_slot=None):
         """deps: "preaccept", "accept" (gq: the global query positions, query_positions) or "ephemeral";
+        kahn_slot: the Kahn waves' READYs per (source, destination) and wave (None: all);
         levels None: stop after the home merge.  timings (dict): seconds per phase, summed over the stores (the
         stores run one after another in this process: each phase's sum is what S GPUs would spend in parallel,
         times S)."""
@@ -805,13 +862,13 @@ class LocalTransport:
             return 0
         fell_back = False
         if levels == "kahn":
-            r = LocalTransport._kahn(stores, None)
+            r = LocalTransport._kahn(stores, None, kahn_slot)
             lap("level_waves")
             return r
         if levels == "auto":
             if all(s.delta for s in stores):
                 try:
-                    r = LocalTransport._kahn(stores, AUTO_ROUND_CAP)
+                    r = LocalTransport._kahn(stores, AUTO_ROUND_CAP, kahn_slot)
                     lap("level_waves")
                     return r
                 except LevelsNotConverged:
@@ -832,18 +889,28 @@ class LocalTransport:
         return r
 
     @staticmethod
-    def _kahn(stores, wave_cap):
-        """run_levels_kahn for stores in one process: each wave's outboxes routed to the inboxes."""
+    def _kahn(stores, wave_cap, slot=None):
+        """run_levels_kahn for stores in one process: each wave's outboxes routed to the inboxes (slot: at most that
+        many READYs per (source, destination) and wave, the rest later, as ad_shard_kahn_run's fixed slots)."""
+        W = len(stores)
+        backlog = [[np.zeros(0, np.uint64) for _ in range(W)] for _ in range(W)]
+
         def route():
-            out = [s.kahn_outbox() for s in stores]
-            if not any(int(cnt.sum()) for cnt, _ in out):
+            moved = False
+            inbox = [[] for _ in range(W)]
+            for k, s in enumerate(stores):
+                cnt, msgs = s.kahn_outbox()
+                o = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
+                for d in range(W):
+                    q = np.concatenate([backlog[k][d], msgs[o[d]:o[d + 1]]])
+                    n = len(q) if slot is None else min(slot, len(q))
+                    inbox[d].append(q[:n])
+                    backlog[k][d] = q[n:]
+                    moved |= n > 0
+            if not moved:
                 return False
             for d, s in enumerate(stores):
-                parts = []
-                for cnt, msgs in out:
-                    o = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
-                    parts.append(msgs[o[d]:o[d + 1]])
-                s.kahn_inbox(np.concatenate(parts) if parts else np.zeros(0, np.uint64))
+                s.kahn_inbox(np.concatenate(inbox[d]))
             return True
         for s in stores:
             s.kahn_begin()
@@ -858,8 +925,9 @@ class LocalTransport:
                 raise LevelsNotConverged("Kahn waves still releasing after %d waves" % level)
         if any(s.kahn_finish() for s in stores):
             raise engine.AccordDepsError(abi.AD_ERR_ARGUMENT, "Kahn waves: rows never released (a cycle)")
+        depth = max(s.kahn_depth() for s in stores)
         for s in stores:
-            s.depth = level
+            s.depth = depth
             s.kahn_bytes = 8 * s.kahn_sent()
         return level + 1
 

@@ -164,6 +164,10 @@ struct ad_handle {
     uint64_t *ks_out = nullptr, *ks_in = nullptr, *ks_xoff = nullptr;
     size_t ks_in_m = 0, ks_unreleased = 0;
     uint64_t ks_sent = 0;            // messages this batch sent to other stores
+    uint32_t *ks_lacc = nullptr, *ks_plv = nullptr;   // per row: greatest READY level bound seen, predecessors' bound
+    uint32_t* ks_head_dev = nullptr;  // per destination: READYs sent (ks_cnt_dev: appended)
+    std::vector<uint32_t> ks_head_host;
+    unsigned long long* ks_sent_dev = nullptr;         // ad_shard_kahn_run's READYs to other stores
     int ks_phase = -1;               // 0 after ad_shard_kahn_begin: the outbox holds the next wave's READYs
     bool ks_levels = false;          // lvl holds this batch's levels from the Kahn waves (ad_shard_order reads them)
     // MaxConflicts carried from earlier batches (ad_max_conflicts_carry): sorted keys + timestamps on the device
@@ -367,6 +371,7 @@ enum Slot : size_t {
     S_STG0, S_STG_END = S_STG0 + 12,
     S_KSSRC, S_KSDST, S_KSSRC2, S_KSDST2, S_KSREM, S_KSXOFF, S_KSRCNT, S_KSFL, S_KSBASE, S_KSCNT, S_KSOUT,
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
+    S_KSLACC, S_KSPLV, S_KSHEAD, S_KSSENT, S_KSSTO, S_KSSTI, S_KSPEND,   // ... READY level bounds, queues, slots
     S_CS0, S_CS_END = S_CS0 + 22,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
     S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles

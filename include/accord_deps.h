@@ -663,26 +663,33 @@ int  ad_shard_order(ad_handle* h, uint32_t* level_out /* [n_home] */, uint32_t* 
 int  ad_shard_level_edges(ad_handle* h, size_t* m, uint64_t* out);
 int  ad_shard_levels_solve(ad_handle* h, const uint64_t* edges, size_t m, uint32_t* depth);
 int  ad_shard_levels_gather(ad_handle* h, uint32_t* depth);
-/* Distributed Kahn wavefronts (the default for shallow graphs): a txn is released at wave l once every store holding
- * it has released all of its local predecessors by wave l - 1 (every constraint is local to one store, see above).
- * Per wave ONE exchange: each store sends READY(txn) to every holder of the txn (itself included) for its rows whose
- * last local predecessor was released; every holder counts them and releases the txns all holders reported, at the
- * same wave on every holder, then decrements their local successors.  A txn costs holders x holders READYs over the
- * batch (8 bytes each; the store's own by a device copy), and each store touches only its own constraint edges.
- * Replaces the CommandsForKey.notifyManaged cascade across CommandStores (local/cfk/CommandsForKey.java:1208-1289,
- * local/CommandStores.java:576-593) with the batch's waves.
- *   ad_shard_set_holders, then ad_shard_kahn_begin (the local graph + wave 0's READYs); per wave l = 0, 1, ...:
- *   exchange (the READYs; stop when no store sent anything: levels = l) -> ad_shard_kahn_step(l) (device only, no host
- *   wait); after the last wave ad_shard_kahn_finish (*unreleased: rows never released, i.e. a cycle), then
- *   ad_shard_order.  Exchange over RCCL: ad_shard_kahn_exchange (the per-destination counts all-gathered: the wave's
- *   one host synchronisation; *any_status = some store sent something; `status` is ignored); over a host transport:
- *   ad_shard_kahn_outbox (per-destination counts and messages) -> peers -> ad_shard_kahn_inbox. */
+/* Distributed Kahn wavefronts (the default for shallow graphs): a txn's level is 1 + the greatest level of its
+ * predecessors over the stores holding it (every constraint is local to one store, see above).  Each store sends
+ * READY(txn, bound) to every holder of the txn (itself included) once its last local predecessor is released, bound =
+ * 1 + the greatest level among them; every holder releases the txn when all holders' READYs are in, at the greatest
+ * bound, then decrements its local successors.  Levels ride in the READYs, so a READY may arrive a wave late.  A txn
+ * costs holders x holders READYs over the batch (8 bytes each; the store's own by a device copy), and each store
+ * touches only its own constraint edges.  Replaces the CommandsForKey.notifyManaged cascade across CommandStores
+ * (local/cfk/CommandsForKey.java:1208-1289, local/CommandStores.java:576-593) with the batch's waves.
+ *   ad_shard_set_holders, then ad_shard_kahn_begin (the local graph + wave 0's READYs); then either
+ *   - ad_shard_kahn_run (RCCL): the whole wave loop with fixed exchange slots of `slot` READYs per (source,
+ *     destination) and wave (0: from the queues' capacities, maxed over the stores), no host synchronisation between
+ *     waves: every `check_every` waves an all-reduce of the READYs still queued anywhere, read by the host `lag`
+ *     checks later; *waves = waves run; AD_ERR_UNSUPPORTED past wave_cap waves (every store together); or
+ *   - per wave: exchange (every queued READY; stop when no store sent anything) -> ad_shard_kahn_step (device only;
+ *     `level` is not used); over RCCL ad_shard_kahn_exchange (the per-destination counts all-gathered: one host
+ *     synchronisation; *any_status = some store sent something; `status` is ignored), over a host transport
+ *     ad_shard_kahn_outbox (per-destination counts and messages) -> peers -> ad_shard_kahn_inbox;
+ *   then ad_shard_kahn_finish (*unreleased: rows never released, i.e. a cycle), ad_shard_kahn_depth (the greatest
+ *   level + 1), ad_shard_order. */
 int  ad_shard_kahn_begin(ad_handle* h);
 int  ad_shard_kahn_outbox(ad_handle* h, uint32_t* counts /* [world] */, uint64_t* msgs /* or NULL: counts only */);
 int  ad_shard_kahn_inbox(ad_handle* h, const uint64_t* msgs, size_t m);
 int  ad_shard_kahn_exchange(ad_handle* h, uint32_t status, uint32_t* any_status);
 int  ad_shard_kahn_step(ad_handle* h, uint32_t level);
+int  ad_shard_kahn_run(ad_handle* h, uint32_t slot, uint32_t check_every, uint32_t lag, uint32_t wave_cap, uint32_t* waves);
 int  ad_shard_kahn_finish(ad_handle* h, uint64_t* unreleased);
+int  ad_shard_kahn_depth(ad_handle* h, uint32_t* depth);
 int  ad_shard_kahn_sent(ad_handle* h, uint64_t* sent);
 
 #ifdef __cplusplus

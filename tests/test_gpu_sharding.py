@@ -30,14 +30,17 @@ def same_txn(got, h, want, g):
     return all(np.array_equal(x, y) for x, y in zip(a, b))
 
 
-@pytest.mark.parametrize("name,shards,levels,delta", [("C2", 2, "gather", False), ("C2", 4, "gather", True),
-                                                       ("C3", 3, "gather", False), ("C2", 2, "rounds", True),
-                                                       ("C3", 3, "rounds", True), ("C3", 3, "rounds", False),
-                                                       ("C2", 4, "rounds", False), ("C2", 2, "kahn", True),
-                                                       ("C3", 3, "kahn", True), ("C2", 4, "kahn", True)])
-def test_sharded_equals_unsharded(engine_factory, name, shards, levels, delta):
+@pytest.mark.parametrize("name,shards,levels,delta,slot", [("C2", 2, "gather", False, None), ("C2", 4, "gather", True, None),
+                                                            ("C3", 3, "gather", False, None), ("C2", 2, "rounds", True, None),
+                                                            ("C3", 3, "rounds", True, None), ("C3", 3, "rounds", False, None),
+                                                            ("C2", 4, "rounds", False, None), ("C2", 2, "kahn", True, None),
+                                                            ("C3", 3, "kahn", True, None), ("C2", 4, "kahn", True, None),
+                                                            ("C2", 4, "kahn", True, 97), ("C3", 3, "kahn", True, 13)])
+def test_sharded_equals_unsharded(engine_factory, name, shards, levels, delta, slot):
     # levels="rounds" + delta: level rounds exchange only raised levels of shared txns (ad_shard_set_holders);
-    # rounds without delta: the dense all-reduce of the whole level array; "gather": one edge exchange
+    # rounds without delta: the dense all-reduce of the whole level array; "gather": one edge exchange; kahn with a
+    # slot: at most that many READYs per (source, destination) and wave, the rest in later waves (ad_shard_kahn_run's
+    # fixed slots): the levels ride in the READYs, so late ones change the wave count, never a level
     w, r, p, s = 32, 3, 0.1, 0xACC0D1
     b = workload.config(name, n=30000)
     views, merged, lv, order = unsharded(engine_factory, b, w, r, p, s)
@@ -52,10 +55,11 @@ def test_sharded_equals_unsharded(engine_factory, name, shards, levels, delta):
             st = sharding.ShardStore(0, window=w, replicas=r, drop_p=p, seed=s)
             stores.append(st)
             st.load(local, gid, hs[gid], b["n"], k, shards, holders=masks[gid] if delta else None)
-        rounds = sharding.LocalTransport.run(stores, levels=levels)
+        rounds = sharding.LocalTransport.run(stores, levels=levels, kahn_slot=slot)
         assert rounds >= 1 and (levels != "gather" or rounds == 1)
         if levels == "kahn":
-            assert rounds == int(lv.max()) + 2 and all(st.depth == lv.max() + 1 for st in stores)
+            assert all(st.depth == lv.max() + 1 for st in stores)
+            assert rounds == int(lv.max()) + 2 if slot is None else rounds > int(lv.max()) + 2
         seen = np.zeros(b["n"], bool)
         pos = {int(t): i for i, t in enumerate(order)}
         for st in stores:
@@ -224,9 +228,9 @@ def test_host_fragments_import(engine_factory):
             st.close()
 
 
-@pytest.mark.parametrize("levels,delta", [("gather", False), ("rounds", True), ("rounds", False), ("kahn", True),
-                                          ("auto", True)])
-def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta):
+@pytest.mark.parametrize("levels,delta,run_loop", [("gather", False, True), ("rounds", True, True), ("rounds", False, True),
+                                                   ("kahn", True, True), ("kahn", True, False), ("auto", True, True)])
+def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta, run_loop):
     # the RCCL transport end to end on the one GPU: a world = 1 communicator (ad_comm_init), the grouped
     # ncclSend/ncclRecv all-to-all (ad_shard_alltoall, to self) and the levels — gather: ncclAllGather of the
     # edge counts + the edge send/recv (ad_shard_levels_gather); rounds + delta: ncclAllGather of the pair counts
@@ -242,10 +246,17 @@ def test_rccl_world1_run_store(engine_factory, tmp_path, levels, delta):
         stores, _, _ = _make_stores(b, 1, w, r, p, s, 10_000_000, delta=delta)
         tr = sharding.RcclTransport(dist, stores[0], 0, 1)
         assert tr.name == "rccl"
+        tr.kahn_run_loop = run_loop
+        if run_loop and levels == "kahn":
+            tr.kahn_slot = 1024             # < the busiest wave's READYs: some arrive waves late
         rounds = sharding.run_store(stores[0], tr, levels=levels)
         assert rounds >= 1 and (levels != "gather" or rounds == 1)
-        if levels in ("kahn", "auto"):      # ad_shard_kahn_exchange: counts all-gather, self copy
-            assert rounds == int(lv.max()) + 2
+        if levels in ("kahn", "auto"):
+            assert stores[0].depth == int(lv.max()) + 1
+            if run_loop:                    # ad_shard_kahn_run: fixed slots, a pending check every 4 waves read 2 later
+                assert rounds >= int(lv.max()) + 1 and (rounds % tr.kahn_check_every == 0 or rounds == 129)
+            else:                           # ad_shard_kahn_exchange: counts all-gather, self copy, one wave per level
+                assert rounds == int(lv.max()) + 2
         seen = _check_against_unsharded(stores, views, merged, lv, order, r, b["n"])
         assert seen[np.diff(b["key_off"]) > 0].all()
         # a second communicator on the same handle is refused (no leak of the first)

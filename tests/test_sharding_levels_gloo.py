@@ -209,10 +209,11 @@ def test_holder_masks():
 
 
 class HostKahnStore:
-    """Host model of ad_shard_kahn_begin / _step / _finish (csrc/kahn_shard_kernels.h) for pure key batches of Reads and
-    Writes: the store's own constraint edges (HostEdgeStore.level_edges, the engine's levels_export_edges) over its local
-    rows; a row whose last local predecessor was released sends READY to every holder of its txn (itself included); a
-    row released once all of its txn's holders reported it, at that wave on every holder."""
+    """Host model of ad_shard_kahn_begin / _step / _finish / _depth (csrc/kahn_shard_kernels.h) for pure key batches of
+    Reads and Writes: the store's own constraint edges (HostEdgeStore.level_edges, the engine's levels_export_edges) over
+    its local rows; a row whose last local predecessor was released sends READY (with its level bound: 1 + the greatest
+    level among its local predecessors) to every holder of its txn (itself included); a row is released once all of its
+    txn's holders reported it, at the greatest bound of their READYs (whatever wave delivered them)."""
 
     delta = True
 
@@ -226,7 +227,7 @@ class HostKahnStore:
     def _ready(self, i):
         for d in range(self.world):
             if (self.holders[i] >> d) & 1:
-                self.out[d].append(int(self.gid[i]))
+                self.out[d].append(int(self.gid[i]) | (int(self.plv[i]) << 32))
 
     def kahn_begin(self):
         n = len(self.gid)
@@ -238,6 +239,8 @@ class HostKahnStore:
             self.succ[s_].append(d_)
             self.rem[d_] += 1
         self.rcnt = np.zeros(n, np.int64)
+        self.lacc = np.zeros(n, np.int64)
+        self.plv = np.zeros(n, np.int64)
         self.lvl = np.full(n, -1, np.int64)
         self.sent = 0
         self.out = {d: [] for d in range(self.world)}
@@ -248,21 +251,25 @@ class HostKahnStore:
         cnt = np.array([len(self.out[d]) for d in range(self.world)], np.uint32)
         self.sent += int(cnt.sum()) - int(cnt[self.rank])
         msgs = np.array([g for d in range(self.world) for g in self.out[d]], np.uint64)
+        self.out = {d: [] for d in range(self.world)}
         return cnt, msgs
 
     def kahn_inbox(self, msgs):
         self.inbox = [int(g) for g in msgs]
 
     def kahn_step(self, level):
-        self.out = {d: [] for d in range(self.world)}
-        for g in self.inbox:
+        for m in self.inbox:
+            g, lb = m & 0xFFFFFFFF, m >> 32
             r = self.row[g]
             assert self.lvl[r] < 0, "no READY for a released txn"
+            self.lacc[r] = max(self.lacc[r], lb)
             self.rcnt[r] += 1
             if self.rcnt[r] == bin(int(self.holders[r])).count("1"):
-                self.lvl[r] = level
-                self.G[g] = level
+                L = int(self.lacc[r])
+                self.lvl[r] = L
+                self.G[g] = L
                 for s_ in self.succ[r]:
+                    self.plv[s_] = max(self.plv[s_], L + 1)
                     self.rem[s_] -= 1
                     if self.rem[s_] == 0:
                         self._ready(s_)
@@ -270,6 +277,9 @@ class HostKahnStore:
 
     def kahn_finish(self):
         return int((self.lvl < 0).sum())
+
+    def kahn_depth(self):
+        return int(self.lvl.max()) + 1 if len(self.lvl) else 0
 
     def kahn_sent(self):
         return self.sent
@@ -287,7 +297,7 @@ class HostAutoStore(HostKahnStore):
         return depth
 
 
-def _kahn_worker(rank, world, port, n, dist_kind):
+def _kahn_worker(rank, world, port, n, dist_kind, slot=None):
     sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -305,10 +315,12 @@ def _kahn_worker(rank, world, port, n, dist_kind):
         hs = sharding.home_stores(b, bounds)
         local, gid, _ = sharding.slice_for_shard(b, bounds[rank], bounds[rank + 1])
         store = HostKahnStore(local, gid, masks[gid], hs[gid], n, rank, world, b)
-        waves = sharding.run_levels_kahn(store, sharding.GlooTransport(dist))
+        waves = sharding.run_levels_kahn(store, sharding.GlooTransport(dist, kahn_slot=slot))
         want, _ = O.OracleResult(b, abi.make_config(32, 1, 0.0, 1), O.FLAG_MERGE | O.FLAG_LEVELS).levels()
         assert np.array_equal(store.lvl.astype(np.uint32), want[gid]), "rank %d: levels differ" % rank
-        assert store.depth == int(want.max()) + 1 and waves == store.depth + 1
+        assert store.depth == int(want.max()) + 1
+        # every queued READY each wave: one wave per level; bounded slots: READYs arrive late, the levels do not move
+        assert waves == store.depth + 1 if slot is None else waves > store.depth + 1
         # per local row exactly one READY to each other holder crosses the wire over the batch (never per round)
         others = ((masks[gid].astype(np.int64) & ~(1 << rank)) != 0).sum()
         bound = torch.tensor([store.kahn_sent(), int(sum(bin(int(m)).count("1") - 1 for m in masks[gid]))],
@@ -323,6 +335,13 @@ def test_kahn_level_waves_over_gloo():
     # uniform keys (C5-like, shallow) and Zipf hot keys (deep chains crossing both stores)
     mp.spawn(_kahn_worker, args=(2, _free_port(), 3000, "uniform"), nprocs=2, join=True)
     mp.spawn(_kahn_worker, args=(2, _free_port(), 2000, "zipf"), nprocs=2, join=True)
+
+
+def test_kahn_level_waves_bounded_slots_over_gloo():
+    # at most a few READYs per (source, destination) and wave (ad_shard_kahn_run's fixed slots): late READYs, exact
+    # levels; three ranks too
+    mp.spawn(_kahn_worker, args=(2, _free_port(), 3000, "uniform", 5), nprocs=2, join=True)
+    mp.spawn(_kahn_worker, args=(3, _free_port(), 2000, "zipf", 3), nprocs=3, join=True)
 
 
 def _auto_worker(rank, world, port, n, dist_kind, cap):
