@@ -559,9 +559,9 @@ def main_sharded(args, rank, world, local, dist):
     dt = float(t.item())
     roof = roofline_of(store.eng, dom, n_loc, P_loc, store.eng.last_times(), pmc=False)
     store.eng.set_trace(0)
-    protocol = ("distributed Kahn waves (each store walks only its own constraint edges; per txn one READY and one "
-                "RELEASE message per holder)" if rounds <= sharding.AUTO_ROUND_CAP
-                else "one exchange of every store's constraint edges")
+    protocol = ("distributed Kahn waves (each store walks only its own constraint edges; per txn one READY per holder "
+                "pair carrying its level bound; over RCCL fixed-slot waves with no host synchronisation between them)"
+                if getattr(store, "levels_via", "") == "kahn" else "one exchange of every store's constraint edges")
     out = {
         "metric": "txn deps+exec-order resolved/sec (1M-txn batch) + % HBM roofline, 1/2/4/8 GPU",
         "value": n_total * args.steps / dt, "unit": "txn/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

@@ -739,6 +739,7 @@ def run_store(store, transport, max_rounds=1 << 16, timings=None, levels="auto",
         levels = "gather"
     if levels == "gather":
         store.depth = transport.gather_levels(store)
+        store.levels_via = "gather"
         lap("levels")
         return 1
     if levels == "kahn":
@@ -755,12 +756,14 @@ def run_levels_auto(store, transport, round_cap=AUTO_ROUND_CAP, lap=None):
     # straight to the gather instead of spending round_cap waves to find out again
     if transport.any(getattr(store, "depth", 0) > round_cap):
         store.depth = transport.gather_levels(store)
+        store.levels_via = "gather"
         lap("levels_gather")
         return round_cap + 1
     try:
         return run_levels_kahn(store, transport, round_cap, lap)
     except LevelsNotConverged:
         store.depth = transport.gather_levels(store)
+        store.levels_via = "gather"
         lap("levels_gather")
         return round_cap + 1
 
@@ -778,7 +781,8 @@ def run_levels_kahn(store, transport, wave_cap=None, lap=None):
     lap("levels_local")
     if getattr(transport, "kahn_run_loop", False):
         try:
-            waves = transport.kahn_run(store, wave_cap)
+            # (a bounded slot spreads a wide level over several waves: the cap on waves is 4x the cap on levels)
+            waves = transport.kahn_run(store, None if wave_cap is None else 4 * wave_cap)
         except LevelsNotConverged:
             store.kahn_finish()
             raise
@@ -799,6 +803,7 @@ def run_levels_kahn(store, transport, wave_cap=None, lap=None):
     # the batch's depth: the greatest level over every store (one all-reduce per batch)
     store.depth = transport.max_u64(store.kahn_depth()) if hasattr(store, "kahn_depth") else exchanges - 1
     store.kahn_bytes = 8 * store.kahn_sent()
+    store.levels_via = "kahn"
     return exchanges
 
 
