@@ -93,6 +93,11 @@ static __global__ __launch_bounds__(256) void k_query_pos(size_t n, const uint64
     if (__ballot(bad) && __lane_id() == 0) atomicOr(&prm->err, (unsigned)ERR_EXECBELOW);
 }
 
+// AD_OVF_MAIN=1: the overflowed rows run on the main stream after the finish (an A/B switch)
+static bool ovf_on_main() {
+    const char* e = getenv("AD_OVF_MAIN");
+    return e && e[0] == '1';
+}
 int side_fork(ad_handle* h) {
     if (!h->xst) {
         HIPCHK(h, hipStreamCreateWithFlags(&h->xst, hipStreamNonBlocking));
@@ -406,10 +411,16 @@ static int stage_deps_impl(ad_handle* h) {
         ta.w = wa;
         ta.spec_bad = spec_bad;
         // the overflowed rows (listed by the offsets scan) on the side stream, beside the finish
-        CK(side_fork(h));
-        launch_finish_ovf_nv(nv, ta, direct, h->xst);
-        KScope ks(K_TXN_LAYOUT, n);
-        launch_finish_nv(nv, ta, direct, st);
+        const bool ovf_main = ovf_on_main();
+        if (!ovf_main) {
+            CK(side_fork(h));
+            launch_finish_ovf_nv(nv, ta, direct, h->xst);
+        }
+        {
+            KScope ks(K_TXN_LAYOUT, n);
+            launch_finish_nv(nv, ta, direct, st);
+        }
+        if (ovf_main) launch_finish_ovf_nv(nv, ta, direct, st);
         ta.spec_bad = nullptr;
     }
     CK(wait_totals(h, seq, tt.count, got.data()));
@@ -469,10 +480,16 @@ static int stage_deps_impl(ad_handle* h) {
     ta.w = wa;
     if (n > 0 && !spec_ok) {
         side_join(h);                                    // a speculative side launch exited on the guard
-        CK(side_fork(h));
-        launch_finish_ovf_nv(nv, ta, direct, h->xst);
-        KScope ks(K_TXN_LAYOUT, n);
-        launch_finish_nv(nv, ta, direct, st);
+        const bool ovf_main = ovf_on_main();
+        if (!ovf_main) {
+            CK(side_fork(h));
+            launch_finish_ovf_nv(nv, ta, direct, h->xst);
+        }
+        {
+            KScope ks(K_TXN_LAYOUT, n);
+            launch_finish_nv(nv, ta, direct, st);
+        }
+        if (ovf_main) launch_finish_ovf_nv(nv, ta, direct, st);
     }
     if (n > 0 && h->V > 0) { KScope ks(K_VITEMS); launch_large_layout_nv(nv, ta, direct, st); }
     wa.items = items; wa.nitems = nitems;

@@ -64,11 +64,13 @@ void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32
     NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy, dtx, dtx_count, ovf_rows, ovf_count);
 }
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_finish, ta, direct, st); }
-// The overflowed rows (a device-side count: rare, so a small grid; each row is a chain of dependent loads — ~27 us
-// of latency for a handful of rows on C2 — which is why it runs on the side stream)
+// The overflowed rows (a device-side count; each row is a chain of dependent loads — ~27 us of latency for a handful
+// of rows on C2 — which is why it runs on the side stream).  Up to 4096 workgroups: C3's hot keys overflow ~10^5 rows,
+// which 256 workgroups walked ~6 rows per thread in series (1.6-2.0 ms, on the merge's critical path since the merge
+// reads the replies); workgroups past the count exit at once.
 template <int NV>
 void launch_finish_ovf(const TxnArgs& ta, bool direct, hipStream_t st) {
-    const unsigned g = (unsigned)std::min<long>(ceil_div((long)ta.nrows * (direct ? 2 * NV : NV), 256), 256);
+    const unsigned g = (unsigned)std::min<long>(ceil_div((long)ta.nrows * (direct ? 2 * NV : NV), 256), 4096);
     if (direct) k_txn_finish_ovf<NV, true><<<g, 256, 0, st>>>(ta);
     else k_txn_finish_ovf<NV, false><<<g, 256, 0, st>>>(ta);
 }
