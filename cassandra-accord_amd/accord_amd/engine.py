@@ -67,6 +67,8 @@ def lib():
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
         L.ad_cfk_notify.argtypes = [vp, C.POINTER(abi.AdCfkState), C.POINTER(C.c_uint8)]
         L.ad_cfk_store_open.argtypes = [vp, C.c_uint32, C.c_uint32]
+        L.ad_cfk_store_open_tiered.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.ad_cfk_store_notify_key.argtypes = [vp, C.c_uint32, vp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.ad_cfk_store_apply.argtypes = [vp, C.POINTER(abi.AdCfkEvents)]
         L.ad_cfk_store_notify.argtypes = [vp, vp, vp]
         L.ad_cfk_store_fetch.argtypes = [vp, C.c_uint32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)] + [vp] * 9
@@ -116,7 +118,7 @@ def lib():
 EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_device_count", "ad_load_batch", "ad_preaccept_deps", "ad_accept_deps",
             "ad_max_conflicts_carry", "ad_max_conflicts_ts", "ad_max_conflicts_export", "ad_max_conflicts_carry_ranges",
             "ad_max_conflicts_export_ranges", "ad_merge_deps_fast",
-            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_cfk_store_query", "ad_cfk_store_query_fetch", "ad_cfk_store_unmanaged", "ad_cfk_store_notified", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
+            "ad_fetch_deps", "ad_fetch_rows", "ad_fetch_inverse", "ad_preaccept_expiry", "ad_cfk_notify", "ad_cfk_store_open", "ad_cfk_store_open_tiered", "ad_cfk_store_notify_key", "ad_cfk_store_apply", "ad_cfk_store_notify", "ad_cfk_store_fetch", "ad_cfk_store_pruning", "ad_cfk_store_query", "ad_cfk_store_query_fetch", "ad_cfk_store_unmanaged", "ad_cfk_store_notified", "ad_merge_deps", "ad_fetch_merged", "ad_merge_host", "ad_exec_levels", "ad_max_conflicts",
             "ad_run_pipeline", "ad_fetch_levels", "ad_last_times", "ad_set_level_mode", "ad_set_pipeline_union", "ad_set_trace", "ad_kernel_count", "ad_kernel_name", "ad_kernel_stats", "ad_kernel_units",
             "ad_reset_kernel_stats", "ad_shard_bounds", "ad_shard_setup", "ad_shard_export", "ad_shard_send_to_host",
             "ad_shard_import_host", "ad_comm_unique_id", "ad_comm_init", "ad_comm_destroy", "ad_shard_query_positions", "ad_shard_alltoall", "ad_shard_merge",
@@ -315,10 +317,25 @@ class DepsEngine:
         return out[:s.rows]
 
     # ---- device-resident CommandsForKey states (ad_cfk_store_*) -------------------------------------------------
-    def cfk_store_open(self, keys, capacity):
-        """K resident CFKs of up to `capacity` rows each (rounded up to a multiple of 64, at most 8192)."""
-        self._check(lib().ad_cfk_store_open(self.h, keys, capacity), "ad_cfk_store_open")
+    def cfk_store_open(self, keys, capacity, big_capacity=0, big_keys=0):
+        """K resident CFKs of up to `capacity` rows each (rounded up to a multiple of 64, at most 8192); with big_keys,
+        a key outgrowing them moves to one of big_keys large-tier slots of big_capacity rows (<= 16384) in the call."""
+        if big_keys:
+            self._check(lib().ad_cfk_store_open_tiered(self.h, keys, capacity, big_capacity, big_keys),
+                        "ad_cfk_store_open_tiered")
+        else:
+            self._check(lib().ad_cfk_store_open(self.h, keys, capacity), "ad_cfk_store_open")
         self._cs_keys, self._cs_cap = keys, capacity          # not_waiting rows at the caller's capacity
+
+    def cfk_store_notify_key(self, key):
+        """After cfk_store_notify: one key's not_waiting flags over all of its rows (a large-tier key's beyond the
+        bulk output's capacity too)."""
+        n = C.c_size_t()
+        self._check(lib().ad_cfk_store_notify_key(self.h, key, None, 0, C.byref(n)), "ad_cfk_store_notify_key")
+        out = np.zeros(max(n.value, 1), np.uint8)
+        self._check(lib().ad_cfk_store_notify_key(self.h, key, out.ctypes.data, out.size, C.byref(n)),
+                    "ad_cfk_store_notify_key")
+        return out[:n.value]
 
     def cfk_store_apply(self, events):
         """CommandsForKey.update events (a dict of abi.CFK_EVENT_FIELDS arrays, grouped by key through ev_off)."""

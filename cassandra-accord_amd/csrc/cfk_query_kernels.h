@@ -66,7 +66,7 @@ __device__ inline CsqItem csq_setup(const CfkQueryArgs& a, uint32_t it) {
     const CfkStoreArgs& s = a.s;
     const uint32_t q = a.iq[it], key = a.qkey[it];
     CsqItem c;
-    c.base = (size_t)key * s.cap;
+    c.base = cs_tier(key, s.K, s.cap, s.words, s.kslot, s.capB, s.wordsB).rbase;
     c.n = s.cnt[key];
     const Ts3 B{a.qbm[q], a.qbl[q], a.qbn[q]};
     c.x = Ts3{a.qtm[q], a.qtl[q], a.qtn[q]};

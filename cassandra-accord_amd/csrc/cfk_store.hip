@@ -12,30 +12,50 @@ static int host_ts_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64
 }
 
 int ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity) {
+    return ad_cfk_store_open_tiered(h, keys, capacity, 0, 0);
+}
+
+int ad_cfk_store_open_tiered(ad_handle* h, uint32_t keys, uint32_t capacity, uint32_t big_capacity, uint32_t big_keys) {
     if (!h) return AD_ERR_ARGUMENT;
-    if (keys == 0 || capacity == 0 || capacity > 64 * NF_MAX_WORDS)
+    if (keys == 0 || capacity == 0 || capacity > 8192)
         return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_open: keys >= 1 and 1 <= capacity <= 8192");
+    if (big_keys && (big_capacity <= capacity || big_capacity > 64 * NF_MAX_WORDS || big_keys > keys))
+        return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_open_tiered: capacity < big_capacity <= 16384 and big_keys <= keys");
     hipSetDevice(h->device);
     auto& c = h->cs;
     c.K = keys;
     c.ucap = capacity;
     c.cap = (capacity + 63) & ~63u;
     c.words = c.cap / 64;
-    const size_t rows = (size_t)c.K * c.cap;
+    c.nbig = big_keys;
+    c.ucapB = big_keys ? big_capacity : 0;
+    c.capB = big_keys ? (big_capacity + 63) & ~63u : 0;
+    c.wordsB = c.capB / 64;
+    c.kslot_host.assign(big_keys ? keys : 0, ~0u);
+    c.big_keys.clear();
+    // regular tier: keys x cap rows; large tier after it: nbig x capB rows (bitmaps: a row of the tier's words per slot)
+    const size_t rows = (size_t)c.K * c.cap + (size_t)c.nbig * c.capB;
+    const size_t bw = (size_t)c.K * c.cap * c.words + (size_t)c.nbig * c.capB * c.wordsB;
     CK(dalloc(h, S_CS0 + 0, &c.cnt, c.K)); CK(dalloc(h, S_CS0 + 1, &c.tm, rows)); CK(dalloc(h, S_CS0 + 2, &c.tl, rows));
     CK(dalloc(h, S_CS0 + 3, &c.tn, rows)); CK(dalloc(h, S_CS0 + 4, &c.em, rows)); CK(dalloc(h, S_CS0 + 5, &c.el, rows));
     CK(dalloc(h, S_CS0 + 6, &c.en, rows)); CK(dalloc(h, S_CS0 + 7, &c.st, rows)); CK(dalloc(h, S_CS0 + 8, &c.slot, rows));
-    CK(dalloc(h, S_CS0 + 9, &c.bits, rows * c.words)); CK(dalloc(h, S_CS0 + 10, &c.out, rows));
+    CK(dalloc(h, S_CS0 + 9, &c.bits, bw)); CK(dalloc(h, S_CS0 + 10, &c.out, rows));
     CK(dalloc(h, S_CS0 + 11, &c.pre, 2 * rows)); CK(dalloc(h, S_CS0 + 12, &c.flags, 4));
     CK(dalloc(h, S_CS0 + 13, &c.pbm, c.K)); CK(dalloc(h, S_CS0 + 14, &c.pbl, c.K)); CK(dalloc(h, S_CS0 + 15, &c.pbn, c.K));
     CK(dalloc(h, S_CS0 + 16, &c.lp_cnt, c.K)); CK(dalloc(h, S_CS0 + 17, &c.lpm, rows));
     CK(dalloc(h, S_CS0 + 18, &c.lpl, rows)); CK(dalloc(h, S_CS0 + 19, &c.lpn, rows));
-    CK(dalloc(h, S_CS0 + 20, &c.lp_bits, rows * c.words));
+    CK(dalloc(h, S_CS0 + 20, &c.lp_bits, bw));
     CK(dalloc(h, S_CSU0 + 0, &c.lp_xm, rows)); CK(dalloc(h, S_CSU0 + 1, &c.lp_xl, rows)); CK(dalloc(h, S_CSU0 + 2, &c.lp_xn, rows));
     CK(dalloc(h, S_CSU0 + 3, &c.lp_xh, rows)); CK(dalloc(h, S_CSU0 + 4, &c.um_cnt, c.K)); CK(dalloc(h, S_CSU0 + 5, &c.um_p, rows));
     CK(dalloc(h, S_CSU0 + 6, &c.um_wm, rows)); CK(dalloc(h, S_CSU0 + 7, &c.um_wl, rows)); CK(dalloc(h, S_CSU0 + 8, &c.um_wn, rows));
     CK(dalloc(h, S_CSU0 + 9, &c.um_tm, rows)); CK(dalloc(h, S_CSU0 + 10, &c.um_tl, rows)); CK(dalloc(h, S_CSU0 + 11, &c.um_tn, rows));
     CK(dalloc(h, S_CSU0 + 12, &c.nt_cnt, c.K));
+    c.kslot = c.kres = nullptr;
+    if (c.nbig) {
+        CK(dalloc(h, S_CSKSLOT, &c.kslot, c.K)); CK(dalloc(h, S_CSKRES, &c.kres, c.K));
+        HIPCHK(h, hipMemsetAsync(c.kslot, 0xFF, (size_t)c.K * 4, h->st));
+        HIPCHK(h, hipMemsetAsync(c.kres, 0xFF, (size_t)c.K * 4, h->st));
+    }
     HIPCHK(h, hipMemsetAsync(c.um_cnt, 0, (size_t)c.K * 4, h->st));
     HIPCHK(h, hipMemsetAsync(c.nt_cnt, 0, (size_t)c.K * 4, h->st));
     c.nt_total = 0;
@@ -47,6 +67,12 @@ int ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity) {
     HIPCHK(h, hipMemsetAsync(c.flags, 0, 16, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return AD_OK;
+}
+
+// the store's tier fields of a kernel's args
+static void cs_tier_args(const ad_handle::CfkStore& c, CfkStoreArgs& a) {
+    a.K = c.K; a.cap = c.cap; a.words = c.words;
+    a.kslot = c.kslot; a.capB = c.capB; a.wordsB = c.wordsB; a.nbig = c.nbig;
 }
 
 int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
@@ -123,7 +149,8 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
         HIPCHK(h, hipMemcpyAsync(dtn, ev->deps_node, nd * 4, hipMemcpyHostToDevice, st));
     }
     CfkStoreArgs a{};
-    a.K = c.K; a.cap = c.cap; a.words = c.words; a.cnt = c.cnt;
+    cs_tier_args(c, a);
+    a.cnt = c.cnt;
     a.tm = c.tm; a.tl = c.tl; a.tn = c.tn; a.em = c.em; a.el = c.el; a.en = c.en; a.st = c.st; a.slot = c.slot; a.bits = c.bits;
     a.ev_off = eo; a.etm = etm; a.etl = etl; a.etn = etn; a.est = est; a.eem = eem; a.eel = eel; a.een = een;
     a.dep_off = doff; a.dtm = dtm; a.dtl = dtl; a.dtn = dtn;
@@ -136,7 +163,7 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     // notifications: per key a region of (its events + the registry's capacity) entries
     {
         std::vector<uint32_t> nb(c.K + 1, 0);
-        for (uint32_t k = 0; k < c.K; ++k) nb[k + 1] = nb[k] + (ev->ev_off[k + 1] - ev->ev_off[k]) + c.cap;
+        for (uint32_t k = 0; k < c.K; ++k) nb[k + 1] = nb[k] + (ev->ev_off[k + 1] - ev->ev_off[k]) + std::max(c.cap, c.capB);
         c.nt_base_host = nb;
         const size_t tot = std::max<size_t>(nb[c.K], 1);
         CK(dalloc(h, S_CSU0 + 13, &c.nt_base, c.K + 1)); CK(dalloc(h, S_CSU0 + 14, &c.nt_ev, tot));
@@ -157,9 +184,73 @@ int ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev) {
     a.dbg = dbg;
     // rows in LDS while the key's events apply when they fit (AD_CFK_STORE_HBM=1: the HBM-resident kernel, for tests)
     const char* hbm = getenv("AD_CFK_STORE_HBM");
-    if (c.cap <= CS_LDS_CAP && !(hbm && hbm[0] == '1')) k_cfk_apply<true><<<c.K, CS_T, 0, st>>>(a);
-    else k_cfk_apply<false><<<c.K, CS_T, 0, st>>>(a);
+    const bool lds_ok = !(hbm && hbm[0] == '1');
+    a.kres = c.kres;
+    // one pass over the keys (klist: nullptr) or over a list of them; the large-tier keys that do not fit LDS take the
+    // HBM kernel
+    auto launch = [&](const uint32_t* klist, uint32_t nk, const uint32_t* big_list, uint32_t nbl) {
+        CfkStoreArgs x = a;
+        x.klist = klist;
+        if (lds_ok && c.cap <= CS_LDS_CAP) {
+            k_cfk_apply<true><<<nk, CS_T, 0, st>>>(x);
+            if (nbl && c.capB > CS_LDS_CAP) {
+                x.klist = big_list;
+                k_cfk_apply<false><<<nbl, CS_T, 0, st>>>(x);
+            }
+        } else {
+            k_cfk_apply<false><<<nk, CS_T, 0, st>>>(x);
+        }
+    };
+    uint32_t* bl = nullptr;
+    if (!c.big_keys.empty()) {
+        CK(dalloc(h, S_CSKLIST, &bl, c.big_keys.size()));
+        HIPCHK(h, hipMemcpyAsync(bl, c.big_keys.data(), c.big_keys.size() * 4, hipMemcpyHostToDevice, st));
+    }
+    launch(nullptr, c.K, bl, (uint32_t)c.big_keys.size());
     HIPCHK(h, hipGetLastError());
+    // keys that ran out of rows stopped before the event (kres): they move to the large tier and resume from it
+    for (int round = 0; c.nbig && round < 2; ++round) {
+        uint32_t f0 = 0;
+        HIPCHK(h, hipMemcpyAsync(&f0, c.flags, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        if (!f0) break;
+        std::vector<uint32_t> kres(c.K);
+        HIPCHK(h, hipMemcpy(kres.data(), c.kres, (size_t)c.K * 4, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> moved, slots, resumed;
+        for (uint32_t k = 0; k < c.K; ++k) {
+            if (kres[k] == ~0u) continue;
+            if (c.kslot_host[k] != ~0u || c.big_keys.size() >= c.nbig) {
+                HIPCHK(h, hipMemsetAsync(c.kres, 0xFF, (size_t)c.K * 4, st));
+                HIPCHK(h, hipStreamSynchronize(st));
+                return set_err(h, AD_ERR_UNSUPPORTED, "ad_cfk_store_apply: a key outgrew the store's large tier (rows or "
+                                                      "loadingPruned entries, or no large-tier slot left); the key keeps "
+                                                      "its state up to the event before");
+            }
+            c.kslot_host[k] = (uint32_t)c.big_keys.size();
+            slots.push_back(c.kslot_host[k]);
+            c.big_keys.push_back(k);
+            moved.push_back(k);
+        }
+        const uint32_t nm = (uint32_t)moved.size();
+        uint32_t *ml = nullptr, *ms = nullptr;
+        CK(dalloc(h, S_CSKLIST, &ml, std::max<size_t>(c.big_keys.size(), nm)));
+        CK(dalloc(h, S_CSKNEW, &ms, nm));
+        HIPCHK(h, hipMemcpyAsync(ml, moved.data(), nm * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(ms, slots.data(), nm * 4, hipMemcpyHostToDevice, st));
+        CfkStoreArgs pa = a;
+        pa.klist = ml;
+        k_cfk_promote<<<nm, 256, 0, st>>>(pa, ms);
+        // resume: each moved key from the event it stopped at (the others skip: ev_start ~0u)
+        uint32_t* ks = nullptr;
+        CK(dalloc(h, S_CSKSTART, &ks, c.K));
+        HIPCHK(h, hipMemcpyAsync(ks, c.kres, (size_t)c.K * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(h, hipMemsetAsync(c.kres, 0xFF, (size_t)c.K * 4, st));
+        HIPCHK(h, hipMemsetAsync(c.flags, 0, 4, st));
+        a.ev_start = ks;
+        launch(ml, nm, ml, nm);
+        a.ev_start = nullptr;
+        HIPCHK(h, hipGetLastError());
+    }
     uint32_t f[2] = {0, 0};
     HIPCHK(h, hipMemcpyAsync(f, c.flags, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
@@ -189,6 +280,7 @@ int ad_cfk_store_notify(ad_handle* h, uint32_t* rows, uint8_t* not_waiting) {
     HIPCHK(h, hipMemsetAsync(c.flags + 2, 0, 8, st));
     NotifyArgs a{};
     a.K = c.K; a.row_off = nullptr; a.cnt = c.cnt; a.cap = c.cap; a.words = c.words; a.slot = c.slot; a.bits = c.bits;
+    a.kslot = c.kslot; a.capB = c.capB; a.wordsB = c.wordsB;
     a.tm = c.tm; a.tl = c.tl; a.tn = c.tn; a.em = c.em; a.el = c.el; a.en = c.en; a.st = c.st;
     a.pre = c.pre; a.out = c.out; a.bad_order = c.flags + 2; a.bad_miss = c.flags + 3;
     a.lp_cnt = c.lp_cnt; a.lpm = c.lpm; a.lpl = c.lpl; a.lpn = c.lpn; a.lp_bits = c.lp_bits;
@@ -197,7 +289,12 @@ int ad_cfk_store_notify(ad_handle* h, uint32_t* rows, uint8_t* not_waiting) {
     if (rows) HIPCHK(h, hipMemcpyAsync(rows, c.cnt, (size_t)c.K * 4, hipMemcpyDeviceToHost, st));
     // not_waiting is [keys * capacity] at the caller's (unrounded) capacity: a 2D copy out of the 64-row-aligned rows
     if (not_waiting)
+    {
         HIPCHK(h, hipMemcpy2DAsync(not_waiting, c.ucap, c.out, c.cap, c.ucap, c.K, hipMemcpyDeviceToHost, st));
+        // large-tier keys: their first `capacity` rows (ad_cfk_store_notify_key has them all)
+        for (uint32_t k : c.big_keys)
+            HIPCHK(h, hipMemcpyAsync(not_waiting + (size_t)k * c.ucap, c.out + c.rbase(k), c.ucap, hipMemcpyDeviceToHost, st));
+    }
     uint32_t f[2] = {0, 0};
     HIPCHK(h, hipMemcpyAsync(f, c.flags + 2, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
@@ -217,12 +314,13 @@ int ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missing
     uint32_t n = 0;
     HIPCHK(h, hipMemcpyAsync(&n, c.cnt + key, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
-    const size_t base = (size_t)key * c.cap;
+    const size_t base = c.rbase(key);
+    const uint32_t words = c.words_of(key);
     std::vector<uint32_t> slot(n);
-    std::vector<uint64_t> bits((size_t)n * c.words);
+    std::vector<uint64_t> bits((size_t)n * words);
     if (n) {
         HIPCHK(h, hipMemcpyAsync(slot.data(), c.slot + base, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipMemcpyAsync(bits.data(), c.bits + base * c.words, (size_t)n * c.words * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(bits.data(), c.bits + c.bbase(key), (size_t)n * words * 8, hipMemcpyDeviceToHost, st));
         if (txn_msb) HIPCHK(h, hipMemcpyAsync(txn_msb, c.tm + base, (size_t)n * 8, hipMemcpyDeviceToHost, st));
         if (txn_lsb) HIPCHK(h, hipMemcpyAsync(txn_lsb, c.tl + base, (size_t)n * 8, hipMemcpyDeviceToHost, st));
         if (txn_node) HIPCHK(h, hipMemcpyAsync(txn_node, c.tn + base, (size_t)n * 4, hipMemcpyDeviceToHost, st));
@@ -242,8 +340,8 @@ int ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missing
     std::vector<uint32_t> tmp;
     for (uint32_t r = 0; r < n; ++r) {
         tmp.clear();
-        const uint64_t* b = bits.data() + (size_t)slot[r] * c.words;
-        for (uint32_t w = 0; w < c.words; ++w)
+        const uint64_t* b = bits.data() + (size_t)slot[r] * words;
+        for (uint32_t w = 0; w < words; ++w)
             for (uint64_t x = b[w]; x; x &= x - 1) {
                 const uint32_t s = w * 64 + (uint32_t)__builtin_ctzll(x);
                 if (s >= n) return set_err(h, AD_ERR_DEVICE, "ad_cfk_store_fetch: a missing bit beyond the rows");
@@ -281,18 +379,19 @@ int ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint6
     if (pruned_msb) *pruned_msb = pm;
     if (pruned_lsb) *pruned_lsb = pl;
     if (pruned_node) *pruned_node = pn;
-    const size_t base = (size_t)key * c.cap;
+    const size_t base = c.rbase(key);
+    const uint32_t words = c.words_of(key);
     std::vector<uint32_t> slot(n);
-    std::vector<uint64_t> bits((size_t)L * c.words);
+    std::vector<uint64_t> bits((size_t)L * words);
     if (n) HIPCHK(h, hipMemcpyAsync(slot.data(), c.slot + base, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     if (L) {
-        HIPCHK(h, hipMemcpyAsync(bits.data(), c.lp_bits + base * c.words, (size_t)L * c.words * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(bits.data(), c.lp_bits + c.bbase(key), (size_t)L * words * 8, hipMemcpyDeviceToHost, st));
         if (lp_msb) HIPCHK(h, hipMemcpyAsync(lp_msb, c.lpm + base, (size_t)L * 8, hipMemcpyDeviceToHost, st));
         if (lp_lsb) HIPCHK(h, hipMemcpyAsync(lp_lsb, c.lpl + base, (size_t)L * 8, hipMemcpyDeviceToHost, st));
         if (lp_node) HIPCHK(h, hipMemcpyAsync(lp_node, c.lpn + base, (size_t)L * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(h, hipStreamSynchronize(st));
-    std::vector<uint32_t> row_of(c.cap, 0xFFFFFFFFu);
+    std::vector<uint32_t> row_of(c.rows_cap(key), 0xFFFFFFFFu);
     for (uint32_t r = 0; r < n; ++r) {
         if (slot[r] >= n) return set_err(h, AD_ERR_DEVICE, "ad_cfk_store_pruning: slot out of range");
         row_of[slot[r]] = r;
@@ -301,8 +400,8 @@ int ad_cfk_store_pruning(ad_handle* h, uint32_t key, uint64_t* pruned_msb, uint6
     std::vector<uint32_t> tmp;
     for (uint32_t j = 0; j < L; ++j) {
         tmp.clear();
-        const uint64_t* b = bits.data() + (size_t)j * c.words;
-        for (uint32_t w = 0; w < c.words; ++w)
+        const uint64_t* b = bits.data() + (size_t)j * words;
+        for (uint32_t w = 0; w < words; ++w)
             for (uint64_t x = b[w]; x; x &= x - 1) {
                 const uint32_t s = w * 64 + (uint32_t)__builtin_ctzll(x);
                 if (s >= n) return set_err(h, AD_ERR_DEVICE, "ad_cfk_store_pruning: a witness bit beyond the rows");
@@ -346,7 +445,8 @@ int ad_cfk_store_query(ad_handle* h, const ad_cfk_queries* q, ad_csr_sizes* size
     r.nq = nq; r.items = items;
     const size_t nq1 = std::max<size_t>(nq, 1), it1 = std::max<size_t>(items, 1);
     CfkQueryArgs a{};
-    a.s.K = c.K; a.s.cap = c.cap; a.s.words = c.words; a.s.cnt = c.cnt;
+    cs_tier_args(c, a.s);
+    a.s.cnt = c.cnt;
     a.s.tm = c.tm; a.s.tl = c.tl; a.s.tn = c.tn; a.s.em = c.em; a.s.el = c.el; a.s.en = c.en; a.s.st = c.st;
     a.s.pbm = c.pbm; a.s.pbl = c.pbl; a.s.pbn = c.pbn;
     a.nq = (uint32_t)nq; a.items = (uint32_t)items;
@@ -478,7 +578,7 @@ int ad_cfk_store_unmanaged(ad_handle* h, uint32_t key, size_t* count, uint8_t* p
     HIPCHK(h, hipMemcpyAsync(&U, c.um_cnt + key, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     *count = U;
-    const size_t b = (size_t)key * c.cap;
+    const size_t b = c.rbase(key);
     if (U) {
         if (pending) HIPCHK(h, hipMemcpyAsync(pending, c.um_p + b, U, hipMemcpyDeviceToHost, st));
         if (wait_msb) HIPCHK(h, hipMemcpyAsync(wait_msb, c.um_wm + b, U * 8, hipMemcpyDeviceToHost, st));
@@ -526,6 +626,26 @@ int ad_cfk_store_notified(ad_handle* h, uint32_t* counts, size_t* total, uint32_
             for (uint32_t i = 0; i < cnt[k]; ++i) event[o + i] -= c.ev_off_host[k];
             o += cnt[k];
         }
+    }
+    return AD_OK;
+}
+
+// After ad_cfk_store_notify: key's notWaiting flags for all of its rows (a large-tier key can hold more rows than the
+// bulk call's [keys x capacity] output has room for).  rows_cap: the caller's room; *rows: the key's rows.
+int ad_cfk_store_notify_key(ad_handle* h, uint32_t key, uint8_t* not_waiting, size_t rows_cap, size_t* rows) {
+    if (!h || !rows) return AD_ERR_ARGUMENT;
+    auto& c = h->cs;
+    if (!c.K) return set_err(h, AD_ERR_STATE, "ad_cfk_store_notify_key before ad_cfk_store_open");
+    if (key >= c.K) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_notify_key: key out of range");
+    hipSetDevice(h->device);
+    uint32_t n = 0;
+    HIPCHK(h, hipMemcpyAsync(&n, c.cnt + key, 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    *rows = n;
+    if (not_waiting && n) {
+        if (rows_cap < n) return set_err(h, AD_ERR_ARGUMENT, "ad_cfk_store_notify_key: not_waiting holds fewer than the key's rows");
+        HIPCHK(h, hipMemcpyAsync(not_waiting, c.out + c.rbase(key), n, hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipStreamSynchronize(h->st));
     }
     return AD_OK;
 }

@@ -74,6 +74,17 @@ struct CfkStoreArgs {
     uint64_t *nt_tm, *nt_tl;
     int32_t* nt_tn;
     uint64_t* dbg;                            // AD_CS_TIMERS=1: per op class clock64 sums and counts (else nullptr)
+    // two tiers (cs_tier): keys outgrowing `cap` rows move to a large-tier slot of capB rows (k_cfk_promote)
+    uint32_t* kslot;                          // [K] large-tier slot or ~0u
+    uint32_t capB, wordsB, nbig;
+    uint32_t* big_used;                       // large-tier slots taken
+    const uint32_t* ev_start;                 // [K] first event to apply per key (nullptr: ev_off[key]); a resumed key
+                                              //   keeps this call's notifications (nt_cnt not reset)
+    uint32_t* kres;                           // [K] out: the event a key stopped at for want of rows (~0u: none)
+    const uint32_t* klist;                    // the keys of this launch, one workgroup each (nullptr: every key)
+    // the workgroup's view of its key (k_cfk_apply): bitmaps at bbase (LDS copy: 0), the HBM regions of its
+    // loadingPruned / registry rows (grbase) and their witness bitmaps (gbbase); cap / words = its tier's
+    size_t bbase, grbase, gbbase;
 };
 // event ops (ad_cfk_events.op)
 constexpr uint32_t CS_OP_UPDATE = 0;         // CommandsForKey.update (or insertAdditionsOnly: status TRANSITIVELY_KNOWN)
@@ -143,7 +154,7 @@ __device__ inline void cs_add_missing(const CfkStoreArgs& a, size_t base, uint32
         if (s == ts || s == skip_slot || !cs_has_deps(a.st[x]) || !witnesses(cs_kind(a.tl[x]), kt)) continue;
         if (dont && ((dont[s >> 6] >> (s & 63)) & 1ull)) continue;
         if (ts3_cmp(cs_dkb(a, x), t) > 0) {
-            uint64_t* w = a.bits + ((size_t)(base + s)) * a.words + (ts >> 6);
+            uint64_t* w = a.bits + (a.bbase + (size_t)s * a.words) + (ts >> 6);
             *w |= 1ull << (ts & 63);
         }
     }
@@ -151,7 +162,7 @@ __device__ inline void cs_add_missing(const CfkStoreArgs& a, size_t base, uint32
 }
 // Utils.removeFromMissingArrays (:70-95): slot ts leaves every missing set (it committed, or was invalidated)
 __device__ inline void cs_remove_missing(const CfkStoreArgs& a, size_t base, uint32_t n, uint32_t ts) {
-    for (uint32_t s = threadIdx.x; s < n; s += CS_T) a.bits[((size_t)(base + s)) * a.words + (ts >> 6)] &= ~(1ull << (ts & 63));
+    for (uint32_t s = threadIdx.x; s < n; s += CS_T) a.bits[(a.bbase + (size_t)s * a.words) + (ts >> 6)] &= ~(1ull << (ts & 63));
     __syncthreads();
 }
 
@@ -160,7 +171,7 @@ __device__ inline uint32_t cs_insert(const CfkStoreArgs& a, size_t base, uint32_
                                      uint32_t status, const Ts3& ex) {
     const uint32_t s = n;
     cs_shift_up(a, base, p, n);
-    for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + s)) * a.words + w] = 0ull;
+    for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[(a.bbase + (size_t)s * a.words) + w] = 0ull;
     if (threadIdx.x == 0) {
         const size_t x = base + p;
         a.tm[x] = t.msb; a.tl[x] = t.lsb; a.tn[x] = t.node;
@@ -178,7 +189,7 @@ __device__ inline int cs_lp_find(const CfkStoreArgs& a, uint32_t key, uint32_t L
     if (L == 0) return -1;                                        // (uniform: L is the workgroup's count)
     if (threadIdx.x == 0) *s_j = -1;
     __syncthreads();
-    const size_t lb = (size_t)key * a.cap;
+    const size_t lb = a.grbase;
     for (uint32_t j = threadIdx.x; j < L; j += CS_T)
         if (ts3_cmp(Ts3{a.lpm[lb + j], a.lpl[lb + j], a.lpn[lb + j]}, t) == 0) *s_j = (int)j;
     __syncthreads();
@@ -190,16 +201,16 @@ __device__ inline int cs_lp_find(const CfkStoreArgs& a, uint32_t key, uint32_t L
 // TxnId `wt` (if has_wt; a row or not) its least witness; false: full
 __device__ inline bool cs_lp_add(const CfkStoreArgs& a, uint32_t key, uint32_t& L, const Ts3& t, uint32_t w, int* s_j,
                                  const Ts3& wt = Ts3{0, 0, 0}, bool has_wt = false) {
-    const size_t lb = (size_t)key * a.cap;
+    const size_t lb = a.grbase;
     int j = cs_lp_find(a, key, L, t, s_j);
     if (j < 0) {
         if (L >= a.cap) return false;
         j = (int)L++;
-        for (uint32_t q = threadIdx.x; q < a.words; q += CS_T) a.lp_bits[(lb + j) * a.words + q] = 0ull;
+        for (uint32_t q = threadIdx.x; q < a.words; q += CS_T) a.lp_bits[a.gbbase + (size_t)j * a.words + q] = 0ull;
         if (threadIdx.x == 0) { a.lpm[lb + j] = t.msb; a.lpl[lb + j] = t.lsb; a.lpn[lb + j] = t.node; a.lp_xh[lb + j] = 0; }
         __syncthreads();
     }
-    if (w != 0xFFFFFFFFu && threadIdx.x == 0) a.lp_bits[(lb + j) * a.words + (w >> 6)] |= 1ull << (w & 63);
+    if (w != 0xFFFFFFFFu && threadIdx.x == 0) a.lp_bits[a.gbbase + (size_t)j * a.words + (w >> 6)] |= 1ull << (w & 63);
     if (has_wt && threadIdx.x == 0) {
         const size_t x = lb + j;
         if (!a.lp_xh[x] || ts3_cmp(wt, Ts3{a.lp_xm[x], a.lp_xl[x], a.lp_xn[x]}) < 0) {
@@ -211,11 +222,11 @@ __device__ inline bool cs_lp_add(const CfkStoreArgs& a, uint32_t key, uint32_t& 
 }
 // Pruning.removeLoadingPruned: entry j leaves (the last entry takes its place)
 __device__ inline void cs_lp_remove(const CfkStoreArgs& a, uint32_t key, uint32_t& L, int j) {
-    const size_t lb = (size_t)key * a.cap;
+    const size_t lb = a.grbase;
     const uint32_t last = L - 1;
     if ((uint32_t)j != last) {
         for (uint32_t q = threadIdx.x; q < a.words; q += CS_T)
-            a.lp_bits[(lb + j) * a.words + q] = a.lp_bits[(lb + last) * a.words + q];
+            a.lp_bits[a.gbbase + (size_t)j * a.words + q] = a.lp_bits[a.gbbase + (size_t)last * a.words + q];
         if (threadIdx.x == 0) {
             a.lpm[lb + j] = a.lpm[lb + last]; a.lpl[lb + j] = a.lpl[lb + last]; a.lpn[lb + j] = a.lpn[lb + last];
             a.lp_xm[lb + j] = a.lp_xm[lb + last]; a.lp_xl[lb + j] = a.lp_xl[lb + last]; a.lp_xn[lb + j] = a.lp_xn[lb + last];
@@ -327,7 +338,7 @@ __device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_
     const Ts3 pt{a.tm[base + p], a.tl[base + p], a.tn[base + p]};
     if (ts3_cmp(pt, Ts3{a.pbm[key], a.pbl[key], a.pbn[key]}) <= 0 || p == 0) return;
     // pruneBefore's byId scan below p
-    const uint64_t* pbits = a.bits + (base + a.slot[base + p]) * a.words;
+    const uint64_t* pbits = a.bits + a.bbase + (size_t)a.slot[base + p] * a.words;
     for (uint32_t q = tid; q < a.words; q += CS_T) { s.merged[q] = pbits[q]; s.gone[q] = 0ull; s.dead[q] = 0ull; }
     __syncthreads();
     bool any = false;
@@ -340,7 +351,7 @@ __device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_
         } else if (st == AD_ST_APPLIED) {
             const Ts3 e{a.em[x], a.el[x], a.en[x]};
             if (ts3_cmp(e, pex) < 0) {
-                const uint64_t* b = a.bits + (base + a.slot[x]) * a.words;
+                const uint64_t* b = a.bits + a.bbase + (size_t)a.slot[x] * a.words;
                 bool extra = false;
                 for (uint32_t q = tid; q < a.words; q += CS_T) extra |= (b[q] & ~s.merged[q]) != 0ull;
                 extra = __syncthreads_or(extra);
@@ -401,21 +412,21 @@ __device__ inline void cs_maybe_prune(const CfkStoreArgs& a, uint32_t key, size_
     for (uint32_t s0 = 0; s0 < n; s0 += CS_T / 64) {
         const uint32_t sl = s0 + wv;
         const bool keep = sl < n && !((s.dead[sl >> 6] >> (sl & 63)) & 1ull);
-        if (keep) cs_remap_row(a, a.bits + (base + sl) * a.words, s.stage[wv], s, lane);
+        if (keep) cs_remap_row(a, a.bits + a.bbase + (size_t)sl * a.words, s.stage[wv], s, lane);
         __syncthreads();
         if (keep) {
-            uint64_t* dst = a.bits + (base + sl - cs_rank(s.dead, s.dpc, sl)) * a.words;
+            uint64_t* dst = a.bits + a.bbase + (size_t)(sl - cs_rank(s.dead, s.dpc, sl)) * a.words;
             for (uint32_t q = lane; q < a.words; q += 64) dst[q] = s.stage[wv][q];
         }
         __syncthreads();
     }
     // loadingPruned witnesses: pruned rows leave, the others renumbered
-    const size_t lb = (size_t)key * a.cap;
+    const size_t lb = a.grbase;
     for (uint32_t j0 = 0; j0 < L; j0 += CS_T / 64) {
         const uint32_t j = j0 + wv;
-        if (j < L) cs_remap_row(a, a.lp_bits + (lb + j) * a.words, s.stage[wv], s, lane);
+        if (j < L) cs_remap_row(a, a.lp_bits + a.gbbase + (size_t)j * a.words, s.stage[wv], s, lane);
         __syncthreads();
-        if (j < L) for (uint32_t q = lane; q < a.words; q += 64) a.lp_bits[(lb + j) * a.words + q] = s.stage[wv][q];
+        if (j < L) for (uint32_t q = lane; q < a.words; q += 64) a.lp_bits[a.gbbase + (size_t)j * a.words + q] = s.stage[wv][q];
         __syncthreads();
     }
     n -= removed;
@@ -479,7 +490,7 @@ __device__ inline void cs_um_notify(const CfkStoreArgs& a, uint32_t key, size_t 
                                     const Ts3& ex, uint32_t e, CsPruneLds& s, uint32_t* s_U) {
     const int tid = threadIdx.x;
     if (*s_U == 0) return;                                        // no unmanaged txn waits on this key
-    const size_t ub = (size_t)key * a.cap, lb = ub;
+    const size_t ub = a.grbase, lb = ub;
     Ts3 b{0, 0, 0};
     bool hb = false;
     for (uint32_t r = tid; r < n; r += CS_T) {
@@ -589,7 +600,7 @@ __device__ inline bool cs_um_update(const CfkStoreArgs& a, uint32_t key, size_t 
         for (uint32_t r = lo + tid; r < hi; r += CS_T)
             if (cs_me(a.tl[base + r])) consider(base + r);
         // Pruning.isAnyPredecessorWaitingOnPruned (:140-157): a loading managed TxnId below t witnessed at or before t
-        const size_t lb = (size_t)key * a.cap;
+        const size_t lb = a.grbase;
         bool anyp = false;
         for (uint32_t j = tid; j < L; j += CS_T) {
             const size_t x = lb + j;
@@ -603,7 +614,7 @@ __device__ inline bool cs_um_update(const CfkStoreArgs& a, uint32_t key, size_t 
     cs_fold<true>(xm, hx);
     bool ok = true;
     if (tid == 0) {
-        const size_t ub = (size_t)key * a.cap;
+        const size_t ub = a.grbase;
         uint32_t U = *s_U;
         if (ready) cs_um_emit(a, key, e, 2, t);
         else if (waiting) ok = cs_um_insert(a, ub, a.cap, U, UM_APPLY, xm, t);
@@ -641,6 +652,13 @@ struct CsEvChunk {                            // a chunk of the key's events and
     int32_t dn[CS_DEP_CHUNK];
     uint32_t m;
 };
+// (thread 0) the key ran out of rows / loadingPruned / registry entries at event e (global index), before changing
+__device__ inline void cs_out_of_rows(const CfkStoreArgs& a, uint32_t key, uint32_t e) {
+    if (threadIdx.x == 0) {
+        *a.overflow = 1u;
+        if (a.kres) a.kres[key] = e;
+    }
+}
 struct CsApplyLds {
     CsEvChunk ev;
     uint64_t miss[CS_MAX_WORDS];
@@ -689,13 +707,13 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                 const uint32_t q = cs_find(a, base, n, wt, f);
                 if (f) w = a.slot[base + q];
             }
-            if (!cs_lp_add(a, key, L, t, w, &s_j, wt, hw)) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
+            if (!cs_lp_add(a, key, L, t, w, &s_j, wt, hw)) { cs_out_of_rows(a, key, e + e_id0); return false; }
             continue;
         }
         if (op == CS_OP_UNMANAGED || op == CS_OP_UNMANAGED_RECHECK) {
             if (!cs_um_update(a, key, base, n, L, t, Ts3{a.eem[e], a.eel[e], a.een[e]}, a.dep_off[e], a.dep_off[e + 1],
                               op == CS_OP_UNMANAGED, e + e_id0, s_prune, &s_U)) {
-                if (threadIdx.x == 0) *a.overflow = 1u;
+                cs_out_of_rows(a, key, e + e_id0);
                 return false;
             }
             continue;
@@ -709,13 +727,13 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
         if (op == CS_OP_LOAD || jl >= 0) {
             // TxnInfo.create: executeAt (statuses with one), no missing(); the loadingPruned entry's witnesses skip it
             const Ts3 ex{a.eem[e], a.eel[e], a.een[e]};
+            if (!found && n >= a.cap) { cs_out_of_rows(a, key, e + e_id0); return false; }   // (before any change)
             for (uint32_t w = threadIdx.x; w < a.words; w += CS_T)
-                s_miss[w] = jl >= 0 ? a.lp_bits[((size_t)key * a.cap + jl) * a.words + w] : 0ull;
+                s_miss[w] = jl >= 0 ? a.lp_bits[a.gbbase + (size_t)jl * a.words + w] : 0ull;
             __syncthreads();
             if (jl >= 0) cs_lp_remove(a, key, L, jl);
             uint32_t ts;
             if (!found) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
                 ts = cs_insert(a, base, n, p, t, ns, ex);
             } else {
                 ts = a.slot[base + p];
@@ -723,7 +741,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                     const size_t x = base + p;
                     a.st[x] = (uint8_t)ns; a.em[x] = ex.msb; a.el[x] = ex.lsb; a.en[x] = ex.node;
                 }
-                for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + ts)) * a.words + w] = 0ull;
+                for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[(a.bbase + (size_t)ts * a.words) + w] = 0ull;
                 __syncthreads();
             }
             if (cs_decided(ns) && !(found && cs_decided(cur))) cs_remove_missing(a, base, n, ts);
@@ -737,6 +755,27 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
         if (cs_has_deps(ns)) {
             const Ts3 ex{a.eem[e], a.eel[e], a.een[e]};
             const Ts3 dkb = cs_decided(ns) ? ex : t;
+            // room for the event's new rows (its unknown deps at or above prunedBefore, and itself) and loadingPruned
+            // entries (its unknown deps below prunedBefore), checked before anything changes: a key that runs out stops
+            // at this event with its state intact, and resumes from it in a larger tier
+            if (n + (d1 - d0) + (found ? 0u : 1u) > a.cap || L + (d1 - d0) > a.cap) {
+                const Ts3 pb0{a.pbm[key], a.pbl[key], a.pbn[key]};
+                uint32_t nr = found ? 0u : 1u, nl = 0;
+                for (uint32_t j = d0 + threadIdx.x; j < d1; j += CS_T) {
+                    const Ts3 d{a.dtm[j], a.dtl[j], a.dtn[j]};
+                    bool f;
+                    cs_find(a, base, n, d, f);
+                    if (f) continue;
+                    if (ts3_cmp(d, pb0) >= 0) { ++nr; continue; }
+                    bool inl = false;                                  // already loading?
+                    for (uint32_t q = 0; q < L && !inl; ++q)
+                        inl = ts3_cmp(Ts3{a.lpm[a.grbase + q], a.lpl[a.grbase + q], a.lpn[a.grbase + q]}, d) == 0;
+                    if (!inl) ++nl;
+                }
+                nr = cs_block_sum(nr, nullptr) - (found ? 0u : (uint32_t)(CS_T - 1));   // (the own row counted per lane)
+                nl = cs_block_sum(nl, nullptr);
+                if (n + nr > a.cap || L + nl > a.cap) { cs_out_of_rows(a, key, e + e_id0); return false; }
+            }
             // the row's missing set over the current rows (before the additions: they are in the deps)
             for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) s_miss[w] = 0ull;
             __syncthreads();
@@ -789,7 +828,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                 const uint32_t q = cs_find(a, base, n, d, f);
                 if (f) continue;
                 if (ts3_cmp(d, pb) < 0) continue;                      // a pruned addition: loadingPruned, below
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
+                if (n >= a.cap) { cs_out_of_rows(a, key, e + e_id0); return false; }
                 if (s_nadd >= (uint32_t)CS_T) flush_adds(cmd_slot);
                 const uint32_t s = cs_insert(a, base, n, q, d, AD_ST_TRANSITIVELY_KNOWN, d);
                 if (threadIdx.x == 0) s_add[s_nadd++] = s;
@@ -799,7 +838,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
             bool fnow;
             const uint32_t p2 = cs_find(a, base, n, t, fnow);           // t's position after the additions
             if (!fnow) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
+                if (n >= a.cap) { cs_out_of_rows(a, key, e + e_id0); return false; }
                 ts = cs_insert(a, base, n, p2, t, ns, ex);
             } else {
                 ts = a.slot[base + p2];
@@ -808,7 +847,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                     a.st[x] = (uint8_t)ns; a.em[x] = ex.msb; a.el[x] = ex.lsb; a.en[x] = ex.node;
                 }
             }
-            for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + ts)) * a.words + w] = s_miss[w];
+            for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[(a.bbase + (size_t)ts * a.words) + w] = s_miss[w];
             __syncthreads();
             // pruned additions (deps below prunedBefore that are not rows): loadingPruned, witnessed by this command
             for (uint32_t j = d0; j < d1; ++j) {
@@ -818,7 +857,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                 cs_find(a, base, n, d, f);
                 if (f) continue;
                 if (!cs_lp_add(a, key, L, d, ts, &s_j, t, true)) {
-                    if (threadIdx.x == 0) *a.overflow = 1u;
+                    cs_out_of_rows(a, key, e + e_id0);
                     return false;
                 }
             }
@@ -829,7 +868,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
             cs_um_notify(a, key, base, n, L, ns, ex, e + e_id0, s_prune, &s_U);
         } else {
             if (!found) {
-                if (n >= a.cap) { if (threadIdx.x == 0) *a.overflow = 1u; return false; }
+                if (n >= a.cap) { cs_out_of_rows(a, key, e + e_id0); return false; }
                 const uint32_t ts = cs_insert(a, base, n, p, t, ns, t);
                 if (ns != AD_ST_INVALID) cs_add_missing(a, base, n, t, ts, 0xFFFFFFFFu);
             } else {
@@ -838,7 +877,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                     const size_t x = base + p;
                     a.st[x] = (uint8_t)ns; a.em[x] = t.msb; a.el[x] = t.lsb; a.en[x] = t.node;
                 }
-                for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[((size_t)(base + ts)) * a.words + w] = 0ull;
+                for (uint32_t w = threadIdx.x; w < a.words; w += CS_T) a.bits[(a.bbase + (size_t)ts * a.words) + w] = 0ull;
                 __syncthreads();
                 if (cur < AD_ST_COMMITTED && ns == AD_ST_INVALID) cs_remove_missing(a, base, n, ts);
             }
@@ -864,15 +903,19 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
     __shared__ int32_t r_tn[RC], r_en[RC];
     __shared__ uint32_t r_slot[RC];
     __shared__ uint8_t r_st[RC];
-    const uint32_t key = blockIdx.x;
+    const uint32_t key = a.klist ? a.klist[blockIdx.x] : blockIdx.x;
     if (key >= a.K) return;
-    if (threadIdx.x == 0) a.nt_cnt[key] = 0;
-    if (a.ev_off[key] == a.ev_off[key + 1]) return;              // no events: the key is unchanged
-    const size_t gbase = (size_t)key * a.cap;
+    const CsTier tr = cs_tier(key, a.K, a.cap, a.words, a.kslot, a.capB, a.wordsB);
+    if (LDS && tr.cap > CS_LDS_CAP) return;                      // a large-tier key: the HBM kernel's
+    const uint32_t e_first = a.ev_start ? a.ev_start[key] : a.ev_off[key];
+    if (!a.ev_start && threadIdx.x == 0) a.nt_cnt[key] = 0;     // (a resumed key keeps this call's notifications)
+    if (e_first >= a.ev_off[key + 1]) return;                    // no events (or none left): the key is unchanged
+    const size_t gbase = tr.rbase;
     uint32_t n = a.cnt[key];
     uint32_t L = a.lp_cnt[key];
     if (threadIdx.x == 0) { sh.U = a.um_cnt[key]; sh.tcls = 8; sh.t0 = 0; }
     CfkStoreArgs v = a;
+    v.cap = tr.cap; v.words = tr.words; v.bbase = tr.bbase; v.grbase = tr.rbase; v.gbbase = tr.bbase;
     size_t base = gbase;
     if (LDS) {
         for (uint32_t r = threadIdx.x; r < n; r += CS_T) {
@@ -880,9 +923,10 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             r_tm[r] = a.tm[x]; r_tl[r] = a.tl[x]; r_tn[r] = a.tn[x]; r_em[r] = a.em[x]; r_el[r] = a.el[x];
             r_en[r] = a.en[x]; r_st[r] = a.st[x]; r_slot[r] = a.slot[x];
         }
-        for (uint32_t i = threadIdx.x; i < n * a.words; i += CS_T) r_bits[i] = a.bits[gbase * a.words + i];
+        for (uint32_t i = threadIdx.x; i < n * tr.words; i += CS_T) r_bits[i] = a.bits[tr.bbase + i];
         v.tm = r_tm; v.tl = r_tl; v.tn = r_tn; v.em = r_em; v.el = r_el; v.en = r_en; v.st = r_st; v.slot = r_slot;
         v.bits = r_bits;
+        v.bbase = 0;
         base = 0;
     }
     __syncthreads();
@@ -890,7 +934,7 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
     // events' fields, then their deps): per event no dependent HBM read is left on the key's serial path (the deps'
     // searches and the additions scan read one dependency after another).  An event with more deps than a chunk holds
     // runs alone from HBM.
-    for (uint32_t e = a.ev_off[key], end = a.ev_off[key + 1]; e < end;) {
+    for (uint32_t e = e_first, end = a.ev_off[key + 1]; e < end;) {
         const uint32_t lim = min(end - e, CS_EV_CHUNK);
         for (uint32_t i = threadIdx.x; i <= lim; i += CS_T) sh.ev.doff[i] = a.dep_off[e + i];
         if (threadIdx.x == 0) sh.ev.m = 0;
@@ -933,9 +977,46 @@ static __global__ __launch_bounds__(CS_T) void k_cfk_apply(CfkStoreArgs a) {
             a.tm[x] = r_tm[r]; a.tl[x] = r_tl[r]; a.tn[x] = r_tn[r]; a.em[x] = r_em[r]; a.el[x] = r_el[r];
             a.en[x] = r_en[r]; a.st[x] = r_st[r]; a.slot[x] = r_slot[r];
         }
-        for (uint32_t i = threadIdx.x; i < n * a.words; i += CS_T) a.bits[gbase * a.words + i] = r_bits[i];
+        for (uint32_t i = threadIdx.x; i < n * tr.words; i += CS_T) a.bits[tr.bbase + i] = r_bits[i];
     }
     if (threadIdx.x == 0) { a.cnt[key] = n; a.lp_cnt[key] = L; a.um_cnt[key] = sh.U; }
+}
+
+// A key that ran out of rows in the regular tier moves to large-tier slot kslot_new[i]: its rows, loadingPruned and
+// registry rows are copied to the slot's region and every bitmap row is re-strided (words -> wordsB words; the new
+// words are zero).  One workgroup per moved key (klist).
+static __global__ __launch_bounds__(256) void k_cfk_promote(CfkStoreArgs a, const uint32_t* __restrict__ slots) {
+    const uint32_t key = a.klist[blockIdx.x];
+    const CsTier from = cs_tier(key, a.K, a.cap, a.words, nullptr, a.capB, a.wordsB);
+    const size_t r0 = (size_t)a.K * a.cap;
+    const uint32_t b = slots[blockIdx.x];
+    const CsTier to{r0 + (size_t)b * a.capB, r0 * a.words + (size_t)b * a.capB * a.wordsB, a.capB, a.wordsB};
+    const uint32_t n = a.cnt[key], L = a.lp_cnt[key], U = a.um_cnt[key];
+    for (uint32_t r = threadIdx.x; r < n; r += blockDim.x) {
+        const size_t x = from.rbase + r, y = to.rbase + r;
+        a.tm[y] = a.tm[x]; a.tl[y] = a.tl[x]; a.tn[y] = a.tn[x]; a.em[y] = a.em[x]; a.el[y] = a.el[x]; a.en[y] = a.en[x];
+        a.st[y] = a.st[x]; a.slot[y] = a.slot[x];
+    }
+    for (uint32_t j = threadIdx.x; j < L; j += blockDim.x) {
+        const size_t x = from.rbase + j, y = to.rbase + j;
+        a.lpm[y] = a.lpm[x]; a.lpl[y] = a.lpl[x]; a.lpn[y] = a.lpn[x];
+        a.lp_xm[y] = a.lp_xm[x]; a.lp_xl[y] = a.lp_xl[x]; a.lp_xn[y] = a.lp_xn[x]; a.lp_xh[y] = a.lp_xh[x];
+    }
+    for (uint32_t u = threadIdx.x; u < U; u += blockDim.x) {
+        const size_t x = from.rbase + u, y = to.rbase + u;
+        a.um_p[y] = a.um_p[x]; a.um_wm[y] = a.um_wm[x]; a.um_wl[y] = a.um_wl[x]; a.um_wn[y] = a.um_wn[x];
+        a.um_tm[y] = a.um_tm[x]; a.um_tl[y] = a.um_tl[x]; a.um_tn[y] = a.um_tn[x];
+    }
+    // bitmaps: the rows' (slots [0, n)) and the loadingPruned entries' ([0, L)), each over the slots
+    for (uint32_t i = threadIdx.x; i < n * a.wordsB; i += blockDim.x) {
+        const uint32_t sl = i / a.wordsB, w = i - sl * a.wordsB;
+        a.bits[to.bbase + i] = w < a.words ? a.bits[from.bbase + (size_t)sl * a.words + w] : 0ull;
+    }
+    for (uint32_t i = threadIdx.x; i < L * a.wordsB; i += blockDim.x) {
+        const uint32_t j = i / a.wordsB, w = i - j * a.wordsB;
+        a.lp_bits[to.bbase + i] = w < a.words ? a.lp_bits[from.bbase + (size_t)j * a.words + w] : 0ull;
+    }
+    if (threadIdx.x == 0) a.kslot[key] = b;
 }
 
 }  // namespace ad

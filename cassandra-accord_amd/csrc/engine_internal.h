@@ -270,6 +270,19 @@ struct ad_handle {
         int32_t* nt_tn = nullptr;
         size_t nt_total = 0;
         std::vector<uint32_t> nt_base_host, ev_off_host;
+        // the large tier (keys outgrowing cap): capB rows per slot, nbig slots, big_keys[slot] = its key
+        uint32_t capB = 0, wordsB = 0, nbig = 0, ucapB = 0;
+        uint32_t *kslot = nullptr, *kres = nullptr, *klist = nullptr, *kstart = nullptr, *kslots_new = nullptr;
+        std::vector<uint32_t> kslot_host, big_keys;
+        uint32_t rows_cap(uint32_t key) const { return kslot_host.empty() || kslot_host[key] == ~0u ? cap : capB; }
+        uint32_t words_of(uint32_t key) const { return kslot_host.empty() || kslot_host[key] == ~0u ? words : wordsB; }
+        size_t rbase(uint32_t key) const {
+            return kslot_host.empty() || kslot_host[key] == ~0u ? (size_t)key * cap : (size_t)K * cap + (size_t)kslot_host[key] * capB;
+        }
+        size_t bbase(uint32_t key) const {
+            return kslot_host.empty() || kslot_host[key] == ~0u ? (size_t)key * cap * words
+                                                                : (size_t)K * cap * words + (size_t)kslot_host[key] * capB * wordsB;
+        }
     } cs;
     // the last ad_cfk_store_query (cfk_query_kernels.h): capacity-laid outputs per class + exact counts on the host
     struct CfkQueryOut {
@@ -372,6 +385,7 @@ enum Slot : size_t {
     S_KSSRC, S_KSDST, S_KSSRC2, S_KSDST2, S_KSREM, S_KSXOFF, S_KSRCNT, S_KSFL, S_KSBASE, S_KSCNT, S_KSOUT,
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
     S_KSLACC, S_KSPLV, S_KSHEAD, S_KSSENT, S_KSSTO, S_KSSTI, S_KSPEND,   // ... READY level bounds, queues, slots
+    S_CSKSLOT, S_CSKRES, S_CSKLIST, S_CSKSTART, S_CSKNEW,                // CFK store large tier
     S_CS0, S_CS_END = S_CS0 + 22,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
     S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles

@@ -38,6 +38,8 @@ struct NotifyArgs {
     // missing() as a bitmap over the key's slots (bits[(k * cap + slot) * words ...]) instead of the CSR
     const uint32_t* cnt;
     uint32_t cap, words;
+    const uint32_t* kslot;                   // two-tier stores: per key its large-tier slot (or ~0u); nullptr: one tier
+    uint32_t capB, wordsB;
     const uint32_t* slot;
     const uint64_t* bits;
     // the store's loadingPruned tables (nullptr: none): a STABLE txn that witnessed a pruned Read / Write TxnId below its
@@ -47,7 +49,19 @@ struct NotifyArgs {
     const int32_t* lpn;
     const uint64_t* lp_bits;
 };
-constexpr uint32_t NF_MAX_WORDS = 128;       // the bitmap reader: at most 8192 rows per key
+constexpr uint32_t NF_MAX_WORDS = 256;       // the bitmap reader: at most 16384 rows per key
+
+// A device store's key region (cfk_store_kernels.h): the K keys' regular tier (cap rows, words-word bitmaps each) first,
+// then the large tier (capB rows, wordsB-word bitmaps per slot) that keys outgrowing cap move to.  Rows, loadingPruned
+// and registry rows at rbase; missing() / witness bitmaps at bbase, one bitmap row of `words` words per slot.
+struct CsTier { size_t rbase, bbase; uint32_t cap, words; };
+__device__ inline CsTier cs_tier(uint32_t key, size_t K, uint32_t cap, uint32_t words, const uint32_t* kslot, uint32_t capB,
+                                 uint32_t wordsB) {
+    const uint32_t b = kslot ? kslot[key] : 0xFFFFFFFFu;
+    if (b == 0xFFFFFFFFu) return CsTier{(size_t)key * cap, (size_t)key * cap * words, cap, words};
+    const size_t r0 = K * cap;
+    return CsTier{r0 + (size_t)b * capB, r0 * words + (size_t)b * capB * wordsB, capB, wordsB};
+}
 
 __device__ inline bool nf_rw(uint64_t lsb) {             // managesExecution: key-domain Read / Write
     const uint32_t k = (uint32_t)(lsb >> 1) & 7u;
@@ -83,8 +97,11 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
     const size_t key = blockIdx.x;
     if (key >= a.K) return;
     const int tid = threadIdx.x;
-    const uint32_t lo = a.row_off ? a.row_off[key] : (uint32_t)key * a.cap;
-    const uint32_t hi = a.row_off ? a.row_off[key + 1] : lo + a.cnt[key], L = hi - lo;
+    const CsTier tr = cs_tier((uint32_t)key, a.K, a.cap, a.words, a.row_off ? nullptr : a.kslot, a.capB, a.wordsB);
+    const size_t lo = a.row_off ? a.row_off[key] : tr.rbase;
+    const size_t hi = a.row_off ? a.row_off[key + 1] : lo + a.cnt[key];
+    const uint32_t L = (uint32_t)(hi - lo);
+    const uint32_t words = tr.words;
     __shared__ uint64_t s_mask[NF_MAX_WORDS];
     // pass 1: maxAW, order check, minUndecided
     Ts3 maw{0, 0, 0};
@@ -164,7 +181,7 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
     __syncthreads();
     // bitmap reader: the slots whose missing bit counts -- Read / Write rows at or after minUndecided
     if (a.bits) {
-        for (uint32_t w = tid; w < a.words; w += NF_T) s_mask[w] = 0ull;
+        for (uint32_t w = tid; w < words; w += NF_T) s_mask[w] = 0ull;
         __syncthreads();
         for (uint32_t r = tid; r < L; r += NF_T)
             if (r >= (minund == L ? 0u : minund) && nf_rw(a.tl[lo + r])) {
@@ -197,8 +214,8 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
                 const uint32_t expect = nf_write(lsb) ? rstar + und_rw : und_w;
                 uint32_t mc = 0;
                 if (a.bits) {
-                    const uint64_t* row = a.bits + ((size_t)lo + a.slot[x]) * a.words;
-                    for (uint32_t w = 0; w < a.words; ++w) mc += (uint32_t)__popcll(row[w] & s_mask[w]);
+                    const uint64_t* row = a.bits + tr.bbase + (size_t)a.slot[x] * words;
+                    for (uint32_t w = 0; w < words; ++w) mc += (uint32_t)__popcll(row[w] & s_mask[w]);
                 } else {
                     for (uint32_t m = a.miss_off[x]; m < a.miss_off[x + 1]; ++m) {
                         const uint32_t j = a.miss[m];
@@ -207,11 +224,11 @@ static __global__ __launch_bounds__(NF_T) void k_cfk_notify(NotifyArgs a) {
                 }
                 rel = expect == mc ? 1 : 0;
                 if (rel && a.lp_cnt) {
-                    const size_t lb = key * a.cap;
+                    const size_t lb = tr.rbase;
                     const uint32_t sl = a.slot[x];
                     for (uint32_t j = 0; j < a.lp_cnt[key]; ++j)
                         if (nf_rw(a.lpl[lb + j]) && ts3_cmp(Ts3{a.lpm[lb + j], a.lpl[lb + j], a.lpn[lb + j]}, e) < 0 &&
-                            ((a.lp_bits[(lb + j) * a.words + (sl >> 6)] >> (sl & 63)) & 1ull)) { rel = 0; break; }
+                            ((a.lp_bits[tr.bbase + (size_t)j * words + (sl >> 6)] >> (sl & 63)) & 1ull)) { rel = 0; break; }
                 }
             }
         }

@@ -536,8 +536,17 @@ typedef struct ad_cfk_events {
     const uint8_t*  op;             /* [m] AD_CFK_OP_* per event, or NULL                              */
 } ad_cfk_events;
 int  ad_cfk_store_open(ad_handle* h, uint32_t keys, uint32_t capacity);
+/* Two tiers: every key starts with `capacity` rows (loadingPruned / unmanaged entries alike); a key that an event would
+ * take past them stops before that event, moves to one of `big_keys` large-tier slots of `big_capacity` rows (its rows
+ * and missing() bitmaps copied and re-strided on the device) and resumes from the event in the same call.  Memory:
+ * keys x capacity + big_keys x big_capacity rows, missing() bitmaps quadratic in each tier's capacity.
+ * 1 <= capacity <= 8192, capacity < big_capacity <= 16384.  ad_cfk_store_open = no large tier. */
+int  ad_cfk_store_open_tiered(ad_handle* h, uint32_t keys, uint32_t capacity, uint32_t big_capacity, uint32_t big_keys);
 int  ad_cfk_store_apply(ad_handle* h, const ad_cfk_events* ev);
+/* not_waiting: each key's first `capacity` rows (a large-tier key's others: ad_cfk_store_notify_key) */
 int  ad_cfk_store_notify(ad_handle* h, uint32_t* rows /* [keys] */, uint8_t* not_waiting /* [keys * capacity] */);
+/* after ad_cfk_store_notify: one key's flags for all of its rows (*rows; not_waiting may be NULL: count only) */
+int  ad_cfk_store_notify_key(ad_handle* h, uint32_t key, uint8_t* not_waiting, size_t rows_cap, size_t* rows);
 /* one key's rows: *rows (and *missing total); arrays may be NULL (two calls); miss_off[rows + 1], missing = byId row
  * indices within the key, ascending per row */
 int  ad_cfk_store_fetch(ad_handle* h, uint32_t key, size_t* rows, size_t* missing_total, uint64_t* txn_msb,

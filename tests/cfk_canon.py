@@ -1133,6 +1133,11 @@ class Run:
                 self.snapshots.append((self.events, self.rows(), frozenset(
                     t for t in self.notified if cfk.info.get(t) is not None and cfk.info[t].status == STABLE),
                     frozenset(full_scan_ready(cfk))))
+        if log and (cfk.log or cfk.notes):             # the CFK updates of tasks run after the last logged event
+            self.event_log.append(list(cfk.log))
+            cfk.log.clear()
+            self.note_log.append(list(cfk.notes))
+            cfk.notes.clear()
         self.queue_left = len(queue)
 
     def _post_update(self, cfk, canon, queue, cur_status, new_info, cmd, changed, sink, prune_now):

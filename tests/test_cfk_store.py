@@ -133,10 +133,15 @@ def _bits_rows(rows, domains):
 
 
 @pytest.mark.gpu
-# (1000 events: ~850 rows per key, the HBM-resident apply kernel; 240 events: <= 256 rows, the LDS-resident one)
-@pytest.mark.parametrize("chunk,prune,events", [(0, False, 1000), (1, False, 1000), (0, True, 1000), (1, True, 1000),
-                                                (0, False, 240), (0, True, 240)])
-def test_gpu_store_follows_the_harness(engine_factory, chunk, prune, events):
+# (1000 events: ~850 rows per key, the HBM-resident apply kernel; 240 events: <= 256 rows, the LDS-resident one;
+# tiered: every key starts in a small regular tier and moves to the large tier mid-stream, within an apply call —
+# 1000 events: 128-row LDS tier -> HBM large tier; 240 events: 64 -> 256 rows, LDS both)
+@pytest.mark.parametrize("chunk,prune,events,tiered", [(0, False, 1000, False), (1, False, 1000, False),
+                                                       (0, True, 1000, False), (1, True, 1000, False),
+                                                       (0, False, 240, False), (0, True, 240, False),
+                                                       (1, False, 1000, True), (1, True, 1000, True),
+                                                       (0, True, 240, True)])
+def test_gpu_store_follows_the_harness(engine_factory, chunk, prune, events, tiered):
     seeds = (PRUNE_SEEDS if prune else SEEDS)[chunk * 10:(chunk + 1) * 10]
     runs = [K.Run(seed, events, snapshot_every=25 if events >= 1000 else 8, log=True, prune=prune, snapshot_lag=prune)
             for seed in seeds]
@@ -146,7 +151,11 @@ def test_gpu_store_follows_the_harness(engine_factory, chunk, prune, events):
         assert max(r.max_rows for r in runs) <= 256
         cap = 256
     extras = 0
-    eng.cfk_store_open(len(runs), cap)
+    if tiered:
+        small = 128 if events >= 1000 else 64
+        eng.cfk_store_open(len(runs), small, big_capacity=cap, big_keys=len(runs))
+    else:
+        eng.cfk_store_open(len(runs), cap)
     snaps = [{ev: (rows, want, full) for ev, rows, want, full in r.snapshots} for r in runs]
     steps = max(len(r.event_log) for r in runs)
     checked = released = 0
@@ -172,7 +181,9 @@ def test_gpu_store_follows_the_harness(engine_factory, chunk, prune, events):
             d = eng.cfk_store_fetch(k)
             assert _device_rows(d, None) == _bits_rows(rows, runs[k].domains), "seed %d step %d: rows" % (seeds[k], e)
             assert int(nrows[k]) == len(rows)
-            dev = {rows[i][0] for i in np.nonzero(out[k, :len(rows)])[0]}
+            flags = eng.cfk_store_notify_key(k) if tiered else out[k, :len(rows)]
+            assert len(flags) == len(rows)
+            dev = {rows[i][0] for i in np.nonzero(flags)[0]}
             if prune:
                 assert dev == set(full), "seed %d step %d: device %s, full scan %s" % (
                     seeds[k], e, sorted(dev - set(full))[:3], sorted(set(full) - dev)[:3])
@@ -180,7 +191,7 @@ def test_gpu_store_follows_the_harness(engine_factory, chunk, prune, events):
                 # the device's release set — including the txns the event-driven harness has not notified yet (a
                 # pruned TxnId loading) — keeps the reference's own execution-order invariants
                 # (CommandsForKeyTest.java:175-180, 206-218) against Canon's committed commands at this step
-                bad = K.release_invariant_violations(runs[k].canon_views[e], [rows[i][0] for i in np.nonzero(out[k, :len(rows)])[0]])
+                bad = K.release_invariant_violations(runs[k].canon_views[e], [rows[i][0] for i in np.nonzero(flags)[0]])
                 assert not bad, "seed %d step %d: %s" % (seeds[k], e, bad[:3])
                 extras += len(dev - set(want))
             else:
