@@ -842,7 +842,11 @@ static __global__ __launch_bounds__(256) void k_large_layout(TxnArgs a) {
 constexpr uint32_t MERGE_HEAVY_HINT = 256;
 template <int NVC>
 struct OffsetsOp {
-    struct S { uint32_t k[NVC], e[NVC]; };
+    // k / e: keys and entries per class; d: deferred txns and o: overflowed (txn, class) rows, whose exclusive prefixes
+    // are the txns' slots in the dtx / ovf_rows lists (an atomic append per wave was ~5x10^4 same-address atomics on
+    // C3, whose hot keys overflow ~10^5 rows: 0.55 ms of the scan); ob: the element's overflowed classes (its own
+    // value only: combine's sum of it is not used)
+    struct S { uint32_t k[NVC], e[NVC], d, o, ob; };
     size_t n;
     const uint8_t* meta;
     const uint32_t* key_off;
@@ -864,6 +868,7 @@ struct OffsetsOp {
         S s;
 #pragma unroll
         for (int c = 0; c < NVC; ++c) { s.k[c] = 0; s.e[c] = 0; }
+        s.d = s.o = s.ob = 0;
         return s;
     }
     __device__ S load(size_t t) const {
@@ -876,18 +881,28 @@ struct OffsetsOp {
         }
         const uint32_t b = key_off[t], e = key_off[t + 1];
         // a pair's NVC counts are contiguous bytes (one dword per pair for NVC <= 4)
+        uint32_t ob = 0, ents = 0;
         for (uint32_t x = b; x < e; ++x) {
             uint32_t v[NVC];
             pair_counts<NVC>(cnt8, cntx, x, v);
 #pragma unroll
-            for (int c = 0; c < NVC; ++c) { s.k[c] += v[c] > 0 ? 1u : 0u; s.e[c] += v[c]; }
+            for (int c = 0; c < NVC; ++c) {
+                s.k[c] += v[c] > 0 ? 1u : 0u; s.e[c] += v[c]; ents += v[c];
+                ob |= (v[c] > (uint32_t)WALK_INL ? 1u : 0u) << c;
+            }
         }
+        // small txns k_txn_finish cannot finish from the inline ids: a pair overflowed them (the walk set dfr), or
+        // more than 4 keys carry entries (deferred); k_txn_finish's small txns (<= 4 pairs) with a class whose list
+        // overflowed the inline ids (overflowed rows)
+        s.d = (dfr[t] != 0 || (ents > 0 && e - b > 4)) ? 1u : 0u;
+        if (e - b <= 4) { s.ob = ob; s.o = (uint32_t)__popc(ob); }
         return s;
     }
     __device__ S combine(const S& x, const S& y) const {
         S r;
 #pragma unroll
         for (int c = 0; c < NVC; ++c) { r.k[c] = x.k[c] + y.k[c]; r.e[c] = x.e[c] + y.e[c]; }
+        r.d = x.d + y.d; r.o = x.o + y.o; r.ob = 0;
         return r;
     }
     __device__ void store(size_t t, const S& ex, const S& inc, const S& el) const {
@@ -906,28 +921,16 @@ struct OffsetsOp {
                 o_k2t_off[c][n] = inc.k[c] + inc.e[c];
             }
         }
-        // small txns k_txn_finish cannot finish from the inline ids: a pair overflowed them (the walk set
-        // dfr), or more than 4 keys carry entries
-        bool d = false;
-        if (!(meta[t] & META_LARGE)) {
-            d = dfr[t] != 0;
-            if (!d && ents > 0 && key_off[t + 1] - key_off[t] > 4) { dfr[t] = 1; d = true; }
+        // the deferred txn and the overflowed rows at their prefix slots (ascending txn order)
+        if (el.d) {
+            if (!dfr[t]) dfr[t] = 1;
+            dtx[ex.d] = (uint32_t)t;
         }
-        wave_append(d, (uint32_t)t, dtx, dtx_count);      // k_txn_union's rows
-        // k_txn_finish's small txns (<= 4 pairs) with a class whose list overflowed the inline ids (that kernel's own
-        // test, on the pair counts the load just read)
-        uint32_t ovf = 0;
-        if (!(meta[t] & META_LARGE) && key_off[t + 1] - key_off[t] <= 4) {
-            for (uint32_t x = key_off[t]; x < key_off[t + 1]; ++x) {
-                uint32_t v[NVC];
-                pair_counts<NVC>(cnt8, cntx, x, v);
+        uint32_t j = ex.o;
 #pragma unroll
-                for (int c = 0; c < NVC; ++c) ovf |= (v[c] > (uint32_t)WALK_INL ? 1u : 0u) << c;
-            }
-        }
-        if (__ballot(ovf != 0))
-#pragma unroll
-            for (int c = 0; c < NVC; ++c) wave_append((ovf >> c) & 1u, (uint32_t)(t * NVC + c), ovf_rows, ovf_count);
+        for (int c = 0; c < NVC; ++c)
+            if ((el.ob >> c) & 1u) ovf_rows[j++] = (uint32_t)(t * NVC + c);
+        if (t + 1 == n) { *dtx_count = inc.d; *ovf_count = inc.o; }
     }
 };
 
