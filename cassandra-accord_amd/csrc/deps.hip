@@ -326,10 +326,20 @@ static int stage_deps_impl(ad_handle* h) {
         launch_walk_nv(nv, wa, false, direct, true, st);
     }
     TxnArgs ta{};
+    static unsigned long long* ovf_dbg = nullptr;             // AD_OVF_TIMERS=1 (diagnostics): printed per batch
+    {
+        const char* e = getenv("AD_OVF_TIMERS");
+        if (e && e[0] == '1') {
+            if (!ovf_dbg) hipMalloc(&ovf_dbg, 64);
+            hipMemsetAsync(ovf_dbg, 0, 64, st);
+            ta.dbg = ovf_dbg;
+        }
+    }
     ta.n = n; ta.P = P; ta.nvc = nc; ta.key_off = h->key_off; ta.keys = h->keys; ta.meta = h->meta; ta.cnt8 = h->cnt8; ta.cntx = h->cntx;
     ta.nk = h->nk; ta.ne = h->ne; ta.dst = h->dst; ta.prm = h->prm;
     ta.voff = h->voff; ta.vcnt = h->vcnt; ta.vdst = h->vcnt; ta.vi_u = h->vi_u; ta.ukey = h->ukey;
-    CK(dalloc(h, S_FOVF, &ta.ovf_rows, std::max<size_t>(n * (size_t)nc, 1)));
+    CK(dalloc(h, S_FOVF, &ta.ovf_rows, std::max<size_t>(n, 1)));
+    CK(dalloc(h, S_FOVFCM, &ta.ovf_cm, std::max<size_t>(n, 1)));
     ta.ovf_count = fovf_count;
     // every large txn's per-CSR totals, also when no range meets a CFK key (V = 0: a batch of range txns only); the
     // offsets scan reads them for every large txn
@@ -339,7 +349,7 @@ static int stage_deps_impl(ad_handle* h) {
     }
     if (n > 0) {
         KScope ks(K_SCAN_OFFSETS, n);
-        launch_offsets_nv(h, nv, direct, cls, heavy, dtx, dtx_count, ta.ovf_rows, fovf_count);
+        launch_offsets_nv(h, nv, direct, cls, heavy, dtx, dtx_count, ta.ovf_rows, ta.ovf_cm, fovf_count);
     } else {
         for (int k = 0; k < nc; ++k) csr_offsets(h, h->deps[cls[k]], h->nk, h->ne);
     }
@@ -547,6 +557,17 @@ static int stage_deps_impl(ad_handle* h) {
     // HBM, when release_dead gives them back (STAGE_MERGE).
     host_mark(h, "deps deps_end");
     if (!h->xdefer) side_join(h);
+    if (ta.dbg) {
+        side_join(h);
+        hipStreamSynchronize(h->xst);
+        hipStreamSynchronize(st);
+        unsigned long long d[5];
+        uint32_t oc = 0;
+        hipMemcpy(d, ta.dbg, sizeof d, hipMemcpyDeviceToHost);
+        hipMemcpy(&oc, ta.ovf_count, 4, hipMemcpyDeviceToHost);
+        fprintf(stderr, "ovf_timers count %u rows %llu clocks avg %.0f max %llu walks %llu emits %llu path %s\n", oc, d[0],
+                d[0] ? (double)d[1] / (double)d[0] : 0.0, d[2], d[3], d[4], fuse ? "fuse" : "three-kernel");
+    }
     h->have_deps = true;
     h->ls.chains_ready = false;
     h->times.deps_entries = h->deps_entries;

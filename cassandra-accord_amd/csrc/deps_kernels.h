@@ -755,7 +755,9 @@ struct TxnArgs {
     uint32_t* vdst;               // [x * nvc + vc] (aliases vcnt: each slot is read, then rewritten, once)
     const uint32_t* vi_u;         // item -> distinct-key index (its key = ukey[u])
     const uint64_t* ukey;
-    uint32_t* ovf_rows;           // k_txn_finish -> k_txn_finish_ovf: (txn * nvc + class) rows whose lists overflowed
+    unsigned long long* dbg;      // AD_OVF_TIMERS=1: k_txn_finish_ovf's rows, clocks (sum, max), walked pairs, emitted
+    uint8_t* ovf_cm;              // ... and their overflowed classes
+    uint32_t* ovf_rows;           // k_txn_finish -> k_txn_finish_ovf: txns with a class whose lists overflowed
     uint32_t* ovf_count;          //   their inline ids (zeroed before the finish)
 };
 
@@ -861,8 +863,9 @@ struct OffsetsOp {
     const uint32_t* lsum_k;       // [c * n + t] large txns' per-CSR key / entry totals (k_large_sums)
     const uint32_t* lsum_e;
     uint32_t* heavy;              // set when some txn's CSRs total more than MERGE_HEAVY keys + entries
-    uint32_t* ovf_rows;           // (txn * NVC + class) rows k_txn_finish_ovf lays out (a pair's list overflowed the
-    uint32_t* ovf_count;          //   walk's inline ids): listed here so that kernel can run beside k_txn_finish
+    uint32_t* ovf_rows;           // txns k_txn_finish_ovf lays out (a pair's list overflowed the walk's inline ids) and
+    uint8_t* ovf_cm;              //   their overflowed classes: listed here so that kernel can run beside k_txn_finish
+    uint32_t* ovf_count;
 
     __device__ S identity() const {
         S s;
@@ -895,7 +898,7 @@ struct OffsetsOp {
         // more than 4 keys carry entries (deferred); k_txn_finish's small txns (<= 4 pairs) with a class whose list
         // overflowed the inline ids (overflowed rows)
         s.d = (dfr[t] != 0 || (ents > 0 && e - b > 4)) ? 1u : 0u;
-        if (e - b <= 4) { s.ob = ob; s.o = (uint32_t)__popc(ob); }
+        if (e - b <= 4) { s.ob = ob; s.o = ob ? 1u : 0u; }
         return s;
     }
     __device__ S combine(const S& x, const S& y) const {
@@ -926,10 +929,7 @@ struct OffsetsOp {
             if (!dfr[t]) dfr[t] = 1;
             dtx[ex.d] = (uint32_t)t;
         }
-        uint32_t j = ex.o;
-#pragma unroll
-        for (int c = 0; c < NVC; ++c)
-            if ((el.ob >> c) & 1u) ovf_rows[j++] = (uint32_t)(t * NVC + c);
+        if (el.ob) { ovf_rows[ex.o] = (uint32_t)t; ovf_cm[ex.o] = (uint8_t)el.ob; }
         if (t + 1 == n) { *dtx_count = inc.d; *ovf_count = inc.o; }
     }
 };
@@ -1171,9 +1171,11 @@ static __global__ __launch_bounds__(256) void k_txn_finish(TxnArgs a) {
     }
     a.out_tcnt[c][t] = u;
 }
-// The (txn, class) rows k_txn_finish listed: the per-key lists in memory (raw TxnIds, ascending) from the inline ids
-// and, for the overflowed pairs, a re-walk of that pair for this class (walk_entry from posof), then the union
-// (union_small).  Rare (C2: a few txns); grid-stride over the device-side count.
+// The txns whose lists overflowed k_txn_finish's inline ids (the offsets scan listed them with their overflowed
+// classes): per overflowed class the per-key lists in memory (raw TxnIds, ascending) from the inline ids and, for
+// the overflowed pairs, ONE re-walk of the pair for all of its overflowed classes (walk_entry from posof; a walk per
+// (txn, class) row walked C3's hot pairs ~3 times: 0.8 ms of random line traffic), then each class's union
+// (union_small).  C2: a few hundred txns; C3: ~3*10^5 (its hot keys' pairs).  Grid-stride over the device-side count.
 template <int NV, bool DIRECT>
 static __global__ __launch_bounds__(256) void k_txn_finish_ovf(TxnArgs a) {
     constexpr int NVC = DIRECT ? 2 * NV : NV;
@@ -1181,33 +1183,62 @@ static __global__ __launch_bounds__(256) void k_txn_finish_ovf(TxnArgs a) {
     if (a.spec_bad && *a.spec_bad) return;
     const uint32_t cnt = *(const volatile uint32_t*)a.ovf_count;
     for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < cnt; x += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t r = a.ovf_rows[x];
-        const size_t t = r / NVC;
-        const int c = (int)(r - t * NVC);
-        const uint32_t kb = a.out_key_off[c][t], nk = a.out_key_off[c][t + 1] - kb;
+        const uint64_t c0 = a.dbg ? clock64() : 0;
+        uint32_t dwalk = 0, demit = 0;
+        const size_t t = a.ovf_rows[x];
+        const uint32_t cm = a.ovf_cm[x];                 // the overflowed classes
         const uint32_t b = a.key_off[t], e = a.key_off[t + 1];
-        const uint32_t mb = a.out_k2t_off[c][t], ob = a.out_ent_off[c][t];
         const uint32_t mt = a.meta[t];
-        int32_t* k2t = a.out_k2t[c];
-        uint32_t run = nk, kk = 0;
+        uint32_t kb[NVC], nk[NVC], mb[NVC], run[NVC], kk[NVC];
+#pragma unroll
+        for (int c = 0; c < NVC; ++c) {
+            const bool on = (cm >> c) & 1u;
+            kb[c] = on ? a.out_key_off[c][t] : 0u;
+            nk[c] = on ? a.out_key_off[c][t + 1] - kb[c] : 0u;
+            mb[c] = on ? a.out_k2t_off[c][t] : 0u;
+            run[c] = nk[c]; kk[c] = 0;
+        }
         for (uint32_t y = b; y < e; ++y) {                   // <= 4 pairs (k_txn_finish's small txns)
-            const uint32_t cc = pair_count(a.cnt8, a.cntx, NCB, NVC, y, c);
-            if (cc == 0) continue;
-            a.out_keys[c][kb + kk] = a.keys[y];               // the key and its keysToTxnIds end (header)
-            k2t[mb + kk] = (int32_t)(run + cc);
-            ++kk;
-            if (cc <= (uint32_t)WALK_INL) {
-                const uint32_t* src = a.inl + ((size_t)y * NVC + c) * WALK_INL;
-                for (uint32_t q = 0; q < cc; ++q) k2t[mb + run + cc - 1 - q] = (int32_t)src[q];
-            } else {
-                uint32_t slot = mb + run + cc - 1;
+            uint32_t cc[NVC];
+            pair_counts<NVC>(a.cnt8, a.cntx, y, cc);
+            uint32_t walk = 0, slot[NVC];
+#pragma unroll
+            for (int c = 0; c < NVC; ++c) {
+                slot[c] = 0;
+                if (!((cm >> c) & 1u) || cc[c] == 0) continue;
+                int32_t* k2t = a.out_k2t[c];
+                a.out_keys[c][kb[c] + kk[c]] = a.keys[y];    // the key and its keysToTxnIds end (header)
+                k2t[mb[c] + kk[c]] = (int32_t)(run[c] + cc[c]);
+                ++kk[c];
+                if (cc[c] <= (uint32_t)WALK_INL) {
+                    const uint32_t* src = a.inl + ((size_t)y * NVC + c) * WALK_INL;
+                    for (uint32_t q = 0; q < cc[c]; ++q) k2t[mb[c] + run[c] + cc[c] - 1 - q] = (int32_t)src[q];
+                } else {
+                    walk |= 1u << c;
+                    slot[c] = mb[c] + run[c] + cc[c] - 1;
+                }
+                run[c] += cc[c];
+            }
+            if (walk) {
+                ++dwalk;
                 walk_entry<NV>(a.w, (size_t)a.w.posof[y], (uint32_t)t, mt, [&](int v, bool direct, uint32_t dj) {
-                    if (walk_class<NV, DIRECT>(v, direct) == c) k2t[slot--] = (int32_t)dj;
+                    ++demit;
+                    const int c = walk_class<NV, DIRECT>(v, direct);
+#pragma unroll
+                    for (int k = 0; k < NVC; ++k)
+                        if (k == c && ((walk >> k) & 1u)) a.out_k2t[k][slot[k]--] = (int32_t)dj;
                 });
             }
-            run += cc;
         }
-        a.out_tcnt[c][t] = union_small<4>(k2t, mb, nk, a.out_txns[c] + ob);
+#pragma unroll
+        for (int c = 0; c < NVC; ++c)
+            if ((cm >> c) & 1u)
+                a.out_tcnt[c][t] = union_small<4>(a.out_k2t[c], mb[c], nk[c], a.out_txns[c] + a.out_ent_off[c][t]);
+        if (a.dbg) {
+            const unsigned long long dc = (unsigned long long)(clock64() - c0);
+            atomicAdd(&a.dbg[0], 1ull); atomicAdd(&a.dbg[1], dc); atomicMax(&a.dbg[2], dc);
+            atomicAdd(&a.dbg[3], (unsigned long long)dwalk); atomicAdd(&a.dbg[4], (unsigned long long)demit);
+        }
     }
 }
 

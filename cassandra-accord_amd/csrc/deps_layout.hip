@@ -7,9 +7,9 @@
 // is CSR cls[k] (every class, or the keyDeps class of each view when the batch has no directKeyDeps).
 template <int NC>
 void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count,
-                       uint32_t* ovf_rows, uint32_t* ovf_count) {
+                       uint32_t* ovf_rows, uint8_t* ovf_cm, uint32_t* ovf_count) {
     OffsetsOp<NC> op{};
-    op.ovf_rows = ovf_rows; op.ovf_count = ovf_count;
+    op.ovf_rows = ovf_rows; op.ovf_cm = ovf_cm; op.ovf_count = ovf_count;
     op.n = h->n; op.meta = h->meta; op.key_off = h->key_off; op.cnt8 = h->cnt8; op.cntx = h->cntx;
     op.dfr = h->dfr; op.dtx = dtx; op.dtx_count = dtx_count;
     op.lsum_k = h->nk; op.lsum_e = h->ne; op.heavy = heavy;
@@ -21,9 +21,9 @@ void launch_offsets_nc(ad_handle* h, const int* cls, uint32_t* heavy, uint32_t* 
 }
 template <int NV>
 void launch_offsets(ad_handle* h, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count,
-                    uint32_t* ovf_rows, uint32_t* ovf_count) {
-    if (direct) launch_offsets_nc<2 * NV>(h, cls, heavy, dtx, dtx_count, ovf_rows, ovf_count);
-    else launch_offsets_nc<NV>(h, cls, heavy, dtx, dtx_count, ovf_rows, ovf_count);
+                    uint32_t* ovf_rows, uint8_t* ovf_cm, uint32_t* ovf_count) {
+    if (direct) launch_offsets_nc<2 * NV>(h, cls, heavy, dtx, dtx_count, ovf_rows, ovf_cm, ovf_count);
+    else launch_offsets_nc<NV>(h, cls, heavy, dtx, dtx_count, ovf_rows, ovf_cm, ovf_count);
 }
 template <int NV>
 void launch_finish(const TxnArgs& ta, bool direct, hipStream_t st) {
@@ -60,8 +60,8 @@ void launch_union(const UnionArgs& ua, bool direct, hipStream_t st) {
 }
 
 void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count,
-                       uint32_t* ovf_rows, uint32_t* ovf_count) {
-    NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy, dtx, dtx_count, ovf_rows, ovf_count);
+                       uint32_t* ovf_rows, uint8_t* ovf_cm, uint32_t* ovf_count) {
+    NV_DISPATCH(nv, launch_offsets, h, direct, cls, heavy, dtx, dtx_count, ovf_rows, ovf_cm, ovf_count);
 }
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st) { NV_DISPATCH(nv, launch_finish, ta, direct, st); }
 // The overflowed rows (a device-side count; each row is a chain of dependent loads — ~27 us of latency for a handful

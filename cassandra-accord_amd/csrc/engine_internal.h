@@ -386,6 +386,7 @@ enum Slot : size_t {
     S_KSIN, S_KSMAT,                                            // distributed Kahn levels (ad_shard_kahn_*)
     S_KSLACC, S_KSPLV, S_KSHEAD, S_KSSENT, S_KSSTO, S_KSSTI, S_KSPEND,   // ... READY level bounds, queues, slots
     S_CSKSLOT, S_CSKRES, S_CSKLIST, S_CSKSTART, S_CSKNEW,                // CFK store large tier
+    S_FOVFCM,                                                           // k_txn_finish_ovf's rows' classes
     S_CS0, S_CS_END = S_CS0 + 22,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
     S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles
@@ -507,7 +508,7 @@ void launch_seg_fuse_nv(int nv, const SegFuseArgs& f, const WalkArgs& w, bool di
 void launch_range_nv(int nv, const RangeArgs& a, bool fill, hipStream_t st);
 // deps_layout.hip: per-txn offsets / layout / unions of the computed key classes
 void launch_offsets_nv(ad_handle* h, int nv, bool direct, const int* cls, uint32_t* heavy, uint32_t* dtx, uint32_t* dtx_count,
-                       uint32_t* ovf_rows, uint32_t* ovf_count);
+                       uint32_t* ovf_rows, uint8_t* ovf_cm, uint32_t* ovf_count);
 void launch_finish_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 void launch_finish_ovf_nv(int nv, const TxnArgs& ta, bool direct, hipStream_t st);
 // k_txn_finish_ovf on the side stream xst (forked after the finish; joined before anything reads the deps CSRs)
