@@ -267,12 +267,14 @@ def end_to_end(eng, batch, steps):
         # and could not say which part moved)
         # two untimed stream steps first: the first page-outs into fresh pinned pages run at about half the
         # steady rate (r04_v2: steps of 6.1, 5.6, then 3.65 ms), which made the mean swing with the step count
+        # batch k's results are paged out (ad_fetch_results_async: a device-side copy into staging, then the copy
+        # stream) while batch k + 1 is committed and runs; the host has them after ad_fetch_wait, one step later
         k = 0
         eng.load_async(pb[k & 1])
-        ph = {"commit": 0.0, "upload_issue": 0.0, "pipeline": 0.0, "fetch_merged": 0.0, "fetch_levels": 0.0}
+        ph = {"commit": 0.0, "upload_issue": 0.0, "pipeline": 0.0, "fetch_wait": 0.0, "fetch_issue": 0.0}
         per_step, cold, dev_ms = [], [], 0.0
         clock = time.perf_counter
-        warm = 2
+        warm = 3        # (the staging buffer's first allocation and the first overlapped page-outs run cold)
         for i in range(warm + steps):
             if i == warm:
                 t0 = clock()
@@ -287,14 +289,15 @@ def end_to_end(eng, batch, steps):
             eng.run_pipeline()
             d = clock()
             dev_ms += eng.last_times()["total"]
-            eng.fetch_merged_all(outs)
+            eng.fetch_wait()                         # the previous batch's merged Deps + levels are in the host buffers
             e = clock()
-            eng.fetch_levels(lvo)
+            eng.fetch_results_async(outs, lvo)
             f = clock()
-            for key, v in (("commit", b_ - a), ("upload_issue", c - b_), ("pipeline", d - c), ("fetch_merged", e - d),
-                           ("fetch_levels", f - e)):
+            for key, v in (("commit", b_ - a), ("upload_issue", c - b_), ("pipeline", d - c), ("fetch_wait", e - d),
+                           ("fetch_issue", f - e)):
                 ph[key] += v
             (per_step if i >= warm else cold).append((f - a) * 1e3)
+        eng.fetch_wait()                             # the last batch's page-out, inside the timed region
         dt = (clock() - t0) / steps
         eng.load_commit()
     finally:
@@ -304,9 +307,11 @@ def end_to_end(eng, batch, steps):
             "h2d_ms": t_h2d * 1e3, "d2h_ms": t_d2h * 1e3,
             "host_ms_per_step": {k_: round(v * 1e3 / steps, 3) for k_, v in ph.items()},
             "pipeline_device_ms": dev_ms / steps, "step_ms": [round(x, 3) for x in per_step],
+            "median_step_ms": round(float(np.median(per_step)), 3),
             "cold_step_ms": [round(x, 3) for x in cold],
-            "what": "pinned host buffers; ad_load_batch_async(batch k+1) || ad_run_pipeline(batch k), "
-                    "ad_fetch_merged_all (3 classes, one call) + ad_fetch_levels, ad_load_batch_commit"}
+            "what": "pinned host buffers; ad_load_batch_async(batch k+1) || ad_run_pipeline(batch k) || page-out of "
+                    "batch k-1 (ad_fetch_results_async: merged Deps 3 classes + levels + order, staged on the device, "
+                    "copy stream), ad_fetch_wait, ad_load_batch_commit"}
 
 
 def union_view_side(eng, n, steps=5):
@@ -727,7 +732,7 @@ def main():
               "frac": gbs / HBM_PEAK_GBS}
     eng.set_trace(0)
     union_view = union_view_side(eng, n) if Q == 0 else None
-    e2e = end_to_end(eng, batch, max(1, min(args.steps, 5))) if args.e2e and Q == 0 else None
+    e2e = end_to_end(eng, batch, max(5, min(args.steps, 20))) if args.e2e and Q == 0 else None
     ms_per_step = dt * 1e3 / args.steps
     value = n * args.steps / dt
     pipe_gbs = pipeline_alg_bytes(n, P, REPLICAS, st, Q) / (dt / args.steps) / 1e9

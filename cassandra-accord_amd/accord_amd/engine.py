@@ -111,6 +111,8 @@ def lib():
         L.ad_host_free.restype = None
         L.ad_merged_sizes.argtypes = [vp, C.POINTER(abi.AdCsrSizes)]
         L.ad_fetch_merged_all.argtypes = [vp, C.POINTER(abi.AdCsrOut)]
+        L.ad_fetch_results_async.argtypes = [vp, C.POINTER(abi.AdCsrOut), vp, vp]
+        L.ad_fetch_wait.argtypes = [vp]
         _LIB = L
     return _LIB
 
@@ -127,7 +129,7 @@ EXPORTED = ("ad_open", "ad_set_replica_model", "ad_close", "ad_last_error", "ad_
             "ad_shard_levels_apply", "ad_shard_levels_exchange", "ad_cfk_retain", "ad_cfk_reset", "ad_cfk_rows", "ad_cfk_update",
             "ad_recover", "ad_fetch_recovery", "ad_fetch_recovery_flags", "ad_shard_level_edges", "ad_shard_levels_solve",
             "ad_shard_levels_gather", "ad_ephemeral_read_deps", "ad_load_batch_async", "ad_load_batch_commit",
-            "ad_host_alloc", "ad_host_free", "ad_merged_sizes", "ad_fetch_merged_all", "ad_shard_kahn_begin",
+            "ad_host_alloc", "ad_host_free", "ad_merged_sizes", "ad_fetch_merged_all", "ad_fetch_results_async", "ad_fetch_wait", "ad_shard_kahn_begin",
             "ad_shard_kahn_outbox", "ad_shard_kahn_inbox", "ad_shard_kahn_exchange", "ad_shard_kahn_step",
             "ad_shard_kahn_finish", "ad_shard_kahn_sent", "ad_shard_kahn_run", "ad_shard_kahn_depth")
 
@@ -249,6 +251,19 @@ class DepsEngine:
         arr = (abi.AdCsrOut * abi.NUM_CLASSES)(*[o.as_out() for o in outs])
         self._check(lib().ad_fetch_merged_all(self.h, arr), "ad_fetch_merged_all")
         return outs
+
+    def fetch_results_async(self, outs, levels=None):
+        """Page out the merged Deps (outs: pinned abi.Csr per class, sized by merged_sizes()) and, with levels = a pinned
+        (levels, order) pair, the levels and order, while the device goes on (ad_fetch_results_async); the buffers
+        hold the results once fetch_wait() returns and must not be touched before."""
+        self._async_outs = (outs, levels, (abi.AdCsrOut * abi.NUM_CLASSES)(*[o.as_out() for o in outs]))
+        lv = levels[0].ctypes.data if levels is not None else None
+        od = levels[1].ctypes.data if levels is not None else None
+        self._check(lib().ad_fetch_results_async(self.h, self._async_outs[2], lv, od), "ad_fetch_results_async")
+
+    def fetch_wait(self):
+        self._check(lib().ad_fetch_wait(self.h), "ad_fetch_wait")
+        self._async_outs = None
 
     def preaccept_deps(self):
         sizes = (abi.AdCsrSizes * (self.replicas * abi.NUM_CLASSES))()

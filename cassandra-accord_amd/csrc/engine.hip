@@ -566,6 +566,9 @@ void ad_close(ad_handle* h) {
     if (h->st) hipStreamSynchronize(h->st);
     if (h->cst) { hipStreamSynchronize(h->cst); hipStreamDestroy(h->cst); }
     if (h->xst) { hipStreamSynchronize(h->xst); hipStreamDestroy(h->xst); }
+    if (h->fst) { hipStreamSynchronize(h->fst); hipStreamDestroy(h->fst); }
+    if (h->fev0) hipEventDestroy(h->fev0);
+    if (h->fev1) hipEventDestroy(h->fev1);
     if (h->xev0) hipEventDestroy(h->xev0);
     if (h->xev1) hipEventDestroy(h->xev1);
     if (h->cev) hipEventDestroy(h->cev);
@@ -1381,6 +1384,78 @@ int ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [3] */) {
         if (nt) HIPCHK(h, hipMemcpyAsync(o.txns, tx, nt * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(h, hipStreamSynchronize(st));
+    return AD_OK;
+}
+
+// The merged Deps (3 classes) and the levels / order of the batch, paged out while the device goes on: on the main
+// stream they are copied into a device staging buffer (after the previous page-out from it has finished), then a
+// copy stream pages the staging buffer out into the caller's (pinned) buffers.  The next ad_run_pipeline may start at
+// once; ad_fetch_wait returns when the host buffers hold the results.
+int ad_fetch_results_async(ad_handle* h, ad_csr_out* out /* [3] */, uint32_t* level_out, uint32_t* order_out) {
+    if (!h || !out) return AD_ERR_ARGUMENT;
+    if (!h->have_merged) return set_err(h, AD_ERR_STATE, "no merged deps");
+    if ((level_out || order_out) && !h->have_levels) return set_err(h, AD_ERR_STATE, "no levels computed for this batch");
+    hipSetDevice(h->device);
+    CK(merged_ready(h));
+    CK(merged_compact(h));
+    hipStream_t st = h->st;
+    if (!h->fst) {
+        HIPCHK(h, hipStreamCreateWithFlags(&h->fst, hipStreamNonBlocking));
+        HIPCHK(h, hipEventCreateWithFlags(&h->fev0, hipEventDisableTiming));
+        HIPCHK(h, hipEventCreateWithFlags(&h->fev1, hipEventDisableTiming));
+    }
+    const size_t n = h->n;
+    struct Piece { void* host; const void* dev; size_t bytes; };
+    std::vector<Piece> ps;
+    for (int c = 0; c < 3; ++c) {
+        const Csr& m = h->merged[c];
+        ad_csr_out& o = out[c];
+        if (c == AD_CLASS_RANGE && !h->merged_has_range) {
+            for (size_t i = 0; i <= n; ++i) { o.key_off[i] = 0; o.k2t_off[i] = 0; o.txn_off[i] = 0; }
+            continue;
+        }
+        const int kw = c == AD_CLASS_RANGE ? 2 : 1;
+        const uint32_t* toff = h->merged_exact ? m.ent_off : h->mx_off[c];
+        const uint32_t* tx = h->merged_exact ? m.txns : h->mx_txns[c];
+        const size_t nt = h->merged_exact ? m.ncap : h->mx_tot[c];
+        ps.push_back({o.key_off, m.key_off, (n + 1) * 4});
+        ps.push_back({o.k2t_off, m.k2t_off, (n + 1) * 4});
+        ps.push_back({o.txn_off, toff, (n + 1) * 4});
+        if (m.nkeys) ps.push_back({o.keys, m.keys, m.nkeys * 8 * kw});
+        if (m.nk2t) ps.push_back({o.k2t, m.k2t, m.nk2t * 4});
+        if (nt) ps.push_back({o.txns, tx, nt * 4});
+    }
+    if (level_out && n) ps.push_back({level_out, h->lvl, n * 4});
+    if (order_out && n) ps.push_back({order_out, h->order, n * 4});
+    size_t tot = 0;
+    for (auto& p : ps) tot += (p.bytes + 255) & ~size_t(255);
+    // the staging buffer is reused: the previous page-out from it must be done before it is overwritten (device-side)
+    if (h->fetch_pending) HIPCHK(h, hipStreamWaitEvent(st, h->fev1, 0));
+    uint8_t* stage = nullptr;
+    CK(dalloc(h, S_FSTAGE, &stage, std::max<size_t>(tot, 256)));
+    size_t at = 0;
+    for (auto& p : ps) {
+        HIPCHK(h, hipMemcpyAsync(stage + at, p.dev, p.bytes, hipMemcpyDeviceToDevice, st));
+        at += (p.bytes + 255) & ~size_t(255);
+    }
+    HIPCHK(h, hipEventRecord(h->fev0, st));
+    HIPCHK(h, hipStreamWaitEvent(h->fst, h->fev0, 0));
+    at = 0;
+    for (auto& p : ps) {
+        HIPCHK(h, hipMemcpyAsync(p.host, stage + at, p.bytes, hipMemcpyDeviceToHost, h->fst));
+        at += (p.bytes + 255) & ~size_t(255);
+    }
+    HIPCHK(h, hipEventRecord(h->fev1, h->fst));
+    h->fetch_pending = true;
+    return AD_OK;
+}
+
+int ad_fetch_wait(ad_handle* h) {
+    if (!h) return AD_ERR_ARGUMENT;
+    if (!h->fetch_pending) return AD_OK;
+    hipSetDevice(h->device);
+    HIPCHK(h, hipEventSynchronize(h->fev1));
+    h->fetch_pending = false;
     return AD_OK;
 }
 

@@ -227,6 +227,10 @@ struct ad_handle {
     bool xjoin = false;              // work queued on xst that the main stream has not waited for
     bool xdefer = false;             // ad_run_pipeline: stage_deps leaves the join to the stages that read its CSRs
     hipEvent_t cev = nullptr, sev = nullptr;
+    // ad_fetch_results_async: the results copied into a device staging buffer on st (fev0), paged out on fst (fev1)
+    hipStream_t fst = nullptr;
+    hipEvent_t fev0 = nullptr, fev1 = nullptr;
+    bool fetch_pending = false;
     bool stage_pending = false;
     size_t stg_n = 0, stg_p = 0, stg_q = 0;
     // CFK history (history_kernels.h): kept rows of earlier batches, prepended to the next loaded batch
@@ -387,6 +391,7 @@ enum Slot : size_t {
     S_KSLACC, S_KSPLV, S_KSHEAD, S_KSSENT, S_KSSTO, S_KSSTI, S_KSPEND,   // ... READY level bounds, queues, slots
     S_CSKSLOT, S_CSKRES, S_CSKLIST, S_CSKSTART, S_CSKNEW,                // CFK store large tier
     S_FOVFCM,                                                           // k_txn_finish_ovf's rows' classes
+    S_FSTAGE,                                                           // ad_fetch_results_async staging
     S_CS0, S_CS_END = S_CS0 + 22,                               // resident CFK store (ad_cfk_store_*)
     S_CSE0, S_CSE_END = S_CSE0 + 14,                            // its event upload
     S_SFLO, S_SFCNT, S_FOVF, S_SFSEC,                                     // k_seg_fuse tiles

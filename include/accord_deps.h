@@ -220,6 +220,12 @@ int  ad_fetch_merged(ad_handle* h, uint32_t cls, ad_csr_out* out);
  * the whole page-out is three DMA streams.  An empty range class gets zero offsets. */
 int  ad_merged_sizes(ad_handle* h, ad_csr_sizes* sizes /* [AD_NUM_CLASSES] */);
 int  ad_fetch_merged_all(ad_handle* h, ad_csr_out* out /* [AD_NUM_CLASSES] */);
+/* The merged Deps (as ad_fetch_merged_all) and the levels / order (as ad_fetch_levels; either may be NULL) paged out
+ * asynchronously: copied on the device into a staging buffer, then paged out on a copy stream while the caller goes
+ * on (the next ad_load_batch_commit / ad_run_pipeline may follow at once).  `out` and the level arrays must be pinned
+ * host memory (ad_host_alloc) and stay untouched until ad_fetch_wait returns. */
+int  ad_fetch_results_async(ad_handle* h, ad_csr_out* out /* [3] */, uint32_t* level_out, uint32_t* order_out);
+int  ad_fetch_wait(ad_handle* h);
 
 /* Stage 2 on the fast path — CoordinateTransaction.onPreAccepted (coordinate/CoordinateTransaction.java:71-101):
  * when the coordinator takes the fast path it merges only the replies whose witnessedAt == TxnId (:75); the slow

@@ -52,6 +52,51 @@ def test_async_stream_matches_oracle(engine_factory, ranges):
         arena.close()
 
 
+@pytest.mark.parametrize("ranges", [False, True])
+def test_async_page_out_matches_the_synchronous_fetch(engine_factory, ranges):
+    # ad_fetch_results_async: batch k's merged Deps + levels paged out on the copy stream while batch k + 1 is committed
+    # and runs; after ad_fetch_wait the host buffers equal what the synchronous fetches returned for batch k
+    batches = [(_mixed(5000 + 400 * k, seed=20 + k) if ranges else workload.generate(7000 + 600 * k, keys_per_txn=4,
+                                                                                       keyspace=20000, seed=20 + k))
+               for k in range(4)]
+    arena = engine.PinnedArena()
+    try:
+        pinned = [arena.batch(b) for b in batches]
+        eng = engine_factory(window=32, replicas=3, drop_p=0.1, seed=0xACC0D1)
+        sync = engine_factory(window=32, replicas=3, drop_p=0.1, seed=0xACC0D1)
+        eng.load_async(pinned[0])
+        eng.load_commit()
+        prev = None
+        for k, b in enumerate(batches):
+            if k + 1 < len(batches):
+                eng.load_async(pinned[k + 1])
+            eng.run_pipeline()
+            if prev is not None:                     # batch k - 1's page-out, overlapped with batch k's pipeline
+                eng.fetch_wait()
+                pk, outs, lvo = prev
+                sync.load(batches[pk])
+                sync.run_pipeline()
+                for c, want in enumerate(sync.fetch_merged_all()):
+                    _same(outs[c], want)
+                wl, wo = sync.fetch_levels()
+                assert np.array_equal(lvo[0][:len(wl)], wl) and np.array_equal(lvo[1][:len(wo)], wo), "batch %d" % pk
+            s = eng.merged_sizes()
+            outs = [arena.csr(s[c], is_range=(c == abi.CLASS_RANGE)) for c in range(abi.NUM_CLASSES)]
+            lvo = (arena.empty(b["n"], np.uint32), arena.empty(b["n"], np.uint32))
+            eng.fetch_results_async(outs, lvo)
+            prev = (k, outs, lvo)
+            if k + 1 < len(batches):
+                eng.load_commit()
+        eng.fetch_wait()
+        pk, outs, lvo = prev
+        sync.load(batches[pk])
+        sync.run_pipeline()
+        for c, want in enumerate(sync.fetch_merged_all()):
+            _same(outs[c], want)
+    finally:
+        arena.close()
+
+
 def test_fetch_merged_all_equals_per_class(engine_factory):
     b = _mixed(20000, seed=11)
     eng = engine_factory(window=32, replicas=3, drop_p=0.1)
