@@ -755,6 +755,7 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
         if (cs_has_deps(ns)) {
             const Ts3 ex{a.eem[e], a.eel[e], a.een[e]};
             const Ts3 dkb = cs_decided(ns) ? ex : t;
+            const uint32_t n_pre = n;
             // room for the event's new rows (its unknown deps at or above prunedBefore, and itself) and loadingPruned
             // entries (its unknown deps below prunedBefore), checked before anything changes: a key that runs out stops
             // at this event with its state intact, and resumes from it in a larger tier
@@ -835,8 +836,9 @@ __device__ __attribute__((always_inline)) inline bool cs_apply_events(const CfkS
                 __syncthreads();
             }
             uint32_t ts;
-            bool fnow;
-            const uint32_t p2 = cs_find(a, base, n, t, fnow);           // t's position after the additions
+            bool fnow = found;
+            // t's position after the additions (none inserted: where it was)
+            const uint32_t p2 = n == n_pre ? p : cs_find(a, base, n, t, fnow);
             if (!fnow) {
                 if (n >= a.cap) { cs_out_of_rows(a, key, e + e_id0); return false; }
                 ts = cs_insert(a, base, n, p2, t, ns, ex);
