@@ -1591,11 +1591,14 @@ int ad_run_pipeline(ad_handle* h) {
     if (rc_deps != AD_OK) { side_join(h); return rc_deps; }
     HIPCHK(h, hipEventRecord(h->ev[3], st));
     host_mark(h, "deps returned");
+    h->merge_side = true;                        // a merge of identical-shape replies may run beside the levels
+    h->merge_sided = false;
     int rc = stage_merge(h);
+    h->merge_side = false;
     host_mark(h, "merge returned");
     if (rc == AD_OK) {
         h->merged_has_range = h->Q > 0;
-        HIPCHK(h, hipEventRecord(h->ev[4], st));
+        if (!h->merge_sided) HIPCHK(h, hipEventRecord(h->ev[4], st));
         rc = stage_levels(h, true);
     }
     host_mark(h, "levels returned");
@@ -1613,8 +1616,9 @@ int ad_run_pipeline(ad_handle* h) {
     hipEventElapsedTime(&ms, h->ev[0], h->ev[1]); h->times.prepare = ms;
     hipEventElapsedTime(&ms, h->ev[1], h->ev[2]); h->times.sort = ms;
     hipEventElapsedTime(&ms, h->ev[2], h->ev[3]); h->times.deps = ms;
+    // (a merge beside the levels: both timed from the end of the deps stage)
     hipEventElapsedTime(&ms, h->ev[3], h->ev[4]); h->times.merge = ms;
-    hipEventElapsedTime(&ms, h->ev[4], h->ev[5]); h->times.levels = ms;
+    hipEventElapsedTime(&ms, h->ev[h->merge_sided ? 3 : 4], h->ev[5]); h->times.levels = ms;
     hipEventElapsedTime(&ms, h->ev[0], h->ev[5]); h->times.total = ms;
     h->times.deps_entries = h->deps_entries;
     h->times.merged_entries = h->merged_entries;

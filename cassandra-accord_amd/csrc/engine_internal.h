@@ -225,6 +225,8 @@ struct ad_handle {
     hipStream_t xst = nullptr;       // side stream: k_txn_finish_ovf's latency-bound rows, overlapped with later stages
     hipEvent_t xev0 = nullptr, xev1 = nullptr;
     bool xjoin = false;              // work queued on xst that the main stream has not waited for
+    bool merge_side = false;         // ad_run_pipeline: stage_merge may run k_merge_ref on xst beside the levels
+    bool merge_sided = false;        // ... and did (ev[4] then marks its end on xst)
     bool xdefer = false;             // ad_run_pipeline: stage_deps leaves the join to the stages that read its CSRs
     hipEvent_t cev = nullptr, sev = nullptr;
     // ad_fetch_results_async: the results copied into a device staging buffer on st (fev0), paged out on fst (fev1)

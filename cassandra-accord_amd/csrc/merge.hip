@@ -315,7 +315,24 @@ int stage_merge(ad_handle* h) {
     side_join(h);                                       // the merge reads every reply's CSRs
     if (!h->merge_heavy && h->Q == 0 && h->n_large == 0 && !getenv_flag("AD_NO_MERGE_CAP")) {
         h->merged_has_range = false;
-        return merge_cap(h);
+        if (!h->merge_side || getenv_flag("AD_NO_MERGE_SIDE")) return merge_cap(h);
+        // ad_run_pipeline: the merge on the side stream, behind everything the main stream has queued (the finish,
+        // and the overflowed rows already on xst), while the main stream runs the levels.  The level paths that
+        // read the merged Deps join it first (stage_levels); the pull pass and the block walk of a key Read/Write
+        // batch read only the key chains — C3's one-workgroup walk leaves the rest of the chip to the merge.
+        CK(side_fork(h));
+        hipStream_t main = h->st, tr = h->tracer.st;
+        h->st = h->xst;
+        h->tracer.st = h->xst;
+        const int rc = merge_cap(h);
+        h->st = main;
+        h->tracer.st = tr;
+        h->xjoin = true;
+        if (rc == AD_OK) {
+            HIPCHK(h, hipEventRecord(h->ev[4], h->xst));
+            h->merge_sided = true;
+        }
+        return rc;
     }
     const Csr* parts[3][MAXV] = {};
     for (int v = 0; v < nv; ++v) {
