@@ -754,6 +754,9 @@ def main():
         "pipeline": {"alg_bytes": pipeline_alg_bytes(n, P, REPLICAS, st, Q), "alg_GBps": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS,
                      "stage_ms": {k: st[k] for k in ("prepare", "sort", "deps", "merge", "levels", "total")},
+                     "stage_note": ("merge and levels overlap (the replicas' merge runs on a side stream beside the "
+                                    "key-chain levels): both are timed from the end of deps, so the stages sum to "
+                                    "more than total"),
                      "deps_entries": st["deps_entries"], "merged_entries": st["merged_entries"],
                      "level_iterations": st["level_iterations"], "level_path": st["level_path"]},
         "max_conflicts": mc,
