@@ -121,6 +121,8 @@ void side_join(ad_handle* h) {
 // sharded level passes).
 int complete_entries(ad_handle* h) {
     if (h->state_partial) {              // k_seg_fuse wrote no entry state: the gather + ElideOp scan rebuild all of it
+        side_join(h);                    // (k_txn_finish_ovf, on the side stream beside the levels, reads the state
+                                         // this rewrites)
         h->state_partial = h->keys_partial = h->entries_partial = false;
         const size_t P = h->P;
         if (P) {
