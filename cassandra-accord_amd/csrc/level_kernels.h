@@ -1604,10 +1604,12 @@ static __global__ __launch_bounds__(256) void k_exec_split_rows(size_t m, const 
 // (no collision, via a sentinel) and that the keys ascend; otherwise the full LSD radix sort runs.
 constexpr int WR_N = 1024, WR_D = 64, WR_T = 256;
 constexpr uint32_t WR_EMPTY = 0xFFFFFFFFu;
+// strip != null (== lvl, rows == null: the pull pass's levels): the levels' LV_FINAL bit cleared here, written back
+// (k_level_strip's pass folded into this one)
 static __global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uint64_t* __restrict__ ex1, const uint32_t* __restrict__ rows,
-                                                      const uint32_t* __restrict__ lvl, uint64_t* __restrict__ okey,
+                                                      const uint32_t* lvl, uint64_t* __restrict__ okey,
                                                       uint32_t* __restrict__ oidx, uint32_t* __restrict__ olvl,
-                                                      uint32_t* __restrict__ bad) {
+                                                      uint32_t* __restrict__ bad, uint32_t* strip = nullptr) {
     __shared__ uint64_t sk[WR_N + 2 * WR_D];
     const long base = (long)blockIdx.x * WR_N;
     for (int x = threadIdx.x; x < WR_N + 2 * WR_D; x += WR_T) {
@@ -1627,11 +1629,13 @@ static __global__ __launch_bounds__(WR_T) void k_window_rank(size_t m, const uin
             r += sk[e + WR_D + k] < key ? 1 : 0;
             r -= sk[e + WR_D - k] > key ? 1 : 0;
         }
+        uint32_t lv = lvl[rows ? rows[i] : (size_t)i];
+        if (strip) { lv &= ~LV_FINAL; strip[i] = lv; }
         const long rank = i + r;
         if (rank < 0 || rank >= (long)m) { oob = true; continue; }
         okey[rank] = key;
         oidx[rank] = (uint32_t)i;
-        olvl[rank] = lvl[rows ? rows[i] : (size_t)i];
+        olvl[rank] = lv;
     }
     wave_set_flag(oob, bad);
 }
@@ -1736,9 +1740,10 @@ static __global__ __launch_bounds__(256) void k_gather_level_rows(size_t m, cons
 // *verify_dev (a host-mapped word the caller zeroed; a device-to-pageable copy here would stall the stream for
 // a host round trip), and the caller, after its own stream sync, reruns order_rows with known_maxl = -1 if set.
 // prefilled: the caller's earlier fill already cleared ls.flags[8..9] and set ls.sv0 to the sentinel (the pull path)
+// strip: lvl holds the pull pass's levels with their LV_FINAL bits (rows == null): k_window_rank clears them
 inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uint64_t* ex1, const uint32_t* lvl,
                        uint32_t exec_bits, uint32_t* order_out, hipStream_t st, int known_maxl = -1,
-                       uint32_t* verify_dev = nullptr, bool prefilled = false) {
+                       uint32_t* verify_dev = nullptr, bool prefilled = false, bool strip = false) {
     KScope ks(K_ORDER, m);
     RadixScratch rs;
     const size_t hl = radix_hist_len(m);
@@ -1753,7 +1758,8 @@ inline bool order_rows(LevelState& ls, size_t m, const uint32_t* rows, const uin
     uint32_t fl[2] = {0, 0};
     // fast path: windowed inversion ranks + verification
     if (!prefilled) fill_multi(st, {{of, 8, 0}, {v, m * 4, 0xFF}});   // flags; WR_EMPTY: detects rank collisions
-    k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1);
+    k_window_rank<<<ceil_div((long)m, WR_N), WR_T, 0, st>>>(m, ex1, rows, lvl, ls.key64, v, k, of + 1,
+                                                            strip && !rows ? const_cast<uint32_t*>(lvl) : nullptr);
     if (optimistic && known_maxl > 0 && known_maxl <= 255) {
         // one stable pass by level whose histogram kernel is also the check, written straight into order_out
         const int ntiles = ceil_div((long)m, RS_TILE);
@@ -1929,6 +1935,10 @@ oom:
     return AD_ERR_NOMEM;
 }
 
+inline bool level_strip_pass() {
+    static const bool on = [] { const char* e = getenv("AD_LEVEL_STRIP"); return e && e[0] == '1'; }();
+    return on;
+}
 inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hipStream_t st, int* iters,
                       std::string& err) {
     const size_t n = in.n, P = in.P;
@@ -2083,7 +2093,10 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 k_level_pull<<<gn, 256, 0, st>>>(n, in.key_off, ls.succ, ls.c_txn, in.lvl, ls.flags + 7, ls.flags + 18, ls.flags + 16,
                                                  ls.sk1, ls.pull_force_abort ? 1 : 0);
                 k_level_pull_max<<<1, 1024, 0, st>>>((uint32_t)gn, ls.sk1, ls.flags + 17);
-                k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
+                // the speculative order below clears the levels' LV_FINAL bits in its rank pass (AD_LEVEL_STRIP=1:
+                // the separate pass, an A/B switch)
+                if (!(want_order && n > 0 && in.order_verify) || level_strip_pass())
+                    k_level_strip<<<gn, 256, 0, st>>>(n, in.lvl);
                 }
                 // the order of the pulled levels, enqueued before the host waits on the pull's flags: one 8-bit
                 // level pass (levels up to 255; k_rank_check flags a deeper batch, then finish_order redoes it)
@@ -2091,7 +2104,7 @@ inline int run_levels(LevelState& ls, const LevelInputs& in, bool want_order, hi
                 const std::function<void()> spec = [&]() {
                     if (want_order && n > 0 && in.order_verify) {
                         *in.order_pending = order_rows(ls, n, nullptr, in.ex1, in.lvl, in.exec_bits, in.order, st, 255, in.order_verify,
-                                                       true);
+                                                       true, !level_strip_pass());
                         spec_order = true;
                     }
                 };
