@@ -263,7 +263,10 @@ int stage_prepare(ad_handle* h) {
     h->small_cleared = false;
     h->chains_pending = false;
     h->chains_prebuilt = false;
-    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));  // 1024 partials: k_minmax_final is a one-workgroup, latency-bound fold
+    // 512 partials: k_minmax_final is a one-workgroup, latency-bound fold (C2: 512 vs 1024 workgroups 0.728 vs 0.733
+    // ms/step, three A/B pairs on one box, profiles/r06/minmax_blocks_ab.json); AD_MM_BLOCKS overrides
+    static const size_t mm_cap = [] { const char* e = getenv("AD_MM_BLOCKS"); return e ? (size_t)std::max(1, atoi(e)) : (size_t)512; }();
+    const int g = (int)std::min<size_t>(mm_cap, std::max<size_t>(1, (std::max(std::max(n, P), Q) + 255) / 256));
     {
         KScope ks(K_MINMAX, n);
         unsigned long long* partial = (unsigned long long*)h->scratch;
